@@ -1,0 +1,119 @@
+#!/usr/bin/env python
+"""Headline benchmark: ResNet-50 v1b training throughput (images/sec, whole node).
+
+Config (BASELINE.json): ResNet-50 v1b, fp16 compute with fp32 master weights
+(multi-precision SGD, momentum 0.9), batch 256 per GPU, 224x224, synthetic
+data / random-init weights, hybridized Gluon model, KVStore('device') RCCL
+all-reduce for N > 1 (one process per GPU, launched by torch.distributed.run).
+
+Timing: W untimed warm-up steps, then exactly K steps bracketed by a barrier +
+device synchronisation on both sides; the max over ranks is reported.  Each
+step = forward + loss + backward + gradient all-reduce + optimizer update.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_IMG_S = 363.69   # reference's published ResNet-50 training number (V100, perf.md)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=30)
+    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--batch', type=int, default=256, help='per-GPU batch size')
+    ap.add_argument('--dtype', default='float16', choices=['float16', 'bfloat16', 'float32'])
+    ap.add_argument('--model', default='resnet50_v1b')
+    ap.add_argument('--no-fuse', action='store_true')
+    ap.add_argument('--image-size', type=int, default=224)
+    args = ap.parse_args()
+
+    import torch
+    import mxnet_maintenance_amd as mx
+    from mxnet_maintenance_amd import gluon, autograd, nd
+    from mxnet_maintenance_amd.parallel import dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    if world > 1:
+        dist.init()
+    rank = dist.rank()
+    local_rank = dist.local_rank()
+    ctx = mx.gpu(local_rank) if torch.cuda.is_available() else mx.cpu()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_rank)
+    mx.random.seed(1234 + rank)
+
+    B = args.batch
+    S = args.image_size
+    net = gluon.model_zoo.vision.get_model(args.model, layout='NHWC', fuse=not args.no_fuse, classes=1000)
+    net.initialize(mx.init.Xavier(rnd_type='gaussian', factor_type='in', magnitude=2), ctx=ctx)
+    if args.dtype != 'float32':
+        net.cast(args.dtype)
+    net.hybridize(static_alloc=True, static_shape=True)
+
+    loss_scale = 128.0 if args.dtype == 'float16' else 1.0
+    trainer = gluon.Trainer(net.collect_params(), 'sgd',
+                            {'learning_rate': 0.1, 'momentum': 0.9, 'wd': 1e-4,
+                             'multi_precision': args.dtype != 'float32',
+                             'rescale_grad': 1.0 / loss_scale},
+                            kvstore='device')
+    loss_fn = gluon.loss.SoftmaxCrossEntropyLoss()
+
+    x = nd.random.uniform(-1, 1, shape=(B, S, S, 3), ctx=ctx).astype(args.dtype)
+    y = nd.array(torch.randint(0, 1000, (B,)).numpy(), ctx=ctx)
+
+    def step():
+        with autograd.record():
+            out = net(x)
+            loss = loss_fn(out, y)
+            if loss_scale != 1.0:
+                loss = loss * loss_scale
+        loss.backward()
+        trainer.step(B)
+        return loss
+
+    def sync():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        last = step()
+    sync()
+    dt = time.perf_counter() - t0
+    if dist.world_size() > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device='cuda' if torch.cuda.is_available() else 'cpu')
+        dist.all_reduce(t, op='max')
+        dt = float(t.item())
+    ms = dt / args.steps * 1000.0
+    n = dist.world_size()
+    value = B * n * args.steps / dt
+    if rank == 0:
+        loss_val = float(last.mean().asscalar()) / loss_scale
+        print(json.dumps({
+            'metric': 'images/sec (whole node) ResNet-50 fp16 batch 256/GPU at 1/2/4/8 MI355X',
+            'value': round(value, 2), 'unit': 'images/sec', 'n_gpus': n, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': round(value / BASELINE_IMG_S, 3), 'dtype': {'float16': 'fp16', 'bfloat16': 'bf16',
+                                                                         'float32': 'fp32'}[args.dtype],
+            'data': 'synthetic (random-init weights, uniform images, random labels)',
+            'config': {'model': args.model.replace('resnet50_v1b', 'ResNet-50 v1b'), 'global_batch': B * n,
+                       'per_gpu_batch': B, 'seq_len': None, 'image_size': S, 'parallelism': 'dp%d' % n,
+                       'layout': 'NHWC', 'optimizer': 'mp-SGD momentum 0.9', 'final_loss': round(loss_val, 4)},
+        }), flush=True)
+    if dist.world_size() > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    main()

@@ -1,0 +1,69 @@
+"""mxnet_maintenance_amd: an MI355X-native deep learning framework with MXNet 1.x's API.
+
+Usage mirrors the reference (geloescht/mxnet-maintenance, python/mxnet/__init__.py)::
+
+    import mxnet_maintenance_amd as mx
+    x = mx.nd.ones((2, 3), ctx=mx.gpu(0))
+    net = mx.gluon.model_zoo.vision.resnet50_v1b(layout='NHWC')
+
+Compute path: PyTorch-ROCm tensors + hand-written gfx950 HIP kernels (src/kernels),
+RCCL over xGMI for data parallelism (kvstore 'device'), a native C++ dependency
+engine / storage / RecordIO runtime (src/native).
+"""
+__version__ = '1.9.1.amd0'
+
+import torch as _torch
+
+from . import base
+from .base import MXNetError
+from .context import Context, cpu, gpu, cpu_pinned, current_context, num_gpus, gpu_memory_info, Device
+from . import context
+from . import ops as _ops
+_ops.load_all()
+from . import engine
+from . import ndarray
+from . import ndarray as nd
+from . import autograd
+from . import random
+from . import name
+from . import attribute
+from .attribute import AttrScope
+from . import symbol
+from . import symbol as sym
+from . import executor
+from . import initializer
+from . import initializer as init
+from . import optimizer
+from . import lr_scheduler
+from . import metric
+from . import kvstore
+from . import kvstore as kv
+from . import gluon
+from . import io
+from . import recordio
+from . import callback
+from . import model
+from . import module
+from . import module as mod
+from . import monitor
+from . import profiler
+from . import runtime
+from . import test_utils
+from . import util
+from . import operator
+from . import image
+from . import visualization
+from . import visualization as viz
+from . import contrib
+from . import parallel
+from . import models
+from . import numpy
+from . import numpy as np
+from . import numpy_extension
+from . import numpy_extension as npx
+from . import rtc
+from .util import is_np_array, is_np_shape, set_np, reset_np, use_np, np_shape, np_array
+
+# Autograd recording decides when torch builds graphs; keep torch's global grad
+# mode off outside record() scopes so inference never builds a tape.
+_torch.set_grad_enabled(False)

@@ -1,0 +1,30 @@
+"""Thread-local imperative state: autograd recording / training flags.
+
+Parity: src/imperative/imperative.cc (Imperative::is_recording_, is_training_,
+is_np_shape_). Kept in its own module so ops can read the flags without
+importing the autograd front-end.
+"""
+import threading
+
+
+class _State(threading.local):
+    def __init__(self):
+        super().__init__()
+        self.recording = False
+        self.training = False
+        self.np_shape = False
+        self.np_array = False
+        # NDArrays marked with attach_grad that were consumed while recording,
+        # keyed by id -> NDArray.  Cleared by backward() (unless retain_graph).
+        self.tape_leaves = {}
+
+
+STATE = _State()
+
+
+def is_recording():
+    return STATE.recording
+
+
+def is_training():
+    return STATE.training

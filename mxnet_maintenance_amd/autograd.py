@@ -1,0 +1,269 @@
+"""Autograd front-end.
+
+Parity: python/mxnet/autograd.py (record, pause, train_mode, predict_mode,
+is_recording, is_training, set_recording, set_training, mark_variables,
+backward, grad, get_symbol, Function) and src/imperative/imperative.cc
+(Imperative::Backward).
+
+The tape is PyTorch's autograd graph; what this module adds is MXNet's
+variable semantics: ``grad_req`` of 'write' (overwrite), 'add' (accumulate) or
+'null', gradient buffers that stay bound to the same storage across
+iterations (so the data-parallel all-reduce can use flat bucket views), and the
+record/train scopes.
+"""
+from contextlib import contextmanager
+
+import torch
+
+from . import _state
+from .base import MXNetError
+
+__all__ = ['record', 'pause', 'train_mode', 'predict_mode', 'is_recording', 'is_training',
+           'set_recording', 'set_training', 'mark_variables', 'backward', 'grad', 'Function',
+           'get_symbol']
+
+
+def set_recording(is_recording):  # pylint: disable=redefined-outer-name
+    prev = _state.STATE.recording
+    _state.STATE.recording = bool(is_recording)
+    return prev
+
+
+def set_training(train_mode):  # pylint: disable=redefined-outer-name
+    prev = _state.STATE.training
+    _state.STATE.training = bool(train_mode)
+    return prev
+
+
+def is_recording():
+    return _state.STATE.recording
+
+
+def is_training():
+    return _state.STATE.training
+
+
+class _RecordingStateScope:
+    def __init__(self, is_record, train_mode):  # pylint: disable=redefined-outer-name
+        self._enter_is_record = is_record
+        self._enter_train_mode = train_mode
+        self._prev_is_record = None
+        self._prev_train_mode = None
+
+    def __enter__(self):
+        if self._enter_is_record is not None:
+            self._prev_is_record = set_recording(self._enter_is_record)
+        if self._enter_train_mode is not None:
+            self._prev_train_mode = set_training(self._enter_train_mode)
+        return self
+
+    def __exit__(self, ptype, value, trace):
+        if self._enter_is_record is not None and self._prev_is_record != self._enter_is_record:
+            set_recording(self._prev_is_record)
+        if self._enter_train_mode is not None and self._prev_train_mode != self._enter_train_mode:
+            set_training(self._prev_train_mode)
+
+
+def record(train_mode=True):  # pylint: disable=redefined-outer-name
+    """Scope in which operations are recorded for gradient computation."""
+    return _RecordingStateScope(True, train_mode)
+
+
+def pause(train_mode=False):  # pylint: disable=redefined-outer-name
+    return _RecordingStateScope(False, train_mode)
+
+
+def train_mode():
+    return _RecordingStateScope(None, True)
+
+
+def predict_mode():
+    return _RecordingStateScope(None, False)
+
+
+def mark_variables(variables, gradients, grad_reqs='write'):
+    """Mark NDArrays as variables whose gradient is written into ``gradients``."""
+    from .ndarray.ndarray import NDArray
+    if isinstance(variables, NDArray):
+        variables, gradients = [variables], [gradients]
+    if isinstance(grad_reqs, str):
+        grad_reqs = [grad_reqs] * len(variables)
+    for v, g, r in zip(variables, gradients, grad_reqs):
+        if r == 'null':
+            v._grad_req = None
+            continue
+        v._set_grad_buffer(g._data, r)
+        v._grad = g
+
+
+def _collect_leaves(retain):
+    leaves = list(_state.STATE.tape_leaves.values())
+    if not retain:
+        _state.STATE.tape_leaves = {}
+    return leaves
+
+
+def _prepare_leaves(leaves):
+    """Zero 'write' buffers (grouped in one multi-tensor launch) and rebind stale .grad."""
+    zero = []
+    for v in leaves:
+        t = v._data
+        if not t.requires_grad or v._grad is None:
+            continue
+        gbuf = v._grad._data
+        if t.grad is not gbuf:
+            t.grad = gbuf
+        if v._grad_req == 'write':
+            zero.append(gbuf)
+    if zero:
+        with torch.no_grad():
+            torch._foreach_zero_(zero)
+
+
+def _finish_leaves(leaves):
+    for v in leaves:
+        t = v._data
+        if v._grad is None:
+            continue
+        g = t.grad
+        if g is not None and g is not v._grad._data:
+            # create_graph path builds a new tensor instead of accumulating in place
+            if v._grad_req == 'add':
+                v._grad._data = g
+            else:
+                v._grad._data = g
+            t.grad = v._grad._data
+        v._fresh_grad = True
+
+
+def backward(heads, head_grads=None, retain_graph=False, train_mode=True, create_graph=False):  # pylint: disable=redefined-outer-name
+    """Compute gradients of ``heads`` w.r.t. previously marked variables."""
+    from .ndarray.ndarray import NDArray
+    if isinstance(heads, NDArray):
+        heads = [heads]
+    if head_grads is not None and isinstance(head_grads, NDArray):
+        head_grads = [head_grads]
+    tensors, grads = [], []
+    for i, h in enumerate(heads):
+        t = h._data
+        if not t.requires_grad:
+            continue
+        tensors.append(t)
+        hg = None if head_grads is None else head_grads[i]
+        grads.append(torch.ones_like(t) if hg is None else hg._data.to(t.dtype))
+    if not tensors:
+        raise MXNetError('Cannot differentiate node because it is not in a computational graph. '
+                         'You need to set is_recording to true or use autograd.record() to save '
+                         'computational graphs for backward.')
+    leaves = _collect_leaves(retain_graph)
+    _prepare_leaves(leaves)
+    prev_train = set_training(train_mode)
+    prev_rec = set_recording(False)
+    try:
+        with torch.enable_grad() if create_graph else torch.no_grad():
+            torch.autograd.backward(tensors, grads, retain_graph=retain_graph or create_graph,
+                                    create_graph=create_graph)
+    finally:
+        set_training(prev_train)
+        set_recording(prev_rec)
+    _finish_leaves(leaves)
+
+
+def grad(heads, variables, head_grads=None, retain_graph=None, create_graph=False, train_mode=True):  # pylint: disable=redefined-outer-name
+    """Return gradients of heads w.r.t. variables (does not touch .grad buffers)."""
+    from .ndarray.ndarray import NDArray
+    single = isinstance(variables, NDArray)
+    if isinstance(heads, NDArray):
+        heads = [heads]
+    if single:
+        variables = [variables]
+    if head_grads is not None and isinstance(head_grads, NDArray):
+        head_grads = [head_grads]
+    hts = [h._data for h in heads]
+    hgs = None if head_grads is None else [g._data for g in head_grads]
+    if retain_graph is None:
+        retain_graph = create_graph
+    prev_train = set_training(train_mode)
+    prev_rec = set_recording(create_graph)
+    try:
+        with torch.enable_grad():
+            gs = torch.autograd.grad(hts, [v._data for v in variables], grad_outputs=hgs,
+                                     retain_graph=retain_graph, create_graph=create_graph,
+                                     allow_unused=True)
+    finally:
+        set_training(prev_train)
+        set_recording(prev_rec)
+    out = [NDArray(g if g is not None else torch.zeros_like(v._data)) for g, v in zip(gs, variables)]
+    return out[0] if single else out
+
+
+def get_symbol(x):
+    """Return a Symbol for the recorded history of ``x`` (only available for
+    arrays produced by a hybridized block; see gluon.block)."""
+    sym = getattr(x, '_symbol', None)
+    if sym is None:
+        raise MXNetError('get_symbol is only supported for outputs of hybridized blocks')
+    return sym
+
+
+class Function:
+    """Customised differentiation (mx.autograd.Function).
+
+    Subclass and implement ``forward`` and ``backward`` over NDArrays; the
+    pair is wrapped into a torch.autograd.Function so it composes with the tape.
+    """
+
+    def __init__(self):
+        self._saved = ()
+        self._used = False
+
+    def save_for_backward(self, *args):
+        self._saved = args
+
+    @property
+    def saved_tensors(self):
+        return self._saved
+
+    def __call__(self, *inputs):
+        from .ndarray.ndarray import NDArray
+        if self._used:
+            raise MXNetError('Each Function instance can only be called once.')
+        self._used = True
+        fself = self
+        nin = len(inputs)
+
+        class _Bridge(torch.autograd.Function):
+            @staticmethod
+            def forward(ctx, *tins):
+                with pause():
+                    outs = fself.forward(*[NDArray(t.detach()) for t in tins])
+                single = isinstance(outs, NDArray)
+                ctx.single = single
+                outs = [outs] if single else list(outs)
+                return tuple(o._data for o in outs)
+
+            @staticmethod
+            def backward(ctx, *gouts):
+                with pause():
+                    gins = fself.backward(*[NDArray(g) for g in gouts])
+                if isinstance(gins, NDArray):
+                    gins = [gins]
+                return tuple(None if g is None else g._data for g in gins)
+
+        from .ndarray.register import _note_leaves
+        _note_leaves(inputs)
+        tins = [x._data for x in inputs]
+        if _state.STATE.recording:
+            with torch.enable_grad():
+                res = _Bridge.apply(*tins)
+        else:
+            with torch.no_grad():
+                res = _Bridge.apply(*tins)
+        outs = [NDArray(r) for r in res]
+        return outs[0] if len(outs) == 1 else outs
+
+    def forward(self, *inputs):
+        raise NotImplementedError
+
+    def backward(self, *output_grads):
+        raise NotImplementedError

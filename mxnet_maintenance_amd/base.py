@@ -1,0 +1,134 @@
+"""Basic types, dtype tables and errors.
+
+Parity: python/mxnet/base.py (MXNetError, numeric_types, string_types,
+_DTYPE_NP_TO_MX / _DTYPE_MX_TO_NP type-flag tables used by the .params format).
+"""
+import numbers
+
+import numpy as np
+import torch
+
+__all__ = ['MXNetError', 'numeric_types', 'integer_types', 'string_types',
+           'np_dtype', 'torch_dtype', 'dtype_to_flag', 'flag_to_dtype']
+
+
+class MXNetError(RuntimeError):
+    """Error raised by the framework (mirrors mxnet.base.MXNetError)."""
+
+
+class NotImplementedForSymbol(MXNetError):
+    def __init__(self, function, alias, *args):
+        super().__init__()
+        self.function = function.__name__ if callable(function) else str(function)
+        self.alias = alias
+        self.args = [str(type(a)) for a in args]
+
+    def __str__(self):
+        msg = 'Function {}'.format(self.function)
+        if self.alias:
+            msg += ' (namely operator "{}")'.format(self.alias)
+        if self.args:
+            msg += ' with arguments ({})'.format(', '.join(self.args))
+        msg += ' is not implemented for Symbol and only available in NDArray.'
+        return msg
+
+
+numeric_types = (float, int, np.generic, numbers.Number)
+integer_types = (int, np.integer)
+string_types = (str,)
+
+# MXNet type flags (include/mxnet/base.h / mshadow type_flag). These values are
+# part of the on-disk .params format, so they must match the reference exactly.
+_FLAG_TO_NP = {
+    0: np.float32, 1: np.float64, 2: np.float16, 3: np.uint8, 4: np.int32,
+    5: np.int8, 6: np.int64, 7: np.bool_, 8: np.int16, 9: np.uint16,
+    10: np.uint32, 11: np.uint64,
+}
+_NP_TO_FLAG = {np.dtype(v): k for k, v in _FLAG_TO_NP.items()}
+# bfloat16 has no numpy dtype; MXNet uses flag 12 for it.
+BFLOAT16_FLAG = 12
+
+_NP_TO_TORCH = {
+    np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
+    np.dtype(np.float16): torch.float16, np.dtype(np.uint8): torch.uint8,
+    np.dtype(np.int32): torch.int32, np.dtype(np.int8): torch.int8,
+    np.dtype(np.int64): torch.int64, np.dtype(np.bool_): torch.bool,
+    np.dtype(np.int16): torch.int16, np.dtype(np.uint16): torch.uint16,
+    np.dtype(np.uint32): torch.uint32, np.dtype(np.uint64): torch.uint64,
+}
+_TORCH_TO_NP = {v: k.type for k, v in _NP_TO_TORCH.items()}
+
+
+class _BF16Marker:
+    """Stand-in numpy-side type object for bfloat16 (numpy has none)."""
+    __name__ = 'bfloat16'
+    name = 'bfloat16'
+
+    def __repr__(self):
+        return "<class 'bfloat16'>"
+
+
+bfloat16 = _BF16Marker()
+
+
+def torch_dtype(dtype):
+    """Convert any dtype spec (str, numpy type, torch dtype, None) to a torch dtype."""
+    if dtype is None:
+        return torch.float32
+    if isinstance(dtype, torch.dtype):
+        return dtype
+    if dtype is bfloat16 or (isinstance(dtype, str) and dtype in ('bfloat16', 'bf16')):
+        return torch.bfloat16
+    if isinstance(dtype, str) and dtype == 'float16':
+        return torch.float16
+    return _NP_TO_TORCH[np.dtype(dtype)]
+
+
+def np_dtype(dtype):
+    """Numpy dtype *type* (e.g. ``np.float32``) used as NDArray.dtype."""
+    if isinstance(dtype, torch.dtype):
+        if dtype == torch.bfloat16:
+            return bfloat16
+        return _TORCH_TO_NP[dtype]
+    if dtype is bfloat16 or dtype == 'bfloat16':
+        return bfloat16
+    return np.dtype(dtype).type
+
+
+def dtype_to_flag(dtype):
+    td = torch_dtype(dtype)
+    if td == torch.bfloat16:
+        return BFLOAT16_FLAG
+    return _NP_TO_FLAG[np.dtype(_TORCH_TO_NP[td])]
+
+
+def flag_to_dtype(flag):
+    if flag == BFLOAT16_FLAG:
+        return torch.bfloat16
+    return torch_dtype(_FLAG_TO_NP[flag])
+
+
+def dtype_name(dtype):
+    td = torch_dtype(dtype)
+    if td == torch.bfloat16:
+        return 'bfloat16'
+    return np.dtype(_TORCH_TO_NP[td]).name
+
+
+def check_call(ret):
+    """Compatibility helper: raise MXNetError on non-zero return codes."""
+    if ret != 0:
+        raise MXNetError('native call failed with code {}'.format(ret))
+
+
+class _NullType:
+    """Placeholder for arguments that were not passed (mirrors base._Null)."""
+
+    def __repr__(self):
+        return '_Null'
+
+    def __bool__(self):
+        return False
+
+
+_Null = _NullType()

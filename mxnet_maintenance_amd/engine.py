@@ -1,0 +1,126 @@
+"""Dependency engine front-end.
+
+Parity: python/mxnet/engine.py (bulk, set_bulk_size) and src/engine/*
+(Engine::Get()->PushAsync / WaitForVar / WaitForAll, MXNET_ENGINE_TYPE,
+MXNET_CPU_WORKER_NTHREADS).
+
+The C++ engine (src/native/engine.cc) schedules host-side work with
+reader/writer dependencies on engine variables.  ``MXNET_ENGINE_TYPE=NaiveEngine``
+runs everything synchronously (the reference's debugging mode).
+"""
+import os
+import threading
+from contextlib import contextmanager
+
+__all__ = ['bulk', 'set_bulk_size', 'get', 'push', 'new_var', 'wait_for_var', 'wait_all',
+           'native_available', 'Engine']
+
+_engine = None
+_lock = threading.Lock()
+_bulk_size = 15
+
+
+def _load_native():
+    try:
+        from ._lib import _native
+        return _native
+    except Exception:  # pragma: no cover - depends on build
+        return None
+
+
+def native_available():
+    return _load_native() is not None
+
+
+class _PyVar:
+    def __init__(self, name=''):
+        self.name = name
+        self.version = 0
+
+
+class _PyEngine:
+    """Synchronous fallback used only when the native library is not built."""
+    naive = True
+    num_workers = 0
+    pending = 0
+    executed = 0
+
+    def new_var(self, name=''):
+        return _PyVar(name)
+
+    def push(self, fn, const_vars, mutable_vars, priority=0, name=''):
+        fn()
+        for v in mutable_vars:
+            v.version += 1
+        self.executed += 1
+
+    def push_write_file(self, path, data, const_vars, mutable_vars):
+        with open(path, 'wb') as f:
+            f.write(data)
+
+    def wait_for_var(self, v):
+        pass
+
+    def wait_for_all(self):
+        pass
+
+
+def get():
+    """Return the process-wide engine (created on first use)."""
+    global _engine
+    if _engine is None:
+        with _lock:
+            if _engine is None:
+                nat = _load_native()
+                etype = os.environ.get('MXNET_ENGINE_TYPE', 'ThreadedEnginePerDevice')
+                nthreads = int(os.environ.get('MXNET_CPU_WORKER_NTHREADS', '4'))
+                if nat is None:
+                    _engine = _PyEngine()
+                else:
+                    _engine = nat.Engine(nthreads, etype == 'NaiveEngine')
+    return _engine
+
+
+Engine = get
+
+
+def new_var(name=''):
+    return get().new_var(name)
+
+
+def push(fn, const_vars=(), mutable_vars=(), priority=0, name=''):
+    """Schedule ``fn()`` after all writers of ``const_vars`` and all users of
+    ``mutable_vars`` pushed before it have finished."""
+    get().push(fn, list(const_vars), list(mutable_vars), priority, name)
+
+
+def push_write_file(path, data, const_vars=(), mutable_vars=()):
+    get().push_write_file(path, data, list(const_vars), list(mutable_vars))
+
+
+def wait_for_var(var):
+    get().wait_for_var(var)
+
+
+def wait_all():
+    if _engine is not None:
+        _engine.wait_for_all()
+
+
+def set_bulk_size(size):
+    """Set the op bulking size; returns the previous value.  Device work is
+    already batched on the HIP stream (and HIP graphs), so this only records
+    the value for API parity."""
+    global _bulk_size
+    prev = _bulk_size
+    _bulk_size = int(size)
+    return prev
+
+
+@contextmanager
+def bulk(size):
+    prev = set_bulk_size(size)
+    try:
+        yield
+    finally:
+        set_bulk_size(prev)

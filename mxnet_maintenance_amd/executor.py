@@ -1,0 +1,225 @@
+"""Graph executor for bound Symbols.
+
+Parity: python/mxnet/executor.py (Executor.forward/backward/outputs/arg_dict/
+grad_dict/aux_dict/output_dict/reshape/copy_params_from) and
+src/executor/graph_executor.cc.
+
+A Symbol is lowered once into a ``GraphProgram``: a flat list of steps
+``(op fn, input slots, parsed attrs, output slots)`` in topological order.  The
+same program drives ``Executor`` and Gluon's hybridized ``CachedOp``; with
+static shapes the program can be captured into a HIP graph (see
+gluon/block.py).  Gradients come from the autograd tape of the forward run.
+"""
+import numpy as np
+import torch
+
+from . import _state
+from .base import MXNetError
+from .ops import registry
+
+
+class GraphProgram:
+    """Topologically ordered, slot-addressed form of a Symbol."""
+
+    def __init__(self, sym):
+        from .symbol.symbol import _aux_var_ids
+        order = sym._topo()
+        self.symbol = sym
+        slot = {}
+        nslots = 0
+        self.var_names = []
+        self.var_slots = []
+        aux = _aux_var_ids(order)
+        self.arg_names = []
+        self.aux_names = []
+        for n in order:
+            if n.op is None:
+                slot[(id(n), 0)] = nslots
+                self.var_names.append(n.name)
+                self.var_slots.append(nslots)
+                (self.aux_names if id(n) in aux else self.arg_names).append(n.name)
+                nslots += 1
+        self.steps = []
+        for n in order:
+            if n.op is None:
+                continue
+            op = n.opdef()
+            parsed = dict(n.parsed())
+            k = op.get_num_outputs(parsed)
+            outs = []
+            for i in range(k):
+                slot[(id(n), i)] = nslots
+                outs.append(nslots)
+                nslots += 1
+            ins = [slot[(id(a), j)] for a, j in n.inputs]
+            self.steps.append((op.fn, ins, parsed, outs, n.name, op.name))
+        self.out_slots = [slot[(id(n), j)] for n, j in sym._outputs]
+        self.nslots = nslots
+        self.name_to_slot = dict(zip(self.var_names, self.var_slots))
+
+    def run(self, feed):
+        """``feed``: dict var name -> torch tensor.  Returns output tensors."""
+        vals = [None] * self.nslots
+        for name, s in self.name_to_slot.items():
+            vals[s] = feed.get(name)
+        for fn, ins, attrs, outs, _name, _op in self.steps:
+            r = fn(*[vals[i] for i in ins], **attrs)
+            if len(outs) == 1:
+                vals[outs[0]] = r[0] if isinstance(r, (tuple, list)) else r
+            else:
+                for o, t in zip(outs, r):
+                    vals[o] = t
+        return [vals[s] for s in self.out_slots]
+
+
+class Executor:
+    """Executor bound to arrays for arguments, gradients and auxiliary states."""
+
+    def __init__(self, sym, ctx, args, args_grad=None, grad_req='write', aux_states=None):
+        from .ndarray.ndarray import NDArray
+        self._symbol = sym
+        self._ctx = ctx
+        self._prog = GraphProgram(sym)
+        arg_names = sym.list_arguments()
+        aux_names = sym.list_auxiliary_states()
+        if isinstance(args, dict):
+            missing = [n for n in arg_names if n not in args]
+            if missing:
+                raise MXNetError('bind: missing arguments %s' % missing)
+            self.arg_arrays = [args[n] for n in arg_names]
+        else:
+            if len(args) != len(arg_names):
+                raise MXNetError('bind: expected %d arguments, got %d' % (len(arg_names), len(args)))
+            self.arg_arrays = list(args)
+        if isinstance(grad_req, str):
+            self._grad_req = {n: grad_req for n in arg_names}
+        elif isinstance(grad_req, (list, tuple)):
+            self._grad_req = dict(zip(arg_names, grad_req))
+        else:
+            self._grad_req = {n: grad_req.get(n, 'null') for n in arg_names}
+        if args_grad is None:
+            self.grad_arrays = [None] * len(arg_names)
+            self._grad_req = {n: 'null' for n in arg_names}
+        elif isinstance(args_grad, dict):
+            self.grad_arrays = [args_grad.get(n) for n in arg_names]
+        else:
+            self.grad_arrays = list(args_grad) + [None] * (len(arg_names) - len(args_grad))
+        for n, g in zip(arg_names, self.grad_arrays):
+            if g is None:
+                self._grad_req[n] = 'null'
+        if aux_states is None:
+            aux_states = []
+        if isinstance(aux_states, dict):
+            self.aux_arrays = [aux_states[n] for n in aux_names]
+        else:
+            self.aux_arrays = list(aux_states)
+        if len(self.aux_arrays) != len(aux_names):
+            raise MXNetError('bind: expected %d aux states, got %d' % (len(aux_names), len(self.aux_arrays)))
+        self.outputs = []
+        self._leaves = None
+        self._out_tensors = None
+        self._monitor = None
+
+    @property
+    def arg_dict(self):
+        return dict(zip(self._symbol.list_arguments(), self.arg_arrays))
+
+    @property
+    def grad_dict(self):
+        return dict(zip(self._symbol.list_arguments(), self.grad_arrays))
+
+    @property
+    def aux_dict(self):
+        return dict(zip(self._symbol.list_auxiliary_states(), self.aux_arrays))
+
+    @property
+    def output_dict(self):
+        return dict(zip(self._symbol.list_outputs(), self.outputs))
+
+    def forward(self, is_train=False, **kwargs):
+        from .ndarray.ndarray import NDArray
+        for k, v in kwargs.items():
+            ad = self.arg_dict
+            if k not in ad:
+                raise MXNetError('forward: unknown argument %s' % k)
+            src = v._data if isinstance(v, NDArray) else torch.as_tensor(np.asarray(v))
+            with torch.no_grad():
+                ad[k]._data.copy_(src.reshape(ad[k].shape))
+        arg_names = self._symbol.list_arguments()
+        feed = {}
+        leaves = []
+        need_grad = is_train and any(r != 'null' for r in self._grad_req.values())
+        for n, a in zip(arg_names, self.arg_arrays):
+            t = a._data.detach()
+            if need_grad and self._grad_req[n] != 'null':
+                t = t.requires_grad_(True)
+                leaves.append((n, t))
+            feed[n] = t
+        for n, a in zip(self._symbol.list_auxiliary_states(), self.aux_arrays):
+            feed[n] = a._data
+        prev_train = _state.STATE.training
+        _state.STATE.training = bool(is_train)
+        try:
+            with torch.set_grad_enabled(need_grad):
+                outs = self._prog.run(feed)
+        finally:
+            _state.STATE.training = prev_train
+        self._leaves = leaves
+        self._out_tensors = outs
+        self.outputs = [NDArray(o.detach()) for o in outs]
+        if self._monitor is not None:
+            self._monitor(self)
+        return self.outputs
+
+    def backward(self, out_grads=None, is_train=True):
+        from .ndarray.ndarray import NDArray
+        if not self._leaves:
+            return
+        if out_grads is None:
+            out_grads = [None] * len(self._out_tensors)
+        elif isinstance(out_grads, NDArray):
+            out_grads = [out_grads]
+        heads, hgs = [], []
+        for o, g in zip(self._out_tensors, out_grads):
+            if not o.requires_grad:
+                continue
+            heads.append(o)
+            hgs.append(torch.ones_like(o) if g is None else g._data.to(o.dtype).reshape(o.shape))
+        names = [n for n, _ in self._leaves]
+        ts = [t for _, t in self._leaves]
+        grads = torch.autograd.grad(heads, ts, hgs, allow_unused=True, retain_graph=False)
+        gd = self.grad_dict
+        with torch.no_grad():
+            for n, g in zip(names, grads):
+                buf = gd[n]
+                if g is None:
+                    if self._grad_req[n] == 'write':
+                        buf._data.zero_()
+                    continue
+                if self._grad_req[n] == 'add':
+                    buf._data.add_(g.to(buf._data.dtype))
+                else:
+                    buf._data.copy_(g)
+        self._leaves = None
+
+    def set_monitor_callback(self, callback, monitor_all=False):
+        self._monitor_cb = callback
+
+    def copy_params_from(self, arg_params, aux_params=None, allow_extra_params=False):
+        for name, array in arg_params.items():
+            if name in self.arg_dict:
+                self.arg_dict[name][:] = array.as_in_context(self.arg_dict[name].context)
+            elif not allow_extra_params:
+                raise ValueError('Find name "%s" that is not in the arguments' % name)
+        if aux_params is not None:
+            for name, array in aux_params.items():
+                if name in self.aux_dict:
+                    self.aux_dict[name][:] = array.as_in_context(self.aux_dict[name].context)
+                elif not allow_extra_params:
+                    raise ValueError('Find name %s that is not in the auxiliary states' % name)
+
+    def reshape(self, partial_shaping=False, allow_up_sizing=False, **kwargs):
+        return self._symbol.simple_bind(self._ctx, grad_req=self._grad_req, **kwargs)
+
+    def debug_str(self):
+        return self._symbol.debug_str()

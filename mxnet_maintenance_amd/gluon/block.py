@@ -1,0 +1,804 @@
+"""Gluon Block / HybridBlock / SymbolBlock.
+
+Parity: python/mxnet/gluon/block.py (_BlockScope naming, Block child/param
+registration, collect_params, save/load_parameters with structural names,
+hooks, initialize, hybridize, cast, summary, HybridBlock.hybrid_forward with
+F = nd | sym, deferred shape inference, export/imports, SymbolBlock) and
+src/imperative/cached_op.cc (CachedOp).
+
+Hybridization on MI355X: ``hybridize()`` traces ``hybrid_forward`` with
+Symbols once, lowers the graph into a slot-addressed ``GraphProgram``
+(executor.py) and runs it directly on torch tensors — one python dispatch per
+operator and no NDArray wrapping inside the graph.  With
+``static_alloc=True, static_shape=True`` inference calls are captured into a
+HIP graph and replayed (``CachedOp``), removing per-kernel launch overhead.
+"""
+import copy
+import re
+import threading
+import warnings
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from .. import _state, autograd, initializer
+from .. import name as _name
+from .. import ndarray, symbol
+from ..base import MXNetError, dtype_name
+from ..context import Context, cpu, current_context
+from ..ndarray.ndarray import NDArray
+from ..symbol.symbol import Symbol
+from .parameter import Parameter, ParameterDict, DeferredInitializationError
+from .utils import _indent, _brief_print_list, HookHandle
+
+__all__ = ['Block', 'HybridBlock', 'SymbolBlock']
+
+
+class _BlockScope:
+    """Scope for collecting child Blocks and assigning name prefixes."""
+    _current = threading.local()
+
+    def __init__(self, block):
+        self._block = block
+        self._counter = {}
+        self._old_scope = None
+        self._name_scope = None
+
+    @staticmethod
+    def create(prefix, params, hint):
+        current = getattr(_BlockScope._current, 'value', None)
+        if current is None:
+            if prefix is None:
+                prefix = _name.NameManager.current().get(None, hint) + '_'
+            if params is None:
+                params = ParameterDict(prefix)
+            else:
+                params = ParameterDict(params.prefix, params)
+            return prefix, params
+        if prefix is None:
+            count = current._counter.get(hint, 0)
+            prefix = '%s%d_' % (hint, count)
+            current._counter[hint] = count + 1
+        if params is None:
+            parent = current._block.params
+            params = ParameterDict(parent.prefix + prefix, parent._shared)
+        else:
+            params = ParameterDict(params.prefix, params)
+        return current._block.prefix + prefix, params
+
+    def __enter__(self):
+        if self._block._empty_prefix:
+            return self
+        self._old_scope = getattr(_BlockScope._current, 'value', None)
+        _BlockScope._current.value = self
+        self._name_scope = _name.Prefix(self._block.prefix)
+        self._name_scope.__enter__()
+        return self
+
+    def __exit__(self, ptype, value, trace):
+        if self._block._empty_prefix:
+            return
+        self._name_scope.__exit__(ptype, value, trace)
+        self._name_scope = None
+        _BlockScope._current.value = self._old_scope
+
+
+def _flatten(args, inout_str):
+    if isinstance(args, NDArray):
+        return [args], int(0)
+    if isinstance(args, Symbol):
+        length = len(args.list_outputs())
+        length = length if length > 1 else 0
+        return [args], int(length)
+    if args is None:
+        return [None], int(-1)
+    if not isinstance(args, (list, tuple)):
+        raise AssertionError('HybridBlock %s must be (nested) list of Symbol or NDArray, but got %s of type %s'
+                             % (inout_str, str(args), str(type(args))))
+    flat, fmts = [], []
+    for i in args:
+        arg, fmt = _flatten(i, inout_str)
+        flat.extend(arg)
+        fmts.append(fmt)
+    return flat, fmts
+
+
+def _regroup(args, fmt):
+    if isinstance(fmt, int):
+        if fmt == 0:
+            return args[0], args[1:]
+        if fmt == -1:
+            if args[0] is not None:
+                raise ValueError('We do not support passing types that are not None when the initial HybridBlock '
+                                 'has received NoneType and has been hybridized.')
+            return None, args[1:]
+        return args[:fmt], args[fmt:]
+    ret = []
+    for i in fmt:
+        res, args = _regroup(args, i)
+        ret.append(res)
+    return ret, args
+
+
+class Block:
+    """Base class for all neural network layers and models."""
+
+    def __init__(self, prefix=None, params=None):
+        self._empty_prefix = prefix == ''
+        self._prefix, self._params = _BlockScope.create(prefix, params, self._alias())
+        self._name = self._prefix[:-1] if self._prefix.endswith('_') else self._prefix
+        self._scope = _BlockScope(self)
+        self._children = OrderedDict()
+        self._reg_params = {}
+        self._forward_hooks = OrderedDict()
+        self._forward_pre_hooks = OrderedDict()
+
+    def __repr__(self):
+        s = '{name}(\n{modstr}\n)'
+        modstr = '\n'.join(['  ({key}): {block}'.format(key=key, block=_indent(block.__repr__(), 2))
+                            for key, block in self.__dict__.items() if isinstance(block, Block)])
+        return s.format(name=self.__class__.__name__, modstr=modstr)
+
+    def __setattr__(self, name, value):
+        if hasattr(self, name):
+            existing = getattr(self, name)
+            if isinstance(existing, (Parameter, Block)) and not isinstance(value, type(existing)):
+                raise TypeError('Changing attribute type for {name} from {type1} to {type2} is not allowed.'
+                                .format(name=name, type1=type(existing), type2=type(value)))
+        if isinstance(value, Block):
+            self.register_child(value, name)
+        elif isinstance(value, Parameter):
+            assert name not in self._reg_params, \
+                'Overriding Parameter attribute %s is not allowed. If you want to share parameters between ' \
+                'blocks, please set \'params\' at Block construction instead.'
+            self._reg_params[name] = value
+        super().__setattr__(name, value)
+
+    def _check_container_with_block(self):
+        children = set(self._children.values())
+
+        def _find_unregistered_block_in_container(data):
+            if isinstance(data, (list, tuple)):
+                return any(_find_unregistered_block_in_container(e) for e in data)
+            if isinstance(data, dict):
+                return any(_find_unregistered_block_in_container(v) for v in data.values())
+            if isinstance(data, Block):
+                return data not in children
+            return False
+        for k, v in self.__dict__.items():
+            if isinstance(v, (list, tuple, dict)) and not (k.startswith('__') or k == '_children'):
+                if _find_unregistered_block_in_container(v):
+                    warnings.warn('"{name}" is an unregistered container with Blocks. Note that Blocks inside the '
+                                  'list, tuple or dict will not be registered automatically. Make sure to register '
+                                  'them using register_child() or switching to nn.Sequential/nn.HybridSequential '
+                                  'instead. '.format(name=self.__class__.__name__ + '.' + k), stacklevel=3)
+
+    def _alias(self):
+        return self.__class__.__name__.lower()
+
+    @property
+    def prefix(self):
+        return self._prefix
+
+    @property
+    def name(self):
+        return self._name
+
+    def name_scope(self):
+        return self._scope
+
+    @property
+    def params(self):
+        return self._params
+
+    def collect_params(self, select=None):
+        self._check_container_with_block()
+        ret = ParameterDict(self._params.prefix)
+        if not select:
+            ret.update(self.params)
+        else:
+            pattern = re.compile(select)
+            ret.update({name: value for name, value in self.params.items() if pattern.match(name)})
+        for cld in self._children.values():
+            ret.update(cld.collect_params(select=select))
+        return ret
+
+    def _collect_params_with_prefix(self, prefix=''):
+        if prefix:
+            prefix += '.'
+        ret = {prefix + key: val for key, val in self._reg_params.items()}
+        for name, child in self._children.items():
+            ret.update(child._collect_params_with_prefix(prefix + name))
+        return ret
+
+    def save_parameters(self, filename, deduplicate=False):
+        params = self._collect_params_with_prefix()
+        if deduplicate:
+            reverse = {}
+            for k, v in params.items():
+                reverse.setdefault(v, []).append(k)
+            params = {v[0]: k for k, v in reverse.items()}
+        arg_dict = {key: val._reduce() for key, val in params.items()}
+        ndarray.save(filename, arg_dict)
+
+    def save_params(self, filename):
+        warnings.warn('save_params is deprecated. Please use save_parameters. Note that if you want load from '
+                      'SymbolBlock later, please use export instead.')
+        try:
+            self.collect_params().save(filename, strip_prefix=self.prefix)
+        except ValueError as e:
+            raise ValueError('%s\nsave_params is deprecated. Using save_parameters may resolve this error.' % e)
+
+    def load_parameters(self, filename, ctx=None, allow_missing=False, ignore_extra=False, cast_dtype=False,
+                        dtype_source='current'):
+        loaded = ndarray.load(filename) if isinstance(filename, str) else filename
+        params = self._collect_params_with_prefix()
+        if not loaded and not params:
+            return
+        if not any('.' in i for i in loaded.keys()):
+            # legacy loading (prefix-named parameters)
+            loaded = None
+            self.collect_params().load(filename, ctx, allow_missing, ignore_extra, self.prefix,
+                                       cast_dtype=cast_dtype, dtype_source=dtype_source)
+            return
+        if not allow_missing:
+            params_inv = {}
+            for k, v in params.items():
+                params_inv.setdefault(v, []).append(k)
+            for name, param in params.items():
+                assert any(p in loaded for p in params_inv[param]), \
+                    "Parameter '%s' is missing in file '%s', which contains parameters: %s. Set allow_missing=True " \
+                    "to ignore missing parameters." % (name, filename, _brief_print_list(loaded.keys()))
+        for name in loaded:
+            if not ignore_extra and name not in params:
+                raise ValueError("Parameter '%s' loaded from file '%s' is not present in ParameterDict, which "
+                                 "contains parameters %s. Set ignore_extra=True to ignore. " % (
+                                     name, filename, _brief_print_list(self._params.keys())))
+            if name in params:
+                params[name]._load_init(loaded[name], ctx, cast_dtype=cast_dtype, dtype_source=dtype_source)
+
+    def load_params(self, filename, ctx=None, allow_missing=False, ignore_extra=False):
+        warnings.warn('load_params is deprecated. Please use load_parameters.')
+        self.load_parameters(filename, ctx, allow_missing, ignore_extra)
+
+    def load_dict(self, param_dict, ctx=None, allow_missing=False, ignore_extra=False, cast_dtype=False,
+                  dtype_source='current'):
+        self.load_parameters(param_dict, ctx, allow_missing, ignore_extra, cast_dtype, dtype_source)
+
+    def register_child(self, block, name=None):
+        if name is None:
+            name = str(len(self._children))
+        self._children[name] = block
+
+    def register_forward_pre_hook(self, hook):
+        handle = HookHandle()
+        handle.attach(self._forward_pre_hooks, hook)
+        return handle
+
+    def register_forward_hook(self, hook):
+        handle = HookHandle()
+        handle.attach(self._forward_hooks, hook)
+        return handle
+
+    def apply(self, fn):
+        for cld in self._children.values():
+            cld.apply(fn)
+        fn(self)
+        return self
+
+    def initialize(self, init=initializer.Uniform(), ctx=None, verbose=False, force_reinit=False):
+        self.collect_params().initialize(init, ctx, verbose, force_reinit)
+
+    def hybridize(self, active=True, **kwargs):
+        for cld in self._children.values():
+            cld.hybridize(active, **kwargs)
+
+    def cast(self, dtype):
+        for child in self._children.values():
+            child.cast(dtype)
+        for _, param in self.params.items():
+            param.cast(dtype)
+
+    def zero_grad(self):
+        self.collect_params().zero_grad()
+
+    def reset_ctx(self, ctx):
+        self.collect_params().reset_ctx(ctx)
+
+    def __call__(self, *args):
+        for hook in self._forward_pre_hooks.values():
+            hook(self, args)
+        out = self.forward(*args)
+        for hook in self._forward_hooks.values():
+            hook(self, args, out)
+        return out
+
+    def forward(self, *args):
+        raise NotImplementedError
+
+    def register_op_hook(self, callback, monitor_all=False):
+        for cld in self._children.values():
+            cld.register_op_hook(callback, monitor_all)
+
+    def summary(self, *inputs):
+        summary = OrderedDict()
+        seen = set()
+        hooks = []
+
+        def _get_shape_str(args):
+            def flatten(args):
+                if not isinstance(args, (list, tuple)):
+                    return [args], int(0)
+                flat, fmts = [], []
+                for i in args:
+                    arg, fmt = flatten(i)
+                    flat.extend(arg)
+                    fmts.append(fmt)
+                return flat, fmts
+
+            def regroup(args, fmt):
+                if isinstance(fmt, int):
+                    if fmt == 0:
+                        return args[0], args[1:]
+                    return args[:fmt], args[fmt:]
+                ret = []
+                for i in fmt:
+                    res, args = regroup(args, i)
+                    ret.append(res)
+                return ret, args
+            flat_args, fmts = flatten(args)
+            flat_arg_shapes = [x.shape if isinstance(x, NDArray) else x for x in flat_args]
+            shapes = regroup(flat_arg_shapes, fmts)[0]
+            if isinstance(shapes, list):
+                shape_str = str(shapes)[1:-1]
+            else:
+                shape_str = str(shapes)
+            return shape_str.replace('L', '')
+
+        def _register_summary_hook(block):
+            assert not isinstance(block, HybridBlock) or not block._active, \
+                '"{}" must not be hybridized to print summary.'.format(block.name)
+
+            def _summary_hook(block, _, outputs):
+                class_name = block.__class__.__name__
+                block_idx = len(summary) - 1
+                m_key = '%s-%i' % (class_name, block_idx + 1)
+                summary[m_key] = OrderedDict()
+                summary[m_key]['output_shape'] = _get_shape_str(outputs)
+                params = 0
+                summary[m_key]['trainable'] = 0
+                summary[m_key]['shared'] = 0
+                for p in block.params.values():
+                    params += p.data().size
+                    summary[m_key]['trainable'] += 0 if p.grad_req == 'null' else p.data().size
+                    if p in seen:
+                        summary[m_key]['shared'] += p.data().size
+                    else:
+                        seen.add(p)
+                summary[m_key]['n_params'] = params
+            from .nn.basic_layers import Sequential, HybridSequential
+            if not isinstance(block, (Sequential, HybridSequential)):
+                hooks.append(block.register_forward_hook(_summary_hook))
+
+        summary['Input'] = OrderedDict()
+        summary['Input']['output_shape'] = _get_shape_str(inputs)
+        summary['Input']['n_params'] = 0
+        summary['Input']['trainable'] = 0
+        summary['Input']['shared'] = 0
+        try:
+            self.apply(_register_summary_hook)
+            self(*inputs)
+            line_format = '{:>20}  {:>42} {:>15}'
+            print('-' * 80)
+            print(line_format.format('Layer (type)', 'Output Shape', 'Param #'))
+            print('=' * 80)
+            total_params = 0
+            trainable_params = 0
+            shared_params = 0
+            for layer in summary:
+                print(line_format.format(layer, str(summary[layer]['output_shape']), summary[layer]['n_params']))
+                total_params += summary[layer]['n_params']
+                trainable_params += summary[layer]['trainable']
+                shared_params += summary[layer]['shared']
+            print('=' * 80)
+            print('Parameters in forward computation graph, duplicate included')
+            print('   Total params: ' + str(total_params))
+            print('   Trainable params: ' + str(trainable_params))
+            print('   Non-trainable params: ' + str(total_params - trainable_params))
+            print('Shared params in forward computation graph: ' + str(shared_params))
+            print('Unique parameters in model: ' + str(total_params - shared_params))
+            print('-' * 80)
+        finally:
+            for h in hooks:
+                h.detach()
+
+
+class CachedOp:
+    """Executes a traced Symbol graph on torch tensors (src/imperative/cached_op.cc).
+
+    ``static_alloc`` + ``static_shape``: inference (not recording) calls are
+    captured once per input signature into a HIP graph and replayed.
+    """
+
+    def __init__(self, sym, flags=()):
+        from ..executor import GraphProgram
+        self.sym = sym
+        self.prog = GraphProgram(sym)
+        self.flags = dict(flags)
+        self._graphs = {}
+
+    def __call__(self, feed, ctx_dev):
+        static = self.flags.get('static_alloc') and self.flags.get('static_shape')
+        if static and not _state.STATE.recording and ctx_dev.type == 'cuda':
+            return self._replay(feed)
+        return self.prog.run(feed)
+
+    def _replay(self, feed):
+        key = tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(feed.items()) if v is not None) + \
+            (_state.STATE.training,)
+        ent = self._graphs.get(key)
+        if ent is None:
+            static_in = {k: (v.clone() if v is not None else None) for k, v in feed.items()}
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    self.prog.run(static_in)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                outs = self.prog.run(static_in)
+            ent = (g, static_in, outs)
+            self._graphs[key] = ent
+        g, static_in, outs = ent
+        for k, v in feed.items():
+            if v is not None and static_in[k].data_ptr() != v.data_ptr():
+                static_in[k].copy_(v)
+        g.replay()
+        return [o.clone() for o in outs]
+
+
+class HybridBlock(Block):
+    """A Block that can be traced into a static graph with ``hybridize()``."""
+
+    def __init__(self, prefix=None, params=None):
+        super().__init__(prefix=prefix, params=params)
+        self._cached_graph = ()
+        self._cached_op = None
+        self._out_format = None
+        self._in_format = None
+        self._active = False
+        self._flags = []
+        self._callback = None
+        self._monitor_all = False
+        self._backend = None
+        self._backend_opts = {}
+        self._param_map = None
+
+    def __setattr__(self, name, value):
+        super().__setattr__(name, value)
+        if isinstance(value, HybridBlock):
+            self._clear_cached_op()
+
+    def _get_graph(self, *args):
+        if not self._cached_graph:
+            flatten_args, self._in_format = _flatten(args, 'input')
+            flatten_inputs = []
+            symbol_inputs = []
+            cnt = 0
+            real_arg_num = sum([ele is not None for ele in flatten_args])
+            if real_arg_num == 0:
+                raise ValueError('All args are None and we do not support such a case.')
+            for arg in flatten_args:
+                if arg is not None:
+                    if real_arg_num > 1:
+                        arg_sym = symbol.var('data{}'.format(cnt))
+                    else:
+                        arg_sym = symbol.var('data')
+                    cnt += 1
+                    flatten_inputs.append(arg_sym)
+                    symbol_inputs.append(arg_sym)
+                else:
+                    flatten_inputs.append(None)
+            grouped_inputs = _regroup(flatten_inputs, self._in_format)[0]
+            params = {i: j.var() for i, j in self._reg_params.items()}
+            with self.name_scope():
+                out = self.hybrid_forward(symbol, *grouped_inputs, **params)
+            out, self._out_format = _flatten(out, 'output')
+            self._cached_graph = symbol_inputs, symbol.Group(out)
+        return self._cached_graph
+
+    def _build_cache(self, *args):
+        data, out = self._get_graph(*args)
+        data_names = {d.name: i for i, d in enumerate(data)}
+        params = self.collect_params()
+        input_names = out.list_inputs()
+        param_names = set(params.keys())
+        expected = set(input_names)
+        for name in expected:
+            assert name in param_names or name in data_names, \
+                'Unknown input to HybridBlock: %s' % name
+        unused = ', '.join(list(data_names.keys() - expected))
+        if unused:
+            warnings.warn('The {input} input(s) {names} of HybridBlock "{name}" are not used by the outputs.'
+                          .format(input='data', names=unused, name=self.name), stacklevel=4)
+        self._data_names = [d.name for d in data]
+        self._param_map = [(n, params[n]) for n in input_names if n in param_names]
+        self._cached_op = CachedOp(out, self._flags)
+
+    def _deferred_infer_shape(self, *args):
+        try:
+            self.infer_shape(*args)
+        except Exception as e:
+            error_msg = 'Deferred initialization failed because shape cannot be inferred. {}'.format(e)
+            raise ValueError(error_msg)
+
+    def _call_cached_op(self, *args):
+        if self._cached_op is None:
+            self._build_cache(*args)
+        args, fmt = _flatten(args, 'input')
+        if fmt != self._in_format:
+            if len(self._in_format) > len(fmt):
+                valid = all([self._in_format[i] == -1 for i in range(len(fmt), len(self._in_format))])
+                valid = valid and (fmt == self._in_format[:len(fmt)])
+            elif len(self._in_format) < len(fmt):
+                valid = all([fmt[i] == -1 for i in range(len(self._in_format), len(fmt))])
+                valid = valid and (fmt[:len(self._in_format)] == self._in_format)
+            else:
+                valid = False
+            if not valid:
+                raise ValueError('The argument structure of HybridBlock does not match the cached version. '
+                                 'Stored format = {}, input format = {}'.format(fmt, self._in_format))
+        args_without_none = [ele for ele in args if ele is not None]
+        ctx = args_without_none[0].context
+        try:
+            pdata = [(n, p.data(ctx)) for n, p in self._param_map]
+        except DeferredInitializationError:
+            self._deferred_infer_shape(*_regroup(args, fmt)[0])
+            for _, p in self._param_map:
+                p._finish_deferred_init()
+            pdata = [(n, p.data(ctx)) for n, p in self._param_map]
+        feed = {}
+        for n, a in zip(self._data_names, args_without_none):
+            feed[n] = a._data
+        rec = _state.STATE.recording
+        if rec:
+            tl = _state.STATE.tape_leaves
+            for _, d in pdata:
+                if d._grad_req is not None:
+                    tl[id(d)] = d
+            for a in args_without_none:
+                if a._grad_req is not None:
+                    tl[id(a)] = a
+        for n, d in pdata:
+            feed[n] = d._data
+        if torch.is_grad_enabled() != rec:
+            with torch.set_grad_enabled(rec):
+                outs = self._cached_op(feed, ctx.torch_device)
+        else:
+            outs = self._cached_op(feed, ctx.torch_device)
+        outs = [NDArray(o) for o in outs]
+        ret, _ = _regroup(outs, self._out_format)
+        return ret
+
+    def _clear_cached_op(self):
+        self._cached_graph = ()
+        self._cached_op = None
+
+    def register_child(self, block, name=None):
+        if not isinstance(block, HybridBlock):
+            raise ValueError('Children of HybridBlock must also be HybridBlock, but %s has type %s. If you are '
+                             'using Sequential, please try HybridSequential instead.' % (str(block), str(type(block))))
+        super().register_child(block, name)
+        self._clear_cached_op()
+
+    def hybridize(self, active=True, backend=None, backend_opts=None, clear=True, **kwargs):
+        self._backend = backend
+        if backend_opts is not None:
+            assert isinstance(backend_opts, dict), 'HybridBlock hybridize requires backend_opts to be a dictionary.'
+            self._backend_opts = backend_opts
+        self._active = active
+        self._flags = list(kwargs.items())
+        if clear:
+            self._clear_cached_op()
+        if active and self._forward_hooks or self._forward_pre_hooks:
+            warnings.warn('"{block}" is being hybridized while still having forward hook/pre-hook. If "{block}" '
+                          'is a child of HybridBlock, the hooks will not take effect.'.format(block=self))
+        super().hybridize(active, **kwargs)
+
+    def cast(self, dtype):
+        self._clear_cached_op()
+        super().cast(dtype)
+
+    def _infer_attrs(self, infer_fn, attr, *args):
+        inputs, out = self._get_graph(*args)
+        args, _ = _flatten(args, 'input')
+        args_without_none = [ele for ele in args if ele is not None]
+        if attr == 'shape':
+            arg_attrs, _, aux_attrs = out.infer_shape_partial(**{i.name: j.shape for i, j in zip(inputs, args_without_none)})
+        else:
+            arg_attrs, _, aux_attrs = out.infer_type(**{i.name: j.dtype for i, j in zip(inputs, args_without_none)})
+        if arg_attrs is None:
+            raise ValueError('%s cannot be inferred' % attr)
+        sdict = {i: j for i, j in zip(out.list_arguments(), arg_attrs)}
+        sdict.update({name: a for name, a in zip(out.list_auxiliary_states(), aux_attrs)})
+        for i in self.collect_params().values():
+            if i.name in sdict:
+                v = sdict[i.name]
+                if attr == 'shape':
+                    if v:
+                        i.shape = tuple(v)
+                else:
+                    setattr(i, attr, v)
+
+    def infer_shape(self, *args):
+        self._infer_attrs('infer_shape', 'shape', *args)
+
+    def infer_type(self, *args):
+        self._infer_attrs('infer_type', 'dtype', *args)
+
+    def export(self, path, epoch=0, remove_amp_cast=True):
+        if not self._cached_graph:
+            raise RuntimeError('Please first call block.hybridize() and then run forward with this block at '
+                               'least once before calling export.')
+        sym = self._cached_graph[1]
+        sym.save('%s-symbol.json' % path)
+        arg_names = set(sym.list_arguments())
+        aux_names = set(sym.list_auxiliary_states())
+        arg_dict = {}
+        for name, param in self.collect_params().items():
+            if name in arg_names:
+                arg_dict['arg:%s' % name] = param._reduce()
+            elif name in aux_names:
+                arg_dict['aux:%s' % name] = param._reduce()
+        params_filename = '%s-%04d.params' % (path, epoch)
+        ndarray.save(params_filename, arg_dict)
+        return '%s-symbol.json' % path, params_filename
+
+    def register_op_hook(self, callback, monitor_all=False):
+        self._callback = callback
+        self._monitor_all = monitor_all
+        for cld in self._children.values():
+            cld._callback = callback
+            cld._monitor_all = monitor_all
+
+    def forward(self, x, *args):
+        has_symbol = isinstance(x, Symbol) or any(isinstance(a, Symbol) for a in args)
+        if not has_symbol and (isinstance(x, NDArray) or any(isinstance(a, NDArray) for a in args)):
+            first = x if isinstance(x, NDArray) else next(a for a in args if isinstance(a, NDArray))
+            ctx = first.context
+            if self._active:
+                return self._call_cached_op(x, *args)
+            try:
+                params = {k: v.data(ctx) for k, v in self._reg_params.items()}
+            except DeferredInitializationError:
+                self._deferred_infer_shape(x, *args)
+                for _, v in self.params.items():
+                    v._finish_deferred_init()
+                params = {k: v.data(ctx) for k, v in self._reg_params.items()}
+            return self.hybrid_forward(ndarray, x, *args, **params)
+        params = {i: j.var() for i, j in self._reg_params.items()}
+        with self.name_scope():
+            return self.hybrid_forward(symbol, x, *args, **params)
+
+    def hybrid_forward(self, F, x, *args, **kwargs):
+        raise NotImplementedError
+
+    def optimize_for(self, x, *args, backend=None, backend_opts=None, clear=True, **kwargs):
+        self.hybridize(True, backend=backend, backend_opts=backend_opts, clear=clear, **kwargs)
+        return self(x, *args)
+
+
+def _common_prefix(names):
+    if not names:
+        return ''
+    prefix = names[0]
+    for name in names:
+        i = 0
+        while i < len(prefix) and i < len(name) and prefix[i] == name[i]:
+            i += 1
+        prefix = prefix[:i]
+    return prefix
+
+
+class SymbolBlock(HybridBlock):
+    """Construct a block from a Symbol (e.g. a network exported with export())."""
+
+    @staticmethod
+    def imports(symbol_file, input_names, param_file=None, ctx=None, allow_missing=False, ignore_extra=False):
+        sym = symbol.load(symbol_file)
+        if isinstance(input_names, str):
+            input_names = [input_names]
+        if param_file is None:
+            inputs = [symbol.var(i, dtype='float32') for i in input_names]
+        else:
+            inputs = [symbol.var(i) for i in input_names]
+        ret = SymbolBlock(sym, inputs)
+        if param_file is not None:
+            ret.collect_params().load(param_file, ctx, allow_missing, ignore_extra, cast_dtype=True,
+                                      dtype_source='saved')
+        return ret
+
+    def __repr__(self):
+        s = '{name}(\n{modstr}\n)'
+        modstr = '\n'.join(['{block} : {numinputs} -> {numoutputs}'.format(
+            block=self._cached_graph[1], numinputs=len(self._cached_graph[0]),
+            numoutputs=len(self._cached_graph[1].list_outputs()))])
+        return s.format(name=self.__class__.__name__, modstr=modstr)
+
+    def __init__(self, outputs, inputs, params=None):
+        super().__init__(prefix=None, params=None)
+        self._prefix = ''
+        self._params = ParameterDict('', params)
+        if isinstance(inputs, Symbol) and len(inputs.list_outputs()) == 1:
+            inputs = [inputs]
+        if isinstance(outputs, (list, tuple)) and len(outputs) == 1:
+            outputs = outputs[0]
+        syms, self._in_format = _flatten(inputs, 'input')
+        out, self._out_format = _flatten(outputs, 'output')
+        input_names = set()
+        for i in syms:
+            assert len(i.get_internals().list_outputs()) == 1, \
+                'Input symbols must be variable, but %s is an output of operators' % str(i)
+            input_names.add(i.name)
+        out = symbol.Group(out) if len(out) > 1 or not isinstance(out[0], Symbol) else out[0]
+        arg_params = out.list_arguments()
+        aux_params = out.list_auxiliary_states()
+        arg_types, aux_types = _infer_param_types(syms, out, arg_params, aux_params)
+        for i, arg in enumerate(arg_params):
+            if arg not in input_names:
+                self.params.get(arg, allow_deferred_init=True, dtype=arg_types[i])
+        for i, aux in enumerate(aux_params):
+            if aux not in input_names:
+                self.params.get(aux, grad_req='null', allow_deferred_init=True, dtype=aux_types[i])
+        self._cached_graph = syms, out
+        len_prefix = len(_common_prefix(list(self._params.keys())))
+        self._reg_params = {key[len_prefix:]: val for key, val in self._params.items()}
+
+    def forward(self, x, *args):
+        if isinstance(x, NDArray):
+            with x.context:
+                return self._call_cached_op(x, *args)
+        args, in_fmt = _flatten([x] + list(args), 'input')
+        assert in_fmt == self._in_format, 'Invalid input format'
+        ret = copy.copy(self._cached_graph[1])
+        ret._compose(**{k.name: v for k, v in zip(self._cached_graph[0], args)})
+        return _regroup(list(ret), self._out_format)[0]
+
+    def _clear_cached_op(self):
+        tmp = self._cached_graph
+        super()._clear_cached_op()
+        self._cached_graph = tmp
+
+    def cast(self, dtype):
+        self._clear_cached_op()
+        super().cast(dtype)
+
+    def hybrid_forward(self, F, x, *args, **kwargs):
+        raise NotImplementedError
+
+
+def _infer_param_types(in_params, out_params, arg_params, aux_params, default_dtype=np.float32):
+    arg_types = None
+    aux_types = None
+    input_sym_names = [in_param.name for in_param in in_params]
+    input_sym_arg_types = []
+    can_infer_input_type = True
+    for in_param in in_params:
+        input_sym_arg_type = in_param.infer_type()[0]
+        if not input_sym_arg_type or len(input_sym_arg_type) < 1:
+            can_infer_input_type = False
+            break
+        input_sym_arg_types.append(in_param.infer_type()[0][0])
+    if can_infer_input_type:
+        params = {k: v for k, v in zip(input_sym_names, input_sym_arg_types)}
+        try:
+            arg_types, _, aux_types = out_params.infer_type(**params)
+        except MXNetError:
+            arg_types, aux_types = None, None
+    if arg_types is None or len(arg_types) != len(arg_params):
+        arg_types = [default_dtype] * len(arg_params)
+    if aux_types is None or len(aux_types) != len(aux_params):
+        aux_types = [default_dtype] * len(aux_params)
+    return arg_types, aux_types

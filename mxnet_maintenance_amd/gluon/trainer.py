@@ -1,0 +1,504 @@
+"""Gluon Trainer.
+
+Parity: python/mxnet/gluon/trainer.py (Trainer: optimizer creation with
+param_dict, kvstore selection/initialisation, update_on_kvstore, step,
+allreduce_grads, update, stale-gradient checks, save_states/load_states,
+learning_rate/set_learning_rate).
+
+MI355X fast path ("flat arenas"): when every trainable parameter lives on one
+GPU (one process per GPU), parameters of equal (dtype, lr_mult, wd_mult) are
+re-homed into one contiguous HBM buffer, their gradients into a second one and
+the optimizer state (momentum, fp32 master weights) into a third/fourth.  Then
+
+* data-parallel gradient reduction is a handful of large RCCL all-reduces on
+  slices of the gradient arena, launched from backward hooks as soon as a
+  bucket is complete (parallel/buckets.py) — overlapped with backward;
+* the optimizer step is ONE fused HIP kernel per arena (mp-SGD-momentum:
+  fp16 grad -> fp32 master update -> fp16 weight write-back), a single pass over
+  HBM instead of ~10 small kernels per parameter.
+
+Per-parameter NDArray views keep the reference semantics (``param.grad()``,
+``save_states``) unchanged.
+"""
+import os
+import warnings
+
+import numpy as np
+import torch
+
+from .. import optimizer as opt
+from ..base import MXNetError
+from ..context import Context
+from ..ndarray.ndarray import NDArray
+from ..kvstore import kvstore as _kvs
+from ..parallel import dist
+from ..parallel.buckets import GradBuckets
+from ..ops import kernels as _K
+from .parameter import ParameterDict, Parameter
+
+__all__ = ['Trainer']
+
+
+class _Arena:
+    """Contiguous weight/grad/state storage for a group of same-dtype parameters."""
+
+    def __init__(self, params, indices, lr_mult, wd_mult):
+        self.params = params
+        self.indices = indices
+        self.lr_mult = lr_mult
+        self.wd_mult = wd_mult
+        d0 = params[0].list_data()[0]._data
+        self.dtype = d0.dtype
+        self.device = d0.device
+        self.numel = sum(p.list_data()[0]._data.numel() for p in params)
+        self.w = torch.empty(self.numel, dtype=self.dtype, device=self.device)
+        self.g = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
+        self.views = []
+        off = 0
+        for p in params:
+            arr = p.list_data()[0]
+            t = arr._data
+            n = t.numel()
+            wv = self.w[off:off + n].view(t.shape)
+            with torch.no_grad():
+                wv.copy_(t)
+            gv = self.g[off:off + n].view(t.shape)
+            arr._data = wv.detach()
+            arr._set_grad_buffer(gv, p.grad_req)
+            self.views.append((off, n, t.shape))
+            off += n
+        self.mom = None
+        self.w32 = None
+
+
+class Trainer:
+    """Applies an Optimizer on a set of Parameters; handles gradient reduction."""
+
+    def __init__(self, params, optimizer, optimizer_params=None, kvstore='device', compression_params=None,
+                 update_on_kvstore=None):
+        param_list = []
+        if isinstance(params, (dict, ParameterDict)):
+            for key in sorted(list(params.keys())):
+                param_list.append(params[key])
+            params = param_list
+        if not isinstance(params, (list, tuple)):
+            raise ValueError('First argument must be a list or dict of Parameters, got %s.' % (type(params)))
+        self._params = []
+        self._param2idx = {}
+        for i, param in enumerate(params):
+            if not isinstance(param, Parameter):
+                raise ValueError('First argument must be a list or dict of Parameters, got list of %s.'
+                                 % (type(param)))
+            self._param2idx[param.name] = i
+            self._params.append(param)
+            param._trainer = self
+        self._compression_params = compression_params
+        self._contexts = self._check_contexts()
+        optimizer_params = optimizer_params if optimizer_params else {}
+        self._init_optimizer(optimizer, optimizer_params)
+        self._scale = self._optimizer.rescale_grad
+        self._kvstore_params = {'kvstore': kvstore, 'update_on_kvstore': update_on_kvstore}
+        self._kv_initialized = False
+        self._kvstore = None
+        self._update_on_kvstore = None
+        self._distributed = None
+        self._params_to_init = []
+        self._arenas = None
+        self._buckets = None
+        self._reset_kvstore()
+
+    def _check_contexts(self):
+        contexts = None
+        for param in self._params:
+            try:
+                ctx = param.list_ctx()
+            except RuntimeError:
+                continue
+            assert contexts is None or contexts == ctx, \
+                'All Parameters must be initialized on the same set of contexts, but Parameter %s is initialized ' \
+                'on %s while previous Parameters are initialized on %s.' % (param.name, str(ctx), str(contexts))
+            contexts = ctx
+        return contexts
+
+    def _init_optimizer(self, optimizer, optimizer_params):
+        param_dict = {i: param for i, param in enumerate(self._params)}
+        if isinstance(optimizer, opt.Optimizer):
+            assert not optimizer_params, 'optimizer_params must be None if optimizer is an instance of ' \
+                                         'Optimizer instead of str'
+            self._optimizer = optimizer
+            self._optimizer.param_dict = param_dict
+        else:
+            self._optimizer = opt.create(optimizer, param_dict=param_dict, **optimizer_params)
+        self._updaters = [opt.get_updater(self._optimizer) for _ in (self._contexts or [None])]
+
+    def _init_params(self):
+        assert self._kv_initialized, 'Cannot initialize parameters in KVStore when KVStore is not initialized.'
+        params_to_init = []
+        if self._kvstore:
+            for param in self._params_to_init:
+                if param._deferred_init:
+                    params_to_init.append(param)
+                else:
+                    param_arrays = param._check_and_get(param._data, list)
+                    idx = self._param2idx[param.name]
+                    if param._stype != 'default':
+                        self._kvstore.init(idx, param_arrays[0])
+                    else:
+                        self._kvstore.broadcast(idx, param_arrays[0], param_arrays)
+        self._params_to_init = params_to_init
+
+    def _reset_kvstore(self):
+        if self._kvstore and 'dist' in self._kvstore.type:
+            raise RuntimeError('Cannot reset distributed KVStore.')
+        self._kv_initialized = False
+        self._kvstore = None
+        self._distributed = None
+        self._update_on_kvstore = None
+        self._params_to_init = [param for param in self._params]
+
+    def _init_kvstore(self):
+        config = self._kvstore_params
+        kvstore = config['kvstore']
+        update_on_kvstore = config['update_on_kvstore']
+        self._contexts = self._check_contexts()
+        multi_ctx = self._contexts is not None and len(self._contexts) > 1
+        if isinstance(kvstore, (_kvs.KVStoreBase,)):
+            kv = kvstore
+        elif kvstore is None or kvstore is False:
+            kv = None
+        else:
+            need = multi_ctx or ('dist' in str(kvstore)) or dist.world_size() > 1 or \
+                int(os.environ.get('WORLD_SIZE', '1')) > 1
+            kv = _kvs.create(kvstore) if need else None
+        if kv is not None and self._compression_params:
+            kv.set_gradient_compression(self._compression_params)
+        self._distributed = kv is not None and (kv.num_workers > 1 if hasattr(kv, 'num_workers') else False)
+        if update_on_kvstore is None:
+            update_on_kvstore = False
+        if kv is not None and update_on_kvstore and not kv.is_capable(_kvs.KVStoreBase.OPTIMIZER):
+            raise ValueError('Please set update_on_kvstore=False when training with {}'.format(type(kv)))
+        self._kvstore = kv
+        self._update_on_kvstore = bool(kv is not None and update_on_kvstore)
+        if self._update_on_kvstore:
+            kv.set_optimizer(self._optimizer)
+        self._kv_initialized = True
+
+    # ------------------------------------------------------------ fast path
+    def _arena_eligible(self):
+        if os.environ.get('MXAMD_FLAT_ARENA', '1') != '1':
+            return False
+        if self._update_on_kvstore or not self._contexts or len(self._contexts) != 1:
+            return False
+        if not isinstance(self._optimizer, opt.SGD) or type(self._optimizer) not in (opt.SGD, opt.ccSGD):
+            return False
+        if self._kvstore is not None and not isinstance(self._kvstore, _kvs.KVStore):
+            return False
+        if self._kvstore is not None and self._kvstore._compression is not None:
+            return False
+        for p in self._params:
+            if p._data is None or p._stype != 'default':
+                return False
+        return True
+
+    def _build_arenas(self):
+        groups = {}
+        order = []
+        for i, p in enumerate(self._params):
+            if p.grad_req == 'null':
+                continue
+            key = (p.list_data()[0]._data.dtype, float(p.lr_mult), float(p.wd_mult))
+            if key not in groups:
+                groups[key] = ([], [])
+                order.append(key)
+            groups[key][0].append(p)
+            groups[key][1].append(i)
+        self._arenas = [_Arena(groups[k][0], groups[k][1], k[1], k[2]) for k in order]
+        o = self._optimizer
+        mp = o.multi_precision
+        upd = self._updaters[0]
+        for a in self._arenas:
+            if o.momentum != 0.0:
+                a.mom = torch.zeros(a.numel, dtype=torch.float32 if (mp and a.dtype != torch.float32) else a.dtype,
+                                    device=a.device)
+            if mp and a.dtype in (torch.float16, torch.bfloat16):
+                a.w32 = a.w.float()
+            for (off, n, shape), idx in zip(a.views, a.indices):
+                mom = NDArray(a.mom[off:off + n].view(shape)) if a.mom is not None else None
+                if a.w32 is not None:
+                    st = (mom, NDArray(a.w32[off:off + n].view(shape)))
+                else:
+                    st = mom
+                upd.states[idx] = st
+                upd.states_synced[idx] = True
+        if self._kvstore is not None and dist.world_size() > 1:
+            arrays = []
+            reqs = []
+            for a in self._arenas:
+                for p in a.params:
+                    arrays.append(p.list_data()[0])
+                    reqs.append(p.grad_req)
+            self._buckets = _ArenaBuckets(self._arenas)
+
+    def _on_param_grad_reset(self, param):
+        if self._arenas is not None:
+            warnings.warn('Parameter %s was re-initialised after the Trainer built its flat arenas; '
+                          'falling back to per-parameter updates.' % param.name)
+            self._arenas = None
+            if self._buckets is not None:
+                self._buckets.remove()
+                self._buckets = None
+
+    # ------------------------------------------------------------- public API
+    @property
+    def learning_rate(self):
+        if not isinstance(self._optimizer, opt.Optimizer):
+            raise UserWarning('Optimizer has to be defined before its learning rate can be accessed.')
+        return self._optimizer.learning_rate
+
+    @property
+    def optimizer(self):
+        if isinstance(self._optimizer, opt.Optimizer):
+            return self._optimizer
+        raise UserWarning('Optimizer has not been initialized yet')
+
+    def set_learning_rate(self, lr):
+        if not isinstance(self._optimizer, opt.Optimizer):
+            raise UserWarning('Optimizer has to be defined before its learning rate is mutated.')
+        self._optimizer.set_learning_rate(lr)
+
+    def _row_sparse_pull(self, parameter, out, row_id, full_idx=False):
+        if not self._kv_initialized:
+            self._init_kvstore()
+        if self._params_to_init:
+            self._init_params()
+        idx = self._param2idx[parameter.name]
+        if self._kvstore is not None:
+            self._kvstore.row_sparse_pull(idx, out=out, row_ids=row_id, priority=-idx)
+
+    def _check_and_rescale_grad(self, scale):
+        if self._update_on_kvstore and self._distributed and self._kv_initialized:
+            if self._optimizer.rescale_grad != scale:
+                raise UserWarning('Possible change in the `batch_size` from previous `step` detected. Optimizer '
+                                  'gradient normalizing factor will not change w.r.t new batch_size when '
+                                  'update_on_kvstore=True and when distributed kvstore is used.')
+        self._optimizer.rescale_grad = scale
+
+    def _prepare(self):
+        if not self._kv_initialized:
+            self._init_kvstore()
+        if self._params_to_init:
+            self._init_params()
+        if self._arenas is None and self._arena_eligible():
+            self._build_arenas()
+
+    def step(self, batch_size, ignore_stale_grad=False):
+        """One optimisation step: reduce gradients, then update with lr * (grad / batch_size)."""
+        rescale_grad = self._scale / batch_size
+        self._check_and_rescale_grad(rescale_grad)
+        self._prepare()
+        self._allreduce_grads()
+        self._update(ignore_stale_grad)
+
+    def allreduce_grads(self):
+        self._prepare()
+        assert not (self._kvstore and self._update_on_kvstore), \
+            'allreduce_grads() when parameters are updated on kvstore is not supported. Try setting ' \
+            '`update_on_kvstore` to False when creating trainer.'
+        self._allreduce_grads()
+
+    def _allreduce_grads(self):
+        if self._kvstore is None:
+            return
+        if self._arenas is not None:
+            if self._buckets is not None:
+                self._buckets.reduce()
+            return
+        keys, vals = [], []
+        for i, param in enumerate(self._params):
+            if param.grad_req != 'null':
+                keys.append(i)
+                vals.append(param.list_grad())
+        if not keys:
+            return
+        if self._update_on_kvstore:
+            self._kvstore.pushpull(keys, vals, [p.list_data() for p in self._params if p.grad_req != 'null'])
+        else:
+            self._kvstore.pushpull(keys, vals, vals)
+
+    def update(self, batch_size, ignore_stale_grad=False):
+        self._prepare()
+        assert not (self._kvstore and self._update_on_kvstore), \
+            'update() when parameters are updated on kvstore is not supported. Try setting `update_on_kvstore` ' \
+            'to False when creating trainer.'
+        self._check_and_rescale_grad(self._scale / batch_size)
+        self._update(ignore_stale_grad)
+
+    def _check_stale(self, ignore_stale_grad):
+        for i, param in enumerate(self._params):
+            if param.grad_req == 'null':
+                continue
+            if not ignore_stale_grad:
+                for data in param._check_and_get(param._data, list):
+                    if not data._fresh_grad:
+                        raise UserWarning(
+                            'Gradient of Parameter `%s` on context %s has not been updated by backward since last '
+                            '`step`. This could mean a bug in your model that made it only use a subset of the '
+                            'Parameters (Blocks) for this iteration. If you are intentionally only using a subset, '
+                            'call step with ignore_stale_grad=True to suppress this warning and skip updating of '
+                            'Parameters with stale gradient' % (param.name, str(data.context)))
+
+    def _update(self, ignore_stale_grad=False):
+        if self._arenas is not None:
+            self._check_stale(ignore_stale_grad)
+            self._fused_update()
+            for p in self._params:
+                if p._data is not None:
+                    for d in p._data:
+                        d._fresh_grad = False
+            return
+        updates = [[] for _ in self._updaters]
+        for i, param in enumerate(self._params):
+            if param.grad_req == 'null':
+                continue
+            if not ignore_stale_grad:
+                for data in param._check_and_get(param._data, list):
+                    if not data._fresh_grad:
+                        raise UserWarning(
+                            'Gradient of Parameter `%s` on context %s has not been updated by backward since last '
+                            '`step`. This could mean a bug in your model that made it only use a subset of the '
+                            'Parameters (Blocks) for this iteration. If you are intentionally only using a subset, '
+                            'call step with ignore_stale_grad=True to suppress this warning and skip updating of '
+                            'Parameters with stale gradient' % (param.name, str(data.context)))
+            if self._kvstore and self._update_on_kvstore:
+                continue
+            for upd, arr, grad in zip(updates, param.list_data(), param.list_grad()):
+                if not ignore_stale_grad or arr._fresh_grad:
+                    upd.append((i, grad, arr))
+                    arr._fresh_grad = False
+        if not (self._kvstore and self._update_on_kvstore):
+            for updater, upd in zip(self._updaters, updates):
+                if upd:
+                    i, g, w = zip(*upd)
+                    updater(list(i), list(g), list(w))
+        else:
+            for param in self._params:
+                for d in (param._data or []):
+                    d._fresh_grad = False
+
+    def _fused_update(self):
+        o = self._optimizer
+        clip = -1.0 if o.clip_gradient is None else o.clip_gradient
+        for a in self._arenas:
+            o._update_count(a.indices)
+            lr = o._get_lrs(a.indices[:1])[0]
+            wd = o._get_wds(a.indices[:1])[0]
+            flat_sgd_update(a.w, a.g, a.mom, a.w32, lr, wd, o.momentum, o.rescale_grad, clip)
+
+    def save_states(self, fname):
+        assert self._optimizer is not None
+        if not self._kv_initialized:
+            self._init_kvstore()
+        if self._params_to_init:
+            self._init_params()
+        if self._update_on_kvstore:
+            assert not self._params_to_init, 'Cannot save trainer states when some parameters are not yet ' \
+                                             'initialized in kvstore.'
+            self._kvstore.save_optimizer_states(fname, dump_optimizer=True)
+        else:
+            with open(fname, 'wb') as fout:
+                fout.write(self._updaters[0].get_states(dump_optimizer=True))
+
+    def load_states(self, fname):
+        if not self._kv_initialized:
+            self._init_kvstore()
+        if self._params_to_init:
+            self._init_params()
+        if self._update_on_kvstore:
+            self._kvstore.load_optimizer_states(fname)
+            self._optimizer = self._kvstore._updater.optimizer
+        else:
+            with open(fname, 'rb') as f:
+                states = f.read()
+            for updater in self._updaters:
+                updater.set_states(states)
+                updater.optimizer = self._updaters[0].optimizer
+            self._optimizer = self._updaters[0].optimizer
+            if self._arenas is not None:
+                upd = self._updaters[0]
+                for a in self._arenas:
+                    for (off, n, shape), idx in zip(a.views, a.indices):
+                        st = upd.states[idx]
+                        with torch.no_grad():
+                            if a.w32 is not None:
+                                mom, w32 = st
+                                a.w32[off:off + n].copy_(w32._data.reshape(-1).to(a.w32.device))
+                            else:
+                                mom = st
+                            if a.mom is not None and mom is not None:
+                                a.mom[off:off + n].copy_(mom._data.reshape(-1).to(a.mom.device))
+                        # rebind state views to the arena
+                        momv = NDArray(a.mom[off:off + n].view(shape)) if a.mom is not None else None
+                        upd.states[idx] = (momv, NDArray(a.w32[off:off + n].view(shape))) \
+                            if a.w32 is not None else momv
+        param_dict = {i: param for i, param in enumerate(self._params)}
+        self._optimizer.param_dict = param_dict
+
+
+class _ArenaBuckets(GradBuckets):
+    """GradBuckets whose buckets are contiguous slices of the trainer's gradient arenas."""
+
+    def __init__(self, arenas, bucket_bytes=None):
+        from ..parallel.buckets import _Bucket
+        if bucket_bytes is None:
+            bucket_bytes = int(float(os.environ.get('MXAMD_BUCKET_MB', '25')) * (1 << 20))
+        self.overlap = dist.world_size() > 1
+        self.average = False
+        self.buckets = []
+        self._hooks = []
+        for a in arenas:
+            esz = a.g.element_size()
+            # walk parameters from the end of the arena (first to receive grads in backward)
+            cur = None
+            cur_lo = None
+            segs = list(zip(a.params, a.views))[::-1]
+            for p, (off, n, shape) in segs:
+                if cur is None or (cur_hi - off) * esz > bucket_bytes:
+                    if cur is not None:
+                        cur.flat = a.g[cur_lo:cur_hi]
+                    cur = _Bucket(a.g.dtype, a.g.device)
+                    self.buckets.append(cur)
+                    cur_hi = off + n
+                cur_lo = off
+                cur.params.append(p.list_data()[0])
+                cur.count += 1
+            if cur is not None:
+                cur.flat = a.g[cur_lo:cur_hi]
+        if self.overlap:
+            for b in self.buckets:
+                if any(p._grad_req == 'add' for p in b.params):
+                    continue
+                for p in b.params:
+                    self._hooks.append(p._data.register_post_accumulate_grad_hook(self._make_hook(b)))
+
+
+@torch.no_grad()
+def flat_sgd_update(w, g, mom, w32, lr, wd, momentum, rescale, clip):
+    """SGD(-momentum) over flat buffers; fused HIP kernel on gfx950."""
+    if w.is_cuda and _K.available() and _K.enabled() and hasattr(_K, 'flat_sgd'):
+        _K.flat_sgd(w, g, mom, w32, lr, wd, momentum, rescale, clip)
+        return
+    tgt = w32 if w32 is not None else w
+    gg = g.to(tgt.dtype) if g.dtype != tgt.dtype else g.clone()
+    if rescale != 1.0:
+        gg.mul_(rescale)
+    if clip is not None and clip >= 0:
+        gg.clamp_(-clip, clip)
+    if wd != 0.0:
+        gg.add_(tgt, alpha=wd)
+    if momentum != 0.0 and mom is not None:
+        mom.mul_(momentum).add_(gg, alpha=-lr)
+        tgt.add_(mom)
+    else:
+        tgt.add_(gg, alpha=-lr)
+    if w32 is not None:
+        w.copy_(w32)

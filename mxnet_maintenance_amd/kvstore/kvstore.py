@@ -1,0 +1,328 @@
+"""Key-value store for data-parallel training.
+
+Parity: python/mxnet/kvstore/kvstore.py (KVStore: init, push, pull, pushpull,
+broadcast, row_sparse_pull, set_optimizer, set_gradient_compression,
+save/load_optimizer_states, rank, num_workers, type, _barrier) and
+python/mxnet/kvstore/base.py (KVStoreBase registry, TestStore, create);
+src/kvstore/{kvstore_local.h, comm.h, kvstore_nccl.h, kvstore_dist.h,
+gradient_compression*}.
+
+MI355X design:
+* one process per GPU; the cross-device reduction is an RCCL all-reduce over
+  xGMI (``torch.distributed`` backend 'nccl') instead of the reference's
+  in-process tree reduce / ps-lite servers;
+* values given as a list (several contexts in one process, e.g. CPU tests) are
+  summed locally first;
+* a list of keys is reduced as ONE flattened collective per dtype (bucket
+  fusion), so per-key launch latency does not dominate on ResNet-sized models;
+* ``dist_async`` is emulated with synchronous all-reduce (no parameter server).
+"""
+import os
+import pickle
+import warnings
+
+import numpy as np
+import torch
+
+from ..base import MXNetError, string_types
+from ..ndarray.ndarray import NDArray
+from .. import optimizer as opt
+from ..parallel import dist
+from .compression import GradientCompression
+
+__all__ = ['KVStoreBase', 'KVStore', 'TestStore', 'create']
+
+
+def _as_list(x):
+    return list(x) if isinstance(x, (list, tuple)) else [x]
+
+
+class KVStoreBase:
+    """Abstract interface; subclasses registered with ``KVStoreBase.register``."""
+    OPTIMIZER = 'optimizer'
+    kv_registry = {}
+
+    def broadcast(self, key, value, out, priority=0):
+        raise NotImplementedError()
+
+    def pushpull(self, key, value, out=None, priority=0):
+        raise NotImplementedError()
+
+    def set_optimizer(self, optimizer):
+        raise NotImplementedError()
+
+    def is_capable(self, capability):
+        raise NotImplementedError()
+
+    def save_optimizer_states(self, fname, dump_optimizer=False):
+        raise NotImplementedError()
+
+    def load_optimizer_states(self, fname):
+        raise NotImplementedError()
+
+    @property
+    def type(self):
+        raise NotImplementedError()
+
+    @property
+    def rank(self):
+        raise NotImplementedError()
+
+    @property
+    def num_workers(self):
+        raise NotImplementedError()
+
+    @staticmethod
+    def register(klass):
+        assert isinstance(klass, type)
+        name = klass.__name__.lower()
+        if name in KVStoreBase.kv_registry:
+            warnings.warn('WARNING: New kvstore %s.%s is overriding existing kvstore %s.%s' % (
+                klass.__module__, klass.__name__, KVStoreBase.kv_registry[name].__module__,
+                KVStoreBase.kv_registry[name].__name__))
+        KVStoreBase.kv_registry[name] = klass
+        return klass
+
+
+@KVStoreBase.register
+class TestStore(KVStoreBase):
+    """A minimal single-process store used to test the KVStoreBase plumbing."""
+
+    def broadcast(self, key, value, out, priority=0):
+        out = _as_list(out)
+        for o in out:
+            o[:] = value
+
+    def pushpull(self, key, value, out=None, priority=0):
+        value = _as_list(value)
+        out = value if out is None else _as_list(out)
+        total = value[0].copy()
+        for v in value[1:]:
+            total += v.as_in_context(total.context)
+        for o in out:
+            o[:] = total.as_in_context(o.context)
+
+    def is_capable(self, capability):
+        if capability.lower() == KVStoreBase.OPTIMIZER:
+            return False
+        raise ValueError('Unknown capability: {}'.format(capability))
+
+    @property
+    def type(self):
+        return 'teststore'
+
+    @property
+    def rank(self):
+        return 0
+
+    @property
+    def num_workers(self):
+        return 1
+
+    def set_optimizer(self, optimizer):
+        raise NotImplementedError()
+
+    def save_optimizer_states(self, fname, dump_optimizer=False):
+        raise NotImplementedError()
+
+    def load_optimizer_states(self, fname):
+        raise NotImplementedError()
+
+
+class KVStore(KVStoreBase):
+    """RCCL-backed key-value store (types local/device/nccl/dist_*/horovod)."""
+
+    def __init__(self, kvtype='local'):
+        self._type = kvtype
+        if kvtype.startswith('dist') or kvtype in ('nccl', 'device', 'horovod', 'byteps'):
+            dist.init()
+        self._store = {}
+        self._updater = None
+        self._optimizer = None
+        self._compression = None
+        self._str_keys = {}
+
+    # ---------------------------------------------------------------- basics
+    @property
+    def type(self):
+        return self._type
+
+    @property
+    def rank(self):
+        return dist.rank()
+
+    @property
+    def num_workers(self):
+        return dist.world_size()
+
+    def is_capable(self, capability):
+        if capability.lower() == KVStoreBase.OPTIMIZER:
+            return True
+        raise ValueError('Unknown capability: {}'.format(capability))
+
+    def _barrier(self):
+        dist.barrier()
+
+    def _send_command_to_servers(self, head, body):
+        pass
+
+    def num_dead_node(self, node_id, timeout=60):
+        return 0
+
+    # ------------------------------------------------------------ reductions
+    def _local_sum(self, values):
+        if len(values) == 1:
+            return values[0]._data
+        dev = values[0]._data.device
+        acc = values[0]._data.clone()
+        for v in values[1:]:
+            acc.add_(v._data.to(dev))
+        return acc
+
+    def _allreduce_many(self, tensors):
+        """All-reduce a list of tensors with one fused collective per (dtype, device)."""
+        if dist.world_size() <= 1 or not tensors:
+            return
+        if self._compression is not None:
+            for t in tensors:
+                self._compression.allreduce(t)
+            return
+        groups = {}
+        for t in tensors:
+            groups.setdefault((t.dtype, t.device), []).append(t)
+        for ts in groups.values():
+            if len(ts) == 1:
+                dist.all_reduce(ts[0])
+                continue
+            flat = torch.cat([t.reshape(-1) for t in ts])
+            dist.all_reduce(flat)
+            off = 0
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[off:off + n].view(t.shape))
+                off += n
+
+    # ------------------------------------------------------------------- API
+    def init(self, key, value):
+        keys = _as_list(key)
+        vals = value if isinstance(key, (list, tuple)) else [value]
+        for k, v in zip(keys, vals):
+            v0 = _as_list(v)[0]
+            t = v0._data.detach().clone()
+            if dist.world_size() > 1:
+                dist.broadcast(t, 0)
+            self._store[k] = NDArray(t)
+
+    def push(self, key, value, priority=0):
+        keys = _as_list(key)
+        vals = value if isinstance(key, (list, tuple)) else [value]
+        merged = []
+        with torch.no_grad():
+            for k, v in zip(keys, vals):
+                merged.append(self._local_sum(_as_list(v)).clone())
+            self._allreduce_many(merged)
+            for k, m in zip(keys, merged):
+                if k not in self._store:
+                    raise MXNetError('key %s has not been initialized' % str(k))
+                stored = self._store[k]
+                if self._updater is not None:
+                    self._updater(k if not isinstance(k, str) else self._str_key(k), NDArray(m), stored)
+                else:
+                    stored._data.copy_(m.to(stored._data.device, stored._data.dtype))
+
+    def _str_key(self, k):
+        if k not in self._str_keys:
+            self._str_keys[k] = len(self._str_keys)
+        return self._str_keys[k]
+
+    def pull(self, key, out=None, priority=0, ignore_sparse=True):
+        assert out is not None
+        keys = _as_list(key)
+        outs = out if isinstance(key, (list, tuple)) else [out]
+        with torch.no_grad():
+            for k, o in zip(keys, outs):
+                src = self._store[k]._data
+                for oo in _as_list(o):
+                    oo._data.copy_(src.to(oo._data.device, oo._data.dtype))
+
+    def pushpull(self, key, value, out=None, priority=0):
+        """Sum ``value`` over devices and workers and write the result to ``out``.
+
+        With an optimizer set (update_on_kvstore) this is push + pull; otherwise
+        it is an in-place all-reduce (the Gluon Trainer fast path).
+        """
+        if self._updater is not None:
+            self.push(key, value, priority)
+            self.pull(key, out if out is not None else value, priority)
+            return
+        keys = _as_list(key)
+        vals = value if isinstance(key, (list, tuple)) else [value]
+        outs = vals if out is None else (out if isinstance(key, (list, tuple)) else [out])
+        with torch.no_grad():
+            sums = [self._local_sum(_as_list(v)) for v in vals]
+            # make sure we do not all-reduce into a caller buffer that is read later as input
+            sums = [s if len(_as_list(v)) > 1 else s for s, v in zip(sums, vals)]
+            self._allreduce_many(sums)
+            for s, o in zip(sums, outs):
+                for oo in _as_list(o):
+                    if oo._data.data_ptr() != s.data_ptr():
+                        oo._data.copy_(s.to(oo._data.device, oo._data.dtype))
+
+    def broadcast(self, key, value, out, priority=0):
+        self.init(key, value)
+        self.pull(key, out, priority)
+
+    def row_sparse_pull(self, key, out=None, priority=0, row_ids=None):
+        assert out is not None and row_ids is not None
+        keys = _as_list(key)
+        outs = out if isinstance(key, (list, tuple)) else [out]
+        rids = row_ids if isinstance(row_ids, (list, tuple)) and isinstance(key, (list, tuple)) else [row_ids]
+        with torch.no_grad():
+            for k, o, r in zip(keys, outs, rids):
+                src = self._store[k]._data
+                for oo, rr in zip(_as_list(o), _as_list(r) * len(_as_list(o))):
+                    idx = rr._data.to(torch.int64).to(src.device)
+                    res = torch.zeros_like(src)
+                    res[idx] = src[idx]
+                    oo._data.copy_(res.to(oo._data.device))
+
+    def set_gradient_compression(self, compression_params):
+        if 'device' in self._type or 'dist' in self._type or self._type in ('local', 'nccl'):
+            self._compression = GradientCompression(**compression_params)
+        else:
+            raise Exception('Gradient compression is not supported for this type of kvstore')
+
+    def set_optimizer(self, optimizer):
+        if isinstance(optimizer, string_types):
+            optimizer = opt.create(optimizer)
+        self._optimizer = optimizer
+        self._updater = opt.get_updater(optimizer)
+
+    def _set_updater(self, updater):
+        self._updater = updater
+
+    def save_optimizer_states(self, fname, dump_optimizer=False):
+        assert self._updater is not None, 'Cannot save states for distributed training'
+        with open(fname, 'wb') as fout:
+            fout.write(self._updater.get_states(dump_optimizer))
+
+    def load_optimizer_states(self, fname):
+        assert self._updater is not None, 'Cannot load states for distributed training'
+        with open(fname, 'rb') as f:
+            self._updater.set_states(f.read())
+
+
+def create(name='local'):
+    """Create a KVStore: local, device, nccl, dist_sync, dist_device_sync, dist_async, horovod,
+    or any registered KVStoreBase subclass (e.g. 'teststore')."""
+    if not isinstance(name, string_types):
+        raise TypeError('name must be a string')
+    name = name.lower()
+    if name in KVStoreBase.kv_registry:
+        return KVStoreBase.kv_registry[name]()
+    valid = ('local', 'device', 'nccl', 'dist_sync', 'dist_device_sync', 'dist_async', 'dist_sync_device',
+             'dist', 'horovod', 'byteps', 'local_update_cpu', 'local_allreduce_cpu', 'local_allreduce_device',
+             'dist_sync_allreduce')
+    if name not in valid:
+        raise MXNetError('Unknown KVStore type %s' % name)
+    return KVStore(name)

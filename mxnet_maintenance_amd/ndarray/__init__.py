@@ -1,0 +1,21 @@
+"""NDArray API (mx.nd).
+
+Parity: python/mxnet/ndarray/__init__.py.  Operator functions are generated
+from the registry (ops/registry.py); helper modules mirror the reference's
+sub-namespaces (contrib, linalg, random, image, sparse, op, _internal).
+"""
+from ..ops import load_all as _load_all
+_load_all()
+
+from .ndarray import *  # noqa: F401,F403
+from .ndarray import NDArray, _op  # noqa: F401
+from . import register as _register
+from .utils import load, save, load_frombuffer, zeros, empty, array  # noqa: F401
+from . import op, _internal, contrib, linalg, random, image, sparse, utils  # noqa: F401
+from .sparse import CSRNDArray, RowSparseNDArray  # noqa: F401
+
+_g = globals()
+for _name, _fn in op.__dict__.items():
+    if not _name.startswith('__') and _name not in _g and callable(_fn):
+        _g[_name] = _fn
+del _g

@@ -1,0 +1,819 @@
+"""NDArray: the imperative tensor type.
+
+Parity: python/mxnet/ndarray/ndarray.py (NDArray class, array/empty/zeros/
+ones/full/arange/concatenate/moveaxis/imdecode, operator overloads, basic and
+advanced indexing, fluent methods) and src/ndarray/ndarray.cc.
+
+An NDArray owns a ``torch.Tensor`` (HBM on an MI355X, host memory on cpu).
+Device work is ordered by the HIP stream, so ``wait_to_read`` is a stream
+synchronisation; host-side asynchrony (IO, kvstore) goes through the native
+dependency engine (engine.py).
+"""
+import numpy as np
+import torch
+
+from .. import _state
+from ..base import (MXNetError, numeric_types, integer_types, torch_dtype, np_dtype,
+                    dtype_name)
+from ..context import Context, current_context, context_from_torch
+
+__all__ = ['NDArray', 'array', 'empty', 'zeros', 'ones', 'full', 'arange', 'linspace',
+           'concatenate', 'moveaxis', 'waitall', 'from_numpy', 'from_dlpack', 'to_dlpack_for_read',
+           'to_dlpack_for_write', 'eye', 'maximum', 'minimum', 'add', 'subtract', 'multiply',
+           'divide', 'modulo', 'power', 'equal', 'not_equal', 'greater', 'greater_equal',
+           'lesser', 'lesser_equal', 'logical_and', 'logical_or', 'logical_xor', 'true_divide',
+           'negative', 'onehot_encode', 'histogram', 'split_v2', 'zeros_like', 'ones_like']
+
+_GRAD_REQ = ('null', 'write', 'add')
+
+
+def _wrap(t):
+    return NDArray(t)
+
+
+class NDArray:
+    """An n-dimensional array on a :class:`Context`."""
+    __slots__ = ('_data', '_grad', '_grad_req', '_stype', '__weakref__', '_fresh_grad')
+    __array_priority__ = 1000.0
+
+    def __init__(self, data, ctx=None, dtype=None, stype='default'):
+        if isinstance(data, NDArray):
+            data = data._data
+        if not isinstance(data, torch.Tensor):
+            data = torch.as_tensor(np.asarray(data))
+        if dtype is not None:
+            data = data.to(torch_dtype(dtype))
+        if ctx is not None:
+            data = data.to(ctx.torch_device)
+        self._data = data
+        self._grad = None
+        self._grad_req = None
+        self._stype = stype
+        self._fresh_grad = False
+
+    # ------------------------------------------------------------------ props
+    @property
+    def data(self):
+        return self._data
+
+    @property
+    def shape(self):
+        return tuple(self._data.shape)
+
+    @property
+    def size(self):
+        return self._data.numel()
+
+    @property
+    def ndim(self):
+        return self._data.dim()
+
+    @property
+    def dtype(self):
+        return np_dtype(self._data.dtype)
+
+    @property
+    def stype(self):
+        return self._stype
+
+    @property
+    def context(self):
+        return context_from_torch(self._data.device)
+
+    ctx = context
+
+    @property
+    def device(self):
+        return self.context
+
+    @property
+    def handle(self):
+        return self._data
+
+    @property
+    def writable(self):
+        return True
+
+    @property
+    def grad(self):
+        return self._grad
+
+    @property
+    def T(self):
+        if self.ndim < 2:
+            return self.copy()
+        return self.transpose()
+
+    @property
+    def _fresh_grad_(self):
+        return self._fresh_grad
+
+    def __len__(self):
+        if self.ndim == 0:
+            raise TypeError('len() of unsized object')
+        return self.shape[0]
+
+    def __repr__(self):
+        shape_info = 'x'.join(str(x) for x in self.shape)
+        return '\n%s\n<%s %s @%s>' % (str(self.asnumpy()), self.__class__.__name__, shape_info, self.context)
+
+    def __str__(self):
+        return self.__repr__()
+
+    def __hash__(self):
+        return id(self)
+
+    def __bool__(self):
+        n = self.size
+        if n == 0:
+            raise ValueError('The truth value of an empty array is ambiguous')
+        if n == 1:
+            return bool(self._data.reshape(-1)[0].item())
+        raise ValueError('The truth value of an NDArray with multiple elements is ambiguous.')
+
+    __nonzero__ = __bool__
+
+    def __float__(self):
+        return float(self.asscalar())
+
+    def __int__(self):
+        return int(self.asscalar())
+
+    def __index__(self):
+        return int(self.asscalar())
+
+    def __iter__(self):
+        if self.ndim == 1:
+            for i in range(self.shape[0]):
+                yield self[i]
+        else:
+            for i in range(self.shape[0]):
+                yield NDArray(self._data[i])
+
+    def __array__(self, dtype=None, copy=None):
+        a = self.asnumpy()
+        return a.astype(dtype) if dtype is not None else a
+
+    def __getstate__(self):
+        return {'data': self.asnumpy(), 'ctx': self.context}
+
+    def __setstate__(self, state):
+        self._data = torch.from_numpy(np.ascontiguousarray(state['data']))
+        self._grad = None
+        self._grad_req = None
+        self._stype = 'default'
+        self._fresh_grad = False
+
+    def __reduce__(self):
+        return (_rebuild, (self.asnumpy(),))
+
+    # ---------------------------------------------------------------- sync/io
+    def wait_to_read(self):
+        if self._data.is_cuda:
+            torch.cuda.current_stream(self._data.device).synchronize()
+
+    wait_to_write = wait_to_read
+
+    def asnumpy(self):
+        t = self._data.detach()
+        if t.dtype == torch.bfloat16:
+            t = t.float()
+        return t.cpu().numpy().copy() if t.device.type == 'cpu' else t.cpu().numpy()
+
+    def asscalar(self):
+        if self.size != 1:
+            raise ValueError('The current array is not a scalar')
+        return self.asnumpy().reshape(-1)[0]
+
+    def item(self):
+        return self.asscalar()
+
+    def tolist(self):
+        return self.asnumpy().tolist()
+
+    def astype(self, dtype, copy=True):
+        td = torch_dtype(dtype)
+        if not copy and td == self._data.dtype:
+            return self
+        return _invoke_unary(lambda t: t.to(td) if t.dtype != td else t.clone(), self)
+
+    def copy(self):
+        return _invoke_unary(lambda t: t.clone(), self)
+
+    def __copy__(self):
+        return self.copy()
+
+    def __deepcopy__(self, memo):
+        return NDArray(self._data.detach().clone())
+
+    def copyto(self, other):
+        if isinstance(other, NDArray):
+            if other is self:
+                return other
+            src = self._data.detach() if not _state.STATE.recording else self._data
+            if other.shape != self.shape:
+                raise MXNetError('copyto: shape mismatch %s vs %s' % (self.shape, other.shape))
+            with torch.no_grad():
+                other._data.copy_(src)
+            return other
+        if isinstance(other, Context):
+            return NDArray(self._data.to(other.torch_device, copy=True))
+        raise TypeError('copyto does not support type ' + str(type(other)))
+
+    def as_in_context(self, context):
+        if self.context == context:
+            return self
+        return _invoke_unary(lambda t: t.to(context.torch_device), self)
+
+    as_in_ctx = as_in_context
+
+    def to_device(self, device):
+        return self.as_in_context(device)
+
+    def detach(self):
+        return NDArray(self._data.detach())
+
+    def tostype(self, stype):
+        from . import sparse
+        return sparse.cast_storage(self, stype)
+
+    def asnd(self):
+        return self
+
+    def as_np_ndarray(self):
+        from ..numpy import ndarray as np_ndarray
+        return np_ndarray(self._data)
+
+    def as_nd_ndarray(self):
+        return self
+
+    def to_dlpack_for_read(self):
+        return torch.utils.dlpack.to_dlpack(self._data)
+
+    to_dlpack_for_write = to_dlpack_for_read
+
+    # ------------------------------------------------------------- autograd
+    def attach_grad(self, grad_req='write', stype=None):
+        """Allocate a gradient buffer and mark this array as a leaf variable."""
+        if grad_req not in _GRAD_REQ:
+            raise ValueError('grad_req must be one of %s' % (_GRAD_REQ,))
+        t = self._data.detach()
+        if grad_req == 'null':
+            self._data = t
+            self._grad = None
+            self._grad_req = None
+            return
+        if not t.is_floating_point():
+            raise MXNetError('attach_grad requires a floating point array')
+        t.requires_grad_(True)
+        self._data = t
+        g = torch.zeros_like(t)
+        t.grad = g
+        self._grad = NDArray(g)
+        self._grad_req = grad_req
+
+    def _set_grad_buffer(self, gbuf, grad_req='write'):
+        """Bind an external (e.g. bucketed flat) gradient buffer to this leaf."""
+        t = self._data.detach().requires_grad_(True)
+        self._data = t
+        t.grad = gbuf
+        if self._grad is None:
+            self._grad = NDArray(gbuf)
+        else:
+            self._grad._data = gbuf
+        self._grad_req = grad_req
+
+    def backward(self, out_grad=None, retain_graph=False, train_mode=True):
+        from .. import autograd
+        autograd.backward([self], None if out_grad is None else [out_grad],
+                          retain_graph=retain_graph, train_mode=train_mode)
+
+    # ------------------------------------------------------------ indexing
+    def __getitem__(self, key):
+        key = _convert_key(key)
+        t = self._data
+        if isinstance(key, int) and t.dim() >= 1:
+            n = t.shape[0]
+            if not -n <= key < n:
+                raise IndexError('index %d is out of bounds for axis 0 with size %d' % (key, n))
+        r = _index_fn(t, key)
+        if r.dim() == 0 and not _state.STATE.np_shape:
+            r = r.reshape(1)
+        return NDArray(r)
+
+    def __setitem__(self, key, value):
+        key = _convert_key(key)
+        if isinstance(value, NDArray):
+            v = value._data
+        elif isinstance(value, numeric_types):
+            v = value
+        else:
+            v = torch.as_tensor(np.asarray(value), dtype=self._data.dtype)
+        t = self._data
+        if _state.STATE.recording and t.requires_grad and not t.is_leaf:
+            new = t.clone()
+            new[key] = v.to(new.device, new.dtype) if torch.is_tensor(v) else v
+            self._data = new
+            return
+        with torch.no_grad():
+            if torch.is_tensor(v):
+                v = v.to(t.device, t.dtype)
+                tgt = t[key] if not (isinstance(key, slice) and key == slice(None)) else t
+                if tgt.dim() and v.dim() > tgt.dim():
+                    v = v.reshape(tgt.shape)
+            t[key] = v
+
+    def slice(self, *args, **kwargs):
+        return _op('slice', self, *args, **kwargs)
+
+    def _at(self, idx):
+        return NDArray(self._data[idx])
+
+    def _slice(self, start, stop):
+        return NDArray(self._data[start:stop])
+
+    # ----------------------------------------------------------- reshaping
+    def reshape(self, *shape, **kwargs):
+        if len(shape) == 1 and isinstance(shape[0], (list, tuple)):
+            shape = tuple(shape[0])
+        if not shape:
+            shape = kwargs.get('shape', ())
+        reverse = kwargs.get('reverse', False)
+        from ..ops.tensor import infer_reshape
+        new = infer_reshape(self.shape, shape, reverse)
+        return _invoke_unary(lambda t: t.reshape(new), self)
+
+    def reshape_like(self, *args, **kwargs):
+        return _op('reshape_like', self, *args, **kwargs)
+
+    def zeros_like(self, *args, **kwargs):
+        return _op('zeros_like', self, *args, **kwargs)
+
+    def ones_like(self, *args, **kwargs):
+        return _op('ones_like', self, *args, **kwargs)
+
+    def broadcast_to(self, shape):
+        return _op('broadcast_to', self, shape=shape)
+
+    def broadcast_like(self, other):
+        return _op('broadcast_like', self, other)
+
+    def flatten(self, inplace=False):
+        return _op('Flatten', self)
+
+    def expand_dims(self, axis, inplace=False):
+        return _op('expand_dims', self, axis=axis)
+
+    def squeeze(self, axis=None, inplace=False):
+        return _op('squeeze', self, axis=axis)
+
+    def transpose(self, *axes, **kwargs):
+        if len(axes) == 1 and isinstance(axes[0], (list, tuple)):
+            axes = tuple(axes[0])
+        if not axes:
+            axes = kwargs.get('axes', ())
+        return _op('transpose', self, axes=axes)
+
+    def diag(self, k=0, **kwargs):
+        return _op('diag', self, k=k, **kwargs)
+
+    def split(self, *args, **kwargs):
+        return _op('split', self, *args, **kwargs)
+
+    def split_v2(self, *args, **kwargs):
+        return split_v2(self, *args, **kwargs)
+
+    # ----------------------------------------------------------- arithmetic
+    def __add__(self, other):
+        return _ufunc(self, other, 'broadcast_add', '_plus_scalar')
+
+    def __iadd__(self, other):
+        return _inplace(self, other, torch.Tensor.add_, 'broadcast_add', '_plus_scalar')
+
+    def __radd__(self, other):
+        return self.__add__(other)
+
+    def __sub__(self, other):
+        return _ufunc(self, other, 'broadcast_sub', '_minus_scalar')
+
+    def __isub__(self, other):
+        return _inplace(self, other, torch.Tensor.sub_, 'broadcast_sub', '_minus_scalar')
+
+    def __rsub__(self, other):
+        return _ufunc(self, other, 'broadcast_sub', '_rminus_scalar', reverse=True)
+
+    def __mul__(self, other):
+        return _ufunc(self, other, 'broadcast_mul', '_mul_scalar')
+
+    def __imul__(self, other):
+        return _inplace(self, other, torch.Tensor.mul_, 'broadcast_mul', '_mul_scalar')
+
+    def __rmul__(self, other):
+        return self.__mul__(other)
+
+    def __truediv__(self, other):
+        return _ufunc(self, other, 'broadcast_div', '_div_scalar')
+
+    __div__ = __truediv__
+
+    def __itruediv__(self, other):
+        return _inplace(self, other, torch.Tensor.div_, 'broadcast_div', '_div_scalar')
+
+    __idiv__ = __itruediv__
+
+    def __rtruediv__(self, other):
+        return _ufunc(self, other, 'broadcast_div', '_rdiv_scalar', reverse=True)
+
+    __rdiv__ = __rtruediv__
+
+    def __mod__(self, other):
+        return _ufunc(self, other, 'broadcast_mod', '_mod_scalar')
+
+    def __rmod__(self, other):
+        return _ufunc(self, other, 'broadcast_mod', '_rmod_scalar', reverse=True)
+
+    def __imod__(self, other):
+        r = self.__mod__(other)
+        self._assign(r)
+        return self
+
+    def __pow__(self, other):
+        return _ufunc(self, other, 'broadcast_power', '_power_scalar')
+
+    def __rpow__(self, other):
+        return _ufunc(self, other, 'broadcast_power', '_rpower_scalar', reverse=True)
+
+    def __neg__(self):
+        return _op('negative', self)
+
+    def __pos__(self):
+        return self
+
+    def __abs__(self):
+        return _op('abs', self)
+
+    def __eq__(self, other):
+        if other is None:
+            return False
+        return _ufunc(self, other, 'broadcast_equal', '_equal_scalar')
+
+    def __ne__(self, other):
+        if other is None:
+            return True
+        return _ufunc(self, other, 'broadcast_not_equal', '_not_equal_scalar')
+
+    def __gt__(self, other):
+        return _ufunc(self, other, 'broadcast_greater', '_greater_scalar')
+
+    def __ge__(self, other):
+        return _ufunc(self, other, 'broadcast_greater_equal', '_greater_equal_scalar')
+
+    def __lt__(self, other):
+        return _ufunc(self, other, 'broadcast_lesser', '_lesser_scalar')
+
+    def __le__(self, other):
+        return _ufunc(self, other, 'broadcast_lesser_equal', '_lesser_equal_scalar')
+
+    def __matmul__(self, other):
+        return _op('dot', self, other)
+
+    def _assign(self, r):
+        if _state.STATE.recording and (self._data.requires_grad or r._data.requires_grad) and not self._data.is_leaf:
+            self._data = r._data
+        else:
+            with torch.no_grad():
+                self._data.copy_(r._data)
+
+    def __getattr__(self, name):
+        # fluent methods: a.sum(axis=1) -> nd.sum(a, axis=1)
+        if name.startswith('__'):
+            raise AttributeError(name)
+        from ..ops import registry
+        if name in _FLUENT and registry.has(_FLUENT[name]):
+            opname = _FLUENT[name]
+            return lambda *args, **kwargs: _op(opname, self, *args, **kwargs)
+        raise AttributeError("'NDArray' object has no attribute '%s'" % name)
+
+
+# fluent method name -> operator name
+_FLUENT = {n: n for n in [
+    'sum', 'mean', 'max', 'min', 'prod', 'nansum', 'nanprod', 'norm', 'argmax', 'argmin',
+    'argmax_channel', 'pick', 'clip', 'abs', 'sign', 'sqrt', 'rsqrt', 'cbrt', 'rcbrt', 'square',
+    'exp', 'expm1', 'log', 'log10', 'log2', 'log1p', 'sin', 'cos', 'tan', 'arcsin', 'arccos',
+    'arctan', 'sinh', 'cosh', 'tanh', 'arcsinh', 'arccosh', 'arctanh', 'degrees', 'radians',
+    'relu', 'sigmoid', 'softmax', 'log_softmax', 'softmin', 'round', 'rint', 'fix', 'floor',
+    'ceil', 'trunc', 'reciprocal', 'tile', 'repeat', 'pad', 'flip', 'sort', 'argsort', 'topk',
+    'take', 'one_hot', 'slice_axis', 'slice_like', 'swapaxes', 'depth_to_space', 'space_to_depth',
+    'shape_array', 'size_array', 'nanprod', 'gamma', 'gammaln', 'erf', 'erfinv', 'ones_like',
+    'log_sigmoid', 'mish', 'where', 'dot', 'batch_dot']}
+_FLUENT['broadcast_axes'] = 'broadcast_axes'
+_FLUENT['sum_axis'] = 'sum'
+_FLUENT['max_axis'] = 'max'
+_FLUENT['min_axis'] = 'min'
+
+
+def _rebuild(arr):
+    return NDArray(torch.from_numpy(np.ascontiguousarray(arr)))
+
+
+# ---------------------------------------------------------------------------
+# indexing helpers
+# ---------------------------------------------------------------------------
+
+def _convert_key(key):
+    if isinstance(key, NDArray):
+        t = key._data
+        return t.to(torch.int64) if t.is_floating_point() else t
+    if isinstance(key, np.ndarray):
+        return torch.as_tensor(key.astype(np.int64) if key.dtype.kind == 'f' else key)
+    if isinstance(key, list):
+        return torch.as_tensor(np.asarray(key, dtype=np.int64))
+    if isinstance(key, tuple):
+        return tuple(_convert_key(k) if isinstance(k, (NDArray, np.ndarray, list)) else
+                     (int(k) if isinstance(k, np.integer) else k) for k in key)
+    if isinstance(key, np.integer):
+        return int(key)
+    return key
+
+
+def _index_fn(t, key):
+    if isinstance(key, tuple):
+        key = tuple(k.to(t.device) if torch.is_tensor(k) else k for k in key)
+        neg = any(isinstance(k, slice) and k.step is not None and k.step < 0 for k in key)
+        if neg:
+            from ..ops.tensor import _neg_step_slice
+            full = list(key) + [slice(None)] * (t.dim() - len(key))
+            if all(isinstance(k, slice) for k in full):
+                return _neg_step_slice(t, full)
+    elif torch.is_tensor(key):
+        key = key.to(t.device)
+    elif isinstance(key, slice) and key.step is not None and key.step < 0:
+        from ..ops.tensor import _neg_step_slice
+        return _neg_step_slice(t, [key])
+    return t[key]
+
+
+# ---------------------------------------------------------------------------
+# op invocation helpers
+# ---------------------------------------------------------------------------
+
+def _op(name, *args, **kwargs):
+    from .register import invoke_by_name
+    return invoke_by_name(name, args, kwargs)
+
+
+def _invoke_unary(fn, arr):
+    from .register import invoke_fn
+    return invoke_fn(fn, [arr])
+
+
+def _ufunc(lhs, rhs, bop, sop, reverse=False):
+    if isinstance(rhs, NDArray):
+        if reverse:
+            return _op(bop, rhs, lhs)
+        return _op(bop, lhs, rhs)
+    if isinstance(rhs, numeric_types):
+        return _op(sop, lhs, scalar=float(rhs) if not isinstance(rhs, bool) else float(rhs))
+    if isinstance(rhs, np.ndarray):
+        other = array(rhs, ctx=lhs.context, dtype=lhs.dtype)
+        return _ufunc(lhs, other, bop, sop, reverse)
+    return NotImplemented
+
+
+def _inplace(self, other, torch_fn, bop, sop):
+    if _state.STATE.recording and (self._data.requires_grad or
+                                   (isinstance(other, NDArray) and other._data.requires_grad)):
+        r = _ufunc(self, other, bop, sop)
+        self._data = r._data
+        return self
+    o = other._data if isinstance(other, NDArray) else other
+    with torch.no_grad():
+        if torch.is_tensor(o) and o.shape != self._data.shape:
+            torch_fn(self._data, o.expand_as(self._data) if o.dim() <= self._data.dim() else o)
+        else:
+            torch_fn(self._data, o)
+    return self
+
+
+# ---------------------------------------------------------------------------
+# creation functions
+# ---------------------------------------------------------------------------
+
+def _ctx(ctx):
+    return ctx if ctx is not None else current_context()
+
+
+def array(source_array, ctx=None, dtype=None):
+    """Create an NDArray from any array-like (float32 by default, like MXNet)."""
+    ctx = _ctx(ctx)
+    if isinstance(source_array, NDArray):
+        dt = torch_dtype(dtype) if dtype is not None else source_array._data.dtype
+        return NDArray(source_array._data.detach().to(device=ctx.torch_device, dtype=dt, copy=True))
+    if isinstance(source_array, torch.Tensor):
+        dt = torch_dtype(dtype) if dtype is not None else source_array.dtype
+        return NDArray(source_array.detach().to(device=ctx.torch_device, dtype=dt, copy=True))
+    if isinstance(source_array, np.ndarray):
+        dt = dtype if dtype is not None else source_array.dtype
+    else:
+        dt = dtype if dtype is not None else np.float32
+        source_array = np.asarray(source_array, dtype=None if dtype is None else None)
+    td = torch_dtype(dt)
+    if td == torch.bfloat16:
+        t = torch.from_numpy(np.ascontiguousarray(np.asarray(source_array, dtype=np.float32))).to(td)
+    else:
+        npd = np.dtype(np_dtype(td)) if td != torch.bfloat16 else np.float32
+        t = torch.from_numpy(np.array(source_array, dtype=npd, copy=True))
+    if ctx.device_typeid == 3:
+        t = t.pin_memory() if torch.cuda.is_available() else t
+    return NDArray(t.to(ctx.torch_device) if ctx.device_typeid == 2 else t)
+
+
+def from_numpy(ndarray, zero_copy=True):
+    return NDArray(torch.from_numpy(ndarray))
+
+
+def from_dlpack(dlpack):
+    return NDArray(torch.utils.dlpack.from_dlpack(dlpack))
+
+
+def to_dlpack_for_read(data):
+    return data.to_dlpack_for_read()
+
+
+def to_dlpack_for_write(data):
+    return data.to_dlpack_for_write()
+
+
+def empty(shape, ctx=None, dtype=None, stype=None):
+    if isinstance(shape, int):
+        shape = (shape,)
+    return NDArray(torch.empty(shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device))
+
+
+def zeros(shape, ctx=None, dtype=None, stype=None, **kwargs):
+    if isinstance(shape, int):
+        shape = (shape,)
+    if stype not in (None, 'default'):
+        from . import sparse
+        return sparse.zeros(stype, shape, ctx=ctx, dtype=dtype)
+    return NDArray(torch.zeros(shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device))
+
+
+def ones(shape, ctx=None, dtype=None, **kwargs):
+    if isinstance(shape, int):
+        shape = (shape,)
+    return NDArray(torch.ones(shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device))
+
+
+def full(shape, val, ctx=None, dtype=np.float32, out=None):
+    if isinstance(shape, int):
+        shape = (shape,)
+    r = NDArray(torch.full(shape, val, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device))
+    if out is not None:
+        out[:] = r
+        return out
+    return r
+
+
+def eye(N, M=0, k=0, ctx=None, dtype=None):
+    return _op('_eye', N=N, M=M, k=k, ctx=_ctx(ctx), dtype=dtype_name(dtype or np.float32))
+
+
+def arange(start, stop=None, step=1.0, repeat=1, infer_range=None, ctx=None, dtype=np.float32):
+    if stop is None:
+        start, stop = 0, start
+    return _op('_arange', start=start, stop=stop, step=step, repeat=repeat, ctx=_ctx(ctx),
+               dtype=dtype_name(dtype))
+
+
+def linspace(start, stop, num, endpoint=True, ctx=None, dtype=np.float32):
+    return _op('_linspace', start=start, stop=stop, num=num, endpoint=endpoint, ctx=_ctx(ctx),
+               dtype=dtype_name(dtype))
+
+
+def zeros_like(data, **kwargs):
+    return _op('zeros_like', data)
+
+
+def ones_like(data, **kwargs):
+    return _op('ones_like', data)
+
+
+def concatenate(arrays, axis=0, always_copy=True):
+    return _op('Concat', *arrays, dim=axis, num_args=len(arrays))
+
+
+def moveaxis(tensor, source, destination):
+    return NDArray(torch.movedim(tensor._data, source, destination).contiguous())
+
+
+def waitall():
+    """Block until all pending device work and engine work has completed."""
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+    from .. import engine
+    engine.wait_all()
+
+
+def onehot_encode(indices, out):
+    r = _op('one_hot', indices, depth=out.shape[1], dtype=dtype_name(out.dtype))
+    out[:] = r
+    return out
+
+
+def split_v2(ary, indices_or_sections, axis=0, squeeze_axis=False):
+    if isinstance(indices_or_sections, int):
+        return _op('_split_v2', ary, axis=axis, squeeze_axis=squeeze_axis, sections=indices_or_sections)
+    return _op('_split_v2', ary, axis=axis, squeeze_axis=squeeze_axis,
+               indices=(0,) + tuple(indices_or_sections))
+
+
+def histogram(a, bins=10, range=None):
+    if isinstance(bins, NDArray):
+        return _op('_histogram', a, bins)
+    return _op('_histogram', a, bin_cnt=bins, range=range)
+
+
+def _binary_helper(lhs, rhs, bop, sop, rsop=None):
+    if isinstance(lhs, NDArray):
+        return _ufunc(lhs, rhs, bop, sop)
+    if isinstance(rhs, NDArray):
+        if rsop is None:
+            return _ufunc(rhs, lhs, bop, sop)
+        return _ufunc(rhs, lhs, bop, rsop, reverse=True)
+    return {'broadcast_add': lambda a, b: a + b}.get(bop, lambda a, b: None)(lhs, rhs)
+
+
+def add(lhs, rhs):
+    return _binary_helper(lhs, rhs, 'broadcast_add', '_plus_scalar')
+
+
+def subtract(lhs, rhs):
+    return _binary_helper(lhs, rhs, 'broadcast_sub', '_minus_scalar', '_rminus_scalar')
+
+
+def multiply(lhs, rhs):
+    return _binary_helper(lhs, rhs, 'broadcast_mul', '_mul_scalar')
+
+
+def divide(lhs, rhs):
+    return _binary_helper(lhs, rhs, 'broadcast_div', '_div_scalar', '_rdiv_scalar')
+
+
+true_divide = divide
+
+
+def modulo(lhs, rhs):
+    return _binary_helper(lhs, rhs, 'broadcast_mod', '_mod_scalar', '_rmod_scalar')
+
+
+def power(base, exp):
+    return _binary_helper(base, exp, 'broadcast_power', '_power_scalar', '_rpower_scalar')
+
+
+def maximum(lhs, rhs):
+    return _binary_helper(lhs, rhs, 'broadcast_maximum', '_maximum_scalar')
+
+
+def minimum(lhs, rhs):
+    return _binary_helper(lhs, rhs, 'broadcast_minimum', '_minimum_scalar')
+
+
+def equal(lhs, rhs):
+    return _binary_helper(lhs, rhs, 'broadcast_equal', '_equal_scalar')
+
+
+def not_equal(lhs, rhs):
+    return _binary_helper(lhs, rhs, 'broadcast_not_equal', '_not_equal_scalar')
+
+
+def greater(lhs, rhs):
+    return _binary_helper(lhs, rhs, 'broadcast_greater', '_greater_scalar', '_lesser_scalar')
+
+
+def greater_equal(lhs, rhs):
+    return _binary_helper(lhs, rhs, 'broadcast_greater_equal', '_greater_equal_scalar', '_lesser_equal_scalar')
+
+
+def lesser(lhs, rhs):
+    return _binary_helper(lhs, rhs, 'broadcast_lesser', '_lesser_scalar', '_greater_scalar')
+
+
+def lesser_equal(lhs, rhs):
+    return _binary_helper(lhs, rhs, 'broadcast_lesser_equal', '_lesser_equal_scalar', '_greater_equal_scalar')
+
+
+def logical_and(lhs, rhs):
+    return _binary_helper(lhs, rhs, 'broadcast_logical_and', '_logical_and_scalar')
+
+
+def logical_or(lhs, rhs):
+    return _binary_helper(lhs, rhs, 'broadcast_logical_or', '_logical_or_scalar')
+
+
+def logical_xor(lhs, rhs):
+    return _binary_helper(lhs, rhs, 'broadcast_logical_xor', '_logical_xor_scalar')
+
+
+def negative(arr):
+    return _op('negative', arr)

@@ -1,0 +1,171 @@
+"""Random sampling (mx.nd.random).
+
+Parity: python/mxnet/ndarray/random.py and src/operator/random/*.cc
+(sample_op, multisample_op, sample_multinomial_op, shuffle_op).  Sampling runs
+on the device's torch generator (Philox on HIP).
+"""
+import numpy as np
+import torch
+
+from ..base import torch_dtype, numeric_types
+from ..context import current_context
+from .ndarray import NDArray
+
+__all__ = ['uniform', 'normal', 'randn', 'randint', 'exponential', 'gamma', 'poisson',
+           'negative_binomial', 'generalized_negative_binomial', 'multinomial', 'shuffle',
+           'bernoulli', 'uniform_like', 'normal_like', 'categorical']
+
+
+def _shape(shape):
+    if shape is None or shape == ():
+        return (1,)
+    if isinstance(shape, int):
+        return (shape,)
+    return tuple(shape)
+
+
+def _dev(ctx):
+    return (ctx or current_context()).torch_device
+
+
+def _out(t, out):
+    if out is not None:
+        out._data.copy_(t.reshape(out.shape))
+        return out
+    return NDArray(t)
+
+
+def _param(p, dev):
+    return p._data.to(dev) if isinstance(p, NDArray) else p
+
+
+def uniform(low=0, high=1, shape=None, dtype=None, ctx=None, out=None, **kwargs):
+    if isinstance(low, NDArray) or isinstance(high, NDArray):
+        lo = low._data if isinstance(low, NDArray) else torch.tensor(low)
+        hi = high._data if isinstance(high, NDArray) else torch.tensor(high)
+        s = _shape(shape) if shape else ()
+        base = torch.rand(tuple(lo.shape) + s, device=lo.device, dtype=lo.dtype if lo.is_floating_point() else torch.float32)
+        lo = lo.reshape(tuple(lo.shape) + (1,) * len(s))
+        hi = hi.reshape(tuple(hi.shape) + (1,) * len(s))
+        return _out(lo + (hi - lo) * base, out)
+    dev = _dev(ctx) if out is None else out._data.device
+    s = _shape(shape) if out is None else out.shape
+    dt = torch_dtype(dtype) if dtype is not None else (out._data.dtype if out is not None else torch.float32)
+    t = torch.empty(s, dtype=dt, device=dev).uniform_(low, high)
+    return _out(t, out)
+
+
+def normal(loc=0, scale=1, shape=None, dtype=None, ctx=None, out=None, **kwargs):
+    if isinstance(loc, NDArray) or isinstance(scale, NDArray):
+        mu = loc._data if isinstance(loc, NDArray) else torch.tensor(loc)
+        sd = scale._data if isinstance(scale, NDArray) else torch.tensor(scale)
+        s = _shape(shape) if shape else ()
+        base = torch.randn(tuple(mu.shape) + s, device=mu.device, dtype=mu.dtype)
+        mu = mu.reshape(tuple(mu.shape) + (1,) * len(s))
+        sd = sd.reshape(tuple(sd.shape) + (1,) * len(s))
+        return _out(mu + sd * base, out)
+    dev = _dev(ctx) if out is None else out._data.device
+    s = _shape(shape) if out is None else out.shape
+    dt = torch_dtype(dtype) if dtype is not None else (out._data.dtype if out is not None else torch.float32)
+    t = torch.empty(s, dtype=dt, device=dev).normal_(loc, scale)
+    return _out(t, out)
+
+
+def randn(*shape, **kwargs):
+    loc = kwargs.pop('loc', 0)
+    scale = kwargs.pop('scale', 1)
+    return normal(loc, scale, shape or None, **kwargs)
+
+
+def randint(low, high, shape=None, dtype=None, ctx=None, out=None, **kwargs):
+    dt = torch_dtype(dtype or 'int32')
+    t = torch.randint(int(low), int(high), _shape(shape), dtype=dt, device=_dev(ctx))
+    return _out(t, out)
+
+
+def exponential(scale=1, shape=None, dtype=None, ctx=None, out=None, **kwargs):
+    if isinstance(scale, NDArray):
+        s = _shape(shape) if shape else ()
+        lam = scale._data.reshape(tuple(scale.shape) + (1,) * len(s))
+        e = torch.empty(tuple(scale.shape) + s, device=lam.device, dtype=lam.dtype).exponential_(1.0)
+        return _out(e * lam, out)
+    t = torch.empty(_shape(shape), dtype=torch_dtype(dtype), device=_dev(ctx)).exponential_(1.0 / scale)
+    return _out(t, out)
+
+
+def gamma(alpha=1, beta=1, shape=None, dtype=None, ctx=None, out=None, **kwargs):
+    if isinstance(alpha, NDArray) or isinstance(beta, NDArray):
+        a = alpha._data if isinstance(alpha, NDArray) else torch.tensor(float(alpha))
+        b = beta._data if isinstance(beta, NDArray) else torch.tensor(float(beta))
+        s = _shape(shape) if shape else ()
+        a = a.reshape(tuple(a.shape) + (1,) * len(s)).expand(tuple(a.shape) + s)
+        b = b.reshape(tuple(b.shape) + (1,) * len(s)).expand(tuple(b.shape) + s)
+        return _out(torch.distributions.Gamma(a.float(), 1.0 / b.float()).sample(), out)
+    dev = _dev(ctx)
+    a = torch.full(_shape(shape), float(alpha), device=dev)
+    t = torch._standard_gamma(a) * beta
+    return _out(t.to(torch_dtype(dtype)), out)
+
+
+def poisson(lam=1, shape=None, dtype=None, ctx=None, out=None, **kwargs):
+    if isinstance(lam, NDArray):
+        s = _shape(shape) if shape else ()
+        l = lam._data.reshape(tuple(lam.shape) + (1,) * len(s)).expand(tuple(lam.shape) + s)
+        return _out(torch.poisson(l.float()).to(lam._data.dtype), out)
+    t = torch.poisson(torch.full(_shape(shape), float(lam), device=_dev(ctx)))
+    return _out(t.to(torch_dtype(dtype)), out)
+
+
+def negative_binomial(k=1, p=1, shape=None, dtype=None, ctx=None, out=None, **kwargs):
+    dev = _dev(ctx)
+    s = _shape(shape)
+    g = torch._standard_gamma(torch.full(s, float(k), device=dev)) * ((1 - p) / p)
+    return _out(torch.poisson(g).to(torch_dtype(dtype)), out)
+
+
+def generalized_negative_binomial(mu=1, alpha=1, shape=None, dtype=None, ctx=None, out=None, **kwargs):
+    dev = _dev(ctx)
+    s = _shape(shape)
+    if alpha == 0:
+        return _out(torch.poisson(torch.full(s, float(mu), device=dev)).to(torch_dtype(dtype)), out)
+    g = torch._standard_gamma(torch.full(s, 1.0 / alpha, device=dev)) * (mu * alpha)
+    return _out(torch.poisson(g).to(torch_dtype(dtype)), out)
+
+
+def multinomial(data, shape=None, get_prob=False, out=None, dtype='int32', **kwargs):
+    p = data._data.float()
+    n = int(np.prod(_shape(shape))) if shape else 1
+    flat = p.reshape(-1, p.shape[-1])
+    idx = torch.multinomial(flat, n, replacement=True)
+    oshape = tuple(p.shape[:-1]) + (_shape(shape) if shape else ())
+    idx = idx.reshape(oshape if oshape else (1,))
+    res = NDArray(idx.to(torch_dtype(dtype)))
+    if get_prob:
+        lp = torch.log(torch.gather(flat, 1, idx.reshape(flat.shape[0], -1).to(torch.int64)))
+        return res, NDArray(lp.reshape(idx.shape).to(data._data.dtype))
+    return res
+
+
+categorical = multinomial
+
+
+def shuffle(data, **kwargs):
+    perm = torch.randperm(data.shape[0], device=data._data.device)
+    return NDArray(data._data[perm])
+
+
+def bernoulli(prob=None, logit=None, size=None, dtype=None, ctx=None, out=None):
+    if prob is None:
+        prob = torch.sigmoid(logit._data if isinstance(logit, NDArray) else torch.tensor(logit))
+    else:
+        prob = prob._data if isinstance(prob, NDArray) else torch.full(_shape(size), float(prob), device=_dev(ctx))
+    t = torch.bernoulli(prob.float())
+    return _out(t.to(torch_dtype(dtype)), out)
+
+
+def uniform_like(data, low=0, high=1, **kwargs):
+    return NDArray(torch.empty_like(data._data).uniform_(low, high))
+
+
+def normal_like(data, loc=0, scale=1, **kwargs):
+    return NDArray(torch.empty_like(data._data).normal_(loc, scale))

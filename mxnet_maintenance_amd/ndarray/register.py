@@ -1,0 +1,141 @@
+"""Imperative operator invocation and ``mx.nd.*`` function generation.
+
+Parity: python/mxnet/ndarray/register.py (_make_ndarray_function) and
+src/imperative/imperative.cc (Imperative::Invoke / RecordOp).  Instead of
+generating ctypes stubs we bind each registered OpDef to a Python function that
+runs the op's torch-level implementation under the right autograd mode.
+"""
+import torch
+
+from .. import _state
+from ..base import MXNetError
+from ..ops import registry
+from .ndarray import NDArray
+
+_SKIP_KW = ('name', 'attr', 'out')
+
+
+def _split_args(op, args, kwargs):
+    """Split python call arguments into (inputs, attrs, out)."""
+    out = kwargs.pop('out', None)
+    kwargs.pop('name', None)
+    kwargs.pop('attr', None)
+    attrs = {}
+    inputs_pos = []
+    extra_pos = []
+    for a in args:
+        if isinstance(a, NDArray) or (a is None and not extra_pos):
+            inputs_pos.append(a)
+        elif isinstance(a, (list, tuple)) and a and all(isinstance(x, NDArray) for x in a) and not extra_pos:
+            inputs_pos.extend(a)
+        else:
+            extra_pos.append(a)
+    named_inputs = {}
+    for k, v in list(kwargs.items()):
+        if isinstance(v, NDArray):
+            named_inputs[k] = v
+        elif v is None:
+            continue
+        else:
+            attrs[k] = v
+    if op.key_var_num_args and op.key_var_num_args not in attrs:
+        attrs[op.key_var_num_args] = len(inputs_pos) + len(named_inputs)
+    pattrs = op.parse_attrs(attrs)
+    if extra_pos:
+        # positional attribute values follow the declared param order
+        pnames = [p for p in op.params if p not in attrs]
+        for p, v in zip(pnames, extra_pos):
+            pattrs[p] = registry.parse_value(op.params[p][0], v) if isinstance(v, str) else v
+    arg_names = op.get_arg_names(pattrs) + op.get_aux_names(pattrs)
+    if named_inputs:
+        inputs = list(inputs_pos) + [None] * max(0, len(arg_names) - len(inputs_pos))
+        for k, v in named_inputs.items():
+            if k in arg_names:
+                inputs[arg_names.index(k)] = v
+            else:
+                inputs.append(v)
+        while inputs and inputs[-1] is None:
+            inputs.pop()
+    else:
+        inputs = inputs_pos
+    return inputs, pattrs, out
+
+
+def _run(fn, tinputs, kw):
+    rec = _state.STATE.recording
+    if torch.is_grad_enabled() != rec:
+        prev = not rec
+        torch._C._set_grad_enabled(rec)
+        try:
+            return fn(*tinputs, **kw)
+        finally:
+            torch._C._set_grad_enabled(prev)
+    return fn(*tinputs, **kw)
+
+
+def _note_leaves(inputs):
+    if _state.STATE.recording:
+        tl = _state.STATE.tape_leaves
+        for x in inputs:
+            if x is not None and x._grad_req is not None:
+                tl[id(x)] = x
+
+
+def invoke(op, inputs, attrs, out=None):
+    """Run ``op`` on NDArray ``inputs`` with parsed ``attrs``."""
+    tin = [None if x is None else x._data for x in inputs]
+    _note_leaves(inputs)
+    res = _run(op.fn, tin, attrs)
+    nvis = op.get_num_visible_outputs(attrs)
+    if isinstance(res, (tuple, list)):
+        outs = [NDArray(r) for r in res[:nvis]]
+    else:
+        outs = [NDArray(res)]
+    if out is not None:
+        targets = out if isinstance(out, (list, tuple)) else [out]
+        for t, o in zip(targets, outs):
+            if _state.STATE.recording and o._data.requires_grad:
+                t._data = o._data
+            else:
+                with torch.no_grad():
+                    t._data.copy_(o._data.reshape(t.shape) if o.shape != t.shape and o.size == t.size else o._data)
+        return out
+    if len(outs) == 1:
+        return outs[0]
+    return outs
+
+
+def invoke_by_name(name, args, kwargs):
+    op = registry.get(name)
+    inputs, attrs, out = _split_args(op, args, dict(kwargs))
+    return invoke(op, inputs, attrs, out)
+
+
+def invoke_fn(fn, arrays):
+    """Run an ad-hoc torch function (reshape, astype, ...) with autograd semantics."""
+    _note_leaves(arrays)
+    res = _run(fn, [a._data for a in arrays], {})
+    return NDArray(res)
+
+
+def make_op_function(name):
+    op = registry.get(name)
+
+    def f(*args, **kwargs):
+        inputs, attrs, out = _split_args(op, args, dict(kwargs))
+        return invoke(op, inputs, attrs, out)
+    f.__name__ = name
+    f.__qualname__ = name
+    params = ', '.join('%s=%r' % (k, v[1]) for k, v in op.params.items())
+    args = op.arg_names if not callable(op.arg_names) else ['*data']
+    f.__doc__ = '%s(%s%s%s)\n\nMXNet operator `%s` (see src/operator for reference semantics).' % (
+        name, ', '.join(args), ', ' if params else '', params, name)
+    return f
+
+
+def populate(namespace, prefix_map=None):
+    """Fill ``namespace`` (a dict) with functions for every registered op."""
+    for name in registry.list_ops():
+        if name not in namespace:
+            namespace[name] = make_op_function(name)
+    return namespace

@@ -1,0 +1,10 @@
+"""Operator library: registry + implementations (torch reference + gfx950 HIP kernels)."""
+_loaded = False
+
+
+def load_all():
+    global _loaded
+    if _loaded:
+        return
+    _loaded = True
+    from . import tensor, nn, optimizer_ops, misc_ops, detection  # noqa: F401

@@ -1,0 +1,230 @@
+"""Dispatch layer between operator definitions and the gfx950 HIP kernels.
+
+Every hot operator (FullyConnected, Convolution, BatchNorm(+ReLU/+add),
+Pooling, ReLU/GELU, LayerNorm, softmax-cross-entropy) goes through a function
+here. On an MI355X with the native extension loaded, the hand-written HIP
+kernels in ``src/kernels/*.hip`` run (wrapped as ``torch.autograd.Function``
+so they compose with the autograd tape); on the CPU the torch reference path
+runs. On a GPU box a missing extension is an error, not a silent fallback
+(set ``MXAMD_ALLOW_TORCH_FALLBACK=1`` to override while debugging).
+
+Parity targets: src/operator/nn/{fully_connected,convolution,batch_norm,
+pooling,activation,layer_norm,softmax}*.cu and the cuDNN wrappers in
+src/operator/nn/cudnn/*.
+"""
+import os
+
+import torch
+import torch.nn.functional as F
+
+from ..base import MXNetError
+from . import kernels as _K
+
+_ALLOW_FALLBACK = os.environ.get('MXAMD_ALLOW_TORCH_FALLBACK', '0') == '1'
+
+
+def _use_hip(t):
+    """True when ``t`` lives on the GPU and the HIP kernels should run."""
+    if not t.is_cuda:
+        return False
+    if _K.available():
+        return _K.enabled()
+    if _ALLOW_FALLBACK:
+        return False
+    raise MXNetError('HIP kernel extension not loaded on a GPU device: %s' % _K.load_error())
+
+
+def _nd_to_ncx(x):
+    nd = x.dim()
+    return x.permute(0, nd - 1, *range(1, nd - 1))
+
+
+def _ncx_to_nd(x):
+    nd = x.dim()
+    return x.permute(0, *range(2, nd), 1)
+
+
+# ---------------------------------------------------------------------------
+# GEMM-shaped ops
+# ---------------------------------------------------------------------------
+
+def linear(data, weight, bias):
+    """y = data @ weight.T + bias (FullyConnected)."""
+    if _use_hip(data) and _K.gemm_ok(data, weight):
+        return _K.Linear.apply(data, weight, bias)
+    if data.dim() == 2:
+        return F.linear(data, weight, bias)
+    return F.linear(data, weight, bias)
+
+
+def conv(data, weight, bias, stride, pad, dilate, groups, channel_last):
+    nsp = data.dim() - 2
+    if channel_last:
+        if _use_hip(data) and _K.conv_ok(data, weight, stride, pad, dilate, groups):
+            return _K.ConvNHWC.apply(data, weight, bias, tuple(stride), tuple(pad), tuple(dilate))
+        x = _nd_to_ncx(data)
+        w = _nd_to_ncx(weight)
+    else:
+        x, w = data, weight
+    fn = {1: F.conv1d, 2: F.conv2d, 3: F.conv3d}[nsp]
+    y = fn(x, w, bias, stride=stride, padding=pad, dilation=dilate, groups=groups)
+    return _ncx_to_nd(y) if channel_last else y
+
+
+# ---------------------------------------------------------------------------
+# BatchNorm
+# ---------------------------------------------------------------------------
+
+def batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_gamma, training,
+               axis, act_type, addend=None):
+    """BatchNorm with MXNet semantics; returns (out, mean, var).
+
+    ``moving_* = moving_* * momentum + batch_* * (1 - momentum)`` (biased
+    variance, src/operator/nn/batch_norm.cc).  ``act_type='relu'`` fuses
+    ReLU; ``addend`` fuses the residual add before the ReLU.
+    """
+    nd = data.dim()
+    axis = axis % nd
+    channel_last = (axis == nd - 1) and nd > 2
+    g = torch.ones_like(gamma) if fix_gamma else gamma
+    if channel_last and _use_hip(data) and _K.bn_ok(data):
+        out, mean, var = _K.BatchNormNHWC.apply(data, g, beta, addend, eps, training,
+                                                act_type == 'relu', moving_mean, moving_var)
+        if training:
+            with torch.no_grad():
+                moving_mean.mul_(momentum).add_(mean.to(moving_mean.dtype), alpha=1 - momentum)
+                moving_var.mul_(momentum).add_(var.to(moving_var.dtype), alpha=1 - momentum)
+        return out, mean, var
+    if channel_last:
+        x = _nd_to_ncx(data)
+    elif axis != 1:
+        perm = [0, axis] + [i for i in range(1, nd) if i != axis]
+        x = data.permute(*perm)
+    else:
+        x = data
+    if training:
+        out, smean, sinvstd = torch.ops.aten.native_batch_norm(x, g, beta, None, None, True, 0.0, eps)
+        with torch.no_grad():
+            var = (1.0 / (sinvstd.float() ** 2) - eps).clamp_(min=0.0) if sinvstd.numel() else sinvstd
+            moving_mean.mul_(momentum).add_(smean.detach().to(moving_mean.dtype), alpha=1 - momentum)
+            moving_var.mul_(momentum).add_(var.to(moving_var.dtype), alpha=1 - momentum)
+        mean_out, var_out = smean, var
+    else:
+        out = F.batch_norm(x, moving_mean, moving_var, g, beta, False, 0.0, eps)
+        mean_out, var_out = moving_mean, moving_var
+    if channel_last:
+        out = _ncx_to_nd(out)
+    elif axis != 1:
+        inv = [0] * nd
+        perm = [0, axis] + [i for i in range(1, nd) if i != axis]
+        for i, p in enumerate(perm):
+            inv[p] = i
+        out = out.permute(*inv)
+    if addend is not None:
+        out = out + addend
+    if act_type == 'relu':
+        out = torch.relu(out)
+    return out, mean_out, var_out
+
+
+# ---------------------------------------------------------------------------
+# Pooling
+# ---------------------------------------------------------------------------
+
+def global_pool(data, pool_type, channel_last):
+    nsp = data.dim() - 2
+    if channel_last:
+        if _use_hip(data) and nsp == 2 and pool_type == 'avg':
+            return _K.GlobalAvgPoolNHWC.apply(data)
+        dims = tuple(range(1, 1 + nsp))
+    else:
+        dims = tuple(range(2, 2 + nsp))
+    if pool_type == 'max':
+        return torch.amax(data, dim=dims, keepdim=True)
+    if pool_type == 'sum':
+        return torch.sum(data, dim=dims, keepdim=True)
+    if pool_type == 'lp':
+        return torch.sqrt(torch.sum(data * data, dim=dims, keepdim=True))
+    return torch.mean(data, dim=dims, keepdim=True)
+
+
+def _pool_out(n, k, s, p, conv):
+    if conv == 'full':
+        return int(-(-(n + 2 * p - k) // s)) + 1
+    return (n + 2 * p - k) // s + 1
+
+
+def pool(data, pool_type, kernel, stride, pad, convention, count_include_pad, channel_last, p_value=None):
+    nsp = data.dim() - 2
+    if channel_last and _use_hip(data) and nsp == 2 and pool_type in ('max', 'avg') \
+            and _K.pool_ok(data, kernel, stride, pad):
+        return _K.PoolNHWC.apply(data, pool_type, tuple(kernel), tuple(stride), tuple(pad),
+                                 convention == 'full', bool(count_include_pad))
+    x = _nd_to_ncx(data) if channel_last else data
+    ceil = convention == 'full'
+    pad_r = list(pad)
+    if convention == 'same':
+        ceil = False
+        for i in range(nsp):
+            n = x.shape[2 + i]
+            out = -(-n // stride[i])
+            tot = max((out - 1) * stride[i] + kernel[i] - n, 0)
+            pad_r[i] = tot // 2
+    if pool_type == 'max':
+        fn = {1: F.max_pool1d, 2: F.max_pool2d, 3: F.max_pool3d}[nsp]
+        y = fn(x, kernel, stride, pad_r, ceil_mode=ceil)
+    elif pool_type == 'avg':
+        fn = {1: F.avg_pool1d, 2: F.avg_pool2d, 3: F.avg_pool3d}[nsp]
+        y = fn(x, kernel, stride, pad_r, ceil_mode=ceil, count_include_pad=count_include_pad)
+    elif pool_type == 'sum':
+        fn = {1: F.avg_pool1d, 2: F.avg_pool2d, 3: F.avg_pool3d}[nsp]
+        y = fn(x, kernel, stride, pad_r, ceil_mode=ceil, count_include_pad=True) * float(torch.tensor(kernel).prod())
+    elif pool_type == 'lp':
+        pv = p_value or 2
+        fn = {1: F.lp_pool1d, 2: F.lp_pool2d, 3: F.lp_pool3d}[nsp]
+        if any(pad_r):
+            x = F.pad(x, [q for pp in reversed(pad_r) for q in (pp, pp)])
+        y = fn(x, pv, kernel, stride, ceil_mode=ceil)
+    else:
+        raise MXNetError('unknown pool_type %s' % pool_type)
+    return _ncx_to_nd(y) if channel_last else y
+
+
+# ---------------------------------------------------------------------------
+# elementwise / normalisation
+# ---------------------------------------------------------------------------
+
+def relu(x):
+    return torch.relu(x)
+
+
+def gelu(x):
+    if _use_hip(x) and _K.ew_ok(x):
+        return _K.GELU.apply(x)
+    return F.gelu(x)
+
+
+def layer_norm(data, gamma, beta, eps):
+    """LayerNorm over the last axis; returns (out, mean, std)."""
+    if _use_hip(data) and _K.ln_ok(data):
+        return _K.LayerNorm.apply(data, gamma, beta, eps)
+    x = data.float()
+    mean = x.mean(-1, keepdim=True)
+    var = x.var(-1, keepdim=True, unbiased=False)
+    std = torch.sqrt(var + eps)
+    y = (x - mean) / std * gamma.float() + beta.float()
+    return y.to(data.dtype), mean.to(data.dtype), std.to(data.dtype)
+
+
+def softmax_ce(logits, label, reduction='none'):
+    """Cross entropy of softmax(logits) against integer labels (fp32 accumulation)."""
+    if _use_hip(logits) and _K.ce_ok(logits):
+        loss = _K.SoftmaxCE.apply(logits, label)
+    else:
+        lg = logits.float() if logits.dtype in (torch.float16, torch.bfloat16) else logits
+        loss = F.cross_entropy(lg, label.to(torch.int64), reduction='none')
+    if reduction == 'sum':
+        return loss.sum()
+    if reduction == 'mean':
+        return loss.mean()
+    return loss

@@ -1,0 +1,79 @@
+"""Loader + autograd wrappers for the gfx950 HIP kernel extension.
+
+The extension ``mxnet_maintenance_amd/_lib/_hip_kernels*.so`` is built in-tree
+by ``tools/build_native.py`` (hipcc --offload-arch=gfx950) from
+``src/kernels/*.hip``.  Launch functions take raw device pointers plus the
+current HIP stream, so every kernel is capturable in a HIP graph.
+"""
+import os
+
+_mod = None
+_err = None
+_tried = False
+
+
+def _load():
+    global _mod, _err, _tried
+    if _tried:
+        return _mod
+    _tried = True
+    try:
+        from .._lib import _hip_kernels as m  # noqa
+        _mod = m
+    except Exception as e:  # pragma: no cover - depends on build
+        _err = repr(e)
+        _mod = None
+    return _mod
+
+
+def available():
+    return _load() is not None
+
+
+def load_error():
+    _load()
+    return _err
+
+
+def enabled():
+    return os.environ.get('MXAMD_DISABLE_HIP', '0') != '1'
+
+
+def lib():
+    m = _load()
+    if m is None:
+        raise RuntimeError('HIP kernel extension not available: %s' % _err)
+    return m
+
+
+# Shape/dtype predicates: which calls the kernels support.  Anything else
+# takes the torch path (which on ROCm is itself MIOpen/hipBLASLt).
+def gemm_ok(x, w):
+    return False
+
+
+def conv_ok(x, w, stride, pad, dilate, groups):
+    return False
+
+
+def pool_ok(x, kernel, stride, pad):
+    return False
+
+
+def ew_ok(x):
+    return False
+
+
+def ln_ok(x):
+    return False
+
+
+def ce_ok(x):
+    return False
+
+
+def bn_ok(x):
+    return False
+
+
+from .kernel_fns import *  # noqa: E402,F401,F403

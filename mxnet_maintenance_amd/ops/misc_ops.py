@@ -1,0 +1,335 @@
+"""Random, linear-algebra and image operators.
+
+Parity: src/operator/random/sample_op.cc, multisample_op.cc, shuffle_op.cc;
+src/operator/tensor/la_op.cc (_linalg_*); src/operator/image/*.cc (_image_*).
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from ..base import torch_dtype
+from .registry import register
+from .tensor import _dev
+
+# ---------------------------------------------------------------------------
+# random (symbol-callable; mx.nd.random has richer python wrappers)
+# ---------------------------------------------------------------------------
+
+_RP = {'shape': ('shape', ()), 'ctx': ('any', None), 'dtype': ('str', 'float32')}
+
+
+def _s(shape):
+    return tuple(shape) if shape else (1,)
+
+
+@register('_random_uniform', aliases=('uniform', 'random_uniform'), arg_names=(),
+          params=dict(_RP, low=('float', 0.0), high=('float', 1.0)))
+def random_uniform(low=0.0, high=1.0, shape=(), ctx=None, dtype='float32'):
+    return torch.empty(_s(shape), dtype=torch_dtype(dtype if dtype != 'None' else 'float32'),
+                       device=_dev(ctx)).uniform_(low, high)
+
+
+@register('_random_normal', aliases=('normal', 'random_normal'), arg_names=(),
+          params=dict(_RP, loc=('float', 0.0), scale=('float', 1.0)))
+def random_normal(loc=0.0, scale=1.0, shape=(), ctx=None, dtype='float32'):
+    return torch.empty(_s(shape), dtype=torch_dtype(dtype if dtype != 'None' else 'float32'),
+                       device=_dev(ctx)).normal_(loc, scale)
+
+
+@register('_random_gamma', arg_names=(), params=dict(_RP, alpha=('float', 1.0), beta=('float', 1.0)))
+def random_gamma(alpha=1.0, beta=1.0, shape=(), ctx=None, dtype='float32'):
+    return (torch._standard_gamma(torch.full(_s(shape), alpha, device=_dev(ctx))) * beta).to(torch_dtype(dtype))
+
+
+@register('_random_exponential', arg_names=(), params=dict(_RP, lam=('float', 1.0)))
+def random_exponential(lam=1.0, shape=(), ctx=None, dtype='float32'):
+    return torch.empty(_s(shape), device=_dev(ctx)).exponential_(lam).to(torch_dtype(dtype))
+
+
+@register('_random_poisson', arg_names=(), params=dict(_RP, lam=('float', 1.0)))
+def random_poisson(lam=1.0, shape=(), ctx=None, dtype='float32'):
+    return torch.poisson(torch.full(_s(shape), lam, device=_dev(ctx))).to(torch_dtype(dtype))
+
+
+@register('_random_randint', arg_names=(), params=dict(_RP, low=('int', 0), high=('int', 1), dtype=('str', 'int32')))
+def random_randint(low=0, high=1, shape=(), ctx=None, dtype='int32'):
+    return torch.randint(low, high, _s(shape), device=_dev(ctx)).to(torch_dtype(dtype))
+
+
+@register('_random_negative_binomial', arg_names=(), params=dict(_RP, k=('int', 1), p=('float', 1.0)))
+def random_negative_binomial(k=1, p=1.0, shape=(), ctx=None, dtype='float32'):
+    g = torch._standard_gamma(torch.full(_s(shape), float(k), device=_dev(ctx))) * ((1 - p) / p)
+    return torch.poisson(g).to(torch_dtype(dtype))
+
+
+@register('_random_generalized_negative_binomial', arg_names=(),
+          params=dict(_RP, mu=('float', 1.0), alpha=('float', 1.0)))
+def random_gen_neg_binomial(mu=1.0, alpha=1.0, shape=(), ctx=None, dtype='float32'):
+    g = torch._standard_gamma(torch.full(_s(shape), 1.0 / alpha, device=_dev(ctx))) * (mu * alpha)
+    return torch.poisson(g).to(torch_dtype(dtype))
+
+
+def _like(f):
+    def g(data, **kw):
+        return f(shape=tuple(data.shape), ctx=None, dtype='float32', **kw).to(data.device, data.dtype)
+    return g
+
+
+register('_random_uniform_like', lambda data, low=0.0, high=1.0: torch.empty_like(data).uniform_(low, high),
+         params={'low': ('float', 0.0), 'high': ('float', 1.0)})
+register('_random_normal_like', lambda data, loc=0.0, scale=1.0: torch.empty_like(data).normal_(loc, scale),
+         params={'loc': ('float', 0.0), 'scale': ('float', 1.0)})
+
+
+def _sample_shape(p, shape):
+    s = tuple(shape) if shape else ()
+    return tuple(p.shape) + s, (1,) * len(s)
+
+
+@register('_sample_uniform', aliases=('sample_uniform',), arg_names=('low', 'high'), params={'shape': ('shape', ()), 'dtype': ('str', 'None')})
+def sample_uniform(low, high, shape=(), dtype='None'):
+    full, ext = _sample_shape(low, shape)
+    u = torch.rand(full, device=low.device, dtype=low.dtype)
+    return low.reshape(tuple(low.shape) + ext) + (high - low).reshape(tuple(low.shape) + ext) * u
+
+
+@register('_sample_normal', aliases=('sample_normal',), arg_names=('mu', 'sigma'), params={'shape': ('shape', ()), 'dtype': ('str', 'None')})
+def sample_normal(mu, sigma, shape=(), dtype='None'):
+    full, ext = _sample_shape(mu, shape)
+    n = torch.randn(full, device=mu.device, dtype=mu.dtype)
+    return mu.reshape(tuple(mu.shape) + ext) + sigma.reshape(tuple(mu.shape) + ext) * n
+
+
+@register('_sample_multinomial', aliases=('sample_multinomial',), arg_names=('data',),
+          num_outputs=lambda a: 2 if str(a.get('get_prob', False)) in ('True', 'true', '1') else 1,
+          params={'shape': ('shape', ()), 'get_prob': ('bool', False), 'dtype': ('str', 'int32')})
+def sample_multinomial(data, shape=(), get_prob=False, dtype='int32'):
+    n = int(math.prod(shape)) if shape else 1
+    flat = data.reshape(-1, data.shape[-1]).float()
+    idx = torch.multinomial(flat, n, replacement=True)
+    oshape = tuple(data.shape[:-1]) + (tuple(shape) if shape else ())
+    out = idx.reshape(oshape if oshape else (1,)).to(torch_dtype(dtype))
+    if get_prob:
+        lp = torch.log(torch.gather(flat, 1, idx)).reshape(out.shape).to(data.dtype)
+        return out, lp
+    return out
+
+
+@register('_shuffle', aliases=('shuffle',))
+def shuffle(data):
+    return data[torch.randperm(data.shape[0], device=data.device)]
+
+
+# ---------------------------------------------------------------------------
+# linalg (la_op.cc)
+# ---------------------------------------------------------------------------
+
+def _t(x, flag):
+    return x.transpose(-1, -2) if flag else x
+
+
+@register('_linalg_gemm', aliases=('linalg_gemm',), arg_names=('A', 'B', 'C'),
+          params={'transpose_a': ('bool', False), 'transpose_b': ('bool', False), 'alpha': ('float', 1.0),
+                  'beta': ('float', 1.0), 'axis': ('int', -2)})
+def linalg_gemm(A, B, C, transpose_a=False, transpose_b=False, alpha=1.0, beta=1.0, axis=-2):
+    return alpha * torch.matmul(_t(A, transpose_a), _t(B, transpose_b)) + beta * C
+
+
+@register('_linalg_gemm2', aliases=('linalg_gemm2',), arg_names=('A', 'B'),
+          params={'transpose_a': ('bool', False), 'transpose_b': ('bool', False), 'alpha': ('float', 1.0),
+                  'axis': ('int', -2)})
+def linalg_gemm2(A, B, transpose_a=False, transpose_b=False, alpha=1.0, axis=-2):
+    return alpha * torch.matmul(_t(A, transpose_a), _t(B, transpose_b))
+
+
+@register('_linalg_potrf', aliases=('linalg_potrf',))
+def linalg_potrf(A):
+    return torch.linalg.cholesky(A)
+
+
+@register('_linalg_potri', aliases=('linalg_potri',))
+def linalg_potri(A):
+    return torch.cholesky_inverse(A)
+
+
+@register('_linalg_trmm', aliases=('linalg_trmm',), arg_names=('A', 'B'),
+          params={'transpose': ('bool', False), 'rightside': ('bool', False), 'lower': ('bool', True),
+                  'alpha': ('float', 1.0)})
+def linalg_trmm(A, B, transpose=False, rightside=False, lower=True, alpha=1.0):
+    T = torch.tril(A) if lower else torch.triu(A)
+    T = _t(T, transpose)
+    return alpha * (torch.matmul(B, T) if rightside else torch.matmul(T, B))
+
+
+@register('_linalg_trsm', aliases=('linalg_trsm',), arg_names=('A', 'B'),
+          params={'transpose': ('bool', False), 'rightside': ('bool', False), 'lower': ('bool', True),
+                  'alpha': ('float', 1.0)})
+def linalg_trsm(A, B, transpose=False, rightside=False, lower=True, alpha=1.0):
+    up = not lower
+    if transpose:
+        A = A.transpose(-1, -2)
+        up = not up
+    return alpha * torch.linalg.solve_triangular(A, B, upper=up, left=not rightside)
+
+
+@register('_linalg_sumlogdiag', aliases=('linalg_sumlogdiag',))
+def linalg_sumlogdiag(A):
+    return torch.log(torch.diagonal(A, dim1=-2, dim2=-1)).sum(-1)
+
+
+@register('_linalg_syrk', aliases=('linalg_syrk',), params={'transpose': ('bool', False), 'alpha': ('float', 1.0)})
+def linalg_syrk(A, transpose=False, alpha=1.0):
+    return alpha * (torch.matmul(A.transpose(-1, -2), A) if transpose else torch.matmul(A, A.transpose(-1, -2)))
+
+
+@register('_linalg_gelqf', aliases=('linalg_gelqf',), num_outputs=2)
+def linalg_gelqf(A):
+    q, r = torch.linalg.qr(A.transpose(-1, -2))
+    return q.transpose(-1, -2), r.transpose(-1, -2)
+
+
+@register('_linalg_syevd', aliases=('linalg_syevd',), num_outputs=2)
+def linalg_syevd(A):
+    w, v = torch.linalg.eigh(A)
+    return v.transpose(-1, -2), w
+
+
+@register('_linalg_inverse', aliases=('linalg_inverse',))
+def linalg_inverse(A):
+    return torch.linalg.inv(A)
+
+
+@register('_linalg_det', aliases=('linalg_det',))
+def linalg_det(A):
+    return torch.linalg.det(A)
+
+
+@register('_linalg_slogdet', aliases=('linalg_slogdet',), num_outputs=2)
+def linalg_slogdet(A):
+    s, l = torch.linalg.slogdet(A)
+    return s, l
+
+
+@register('_linalg_extractdiag', aliases=('linalg_extractdiag',), params={'offset': ('int', 0)})
+def linalg_extractdiag(A, offset=0):
+    return torch.diagonal(A, offset=offset, dim1=-2, dim2=-1).contiguous()
+
+
+@register('_linalg_makediag', aliases=('linalg_makediag',), params={'offset': ('int', 0)})
+def linalg_makediag(A, offset=0):
+    return torch.diag_embed(A, offset=offset)
+
+
+@register('_linalg_extracttrian', aliases=('linalg_extracttrian',), params={'offset': ('int', 0), 'lower': ('bool', True)})
+def linalg_extracttrian(A, offset=0, lower=True):
+    n = A.shape[-1]
+    idx = torch.tril_indices(n, n, offset) if lower else torch.triu_indices(n, n, offset)
+    return A[..., idx[0], idx[1]]
+
+
+@register('_linalg_maketrian', aliases=('linalg_maketrian',), params={'offset': ('int', 0), 'lower': ('bool', True)})
+def linalg_maketrian(A, offset=0, lower=True):
+    m = A.shape[-1]
+    n = int((math.sqrt(8 * m + 1) - 1) / 2) + abs(offset)
+    out = torch.zeros(A.shape[:-1] + (n, n), dtype=A.dtype, device=A.device)
+    idx = torch.tril_indices(n, n, offset) if lower else torch.triu_indices(n, n, offset)
+    out[..., idx[0], idx[1]] = A
+    return out
+
+
+# ---------------------------------------------------------------------------
+# image ops (src/operator/image)
+# ---------------------------------------------------------------------------
+
+@register('_image_to_tensor', aliases=('to_tensor',))
+def image_to_tensor(data):
+    x = data.float() / 255.0
+    if data.dim() == 3:
+        return x.permute(2, 0, 1).contiguous()
+    return x.permute(0, 3, 1, 2).contiguous()
+
+
+@register('_image_normalize', aliases=('image_normalize',), params={'mean': ('floats', (0.0,)), 'std': ('floats', (1.0,))})
+def image_normalize(data, mean=(0.0,), std=(1.0,)):
+    c = data.shape[-3]
+    m = torch.tensor(list(mean) * (c if len(mean) == 1 else 1), dtype=data.dtype, device=data.device)[:c]
+    s = torch.tensor(list(std) * (c if len(std) == 1 else 1), dtype=data.dtype, device=data.device)[:c]
+    shape = (c, 1, 1)
+    return (data - m.reshape(shape)) / s.reshape(shape)
+
+
+@register('_image_resize', aliases=('image_resize',), params={'size': ('shape', ()), 'keep_ratio': ('bool', False),
+                                                              'interp': ('int', 1)})
+def image_resize(data, size=(), keep_ratio=False, interp=1):
+    if len(size) == 1:
+        size = (size[0], size[0])
+    w, h = size
+    hwc = data.dim() == 3
+    x = data.permute(2, 0, 1).unsqueeze(0) if hwc else data.permute(0, 3, 1, 2)
+    mode = 'nearest' if interp == 0 else 'bilinear'
+    y = F.interpolate(x.float(), size=(h, w), mode=mode, align_corners=False if mode == 'bilinear' else None)
+    y = y.round().clamp(0, 255) if not data.is_floating_point() else y
+    y = y.to(data.dtype)
+    return y[0].permute(1, 2, 0) if hwc else y.permute(0, 2, 3, 1)
+
+
+@register('_image_crop', aliases=('image_crop',), params={'x': ('int', 0), 'y': ('int', 0), 'width': ('int', 1),
+                                                          'height': ('int', 1)})
+def image_crop(data, x=0, y=0, width=1, height=1):
+    if data.dim() == 3:
+        return data[y:y + height, x:x + width].contiguous()
+    return data[:, y:y + height, x:x + width].contiguous()
+
+
+@register('_image_flip_left_right', aliases=('flip_left_right',))
+def image_flip_lr(data):
+    return torch.flip(data, dims=[-2])
+
+
+@register('_image_flip_top_bottom', aliases=('flip_top_bottom',))
+def image_flip_tb(data):
+    return torch.flip(data, dims=[-3])
+
+
+@register('_image_random_flip_left_right')
+def image_random_flip_lr(data):
+    return torch.flip(data, dims=[-2]) if torch.rand(()) < 0.5 else data.clone()
+
+
+@register('_image_random_flip_top_bottom')
+def image_random_flip_tb(data):
+    return torch.flip(data, dims=[-3]) if torch.rand(()) < 0.5 else data.clone()
+
+
+def _gray(x):
+    w = torch.tensor([0.299, 0.587, 0.114], dtype=torch.float32, device=x.device)
+    return (x.float() * w).sum(-1, keepdim=True)
+
+
+@register('_image_adjust_lighting', params={'alpha': ('floats', (0.0, 0.0, 0.0))})
+def image_adjust_lighting(data, alpha=(0.0, 0.0, 0.0)):
+    eigval = torch.tensor([55.46, 4.794, 1.148])
+    eigvec = torch.tensor([[-0.5675, 0.7192, 0.4009], [-0.5808, -0.0045, -0.8140], [-0.5836, -0.6948, 0.4203]])
+    rgb = (eigvec * torch.tensor(alpha) * eigval).sum(1).to(data.device)
+    return (data.float() + rgb).to(data.dtype)
+
+
+@register('_image_random_brightness', params={'min_factor': ('float', 1.0), 'max_factor': ('float', 1.0)})
+def image_random_brightness(data, min_factor=1.0, max_factor=1.0):
+    a = float(torch.empty(()).uniform_(min_factor, max_factor))
+    return (data.float() * a).to(data.dtype)
+
+
+@register('_image_random_contrast', params={'min_factor': ('float', 1.0), 'max_factor': ('float', 1.0)})
+def image_random_contrast(data, min_factor=1.0, max_factor=1.0):
+    a = float(torch.empty(()).uniform_(min_factor, max_factor))
+    m = _gray(data).mean()
+    return (data.float() * a + m * (1 - a)).to(data.dtype)
+
+
+@register('_image_random_saturation', params={'min_factor': ('float', 1.0), 'max_factor': ('float', 1.0)})
+def image_random_saturation(data, min_factor=1.0, max_factor=1.0):
+    a = float(torch.empty(()).uniform_(min_factor, max_factor))
+    g = _gray(data)
+    return (data.float() * a + g * (1 - a)).to(data.dtype)

@@ -1,0 +1,920 @@
+"""Optimizers.
+
+Parity: python/mxnet/optimizer/optimizer.py (Optimizer registry/create,
+lr/wd multipliers, update counts, multi-precision master weights, Updater,
+get_updater; SGD, Signum, FTML, LARS, LBSGD, LAMB, DCASGD, NAG, SGLD, ccSGD,
+Adam, AdaGrad, RMSProp, AdaDelta, Ftrl, Adamax, Nadam, Test) and
+python/mxnet/optimizer/contrib.py (GroupAdaGrad), plus AdamW
+(src/operator/contrib/adamw*).
+
+Updates run in place on the parameter tensors.  ``SGD`` and ``Adam`` accept
+lists of indices (``aggregate_num``) and then run as one multi-tensor update:
+the fused gfx950 HIP kernel when available, ``torch._foreach_*`` otherwise.
+"""
+import math
+import pickle
+import warnings
+
+import numpy as np
+import torch
+
+from ..base import MXNetError, torch_dtype
+from ..ndarray.ndarray import NDArray
+from .. import ndarray as nd
+from ..ops import optimizer_ops as _oo
+from ..ops import kernels as _K
+
+__all__ = ['Optimizer', 'register', 'create', 'SGD', 'Signum', 'FTML', 'LARS', 'LBSGD', 'LAMB', 'DCASGD', 'NAG',
+           'SGLD', 'ccSGD', 'Adam', 'AdamW', 'AdaGrad', 'RMSProp', 'AdaDelta', 'Ftrl', 'Adamax', 'Nadam', 'Test',
+           'Updater', 'get_updater', 'GroupAdaGrad']
+
+
+def _t(x):
+    return x._data if isinstance(x, NDArray) else x
+
+
+class Optimizer:
+    """Base class of all optimizers."""
+    opt_registry = {}
+
+    def __init__(self, rescale_grad=1., param_idx2name=None, wd=0., clip_gradient=None, learning_rate=None,
+                 lr_scheduler=None, sym=None, begin_num_update=0, multi_precision=False, param_dict=None,
+                 aggregate_num=None, use_fused_step=None, **kwargs):
+        self.rescale_grad = rescale_grad
+        self.lr_scheduler = lr_scheduler
+        if learning_rate is None:
+            learning_rate = 0.01
+        if self.lr_scheduler is None:
+            self.lr = learning_rate
+        else:
+            if lr_scheduler.base_lr != learning_rate:
+                warnings.warn('learning rate from ``lr_scheduler`` has been overwritten by ``learning_rate`` in '
+                              'optimizer.', UserWarning)
+            self.lr_scheduler.base_lr = learning_rate
+            self.lr = learning_rate
+        self.wd = wd
+        self.lr_mult = {}
+        self.wd_mult = {}
+        self.begin_num_update = begin_num_update
+        self.num_update = begin_num_update
+        self._all_index_update_counts = {0: {}}
+        self._index_update_count = self._all_index_update_counts[0]
+        self.clip_gradient = clip_gradient
+        self.multi_precision = multi_precision
+        self.aggregate_num = 0 if aggregate_num is None else aggregate_num
+        if param_idx2name is None:
+            param_idx2name = {}
+        assert isinstance(param_idx2name, dict), 'param_idx2name should be a dict of param indexes to names.'
+        self.idx2name = param_idx2name.copy()
+        self.sym_info = (sym.attr_dict(), sym.list_arguments()) if sym is not None else ()
+        self.param_dict = param_dict if param_dict else {}
+        self.allow_np_array = False
+        self.set_lr_mult({})
+        self.set_wd_mult({})
+
+    @staticmethod
+    def register(klass):
+        assert isinstance(klass, type)
+        name = klass.__name__.lower()
+        if name in Optimizer.opt_registry:
+            warnings.warn('WARNING: New optimizer %s.%s is overriding existing optimizer %s.%s' % (
+                klass.__module__, klass.__name__, Optimizer.opt_registry[name].__module__,
+                Optimizer.opt_registry[name].__name__))
+        Optimizer.opt_registry[name] = klass
+        return klass
+
+    @staticmethod
+    def create_optimizer(name, **kwargs):
+        if name.lower() in Optimizer.opt_registry:
+            return Optimizer.opt_registry[name.lower()](**kwargs)
+        raise ValueError('Cannot find optimizer %s' % name)
+
+    @property
+    def learning_rate(self):
+        if self.lr_scheduler is not None:
+            return self.lr_scheduler(self.num_update)
+        return self.lr
+
+    def create_state(self, index, weight):
+        return None
+
+    def create_state_multi_precision(self, index, weight):
+        weight_master_copy = None
+        if self.multi_precision and weight.dtype in (np.float16,) or \
+                (self.multi_precision and weight._data.dtype == torch.bfloat16):
+            weight_master_copy = NDArray(weight._data.detach().float().clone())
+            return (weight_master_copy,) + (self.create_state(index, weight_master_copy),)
+        if weight._data.dtype in (torch.float16, torch.bfloat16) and not self.multi_precision:
+            warnings.warn('Accumulating with float16 in optimizer can lead to poor accuracy or slow convergence. '
+                          'Consider using multi_precision=True option of the optimizer')
+        return self.create_state(index, weight)
+
+    def update(self, index, weight, grad, state):
+        raise NotImplementedError()
+
+    def update_multi_precision(self, index, weight, grad, state):
+        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
+            weight_master_copy = state[0]
+            original_state = state[1]
+            grad32 = NDArray(grad._data.float())
+            self.update(index, weight_master_copy, grad32, original_state)
+            with torch.no_grad():
+                weight._data.copy_(weight_master_copy._data)
+        else:
+            self.update(index, weight, grad, state)
+
+    def set_learning_rate(self, lr):
+        if self.lr_scheduler is not None:
+            raise UserWarning('LRScheduler of the optimizer has already been defined. Note that '
+                              'set_learning_rate can mutate the value of the learning rate of the optimizer only '
+                              'when the LRScheduler of the optimizer is undefined.')
+        self.lr = lr
+
+    def set_lr_scale(self, args_lrscale):
+        raise DeprecationWarning
+
+    def set_lr_mult(self, args_lr_mult):
+        self.lr_mult = {}
+        if self.sym_info:
+            attr, arg_names = self.sym_info
+            for name in arg_names:
+                if name in attr and '__lr_mult__' in attr[name]:
+                    self.lr_mult[name] = float(attr[name]['__lr_mult__'])
+        self.lr_mult.update(args_lr_mult)
+
+    def set_wd_mult(self, args_wd_mult):
+        self.wd_mult = {}
+        for n in self.idx2name.values():
+            if not (n.endswith('_weight') or n.endswith('_gamma')):
+                self.wd_mult[n] = 0.0
+        if self.sym_info:
+            attr, arg_names = self.sym_info
+            for name in arg_names:
+                if name in attr and '__wd_mult__' in attr[name]:
+                    self.wd_mult[name] = float(attr[name]['__wd_mult__'])
+        self.wd_mult.update(args_wd_mult)
+
+    def _set_current_context(self, device_id):
+        if device_id not in self._all_index_update_counts:
+            self._all_index_update_counts[device_id] = {}
+        self._index_update_count = self._all_index_update_counts[device_id]
+
+    def _update_count(self, index):
+        if not isinstance(index, (list, tuple)):
+            index = [index]
+        for idx in index:
+            if idx not in self._index_update_count:
+                self._index_update_count[idx] = self.begin_num_update
+            self._index_update_count[idx] += 1
+            self.num_update = max(self._index_update_count[idx], self.num_update)
+
+    def _get_lrs(self, indices):
+        if self.lr_scheduler is not None:
+            lr = self.lr_scheduler(self.num_update)
+        else:
+            lr = self.lr
+        lrs = [lr for _ in indices]
+        for i, index in enumerate(indices):
+            if index in self.param_dict:
+                lrs[i] *= self.param_dict[index].lr_mult
+            elif index in self.lr_mult:
+                lrs[i] *= self.lr_mult[index]
+            elif index in self.idx2name:
+                lrs[i] *= self.lr_mult.get(self.idx2name[index], 1.0)
+        return lrs
+
+    def _get_lr(self, index):
+        return self._get_lrs([index])[0]
+
+    def _get_wds(self, indices):
+        wds = [self.wd for _ in indices]
+        for i, index in enumerate(indices):
+            if index in self.param_dict:
+                wds[i] *= self.param_dict[index].wd_mult
+            elif index in self.wd_mult:
+                wds[i] *= self.wd_mult[index]
+            elif index in self.idx2name:
+                wds[i] *= self.wd_mult.get(self.idx2name[index], 1.0)
+        return wds
+
+    def _get_wd(self, index):
+        return self._get_wds([index])[0]
+
+    def _clip(self):
+        return -1.0 if self.clip_gradient is None else self.clip_gradient
+
+    def __getstate__(self):
+        ret = self.__dict__.copy()
+        del ret['param_dict']
+        return ret
+
+    def __setstate__(self, state):
+        self.__dict__ = state
+        self.param_dict = {}
+
+
+register = Optimizer.register
+create = Optimizer.create_optimizer
+
+
+def _as_list(x):
+    return x if isinstance(x, (list, tuple)) else [x]
+
+
+@register
+class SGD(Optimizer):
+    """SGD with optional momentum and multi-precision (fp32 master weights).
+
+    ``state = momentum * state + lr * (rescale_grad * clip(grad) + wd * weight)``;
+    ``weight -= state`` (MXNet's sign convention: mom stores -lr*update).
+    """
+
+    def __init__(self, momentum=0.0, lazy_update=True, **kwargs):
+        super().__init__(**kwargs)
+        self.momentum = momentum
+        self.lazy_update = lazy_update
+        self.aggregate_num = int(kwargs.get('aggregate_num') or 1 << 30)
+
+    def create_state_multi_precision(self, index, weight):
+        weight_master_copy = None
+        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
+            weight_master_copy = NDArray(weight._data.detach().float().clone())
+            return (self.create_state(index, weight_master_copy), weight_master_copy)
+        if weight._data.dtype in (torch.float16, torch.bfloat16) and not self.multi_precision:
+            warnings.warn('Accumulating with float16 in optimizer can lead to poor accuracy or slow convergence. '
+                          'Consider using multi_precision=True option of the SGD optimizer')
+        return self.create_state(index, weight)
+
+    def create_state(self, index, weight):
+        if self.momentum != 0.0:
+            return NDArray(torch.zeros_like(weight._data))
+        return None
+
+    def _update_impl(self, indices, weights, grads, states, multi_precision=False):
+        indices, weights, grads, states = map(_as_list, (indices, weights, grads, states)) \
+            if isinstance(indices, (list, tuple)) else ([indices], [weights], [grads], [states])
+        self._update_count(indices)
+        lrs = self._get_lrs(indices)
+        wds = self._get_wds(indices)
+        clip = self._clip()
+        W = [w._data for w in weights]
+        G = [g._data for g in grads]
+        if multi_precision:
+            M = [s[0]._data if s[0] is not None else None for s in states]
+            W32 = [s[1]._data for s in states]
+        else:
+            M = [s._data if s is not None else None for s in states]
+            W32 = None
+        multi_sgd(W, G, M, W32, lrs, wds, self.momentum, self.rescale_grad, clip)
+
+    def update(self, index, weight, grad, state):
+        self._update_impl(index, weight, grad, state, multi_precision=False)
+
+    def update_multi_precision(self, index, weight, grad, state):
+        ws = _as_list(weight)
+        use_mp = self.multi_precision and ws[0]._data.dtype in (torch.float16, torch.bfloat16)
+        self._update_impl(index, weight, grad, state, multi_precision=use_mp)
+
+
+@torch.no_grad()
+def multi_sgd(W, G, M, W32, lrs, wds, momentum, rescale, clip):
+    """One fused update over many tensors (SGD / SGD-momentum, optional fp32 masters)."""
+    if not W:
+        return
+    if W[0].is_cuda and _K.available() and _K.enabled() and hasattr(_K, 'multi_sgd_mom_tensors') \
+            and (momentum == 0.0 or all(m is not None for m in M)):
+        _K.multi_sgd_mom_tensors(W, G, M, W32, lrs, wds, momentum, rescale, clip)
+        return
+    tgt = W32 if W32 is not None else W
+    # group by (lr, wd) so each group is a handful of foreach launches
+    groups = {}
+    for i, (lr, wd) in enumerate(zip(lrs, wds)):
+        groups.setdefault((lr, wd), []).append(i)
+    for (lr, wd), idx in groups.items():
+        g = [G[i].float() if G[i].dtype != tgt[i].dtype else G[i] for i in idx]
+        if rescale != 1.0:
+            g = torch._foreach_mul(g, rescale)
+        if clip is not None and clip >= 0:
+            g = [torch.clamp(x, -clip, clip) for x in g]
+        w = [tgt[i] for i in idx]
+        if wd != 0.0:
+            g = torch._foreach_add(g, w, alpha=wd)
+        if momentum != 0.0:
+            m = [M[i] for i in idx]
+            torch._foreach_mul_(m, momentum)
+            torch._foreach_add_(m, g, alpha=-lr)
+            torch._foreach_add_(w, m)
+        else:
+            torch._foreach_add_(w, g, alpha=-lr)
+        if W32 is not None:
+            for i in idx:
+                W[i].copy_(W32[i])
+
+
+@register
+class Signum(Optimizer):
+    def __init__(self, learning_rate=0.01, momentum=0.9, wd_lh=0.0, **kwargs):
+        super().__init__(learning_rate=learning_rate, **kwargs)
+        self.momentum = momentum
+        self.wd_lh = wd_lh
+
+    def create_state(self, index, weight):
+        if self.momentum != 0.0:
+            return NDArray(torch.zeros_like(weight._data))
+        return None
+
+    def update(self, index, weight, grad, state):
+        self._update_count(index)
+        lr = self._get_lr(index)
+        wd = self._get_wd(index)
+        if state is not None:
+            _oo.signum_update(weight._data, grad._data, state._data, lr=lr, momentum=self.momentum, wd=wd,
+                              rescale_grad=self.rescale_grad, clip_gradient=self._clip(), wd_lh=self.wd_lh)
+        else:
+            _oo.signsgd_update(weight._data, grad._data, lr=lr, wd=wd, rescale_grad=self.rescale_grad,
+                               clip_gradient=self._clip())
+
+
+@register
+class FTML(Optimizer):
+    def __init__(self, beta1=0.6, beta2=0.999, epsilon=1e-8, **kwargs):
+        super().__init__(**kwargs)
+        self.beta1 = beta1
+        self.beta2 = beta2
+        self.epsilon = epsilon
+
+    def create_state(self, index, weight):
+        z = lambda: NDArray(torch.zeros_like(weight._data))
+        return (z(), z(), z())
+
+    def update(self, index, weight, grad, state):
+        self._update_count(index)
+        t = self._index_update_count[index]
+        d, v, z = state
+        _oo.ftml_update(weight._data, grad._data, d._data, v._data, z._data, lr=self._get_lr(index),
+                        beta1=self.beta1, beta2=self.beta2, epsilon=self.epsilon, t=t, wd=self._get_wd(index),
+                        rescale_grad=self.rescale_grad, clip_grad=self._clip())
+
+
+@register
+class LARS(Optimizer):
+    """SGD with layer-wise adaptive rate scaling (You et al. 2017)."""
+
+    def __init__(self, momentum=0.0, lazy_update=True, eta=0.001, eps=0, momentum_correction=True, **kwargs):
+        super().__init__(**kwargs)
+        self.momentum = momentum
+        self.eta = eta
+        self.eps = eps
+        self.lazy_update = lazy_update
+
+    def create_state(self, index, weight):
+        if self.momentum != 0.0:
+            return NDArray(torch.zeros_like(weight._data, dtype=torch.float32))
+        return None
+
+    def create_state_multi_precision(self, index, weight):
+        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
+            w32 = NDArray(weight._data.float())
+            return (self.create_state(index, w32), w32)
+        return self.create_state(index, weight)
+
+    def _l2norm(self, v):
+        return float(torch.linalg.vector_norm(v.float()))
+
+    def update(self, index, weight, grad, state):
+        self._update_count(index)
+        lr = self._get_lr(index)
+        wd = self._get_wd(index)
+        name = self.idx2name.get(index, '')
+        if not (name.endswith('gamma') or name.endswith('beta') or name.endswith('bias')):
+            w_norm = self._l2norm(weight._data)
+            g_norm = self._l2norm(grad._data * self.rescale_grad)
+            if w_norm > 0.0 and g_norm > 0.0:
+                lr = lr * self.eta * w_norm / (g_norm + wd * w_norm + self.eps)
+        multi_sgd([weight._data], [grad._data], [state._data if state is not None else None], None, [lr], [wd],
+                  self.momentum, self.rescale_grad, self._clip())
+
+    def update_multi_precision(self, index, weight, grad, state):
+        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
+            mom, w32 = state
+            self.update(index, w32, NDArray(grad._data.float()), mom)
+            with torch.no_grad():
+                weight._data.copy_(w32._data)
+        else:
+            self.update(index, weight, grad, state)
+
+
+@register
+class LBSGD(Optimizer):
+    """Large-batch SGD with warmup strategies (reference optimizer.py LBSGD)."""
+
+    def __init__(self, momentum=0.0, multi_precision=False, warmup_strategy='linear', warmup_epochs=5,
+                 batch_scale=1, updates_per_epoch=32, begin_epoch=0, num_epochs=60, **kwargs):
+        super().__init__(multi_precision=multi_precision, **kwargs)
+        self.momentum = momentum
+        self.warmup_strategy = warmup_strategy
+        self.warmup_epochs = warmup_epochs
+        self.batch_scale = batch_scale
+        self.updates_per_epoch = updates_per_epoch
+        self.init_updates = begin_epoch * updates_per_epoch
+        self.num_epochs = num_epochs
+        self.lbmult = 1
+        self.cumgrads = {}
+        self.adaptive = False
+        self.admult = 1
+
+    def create_state(self, index, weight):
+        if self.momentum != 0.0:
+            return NDArray(torch.zeros_like(weight._data))
+        return None
+
+    def _get_lbmult(self, nup):
+        nwup = self.warmup_epochs * self.updates_per_epoch
+        strategy = self.warmup_strategy
+        maxmult = float(self.batch_scale)
+        if nup >= nwup:
+            mult = maxmult
+        elif nwup <= 1:
+            mult = 1.0
+        else:
+            if strategy == 'linear':
+                mult = 1.0 + (maxmult - 1) * nup / nwup
+            elif strategy == 'power2':
+                mult = 1.0 + (maxmult - 1) * (nup * nup) / (nwup * nwup)
+            elif strategy == 'sqrt':
+                mult = 1.0 + (maxmult - 1) * math.sqrt(float(nup) / nwup)
+            else:
+                mult = 1.0
+        return mult
+
+    def update(self, index, weight, grad, state):
+        self._update_count(index)
+        lr = self._get_lr(index) * self._get_lbmult(self.num_update - self.init_updates)
+        wd = self._get_wd(index)
+        multi_sgd([weight._data], [grad._data], [state._data if state is not None else None], None, [lr], [wd],
+                  self.momentum, self.rescale_grad, self._clip())
+
+
+@register
+class LAMB(Optimizer):
+    """LAMB optimizer (You et al. 2019), two-phase update as in the reference ops."""
+
+    def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-6, lower_bound=None,
+                 upper_bound=None, bias_correction=True, **kwargs):
+        super().__init__(learning_rate=learning_rate, **kwargs)
+        self.beta1 = beta1
+        self.beta2 = beta2
+        self.epsilon = epsilon
+        self.lower_bound = lower_bound
+        self.upper_bound = upper_bound
+        self.bias_correction = bias_correction
+
+    def create_state(self, index, weight):
+        z = lambda: NDArray(torch.zeros_like(weight._data, dtype=torch.float32))
+        return (z(), z())
+
+    def create_state_multi_precision(self, index, weight):
+        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
+            w32 = NDArray(weight._data.float())
+            return (w32,) + self.create_state(index, w32)
+        return self.create_state(index, weight)
+
+    def _step(self, index, weight, grad, mean, var, w32=None):
+        self._update_count(index)
+        lr = self._get_lr(index)
+        wd = self._get_wd(index)
+        t = self._index_update_count[index]
+        tgt = w32 if w32 is not None else weight._data
+        g = _oo._lamb1(tgt, grad._data.float(), mean, var, self.beta1, self.beta2, self.epsilon, t,
+                       self.bias_correction, wd, self.rescale_grad, self._clip())
+        r1 = torch.linalg.vector_norm(tgt.float()).reshape(1)
+        r2 = torch.linalg.vector_norm(g).reshape(1)
+        lb = -1.0 if self.lower_bound is None else self.lower_bound
+        ub = -1.0 if self.upper_bound is None else self.upper_bound
+        _oo._lamb2(weight._data, g, r1, r2, lr, lb, ub, w32=w32)
+
+    def update(self, index, weight, grad, state):
+        mean, var = state
+        self._step(index, weight, grad, mean._data, var._data)
+
+    def update_multi_precision(self, index, weight, grad, state):
+        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
+            w32, mean, var = state
+            self._step(index, weight, grad, mean._data, var._data, w32=w32._data)
+        else:
+            self.update(index, weight, grad, state)
+
+
+@register
+class DCASGD(Optimizer):
+    def __init__(self, momentum=0.0, lamda=0.04, **kwargs):
+        super().__init__(**kwargs)
+        self.momentum = momentum
+        self.weight_previous = {}
+        self.lamda = lamda
+
+    def create_state(self, index, weight):
+        if self.momentum == 0.0:
+            return (None, NDArray(weight._data.clone()))
+        return (NDArray(torch.zeros_like(weight._data)), NDArray(weight._data.clone()))
+
+    @torch.no_grad()
+    def update(self, index, weight, grad, state):
+        self._update_count(index)
+        lr = self._get_lr(index)
+        wd = self._get_wd(index)
+        g = grad._data * self.rescale_grad
+        if self.clip_gradient is not None:
+            g = torch.clamp(g, -self.clip_gradient, self.clip_gradient)
+        mom, previous_weight = state
+        w = weight._data
+        delta = -lr * (g + wd * w + self.lamda * g * g * (w - previous_weight._data))
+        if mom is not None:
+            mom._data.mul_(self.momentum).add_(delta)
+            delta = mom._data
+        previous_weight._data.copy_(w)
+        w.add_(delta)
+
+
+@register
+class NAG(Optimizer):
+    def __init__(self, momentum=0.0, **kwargs):
+        super().__init__(**kwargs)
+        self.momentum = momentum
+
+    def create_state_multi_precision(self, index, weight):
+        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
+            w32 = NDArray(weight._data.float())
+            return (self.create_state(index, w32), w32)
+        return self.create_state(index, weight)
+
+    def create_state(self, index, weight):
+        if self.momentum != 0.0:
+            return NDArray(torch.zeros_like(weight._data))
+        return None
+
+    def _upd(self, index, weight, grad, state, w32=None):
+        self._update_count(index)
+        lr = self._get_lr(index)
+        wd = self._get_wd(index)
+        if state is not None:
+            _oo._nag(weight._data, grad._data, state._data, lr, self.momentum, wd, self.rescale_grad,
+                     self._clip(), w32=w32)
+        else:
+            _oo._sgd(weight._data, grad._data, lr, wd, self.rescale_grad, self._clip(), w32=w32)
+
+    def update(self, index, weight, grad, state):
+        self._upd(index, weight, grad, state)
+
+    def update_multi_precision(self, index, weight, grad, state):
+        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
+            mom, w32 = state
+            self._upd(index, weight, NDArray(grad._data.float()), mom, w32=w32._data)
+        else:
+            self.update(index, weight, grad, state)
+
+
+@register
+class SGLD(Optimizer):
+    def create_state(self, index, weight):
+        return None
+
+    @torch.no_grad()
+    def update(self, index, weight, grad, state):
+        self._update_count(index)
+        lr = self._get_lr(index)
+        wd = self._get_wd(index)
+        g = grad._data * self.rescale_grad
+        if self.clip_gradient is not None:
+            g = torch.clamp(g, -self.clip_gradient, self.clip_gradient)
+        w = weight._data
+        w.add_(-lr / 2 * (g + wd * w) + torch.randn_like(w) * math.sqrt(lr))
+
+
+@register
+class ccSGD(SGD):
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+
+
+@register
+class Adam(Optimizer):
+    """Adam (Kingma & Ba); bias correction folded into the learning rate like the reference."""
+
+    def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8, lazy_update=True, **kwargs):
+        super().__init__(learning_rate=learning_rate, **kwargs)
+        self.beta1 = beta1
+        self.beta2 = beta2
+        self.epsilon = epsilon
+        self.lazy_update = lazy_update
+
+    def create_state(self, index, weight):
+        return (NDArray(torch.zeros_like(weight._data)), NDArray(torch.zeros_like(weight._data)))
+
+    def update(self, index, weight, grad, state):
+        self._update_count(index)
+        lr = self._get_lr(index)
+        wd = self._get_wd(index)
+        t = self._index_update_count[index]
+        coef1 = 1. - self.beta1 ** t
+        coef2 = 1. - self.beta2 ** t
+        lr *= math.sqrt(coef2) / coef1
+        mean, var = state
+        _oo.adam_update(weight._data, grad._data, mean._data, var._data, lr=lr, beta1=self.beta1,
+                        beta2=self.beta2, epsilon=self.epsilon, wd=wd, rescale_grad=self.rescale_grad,
+                        clip_gradient=self._clip())
+
+
+@register
+class AdamW(Optimizer):
+    """Adam with decoupled weight decay (contrib adamw_update)."""
+
+    def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8, correct_bias=True, **kwargs):
+        super().__init__(learning_rate=learning_rate, **kwargs)
+        self.beta1 = beta1
+        self.beta2 = beta2
+        self.epsilon = epsilon
+        self.correct_bias = correct_bias
+
+    def create_state(self, index, weight):
+        z = lambda: NDArray(torch.zeros_like(weight._data, dtype=torch.float32))
+        return (z(), z())
+
+    def create_state_multi_precision(self, index, weight):
+        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
+            w32 = NDArray(weight._data.float())
+            return (w32,) + self.create_state(index, w32)
+        return self.create_state(index, weight)
+
+    def _upd(self, index, weight, grad, mean, var, w32=None):
+        self._update_count(index)
+        lr = self._get_lr(index)
+        wd = self._get_wd(index)
+        t = self._index_update_count[index]
+        if self.correct_bias:
+            lr *= math.sqrt(1. - self.beta2 ** t) / (1. - self.beta1 ** t)
+        _oo._adamw(weight._data, grad._data.float(), mean._data, var._data, self.rescale_grad, lr,
+                   self.beta1, self.beta2, self.epsilon, wd, 1.0,
+                   self._clip(), w32=w32)
+
+    def update(self, index, weight, grad, state):
+        self._upd(index, weight, grad, state[0], state[1])
+
+    def update_multi_precision(self, index, weight, grad, state):
+        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
+            w32, mean, var = state
+            self._upd(index, weight, grad, mean, var, w32=w32._data)
+        else:
+            self.update(index, weight, grad, state)
+
+
+@register
+class AdaGrad(Optimizer):
+    def __init__(self, eps=1e-7, **kwargs):
+        super().__init__(**kwargs)
+        self.float_stable_eps = eps
+
+    def create_state(self, index, weight):
+        return NDArray(torch.zeros_like(weight._data))
+
+    @torch.no_grad()
+    def update(self, index, weight, grad, state):
+        self._update_count(index)
+        lr = self._get_lr(index)
+        wd = self._get_wd(index)
+        g = grad._data * self.rescale_grad
+        if self.clip_gradient is not None:
+            g = torch.clamp(g, -self.clip_gradient, self.clip_gradient)
+        h = state._data
+        h.add_(g * g)
+        w = weight._data
+        w.add_(-lr * (g / torch.sqrt(h + self.float_stable_eps) + wd * w))
+
+
+@register
+class RMSProp(Optimizer):
+    def __init__(self, learning_rate=0.001, gamma1=0.9, gamma2=0.9, epsilon=1e-8, centered=False,
+                 clip_weights=None, **kwargs):
+        super().__init__(learning_rate=learning_rate, **kwargs)
+        self.gamma1 = gamma1
+        self.gamma2 = gamma2
+        self.centered = centered
+        self.epsilon = epsilon
+        self.clip_weights = clip_weights
+
+    def create_state(self, index, weight):
+        z = lambda: NDArray(torch.zeros_like(weight._data))
+        if self.centered:
+            return (z(), z(), z())
+        return (z(),)
+
+    def update(self, index, weight, grad, state):
+        self._update_count(index)
+        lr = self._get_lr(index)
+        wd = self._get_wd(index)
+        cw = -1.0 if self.clip_weights is None else self.clip_weights
+        if not self.centered:
+            _oo.rmsprop_update(weight._data, grad._data, state[0]._data, lr=lr, gamma1=self.gamma1,
+                               epsilon=self.epsilon, wd=wd, rescale_grad=self.rescale_grad,
+                               clip_gradient=self._clip(), clip_weights=cw)
+        else:
+            n, g, delta = state
+            _oo.rmspropalex_update(weight._data, grad._data, n._data, g._data, delta._data, lr=lr,
+                                   gamma1=self.gamma1, gamma2=self.gamma2, epsilon=self.epsilon, wd=wd,
+                                   rescale_grad=self.rescale_grad, clip_gradient=self._clip(), clip_weights=cw)
+
+
+@register
+class AdaDelta(Optimizer):
+    def __init__(self, rho=0.90, epsilon=1e-5, **kwargs):
+        super().__init__(**kwargs)
+        self.rho = rho
+        self.epsilon = epsilon
+
+    def create_state(self, index, weight):
+        return (NDArray(torch.zeros_like(weight._data)), NDArray(torch.zeros_like(weight._data)))
+
+    @torch.no_grad()
+    def update(self, index, weight, grad, state):
+        self._update_count(index)
+        wd = self._get_wd(index)
+        g = grad._data * self.rescale_grad
+        if self.clip_gradient is not None:
+            g = torch.clamp(g, -self.clip_gradient, self.clip_gradient)
+        acc_g, acc_delta = state
+        acc_g._data.mul_(self.rho).add_((1. - self.rho) * g * g)
+        current_delta = torch.sqrt(acc_delta._data + self.epsilon) / torch.sqrt(acc_g._data + self.epsilon) * g
+        acc_delta._data.mul_(self.rho).add_((1. - self.rho) * current_delta * current_delta)
+        weight._data.sub_(current_delta + wd * weight._data)
+
+
+@register
+class Ftrl(Optimizer):
+    def __init__(self, lamda1=0.01, learning_rate=0.1, beta=1, **kwargs):
+        super().__init__(learning_rate=learning_rate, **kwargs)
+        self.lamda1 = lamda1
+        self.beta = beta
+
+    def create_state(self, index, weight):
+        return (NDArray(torch.zeros_like(weight._data)), NDArray(torch.zeros_like(weight._data)))
+
+    def update(self, index, weight, grad, state):
+        self._update_count(index)
+        wd = self._get_wd(index)
+        lr = self._get_lr(index)
+        z, n = state
+        _oo.ftrl_update(weight._data, grad._data, z._data, n._data, lr=lr, lamda1=self.lamda1, beta=self.beta,
+                        wd=wd, rescale_grad=self.rescale_grad, clip_gradient=self._clip())
+
+
+@register
+class Adamax(Optimizer):
+    def __init__(self, learning_rate=0.002, beta1=0.9, beta2=0.999, **kwargs):
+        super().__init__(learning_rate=learning_rate, **kwargs)
+        self.beta1 = beta1
+        self.beta2 = beta2
+
+    def create_state(self, index, weight):
+        return (NDArray(torch.zeros_like(weight._data)), NDArray(torch.zeros_like(weight._data)))
+
+    @torch.no_grad()
+    def update(self, index, weight, grad, state):
+        self._update_count(index)
+        lr = self._get_lr(index)
+        wd = self._get_wd(index)
+        t = self._index_update_count[index]
+        lr /= (1. - self.beta1 ** t)
+        g = grad._data * self.rescale_grad + wd * weight._data
+        if self.clip_gradient is not None:
+            g = torch.clamp(g, -self.clip_gradient, self.clip_gradient)
+        m_t, u_t = state
+        m_t._data.mul_(self.beta1).add_((1. - self.beta1) * g)
+        u_t._data.copy_(torch.maximum(self.beta2 * u_t._data, torch.abs(g)))
+        weight._data.sub_(lr * m_t._data / u_t._data)
+
+
+@register
+class Nadam(Optimizer):
+    def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8, schedule_decay=0.004, **kwargs):
+        super().__init__(learning_rate=learning_rate, **kwargs)
+        self.beta1 = beta1
+        self.beta2 = beta2
+        self.epsilon = epsilon
+        self.schedule_decay = schedule_decay
+        self.m_schedule = 1.
+
+    def create_state(self, index, weight):
+        return (NDArray(torch.zeros_like(weight._data)), NDArray(torch.zeros_like(weight._data)))
+
+    @torch.no_grad()
+    def update(self, index, weight, grad, state):
+        self._update_count(index)
+        lr = self._get_lr(index)
+        wd = self._get_wd(index)
+        t = self._index_update_count[index]
+        g = grad._data * self.rescale_grad + wd * weight._data
+        if self.clip_gradient is not None:
+            g = torch.clamp(g, -self.clip_gradient, self.clip_gradient)
+        momentum_t = self.beta1 * (1. - 0.5 * (pow(0.96, t * self.schedule_decay)))
+        momentum_t_1 = self.beta1 * (1. - 0.5 * (pow(0.96, (t + 1) * self.schedule_decay)))
+        self.m_schedule = self.m_schedule * momentum_t
+        m_schedule_next = self.m_schedule * momentum_t_1
+        m_t, v_t = state
+        m_t._data.mul_(self.beta1).add_((1. - self.beta1) * g)
+        v_t._data.mul_(self.beta2).add_((1. - self.beta2) * g * g)
+        grad_prime = g / (1. - self.m_schedule)
+        m_t_prime = m_t._data / (1. - m_schedule_next)
+        v_t_prime = v_t._data / (1. - pow(self.beta2, t))
+        m_t_bar = (1. - momentum_t) * grad_prime + momentum_t_1 * m_t_prime
+        weight._data.sub_(lr * m_t_bar / (torch.sqrt(v_t_prime) + self.epsilon))
+
+
+@register
+class GroupAdaGrad(Optimizer):
+    """AdaGrad with one accumulator per row (python/mxnet/optimizer/contrib.py)."""
+
+    def __init__(self, eps=1e-6, **kwargs):
+        super().__init__(**kwargs)
+        self.float_stable_eps = eps
+
+    def create_state(self, index, weight):
+        assert len(weight.shape) == 2
+        return NDArray(torch.zeros((weight.shape[0], 1), dtype=weight._data.dtype, device=weight._data.device))
+
+    @torch.no_grad()
+    def update(self, index, weight, grad, state):
+        self._update_count(index)
+        lr = self._get_lr(index)
+        wd = self._get_wd(index)
+        assert wd == 0, 'Weight decay is not supported for GroupAdaGrad'
+        g = grad._data * self.rescale_grad
+        if self.clip_gradient is not None:
+            g = torch.clamp(g, -self.clip_gradient, self.clip_gradient)
+        state._data.add_((g * g).mean(1, keepdim=True))
+        weight._data.sub_(lr * g / torch.sqrt(state._data + self.float_stable_eps))
+
+
+@register
+class Test(Optimizer):
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+
+    def create_state(self, index, weight):
+        return NDArray(torch.zeros_like(weight._data))
+
+    @torch.no_grad()
+    def update(self, index, weight, grad, state):
+        weight._data.add_(grad._data * self.rescale_grad)
+        state._data.copy_(weight._data)
+
+
+class Updater:
+    """Updater for kvstore (applies an Optimizer given index, grad, weight)."""
+
+    def __init__(self, optimizer):
+        self.optimizer = optimizer
+        self.states = {}
+        self.states_synced = {}
+        self.aggregate_updates = optimizer.aggregate_num > 0
+
+    def __call__(self, index, grad, weight):
+        if not isinstance(index, (list, tuple)):
+            indices, grads, weights = [index], [grad], [weight]
+        else:
+            indices, grads, weights = index, grad, weight
+        for i, idx in enumerate(indices):
+            if idx not in self.states:
+                self.states[idx] = self.optimizer.create_state_multi_precision(idx, weights[i])
+                self.states_synced[idx] = True
+            elif not self.states_synced[idx]:
+                self.states[idx] = self.sync_state_context(self.states[idx], weights[i].context)
+                self.states_synced[idx] = True
+        if self.aggregate_updates and isinstance(self.optimizer, SGD):
+            self.optimizer.update_multi_precision(list(indices), list(weights), list(grads),
+                                                  [self.states[i] for i in indices])
+        else:
+            for i, w, g in zip(indices, weights, grads):
+                self.optimizer.update_multi_precision(i, w, g, self.states[i])
+
+    def sync_state_context(self, state, context):
+        if isinstance(state, NDArray):
+            return state.as_in_context(context)
+        if isinstance(state, (tuple, list)):
+            synced = [self.sync_state_context(i, context) for i in state]
+            return tuple(synced) if isinstance(state, tuple) else synced
+        return state
+
+    def set_states(self, states):
+        states = pickle.loads(states)
+        if isinstance(states, tuple) and len(states) == 2:
+            self.states, self.optimizer = states
+        else:
+            self.states = states
+        self.states_synced = dict.fromkeys(self.states.keys(), False)
+
+    def get_states(self, dump_optimizer=False):
+        return pickle.dumps((self.states, self.optimizer) if dump_optimizer else self.states)
+
+
+def get_updater(optimizer):
+    return Updater(optimizer)

@@ -1,0 +1,13 @@
+"""Symbolic API (mx.sym).  Parity: python/mxnet/symbol/__init__.py."""
+from ..ops import load_all as _load_all
+_load_all()
+from ..ops import registry as _registry
+from .symbol import *  # noqa: F401,F403
+from .symbol import Symbol, _op_func, _create  # noqa: F401
+from . import op, _internal, contrib, linalg, random, image, sparse  # noqa: F401
+
+_g = globals()
+for _n in _registry.list_ops():
+    if _n not in _g:
+        _g[_n] = _op_func(_n)
+del _g

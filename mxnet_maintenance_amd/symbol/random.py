@@ -1,0 +1,35 @@
+"""Symbolic random sampling (mx.sym.random).  Parity: python/mxnet/symbol/random.py."""
+from .symbol import _op_func, Symbol
+
+
+def _dispatch(scalar_op, tensor_op, params):
+    def f(*args, shape=None, dtype=None, name=None, **kwargs):
+        vals = dict(zip(params, args))
+        vals.update({k: v for k, v in kwargs.items() if k in params})
+        if any(isinstance(v, Symbol) for v in vals.values()):
+            return _op_func(tensor_op)(*[vals[p] for p in params], shape=shape or (), name=name)
+        kw = {k: v for k, v in vals.items()}
+        kw['shape'] = shape or ()
+        if dtype is not None:
+            kw['dtype'] = dtype
+        return _op_func(scalar_op)(name=name, **kw)
+    return f
+
+
+uniform = _dispatch('_random_uniform', '_sample_uniform', ['low', 'high'])
+normal = _dispatch('_random_normal', '_sample_normal', ['loc', 'scale'])
+gamma = _dispatch('_random_gamma', '_random_gamma', ['alpha', 'beta'])
+exponential = _dispatch('_random_exponential', '_random_exponential', ['lam'])
+poisson = _dispatch('_random_poisson', '_random_poisson', ['lam'])
+negative_binomial = _dispatch('_random_negative_binomial', '_random_negative_binomial', ['k', 'p'])
+generalized_negative_binomial = _dispatch('_random_generalized_negative_binomial',
+                                          '_random_generalized_negative_binomial', ['mu', 'alpha'])
+randint = _dispatch('_random_randint', '_random_randint', ['low', 'high'])
+
+
+def multinomial(data, shape=None, get_prob=False, dtype='int32', name=None):
+    return _op_func('_sample_multinomial')(data, shape=shape or (), get_prob=get_prob, dtype=dtype, name=name)
+
+
+def shuffle(data, name=None):
+    return _op_func('_shuffle')(data, name=name)

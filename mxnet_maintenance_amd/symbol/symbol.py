@@ -1,0 +1,839 @@
+"""Symbolic graphs.
+
+Parity: python/mxnet/symbol/symbol.py (Symbol, Variable/var, Group, load,
+load_json, composition, attributes, list_arguments/outputs/auxiliary_states,
+get_internals, get_children, infer_shape(_partial), infer_type, tojson, save,
+bind, simple_bind, eval, arithmetic overloads) and the nnvm graph JSON format
+(3rdparty/tvm/nnvm/src/pass/saveload_json.cc, including the legacy
+``param``/``attr``/``backward_source_id`` layout read by LoadLegacyJSON).
+
+A Symbol is a list of output entries ``(node, index)`` over a DAG of ``_Node``.
+Shape/type inference executes the operator implementations on PyTorch ``meta``
+tensors, so every registered operator is inferable without a separate
+shape function; parameter shapes that cannot be derived forward (weights) come
+from the operator's ``infer_params`` hook.
+"""
+import copy
+import json
+import warnings
+
+import numpy as np
+import torch
+
+from ..attribute import AttrScope
+from ..base import MXNetError, numeric_types, torch_dtype, np_dtype, dtype_name
+from ..name import NameManager
+from ..ops import registry
+
+__all__ = ['Symbol', 'var', 'Variable', 'Group', 'load', 'load_json', 'zeros', 'ones', 'full', 'arange',
+           'pow', 'maximum', 'minimum', 'hypot', 'eye', 'linspace', 'histogram', 'split_v2']
+
+_MXNET_VERSION = 10901
+
+
+class _Node:
+    __slots__ = ('op', 'name', 'attrs', 'inputs', '_parsed', '__weakref__')
+
+    def __init__(self, op, name, attrs=None, inputs=None):
+        self.op = op          # OpDef name or None for a variable
+        self.name = name
+        self.attrs = dict(attrs or {})   # string attributes (op params + user attrs)
+        self.inputs = list(inputs or [])  # list of (node, out_index)
+        self._parsed = None
+
+    def is_var(self):
+        return self.op is None
+
+    def opdef(self):
+        return registry.get(self.op)
+
+    def parsed(self):
+        if self._parsed is None:
+            op = self.opdef()
+            params = {k: v for k, v in self.attrs.items() if k in op.params}
+            self._parsed = op.parse_attrs(params)
+        return self._parsed
+
+    def num_outputs(self):
+        if self.op is None:
+            return 1
+        return self.opdef().get_num_outputs(self.parsed())
+
+    def num_visible_outputs(self):
+        if self.op is None:
+            return 1
+        return self.opdef().get_num_visible_outputs(self.parsed())
+
+
+def _topo(entries):
+    order, seen = [], set()
+    stack = [(e[0], False) for e in reversed(entries)]
+    while stack:
+        node, done = stack.pop()
+        if done:
+            order.append(node)
+            continue
+        if id(node) in seen:
+            continue
+        seen.add(id(node))
+        stack.append((node, True))
+        for inp, _ in reversed(node.inputs):
+            if id(inp) not in seen:
+                stack.append((inp, False))
+    return order
+
+
+def _aux_var_ids(order):
+    aux = set()
+    for n in order:
+        if n.op is None:
+            continue
+        op = n.opdef()
+        nargs = len(op.get_arg_names(n.parsed()))
+        for i, (inp, _) in enumerate(n.inputs):
+            if i >= nargs and inp.op is None:
+                aux.add(id(inp))
+    return aux
+
+
+def _attr_lookup(attrs, key):
+    if key in attrs:
+        return attrs[key]
+    dk = '__%s__' % key
+    if dk in attrs:
+        return attrs[dk]
+    if key.startswith('__') and key.endswith('__') and key[2:-2] in attrs:
+        return attrs[key[2:-2]]
+    return None
+
+
+class Symbol:
+    """Symbolic expression: an ordered list of output entries of a graph."""
+    __array_priority__ = 1000.0
+
+    def __init__(self, outputs):
+        self._outputs = list(outputs)
+
+    # ------------------------------------------------------------ structure
+    @property
+    def name(self):
+        if len(self._outputs) != 1:
+            return None
+        node, idx = self._outputs[0]
+        return node.name
+
+    @property
+    def handle(self):
+        return self
+
+    def __repr__(self):
+        name = self.name
+        if name is None:
+            return '<Symbol group [%s]>' % ', '.join(s.name for s in self)
+        return '<Symbol %s>' % name
+
+    def __iter__(self):
+        return (Symbol([o]) for o in self._outputs)
+
+    def __len__(self):
+        return len(self._outputs)
+
+    def __copy__(self):
+        return self.__deepcopy__(None)
+
+    def __deepcopy__(self, memo):
+        return load_json(self.tojson())
+
+    def __getstate__(self):
+        return {'json': self.tojson()}
+
+    def __setstate__(self, state):
+        self._outputs = load_json(state['json'])._outputs
+
+    def __getitem__(self, index):
+        if isinstance(index, str):
+            names = self.list_outputs()
+            idx = [i for i, n in enumerate(names) if n == index]
+            if len(idx) != 1:
+                raise ValueError('There are multiple outputs with name "%s"' % index if idx else
+                                 'Cannot find output that matches name "%s"' % index)
+            index = idx[0]
+        if isinstance(index, slice):
+            return Symbol(self._outputs[index])
+        return Symbol([self._outputs[index]])
+
+    def _topo(self):
+        return _topo(self._outputs)
+
+    def list_arguments(self):
+        order = self._topo()
+        aux = _aux_var_ids(order)
+        return [n.name for n in order if n.op is None and id(n) not in aux]
+
+    def list_auxiliary_states(self):
+        order = self._topo()
+        aux = _aux_var_ids(order)
+        return [n.name for n in order if n.op is None and id(n) in aux]
+
+    def list_inputs(self):
+        return [n.name for n in self._topo() if n.op is None]
+
+    def list_outputs(self):
+        names = []
+        for node, idx in self._outputs:
+            if node.op is None:
+                names.append(node.name)
+                continue
+            op = node.opdef()
+            if op.output_names:
+                names.append('%s_%s' % (node.name, op.output_names[idx]))
+            elif node.num_outputs() == 1:
+                names.append(node.name + '_output')
+            else:
+                names.append('%s_output%d' % (node.name, idx))
+        return names
+
+    def get_internals(self):
+        outs = []
+        for n in self._topo():
+            k = n.num_outputs() if n.op is not None else 1
+            for i in range(k):
+                outs.append((n, i))
+        return Symbol(outs)
+
+    def get_children(self):
+        if len(self._outputs) != 1:
+            return None
+        node, _ = self._outputs[0]
+        if not node.inputs:
+            return None
+        return Symbol(list(node.inputs))
+
+    def _var_nodes(self):
+        return {n.name: n for n in self._topo() if n.op is None}
+
+    # ------------------------------------------------------------ attributes
+    def attr(self, key):
+        if len(self._outputs) != 1:
+            return None
+        return _attr_lookup(self._outputs[0][0].attrs, key)
+
+    def list_attr(self, recursive=False):
+        if recursive:
+            raise DeprecationWarning('Symbol.list_attr with recursive=True has been deprecated. '
+                                     'Please use attr_dict instead.')
+        return dict(self._outputs[0][0].attrs)
+
+    def attr_dict(self):
+        ret = {}
+        for n in self._topo():
+            if n.attrs:
+                ret[n.name] = dict(n.attrs)
+        return ret
+
+    def _set_attr(self, **kwargs):
+        for k, v in kwargs.items():
+            if not isinstance(v, str):
+                raise ValueError('Set Attr only accepts string values')
+            for node, _ in self._outputs:
+                node.attrs[k] = v
+                node._parsed = None
+
+    # ----------------------------------------------------------- composition
+    def __call__(self, *args, **kwargs):
+        s = copy.deepcopy(self)
+        s._compose(*args, **kwargs)
+        return s
+
+    def _compose(self, *args, **kwargs):
+        name = kwargs.pop('name', None)
+        vars_ = self._var_nodes()
+        order = self._topo()
+        repl = {}
+        if args:
+            argnames = self.list_arguments()
+            for n, a in zip(argnames, args):
+                repl[n] = a
+        for k, v in kwargs.items():
+            if k in vars_:
+                repl[k] = v
+        for n in order:
+            n.inputs = [((repl[i.name]._outputs[0][0], repl[i.name]._outputs[0][1]) if i.op is None and i.name in repl
+                         else (i, j)) for i, j in n.inputs]
+        self._outputs = [((repl[o.name]._outputs[0]) if o.op is None and o.name in repl else (o, i))
+                         for o, i in self._outputs]
+        if name and len(self._outputs) == 1:
+            self._outputs[0][0].name = name
+
+    # ------------------------------------------------------------ arithmetic
+    def _bin(self, other, bop, sop, reverse=False):
+        if isinstance(other, Symbol):
+            return _create(bop, [other, self] if reverse else [self, other], {})
+        if isinstance(other, numeric_types):
+            return _create(sop, [self], {'scalar': float(other)})
+        raise TypeError('type %s not supported' % str(type(other)))
+
+    def __add__(self, o):
+        return self._bin(o, 'elemwise_add', '_plus_scalar')
+
+    __radd__ = __add__
+
+    def __sub__(self, o):
+        return self._bin(o, 'elemwise_sub', '_minus_scalar')
+
+    def __rsub__(self, o):
+        return self._bin(o, 'elemwise_sub', '_rminus_scalar', reverse=True)
+
+    def __mul__(self, o):
+        return self._bin(o, 'elemwise_mul', '_mul_scalar')
+
+    __rmul__ = __mul__
+
+    def __truediv__(self, o):
+        return self._bin(o, 'elemwise_div', '_div_scalar')
+
+    def __rtruediv__(self, o):
+        return self._bin(o, 'elemwise_div', '_rdiv_scalar', reverse=True)
+
+    __div__ = __truediv__
+    __rdiv__ = __rtruediv__
+
+    def __mod__(self, o):
+        return self._bin(o, '_mod', '_mod_scalar')
+
+    def __rmod__(self, o):
+        return self._bin(o, '_mod', '_rmod_scalar', reverse=True)
+
+    def __pow__(self, o):
+        return self._bin(o, '_power', '_power_scalar')
+
+    def __rpow__(self, o):
+        return self._bin(o, '_power', '_rpower_scalar', reverse=True)
+
+    def __neg__(self):
+        return self.__mul__(-1.0)
+
+    def __eq__(self, o):
+        return self._bin(o, '_equal', '_equal_scalar')
+
+    def __ne__(self, o):
+        return self._bin(o, '_not_equal', '_not_equal_scalar')
+
+    def __gt__(self, o):
+        return self._bin(o, '_greater', '_greater_scalar')
+
+    def __ge__(self, o):
+        return self._bin(o, '_greater_equal', '_greater_equal_scalar')
+
+    def __lt__(self, o):
+        return self._bin(o, '_lesser', '_lesser_scalar')
+
+    def __le__(self, o):
+        return self._bin(o, '_lesser_equal', '_lesser_equal_scalar')
+
+    def __hash__(self):
+        return id(self)
+
+    def __abs__(self):
+        return _create('abs', [self], {})
+
+    def __getattr__(self, name):
+        if name.startswith('__'):
+            raise AttributeError(name)
+        from ..ndarray.ndarray import _FLUENT
+        if name in _FLUENT and registry.has(_FLUENT[name]):
+            opname = _FLUENT[name]
+            return lambda *a, **k: _op_func(opname)(self, *a, **k)
+        if name in ('reshape', 'transpose', 'flatten', 'expand_dims', 'squeeze', 'astype', 'split',
+                    'broadcast_to', 'broadcast_like', 'reshape_like', 'zeros_like', 'ones_like',
+                    'slice', 'swapaxes', 'diag'):
+            opname = {'reshape': 'Reshape', 'flatten': 'Flatten', 'astype': 'Cast', 'split': 'SliceChannel'}.get(name, name)
+
+            def f(*a, **k):
+                if name == 'reshape' and a:
+                    k['shape'] = a[0] if len(a) == 1 and isinstance(a[0], (tuple, list)) else a
+                    a = ()
+                if name == 'transpose' and a:
+                    k['axes'] = a[0] if len(a) == 1 and isinstance(a[0], (tuple, list)) else a
+                    a = ()
+                if name == 'astype' and a:
+                    k['dtype'] = a[0]
+                    a = ()
+                return _op_func(opname)(self, *a, **k)
+            return f
+        raise AttributeError("'Symbol' object has no attribute '%s'" % name)
+
+    # ----------------------------------------------------------- inference
+    def infer_shape(self, *args, **kwargs):
+        res = self._infer(args, kwargs, partial=False, what='shape')
+        return res
+
+    def infer_shape_partial(self, *args, **kwargs):
+        return self._infer(args, kwargs, partial=True, what='shape')
+
+    def infer_type(self, *args, **kwargs):
+        return self._infer(args, kwargs, partial=False, what='type')
+
+    def infer_type_partial(self, *args, **kwargs):
+        return self._infer(args, kwargs, partial=True, what='type')
+
+    def _infer(self, args, kwargs, partial, what):
+        arg_names = self.list_arguments()
+        known = {}
+        if args:
+            for n, v in zip(arg_names, args):
+                if v is not None:
+                    known[n] = v
+        for k, v in kwargs.items():
+            if v is not None:
+                known[k] = v
+        if what == 'shape':
+            shapes, dtypes = {k: tuple(v) for k, v in known.items()}, {}
+        else:
+            shapes, dtypes = {}, {k: torch_dtype(v) for k, v in known.items()}
+        res = infer_graph(self, shapes, dtypes, what=what)
+        arg_res, out_res, aux_res = res
+        if what == 'shape':
+            complete = all(s is not None for s in arg_res + out_res + aux_res)
+            if not complete and not partial:
+                warnings.warn('Cannot decide shape for some arguments', stacklevel=2)
+                return None, None, None
+            fix = lambda l: [s if s is not None else () for s in l]
+            return fix(arg_res), fix(out_res), fix(aux_res)
+        complete = all(s is not None for s in arg_res + out_res + aux_res)
+        if not complete and not partial:
+            return None, None, None
+        conv = lambda l: [np_dtype(d) if d is not None else None for d in l]
+        return conv(arg_res), conv(out_res), conv(aux_res)
+
+    # --------------------------------------------------------- serialization
+    def tojson(self, remove_amp_cast=True):
+        order = self._topo()
+        index = {id(n): i for i, n in enumerate(order)}
+        nodes, arg_nodes, row_ptr = [], [], [0]
+        for i, n in enumerate(order):
+            d = {'op': 'null' if n.op is None else n.op, 'name': n.name,
+                 'inputs': [[index[id(a)], j, 0] for a, j in n.inputs]}
+            if n.attrs:
+                d['attrs'] = {k: str(v) for k, v in n.attrs.items()}
+            nodes.append(d)
+            if n.op is None:
+                arg_nodes.append(i)
+            row_ptr.append(row_ptr[-1] + (n.num_outputs() if n.op is not None else 1))
+        heads = [[index[id(n)], j, 0] for n, j in self._outputs]
+        return json.dumps({'nodes': nodes, 'arg_nodes': arg_nodes, 'node_row_ptr': row_ptr,
+                           'heads': heads, 'attrs': {'mxnet_version': ['int', _MXNET_VERSION]}},
+                          indent=2)
+
+    def save(self, fname, remove_amp_cast=True):
+        with open(fname, 'w') as f:
+            f.write(self.tojson())
+
+    # --------------------------------------------------------------- binding
+    def bind(self, ctx, args, args_grad=None, grad_req='write', aux_states=None, group2ctx=None,
+             shared_exec=None):
+        from ..executor import Executor
+        return Executor(self, ctx, args, args_grad, grad_req, aux_states)
+
+    def _bind(self, *a, **k):
+        return self.bind(*a, **k)
+
+    def simple_bind(self, ctx, grad_req='write', type_dict=None, stype_dict=None, group2ctx=None,
+                    shared_arg_names=None, shared_exec=None, shared_buffer=None, **kwargs):
+        from ..executor import Executor
+        from .. import ndarray as nd
+        arg_shapes, _, aux_shapes = self.infer_shape(**kwargs)
+        if arg_shapes is None:
+            raise MXNetError('simple_bind: cannot infer shapes from %s' % kwargs)
+        arg_names = self.list_arguments()
+        type_dict = type_dict or {}
+        arg_types, _, aux_types = self.infer_type(**{k: v for k, v in type_dict.items() if k in arg_names})
+        if arg_types is None:
+            arg_types = [np.float32] * len(arg_names)
+            aux_types = [np.float32] * len(aux_shapes)
+        args = []
+        for n, s, t in zip(arg_names, arg_shapes, arg_types):
+            if shared_buffer is not None and n in shared_buffer and shared_buffer[n].shape == tuple(s):
+                args.append(shared_buffer[n])
+            else:
+                a = nd.zeros(s, ctx=ctx, dtype=t or np.float32)
+                if shared_buffer is not None:
+                    shared_buffer[n] = a
+                args.append(a)
+        if isinstance(grad_req, str):
+            reqs = {n: grad_req for n in arg_names}
+        elif isinstance(grad_req, (list, tuple)):
+            reqs = dict(zip(arg_names, grad_req))
+        else:
+            reqs = {n: grad_req.get(n, 'null') for n in arg_names}
+        grads = {n: nd.zeros(s, ctx=ctx, dtype=t or np.float32)
+                 for n, s, t in zip(arg_names, arg_shapes, arg_types) if reqs.get(n, 'null') != 'null'}
+        aux = [nd.zeros(s, ctx=ctx, dtype=t or np.float32) for s, t in zip(aux_shapes, aux_types)]
+        return Executor(self, ctx, args, grads, reqs, aux)
+
+    def eval(self, ctx=None, **kwargs):
+        from ..context import current_context
+        ctx = ctx or current_context()
+        ex = self.bind(ctx, kwargs)
+        return ex.forward()
+
+    def gradient(self, wrt):
+        raise NotImplementedError('Symbol.gradient is not supported; use autograd or Executor.backward')
+
+    def debug_str(self):
+        lines = []
+        for n in self._topo():
+            if n.op is None:
+                lines.append('Variable:%s' % n.name)
+            else:
+                lines.append('Op:%s, Name=%s\nInputs:\n%s' % (n.op, n.name, '\n'.join(
+                    '\targ[%d]=%s(%d)' % (i, a.name, j) for i, (a, j) in enumerate(n.inputs))))
+        return '\n'.join(lines)
+
+    def optimize_for(self, backend, args=None, aux=None, ctx=None, **kwargs):
+        return self
+
+    def get_backend_symbol(self, backend):
+        return self
+
+
+# ---------------------------------------------------------------------------
+# graph construction
+# ---------------------------------------------------------------------------
+
+def _create(op_name, inputs, attrs, name=None, attr=None):
+    """Create a Symbol applying ``op_name`` to input Symbols (missing args become variables)."""
+    op = registry.get(op_name)
+    hint = op.name.lower()
+    name = NameManager.current().get(name, hint)
+    scope_attr = AttrScope.current().get(attr)
+    node_attrs = {}
+    for k, v in attrs.items():
+        if v is None:
+            continue
+        node_attrs[k] = registry.format_value(v) if not isinstance(v, str) else v
+    for k, v in (scope_attr or {}).items():
+        node_attrs[k] = v
+        if not (k.startswith('__') and k.endswith('__')):
+            node_attrs['__%s__' % k] = v
+    node = _Node(op.name, name, node_attrs)
+    parsed = node.parsed()
+    arg_names = op.get_arg_names(parsed)
+    aux_names = op.get_aux_names(parsed)
+    entries = []
+    if isinstance(inputs, dict):
+        pos, named = inputs.get('_pos', []), {k: v for k, v in inputs.items() if k != '_pos'}
+    else:
+        pos, named = inputs, {}
+    all_names = arg_names + aux_names
+    var_attrs = {k: v for k, v in (scope_attr or {}).items() if k.startswith('__') and k.endswith('__')}
+    for i, an in enumerate(all_names):
+        s = None
+        if i < len(pos):
+            s = pos[i]
+        elif an in named:
+            s = named[an]
+        if s is None:
+            v = _Node(None, '%s_%s' % (name, an), dict(var_attrs))
+            entries.append((v, 0))
+        else:
+            if len(s._outputs) != 1:
+                raise MXNetError('Cannot compose a grouped symbol as input %s of %s' % (an, name))
+            entries.append(s._outputs[0])
+    for s in pos[len(all_names):]:
+        entries.append(s._outputs[0])
+    node.inputs = entries
+    nvis = node.num_visible_outputs()
+    return Symbol([(node, i) for i in range(nvis)])
+
+
+def _op_func(op_name):
+    op = registry.get(op_name)
+
+    def f(*args, **kwargs):
+        name = kwargs.pop('name', None)
+        attr = kwargs.pop('attr', None)
+        kwargs.pop('out', None)
+        pos = []
+        for a in args:
+            if isinstance(a, Symbol):
+                pos.append(a)
+            elif isinstance(a, (list, tuple)) and a and all(isinstance(x, Symbol) for x in a):
+                pos.extend(a)
+            elif a is None:
+                pos.append(None)
+            else:
+                raise TypeError('%s: positional arguments must be Symbols, got %s' % (op_name, type(a)))
+        named = {k: v for k, v in kwargs.items() if isinstance(v, Symbol)}
+        attrs = {k: v for k, v in kwargs.items() if not isinstance(v, Symbol)}
+        extra = {}
+        for k in list(attrs):
+            if k not in op.params and k not in ('num_args',) and not callable(op.arg_names):
+                if k in ('lr_mult', 'wd_mult', 'ctx_group', 'force_mirroring', 'init', 'dtype_hint'):
+                    extra[k] = str(attrs.pop(k))
+        if op.key_var_num_args and op.key_var_num_args not in attrs:
+            attrs[op.key_var_num_args] = len(pos) + len(named)
+        if 'dtype' in attrs and attrs['dtype'] is not None and not isinstance(attrs['dtype'], str):
+            attrs['dtype'] = dtype_name(attrs['dtype'])
+        if extra:
+            attr = dict(attr or {})
+            for k, v in extra.items():
+                attr[k] = v
+        inputs = {'_pos': pos}
+        inputs.update(named)
+        return _create(op_name, inputs, attrs, name=name, attr=attr)
+    f.__name__ = op_name
+    return f
+
+
+def var(name, attr=None, shape=None, lr_mult=None, wd_mult=None, dtype=None, init=None, stype=None,
+        **kwargs):
+    """Create a symbolic variable."""
+    if not isinstance(name, str):
+        raise TypeError('Expect a string for variable `name`')
+    attr = AttrScope.current().get(attr)
+    attrs = {}
+    for k, v in (attr or {}).items():
+        attrs[k] = v
+    if shape is not None:
+        attrs['__shape__'] = registry.format_value(tuple(shape))
+    if lr_mult is not None:
+        attrs['__lr_mult__'] = str(lr_mult)
+    if wd_mult is not None:
+        attrs['__wd_mult__'] = str(wd_mult)
+    if dtype is not None:
+        attrs['__dtype__'] = str(np.dtype(dtype).name if dtype != 'bfloat16' else 'bfloat16')
+    if init is not None:
+        if not isinstance(init, str):
+            init = init.dumps()
+        attrs['__init__'] = init
+    if stype is not None:
+        attrs['__storage_type__'] = str(stype)
+    for k, v in kwargs.items():
+        if k.startswith('__') and k.endswith('__'):
+            attrs[k] = str(v)
+        else:
+            raise ValueError('Attribute name=%s is not supported. Additional attributes must start and '
+                             'end with double underscores, e.g, __yourattr__' % k)
+    return Symbol([(_Node(None, name, attrs), 0)])
+
+
+Variable = var
+
+
+def Group(symbols, create_fn=None):
+    if not symbols or any(not isinstance(s, Symbol) for s in symbols):
+        raise TypeError('Expected a list of symbols as input')
+    outs = []
+    for s in symbols:
+        outs.extend(s._outputs)
+    return Symbol(outs)
+
+
+def load_json(json_str):
+    """Load a Symbol from MXNet JSON (current nnvm layout and the legacy 0.8 layout)."""
+    g = json.loads(json_str)
+    nodes = []
+    for nd_ in g['nodes']:
+        op = nd_['op']
+        attrs = {}
+        for key in ('attrs', 'attr', 'param'):
+            if key in nd_ and nd_[key]:
+                attrs.update({k: str(v) for k, v in nd_[key].items()})
+        if 'attr' in nd_ and nd_['attr']:
+            for k, v in nd_['attr'].items():
+                if not (k.startswith('__') and k.endswith('__')):
+                    attrs['__%s__' % k] = str(v)
+        node = _Node(None if op == 'null' else op, nd_['name'], attrs)
+        if op != 'null' and not registry.has(op):
+            raise MXNetError('Operator %s is not registered' % op)
+        node.inputs = [(nodes[e[0]], e[1]) for e in nd_['inputs']]
+        nodes.append(node)
+    # legacy files: ops whose implicit aux inputs were not serialised
+    heads = g.get('heads')
+    if heads is None:
+        heads = [[len(nodes) - 1, 0, 0]]
+    return Symbol([(nodes[h[0]], h[1]) for h in heads])
+
+
+def load(fname):
+    with open(fname) as f:
+        return load_json(f.read())
+
+
+# ---------------------------------------------------------------------------
+# shape/type inference
+# ---------------------------------------------------------------------------
+
+def _attr_shape(node):
+    s = node.attrs.get('__shape__')
+    if s is None:
+        return None
+    t = registry.parse_value('shape', s)
+    if t is None or any(d == 0 for d in t) or len(t) == 0:
+        return None
+    return t
+
+
+def _attr_dtype(node):
+    d = node.attrs.get('__dtype__')
+    if d is None:
+        return None
+    try:
+        return torch_dtype(d)
+    except Exception:
+        return None
+
+
+def _run_meta(op, parsed, shapes, dtypes):
+    ins = []
+    for s, d in zip(shapes, dtypes):
+        if s is None:
+            ins.append(None)
+        else:
+            ins.append(torch.empty(s, dtype=d or torch.float32, device='meta'))
+    kw = dict(parsed)
+    for k in ('ctx',):
+        if k in kw:
+            kw[k] = None
+    try:
+        with torch.no_grad():
+            out = op.fn(*ins, **kw)
+    except Exception:
+        # ops with data-dependent host logic: run on small zero CPU tensors
+        if any(s is not None and int(np.prod(s)) > (1 << 22) for s in shapes):
+            raise
+        ins = [None if s is None else torch.zeros(s, dtype=d or torch.float32) for s, d in zip(shapes, dtypes)]
+        with torch.no_grad():
+            out = op.fn(*ins, **kw)
+    if not isinstance(out, (tuple, list)):
+        out = [out]
+    return [(tuple(o.shape), o.dtype) for o in out]
+
+
+def infer_graph(sym, known_shapes, known_dtypes, what='shape'):
+    """Propagate shapes and dtypes through the graph.
+
+    Returns (arg_list, out_list, aux_list) of shapes (or dtypes), None for unknown.
+    """
+    order = sym._topo()
+    shape = {}   # (id(node), idx) -> shape
+    dtype = {}
+    for n in order:
+        if n.op is None:
+            s = known_shapes.get(n.name, _attr_shape(n))
+            if s is not None:
+                shape[(id(n), 0)] = tuple(s)
+            d = known_dtypes.get(n.name, _attr_dtype(n))
+            if d is not None:
+                dtype[(id(n), 0)] = d
+    default_dt = torch.float32
+    if known_dtypes:
+        default_dt = next(iter(known_dtypes.values()))
+    progress = True
+    done = set()
+    while progress:
+        progress = False
+        for n in order:
+            if n.op is None or id(n) in done:
+                continue
+            op = n.opdef()
+            parsed = n.parsed()
+            in_shapes = [shape.get((id(a), j)) for a, j in n.inputs]
+            if any(s is None for s in in_shapes) and op.infer_params is not None and in_shapes and in_shapes[0] is not None:
+                try:
+                    fill = op.infer_params(in_shapes, parsed)
+                except Exception:
+                    fill = {}
+                for idx, s in fill.items():
+                    if idx < len(n.inputs) and in_shapes[idx] is None:
+                        a, j = n.inputs[idx]
+                        shape[(id(a), j)] = tuple(s)
+                        in_shapes[idx] = tuple(s)
+                        progress = True
+            if any(s is None for s in in_shapes):
+                continue
+            in_dt = [dtype.get((id(a), j)) for a, j in n.inputs]
+            base_dt = next((d for d in in_dt if d is not None), default_dt)
+            in_dt = [d if d is not None else base_dt for d in in_dt]
+            # parameters follow the data dtype unless declared
+            for (a, j), d in zip(n.inputs, in_dt):
+                if (id(a), j) not in dtype and a.op is None:
+                    dtype[(id(a), j)] = d
+            try:
+                outs = _run_meta(op, parsed, in_shapes, in_dt)
+            except Exception as e:
+                raise MXNetError('Error in operator %s (%s): %s' % (n.name, n.op, e))
+            for i, (s, d) in enumerate(outs):
+                shape[(id(n), i)] = s
+                dtype[(id(n), i)] = d
+            done.add(id(n))
+            progress = True
+    aux = _aux_var_ids(order)
+    table = shape if what == 'shape' else dtype
+    args = [table.get((id(n), 0)) for n in order if n.op is None and id(n) not in aux]
+    auxl = [table.get((id(n), 0)) for n in order if n.op is None and id(n) in aux]
+    outs = [table.get((id(n), j)) for n, j in sym._outputs]
+    return args, outs, auxl
+
+
+# ---------------------------------------------------------------------------
+# helper constructors (mirror python/mxnet/symbol/symbol.py module functions)
+# ---------------------------------------------------------------------------
+
+def zeros(shape, dtype=None, **kwargs):
+    return _op_func('_zeros')(shape=shape, dtype=dtype_name(dtype or np.float32), **kwargs)
+
+
+def ones(shape, dtype=None, **kwargs):
+    return _op_func('_ones')(shape=shape, dtype=dtype_name(dtype or np.float32), **kwargs)
+
+
+def full(shape, val, dtype=None, **kwargs):
+    return _op_func('_full')(shape=shape, value=val, dtype=dtype_name(dtype or np.float32), **kwargs)
+
+
+def arange(start, stop=None, step=1.0, repeat=1, infer_range=False, name=None, dtype=None):
+    return _op_func('_arange')(start=start, stop=stop, step=step, repeat=repeat, name=name,
+                               dtype=dtype_name(dtype or np.float32))
+
+
+def linspace(start, stop, num, endpoint=True, name=None, dtype=None):
+    return _op_func('_linspace')(start=start, stop=stop, num=num, endpoint=endpoint, name=name,
+                                 dtype=dtype_name(dtype or np.float32))
+
+
+def eye(N, M=0, k=0, dtype=None, **kwargs):
+    return _op_func('_eye')(N=N, M=M, k=k, dtype=dtype_name(dtype or np.float32), **kwargs)
+
+
+def _sym_or_scalar(bop, sop, rsop=None):
+    def f(left, right):
+        if isinstance(left, Symbol) and isinstance(right, Symbol):
+            return _op_func(bop)(left, right)
+        if isinstance(left, Symbol):
+            return _op_func(sop)(left, scalar=float(right))
+        if isinstance(right, Symbol):
+            return _op_func(rsop or sop)(right, scalar=float(left))
+        raise TypeError('at least one argument must be a Symbol')
+    return f
+
+
+pow = _sym_or_scalar('_power', '_power_scalar', '_rpower_scalar')  # pylint: disable=redefined-builtin
+power = pow
+maximum = _sym_or_scalar('_maximum', '_maximum_scalar')
+minimum = _sym_or_scalar('_minimum', '_minimum_scalar')
+hypot = _sym_or_scalar('_hypot', '_hypot_scalar')
+
+
+def histogram(a, bins=10, range=None, **kwargs):  # pylint: disable=redefined-builtin
+    if isinstance(bins, Symbol):
+        return _op_func('_histogram')(a, bins, **kwargs)
+    return _op_func('_histogram')(a, bin_cnt=bins, range=range, **kwargs)
+
+
+def split_v2(ary, indices_or_sections, axis=0, squeeze_axis=False):
+    if isinstance(indices_or_sections, int):
+        return _op_func('_split_v2')(ary, axis=axis, squeeze_axis=squeeze_axis, sections=indices_or_sections)
+    return _op_func('_split_v2')(ary, axis=axis, squeeze_axis=squeeze_axis,
+                                 indices=(0,) + tuple(indices_or_sections))
