@@ -50,12 +50,17 @@ class _Arena:
         d0 = params[0].list_data()[0]._data
         self.dtype = d0.dtype
         self.device = d0.device
-        self.numel = sum(p.list_data()[0]._data.numel() for p in params)
-        self.w = torch.empty(self.numel, dtype=self.dtype, device=self.device)
-        self.g = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
-        self.views = []
+        align = 64   # every parameter starts on a 64-element (>=128 B) boundary
+        offs = []
         off = 0
         for p in params:
+            offs.append(off)
+            off += (p.list_data()[0]._data.numel() + align - 1) // align * align
+        self.numel = off
+        self.w = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
+        self.g = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
+        self.views = []
+        for p, off in zip(params, offs):
             arr = p.list_data()[0]
             t = arr._data
             n = t.numel()
@@ -66,7 +71,6 @@ class _Arena:
             arr._data = wv.detach()
             arr._set_grad_buffer(gv, p.grad_req)
             self.views.append((off, n, t.shape))
-            off += n
         self.mom = None
         self.w32 = None
 
@@ -218,8 +222,7 @@ class Trainer:
         upd = self._updaters[0]
         for a in self._arenas:
             if o.momentum != 0.0:
-                a.mom = torch.zeros(a.numel, dtype=torch.float32 if (mp and a.dtype != torch.float32) else a.dtype,
-                                    device=a.device)
+                a.mom = torch.zeros(a.numel, dtype=torch.float32, device=a.device)
             if mp and a.dtype in (torch.float16, torch.bfloat16):
                 a.w32 = a.w.float()
             for (off, n, shape), idx in zip(a.views, a.indices):

@@ -134,7 +134,7 @@ def batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_ga
 def global_pool(data, pool_type, channel_last):
     nsp = data.dim() - 2
     if channel_last:
-        if _use_hip(data) and nsp == 2 and pool_type == 'avg':
+        if _use_hip(data) and nsp == 2 and pool_type == 'avg' and _K.gap_ok(data):
             return _K.GlobalAvgPoolNHWC.apply(data)
         dims = tuple(range(1, 1 + nsp))
     else:

@@ -76,4 +76,8 @@ def bn_ok(x):
     return False
 
 
+def gap_ok(x):
+    return False
+
+
 from .kernel_fns import *  # noqa: E402,F401,F403

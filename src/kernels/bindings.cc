@@ -1,0 +1,96 @@
+// pybind11 bindings for the gfx950 kernels (_hip_kernels.so).
+//
+// Every entry point takes raw device pointers (as integers), shapes and the
+// HIP stream to launch on (torch.cuda.current_stream().cuda_stream), so the
+// launches are captured by HIP graphs like any other work on that stream.
+// Shape/alignment validation happens in Python (ops/kernel_fns.py) before the
+// call; the launchers re-check the invariants they rely on.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+
+#include <cstdint>
+#include <stdexcept>
+
+namespace py = pybind11;
+
+namespace mxamd {
+void bn_nhwc_forward(int dtype, const void* x, const void* addend, void* y, const float* gamma, const float* beta,
+                     const float* center, float* part, float* mean, float* invstd, float* var, float* scale,
+                     float* shift, int64_t R, int C, float eps, int training, int relu, int fix_gamma,
+                     hipStream_t s);
+void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, void* dx, void* dz,
+                      const float* gamma, const float* mean, const float* invstd, float* part, float* dgamma,
+                      float* dbeta, float* coef, int64_t R, int C, int relu, int fix_gamma, int training,
+                      hipStream_t s);
+int bn_partials_rows(int64_t R, int C);
+void softmax_ce_forward(int dtype, int label_is_int, const void* logits, const void* label, float* loss, float* lse,
+                        int N, int K, hipStream_t s);
+void softmax_ce_backward(int dtype, int label_is_int, const void* logits, const void* label, const float* lse,
+                         const float* gout, void* dlogits, int N, int K, hipStream_t s);
+void gap_nhwc_forward(int dtype, const void* x, void* y, int N, int HW, int C, hipStream_t s);
+void gap_nhwc_backward(int dtype, const void* dy, void* dx, int N, int HW, int C, hipStream_t s);
+void flat_sgd(int dtype, void* w, const void* g, float* mom, float* w32, int64_t n, float lr, float wd,
+              float momentum, float rescale, float clip, hipStream_t s);
+}  // namespace mxamd
+
+using namespace mxamd;
+
+template <typename T>
+static inline T* P(uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+static inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+static void check_launch(const char* name) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(name) + ": " + hipGetErrorString(e));
+}
+
+PYBIND11_MODULE(_hip_kernels, m) {
+  m.doc() = "gfx950 HIP kernels for mxnet_maintenance_amd";
+  m.attr("arch") = "gfx950";
+
+  m.def("bn_partials_rows", &bn_partials_rows);
+  m.def("bn_nhwc_forward", [](int dt, uintptr_t x, uintptr_t add, uintptr_t y, uintptr_t g, uintptr_t b,
+                              uintptr_t center, uintptr_t part, uintptr_t mean, uintptr_t inv, uintptr_t var,
+                              uintptr_t scale, uintptr_t shift, int64_t R, int C, float eps, int training, int relu,
+                              int fix_gamma, uintptr_t s) {
+    bn_nhwc_forward(dt, P<void>(x), P<void>(add), P<void>(y), P<float>(g), P<float>(b), P<float>(center),
+                    P<float>(part), P<float>(mean), P<float>(inv), P<float>(var), P<float>(scale), P<float>(shift), R,
+                    C, eps, training, relu, fix_gamma, S(s));
+    check_launch("bn_nhwc_forward");
+  });
+  m.def("bn_nhwc_backward", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t y, uintptr_t dx, uintptr_t dz,
+                               uintptr_t g, uintptr_t mean, uintptr_t inv, uintptr_t part, uintptr_t dgamma,
+                               uintptr_t dbeta, uintptr_t coef, int64_t R, int C, int relu, int fix_gamma,
+                               int training, uintptr_t s) {
+    bn_nhwc_backward(dt, P<void>(x), P<void>(dy), P<void>(y), P<void>(dx), P<void>(dz), P<float>(g), P<float>(mean),
+                     P<float>(inv), P<float>(part), P<float>(dgamma), P<float>(dbeta), P<float>(coef), R, C, relu,
+                     fix_gamma, training, S(s));
+    check_launch("bn_nhwc_backward");
+  });
+  m.def("softmax_ce_forward", [](int dt, int li, uintptr_t logits, uintptr_t label, uintptr_t loss, uintptr_t lse,
+                                 int N, int K, uintptr_t s) {
+    softmax_ce_forward(dt, li, P<void>(logits), P<void>(label), P<float>(loss), P<float>(lse), N, K, S(s));
+    check_launch("softmax_ce_forward");
+  });
+  m.def("softmax_ce_backward", [](int dt, int li, uintptr_t logits, uintptr_t label, uintptr_t lse, uintptr_t gout,
+                                  uintptr_t dlogits, int N, int K, uintptr_t s) {
+    softmax_ce_backward(dt, li, P<void>(logits), P<void>(label), P<float>(lse), P<float>(gout), P<void>(dlogits), N,
+                        K, S(s));
+    check_launch("softmax_ce_backward");
+  });
+  m.def("gap_nhwc_forward", [](int dt, uintptr_t x, uintptr_t y, int N, int HW, int C, uintptr_t s) {
+    gap_nhwc_forward(dt, P<void>(x), P<void>(y), N, HW, C, S(s));
+    check_launch("gap_nhwc_forward");
+  });
+  m.def("gap_nhwc_backward", [](int dt, uintptr_t dy, uintptr_t dx, int N, int HW, int C, uintptr_t s) {
+    gap_nhwc_backward(dt, P<void>(dy), P<void>(dx), N, HW, C, S(s));
+    check_launch("gap_nhwc_backward");
+  });
+  m.def("flat_sgd", [](int dt, uintptr_t w, uintptr_t g, uintptr_t mom, uintptr_t w32, int64_t n, float lr,
+                       float wd, float momentum, float rescale, float clip, uintptr_t s) {
+    flat_sgd(dt, P<void>(w), P<void>(g), P<float>(mom), P<float>(w32), n, lr, wd, momentum, rescale, clip, S(s));
+    check_launch("flat_sgd");
+  });
+}

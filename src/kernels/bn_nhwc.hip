@@ -1,0 +1,367 @@
+// Channel-last (NHWC) BatchNorm for gfx950: training statistics, fused
+// apply (+residual add, +ReLU) and fused backward.
+//
+// Parity: src/operator/nn/batch_norm.cu / cudnn_batch_norm (forward with
+// moving statistics, fix_gamma, use_global_stats), contrib BatchNormWithReLU
+// and the "BatchNormAddReLU" residual tail used by MXNet's NHWC ResNet.
+//
+// Design (memory-bound op, so everything is about HBM passes):
+//   forward : 1 read pass for shifted sums (sum(x-k), sum((x-k)^2), k = running
+//             mean: no catastrophic cancellation), 1 read + 1 write pass for
+//             y = x*scale + shift (+addend) (relu).
+//   backward: 1 read pass over (dy, y, x) for sum(dz), sum(dz*(x-mean)) where
+//             dz = relu ? dy*(y>0) : dy, then 1 pass writing
+//             dx = A*dz + B*x + C (and d_addend = dz for the residual branch).
+// Every thread moves 16 bytes (8 x fp16/bf16) per access; a row of C channels
+// is covered by C/8 lanes so loads are fully coalesced for any C % 8 == 0.
+// Reductions: per-thread fp32 registers -> LDS tree -> per-block partials ->
+// one wave per channel combines partials in fp64.
+#include <stdexcept>
+
+#include "common.h"
+
+namespace mxamd {
+
+constexpr int kBnThreads = 256;
+
+struct BnGeom {
+  int tpr;   // threads per row (each covers 8 channels)
+  int cb;    // channels per block (= tpr * 8)
+  int rpi;   // rows per iteration of the block
+};
+
+static inline BnGeom bn_geom(int C) {
+  BnGeom g;
+  g.tpr = C / 8 < kBnThreads ? C / 8 : kBnThreads;
+  g.cb = g.tpr * 8;
+  g.rpi = kBnThreads / g.tpr;
+  return g;
+}
+
+// MODE 0: forward sums of (x - shift) and (x - shift)^2
+// MODE 1: backward sums of dz and dz * (x - mean), dz = relu ? dy * (y > 0) : dy
+template <typename T, int MODE, bool RELU>
+__global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(
+    const T* __restrict__ x, const T* __restrict__ dy, const T* __restrict__ y,
+    const float* __restrict__ center, float* __restrict__ part1, float* __restrict__ part2,
+    int64_t R, int C, int tpr, int rpi, int64_t rows_per_block) {
+  const int tid = threadIdx.x;
+  const int lane_c = tid % tpr;   // which 8-channel group inside the block's channel slice
+  const int lane_r = tid / tpr;   // row offset within an iteration
+  const int cbase = blockIdx.y * tpr * 8 + lane_c * 8;
+  float s1[8], s2[8], k[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    s1[i] = 0.f;
+    s2[i] = 0.f;
+    k[i] = center[cbase + i];
+  }
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  int64_t r1 = r0 + rows_per_block;
+  if (r1 > R) r1 = R;
+  for (int64_t r = r0 + lane_r; r < r1; r += rpi) {
+    const int64_t off = r * C + cbase;
+    Vec8<T> vx;
+    vx.load(x + off);
+    if (MODE == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float d = vx.get(i) - k[i];
+        s1[i] += d;
+        s2[i] += d * d;
+      }
+    } else {
+      Vec8<T> vdy;
+      vdy.load(dy + off);
+      if (RELU) {
+        Vec8<T> vy;
+        vy.load(y + off);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float dz = vy.get(i) > 0.f ? vdy.get(i) : 0.f;
+          s1[i] += dz;
+          s2[i] += dz * (vx.get(i) - k[i]);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float dz = vdy.get(i);
+          s1[i] += dz;
+          s2[i] += dz * (vx.get(i) - k[i]);
+        }
+      }
+    }
+  }
+  // reduce the rpi row-lanes that share a channel group through LDS
+  __shared__ float sh1[kBnThreads * 8];
+  __shared__ float sh2[kBnThreads * 8];
+  const int cb = tpr * 8;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sh1[lane_r * cb + lane_c * 8 + i] = s1[i];
+    sh2[lane_r * cb + lane_c * 8 + i] = s2[i];
+  }
+  __syncthreads();
+  for (int c = tid; c < cb; c += kBnThreads) {
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < rpi; ++rr) {
+      a += sh1[rr * cb + c];
+      b += sh2[rr * cb + c];
+    }
+    const int64_t o = static_cast<int64_t>(blockIdx.x) * C + blockIdx.y * cb + c;
+    part1[o] = a;
+    part2[o] = b;
+  }
+}
+
+// One wave per channel: combine per-block partials (fp64) and emit statistics.
+// MODE 0 (forward): out mean, invstd, var(biased); scale = g*invstd, shift = b - mean*scale
+// MODE 1 (backward): dgamma, dbeta and the dx coefficients A, B, Cc
+template <int MODE>
+__global__ void __launch_bounds__(64) bn_finalize_kernel(
+    const float* __restrict__ part1, const float* __restrict__ part2, int nblk, int C, int64_t R,
+    const float* __restrict__ center, const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ invstd_in, float eps, float* __restrict__ o0, float* __restrict__ o1,
+    float* __restrict__ o2, float* __restrict__ o3, float* __restrict__ o4, float* __restrict__ o5,
+    int fix_gamma, int training) {
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x;
+  double a = 0.0, b = 0.0;
+  for (int i = lane; i < nblk; i += 64) {
+    a += part1[static_cast<int64_t>(i) * C + c];
+    b += part2[static_cast<int64_t>(i) * C + c];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  if (lane != 0) return;
+  const double n = static_cast<double>(R);
+  const float g = fix_gamma ? 1.f : gamma[c];
+  if (MODE == 0) {
+    double m1 = a / n;
+    double var = b / n - m1 * m1;
+    if (var < 0) var = 0;
+    double mean = center[c] + m1;
+    float inv = static_cast<float>(1.0 / sqrt(var + eps));
+    o0[c] = static_cast<float>(mean);
+    o1[c] = inv;
+    o2[c] = static_cast<float>(var);
+    float sc = g * inv;
+    o3[c] = sc;
+    o4[c] = beta[c] - static_cast<float>(mean) * sc;
+  } else {
+    // a = sum(dz), b = sum(dz * (x - mean)); center = mean, invstd_in = invstd
+    const float inv = invstd_in[c];
+    const double dbeta = a;
+    const double dgamma = b * inv;
+    o0[c] = static_cast<float>(dgamma);
+    o1[c] = static_cast<float>(dbeta);
+    const double A = static_cast<double>(g) * inv;
+    const double B = training ? -A * inv * dgamma / n : 0.0;
+    const double Cc = training ? A * (static_cast<double>(center[c]) * inv * dgamma / n - dbeta / n) : 0.0;
+    o2[c] = static_cast<float>(A);
+    o3[c] = static_cast<float>(B);
+    o4[c] = static_cast<float>(Cc);
+  }
+}
+
+// y = x * scale + shift (+ addend) (relu)
+template <typename T, bool ADD, bool RELU>
+__global__ void __launch_bounds__(kBnThreads) bn_apply_kernel(
+    const T* __restrict__ x, const T* __restrict__ addend, const float* __restrict__ scale,
+    const float* __restrict__ shift, T* __restrict__ y, int64_t nvec, int C) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const int64_t off = v * 8;
+    const int c = static_cast<int>(off % C);
+    Vec8<T> vx, out;
+    vx.load(x + off);
+    const float4 s0 = *reinterpret_cast<const float4*>(scale + c);
+    const float4 s1 = *reinterpret_cast<const float4*>(scale + c + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(shift + c);
+    const float4 h1 = *reinterpret_cast<const float4*>(shift + c + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    Vec8<T> va;
+    if (ADD) va.load(addend + off);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float r = vx.get(i) * sc[i] + sh[i];
+      if (ADD) r += va.get(i);
+      if (RELU) r = r > 0.f ? r : 0.f;
+      out.set(i, r);
+    }
+    out.store(y + off);
+  }
+}
+
+// dx = A*dz + B*x + Cc, dz = relu ? dy * (y > 0) : dy; optionally d_addend = dz
+template <typename T, bool RELU, bool WRITE_DZ>
+__global__ void __launch_bounds__(kBnThreads) bn_bwd_apply_kernel(
+    const T* __restrict__ x, const T* __restrict__ dy, const T* __restrict__ y,
+    const float* __restrict__ A, const float* __restrict__ B, const float* __restrict__ Cc,
+    T* __restrict__ dx, T* __restrict__ dz_out, int64_t nvec, int C) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const int64_t off = v * 8;
+    const int c = static_cast<int>(off % C);
+    Vec8<T> vx, vdy, vy, out, dz;
+    vx.load(x + off);
+    vdy.load(dy + off);
+    if (RELU) vy.load(y + off);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float d = vdy.get(i);
+      if (RELU) d = vy.get(i) > 0.f ? d : 0.f;
+      if (WRITE_DZ) dz.set(i, d);
+      out.set(i, A[c + i] * d + B[c + i] * vx.get(i) + Cc[c + i]);
+    }
+    out.store(dx + off);
+    if (WRITE_DZ) dz.store(dz_out + off);
+  }
+}
+
+// ---------------------------------------------------------------- launchers
+
+static inline int64_t bn_rows_per_block(int64_t R, int C, const BnGeom& g, int* nblk) {
+  const int cblocks = C / g.cb;
+  int64_t target = 1024 / cblocks;
+  if (target < 8) target = 8;
+  int64_t rpb = (R + target - 1) / target;
+  rpb = (rpb + g.rpi - 1) / g.rpi * g.rpi;
+  if (rpb < g.rpi * 4) rpb = g.rpi * 4;
+  *nblk = static_cast<int>((R + rpb - 1) / rpb);
+  return rpb;
+}
+
+int bn_partials_rows(int64_t R, int C) {
+  BnGeom g = bn_geom(C);
+  int nblk;
+  bn_rows_per_block(R, C, g, &nblk);
+  return nblk;
+}
+
+template <typename T>
+static void bn_forward_impl(const void* x, const void* addend, void* y, const float* gamma,
+                            const float* beta, const float* center, float* part, float* mean, float* invstd,
+                            float* var, float* scale, float* shift, int64_t R, int C, float eps, int training,
+                            int relu, int fix_gamma, hipStream_t s) {
+  MXAMD_HOST_CHECK(C % 8 == 0, "bn_nhwc: channels must be a multiple of 8");
+  BnGeom g = bn_geom(C);
+  MXAMD_HOST_CHECK(C % g.cb == 0, "bn_nhwc: unsupported channel count");
+  if (training) {
+    int nblk;
+    int64_t rpb = bn_rows_per_block(R, C, g, &nblk);
+    dim3 grid(nblk, C / g.cb);
+    float* p1 = part;
+    float* p2 = part + static_cast<int64_t>(nblk) * C;
+    hipLaunchKernelGGL((bn_reduce_kernel<T, 0, false>), grid, dim3(kBnThreads), 0, s,
+                       static_cast<const T*>(x), nullptr, nullptr, center, p1, p2, R, C, g.tpr, g.rpi, rpb);
+    hipLaunchKernelGGL((bn_finalize_kernel<0>), dim3(C), dim3(64), 0, s, p1, p2, nblk, C, R, center, gamma,
+                       beta, nullptr, eps, mean, invstd, var, scale, shift, nullptr, fix_gamma, 1);
+  }
+  const int64_t nvec = R * C / 8;
+  int blocks = static_cast<int>((nvec + kBnThreads - 1) / kBnThreads);
+  if (blocks > 256 * 16) blocks = 256 * 16;
+  const T* xa = static_cast<const T*>(x);
+  const T* aa = static_cast<const T*>(addend);
+  T* ya = static_cast<T*>(y);
+  if (addend) {
+    if (relu)
+      hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), dim3(blocks), dim3(kBnThreads), 0, s, xa, aa, scale,
+                         shift, ya, nvec, C);
+    else
+      hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), dim3(blocks), dim3(kBnThreads), 0, s, xa, aa, scale,
+                         shift, ya, nvec, C);
+  } else {
+    if (relu)
+      hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), dim3(blocks), dim3(kBnThreads), 0, s, xa, aa, scale,
+                         shift, ya, nvec, C);
+    else
+      hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), dim3(blocks), dim3(kBnThreads), 0, s, xa, aa, scale,
+                         shift, ya, nvec, C);
+  }
+}
+
+template <typename T>
+static void bn_backward_impl(const void* x, const void* dy, const void* y, void* dx, void* dz,
+                             const float* gamma, const float* mean, const float* invstd, float* part,
+                             float* dgamma, float* dbeta, float* coef, int64_t R, int C, int relu,
+                             int fix_gamma, int training, hipStream_t s) {
+  BnGeom g = bn_geom(C);
+  int nblk;
+  int64_t rpb = bn_rows_per_block(R, C, g, &nblk);
+  dim3 grid(nblk, C / g.cb);
+  float* p1 = part;
+  float* p2 = part + static_cast<int64_t>(nblk) * C;
+  const T* xa = static_cast<const T*>(x);
+  const T* dya = static_cast<const T*>(dy);
+  const T* ya = static_cast<const T*>(y);
+  if (relu)
+    hipLaunchKernelGGL((bn_reduce_kernel<T, 1, true>), grid, dim3(kBnThreads), 0, s, xa, dya, ya, mean, p1, p2, R,
+                       C, g.tpr, g.rpi, rpb);
+  else
+    hipLaunchKernelGGL((bn_reduce_kernel<T, 1, false>), grid, dim3(kBnThreads), 0, s, xa, dya, ya, mean, p1, p2,
+                       R, C, g.tpr, g.rpi, rpb);
+  float* A = coef;
+  float* B = coef + C;
+  float* Cc = coef + 2 * C;
+  hipLaunchKernelGGL((bn_finalize_kernel<1>), dim3(C), dim3(64), 0, s, p1, p2, nblk, C, R, mean, gamma, nullptr,
+                     invstd, 0.f, dgamma, dbeta, A, B, Cc, nullptr, fix_gamma, training);
+  const int64_t nvec = R * C / 8;
+  int blocks = static_cast<int>((nvec + kBnThreads - 1) / kBnThreads);
+  if (blocks > 256 * 16) blocks = 256 * 16;
+  T* dxa = static_cast<T*>(dx);
+  T* dza = static_cast<T*>(dz);
+#define BWD(RL, WD)                                                                                      \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RL, WD>), dim3(blocks), dim3(kBnThreads), 0, s, xa, dya, ya, A, B, \
+                     Cc, dxa, dza, nvec, C)
+  if (relu) {
+    if (dz) BWD(true, true); else BWD(true, false);
+  } else {
+    if (dz) BWD(false, true); else BWD(false, false);
+  }
+#undef BWD
+}
+
+void bn_nhwc_forward(int dtype, const void* x, const void* addend, void* y, const float* gamma, const float* beta,
+                     const float* center, float* part, float* mean, float* invstd, float* var, float* scale,
+                     float* shift, int64_t R, int C, float eps, int training, int relu, int fix_gamma,
+                     hipStream_t s) {
+  switch (dtype) {
+    case kF16:
+      bn_forward_impl<__half>(x, addend, y, gamma, beta, center, part, mean, invstd, var, scale, shift, R, C, eps,
+                              training, relu, fix_gamma, s);
+      break;
+    case kBF16:
+      bn_forward_impl<__hip_bfloat16>(x, addend, y, gamma, beta, center, part, mean, invstd, var, scale, shift, R,
+                                      C, eps, training, relu, fix_gamma, s);
+      break;
+    default:
+      bn_forward_impl<float>(x, addend, y, gamma, beta, center, part, mean, invstd, var, scale, shift, R, C, eps,
+                             training, relu, fix_gamma, s);
+  }
+}
+
+void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, void* dx, void* dz,
+                      const float* gamma, const float* mean, const float* invstd, float* part, float* dgamma,
+                      float* dbeta, float* coef, int64_t R, int C, int relu, int fix_gamma, int training,
+                      hipStream_t s) {
+  switch (dtype) {
+    case kF16:
+      bn_backward_impl<__half>(x, dy, y, dx, dz, gamma, mean, invstd, part, dgamma, dbeta, coef, R, C, relu,
+                               fix_gamma, training, s);
+      break;
+    case kBF16:
+      bn_backward_impl<__hip_bfloat16>(x, dy, y, dx, dz, gamma, mean, invstd, part, dgamma, dbeta, coef, R, C,
+                                       relu, fix_gamma, training, s);
+      break;
+    default:
+      bn_backward_impl<float>(x, dy, y, dx, dz, gamma, mean, invstd, part, dgamma, dbeta, coef, R, C, relu,
+                              fix_gamma, training, s);
+  }
+}
+
+}  // namespace mxamd

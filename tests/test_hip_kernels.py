@@ -1,0 +1,184 @@
+"""Numerics of the gfx950 HIP kernels vs plain PyTorch fp32 references (GPU only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from mxnet_maintenance_amd.ops import kernels
+    assert kernels.available(), 'HIP kernel extension not loaded: %s' % kernels.load_error()
+    return kernels
+
+
+def _bn_ref(x, g, b, eps, addend=None, relu=False):
+    xf = x.float()
+    dims = tuple(range(x.dim() - 1))
+    mean = xf.mean(dims)
+    var = xf.var(dims, unbiased=False)
+    y = (xf - mean) / torch.sqrt(var + eps) * g + b
+    if addend is not None:
+        y = y + addend.float()
+    if relu:
+        y = torch.relu(y)
+    return y, mean, var
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('shape', [(4, 7, 7, 64), (2, 14, 14, 256), (3, 5, 5, 2048), (8, 3, 3, 24)])
+@pytest.mark.parametrize('mode', ['plain', 'relu', 'add_relu'])
+def test_bn_nhwc_forward_backward(dtype, shape, mode):
+    K = _lib()
+    torch.manual_seed(0)
+    dev = 'cuda'
+    C = shape[-1]
+    x = (torch.randn(shape, device=dev) * 2 + 0.5).to(dtype)
+    g = torch.rand(C, device=dev) + 0.5
+    b = torch.randn(C, device=dev)
+    add = torch.randn(shape, device=dev).to(dtype) if mode == 'add_relu' else None
+    relu = mode != 'plain'
+    mm = torch.zeros(C, device=dev)
+    mv = torch.ones(C, device=dev)
+    xr = x.detach().float().requires_grad_()
+    gr = g.clone().requires_grad_()
+    br = b.clone().requires_grad_()
+    ar = add.detach().float().requires_grad_() if add is not None else None
+    yr, mr, vr = _bn_ref(xr, gr, br, 1e-5, ar, relu)
+    dy = torch.randn(shape, device=dev)
+    yr.backward(dy)
+
+    xk = x.detach().requires_grad_()
+    gk = g.clone().requires_grad_()
+    bk = b.clone().requires_grad_()
+    ak = add.detach().requires_grad_() if add is not None else None
+    y, mean, var = K.BatchNormNHWC.apply(xk, gk, bk, ak, 1e-5, True, relu, mm, mv)
+    y.backward(dy.to(dtype))
+    tol = {torch.float16: 2e-2, torch.bfloat16: 8e-2, torch.float32: 1e-4}[dtype]
+    torch.testing.assert_close(mean, mr, atol=1e-3, rtol=1e-3)
+    torch.testing.assert_close(var, vr, atol=1e-3 * vr.abs().max().item(), rtol=1e-3)
+    torch.testing.assert_close(y.float(), yr, atol=tol * 4, rtol=tol)
+    torch.testing.assert_close(xk.grad.float(), xr.grad, atol=tol * 4, rtol=tol)
+    torch.testing.assert_close(gk.grad, gr.grad, atol=tol * shape[0] * 5, rtol=tol)
+    torch.testing.assert_close(bk.grad, br.grad, atol=tol * shape[0] * 5, rtol=tol)
+    if add is not None:
+        torch.testing.assert_close(ak.grad.float(), ar.grad, atol=tol * 4, rtol=tol)
+
+
+def test_bn_nhwc_eval_mode():
+    K = _lib()
+    dev = 'cuda'
+    x = torch.randn(4, 6, 6, 32, device=dev, dtype=torch.float16)
+    g = torch.rand(32, device=dev) + 0.5
+    b = torch.randn(32, device=dev)
+    mm = torch.randn(32, device=dev) * 0.1
+    mv = torch.rand(32, device=dev) + 0.5
+    y, _, _ = K.BatchNormNHWC.apply(x, g, b, None, 1e-5, False, False, mm, mv)
+    ref = (x.float() - mm) / torch.sqrt(mv + 1e-5) * g + b
+    torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+def test_bn_op_through_framework_matches_nchw():
+    """BatchNorm(axis=3) on NHWC data through mx.nd equals axis=1 BN on the transposed data."""
+    import mxnet_maintenance_amd as mx
+    ctx = mx.gpu(0)
+    x = mx.nd.random.normal(shape=(8, 5, 5, 16), ctx=ctx)
+    g = mx.nd.random.uniform(0.5, 1.5, shape=(16,), ctx=ctx)
+    b = mx.nd.random.normal(shape=(16,), ctx=ctx)
+    mm = mx.nd.zeros((16,), ctx=ctx)
+    mv = mx.nd.ones((16,), ctx=ctx)
+    with mx.autograd.train_mode():
+        y = mx.nd.BatchNorm(x, g, b, mm, mv, axis=3, fix_gamma=False, eps=1e-5)
+    xt = x.transpose((0, 3, 1, 2))
+    mm2 = mx.nd.zeros((16,), ctx=ctx)
+    mv2 = mx.nd.ones((16,), ctx=ctx)
+    with mx.autograd.train_mode():
+        y2 = mx.nd.BatchNorm(xt, g, b, mm2, mv2, axis=1, fix_gamma=False, eps=1e-5)
+    torch.testing.assert_close(y._data, y2._data.permute(0, 2, 3, 1), atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(mm._data, mm2._data, atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(mv._data, mv2._data, atol=1e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('int_label', [True, False])
+def test_softmax_ce(dtype, int_label):
+    K = _lib()
+    dev = 'cuda'
+    N, C = 37, 1000
+    logits = (torch.randn(N, C, device=dev) * 3).to(dtype)
+    lab = torch.randint(0, C, (N,), device=dev)
+    lr = logits.detach().float().requires_grad_()
+    ref = F.cross_entropy(lr, lab, reduction='none')
+    g = torch.rand(N, device=dev)
+    ref.backward(g)
+    lk = logits.detach().requires_grad_()
+    out = K.SoftmaxCE.apply(lk, lab if int_label else lab.float())
+    out.backward(g)
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(out, ref, atol=tol, rtol=tol)
+    torch.testing.assert_close(lk.grad.float(), lr.grad, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.float32])
+def test_global_avg_pool_nhwc(dtype):
+    K = _lib()
+    x = torch.randn(4, 7, 7, 2048, device='cuda').to(dtype).requires_grad_()
+    y = K.GlobalAvgPoolNHWC.apply(x)
+    xr = x.detach().float().requires_grad_()
+    yr = xr.mean((1, 2), keepdim=True)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize('mp', [True, False])
+def test_flat_sgd(mp):
+    K = _lib()
+    n = 1 << 16
+    dt = torch.float16 if mp else torch.float32
+    w32 = torch.randn(n, device='cuda')
+    w = w32.to(dt)
+    g = torch.randn(n, device='cuda').to(dt)
+    mom = torch.randn(n, device='cuda')
+    ref_w = (w32 if mp else w.float()).clone()
+    ref_m = mom.clone()
+    lr, wd, m, rs = 0.1, 1e-4, 0.9, 1.0 / 128
+    gg = g.float() * rs + wd * ref_w
+    ref_m = m * ref_m - lr * gg
+    ref_w = ref_w + ref_m
+    K.flat_sgd(w, g, mom, w32 if mp else None, lr, wd, m, rs, -1.0)
+    torch.testing.assert_close(mom, ref_m, atol=1e-5, rtol=1e-5)
+    if mp:
+        torch.testing.assert_close(w32, ref_w, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(w.float(), ref_w, atol=2e-3, rtol=2e-3)
+
+
+def test_resnet_block_train_step_gpu():
+    """Fused NHWC ResNet bottleneck forward/backward on the GPU matches the unfused graph."""
+    import mxnet_maintenance_amd as mx
+    from mxnet_maintenance_amd import gluon, autograd
+    from mxnet_maintenance_amd.gluon.model_zoo.vision.resnet import BottleneckV1b
+    ctx = mx.gpu(0)
+    mx.random.seed(3)
+    x = mx.nd.random.normal(shape=(4, 8, 8, 64), ctx=ctx)
+    outs, grads = [], []
+    for fuse in (True, False):
+        blk = BottleneckV1b(64, 1, False, in_channels=64, layout='NHWC', fuse=fuse)
+        blk.initialize(mx.init.One(), ctx=ctx)
+        for i, p in enumerate(blk.collect_params().values()):
+            if p.name.endswith('weight'):
+                torch.manual_seed(i)
+                p.set_data(mx.nd.array(torch.randn(p.shape).numpy() * 0.05, ctx=ctx))
+        xx = x.copy()
+        xx.attach_grad()
+        with autograd.record():
+            y = blk(xx)
+        y.backward()
+        outs.append(y.asnumpy())
+        grads.append(xx.grad.asnumpy())
+    import numpy as np
+    np.testing.assert_allclose(outs[0], outs[1], atol=1e-4, rtol=1e-4)
+    np.testing.assert_allclose(grads[0], grads[1], atol=1e-4, rtol=1e-4)

@@ -93,8 +93,8 @@ def build_hip(jobs):
         o = os.path.join(objdir, os.path.basename(s) + '.o')
         objs.append(o)
         if _newer([s] + hdrs, o):
-            tasks.append([HIPCC, '-O2', '-fPIC', '-std=c++17', '-fvisibility=hidden',
-                          '-D__HIP_PLATFORM_AMD__'] + _includes() + ['-I/opt/rocm/include', '-c', s, '-o', o])
+            tasks.append([HIPCC, '-O2', '-fPIC', '-std=c++17', '-fvisibility=hidden'] + _includes() +
+                         ['-I/opt/rocm/include', '-c', s, '-o', o])
     with ThreadPoolExecutor(jobs) as ex:
         list(ex.map(_run, tasks))
     out = os.path.join(LIB, '_hip_kernels' + _ext_suffix())
