@@ -63,7 +63,3 @@ from . import numpy_extension
 from . import numpy_extension as npx
 from . import rtc
 from .util import is_np_array, is_np_shape, set_np, reset_np, use_np, np_shape, np_array
-
-# Autograd recording decides when torch builds graphs; keep torch's global grad
-# mode off outside record() scopes so inference never builds a tape.
-_torch.set_grad_enabled(False)

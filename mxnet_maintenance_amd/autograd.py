@@ -106,6 +106,7 @@ def _collect_leaves(retain):
 def _prepare_leaves(leaves):
     """Zero 'write' buffers (grouped in one multi-tensor launch) and rebind stale .grad."""
     zero = []
+    arenas = {}
     for v in leaves:
         t = v._data
         if not t.requires_grad or v._grad is None:
@@ -114,9 +115,15 @@ def _prepare_leaves(leaves):
         if t.grad is not gbuf:
             t.grad = gbuf
         if v._grad_req == 'write':
-            zero.append(gbuf)
-    if zero:
-        with torch.no_grad():
+            a = v._arena
+            if a is not None and a.all_write:
+                arenas[id(a)] = a      # whole flat gradient arena: one memset
+            else:
+                zero.append(gbuf)
+    with torch.no_grad():
+        for a in arenas.values():
+            a.g.zero_()
+        if zero:
             torch._foreach_zero_(zero)
 
 

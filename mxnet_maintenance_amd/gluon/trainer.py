@@ -70,9 +70,11 @@ class _Arena:
             gv = self.g[off:off + n].view(t.shape)
             arr._data = wv.detach()
             arr._set_grad_buffer(gv, p.grad_req)
+            arr._arena = self
             self.views.append((off, n, t.shape))
         self.mom = None
         self.w32 = None
+        self.all_write = all(p.grad_req == 'write' for p in params)
 
 
 class Trainer:

@@ -33,7 +33,7 @@ def _wrap(t):
 
 class NDArray:
     """An n-dimensional array on a :class:`Context`."""
-    __slots__ = ('_data', '_grad', '_grad_req', '_stype', '__weakref__', '_fresh_grad')
+    __slots__ = ('_data', '_grad', '_grad_req', '_stype', '__weakref__', '_fresh_grad', '_arena')
     __array_priority__ = 1000.0
 
     def __init__(self, data, ctx=None, dtype=None, stype='default'):
@@ -50,6 +50,7 @@ class NDArray:
         self._grad_req = None
         self._stype = stype
         self._fresh_grad = False
+        self._arena = None
 
     # ------------------------------------------------------------------ props
     @property
@@ -163,6 +164,7 @@ class NDArray:
         self._grad_req = None
         self._stype = 'default'
         self._fresh_grad = False
+        self._arena = None
 
     def __reduce__(self):
         return (_rebuild, (self.asnumpy(),))

@@ -88,13 +88,8 @@ def batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_ga
     channel_last = (axis == nd - 1) and nd > 2
     g = torch.ones_like(gamma) if fix_gamma else gamma
     if channel_last and _use_hip(data) and _K.bn_ok(data):
-        out, mean, var = _K.BatchNormNHWC.apply(data, g, beta, addend, eps, training,
-                                                act_type == 'relu', moving_mean, moving_var)
-        if training:
-            with torch.no_grad():
-                moving_mean.mul_(momentum).add_(mean.to(moving_mean.dtype), alpha=1 - momentum)
-                moving_var.mul_(momentum).add_(var.to(moving_var.dtype), alpha=1 - momentum)
-        return out, mean, var
+        return _K.BatchNormNHWC.apply(data, g, beta, addend, eps, training, act_type == 'relu',
+                                      moving_mean, moving_var, momentum)
     if channel_last:
         x = _nd_to_ncx(data)
     elif axis != 1:

@@ -47,7 +47,7 @@ class BatchNormNHWC(torch.autograd.Function):
     """BatchNorm over the last (channel) axis with optional fused residual add + ReLU."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, addend, eps, training, relu, moving_mean, moving_var):
+    def forward(ctx, x, gamma, beta, addend, eps, training, relu, moving_mean, moving_var, momentum=None):
         lib = _K.lib()
         C = x.shape[-1]
         R = x.numel() // C
@@ -71,10 +71,19 @@ class BatchNormNHWC(torch.autograd.Function):
             var = _f32(moving_var)
             scale = g * invstd
             shift = b - mean * scale
+        # moving statistics are updated inside the finalize kernel when the
+        # buffers are fp32 + contiguous (always true for Gluon BN params)
+        upd = (training and momentum is not None and mm is moving_mean and moving_var.dtype == torch.float32
+               and moving_var.is_contiguous())
         lib.bn_nhwc_forward(_DT[x.dtype], x.data_ptr(), _p(addend), y.data_ptr(), g.data_ptr(), b.data_ptr(),
                             mm.data_ptr(), _p(part), mean.data_ptr(), invstd.data_ptr(), var.data_ptr(),
                             scale.data_ptr(), shift.data_ptr(), R, C, float(eps), int(bool(training)),
-                            int(bool(relu)), 0, _stream())
+                            int(bool(relu)), 0, float(momentum or 0.0), moving_mean.data_ptr() if upd else 0,
+                            moving_var.data_ptr() if upd else 0, _stream())
+        if training and momentum is not None and not upd:
+            with torch.no_grad():
+                moving_mean.mul_(momentum).add_(mean.to(moving_mean.dtype), alpha=1 - momentum)
+                moving_var.mul_(momentum).add_(var.to(moving_var.dtype), alpha=1 - momentum)
         ctx.save_for_backward(x, y if relu else None, g, mean, invstd)
         ctx.cfg = (bool(relu), bool(training), addend is not None, gamma.dtype, beta.dtype)
         ctx.mark_non_differentiable(mean, var)
@@ -99,7 +108,7 @@ class BatchNormNHWC(torch.autograd.Function):
                              out[1].data_ptr(), out[2].data_ptr(), R, C, int(relu), 0, int(training), _stream())
         dgamma = out[0].to(gdt) if ctx.needs_input_grad[1] else None
         dbeta = out[1].to(bdt) if ctx.needs_input_grad[2] else None
-        return dx, dgamma, dbeta, dz, None, None, None, None, None
+        return dx, dgamma, dbeta, dz, None, None, None, None, None, None
 
 
 class SoftmaxCE(torch.autograd.Function):

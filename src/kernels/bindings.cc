@@ -17,7 +17,7 @@ namespace mxamd {
 void bn_nhwc_forward(int dtype, const void* x, const void* addend, void* y, const float* gamma, const float* beta,
                      const float* center, float* part, float* mean, float* invstd, float* var, float* scale,
                      float* shift, int64_t R, int C, float eps, int training, int relu, int fix_gamma,
-                     hipStream_t s);
+                     float momentum, float* mm_upd, float* mv_upd, hipStream_t s);
 void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, void* dx, void* dz,
                       const float* gamma, const float* mean, const float* invstd, float* part, float* dgamma,
                       float* dbeta, float* coef, int64_t R, int C, int relu, int fix_gamma, int training,
@@ -54,10 +54,10 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("bn_nhwc_forward", [](int dt, uintptr_t x, uintptr_t add, uintptr_t y, uintptr_t g, uintptr_t b,
                               uintptr_t center, uintptr_t part, uintptr_t mean, uintptr_t inv, uintptr_t var,
                               uintptr_t scale, uintptr_t shift, int64_t R, int C, float eps, int training, int relu,
-                              int fix_gamma, uintptr_t s) {
+                              int fix_gamma, float momentum, uintptr_t mm_upd, uintptr_t mv_upd, uintptr_t s) {
     bn_nhwc_forward(dt, P<void>(x), P<void>(add), P<void>(y), P<float>(g), P<float>(b), P<float>(center),
                     P<float>(part), P<float>(mean), P<float>(inv), P<float>(var), P<float>(scale), P<float>(shift), R,
-                    C, eps, training, relu, fix_gamma, S(s));
+                    C, eps, training, relu, fix_gamma, momentum, P<float>(mm_upd), P<float>(mv_upd), S(s));
     check_launch("bn_nhwc_forward");
   });
   m.def("bn_nhwc_backward", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t y, uintptr_t dx, uintptr_t dz,

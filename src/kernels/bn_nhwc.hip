@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(64) bn_finalize_kernel(
     const float* __restrict__ center, const float* __restrict__ gamma, const float* __restrict__ beta,
     const float* __restrict__ invstd_in, float eps, float* __restrict__ o0, float* __restrict__ o1,
     float* __restrict__ o2, float* __restrict__ o3, float* __restrict__ o4, float* __restrict__ o5,
-    int fix_gamma, int training) {
+    int fix_gamma, int training, float momentum, float* __restrict__ mm_upd, float* __restrict__ mv_upd) {
   const int c = blockIdx.x;
   const int lane = threadIdx.x;
   double a = 0.0, b = 0.0;
@@ -151,6 +151,9 @@ __global__ void __launch_bounds__(64) bn_finalize_kernel(
     float sc = g * inv;
     o3[c] = sc;
     o4[c] = beta[c] - static_cast<float>(mean) * sc;
+    // moving statistics (MXNet: moving = moving * momentum + batch * (1 - momentum), biased var)
+    if (mm_upd) mm_upd[c] = mm_upd[c] * momentum + static_cast<float>(mean) * (1.f - momentum);
+    if (mv_upd) mv_upd[c] = mv_upd[c] * momentum + static_cast<float>(var) * (1.f - momentum);
   } else {
     // a = sum(dz), b = sum(dz * (x - mean)); center = mean, invstd_in = invstd
     const float inv = invstd_in[c];
@@ -173,9 +176,13 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_kernel(
     const T* __restrict__ x, const T* __restrict__ addend, const float* __restrict__ scale,
     const float* __restrict__ shift, T* __restrict__ y, int64_t nvec, int C) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+  int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  // channel of this thread's first vector; advancing by `stride` vectors moves
+  // the channel by a fixed step (< C), so no per-iteration 64-bit modulo.
+  int c = static_cast<int>((v * 8) % C);
+  const int cstep = static_cast<int>((stride * 8) % C);
+  for (; v < nvec; v += stride, c = (c + cstep >= C) ? c + cstep - C : c + cstep) {
     const int64_t off = v * 8;
-    const int c = static_cast<int>(off % C);
     Vec8<T> vx, out;
     vx.load(x + off);
     const float4 s0 = *reinterpret_cast<const float4*>(scale + c);
@@ -204,19 +211,30 @@ __global__ void __launch_bounds__(kBnThreads) bn_bwd_apply_kernel(
     const float* __restrict__ A, const float* __restrict__ B, const float* __restrict__ Cc,
     T* __restrict__ dx, T* __restrict__ dz_out, int64_t nvec, int C) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+  int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  int c = static_cast<int>((v * 8) % C);
+  const int cstep = static_cast<int>((stride * 8) % C);
+  for (; v < nvec; v += stride, c = (c + cstep >= C) ? c + cstep - C : c + cstep) {
     const int64_t off = v * 8;
-    const int c = static_cast<int>(off % C);
     Vec8<T> vx, vdy, vy, out, dz;
     vx.load(x + off);
     vdy.load(dy + off);
     if (RELU) vy.load(y + off);
+    const float4 a0 = *reinterpret_cast<const float4*>(A + c);
+    const float4 a1 = *reinterpret_cast<const float4*>(A + c + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(B + c);
+    const float4 b1 = *reinterpret_cast<const float4*>(B + c + 4);
+    const float4 c0 = *reinterpret_cast<const float4*>(Cc + c);
+    const float4 c1 = *reinterpret_cast<const float4*>(Cc + c + 4);
+    const float ka[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float kb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    const float kc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float d = vdy.get(i);
       if (RELU) d = vy.get(i) > 0.f ? d : 0.f;
       if (WRITE_DZ) dz.set(i, d);
-      out.set(i, A[c + i] * d + B[c + i] * vx.get(i) + Cc[c + i]);
+      out.set(i, ka[i] * d + kb[i] * vx.get(i) + kc[i]);
     }
     out.store(dx + off);
     if (WRITE_DZ) dz.store(dz_out + off);
@@ -247,7 +265,7 @@ template <typename T>
 static void bn_forward_impl(const void* x, const void* addend, void* y, const float* gamma,
                             const float* beta, const float* center, float* part, float* mean, float* invstd,
                             float* var, float* scale, float* shift, int64_t R, int C, float eps, int training,
-                            int relu, int fix_gamma, hipStream_t s) {
+                            int relu, int fix_gamma, float momentum, float* mm_upd, float* mv_upd, hipStream_t s) {
   MXAMD_HOST_CHECK(C % 8 == 0, "bn_nhwc: channels must be a multiple of 8");
   BnGeom g = bn_geom(C);
   MXAMD_HOST_CHECK(C % g.cb == 0, "bn_nhwc: unsupported channel count");
@@ -260,7 +278,8 @@ static void bn_forward_impl(const void* x, const void* addend, void* y, const fl
     hipLaunchKernelGGL((bn_reduce_kernel<T, 0, false>), grid, dim3(kBnThreads), 0, s,
                        static_cast<const T*>(x), nullptr, nullptr, center, p1, p2, R, C, g.tpr, g.rpi, rpb);
     hipLaunchKernelGGL((bn_finalize_kernel<0>), dim3(C), dim3(64), 0, s, p1, p2, nblk, C, R, center, gamma,
-                       beta, nullptr, eps, mean, invstd, var, scale, shift, nullptr, fix_gamma, 1);
+                       beta, nullptr, eps, mean, invstd, var, scale, shift, nullptr, fix_gamma, 1, momentum, mm_upd,
+                       mv_upd);
   }
   const int64_t nvec = R * C / 8;
   int blocks = static_cast<int>((nvec + kBnThreads - 1) / kBnThreads);
@@ -309,7 +328,8 @@ static void bn_backward_impl(const void* x, const void* dy, const void* y, void*
   float* B = coef + C;
   float* Cc = coef + 2 * C;
   hipLaunchKernelGGL((bn_finalize_kernel<1>), dim3(C), dim3(64), 0, s, p1, p2, nblk, C, R, mean, gamma, nullptr,
-                     invstd, 0.f, dgamma, dbeta, A, B, Cc, nullptr, fix_gamma, training);
+                     invstd, 0.f, dgamma, dbeta, A, B, Cc, nullptr, fix_gamma, training, 0.f, nullptr,
+                     nullptr);
   const int64_t nvec = R * C / 8;
   int blocks = static_cast<int>((nvec + kBnThreads - 1) / kBnThreads);
   if (blocks > 256 * 16) blocks = 256 * 16;
@@ -329,19 +349,19 @@ static void bn_backward_impl(const void* x, const void* dy, const void* y, void*
 void bn_nhwc_forward(int dtype, const void* x, const void* addend, void* y, const float* gamma, const float* beta,
                      const float* center, float* part, float* mean, float* invstd, float* var, float* scale,
                      float* shift, int64_t R, int C, float eps, int training, int relu, int fix_gamma,
-                     hipStream_t s) {
+                     float momentum, float* mm_upd, float* mv_upd, hipStream_t s) {
   switch (dtype) {
     case kF16:
       bn_forward_impl<__half>(x, addend, y, gamma, beta, center, part, mean, invstd, var, scale, shift, R, C, eps,
-                              training, relu, fix_gamma, s);
+                              training, relu, fix_gamma, momentum, mm_upd, mv_upd, s);
       break;
     case kBF16:
       bn_forward_impl<__hip_bfloat16>(x, addend, y, gamma, beta, center, part, mean, invstd, var, scale, shift, R,
-                                      C, eps, training, relu, fix_gamma, s);
+                                      C, eps, training, relu, fix_gamma, momentum, mm_upd, mv_upd, s);
       break;
     default:
       bn_forward_impl<float>(x, addend, y, gamma, beta, center, part, mean, invstd, var, scale, shift, R, C, eps,
-                             training, relu, fix_gamma, s);
+                             training, relu, fix_gamma, momentum, mm_upd, mv_upd, s);
   }
 }
 
