@@ -187,7 +187,10 @@ def grad(heads, variables, head_grads=None, retain_graph=None, create_graph=Fals
     if head_grads is not None and isinstance(head_grads, NDArray):
         head_grads = [head_grads]
     hts = [h._data for h in heads]
-    hgs = None if head_grads is None else [g._data for g in head_grads]
+    if head_grads is None:
+        hgs = [torch.ones_like(h) for h in hts]
+    else:
+        hgs = [torch.ones_like(h) if g is None else g._data for h, g in zip(hts, head_grads)]
     if retain_graph is None:
         retain_graph = create_graph
     prev_train = set_training(train_mode)

@@ -68,6 +68,9 @@ class _Arena:
             with torch.no_grad():
                 wv.copy_(t)
             gv = self.g[off:off + n].view(t.shape)
+            if arr._grad is not None:
+                with torch.no_grad():
+                    gv.copy_(arr._grad._data)
             arr._data = wv.detach()
             arr._set_grad_buffer(gv, p.grad_req)
             arr._arena = self

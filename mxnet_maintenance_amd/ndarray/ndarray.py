@@ -542,11 +542,23 @@ def _index_fn(t, key):
     if isinstance(key, tuple):
         key = tuple(k.to(t.device) if torch.is_tensor(k) else k for k in key)
         neg = any(isinstance(k, slice) and k.step is not None and k.step < 0 for k in key)
-        if neg:
-            from ..ops.tensor import _neg_step_slice
-            full = list(key) + [slice(None)] * (t.dim() - len(key))
-            if all(isinstance(k, slice) for k in full):
-                return _neg_step_slice(t, full)
+        if neg and not any(k is Ellipsis for k in key):
+            # torch has no negative-step slicing: apply those axes with index_select
+            # first (keeps the rank), then the rest of the key.
+            ax = 0
+            newkey = []
+            for k in key:
+                if k is None:
+                    newkey.append(k)
+                    continue
+                if isinstance(k, slice) and k.step is not None and k.step < 0:
+                    b, e, s = k.indices(t.shape[ax])
+                    t = t.index_select(ax, torch.arange(b, e, s, device=t.device))
+                    newkey.append(slice(None))
+                else:
+                    newkey.append(k)
+                ax += 1
+            key = tuple(newkey)
     elif torch.is_tensor(key):
         key = key.to(t.device)
     elif isinstance(key, slice) and key.step is not None and key.step < 0:
@@ -615,7 +627,8 @@ def array(source_array, ctx=None, dtype=None):
         dt = torch_dtype(dtype) if dtype is not None else source_array.dtype
         return NDArray(source_array.detach().to(device=ctx.torch_device, dtype=dt, copy=True))
     if isinstance(source_array, np.ndarray):
-        dt = dtype if dtype is not None else source_array.dtype
+        # MXNet: only NDArray sources keep their dtype; everything else defaults to float32
+        dt = dtype if dtype is not None else np.float32
     else:
         dt = dtype if dtype is not None else np.float32
         source_array = np.asarray(source_array, dtype=None if dtype is None else None)

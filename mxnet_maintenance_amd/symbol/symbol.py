@@ -568,8 +568,9 @@ def _op_func(op_name):
         attrs = {k: v for k, v in kwargs.items() if not isinstance(v, Symbol)}
         extra = {}
         for k in list(attrs):
-            if k not in op.params and k not in ('num_args',) and not callable(op.arg_names):
-                if k in ('lr_mult', 'wd_mult', 'ctx_group', 'force_mirroring', 'init', 'dtype_hint'):
+            if k not in op.params and k != op.key_var_num_args:
+                if k in ('lr_mult', 'wd_mult', 'ctx_group', 'force_mirroring', 'init', 'dtype_hint',
+                         'mirror_stage', 'storage_type'):
                     extra[k] = str(attrs.pop(k))
         if op.key_var_num_args and op.key_var_num_args not in attrs:
             attrs[op.key_var_num_args] = len(pos) + len(named)
@@ -752,6 +753,22 @@ def infer_graph(sym, known_shapes, known_dtypes, what='shape'):
                         in_shapes[idx] = tuple(s)
                         progress = True
             if any(s is None for s in in_shapes):
+                if what == 'type':
+                    # dtype-only propagation: parameters follow the data dtype, outputs
+                    # follow the first input unless the op declares an output dtype.
+                    in_dt = [dtype.get((id(a), j)) for a, j in n.inputs]
+                    base_dt = next((d for d in in_dt if d is not None), None)
+                    if base_dt is None:
+                        continue
+                    for (a, j) in n.inputs:
+                        if (id(a), j) not in dtype and a.op is None:
+                            dtype[(id(a), j)] = base_dt
+                    odt = parsed.get('dtype') if n.op in ('Cast', 'cast', 'amp_cast') else None
+                    odt = torch_dtype(odt) if odt else base_dt
+                    for i in range(n.num_outputs()):
+                        if (id(n), i) not in dtype:
+                            dtype[(id(n), i)] = odt
+                            progress = True
                 continue
             in_dt = [dtype.get((id(a), j)) for a, j in n.inputs]
             base_dt = next((d for d in in_dt if d is not None), default_dt)

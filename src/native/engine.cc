@@ -49,9 +49,10 @@ bool Engine::AppendWrite(const VarHandle& v, const std::shared_ptr<Opr>& op) {
 
 void Engine::Push(Fn fn, const std::vector<VarHandle>& const_vars,
                   const std::vector<VarHandle>& mutable_vars, int priority,
-                  const std::string& name) {
+                  const std::string& name, bool always_run) {
   auto op = std::make_shared<Opr>();
   op->fn = std::move(fn);
+  op->always_run = always_run;
   op->mutable_vars = mutable_vars;
   // a variable that is both read and written is only written
   for (const auto& v : const_vars) {
@@ -98,6 +99,19 @@ void Engine::WorkerLoop() {
 
 void Engine::Execute(std::shared_ptr<Opr> op) {
   std::exception_ptr exc;
+  if (op->always_run) {
+    if (op->fn) op->fn();
+    ++executed_;
+    if (naive_) {
+      if (--pending_ == 0) {
+        std::lock_guard<std::mutex> lk(allmu_);
+        allcv_.notify_all();
+      }
+      return;
+    }
+    Complete(op, nullptr);
+    return;
+  }
   // exception propagation: an input written by a failed op poisons this op
   for (const auto& v : op->const_vars) {
     std::lock_guard<std::mutex> lk(v->mu);
@@ -197,7 +211,7 @@ void Engine::WaitForVar(const VarHandle& v) {
          *flag = true;
          done->second.notify_all();
        },
-       {v}, {}, 1 << 20, "WaitForVar");
+       {v}, {}, 1 << 20, "WaitForVar", /*always_run=*/true);
   {
     std::unique_lock<std::mutex> lk(done->first);
     done->second.wait(lk, [&] { return *flag; });

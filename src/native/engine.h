@@ -51,6 +51,7 @@ struct Opr {
   int priority = 0;
   std::string name;
   uint64_t seq = 0;
+  bool always_run = false;  // synchronisation ops run even if an input carries an exception
 };
 
 class Engine {
@@ -60,7 +61,7 @@ class Engine {
   VarHandle NewVar(const std::string& name = "");
   void Push(Fn fn, const std::vector<VarHandle>& const_vars,
             const std::vector<VarHandle>& mutable_vars, int priority,
-            const std::string& name);
+            const std::string& name, bool always_run = false);
   void WaitForVar(const VarHandle& v);
   void WaitForAll();
   int64_t Pending() const { return pending_.load(); }

@@ -1,0 +1,135 @@
+"""Symbol composition, attributes, inference, JSON, executor (parity: test_symbol.py,
+test_attr.py, test_infer_shape.py, test_executor.py)."""
+import json
+import os
+import pickle
+
+import numpy as np
+
+import mxnet_maintenance_amd as mx
+from mxnet_maintenance_amd import nd, sym
+
+DATA = os.path.join(os.path.dirname(__file__), 'data')
+
+
+def _mlp():
+    data = sym.Variable('data')
+    fc1 = sym.FullyConnected(data=data, name='fc1', num_hidden=10)
+    act = sym.Activation(fc1, act_type='relu', name='relu1')
+    fc2 = sym.FullyConnected(act, name='fc2', num_hidden=3)
+    return sym.SoftmaxOutput(fc2, name='softmax')
+
+
+def test_compose_and_lists():
+    net = _mlp()
+    assert net.list_arguments() == ['data', 'fc1_weight', 'fc1_bias', 'fc2_weight', 'fc2_bias', 'softmax_label']
+    assert net.list_outputs() == ['softmax_output']
+    internals = net.get_internals()
+    assert 'fc1_output' in internals.list_outputs()
+    assert internals['fc1_output'].list_arguments() == ['data', 'fc1_weight', 'fc1_bias']
+    bn = sym.BatchNorm(sym.Variable('x'), name='bn')
+    assert bn.list_auxiliary_states() == ['bn_moving_mean', 'bn_moving_var']
+    g = sym.Group([net, internals['fc1_output']])
+    assert len(g.list_outputs()) == 2
+
+
+def test_auto_naming():
+    with mx.name.NameManager():
+        a = sym.FullyConnected(sym.Variable('x'), num_hidden=2)
+        b = sym.FullyConnected(a, num_hidden=2)
+    assert a.name == 'fullyconnected0' and b.name == 'fullyconnected1'
+
+
+def test_attributes():
+    with mx.AttrScope(group='4', data='great'):
+        data = sym.Variable('data', attr={'dtype': 'data', 'group': '1', 'force_mirroring': 'True'}, lr_mult=1)
+        gdata = sym.Variable('data2')
+    assert gdata.attr('group') == '4'
+    assert data.attr('group') == '1'
+    assert data.attr('lr_mult') == '1'
+    assert data.attr('__lr_mult__') == '1'
+    assert data.attr('force_mirroring') == 'True'
+    data2 = pickle.loads(pickle.dumps(data))
+    assert data.attr('dtype') == data2.attr('dtype')
+    d = sym.Variable('data', attr={'mood': 'angry'})
+    op = sym.Convolution(data=d, name='conv', kernel=(1, 1), num_filter=1, attr={'__mood__': 'so so'}, lr_mult=1)
+    ad = op.attr_dict()
+    assert ad['data']['mood'] == 'angry'
+    assert ad['conv_weight']['__mood__'] == 'so so'
+    assert ad['conv']['kernel'] == '(1, 1)' and ad['conv']['num_filter'] == '1'
+    assert ad['conv']['lr_mult'] == '1' and ad['conv']['__lr_mult__'] == '1'
+
+
+def test_infer_shape_and_type():
+    net = _mlp()
+    arg, out, aux = net.infer_shape(data=(5, 7))
+    assert dict(zip(net.list_arguments(), arg)) == {
+        'data': (5, 7), 'fc1_weight': (10, 7), 'fc1_bias': (10,), 'fc2_weight': (3, 10), 'fc2_bias': (3,),
+        'softmax_label': (5,)}
+    assert out == [(5, 3)]
+    conv = sym.Convolution(sym.Variable('data'), kernel=(3, 3), num_filter=8, pad=(1, 1), name='c')
+    pool = sym.Pooling(conv, kernel=(2, 2), stride=(2, 2), pool_type='max')
+    bn = sym.BatchNorm(pool, name='bn')
+    arg, out, aux = bn.infer_shape(data=(2, 3, 16, 16))
+    assert out == [(2, 8, 8, 8)] and aux == [(8,), (8,)]
+    assert dict(zip(bn.list_arguments(), arg))['c_weight'] == (8, 3, 3, 3)
+    nhwc = sym.Convolution(sym.Variable('data'), kernel=(3, 3), num_filter=8, layout='NHWC', name='n')
+    arg, out, _ = nhwc.infer_shape(data=(2, 10, 10, 4))
+    assert out == [(2, 8, 8, 8)] and arg[1] == (8, 3, 3, 4)
+    a, o, _ = net.infer_type(data='float16')
+    assert o == [np.float16]
+    partial = sym.FullyConnected(sym.Variable('x'), num_hidden=4) + sym.Variable('y')
+    a, o, _ = partial.infer_shape_partial()
+    assert a[0] == ()
+
+
+def test_json_roundtrip_and_legacy():
+    net = _mlp()
+    js = net.tojson()
+    d = json.loads(js)
+    assert {'nodes', 'arg_nodes', 'heads', 'node_row_ptr'} <= set(d)
+    net2 = sym.load_json(js)
+    assert net2.tojson() == js
+    legacy = sym.load(os.path.join(DATA, 'save_000800.json'))
+    assert 'data' in legacy.list_arguments()
+    assert legacy.attr_dict()['data']['ctx_group'] == 'stage1'
+
+
+def test_executor_forward_backward():
+    data = sym.Variable('data')
+    w = sym.Variable('w')
+    out = sym.FullyConnected(data, w, num_hidden=2, no_bias=True, name='fc')
+    x = np.random.rand(3, 4).astype(np.float32)
+    wv = np.random.rand(2, 4).astype(np.float32)
+    ex = out.bind(mx.cpu(), args={'data': nd.array(x), 'w': nd.array(wv)},
+                  args_grad={'w': nd.zeros((2, 4))}, grad_req={'data': 'null', 'w': 'write'})
+    y = ex.forward(is_train=True)[0]
+    np.testing.assert_allclose(y.asnumpy(), x @ wv.T, rtol=1e-5)
+    og = np.random.rand(3, 2).astype(np.float32)
+    ex.backward(nd.array(og))
+    np.testing.assert_allclose(ex.grad_dict['w'].asnumpy(), og.T @ x, rtol=1e-5)
+
+
+def test_simple_bind_softmax_output_grad():
+    net = _mlp()
+    ex = net.simple_bind(mx.cpu(), data=(4, 5))
+    for k, v in ex.arg_dict.items():
+        if k not in ('data', 'softmax_label'):
+            v[:] = nd.random.uniform(-0.5, 0.5, shape=v.shape)
+    label = np.array([0, 1, 2, 1])
+    ex.arg_dict['softmax_label'][:] = nd.array(label)
+    out = ex.forward(is_train=True, data=nd.random.uniform(shape=(4, 5)))[0].asnumpy()
+    ex.backward()
+    # gradient w.r.t. fc2 bias of SoftmaxOutput = sum over batch of (p - onehot)
+    oh = np.eye(3)[label]
+    np.testing.assert_allclose(ex.grad_dict['fc2_bias'].asnumpy(), (out - oh).sum(0), rtol=1e-4, atol=1e-5)
+
+
+def test_symbol_arithmetic_eval():
+    a = sym.Variable('a')
+    b = sym.Variable('b')
+    c = (a + b) * 2 - a / 2 + 1
+    r = c.eval(ctx=mx.cpu(), a=nd.array([1., 2.]), b=nd.array([3., 4.]))[0]
+    np.testing.assert_allclose(r.asnumpy(), (np.array([1, 2]) + [3, 4]) * 2 - np.array([1, 2]) / 2 + 1)
+    s = sym.reshape(a, shape=(2, -1))
+    assert s.infer_shape(a=(4, 3))[1] == [(2, 6)]
