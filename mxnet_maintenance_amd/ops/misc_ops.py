@@ -333,3 +333,40 @@ def image_random_saturation(data, min_factor=1.0, max_factor=1.0):
     a = float(torch.empty(()).uniform_(min_factor, max_factor))
     g = _gray(data)
     return (data.float() * a + g * (1 - a)).to(data.dtype)
+
+
+def _hue_matrix(alpha, device):
+    u, w = math.cos(alpha * math.pi), math.sin(alpha * math.pi)
+    tyiq = torch.tensor([[0.299, 0.587, 0.114], [0.596, -0.274, -0.321], [0.211, -0.523, 0.311]])
+    ityiq = torch.tensor([[1.0, 0.956, 0.621], [1.0, -0.272, -0.647], [1.0, -1.107, 1.705]])
+    bt = torch.tensor([[1.0, 0.0, 0.0], [0.0, u, -w], [0.0, w, u]])
+    return (ityiq @ bt @ tyiq).t().to(device)
+
+
+@register('_image_random_hue', params={'min_factor': ('float', 0.0), 'max_factor': ('float', 0.0)})
+def image_random_hue(data, min_factor=0.0, max_factor=0.0):
+    a = float(torch.empty(()).uniform_(min_factor, max_factor))
+    return (data.float() @ _hue_matrix(a, data.device)).to(data.dtype)
+
+
+@register('_image_random_color_jitter', params={'brightness': ('float', 0.0), 'contrast': ('float', 0.0),
+                                                'saturation': ('float', 0.0), 'hue': ('float', 0.0)})
+def image_random_color_jitter(data, brightness=0.0, contrast=0.0, saturation=0.0, hue=0.0):
+    ops = []
+    if brightness > 0:
+        ops.append(lambda x: image_random_brightness(x, 1 - brightness, 1 + brightness))
+    if contrast > 0:
+        ops.append(lambda x: image_random_contrast(x, 1 - contrast, 1 + contrast))
+    if saturation > 0:
+        ops.append(lambda x: image_random_saturation(x, 1 - saturation, 1 + saturation))
+    if hue > 0:
+        ops.append(lambda x: image_random_hue(x, -hue, hue))
+    for i in torch.randperm(len(ops)).tolist():
+        data = ops[i](data)
+    return data
+
+
+@register('_image_random_lighting', params={'alpha_std': ('float', 0.05)})
+def image_random_lighting(data, alpha_std=0.05):
+    alpha = torch.randn(3) * alpha_std
+    return image_adjust_lighting(data, tuple(alpha.tolist()))

@@ -555,17 +555,24 @@ def _op_func(op_name):
         attr = kwargs.pop('attr', None)
         kwargs.pop('out', None)
         pos = []
+        extra_pos = []
         for a in args:
-            if isinstance(a, Symbol):
+            if isinstance(a, Symbol) and not extra_pos:
                 pos.append(a)
-            elif isinstance(a, (list, tuple)) and a and all(isinstance(x, Symbol) for x in a):
+            elif isinstance(a, (list, tuple)) and a and all(isinstance(x, Symbol) for x in a) and not extra_pos:
                 pos.extend(a)
-            elif a is None:
+            elif a is None and not extra_pos:
                 pos.append(None)
+            elif isinstance(a, Symbol):
+                raise TypeError('%s: Symbol inputs must precede positional parameters' % op_name)
             else:
-                raise TypeError('%s: positional arguments must be Symbols, got %s' % (op_name, type(a)))
+                extra_pos.append(a)
         named = {k: v for k, v in kwargs.items() if isinstance(v, Symbol)}
-        attrs = {k: v for k, v in kwargs.items() if not isinstance(v, Symbol)}
+        attrs = {k: v for k, v in kwargs.items() if not isinstance(v, Symbol) and v is not None}
+        if extra_pos:
+            # positional attribute values follow the declared param order (as in the nd frontend)
+            for p, v in zip([p for p in op.params if p not in attrs], extra_pos):
+                attrs[p] = v
         extra = {}
         for k in list(attrs):
             if k not in op.params and k != op.key_var_num_args:
