@@ -932,10 +932,13 @@ _GATES = {'rnn_relu': 1, 'rnn_tanh': 1, 'lstm': 4, 'gru': 3}
 def rnn_param_size(mode, num_layers, input_size, state_size, bidirectional, projection_size=None):
     g = _GATES[mode]
     d = 2 if bidirectional else 1
+    hp = projection_size or state_size
     size = 0
     for layer in range(num_layers):
-        ni = input_size if layer == 0 else state_size * d
-        size += d * (g * state_size * ni + g * state_size * state_size + 2 * g * state_size)
+        ni = input_size if layer == 0 else hp * d
+        size += d * (g * state_size * ni + g * state_size * hp + 2 * g * state_size)
+        if projection_size:
+            size += d * projection_size * state_size
     return size
 
 
@@ -953,33 +956,117 @@ def _rnn_infer(in_shapes, a):
     bi = str(a.get('bidirectional', False)) in ('True', 'true', '1')
     nl = int(a.get('num_layers', 1))
     ss = int(a['state_size'])
-    res = {1: (rnn_param_size(a['mode'], nl, d[2], ss, bi),), 2: (nl * (2 if bi else 1), d[1], ss)}
+    ps = a.get('projection_size')
+    ps = int(ps) if ps not in (None, 'None', '') else None
+    res = {1: (rnn_param_size(a['mode'], nl, d[2], ss, bi, ps),), 2: (nl * (2 if bi else 1), d[1], ps or ss)}
     if a.get('mode') == 'lstm':
-        res[3] = res[2]
+        res[3] = (nl * (2 if bi else 1), d[1], ss)
     return res
 
 
-def unpack_rnn_params(params, mode, num_layers, input_size, state_size, bidirectional):
-    """Split MXNet's flat vector into per-(layer, direction) [w_ih, w_hh, b_ih, b_hh]."""
+def unpack_rnn_params(params, mode, num_layers, input_size, state_size, bidirectional, projection_size=None):
+    """Split MXNet's flat vector into per-(layer, direction) [w_ih, w_hh, b_ih, b_hh(, w_hr)].
+
+    Layout (src/operator/rnn-inl.h): all weights first — for every layer and
+    direction ``i2h``, ``h2h`` (and ``h2r`` with projection) — then all biases
+    ``i2h``, ``h2h`` in the same order.
+    """
     g = _GATES[mode]
     d = 2 if bidirectional else 1
+    hp = projection_size or state_size
     ws = []
     off = 0
     for layer in range(num_layers):
-        ni = input_size if layer == 0 else state_size * d
+        ni = input_size if layer == 0 else hp * d
         for _ in range(d):
-            wi = params[off:off + g * state_size * ni].reshape(g * state_size, ni); off += g * state_size * ni
-            wh = params[off:off + g * state_size * state_size].reshape(g * state_size, state_size)
-            off += g * state_size * state_size
-            ws.append([wi, wh])
+            wi = params[off:off + g * state_size * ni].reshape(g * state_size, ni)
+            off += g * state_size * ni
+            wh = params[off:off + g * state_size * hp].reshape(g * state_size, hp)
+            off += g * state_size * hp
+            entry = [wi, wh]
+            if projection_size:
+                wr = params[off:off + projection_size * state_size].reshape(projection_size, state_size)
+                off += projection_size * state_size
+                entry.append(wr)
+            ws.append(entry)
     k = 0
     for layer in range(num_layers):
         for _ in range(d):
-            bi = params[off:off + g * state_size]; off += g * state_size
-            bh = params[off:off + g * state_size]; off += g * state_size
-            ws[k] += [bi, bh]
+            bi = params[off:off + g * state_size]
+            off += g * state_size
+            bh = params[off:off + g * state_size]
+            off += g * state_size
+            wr = ws[k][2:] if projection_size else []
+            ws[k] = ws[k][:2] + [bi, bh] + wr
             k += 1
     return ws
+
+
+def _cell_step(mode, x, h, c, wi, wh, bi, bh, wr, clip):
+    gi = F.linear(x, wi, bi)
+    gh = F.linear(h, wh, bh)
+    if mode == 'lstm':
+        i, f, g, o = (gi + gh).chunk(4, -1)
+        c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(g)
+        if clip is not None:
+            lo, hi, nan = clip
+            c = c.clamp(lo if lo is not None else -float('inf'), hi if hi is not None else float('inf'))
+            if nan:
+                c = torch.nan_to_num(c, nan=0.0)
+        h = torch.sigmoid(o) * torch.tanh(c)
+        if wr is not None:
+            h = F.linear(h, wr)
+        return h, c
+    if mode == 'gru':
+        ir, iz, in_ = gi.chunk(3, -1)
+        hr, hz, hn = gh.chunk(3, -1)
+        r = torch.sigmoid(ir + hr)
+        z = torch.sigmoid(iz + hz)
+        n = torch.tanh(in_ + r * hn)
+        return (1 - z) * n + z * h, None
+    act = torch.tanh if mode == 'rnn_tanh' else torch.relu
+    return act(gi + gh), None
+
+
+def _rnn_loop(data, ws, h0, c0, mode, num_layers, d, p, train, clip, seq_len):
+    """Explicit time loop for the features the fused path lacks (clipping, variable lengths, LSTMP)."""
+    T = data.shape[0]
+    x = data
+    hs, cs = [], []
+    lens = seq_len.long() if seq_len is not None else None
+    for layer in range(num_layers):
+        outs = []
+        for di in range(d):
+            k = layer * d + di
+            w = ws[k]
+            wr = w[4] if len(w) > 4 else None
+            h = h0[k]
+            c = c0[k] if c0 is not None else None
+            ys = [None] * T
+            steps = range(T - 1, -1, -1) if di == 1 else range(T)
+            for t in steps:
+                if lens is not None and di == 1:
+                    valid = (t < lens).to(x.dtype).unsqueeze(-1)
+                else:
+                    valid = None
+                nh, nc = _cell_step(mode, x[t], h, c, w[0], w[1], w[2], w[3], wr, clip)
+                if lens is not None:
+                    m = (t < lens).to(x.dtype).unsqueeze(-1) if valid is None else valid
+                    h = m * nh + (1 - m) * h
+                    if c is not None:
+                        c = m * nc + (1 - m) * c
+                    ys[t] = nh * m
+                else:
+                    h, c = nh, nc
+                    ys[t] = nh
+            outs.append(torch.stack(ys))
+            hs.append(h)
+            if c is not None:
+                cs.append(c)
+        x = torch.cat(outs, -1) if d == 2 else outs[0]
+        if p > 0 and train and layer < num_layers - 1:
+            x = F.dropout(x, p, True)
+    return x, torch.stack(hs), (torch.stack(cs) if cs else None)
 
 
 @register('RNN', arg_names=_rnn_args, num_outputs=_rnn_nout, infer_params=_rnn_infer,
@@ -992,11 +1079,21 @@ def rnn(data, parameters, state, state_cell=None, sequence_length=None, state_si
         bidirectional=False, mode='lstm', p=0.0, state_outputs=False, projection_size=None,
         lstm_state_clip_min=None, lstm_state_clip_max=None, lstm_state_clip_nan=False,
         use_sequence_length=False):
-    if mode == 'rnn' or mode == 'lstm' and state_cell is None:
-        pass
-    ws = unpack_rnn_params(parameters, mode, num_layers, data.shape[2], state_size, bidirectional)
-    flat = [t for group in ws for t in group]
+    """Fused multi-layer RNN (src/operator/rnn.cc); TNC layout, MXNet flat parameter vector."""
+    ws = unpack_rnn_params(parameters, mode, num_layers, data.shape[2], state_size, bidirectional,
+                           projection_size)
     train = _state.STATE.training
+    d = 2 if bidirectional else 1
+    clip = None
+    if mode == 'lstm' and (lstm_state_clip_min is not None or lstm_state_clip_max is not None):
+        clip = (lstm_state_clip_min, lstm_state_clip_max, lstm_state_clip_nan)
+    if clip is not None or (use_sequence_length and sequence_length is not None):
+        out, h, c = _rnn_loop(data, ws, state, state_cell, mode, num_layers, d, p, train, clip,
+                              sequence_length if use_sequence_length else None)
+        if mode == 'lstm':
+            return (out, h, c) if state_outputs else out
+        return (out, h) if state_outputs else out
+    flat = [t for group in ws for t in group]
     if mode == 'lstm':
         out, h, c = torch._VF.lstm(data, (state, state_cell), flat, True, num_layers, p, train,
                                    bidirectional, False)

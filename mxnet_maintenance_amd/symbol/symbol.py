@@ -719,12 +719,50 @@ def _run_meta(op, parsed, shapes, dtypes):
     return [(tuple(o.shape), o.dtype) for o in out]
 
 
-def infer_graph(sym, known_shapes, known_dtypes, what='shape'):
+_INIT_OPS = ('_zeros', '_ones', '_full', '_empty', 'zeros', 'ones', 'full')
+
+
+def _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what):
+    """Init ops declared with 0 (unknown) dims, e.g. RNN ``begin_state`` via ``sym.zeros``.
+
+    The reference fills those dims by backward shape inference; here the
+    candidate sizes are the dims of the known argument shapes, and the first
+    candidate under which the whole graph infers consistently is written
+    back into the node's ``shape`` attribute (so executors allocate it).
+    """
+    zero_nodes = []
+    for n in order:
+        if n.op in _INIT_OPS and 'shape' in n.attrs:
+            shp = n.parsed().get('shape')
+            if shp and any(int(d) == 0 for d in shp):
+                zero_nodes.append((n, tuple(int(d) for d in shp)))
+    if not zero_nodes:
+        return None
+    cands = sorted({int(d) for s in known_shapes.values() if s for d in s if int(d) > 1})
+    for v in cands:
+        for n, shp in zero_nodes:
+            n.attrs['shape'] = str(tuple(d if d else v for d in shp))
+            n._parsed = None
+        try:
+            return infer_graph(sym, known_shapes, known_dtypes, what, _resolve=False)
+        except MXNetError:
+            continue
+    for n, shp in zero_nodes:
+        n.attrs['shape'] = str(shp)
+        n._parsed = None
+    return None
+
+
+def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True):
     """Propagate shapes and dtypes through the graph.
 
     Returns (arg_list, out_list, aux_list) of shapes (or dtypes), None for unknown.
     """
     order = sym._topo()
+    if _resolve and what == 'shape' and known_shapes:
+        res = _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what)
+        if res is not None:
+            return res
     shape = {}   # (id(node), idx) -> shape
     dtype = {}
     for n in order:
