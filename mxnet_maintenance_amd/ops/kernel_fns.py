@@ -183,3 +183,95 @@ def flat_sgd(w, g, mom, w32, lr, wd, momentum, rescale, clip):
         mom = None
     lib.flat_sgd(_DT[w.dtype], w.data_ptr(), g.data_ptr(), _p(mom), _p(w32), n, float(lr), float(wd),
                  float(momentum), float(rescale), float(clip), _stream())
+
+
+# ---------------------------------------------------------------------------
+# NHWC implicit-GEMM convolution (src/kernels/conv_igemm.hip)
+# ---------------------------------------------------------------------------
+
+import os as _os
+
+_CONV_HIP = _os.environ.get('MXAMD_CONV_HIP', '1') != '0'
+
+
+def conv_ok_shape(x, w, stride, pad, dilate=(1, 1), groups=1):
+    """True when the HIP implicit-GEMM forward kernel handles this 2-D conv."""
+    return (_CONV_HIP and x.dim() == 4 and w.dim() == 4 and groups == 1 and tuple(dilate) == (1, 1)
+            and x.dtype in (torch.float16, torch.bfloat16) and w.dtype == x.dtype
+            and x.is_contiguous() and w.is_contiguous() and x.shape[3] % 32 == 0 and w.shape[0] % 64 == 0
+            and w.shape[3] == x.shape[3] and x.numel() < 2 ** 31 and x.data_ptr() % 16 == 0
+            and w.data_ptr() % 16 == 0)
+
+
+def conv_fwd(x, w, stride, pad, bias=None):
+    """y[N,Ho,Wo,K] = conv(x[N,H,W,C], w[K,R,S,C]) on the MFMA implicit-GEMM kernel."""
+    N, H, W, C = x.shape
+    K, R, S, _ = w.shape
+    Ho = (H + 2 * pad[0] - R) // stride[0] + 1
+    Wo = (W + 2 * pad[1] - S) // stride[1] + 1
+    y = torch.empty((N, Ho, Wo, K), dtype=x.dtype, device=x.device)
+    if N * Ho * Wo * K >= 2 ** 31:
+        raise ValueError('conv_fwd: output too large for 32-bit indexing')
+    b = _f32(bias) if bias is not None else None
+    _K.lib().conv_nhwc_fwd(_DT[x.dtype], x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), N, H, W, C, K, R, S,
+                           stride[0], stride[1], pad[0], pad[1], _stream())
+    return y
+
+
+def _dgrad_weight(w):
+    """Weight of the equivalent forward conv computing dX from dY (stride 1): [Cin][R][S][Cout], flipped."""
+    return w.flip(1, 2).permute(3, 1, 2, 0).contiguous()
+
+
+def _conv_bwd_torch(dy, x, w, stride, pad, mask):
+    xc = x.permute(0, 3, 1, 2)
+    wc = w.permute(0, 3, 1, 2)
+    dyc = dy.permute(0, 3, 1, 2)
+    dx, dw, _ = torch.ops.aten.convolution_backward(dyc, xc, wc, None, list(stride), list(pad), [1, 1], False,
+                                                    [0, 0], 1, [mask[0], mask[1], False])
+    if dx is not None:
+        dx = dx.permute(0, 2, 3, 1)
+    if dw is not None:
+        dw = dw.permute(0, 2, 3, 1)
+    return dx, dw
+
+
+class ConvNHWC(torch.autograd.Function):
+    """2-D NHWC convolution: forward (and stride-1 backward-data) on the HIP MFMA kernel."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, stride, pad, dilate):
+        y = conv_fwd(x, w, stride, pad, bias)
+        ctx.save_for_backward(x, w)
+        ctx.stride, ctx.pad = stride, pad
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        stride, pad = ctx.stride, ctx.pad
+        need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dx = dw = db = None
+        R, S = w.shape[1], w.shape[2]
+        hip_dgrad = (need_dx and tuple(stride) == (1, 1) and w.shape[3] % 64 == 0 and w.shape[0] % 32 == 0
+                     and 2 * pad[0] == R - 1 and 2 * pad[1] == S - 1)
+        if hip_dgrad:
+            dx = conv_fwd(dy, _dgrad_weight(w), (1, 1), (R - 1 - pad[0], S - 1 - pad[1]))
+        if need_dw or (need_dx and not hip_dgrad):
+            tdx, tdw = _conv_bwd_torch(dy, x, w, stride, pad, (need_dx and not hip_dgrad, need_dw))
+            if not hip_dgrad:
+                dx = tdx
+            dw = tdw
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy.float().sum(dim=(0, 1, 2))
+        return dx, dw, db, None, None, None
+
+
+def conv_ok(x, w, stride, pad, dilate, groups):
+    return len(stride) == 2 and conv_ok_shape(x, w, stride, pad, dilate, groups)
+
+
+_K.conv_ok = conv_ok
+__all__ += ['ConvNHWC', 'conv_fwd', 'conv_ok_shape']

@@ -31,6 +31,8 @@ void gap_nhwc_forward(int dtype, const void* x, void* y, int N, int HW, int C, h
 void gap_nhwc_backward(int dtype, const void* dy, void* dx, int N, int HW, int C, hipStream_t s);
 void flat_sgd(int dtype, void* w, const void* g, float* mom, float* w32, int64_t n, float lr, float wd,
               float momentum, float rescale, float clip, hipStream_t s);
+void conv_nhwc_fwd(int dtype, const void* x, const void* w, const float* bias, void* y, int N, int H, int W, int C,
+                   int K, int R, int S, int sh, int sw, int ph, int pw, hipStream_t s);
 }  // namespace mxamd
 
 using namespace mxamd;
@@ -92,5 +94,11 @@ PYBIND11_MODULE(_hip_kernels, m) {
                        float wd, float momentum, float rescale, float clip, uintptr_t s) {
     flat_sgd(dt, P<void>(w), P<void>(g), P<float>(mom), P<float>(w32), n, lr, wd, momentum, rescale, clip, S(s));
     check_launch("flat_sgd");
+  });
+  m.def("conv_nhwc_fwd", [](int dt, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int N, int H, int W,
+                            int C, int K, int R, int Sf, int sh, int sw, int ph, int pw, uintptr_t s) {
+    conv_nhwc_fwd(dt, P<void>(x), P<void>(w), P<float>(bias), P<void>(y), N, H, W, C, K, R, Sf, sh, sw, ph, pw,
+                  S(s));
+    check_launch("conv_nhwc_fwd");
   });
 }

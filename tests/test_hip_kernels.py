@@ -182,3 +182,46 @@ def test_resnet_block_train_step_gpu():
     import numpy as np
     np.testing.assert_allclose(outs[0], outs[1], atol=1e-4, rtol=1e-4)
     np.testing.assert_allclose(grads[0], grads[1], atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('cfg', [
+    # (N, H, Cin, Cout, k, stride)
+    (2, 14, 64, 64, 1, 1), (3, 9, 64, 128, 3, 1), (2, 15, 128, 64, 3, 2), (2, 14, 256, 128, 1, 2),
+    (1, 7, 96, 192, 3, 1), (5, 5, 32, 64, 1, 1), (2, 11, 64, 256, 5, 1)])
+def test_conv_nhwc_fwd_matches_fp32(dtype, cfg):
+    from mxnet_maintenance_amd.ops import kernel_fns as KF
+    _lib()
+    N, H, Cin, Cout, k, s = cfg
+    pad = k // 2
+    torch.manual_seed(0)
+    x = torch.randn(N, H, H, Cin, device='cuda').to(dtype)
+    w = (torch.randn(Cout, k, k, Cin, device='cuda') / (k * k * Cin) ** 0.5).to(dtype)
+    bias = torch.randn(Cout, device='cuda')
+    assert KF.conv_ok_shape(x, w, (s, s), (pad, pad))
+    y = KF.conv_fwd(x, w, (s, s), (pad, pad), bias)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), bias, s, pad).permute(0, 2, 3, 1)
+    assert y.shape == ref.shape
+    tol = 2e-2 if dtype == torch.float16 else 6e-2
+    torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize('cfg', [(2, 14, 64, 128, 3, 1), (2, 14, 128, 64, 1, 1), (2, 14, 64, 64, 3, 2)])
+def test_conv_nhwc_autograd_matches_fp32(cfg):
+    from mxnet_maintenance_amd.ops import kernel_fns as KF
+    _lib()
+    N, H, Cin, Cout, k, s = cfg
+    pad = k // 2
+    torch.manual_seed(1)
+    x = torch.randn(N, H, H, Cin, device='cuda').half().requires_grad_()
+    w = (torch.randn(Cout, k, k, Cin, device='cuda') / (k * k * Cin) ** 0.5).half().requires_grad_()
+    y = KF.ConvNHWC.apply(x, w, None, (s, s), (pad, pad), (1, 1))
+    dy = torch.randn_like(y)
+    dx, dw = torch.autograd.grad(y, (x, w), dy)
+    xf = x.detach().float().requires_grad_()
+    wf = w.detach().float().requires_grad_()
+    yf = F.conv2d(xf.permute(0, 3, 1, 2), wf.permute(0, 3, 1, 2), None, s, pad).permute(0, 2, 3, 1)
+    dxf, dwf = torch.autograd.grad(yf, (xf, wf), dy.float())
+    torch.testing.assert_close(y.float(), yf, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(dx.float(), dxf, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(dw.float(), dwf, rtol=5e-2, atol=5e-1)
