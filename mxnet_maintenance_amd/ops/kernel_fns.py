@@ -236,12 +236,102 @@ def _conv_bwd_torch(dy, x, w, stride, pad, mask):
     return dx, dw
 
 
+# ---- algorithm selection (the MXNET_CUDNN_AUTOTUNE_DEFAULT analogue) -------------------------------
+# Candidates per conv pass: the in-tree MFMA implicit-GEMM kernel, hipBLASLt
+# (torch.mm on the NHWC tensor viewed as a matrix; only 1x1/stride-1, a plain
+# library GEMM) and MIOpen.  With autotuning on (default) the first call of
+# every (pass, shape, dtype) times each candidate on the live inputs and
+# caches the fastest; during HIP-graph capture, or with autotuning off, a
+# measured heuristic picks.
+
+_AUTOTUNE = int(_os.environ.get('MXNET_CUDNN_AUTOTUNE_DEFAULT', '1')) > 0
+_ALGO = {}
+
+
+def _time_candidates(cands, reps=3):
+    best, best_t, out = None, None, None
+    for name, fn in cands:
+        fn()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            r = fn()
+        e.record()
+        e.synchronize()
+        t = s.elapsed_time(e)
+        if best_t is None or t < best_t:
+            best, best_t, out = name, t, r
+    return best, out
+
+
+def _select(key, cands, default):
+    """Run the cached / autotuned / default candidate and return its result."""
+    name = _ALGO.get(key)
+    if name is None:
+        if _AUTOTUNE and not torch.cuda.is_current_stream_capturing() and len(cands) > 1:
+            name, out = _time_candidates(cands)
+            _ALGO[key] = name
+            return out
+        name = default
+    table = dict(cands)
+    return (table[name] if name in table else cands[0][1])()
+
+
+def _fwd_candidates(x, w, stride, pad, bias):
+    c = []
+    K, R, S, C = w.shape
+    if conv_ok_shape(x, w, stride, pad):
+        c.append(('hip', lambda: conv_fwd(x, w, stride, pad, bias)))
+    if R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0):
+        def mm():
+            y = torch.mm(x.reshape(-1, C), w.reshape(K, C).t())
+            if bias is not None:
+                y = y + bias.to(y.dtype)
+            return y.view(x.shape[0], x.shape[1], x.shape[2], K)
+        c.append(('mm', mm))
+
+    def miopen():
+        y = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), bias, tuple(stride), tuple(pad))
+        return y.permute(0, 2, 3, 1).contiguous()
+    c.append(('miopen', miopen))
+    return c
+
+
+def _fwd_default(x, w, stride):
+    K, R, S, C = w.shape
+    if R == 1 and S == 1 and tuple(stride) == (1, 1) and (K >= 256 or x.shape[1] * x.shape[2] <= 784):
+        return 'mm'
+    return 'hip'
+
+
+def _dgrad_candidates(dy, x, w, stride, pad):
+    c = []
+    K, R, S, C = w.shape
+    if R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0):
+        c.append(('mm', lambda: torch.mm(dy.reshape(-1, K), w.reshape(K, C)).view(x.shape)))
+    if (tuple(stride) == (1, 1) and C % 64 == 0 and K % 32 == 0 and 2 * pad[0] == R - 1 and 2 * pad[1] == S - 1
+            and _CONV_HIP):
+        c.append(('hip', lambda: conv_fwd(dy, _dgrad_weight(w), (1, 1), (R - 1 - pad[0], S - 1 - pad[1]))))
+    c.append(('miopen', lambda: _conv_bwd_torch(dy, x, w, stride, pad, (True, False))[0]))
+    return c
+
+
+def _dgrad_default(w, stride):
+    K, R, S, C = w.shape
+    if tuple(stride) != (1, 1):
+        return 'miopen'
+    if R == 1 and S == 1:
+        return 'mm' if C >= 128 else 'miopen'
+    return 'hip' if C >= 128 and C % 64 == 0 else 'miopen'
+
+
 class ConvNHWC(torch.autograd.Function):
-    """2-D NHWC convolution: forward (and stride-1 backward-data) on the HIP MFMA kernel."""
+    """2-D NHWC convolution with per-shape algorithm selection (HIP MFMA kernel / hipBLASLt / MIOpen)."""
 
     @staticmethod
     def forward(ctx, x, w, bias, stride, pad, dilate):
-        y = conv_fwd(x, w, stride, pad, bias)
+        key = ('fwd', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype, bias is not None)
+        y = _select(key, _fwd_candidates(x, w, stride, pad, bias), _fwd_default(x, w, stride))
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.pad = stride, pad
         ctx.has_bias = bias is not None
@@ -252,25 +342,26 @@ class ConvNHWC(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dy = dy.contiguous()
         stride, pad = ctx.stride, ctx.pad
-        need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         dx = dw = db = None
-        R, S = w.shape[1], w.shape[2]
-        hip_dgrad = (need_dx and tuple(stride) == (1, 1) and w.shape[3] % 64 == 0 and w.shape[0] % 32 == 0
-                     and 2 * pad[0] == R - 1 and 2 * pad[1] == S - 1)
-        if hip_dgrad:
-            dx = conv_fwd(dy, _dgrad_weight(w), (1, 1), (R - 1 - pad[0], S - 1 - pad[1]))
-        if need_dw or (need_dx and not hip_dgrad):
-            tdx, tdw = _conv_bwd_torch(dy, x, w, stride, pad, (need_dx and not hip_dgrad, need_dw))
-            if not hip_dgrad:
-                dx = tdx
-            dw = tdw
+        if ctx.needs_input_grad[0]:
+            key = ('dgrad', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype)
+            dx = _select(key, _dgrad_candidates(dy, x, w, stride, pad), _dgrad_default(w, stride))
+        if ctx.needs_input_grad[1]:
+            dw = _conv_bwd_torch(dy, x, w, stride, pad, (False, True))[1]
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum(dim=(0, 1, 2))
         return dx, dw, db, None, None, None
 
 
+def conv_algos():
+    """The algorithm chosen for every (pass, shape) seen so far."""
+    return dict(_ALGO)
+
+
 def conv_ok(x, w, stride, pad, dilate, groups):
-    return len(stride) == 2 and conv_ok_shape(x, w, stride, pad, dilate, groups)
+    # any 2-D fp16/bf16 NHWC conv goes through ConvNHWC's algorithm selection
+    return (len(stride) == 2 and x.dim() == 4 and groups == 1 and tuple(dilate) == (1, 1) and x.is_contiguous()
+            and w.is_contiguous() and x.dtype in (torch.float16, torch.bfloat16) and w.dtype == x.dtype)
 
 
 _K.conv_ok = conv_ok

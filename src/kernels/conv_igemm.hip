@@ -278,7 +278,10 @@ template <typename T>
 static void dispatch_fwd(const void* x, const void* w, const float* bias, void* y, const ConvGeom& g,
                          hipStream_t s) {
   const bool co128 = (g.K % 128) == 0;
-  const bool bk64 = (g.C % 64) == 0;
+  // BK=64 halves the barriers per FLOP but its LDS/VGPR footprint allows only
+  // 1-2 blocks per CU; short reductions (1x1 over <=128 channels) are
+  // bandwidth-bound and want the occupancy of BK=32 instead.
+  const bool bk64 = (g.C % 64) == 0 && g.Ktot >= 256;
   if (co128 && bk64) launch_fwd<T, 128, 64>(x, w, bias, y, g, s);
   else if (co128) launch_fwd<T, 128, 32>(x, w, bias, y, g, s);
   else if (bk64) launch_fwd<T, 64, 64>(x, w, bias, y, g, s);
