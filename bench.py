@@ -110,6 +110,13 @@ def main():
                        'per_gpu_batch': B, 'seq_len': None, 'image_size': S, 'parallelism': 'dp%d' % n,
                        'layout': 'NHWC', 'optimizer': 'mp-SGD momentum 0.9', 'final_loss': round(loss_val, 4)},
         }), flush=True)
+    if os.environ.get('MXAMD_BENCH_VERBOSE', '0') == '1' and rank == 0:
+        try:
+            from mxnet_maintenance_amd.ops import kernel_fns
+            for k, v in sorted(kernel_fns.conv_algos().items(), key=str):
+                print('conv-algo', v, k, file=sys.stderr)
+        except Exception as e:  # pragma: no cover
+            print('conv-algo unavailable:', e, file=sys.stderr)
     if dist.world_size() > 1:
         torch.distributed.destroy_process_group()
 

@@ -87,6 +87,8 @@ class BatchNormNHWC(torch.autograd.Function):
         ctx.save_for_backward(x, y if relu else None, g, mean, invstd)
         ctx.cfg = (bool(relu), bool(training), addend is not None, gamma.dtype, beta.dtype)
         ctx.mark_non_differentiable(mean, var)
+        # mean/var never receive gradients: skip materialising two zero tensors per call
+        ctx.set_materialize_grads(False)
         return y, mean, var
 
     @staticmethod
@@ -94,6 +96,8 @@ class BatchNormNHWC(torch.autograd.Function):
         lib = _K.lib()
         x, y, g, mean, invstd = ctx.saved_tensors
         relu, training, has_add, gdt, bdt = ctx.cfg
+        if gy is None:
+            return (None,) * 10
         gy = gy.contiguous()
         C = x.shape[-1]
         R = x.numel() // C
@@ -366,3 +370,54 @@ def conv_ok(x, w, stride, pad, dilate, groups):
 
 _K.conv_ok = conv_ok
 __all__ += ['ConvNHWC', 'conv_fwd', 'conv_ok_shape']
+
+
+# ---------------------------------------------------------------------------
+# NHWC pooling (src/kernels/pool_nhwc.hip)
+# ---------------------------------------------------------------------------
+
+def _pool_out(n, k, s, p, full):
+    # MXNet: valid = floor, full = ceil (src/operator/nn/pooling-inl.h), no window clipping
+    if full:
+        return -(-(n + 2 * p - k) // s) + 1
+    return (n + 2 * p - k) // s + 1
+
+
+def pool_ok(x, kernel, stride, pad):
+    return (x.dim() == 4 and x.dtype in _DT and x.is_contiguous() and x.shape[3] % 8 == 0
+            and len(kernel) == 2 and kernel[0] * kernel[1] <= 256 and x.data_ptr() % 16 == 0
+            and all(p < k for p, k in zip(pad, kernel)))
+
+
+class PoolNHWC(torch.autograd.Function):
+    """Max/avg 2-D pooling on NHWC tensors (max keeps a uint8 argmax per element)."""
+
+    @staticmethod
+    def forward(ctx, x, pool_type, kernel, stride, pad, full, count_include_pad):
+        N, H, W, C = x.shape
+        Ho = _pool_out(H, kernel[0], stride[0], pad[0], full)
+        Wo = _pool_out(W, kernel[1], stride[1], pad[1], full)
+        is_max = pool_type == 'max'
+        y = torch.empty((N, Ho, Wo, C), dtype=x.dtype, device=x.device)
+        arg = torch.empty((N, Ho, Wo, C), dtype=torch.uint8, device=x.device) if is_max else None
+        geo = (N, H, W, C, Ho, Wo, kernel[0], kernel[1], stride[0], stride[1], pad[0], pad[1],
+               int(bool(count_include_pad)))
+        _K.lib().pool_nhwc_forward(_DT[x.dtype], int(is_max), x.data_ptr(), y.data_ptr(), _p(arg), *geo, _stream())
+        ctx.geo, ctx.is_max, ctx.dt = geo, is_max, x.dtype
+        if is_max:
+            ctx.save_for_backward(arg)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        geo = ctx.geo
+        arg = ctx.saved_tensors[0] if ctx.is_max else None
+        dx = torch.empty((geo[0], geo[1], geo[2], geo[3]), dtype=ctx.dt, device=dy.device)
+        _K.lib().pool_nhwc_backward(_DT[ctx.dt], int(ctx.is_max), dy.data_ptr(), _p(arg), dx.data_ptr(), *geo,
+                                    _stream())
+        return dx, None, None, None, None, None, None
+
+
+_K.pool_ok = pool_ok
+__all__ += ['PoolNHWC']

@@ -33,6 +33,11 @@ void flat_sgd(int dtype, void* w, const void* g, float* mom, float* w32, int64_t
               float momentum, float rescale, float clip, hipStream_t s);
 void conv_nhwc_fwd(int dtype, const void* x, const void* w, const float* bias, void* y, int N, int H, int W, int C,
                    int K, int R, int S, int sh, int sw, int ph, int pw, hipStream_t s);
+void pool_nhwc_forward(int dtype, int is_max, const void* x, void* y, uint8_t* arg, int N, int H, int W, int C,
+                       int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip, hipStream_t s);
+void pool_nhwc_backward(int dtype, int is_max, const void* dy, const uint8_t* arg, void* dx, int N, int H, int W,
+                        int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip,
+                        hipStream_t s);
 }  // namespace mxamd
 
 using namespace mxamd;
@@ -100,5 +105,19 @@ PYBIND11_MODULE(_hip_kernels, m) {
     conv_nhwc_fwd(dt, P<void>(x), P<void>(w), P<float>(bias), P<void>(y), N, H, W, C, K, R, Sf, sh, sw, ph, pw,
                   S(s));
     check_launch("conv_nhwc_fwd");
+  });
+  m.def("pool_nhwc_forward", [](int dt, int is_max, uintptr_t x, uintptr_t y, uintptr_t arg, int N, int H, int W,
+                                int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip,
+                                uintptr_t s) {
+    pool_nhwc_forward(dt, is_max, P<void>(x), P<void>(y), P<uint8_t>(arg), N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw,
+                      cip, S(s));
+    check_launch("pool_nhwc_forward");
+  });
+  m.def("pool_nhwc_backward", [](int dt, int is_max, uintptr_t dy, uintptr_t arg, uintptr_t dx, int N, int H, int W,
+                                 int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip,
+                                 uintptr_t s) {
+    pool_nhwc_backward(dt, is_max, P<void>(dy), P<uint8_t>(arg), P<void>(dx), N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph,
+                       pw, cip, S(s));
+    check_launch("pool_nhwc_backward");
   });
 }

@@ -15,7 +15,7 @@
 // Every thread moves 16 bytes (8 x fp16/bf16) per access; a row of C channels
 // is covered by C/8 lanes so loads are fully coalesced for any C % 8 == 0.
 // Reductions: per-thread fp32 registers -> LDS tree -> per-block partials ->
-// one wave per channel combines partials in fp64.
+// one block per channel combines the (channel-major) partials in fp64.
 #include <stdexcept>
 
 #include "common.h"
@@ -59,38 +59,44 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   int64_t r1 = r0 + rows_per_block;
   if (r1 > R) r1 = R;
-  for (int64_t r = r0 + lane_r; r < r1; r += rpi) {
-    const int64_t off = r * C + cbase;
-    Vec8<T> vx;
-    vx.load(x + off);
-    if (MODE == 0) {
+  // rows are consumed UNR at a time: all loads of a batch are issued before any
+  // accumulation, so each thread keeps UNR (x3 in backward) 16-byte loads in flight
+  constexpr int UNR = 4;
+  auto accum = [&](const Vec8<T>& vx, const Vec8<T>& vdy, const Vec8<T>& vy) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 8; ++i) {
+      if (MODE == 0) {
         float d = vx.get(i) - k[i];
         s1[i] += d;
         s2[i] += d * d;
-      }
-    } else {
-      Vec8<T> vdy;
-      vdy.load(dy + off);
-      if (RELU) {
-        Vec8<T> vy;
-        vy.load(y + off);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          float dz = vy.get(i) > 0.f ? vdy.get(i) : 0.f;
-          s1[i] += dz;
-          s2[i] += dz * (vx.get(i) - k[i]);
-        }
       } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          float dz = vdy.get(i);
-          s1[i] += dz;
-          s2[i] += dz * (vx.get(i) - k[i]);
-        }
+        float dz = vdy.get(i);
+        if (RELU) dz = vy.get(i) > 0.f ? dz : 0.f;
+        s1[i] += dz;
+        s2[i] += dz * (vx.get(i) - k[i]);
       }
     }
+  };
+  int64_t r = r0 + lane_r;
+  for (; r + (UNR - 1) * rpi < r1; r += UNR * rpi) {
+    Vec8<T> vx[UNR], vdy[UNR], vy[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int64_t off = (r + u * rpi) * C + cbase;
+      vx[u].load(x + off);
+      if (MODE == 1) vdy[u].load(dy + off);
+      if (MODE == 1 && RELU) vy[u].load(y + off);
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) accum(vx[u], vdy[u], vy[u]);
+  }
+  for (; r < r1; r += rpi) {
+    const int64_t off = r * C + cbase;
+    Vec8<T> vx, vdy, vy;
+    vx.load(x + off);
+    if (MODE == 1) vdy.load(dy + off);
+    if (MODE == 1 && RELU) vy.load(y + off);
+    accum(vx, vdy, vy);
   }
   // reduce the rpi row-lanes that share a channel group through LDS
   __shared__ float sh1[kBnThreads * 8];
@@ -108,35 +114,55 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(
       a += sh1[rr * cb + c];
       b += sh2[rr * cb + c];
     }
-    const int64_t o = static_cast<int64_t>(blockIdx.x) * C + blockIdx.y * cb + c;
+    // channel-major partials [C][nblk]: the finalize reads each channel's
+    // partials contiguously
+    const int64_t o = static_cast<int64_t>(blockIdx.y * cb + c) * gridDim.x + blockIdx.x;
     part1[o] = a;
     part2[o] = b;
   }
 }
 
-// One wave per channel: combine per-block partials (fp64) and emit statistics.
+// One 256-thread block per channel: combine the channel's per-block partials
+// (contiguous, channel-major) in fp64 and emit statistics.
 // MODE 0 (forward): out mean, invstd, var(biased); scale = g*invstd, shift = b - mean*scale
 // MODE 1 (backward): dgamma, dbeta and the dx coefficients A, B, Cc
+constexpr int kFinThreads = 256;
 template <int MODE>
-__global__ void __launch_bounds__(64) bn_finalize_kernel(
+__global__ void __launch_bounds__(kFinThreads) bn_finalize_kernel(
     const float* __restrict__ part1, const float* __restrict__ part2, int nblk, int C, int64_t R,
     const float* __restrict__ center, const float* __restrict__ gamma, const float* __restrict__ beta,
     const float* __restrict__ invstd_in, float eps, float* __restrict__ o0, float* __restrict__ o1,
     float* __restrict__ o2, float* __restrict__ o3, float* __restrict__ o4, float* __restrict__ o5,
     int fix_gamma, int training, float momentum, float* __restrict__ mm_upd, float* __restrict__ mv_upd) {
   const int c = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x;
+  const float* p1 = part1 + static_cast<int64_t>(c) * nblk;
+  const float* p2 = part2 + static_cast<int64_t>(c) * nblk;
   double a = 0.0, b = 0.0;
-  for (int i = lane; i < nblk; i += 64) {
-    a += part1[static_cast<int64_t>(i) * C + c];
-    b += part2[static_cast<int64_t>(i) * C + c];
+  for (int i = tid; i < nblk; i += kFinThreads) {
+    a += p1[i];
+    b += p2[i];
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     a += __shfl_xor(a, o, 64);
     b += __shfl_xor(b, o, 64);
   }
-  if (lane != 0) return;
+  __shared__ double sa[kFinThreads / 64], sb[kFinThreads / 64];
+  const int lane = tid & 63;
+  if (lane == 0) {
+    sa[tid >> 6] = a;
+    sb[tid >> 6] = b;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  a = 0.0;
+  b = 0.0;
+#pragma unroll
+  for (int w = 0; w < kFinThreads / 64; ++w) {
+    a += sa[w];
+    b += sb[w];
+  }
   const double n = static_cast<double>(R);
   const float g = fix_gamma ? 1.f : gamma[c];
   if (MODE == 0) {
@@ -245,7 +271,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_bwd_apply_kernel(
 
 static inline int64_t bn_rows_per_block(int64_t R, int C, const BnGeom& g, int* nblk) {
   const int cblocks = C / g.cb;
-  int64_t target = 1024 / cblocks;
+  int64_t target = 512 / cblocks;   // ~2 blocks per CU; partial rows stay few
   if (target < 8) target = 8;
   int64_t rpb = (R + target - 1) / target;
   rpb = (rpb + g.rpi - 1) / g.rpi * g.rpi;
@@ -277,7 +303,7 @@ static void bn_forward_impl(const void* x, const void* addend, void* y, const fl
     float* p2 = part + static_cast<int64_t>(nblk) * C;
     hipLaunchKernelGGL((bn_reduce_kernel<T, 0, false>), grid, dim3(kBnThreads), 0, s,
                        static_cast<const T*>(x), nullptr, nullptr, center, p1, p2, R, C, g.tpr, g.rpi, rpb);
-    hipLaunchKernelGGL((bn_finalize_kernel<0>), dim3(C), dim3(64), 0, s, p1, p2, nblk, C, R, center, gamma,
+    hipLaunchKernelGGL((bn_finalize_kernel<0>), dim3(C), dim3(kFinThreads), 0, s, p1, p2, nblk, C, R, center, gamma,
                        beta, nullptr, eps, mean, invstd, var, scale, shift, nullptr, fix_gamma, 1, momentum, mm_upd,
                        mv_upd);
   }
@@ -327,7 +353,7 @@ static void bn_backward_impl(const void* x, const void* dy, const void* y, void*
   float* A = coef;
   float* B = coef + C;
   float* Cc = coef + 2 * C;
-  hipLaunchKernelGGL((bn_finalize_kernel<1>), dim3(C), dim3(64), 0, s, p1, p2, nblk, C, R, mean, gamma, nullptr,
+  hipLaunchKernelGGL((bn_finalize_kernel<1>), dim3(C), dim3(kFinThreads), 0, s, p1, p2, nblk, C, R, mean, gamma, nullptr,
                      invstd, 0.f, dgamma, dbeta, A, B, Cc, nullptr, fix_gamma, training, 0.f, nullptr,
                      nullptr);
   const int64_t nvec = R * C / 8;

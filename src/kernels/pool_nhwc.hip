@@ -1,0 +1,199 @@
+// NHWC 2-D max / average pooling for gfx950 (forward + backward).
+//
+// Parity: src/operator/nn/pooling.cc / cudnn_pooling (pool_type max|avg,
+// pooling_convention valid|full, count_include_pad).
+//
+// Memory-bound: every thread owns 8 consecutive channels (one 16-byte
+// vector) of one output (forward) or one input (backward) pixel.
+//   max forward : y = max over the window, plus a uint8 window index per
+//                 element (the argmax) so the backward never re-reads x.
+//   max backward: gather form — each input element sums dy of the (few)
+//                 windows that cover it and chose it; no atomics, no memset.
+//   avg         : forward averages, backward gathers dy / count.
+#include "common.h"
+
+namespace mxamd {
+
+struct PoolGeom {
+  int N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw;
+  int count_include_pad;
+};
+
+template <typename T, bool MAX>
+__global__ void __launch_bounds__(256) pool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                       uint8_t* __restrict__ arg, PoolGeom g, int64_t nvec) {
+  const int cv = g.C / 8;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec;
+       v += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int c8 = static_cast<int>(v % cv) * 8;
+    int64_t p = v / cv;
+    const int wo = static_cast<int>(p % g.Wo);
+    p /= g.Wo;
+    const int ho = static_cast<int>(p % g.Ho);
+    const int n = static_cast<int>(p / g.Ho);
+    const int h0 = ho * g.sh - g.ph, w0 = wo * g.sw - g.pw;
+    float acc[8];
+    uint8_t am[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      acc[i] = MAX ? -INFINITY : 0.f;
+      am[i] = 0;
+    }
+    int cnt = 0;
+    for (int a = 0; a < g.kh; ++a) {
+      const int h = h0 + a;
+      if ((unsigned)h >= (unsigned)g.H) continue;
+      for (int b = 0; b < g.kw; ++b) {
+        const int w = w0 + b;
+        if ((unsigned)w >= (unsigned)g.W) continue;
+        Vec8<T> vx;
+        vx.load(x + ((static_cast<int64_t>(n) * g.H + h) * g.W + w) * g.C + c8);
+        ++cnt;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float f = vx.get(i);
+          if (MAX) {
+            if (f > acc[i]) {
+              acc[i] = f;
+              am[i] = static_cast<uint8_t>(a * g.kw + b);
+            }
+          } else {
+            acc[i] += f;
+          }
+        }
+      }
+    }
+    Vec8<T> out;
+    if (MAX) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) out.set(i, cnt ? acc[i] : 0.f);   // empty window (full convention edge)
+      uint2 packed;
+      packed.x = am[0] | (am[1] << 8) | (am[2] << 16) | (static_cast<uint32_t>(am[3]) << 24);
+      packed.y = am[4] | (am[5] << 8) | (am[6] << 16) | (static_cast<uint32_t>(am[7]) << 24);
+      *reinterpret_cast<uint2*>(arg + v * 8) = packed;
+    } else {
+      int den = cnt;
+      if (g.count_include_pad) {
+        const int he = min(h0 + g.kh, g.H + g.ph), we = min(w0 + g.kw, g.W + g.pw);
+        den = (he - h0) * (we - w0);
+      }
+      const float inv = den > 0 ? 1.f / den : 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) out.set(i, acc[i] * inv);
+    }
+    out.store(y + v * 8);
+  }
+}
+
+template <typename T, bool MAX>
+__global__ void __launch_bounds__(256) pool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                                       T* __restrict__ dx, PoolGeom g, int64_t nvec) {
+  const int cv = g.C / 8;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec;
+       v += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int c8 = static_cast<int>(v % cv) * 8;
+    int64_t p = v / cv;
+    const int w = static_cast<int>(p % g.W);
+    p /= g.W;
+    const int h = static_cast<int>(p % g.H);
+    const int n = static_cast<int>(p / g.H);
+    // output windows covering (h, w): ho*sh - ph <= h <= ho*sh - ph + kh - 1
+    const int hp = h + g.ph, wp = w + g.pw;
+    const int ho_lo = hp - g.kh + 1 > 0 ? (hp - g.kh + g.sh) / g.sh : 0;
+    const int ho_hi = min(hp / g.sh, g.Ho - 1);
+    const int wo_lo = wp - g.kw + 1 > 0 ? (wp - g.kw + g.sw) / g.sw : 0;
+    const int wo_hi = min(wp / g.sw, g.Wo - 1);
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        const int64_t o = ((static_cast<int64_t>(n) * g.Ho + ho) * g.Wo + wo) * g.C + c8;
+        Vec8<T> vd;
+        vd.load(dy + o);
+        if (MAX) {
+          const int idx = (h - (ho * g.sh - g.ph)) * g.kw + (w - (wo * g.sw - g.pw));
+          const uint2 packed = *reinterpret_cast<const uint2*>(arg + o);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const uint32_t word = i < 4 ? packed.x : packed.y;
+            const int a = (word >> ((i & 3) * 8)) & 0xff;
+            if (a == idx) acc[i] += vd.get(i);
+          }
+        } else {
+          const int h0 = ho * g.sh - g.ph, w0 = wo * g.sw - g.pw;
+          int den;
+          if (g.count_include_pad) {
+            const int he = min(h0 + g.kh, g.H + g.ph), we = min(w0 + g.kw, g.W + g.pw);
+            den = (he - h0) * (we - w0);
+          } else {
+            const int hs = max(h0, 0), ws = max(w0, 0);
+            const int he = min(h0 + g.kh, g.H), we = min(w0 + g.kw, g.W);
+            den = (he - hs) * (we - ws);
+          }
+          const float inv = den > 0 ? 1.f / den : 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) acc[i] += vd.get(i) * inv;
+        }
+      }
+    }
+    Vec8<T> out;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out.set(i, acc[i]);
+    out.store(dx + v * 8);
+  }
+}
+
+static inline int grid_for(int64_t nvec) {
+  int64_t b = (nvec + 255) / 256;
+  return static_cast<int>(b < 256 * 32 ? b : 256 * 32);
+}
+
+template <typename T>
+static void pool_fwd_t(int is_max, const void* x, void* y, uint8_t* arg, const PoolGeom& g, hipStream_t s) {
+  const int64_t nvec = static_cast<int64_t>(g.N) * g.Ho * g.Wo * (g.C / 8);
+  if (is_max)
+    hipLaunchKernelGGL((pool_fwd_kernel<T, true>), dim3(grid_for(nvec)), dim3(256), 0, s,
+                       static_cast<const T*>(x), static_cast<T*>(y), arg, g, nvec);
+  else
+    hipLaunchKernelGGL((pool_fwd_kernel<T, false>), dim3(grid_for(nvec)), dim3(256), 0, s,
+                       static_cast<const T*>(x), static_cast<T*>(y), arg, g, nvec);
+}
+
+template <typename T>
+static void pool_bwd_t(int is_max, const void* dy, const uint8_t* arg, void* dx, const PoolGeom& g, hipStream_t s) {
+  const int64_t nvec = static_cast<int64_t>(g.N) * g.H * g.W * (g.C / 8);
+  if (is_max)
+    hipLaunchKernelGGL((pool_bwd_kernel<T, true>), dim3(grid_for(nvec)), dim3(256), 0, s,
+                       static_cast<const T*>(dy), arg, static_cast<T*>(dx), g, nvec);
+  else
+    hipLaunchKernelGGL((pool_bwd_kernel<T, false>), dim3(grid_for(nvec)), dim3(256), 0, s,
+                       static_cast<const T*>(dy), arg, static_cast<T*>(dx), g, nvec);
+}
+
+static PoolGeom make_geom(int N, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw,
+                          int cip) {
+  MXAMD_HOST_CHECK(C % 8 == 0, "pool_nhwc: channels must be a multiple of 8");
+  MXAMD_HOST_CHECK(kh * kw <= 256, "pool_nhwc: window larger than 256 elements");
+  PoolGeom g{N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, cip};
+  return g;
+}
+
+void pool_nhwc_forward(int dtype, int is_max, const void* x, void* y, uint8_t* arg, int N, int H, int W, int C,
+                       int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip, hipStream_t s) {
+  PoolGeom g = make_geom(N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, cip);
+  if (dtype == kF16) pool_fwd_t<__half>(is_max, x, y, arg, g, s);
+  else if (dtype == kBF16) pool_fwd_t<__hip_bfloat16>(is_max, x, y, arg, g, s);
+  else pool_fwd_t<float>(is_max, x, y, arg, g, s);
+}
+
+void pool_nhwc_backward(int dtype, int is_max, const void* dy, const uint8_t* arg, void* dx, int N, int H, int W,
+                        int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip,
+                        hipStream_t s) {
+  PoolGeom g = make_geom(N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, cip);
+  if (dtype == kF16) pool_bwd_t<__half>(is_max, dy, arg, dx, g, s);
+  else if (dtype == kBF16) pool_bwd_t<__hip_bfloat16>(is_max, dy, arg, dx, g, s);
+  else pool_bwd_t<float>(is_max, dy, arg, dx, g, s);
+}
+
+}  // namespace mxamd

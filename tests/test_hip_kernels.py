@@ -225,3 +225,26 @@ def test_conv_nhwc_autograd_matches_fp32(cfg):
     torch.testing.assert_close(y.float(), yf, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(dx.float(), dxf, rtol=3e-2, atol=3e-2)
     torch.testing.assert_close(dw.float(), dwf, rtol=5e-2, atol=5e-1)
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('cfg', [((3, 3), (2, 2), (1, 1), 'max'), ((2, 2), (2, 2), (0, 0), 'max'),
+                                 ((3, 3), (1, 1), (1, 1), 'avg'), ((3, 3), (2, 2), (1, 1), 'avg')])
+def test_pool_nhwc_matches_torch(dtype, cfg):
+    from mxnet_maintenance_amd.ops import kernel_fns as KF
+    _lib()
+    k, s, p, kind = cfg
+    torch.manual_seed(0)
+    x = torch.randn(2, 13, 11, 24, device='cuda').to(dtype).requires_grad_()
+    y = KF.PoolNHWC.apply(x, kind, k, s, p, False, True)
+    xf = x.detach().float().permute(0, 3, 1, 2).requires_grad_()
+    if kind == 'max':
+        yf = F.max_pool2d(xf, k, s, p)
+    else:
+        yf = F.avg_pool2d(xf, k, s, p, count_include_pad=True)
+    yf = yf.permute(0, 2, 3, 1)
+    torch.testing.assert_close(y.float(), yf, rtol=1e-2, atol=1e-2)
+    dy = torch.randn_like(y)
+    dx, = torch.autograd.grad(y, x, dy)
+    dxf, = torch.autograd.grad(yf, xf, dy.float())
+    torch.testing.assert_close(dx.float(), dxf.permute(0, 2, 3, 1), rtol=2e-2, atol=2e-2)

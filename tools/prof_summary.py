@@ -24,8 +24,11 @@ def classify(name):
 
 
 def main(d, steps):
-    f = glob.glob(d + '/*kernel_stats.csv')[0]
+    f = glob.glob(d + '/**/*kernel_stats.csv', recursive=True)[0]
     rows = list(csv.DictReader(open(f)))
+    if steps <= 0:
+        # one fused optimizer launch per training step (warmup included)
+        steps = max(1, sum(int(r['Calls']) for r in rows if 'flat_sgd' in r['Name']))
     tot = sum(float(r['TotalDurationNs']) for r in rows)
     print('total kernel time %.2f ms (%d steps profiled -> %.2f ms/step)' % (tot / 1e6, steps, tot / 1e6 / steps))
     cls = {}
@@ -35,10 +38,10 @@ def main(d, steps):
     for c, v in sorted(cls.items(), key=lambda kv: -kv[1]):
         print('  %-32s %8.2f ms/step  %5.1f%%' % (c, v / 1e6 / steps, 100 * v / tot))
     print('top kernels:')
-    for r in sorted(rows, key=lambda r: -float(r['TotalDurationNs']))[:25]:
+    for r in sorted(rows, key=lambda r: -float(r['TotalDurationNs']))[:40]:
         print('  %8.3f ms/step %5.1f%% %6s  %s' % (float(r['TotalDurationNs']) / 1e6 / steps, float(r['Percentage']),
                                               r['Calls'], re.sub(r'\s+', ' ', r['Name'])[:110]))
 
 
 if __name__ == '__main__':
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 1)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 0)
