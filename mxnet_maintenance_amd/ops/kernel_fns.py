@@ -329,6 +329,37 @@ def _dgrad_default(w, stride):
     return 'hip' if C >= 128 and C % 64 == 0 else 'miopen'
 
 
+def _wgrad_candidates(dy, x, w, stride, pad):
+    c = [('miopen', lambda: _conv_bwd_torch(dy, x, w, stride, pad, (False, True))[1])]
+    K, R, S, C = w.shape
+    if R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0):
+        P = dy.numel() // K
+        for chunks in (16, 64):
+            if P % chunks == 0 and P // chunks >= 1024:
+                def splitk(chunks=chunks):
+                    # split-K batched GEMM (hipBLASLt): [chunks, K, P/chunks] x [chunks, P/chunks, C], fp32 sum
+                    d3 = dy.reshape(chunks, P // chunks, K).transpose(1, 2)
+                    x3 = x.reshape(chunks, P // chunks, C)
+                    return _bmm_f32(d3, x3).sum(0).to(w.dtype).view(K, 1, 1, C)
+                c.append(('splitk%d' % chunks, splitk))
+    return c
+
+
+_BMM_OUT_DTYPE = [None]
+
+
+def _bmm_f32(a, b):
+    """Batched GEMM with fp32 output (fp32 accumulation kept for the split-K sum)."""
+    if _BMM_OUT_DTYPE[0] is not False:
+        try:
+            r = torch.bmm(a, b, out_dtype=torch.float32)
+            _BMM_OUT_DTYPE[0] = True
+            return r
+        except (RuntimeError, TypeError):
+            _BMM_OUT_DTYPE[0] = False
+    return torch.bmm(a, b).float()
+
+
 class ConvNHWC(torch.autograd.Function):
     """2-D NHWC convolution with per-shape algorithm selection (HIP MFMA kernel / hipBLASLt / MIOpen)."""
 
@@ -351,7 +382,8 @@ class ConvNHWC(torch.autograd.Function):
             key = ('dgrad', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype)
             dx = _select(key, _dgrad_candidates(dy, x, w, stride, pad), _dgrad_default(w, stride))
         if ctx.needs_input_grad[1]:
-            dw = _conv_bwd_torch(dy, x, w, stride, pad, (False, True))[1]
+            key = ('wgrad', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype)
+            dw = _select(key, _wgrad_candidates(dy, x, w, stride, pad), 'miopen')
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum(dim=(0, 1, 2))
         return dx, dw, db, None, None, None
