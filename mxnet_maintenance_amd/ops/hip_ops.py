@@ -156,6 +156,9 @@ def pool(data, pool_type, kernel, stride, pad, convention, count_include_pad, ch
         return _K.PoolNHWC.apply(data, pool_type, tuple(kernel), tuple(stride), tuple(pad),
                                  convention == 'full', bool(count_include_pad))
     x = _nd_to_ncx(data) if channel_last else data
+    if channel_last and x.is_cuda and pool_type != 'max':
+        # torch's channels_last avg-pool backward is wrong on ROCm (see tests/test_hip_kernels.py)
+        x = x.contiguous()
     ceil = convention == 'full'
     pad_r = list(pad)
     if convention == 'same':
