@@ -46,6 +46,7 @@ from . import model
 from . import module
 from . import module as mod
 from . import monitor
+from . import monitor as mon
 from . import profiler
 from . import runtime
 from . import test_utils

@@ -57,18 +57,35 @@ class GraphProgram:
         self.nslots = nslots
         self.name_to_slot = dict(zip(self.var_names, self.var_slots))
 
-    def run(self, feed):
-        """``feed``: dict var name -> torch tensor.  Returns output tensors."""
+    def run(self, feed, monitor=None, monitor_all=False):
+        """``feed``: dict var name -> torch tensor.  Returns output tensors.
+
+        ``monitor(name, tensor)`` is called for every operator output (and,
+        with ``monitor_all``, every operator input) — the engine-level monitor
+        callback of src/executor/graph_executor.cc (ExecuteMonCallback).
+        """
         vals = [None] * self.nslots
         for name, s in self.name_to_slot.items():
             vals[s] = feed.get(name)
-        for fn, ins, attrs, outs, _name, _op in self.steps:
-            r = fn(*[vals[i] for i in ins], **attrs)
+        for fn, ins, attrs, outs, name, opname in self.steps:
+            args = [vals[i] for i in ins]
+            if monitor is not None and monitor_all:
+                for j, a in enumerate(args):
+                    if a is not None:
+                        monitor('%s_input%d' % (name, j), a)
+            r = fn(*args, **attrs)
             if len(outs) == 1:
                 vals[outs[0]] = r[0] if isinstance(r, (tuple, list)) else r
             else:
                 for o, t in zip(outs, r):
                     vals[o] = t
+            if monitor is not None:
+                op = registry.get(opname)
+                onames = op.output_names or (['output'] if len(outs) == 1 else
+                                             ['output%d' % k for k in range(len(outs))])
+                for o, on in zip(outs, onames):
+                    if vals[o] is not None:
+                        monitor('%s_%s' % (name, on), vals[o])
         return [vals[s] for s in self.out_slots]
 
 
@@ -118,7 +135,8 @@ class Executor:
         self.outputs = []
         self._leaves = None
         self._out_tensors = None
-        self._monitor = None
+        self._monitor_cb = None
+        self._monitor_all = False
 
     @property
     def arg_dict(self):
@@ -160,15 +178,19 @@ class Executor:
         prev_train = _state.STATE.training
         _state.STATE.training = bool(is_train)
         try:
+            mon = None
+            if self._monitor_cb is not None:
+                cb = self._monitor_cb
+
+                def mon(name, t):
+                    cb(name, NDArray(t.detach()))
             with torch.set_grad_enabled(need_grad):
-                outs = self._prog.run(feed)
+                outs = self._prog.run(feed, mon, self._monitor_all)
         finally:
             _state.STATE.training = prev_train
         self._leaves = leaves
         self._out_tensors = outs
         self.outputs = [NDArray(o.detach()) for o in outs]
-        if self._monitor is not None:
-            self._monitor(self)
         return self.outputs
 
     def backward(self, out_grads=None, is_train=True):
@@ -203,7 +225,9 @@ class Executor:
         self._leaves = None
 
     def set_monitor_callback(self, callback, monitor_all=False):
+        """``callback(name, NDArray)`` for every operator output (inputs too with ``monitor_all``)."""
         self._monitor_cb = callback
+        self._monitor_all = monitor_all
 
     def copy_params_from(self, arg_params, aux_params=None, allow_extra_params=False):
         for name, array in arg_params.items():

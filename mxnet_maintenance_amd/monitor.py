@@ -1,1 +1,85 @@
-"""monitor (being implemented)."""
+"""Executor monitor (parity: python/mxnet/monitor.py).
+
+Installs a callback on executors that records a statistic (default: the
+L2 norm / sqrt(size)) of every operator output whose name matches
+``pattern`` every ``interval`` batches.
+"""
+import logging
+import re
+
+from . import ndarray as nd
+from .ndarray.ndarray import NDArray
+
+__all__ = ['Monitor']
+
+
+class Monitor:
+    def __init__(self, interval, stat_func=None, pattern='.*', sort=False, monitor_all=False):
+        if stat_func is None:
+            def asum_stat(x):
+                return nd.norm(x) / (x.size ** 0.5)
+            stat_func = asum_stat
+        self.stat_func = stat_func
+        self.interval = interval
+        self.activated = False
+        self.queue = []
+        self.step = 0
+        self.exes = []
+        self.re_prog = re.compile(pattern)
+        self.sort = sort
+        self.monitor_all = monitor_all
+
+        def stat_helper(name, array):
+            if not self.activated or not self.re_prog.match(name):
+                return
+            self.queue.append((self.step, name, self.stat_func(array)))
+        self.stat_helper = stat_helper
+
+    def install(self, exe):
+        exe.set_monitor_callback(self.stat_helper, self.monitor_all)
+        self.exes.append(exe)
+
+    def tic(self):
+        if self.step % self.interval == 0:
+            self.queue = []
+            self.activated = True
+        self.step += 1
+
+    def toc(self):
+        if not self.activated:
+            return []
+        for exe in self.exes:
+            for array in exe.arg_arrays:
+                array.wait_to_read()
+            for array in exe.aux_arrays:
+                array.wait_to_read()
+        for exe in self.exes:
+            for name, array in zip(exe._symbol.list_arguments(), exe.arg_arrays):
+                if self.re_prog.match(name):
+                    self.queue.append((self.step, name, self.stat_func(array)))
+            for name, array in zip(exe._symbol.list_auxiliary_states(), exe.aux_arrays):
+                if self.re_prog.match(name):
+                    self.queue.append((self.step, name, self.stat_func(array)))
+        self.activated = False
+        res = []
+        if self.sort:
+            self.queue.sort(key=lambda x: x[1])
+        for n, k, v_list in self.queue:
+            if isinstance(v_list, NDArray):
+                v_list = [v_list]
+            assert isinstance(v_list, list)
+            s = ''
+            for v in v_list:
+                assert isinstance(v, NDArray)
+                if v.shape == (1,) or v.shape == ():
+                    s += str(v.asscalar()) + '\t'
+                else:
+                    s += str(v.asnumpy()) + '\t'
+            res.append((n, k, s))
+        self.queue = []
+        return res
+
+    def toc_print(self):
+        res = self.toc()
+        for n, k, v in res:
+            logging.info('Batch: {:7d} {:30s} {:s}'.format(n, k, v))

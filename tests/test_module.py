@@ -1,0 +1,138 @@
+"""Module API, callbacks, monitor, checkpoints (parity: tests/python/unittest/test_module.py,
+test_model_parallel / test_callback style checks)."""
+import logging
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+import mxnet_maintenance_amd as mx
+from mxnet_maintenance_amd import nd
+
+
+def _mlp(nh=16, nout=4):
+    data = mx.sym.var('data')
+    fc1 = mx.sym.FullyConnected(data, num_hidden=nh, name='fc1')
+    act = mx.sym.Activation(fc1, act_type='relu', name='relu1')
+    fc2 = mx.sym.FullyConnected(act, num_hidden=nout, name='fc2')
+    return mx.sym.SoftmaxOutput(fc2, name='softmax')
+
+
+def _data(n=200, d=10, k=4, seed=0):
+    rng = np.random.RandomState(seed)
+    X = rng.randn(n, d).astype('float32')
+    y = (X @ rng.randn(d, k)).argmax(1).astype('float32')
+    return X, y
+
+
+def test_module_fit_score_predict_multi_context_and_checkpoint():
+    X, y = _data()
+    it = mx.io.NDArrayIter(X, y, batch_size=40, shuffle=True)
+    mod = mx.mod.Module(_mlp(), context=[mx.cpu(0), mx.cpu(1)])
+    with tempfile.TemporaryDirectory() as d:
+        prefix = os.path.join(d, 'mlp')
+        mod.fit(it, num_epoch=10, optimizer='sgd', optimizer_params={'learning_rate': 0.5, 'momentum': 0.9},
+                epoch_end_callback=mx.callback.do_checkpoint(prefix),
+                batch_end_callback=[mx.callback.Speedometer(40, 2), mx.callback.ProgressBar(5)])
+        acc = dict(mod.score(mx.io.NDArrayIter(X, y, batch_size=40), 'acc'))['accuracy']
+        assert acc > 0.85
+        assert os.path.exists(prefix + '-symbol.json') and os.path.exists(prefix + '-0010.params')
+        sym, args, auxs = mx.model.load_checkpoint(prefix, 10)
+        assert 'fc1_weight' in args
+        m2 = mx.mod.Module.load(prefix, 10)
+        m2.bind([('data', (40, 10))], [('softmax_label', (40,))], for_training=False)
+        acc2 = dict(m2.score(mx.io.NDArrayIter(X, y, batch_size=40), 'acc'))['accuracy']
+        assert acc2 == pytest.approx(acc)
+        mod.save_checkpoint(prefix, 11, save_optimizer_states=True)
+        m3 = mx.mod.Module.load(prefix, 11, load_optimizer_states=True)
+        m3.bind([('data', (40, 10))], [('softmax_label', (40,))])
+        m3.init_optimizer(optimizer='sgd', optimizer_params={'learning_rate': 0.5, 'momentum': 0.9})
+    pred = mod.predict(mx.io.NDArrayIter(X, y, batch_size=40))
+    assert pred.shape == (200, 4)
+    np.testing.assert_allclose(pred.asnumpy().sum(1), 1, rtol=1e-5)
+
+
+def test_module_forward_backward_input_grads_and_reshape():
+    mod = mx.mod.Module(_mlp(), context=mx.cpu())
+    mod.bind([('data', (8, 10))], [('softmax_label', (8,))], inputs_need_grad=True)
+    mod.init_params(mx.init.Xavier())
+    mod.init_optimizer(optimizer='adam')
+    X, y = _data(8)
+    batch = mx.io.DataBatch([nd.array(X)], [nd.array(y)])
+    mod.forward_backward(batch)
+    g = mod.get_input_grads()[0]
+    assert g.shape == (8, 10) and float(nd.abs(g).sum().asscalar()) > 0
+    mod.update()
+    # new batch size triggers a reshape and keeps the parameters
+    before = mod.get_params()[0]['fc1_weight'].asnumpy().copy()
+    X2, y2 = _data(5)
+    mod.forward(mx.io.DataBatch([nd.array(X2)], [nd.array(y2)]), is_train=False)
+    assert mod.get_outputs()[0].shape == (5, 4)
+    np.testing.assert_allclose(mod.get_params()[0]['fc1_weight'].asnumpy(), before)
+
+
+def test_bucketing_module_shares_params():
+    def sym_gen(seq_len):
+        data = mx.sym.var('data')
+        w = mx.sym.var('shared_weight')
+        fc = mx.sym.FullyConnected(mx.sym.reshape(data, shape=(-1, seq_len * 3)), weight=w, num_hidden=4,
+                                   no_bias=True, name='fc') if False else None
+        emb = mx.sym.FullyConnected(data, weight=w, num_hidden=4, no_bias=True, flatten=False, name='fc')
+        pooled = mx.sym.mean(emb, axis=1)
+        return mx.sym.SoftmaxOutput(pooled, name='softmax'), ('data',), ('softmax_label',)
+    mod = mx.mod.BucketingModule(sym_gen, default_bucket_key=5, context=mx.cpu())
+    mod.bind([('data', (4, 5, 3))], [('softmax_label', (4,))])
+    mod.init_params()
+    mod.init_optimizer(optimizer_params={'learning_rate': 0.1})
+    for key in (5, 3, 7, 3):
+        b = mx.io.DataBatch([nd.ones((4, key, 3))], [nd.zeros((4,))], bucket_key=key,
+                            provide_data=[mx.io.DataDesc('data', (4, key, 3))],
+                            provide_label=[mx.io.DataDesc('softmax_label', (4,))])
+        mod.forward_backward(b)
+        mod.update()
+    w_default = mod._buckets[5]._exec_group.execs[0].arg_dict['shared_weight']
+    w_other = mod._buckets[3]._exec_group.execs[0].arg_dict['shared_weight']
+    assert w_default is w_other
+    assert len(mod._buckets) == 3
+
+
+def test_sequential_and_python_loss_module():
+    X, y = _data(64)
+    net1 = mx.sym.FullyConnected(mx.sym.var('data'), num_hidden=16, name='l1')
+    net1 = mx.sym.Activation(net1, act_type='relu')
+    net2 = mx.sym.FullyConnected(mx.sym.var('data'), num_hidden=4, name='l2')
+    net2 = mx.sym.SoftmaxOutput(net2, name='softmax')
+    seq = mx.mod.SequentialModule()
+    seq.add(mx.mod.Module(net1, label_names=None)).add(mx.mod.Module(net2), take_labels=True, auto_wiring=True)
+    it = mx.io.NDArrayIter(X, y, batch_size=16)
+    seq.fit(it, num_epoch=5, optimizer_params={'learning_rate': 0.3})
+    acc = dict(seq.score(it, 'acc'))['accuracy']
+    assert acc > 0.5
+    loss = mx.mod.PythonLossModule(grad_func=lambda s, l: s - nd.one_hot(l, 4))
+    loss.bind([('data', (16, 4))], [('softmax_label', (16,))])
+    loss.forward(mx.io.DataBatch([nd.ones((16, 4))], [nd.zeros((16,))]), is_train=True)
+    loss.backward()
+    assert loss.get_input_grads()[0].shape == (16, 4)
+
+
+def test_monitor_collects_stats():
+    mod = mx.mod.Module(_mlp(), context=mx.cpu())
+    mod.bind([('data', (4, 10))], [('softmax_label', (4,))])
+    mod.init_params()
+    mon = mx.mon.Monitor(1, pattern='fc.*')
+    mod.install_monitor(mon)
+    mon.tic()
+    mod.forward(mx.io.DataBatch([nd.ones((4, 10))], [nd.zeros((4,))]), is_train=False)
+    res = mon.toc()
+    names = {r[1] for r in res}
+    assert 'fc1_output' in names and 'fc1_weight' in names
+
+
+def test_feedforward_legacy_api():
+    X, y = _data(120)
+    model = mx.model.FeedForward(_mlp(), num_epoch=6, numpy_batch_size=30, learning_rate=0.5, momentum=0.9)
+    model.fit(X, y)
+    p = model.predict(X)
+    assert p.shape == (120, 4)
+    assert model.score(mx.io.NDArrayIter(X, y, batch_size=30)) > 0.7
