@@ -21,3 +21,16 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if 'gpu' in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _seed_everything():
+    """Every test starts from the same RNG state (numpy, python, torch via mx.random.seed),
+    like the reference's @with_seed() decorator (tests/python/unittest/common.py)."""
+    import random
+    import numpy as np
+    random.seed(1234)
+    np.random.seed(1234)
+    import mxnet_maintenance_amd as mx
+    mx.random.seed(1234)
+    yield

@@ -98,6 +98,7 @@ def test_bucketing_module_shares_params():
 
 
 def test_sequential_and_python_loss_module():
+    mx.random.seed(3)
     X, y = _data(64)
     net1 = mx.sym.FullyConnected(mx.sym.var('data'), num_hidden=16, name='l1')
     net1 = mx.sym.Activation(net1, act_type='relu')
@@ -106,9 +107,9 @@ def test_sequential_and_python_loss_module():
     seq = mx.mod.SequentialModule()
     seq.add(mx.mod.Module(net1, label_names=None)).add(mx.mod.Module(net2), take_labels=True, auto_wiring=True)
     it = mx.io.NDArrayIter(X, y, batch_size=16)
-    seq.fit(it, num_epoch=5, optimizer_params={'learning_rate': 0.3})
+    seq.fit(it, num_epoch=15, initializer=mx.init.Xavier(), optimizer_params={'learning_rate': 0.3})
     acc = dict(seq.score(it, 'acc'))['accuracy']
-    assert acc > 0.5
+    assert acc > 0.7
     loss = mx.mod.PythonLossModule(grad_func=lambda s, l: s - nd.one_hot(l, 4))
     loss.bind([('data', (16, 4))], [('softmax_label', (16,))])
     loss.forward(mx.io.DataBatch([nd.ones((16, 4))], [nd.zeros((16,))]), is_train=True)
