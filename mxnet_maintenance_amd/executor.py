@@ -14,6 +14,7 @@ import numpy as np
 import torch
 
 from . import _state
+from . import profiler as _profiler
 from .base import MXNetError
 from .ops import registry
 
@@ -73,7 +74,11 @@ class GraphProgram:
                 for j, a in enumerate(args):
                     if a is not None:
                         monitor('%s_input%d' % (name, j), a)
-            r = fn(*args, **attrs)
+            if _profiler.active_symbolic:
+                with _profiler.op_span(_profiler.current_scope() + opname, symbolic=True):
+                    r = fn(*args, **attrs)
+            else:
+                r = fn(*args, **attrs)
             if len(outs) == 1:
                 vals[outs[0]] = r[0] if isinstance(r, (tuple, list)) else r
             else:

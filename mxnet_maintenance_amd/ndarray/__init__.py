@@ -19,3 +19,13 @@ for _name, _fn in op.__dict__.items():
     if not _name.startswith('__') and _name not in _g and callable(_fn):
         _g[_name] = _fn
 del _g
+
+
+def __getattr__(name):
+    # operators registered after import (mx.operator 'Custom', user ops) resolve lazily
+    from ..ops import registry as _registry
+    if _registry.has(name):
+        fn = _register.make_op_function(name)
+        globals()[name] = fn
+        return fn
+    raise AttributeError("module 'mxnet_maintenance_amd.ndarray' has no attribute '%s'" % name)

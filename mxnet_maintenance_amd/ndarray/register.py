@@ -8,6 +8,7 @@ runs the op's torch-level implementation under the right autograd mode.
 import torch
 
 from .. import _state
+from .. import profiler as _profiler
 from ..base import MXNetError
 from ..ops import registry
 from .ndarray import NDArray
@@ -85,7 +86,11 @@ def invoke(op, inputs, attrs, out=None):
     """Run ``op`` on NDArray ``inputs`` with parsed ``attrs``."""
     tin = [None if x is None else x._data for x in inputs]
     _note_leaves(inputs)
-    res = _run(op.fn, tin, attrs)
+    if _profiler.active_imperative:
+        with _profiler.op_span(_profiler.current_scope() + op.name):
+            res = _run(op.fn, tin, attrs)
+    else:
+        res = _run(op.fn, tin, attrs)
     nvis = op.get_num_visible_outputs(attrs)
     if isinstance(res, (tuple, list)):
         outs = [NDArray(r) for r in res[:nvis]]

@@ -1,1 +1,238 @@
-"""operator (being implemented)."""
+"""User-defined operators in Python (parity: python/mxnet/operator.py, src/operator/custom/custom.cc).
+
+::
+
+    class Sigmoid(mx.operator.CustomOp):
+        def forward(self, is_train, req, in_data, out_data, aux):
+            self.assign(out_data[0], req[0], 1 / (1 + mx.nd.exp(-in_data[0])))
+        def backward(self, req, out_grad, in_data, out_data, in_grad, aux):
+            y = out_data[0]
+            self.assign(in_grad[0], req[0], out_grad[0] * y * (1 - y))
+
+    @mx.operator.register('sigmoid')
+    class SigmoidProp(mx.operator.CustomOpProp):
+        def create_operator(self, ctx, shapes, dtypes):
+            return Sigmoid()
+
+    y = mx.nd.Custom(x, op_type='sigmoid')      # or mx.sym.Custom(...)
+
+The ``Custom`` operator is registered like any other op, so it works
+imperatively (with autograd), symbolically (infer_shape via the prop's
+``infer_shape``) and inside hybridized blocks.
+"""
+import torch
+
+from . import _state
+from .base import MXNetError
+from .ops import registry
+
+__all__ = ['CustomOp', 'CustomOpProp', 'register', 'get_all_registered_operators', 'NDArrayOp', 'NumpyOp',
+           'PythonOp']
+
+_REGISTRY = {}
+
+
+class CustomOp:
+    """Base class for the computation of a custom operator."""
+
+    def forward(self, is_train, req, in_data, out_data, aux):
+        raise NotImplementedError
+
+    def backward(self, req, out_grad, in_data, out_data, in_grad, aux):
+        raise NotImplementedError
+
+    def assign(self, dst, req, src):
+        """Write ``src`` into ``dst`` according to ``req`` (null / write / inplace / add)."""
+        if req == 'null':
+            return
+        if req in ('write', 'inplace'):
+            dst[:] = src
+        elif req == 'add':
+            dst[:] = dst + src
+
+
+class CustomOpProp:
+    """Describes a custom operator: arguments, outputs, shape/type inference and the op factory."""
+
+    def __init__(self, need_top_grad=True):
+        self.need_top_grad_ = need_top_grad
+
+    def infer_shape(self, in_shape):
+        return in_shape, (in_shape[0],) * len(self.list_outputs()), ()
+
+    def infer_type(self, in_type):
+        return in_type, [in_type[0]] * len(self.list_outputs()), [in_type[0]] * len(self.list_auxiliary_states())
+
+    def infer_storage_type(self, in_stype):
+        return in_stype, ['default'] * len(self.list_outputs()), ['default'] * len(self.list_auxiliary_states())
+
+    def infer_storage_type_backward(self, ograd_stype, in_stype, out_stype, igrad_stype, aux_stype):
+        return (ograd_stype, in_stype, out_stype, ['default'] * len(igrad_stype),
+                ['default'] * len(aux_stype))
+
+    def list_outputs(self):
+        return ['output']
+
+    def list_arguments(self):
+        return ['data']
+
+    def list_auxiliary_states(self):
+        return []
+
+    def declare_backward_dependency(self, out_grad, in_data, out_data):
+        deps = []
+        if self.need_top_grad_:
+            deps.extend(out_grad)
+        deps.extend(in_data)
+        deps.extend(out_data)
+        return deps
+
+    def create_operator(self, ctx, in_shapes, in_dtypes):
+        return CustomOp()
+
+
+def register(reg_name):
+    """Class decorator registering a CustomOpProp subclass under ``reg_name``."""
+    def do_register(prop_cls):
+        _REGISTRY[reg_name] = prop_cls
+        return prop_cls
+    return do_register
+
+
+def get_all_registered_operators():
+    return list(_REGISTRY)
+
+
+def _make_prop(attrs):
+    op_type = attrs.get('op_type')
+    if op_type not in _REGISTRY:
+        raise MXNetError('Custom operator %s is not registered' % op_type)
+    kw = {k: (v if isinstance(v, str) else str(v)) for k, v in attrs.items() if k != 'op_type'
+          and not (k.startswith('__') and k.endswith('__'))}
+    return _REGISTRY[op_type](**kw)
+
+
+def _custom_args(attrs):
+    return _make_prop(attrs).list_arguments()
+
+
+def _custom_aux(attrs):
+    return _make_prop(attrs).list_auxiliary_states()
+
+
+def _custom_nout(attrs):
+    return len(_make_prop(attrs).list_outputs())
+
+
+def _custom_infer(in_shapes, attrs):
+    prop = _make_prop(attrs)
+    if any(s is None for s in in_shapes[:1]):
+        return {}
+    n_args = len(prop.list_arguments())
+    shapes = [list(s) if s is not None else None for s in in_shapes[:n_args]]
+    try:
+        ins, _, auxs = prop.infer_shape(shapes)
+    except Exception:
+        return {}
+    res = {i: tuple(s) for i, s in enumerate(ins) if s is not None}
+    res.update({n_args + i: tuple(s) for i, s in enumerate(auxs)})
+    return res
+
+
+class _CustomFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, op, prop, n_in, is_train, *tensors):
+        from .ndarray.ndarray import NDArray
+        ins = [NDArray(t.detach()) for t in tensors[:n_in]]
+        aux = [NDArray(t) for t in tensors[n_in:]]
+        in_shapes = [list(t.shape) for t in tensors[:n_in]]
+        _, out_shapes, _ = prop.infer_shape(in_shapes)
+        in_types = [t.dtype for t in tensors[:n_in]]
+        outs = [NDArray(torch.zeros(tuple(s), dtype=in_types[0], device=tensors[0].device)) for s in out_shapes]
+        with torch.no_grad():
+            op.forward(is_train=is_train, req=['write'] * len(outs), in_data=ins, out_data=outs, aux=aux)
+        ctx.op, ctx.n_in = op, n_in
+        ctx.save_for_backward(*tensors)
+        ctx.outs = [o._data for o in outs]
+        return tuple(o._data for o in outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        from .ndarray.ndarray import NDArray
+        tensors = ctx.saved_tensors
+        n_in = ctx.n_in
+        ins = [NDArray(t) for t in tensors[:n_in]]
+        aux = [NDArray(t) for t in tensors[n_in:]]
+        outs = [NDArray(t) for t in ctx.outs]
+        ograds = [NDArray(g if g is not None else torch.zeros_like(o)) for g, o in zip(grads, ctx.outs)]
+        igrads = [NDArray(torch.zeros_like(t)) for t in tensors[:n_in]]
+        with torch.no_grad():
+            ctx.op.backward(req=['write'] * n_in, out_grad=ograds, in_data=ins, out_data=outs, in_grad=igrads,
+                            aux=aux)
+        return (None, None, None, None) + tuple(g._data for g in igrads) + (None,) * (len(tensors) - n_in)
+
+
+_OP_CACHE = {}
+
+
+def _custom_fn(*inputs, op_type=None, **kwargs):
+    attrs = dict(kwargs, op_type=op_type)
+    prop = _make_prop(attrs)
+    n_in = len(prop.list_arguments())
+    tensors = [t for t in inputs if t is not None]
+    if tensors and tensors[0].device.type == 'meta':
+        _, out_shapes, _ = prop.infer_shape([list(t.shape) for t in tensors[:n_in]])
+        outs = [torch.empty(tuple(s), dtype=tensors[0].dtype, device='meta') for s in out_shapes]
+        return outs[0] if len(outs) == 1 else tuple(outs)
+    from .context import context_from_torch
+    key = (op_type, tuple(sorted((k, str(v)) for k, v in kwargs.items())),
+           tuple(tuple(t.shape) for t in tensors), tuple(str(t.dtype) for t in tensors), str(tensors[0].device))
+    op = _OP_CACHE.get(key)
+    if op is None:
+        op = prop.create_operator(context_from_torch(tensors[0].device), [list(t.shape) for t in tensors[:n_in]],
+                                  [t.dtype for t in tensors[:n_in]])
+        _OP_CACHE[key] = op
+    outs = _CustomFunction.apply(op, prop, n_in, bool(_state.STATE.training), *tensors)
+    return outs[0] if len(outs) == 1 else tuple(outs)
+
+
+registry.register('Custom', _custom_fn, arg_names=_custom_args, aux_names=_custom_aux, num_outputs=_custom_nout,
+                  infer_params=_custom_infer, params={'op_type': ('str', None)}, extra_params=True)
+
+
+# ---------------------------------------------------------------------------
+# deprecated numpy/ndarray op front-ends of the reference (NumpyOp / NDArrayOp):
+# kept as thin CustomOp adapters so old code keeps running.
+# ---------------------------------------------------------------------------
+
+class PythonOp:
+    def __init__(self, need_top_grad=True):
+        self.need_top_grad_ = need_top_grad
+
+    def list_outputs(self):
+        return ['output']
+
+    def list_arguments(self):
+        return ['data']
+
+    def infer_shape(self, in_shape):
+        return in_shape, [in_shape[0]]
+
+    def need_top_grad(self):
+        return self.need_top_grad_
+
+
+class NDArrayOp(PythonOp):
+    def forward(self, in_data, out_data):
+        raise NotImplementedError
+
+    def backward(self, out_grad, in_data, out_data, in_grad):
+        raise NotImplementedError
+
+
+class NumpyOp(PythonOp):
+    def forward(self, in_data, out_data):
+        raise NotImplementedError
+
+    def backward(self, out_grad, in_data, out_data, in_grad):
+        raise NotImplementedError

@@ -27,11 +27,11 @@ _OPS = {}
 class OpDef:
     __slots__ = ('name', 'fn', 'arg_names', 'aux_names', 'params', 'num_outputs',
                  'infer_params', 'key_var_num_args', 'doc', 'num_visible_outputs',
-                 'output_names')
+                 'output_names', 'extra_params')
 
     def __init__(self, name, fn, arg_names=('data',), aux_names=(), params=None,
                  num_outputs=1, infer_params=None, key_var_num_args=None, doc=None,
-                 num_visible_outputs=None, output_names=None):
+                 num_visible_outputs=None, output_names=None, extra_params=False):
         self.name = name
         self.fn = fn
         self.arg_names = arg_names
@@ -43,6 +43,7 @@ class OpDef:
         self.doc = doc
         self.num_visible_outputs = num_visible_outputs
         self.output_names = output_names
+        self.extra_params = extra_params   # keep undeclared attributes (Custom op kwargs)
 
     def get_arg_names(self, attrs):
         a = self.arg_names

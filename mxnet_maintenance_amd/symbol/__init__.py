@@ -11,3 +11,13 @@ for _n in _registry.list_ops():
     if _n not in _g:
         _g[_n] = _op_func(_n)
 del _g
+
+
+def __getattr__(name):
+    # operators registered after import resolve lazily
+    from ..ops import registry as _registry
+    if _registry.has(name):
+        fn = _op_func(name)
+        globals()[name] = fn
+        return fn
+    raise AttributeError("module 'mxnet_maintenance_amd.symbol' has no attribute '%s'" % name)

@@ -50,7 +50,8 @@ class _Node:
     def parsed(self):
         if self._parsed is None:
             op = self.opdef()
-            params = {k: v for k, v in self.attrs.items() if k in op.params}
+            params = {k: v for k, v in self.attrs.items()
+                      if k in op.params or (op.extra_params and not (k.startswith('__') and k.endswith('__')))}
             self._parsed = op.parse_attrs(params)
         return self._parsed
 

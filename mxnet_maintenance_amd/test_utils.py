@@ -1,1 +1,840 @@
-"""test_utils (being implemented)."""
+"""Testing utilities (parity: python/mxnet/test_utils.py).
+
+Numerical comparison helpers, random array/shape generators, numeric
+(finite-difference) gradient checking, symbolic forward/backward checks,
+cross-context consistency checks, statistical generator checks and small
+data helpers (offline: MNIST is synthesised when the files are absent).
+"""
+import contextlib
+import functools
+import os
+import random as _pyrandom
+import sys
+from contextlib import contextmanager
+
+import numpy as np
+
+from . import ndarray as nd
+from . import symbol as sym_mod
+from .base import MXNetError
+from .context import Context, cpu, gpu, current_context
+from .ndarray.ndarray import NDArray
+
+_default_ctx = [None]
+
+
+def default_context():
+    """Context used by tests (MXNET_TEST_DEVICE=gpu selects the first GPU)."""
+    if _default_ctx[0] is not None:
+        return _default_ctx[0]
+    if os.environ.get('MXNET_TEST_DEVICE', 'cpu') == 'gpu':
+        return gpu(0)
+    return current_context()
+
+
+def set_default_context(ctx):
+    _default_ctx[0] = ctx
+
+
+def default_dtype():
+    return np.float32
+
+
+def default_rtols():
+    return {np.dtype(np.float16): 1e-2, np.dtype(np.float32): 1e-4, np.dtype(np.float64): 1e-5,
+            np.dtype(np.bool_): 0, np.dtype(np.int8): 0, np.dtype(np.uint8): 0, np.dtype(np.int32): 0,
+            np.dtype(np.int64): 0}
+
+
+def default_atols():
+    return {np.dtype(np.float16): 1e-1, np.dtype(np.float32): 1e-3, np.dtype(np.float64): 1e-20,
+            np.dtype(np.bool_): 0, np.dtype(np.int8): 0, np.dtype(np.uint8): 0, np.dtype(np.int32): 0,
+            np.dtype(np.int64): 0}
+
+
+def default_numeric_eps():
+    return {np.dtype(np.float16): 1.0 / 2 ** 6, np.dtype(np.float32): 1.0 / 2 ** 9,
+            np.dtype(np.float64): 1.0 / 2 ** 14}
+
+
+def _np(a):
+    if isinstance(a, NDArray):
+        return a.asnumpy()
+    return np.asarray(a)
+
+
+def effective_dtype(dat):
+    dt = _np(dat).dtype if not isinstance(dat, NDArray) else np.dtype(dat.dtype)
+    return dt
+
+
+def get_tolerance(dat, tol, default_tol):
+    if isinstance(tol, (float, int)):
+        return tol
+    dt = effective_dtype(dat)
+    if isinstance(tol, dict):
+        return tol.get(dt, default_tol.get(dt, 0))
+    return default_tol.get(dt, 1e-5)
+
+
+def get_tols(x, y, rtol, atol):
+    if isinstance(x, (int, float)):
+        x = np.array(x)
+    rtol = max(get_tolerance(x, rtol, default_rtols()), get_tolerance(y, rtol, default_rtols()))
+    atol = max(get_tolerance(x, atol, default_atols()), get_tolerance(y, atol, default_atols()))
+    return rtol, atol
+
+
+def get_atol(atol=None, dtype=np.dtype(np.float64)):
+    return default_atols().get(np.dtype(dtype), 1e-20) if atol is None else atol
+
+
+def get_rtol(rtol=None, dtype=np.dtype(np.float64)):
+    return default_rtols().get(np.dtype(dtype), 1e-5) if rtol is None else rtol
+
+
+def get_etol(etol=None):
+    return 0 if etol is None else etol
+
+
+def random_arrays(*shapes):
+    """Standard-normal float32 numpy arrays of the given shapes (scalars for ``()``)."""
+    arrays = [np.array(np.random.randn(), dtype=default_dtype()) if len(s) == 0 else
+              np.random.randn(*s).astype(default_dtype()) for s in shapes]
+    if len(arrays) == 1:
+        return arrays[0]
+    return arrays
+
+
+def random_uniform_arrays(*shapes, **kwargs):
+    low = kwargs.pop('low', 0.0)
+    high = kwargs.pop('high', 1.0)
+    dtype = kwargs.pop('dtype', default_dtype())
+    arrays = [np.random.uniform(low, high, size=s).astype(dtype) for s in shapes]
+    return arrays
+
+
+def random_sample(population, k):
+    population_copy = population[:]
+    np.random.shuffle(population_copy)
+    return population_copy[0:k]
+
+
+def rand_shape_2d(dim0=10, dim1=10, allow_zero_size=False):
+    low = 0 if allow_zero_size else 1
+    return np.random.randint(low, dim0 + 1), np.random.randint(low, dim1 + 1)
+
+
+def rand_shape_3d(dim0=10, dim1=10, dim2=10, allow_zero_size=False):
+    low = 0 if allow_zero_size else 1
+    return np.random.randint(low, dim0 + 1), np.random.randint(low, dim1 + 1), np.random.randint(low, dim2 + 1)
+
+
+def rand_shape_nd(num_dim, dim=10, allow_zero_size=False):
+    low = 0 if allow_zero_size else 1
+    return tuple(np.random.randint(low, dim + 1, size=num_dim))
+
+
+def rand_coord_2d(x_low, x_high, y_low, y_high):
+    return _pyrandom.randint(x_low, x_high), _pyrandom.randint(y_low, y_high)
+
+
+def rand_sparse_ndarray(shape, stype, density=None, dtype=None, distribution=None, data_init=None,
+                        rsp_indices=None, modifier_func=None, shuffle_csr_indices=False, ctx=None):
+    density = np.random.rand() if density is None else density
+    dtype = default_dtype() if dtype is None else dtype
+    dense = np.random.uniform(-1, 1, size=shape).astype(dtype)
+    mask = np.random.rand(*shape) < density
+    if stype == 'row_sparse':
+        if rsp_indices is not None:
+            rows = np.zeros(shape[0], dtype=bool)
+            rows[np.asarray(rsp_indices, dtype=np.int64)] = True
+        else:
+            rows = np.random.rand(shape[0]) < density
+        mask = np.broadcast_to(rows.reshape((-1,) + (1,) * (len(shape) - 1)), shape)
+    arr = np.where(mask, dense if data_init is None else np.full(shape, data_init, dtype), 0).astype(dtype)
+    if modifier_func is not None:
+        arr = np.vectorize(modifier_func)(arr).astype(dtype)
+    res = nd.array(arr, ctx=ctx, dtype=dtype).tostype(stype)
+    return res, (arr,)
+
+
+def rand_ndarray(shape, stype='default', density=None, dtype=None, modifier_func=None,
+                 shuffle_csr_indices=False, distribution=None, ctx=None):
+    ctx = ctx or default_context()
+    if stype == 'default':
+        arr = np.random.uniform(-1, 1, size=shape).astype(dtype or default_dtype())
+        return nd.array(arr if modifier_func is None else np.vectorize(modifier_func)(arr), ctx=ctx,
+                        dtype=dtype or default_dtype())
+    return rand_sparse_ndarray(shape, stype, density=density, dtype=dtype, modifier_func=modifier_func,
+                               ctx=ctx)[0]
+
+
+def create_sparse_array(shape, stype, data_init=None, rsp_indices=None, dtype=None, modifier_func=None,
+                        density=.5, shuffle_csr_indices=False):
+    return rand_sparse_ndarray(shape, stype, density=density, dtype=dtype, data_init=data_init,
+                               rsp_indices=rsp_indices, modifier_func=modifier_func)[0]
+
+
+def np_reduce(dat, axis, keepdims, numpy_reduce_func):
+    if isinstance(axis, int):
+        axis = [axis]
+    else:
+        axis = list(axis) if axis is not None else range(len(dat.shape))
+    ret = dat
+    for i in reversed(sorted(axis)):
+        ret = numpy_reduce_func(ret, axis=i)
+    if keepdims:
+        keepdims_shape = list(dat.shape)
+        for i in axis:
+            keepdims_shape[i] = 1
+        ret = ret.reshape(tuple(keepdims_shape))
+    return ret
+
+
+def _find_max_violation(a, b, rtol, atol):
+    diff = np.abs(a - b)
+    tol = atol + rtol * np.abs(b)
+    violation = diff / (tol + 1e-20)
+    loc = np.argmax(violation)
+    idx = np.unravel_index(loc, violation.shape)
+    return idx, np.max(violation)
+
+
+def same(a, b):
+    return np.array_equal(_np(a), _np(b))
+
+
+def checkShapes(a, b):
+    if a.shape != b.shape:
+        msg = 'Shape mismatch: %s vs %s' % (str(a.shape), str(b.shape))
+        raise AssertionError(msg)
+
+
+def almost_equal(a, b, rtol=None, atol=None, equal_nan=False, use_broadcast=True):
+    a, b = _np(a), _np(b)
+    rtol, atol = get_tols(a, b, rtol, atol)
+    if not use_broadcast:
+        checkShapes(a, b)
+    return np.allclose(a, b, rtol=rtol, atol=atol, equal_nan=equal_nan)
+
+
+def locationError(a, b, index, names, maxError=False):
+    return 'Error %f exceeds tolerance rtol=%f, atol=%f (mismatch at %s). Location of maximum error: %s, ' \
+           '%s=%f, %s=%f' % (0, 0, 0, index, str(index), names[0], a[index], names[1], b[index])
+
+
+def assert_almost_equal(a, b, rtol=None, atol=None, names=('a', 'b'), equal_nan=False, use_broadcast=True,
+                        mismatches=(10, 10)):
+    """Assert ``|a - b| <= atol + rtol*|b|`` elementwise, reporting the worst violation."""
+    a, b = _np(a), _np(b)
+    rtol, atol = get_tols(a, b, rtol, atol)
+    if not use_broadcast:
+        checkShapes(a, b)
+    a64 = a.astype(np.float64) if a.dtype.kind in 'fiub' else a
+    b64 = b.astype(np.float64) if b.dtype.kind in 'fiub' else b
+    if np.allclose(a64, b64, rtol=rtol, atol=atol, equal_nan=equal_nan):
+        return
+    a64, b64 = np.broadcast_arrays(a64, b64)
+    index, rel = _find_max_violation(a64, b64, rtol, atol)
+    raise AssertionError('\nError %f exceeds tolerance rtol=%e, atol=%e.  Location of maximum error: %s, %s=%.8f, '
+                         '%s=%.8f' % (rel, rtol, atol, str(index), names[0], a64[index], names[1], b64[index]))
+
+
+def assert_allclose(a, b, rtol=1e-07, atol=0, equal_nan=True):
+    assert_almost_equal(a, b, rtol=rtol, atol=atol, equal_nan=equal_nan)
+
+
+def assert_almost_equal_with_err(a, b, rtol=None, atol=None, etol=None, names=('a', 'b'), equal_nan=False,
+                                 mismatches=(10, 10)):
+    etol = get_etol(etol)
+    if etol > 0:
+        a, b = _np(a), _np(b)
+        rtol, atol = get_tols(a, b, rtol, atol)
+        bad = ~np.isclose(a, b, rtol=rtol, atol=atol, equal_nan=equal_nan)
+        if bad.mean() > etol:
+            raise AssertionError('error rate %f exceeds etol %f' % (bad.mean(), etol))
+    else:
+        assert_almost_equal(a, b, rtol, atol, names, equal_nan)
+
+
+def assert_almost_equal_ignore_nan(a, b, rtol=None, atol=None, names=('a', 'b')):
+    a = np.copy(_np(a))
+    b = np.copy(_np(b))
+    nan_mask = np.logical_or(np.isnan(a), np.isnan(b))
+    a[nan_mask] = 0
+    b[nan_mask] = 0
+    assert_almost_equal(a, b, rtol, atol, names)
+
+
+def assert_exception(f, exception_type, *args, **kwargs):
+    try:
+        f(*args, **kwargs)
+        assert False
+    except exception_type:
+        return
+
+
+def retry(n):
+    """Decorator: retry a (stochastic) test up to ``n`` times."""
+    assert n > 0
+
+    def decorate(f):
+        @functools.wraps(f)
+        def wrapper(*args, **kwargs):
+            err = None
+            for _ in range(n):
+                try:
+                    return f(*args, **kwargs)
+                except AssertionError as e:
+                    err = e
+            raise err
+        return wrapper
+    return decorate
+
+
+def simple_forward(sym, ctx=None, is_train=False, **inputs):
+    ctx = ctx or default_context()
+    inputs = {k: nd.array(v) if not isinstance(v, NDArray) else v for k, v in inputs.items()}
+    exe = sym.bind(ctx, args=inputs)
+    exe.forward(is_train=is_train)
+    outputs = [x.asnumpy() for x in exe.outputs]
+    if len(outputs) == 1:
+        outputs = outputs[0]
+    return outputs
+
+
+def _parse_location(sym, location, ctx, dtype=default_dtype()):
+    if isinstance(location, dict):
+        if set(location.keys()) != set(sym.list_arguments()):
+            raise ValueError('Symbol arguments and keys of the given location do not match. symbol args:%s, '
+                             'location.keys():%s' % (str(set(sym.list_arguments())), str(set(location.keys()))))
+    else:
+        location = {k: v for k, v in zip(sym.list_arguments(), location)}
+    return {k: v.as_in_context(ctx) if isinstance(v, NDArray) else nd.array(v, ctx=ctx, dtype=v.dtype
+                                                                               if hasattr(v, 'dtype') else dtype)
+            for k, v in location.items()}
+
+
+def _parse_aux_states(sym, aux_states, ctx, dtype=default_dtype()):
+    if aux_states is None:
+        return None
+    if isinstance(aux_states, dict):
+        if set(aux_states.keys()) != set(sym.list_auxiliary_states()):
+            raise ValueError('Symbol aux_states names and given aux_states do not match.')
+    elif isinstance(aux_states, (list, tuple)):
+        aux_states = {k: v for k, v in zip(sym.list_auxiliary_states(), aux_states)}
+    return {k: nd.array(v, ctx=ctx, dtype=dtype) if not isinstance(v, NDArray) else v.as_in_context(ctx)
+            for k, v in aux_states.items()}
+
+
+def numeric_grad(executor, location, aux_states=None, eps=1e-4, use_forward_train=True, dtype=default_dtype()):
+    """Central finite differences of sum(outputs) w.r.t. every input in ``location``."""
+    def as_stype(v):
+        return v
+    approx_grads = {k: np.zeros(v.shape, dtype=dtype) for k, v in location.items()}
+    for k, v in location.items():
+        executor.arg_dict[k][:] = v
+    if aux_states is not None:
+        for k, v in aux_states.items():
+            executor.aux_dict[k][:] = v
+    for k, v in location.items():
+        old_value = _np(v).astype(np.float64).copy()
+        flat = old_value.reshape(-1)
+        for i in range(flat.size):
+            orig = flat[i]
+            flat[i] = orig + eps / 2.0
+            executor.arg_dict[k][:] = nd.array(old_value.astype(dtype))
+            if aux_states is not None:
+                for key, val in aux_states.items():
+                    executor.aux_dict[key][:] = val
+            executor.forward(is_train=use_forward_train)
+            f_peps = sum(float(o.asnumpy().astype(np.float64).sum()) for o in executor.outputs)
+            flat[i] = orig - eps / 2.0
+            executor.arg_dict[k][:] = nd.array(old_value.astype(dtype))
+            if aux_states is not None:
+                for key, val in aux_states.items():
+                    executor.aux_dict[key][:] = val
+            executor.forward(is_train=use_forward_train)
+            f_neps = sum(float(o.asnumpy().astype(np.float64).sum()) for o in executor.outputs)
+            approx_grads[k].reshape(-1)[i] = (f_peps - f_neps) / eps
+            flat[i] = orig
+        executor.arg_dict[k][:] = nd.array(old_value.astype(dtype))
+    return approx_grads
+
+
+def check_numeric_gradient(sym, location, aux_states=None, numeric_eps=None, rtol=None, atol=None,
+                           grad_nodes=None, use_forward_train=True, ctx=None, grad_stype_dict=None,
+                           dtype=default_dtype()):
+    """Compare the symbol's backward against finite differences of sum(outputs * random projection)."""
+    ctx = ctx or default_context()
+    eps = numeric_eps if numeric_eps is not None else default_numeric_eps()[np.dtype(dtype)]
+    rtol = 1e-2 if rtol is None else rtol
+    atol = 1e-4 if atol is None else atol
+    location = _parse_location(sym, location, ctx, dtype)
+    location_npy = {k: v.asnumpy() for k, v in location.items()}
+    aux_states = _parse_aux_states(sym, aux_states, ctx, dtype)
+    aux_npy = {k: v.asnumpy() for k, v in aux_states.items()} if aux_states is not None else None
+    if grad_nodes is None:
+        grad_nodes = sym.list_arguments()
+        grad_req = {k: 'write' for k in grad_nodes}
+    elif isinstance(grad_nodes, (list, tuple)):
+        grad_nodes = list(grad_nodes)
+        grad_req = {k: 'write' for k in grad_nodes}
+    elif isinstance(grad_nodes, dict):
+        grad_req = grad_nodes.copy()
+        grad_nodes = grad_nodes.keys()
+    else:
+        raise ValueError
+    input_shape = {k: v.shape for k, v in location.items()}
+    _, out_shape, _ = sym.infer_shape(**input_shape)
+    proj = sym_mod.var('__random_proj')
+    out = sym_mod.sum(sym * proj) if len(out_shape) == 1 else sym_mod.sum(sym_mod.Group(list(sym))[0] * proj)
+    out = sym_mod.make_loss(out)
+    location = dict(list(location.items()) + [('__random_proj', nd.array(np.random.normal(0, 0.01,
+                                                                                          size=out_shape[0]),
+                                                                         ctx=ctx, dtype=dtype))])
+    args_grad_npy = {k: np.random.normal(0, 0.01, size=location[k].shape) for k in grad_nodes}
+    args_grad_npy['__random_proj'] = np.random.normal(0, 0.01, size=out_shape[0])
+    args_grad = {k: nd.array(v, ctx=ctx, dtype=dtype) for k, v in args_grad_npy.items()}
+    grad_req['__random_proj'] = 'write'
+    executor = out.bind(ctx, args=location, args_grad=args_grad, grad_req=grad_req, aux_states=aux_states)
+    inps = executor.arg_arrays
+    if len(inps) != len(location):
+        raise ValueError('Executor arg_arrays and location len do not match.')
+    executor.forward(is_train=True)
+    executor.backward()
+    symbolic_grads = {k: executor.grad_dict[k].asnumpy() for k in grad_nodes}
+    numeric_gradients = numeric_grad(executor, {k: v for k, v in location_npy.items()} | {
+        '__random_proj': location['__random_proj'].asnumpy()}, aux_npy, eps=eps,
+        use_forward_train=use_forward_train, dtype=dtype)
+    for name in grad_nodes:
+        fd_grad = numeric_gradients[name]
+        orig_grad = args_grad_npy[name]
+        sym_grad = symbolic_grads[name]
+        if grad_req[name] == 'write':
+            assert_almost_equal(fd_grad, sym_grad, rtol, atol, ('NUMERICAL_%s' % name, 'BACKWARD_%s' % name))
+        elif grad_req[name] == 'add':
+            assert_almost_equal(fd_grad, sym_grad - orig_grad, rtol, atol,
+                                ('NUMERICAL_%s' % name, 'BACKWARD_%s' % name))
+        elif grad_req[name] == 'null':
+            assert_almost_equal(orig_grad, sym_grad, rtol, atol, ('NUMERICAL_%s' % name, 'BACKWARD_%s' % name))
+        else:
+            raise ValueError('Invalid grad_req %s for argument %s' % (grad_req[name], name))
+
+
+def check_symbolic_forward(sym, location, expected, rtol=None, atol=None, aux_states=None, ctx=None,
+                           equal_nan=False, dtype=default_dtype()):
+    ctx = ctx or default_context()
+    location = _parse_location(sym, location, ctx, dtype)
+    aux_states = _parse_aux_states(sym, aux_states, ctx, dtype)
+    if isinstance(expected, dict):
+        expected = [expected[k] for k in sym.list_outputs()]
+    args_grad_data = {k: nd.empty(v.shape, ctx=ctx, dtype=dtype) for k, v in location.items()}
+    executor = sym.bind(ctx=ctx, args=location, args_grad=args_grad_data, aux_states=aux_states)
+    for g in executor.grad_arrays:
+        if g is not None:
+            g[:] = 0
+    executor.forward(is_train=False)
+    outputs = [x.asnumpy() for x in executor.outputs]
+    for output_name, expect, output in zip(sym.list_outputs(), expected, outputs):
+        assert_almost_equal(expect, output, rtol, atol, ('EXPECTED_%s' % output_name, 'FORWARD_%s' % output_name),
+                            equal_nan=equal_nan)
+    return executor.outputs
+
+
+def check_symbolic_backward(sym, location, out_grads, expected, rtol=None, atol=None, aux_states=None,
+                            grad_req='write', ctx=None, grad_stypes=None, equal_nan=False, dtype=default_dtype()):
+    ctx = ctx or default_context()
+    location = _parse_location(sym, location, ctx, dtype)
+    aux_states = _parse_aux_states(sym, aux_states, ctx, dtype)
+    if isinstance(expected, (list, tuple)):
+        expected = {k: v for k, v in zip(sym.list_arguments(), expected)}
+    args_grad_npy = {k: np.random.normal(size=v.shape) for k, v in expected.items()}
+    args_grad_data = {k: nd.array(v, ctx=ctx, dtype=dtype) for k, v in args_grad_npy.items()}
+    if isinstance(grad_req, str):
+        grad_req = {k: grad_req for k in sym.list_arguments()}
+    elif isinstance(grad_req, (list, tuple)):
+        grad_req = {k: v for k, v in zip(sym.list_arguments(), grad_req)}
+    executor = sym.bind(ctx=ctx, args=location, args_grad=args_grad_data, aux_states=aux_states,
+                        grad_req=grad_req)
+    executor.forward(is_train=True)
+    if isinstance(out_grads, (tuple, list)):
+        outg = [nd.array(v, ctx=ctx, dtype=dtype) if not isinstance(v, NDArray) else v for v in out_grads]
+    elif isinstance(out_grads, dict):
+        outg = [nd.array(out_grads[k], ctx=ctx, dtype=dtype) for k in sym.list_outputs()]
+    else:
+        outg = out_grads
+    executor.backward(outg)
+    grads = {k: v.asnumpy() for k, v in executor.grad_dict.items() if v is not None}
+    for name in expected:
+        if grad_req[name] == 'write':
+            assert_almost_equal(expected[name], grads[name], rtol, atol,
+                                ('EXPECTED_%s' % name, 'BACKWARD_%s' % name), equal_nan=equal_nan)
+        elif grad_req[name] == 'add':
+            assert_almost_equal(expected[name], grads[name] - args_grad_npy[name], rtol, atol,
+                                ('EXPECTED_%s' % name, 'BACKWARD_%s' % name), equal_nan=equal_nan)
+        elif grad_req[name] == 'null':
+            assert_almost_equal(args_grad_npy[name], grads[name], rtol, atol,
+                                ('EXPECTED_%s' % name, 'BACKWARD_%s' % name), equal_nan=equal_nan)
+    return grads
+
+
+def check_speed(sym, location=None, ctx=None, N=20, grad_req=None, typ='whole', **kwargs):
+    """Average seconds per forward ('forward') or forward+backward ('whole') iteration."""
+    import time
+    ctx = ctx or default_context()
+    if grad_req is None:
+        grad_req = 'write'
+    if location is None:
+        exe = sym.simple_bind(grad_req=grad_req, ctx=ctx, **kwargs)
+        location = {k: np.random.normal(size=arr.shape, scale=1.0) for k, arr in exe.arg_dict.items()}
+    else:
+        exe = sym.simple_bind(grad_req=grad_req, ctx=ctx, **{k: v.shape for k, v in location.items()})
+    for name, iarr in location.items():
+        exe.arg_dict[name][:] = iarr.astype(exe.arg_dict[name].dtype)
+    nd.waitall()
+    if typ == 'whole':
+        exe.forward(is_train=True)
+        exe.backward(out_grads=exe.outputs)
+        nd.waitall()
+        tic = time.time()
+        for _ in range(N):
+            exe.forward(is_train=True)
+            exe.backward(out_grads=exe.outputs)
+        nd.waitall()
+    elif typ == 'forward':
+        exe.forward(is_train=False)
+        nd.waitall()
+        tic = time.time()
+        for _ in range(N):
+            exe.forward(is_train=False)
+        nd.waitall()
+    else:
+        raise ValueError('typ can only be "whole" or "forward".')
+    return (time.time() - tic) / N
+
+
+def check_consistency(sym, ctx_list, scale=1.0, grad_req='write', arg_params=None, aux_params=None, tol=None,
+                      raise_on_err=True, ground_truth=None, equal_nan=False, use_uniform=False, rand_type=np.float64):
+    """Run ``sym`` on every (ctx, shapes, dtypes) entry of ``ctx_list`` and compare to the highest precision one."""
+    if tol is None:
+        tol = {np.dtype(np.float16): 1e-1, np.dtype(np.float32): 1e-3, np.dtype(np.float64): 1e-5,
+               np.dtype(np.uint8): 0, np.dtype(np.int32): 0, np.dtype(np.int64): 0}
+    elif isinstance(tol, (int, float)):
+        tol = {np.dtype(t): tol for t in (np.float16, np.float32, np.float64, np.uint8, np.int32, np.int64)}
+    assert len(ctx_list) > 1
+    if isinstance(sym, sym_mod.Symbol):
+        sym = [sym] * len(ctx_list)
+    output_names = sym[0].list_outputs()
+    arg_names = sym[0].list_arguments()
+    exe_list = []
+    for s, ctx in zip(sym, ctx_list):
+        ctx = dict(ctx)
+        c = ctx.pop('ctx')
+        types = ctx.pop('type_dict', {})
+        exe_list.append(s.simple_bind(c, grad_req=grad_req, type_dict=types, **ctx))
+    arg_params = {} if arg_params is None else arg_params
+    aux_params = {} if aux_params is None else aux_params
+    for n, arr in exe_list[0].arg_dict.items():
+        if n not in arg_params:
+            arg_params[n] = (np.random.uniform(-scale, scale, size=arr.shape) if use_uniform else
+                             np.random.normal(size=arr.shape, scale=scale)).astype(rand_type)
+    for n, arr in exe_list[0].aux_dict.items():
+        if n not in aux_params:
+            aux_params[n] = 0
+    for exe in exe_list:
+        for name, arr in exe.arg_dict.items():
+            arr[:] = nd.array(np.asarray(arg_params[name]), dtype=arr.dtype)
+        for name, arr in exe.aux_dict.items():
+            arr[:] = aux_params[name]
+    dtypes = [np.dtype(exe.outputs[0].dtype) if exe.outputs else np.dtype(exe.arg_arrays[0].dtype)
+              for exe in exe_list]
+    for exe in exe_list:
+        exe.forward(is_train=False)
+    dtypes = [np.dtype(exe.outputs[0].dtype) for exe in exe_list]
+    max_idx = int(np.argmax([d.itemsize for d in dtypes]))
+    gt = ground_truth
+    if gt is None:
+        gt = exe_list[max_idx].output_dict.copy()
+    for i, exe in enumerate(exe_list):
+        if i == max_idx:
+            continue
+        for name, arr in zip(output_names, exe.outputs):
+            gtarr = gt[name].astype(dtypes[i]).asnumpy() if isinstance(gt[name], NDArray) else gt[name]
+            try:
+                assert_almost_equal(arr.asnumpy(), gtarr, rtol=tol[dtypes[i]], atol=tol[dtypes[i]],
+                                    equal_nan=equal_nan)
+            except AssertionError as e:
+                if raise_on_err:
+                    raise e
+    if grad_req != 'null':
+        for exe in exe_list:
+            exe.forward(is_train=True)
+            exe.backward(exe.outputs)
+        gt_g = {n: g for n, g in exe_list[max_idx].grad_dict.items() if g is not None}
+        for i, exe in enumerate(exe_list):
+            if i == max_idx:
+                continue
+            for name, g in exe.grad_dict.items():
+                if g is None or name not in gt_g:
+                    continue
+                try:
+                    assert_almost_equal(g.asnumpy(), gt_g[name].astype(g.dtype).asnumpy(), rtol=tol[dtypes[i]],
+                                        atol=tol[dtypes[i]], equal_nan=equal_nan)
+                except AssertionError as e:
+                    if raise_on_err:
+                        raise e
+    return gt
+
+
+def list_gpus():
+    try:
+        import torch
+        return list(range(torch.cuda.device_count()))
+    except Exception:
+        return []
+
+
+def download(url, fname=None, dirname=None, overwrite=False, retries=5):
+    """No network on the target nodes: returns the local path if it exists, otherwise raises."""
+    if fname is None:
+        fname = url.split('/')[-1]
+    if dirname is not None:
+        fname = os.path.join(dirname, fname)
+    if os.path.exists(fname) and not overwrite:
+        return fname
+    raise MXNetError('download(%s): no network access; place the file at %s' % (url, fname))
+
+
+def get_mnist(num_train=60000, num_test=10000, seed=42):
+    """MNIST arrays; synthesised deterministically (class-dependent blobs) when the dataset is absent."""
+    root = os.path.join(os.environ.get('MXNET_HOME', os.path.expanduser('~/.mxnet')), 'datasets', 'mnist')
+    try:
+        from .gluon.data.vision import MNIST
+        tr = MNIST(root, train=True)
+        te = MNIST(root, train=False)
+        return {'train_data': tr._data.asnumpy().transpose(0, 3, 1, 2).astype(np.float32) / 255,
+                'train_label': tr._label.astype(np.float32),
+                'test_data': te._data.asnumpy().transpose(0, 3, 1, 2).astype(np.float32) / 255,
+                'test_label': te._label.astype(np.float32)}
+    except Exception:
+        rng = np.random.RandomState(seed)
+        protos = rng.rand(10, 1, 28, 28).astype(np.float32)
+
+        def make(n):
+            y = rng.randint(0, 10, size=n)
+            x = np.clip(protos[y] + 0.3 * rng.randn(n, 1, 28, 28).astype(np.float32), 0, 1)
+            return x, y.astype(np.float32)
+        trd, trl = make(num_train)
+        ted, tel = make(num_test)
+        return {'train_data': trd, 'train_label': trl, 'test_data': ted, 'test_label': tel}
+
+
+def get_mnist_iterator(batch_size, input_shape, num_parts=1, part_index=0):
+    from . import io
+    mnist = get_mnist()
+    flat = len(input_shape) == 1
+    tr = mnist['train_data'].reshape((-1,) + tuple(input_shape)) if flat else mnist['train_data']
+    te = mnist['test_data'].reshape((-1,) + tuple(input_shape)) if flat else mnist['test_data']
+    n = tr.shape[0] // num_parts
+    train = io.NDArrayIter(tr[part_index * n:(part_index + 1) * n], mnist['train_label'][part_index * n:
+                                                                                        (part_index + 1) * n],
+                           batch_size, shuffle=True)
+    val = io.NDArrayIter(te, mnist['test_label'], batch_size)
+    return train, val
+
+
+def same_array(array1, array2):
+    """True when two NDArrays share memory (writing one changes the other)."""
+    array1[:] += 1
+    if not same(array1.asnumpy(), array2.asnumpy()):
+        array1[:] -= 1
+        return False
+    array1[:] -= 1
+    return same(array1.asnumpy(), array2.asnumpy())
+
+
+@contextmanager
+def discard_stderr():
+    try:
+        stderr_fileno = sys.stderr.fileno()
+        old_stderr = os.dup(stderr_fileno)
+        bit_bucket = open(os.devnull, 'w')
+        os.dup2(bit_bucket.fileno(), stderr_fileno)
+        yield
+    finally:
+        os.dup2(old_stderr, stderr_fileno)
+        bit_bucket.close()
+
+
+class DummyIter:
+    """Repeats the first batch of ``real_iter`` forever (for speed tests)."""
+
+    def __init__(self, real_iter):
+        self.batch_size = real_iter.batch_size
+        self.provide_data = real_iter.provide_data
+        self.provide_label = real_iter.provide_label
+        self.the_batch = next(iter(real_iter))
+
+    def __iter__(self):
+        return self
+
+    def reset(self):
+        pass
+
+    def __next__(self):
+        return self.the_batch
+
+    next = __next__
+
+
+def gen_buckets_probs_with_ppf(ppf, nbuckets):
+    assert nbuckets > 0
+    probs = [1.0 / nbuckets for _ in range(nbuckets)]
+    buckets = [(ppf(i / float(nbuckets)), ppf((i + 1) / float(nbuckets))) for i in range(nbuckets)]
+    return buckets, probs
+
+
+def mean_check(generator, mu, sigma, nsamples=1000000):
+    samples = np.array(generator(nsamples))
+    sample_mean = samples.mean()
+    return (sample_mean > mu - 3 * sigma / np.sqrt(nsamples)) and (sample_mean < mu + 3 * sigma / np.sqrt(nsamples))
+
+
+def var_check(generator, sigma, nsamples=1000000):
+    samples = np.array(generator(nsamples))
+    sample_var = samples.var(ddof=1)
+    return (sample_var > sigma ** 2 - 3 * np.sqrt(2 * sigma ** 4 / (nsamples - 1))) and \
+        (sample_var < sigma ** 2 + 3 * np.sqrt(2 * sigma ** 4 / (nsamples - 1)))
+
+
+def chi_square_check(generator, buckets, probs, nsamples=1000000):
+    """Pearson chi-square goodness of fit of ``generator`` samples against bucket probabilities."""
+    import scipy.stats as ss
+    if not isinstance(buckets, list):
+        raise ValueError('buckets must be a list')
+    samples = np.array(generator(nsamples)).reshape(-1)
+    continuous_dist = isinstance(buckets[0], tuple)
+    if continuous_dist:
+        buckets_npy = np.array([b for bucket in buckets for b in bucket])
+        sample_bucket_ids = np.searchsorted(buckets_npy, samples, side='right')
+        sample_bucket_ids = np.where(sample_bucket_ids % 2 == 1, sample_bucket_ids // 2, -1)
+    else:
+        lookup = {b: i for i, b in enumerate(buckets)}
+        sample_bucket_ids = np.array([lookup.get(s, -1) for s in samples])
+    obs_freq = np.bincount(sample_bucket_ids[sample_bucket_ids >= 0], minlength=len(buckets))
+    expected_freq = np.array(probs) * nsamples
+    _, p = ss.chisquare(f_obs=obs_freq, f_exp=expected_freq * obs_freq.sum() / expected_freq.sum())
+    return p, obs_freq, expected_freq
+
+
+def verify_generator(generator, buckets, probs, nsamples=1000000, nrepeat=5, success_rate=0.2, alpha=0.05):
+    cs_ret_l = []
+    obs_freq_l = []
+    expected_freq_l = []
+    for _ in range(nrepeat):
+        cs_ret, obs_freq, expected_freq = chi_square_check(generator=generator, buckets=buckets, probs=probs,
+                                                           nsamples=nsamples)
+        cs_ret_l.append(cs_ret)
+        obs_freq_l.append(obs_freq)
+        expected_freq_l.append(expected_freq)
+    success_num = (np.array(cs_ret_l) > alpha).sum()
+    if success_num < nrepeat * success_rate:
+        raise AssertionError('Generator test fails, Chi-square p=%s, obs_freq=%s, expected_freq=%s.'
+                             % (str(cs_ret_l), str(obs_freq_l), str(expected_freq_l)))
+    return cs_ret_l
+
+
+def compare_ndarray_tuple(t1, t2, rtol=None, atol=None):
+    if t1 is None or t2 is None:
+        return
+    if isinstance(t1, tuple):
+        for s1, s2 in zip(t1, t2):
+            compare_ndarray_tuple(s1, s2, rtol, atol)
+    else:
+        assert_almost_equal(t1, t2, rtol=rtol, atol=atol)
+
+
+def compare_optimizer(opt1, opt2, shape, dtype, w_stype='default', g_stype='default', rtol=1e-4, atol=1e-5,
+                      compare_states=True, ntensors=1):
+    """Run one update of two optimizers on identical random weights/grads and compare."""
+    if ntensors == 1:
+        w1 = rand_ndarray(shape, w_stype, dtype=dtype)
+        w2 = w1.copy()
+        g1 = rand_ndarray(shape, g_stype, dtype=dtype)
+        g2 = g1.copy()
+        state1 = opt1.create_state_multi_precision(0, w1)
+        state2 = opt2.create_state_multi_precision(0, w2)
+        if compare_states:
+            compare_ndarray_tuple(state1, state2)
+        opt1.update_multi_precision(0, w1, g1, state1)
+        opt2.update_multi_precision(0, w2, g2, state2)
+        if compare_states:
+            compare_ndarray_tuple(state1, state2, rtol=rtol, atol=atol)
+        assert_almost_equal(w1, w2, rtol=rtol, atol=atol)
+    else:
+        for i in range(ntensors):
+            compare_optimizer(opt1, opt2, shape, dtype, w_stype, g_stype, rtol, atol, compare_states, 1)
+
+
+def same_symbol_structure(sym1, sym2):
+    conf = [sym1.tojson(), sym2.tojson()]
+    import json
+    a, b = json.loads(conf[0]), json.loads(conf[1])
+    if len(a['nodes']) != len(b['nodes']):
+        return False
+    for n1, n2 in zip(a['nodes'], b['nodes']):
+        if n1['op'] != n2['op'] or n1.get('inputs') != n2.get('inputs'):
+            return False
+    return True
+
+
+@contextmanager
+def environment(*args):
+    """Temporarily set environment variables: ``environment('K', 'v')`` or ``environment({'K': 'v'})``."""
+    if len(args) == 2:
+        values = {args[0]: args[1]}
+    elif len(args) == 1:
+        values = args[0]
+    else:
+        raise ValueError('environment() takes (name, value) or a dict')
+    old = {k: os.environ.get(k) for k in values}
+    try:
+        for k, v in values.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = str(v)
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def collapse_sum_like(a, shape):
+    assert len(a.shape) >= len(shape)
+    if np.prod(shape) == 0 or a.size == 0:
+        return np.zeros(shape, dtype=a.dtype)
+    axes = []
+    ndim_diff = len(a.shape) - len(shape)
+    for i in range(ndim_diff):
+        axes.append(i)
+    for i, s in enumerate(shape):
+        if s != a.shape[i + ndim_diff]:
+            assert s == 1
+            axes.append(i + ndim_diff)
+    return np.sum(a, axis=tuple(axes)).reshape(shape)
+
+
+def is_op_runnable():
+    return True
+
+
+def assert_raises_cudnn_not_satisfied(min_version):
+    def test_helper(orig_test):
+        return orig_test
+    return test_helper
