@@ -15,6 +15,7 @@ import torch
 
 from . import _state
 from . import profiler as _profiler
+from .ops import amp_dispatch as _amp
 from .base import MXNetError
 from .ops import registry
 
@@ -70,6 +71,8 @@ class GraphProgram:
             vals[s] = feed.get(name)
         for fn, ins, attrs, outs, name, opname in self.steps:
             args = [vals[i] for i in ins]
+            if _amp.active:
+                args = _amp.cast_inputs(opname, args, attrs)
             if monitor is not None and monitor_all:
                 for j, a in enumerate(args):
                     if a is not None:

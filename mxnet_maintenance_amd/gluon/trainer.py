@@ -305,7 +305,21 @@ class Trainer:
         self._check_and_rescale_grad(rescale_grad)
         self._prepare()
         self._allreduce_grads()
+        if self._amp_overflow():
+            return
         self._update(ignore_stale_grad)
+
+    def _amp_overflow(self):
+        """AMP dynamic loss scaling: skip the update when any gradient is non-finite."""
+        scaler = getattr(self, '_amp_loss_scaler', None)
+        if scaler is None:
+            return False
+        if scaler.has_overflow(self._params, self._arenas):
+            for p in self._params:
+                for d in (p._data or []):
+                    d._fresh_grad = False
+            return True
+        return False
 
     def allreduce_grads(self):
         self._prepare()
@@ -339,6 +353,8 @@ class Trainer:
             'update() when parameters are updated on kvstore is not supported. Try setting `update_on_kvstore` ' \
             'to False when creating trainer.'
         self._check_and_rescale_grad(self._scale / batch_size)
+        if self._amp_overflow():
+            return
         self._update(ignore_stale_grad)
 
     def _check_stale(self, ignore_stale_grad):

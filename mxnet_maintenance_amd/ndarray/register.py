@@ -9,6 +9,7 @@ import torch
 
 from .. import _state
 from .. import profiler as _profiler
+from ..ops import amp_dispatch as _amp
 from ..base import MXNetError
 from ..ops import registry
 from .ndarray import NDArray
@@ -86,6 +87,8 @@ def invoke(op, inputs, attrs, out=None):
     """Run ``op`` on NDArray ``inputs`` with parsed ``attrs``."""
     tin = [None if x is None else x._data for x in inputs]
     _note_leaves(inputs)
+    if _amp.active:
+        tin = _amp.cast_inputs(op.name, tin, attrs)
     if _profiler.active_imperative:
         with _profiler.op_span(_profiler.current_scope() + op.name):
             res = _run(op.fn, tin, attrs)

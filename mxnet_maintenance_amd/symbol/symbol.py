@@ -720,6 +720,9 @@ def _run_meta(op, parsed, shapes, dtypes):
     return [(tuple(o.shape), o.dtype) for o in out]
 
 
+_SHAPE_PRESERVING = ('Cast', 'cast', 'amp_cast', 'amp_multicast', '_copy', 'identity', 'BlockGrad',
+                     'stop_gradient')
+
 _INIT_OPS = ('_zeros', '_ones', '_full', '_empty', 'zeros', 'ones', 'full')
 
 
@@ -798,12 +801,25 @@ def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True):
                         shape[(id(a), j)] = tuple(s)
                         in_shapes[idx] = tuple(s)
                         progress = True
+                        # shape-preserving producers (casts inserted by AMP, copies): the
+                        # parameter behind them has the same shape
+                        while a.op in _SHAPE_PRESERVING and a.inputs:
+                            a, j = a.inputs[j if a.op == 'amp_multicast' else 0]
+                            if (id(a), j) in shape:
+                                break
+                            shape[(id(a), j)] = tuple(s)
             if any(s is None for s in in_shapes):
                 if what == 'type':
                     # dtype-only propagation: parameters follow the data dtype, outputs
                     # follow the first input unless the op declares an output dtype.
                     in_dt = [dtype.get((id(a), j)) for a, j in n.inputs]
                     base_dt = next((d for d in in_dt if d is not None), None)
+                    if base_dt is None and n.op in ('Cast', 'cast', 'amp_cast') and parsed.get('dtype'):
+                        # a cast fixes its output type whatever the input is
+                        if (id(n), 0) not in dtype:
+                            dtype[(id(n), 0)] = torch_dtype(parsed['dtype'])
+                            progress = True
+                        continue
                     if base_dt is None:
                         continue
                     for (a, j) in n.inputs:
@@ -832,6 +848,17 @@ def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True):
                 dtype[(id(n), i)] = d
             done.add(id(n))
             progress = True
+    if what == 'type':
+        # variables only consumed through explicit casts (AMP graphs) default to fp32 storage
+        consumers = {}
+        for n in order:
+            for a, _ in n.inputs:
+                consumers.setdefault(id(a), []).append(n.op)
+        for n in order:
+            if n.op is None and (id(n), 0) not in dtype:
+                ops = consumers.get(id(n), [])
+                if ops and all(o in ('Cast', 'cast', 'amp_cast', 'amp_multicast') for o in ops):
+                    dtype[(id(n), 0)] = torch.float32
     aux = _aux_var_ids(order)
     table = shape if what == 'shape' else dtype
     args = [table.get((id(n), 0)) for n in order if n.op is None and id(n) not in aux]
