@@ -734,7 +734,7 @@ class Loss(EvalMetric):
             preds = [preds]
         for pred in preds:
             if isinstance(pred, NDArray):
-                loss = float(pred._data.float().sum())
+                loss = float(pred._data.detach().float().sum())
             else:
                 loss = float(numpy.sum(pred))
             self._add(loss, pred.size)

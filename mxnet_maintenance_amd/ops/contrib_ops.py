@@ -1,0 +1,214 @@
+"""contrib operators: deformable convolution (v1 / modulated v2), SyncBatchNorm, PixelShuffle helpers.
+
+Parity: src/operator/contrib/deformable_convolution*, modulated_deformable_convolution*,
+sync_batch_norm*.  Deformable sampling is expressed as one ``grid_sample`` per
+kernel tap (bilinear, zero outside, the reference's im2col semantics) followed
+by a grouped GEMM over the gathered columns; autograd gives the gradients
+w.r.t. data, offsets, masks and weights.
+"""
+import torch
+import torch.nn.functional as F
+
+from .. import _state
+from .registry import register
+
+
+def _deform_columns(x, offset, mask, kernel, stride, pad, dilate, dg):
+    """Sampled columns [N, C, K, Ho, Wo] for deformable convolution."""
+    N, C, H, W = x.shape
+    kh, kw = kernel
+    sh, sw = stride
+    ph, pw = pad
+    dh, dw = dilate
+    Ho, Wo = offset.shape[2], offset.shape[3]
+    K = kh * kw
+    dev, dt = x.device, x.dtype
+    base_h = (torch.arange(Ho, device=dev, dtype=dt) * sh - ph).view(1, Ho, 1)
+    base_w = (torch.arange(Wo, device=dev, dtype=dt) * sw - pw).view(1, 1, Wo)
+    cpg = C // dg
+    off = offset.view(N, dg, K, 2, Ho, Wo)
+    cols = []
+    for k in range(K):
+        i, j = divmod(k, kw)
+        hs = base_h + i * dh + off[:, :, k, 0]          # [N, dg, Ho, Wo]
+        ws = base_w + j * dw + off[:, :, k, 1]
+        gy = 2.0 * hs / max(H - 1, 1) - 1.0
+        gx = 2.0 * ws / max(W - 1, 1) - 1.0
+        grid = torch.stack([gx, gy], dim=-1).view(N * dg, Ho, Wo, 2)
+        xs = x.view(N * dg, cpg, H, W)
+        s = F.grid_sample(xs, grid, mode='bilinear', padding_mode='zeros', align_corners=True)
+        s = s.view(N, dg, cpg, Ho, Wo)
+        if mask is not None:
+            s = s * mask.view(N, dg, K, Ho, Wo)[:, :, k].unsqueeze(2)
+        cols.append(s.reshape(N, C, Ho, Wo))
+    return torch.stack(cols, dim=2)                     # [N, C, K, Ho, Wo]
+
+
+def _deform_conv(x, offset, mask, weight, bias, kernel, stride, pad, dilate, num_group, dg):
+    cols = _deform_columns(x, offset, mask, kernel, stride, pad, dilate, dg)
+    N, C, K, Ho, Wo = cols.shape
+    O = weight.shape[0]
+    g = num_group
+    cols = cols.view(N, g, C // g, K, Ho, Wo)
+    w = weight.view(g, O // g, C // g, K)
+    out = torch.einsum('ngckhw,gock->ngohw', cols, w).reshape(N, O, Ho, Wo)
+    if bias is not None:
+        out = out + bias.view(1, -1, 1, 1)
+    return out
+
+
+def _dc_out_shape(x, kernel, stride, pad, dilate):
+    H, W = x.shape[2], x.shape[3]
+    Ho = (H + 2 * pad[0] - dilate[0] * (kernel[0] - 1) - 1) // stride[0] + 1
+    Wo = (W + 2 * pad[1] - dilate[1] * (kernel[1] - 1) - 1) // stride[1] + 1
+    return Ho, Wo
+
+
+def _dc_args(a):
+    nb = str(a.get('no_bias', False)) in ('True', 'true', '1')
+    return ['data', 'offset', 'weight'] + ([] if nb else ['bias'])
+
+
+def _dc_infer(in_shapes, a):
+    from .registry import parse_value
+    d = in_shapes[0]
+    if d is None:
+        return {}
+    k = parse_value('shape', a.get('kernel', '(1,1)'))
+    s = parse_value('shape', a.get('stride', '(1,1)')) or (1, 1)
+    p = parse_value('shape', a.get('pad', '(0,0)')) or (0, 0)
+    dl = parse_value('shape', a.get('dilate', '(1,1)')) or (1, 1)
+    nf = int(a['num_filter'])
+    g = int(a.get('num_group', 1))
+    dg = int(a.get('num_deformable_group', 1))
+    Ho = (d[2] + 2 * p[0] - dl[0] * (k[0] - 1) - 1) // s[0] + 1
+    Wo = (d[3] + 2 * p[1] - dl[1] * (k[1] - 1) - 1) // s[1] + 1
+    res = {1: (d[0], 2 * dg * k[0] * k[1], Ho, Wo), 2: (nf, d[1] // g) + tuple(k)}
+    if not (str(a.get('no_bias', False)) in ('True', 'true', '1')):
+        res[3] = (nf,)
+    return res
+
+
+_DC_PARAMS = {'kernel': ('shape', ()), 'stride': ('shape', ()), 'dilate': ('shape', ()), 'pad': ('shape', ()),
+              'num_filter': ('int', 1), 'num_group': ('int', 1), 'num_deformable_group': ('int', 1),
+              'workspace': ('int', 1024), 'no_bias': ('bool', False), 'layout': ('str?', None)}
+
+
+@register('_contrib_DeformableConvolution', aliases=('DeformableConvolution',), arg_names=_dc_args,
+          infer_params=_dc_infer, params=_DC_PARAMS)
+def deformable_convolution(data, offset, weight, bias=None, kernel=(), stride=(), dilate=(), pad=(), num_filter=1,
+                           num_group=1, num_deformable_group=1, workspace=1024, no_bias=False, layout=None):
+    stride = tuple(stride) or (1, 1)
+    dilate = tuple(dilate) or (1, 1)
+    pad = tuple(pad) or (0, 0)
+    return _deform_conv(data, offset, None, weight, None if no_bias else bias, tuple(kernel), stride, pad, dilate,
+                        num_group, num_deformable_group)
+
+
+def _mdc_args(a):
+    nb = str(a.get('no_bias', False)) in ('True', 'true', '1')
+    return ['data', 'offset', 'mask', 'weight'] + ([] if nb else ['bias'])
+
+
+def _mdc_infer(in_shapes, a):
+    r = _dc_infer(in_shapes, a)
+    if not r:
+        return r
+    from .registry import parse_value
+    k = parse_value('shape', a.get('kernel', '(1,1)'))
+    dg = int(a.get('num_deformable_group', 1))
+    off = r[1]
+    out = {1: off, 2: (off[0], dg * k[0] * k[1], off[2], off[3]), 3: r[2]}
+    if 3 in r:
+        out[4] = r[3]
+    return out
+
+
+@register('_contrib_ModulatedDeformableConvolution', aliases=('ModulatedDeformableConvolution',),
+          arg_names=_mdc_args, infer_params=_mdc_infer, params=dict(_DC_PARAMS, im2col_step=('int', 64)))
+def modulated_deformable_convolution(data, offset, mask, weight, bias=None, kernel=(), stride=(), dilate=(), pad=(),
+                                     num_filter=1, num_group=1, num_deformable_group=1, workspace=1024,
+                                     no_bias=False, layout=None, im2col_step=64):
+    stride = tuple(stride) or (1, 1)
+    dilate = tuple(dilate) or (1, 1)
+    pad = tuple(pad) or (0, 0)
+    return _deform_conv(data, offset, mask, weight, None if no_bias else bias, tuple(kernel), stride, pad, dilate,
+                        num_group, num_deformable_group)
+
+
+# ---------------------------------------------------------------------------
+# SyncBatchNorm: batch statistics all-reduced over the data-parallel group
+# ---------------------------------------------------------------------------
+
+def _allreduce_(t):
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        if t.is_cuda or dist.get_backend() != 'nccl':
+            dist.all_reduce(t)
+        else:
+            tc = t.cuda()
+            dist.all_reduce(tc)
+            t.copy_(tc.cpu())
+    return t
+
+
+class _SyncBN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps, axis):
+        dims = [d for d in range(x.dim()) if d != axis]
+        xf = x.float()
+        n_local = torch.tensor([float(x.numel() // x.shape[axis])], device=x.device)
+        stats = torch.cat([xf.sum(dims), (xf * xf).sum(dims), n_local])
+        _allreduce_(stats)
+        C = x.shape[axis]
+        n = stats[-1]
+        mean = stats[:C] / n
+        var = torch.clamp(stats[C:2 * C] / n - mean * mean, min=0.0)
+        invstd = torch.rsqrt(var + eps)
+        shape = [1] * x.dim()
+        shape[axis] = C
+        xhat = (xf - mean.view(shape)) * invstd.view(shape)
+        y = xhat * gamma.float().view(shape) + beta.float().view(shape)
+        ctx.save_for_backward(xhat, gamma, invstd, n)
+        ctx.axis = axis
+        return y.to(x.dtype), mean, var
+
+    @staticmethod
+    def backward(ctx, dy, _dm, _dv):
+        xhat, gamma, invstd, n = ctx.saved_tensors
+        axis = ctx.axis
+        dims = [d for d in range(xhat.dim()) if d != axis]
+        C = xhat.shape[axis]
+        shape = [1] * xhat.dim()
+        shape[axis] = C
+        dyf = dy.float()
+        sums = torch.cat([dyf.sum(dims), (dyf * xhat).sum(dims)])
+        dbeta_local, dgamma_local = sums[:C].clone(), sums[C:].clone()
+        _allreduce_(sums)
+        dbeta, dgamma = sums[:C], sums[C:]
+        dx = (dyf - dbeta.view(shape) / n - xhat * dgamma.view(shape) / n) * (gamma.float() * invstd).view(shape)
+        # parameter gradients are the LOCAL sums: the trainer's kvstore reduces them like any other grad
+        return dx.to(dy.dtype), dgamma_local.to(gamma.dtype), dbeta_local.to(gamma.dtype), None, None
+
+
+@register('_contrib_SyncBatchNorm', aliases=('SyncBatchNorm',), arg_names=('data', 'gamma', 'beta'),
+          aux_names=('moving_mean', 'moving_var'), num_outputs=3, num_visible_outputs=1,
+          infer_params=lambda s, a: {} if s[0] is None else {i: (s[0][1],) for i in (1, 2, 3, 4)},
+          params={'eps': ('float', 1e-3), 'momentum': ('float', 0.9), 'fix_gamma': ('bool', True),
+                  'use_global_stats': ('bool', False), 'output_mean_var': ('bool', False), 'ndev': ('int', 1),
+                  'key': ('str', ''), 'axis': ('int', 1)})
+def sync_batch_norm(data, gamma, beta, moving_mean, moving_var, eps=1e-3, momentum=0.9, fix_gamma=True,
+                    use_global_stats=False, output_mean_var=False, ndev=1, key='', axis=1):
+    axis = axis % data.dim()
+    g = torch.ones_like(gamma) if fix_gamma else gamma
+    if _state.STATE.training and not use_global_stats:
+        y, mean, var = _SyncBN.apply(data, g, beta, eps, axis)
+        with torch.no_grad():
+            moving_mean.mul_(momentum).add_(mean.to(moving_mean.dtype), alpha=1 - momentum)
+            moving_var.mul_(momentum).add_(var.to(moving_var.dtype), alpha=1 - momentum)
+        return y, mean, var
+    shape = [1] * data.dim()
+    shape[axis] = data.shape[axis]
+    inv = torch.rsqrt(moving_var.float() + eps)
+    y = (data.float() - moving_mean.float().view(shape)) * (inv * g.float()).view(shape) + beta.float().view(shape)
+    return y.to(data.dtype), moving_mean, moving_var
