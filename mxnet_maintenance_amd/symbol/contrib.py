@@ -4,3 +4,91 @@ from .symbol import _op_func
 for _n in _registry.list_ops():
     if _n.startswith('_contrib_'):
         globals()[_n[len('_contrib_'):]] = _op_func(_n)
+
+
+# ---------------------------------------------------------------------------
+# control flow (parity: python/mxnet/symbol/contrib.py foreach / while_loop / cond)
+# ---------------------------------------------------------------------------
+import json as _json
+
+
+def _as_list(x):
+    return (list(x), True) if isinstance(x, (list, tuple)) else ([x], False)
+
+
+def _free_vars(g, exclude):
+    from .symbol import Symbol
+    out = []
+    for n in g._topo():
+        if n.op is None and n.name not in exclude:
+            out.append(Symbol([(n, 0)]))
+    return out
+
+
+def foreach(body, data, init_states, name='foreach'):
+    """Run ``body(data_t, states) -> (outputs, new_states)`` over the leading axis of ``data``."""
+    from .symbol import var, Group, _create
+    data_l, data_is_list = _as_list(data)
+    states_l, states_is_list = _as_list(init_states)
+    d_ph = [var('%s_data%d' % (name, i)) for i in range(len(data_l))]
+    s_ph = [var('%s_state%d' % (name, i)) for i in range(len(states_l))]
+    outs, new_states = body(d_ph if data_is_list else d_ph[0], s_ph if states_is_list else s_ph[0])
+    outs_l, outs_is_list = _as_list(outs)
+    new_l, _ = _as_list(new_states)
+    g = Group(outs_l + new_l)
+    ph_names = {s.name for s in d_ph + s_ph}
+    remain = _free_vars(g, ph_names)
+    attrs = {'subgraph': g.tojson(), 'data_names': _json.dumps([s.name for s in d_ph]),
+             'state_names': _json.dumps([s.name for s in s_ph]),
+             'remain_names': _json.dumps([s.name for s in remain]), 'num_out_data': len(outs_l)}
+    node = _create('_foreach', {'_pos': data_l + states_l + remain}, attrs, name=name)
+    res = list(node)
+    o = res[:len(outs_l)]
+    st = res[len(outs_l):]
+    return (o if outs_is_list else o[0]), (st if states_is_list else st[0])
+
+
+def while_loop(cond, func, loop_vars, max_iterations=None, name='while_loop'):
+    """Symbolic while loop; per-step outputs are padded to ``max_iterations``."""
+    from .symbol import var, Group, _create
+    if max_iterations is None:
+        raise ValueError('max_iterations should be specified')
+    vars_l, vars_is_list = _as_list(loop_vars)
+    ph = [var('%s_var%d' % (name, i)) for i in range(len(vars_l))]
+    arg = ph if vars_is_list else ph[0]
+    c = cond(*ph) if vars_is_list else cond(arg)
+    outs, new_vars = func(*ph) if vars_is_list else func(arg)
+    outs_l, outs_is_list = _as_list(outs) if outs is not None else ([], True)
+    new_l, _ = _as_list(new_vars)
+    fg = Group(outs_l + new_l)
+    cg = Group([c])
+    ph_names = {s.name for s in ph}
+    remain = {s.name: s for s in _free_vars(fg, ph_names) + _free_vars(cg, ph_names)}
+    remain = list(remain.values())
+    attrs = {'cond_graph': cg.tojson(), 'func_graph': fg.tojson(), 'var_names': _json.dumps([s.name for s in ph]),
+             'remain_names': _json.dumps([s.name for s in remain]), 'num_out_data': len(outs_l),
+             'max_iterations': int(max_iterations)}
+    node = _create('_while_loop', {'_pos': vars_l + remain}, attrs, name=name)
+    res = list(node)
+    o = res[:len(outs_l)]
+    v = res[len(outs_l):]
+    return (o if outs_is_list else (o[0] if o else [])), (v if vars_is_list else v[0])
+
+
+def cond(pred, then_func, else_func, name='cond'):
+    """Symbolic if/else: both branches are subgraphs over the free variables they use."""
+    from .symbol import Group, _create
+    then_out = then_func()
+    else_out = else_func()
+    t_l, t_is_list = _as_list(then_out)
+    e_l, _ = _as_list(else_out)
+    if len(t_l) != len(e_l):
+        raise ValueError('then_func and else_func must return the same number of outputs')
+    tg, eg = Group(t_l), Group(e_l)
+    inputs = {s.name: s for s in _free_vars(tg, set()) + _free_vars(eg, set())}
+    inputs = list(inputs.values())
+    attrs = {'then_graph': tg.tojson(), 'else_graph': eg.tojson(),
+             'input_names': _json.dumps([s.name for s in inputs]), 'num_outputs': len(t_l)}
+    node = _create('_cond', {'_pos': [pred] + inputs}, attrs, name=name)
+    res = list(node)
+    return res if t_is_list else res[0]
