@@ -579,6 +579,9 @@ class HybridBlock(Block):
         else:
             outs = self._cached_op(feed, ctx.torch_device)
         outs = [NDArray(o) for o in outs]
+        if _state.STATE.np_array:
+            from ..numpy import _np_out
+            outs = _np_out(outs)
         ret, _ = _regroup(outs, self._out_format)
         return ret
 

@@ -11,7 +11,7 @@ from collections import OrderedDict
 import numpy as np
 import torch
 
-from .. import autograd, initializer
+from .. import _state, autograd, initializer
 from ..base import MXNetError, np_dtype, torch_dtype, dtype_name
 from ..context import Context, cpu, current_context
 from ..ndarray.ndarray import NDArray
@@ -28,6 +28,14 @@ class DeferredInitializationError(MXNetError):
 
 def _shape_known(shape):
     return shape is not None and all(d > 0 for d in shape) and len(shape) > 0
+
+
+def _to_np_class(arrs):
+    """Under ``npx.set_np()`` parameters hand out ``mx.np.ndarray`` (same object, NumPy semantics)."""
+    from ..numpy import ndarray as _npnd
+    for a in arrs:
+        if a is not None and a.__class__ is NDArray:
+            a.__class__ = _npnd
 
 
 class Parameter:
@@ -115,6 +123,8 @@ class Parameter:
 
     # ------------------------------------------------------------------ data
     def _check_and_get(self, arr_list, ctx):
+        if arr_list is not None and _state.STATE.np_array:
+            _to_np_class(arr_list)
         if arr_list is not None:
             if ctx is list:
                 return arr_list

@@ -23,6 +23,11 @@ del _g
 
 def __getattr__(name):
     # operators registered after import (mx.operator 'Custom', user ops) resolve lazily
+    if name in ('np', 'npx'):
+        import importlib
+        mod = importlib.import_module('..numpy' if name == 'np' else '..numpy_extension', __name__)
+        globals()[name] = mod
+        return mod
     from ..ops import registry as _registry
     if _registry.has(name):
         fn = _register.make_op_function(name)

@@ -243,8 +243,12 @@ class NDArray:
         return self
 
     def as_np_ndarray(self):
+        """Zero-copy ``mx.np.ndarray`` view sharing data, gradient buffer and grad_req."""
         from ..numpy import ndarray as np_ndarray
-        return np_ndarray(self._data)
+        r = np_ndarray.__new__(np_ndarray)
+        for k in ('_data', '_grad', '_grad_req', '_stype', '_fresh_grad', '_arena'):
+            setattr(r, k, getattr(self, k))
+        return r
 
     def as_nd_ndarray(self):
         return self
@@ -272,6 +276,8 @@ class NDArray:
         g = torch.zeros_like(t)
         t.grad = g
         self._grad = NDArray(g)
+        if self.__class__ is not NDArray and self._stype == 'default':
+            self._grad.__class__ = self.__class__
         self._grad_req = grad_req
 
     def _set_grad_buffer(self, gbuf, grad_req='write'):

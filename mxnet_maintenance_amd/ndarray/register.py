@@ -15,6 +15,19 @@ from ..ops import registry
 from .ndarray import NDArray
 
 _SKIP_KW = ('name', 'attr', 'out')
+_NP_CLS = [None]     # mx.np.ndarray, set when mx.numpy is imported
+
+
+def _np_wrap(inputs, outs):
+    """Outputs become mx.np.ndarray under npx.set_np() or when any input is one."""
+    cls = _NP_CLS[0]
+    if cls is None:
+        return outs
+    if _state.STATE.np_array or any(x is not None and x.__class__ is cls for x in inputs):
+        for o in outs:
+            if o.__class__ is NDArray:
+                o.__class__ = cls
+    return outs
 
 
 def _split_args(op, args, kwargs):
@@ -99,6 +112,7 @@ def invoke(op, inputs, attrs, out=None):
         outs = [NDArray(r) for r in res[:nvis]]
     else:
         outs = [NDArray(res)]
+    _np_wrap(inputs, outs)
     if out is not None:
         targets = out if isinstance(out, (list, tuple)) else [out]
         for t, o in zip(targets, outs):
@@ -123,7 +137,7 @@ def invoke_fn(fn, arrays):
     """Run an ad-hoc torch function (reshape, astype, ...) with autograd semantics."""
     _note_leaves(arrays)
     res = _run(fn, [a._data for a in arrays], {})
-    return NDArray(res)
+    return _np_wrap(arrays, [NDArray(res)])[0]
 
 
 def make_op_function(name):

@@ -1,0 +1,1427 @@
+"""``mx.np.ndarray`` and the NumPy-compatible function set.
+
+Parity: python/mxnet/numpy/multiarray.py (ndarray class, creation, ufuncs,
+reductions, manipulation), python/mxnet/numpy/_op.py / fallback.py.
+
+``ndarray`` is a slot-compatible subclass of the legacy NDArray: the same
+torch tensor, gradient buffer and autograd tape, but NumPy semantics (0-d
+arrays, ``bool`` comparisons, NumPy broadcasting/promotion, ``reshape`` without
+MXNet's special codes).  Every function dispatches to a registered ``_npi_*``
+operator, so it works imperatively on ndarrays and builds graph nodes when given
+Symbols (``F.np.*`` inside a hybridized block).
+"""
+import builtins
+import numbers
+
+import numpy as onp
+import torch
+
+from .. import _state
+from ..base import numeric_types, torch_dtype
+from ..context import current_context
+from ..ndarray import ndarray as _ndm
+from ..ndarray.ndarray import NDArray, _convert_key, _index_fn
+from ..ndarray import register as _reg
+from ..ops import registry as _registry
+
+__all__ = []   # filled at the end
+
+
+def _export(f):
+    __all__.append(f.__name__)
+    return f
+
+
+# ---------------------------------------------------------------------------
+# dispatch helpers
+# ---------------------------------------------------------------------------
+
+def _is_sym(x):
+    from ..symbol.symbol import Symbol
+    return isinstance(x, Symbol)
+
+
+_FORCE_SYM = [False]
+
+
+def _np_out(res):
+    if isinstance(res, NDArray):
+        if res.__class__ is NDArray:
+            res.__class__ = ndarray
+        return res
+    if isinstance(res, (list, tuple)):
+        return [_np_out(r) for r in res]
+    return res
+
+
+def _call(name, *inputs, **attrs):
+    """Invoke registered op ``name`` imperatively, or build a graph node for Symbol inputs."""
+    if _FORCE_SYM[0] or builtins.any(_is_sym(x) for x in inputs):
+        from ..symbol.symbol import _op_func
+        attrs = {k: v for k, v in attrs.items() if v is not None}
+        if 'dtype' in attrs and not isinstance(attrs['dtype'], str):
+            attrs['dtype'] = _dtype_name(attrs['dtype'])
+        return _op_func(name)(*inputs, **attrs)
+    op = _registry.get(name)
+    out = attrs.pop('out', None)
+    if op.key_var_num_args:
+        attrs[op.key_var_num_args] = len(inputs)
+    res = _reg.invoke(op, list(inputs), op.parse_attrs(attrs))
+    res = _np_out(res)
+    if out is not None:
+        out[...] = res
+        return out
+    return res
+
+
+def _dtype_name(dt):
+    if dt is None:
+        return None
+    if isinstance(dt, str):
+        return dt
+    if isinstance(dt, torch.dtype):
+        return str(dt).replace('torch.', '')
+    try:
+        return onp.dtype(dt).name
+    except TypeError:
+        return getattr(dt, '__name__', str(dt))
+
+
+def _ctx(ctx):
+    return ctx if ctx is not None else current_context()
+
+
+def _is_scalar(x):
+    return isinstance(x, (numbers.Number, onp.generic, bool)) and not isinstance(x, onp.ndarray)
+
+
+def _py(x):
+    return x.item() if isinstance(x, onp.generic) else x
+
+
+def _as_nd(x, ctx=None):
+    if isinstance(x, NDArray) or _is_sym(x):
+        return x
+    return array(x, ctx=ctx)
+
+
+def _first_ctx(*xs):
+    for x in xs:
+        if isinstance(x, NDArray):
+            return x.context
+    return None
+
+
+# ---------------------------------------------------------------------------
+# ndarray
+# ---------------------------------------------------------------------------
+
+class ndarray(NDArray):
+    """A NumPy-compatible n-dimensional array living on a :class:`Context`."""
+    __slots__ = ()
+
+    # ---- numpy-facing basics
+    def __repr__(self):
+        a = self.asnumpy()
+        r = onp.array_repr(a) if a.ndim else 'array(%s)' % onp.array2string(a) + (
+            '' if a.dtype == onp.float32 else ', dtype=%s' % a.dtype)
+        if a.dtype == onp.float32:
+            r = r.replace(', dtype=float32', '')
+        elif a.dtype == onp.float64 and 'dtype' not in r:
+            r = r[:-1] + ', dtype=float64)'
+        ctx = self.context
+        if ctx.device_type != 'cpu':
+            r = r[:-1] + ', ctx=%s)' % ctx
+        return r
+
+    __str__ = __repr__
+
+    def __getitem__(self, key):
+        if isinstance(key, ndarray) and key.dtype == onp.bool_:
+            m = key._data
+            return _np_out(_reg.invoke_fn(lambda t: t[m.to(t.device)], [self]))
+        key = _convert_key(key)
+        if isinstance(key, int) and self.ndim >= 1:
+            n = self.shape[0]
+            if not -n <= key < n:
+                raise IndexError('index %d is out of bounds for axis 0 with size %d' % (key, n))
+        return _np_out(_reg.invoke_fn(lambda t: _index_fn(t, key), [self]))
+
+    def __setitem__(self, key, value):
+        if isinstance(key, ndarray) and key.dtype == onp.bool_:
+            key = key._data
+        NDArray.__setitem__(self, key, value._data if isinstance(value, NDArray) else value)
+
+    def __iter__(self):
+        for i in range(self.shape[0]):
+            yield self[i]
+
+    def __len__(self):
+        if self.ndim == 0:
+            raise TypeError('len() of unsized object')
+        return self.shape[0]
+
+    def __bool__(self):
+        if self.size == 1:
+            return bool(self._data.reshape(-1)[0].item())
+        if self.size == 0:
+            return False
+        raise ValueError('The truth value of an ndarray with more than one element is ambiguous. '
+                         'Use a.any() or a.all()')
+
+    def __hash__(self):
+        return id(self)
+
+    def __float__(self):
+        return float(self.item())
+
+    def __int__(self):
+        return int(self.item())
+
+    def __index__(self):
+        if self._data.is_floating_point():
+            raise TypeError('only integer arrays can be converted to an index')
+        return int(self.item())
+
+    def item(self, *args):
+        a = self.asnumpy()
+        return a.item(*args)
+
+    def asscalar(self):
+        return self.item()
+
+    @property
+    def dtype(self):
+        return onp.dtype(NDArray.dtype.fget(self)) if self._data.dtype != torch.bfloat16 else NDArray.dtype.fget(self)
+
+    @property
+    def T(self):
+        return self.transpose()
+
+    @property
+    def itemsize(self):
+        return self._data.element_size()
+
+    @property
+    def nbytes(self):
+        return self._data.element_size() * self.size
+
+    @property
+    def strides(self):
+        return tuple(s * self._data.element_size() for s in self._data.stride())
+
+    # ---- conversions
+    def as_nd_ndarray(self):
+        return NDArray(self._data)
+
+    def as_np_ndarray(self):
+        return self
+
+    def astype(self, dtype, order='K', casting='unsafe', subok=True, copy=True):
+        td = torch_dtype(dtype)
+        if not copy and td == self._data.dtype:
+            return self
+        return _np_out(_reg.invoke_fn(lambda t: t.to(td) if t.dtype != td else t.clone(), [self]))
+
+    def copy(self, order='C'):
+        return _np_out(_reg.invoke_fn(lambda t: t.clone(), [self]))
+
+    def detach(self):
+        return ndarray(self._data.detach())
+
+    def tolist(self):
+        return self.asnumpy().tolist()
+
+    def as_in_ctx(self, ctx):
+        return _np_out(NDArray.as_in_context(self, ctx))
+
+    as_in_context = as_in_ctx
+
+    def to_device(self, device):
+        return self.as_in_ctx(device)
+
+    def copyto(self, other):
+        r = NDArray.copyto(self, other)
+        return _np_out(r)
+
+    # ---- arithmetic
+    def __add__(self, o):
+        return add(self, o)
+
+    def __radd__(self, o):
+        return add(o, self)
+
+    def __iadd__(self, o):
+        return _inplace(self, add(self, o))
+
+    def __sub__(self, o):
+        return subtract(self, o)
+
+    def __rsub__(self, o):
+        return subtract(o, self)
+
+    def __isub__(self, o):
+        return _inplace(self, subtract(self, o))
+
+    def __mul__(self, o):
+        return multiply(self, o)
+
+    def __rmul__(self, o):
+        return multiply(o, self)
+
+    def __imul__(self, o):
+        return _inplace(self, multiply(self, o))
+
+    def __truediv__(self, o):
+        return true_divide(self, o)
+
+    def __rtruediv__(self, o):
+        return true_divide(o, self)
+
+    def __itruediv__(self, o):
+        return _inplace(self, true_divide(self, o))
+
+    def __floordiv__(self, o):
+        return floor_divide(self, o)
+
+    def __rfloordiv__(self, o):
+        return floor_divide(o, self)
+
+    def __mod__(self, o):
+        return mod(self, o)
+
+    def __rmod__(self, o):
+        return mod(o, self)
+
+    def __imod__(self, o):
+        return _inplace(self, mod(self, o))
+
+    def __pow__(self, o):
+        return power(self, o)
+
+    def __rpow__(self, o):
+        return power(o, self)
+
+    def __matmul__(self, o):
+        return matmul(self, o)
+
+    def __rmatmul__(self, o):
+        return matmul(o, self)
+
+    def __neg__(self):
+        return negative(self)
+
+    def __pos__(self):
+        return self
+
+    def __abs__(self):
+        return absolute(self)
+
+    def __invert__(self):
+        return invert(self)
+
+    def __and__(self, o):
+        return bitwise_and(self, o)
+
+    def __or__(self, o):
+        return bitwise_or(self, o)
+
+    def __xor__(self, o):
+        return bitwise_xor(self, o)
+
+    def __rand__(self, o):
+        return bitwise_and(o, self)
+
+    def __ror__(self, o):
+        return bitwise_or(o, self)
+
+    def __rxor__(self, o):
+        return bitwise_xor(o, self)
+
+    def __lshift__(self, o):
+        return _binary('bitwise_left_shift', self, o)
+
+    def __rshift__(self, o):
+        return _binary('bitwise_right_shift', self, o)
+
+    def __eq__(self, o):
+        if o is None:
+            return False
+        return equal(self, o)
+
+    def __ne__(self, o):
+        if o is None:
+            return True
+        return not_equal(self, o)
+
+    def __gt__(self, o):
+        return greater(self, o)
+
+    def __ge__(self, o):
+        return greater_equal(self, o)
+
+    def __lt__(self, o):
+        return less(self, o)
+
+    def __le__(self, o):
+        return less_equal(self, o)
+
+    # ---- fluent methods
+    def reshape(self, *shape, order='C', **kwargs):
+        if len(shape) == 1 and isinstance(shape[0], (list, tuple)):
+            shape = tuple(shape[0])
+        if not shape:
+            shape = kwargs.get('newshape', kwargs.get('shape', ()))
+        return reshape(self, shape, order=order)
+
+    def reshape_like(self, other):
+        return reshape(self, other.shape)
+
+    def transpose(self, *axes):
+        if len(axes) == 1 and isinstance(axes[0], (list, tuple)):
+            axes = tuple(axes[0])
+        elif len(axes) == 1 and axes[0] is None:
+            axes = ()
+        return transpose(self, axes or None)
+
+    def swapaxes(self, axis1, axis2):
+        return swapaxes(self, axis1, axis2)
+
+    def flatten(self, order='C'):
+        return ravel(self, order)
+
+    def ravel(self, order='C'):
+        return ravel(self, order)
+
+    def squeeze(self, axis=None):
+        return squeeze(self, axis)
+
+    def expand_dims(self, axis):
+        return expand_dims(self, axis)
+
+    def broadcast_to(self, shape):
+        return broadcast_to(self, shape)
+
+    def repeat(self, repeats, axis=None):
+        return repeat(self, repeats, axis)
+
+    def tile(self, reps):
+        return tile(self, reps)
+
+    def flip(self, axis=None):
+        return flip(self, axis)
+
+    def sum(self, axis=None, dtype=None, out=None, keepdims=False):
+        return sum(self, axis=axis, dtype=dtype, out=out, keepdims=keepdims)
+
+    def prod(self, axis=None, dtype=None, out=None, keepdims=False):
+        return prod(self, axis=axis, dtype=dtype, out=out, keepdims=keepdims)
+
+    def mean(self, axis=None, dtype=None, out=None, keepdims=False):
+        return mean(self, axis=axis, dtype=dtype, out=out, keepdims=keepdims)
+
+    def std(self, axis=None, dtype=None, out=None, ddof=0, keepdims=False):
+        return std(self, axis=axis, dtype=dtype, out=out, ddof=ddof, keepdims=keepdims)
+
+    def var(self, axis=None, dtype=None, out=None, ddof=0, keepdims=False):
+        return var(self, axis=axis, dtype=dtype, out=out, ddof=ddof, keepdims=keepdims)
+
+    def max(self, axis=None, out=None, keepdims=False):
+        return amax(self, axis=axis, out=out, keepdims=keepdims)
+
+    def min(self, axis=None, out=None, keepdims=False):
+        return amin(self, axis=axis, out=out, keepdims=keepdims)
+
+    def argmax(self, axis=None, out=None):
+        return argmax(self, axis, out)
+
+    def argmin(self, axis=None, out=None):
+        return argmin(self, axis, out)
+
+    def all(self, axis=None, out=None, keepdims=False):
+        return all(self, axis=axis, out=out, keepdims=keepdims)
+
+    def any(self, axis=None, out=None, keepdims=False):
+        return any(self, axis=axis, out=out, keepdims=keepdims)
+
+    def cumsum(self, axis=None, dtype=None, out=None):
+        return cumsum(self, axis, dtype, out)
+
+    def clip(self, min=None, max=None, out=None):  # pylint: disable=redefined-builtin
+        return clip(self, min, max, out)
+
+    def round(self, decimals=0, out=None):
+        return around(self, decimals, out)
+
+    def take(self, indices, axis=None, mode='raise'):
+        return take(self, indices, axis, mode)
+
+    def dot(self, b, out=None):
+        return dot(self, b, out)
+
+    def sort(self, axis=-1, kind=None, order=None):
+        r = sort(self, axis, kind, order)
+        self._data = r._data
+        return None
+
+    def argsort(self, axis=-1, kind=None, order=None):
+        return argsort(self, axis, kind, order)
+
+    def nonzero(self):
+        return nonzero(self)
+
+    def diagonal(self, offset=0, axis1=0, axis2=1):
+        return diagonal(self, offset, axis1, axis2)
+
+    def trace(self, offset=0, axis1=0, axis2=1):
+        return trace(self, offset, axis1, axis2)
+
+    def square(self):
+        return square(self)
+
+    def sqrt(self):
+        return sqrt(self)
+
+    def exp(self):
+        return exp(self)
+
+    def log(self):
+        return log(self)
+
+    def abs(self):
+        return absolute(self)
+
+    def sign(self):
+        return sign(self)
+
+    def tanh(self):
+        return tanh(self)
+
+    def sigmoid(self):
+        return _call('_npi_sigmoid', self)
+
+    def fill(self, value):
+        with torch.no_grad():
+            self._data.fill_(value)
+
+
+def _inplace(a, r):
+    if _state.STATE.recording:
+        a._data = r._data.to(a._data.dtype)
+    else:
+        with torch.no_grad():
+            a._data.copy_(r._data)
+    return a
+
+
+def _rebuild_np(a):
+    return ndarray(torch.from_numpy(onp.ascontiguousarray(a)))
+
+
+# ---------------------------------------------------------------------------
+# creation
+# ---------------------------------------------------------------------------
+
+@_export
+def array(object, dtype=None, ctx=None, copy=True):  # pylint: disable=redefined-builtin
+    """Create an ndarray.  NumPy/mx.np inputs keep their dtype; Python data default to float32."""
+    if ctx is None:
+        ctx = current_context()
+    if isinstance(object, NDArray):
+        t = object._data.detach().to(ctx.torch_device)
+        if dtype is not None:
+            t = t.to(torch_dtype(dtype))
+        if copy and t.data_ptr() == object._data.data_ptr():
+            t = t.clone()
+        return ndarray(t)
+    if isinstance(object, (list, tuple)) and builtins.any(isinstance(x, NDArray) for x in object):
+        object = [x.asnumpy() if isinstance(x, NDArray) else x for x in object]
+    if dtype is None:
+        dtype = object.dtype if isinstance(object, onp.ndarray) else (
+            object.dtype if isinstance(object, onp.generic) else onp.float32)
+    if isinstance(dtype, str) and dtype == 'bfloat16':
+        t = torch.as_tensor(onp.array(object, dtype=onp.float32)).to(torch.bfloat16)
+    else:
+        t = torch.as_tensor(onp.array(object, dtype=dtype, order="C"))
+    return ndarray(t.to(ctx.torch_device))
+
+
+@_export
+def asarray(obj, dtype=None, ctx=None):
+    if isinstance(obj, ndarray) and dtype is None and (ctx is None or ctx == obj.context):
+        return obj
+    return array(obj, dtype=dtype, ctx=ctx, copy=False)
+
+
+def _shape(shape):
+    return (shape,) if isinstance(shape, int) else tuple(shape)
+
+
+@_export
+def zeros(shape, dtype=None, order='C', ctx=None):
+    return _call('_npi_zeros', shape=_shape(shape), ctx=_ctx(ctx), dtype=dtype or 'float32')
+
+
+@_export
+def ones(shape, dtype=None, order='C', ctx=None):
+    return _call('_npi_ones', shape=_shape(shape), ctx=_ctx(ctx), dtype=dtype or 'float32')
+
+
+@_export
+def empty(shape, dtype=None, order='C', ctx=None):
+    return zeros(shape, dtype, order, ctx)
+
+
+@_export
+def full(shape, fill_value, dtype=None, order='C', ctx=None, out=None):
+    if isinstance(fill_value, NDArray):
+        return broadcast_to(fill_value.astype(dtype) if dtype else fill_value, _shape(shape))
+    if dtype is None:
+        dtype = 'bool' if isinstance(fill_value, bool) else ('int64' if isinstance(fill_value, int) else 'float32')
+    return _call('_npi_full', shape=_shape(shape), ctx=_ctx(ctx), dtype=dtype, value=_py(fill_value), out=out)
+
+
+@_export
+def zeros_like(a, dtype=None, order='C', ctx=None, out=None):
+    return _call('_npi_zeros_like', a, dtype=dtype, out=out)
+
+
+@_export
+def ones_like(a, dtype=None, order='C', ctx=None, out=None):
+    return _call('_npi_ones_like', a, dtype=dtype, out=out)
+
+
+@_export
+def empty_like(prototype, dtype=None, order='C', subok=False, shape=None):
+    return zeros(shape, dtype or prototype.dtype, ctx=prototype.context) if shape is not None else \
+        zeros_like(prototype, dtype=dtype)
+
+
+@_export
+def full_like(a, fill_value, dtype=None, order='C', ctx=None, out=None):
+    return _call('_npi_full_like', a, fill_value=_py(fill_value), dtype=dtype, out=out)
+
+
+@_export
+def arange(start, stop=None, step=1, dtype=None, ctx=None):
+    if stop is None:
+        start, stop = 0, start
+    return _call('_npi_arange', start=float(start), stop=float(stop), step=float(step), ctx=_ctx(ctx),
+                 dtype=dtype or 'float32')
+
+
+@_export
+def linspace(start, stop, num=50, endpoint=True, retstep=False, dtype=None, axis=0, ctx=None):
+    r = _call('_npi_linspace', start=float(start), stop=float(stop), num=int(num), endpoint=endpoint,
+              ctx=_ctx(ctx), dtype=dtype or 'float32')
+    if retstep:
+        step = (stop - start) / ((num - 1) if endpoint else num) if num > 1 else float('nan')
+        return r, step
+    return r
+
+
+@_export
+def logspace(start, stop, num=50, endpoint=True, base=10.0, dtype=None, axis=0, ctx=None):
+    return _call('_npi_logspace', start=float(start), stop=float(stop), num=int(num), endpoint=endpoint,
+                 base=float(base), ctx=_ctx(ctx), dtype=dtype or 'float32')
+
+
+@_export
+def eye(N, M=None, k=0, dtype=None, ctx=None, **kwargs):
+    return _call('_npi_eye', N=N, M=M, k=k, ctx=_ctx(ctx), dtype=dtype or 'float32')
+
+
+@_export
+def identity(n, dtype=None, ctx=None):
+    return eye(n, dtype=dtype, ctx=ctx)
+
+
+@_export
+def tri(N, M=None, k=0, dtype=None, ctx=None):
+    return _call('_npi_tri', N=N, M=M, k=k, ctx=_ctx(ctx), dtype=dtype or 'float32')
+
+
+@_export
+def indices(dimensions, dtype=None, ctx=None):
+    return _call('_npi_indices', dimensions=tuple(dimensions), ctx=_ctx(ctx), dtype=dtype or 'int64')
+
+
+@_export
+def copy(a):
+    return _as_nd(a).copy()
+
+
+@_export
+def shape(a):
+    return tuple(a.shape) if hasattr(a, 'shape') else onp.shape(a)
+
+
+@_export
+def size(a, axis=None):
+    return a.size if axis is None else a.shape[axis]
+
+
+@_export
+def ndim(a):
+    return a.ndim if hasattr(a, 'ndim') else onp.ndim(a)
+
+
+@_export
+def meshgrid(*xi, **kwargs):
+    indexing = kwargs.get('indexing', 'xy')
+    arrs = [_as_nd(x) for x in xi]
+    return [_np_out(_reg.invoke_fn(lambda *ts, i=i: torch.meshgrid(*ts, indexing=indexing)[i].clone(), arrs))
+            for i in range(len(arrs))]
+
+
+# ---------------------------------------------------------------------------
+# ufuncs
+# ---------------------------------------------------------------------------
+
+def _unary(name, x, out=None, **kw):
+    if _is_scalar(x):
+        return getattr(onp, name)(x)
+    return _call('_npi_' + name, _as_nd(x), out=out, **kw)
+
+
+def _binary(name, x1, x2, out=None):
+    if _is_scalar(x1) and _is_scalar(x2):
+        f = getattr(onp, {'true_divide': 'true_divide', 'mod': 'mod'}.get(name, name))
+        return f(x1, x2)
+    if _is_scalar(x2):
+        return _call('_npi_%s_scalar' % name, _as_nd(x1), scalar=_py(x2), out=out)
+    if _is_scalar(x1):
+        return _call('_npi_%s_scalar' % name, _as_nd(x2), scalar=_py(x1), reverse=True, out=out)
+    ctx = _first_ctx(x1, x2)
+    return _call('_npi_' + name, _as_nd(x1, ctx), _as_nd(x2, ctx), out=out)
+
+
+def _mk_unary(name, opname=None):
+    opname = opname or name
+
+    def f(x, out=None, **kwargs):
+        return _unary(opname, x, out)
+    f.__name__ = name
+    f.__doc__ = 'Element-wise ``%s`` (NumPy semantics).' % name
+    globals()[name] = f
+    __all__.append(name)
+
+
+def _mk_binary(name, opname=None):
+    opname = opname or name
+
+    def f(x1, x2, out=None, **kwargs):
+        return _binary(opname, x1, x2, out)
+    f.__name__ = name
+    f.__doc__ = 'Element-wise ``%s`` with broadcasting (NumPy semantics).' % name
+    globals()[name] = f
+    __all__.append(name)
+
+
+for _n in ('negative', 'absolute', 'fabs', 'sign', 'rint', 'ceil', 'floor', 'trunc', 'fix', 'square', 'sqrt',
+           'cbrt', 'exp', 'expm1', 'log', 'log2', 'log10', 'log1p', 'sin', 'cos', 'tan', 'arcsin', 'arccos', 'arctan',
+           'sinh', 'cosh', 'tanh', 'arcsinh', 'arccosh', 'arctanh', 'degrees', 'rad2deg', 'radians', 'deg2rad',
+           'reciprocal', 'logical_not', 'bitwise_not', 'invert', 'isnan', 'isinf', 'isfinite', 'isposinf',
+           'isneginf', 'signbit', 'positive'):
+    _mk_unary(_n)
+_mk_unary('abs', 'absolute')
+
+for _n in ('add', 'subtract', 'multiply', 'true_divide', 'floor_divide', 'mod', 'fmod', 'power', 'maximum',
+           'minimum', 'fmax', 'fmin', 'arctan2', 'hypot', 'copysign', 'ldexp', 'lcm', 'gcd', 'bitwise_and',
+           'bitwise_or', 'bitwise_xor', 'logical_and', 'logical_or', 'logical_xor', 'equal', 'not_equal', 'greater',
+           'greater_equal', 'less', 'less_equal', 'float_power', 'heaviside'):
+    _mk_binary(_n)
+_mk_binary('divide', 'true_divide')
+_mk_binary('remainder', 'mod')
+
+
+@_export
+def around(x, decimals=0, out=None, **kwargs):
+    if _is_scalar(x):
+        return onp.around(x, decimals)
+    return _call('_npi_around', _as_nd(x), decimals=decimals, out=out)
+
+
+round = around  # noqa: A001  pylint: disable=redefined-builtin
+round_ = around
+__all__ += ['round', 'round_']
+
+
+@_export
+def nan_to_num(x, copy=True, nan=0.0, posinf=None, neginf=None, **kwargs):
+    r = _call('_npi_nan_to_num', _as_nd(x), copy=copy, nan=nan, posinf=posinf, neginf=neginf)
+    if not copy and isinstance(x, NDArray):
+        return _inplace(x, r)
+    return r
+
+
+@_export
+def clip(a, a_min=None, a_max=None, out=None):
+    if a_min is None and a_max is None:
+        raise ValueError('array_clip: must set either max or min')
+    return _call('_npi_clip', _as_nd(a), a_min=None if a_min is None else float(a_min),
+                 a_max=None if a_max is None else float(a_max), out=out)
+
+
+@_export
+def where(condition, x=None, y=None):
+    if x is None and y is None:
+        return nonzero(condition)
+    if _is_scalar(condition):
+        return (x if condition else y)
+    xs, ys = _is_scalar(x), _is_scalar(y)
+    if xs and ys:
+        return _call('_npi_where_scalar2', condition, x=_py(x), y=_py(y))
+    if xs:
+        return _call('_npi_where_lscalar', condition, _as_nd(y), scalar=_py(x))
+    if ys:
+        return _call('_npi_where_rscalar', condition, _as_nd(x), scalar=_py(y))
+    return _call('_npi_where', condition, _as_nd(x), _as_nd(y))
+
+
+# ---------------------------------------------------------------------------
+# reductions
+# ---------------------------------------------------------------------------
+
+def _axis(axis):
+    if isinstance(axis, list):
+        return tuple(axis)
+    return axis
+
+
+@_export
+def sum(a, axis=None, dtype=None, out=None, keepdims=False, initial=None, where=None):  # pylint: disable=redefined-builtin
+    return _call('_np_sum', _as_nd(a), axis=_axis(axis), dtype=dtype, keepdims=keepdims, initial=initial, out=out)
+
+
+@_export
+def prod(a, axis=None, dtype=None, out=None, keepdims=False, initial=None):
+    return _call('_np_prod', _as_nd(a), axis=_axis(axis), dtype=dtype, keepdims=keepdims, initial=initial, out=out)
+
+
+@_export
+def mean(a, axis=None, dtype=None, out=None, keepdims=False):
+    return _call('_npi_mean', _as_nd(a), axis=_axis(axis), dtype=dtype, keepdims=keepdims, out=out)
+
+
+@_export
+def std(a, axis=None, dtype=None, out=None, ddof=0, keepdims=False):
+    return _call('_npi_std', _as_nd(a), axis=_axis(axis), dtype=dtype, ddof=ddof, keepdims=keepdims, out=out)
+
+
+@_export
+def var(a, axis=None, dtype=None, out=None, ddof=0, keepdims=False):
+    return _call('_npi_var', _as_nd(a), axis=_axis(axis), dtype=dtype, ddof=ddof, keepdims=keepdims, out=out)
+
+
+@_export
+def amax(a, axis=None, out=None, keepdims=False, initial=None):
+    return _call('_np_max', _as_nd(a), axis=_axis(axis), keepdims=keepdims, out=out)
+
+
+@_export
+def amin(a, axis=None, out=None, keepdims=False, initial=None):
+    return _call('_np_min', _as_nd(a), axis=_axis(axis), keepdims=keepdims, out=out)
+
+
+max = amax  # noqa: A001  pylint: disable=redefined-builtin
+min = amin  # noqa: A001  pylint: disable=redefined-builtin
+__all__ += ['max', 'min']
+
+
+@_export
+def ptp(a, axis=None, keepdims=False):
+    return subtract(amax(a, axis, keepdims=keepdims), amin(a, axis, keepdims=keepdims))
+
+
+@_export
+def all(a, axis=None, out=None, keepdims=False):  # pylint: disable=redefined-builtin
+    return _call('_np_all', _as_nd(a), axis=_axis(axis), keepdims=keepdims, out=out)
+
+
+@_export
+def any(a, axis=None, out=None, keepdims=False):  # pylint: disable=redefined-builtin
+    return _call('_np_any', _as_nd(a), axis=_axis(axis), keepdims=keepdims, out=out)
+
+
+alltrue = all
+__all__.append('alltrue')
+
+
+@_export
+def argmax(a, axis=None, out=None, keepdims=False):
+    return _call('_npi_argmax', _as_nd(a), axis=axis, keepdims=keepdims, out=out)
+
+
+@_export
+def argmin(a, axis=None, out=None, keepdims=False):
+    return _call('_npi_argmin', _as_nd(a), axis=axis, keepdims=keepdims, out=out)
+
+
+@_export
+def cumsum(a, axis=None, dtype=None, out=None):
+    return _call('_np_cumsum', _as_nd(a), axis=axis, dtype=dtype, out=out)
+
+
+@_export
+def cumprod(a, axis=None, dtype=None, out=None):
+    return _call('_npi_cumprod', _as_nd(a), axis=axis, dtype=dtype, out=out)
+
+
+@_export
+def average(a, axis=None, weights=None, returned=False, out=None):
+    if weights is None:
+        return _call('_npi_average', _as_nd(a), axis=_axis(axis), returned=returned)
+    return _call('_npi_average', _as_nd(a), _as_nd(weights), axis=_axis(axis), returned=returned, weighted=True)
+
+
+@_export
+def quantile(a, q, axis=None, out=None, overwrite_input=None, interpolation='linear', keepdims=False):
+    q = q.tolist() if isinstance(q, NDArray) else q
+    return _call('_npi_quantile', _as_nd(a), q=q, axis=_axis(axis), interpolation=interpolation, keepdims=keepdims,
+                 out=out)
+
+
+@_export
+def percentile(a, q, axis=None, out=None, overwrite_input=None, interpolation='linear', keepdims=False):
+    q = q.tolist() if isinstance(q, NDArray) else q
+    return _call('_npi_percentile', _as_nd(a), q=q, axis=_axis(axis), interpolation=interpolation,
+                 keepdims=keepdims, out=out)
+
+
+@_export
+def median(a, axis=None, out=None, overwrite_input=None, keepdims=False):
+    return _call('_npi_median', _as_nd(a), axis=_axis(axis), keepdims=keepdims, out=out)
+
+
+@_export
+def count_nonzero(a, axis=None):
+    return sum(not_equal(a, 0), axis=axis, dtype='int64')
+
+
+# ---------------------------------------------------------------------------
+# manipulation
+# ---------------------------------------------------------------------------
+
+@_export
+def reshape(a, newshape, order='C'):
+    if isinstance(newshape, int):
+        newshape = (newshape,)
+    return _call('_np_reshape', _as_nd(a), newshape=tuple(newshape), order=order)
+
+
+@_export
+def transpose(a, axes=None):
+    return _call('_np_transpose', _as_nd(a), axes=None if axes is None else tuple(axes))
+
+
+@_export
+def swapaxes(a, axis1, axis2):
+    return _call('_npi_swapaxes', _as_nd(a), axis1=axis1, axis2=axis2)
+
+
+@_export
+def moveaxis(a, source, destination):
+    return _call('_npi_moveaxis', _as_nd(a), source=_axis(source), destination=_axis(destination))
+
+
+@_export
+def rollaxis(a, axis, start=0):
+    return _call('_npi_rollaxis', _as_nd(a), axis=axis, start=start)
+
+
+@_export
+def expand_dims(a, axis):
+    return _call('_npi_expand_dims', _as_nd(a), axis=_axis(axis))
+
+
+@_export
+def squeeze(a, axis=None):
+    return _call('_np_squeeze', _as_nd(a), axis=_axis(axis))
+
+
+@_export
+def flip(m, axis=None, out=None):
+    return _call('_npi_flip', _as_nd(m), axis=_axis(axis), out=out)
+
+
+@_export
+def flipud(m):
+    return flip(m, 0)
+
+
+@_export
+def fliplr(m):
+    return flip(m, 1)
+
+
+@_export
+def roll(a, shift, axis=None):
+    return _call('_npi_roll', _as_nd(a), shift=_axis(shift), axis=_axis(axis))
+
+
+@_export
+def rot90(m, k=1, axes=(0, 1)):
+    return _call('_npi_rot90', _as_nd(m), k=k, axes=tuple(axes))
+
+
+@_export
+def tile(A, reps):
+    return _call('_npi_tile', _as_nd(A), reps=(reps,) if isinstance(reps, int) else tuple(reps))
+
+
+@_export
+def repeat(a, repeats, axis=None):
+    return _call('_np_repeat', _as_nd(a), repeats=repeats.tolist() if isinstance(repeats, NDArray) else repeats,
+                 axis=axis)
+
+
+@_export
+def broadcast_to(array, shape):  # pylint: disable=redefined-outer-name
+    return _call('_npi_broadcast_to', _as_nd(array), shape=_shape(shape))
+
+
+@_export
+def broadcast_arrays(*args):
+    shp = onp.broadcast_shapes(*[a.shape for a in args])
+    return [broadcast_to(a, shp) for a in args]
+
+
+@_export
+def ravel(x, order='C'):
+    return _call('_npi_ravel', _as_nd(x), order=order)
+
+
+@_export
+def tril(m, k=0):
+    return _call('_npi_tril', _as_nd(m), k=k)
+
+
+@_export
+def triu(m, k=0):
+    return _call('_npi_triu', _as_nd(m), k=k)
+
+
+@_export
+def diag(v, k=0):
+    return _call('_np_diag', _as_nd(v), k=k)
+
+
+@_export
+def diagflat(v, k=0):
+    return _call('_np_diagflat', _as_nd(v), k=k)
+
+
+@_export
+def diagonal(a, offset=0, axis1=0, axis2=1):
+    return _call('_np_diagonal', _as_nd(a), offset=offset, axis1=axis1, axis2=axis2)
+
+
+@_export
+def trace(a, offset=0, axis1=0, axis2=1, out=None):
+    return _call('_np_trace', _as_nd(a), offset=offset, axis1=axis1, axis2=axis2, out=out)
+
+
+@_export
+def pad(x, pad_width, mode='constant', **kwargs):
+    pw = pad_width.tolist() if isinstance(pad_width, NDArray) else pad_width
+    return _call('_npi_pad', _as_nd(x), pad_width=pw, mode=mode,
+                 constant_values=float(kwargs.get('constant_values', 0)))
+
+
+@_export
+def take(a, indices, axis=None, mode='raise', out=None):
+    if _is_scalar(indices):
+        r = _call('_npi_take', _as_nd(a), array(indices, dtype='int64', ctx=a.context), axis=axis, mode=mode)
+        return r
+    return _call('_npi_take', _as_nd(a), _as_nd(indices), axis=axis, mode=mode, out=out)
+
+
+@_export
+def take_along_axis(arr, indices, axis):
+    return _call('_npi_take_along_axis', arr, indices, axis=axis)
+
+
+@_export
+def concatenate(seq, axis=0, out=None):
+    return _call('_npi_concatenate', *[_as_nd(x) for x in seq], axis=axis, out=out)
+
+
+@_export
+def append(arr, values, axis=None):
+    return concatenate([arr, values], axis=axis)
+
+
+@_export
+def stack(arrays, axis=0, out=None):
+    return _call('_npi_stack', *[_as_nd(x) for x in arrays], axis=axis, out=out)
+
+
+@_export
+def vstack(arrays, out=None):
+    return _call('_npi_vstack', *[_as_nd(x) for x in arrays], out=out)
+
+
+row_stack = vstack
+__all__.append('row_stack')
+
+
+@_export
+def hstack(arrays):
+    return _call('_npi_hstack', *[_as_nd(x) for x in arrays])
+
+
+@_export
+def dstack(arrays):
+    return _call('_npi_dstack', *[_as_nd(x) for x in arrays])
+
+
+@_export
+def column_stack(tup):
+    return _call('_npi_column_stack', *[_as_nd(x) for x in tup])
+
+
+def _split_call(name, ary, ios, axis):
+    ios = ios.tolist() if isinstance(ios, NDArray) else ios
+    ios = list(ios) if isinstance(ios, (list, tuple)) else int(ios)
+    r = _call('_npi_' + name, ary, indices_or_sections=ios, axis=axis)
+    return list(r) if isinstance(r, (list, tuple)) else [r]
+
+
+@_export
+def split(ary, indices_or_sections, axis=0):
+    return _split_call('split', ary, indices_or_sections, axis)
+
+
+@_export
+def array_split(ary, indices_or_sections, axis=0):
+    return _split_call('array_split', ary, indices_or_sections, axis)
+
+
+@_export
+def hsplit(ary, indices_or_sections):
+    return _split_call('hsplit', ary, indices_or_sections, 1)
+
+
+@_export
+def vsplit(ary, indices_or_sections):
+    return _split_call('vsplit', ary, indices_or_sections, 0)
+
+
+@_export
+def dsplit(ary, indices_or_sections):
+    return _split_call('dsplit', ary, indices_or_sections, 2)
+
+
+@_export
+def atleast_1d(*arys):
+    r = [a if a.ndim >= 1 else reshape(a, (1,)) for a in map(_as_nd, arys)]
+    return r[0] if len(r) == 1 else r
+
+
+@_export
+def atleast_2d(*arys):
+    r = []
+    for a in map(_as_nd, arys):
+        r.append(a if a.ndim >= 2 else reshape(a, (1, -1) if a.ndim == 1 else (1, 1)))
+    return r[0] if len(r) == 1 else r
+
+
+@_export
+def atleast_3d(*arys):
+    r = []
+    for a in map(_as_nd, arys):
+        if a.ndim == 0:
+            a = reshape(a, (1, 1, 1))
+        elif a.ndim == 1:
+            a = reshape(a, (1, -1, 1))
+        elif a.ndim == 2:
+            a = expand_dims(a, 2)
+        r.append(a)
+    return r[0] if len(r) == 1 else r
+
+
+@_export
+def sort(a, axis=-1, kind=None, order=None):
+    return _call('_npi_sort', _as_nd(a), axis=axis, kind=kind)
+
+
+@_export
+def argsort(a, axis=-1, kind=None, order=None):
+    return _call('_npi_argsort', _as_nd(a), axis=axis, kind=kind)
+
+
+@_export
+def diff(a, n=1, axis=-1, prepend=None, append=None):  # pylint: disable=redefined-outer-name
+    if prepend is not None or append is not None:
+        parts = ([_as_nd(prepend)] if prepend is not None else []) + [a] + \
+            ([_as_nd(append)] if append is not None else [])
+        a = concatenate(parts, axis=axis)
+    return _call('_npi_diff', _as_nd(a), n=n, axis=axis)
+
+
+@_export
+def ediff1d(ary, to_end=None, to_begin=None):
+    d = diff(ravel(ary))
+    parts = ([ravel(_as_nd(to_begin, ary.context))] if to_begin is not None else []) + [d] + \
+        ([ravel(_as_nd(to_end, ary.context))] if to_end is not None else [])
+    return concatenate(parts) if len(parts) > 1 else d
+
+
+@_export
+def cross(a, b, axisa=-1, axisb=-1, axisc=-1, axis=None):
+    return _call('_npi_cross', _as_nd(a), _as_nd(b), axisa=axisa, axisb=axisb, axisc=axisc, axis=axis)
+
+
+@_export
+def delete(arr, obj, axis=None):
+    o = obj.tolist() if isinstance(obj, NDArray) else obj
+    if isinstance(o, slice):
+        n = arr.shape[axis] if axis is not None else arr.size
+        o = list(range(n))[o]
+    return _call('_npi_delete', arr, obj=o, axis=axis)
+
+
+@_export
+def insert(arr, obj, values, axis=None):
+    o = obj.tolist() if isinstance(obj, NDArray) else obj
+    if isinstance(o, slice):
+        n = arr.shape[axis] if axis is not None else arr.size
+        o = list(range(n + 1))[o]
+    if _is_scalar(values):
+        return _call('_npi_insert_scalar', arr, obj=o, values=_py(values), axis=axis)
+    return _call('_npi_insert_tensor', arr, _as_nd(values, arr.context), obj=o, axis=axis)
+
+
+@_export
+def resize(a, new_shape):
+    new_shape = _shape(new_shape)
+    n = int(onp.prod(new_shape))
+    flat = ravel(a)
+    if flat.size == 0:
+        return zeros(new_shape, dtype=a.dtype, ctx=a.context)
+    reps = -(-n // flat.size)
+    return reshape(tile(flat, reps)[:n], new_shape)
+
+
+# ---------------------------------------------------------------------------
+# products
+# ---------------------------------------------------------------------------
+
+@_export
+def dot(a, b, out=None):
+    return _call('_np_dot', _as_nd(a), _as_nd(b), out=out)
+
+
+@_export
+def matmul(a, b, out=None, **kwargs):
+    return _call('_npi_matmul', _as_nd(a), _as_nd(b), out=out)
+
+
+@_export
+def tensordot(a, b, axes=2):
+    return _call('_npi_tensordot', _as_nd(a), _as_nd(b), axes=axes)
+
+
+@_export
+def inner(a, b):
+    return _call('_npi_inner', _as_nd(a), _as_nd(b))
+
+
+@_export
+def outer(a, b):
+    return _call('_npi_outer', _as_nd(a), _as_nd(b))
+
+
+@_export
+def vdot(a, b):
+    return _call('_npi_vdot', _as_nd(a), _as_nd(b))
+
+
+@_export
+def kron(a, b):
+    return _call('_npi_kron', _as_nd(a), _as_nd(b))
+
+
+@_export
+def einsum(*operands, **kwargs):
+    subscripts = operands[0]
+    return _call('_npi_einsum', *[_as_nd(x) for x in operands[1:]], subscripts=subscripts,
+                 optimize=kwargs.get('optimize', False), out=kwargs.get('out'))
+
+
+# ---------------------------------------------------------------------------
+# data-dependent shapes (imperative only)
+# ---------------------------------------------------------------------------
+
+def _host(a):
+    return a.asnumpy() if isinstance(a, NDArray) else onp.asarray(a)
+
+
+@_export
+def nonzero(a):
+    t = _as_nd(a)._data
+    return tuple(ndarray(x) for x in torch.nonzero(t, as_tuple=True))
+
+
+@_export
+def argwhere(a):
+    return ndarray(torch.nonzero(_as_nd(a)._data))
+
+
+@_export
+def flatnonzero(a):
+    return ndarray(torch.nonzero(_as_nd(a)._data.reshape(-1)).reshape(-1))
+
+
+@_export
+def unique(ar, return_index=False, return_inverse=False, return_counts=False, axis=None):
+    res = onp.unique(_host(ar), return_index, return_inverse, return_counts, axis)
+    ctx = ar.context if isinstance(ar, NDArray) else None
+    if isinstance(res, tuple):
+        return tuple(array(r, dtype=r.dtype, ctx=ctx) for r in res)
+    return array(res, dtype=res.dtype, ctx=ctx)
+
+
+@_export
+def bincount(x, weights=None, minlength=0):
+    t = _as_nd(x)._data
+    w = None if weights is None else _as_nd(weights)._data
+    return ndarray(torch.bincount(t.long(), w, minlength))
+
+
+@_export
+def histogram(a, bins=10, range=None, normed=None, weights=None, density=None):  # pylint: disable=redefined-builtin
+    b = _host(bins) if isinstance(bins, NDArray) else bins
+    h, e = onp.histogram(_host(a), b, range, density=density,
+                         weights=None if weights is None else _host(weights))
+    ctx = a.context if isinstance(a, NDArray) else None
+    return array(h, dtype=onp.int64 if h.dtype.kind in 'iu' else onp.float32, ctx=ctx), array(e, ctx=ctx)
+
+
+@_export
+def unravel_index(indices, shape, order='C'):
+    r = onp.unravel_index(_host(indices).astype(onp.int64), shape, order)
+    return tuple(array(x, dtype=onp.int64) for x in r)
+
+
+@_export
+def ravel_multi_index(multi_index, dims, mode='raise', order='C'):
+    r = onp.ravel_multi_index(tuple(_host(x).astype(onp.int64) for x in multi_index), dims, mode=mode, order=order)
+    return array(r, dtype=onp.int64)
+
+
+@_export
+def diag_indices_from(arr):
+    n = arr.shape[0]
+    return tuple(arange(n, dtype='int64', ctx=arr.context) for _ in range(arr.ndim))
+
+
+@_export
+def tril_indices(n, k=0, m=None):
+    r = onp.tril_indices(n, k, m)
+    return tuple(array(x, dtype=onp.int64) for x in r)
+
+
+@_export
+def triu_indices(n, k=0, m=None):
+    r = onp.triu_indices(n, k, m)
+    return tuple(array(x, dtype=onp.int64) for x in r)
+
+
+@_export
+def searchsorted(a, v, side='left', sorter=None):
+    ta = _as_nd(a)._data
+    tv = _as_nd(v, a.context)._data if not _is_scalar(v) else torch.tensor([v], dtype=ta.dtype)
+    r = torch.searchsorted(ta, tv.to(ta.dtype), right=(side == 'right'),
+                           sorter=None if sorter is None else _as_nd(sorter)._data)
+    return ndarray(r[0]) if _is_scalar(v) else ndarray(r)
+
+
+@_export
+def polyval(p, x):
+    r = zeros_like(x) if isinstance(x, NDArray) else 0.0
+    for c in (p if not isinstance(p, NDArray) else [p[i] for i in range(p.shape[0])]):
+        r = r * x + c
+    return r
+
+
+@_export
+def interp(x, xp, fp, left=None, right=None, period=None):
+    r = onp.interp(_host(x), _host(xp), _host(fp), left, right, period)
+    return array(r, dtype=onp.float32)
+
+
+# ---------------------------------------------------------------------------
+# window functions
+# ---------------------------------------------------------------------------
+
+@_export
+def hanning(M, dtype=None, ctx=None):
+    return array(onp.hanning(M), dtype=dtype or onp.float32, ctx=ctx)
+
+
+@_export
+def hamming(M, dtype=None, ctx=None):
+    return array(onp.hamming(M), dtype=dtype or onp.float32, ctx=ctx)
+
+
+@_export
+def blackman(M, dtype=None, ctx=None):
+    return array(onp.blackman(M), dtype=dtype or onp.float32, ctx=ctx)
+
+
+# ---------------------------------------------------------------------------
+# memory / misc
+# ---------------------------------------------------------------------------
+
+@_export
+def shares_memory(a, b, max_work=None):
+    ta, tb = a._data, b._data
+    sa = ta.untyped_storage().data_ptr()
+    return sa == tb.untyped_storage().data_ptr()
+
+
+may_share_memory = shares_memory
+__all__.append('may_share_memory')
+
+
+@_export
+def array_equal(a1, a2, equal_nan=False):
+    if tuple(a1.shape) != tuple(a2.shape):
+        return False
+    return bool(all(equal(a1, a2)).item())
+
+
+@_export
+def allclose(a, b, rtol=1e-05, atol=1e-08, equal_nan=False):
+    return bool(onp.allclose(_host(a), _host(b), rtol, atol, equal_nan))
+
+
+@_export
+def isclose(a, b, rtol=1e-05, atol=1e-08, equal_nan=False):
+    ta, tb = _as_nd(a)._data, _as_nd(b)._data
+    return ndarray(torch.isclose(ta, tb.to(ta.dtype), rtol, atol, equal_nan))
+
+
+@_export
+def result_type(*arrays_and_dtypes):
+    return onp.result_type(*[a.dtype if isinstance(a, NDArray) else a for a in arrays_and_dtypes])
+
+
+dtype = onp.dtype
+float16, float32, float64 = onp.float16, onp.float32, onp.float64
+int8, int16, int32, int64, uint8 = onp.int8, onp.int16, onp.int32, onp.int64, onp.uint8
+bool_ = onp.bool_
+pi, e, inf, nan, newaxis, euler_gamma = onp.pi, onp.e, onp.inf, onp.nan, None, onp.euler_gamma
+PZERO, NZERO = 0.0, -0.0
+__all__ += ['dtype', 'float16', 'float32', 'float64', 'int8', 'int16', 'int32', 'int64', 'uint8', 'bool_',
+            'pi', 'e', 'inf', 'nan', 'newaxis', 'euler_gamma', 'PZERO', 'NZERO']
+
+
+def _install_nd_hooks():
+    """Let legacy NDArray code create mx.np arrays (``as_np_ndarray``) and pickle them."""
+    _reg._NP_CLS[0] = ndarray
+
+
+_install_nd_hooks()

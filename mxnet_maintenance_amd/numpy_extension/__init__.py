@@ -1,1 +1,160 @@
-"""numpy_extension (being implemented)."""
+"""``mx.npx``: MXNet-specific operators for the NumPy interface.
+
+Parity: python/mxnet/numpy_extension/{__init__,_op,utils,random,image}.py and
+src/operator/numpy_extension.  Neural-network operators are the same registered
+kernels as the legacy ``mx.nd`` ops (HIP kernels for conv/BN/pool on gfx950),
+returning ``mx.np.ndarray``; given Symbols they build graph nodes so they work in
+hybridized blocks.
+"""
+import functools
+
+from .. import _state
+from ..context import cpu, gpu, num_gpus, current_context, cpu_pinned  # noqa: F401
+from ..util import (set_np, reset_np, is_np_array, is_np_shape, use_np, use_np_array, use_np_shape,  # noqa: F401
+                    np_array, np_shape, set_np_shape)
+from ..ndarray.ndarray import NDArray, waitall  # noqa: F401
+from ..ndarray import register as _reg
+from ..ops import registry as _registry
+
+
+def _is_sym(x):
+    from ..symbol.symbol import Symbol
+    return isinstance(x, Symbol)
+
+
+def _op(opname, defaults=None, doc=None, pyname=None):
+    def f(*args, **kwargs):
+        for k, v in (defaults or {}).items():
+            kwargs.setdefault(k, v)
+        if any(_is_sym(a) for a in args) or any(_is_sym(v) for v in kwargs.values()):
+            from ..symbol.symbol import _op_func
+            return _op_func(opname)(*args, **kwargs)
+        from ..numpy.multiarray import _np_out
+        return _np_out(_reg.invoke_by_name(opname, args, kwargs))
+    f.__name__ = pyname or opname
+    f.__doc__ = doc or 'npx wrapper of operator ``%s`` (returns mx.np.ndarray).' % opname
+    return f
+
+
+_MAP = {
+    'activation': ('Activation', None), 'relu': ('Activation', {'act_type': 'relu'}),
+    'sigmoid': ('Activation', {'act_type': 'sigmoid'}), 'softmax': ('softmax', None),
+    'log_softmax': ('log_softmax', None), 'masked_softmax': ('masked_softmax', None),
+    'masked_log_softmax': ('masked_log_softmax', None), 'batch_norm': ('BatchNorm', None),
+    'convolution': ('Convolution', None), 'deconvolution': ('Deconvolution', None), 'pooling': ('Pooling', None),
+    'dropout': ('Dropout', None), 'embedding': ('Embedding', None), 'fully_connected': ('FullyConnected', None),
+    'layer_norm': ('LayerNorm', None), 'group_norm': ('GroupNorm', None), 'instance_norm': ('InstanceNorm', None),
+    'leaky_relu': ('LeakyReLU', None), 'one_hot': ('one_hot', None), 'pick': ('pick', None), 'topk': ('topk', None),
+    'rnn': ('RNN', None), 'arange_like': ('_contrib_arange_like', None), 'batch_dot': ('batch_dot', None),
+    'batch_flatten': ('Flatten', None), 'broadcast_like': ('broadcast_like', None), 'gamma': ('gamma', None),
+    'gammaln': ('gammaln', None), 'erf': ('erf', None), 'erfinv': ('erfinv', None),
+    'sequence_mask': ('SequenceMask', None), 'sequence_last': ('SequenceLast', None),
+    'sequence_reverse': ('SequenceReverse', None), 'slice': ('slice', None), 'smooth_l1': ('smooth_l1', None),
+    'stop_gradient': ('BlockGrad', None), 'shape_array': ('shape_array', None), 'roi_pooling': ('ROIPooling', None),
+    'roi_align': ('_contrib_ROIAlign', None), 'ctc_loss': ('CTCLoss', None), 'reshape_like': ('reshape_like', None),
+    'index_add': ('_contrib_index_add', None), 'index_update': ('_contrib_index_update', None),
+    'constraint_check': ('_npx_constraint_check', None), 'cast': ('Cast', None), 'amp_cast': ('amp_cast', None),
+    'softmax_cross_entropy': ('softmax_cross_entropy', None), 'box_nms': ('_contrib_box_nms', None),
+    'box_iou': ('_contrib_box_iou', None), 'multibox_prior': ('_contrib_MultiBoxPrior', None),
+    'multibox_target': ('_contrib_MultiBoxTarget', None), 'multibox_detection': ('_contrib_MultiBoxDetection', None),
+    'bipartite_matching': ('_contrib_bipartite_matching', None),
+}
+
+__all__ = ['set_np', 'reset_np', 'is_np_array', 'is_np_shape', 'use_np', 'use_np_array', 'use_np_shape', 'np_array',
+           'np_shape', 'cpu', 'gpu', 'num_gpus', 'current_context', 'waitall', 'save', 'load', 'seed', 'reshape',
+           'nonzero', 'random', 'image', 'sigmoid', 'relu'] + list(_MAP)
+
+for _name, (_opn, _defaults) in _MAP.items():
+    globals()[_name] = _op(_opn, _defaults, pyname=_name)
+
+
+def reshape(a, newshape, reverse=False, order='C'):
+    """Reshape with npx special codes (-1 infer, -2 copy, -3 drop unit dim, -4 copy rest, -5 merge, -6 split)."""
+    if _is_sym(a):
+        from ..symbol.symbol import _op_func
+        return _op_func('_npx_reshape')(a, newshape=tuple(newshape), reverse=reverse, order=order)
+    from ..numpy.multiarray import _call
+    return _call('_npx_reshape', a, newshape=tuple(newshape) if not isinstance(newshape, int) else (newshape,),
+                 reverse=reverse, order=order)
+
+
+def nonzero(a):
+    """Indices of non-zero elements as an ``(N, ndim)`` int64 array."""
+    import torch
+    from ..numpy import ndarray
+    return ndarray(torch.nonzero(a._data))
+
+
+def seed(s, ctx='all'):
+    from .. import random as _r
+    _r.seed(s, ctx)
+
+
+def save(file, arr):
+    """Save an ndarray, list or dict of ndarrays (``.params``/npz-like container)."""
+    from ..ndarray import utils as _u
+    if isinstance(arr, NDArray):
+        arr = [arr]
+    if isinstance(arr, dict):
+        arr = {k: v.as_nd_ndarray() if hasattr(v, 'as_nd_ndarray') else v for k, v in arr.items()}
+    else:
+        arr = [v.as_nd_ndarray() if hasattr(v, 'as_nd_ndarray') else v for v in arr]
+    _u.save(file, arr)
+
+
+def load(file):
+    from ..ndarray import utils as _u
+    r = _u.load(file)
+    if isinstance(r, dict):
+        return {k: v.as_np_ndarray() for k, v in r.items()}
+    return [v.as_np_ndarray() for v in r]
+
+
+class _Namespace:
+    def __init__(self, name, entries):
+        self.__name__ = name
+        self.__dict__.update(entries)
+
+
+def _random_ns():
+    import torch
+    from ..numpy import ndarray, random as nprand
+
+    def bernoulli(prob=None, logit=None, size=None, dtype=None, ctx=None, out=None):
+        from ..numpy.multiarray import _call
+        if logit is not None:
+            prob = 1.0 / (1.0 + __import__('math').exp(-logit)) if not isinstance(logit, NDArray) else \
+                ndarray(torch.sigmoid(logit._data))
+        if isinstance(prob, NDArray):
+            shp = tuple(size) if size is not None else tuple(prob.shape)
+            return ndarray((torch.rand(shp, device=prob._data.device) < prob._data).float())
+        return _call('_npi_bernoulli', prob=float(prob), size=(size,) if isinstance(size, int) else (size or ()),
+                     ctx=ctx or current_context(), dtype=dtype or 'float32')
+
+    def uniform_n(low=0.0, high=1.0, batch_shape=None, dtype=None, ctx=None):
+        return nprand.uniform(low, high, size=batch_shape, dtype=dtype, ctx=ctx)
+
+    def normal_n(loc=0.0, scale=1.0, batch_shape=None, dtype=None, ctx=None):
+        return nprand.normal(loc, scale, size=batch_shape, dtype=dtype, ctx=ctx)
+    return _Namespace('mxnet.numpy_extension.random', {'seed': seed, 'bernoulli': bernoulli,
+                                                       'uniform_n': uniform_n, 'normal_n': normal_n})
+
+
+def _image_ns():
+    ents = {}
+    for n, opn in (('to_tensor', '_image_to_tensor'), ('normalize', '_image_normalize'), ('resize', '_image_resize'),
+                   ('crop', '_image_crop'), ('flip_left_right', '_image_flip_left_right'),
+                   ('random_flip_left_right', '_image_random_flip_left_right'),
+                   ('flip_top_bottom', '_image_flip_top_bottom'),
+                   ('random_flip_top_bottom', '_image_random_flip_top_bottom'),
+                   ('random_brightness', '_image_random_brightness'), ('random_contrast', '_image_random_contrast'),
+                   ('random_saturation', '_image_random_saturation'), ('random_hue', '_image_random_hue'),
+                   ('random_color_jitter', '_image_random_color_jitter'), ('adjust_lighting', '_image_adjust_lighting'),
+                   ('random_lighting', '_image_random_lighting')):
+        if _registry.has(opn):
+            ents[n] = _op(opn, pyname=n)
+    return _Namespace('mxnet.numpy_extension.image', ents)
+
+
+random = _random_ns()
+image = _image_ns()

@@ -15,6 +15,15 @@ del _g
 
 def __getattr__(name):
     # operators registered after import resolve lazily
+    if name in ('np', 'npx'):
+        if name == 'np':
+            from ..numpy import _symbol
+            mod = _symbol.make()
+        else:
+            import importlib
+            mod = importlib.import_module('..numpy_extension', __name__)
+        globals()[name] = mod
+        return mod
     from ..ops import registry as _registry
     if _registry.has(name):
         fn = _op_func(name)
