@@ -58,6 +58,7 @@ from . import visualization as viz
 from . import contrib
 from . import parallel
 from . import models
+from . import utils
 from . import numpy
 from . import numpy as np
 from . import numpy_extension

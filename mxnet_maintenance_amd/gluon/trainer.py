@@ -35,6 +35,7 @@ from ..parallel import dist
 from ..parallel.buckets import GradBuckets
 from ..ops import kernels as _K
 from .parameter import ParameterDict, Parameter
+from ..utils import env as _env
 
 __all__ = ['Trainer']
 
@@ -194,7 +195,7 @@ class Trainer:
 
     # ------------------------------------------------------------ fast path
     def _arena_eligible(self):
-        if os.environ.get('MXAMD_FLAT_ARENA', '1') != '1':
+        if _env.get('MXAMD_FLAT_ARENA') != 1:
             return False
         if self._update_on_kvstore or not self._contexts or len(self._contexts) != 1:
             return False
@@ -474,7 +475,7 @@ class _ArenaBuckets(GradBuckets):
     def __init__(self, arenas, bucket_bytes=None):
         from ..parallel.buckets import _Bucket
         if bucket_bytes is None:
-            bucket_bytes = int(float(os.environ.get('MXAMD_BUCKET_MB', '25')) * (1 << 20))
+            bucket_bytes = int(_env.get('MXAMD_BUCKET_MB') * (1 << 20))
         self.overlap = dist.world_size() > 1
         self.average = False
         self.buckets = []

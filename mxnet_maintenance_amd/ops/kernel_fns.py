@@ -8,6 +8,7 @@ tests/test_hip_kernels.py.
 import torch
 
 from . import kernels as _K
+from ..utils import env as _env
 
 __all__ = ['BatchNormNHWC', 'SoftmaxCE', 'GlobalAvgPoolNHWC', 'flat_sgd']
 
@@ -195,7 +196,7 @@ def flat_sgd(w, g, mom, w32, lr, wd, momentum, rescale, clip):
 
 import os as _os
 
-_CONV_HIP = _os.environ.get('MXAMD_CONV_HIP', '1') != '0'
+_CONV_HIP = _env.get('MXAMD_CONV_HIP') != 0
 
 
 def conv_ok_shape(x, w, stride, pad, dilate=(1, 1), groups=1):
@@ -248,7 +249,7 @@ def _conv_bwd_torch(dy, x, w, stride, pad, mask):
 # caches the fastest; during HIP-graph capture, or with autotuning off, a
 # measured heuristic picks.
 
-_AUTOTUNE = int(_os.environ.get('MXNET_CUDNN_AUTOTUNE_DEFAULT', '1')) > 0
+_AUTOTUNE = _env.get('MXNET_CUDNN_AUTOTUNE_DEFAULT') > 0
 _ALGO = {}
 
 

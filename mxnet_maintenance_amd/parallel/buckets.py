@@ -20,6 +20,7 @@ import os
 import torch
 
 from . import dist
+from ..utils import env as _env
 
 __all__ = ['GradBuckets']
 
@@ -42,7 +43,7 @@ class GradBuckets:
 
     def __init__(self, arrays, grad_reqs, bucket_bytes=None, overlap=True, average=False):
         if bucket_bytes is None:
-            bucket_bytes = int(float(os.environ.get('MXAMD_BUCKET_MB', '25')) * (1 << 20))
+            bucket_bytes = int(_env.get('MXAMD_BUCKET_MB') * (1 << 20))
         self.overlap = overlap and dist.world_size() > 1
         self.average = average
         self.buckets = []
