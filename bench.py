@@ -113,8 +113,10 @@ def main():
     if os.environ.get('MXAMD_BENCH_VERBOSE', '0') == '1' and rank == 0:
         try:
             from mxnet_maintenance_amd.ops import kernel_fns
+            times = kernel_fns.conv_algo_times()
             for k, v in sorted(kernel_fns.conv_algos().items(), key=str):
-                print('conv-algo', v, k, file=sys.stderr)
+                t = ' '.join('%s=%.3f' % (n, ms) for n, ms in sorted(times.get(k, {}).items(), key=lambda z: z[1]))
+                print('conv-algo', v, k, t, file=sys.stderr)
         except Exception as e:  # pragma: no cover
             print('conv-algo unavailable:', e, file=sys.stderr)
     if dist.world_size() > 1:

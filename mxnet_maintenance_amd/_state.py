@@ -21,6 +21,11 @@ class _State(threading.local):
 
 STATE = _State()
 
+# >0 while mx.autograd.backward runs (plain, no create_graph): backward kernels may
+# accumulate parameter gradients straight into the leaves' .grad buffers.  Process-wide
+# (not thread-local) because torch runs GPU backward functions on its device threads.
+DIRECT_GRAD = [0]
+
 
 def is_recording():
     return STATE.recording

@@ -166,6 +166,9 @@ def backward(heads, head_grads=None, retain_graph=False, train_mode=True, create
     _prepare_leaves(leaves)
     prev_train = set_training(train_mode)
     prev_rec = set_recording(False)
+    direct = not create_graph
+    if direct:
+        _state.DIRECT_GRAD[0] += 1
     try:
         with torch.enable_grad() if create_graph else torch.no_grad():
             torch.autograd.backward(tensors, grads, retain_graph=retain_graph or create_graph,
@@ -173,6 +176,8 @@ def backward(heads, head_grads=None, retain_graph=False, train_mode=True, create
     finally:
         set_training(prev_train)
         set_recording(prev_rec)
+        if direct:
+            _state.DIRECT_GRAD[0] -= 1
     _finish_leaves(leaves)
 
 

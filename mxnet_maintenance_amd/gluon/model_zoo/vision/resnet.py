@@ -98,8 +98,22 @@ class BottleneckV1(HybridBlock):
         if downsample:
             self.downsample = nn.HybridSequential(prefix='')
             self.downsample.add(_conv(channels, 1, stride, 0, in_channels, layout), _bn(layout))
+        # channel-last 1x1/stride-1 first conv: that conv also emits x for the shortcut branch, so
+        # the shortcut's gradient (identity: the tail's d_addend; projection: the downsample conv's
+        # dgrad) is folded into this conv's dgrad GEMM (ConvolutionTee, beta = 1) instead of autograd
+        # adding two activation-sized gradients in a separate kernel
+        self._tee = fuse and s1 == 1 and layout == 'NHWC'
+        if self._tee:
+            self.body[0]._tee = True
 
     def hybrid_forward(self, F, x):
+        if self._tee:
+            blocks = list(self.body._children.values())
+            out, passthrough = blocks[0](x)
+            for b in blocks[1:]:
+                out = b(out)
+            shortcut = self.downsample(passthrough) if self.downsample is not None else passthrough
+            return self.tail(out, shortcut)
         shortcut = self.downsample(x) if self.downsample is not None else x
         return self.tail(self.body(x), shortcut)
 

@@ -64,6 +64,9 @@ class _Conv(HybridBlock):
                 self.act = None
 
     def hybrid_forward(self, F, x, weight, bias=None):
+        if getattr(self, '_tee', False) and bias is None and self.act is None:
+            # (conv(x), x): identity-shortcut pass-through fused into the backward GEMM
+            return F.contrib.ConvolutionTee(x, weight, name='fwd', inplace_shortcut_grad=True, **self._kwargs)
         if bias is None:
             act = getattr(F, self._op_name)(x, weight, name='fwd', **self._kwargs)
         else:

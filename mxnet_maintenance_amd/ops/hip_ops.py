@@ -71,6 +71,13 @@ def conv(data, weight, bias, stride, pad, dilate, groups, channel_last):
     return _ncx_to_nd(y) if channel_last else y
 
 
+def conv_tee(data, weight, inplace_grad=False):
+    """(conv1x1(data), data) with the identity-shortcut gradient fused into the dgrad GEMM."""
+    if _use_hip(data) and hasattr(_K, 'ConvTeeNHWC') and _K.conv_tee_ok(data, weight):
+        return _K.ConvTeeNHWC.apply(data, weight, bool(inplace_grad))
+    return conv(data, weight, None, (1, 1), (0, 0), (1, 1), 1, True), data
+
+
 # ---------------------------------------------------------------------------
 # BatchNorm
 # ---------------------------------------------------------------------------

@@ -8,6 +8,7 @@ tests/test_hip_kernels.py.
 import torch
 
 from . import kernels as _K
+from .. import _state
 from ..utils import env as _env
 
 __all__ = ['BatchNormNHWC', 'SoftmaxCE', 'GlobalAvgPoolNHWC', 'flat_sgd']
@@ -42,6 +43,28 @@ def ce_ok(x):
 
 _K.bn_ok = bn_ok
 _K.ce_ok = ce_ok
+
+
+def _leaf_grad(t, numel=None, dtype=torch.float32):
+    """The .grad buffer of leaf ``t`` when a kernel may accumulate into it directly.
+
+    Only inside mx.autograd.backward (not torch.autograd.grad, not create_graph),
+    where .grad IS the destination: the buffer exists (our autograd
+    zeroes grad_req='write' buffers before backward), is contiguous, of the
+    expected dtype/size.  The caller then returns None for that input so
+    torch's AccumulateGrad (a separate add kernel per parameter) never runs.
+    """
+    if t is None or _state.DIRECT_GRAD[0] <= 0 or torch.is_grad_enabled() or not t.is_leaf or not t.requires_grad:
+        return None
+    gb = t.grad
+    if gb is None or gb.dtype != dtype or not gb.is_contiguous() or gb.shape != t.shape:
+        return None
+    if numel is not None and gb.numel() != numel:
+        return None
+    return gb
+
+
+_RELU_FROM_X = [True]    # BN+ReLU backward recomputes the mask from x (debug switch)
 
 
 class BatchNormNHWC(torch.autograd.Function):
@@ -85,8 +108,13 @@ class BatchNormNHWC(torch.autograd.Function):
             with torch.no_grad():
                 moving_mean.mul_(momentum).add_(mean.to(moving_mean.dtype), alpha=1 - momentum)
                 moving_var.mul_(momentum).add_(var.to(moving_var.dtype), alpha=1 - momentum)
-        ctx.save_for_backward(x, y if relu else None, g, mean, invstd)
-        ctx.cfg = (bool(relu), bool(training), addend is not None, gamma.dtype, beta.dtype)
+        # ReLU mask in backward: recomputed from x*scale+shift for BN+ReLU (y not kept),
+        # read from y only for the residual tail (its mask also depends on the addend)
+        relu_mode = 0 if not relu else (1 if (addend is not None or not _RELU_FROM_X[0]) else 2)
+        ctx.save_for_backward(x, y if relu_mode == 1 else None, g, mean, invstd,
+                              scale if relu_mode == 2 else None, shift if relu_mode == 2 else None)
+        ctx.cfg = (relu_mode, bool(training), addend is not None, gamma.dtype, beta.dtype)
+        ctx.refs = (gamma, beta)
         ctx.mark_non_differentiable(mean, var)
         # mean/var never receive gradients: skip materialising two zero tensors per call
         ctx.set_materialize_grads(False)
@@ -95,8 +123,9 @@ class BatchNormNHWC(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy, _gm, _gv):
         lib = _K.lib()
-        x, y, g, mean, invstd = ctx.saved_tensors
-        relu, training, has_add, gdt, bdt = ctx.cfg
+        x, y, g, mean, invstd, fscale, fshift = ctx.saved_tensors
+        relu_mode, training, has_add, gdt, bdt = ctx.cfg
+        gamma_ref, beta_ref = ctx.refs
         if gy is None:
             return (None,) * 10
         gy = gy.contiguous()
@@ -108,11 +137,27 @@ class BatchNormNHWC(torch.autograd.Function):
         nblk = lib.bn_partials_rows(R, C)
         part = torch.empty(2 * nblk * C, dtype=torch.float32, device=dev)
         out = torch.empty(5, C, dtype=torch.float32, device=dev)
+        need_g, need_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        # accumulate dgamma/dbeta straight into the parameters' fp32 grad buffers (arena views)
+        tg = _leaf_grad(gamma_ref, C) if need_g else None
+        tb = _leaf_grad(beta_ref, C) if need_b else None
+        direct = tb is not None and (tg is not None or not need_g) and (tg is not None or tb is not None)
+        if direct:
+            dg_buf = tg if tg is not None else torch.zeros(C, dtype=torch.float32, device=dev)
+            dg_ptr, db_ptr, accum = dg_buf.data_ptr(), tb.data_ptr(), 1
+        else:
+            dg_ptr, db_ptr, accum = out[0].data_ptr(), out[1].data_ptr(), 0
         lib.bn_nhwc_backward(_DT[x.dtype], x.data_ptr(), gy.data_ptr(), _p(y), dx.data_ptr(), _p(dz), g.data_ptr(),
-                             mean.data_ptr(), invstd.data_ptr(), part.data_ptr(), out[0].data_ptr(),
-                             out[1].data_ptr(), out[2].data_ptr(), R, C, int(relu), 0, int(training), _stream())
-        dgamma = out[0].to(gdt) if ctx.needs_input_grad[1] else None
-        dbeta = out[1].to(bdt) if ctx.needs_input_grad[2] else None
+                             mean.data_ptr(), invstd.data_ptr(), _p(fscale), _p(fshift), part.data_ptr(), dg_ptr,
+                             db_ptr, out[2].data_ptr(), R, C, relu_mode, 0, int(training), accum, _stream())
+        if direct:
+            # returning None: torch still runs the leaves' AccumulateGrad node with an undefined
+            # gradient, which fires their post-accumulate hooks (bucketed all-reduce readiness)
+            dgamma = None
+            dbeta = None
+        else:
+            dgamma = out[0].to(gdt) if need_g else None
+            dbeta = out[1].to(bdt) if need_b else None
         return dx, dgamma, dbeta, dz, None, None, None, None, None, None
 
 
@@ -251,9 +296,10 @@ def _conv_bwd_torch(dy, x, w, stride, pad, mask):
 
 _AUTOTUNE = _env.get('MXNET_CUDNN_AUTOTUNE_DEFAULT') > 0
 _ALGO = {}
+_TIMES = {}   # key -> {candidate: ms per call} from the autotuning run
 
 
-def _time_candidates(cands, reps=3):
+def _time_candidates(cands, reps=3, key=None):
     best, best_t, out = None, None, None
     for name, fn in cands:
         fn()
@@ -264,6 +310,8 @@ def _time_candidates(cands, reps=3):
         e.record()
         e.synchronize()
         t = s.elapsed_time(e)
+        if key is not None:
+            _TIMES.setdefault(key, {})[name] = t / reps
         if best_t is None or t < best_t:
             best, best_t, out = name, t, r
     return best, out
@@ -274,7 +322,7 @@ def _select(key, cands, default):
     name = _ALGO.get(key)
     if name is None:
         if _AUTOTUNE and not torch.cuda.is_current_stream_capturing() and len(cands) > 1:
-            name, out = _time_candidates(cands)
+            name, out = _time_candidates(cands, key=key)
             _ALGO[key] = name
             return out
         name = default
@@ -341,7 +389,8 @@ def _wgrad_candidates(dy, x, w, stride, pad):
                     # split-K batched GEMM (hipBLASLt): [chunks, K, P/chunks] x [chunks, P/chunks, C], fp32 sum
                     d3 = dy.reshape(chunks, P // chunks, K).transpose(1, 2)
                     x3 = x.reshape(chunks, P // chunks, C)
-                    return _bmm_f32(d3, x3).sum(0).to(w.dtype).view(K, 1, 1, C)
+                    # fp32 result: the caller accumulates it into the fp16 grad buffer (no cast pass)
+                    return _bmm_f32(d3, x3).sum(0).view(K, 1, 1, C)
                 c.append(('splitk%d' % chunks, splitk))
     return c
 
@@ -371,6 +420,7 @@ class ConvNHWC(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.pad = stride, pad
         ctx.has_bias = bias is not None
+        ctx.w_ref = w
         return y
 
     @staticmethod
@@ -385,14 +435,86 @@ class ConvNHWC(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             key = ('wgrad', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype)
             dw = _select(key, _wgrad_candidates(dy, x, w, stride, pad), 'miopen')
+            if dw.dtype != w.dtype:
+                tgt = _leaf_grad(ctx.w_ref, dtype=w.dtype)
+                if tgt is not None:
+                    tgt.add_(dw)          # fp32 split-K sum accumulated straight into the fp16/bf16 grad
+                    dw = None
+                else:
+                    dw = dw.to(w.dtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum(dim=(0, 1, 2))
         return dx, dw, db, None, None, None
 
 
+class ConvTeeNHWC(torch.autograd.Function):
+    """1x1 stride-1 NHWC conv whose input also feeds an identity shortcut.
+
+    Returns ``(y, x_passthrough)``.  The shortcut's gradient arrives here with
+    the conv's, so dX = dY·W + dShortcut is ONE hipBLASLt GEMM with beta = 1
+    (the residual gradient rides in as the C matrix) instead of a dgrad GEMM
+    followed by a separate 3-pass elementwise add of two activation-sized
+    tensors (what autograd's input-buffer accumulation would launch).
+    """
+
+    @staticmethod
+    def forward(ctx, x, w, inplace_grad=False):
+        stride, pad = (1, 1), (0, 0)
+        key = ('fwd', tuple(x.shape), tuple(w.shape), stride, pad, x.dtype, False)
+        y = _select(key, _fwd_candidates(x, w, stride, pad, None), _fwd_default(x, w, stride))
+        ctx.save_for_backward(x, w)
+        ctx.w_ref = w
+        ctx.inplace_grad = inplace_grad
+        return y, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, gy, gpass):
+        x, w = ctx.saved_tensors
+        K, C = w.shape[0], w.shape[3]
+        dx = dw = None
+        if gy is None:
+            return gpass, None, None
+        gy = gy.contiguous()
+        if ctx.needs_input_grad[0]:
+            g2 = gy.reshape(-1, K)
+            w2 = w.reshape(K, C)
+            if gpass is not None and ctx.inplace_grad and gpass.is_contiguous():
+                # the shortcut's gradient buffer is private to this edge (the fused residual tail
+                # returns a fresh d_addend): accumulate the GEMM into it, beta = 1, no copy
+                dx = gpass.view(-1, C).addmm_(g2, w2).view(x.shape)
+            elif gpass is not None:
+                dx = torch.addmm(gpass.contiguous().reshape(-1, C), g2, w2).view(x.shape)
+            else:
+                dx = torch.mm(g2, w2).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            key = ('wgrad', tuple(x.shape), tuple(w.shape), (1, 1), (0, 0), x.dtype)
+            dw = _select(key, _wgrad_candidates(gy, x, w, (1, 1), (0, 0)), 'miopen')
+            if dw.dtype != w.dtype:
+                tgt = _leaf_grad(ctx.w_ref, dtype=w.dtype)
+                if tgt is not None:
+                    tgt.add_(dw)
+                    dw = None
+                else:
+                    dw = dw.to(w.dtype)
+        return dx, dw, None
+
+
+def conv_tee_ok(x, w):
+    return (conv_ok(x, w, (1, 1), (0, 0), (1, 1), 1) and w.shape[1] == 1 and w.shape[2] == 1
+            and x.shape[3] == w.shape[3])
+
+
+_K.conv_tee_ok = conv_tee_ok
+
+
 def conv_algos():
     """The algorithm chosen for every (pass, shape) seen so far."""
     return dict(_ALGO)
+
+
+def conv_algo_times():
+    """Autotuning measurements: (pass, shape...) -> {candidate: ms}."""
+    return {k: dict(v) for k, v in _TIMES.items()}
 
 
 def conv_ok(x, w, stride, pad, dilate, groups):
@@ -402,7 +524,7 @@ def conv_ok(x, w, stride, pad, dilate, groups):
 
 
 _K.conv_ok = conv_ok
-__all__ += ['ConvNHWC', 'conv_fwd', 'conv_ok_shape']
+__all__ += ['ConvNHWC', 'ConvTeeNHWC', 'conv_fwd', 'conv_ok_shape']
 
 
 # ---------------------------------------------------------------------------

@@ -131,6 +131,23 @@ def convolution(data, weight, bias=None, kernel=(), stride=(), dilate=(), pad=()
                         _is_channel_last(layout))
 
 
+@register('_contrib_ConvolutionTee', aliases=('ConvolutionTee',), arg_names=('data', 'weight'),
+          infer_params=_conv_infer, num_outputs=2,
+          params=dict(_CONV_PARAMS, no_bias=('bool', True), inplace_shortcut_grad=('bool', False)))
+def convolution_tee(data, weight, kernel=(1, 1), stride=(), dilate=(), pad=(), num_filter=0, num_group=1,
+                    workspace=1024, no_bias=True, cudnn_tune=None, cudnn_off=False, layout=None,
+                    inplace_shortcut_grad=False):
+    """Channel-last 1x1 convolution that also passes its input through (second output) for an identity
+    shortcut; on gfx950 the shortcut's gradient is folded into the dgrad GEMM (beta=1) instead of a
+    separate add.  Semantically ``(Convolution(data, weight), data)``.  ``inplace_shortcut_grad``: the
+    pass-through output's only consumer returns a freshly allocated gradient for it (e.g. the fused
+    BatchNormAddReLU tail), so the GEMM may accumulate into that buffer without a copy."""
+    if tuple(kernel) != (1, 1) or tuple(stride or (1, 1)) != (1, 1) or tuple(pad or (0, 0)) != (0, 0) \
+            or not _is_channel_last(layout) or num_group != 1:
+        raise ValueError('ConvolutionTee: only channel-last 1x1 stride-1 convolutions')
+    return hip_ops.conv_tee(data, weight, inplace_shortcut_grad)
+
+
 def _deconv_infer(in_shapes, a):
     d = in_shapes[0]
     if d is None:

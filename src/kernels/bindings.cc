@@ -19,9 +19,9 @@ void bn_nhwc_forward(int dtype, const void* x, const void* addend, void* y, cons
                      float* shift, int64_t R, int C, float eps, int training, int relu, int fix_gamma,
                      float momentum, float* mm_upd, float* mv_upd, hipStream_t s);
 void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, void* dx, void* dz,
-                      const float* gamma, const float* mean, const float* invstd, float* part, float* dgamma,
-                      float* dbeta, float* coef, int64_t R, int C, int relu, int fix_gamma, int training,
-                      hipStream_t s);
+                      const float* gamma, const float* mean, const float* invstd, const float* fscale,
+                      const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R, int C,
+                      int relu_mode, int fix_gamma, int training, int accum, hipStream_t s);
 int bn_partials_rows(int64_t R, int C);
 void softmax_ce_forward(int dtype, int label_is_int, const void* logits, const void* label, float* loss, float* lse,
                         int N, int K, hipStream_t s);
@@ -67,13 +67,14 @@ PYBIND11_MODULE(_hip_kernels, m) {
                     C, eps, training, relu, fix_gamma, momentum, P<float>(mm_upd), P<float>(mv_upd), S(s));
     check_launch("bn_nhwc_forward");
   });
+  // relu_mode: 0 none, 1 mask from y, 2 mask recomputed from x*fscale+fshift; accum: += into dgamma/dbeta
   m.def("bn_nhwc_backward", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t y, uintptr_t dx, uintptr_t dz,
-                               uintptr_t g, uintptr_t mean, uintptr_t inv, uintptr_t part, uintptr_t dgamma,
-                               uintptr_t dbeta, uintptr_t coef, int64_t R, int C, int relu, int fix_gamma,
-                               int training, uintptr_t s) {
+                               uintptr_t g, uintptr_t mean, uintptr_t inv, uintptr_t fscale, uintptr_t fshift,
+                               uintptr_t part, uintptr_t dgamma, uintptr_t dbeta, uintptr_t coef, int64_t R, int C,
+                               int relu_mode, int fix_gamma, int training, int accum, uintptr_t s) {
     bn_nhwc_backward(dt, P<void>(x), P<void>(dy), P<void>(y), P<void>(dx), P<void>(dz), P<float>(g), P<float>(mean),
-                     P<float>(inv), P<float>(part), P<float>(dgamma), P<float>(dbeta), P<float>(coef), R, C, relu,
-                     fix_gamma, training, S(s));
+                     P<float>(inv), P<float>(fscale), P<float>(fshift), P<float>(part), P<float>(dgamma),
+                     P<float>(dbeta), P<float>(coef), R, C, relu_mode, fix_gamma, training, accum, S(s));
     check_launch("bn_nhwc_backward");
   });
   m.def("softmax_ce_forward", [](int dt, int li, uintptr_t logits, uintptr_t label, uintptr_t loss, uintptr_t lse,

@@ -9,9 +9,15 @@
 //   forward : 1 read pass for shifted sums (sum(x-k), sum((x-k)^2), k = running
 //             mean: no catastrophic cancellation), 1 read + 1 write pass for
 //             y = x*scale + shift (+addend) (relu).
-//   backward: 1 read pass over (dy, y, x) for sum(dz), sum(dz*(x-mean)) where
-//             dz = relu ? dy*(y>0) : dy, then 1 pass writing
+//   backward: 1 read pass over (dy, x[, y]) for sum(dz), sum(dz*(x-mean)) where
+//             dz = relu ? dy*mask : dy, then 1 pass writing
 //             dx = A*dz + B*x + C (and d_addend = dz for the residual branch).
+//             The ReLU mask of a plain BN+ReLU is recomputed from x and the
+//             forward's (scale, shift) -- (x*scale + shift > 0) -- so y is never
+//             saved or re-read (one pass fewer in each backward kernel); only the
+//             residual tail, whose mask also depends on the addend, reads y.
+//             dgamma/dbeta can be accumulated straight into the parameters'
+//             fp32 gradient buffers (no separate accumulate kernels).
 // Every thread moves 16 bytes (8 x fp16/bf16) per access; a row of C channels
 // is covered by C/8 lanes so loads are fully coalesced for any C % 8 == 0.
 // Reductions: per-thread fp32 registers -> LDS tree -> per-block partials ->
@@ -38,23 +44,33 @@ static inline BnGeom bn_geom(int C) {
   return g;
 }
 
+// ReLU mask source in the backward kernels
+constexpr int kReluNone = 0;   // no ReLU
+constexpr int kReluFromY = 1;  // mask = y > 0 (residual tail: y depends on the addend)
+constexpr int kReluFromX = 2;  // mask = x*scale + shift > 0 (recomputed, y not needed)
+
 // MODE 0: forward sums of (x - shift) and (x - shift)^2
-// MODE 1: backward sums of dz and dz * (x - mean), dz = relu ? dy * (y > 0) : dy
-template <typename T, int MODE, bool RELU>
+// MODE 1: backward sums of dz and dz * (x - mean), dz = dy * mask (RELU != kReluNone)
+template <typename T, int MODE, int RELU>
 __global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(
     const T* __restrict__ x, const T* __restrict__ dy, const T* __restrict__ y,
-    const float* __restrict__ center, float* __restrict__ part1, float* __restrict__ part2,
-    int64_t R, int C, int tpr, int rpi, int64_t rows_per_block) {
+    const float* __restrict__ center, const float* __restrict__ fscale, const float* __restrict__ fshift,
+    float* __restrict__ part1, float* __restrict__ part2, int64_t R, int C, int tpr, int rpi,
+    int64_t rows_per_block) {
   const int tid = threadIdx.x;
   const int lane_c = tid % tpr;   // which 8-channel group inside the block's channel slice
   const int lane_r = tid / tpr;   // row offset within an iteration
   const int cbase = blockIdx.y * tpr * 8 + lane_c * 8;
-  float s1[8], s2[8], k[8];
+  float s1[8], s2[8], k[8], fs[8], fh[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     s1[i] = 0.f;
     s2[i] = 0.f;
     k[i] = center[cbase + i];
+    if (RELU == kReluFromX) {
+      fs[i] = fscale[cbase + i];
+      fh[i] = fshift[cbase + i];
+    }
   }
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   int64_t r1 = r0 + rows_per_block;
@@ -71,9 +87,11 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(
         s2[i] += d * d;
       } else {
         float dz = vdy.get(i);
-        if (RELU) dz = vy.get(i) > 0.f ? dz : 0.f;
+        const float xi = vx.get(i);
+        if (RELU == kReluFromY) dz = vy.get(i) > 0.f ? dz : 0.f;
+        if (RELU == kReluFromX) dz = fmaf(xi, fs[i], fh[i]) > 0.f ? dz : 0.f;
         s1[i] += dz;
-        s2[i] += dz * (vx.get(i) - k[i]);
+        s2[i] += dz * (xi - k[i]);
       }
     }
   };
@@ -85,7 +103,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(
       const int64_t off = (r + u * rpi) * C + cbase;
       vx[u].load(x + off);
       if (MODE == 1) vdy[u].load(dy + off);
-      if (MODE == 1 && RELU) vy[u].load(y + off);
+      if (MODE == 1 && RELU == kReluFromY) vy[u].load(y + off);
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) accum(vx[u], vdy[u], vy[u]);
@@ -95,7 +113,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(
     Vec8<T> vx, vdy, vy;
     vx.load(x + off);
     if (MODE == 1) vdy.load(dy + off);
-    if (MODE == 1 && RELU) vy.load(y + off);
+    if (MODE == 1 && RELU == kReluFromY) vy.load(y + off);
     accum(vx, vdy, vy);
   }
   // reduce the rpi row-lanes that share a channel group through LDS
@@ -133,7 +151,8 @@ __global__ void __launch_bounds__(kFinThreads) bn_finalize_kernel(
     const float* __restrict__ center, const float* __restrict__ gamma, const float* __restrict__ beta,
     const float* __restrict__ invstd_in, float eps, float* __restrict__ o0, float* __restrict__ o1,
     float* __restrict__ o2, float* __restrict__ o3, float* __restrict__ o4, float* __restrict__ o5,
-    int fix_gamma, int training, float momentum, float* __restrict__ mm_upd, float* __restrict__ mv_upd) {
+    int fix_gamma, int training, float momentum, float* __restrict__ mm_upd, float* __restrict__ mv_upd,
+    int accum) {
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
   const float* p1 = part1 + static_cast<int64_t>(c) * nblk;
@@ -185,8 +204,14 @@ __global__ void __launch_bounds__(kFinThreads) bn_finalize_kernel(
     const float inv = invstd_in[c];
     const double dbeta = a;
     const double dgamma = b * inv;
-    o0[c] = static_cast<float>(dgamma);
-    o1[c] = static_cast<float>(dbeta);
+    // accum: o0/o1 are the parameters' gradient buffers (grad_req write was zeroed, add accumulates)
+    if (accum) {
+      o0[c] += static_cast<float>(dgamma);
+      o1[c] += static_cast<float>(dbeta);
+    } else {
+      o0[c] = static_cast<float>(dgamma);
+      o1[c] = static_cast<float>(dbeta);
+    }
     const double A = static_cast<double>(g) * inv;
     const double B = training ? -A * inv * dgamma / n : 0.0;
     const double Cc = training ? A * (static_cast<double>(center[c]) * inv * dgamma / n - dbeta / n) : 0.0;
@@ -230,11 +255,12 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_kernel(
   }
 }
 
-// dx = A*dz + B*x + Cc, dz = relu ? dy * (y > 0) : dy; optionally d_addend = dz
-template <typename T, bool RELU, bool WRITE_DZ>
+// dx = A*dz + B*x + Cc, dz = dy * mask (see RELU modes); optionally d_addend = dz
+template <typename T, int RELU, bool WRITE_DZ>
 __global__ void __launch_bounds__(kBnThreads) bn_bwd_apply_kernel(
     const T* __restrict__ x, const T* __restrict__ dy, const T* __restrict__ y,
     const float* __restrict__ A, const float* __restrict__ B, const float* __restrict__ Cc,
+    const float* __restrict__ fscale, const float* __restrict__ fshift,
     T* __restrict__ dx, T* __restrict__ dz_out, int64_t nvec, int C) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -245,7 +271,16 @@ __global__ void __launch_bounds__(kBnThreads) bn_bwd_apply_kernel(
     Vec8<T> vx, vdy, vy, out, dz;
     vx.load(x + off);
     vdy.load(dy + off);
-    if (RELU) vy.load(y + off);
+    if (RELU == kReluFromY) vy.load(y + off);
+    float fs[8], fh[8];
+    if (RELU == kReluFromX) {
+      const float4 s0 = *reinterpret_cast<const float4*>(fscale + c);
+      const float4 s1 = *reinterpret_cast<const float4*>(fscale + c + 4);
+      const float4 h0 = *reinterpret_cast<const float4*>(fshift + c);
+      const float4 h1 = *reinterpret_cast<const float4*>(fshift + c + 4);
+      fs[0] = s0.x; fs[1] = s0.y; fs[2] = s0.z; fs[3] = s0.w; fs[4] = s1.x; fs[5] = s1.y; fs[6] = s1.z; fs[7] = s1.w;
+      fh[0] = h0.x; fh[1] = h0.y; fh[2] = h0.z; fh[3] = h0.w; fh[4] = h1.x; fh[5] = h1.y; fh[6] = h1.z; fh[7] = h1.w;
+    }
     const float4 a0 = *reinterpret_cast<const float4*>(A + c);
     const float4 a1 = *reinterpret_cast<const float4*>(A + c + 4);
     const float4 b0 = *reinterpret_cast<const float4*>(B + c);
@@ -258,7 +293,8 @@ __global__ void __launch_bounds__(kBnThreads) bn_bwd_apply_kernel(
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float d = vdy.get(i);
-      if (RELU) d = vy.get(i) > 0.f ? d : 0.f;
+      if (RELU == kReluFromY) d = vy.get(i) > 0.f ? d : 0.f;
+      if (RELU == kReluFromX) d = fmaf(vx.get(i), fs[i], fh[i]) > 0.f ? d : 0.f;
       if (WRITE_DZ) dz.set(i, d);
       out.set(i, ka[i] * d + kb[i] * vx.get(i) + kc[i]);
     }
@@ -301,11 +337,12 @@ static void bn_forward_impl(const void* x, const void* addend, void* y, const fl
     dim3 grid(nblk, C / g.cb);
     float* p1 = part;
     float* p2 = part + static_cast<int64_t>(nblk) * C;
-    hipLaunchKernelGGL((bn_reduce_kernel<T, 0, false>), grid, dim3(kBnThreads), 0, s,
-                       static_cast<const T*>(x), nullptr, nullptr, center, p1, p2, R, C, g.tpr, g.rpi, rpb);
+    hipLaunchKernelGGL((bn_reduce_kernel<T, 0, kReluNone>), grid, dim3(kBnThreads), 0, s,
+                       static_cast<const T*>(x), nullptr, nullptr, center, nullptr, nullptr, p1, p2, R, C, g.tpr,
+                       g.rpi, rpb);
     hipLaunchKernelGGL((bn_finalize_kernel<0>), dim3(C), dim3(kFinThreads), 0, s, p1, p2, nblk, C, R, center, gamma,
                        beta, nullptr, eps, mean, invstd, var, scale, shift, nullptr, fix_gamma, 1, momentum, mm_upd,
-                       mv_upd);
+                       mv_upd, 0);
   }
   const int64_t nvec = R * C / 8;
   int blocks = static_cast<int>((nvec + kBnThreads - 1) / kBnThreads);
@@ -332,9 +369,9 @@ static void bn_forward_impl(const void* x, const void* addend, void* y, const fl
 
 template <typename T>
 static void bn_backward_impl(const void* x, const void* dy, const void* y, void* dx, void* dz,
-                             const float* gamma, const float* mean, const float* invstd, float* part,
-                             float* dgamma, float* dbeta, float* coef, int64_t R, int C, int relu,
-                             int fix_gamma, int training, hipStream_t s) {
+                             const float* gamma, const float* mean, const float* invstd, const float* fscale,
+                             const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R,
+                             int C, int relu_mode, int fix_gamma, int training, int accum, hipStream_t s) {
   BnGeom g = bn_geom(C);
   int nblk;
   int64_t rpb = bn_rows_per_block(R, C, g, &nblk);
@@ -344,18 +381,21 @@ static void bn_backward_impl(const void* x, const void* dy, const void* y, void*
   const T* xa = static_cast<const T*>(x);
   const T* dya = static_cast<const T*>(dy);
   const T* ya = static_cast<const T*>(y);
-  if (relu)
-    hipLaunchKernelGGL((bn_reduce_kernel<T, 1, true>), grid, dim3(kBnThreads), 0, s, xa, dya, ya, mean, p1, p2, R,
-                       C, g.tpr, g.rpi, rpb);
-  else
-    hipLaunchKernelGGL((bn_reduce_kernel<T, 1, false>), grid, dim3(kBnThreads), 0, s, xa, dya, ya, mean, p1, p2,
-                       R, C, g.tpr, g.rpi, rpb);
+  MXAMD_HOST_CHECK(relu_mode != kReluFromY || y != nullptr, "bn_nhwc_backward: relu mask from y needs y");
+  MXAMD_HOST_CHECK(relu_mode != kReluFromX || (fscale && fshift), "bn_nhwc_backward: relu-from-x needs scale/shift");
+#define RED(RL)                                                                                                \
+  hipLaunchKernelGGL((bn_reduce_kernel<T, 1, RL>), grid, dim3(kBnThreads), 0, s, xa, dya, ya, mean, fscale, fshift, \
+                     p1, p2, R, C, g.tpr, g.rpi, rpb)
+  if (relu_mode == kReluFromY) RED(kReluFromY);
+  else if (relu_mode == kReluFromX) RED(kReluFromX);
+  else RED(kReluNone);
+#undef RED
   float* A = coef;
   float* B = coef + C;
   float* Cc = coef + 2 * C;
   hipLaunchKernelGGL((bn_finalize_kernel<1>), dim3(C), dim3(kFinThreads), 0, s, p1, p2, nblk, C, R, mean, gamma, nullptr,
                      invstd, 0.f, dgamma, dbeta, A, B, Cc, nullptr, fix_gamma, training, 0.f, nullptr,
-                     nullptr);
+                     nullptr, accum);
   const int64_t nvec = R * C / 8;
   int blocks = static_cast<int>((nvec + kBnThreads - 1) / kBnThreads);
   if (blocks > 256 * 16) blocks = 256 * 16;
@@ -363,11 +403,13 @@ static void bn_backward_impl(const void* x, const void* dy, const void* y, void*
   T* dza = static_cast<T*>(dz);
 #define BWD(RL, WD)                                                                                      \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RL, WD>), dim3(blocks), dim3(kBnThreads), 0, s, xa, dya, ya, A, B, \
-                     Cc, dxa, dza, nvec, C)
-  if (relu) {
-    if (dz) BWD(true, true); else BWD(true, false);
+                     Cc, fscale, fshift, dxa, dza, nvec, C)
+  if (relu_mode == kReluFromY) {
+    if (dz) BWD(kReluFromY, true); else BWD(kReluFromY, false);
+  } else if (relu_mode == kReluFromX) {
+    if (dz) BWD(kReluFromX, true); else BWD(kReluFromX, false);
   } else {
-    if (dz) BWD(false, true); else BWD(false, false);
+    if (dz) BWD(kReluNone, true); else BWD(kReluNone, false);
   }
 #undef BWD
 }
@@ -392,21 +434,21 @@ void bn_nhwc_forward(int dtype, const void* x, const void* addend, void* y, cons
 }
 
 void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, void* dx, void* dz,
-                      const float* gamma, const float* mean, const float* invstd, float* part, float* dgamma,
-                      float* dbeta, float* coef, int64_t R, int C, int relu, int fix_gamma, int training,
-                      hipStream_t s) {
+                      const float* gamma, const float* mean, const float* invstd, const float* fscale,
+                      const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R, int C,
+                      int relu_mode, int fix_gamma, int training, int accum, hipStream_t s) {
   switch (dtype) {
     case kF16:
-      bn_backward_impl<__half>(x, dy, y, dx, dz, gamma, mean, invstd, part, dgamma, dbeta, coef, R, C, relu,
-                               fix_gamma, training, s);
+      bn_backward_impl<__half>(x, dy, y, dx, dz, gamma, mean, invstd, fscale, fshift, part, dgamma, dbeta, coef, R,
+                               C, relu_mode, fix_gamma, training, accum, s);
       break;
     case kBF16:
-      bn_backward_impl<__hip_bfloat16>(x, dy, y, dx, dz, gamma, mean, invstd, part, dgamma, dbeta, coef, R, C,
-                                       relu, fix_gamma, training, s);
+      bn_backward_impl<__hip_bfloat16>(x, dy, y, dx, dz, gamma, mean, invstd, fscale, fshift, part, dgamma, dbeta,
+                                       coef, R, C, relu_mode, fix_gamma, training, accum, s);
       break;
     default:
-      bn_backward_impl<float>(x, dy, y, dx, dz, gamma, mean, invstd, part, dgamma, dbeta, coef, R, C, relu,
-                              fix_gamma, training, s);
+      bn_backward_impl<float>(x, dy, y, dx, dz, gamma, mean, invstd, fscale, fshift, part, dgamma, dbeta, coef, R,
+                              C, relu_mode, fix_gamma, training, accum, s);
   }
 }
 
