@@ -99,7 +99,12 @@ class BatchNormNHWC(torch.autograd.Function):
         # buffers are fp32 + contiguous (always true for Gluon BN params)
         upd = (training and momentum is not None and mm is moving_mean and moving_var.dtype == torch.float32
                and moving_var.is_contiguous())
-        lib.bn_nhwc_forward(_DT[x.dtype], x.data_ptr(), _p(addend), y.data_ptr(), g.data_ptr(), b.data_ptr(),
+        # residual tail (add + relu): the forward writes a 1-bit-per-element ReLU mask so the backward
+        # never re-reads y (two full-tensor reads fewer per call)
+        mask = (torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev)
+                if (addend is not None and relu and _RELU_FROM_X[0]) else None)
+        lib.bn_nhwc_forward(_DT[x.dtype], x.data_ptr(), _p(addend), y.data_ptr(), _p(mask), g.data_ptr(),
+                            b.data_ptr(),
                             mm.data_ptr(), _p(part), mean.data_ptr(), invstd.data_ptr(), var.data_ptr(),
                             scale.data_ptr(), shift.data_ptr(), R, C, float(eps), int(bool(training)),
                             int(bool(relu)), 0, float(momentum or 0.0), moving_mean.data_ptr() if upd else 0,
@@ -110,8 +115,8 @@ class BatchNormNHWC(torch.autograd.Function):
                 moving_var.mul_(momentum).add_(var.to(moving_var.dtype), alpha=1 - momentum)
         # ReLU mask in backward: recomputed from x*scale+shift for BN+ReLU (y not kept),
         # read from y only for the residual tail (its mask also depends on the addend)
-        relu_mode = 0 if not relu else (1 if (addend is not None or not _RELU_FROM_X[0]) else 2)
-        ctx.save_for_backward(x, y if relu_mode == 1 else None, g, mean, invstd,
+        relu_mode = 0 if not relu else (1 if not _RELU_FROM_X[0] else (3 if addend is not None else 2))
+        ctx.save_for_backward(x, y if relu_mode == 1 else mask, g, mean, invstd,
                               scale if relu_mode == 2 else None, shift if relu_mode == 2 else None)
         ctx.cfg = (relu_mode, bool(training), addend is not None, gamma.dtype, beta.dtype)
         ctx.refs = (gamma, beta)
@@ -147,7 +152,10 @@ class BatchNormNHWC(torch.autograd.Function):
             dg_ptr, db_ptr, accum = dg_buf.data_ptr(), tb.data_ptr(), 1
         else:
             dg_ptr, db_ptr, accum = out[0].data_ptr(), out[1].data_ptr(), 0
-        lib.bn_nhwc_backward(_DT[x.dtype], x.data_ptr(), gy.data_ptr(), _p(y), dx.data_ptr(), _p(dz), g.data_ptr(),
+        ymask = y if relu_mode == 3 else None
+        y = y if relu_mode == 1 else None
+        lib.bn_nhwc_backward(_DT[x.dtype], x.data_ptr(), gy.data_ptr(), _p(y), _p(ymask), dx.data_ptr(), _p(dz),
+                             g.data_ptr(),
                              mean.data_ptr(), invstd.data_ptr(), _p(fscale), _p(fshift), part.data_ptr(), dg_ptr,
                              db_ptr, out[2].data_ptr(), R, C, relu_mode, 0, int(training), accum, _stream())
         if direct:
@@ -268,6 +276,39 @@ def conv_fwd(x, w, stride, pad, bias=None):
     return y
 
 
+def conv_wgrad_ok(x, w):
+    """True when the HIP MFMA weight-gradient kernel (src/kernels/conv_wgrad.hip) handles this conv."""
+    return (_CONV_HIP and x.dim() == 4 and w.dim() == 4 and x.dtype in (torch.float16, torch.bfloat16)
+            and x.is_contiguous() and x.shape[3] % 64 == 0 and w.shape[0] % 64 == 0 and w.shape[3] == x.shape[3]
+            and x.numel() < 2 ** 31 and x.data_ptr() % 16 == 0)
+
+
+def conv_wgrad(x, dy, wshape, stride, pad, out=None, accum=False):
+    """dW[K,R,S,C] of an NHWC conv on MFMA (split-pixel fp32 slabs + reduce).
+
+    ``out`` (optional, contiguous, f16/bf16/f32) receives the result; with
+    ``accum`` the gradient is added to it (e.g. straight into a parameter's grad).
+    """
+    N, H, W, C = x.shape
+    K, R, S, _ = wshape
+    dy = dy.contiguous()
+    assert dy.dtype == x.dtype and dy.shape[0] == N and dy.shape[3] == K
+    Ho = (H + 2 * pad[0] - R) // stride[0] + 1
+    Wo = (W + 2 * pad[1] - S) // stride[1] + 1
+    assert tuple(dy.shape[1:3]) == (Ho, Wo), 'conv_wgrad: dy shape does not match the conv geometry'
+    assert dy.numel() < 2 ** 31 and dy.data_ptr() % 16 == 0
+    lib = _K.lib()
+    ws = lib.conv_nhwc_wgrad_workspace(N, H, W, C, K, R, S, stride[0], stride[1], pad[0], pad[1])
+    slab = torch.empty(ws, dtype=torch.float32, device=x.device)
+    if out is None:
+        out = torch.empty((K, R, S, C), dtype=x.dtype, device=x.device)
+        accum = False
+    assert out.is_contiguous() and out.numel() == K * R * S * C and out.dtype in _DT
+    lib.conv_nhwc_wgrad(_DT[x.dtype], x.data_ptr(), dy.data_ptr(), slab.data_ptr(), _DT[out.dtype], out.data_ptr(),
+                        int(bool(accum)), N, H, W, C, K, R, S, stride[0], stride[1], pad[0], pad[1], _stream())
+    return out
+
+
 def _dgrad_weight(w):
     """Weight of the equivalent forward conv computing dX from dY (stride 1): [Cin][R][S][Cout], flipped."""
     return w.flip(1, 2).permute(3, 1, 2, 0).contiguous()
@@ -381,6 +422,8 @@ def _dgrad_default(w, stride):
 def _wgrad_candidates(dy, x, w, stride, pad):
     c = [('miopen', lambda: _conv_bwd_torch(dy, x, w, stride, pad, (False, True))[1])]
     K, R, S, C = w.shape
+    if conv_wgrad_ok(x, w):
+        c.insert(0, ('hip', lambda: conv_wgrad(x, dy, w.shape, stride, pad)))
     if R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0):
         P = dy.numel() // K
         for chunks in (16, 64):
@@ -410,6 +453,29 @@ def _bmm_f32(a, b):
     return torch.bmm(a, b).float()
 
 
+def _wgrad(dy, x, w, w_ref, stride, pad):
+    """Weight gradient through the selected algorithm.
+
+    Returns dW, or None when it was accumulated straight into the weight's
+    .grad buffer (HIP kernel: its slab-reduce kernel adds into the buffer; the
+    split-K GEMM candidates add their fp32 sum into it).
+    """
+    key = ('wgrad', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype)
+    if _ALGO.get(key) == 'hip':
+        tgt = _leaf_grad(w_ref, dtype=w.dtype)
+        if tgt is not None:
+            conv_wgrad(x, dy, w.shape, stride, pad, out=tgt, accum=True)
+            return None
+    dw = _select(key, _wgrad_candidates(dy, x, w, stride, pad), 'hip' if conv_wgrad_ok(x, w) else 'miopen')
+    if dw.dtype != w.dtype:
+        tgt = _leaf_grad(w_ref, dtype=w.dtype)
+        if tgt is not None:
+            tgt.add_(dw)          # fp32 split-K sum accumulated straight into the fp16/bf16 grad
+            return None
+        dw = dw.to(w.dtype)
+    return dw
+
+
 class ConvNHWC(torch.autograd.Function):
     """2-D NHWC convolution with per-shape algorithm selection (HIP MFMA kernel / hipBLASLt / MIOpen)."""
 
@@ -433,15 +499,7 @@ class ConvNHWC(torch.autograd.Function):
             key = ('dgrad', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype)
             dx = _select(key, _dgrad_candidates(dy, x, w, stride, pad), _dgrad_default(w, stride))
         if ctx.needs_input_grad[1]:
-            key = ('wgrad', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype)
-            dw = _select(key, _wgrad_candidates(dy, x, w, stride, pad), 'miopen')
-            if dw.dtype != w.dtype:
-                tgt = _leaf_grad(ctx.w_ref, dtype=w.dtype)
-                if tgt is not None:
-                    tgt.add_(dw)          # fp32 split-K sum accumulated straight into the fp16/bf16 grad
-                    dw = None
-                else:
-                    dw = dw.to(w.dtype)
+            dw = _wgrad(dy, x, w, ctx.w_ref, stride, pad)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum(dim=(0, 1, 2))
         return dx, dw, db, None, None, None
@@ -487,15 +545,7 @@ class ConvTeeNHWC(torch.autograd.Function):
             else:
                 dx = torch.mm(g2, w2).view(x.shape)
         if ctx.needs_input_grad[1]:
-            key = ('wgrad', tuple(x.shape), tuple(w.shape), (1, 1), (0, 0), x.dtype)
-            dw = _select(key, _wgrad_candidates(gy, x, w, (1, 1), (0, 0)), 'miopen')
-            if dw.dtype != w.dtype:
-                tgt = _leaf_grad(ctx.w_ref, dtype=w.dtype)
-                if tgt is not None:
-                    tgt.add_(dw)
-                    dw = None
-                else:
-                    dw = dw.to(w.dtype)
+            dw = _wgrad(gy, x, w, ctx.w_ref, (1, 1), (0, 0))
         return dx, dw, None
 
 
@@ -524,7 +574,7 @@ def conv_ok(x, w, stride, pad, dilate, groups):
 
 
 _K.conv_ok = conv_ok
-__all__ += ['ConvNHWC', 'ConvTeeNHWC', 'conv_fwd', 'conv_ok_shape']
+__all__ += ['ConvNHWC', 'ConvTeeNHWC', 'conv_fwd', 'conv_ok_shape', 'conv_wgrad', 'conv_wgrad_ok']
 
 
 # ---------------------------------------------------------------------------

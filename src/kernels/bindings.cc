@@ -14,11 +14,13 @@
 namespace py = pybind11;
 
 namespace mxamd {
-void bn_nhwc_forward(int dtype, const void* x, const void* addend, void* y, const float* gamma, const float* beta,
+void bn_nhwc_forward(int dtype, const void* x, const void* addend, void* y, uint8_t* mask, const float* gamma,
+                     const float* beta,
                      const float* center, float* part, float* mean, float* invstd, float* var, float* scale,
                      float* shift, int64_t R, int C, float eps, int training, int relu, int fix_gamma,
                      float momentum, float* mm_upd, float* mv_upd, hipStream_t s);
-void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, void* dx, void* dz,
+void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, const uint8_t* mask, void* dx,
+                      void* dz,
                       const float* gamma, const float* mean, const float* invstd, const float* fscale,
                       const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R, int C,
                       int relu_mode, int fix_gamma, int training, int accum, hipStream_t s);
@@ -33,6 +35,9 @@ void flat_sgd(int dtype, void* w, const void* g, float* mom, float* w32, int64_t
               float momentum, float rescale, float clip, hipStream_t s);
 void conv_nhwc_fwd(int dtype, const void* x, const void* w, const float* bias, void* y, int N, int H, int W, int C,
                    int K, int R, int S, int sh, int sw, int ph, int pw, hipStream_t s);
+int64_t conv_nhwc_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw);
+void conv_nhwc_wgrad(int dtype, const void* x, const void* dy, float* slab, int out_dtype, void* out, int accum, int N,
+                     int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, hipStream_t s);
 void pool_nhwc_forward(int dtype, int is_max, const void* x, void* y, uint8_t* arg, int N, int H, int W, int C,
                        int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip, hipStream_t s);
 void pool_nhwc_backward(int dtype, int is_max, const void* dy, const uint8_t* arg, void* dx, int N, int H, int W,
@@ -58,21 +63,24 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.attr("arch") = "gfx950";
 
   m.def("bn_partials_rows", &bn_partials_rows);
-  m.def("bn_nhwc_forward", [](int dt, uintptr_t x, uintptr_t add, uintptr_t y, uintptr_t g, uintptr_t b,
+  // mask: optional uint8 ReLU bitmask (one byte per 8 elements) written by the add+relu tail
+  m.def("bn_nhwc_forward", [](int dt, uintptr_t x, uintptr_t add, uintptr_t y, uintptr_t mask, uintptr_t g, uintptr_t b,
                               uintptr_t center, uintptr_t part, uintptr_t mean, uintptr_t inv, uintptr_t var,
                               uintptr_t scale, uintptr_t shift, int64_t R, int C, float eps, int training, int relu,
                               int fix_gamma, float momentum, uintptr_t mm_upd, uintptr_t mv_upd, uintptr_t s) {
-    bn_nhwc_forward(dt, P<void>(x), P<void>(add), P<void>(y), P<float>(g), P<float>(b), P<float>(center),
+    bn_nhwc_forward(dt, P<void>(x), P<void>(add), P<void>(y), P<uint8_t>(mask), P<float>(g), P<float>(b), P<float>(center),
                     P<float>(part), P<float>(mean), P<float>(inv), P<float>(var), P<float>(scale), P<float>(shift), R,
                     C, eps, training, relu, fix_gamma, momentum, P<float>(mm_upd), P<float>(mv_upd), S(s));
     check_launch("bn_nhwc_forward");
   });
-  // relu_mode: 0 none, 1 mask from y, 2 mask recomputed from x*fscale+fshift; accum: += into dgamma/dbeta
-  m.def("bn_nhwc_backward", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t y, uintptr_t dx, uintptr_t dz,
+  // relu_mode: 0 none, 1 mask from y, 2 mask recomputed from x*fscale+fshift, 3 from the forward's bitmask;
+  // accum: += into dgamma/dbeta
+  m.def("bn_nhwc_backward", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t y, uintptr_t mask, uintptr_t dx,
+                               uintptr_t dz,
                                uintptr_t g, uintptr_t mean, uintptr_t inv, uintptr_t fscale, uintptr_t fshift,
                                uintptr_t part, uintptr_t dgamma, uintptr_t dbeta, uintptr_t coef, int64_t R, int C,
                                int relu_mode, int fix_gamma, int training, int accum, uintptr_t s) {
-    bn_nhwc_backward(dt, P<void>(x), P<void>(dy), P<void>(y), P<void>(dx), P<void>(dz), P<float>(g), P<float>(mean),
+    bn_nhwc_backward(dt, P<void>(x), P<void>(dy), P<void>(y), P<uint8_t>(mask), P<void>(dx), P<void>(dz), P<float>(g), P<float>(mean),
                      P<float>(inv), P<float>(fscale), P<float>(fshift), P<float>(part), P<float>(dgamma),
                      P<float>(dbeta), P<float>(coef), R, C, relu_mode, fix_gamma, training, accum, S(s));
     check_launch("bn_nhwc_backward");
@@ -106,6 +114,14 @@ PYBIND11_MODULE(_hip_kernels, m) {
     conv_nhwc_fwd(dt, P<void>(x), P<void>(w), P<float>(bias), P<void>(y), N, H, W, C, K, R, Sf, sh, sw, ph, pw,
                   S(s));
     check_launch("conv_nhwc_fwd");
+  });
+  m.def("conv_nhwc_wgrad_workspace", &conv_nhwc_wgrad_workspace);
+  m.def("conv_nhwc_wgrad", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t slab, int odt, uintptr_t out, int accum,
+                              int N, int H, int W, int C, int K, int R, int Sf, int sh, int sw, int ph, int pw,
+                              uintptr_t s) {
+    conv_nhwc_wgrad(dt, P<void>(x), P<void>(dy), P<float>(slab), odt, P<void>(out), accum, N, H, W, C, K, R, Sf, sh,
+                    sw, ph, pw, S(s));
+    check_launch("conv_nhwc_wgrad");
   });
   m.def("pool_nhwc_forward", [](int dt, int is_max, uintptr_t x, uintptr_t y, uintptr_t arg, int N, int H, int W,
                                 int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip,

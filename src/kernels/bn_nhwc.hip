@@ -48,12 +48,13 @@ static inline BnGeom bn_geom(int C) {
 constexpr int kReluNone = 0;   // no ReLU
 constexpr int kReluFromY = 1;  // mask = y > 0 (residual tail: y depends on the addend)
 constexpr int kReluFromX = 2;  // mask = x*scale + shift > 0 (recomputed, y not needed)
+constexpr int kReluFromMask = 3;  // residual tail: 1 bit per element written by the forward (y not kept)
 
 // MODE 0: forward sums of (x - shift) and (x - shift)^2
 // MODE 1: backward sums of dz and dz * (x - mean), dz = dy * mask (RELU != kReluNone)
 template <typename T, int MODE, int RELU>
 __global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(
-    const T* __restrict__ x, const T* __restrict__ dy, const T* __restrict__ y,
+    const T* __restrict__ x, const T* __restrict__ dy, const T* __restrict__ y, const uint8_t* __restrict__ mask,
     const float* __restrict__ center, const float* __restrict__ fscale, const float* __restrict__ fshift,
     float* __restrict__ part1, float* __restrict__ part2, int64_t R, int C, int tpr, int rpi,
     int64_t rows_per_block) {
@@ -78,7 +79,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(
   // rows are consumed UNR at a time: all loads of a batch are issued before any
   // accumulation, so each thread keeps UNR (x3 in backward) 16-byte loads in flight
   constexpr int UNR = 4;
-  auto accum = [&](const Vec8<T>& vx, const Vec8<T>& vdy, const Vec8<T>& vy) {
+  auto accum = [&](const Vec8<T>& vx, const Vec8<T>& vdy, const Vec8<T>& vy, uint32_t mb) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       if (MODE == 0) {
@@ -90,6 +91,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(
         const float xi = vx.get(i);
         if (RELU == kReluFromY) dz = vy.get(i) > 0.f ? dz : 0.f;
         if (RELU == kReluFromX) dz = fmaf(xi, fs[i], fh[i]) > 0.f ? dz : 0.f;
+        if (RELU == kReluFromMask) dz = ((mb >> i) & 1u) ? dz : 0.f;
         s1[i] += dz;
         s2[i] += dz * (xi - k[i]);
       }
@@ -98,15 +100,17 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(
   int64_t r = r0 + lane_r;
   for (; r + (UNR - 1) * rpi < r1; r += UNR * rpi) {
     Vec8<T> vx[UNR], vdy[UNR], vy[UNR];
+    uint32_t vm[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int64_t off = (r + u * rpi) * C + cbase;
       vx[u].load(x + off);
       if (MODE == 1) vdy[u].load(dy + off);
       if (MODE == 1 && RELU == kReluFromY) vy[u].load(y + off);
+      vm[u] = (MODE == 1 && RELU == kReluFromMask) ? mask[off >> 3] : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) accum(vx[u], vdy[u], vy[u]);
+    for (int u = 0; u < UNR; ++u) accum(vx[u], vdy[u], vy[u], vm[u]);
   }
   for (; r < r1; r += rpi) {
     const int64_t off = r * C + cbase;
@@ -114,7 +118,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(
     vx.load(x + off);
     if (MODE == 1) vdy.load(dy + off);
     if (MODE == 1 && RELU == kReluFromY) vy.load(y + off);
-    accum(vx, vdy, vy);
+    accum(vx, vdy, vy, (MODE == 1 && RELU == kReluFromMask) ? mask[off >> 3] : 0u);
   }
   // reduce the rpi row-lanes that share a channel group through LDS
   __shared__ float sh1[kBnThreads * 8];
@@ -222,10 +226,11 @@ __global__ void __launch_bounds__(kFinThreads) bn_finalize_kernel(
 }
 
 // y = x * scale + shift (+ addend) (relu)
-template <typename T, bool ADD, bool RELU>
+// MASK: also write the ReLU mask, one byte per 8-element vector (bit i = y[8v+i] > 0)
+template <typename T, bool ADD, bool RELU, bool MASK>
 __global__ void __launch_bounds__(kBnThreads) bn_apply_kernel(
     const T* __restrict__ x, const T* __restrict__ addend, const float* __restrict__ scale,
-    const float* __restrict__ shift, T* __restrict__ y, int64_t nvec, int C) {
+    const float* __restrict__ shift, T* __restrict__ y, uint8_t* __restrict__ mask, int64_t nvec, int C) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   // channel of this thread's first vector; advancing by `stride` vectors moves
@@ -244,21 +249,24 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_kernel(
     const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
     Vec8<T> va;
     if (ADD) va.load(addend + off);
+    uint32_t bits = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float r = vx.get(i) * sc[i] + sh[i];
       if (ADD) r += va.get(i);
+      if (MASK) bits |= (r > 0.f ? 1u : 0u) << i;
       if (RELU) r = r > 0.f ? r : 0.f;
       out.set(i, r);
     }
     out.store(y + off);
+    if (MASK) mask[v] = static_cast<uint8_t>(bits);
   }
 }
 
 // dx = A*dz + B*x + Cc, dz = dy * mask (see RELU modes); optionally d_addend = dz
 template <typename T, int RELU, bool WRITE_DZ>
 __global__ void __launch_bounds__(kBnThreads) bn_bwd_apply_kernel(
-    const T* __restrict__ x, const T* __restrict__ dy, const T* __restrict__ y,
+    const T* __restrict__ x, const T* __restrict__ dy, const T* __restrict__ y, const uint8_t* __restrict__ mask,
     const float* __restrict__ A, const float* __restrict__ B, const float* __restrict__ Cc,
     const float* __restrict__ fscale, const float* __restrict__ fshift,
     T* __restrict__ dx, T* __restrict__ dz_out, int64_t nvec, int C) {
@@ -272,6 +280,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_bwd_apply_kernel(
     vx.load(x + off);
     vdy.load(dy + off);
     if (RELU == kReluFromY) vy.load(y + off);
+    const uint32_t mb = RELU == kReluFromMask ? mask[v] : 0u;
     float fs[8], fh[8];
     if (RELU == kReluFromX) {
       const float4 s0 = *reinterpret_cast<const float4*>(fscale + c);
@@ -295,6 +304,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_bwd_apply_kernel(
       float d = vdy.get(i);
       if (RELU == kReluFromY) d = vy.get(i) > 0.f ? d : 0.f;
       if (RELU == kReluFromX) d = fmaf(vx.get(i), fs[i], fh[i]) > 0.f ? d : 0.f;
+      if (RELU == kReluFromMask) d = ((mb >> i) & 1u) ? d : 0.f;
       if (WRITE_DZ) dz.set(i, d);
       out.set(i, ka[i] * d + kb[i] * vx.get(i) + kc[i]);
     }
@@ -324,7 +334,7 @@ int bn_partials_rows(int64_t R, int C) {
 }
 
 template <typename T>
-static void bn_forward_impl(const void* x, const void* addend, void* y, const float* gamma,
+static void bn_forward_impl(const void* x, const void* addend, void* y, uint8_t* mask, const float* gamma,
                             const float* beta, const float* center, float* part, float* mean, float* invstd,
                             float* var, float* scale, float* shift, int64_t R, int C, float eps, int training,
                             int relu, int fix_gamma, float momentum, float* mm_upd, float* mv_upd, hipStream_t s) {
@@ -338,7 +348,7 @@ static void bn_forward_impl(const void* x, const void* addend, void* y, const fl
     float* p1 = part;
     float* p2 = part + static_cast<int64_t>(nblk) * C;
     hipLaunchKernelGGL((bn_reduce_kernel<T, 0, kReluNone>), grid, dim3(kBnThreads), 0, s,
-                       static_cast<const T*>(x), nullptr, nullptr, center, nullptr, nullptr, p1, p2, R, C, g.tpr,
+                       static_cast<const T*>(x), nullptr, nullptr, nullptr, center, nullptr, nullptr, p1, p2, R, C, g.tpr,
                        g.rpi, rpb);
     hipLaunchKernelGGL((bn_finalize_kernel<0>), dim3(C), dim3(kFinThreads), 0, s, p1, p2, nblk, C, R, center, gamma,
                        beta, nullptr, eps, mean, invstd, var, scale, shift, nullptr, fix_gamma, 1, momentum, mm_upd,
@@ -350,25 +360,24 @@ static void bn_forward_impl(const void* x, const void* addend, void* y, const fl
   const T* xa = static_cast<const T*>(x);
   const T* aa = static_cast<const T*>(addend);
   T* ya = static_cast<T*>(y);
+#define APPLY(ADD, RELU, MASK)                                                                              \
+  hipLaunchKernelGGL((bn_apply_kernel<T, ADD, RELU, MASK>), dim3(blocks), dim3(kBnThreads), 0, s, xa, aa, scale, \
+                     shift, ya, mask, nvec, C)
+  MXAMD_HOST_CHECK(mask == nullptr || (addend && relu), "bn_nhwc_forward: mask output only for add+relu");
   if (addend) {
-    if (relu)
-      hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), dim3(blocks), dim3(kBnThreads), 0, s, xa, aa, scale,
-                         shift, ya, nvec, C);
-    else
-      hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), dim3(blocks), dim3(kBnThreads), 0, s, xa, aa, scale,
-                         shift, ya, nvec, C);
+    if (relu) {
+      if (mask) APPLY(true, true, true); else APPLY(true, true, false);
+    } else {
+      APPLY(true, false, false);
+    }
   } else {
-    if (relu)
-      hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), dim3(blocks), dim3(kBnThreads), 0, s, xa, aa, scale,
-                         shift, ya, nvec, C);
-    else
-      hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), dim3(blocks), dim3(kBnThreads), 0, s, xa, aa, scale,
-                         shift, ya, nvec, C);
+    if (relu) APPLY(false, true, false); else APPLY(false, false, false);
   }
+#undef APPLY
 }
 
 template <typename T>
-static void bn_backward_impl(const void* x, const void* dy, const void* y, void* dx, void* dz,
+static void bn_backward_impl(const void* x, const void* dy, const void* y, const uint8_t* mask, void* dx, void* dz,
                              const float* gamma, const float* mean, const float* invstd, const float* fscale,
                              const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R,
                              int C, int relu_mode, int fix_gamma, int training, int accum, hipStream_t s) {
@@ -383,11 +392,14 @@ static void bn_backward_impl(const void* x, const void* dy, const void* y, void*
   const T* ya = static_cast<const T*>(y);
   MXAMD_HOST_CHECK(relu_mode != kReluFromY || y != nullptr, "bn_nhwc_backward: relu mask from y needs y");
   MXAMD_HOST_CHECK(relu_mode != kReluFromX || (fscale && fshift), "bn_nhwc_backward: relu-from-x needs scale/shift");
+  MXAMD_HOST_CHECK(relu_mode != kReluFromMask || mask != nullptr, "bn_nhwc_backward: relu-from-mask needs the mask");
 #define RED(RL)                                                                                                \
-  hipLaunchKernelGGL((bn_reduce_kernel<T, 1, RL>), grid, dim3(kBnThreads), 0, s, xa, dya, ya, mean, fscale, fshift, \
+  hipLaunchKernelGGL((bn_reduce_kernel<T, 1, RL>), grid, dim3(kBnThreads), 0, s, xa, dya, ya, mask, mean, fscale, \
+                     fshift,                                                                                         \
                      p1, p2, R, C, g.tpr, g.rpi, rpb)
   if (relu_mode == kReluFromY) RED(kReluFromY);
   else if (relu_mode == kReluFromX) RED(kReluFromX);
+  else if (relu_mode == kReluFromMask) RED(kReluFromMask);
   else RED(kReluNone);
 #undef RED
   float* A = coef;
@@ -402,52 +414,56 @@ static void bn_backward_impl(const void* x, const void* dy, const void* y, void*
   T* dxa = static_cast<T*>(dx);
   T* dza = static_cast<T*>(dz);
 #define BWD(RL, WD)                                                                                      \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RL, WD>), dim3(blocks), dim3(kBnThreads), 0, s, xa, dya, ya, A, B, \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RL, WD>), dim3(blocks), dim3(kBnThreads), 0, s, xa, dya, ya, mask, A, B, \
                      Cc, fscale, fshift, dxa, dza, nvec, C)
   if (relu_mode == kReluFromY) {
     if (dz) BWD(kReluFromY, true); else BWD(kReluFromY, false);
   } else if (relu_mode == kReluFromX) {
     if (dz) BWD(kReluFromX, true); else BWD(kReluFromX, false);
+  } else if (relu_mode == kReluFromMask) {
+    if (dz) BWD(kReluFromMask, true); else BWD(kReluFromMask, false);
   } else {
     if (dz) BWD(kReluNone, true); else BWD(kReluNone, false);
   }
 #undef BWD
 }
 
-void bn_nhwc_forward(int dtype, const void* x, const void* addend, void* y, const float* gamma, const float* beta,
+void bn_nhwc_forward(int dtype, const void* x, const void* addend, void* y, uint8_t* mask, const float* gamma,
+                     const float* beta,
                      const float* center, float* part, float* mean, float* invstd, float* var, float* scale,
                      float* shift, int64_t R, int C, float eps, int training, int relu, int fix_gamma,
                      float momentum, float* mm_upd, float* mv_upd, hipStream_t s) {
   switch (dtype) {
     case kF16:
-      bn_forward_impl<__half>(x, addend, y, gamma, beta, center, part, mean, invstd, var, scale, shift, R, C, eps,
+      bn_forward_impl<__half>(x, addend, y, mask, gamma, beta, center, part, mean, invstd, var, scale, shift, R, C, eps,
                               training, relu, fix_gamma, momentum, mm_upd, mv_upd, s);
       break;
     case kBF16:
-      bn_forward_impl<__hip_bfloat16>(x, addend, y, gamma, beta, center, part, mean, invstd, var, scale, shift, R,
+      bn_forward_impl<__hip_bfloat16>(x, addend, y, mask, gamma, beta, center, part, mean, invstd, var, scale, shift, R,
                                       C, eps, training, relu, fix_gamma, momentum, mm_upd, mv_upd, s);
       break;
     default:
-      bn_forward_impl<float>(x, addend, y, gamma, beta, center, part, mean, invstd, var, scale, shift, R, C, eps,
+      bn_forward_impl<float>(x, addend, y, mask, gamma, beta, center, part, mean, invstd, var, scale, shift, R, C, eps,
                              training, relu, fix_gamma, momentum, mm_upd, mv_upd, s);
   }
 }
 
-void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, void* dx, void* dz,
+void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, const uint8_t* mask, void* dx,
+                      void* dz,
                       const float* gamma, const float* mean, const float* invstd, const float* fscale,
                       const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R, int C,
                       int relu_mode, int fix_gamma, int training, int accum, hipStream_t s) {
   switch (dtype) {
     case kF16:
-      bn_backward_impl<__half>(x, dy, y, dx, dz, gamma, mean, invstd, fscale, fshift, part, dgamma, dbeta, coef, R,
+      bn_backward_impl<__half>(x, dy, y, mask, dx, dz, gamma, mean, invstd, fscale, fshift, part, dgamma, dbeta, coef, R,
                                C, relu_mode, fix_gamma, training, accum, s);
       break;
     case kBF16:
-      bn_backward_impl<__hip_bfloat16>(x, dy, y, dx, dz, gamma, mean, invstd, fscale, fshift, part, dgamma, dbeta,
+      bn_backward_impl<__hip_bfloat16>(x, dy, y, mask, dx, dz, gamma, mean, invstd, fscale, fshift, part, dgamma, dbeta,
                                        coef, R, C, relu_mode, fix_gamma, training, accum, s);
       break;
     default:
-      bn_backward_impl<float>(x, dy, y, dx, dz, gamma, mean, invstd, fscale, fshift, part, dgamma, dbeta, coef, R,
+      bn_backward_impl<float>(x, dy, y, mask, dx, dz, gamma, mean, invstd, fscale, fshift, part, dgamma, dbeta, coef, R,
                               C, relu_mode, fix_gamma, training, accum, s);
   }
 }
