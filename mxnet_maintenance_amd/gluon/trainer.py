@@ -78,6 +78,11 @@ class _Arena:
             self.views.append((off, n, t.shape))
         self.mom = None
         self.w32 = None
+        self.mean = None     # Adam / AdamW / LAMB fp32 state
+        self.var = None
+        self.upd = None      # LAMB phase-1 direction (fp32)
+        self.table = None    # LAMB chunk -> parameter segment table
+        self.nrm = None
         self.all_write = all(p.grad_req == 'write' for p in params)
 
 
@@ -199,7 +204,7 @@ class Trainer:
             return False
         if self._update_on_kvstore or not self._contexts or len(self._contexts) != 1:
             return False
-        if not isinstance(self._optimizer, opt.SGD) or type(self._optimizer) not in (opt.SGD, opt.ccSGD):
+        if type(self._optimizer) not in (opt.SGD, opt.ccSGD, opt.Adam, opt.AdamW, opt.LAMB):
             return False
         if self._kvstore is not None and not isinstance(self._kvstore, _kvs.KVStore):
             return False
@@ -226,19 +231,38 @@ class Trainer:
         o = self._optimizer
         mp = o.multi_precision
         upd = self._updaters[0]
+        kind = 'sgd' if isinstance(o, opt.SGD) else type(o).__name__.lower()
         for a in self._arenas:
-            if o.momentum != 0.0:
-                a.mom = torch.zeros(a.numel, dtype=torch.float32, device=a.device)
-            if mp and a.dtype in (torch.float16, torch.bfloat16):
+            half = a.dtype in (torch.float16, torch.bfloat16)
+            if mp and half:
                 a.w32 = a.w.float()
+            if kind == 'sgd':
+                if o.momentum != 0.0:
+                    a.mom = torch.zeros(a.numel, dtype=torch.float32, device=a.device)
+            else:
+                a.mean = torch.zeros(a.numel, dtype=torch.float32, device=a.device)
+                a.var = torch.zeros(a.numel, dtype=torch.float32, device=a.device)
+                if kind == 'lamb':
+                    from ..ops.nlp_fns import ChunkTable
+                    a.upd = torch.empty(a.numel, dtype=torch.float32, device=a.device)
+                    a.table = ChunkTable([(off, n) for (off, n, _shape) in a.views], a.device)
+                    a.nrm = torch.zeros(2 * len(a.views), dtype=torch.float32, device=a.device)
             for (off, n, shape), idx in zip(a.views, a.indices):
-                mom = NDArray(a.mom[off:off + n].view(shape)) if a.mom is not None else None
-                if a.w32 is not None:
-                    st = (mom, NDArray(a.w32[off:off + n].view(shape)))
+                w32v = NDArray(a.w32[off:off + n].view(shape)) if a.w32 is not None else None
+                if kind == 'sgd':
+                    mom = NDArray(a.mom[off:off + n].view(shape)) if a.mom is not None else None
+                    st = (mom, w32v) if w32v is not None else mom
                 else:
-                    st = mom
+                    mv = (NDArray(a.mean[off:off + n].view(shape)), NDArray(a.var[off:off + n].view(shape)))
+                    if w32v is None:
+                        st = mv
+                    elif kind == 'adam':
+                        st = (w32v, mv)       # Optimizer.create_state_multi_precision layout
+                    else:
+                        st = (w32v,) + mv     # AdamW / LAMB layout
                 upd.states[idx] = st
                 upd.states_synced[idx] = True
+        self._arena_kind = kind
         if self._kvstore is not None and dist.world_size() > 1:
             arrays = []
             reqs = []
@@ -411,13 +435,23 @@ class Trainer:
                     d._fresh_grad = False
 
     def _fused_update(self):
+        import math
         o = self._optimizer
         clip = -1.0 if o.clip_gradient is None else o.clip_gradient
+        kind = getattr(self, '_arena_kind', 'sgd')
         for a in self._arenas:
             o._update_count(a.indices)
             lr = o._get_lrs(a.indices[:1])[0]
             wd = o._get_wds(a.indices[:1])[0]
-            flat_sgd_update(a.w, a.g, a.mom, a.w32, lr, wd, o.momentum, o.rescale_grad, clip)
+            t = o._index_update_count[a.indices[0]]
+            if kind == 'sgd':
+                flat_sgd_update(a.w, a.g, a.mom, a.w32, lr, wd, o.momentum, o.rescale_grad, clip)
+            elif kind in ('adam', 'adamw'):
+                if kind == 'adam' or o.correct_bias:
+                    lr *= math.sqrt(1. - o.beta2 ** t) / (1. - o.beta1 ** t)
+                flat_adam_update(a, lr, o.beta1, o.beta2, o.epsilon, wd, o.rescale_grad, clip, kind == 'adamw')
+            else:
+                lamb_flat_update(a, lr, o, t, wd, clip)
 
     def save_states(self, fname):
         assert self._optimizer is not None
@@ -451,20 +485,40 @@ class Trainer:
             if self._arenas is not None:
                 upd = self._updaters[0]
                 for a in self._arenas:
+                    kind = getattr(self, '_arena_kind', 'sgd')
                     for (off, n, shape), idx in zip(a.views, a.indices):
                         st = upd.states[idx]
+
+                        def cp(dst, src):
+                            dst[off:off + n].copy_(src._data.reshape(-1).to(dst.device, dst.dtype))
                         with torch.no_grad():
-                            if a.w32 is not None:
-                                mom, w32 = st
-                                a.w32[off:off + n].copy_(w32._data.reshape(-1).to(a.w32.device))
+                            if kind == 'sgd':
+                                if a.w32 is not None:
+                                    mom, w32 = st
+                                    cp(a.w32, w32)
+                                else:
+                                    mom = st
+                                if a.mom is not None and mom is not None:
+                                    cp(a.mom, mom)
                             else:
-                                mom = st
-                            if a.mom is not None and mom is not None:
-                                a.mom[off:off + n].copy_(mom._data.reshape(-1).to(a.mom.device))
+                                if a.w32 is None:
+                                    mean, var = st
+                                elif kind == 'adam':
+                                    w32, (mean, var) = st
+                                    cp(a.w32, w32)
+                                else:
+                                    w32, mean, var = st
+                                    cp(a.w32, w32)
+                                cp(a.mean, mean)
+                                cp(a.var, var)
                         # rebind state views to the arena
-                        momv = NDArray(a.mom[off:off + n].view(shape)) if a.mom is not None else None
-                        upd.states[idx] = (momv, NDArray(a.w32[off:off + n].view(shape))) \
-                            if a.w32 is not None else momv
+                        w32v = NDArray(a.w32[off:off + n].view(shape)) if a.w32 is not None else None
+                        if kind == 'sgd':
+                            momv = NDArray(a.mom[off:off + n].view(shape)) if a.mom is not None else None
+                            upd.states[idx] = (momv, w32v) if w32v is not None else momv
+                        else:
+                            mv = (NDArray(a.mean[off:off + n].view(shape)), NDArray(a.var[off:off + n].view(shape)))
+                            upd.states[idx] = mv if w32v is None else ((w32v, mv) if kind == 'adam' else (w32v,) + mv)
         param_dict = {i: param for i, param in enumerate(self._params)}
         self._optimizer.param_dict = param_dict
 
@@ -527,3 +581,46 @@ def flat_sgd_update(w, g, mom, w32, lr, wd, momentum, rescale, clip):
         tgt.add_(gg, alpha=-lr)
     if w32 is not None:
         w.copy_(w32)
+
+
+@torch.no_grad()
+def flat_adam_update(a, lr, beta1, beta2, eps, wd, rescale, clip, adamw):
+    """Adam / AdamW over one arena: fused HIP kernel on gfx950, torch ops elsewhere (same math)."""
+    if a.w.is_cuda and _K.available() and _K.enabled() and hasattr(_K, 'flat_adam'):
+        _K.flat_adam(a.w, a.g, a.mean, a.var, a.w32, lr, beta1, beta2, eps, wd, rescale, clip, adamw=adamw)
+        return
+    w = a.w32 if a.w32 is not None else a.w
+    g = a.g.float() * rescale
+    if not adamw and wd:
+        g = g + wd * w.float()
+    if clip is not None and clip >= 0:
+        g = g.clamp(-clip, clip)
+    a.mean.mul_(beta1).add_(g, alpha=1 - beta1)
+    a.var.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+    step = lr * a.mean / (a.var.sqrt() + eps)
+    if adamw:
+        step = step + wd * w.float()
+    w.sub_(step.to(w.dtype))
+    if a.w32 is not None:
+        a.w.copy_(a.w32)
+
+
+@torch.no_grad()
+def lamb_flat_update(a, lr, o, t, wd, clip):
+    """LAMB (phase 1 + per-parameter trust ratio + phase 2) over one arena."""
+    lb = -1.0 if o.lower_bound is None else o.lower_bound
+    ub = -1.0 if o.upper_bound is None else o.upper_bound
+    if a.w.is_cuda and _K.available() and _K.enabled() and hasattr(_K, 'lamb_update'):
+        _K.lamb_update(a.w, a.g, a.mean, a.var, a.w32, a.upd, a.table, a.nrm, lr, o.beta1, o.beta2, o.epsilon, t,
+                       o.bias_correction, wd, o.rescale_grad, clip, lb, ub)
+        return
+    from ..ops import optimizer_ops as _oo
+    for off, n, _shape in a.views:
+        w = a.w[off:off + n]
+        w32 = a.w32[off:off + n] if a.w32 is not None else None
+        tgt = w32 if w32 is not None else w
+        g = _oo._lamb1(tgt, a.g[off:off + n].float(), a.mean[off:off + n], a.var[off:off + n], o.beta1, o.beta2,
+                       o.epsilon, t, o.bias_correction, wd, o.rescale_grad, clip)
+        r1 = torch.linalg.vector_norm(tgt.float()).reshape(1)
+        r2 = torch.linalg.vector_norm(g).reshape(1)
+        _oo._lamb2(w, g, r1, r2, lr, lb, ub, w32=w32)

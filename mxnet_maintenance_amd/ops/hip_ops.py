@@ -221,6 +221,20 @@ def layer_norm(data, gamma, beta, eps):
     return y.to(data.dtype), mean.to(data.dtype), std.to(data.dtype)
 
 
+def softmax(x, axis=-1, scale=1.0, log=False):
+    """softmax / log_softmax of x*scale along ``axis``; None when the HIP kernel does not apply."""
+    if _use_hip(x) and hasattr(_K, 'Softmax') and _K.softmax_ok(x, axis):
+        return _K.Softmax.apply(x, scale, log)
+    return None
+
+
+def dropout(x, p):
+    """(y, mask) Philox dropout on the GPU; None when the HIP kernel does not apply."""
+    if _use_hip(x) and hasattr(_K, 'Dropout') and _K.ew_ok(x) and 0.0 < p < 1.0:
+        return _K.Dropout.apply(x, p)
+    return None
+
+
 def softmax_ce(logits, label, reduction='none'):
     """Cross entropy of softmax(logits) against integer labels (fp32 accumulation)."""
     if _use_hip(logits) and _K.ce_ok(logits):

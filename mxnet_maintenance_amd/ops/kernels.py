@@ -81,3 +81,4 @@ def gap_ok(x):
 
 
 from .kernel_fns import *  # noqa: E402,F401,F403
+from .nlp_fns import *  # noqa: E402,F401,F403

@@ -1,0 +1,318 @@
+"""torch.autograd wrappers for the transformer-path gfx950 kernels (src/kernels/nlp_kernels.hip)
+and the fused flat-arena optimizer kernels (src/kernels/optim_kernels.hip).
+
+LayerNorm (fwd/bwd with dgamma/dbeta straight into the parameters' fp32 grad
+buffers), erf-GELU, last-axis softmax / log_softmax (with temperature) and
+Philox dropout with a 1-bit mask.  Numerics vs fp32 torch references:
+tests/test_hip_kernels.py.
+"""
+import torch
+
+from . import kernels as _K
+from .kernel_fns import _DT, _stream, _p, _f32, _leaf_grad
+
+__all__ = ['LayerNorm', 'GELU', 'Softmax', 'Dropout', 'ln_ok', 'ew_ok', 'softmax_ok',
+           'flat_adam', 'lamb_update', 'seg_sumsq', 'all_finite', 'ChunkTable']
+
+
+def _aligned(t):
+    return t.is_contiguous() and t.data_ptr() % 16 == 0
+
+
+def ln_ok(x):
+    return x.dtype in _DT and x.dim() >= 2 and _aligned(x) and x.shape[-1] % 8 == 0 and 8 <= x.shape[-1] <= 4096
+
+
+def ew_ok(x):
+    return x.dtype in _DT and _aligned(x) and x.numel() % 8 == 0 and x.numel() > 0
+
+
+def softmax_ok(x, axis):
+    return (x.dtype in _DT and x.dim() >= 1 and axis % x.dim() == x.dim() - 1 and _aligned(x)
+            and x.shape[-1] % 8 == 0 and 8 <= x.shape[-1] <= 8192 and x.numel() > 0)
+
+
+_K.ln_ok = ln_ok
+_K.ew_ok = ew_ok
+
+
+class LayerNorm(torch.autograd.Function):
+    """y = (x - mean) / sqrt(var + eps) * gamma + beta over the last axis; returns (y, mean, std)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        lib = _K.lib()
+        D = x.shape[-1]
+        M = x.numel() // D
+        g = _f32(gamma)
+        b = _f32(beta)
+        y = torch.empty_like(x)
+        stats = torch.empty(2, M, dtype=torch.float32, device=x.device)
+        mean, rstd = stats[0], stats[1]
+        lib.layernorm_forward(_DT[x.dtype], x.data_ptr(), g.data_ptr(), b.data_ptr(), y.data_ptr(), mean.data_ptr(),
+                              rstd.data_ptr(), M, D, float(eps), _stream())
+        ctx.save_for_backward(x, g, mean, rstd)
+        ctx.refs = (gamma, beta)
+        shp = tuple(x.shape[:-1]) + (1,)
+        m_out = mean.view(shp).to(x.dtype)
+        s_out = torch.reciprocal(rstd).view(shp).to(x.dtype)     # std = sqrt(var + eps)
+        ctx.mark_non_differentiable(m_out, s_out)
+        ctx.set_materialize_grads(False)
+        return y, m_out, s_out
+
+    @staticmethod
+    def backward(ctx, gy, _gm, _gs):
+        if gy is None:
+            return None, None, None, None
+        lib = _K.lib()
+        x, g, mean, rstd = ctx.saved_tensors
+        gamma, beta = ctx.refs
+        gy = gy.contiguous()
+        D = x.shape[-1]
+        M = x.numel() // D
+        dx = torch.empty_like(x)
+        nb = lib.layernorm_bwd_partials(M)
+        part = torch.empty(nb * 2 * D, dtype=torch.float32, device=x.device)
+        need_g, need_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        tg = _leaf_grad(gamma, D) if need_g else None
+        tb = _leaf_grad(beta, D) if need_b else None
+        if tg is not None and tb is not None:
+            dg, db, accum = tg, tb, 1
+        else:
+            out = torch.empty(2, D, dtype=torch.float32, device=x.device)
+            dg, db, accum = out[0], out[1], 0
+        lib.layernorm_backward(_DT[x.dtype], x.data_ptr(), gy.data_ptr(), g.data_ptr(), mean.data_ptr(),
+                               rstd.data_ptr(), dx.data_ptr(), part.data_ptr(), dg.data_ptr(), db.data_ptr(), accum,
+                               M, D, _stream())
+        if accum:
+            return dx, None, None, None
+        return (dx, dg.view(gamma.shape).to(gamma.dtype) if need_g else None,
+                db.view(beta.shape).to(beta.dtype) if need_b else None, None)
+
+
+class GELU(torch.autograd.Function):
+    """erf-GELU (MXNet LeakyReLU act_type='gelu')."""
+
+    @staticmethod
+    def forward(ctx, x):
+        y = torch.empty_like(x)
+        _K.lib().gelu_forward(_DT[x.dtype], x.data_ptr(), y.data_ptr(), x.numel(), _stream())
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, = ctx.saved_tensors
+        gy = gy.contiguous()
+        dx = torch.empty_like(x)
+        _K.lib().gelu_backward(_DT[x.dtype], x.data_ptr(), gy.data_ptr(), dx.data_ptr(), x.numel(), _stream())
+        return dx
+
+
+class Softmax(torch.autograd.Function):
+    """softmax / log_softmax of (x * scale) over the last axis, one wave per row."""
+
+    @staticmethod
+    def forward(ctx, x, scale=1.0, log=False):
+        L = x.shape[-1]
+        M = x.numel() // L
+        y = torch.empty_like(x)
+        _K.lib().softmax_forward(_DT[x.dtype], int(bool(log)), x.data_ptr(), y.data_ptr(), M, L, float(scale),
+                                 _stream())
+        ctx.save_for_backward(y)
+        ctx.cfg = (float(scale), bool(log))
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        y, = ctx.saved_tensors
+        scale, log = ctx.cfg
+        gy = gy.contiguous()
+        L = y.shape[-1]
+        M = y.numel() // L
+        dx = torch.empty_like(y)
+        _K.lib().softmax_backward(_DT[y.dtype], int(log), y.data_ptr(), gy.data_ptr(), dx.data_ptr(), M, L, scale,
+                                  _stream())
+        return dx, None, None
+
+
+def _seed():
+    # drawn from torch's default CPU generator, so mx.random.seed() makes the masks reproducible
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+class Dropout(torch.autograd.Function):
+    """y = x * keep / (1 - p), keep ~ Bernoulli(1 - p) from Philox(seed, index); returns (y, bitmask)."""
+
+    @staticmethod
+    def forward(ctx, x, p):
+        y = torch.empty_like(x)
+        mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device)
+        _K.lib().dropout_forward(_DT[x.dtype], x.data_ptr(), y.data_ptr(), mask.data_ptr(), x.numel(), float(p),
+                                 _seed(), _stream())
+        ctx.save_for_backward(mask)
+        ctx.p = float(p)
+        ctx.mark_non_differentiable(mask)
+        return y, mask
+
+    @staticmethod
+    def backward(ctx, gy, _gm):
+        mask, = ctx.saved_tensors
+        gy = gy.contiguous()
+        dx = torch.empty_like(gy)
+        _K.lib().dropout_backward(_DT[gy.dtype], gy.data_ptr(), mask.data_ptr(), dx.data_ptr(), gy.numel(), ctx.p,
+                                  _stream())
+        return dx, None
+
+
+# ---------------------------------------------------------------------------
+# flat-arena optimizers
+# ---------------------------------------------------------------------------
+
+class ChunkTable:
+    """Device table mapping <= chunk-element pieces of an arena to parameter segments.
+
+    ``segments``: list of (offset, length) in elements (offsets 8-aligned).  Each
+    entry is (int64 start, int32 len, int32 seg) = 16 bytes, the layout of
+    ``struct Chunk`` in src/kernels/optim_kernels.hip.
+    """
+
+    def __init__(self, segments, device, chunk=2048 * 8):
+        import numpy as np
+        rows = []
+        for seg, (off, n) in enumerate(segments):
+            n8 = (n + 7) // 8 * 8
+            for s in range(0, n8, chunk):
+                rows.append((off + s, min(chunk, n8 - s), seg))
+        arr = np.zeros(len(rows), dtype=[('start', '<i8'), ('len', '<i4'), ('seg', '<i4')])
+        for i, r in enumerate(rows):
+            arr[i] = r
+        self.n = len(rows)
+        self.nseg = len(segments)
+        self.table = torch.from_numpy(arr.view(np.uint8).copy()).to(device)
+
+
+def flat_adam(w, g, mean, var, w32, lr, beta1, beta2, eps, wd, rescale, clip, adamw=False, eta=1.0):
+    lib = _K.lib()
+    n = w.numel()
+    assert n % 8 == 0 and g.numel() == n and mean.numel() == n and var.numel() == n
+    lib.flat_adam(_DT[w.dtype], int(bool(adamw)), w.data_ptr(), g.data_ptr(), mean.data_ptr(), var.data_ptr(), _p(w32),
+                  n, float(lr), float(beta1), float(beta2), float(eps), float(wd), float(eta), float(rescale),
+                  float(clip), _stream())
+
+
+def lamb_update(w, g, mean, var, w32, upd, table, nrm, lr, beta1, beta2, eps, t, bias_correction, wd, rescale, clip,
+                lower_bound=-1.0, upper_bound=-1.0):
+    bc1 = 1.0 - beta1 ** t if bias_correction else 1.0
+    bc2 = 1.0 - beta2 ** t if bias_correction else 1.0
+    _K.lib().lamb_update(_DT[w.dtype], w.data_ptr(), g.data_ptr(), mean.data_ptr(), var.data_ptr(), _p(w32),
+                         upd.data_ptr(), table.table.data_ptr(), table.n, nrm.data_ptr(), table.nseg, float(lr),
+                         float(beta1), float(beta2), float(eps), float(bc1), float(bc2), float(wd), float(rescale),
+                         float(clip), float(lower_bound), float(upper_bound), _stream())
+
+
+def seg_sumsq(x, table):
+    out = torch.empty(table.nseg, dtype=torch.float32, device=x.device)
+    _K.lib().seg_sumsq(_DT[x.dtype], x.data_ptr(), table.table.data_ptr(), table.n, out.data_ptr(), table.nseg,
+                       _stream())
+    return out
+
+
+def all_finite(x, scale=1.0, flag=None):
+    """int32 device flag: 1 when every element of x*scale is finite (x flat, numel % 8 == 0)."""
+    init = flag is None
+    if flag is None:
+        flag = torch.empty(1, dtype=torch.int32, device=x.device)
+    _K.lib().all_finite(_DT[x.dtype], x.data_ptr(), x.numel(), float(scale), flag.data_ptr(), int(init), _stream())
+    return flag
+
+
+_K.LayerNorm = LayerNorm
+_K.GELU = GELU
+
+
+# ---------------------------------------------------------------------------
+# FullyConnected on MFMA: the NHWC implicit-GEMM kernels with a 1x1 "image"
+# ---------------------------------------------------------------------------
+# y[M,N] = x[M,K] W[N,K]^T + b is conv_nhwc_fwd on x viewed as [M,1,1,K] with the
+# OHWI weight [N,1,1,K] (bias in the epilogue); dX = dY W is the same kernel with
+# W^T; dW = dY^T X is the split-pixel MFMA wgrad kernel.  Per (pass, shape) the
+# autotuner (kernel_fns._select) compares them with hipBLASLt (torch.mm) and
+# keeps the faster.
+
+from . import kernel_fns as _KF  # noqa: E402
+
+
+def gemm_ok(x, w):
+    return (x.is_cuda and x.dtype in (torch.float16, torch.bfloat16) and w.dtype == x.dtype and w.dim() == 2
+            and x.shape[-1] == w.shape[1] and x.numel() > 0 and x.numel() // x.shape[-1] < 2 ** 31 // max(1, w.shape[0]))
+
+
+def _fc_fwd_cands(x2, w, b):
+    M, K = x2.shape
+    N = w.shape[0]
+    c = []
+    if K % 32 == 0 and N % 64 == 0 and x2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0:
+        c.append(('hip', lambda: _KF.conv_fwd(x2.view(M, 1, 1, K), w.view(N, 1, 1, K), (1, 1), (0, 0),
+                                              b).view(M, N)))
+    c.append(('mm', lambda: torch.nn.functional.linear(x2, w, None if b is None else b.to(x2.dtype))))
+    return c
+
+
+def _fc_dgrad_cands(dy2, w):
+    M, N = dy2.shape
+    K = w.shape[1]
+    c = []
+    if N % 32 == 0 and K % 64 == 0:
+        c.append(('hip', lambda: _KF.conv_fwd(dy2.view(M, 1, 1, N), w.t().contiguous().view(K, 1, 1, N), (1, 1),
+                                              (0, 0)).view(M, K)))
+    c.append(('mm', lambda: torch.mm(dy2, w)))
+    return c
+
+
+def _fc_wgrad_cands(dy2, x2, w):
+    M, N = dy2.shape
+    K = x2.shape[1]
+    c = []
+    if K % 64 == 0 and N % 64 == 0 and x2.data_ptr() % 16 == 0:
+        c.append(('hip', lambda: _KF.conv_wgrad(x2.view(M, 1, 1, K), dy2.view(M, 1, 1, N), (N, 1, 1, K), (1, 1),
+                                                (0, 0)).view(N, K)))
+    c.append(('mm', lambda: torch.mm(dy2.t(), x2)))
+    return c
+
+
+class Linear(torch.autograd.Function):
+    """FullyConnected (flatten=False semantics on the last axis) with per-shape kernel selection."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K).contiguous()
+        key = ('fc_fwd', tuple(x2.shape), tuple(w.shape), x.dtype, b is not None)
+        y = _KF._select(key, _fc_fwd_cands(x2, w.contiguous(), b), 'mm')
+        ctx.save_for_backward(x2, w)
+        ctx.has_b = b is not None
+        ctx.bdt = b.dtype if b is not None else None
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        N = w.shape[0]
+        dy2 = dy.reshape(-1, N).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            key = ('fc_dgrad', tuple(dy2.shape), tuple(w.shape), dy.dtype)
+            dx = _KF._select(key, _fc_dgrad_cands(dy2, w.contiguous()), 'mm').view(ctx.xshape)
+        if ctx.needs_input_grad[1]:
+            key = ('fc_wgrad', tuple(dy2.shape), tuple(x2.shape), dy.dtype)
+            dw = _KF._select(key, _fc_wgrad_cands(dy2, x2, w), 'mm').to(w.dtype)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = dy2.float().sum(0).to(ctx.bdt)
+        return dx, dw, db
+
+
+_K.gemm_ok = gemm_ok
+_K.Linear = Linear
+__all__ += ['Linear', 'gemm_ok']

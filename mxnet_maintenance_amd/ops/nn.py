@@ -382,6 +382,10 @@ _SM_PARAMS = {'axis': ('int', -1), 'temperature': ('float?', None), 'dtype': ('s
 
 @register('softmax', arg_names=_softmax_args, params=_SM_PARAMS)
 def softmax(data, length=None, axis=-1, temperature=None, dtype=None, use_length=False):
+    if not (length is not None and use_length) and (dtype is None or torch_dtype(dtype) == data.dtype):
+        r = hip_ops.softmax(data, axis, 1.0 / temperature if temperature else 1.0)
+        if r is not None:
+            return r
     x = data if temperature is None or temperature == 1.0 else data / temperature
     if length is not None and use_length:
         m = _length_mask(x, length, axis % x.dim())
@@ -395,6 +399,10 @@ def softmax(data, length=None, axis=-1, temperature=None, dtype=None, use_length
 
 @register('log_softmax', arg_names=_softmax_args, params=_SM_PARAMS)
 def log_softmax(data, length=None, axis=-1, temperature=None, dtype=None, use_length=False):
+    if dtype is None or torch_dtype(dtype) == data.dtype:
+        r = hip_ops.softmax(data, axis, 1.0 / temperature if temperature else 1.0, log=True)
+        if r is not None:
+            return r
     x = data if temperature is None or temperature == 1.0 else data / temperature
     r = torch.log_softmax(x.float() if x.dtype in (torch.float16, torch.bfloat16) else x, dim=axis)
     return r.to(torch_dtype(dtype) if dtype else data.dtype)
@@ -585,6 +593,10 @@ def dropout(data, p=0.5, mode='training', axes=(), cudnn_off=False):
     active = (mode == 'always') or _state.STATE.training
     if not active or p == 0:
         return data, torch.ones_like(data)
+    if not axes:
+        r = hip_ops.dropout(data, p)
+        if r is not None:
+            return r
     if axes:
         mshape = [1 if i in axes else s for i, s in enumerate(data.shape)]
         mask = (torch.rand(mshape, device=data.device) >= p).to(data.dtype) / (1 - p)

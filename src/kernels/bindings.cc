@@ -38,6 +38,27 @@ void conv_nhwc_fwd(int dtype, const void* x, const void* w, const float* bias, v
 int64_t conv_nhwc_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw);
 void conv_nhwc_wgrad(int dtype, const void* x, const void* dy, float* slab, int out_dtype, void* out, int accum, int N,
                      int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, hipStream_t s);
+int layernorm_bwd_partials(int M);
+void layernorm_forward(int dtype, const void* x, const float* gamma, const float* beta, void* y, float* mean,
+                       float* rstd, int M, int D, float eps, hipStream_t s);
+void layernorm_backward(int dtype, const void* x, const void* dy, const float* gamma, const float* mean,
+                        const float* rstd, void* dx, float* part, float* dgamma, float* dbeta, int accum, int M, int D,
+                        hipStream_t s);
+void gelu_forward(int dtype, const void* x, void* y, int64_t n, hipStream_t s);
+void gelu_backward(int dtype, const void* x, const void* dy, void* dx, int64_t n, hipStream_t s);
+void softmax_forward(int dtype, int log, const void* x, void* y, int M, int L, float scale, hipStream_t s);
+void softmax_backward(int dtype, int log, const void* y, const void* dy, void* dx, int M, int L, float scale,
+                      hipStream_t s);
+void dropout_forward(int dtype, const void* x, void* y, uint8_t* mask, int64_t n, float p, uint64_t seed,
+                     hipStream_t s);
+void dropout_backward(int dtype, const void* dy, const uint8_t* mask, void* dx, int64_t n, float p, hipStream_t s);
+void flat_adam(int dtype, int mode, void* w, const void* g, float* mean, float* var, float* w32, int64_t n, float lr,
+               float beta1, float beta2, float eps, float wd, float eta, float rescale, float clip, hipStream_t s);
+void lamb_update(int dtype, void* w, const void* g, float* mean, float* var, float* w32, float* upd,
+                 const void* chunks, int nchunks, float* nrm, int nseg, float lr, float beta1, float beta2, float eps,
+                 float bc1, float bc2, float wd, float rescale, float clip, float lb, float ub, hipStream_t s);
+void seg_sumsq(int dtype, const void* x, const void* chunks, int nchunks, float* out, int nseg, hipStream_t s);
+void all_finite(int dtype, const void* x, int64_t n, float scale, int* flag, int init, hipStream_t s);
 void pool_nhwc_forward(int dtype, int is_max, const void* x, void* y, uint8_t* arg, int N, int H, int W, int C,
                        int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip, hipStream_t s);
 void pool_nhwc_backward(int dtype, int is_max, const void* dy, const uint8_t* arg, void* dx, int N, int H, int W,
@@ -122,6 +143,71 @@ PYBIND11_MODULE(_hip_kernels, m) {
     conv_nhwc_wgrad(dt, P<void>(x), P<void>(dy), P<float>(slab), odt, P<void>(out), accum, N, H, W, C, K, R, Sf, sh,
                     sw, ph, pw, S(s));
     check_launch("conv_nhwc_wgrad");
+  });
+  m.def("layernorm_bwd_partials", &layernorm_bwd_partials);
+  m.def("layernorm_forward", [](int dt, uintptr_t x, uintptr_t g, uintptr_t b, uintptr_t y, uintptr_t mean,
+                                uintptr_t rstd, int M, int D, float eps, uintptr_t s) {
+    layernorm_forward(dt, P<void>(x), P<float>(g), P<float>(b), P<void>(y), P<float>(mean), P<float>(rstd), M, D, eps,
+                      S(s));
+    check_launch("layernorm_forward");
+  });
+  m.def("layernorm_backward", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t g, uintptr_t mean, uintptr_t rstd,
+                                 uintptr_t dx, uintptr_t part, uintptr_t dg, uintptr_t db, int accum, int M, int D,
+                                 uintptr_t s) {
+    layernorm_backward(dt, P<void>(x), P<void>(dy), P<float>(g), P<float>(mean), P<float>(rstd), P<void>(dx),
+                       P<float>(part), P<float>(dg), P<float>(db), accum, M, D, S(s));
+    check_launch("layernorm_backward");
+  });
+  m.def("gelu_forward", [](int dt, uintptr_t x, uintptr_t y, int64_t n, uintptr_t s) {
+    gelu_forward(dt, P<void>(x), P<void>(y), n, S(s));
+    check_launch("gelu_forward");
+  });
+  m.def("gelu_backward", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t dx, int64_t n, uintptr_t s) {
+    gelu_backward(dt, P<void>(x), P<void>(dy), P<void>(dx), n, S(s));
+    check_launch("gelu_backward");
+  });
+  m.def("softmax_forward", [](int dt, int log, uintptr_t x, uintptr_t y, int M, int L, float scale, uintptr_t s) {
+    softmax_forward(dt, log, P<void>(x), P<void>(y), M, L, scale, S(s));
+    check_launch("softmax_forward");
+  });
+  m.def("softmax_backward", [](int dt, int log, uintptr_t y, uintptr_t dy, uintptr_t dx, int M, int L, float scale,
+                               uintptr_t s) {
+    softmax_backward(dt, log, P<void>(y), P<void>(dy), P<void>(dx), M, L, scale, S(s));
+    check_launch("softmax_backward");
+  });
+  m.def("dropout_forward", [](int dt, uintptr_t x, uintptr_t y, uintptr_t mask, int64_t n, float p, uint64_t seed,
+                              uintptr_t s) {
+    dropout_forward(dt, P<void>(x), P<void>(y), P<uint8_t>(mask), n, p, seed, S(s));
+    check_launch("dropout_forward");
+  });
+  m.def("dropout_backward", [](int dt, uintptr_t dy, uintptr_t mask, uintptr_t dx, int64_t n, float p, uintptr_t s) {
+    dropout_backward(dt, P<void>(dy), P<uint8_t>(mask), P<void>(dx), n, p, S(s));
+    check_launch("dropout_backward");
+  });
+  // mode 0: Adam (wd folded into the gradient), 1: AdamW (decoupled, eta-scaled)
+  m.def("flat_adam", [](int dt, int mode, uintptr_t w, uintptr_t g, uintptr_t mean, uintptr_t var, uintptr_t w32,
+                        int64_t n, float lr, float b1, float b2, float eps, float wd, float eta, float rescale,
+                        float clip, uintptr_t s) {
+    flat_adam(dt, mode, P<void>(w), P<void>(g), P<float>(mean), P<float>(var), P<float>(w32), n, lr, b1, b2, eps, wd,
+              eta, rescale, clip, S(s));
+    check_launch("flat_adam");
+  });
+  m.def("lamb_update", [](int dt, uintptr_t w, uintptr_t g, uintptr_t mean, uintptr_t var, uintptr_t w32,
+                          uintptr_t upd, uintptr_t chunks, int nchunks, uintptr_t nrm, int nseg, float lr, float b1,
+                          float b2, float eps, float bc1, float bc2, float wd, float rescale, float clip, float lb,
+                          float ub, uintptr_t s) {
+    lamb_update(dt, P<void>(w), P<void>(g), P<float>(mean), P<float>(var), P<float>(w32), P<float>(upd),
+                P<void>(chunks), nchunks, P<float>(nrm), nseg, lr, b1, b2, eps, bc1, bc2, wd, rescale, clip, lb, ub,
+                S(s));
+    check_launch("lamb_update");
+  });
+  m.def("seg_sumsq", [](int dt, uintptr_t x, uintptr_t chunks, int nchunks, uintptr_t out, int nseg, uintptr_t s) {
+    seg_sumsq(dt, P<void>(x), P<void>(chunks), nchunks, P<float>(out), nseg, S(s));
+    check_launch("seg_sumsq");
+  });
+  m.def("all_finite", [](int dt, uintptr_t x, int64_t n, float scale, uintptr_t flag, int init, uintptr_t s) {
+    all_finite(dt, P<void>(x), n, scale, P<int>(flag), init, S(s));
+    check_launch("all_finite");
   });
   m.def("pool_nhwc_forward", [](int dt, int is_max, uintptr_t x, uintptr_t y, uintptr_t arg, int N, int H, int W,
                                 int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip,

@@ -1,0 +1,492 @@
+// Transformer-path kernels for gfx950: LayerNorm, GELU, softmax, dropout.
+//
+// Parity: src/operator/nn/layer_norm.cu (LayerNorm fwd/bwd with mean/std
+// outputs), src/operator/leaky_relu-inl.h (act_type='gelu', erf form),
+// src/operator/nn/softmax-inl.h (softmax / log_softmax along the last axis,
+// with temperature) and src/operator/nn/dropout-inl.h (Bernoulli mask,
+// scaled by 1/(1-p)).  Design for MI355X:
+//
+// * rows (hidden <= 8192 or seq <= 8192) are held in registers by ONE wave64
+//   (VPL 16-byte vectors per lane); mean/var/max/sum are wave reductions
+//   (DPP/permute shuffles), so every row is read from HBM exactly once per pass;
+// * a 256-thread block runs 4 rows; grids are sized to fill 256 CUs;
+// * LayerNorm dgamma/dbeta: per-block column partials (fp32, LDS combine of the
+//   4 waves) + one column-reduce kernel that writes or accumulates the fp32
+//   parameter gradient -- no atomics, deterministic;
+// * dropout draws Philox-4x32-10 counters keyed by (seed, element index), so the
+//   mask is reproducible from the seed and is stored as 1 bit per element.
+#include <stdexcept>
+
+#include "common.h"
+
+namespace mxamd {
+
+namespace {
+
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, float (&v)[8]) {
+  Vec8<T> t;
+  t.load(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = t.get(i);
+}
+
+template <typename T>
+__device__ __forceinline__ void st8(T* p, const float (&v)[8]) {
+  Vec8<T> t;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t.set(i, v[i]);
+  t.store(p);
+}
+
+__device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// ------------------------------------------------------------------ LayerNorm
+// x, y: [M, D] (D % 8 == 0, D <= 512*VPL); gamma/beta fp32 [D]; mean/rstd fp32 [M]
+template <typename T, int VPL>
+__global__ void __launch_bounds__(256) layernorm_fwd_kernel(const T* __restrict__ x, const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, T* __restrict__ y,
+                                                            float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                            int M, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nv = D >> 3;
+  const T* xr = x + (int64_t)row * D;
+  float v[VPL][8];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + j * 64;
+    if (c < nv) {
+      ld8(xr + c * 8, v[j]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[j][i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[j][i] = 0.f;
+    }
+  }
+  const float mean = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    if (lane + j * 64 < nv) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = v[j][i] - mean;
+        q += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / D + eps);
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+  T* yr = y + (int64_t)row * D;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + j * 64;
+    if (c < nv) {
+      float g[8], b[8], o[8];
+      ld8f(gamma + c * 8, g);
+      ld8f(beta + c * 8, b);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (v[j][i] - mean) * rstd * g[i] + b[i];
+      st8(yr + c * 8, o);
+    }
+  }
+}
+
+// dx = rstd * (dy*g - mean(dy*g) - xhat * mean(dy*g*xhat)); per-block partial dgamma/dbeta
+template <typename T, int VPL>
+__global__ void __launch_bounds__(256) layernorm_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ mean_in,
+                                                            const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                            float* __restrict__ part, int M, int D) {
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int nv = D >> 3;
+  float pg[VPL][8], pb[VPL][8];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pg[j][i] = pb[j][i] = 0.f;
+  for (int row = blockIdx.x * 4 + w; row < M; row += gridDim.x * 4) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    const T* xr = x + (int64_t)row * D;
+    const T* dyr = dy + (int64_t)row * D;
+    float xh[VPL][8], gd[VPL][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + j * 64;
+      if (c < nv) {
+        float xv[8], dv[8], g[8];
+        ld8(xr + c * 8, xv);
+        ld8(dyr + c * 8, dv);
+        ld8f(gamma + c * 8, g);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          xh[j][i] = (xv[i] - mean) * rstd;
+          gd[j][i] = dv[i] * g[i];
+          s1 += gd[j][i];
+          s2 += gd[j][i] * xh[j][i];
+          pg[j][i] += dv[i] * xh[j][i];
+          pb[j][i] += dv[i];
+        }
+      }
+    }
+    const float m1 = wave_sum(s1) / D, m2 = wave_sum(s2) / D;
+    T* dxr = dx + (int64_t)row * D;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + j * 64;
+      if (c < nv) {
+        float o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = rstd * (gd[j][i] - m1 - xh[j][i] * m2);
+        st8(dxr + c * 8, o);
+      }
+    }
+  }
+  // combine the 4 waves' column partials through LDS, one row of partials per block
+  __shared__ float sh[2][4][512];  // [g|b][wave][column chunk of 512]
+  float* pgo = part + (int64_t)blockIdx.x * 2 * D;
+  for (int base = 0; base < D; base += 512) {
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + j * 64;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int col = c * 8 + i - base;
+        if (c < nv && col >= 0 && col < 512) {
+          sh[0][w][col] = pg[j][i];
+          sh[1][w][col] = pb[j][i];
+        }
+      }
+    }
+    __syncthreads();
+    for (int col = threadIdx.x; col < 512 && base + col < D; col += 256) {
+      pgo[base + col] = sh[0][0][col] + sh[0][1][col] + sh[0][2][col] + sh[0][3][col];
+      pgo[D + base + col] = sh[1][0][col] + sh[1][1][col] + sh[1][2][col] + sh[1][3][col];
+    }
+    __syncthreads();
+  }
+}
+
+// out[c] (+)= sum_b part[b][c] for the 2*D columns (dgamma then dbeta)
+__global__ void __launch_bounds__(256) column_sum_kernel(const float* __restrict__ part, int nb, int ncol,
+                                                         float* __restrict__ out0, float* __restrict__ out1, int D,
+                                                         int accum) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= ncol) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += part[(int64_t)b * ncol + col];
+  float* o = col < D ? out0 + col : out1 + (col - D);
+  if (accum) *o += s;
+  else *o = s;
+}
+
+// ------------------------------------------------------------------ GELU (erf form)
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+
+template <typename T, bool BWD>
+__global__ void __launch_bounds__(256) gelu_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                   T* __restrict__ out, int64_t nvec) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    float xv[8], o[8];
+    ld8(x + v * 8, xv);
+    if (BWD) {
+      float d[8];
+      ld8(dy + v * 8, d);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = d[i] * gelu_grad_f(xv[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = gelu_f(xv[i]);
+    }
+    st8(out + v * 8, o);
+  }
+}
+
+// ------------------------------------------------------------------ softmax (last axis)
+// y = softmax(x * scale) (LOG: log_softmax); one wave per row, row in registers
+template <typename T, int VPL, bool LOG>
+__global__ void __launch_bounds__(256) softmax_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int M, int L,
+                                                          float scale) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nv = L >> 3;
+  const T* xr = x + (int64_t)row * L;
+  float v[VPL][8];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + j * 64;
+    if (c < nv) {
+      ld8(xr + c * 8, v[j]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        v[j][i] *= scale;
+        mx = fmaxf(mx, v[j][i]);
+      }
+    }
+  }
+  mx = wave_max(mx);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    if (lane + j * 64 < nv) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        v[j][i] -= mx;
+        s += __expf(v[j][i]);
+      }
+    }
+  }
+  s = wave_sum(s);
+  const float ls = __logf(s), inv = 1.f / s;
+  T* yr = y + (int64_t)row * L;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + j * 64;
+    if (c < nv) {
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = LOG ? v[j][i] - ls : __expf(v[j][i]) * inv;
+      st8(yr + c * 8, o);
+    }
+  }
+}
+
+// softmax:     dx = scale * y * (dy - sum(dy*y))
+// log_softmax: dx = scale * (dy - exp(y) * sum(dy))
+template <typename T, int VPL, bool LOG>
+__global__ void __launch_bounds__(256) softmax_bwd_kernel(const T* __restrict__ y, const T* __restrict__ dy,
+                                                          T* __restrict__ dx, int M, int L, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nv = L >> 3;
+  const T* yr = y + (int64_t)row * L;
+  const T* dr = dy + (int64_t)row * L;
+  float yv[VPL][8], dv[VPL][8];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + j * 64;
+    if (c < nv) {
+      ld8(yr + c * 8, yv[j]);
+      ld8(dr + c * 8, dv[j]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += LOG ? dv[j][i] : dv[j][i] * yv[j][i];
+    }
+  }
+  s = wave_sum(s);
+  T* xr = dx + (int64_t)row * L;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + j * 64;
+    if (c < nv) {
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        o[i] = scale * (LOG ? dv[j][i] - __expf(yv[j][i]) * s : yv[j][i] * (dv[j][i] - s));
+      st8(xr + c * 8, o);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ dropout
+struct Philox {
+  // Philox-4x32-10 (Salmon et al., SC'11)
+  static __device__ __forceinline__ uint4 run(uint4 ctr, uint2 key) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      const uint32_t lo0 = ctr.x * 0xD2511F53u, hi0 = __umulhi(ctr.x, 0xD2511F53u);
+      const uint32_t lo1 = ctr.z * 0xCD9E8D57u, hi1 = __umulhi(ctr.z, 0xCD9E8D57u);
+      ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
+      key.x += 0x9E3779B9u;
+      key.y += 0xBB67AE85u;
+    }
+    return ctr;
+  }
+};
+
+// keep element with probability (1-p): y = x * keep / (1-p); mask byte per 8 elements
+template <typename T>
+__global__ void __launch_bounds__(256) dropout_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                          uint8_t* __restrict__ mask, int64_t nvec, float p,
+                                                          uint64_t seed) {
+  const uint32_t thresh = (uint32_t)fminf(p * 4294967296.f, 4294967295.f);
+  const float sc = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const uint4 r0 = Philox::run(make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u), key);
+    const uint4 r1 = Philox::run(make_uint4((uint32_t)v, (uint32_t)(v >> 32), 1u, 0u), key);
+    const uint32_t u[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    float xv[8], o[8];
+    ld8(x + v * 8, xv);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const bool keep = u[i] >= thresh;
+      bits |= (keep ? 1u : 0u) << i;
+      o[i] = keep ? xv[i] * sc : 0.f;
+    }
+    st8(y + v * 8, o);
+    mask[v] = (uint8_t)bits;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) dropout_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                          T* __restrict__ dx, int64_t nvec, float p) {
+  const float sc = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    float d[8], o[8];
+    ld8(dy + v * 8, d);
+    const uint32_t bits = mask[v];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = ((bits >> i) & 1u) ? d[i] * sc : 0.f;
+    st8(dx + v * 8, o);
+  }
+}
+
+inline int ew_blocks(int64_t nvec) {
+  int64_t b = (nvec + 255) / 256;
+  return (int)(b > 256 * 16 ? 256 * 16 : (b < 1 ? 1 : b));
+}
+
+// rows of up to 512*VPL elements; VPL chosen from {1,2,4,8,16}
+inline int pick_vpl(int D) {
+  const int nv = D / 8;
+  if (nv <= 64) return 1;
+  if (nv <= 128) return 2;
+  if (nv <= 256) return 4;
+  if (nv <= 512) return 8;
+  if (nv <= 1024) return 16;
+  return 0;
+}
+
+#define MXAMD_VPL_SWITCH(vpl, ...)                                   \
+  switch (vpl) {                                                     \
+    case 1: { constexpr int VPL = 1; __VA_ARGS__; } break;           \
+    case 2: { constexpr int VPL = 2; __VA_ARGS__; } break;           \
+    case 4: { constexpr int VPL = 4; __VA_ARGS__; } break;           \
+    case 8: { constexpr int VPL = 8; __VA_ARGS__; } break;           \
+    case 16: { constexpr int VPL = 16; __VA_ARGS__; } break;         \
+    default: throw std::runtime_error("row length must be a multiple of 8 and <= 8192"); \
+  }
+
+#define MXAMD_DTYPE_SWITCH(dtype, ...)                                \
+  if (dtype == kF16) { typedef __half T; __VA_ARGS__; }               \
+  else if (dtype == kBF16) { typedef __hip_bfloat16 T; __VA_ARGS__; } \
+  else { typedef float T; __VA_ARGS__; }
+
+}  // namespace
+
+int layernorm_bwd_partials(int M) {
+  int nb = (M + 3) / 4;
+  return nb > 1024 ? 1024 : nb;
+}
+
+void layernorm_forward(int dtype, const void* x, const float* gamma, const float* beta, void* y, float* mean,
+                       float* rstd, int M, int D, float eps, hipStream_t s) {
+  MXAMD_HOST_CHECK(D % 8 == 0, "layernorm: D must be a multiple of 8");
+  const int vpl = pick_vpl(D);
+  dim3 grid((M + 3) / 4);
+  MXAMD_DTYPE_SWITCH(dtype, MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((layernorm_fwd_kernel<T, VPL>), grid, dim3(256),
+                                                                     0, s, static_cast<const T*>(x), gamma, beta,
+                                                                     static_cast<T*>(y), mean, rstd, M, D, eps)))
+}
+
+// part: fp32 workspace of layernorm_bwd_partials(M) * 2 * D; dgamma/dbeta fp32 [D] (written or accumulated)
+void layernorm_backward(int dtype, const void* x, const void* dy, const float* gamma, const float* mean,
+                        const float* rstd, void* dx, float* part, float* dgamma, float* dbeta, int accum, int M, int D,
+                        hipStream_t s) {
+  MXAMD_HOST_CHECK(D % 8 == 0, "layernorm: D must be a multiple of 8");
+  const int vpl = pick_vpl(D);
+  const int nb = layernorm_bwd_partials(M);
+  MXAMD_DTYPE_SWITCH(dtype, MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((layernorm_bwd_kernel<T, VPL>), dim3(nb),
+                                                                     dim3(256), 0, s, static_cast<const T*>(x),
+                                                                     static_cast<const T*>(dy), gamma, mean, rstd,
+                                                                     static_cast<T*>(dx), part, M, D)))
+  hipLaunchKernelGGL(column_sum_kernel, dim3((2 * D + 255) / 256), dim3(256), 0, s, part, nb, 2 * D, dgamma, dbeta, D,
+                     accum);
+}
+
+void gelu_forward(int dtype, const void* x, void* y, int64_t n, hipStream_t s) {
+  MXAMD_HOST_CHECK(n % 8 == 0, "gelu: numel must be a multiple of 8");
+  MXAMD_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((gelu_kernel<T, false>), dim3(ew_blocks(n / 8)), dim3(256), 0, s,
+                                               static_cast<const T*>(x), nullptr, static_cast<T*>(y), n / 8))
+}
+
+void gelu_backward(int dtype, const void* x, const void* dy, void* dx, int64_t n, hipStream_t s) {
+  MXAMD_HOST_CHECK(n % 8 == 0, "gelu: numel must be a multiple of 8");
+  MXAMD_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((gelu_kernel<T, true>), dim3(ew_blocks(n / 8)), dim3(256), 0, s,
+                                               static_cast<const T*>(x), static_cast<const T*>(dy),
+                                               static_cast<T*>(dx), n / 8))
+}
+
+void softmax_forward(int dtype, int log, const void* x, void* y, int M, int L, float scale, hipStream_t s) {
+  MXAMD_HOST_CHECK(L % 8 == 0, "softmax: row length must be a multiple of 8");
+  const int vpl = pick_vpl(L);
+  dim3 grid((M + 3) / 4);
+  if (log) {
+    MXAMD_DTYPE_SWITCH(dtype, MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((softmax_fwd_kernel<T, VPL, true>), grid,
+                                                                       dim3(256), 0, s, static_cast<const T*>(x),
+                                                                       static_cast<T*>(y), M, L, scale)))
+  } else {
+    MXAMD_DTYPE_SWITCH(dtype, MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((softmax_fwd_kernel<T, VPL, false>), grid,
+                                                                       dim3(256), 0, s, static_cast<const T*>(x),
+                                                                       static_cast<T*>(y), M, L, scale)))
+  }
+}
+
+void softmax_backward(int dtype, int log, const void* y, const void* dy, void* dx, int M, int L, float scale,
+                      hipStream_t s) {
+  MXAMD_HOST_CHECK(L % 8 == 0, "softmax: row length must be a multiple of 8");
+  const int vpl = pick_vpl(L);
+  dim3 grid((M + 3) / 4);
+  if (log) {
+    MXAMD_DTYPE_SWITCH(dtype, MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((softmax_bwd_kernel<T, VPL, true>), grid,
+                                                                       dim3(256), 0, s, static_cast<const T*>(y),
+                                                                       static_cast<const T*>(dy),
+                                                                       static_cast<T*>(dx), M, L, scale)))
+  } else {
+    MXAMD_DTYPE_SWITCH(dtype, MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((softmax_bwd_kernel<T, VPL, false>), grid,
+                                                                       dim3(256), 0, s, static_cast<const T*>(y),
+                                                                       static_cast<const T*>(dy),
+                                                                       static_cast<T*>(dx), M, L, scale)))
+  }
+}
+
+void dropout_forward(int dtype, const void* x, void* y, uint8_t* mask, int64_t n, float p, uint64_t seed,
+                     hipStream_t s) {
+  MXAMD_HOST_CHECK(n % 8 == 0, "dropout: numel must be a multiple of 8");
+  MXAMD_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((dropout_fwd_kernel<T>), dim3(ew_blocks(n / 8)), dim3(256), 0, s,
+                                               static_cast<const T*>(x), static_cast<T*>(y), mask, n / 8, p, seed))
+}
+
+void dropout_backward(int dtype, const void* dy, const uint8_t* mask, void* dx, int64_t n, float p, hipStream_t s) {
+  MXAMD_HOST_CHECK(n % 8 == 0, "dropout: numel must be a multiple of 8");
+  MXAMD_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((dropout_bwd_kernel<T>), dim3(ew_blocks(n / 8)), dim3(256), 0, s,
+                                               static_cast<const T*>(dy), mask, static_cast<T*>(dx), n / 8, p))
+}
+
+}  // namespace mxamd

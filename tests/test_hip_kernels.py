@@ -397,3 +397,195 @@ def test_bottleneck_fused_tee_matches_fp32_reference(cfg):
         ef = float(((gf - gr) ** 2).sum() ** 0.5) / nr
         eu = float(((gu - gr) ** 2).sum() ** 0.5) / nr
         assert ef < max(2 * eu, 1e-2), (ef, eu)
+
+
+# ---------------------------------------------------------------- transformer-path kernels
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('shape', [(64, 768), (3, 37, 1024), (8, 4096), (5, 24)])
+def test_layernorm_fwd_bwd(dtype, shape):
+    K = _lib()
+    torch.manual_seed(3)
+    D = shape[-1]
+    x = torch.randn(*shape, device='cuda').to(dtype).requires_grad_()
+    g = (torch.rand(D, device='cuda') + 0.5).requires_grad_()
+    b = torch.randn(D, device='cuda').requires_grad_()
+    assert K.ln_ok(x)
+    y, mean, std = K.LayerNorm.apply(x, g, b, 1e-5)
+    dy = torch.randn_like(y)
+    dx, dg, db = torch.autograd.grad(y, (x, g, b), dy)
+    xf = x.detach().float().requires_grad_()
+    gf = g.detach().clone().requires_grad_()
+    bf = b.detach().clone().requires_grad_()
+    yf = F.layer_norm(xf, (D,), gf, bf, 1e-5)
+    dxf, dgf, dbf = torch.autograd.grad(yf, (xf, gf, bf), dy.float())
+    tol = {torch.float16: 2e-2, torch.bfloat16: 8e-2, torch.float32: 1e-4}[dtype]
+    torch.testing.assert_close(y.float(), yf, rtol=tol, atol=tol)
+    torch.testing.assert_close(mean.float().squeeze(-1), xf.mean(-1), rtol=tol, atol=tol)
+    torch.testing.assert_close(dx.float(), dxf, rtol=tol, atol=tol * 4)
+    torch.testing.assert_close(dg, dgf, rtol=tol, atol=tol * max(1.0, x.numel() / D / 8))
+    torch.testing.assert_close(db, dbf, rtol=tol, atol=tol * max(1.0, x.numel() / D / 8))
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16, torch.float32])
+def test_gelu_fwd_bwd(dtype):
+    K = _lib()
+    x = (torch.randn(4096, 24, device='cuda') * 3).to(dtype).requires_grad_()
+    y = K.GELU.apply(x)
+    dy = torch.randn_like(y)
+    dx, = torch.autograd.grad(y, x, dy)
+    xf = x.detach().float().requires_grad_()
+    yf = F.gelu(xf)
+    dxf, = torch.autograd.grad(yf, xf, dy.float())
+    tol = {torch.float16: 1e-2, torch.bfloat16: 5e-2, torch.float32: 1e-5}[dtype]
+    torch.testing.assert_close(y.float(), yf, rtol=tol, atol=tol)
+    torch.testing.assert_close(dx.float(), dxf, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('L', [8, 128, 520, 4096])
+@pytest.mark.parametrize('log', [False, True])
+def test_softmax_fwd_bwd(dtype, L, log):
+    K = _lib()
+    torch.manual_seed(4)
+    x = (torch.randn(3, 7, L, device='cuda') * 2).to(dtype).requires_grad_()
+    scale = 0.5
+    assert K.softmax_ok(x, -1)
+    y = K.Softmax.apply(x, scale, log)
+    dy = torch.randn_like(y)
+    dx, = torch.autograd.grad(y, x, dy)
+    xf = x.detach().float().requires_grad_()
+    yf = (torch.log_softmax if log else torch.softmax)(xf * scale, dim=-1)
+    dxf, = torch.autograd.grad(yf, xf, dy.float())
+    tol = {torch.float16: 1e-2, torch.bfloat16: 4e-2, torch.float32: 1e-5}[dtype]
+    torch.testing.assert_close(y.float(), yf, rtol=tol, atol=tol)
+    torch.testing.assert_close(dx.float(), dxf, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.float32])
+def test_dropout_mask_rate_and_grad(dtype):
+    K = _lib()
+    torch.manual_seed(5)
+    x = torch.randn(1024, 1024, device='cuda').to(dtype).requires_grad_()
+    p = 0.3
+    y, mask = K.Dropout.apply(x, p)
+    keep = y != 0
+    rate = 1 - keep.float().mean().item()
+    assert abs(rate - p) < 0.01
+    torch.testing.assert_close(y[keep].float(), (x[keep] / (1 - p)).float(), rtol=1e-3, atol=1e-3)
+    dy = torch.randn_like(y)
+    dx, = torch.autograd.grad(y, x, dy)
+    torch.testing.assert_close(dx.float(), (dy * keep / (1 - p)).float(), rtol=1e-3, atol=1e-3)
+    # reproducible from the torch CPU generator
+    torch.manual_seed(11)
+    y1, _ = K.Dropout.apply(x.detach(), p)
+    torch.manual_seed(11)
+    y2, _ = K.Dropout.apply(x.detach(), p)
+    assert torch.equal(y1, y2)
+
+
+@pytest.mark.parametrize('adamw', [False, True])
+@pytest.mark.parametrize('mp', [False, True])
+def test_flat_adam_kernel_matches_torch(adamw, mp):
+    K = _lib()
+    torch.manual_seed(6)
+    n = 4096 + 64
+    dt = torch.float16 if mp else torch.float32
+    w32 = torch.randn(n, device='cuda')
+    w = w32.to(dt)
+    g = torch.randn(n, device='cuda').to(dt)
+    m = torch.randn(n, device='cuda') * 0.1
+    v = torch.rand(n, device='cuda') * 0.1
+    ref_w = (w32 if mp else w.float()).clone()
+    ref_m, ref_v = m.clone(), v.clone()
+    lr, b1, b2, eps, wd, rs, clip = 0.01, 0.9, 0.999, 1e-8, 0.01, 0.5, 0.8
+    K.flat_adam(w, g, m, v, w32 if mp else None, lr, b1, b2, eps, wd, rs, clip, adamw=adamw)
+    gg = g.float() * rs
+    if not adamw:
+        gg = gg + wd * ref_w
+    gg = gg.clamp(-clip, clip)
+    ref_m.mul_(b1).add_(gg, alpha=1 - b1)
+    ref_v.mul_(b2).addcmul_(gg, gg, value=1 - b2)
+    step = lr * ref_m / (ref_v.sqrt() + eps)
+    if adamw:
+        step = step + wd * ref_w
+    ref_w -= step
+    torch.testing.assert_close(m, ref_m, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(v, ref_v, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close((w32 if mp else w).float(), ref_w, rtol=1e-5, atol=1e-5)
+
+
+def test_lamb_arena_kernel_matches_per_segment_reference():
+    K = _lib()
+    torch.manual_seed(7)
+    sizes = [1000, 64, 40000, 8]
+    offs, off = [], 0
+    for s in sizes:
+        offs.append(off)
+        off += (s + 63) // 64 * 64
+    n = off
+    w = torch.zeros(n, device='cuda')
+    g = torch.zeros(n, device='cuda')
+    for o, s in zip(offs, sizes):
+        w[o:o + s] = torch.randn(s, device='cuda')
+        g[o:o + s] = torch.randn(s, device='cuda')
+    m = torch.zeros(n, device='cuda')
+    v = torch.zeros(n, device='cuda')
+    upd = torch.empty(n, device='cuda')
+    table = K.ChunkTable(list(zip(offs, sizes)), 'cuda')
+    nrm = torch.zeros(2 * len(sizes), device='cuda')
+    ref_w = w.clone()
+    lr, b1, b2, eps, wd, t = 0.01, 0.9, 0.999, 1e-6, 0.01, 1
+    K.lamb_update(w, g, m, v, None, upd, table, nrm, lr, b1, b2, eps, t, True, wd, 1.0, -1.0)
+    for o, s in zip(offs, sizes):
+        gg = g[o:o + s]
+        mm = (1 - b1) * gg
+        vv = (1 - b2) * gg * gg
+        r = (mm / (1 - b1)) / ((vv / (1 - b2)).sqrt() + eps) + wd * ref_w[o:o + s]
+        r1 = ref_w[o:o + s].norm()
+        r2 = r.norm()
+        ref_w[o:o + s] -= lr * (r1 / r2) * r
+    torch.testing.assert_close(w, ref_w, rtol=1e-4, atol=1e-5)
+    sq = K.seg_sumsq(g, table)
+    torch.testing.assert_close(sq, torch.stack([g[o:o + s].pow(2).sum() for o, s in zip(offs, sizes)]),
+                               rtol=1e-4, atol=1e-3)
+
+
+def test_all_finite_kernel():
+    K = _lib()
+    x = torch.randn(8192, device='cuda').half()
+    assert K.all_finite(x).item() == 1
+    x[777] = float('inf')
+    assert K.all_finite(x).item() == 0
+    y = torch.ones(64, device='cuda')
+    assert K.all_finite(y, scale=float('nan')).item() == 0
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('mkn', [(256, 768, 768), (100, 3072, 768), (64, 768, 2)])
+def test_linear_mfma_matches_fp32(dtype, mkn):
+    K = _lib()
+    from mxnet_maintenance_amd.ops import kernel_fns as KF
+    M, Kd, N = mkn
+    torch.manual_seed(8)
+    x = torch.randn(M, Kd, device='cuda').to(dtype).requires_grad_()
+    w = (torch.randn(N, Kd, device='cuda') / Kd ** 0.5).to(dtype).requires_grad_()
+    b = torch.randn(N, device='cuda').to(dtype).requires_grad_()
+    y = K.Linear.apply(x, w, b)
+    dy = torch.randn_like(y)
+    dx, dw, db = torch.autograd.grad(y, (x, w, b), dy)
+    xf, wf, bf = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yf = F.linear(xf, wf, bf)
+    dxf, dwf, dbf = torch.autograd.grad(yf, (xf, wf, bf), dy.float())
+    tol = 3e-2 if dtype == torch.float16 else 1e-1
+    torch.testing.assert_close(y.float(), yf, rtol=tol, atol=tol)
+    torch.testing.assert_close(dx.float(), dxf, rtol=tol, atol=tol)
+    torch.testing.assert_close(dw.float(), dwf, rtol=tol, atol=tol * 4)
+    torch.testing.assert_close(db.float(), dbf, rtol=tol, atol=tol * 4)
+    # the HIP candidates themselves (whatever the autotuner picked)
+    from mxnet_maintenance_amd.ops import nlp_fns
+    for _name, fn in nlp_fns._fc_fwd_cands(x.detach(), w.detach(), b.detach()):
+        torch.testing.assert_close(fn().float(), yf.detach(), rtol=tol, atol=tol)
+    for _name, fn in nlp_fns._fc_dgrad_cands(dy, w.detach()):
+        torch.testing.assert_close(fn().float(), dxf, rtol=tol, atol=tol)
+    for _name, fn in nlp_fns._fc_wgrad_cands(dy, x.detach(), w.detach()):
+        torch.testing.assert_close(fn().float(), dwf, rtol=tol, atol=tol * 4)

@@ -163,3 +163,70 @@ def test_metrics():
     pcc = mx.metric.PCC()
     pcc.update([nd.array([0, 1, 1, 0])], [nd.array([[0.9, 0.1], [0.2, 0.8], [0.3, 0.7], [0.6, 0.4]])])
     assert pcc.get()[1] == pytest.approx(1.0)
+
+
+def _train_arena(opt_name, opt_params, arena, steps=3):
+    import os
+    import numpy as np
+    import mxnet_maintenance_amd as mx
+    from mxnet_maintenance_amd import gluon, autograd, nd
+    old = os.environ.get('MXAMD_FLAT_ARENA')
+    os.environ['MXAMD_FLAT_ARENA'] = '1' if arena else '0'
+    try:
+        mx.random.seed(7)
+        net = gluon.nn.HybridSequential()
+        net.add(gluon.nn.Dense(16, activation='relu', in_units=8), gluon.nn.Dense(4, in_units=16))
+        net.initialize(mx.init.Xavier())
+        tr = gluon.Trainer(net.collect_params(), opt_name, dict(opt_params))
+        rng = np.random.RandomState(0)
+        for _ in range(steps):
+            x = nd.array(rng.randn(5, 8).astype('float32'))
+            y = nd.array(rng.randint(0, 4, size=(5,)).astype('float32'))
+            with autograd.record():
+                loss = gluon.loss.SoftmaxCrossEntropyLoss()(net(x), y)
+            loss.backward()
+            tr.step(5)
+        assert (tr._arenas is not None) == arena
+        return [p.data().asnumpy() for p in net.collect_params().values()], tr
+    finally:
+        if old is None:
+            os.environ.pop('MXAMD_FLAT_ARENA', None)
+        else:
+            os.environ['MXAMD_FLAT_ARENA'] = old
+
+
+import pytest as _pytest  # noqa: E402
+
+
+@_pytest.mark.parametrize('opt_name,opt_params', [
+    ('adam', {'learning_rate': 0.01, 'wd': 0.01, 'clip_gradient': 0.5}),
+    ('adamw', {'learning_rate': 0.01, 'wd': 0.01}),
+    ('lamb', {'learning_rate': 0.01, 'wd': 0.01, 'lower_bound': 0.01, 'upper_bound': 10.0}),
+    ('sgd', {'learning_rate': 0.1, 'momentum': 0.9, 'wd': 1e-3}),
+])
+def test_flat_arena_optimizers_match_per_parameter(opt_name, opt_params):
+    """The Trainer's flat-arena fused update (HIP kernel on GPU, same math in torch here) equals the
+    reference per-parameter optimizer path (python/mxnet/optimizer/optimizer.py semantics)."""
+    import numpy as np
+    a, tr = _train_arena(opt_name, opt_params, arena=True)
+    b, _ = _train_arena(opt_name, opt_params, arena=False)
+    for x, y in zip(a, b):
+        np.testing.assert_allclose(x, y, rtol=1e-5, atol=1e-6)
+
+
+def test_flat_arena_adam_save_load_states(tmp_path):
+    import numpy as np
+    _, tr = _train_arena('adam', {'learning_rate': 0.01}, arena=True)
+    f = str(tmp_path / 'adam.states')
+    tr.save_states(f)
+    st = tr._updaters[0].states
+    means = {k: v[0].asnumpy().copy() for k, v in st.items()}
+    for a in tr._arenas:
+        a.mean.zero_()
+    tr.load_states(f)
+    st = tr._updaters[0].states
+    for k, v in st.items():
+        np.testing.assert_allclose(v[0].asnumpy(), means[k])
+    a = tr._arenas[0]
+    off, n, shape = a.views[0]
+    np.testing.assert_allclose(a.mean[off:off + n].numpy(), means[a.indices[0]].reshape(-1))
