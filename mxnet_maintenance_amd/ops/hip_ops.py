@@ -209,10 +209,10 @@ def gelu(x):
     return F.gelu(x)
 
 
-def layer_norm(data, gamma, beta, eps):
-    """LayerNorm over the last axis; returns (out, mean, std)."""
+def layer_norm(data, gamma, beta, eps, want_stats=True):
+    """LayerNorm over the last axis; returns (out, mean, std) (mean/std only meaningful with want_stats)."""
     if _use_hip(data) and _K.ln_ok(data):
-        return _K.LayerNorm.apply(data, gamma, beta, eps)
+        return _K.LayerNorm.apply(data, gamma, beta, eps, bool(want_stats))
     x = data.float()
     mean = x.mean(-1, keepdim=True)
     var = x.var(-1, keepdim=True, unbiased=False)

@@ -40,7 +40,7 @@ class LayerNorm(torch.autograd.Function):
     """y = (x - mean) / sqrt(var + eps) * gamma + beta over the last axis; returns (y, mean, std)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, eps):
+    def forward(ctx, x, gamma, beta, eps, want_stats=True):
         lib = _K.lib()
         D = x.shape[-1]
         M = x.numel() // D
@@ -54,8 +54,12 @@ class LayerNorm(torch.autograd.Function):
         ctx.save_for_backward(x, g, mean, rstd)
         ctx.refs = (gamma, beta)
         shp = tuple(x.shape[:-1]) + (1,)
-        m_out = mean.view(shp).to(x.dtype)
-        s_out = torch.reciprocal(rstd).view(shp).to(x.dtype)     # std = sqrt(var + eps)
+        if want_stats:
+            m_out = mean.view(shp).to(x.dtype)
+            s_out = torch.reciprocal(rstd).view(shp).to(x.dtype)     # std = sqrt(var + eps)
+        else:
+            # hidden outputs (output_mean_var=False): fp32 views, no conversion kernels
+            m_out, s_out = mean.view(shp), rstd.view(shp)
         ctx.mark_non_differentiable(m_out, s_out)
         ctx.set_materialize_grads(False)
         return y, m_out, s_out
@@ -63,7 +67,7 @@ class LayerNorm(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy, _gm, _gs):
         if gy is None:
-            return None, None, None, None
+            return None, None, None, None, None
         lib = _K.lib()
         x, g, mean, rstd = ctx.saved_tensors
         gamma, beta = ctx.refs
@@ -85,9 +89,9 @@ class LayerNorm(torch.autograd.Function):
                                rstd.data_ptr(), dx.data_ptr(), part.data_ptr(), dg.data_ptr(), db.data_ptr(), accum,
                                M, D, _stream())
         if accum:
-            return dx, None, None, None
+            return dx, None, None, None, None
         return (dx, dg.view(gamma.shape).to(gamma.dtype) if need_g else None,
-                db.view(beta.shape).to(beta.dtype) if need_b else None, None)
+                db.view(beta.shape).to(beta.dtype) if need_b else None, None, None)
 
 
 class GELU(torch.autograd.Function):
@@ -309,7 +313,7 @@ class Linear(torch.autograd.Function):
             key = ('fc_wgrad', tuple(dy2.shape), tuple(x2.shape), dy.dtype)
             dw = _KF._select(key, _fc_wgrad_cands(dy2, x2, w), 'mm').to(w.dtype)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = dy2.float().sum(0).to(ctx.bdt)
+            db = torch.sum(dy2, 0, dtype=torch.float32).to(ctx.bdt)
         return dx, dw, db
 
 

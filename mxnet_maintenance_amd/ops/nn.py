@@ -631,7 +631,7 @@ def _ln_nvis(a):
 def layer_norm(data, gamma, beta, axis=-1, eps=1e-5, output_mean_var=False):
     axis = axis % data.dim()
     if axis == data.dim() - 1:
-        return hip_ops.layer_norm(data, gamma, beta, eps)
+        return hip_ops.layer_norm(data, gamma, beta, eps, output_mean_var)
     x = data.float()
     mean = x.mean(dim=axis, keepdim=True)
     var = x.var(dim=axis, keepdim=True, unbiased=False)

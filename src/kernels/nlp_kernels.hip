@@ -181,17 +181,33 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const T* __restrict_
   }
 }
 
-// out[c] (+)= sum_b part[b][c] for the 2*D columns (dgamma then dbeta)
+// out[c] (+)= sum_b part[b][c] for the 2*D columns (dgamma then dbeta):
+// 32 columns x 8 row-groups per block, LDS combine of the 8 partial sums
 __global__ void __launch_bounds__(256) column_sum_kernel(const float* __restrict__ part, int nb, int ncol,
                                                          float* __restrict__ out0, float* __restrict__ out1, int D,
                                                          int accum) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= ncol) return;
-  float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += part[(int64_t)b * ncol + col];
-  float* o = col < D ? out0 + col : out1 + (col - D);
-  if (accum) *o += s;
-  else *o = s;
+  const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int col = blockIdx.x * 32 + cl;
+  float s0 = 0.f, s1 = 0.f;
+  if (col < ncol) {
+    int b = grp;
+    for (; b + 8 < nb; b += 16) {
+      s0 += part[(int64_t)b * ncol + col];
+      s1 += part[(int64_t)(b + 8) * ncol + col];
+    }
+    if (b < nb) s0 += part[(int64_t)b * ncol + col];
+  }
+  __shared__ float red[8][32];
+  red[grp][cl] = s0 + s1;
+  __syncthreads();
+  if (grp == 0 && col < ncol) {
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) s += red[g][cl];
+    float* o = col < D ? out0 + col : out1 + (col - D);
+    if (accum) *o += s;
+    else *o = s;
+  }
 }
 
 // ------------------------------------------------------------------ GELU (erf form)
@@ -400,9 +416,10 @@ inline int pick_vpl(int D) {
 
 }  // namespace
 
+// blocks of the backward kernel (each loops over rows): enough to fill the chip, few partial rows
 int layernorm_bwd_partials(int M) {
   int nb = (M + 3) / 4;
-  return nb > 1024 ? 1024 : nb;
+  return nb > 512 ? 512 : nb;
 }
 
 void layernorm_forward(int dtype, const void* x, const float* gamma, const float* beta, void* y, float* mean,
@@ -426,7 +443,7 @@ void layernorm_backward(int dtype, const void* x, const void* dy, const float* g
                                                                      dim3(256), 0, s, static_cast<const T*>(x),
                                                                      static_cast<const T*>(dy), gamma, mean, rstd,
                                                                      static_cast<T*>(dx), part, M, D)))
-  hipLaunchKernelGGL(column_sum_kernel, dim3((2 * D + 255) / 256), dim3(256), 0, s, part, nb, 2 * D, dgamma, dbeta, D,
+  hipLaunchKernelGGL(column_sum_kernel, dim3((2 * D + 31) / 32), dim3(256), 0, s, part, nb, 2 * D, dgamma, dbeta, D,
                      accum);
 }
 

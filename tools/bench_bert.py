@@ -1,0 +1,108 @@
+#!/usr/bin/env python
+"""BERT pre-training throughput (BASELINE.json config 4: BERT-base, seq 128, bf16).
+
+One step = embeddings + 12 encoder layers (fused QKV projection, SDPA attention,
+LayerNorm / GELU / dropout HIP kernels) + MLM (20 masked positions per
+sequence, tied decoder) + NSP heads, softmax-CE losses, backward, bucketed
+gradient all-reduce (N > 1, torch.distributed.run) and a fused flat-arena
+LAMB (default) or AdamW update.  Synthetic token ids / random-init weights.
+
+Usage: python tools/bench_bert.py [--batch 32] [--seq 128] [--steps 20] [--warmup 5]
+       [--model bert_12_768_12] [--optimizer lamb|adamw] [--dtype bfloat16]
+Prints one JSON line (tokens/s and sequences/s for the whole job).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--batch', type=int, default=32, help='per-GPU sequences')
+    ap.add_argument('--seq', type=int, default=128)
+    ap.add_argument('--masked', type=int, default=20)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--model', default='bert_12_768_12')
+    ap.add_argument('--optimizer', default='lamb', choices=['lamb', 'adamw', 'adam'])
+    ap.add_argument('--dtype', default='bfloat16', choices=['bfloat16', 'float16', 'float32'])
+    ap.add_argument('--vocab', type=int, default=30528, help='30522 padded to a multiple of 64')
+    args = ap.parse_args()
+
+    import torch
+    import mxnet_maintenance_amd as mx
+    from mxnet_maintenance_amd import gluon, autograd, nd
+    from mxnet_maintenance_amd.models import bert as bert_mod
+    from mxnet_maintenance_amd.parallel import dist
+
+    if int(os.environ.get('WORLD_SIZE', '1')) > 1:
+        dist.init()
+    rank = dist.rank()
+    ctx = mx.gpu(dist.local_rank()) if torch.cuda.is_available() else mx.cpu()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(dist.local_rank())
+    mx.random.seed(4321 + rank)
+    B, S, P = args.batch, args.seq, args.masked
+    net = bert_mod.get_bert_model(args.model, vocab_size=args.vocab)
+    net.initialize(mx.init.Normal(0.02), ctx=ctx)
+    if args.dtype != 'float32':
+        net.cast(args.dtype)
+    net.hybridize(static_alloc=True, static_shape=True)
+    opt_params = {'learning_rate': 1e-4, 'wd': 0.01, 'multi_precision': args.dtype != 'float32'}
+    trainer = gluon.Trainer(net.collect_params(), args.optimizer, opt_params, kvstore='device')
+    ce = gluon.loss.SoftmaxCrossEntropyLoss()
+
+    g = torch.Generator().manual_seed(rank)
+    tokens = nd.array(torch.randint(0, args.vocab, (B, S), generator=g).numpy(), ctx=ctx)
+    types = nd.array(torch.randint(0, 2, (B, S), generator=g).numpy(), ctx=ctx)
+    valid = nd.array(torch.full((B,), S).numpy(), ctx=ctx)
+    pos = nd.array(torch.stack([torch.randperm(S, generator=g)[:P] for _ in range(B)]).numpy(), ctx=ctx)
+    mlm_label = nd.array(torch.randint(0, args.vocab, (B, P), generator=g).numpy(), ctx=ctx)
+    nsp_label = nd.array(torch.randint(0, 2, (B,), generator=g).numpy(), ctx=ctx)
+
+    def step():
+        with autograd.record():
+            _seq, _pooled, nsp, mlm = net(tokens, types, valid, pos)
+            loss = ce(mlm.reshape((-1, args.vocab)), mlm_label.reshape((-1,))).mean() + ce(nsp, nsp_label).mean()
+        loss.backward()
+        trainer.step(1)
+        return loss
+
+    def sync():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        last = step()
+    sync()
+    dt = time.perf_counter() - t0
+    if dist.world_size() > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device='cuda' if torch.cuda.is_available() else 'cpu')
+        dist.all_reduce(t, op='max')
+        dt = float(t.item())
+    n = dist.world_size()
+    if rank == 0:
+        print(json.dumps({
+            'metric': 'BERT pre-training tokens/sec (whole job)', 'value': round(B * S * n * args.steps / dt, 1),
+            'unit': 'tokens/sec', 'sequences_per_sec': round(B * n * args.steps / dt, 2), 'n_gpus': n,
+            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(dt / args.steps * 1000, 3),
+            'dtype': {'bfloat16': 'bf16', 'float16': 'fp16', 'float32': 'fp32'}[args.dtype],
+            'data': 'synthetic token ids, random-init weights',
+            'config': {'model': args.model, 'per_gpu_batch': B, 'seq_len': S, 'masked_positions': P,
+                       'optimizer': args.optimizer, 'parallelism': 'dp%d' % n,
+                       'final_loss': round(float(last.asscalar()), 4)}}), flush=True)
+    if dist.world_size() > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,6 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 300 python -u tools/bench_bert.py --steps 20 --warmup 5 > gpurun_out/bench_bert.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bert -- python tools/bench_bert.py --steps 6 --warmup 3 > gpurun_out/prof_bert.log 2>&1 && \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_resnet -- python bench.py --steps 6 --warmup 4 > gpurun_out/prof_resnet.log 2>&1

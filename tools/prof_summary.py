@@ -8,13 +8,21 @@ import sys
 
 def classify(name):
     n = name.lower()
+    if 'mxamd::conv' in n or 'wgrad_reduce' in n:
+        return 'conv (in-tree HIP MFMA)'
     if 'igemm' in n or 'conv' in n or 'gemm' in n or 'ck::' in n or 'xdl' in n or 'cijk' in n:
         return 'conv/gemm (MIOpen/hipBLASLt)'
+    if 'attn' in n or 'fmha' in n or 'flash' in n or 'attention' in n:
+        return 'attention (torch SDPA)'
     if 'bn_' in n or 'batch_norm' in n:
         return 'batchnorm'
+    if 'layernorm' in n or 'column_sum' in n:
+        return 'layernorm'
+    if 'gelu' in n or 'dropout' in n:
+        return 'gelu/dropout'
     if 'pool' in n or 'gap_' in n:
         return 'pooling'
-    if 'sgd' in n:
+    if 'sgd' in n or 'adam' in n or 'lamb_' in n or 'sumsq' in n or 'finite' in n:
         return 'optimizer'
     if 'softmax' in n or 'cross' in n:
         return 'softmax/ce'
@@ -28,7 +36,7 @@ def main(d, steps):
     rows = list(csv.DictReader(open(f)))
     if steps <= 0:
         # one fused optimizer launch per training step (warmup included)
-        steps = max(1, sum(int(r['Calls']) for r in rows if 'flat_sgd' in r['Name']))
+        steps = max(1, sum(int(r['Calls']) for r in rows if any(k in r['Name'] for k in ('flat_sgd', 'flat_adam', 'lamb_phase2'))))
     tot = sum(float(r['TotalDurationNs']) for r in rows)
     print('total kernel time %.2f ms (%d steps profiled -> %.2f ms/step)' % (tot / 1e6, steps, tot / 1e6 / steps))
     cls = {}

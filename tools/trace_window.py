@@ -25,7 +25,7 @@ def main():
     f = glob.glob(a.d + '/**/*kernel_trace.csv', recursive=True)[0]
     rows = list(csv.DictReader(open(f)))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
-    sgd = [int(r['End_Timestamp']) for r in rows if 'flat_sgd' in r['Kernel_Name']]
+    sgd = [int(r['End_Timestamp']) for r in rows if any(k in r['Kernel_Name'] for k in ('flat_sgd', 'flat_adam', 'lamb_phase2'))]
     # one step ends at its last optimizer launch; group launches closer than 1 ms
     ends = []
     for t in sgd:
