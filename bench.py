@@ -43,9 +43,11 @@ def main():
         dist.init()
     rank = dist.rank()
     local_rank = dist.local_rank()
-    ctx = mx.gpu(local_rank) if torch.cuda.is_available() else mx.cpu()
+    # one process per GPU; ranks beyond the visible devices share them (single-GPU rehearsals)
+    dev = local_rank % max(1, torch.cuda.device_count()) if torch.cuda.is_available() else 0
+    ctx = mx.gpu(dev) if torch.cuda.is_available() else mx.cpu()
     if torch.cuda.is_available():
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(dev)
     mx.random.seed(1234 + rank)
 
     B = args.batch

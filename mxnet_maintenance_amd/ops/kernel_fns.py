@@ -261,8 +261,11 @@ def conv_ok_shape(x, w, stride, pad, dilate=(1, 1), groups=1):
             and w.data_ptr() % 16 == 0)
 
 
-def conv_fwd(x, w, stride, pad, bias=None):
-    """y[N,Ho,Wo,K] = conv(x[N,H,W,C], w[K,R,S,C]) on the MFMA implicit-GEMM kernel."""
+def conv_fwd(x, w, stride, pad, bias=None, variant=0):
+    """y[N,Ho,Wo,K] = conv(x[N,H,W,C], w[K,R,S,C]) on the MFMA implicit-GEMM kernel.
+
+    ``variant``: 0 = heuristic tile, 1..4 = (BCO, BK) in (128,64) (128,32) (64,64) (64,32),
+    5 / 6 = LDS-DMA pipelined kernel with a 128x128 / 64x256 tile (Cin % 64 == 0)."""
     N, H, W, C = x.shape
     K, R, S, _ = w.shape
     Ho = (H + 2 * pad[0] - R) // stride[0] + 1
@@ -271,9 +274,45 @@ def conv_fwd(x, w, stride, pad, bias=None):
     if N * Ho * Wo * K >= 2 ** 31:
         raise ValueError('conv_fwd: output too large for 32-bit indexing')
     b = _f32(bias) if bias is not None else None
+    if variant in (5, 6):
+        _K.lib().conv_nhwc_fwd_glds(_DT[x.dtype], x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(),
+                                    _zero_page(x.device).data_ptr(), N, H, W, C, K, R, S, stride[0], stride[1],
+                                    pad[0], pad[1], 128 if variant == 5 else 64, _stream())
+        return y
     _K.lib().conv_nhwc_fwd(_DT[x.dtype], x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), N, H, W, C, K, R, S,
-                           stride[0], stride[1], pad[0], pad[1], _stream())
+                           stride[0], stride[1], pad[0], pad[1], int(variant), _stream())
     return y
+
+
+_ZERO = {}
+
+
+def _zero_page(dev):
+    """128+ bytes of zeros the LDS-DMA conv kernel reads for halo / out-of-range pixels."""
+    z = _ZERO.get(dev)
+    if z is None:
+        z = _ZERO[dev] = torch.zeros(128, dtype=torch.float16, device=dev)
+    return z
+
+
+def _fwd_variants(C, K):
+    """Tile variants of conv_fwd valid for Cin=C, Cout=K.
+
+    1..4: register-staged kernel (conv_igemm.hip) with (BCO, BK) = (128,64) (128,32) (64,64) (64,32);
+    5, 6: LDS-DMA kernel (conv_glds.hip) with 128x128 / 64x256 tiles."""
+    v = []
+    if C % 64 == 0 and K % 128 == 0:
+        v.append(5)
+    if C % 64 == 0:
+        v.append(6)
+    if K % 128 == 0 and C % 64 == 0:
+        v.append(1)
+    if K % 128 == 0:
+        v.append(2)
+    if C % 64 == 0:
+        v.append(3)
+    v.append(4)
+    return v
 
 
 def conv_wgrad_ok(x, w):
@@ -376,6 +415,8 @@ def _fwd_candidates(x, w, stride, pad, bias):
     K, R, S, C = w.shape
     if conv_ok_shape(x, w, stride, pad):
         c.append(('hip', lambda: conv_fwd(x, w, stride, pad, bias)))
+        for v in _fwd_variants(C, K):
+            c.append(('hip%d' % v, lambda v=v: conv_fwd(x, w, stride, pad, bias, v)))
     if R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0):
         def mm():
             y = torch.mm(x.reshape(-1, C), w.reshape(K, C).t())
@@ -406,6 +447,9 @@ def _dgrad_candidates(dy, x, w, stride, pad):
     if (tuple(stride) == (1, 1) and C % 64 == 0 and K % 32 == 0 and 2 * pad[0] == R - 1 and 2 * pad[1] == S - 1
             and _CONV_HIP):
         c.append(('hip', lambda: conv_fwd(dy, _dgrad_weight(w), (1, 1), (R - 1 - pad[0], S - 1 - pad[1]))))
+        for v in _fwd_variants(K, C):
+            c.append(('hip%d' % v, lambda v=v: conv_fwd(dy, _dgrad_weight(w), (1, 1), (R - 1 - pad[0], S - 1 - pad[1]),
+                                                        None, v)))
     c.append(('miopen', lambda: _conv_bwd_torch(dy, x, w, stride, pad, (True, False))[0]))
     return c
 

@@ -38,10 +38,10 @@ def init(backend=None, timeout_s=1800):
         backend = 'nccl' if (torch.cuda.is_available() and os.environ.get('MXAMD_DIST_BACKEND', '') != 'gloo') \
             else 'gloo'
     if backend == 'nccl':
-        torch.cuda.set_device(local_rank())
+        torch.cuda.set_device(local_device())
     kw = {}
     if backend == 'nccl':
-        kw['device_id'] = torch.device('cuda', local_rank())
+        kw['device_id'] = torch.device('cuda', local_device())
     dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
     if backend == 'nccl':
         _cpu_group = dist.new_group(backend='gloo')
@@ -65,6 +65,12 @@ def world_size():
 
 def local_rank():
     return int(os.environ.get('LOCAL_RANK', os.environ.get('RANK', '0')))
+
+
+def local_device():
+    """GPU index of this process (local rank modulo the visible devices)."""
+    n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    return local_rank() % n if n else 0
 
 
 def barrier():

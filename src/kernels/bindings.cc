@@ -34,7 +34,10 @@ void gap_nhwc_backward(int dtype, const void* dy, void* dx, int N, int HW, int C
 void flat_sgd(int dtype, void* w, const void* g, float* mom, float* w32, int64_t n, float lr, float wd,
               float momentum, float rescale, float clip, hipStream_t s);
 void conv_nhwc_fwd(int dtype, const void* x, const void* w, const float* bias, void* y, int N, int H, int W, int C,
-                   int K, int R, int S, int sh, int sw, int ph, int pw, hipStream_t s);
+                   int K, int R, int S, int sh, int sw, int ph, int pw, int variant, hipStream_t s);
+void conv_nhwc_fwd_glds(int dtype, const void* x, const void* w, const float* bias, void* y, const void* zero, int N,
+                        int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int bco,
+                        hipStream_t s);
 int64_t conv_nhwc_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw);
 void conv_nhwc_wgrad(int dtype, const void* x, const void* dy, float* slab, int out_dtype, void* out, int accum, int N,
                      int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, hipStream_t s);
@@ -130,11 +133,19 @@ PYBIND11_MODULE(_hip_kernels, m) {
     flat_sgd(dt, P<void>(w), P<void>(g), P<float>(mom), P<float>(w32), n, lr, wd, momentum, rescale, clip, S(s));
     check_launch("flat_sgd");
   });
+  // variant: 0 heuristic tile, 1..4 = (BCO, BK) in (128,64) (128,32) (64,64) (64,32)
   m.def("conv_nhwc_fwd", [](int dt, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int N, int H, int W,
-                            int C, int K, int R, int Sf, int sh, int sw, int ph, int pw, uintptr_t s) {
+                            int C, int K, int R, int Sf, int sh, int sw, int ph, int pw, int variant, uintptr_t s) {
     conv_nhwc_fwd(dt, P<void>(x), P<void>(w), P<float>(bias), P<void>(y), N, H, W, C, K, R, Sf, sh, sw, ph, pw,
-                  S(s));
+                  variant, S(s));
     check_launch("conv_nhwc_fwd");
+  });
+  m.def("conv_nhwc_fwd_glds", [](int dt, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, uintptr_t zero, int N,
+                                 int H, int W, int C, int K, int R, int Sf, int sh, int sw, int ph, int pw, int bco,
+                                 uintptr_t s) {
+    conv_nhwc_fwd_glds(dt, P<void>(x), P<void>(w), P<float>(bias), P<void>(y), P<void>(zero), N, H, W, C, K, R, Sf,
+                       sh, sw, ph, pw, bco, S(s));
+    check_launch("conv_nhwc_fwd_glds");
   });
   m.def("conv_nhwc_wgrad_workspace", &conv_nhwc_wgrad_workspace);
   m.def("conv_nhwc_wgrad", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t slab, int odt, uintptr_t out, int accum,

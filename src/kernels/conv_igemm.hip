@@ -272,16 +272,38 @@ static void launch_fwd(const void* x, const void* w, const float* bias, void* y,
                      static_cast<const T*>(w), bias, static_cast<T*>(y), g, tiles_co);
 }
 
-// Tile choice: BCO=128 when Cout allows it (128x128 tile), else 64 x 256.
+// Tile choice (variant 0): BCO=128 when Cout allows it (128x128 tile), else 64 x 256.
 // BK=64 when Cin is a multiple of 64 (all ResNet layers but the stem).
+// variant 1..4 force (BCO, BK) = (128,64) (128,32) (64,64) (64,32): the autotuner
+// (ops/kernel_fns.py) times them per shape -- LDS footprint sets blocks/CU
+// (73.7 / 41 / 92 / 51 KB -> 2 / 3 / 1 / 3 blocks), which decides latency hiding.
 template <typename T>
-static void dispatch_fwd(const void* x, const void* w, const float* bias, void* y, const ConvGeom& g,
+static void dispatch_fwd(const void* x, const void* w, const float* bias, void* y, const ConvGeom& g, int variant,
                          hipStream_t s) {
   const bool co128 = (g.K % 128) == 0;
   // BK=64 halves the barriers per FLOP but its LDS/VGPR footprint allows only
   // 1-2 blocks per CU; short reductions (1x1 over <=128 channels) are
   // bandwidth-bound and want the occupancy of BK=32 instead.
   const bool bk64 = (g.C % 64) == 0 && g.Ktot >= 256;
+  switch (variant) {
+    case 1:
+      MXAMD_HOST_CHECK(co128 && g.C % 64 == 0, "conv variant 1 needs Cout%128, Cin%64");
+      launch_fwd<T, 128, 64>(x, w, bias, y, g, s);
+      return;
+    case 2:
+      MXAMD_HOST_CHECK(co128, "conv variant 2 needs Cout%128");
+      launch_fwd<T, 128, 32>(x, w, bias, y, g, s);
+      return;
+    case 3:
+      MXAMD_HOST_CHECK(g.C % 64 == 0, "conv variant 3 needs Cin%64");
+      launch_fwd<T, 64, 64>(x, w, bias, y, g, s);
+      return;
+    case 4:
+      launch_fwd<T, 64, 32>(x, w, bias, y, g, s);
+      return;
+    default:
+      break;
+  }
   if (co128 && bk64) launch_fwd<T, 128, 64>(x, w, bias, y, g, s);
   else if (co128) launch_fwd<T, 128, 32>(x, w, bias, y, g, s);
   else if (bk64) launch_fwd<T, 64, 64>(x, w, bias, y, g, s);
@@ -289,7 +311,7 @@ static void dispatch_fwd(const void* x, const void* w, const float* bias, void* 
 }
 
 void conv_nhwc_fwd(int dtype, const void* x, const void* w, const float* bias, void* y, int N, int H, int W, int C,
-                   int K, int R, int S, int sh, int sw, int ph, int pw, hipStream_t s) {
+                   int K, int R, int S, int sh, int sw, int ph, int pw, int variant, hipStream_t s) {
   ConvGeom g;
   g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S;
   g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw;
@@ -300,8 +322,8 @@ void conv_nhwc_fwd(int dtype, const void* x, const void* w, const float* bias, v
   MXAMD_HOST_CHECK(C % 32 == 0 && K % 64 == 0, "conv_nhwc_fwd: need Cin % 32 == 0 and Cout % 64 == 0");
   MXAMD_HOST_CHECK((int64_t)N * H * W * C < (1ll << 31) && (int64_t)g.M * K < (1ll << 31),
                    "conv_nhwc_fwd: tensor too large for 32-bit pixel indexing");
-  if (dtype == kF16) dispatch_fwd<__half>(x, w, bias, y, g, s);
-  else if (dtype == kBF16) dispatch_fwd<__hip_bfloat16>(x, w, bias, y, g, s);
+  if (dtype == kF16) dispatch_fwd<__half>(x, w, bias, y, g, variant, s);
+  else if (dtype == kBF16) dispatch_fwd<__hip_bfloat16>(x, w, bias, y, g, variant, s);
   else throw std::runtime_error("conv_nhwc_fwd: dtype must be f16 or bf16");
 }
 

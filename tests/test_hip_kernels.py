@@ -199,11 +199,12 @@ def test_conv_nhwc_fwd_matches_fp32(dtype, cfg):
     w = (torch.randn(Cout, k, k, Cin, device='cuda') / (k * k * Cin) ** 0.5).to(dtype)
     bias = torch.randn(Cout, device='cuda')
     assert KF.conv_ok_shape(x, w, (s, s), (pad, pad))
-    y = KF.conv_fwd(x, w, (s, s), (pad, pad), bias)
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), bias, s, pad).permute(0, 2, 3, 1)
-    assert y.shape == ref.shape
     tol = 2e-2 if dtype == torch.float16 else 6e-2
-    torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+    for v in [0] + KF._fwd_variants(Cin, Cout):     # heuristic tile + every forced (BCO, BK) tile
+        y = KF.conv_fwd(x, w, (s, s), (pad, pad), bias, v)
+        assert y.shape == ref.shape
+        torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol, msg=lambda m: 'variant %d: %s' % (v, m))
 
 
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
