@@ -322,7 +322,7 @@ def conv_wgrad_ok(x, w):
             and x.numel() < 2 ** 31 and x.data_ptr() % 16 == 0)
 
 
-def conv_wgrad(x, dy, wshape, stride, pad, out=None, accum=False):
+def conv_wgrad(x, dy, wshape, stride, pad, out=None, accum=False, dma=True):
     """dW[K,R,S,C] of an NHWC conv on MFMA (split-pixel fp32 slabs + reduce).
 
     ``out`` (optional, contiguous, f16/bf16/f32) receives the result; with
@@ -344,7 +344,8 @@ def conv_wgrad(x, dy, wshape, stride, pad, out=None, accum=False):
         accum = False
     assert out.is_contiguous() and out.numel() == K * R * S * C and out.dtype in _DT
     lib.conv_nhwc_wgrad(_DT[x.dtype], x.data_ptr(), dy.data_ptr(), slab.data_ptr(), _DT[out.dtype], out.data_ptr(),
-                        int(bool(accum)), N, H, W, C, K, R, S, stride[0], stride[1], pad[0], pad[1], _stream())
+                        int(bool(accum)), N, H, W, C, K, R, S, stride[0], stride[1], pad[0], pad[1],
+                        _zero_page(x.device).data_ptr() if dma else 0, _stream())
     return out
 
 
@@ -468,6 +469,7 @@ def _wgrad_candidates(dy, x, w, stride, pad):
     K, R, S, C = w.shape
     if conv_wgrad_ok(x, w):
         c.insert(0, ('hip', lambda: conv_wgrad(x, dy, w.shape, stride, pad)))
+        c.insert(1, ('hipreg', lambda: conv_wgrad(x, dy, w.shape, stride, pad, dma=False)))
     if R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0):
         P = dy.numel() // K
         for chunks in (16, 64):
@@ -505,10 +507,10 @@ def _wgrad(dy, x, w, w_ref, stride, pad):
     split-K GEMM candidates add their fp32 sum into it).
     """
     key = ('wgrad', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype)
-    if _ALGO.get(key) == 'hip':
+    if _ALGO.get(key) in ('hip', 'hipreg'):
         tgt = _leaf_grad(w_ref, dtype=w.dtype)
         if tgt is not None:
-            conv_wgrad(x, dy, w.shape, stride, pad, out=tgt, accum=True)
+            conv_wgrad(x, dy, w.shape, stride, pad, out=tgt, accum=True, dma=_ALGO[key] == 'hip')
             return None
     dw = _select(key, _wgrad_candidates(dy, x, w, stride, pad), 'hip' if conv_wgrad_ok(x, w) else 'miopen')
     if dw.dtype != w.dtype:

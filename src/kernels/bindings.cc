@@ -40,7 +40,8 @@ void conv_nhwc_fwd_glds(int dtype, const void* x, const void* w, const float* bi
                         hipStream_t s);
 int64_t conv_nhwc_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw);
 void conv_nhwc_wgrad(int dtype, const void* x, const void* dy, float* slab, int out_dtype, void* out, int accum, int N,
-                     int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, hipStream_t s);
+                     int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, const void* zero,
+                     hipStream_t s);
 int layernorm_bwd_partials(int M);
 void layernorm_forward(int dtype, const void* x, const float* gamma, const float* beta, void* y, float* mean,
                        float* rstd, int M, int D, float eps, hipStream_t s);
@@ -148,11 +149,12 @@ PYBIND11_MODULE(_hip_kernels, m) {
     check_launch("conv_nhwc_fwd_glds");
   });
   m.def("conv_nhwc_wgrad_workspace", &conv_nhwc_wgrad_workspace);
+  // zero: 0 -> register-staged kernel, else a >=128-byte zero page -> LDS-DMA kernel
   m.def("conv_nhwc_wgrad", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t slab, int odt, uintptr_t out, int accum,
                               int N, int H, int W, int C, int K, int R, int Sf, int sh, int sw, int ph, int pw,
-                              uintptr_t s) {
+                              uintptr_t zero, uintptr_t s) {
     conv_nhwc_wgrad(dt, P<void>(x), P<void>(dy), P<float>(slab), odt, P<void>(out), accum, N, H, W, C, K, R, Sf, sh,
-                    sw, ph, pw, S(s));
+                    sw, ph, pw, P<void>(zero), S(s));
     check_launch("conv_nhwc_wgrad");
   });
   m.def("layernorm_bwd_partials", &layernorm_bwd_partials);

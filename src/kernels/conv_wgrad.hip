@@ -247,6 +247,148 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const T* __res
   }
 }
 
+// LDS-DMA variant: the same sub-tile images filled with global_load_lds_dwordx4
+// (one wave-instruction = 8 rows x 128 B of a sub-tile, lane L -> row L>>3,
+// position L&7, fetching global chunk (L&7) ^ swz(row)); out-of-range pixels
+// come from a zero page.  No staging registers, no ds_write in the loop; the
+// next 64-pixel stage is in flight during the current stage's MFMAs.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+template <typename T, int WM, int WN, bool IDENT>
+__global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_glds_kernel(const T* __restrict__ x,
+                                                                       const T* __restrict__ dy,
+                                                                       float* __restrict__ slab,
+                                                                       const T* __restrict__ zero, WgradGeom g) {
+  constexpr int NW = WM * WN;
+  constexpr int NSUB = WM + WN;
+  constexpr int SUB = 64 * 64;
+  constexpr int NINS = NSUB * 8;                 // wave-instructions per stage
+  constexpr int IPW = (NINS + NW - 1) / NW;      // per wave
+  __shared__ __attribute__((aligned(1024))) T smem[2 * NSUB * SUB];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid % WM;
+  const int wn = wid / WM;
+
+  const int nblk = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7;
+  const int q8 = nblk >> 3, r8 = nblk & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tile = wgid % g.tiles;
+  const int split = wgid / g.tiles;
+  const int tm = tile % g.tiles_m;
+  const int tn = tile / g.tiles_m;
+  const int m0 = tm * 64 * WM;
+  const int n0 = tn * 64 * WN;
+  const int pbeg = split * g.plen;
+  const int pend = min(g.P, pbeg + g.plen);
+  const int KT = (pend - pbeg + 63) >> 6;
+
+  // per-instruction descriptors (instruction ins = wid + i*NW: sub-tile ins>>3, row group ins&7)
+  const int t = lane >> 3;
+  int d_row[IPW], d_col[IPW], d_r[IPW], d_s[IPW], d_lds[IPW];
+  bool d_on[IPW], d_isx[IPW];
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int ins = wid + i * NW;
+    d_on[i] = ins < NINS;
+    const int sub = d_on[i] ? ins >> 3 : 0;
+    const int row = (ins & 7) * 8 + t;
+    const int gch = (lane & 7) ^ swz(row);
+    d_row[i] = row;
+    d_lds[i] = sub * SUB * (int)sizeof(T) + (ins & 7) * 1024;
+    d_isx[i] = sub < WM;
+    if (d_isx[i]) {
+      const int n = m0 + sub * 64;           // first rsc column of the sub-tile (one (r, s): C % 64 == 0)
+      const int rs = n / g.C;
+      d_col[i] = n - rs * g.C + gch * 8;
+      d_r[i] = rs / g.S;
+      d_s[i] = rs - d_r[i] * g.S;
+    } else {
+      d_col[i] = n0 + (sub - WM) * 64 + gch * 8;
+      d_r[i] = d_s[i] = 0;
+    }
+  }
+  const T* zsrc = zero + ((lane & 7) << 3);
+
+  auto issue = [&](int kt, int buf) {
+    char* sbase = reinterpret_cast<char*>(smem + buf * NSUB * SUB);
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      if (!d_on[i]) continue;                 // wave-uniform
+      const int p = pbeg + kt * 64 + d_row[i];
+      bool ok = p < pend;
+      const T* src;
+      if (!d_isx[i]) {
+        src = dy + (int64_t)p * g.K + d_col[i];
+      } else if (IDENT) {
+        src = x + (int64_t)p * g.C + d_col[i];
+      } else {
+        const int nimg = (int)fdiv((uint32_t)p, g.fHoWo);
+        const int rem = p - nimg * (g.Ho * g.Wo);
+        const int ho = (int)fdiv((uint32_t)rem, g.fWo);
+        const int wo = rem - ho * g.Wo;
+        const int hi = ho * g.sh - g.ph + d_r[i];
+        const int wi = wo * g.sw - g.pw + d_s[i];
+        ok = ok && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+        src = x + ((int64_t)(nimg * g.H + hi) * g.W + wi) * g.C + d_col[i];
+      }
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(ok ? src : zsrc), (lds_void_t*)(sbase + d_lds[i]), 16, 0, 0);
+    }
+  };
+
+  const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
+  const int frow = 8 * fg + fq;
+  int foff[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) foff[f] = frow * 128 + ((((2 * f) + (fp >> 1)) ^ swz(frow)) << 4) + ((fp & 1) << 3);
+
+  f4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (KT > 0) issue(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < KT) issue(kt + 1, buf ^ 1);
+    const T* sx = smem + buf * NSUB * SUB + wm * SUB;
+    const T* sd = smem + buf * NSUB * SUB + (WM + wn) * SUB;
+#pragma unroll
+    for (int kk = 0; kk < 64; kk += 32) {
+      v8s a[4], b[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) b[f] = tr_frag(sd, kk * 128 + foff[f]);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) a[f] = tr_frag(sx, kk * 128 + foff[f]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = Mfma16<T>::run(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+
+  float* out = slab + (size_t)split * g.K * g.RSC;
+  const int rsc_l = (lane >> 4) * 4;
+  const int k_l = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rsc = m0 + wm * 64 + i * 16 + rsc_l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = n0 + wn * 64 + j * 16 + k_l;
+      *reinterpret_cast<f4_t*>(out + (size_t)k * g.RSC + rsc) = acc[i][j];
+    }
+  }
+}
+
 template <typename OutT>
 __device__ __forceinline__ void store4(OutT* p, f4_t v);
 template <>
@@ -377,8 +519,17 @@ WgradPlan plan_wgrad(int N, int H, int W, int C, int K, int R, int S, int sh, in
 
 template <typename T, int WM, int WN, int FM>
 void launch_wgrad(const void* x, const void* dy, float* slab, const WgradGeom& g, int splits, bool ident,
-                  hipStream_t s) {
+                  const void* zero, hipStream_t s) {
   dim3 grid(g.tiles * splits);
+  if (zero && FM == 4) {
+    if (ident)
+      hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, WM, WN, true>), grid, dim3(64 * WM * WN), 0, s,
+                         static_cast<const T*>(x), static_cast<const T*>(dy), slab, static_cast<const T*>(zero), g);
+    else
+      hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, WM, WN, false>), grid, dim3(64 * WM * WN), 0, s,
+                         static_cast<const T*>(x), static_cast<const T*>(dy), slab, static_cast<const T*>(zero), g);
+    return;
+  }
   if (ident)
     hipLaunchKernelGGL((conv_wgrad_kernel<T, WM, WN, FM, true>), grid, dim3(64 * WM * WN), 0, s,
                        static_cast<const T*>(x), static_cast<const T*>(dy), slab, g);
@@ -389,13 +540,13 @@ void launch_wgrad(const void* x, const void* dy, float* slab, const WgradGeom& g
 
 template <typename T>
 void dispatch_wgrad(const void* x, const void* dy, float* slab, const WgradGeom& g, const WgradPlan& pl, bool ident,
-                    hipStream_t s) {
-  if (pl.wm == 2 && pl.wn == 2 && pl.fm == 8) launch_wgrad<T, 2, 2, 8>(x, dy, slab, g, pl.splits, ident, s);
-  else if (pl.wm == 2 && pl.wn == 2) launch_wgrad<T, 2, 2, 4>(x, dy, slab, g, pl.splits, ident, s);
-  else if (pl.wm == 3) launch_wgrad<T, 3, 1, 4>(x, dy, slab, g, pl.splits, ident, s);
-  else if (pl.wm == 2) launch_wgrad<T, 2, 1, 4>(x, dy, slab, g, pl.splits, ident, s);
-  else if (pl.wn == 2) launch_wgrad<T, 1, 2, 4>(x, dy, slab, g, pl.splits, ident, s);
-  else launch_wgrad<T, 1, 1, 4>(x, dy, slab, g, pl.splits, ident, s);
+                    const void* zero, hipStream_t s) {
+  if (pl.wm == 2 && pl.wn == 2 && pl.fm == 8) launch_wgrad<T, 2, 2, 8>(x, dy, slab, g, pl.splits, ident, zero, s);
+  else if (pl.wm == 2 && pl.wn == 2) launch_wgrad<T, 2, 2, 4>(x, dy, slab, g, pl.splits, ident, zero, s);
+  else if (pl.wm == 3) launch_wgrad<T, 3, 1, 4>(x, dy, slab, g, pl.splits, ident, zero, s);
+  else if (pl.wm == 2) launch_wgrad<T, 2, 1, 4>(x, dy, slab, g, pl.splits, ident, zero, s);
+  else if (pl.wn == 2) launch_wgrad<T, 1, 2, 4>(x, dy, slab, g, pl.splits, ident, zero, s);
+  else launch_wgrad<T, 1, 1, 4>(x, dy, slab, g, pl.splits, ident, zero, s);
 }
 
 }  // namespace
@@ -408,8 +559,10 @@ int64_t conv_nhwc_wgrad_workspace(int N, int H, int W, int C, int K, int R, int 
 
 // dW (OHWI, dtype out_dtype) = / += wgrad(x, dy).  slab: fp32 workspace of
 // conv_nhwc_wgrad_workspace() elements.
+// zero: optional >= 128-byte zero page; when given, the LDS-DMA kernel variant runs.
 void conv_nhwc_wgrad(int dtype, const void* x, const void* dy, float* slab, int out_dtype, void* out, int accum, int N,
-                     int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, hipStream_t s) {
+                     int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, const void* zero,
+                     hipStream_t s) {
   MXAMD_HOST_CHECK(C % 64 == 0 && K % 64 == 0, "conv_nhwc_wgrad: need Cin % 64 == 0 and Cout % 64 == 0");
   WgradGeom g;
   g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S;
@@ -428,8 +581,8 @@ void conv_nhwc_wgrad(int dtype, const void* x, const void* dy, float* slab, int 
   g.fWo = make_fastdiv(g.Wo);
   g.fHoWo = make_fastdiv(g.Ho * g.Wo);
   const bool ident = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
-  if (dtype == kF16) dispatch_wgrad<__half>(x, dy, slab, g, pl, ident, s);
-  else if (dtype == kBF16) dispatch_wgrad<__hip_bfloat16>(x, dy, slab, g, pl, ident, s);
+  if (dtype == kF16) dispatch_wgrad<__half>(x, dy, slab, g, pl, ident, zero, s);
+  else if (dtype == kBF16) dispatch_wgrad<__hip_bfloat16>(x, dy, slab, g, pl, ident, zero, s);
   else throw std::runtime_error("conv_nhwc_wgrad: dtype must be f16 or bf16");
   const int64_t n = (int64_t)K * g.RSC;
   if (out_dtype == kF32) launch_reduce<float>(slab, pl.splits, n, static_cast<float*>(out), accum, s);

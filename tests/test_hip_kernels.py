@@ -224,13 +224,14 @@ def test_conv_wgrad_matches_fp32(dtype, cfg):
     Ho = (H + 2 * pad - k) // s + 1
     dy = torch.randn(N, Ho, Ho, Cout, device='cuda').to(dtype)
     assert KF.conv_wgrad_ok(x, w)
-    dw = KF.conv_wgrad(x, dy, w.shape, (s, s), (pad, pad))
     ref = torch.ops.aten.convolution_backward(
         dy.float().permute(0, 3, 1, 2), x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None,
         [s, s], [pad, pad], [1, 1], False, [0, 0], 1, [False, True, False])[1].permute(0, 2, 3, 1)
     scale = ref.abs().max().item()
     tol = (2e-3 if dtype == torch.float16 else 1e-2) * scale
-    torch.testing.assert_close(dw.float(), ref, rtol=0, atol=tol)
+    for dma in (True, False):          # LDS-DMA kernel and register-staged kernel
+        dw = KF.conv_wgrad(x, dy, w.shape, (s, s), (pad, pad), dma=dma)
+        torch.testing.assert_close(dw.float(), ref, rtol=0, atol=tol)
     # accumulate into an fp32 buffer (the direct-to-.grad path)
     acc = torch.ones(Cout, k, k, Cin, device='cuda')
     KF.conv_wgrad(x, dy, w.shape, (s, s), (pad, pad), out=acc, accum=True)

@@ -29,8 +29,11 @@ def main():
                                                                              fl / t_m / 1e9)
         tot['miopen'] += t_m * cnt
         if KF.conv_wgrad_ok(x, w):
+            t_r = timeit(lambda: KF.conv_wgrad(x, dy, w.shape, (s, s), (pad, pad), dma=False))
             t_h = timeit(lambda: KF.conv_wgrad(x, dy, w.shape, (s, s), (pad, pad)))
-            line += '  hip %.3f ms (%4.0f TF/s)' % (t_h, fl / t_h / 1e9)
+            line += '  hip-reg %.3f ms (%4.0f TF/s)  hip-dma %.3f ms (%4.0f TF/s)' % (t_r, fl / t_r / 1e9, t_h,
+                                                                                  fl / t_h / 1e9)
+            t_h = min(t_h, t_r)
             tot['hip'] += t_h * cnt
         else:
             tot['hip'] += t_m * cnt
