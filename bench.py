@@ -69,6 +69,8 @@ def main():
     x = nd.random.uniform(-1, 1, shape=(B, S, S, 3), ctx=ctx).astype(args.dtype)
     y = nd.array(torch.randint(0, 1000, (B,)).numpy(), ctx=ctx)
 
+    n_ranks = dist.world_size()
+
     def step():
         with autograd.record():
             out = net(x)
@@ -76,7 +78,9 @@ def main():
             if loss_scale != 1.0:
                 loss = loss * loss_scale
         loss.backward()
-        trainer.step(B)
+        # gradients are summed over ranks by the RCCL all-reduce: normalise by the GLOBAL batch so
+        # N-GPU data parallelism is the same optimisation as one GPU at batch B*N
+        trainer.step(B * n_ranks)
         return loss
 
     def sync():

@@ -140,32 +140,43 @@ def multibox_detection(cls_prob, loc_pred, anchor, clip=True, threshold=0.01, ba
                   'minimum_negative_samples': ('int', 0), 'variances': ('floats', (0.1, 0.1, 0.2, 0.2))})
 def multibox_target(anchor, label, cls_pred, overlap_threshold=0.5, ignore_label=-1.0, negative_mining_ratio=-1.0,
                     negative_mining_thresh=0.5, minimum_negative_samples=0, variances=(0.1, 0.1, 0.2, 0.2)):
-    anchors = anchor.reshape(-1, 4).float()
+    """SSD target assignment.  GPU tensors run the gfx950 kernel (src/kernels/detection.hip,
+    one workgroup per image); CPU tensors run the vectorised reference below."""
+    anchors = anchor.reshape(-1, 4).float().contiguous()
     A = anchors.shape[0]
     B = label.shape[0]
+    if anchor.is_cuda:
+        from . import kernels as _K
+        if _K.enabled() and _K.available():
+            return _multibox_target_hip(_K.lib(), anchors, label, cls_pred, overlap_threshold, ignore_label,
+                                        negative_mining_ratio, negative_mining_thresh, minimum_negative_samples,
+                                        variances)
+        from .hip_ops import _ALLOW_FALLBACK
+        if not _ALLOW_FALLBACK:
+            raise RuntimeError('MultiBoxTarget on GPU needs the HIP kernel extension: %s' % _K.load_error())
     dev = anchor.device
     loc_target = torch.zeros(B, A, 4, device=dev)
     loc_mask = torch.zeros(B, A, 4, device=dev)
     cls_target = torch.full((B, A), float(ignore_label), device=dev)
+    anchors_c = anchors.cpu()
     for b in range(B):
-        lab = label[b].float()
-        valid = lab[:, 0] >= 0
-        gt = lab[valid]
-        ng = gt.shape[0]
+        lab = label[b].float().cpu()
+        inval = (lab[:, 0] == -1).nonzero()
+        ng = int(inval[0]) if inval.numel() else lab.shape[0]      # valid gts end at the first class == -1
         if ng == 0:
             continue
-        iou = _iou(anchors, gt[:, 1:5]).cpu()                            # [A, G]
+        gt = lab[:ng]
+        iou = _iou(anchors_c, gt[:, 1:5])                                # [A, G]
         match_iou = torch.full((A,), -1.0)
         match_gt = torch.full((A,), -1, dtype=torch.long)
         aflag = torch.full((A,), -1, dtype=torch.long)
         gflag = torch.zeros(ng, dtype=torch.bool)
-        work = iou.clone()
         npos = 0
-        while not bool(gflag.all()):                                     # greedy bipartite stage
-            w = work.clone()
+        for _ in range(ng):                                              # greedy bipartite stage
+            w = iou.clone()
             w[aflag == 1] = -1
             w[:, gflag] = -1
-            v, flat = w.reshape(-1).max(0)
+            v, flat = w.reshape(-1).max(0)                               # first max in (anchor, gt) order
             if float(v) <= 1e-6:
                 break
             j, k = divmod(int(flat), ng)
@@ -173,20 +184,18 @@ def multibox_target(anchor, label, cls_pred, overlap_threshold=0.5, ignore_label
             aflag[j] = 1
             gflag[k] = True
             npos += 1
+        best_iou, best_gt = _first_max(iou)
         if overlap_threshold > 0:
-            best_iou, best_gt = iou.max(1)
-            for j in range(A):
-                if aflag[j] == 1:
-                    continue
-                match_iou[j], match_gt[j] = float(best_iou[j]), int(best_gt[j])
-                if best_iou[j] > overlap_threshold:
-                    aflag[j] = 1
-                    npos += 1
+            free = aflag != 1
+            match_iou = torch.where(free, best_iou, match_iou)
+            match_gt = torch.where(free, best_gt, match_gt)
+            newpos = free & (best_iou > overlap_threshold)
+            aflag[newpos] = 1
+            npos += int(newpos.sum())
         if negative_mining_ratio > 0:
             nneg = min(int(npos * negative_mining_ratio), A - npos)
             nneg = max(nneg, min(minimum_negative_samples, A - npos))
             if nneg > 0:
-                best_iou, best_gt = iou.max(1)
                 unset = match_iou < 0
                 match_iou = torch.where(unset, best_iou, match_iou)
                 match_gt = torch.where(unset, best_gt, match_gt)
@@ -201,7 +210,7 @@ def multibox_target(anchor, label, cls_pred, overlap_threshold=0.5, ignore_label
         pos = aflag == 1
         neg = aflag == 0
         if pos.any():
-            g = gt[match_gt[pos].to(dev)]
+            g = gt[match_gt[pos]].to(dev)
             a = anchors[pos.to(dev)]
             aw, ah = a[:, 2] - a[:, 0], a[:, 3] - a[:, 1]
             ax, ay = (a[:, 0] + a[:, 2]) / 2, (a[:, 1] + a[:, 3]) / 2
@@ -214,6 +223,37 @@ def multibox_target(anchor, label, cls_pred, overlap_threshold=0.5, ignore_label
             cls_target[b, pos.to(dev)] = g[:, 0] + 1
         cls_target[b, neg.to(dev)] = 0
     return loc_target.reshape(B, -1), loc_mask.reshape(B, -1), cls_target
+
+
+def _first_max(m):
+    """Row-wise max and the FIRST column attaining it (the reference's strict '>' scan)."""
+    v = m.max(1).values
+    hit = m == v[:, None]
+    idx = torch.argmax(hit.to(torch.uint8), 1)
+    return v, idx
+
+
+def _multibox_target_hip(lib, anchors, label, cls_pred, thr, ignore_label, ratio, neg_thresh, min_neg, var):
+    from .kernel_fns import _DT, _stream
+    B, L, W = label.shape
+    A = anchors.shape[0]
+    dev = anchors.device
+    lab = label.float().contiguous()
+    cp = cls_pred.contiguous()
+    if cp.dtype not in _DT:
+        cp = cp.float()
+    if tuple(cp.shape) != (B, cp.shape[1], A):
+        raise ValueError('MultiBoxTarget: cls_pred must be [batch, classes, anchors], got %s' % (tuple(cp.shape),))
+    loc_target = torch.empty(B, A * 4, device=dev)
+    loc_mask = torch.empty(B, A * 4, device=dev)
+    cls_target = torch.empty(B, A, device=dev)
+    scratch = torch.empty(3, B, A, dtype=torch.int32, device=dev)
+    lib.multibox_target(_DT[cp.dtype], anchors.data_ptr(), lab.data_ptr(), cp.data_ptr(), loc_target.data_ptr(),
+                        loc_mask.data_ptr(), cls_target.data_ptr(), scratch[0].data_ptr(), scratch[1].data_ptr(),
+                        scratch[2].data_ptr(), B, A, L, W, cp.shape[1], float(thr), float(ignore_label), float(ratio),
+                        float(neg_thresh), int(min_neg), float(var[0]), float(var[1]), float(var[2]), float(var[3]),
+                        _stream())
+    return loc_target, loc_mask, cls_target
 
 
 # ---------------------------------------------------------------------------

@@ -68,6 +68,10 @@ void pool_nhwc_forward(int dtype, int is_max, const void* x, void* y, uint8_t* a
 void pool_nhwc_backward(int dtype, int is_max, const void* dy, const uint8_t* arg, void* dx, int N, int H, int W,
                         int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip,
                         hipStream_t s);
+void multibox_target(int dtype, const float* anchors, const float* labels, const void* cls_pred, float* loc_target,
+                     float* loc_mask, float* cls_target, float* match_iou, int* match_gt, uint32_t* key, int B, int A,
+                     int L, int W, int C, float thr, float ignore_label, float neg_ratio, float neg_thresh,
+                     int min_neg, float v0, float v1, float v2, float v3, hipStream_t s);
 }  // namespace mxamd
 
 using namespace mxamd;
@@ -88,6 +92,17 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.attr("arch") = "gfx950";
 
   m.def("bn_partials_rows", &bn_partials_rows);
+  m.def("multibox_target", [](int dt, uintptr_t anchors, uintptr_t labels, uintptr_t cls_pred, uintptr_t loc_target,
+                              uintptr_t loc_mask, uintptr_t cls_target, uintptr_t match_iou, uintptr_t match_gt,
+                              uintptr_t key, int B, int A, int L, int W, int C, float thr, float ignore_label,
+                              float neg_ratio, float neg_thresh, int min_neg, float v0, float v1, float v2, float v3,
+                              uintptr_t s) {
+    multibox_target(dt, P<float>(anchors), P<float>(labels), P<void>(cls_pred), P<float>(loc_target),
+                    P<float>(loc_mask), P<float>(cls_target), P<float>(match_iou), P<int>(match_gt),
+                    P<uint32_t>(key), B, A, L, W, C, thr, ignore_label, neg_ratio, neg_thresh, min_neg, v0, v1, v2,
+                    v3, S(s));
+    check_launch("multibox_target");
+  });
   // mask: optional uint8 ReLU bitmask (one byte per 8 elements) written by the add+relu tail
   m.def("bn_nhwc_forward", [](int dt, uintptr_t x, uintptr_t add, uintptr_t y, uintptr_t mask, uintptr_t g, uintptr_t b,
                               uintptr_t center, uintptr_t part, uintptr_t mean, uintptr_t inv, uintptr_t var,
