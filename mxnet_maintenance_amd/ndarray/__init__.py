@@ -12,7 +12,7 @@ from .ndarray import NDArray, _op  # noqa: F401
 from . import register as _register
 from .utils import load, save, load_frombuffer, zeros, empty, array  # noqa: F401
 from . import op, _internal, contrib, linalg, random, image, sparse, utils  # noqa: F401
-from .sparse import CSRNDArray, RowSparseNDArray  # noqa: F401
+from .sparse import CSRNDArray, RowSparseNDArray, cast_storage  # noqa: F401
 
 _g = globals()
 for _name, _fn in op.__dict__.items():

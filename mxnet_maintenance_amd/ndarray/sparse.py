@@ -15,7 +15,7 @@ from ..base import torch_dtype, MXNetError
 from ..context import current_context
 from .ndarray import NDArray
 
-__all__ = ['CSRNDArray', 'RowSparseNDArray', 'csr_matrix', 'row_sparse_array', 'cast_storage',
+__all__ = ['elemwise_add', 'elemwise_sub', 'elemwise_mul', 'elemwise_div', 'CSRNDArray', 'RowSparseNDArray', 'csr_matrix', 'row_sparse_array', 'cast_storage',
            'zeros', 'empty', 'array', 'retain', 'dot', 'add', 'subtract', 'multiply', 'divide']
 
 
@@ -211,3 +211,4 @@ add = _elem('broadcast_add')
 subtract = _elem('broadcast_sub')
 multiply = _elem('broadcast_mul')
 divide = _elem('broadcast_div')
+elemwise_add, elemwise_sub, elemwise_mul, elemwise_div = add, subtract, multiply, divide

@@ -8,12 +8,14 @@ import sys
 
 def classify(name):
     n = name.lower()
-    if 'mxamd::conv' in n or 'wgrad_reduce' in n:
+    if ('mxamd::' in n and 'conv' in n) or 'wgrad_reduce' in n:
         return 'conv (in-tree HIP MFMA)'
     if 'igemm' in n or 'conv' in n or 'gemm' in n or 'ck::' in n or 'xdl' in n or 'cijk' in n:
         return 'conv/gemm (MIOpen/hipBLASLt)'
     if 'attn' in n or 'fmha' in n or 'flash' in n or 'attention' in n:
         return 'attention (torch SDPA)'
+    if 'multibox' in n:
+        return 'detection (MultiBoxTarget)'
     if 'bn_' in n or 'batch_norm' in n:
         return 'batchnorm'
     if 'layernorm' in n or 'column_sum' in n:
