@@ -475,16 +475,37 @@ def _wgrad_candidates(dy, x, w, stride, pad):
         for chunks in (16, 64):
             if P % chunks == 0 and P // chunks >= 1024:
                 def splitk(chunks=chunks):
-                    # split-K batched GEMM (hipBLASLt): [chunks, K, P/chunks] x [chunks, P/chunks, C], fp32 sum
-                    d3 = dy.reshape(chunks, P // chunks, K).transpose(1, 2)
-                    x3 = x.reshape(chunks, P // chunks, C)
                     # fp32 result: the caller accumulates it into the fp16 grad buffer (no cast pass)
-                    return _bmm_f32(d3, x3).sum(0).view(K, 1, 1, C)
+                    return _splitk_wgrad(dy, x, chunks)
                 c.append(('splitk%d' % chunks, splitk))
     return c
 
 
 _BMM_OUT_DTYPE = [None]
+
+
+def _splitk_wgrad(dy, x, chunks, out=None):
+    """1x1 wgrad as a split-K batched GEMM (hipBLASLt): [chunks, K, P/chunks] x [chunks, P/chunks, C]
+    with fp32 partial products, column-summed by the HIP slab reduce kernel — into a fresh fp32
+    dW, or added straight into ``out`` (the weight's fp16/bf16 .grad buffer)."""
+    K, C = dy.shape[-1], x.shape[-1]
+    P = dy.numel() // K
+    d3 = dy.reshape(chunks, P // chunks, K).transpose(1, 2)
+    x3 = x.reshape(chunks, P // chunks, C)
+    part = _bmm_f32(d3, x3)
+    if not part.is_contiguous() or (K * C) % 4:
+        r = part.sum(0).view(K, 1, 1, C)
+        if out is not None:
+            out.add_(r.view(out.shape))
+            return None
+        return r
+    lib = _K.lib()
+    if out is None:
+        r = torch.empty(K, 1, 1, C, dtype=torch.float32, device=dy.device)
+        lib.slab_reduce(0, part.data_ptr(), chunks, K * C, r.data_ptr(), 0, _stream())
+        return r
+    lib.slab_reduce(_DT[out.dtype], part.data_ptr(), chunks, K * C, out.data_ptr(), 1, _stream())
+    return None
 
 
 def _bmm_f32(a, b):
@@ -507,10 +528,16 @@ def _wgrad(dy, x, w, w_ref, stride, pad):
     split-K GEMM candidates add their fp32 sum into it).
     """
     key = ('wgrad', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype)
-    if _ALGO.get(key) in ('hip', 'hipreg'):
+    algo = _ALGO.get(key)
+    if algo in ('hip', 'hipreg'):
         tgt = _leaf_grad(w_ref, dtype=w.dtype)
         if tgt is not None:
-            conv_wgrad(x, dy, w.shape, stride, pad, out=tgt, accum=True, dma=_ALGO[key] == 'hip')
+            conv_wgrad(x, dy, w.shape, stride, pad, out=tgt, accum=True, dma=algo == 'hip')
+            return None
+    elif algo is not None and algo.startswith('splitk'):
+        tgt = _leaf_grad(w_ref, dtype=w.dtype)
+        if tgt is not None:
+            _splitk_wgrad(dy, x, int(algo[6:]), out=tgt)
             return None
     dw = _select(key, _wgrad_candidates(dy, x, w, stride, pad), 'hip' if conv_wgrad_ok(x, w) else 'miopen')
     if dw.dtype != w.dtype:

@@ -72,6 +72,7 @@ void multibox_target(int dtype, const float* anchors, const float* labels, const
                      float* loc_mask, float* cls_target, float* match_iou, int* match_gt, uint32_t* key, int B, int A,
                      int L, int W, int C, float thr, float ignore_label, float neg_ratio, float neg_thresh,
                      int min_neg, float v0, float v1, float v2, float v3, hipStream_t s);
+void slab_reduce(int out_dtype, float* slab, int splits, int64_t n, void* out, int accum, hipStream_t s);
 }  // namespace mxamd
 
 using namespace mxamd;
@@ -92,6 +93,10 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.attr("arch") = "gfx950";
 
   m.def("bn_partials_rows", &bn_partials_rows);
+  m.def("slab_reduce", [](int odt, uintptr_t slab, int splits, int64_t n, uintptr_t out, int accum, uintptr_t s) {
+    slab_reduce(odt, P<float>(slab), splits, n, P<void>(out), accum, S(s));
+    check_launch("slab_reduce");
+  });
   m.def("multibox_target", [](int dt, uintptr_t anchors, uintptr_t labels, uintptr_t cls_pred, uintptr_t loc_target,
                               uintptr_t loc_mask, uintptr_t cls_target, uintptr_t match_iou, uintptr_t match_gt,
                               uintptr_t key, int B, int A, int L, int W, int C, float thr, float ignore_label,

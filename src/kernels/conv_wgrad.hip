@@ -590,4 +590,15 @@ void conv_nhwc_wgrad(int dtype, const void* x, const void* dy, float* slab, int 
   else launch_reduce<__hip_bfloat16>(slab, pl.splits, n, static_cast<__hip_bfloat16*>(out), accum, s);
 }
 
+// Column-sum of `splits` fp32 rows of length n (a split-K GEMM's partial products) into `out`
+// (+= when accum): the split-K 1x1 wgrad candidate reduces straight into the .grad buffer.
+void slab_reduce(int out_dtype, float* slab, int splits, int64_t n, void* out, int accum, hipStream_t s) {
+  MXAMD_HOST_CHECK(n % 4 == 0 && (reinterpret_cast<uintptr_t>(slab) & 15) == 0 &&
+                       (reinterpret_cast<uintptr_t>(out) & (out_dtype == kF32 ? 15 : 7)) == 0 && splits >= 1,
+                   "slab_reduce: n % 4 == 0 and aligned slab/out required");
+  if (out_dtype == kF32) launch_reduce<float>(slab, splits, n, static_cast<float*>(out), accum, s);
+  else if (out_dtype == kF16) launch_reduce<__half>(slab, splits, n, static_cast<__half*>(out), accum, s);
+  else launch_reduce<__hip_bfloat16>(slab, splits, n, static_cast<__hip_bfloat16*>(out), accum, s);
+}
+
 }  // namespace mxamd

@@ -591,3 +591,21 @@ def test_linear_mfma_matches_fp32(dtype, mkn):
         torch.testing.assert_close(fn().float(), dxf, rtol=tol, atol=tol)
     for _name, fn in nlp_fns._fc_wgrad_cands(dy, x.detach(), w.detach()):
         torch.testing.assert_close(fn().float(), dwf, rtol=tol, atol=tol * 4)
+
+
+@pytest.mark.parametrize('chunks', [16, 64])
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+def test_splitk_wgrad_slab_reduce(chunks, dtype):
+    _lib()
+    from mxnet_maintenance_amd.ops import kernel_fns as kf
+    torch.manual_seed(0)
+    P, K, C = 64 * 1024, 128, 64
+    dy = (torch.randn(P, K, device='cuda') * 0.1).to(dtype)
+    x = (torch.randn(P, C, device='cuda') * 0.1).to(dtype)
+    ref = dy.float().t() @ x.float()
+    r = kf._splitk_wgrad(dy.view(16, 64, 64, K), x.view(16, 64, 64, C), chunks)
+    torch.testing.assert_close(r.view(K, C), ref, rtol=2e-3, atol=2e-3)
+    g = (torch.randn(K, 1, 1, C, device='cuda') * 0.1).to(dtype)
+    g0 = g.float().clone()
+    assert kf._splitk_wgrad(dy.view(16, 64, 64, K), x.view(16, 64, 64, C), chunks, out=g) is None
+    torch.testing.assert_close(g.float().view(K, C), g0.view(K, C) + ref, rtol=2e-2, atol=2e-2)
