@@ -23,6 +23,11 @@ from . import kernels as _K
 _ALLOW_FALLBACK = os.environ.get('MXAMD_ALLOW_TORCH_FALLBACK', '0') == '1'
 
 
+def _acc(t):
+    """Accumulation dtype: fp32 for fp16/bf16/fp32 inputs, fp64 stays fp64 (reference CPU semantics)."""
+    return t if t.dtype == torch.float64 else t.float()
+
+
 def _use_hip(t):
     """True when ``t`` lives on the GPU and the HIP kernels should run."""
     if not t.is_cuda:
@@ -213,11 +218,11 @@ def layer_norm(data, gamma, beta, eps, want_stats=True):
     """LayerNorm over the last axis; returns (out, mean, std) (mean/std only meaningful with want_stats)."""
     if _use_hip(data) and _K.ln_ok(data):
         return _K.LayerNorm.apply(data, gamma, beta, eps, bool(want_stats))
-    x = data.float()
+    x = _acc(data)
     mean = x.mean(-1, keepdim=True)
     var = x.var(-1, keepdim=True, unbiased=False)
     std = torch.sqrt(var + eps)
-    y = (x - mean) / std * gamma.float() + beta.float()
+    y = (x - mean) / std * _acc(gamma) + _acc(beta)
     return y.to(data.dtype), mean.to(data.dtype), std.to(data.dtype)
 
 

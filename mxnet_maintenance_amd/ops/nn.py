@@ -28,6 +28,11 @@ from . import hip_ops
 # ---------------------------------------------------------------------------
 
 
+def _acc(t):
+    """Accumulation dtype: fp32 for fp16/bf16/fp32 inputs, fp64 stays fp64 (reference CPU semantics)."""
+    return t if t.dtype == torch.float64 else t.float()
+
+
 def _is_channel_last(layout):
     return layout is not None and layout.endswith('C') and len(layout) > 2
 
@@ -390,7 +395,7 @@ def softmax(data, length=None, axis=-1, temperature=None, dtype=None, use_length
     if length is not None and use_length:
         m = _length_mask(x, length, axis % x.dim())
         x = x.masked_fill(~m, float('-inf'))
-        r = torch.softmax(x.float(), dim=axis)
+        r = torch.softmax(_acc(x), dim=axis)
         r = torch.nan_to_num(r, nan=0.0).masked_fill(~m, 0.0)
     else:
         r = torch.softmax(x, dim=axis, dtype=torch.float32) if x.dtype in (torch.float16, torch.bfloat16) else torch.softmax(x, dim=axis)
@@ -429,11 +434,11 @@ class _SoftmaxOutputFn(torch.autograd.Function):
         if multi_output:
             n, c = data.shape[0], data.shape[1]
             x = data.reshape(n, c, -1)
-            p = torch.softmax(x.float(), dim=1)
+            p = torch.softmax(_acc(x), dim=1)
         elif preserve_shape:
-            p = torch.softmax(data.float(), dim=-1)
+            p = torch.softmax(_acc(data), dim=-1)
         else:
-            p = torch.softmax(data.reshape(data.shape[0], -1).float(), dim=1)
+            p = torch.softmax(_acc(data.reshape(data.shape[0], -1)), dim=1)
         ctx.save_for_backward(p, label)
         ctx.cfg = (grad_scale, ignore_label, multi_output, use_ignore, preserve_shape, normalization,
                    smooth_alpha, data.shape, data.dtype)
@@ -632,13 +637,13 @@ def layer_norm(data, gamma, beta, axis=-1, eps=1e-5, output_mean_var=False):
     axis = axis % data.dim()
     if axis == data.dim() - 1:
         return hip_ops.layer_norm(data, gamma, beta, eps, output_mean_var)
-    x = data.float()
+    x = _acc(data)
     mean = x.mean(dim=axis, keepdim=True)
     var = x.var(dim=axis, keepdim=True, unbiased=False)
     std = torch.sqrt(var + eps)
     shape = [1] * data.dim()
     shape[axis] = -1
-    y = (x - mean) / std * gamma.reshape(shape).float() + beta.reshape(shape).float()
+    y = (x - mean) / std * _acc(gamma.reshape(shape)) + _acc(beta.reshape(shape))
     return y.to(data.dtype), mean.to(data.dtype), std.to(data.dtype)
 
 
@@ -647,13 +652,13 @@ def layer_norm(data, gamma, beta, axis=-1, eps=1e-5, output_mean_var=False):
           params={'num_groups': ('int', 1), 'eps': ('float', 1e-5), 'output_mean_var': ('bool', False)})
 def group_norm(data, gamma, beta, num_groups=1, eps=1e-5, output_mean_var=False):
     n = data.shape[0]
-    x = data.reshape(n, num_groups, -1).float()
+    x = _acc(data.reshape(n, num_groups, -1))
     mean = x.mean(-1, keepdim=True)
     var = x.var(-1, keepdim=True, unbiased=False)
     std = torch.sqrt(var + eps)
     y = ((x - mean) / std).reshape(data.shape)
     gshape = (1, num_groups, -1)
-    y = (y.reshape(n, num_groups, -1) * gamma.reshape(gshape).float() + beta.reshape(gshape).float()).reshape(data.shape)
+    y = (y.reshape(n, num_groups, -1) * _acc(gamma.reshape(gshape)) + _acc(beta.reshape(gshape))).reshape(data.shape)
     return y.to(data.dtype), mean.reshape(n, num_groups).to(data.dtype), std.reshape(n, num_groups).to(data.dtype)
 
 
@@ -661,12 +666,12 @@ def group_norm(data, gamma, beta, num_groups=1, eps=1e-5, output_mean_var=False)
           infer_params=lambda s, a: ({1: (s[0][1],), 2: (s[0][1],)} if s[0] is not None else {}),
           params={'eps': ('float', 1e-3)})
 def instance_norm(data, gamma, beta, eps=1e-3):
-    x = data.float()
+    x = _acc(data)
     dims = list(range(2, data.dim()))
     mean = x.mean(dims, keepdim=True)
     var = x.var(dims, keepdim=True, unbiased=False)
     shape = (1, -1) + (1,) * (data.dim() - 2)
-    y = (x - mean) / torch.sqrt(var + eps) * gamma.reshape(shape).float() + beta.reshape(shape).float()
+    y = (x - mean) / torch.sqrt(var + eps) * _acc(gamma.reshape(shape)) + _acc(beta.reshape(shape))
     return y.to(data.dtype)
 
 

@@ -344,14 +344,14 @@ def numeric_grad(executor, location, aux_states=None, eps=1e-4, use_forward_trai
         for i in range(flat.size):
             orig = flat[i]
             flat[i] = orig + eps / 2.0
-            executor.arg_dict[k][:] = nd.array(old_value.astype(dtype))
+            executor.arg_dict[k][:] = nd.array(old_value.astype(dtype), dtype=dtype)
             if aux_states is not None:
                 for key, val in aux_states.items():
                     executor.aux_dict[key][:] = val
             executor.forward(is_train=use_forward_train)
             f_peps = sum(float(o.asnumpy().astype(np.float64).sum()) for o in executor.outputs)
             flat[i] = orig - eps / 2.0
-            executor.arg_dict[k][:] = nd.array(old_value.astype(dtype))
+            executor.arg_dict[k][:] = nd.array(old_value.astype(dtype), dtype=dtype)
             if aux_states is not None:
                 for key, val in aux_states.items():
                     executor.aux_dict[key][:] = val
@@ -359,7 +359,7 @@ def numeric_grad(executor, location, aux_states=None, eps=1e-4, use_forward_trai
             f_neps = sum(float(o.asnumpy().astype(np.float64).sum()) for o in executor.outputs)
             approx_grads[k].reshape(-1)[i] = (f_peps - f_neps) / eps
             flat[i] = orig
-        executor.arg_dict[k][:] = nd.array(old_value.astype(dtype))
+        executor.arg_dict[k][:] = nd.array(old_value.astype(dtype), dtype=dtype)
     return approx_grads
 
 
