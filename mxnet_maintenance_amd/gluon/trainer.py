@@ -526,10 +526,13 @@ class Trainer:
 class _ArenaBuckets(GradBuckets):
     """GradBuckets whose buckets are contiguous slices of the trainer's gradient arenas."""
 
-    def __init__(self, arenas, bucket_bytes=None):
+    def __init__(self, arenas, bucket_bytes=None, tail_bytes=None):
         from ..parallel.buckets import _Bucket
         if bucket_bytes is None:
             bucket_bytes = int(_env.get('MXAMD_BUCKET_MB') * (1 << 20))
+        if tail_bytes is None:
+            tail_bytes = int(_env.get('MXAMD_TAIL_BUCKET_MB') * (1 << 20))
+        tail_bytes = max(1, min(tail_bytes, bucket_bytes))
         self.overlap = dist.world_size() > 1
         self.average = False
         self.buckets = []
@@ -541,7 +544,10 @@ class _ArenaBuckets(GradBuckets):
             cur_lo = None
             segs = list(zip(a.params, a.views))[::-1]
             for p, (off, n, shape) in segs:
-                if cur is None or (cur_hi - off) * esz > bucket_bytes:
+                # the first layers' gradients (produced last, reduced after backward ends) go into small
+                # tail buckets so the un-overlapped final all-reduce stays short
+                cap = tail_bytes if (off + n) * esz <= 2 * tail_bytes else bucket_bytes
+                if cur is None or (cur_hi - off) * esz > cap:
                     if cur is not None:
                         cur.flat = a.g[cur_lo:cur_hi]
                     cur = _Bucket(a.g.dtype, a.g.device)

@@ -28,6 +28,9 @@ KNOBS = {
     'MXAMD_BUCKET_MB': (float, 25.0, 'gradient bucket size for the overlapped RCCL all-reduce (MiB); larger buckets '
                         'amortise per-collective latency on point-to-point xGMI rings',
                         'MXNET_KVSTORE_BIGARRAY_BOUND'),
+    'MXAMD_TAIL_BUCKET_MB': (float, 4.0, 'bucket cap for the gradients of the first layers (the last to be produced '
+                             'in backward): their all-reduce cannot overlap compute, so smaller buckets shorten the '
+                             'exposed tail', ''),
     'MXAMD_FLAT_ARENA': (int, 1, 'Trainer keeps params/grads in flat per-dtype arenas (one fused optimizer kernel, '
                          'zero-copy all-reduce buckets)', ''),
     'MXAMD_DIST_BACKEND': (str, '', 'force torch.distributed backend (gloo for CPU runs); default nccl(=RCCL) on GPU',

@@ -238,3 +238,105 @@ def test_kvstore_dist_sync_two_processes_gloo():
     expect = 1 - 0.1 * 12 / 8
     np.testing.assert_allclose(res[0][3], expect, rtol=1e-5)
     assert res[0][3] == res[1][3]
+
+
+def test_arena_bucket_layout_small_tail():
+    """Trainer gradient buckets: contiguous arena slices, big buckets first, small tail buckets for the
+    first layers (reduced after backward ends)."""
+    import torch
+    from mxnet_maintenance_amd.gluon.trainer import _ArenaBuckets
+
+    class _P:
+        def __init__(self, t):
+            self._t = t
+
+        def list_data(self):
+            return [self._t]
+
+    sizes = [3000, 500, 800, 12000, 9000, 7000, 100]
+    offs = np.cumsum([0] + sizes[:-1]).tolist()
+
+    class _A:
+        g = torch.zeros(sum(sizes), dtype=torch.float16)
+        params = [_P(mx.nd.zeros((n,))) for n in sizes]
+        views = [(o, n, (n,)) for o, n in zip(offs, sizes)]
+
+    kb = 1024
+    b = _ArenaBuckets([_A()], bucket_bytes=24 * kb, tail_bytes=4 * kb)
+    spans = [(x.flat.data_ptr() - _A.g.data_ptr()) // 2 for x in b.buckets]
+    lens = [x.flat.numel() for x in b.buckets]
+    # buckets tile the arena back to front without gaps
+    assert sum(lens) == sum(sizes)
+    assert all(s + n == prev for s, n, prev in zip(spans[1:], lens[1:], spans[:-1]))
+    # the last bucket (first layers) is under the tail cap unless a single tensor is larger
+    assert lens[-1] * 2 <= 4 * kb or b.buckets[-1].count == 1
+    assert max(lens[:2]) * 2 > 4 * kb
+
+
+def _dp_mlp_train(rank, world, xs, ys, steps):
+    import mxnet_maintenance_amd as mx
+    from mxnet_maintenance_amd import nd, gluon, autograd
+    mx.random.seed(3)
+    net = gluon.nn.HybridSequential()
+    net.add(gluon.nn.Dense(16, activation='relu', in_units=6), gluon.nn.Dense(16, activation='tanh', in_units=16),
+            gluon.nn.Dense(3, in_units=16))
+    net.initialize(mx.init.Xavier())
+    net.hybridize()
+    tr = gluon.Trainer(net.collect_params(), 'sgd', {'learning_rate': 0.2, 'momentum': 0.9, 'wd': 1e-3},
+                       kvstore='device')
+    loss_fn = gluon.loss.SoftmaxCrossEntropyLoss()
+    for s in range(steps):
+        x, y = nd.array(xs[s]), nd.array(ys[s])
+        with autograd.record():
+            l = loss_fn(net(x), y)
+        l.backward()
+        tr.step(x.shape[0] * world)
+    return [p.data().asnumpy() for p in net.collect_params().values()], len(getattr(tr, '_buckets', None).buckets
+                                                                             if getattr(tr, '_buckets', None) else [])
+
+
+def _dp_worker(rank, world, port, q, xs, ys, steps):
+    os.environ.update({'RANK': str(rank), 'WORLD_SIZE': str(world), 'LOCAL_RANK': str(rank),
+                       'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port), 'MXAMD_DIST_BACKEND': 'gloo',
+                       'MXAMD_BUCKET_MB': '0.0005', 'MXAMD_TAIL_BUCKET_MB': '0.0002'})
+    try:
+        import mxnet_maintenance_amd as mx  # noqa: F401
+        from mxnet_maintenance_amd.parallel import dist
+        dist.init()
+        w, nb = _dp_mlp_train(rank, world, [x[rank] for x in xs], [y[rank] for y in ys], steps)
+        q.put((rank, w, nb))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, 'ERR', traceback.format_exc()))
+    finally:
+        import torch.distributed as d
+        if d.is_initialized():
+            d.destroy_process_group()
+
+
+def test_data_parallel_bucketed_overlap_matches_single_process():
+    """2-rank DP (gloo) with several overlapped gradient buckets == one process on the concatenated
+    batch (SGD momentum + wd, global-batch normalisation)."""
+    rs = np.random.RandomState(1)
+    steps, world = 3, 2
+    xs = [rs.randn(world, 5, 6).astype('float32') for _ in range(steps)]
+    ys = [rs.randint(0, 3, size=(world, 5)).astype('float32') for _ in range(steps)]
+    ctx = tmp.get_context('spawn')
+    q = ctx.Queue()
+    port = 30000 + os.getpid() % 1000
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, q, xs, ys, steps)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        item = q.get(timeout=240)
+        res[item[0]] = item
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert res[r][1] != 'ERR', res[r][2]
+    assert res[0][2] >= 3, 'expected several gradient buckets, got %d' % res[0][2]
+    ref, _ = _dp_mlp_train(0, 1, [x.reshape(-1, 6) for x in xs], [y.reshape(-1) for y in ys], steps)
+    for a, b, c in zip(res[0][1], res[1][1], ref):
+        np.testing.assert_array_equal(a, b)
+        np.testing.assert_allclose(a, c, rtol=1e-4, atol=1e-5)
