@@ -59,9 +59,33 @@ class GradientCompression:
         if res is None:
             res = torch.zeros(t.numel(), dtype=torch.float32, device=t.device)
             self._residuals[key] = res
+        lib = _hip(t)
+        if lib is not None:
+            # gfx950 kernels: quantise (+ residual update) and decode-and-sum of all ranks in one pass each
+            from ..ops.kernel_fns import _DT, _stream
+            n = t.numel()
+            g = t.contiguous()
+            packed = torch.empty(((n + 15) // 16) * 4, dtype=torch.uint8, device=t.device)
+            lib.twobit_quantize(_DT[g.dtype], g.data_ptr(), res.data_ptr(), packed.data_ptr(), n, self.threshold,
+                                _stream())
+            allp = dist.all_gather(packed).contiguous()
+            total = torch.empty(n, dtype=torch.float32, device=t.device)
+            lib.twobit_dequantize_sum(allp.data_ptr(), packed.numel(), allp.shape[0], n, self.threshold,
+                                      total.data_ptr(), _stream())
+            t.copy_(total.view(t.shape).to(t.dtype))
+            return
         packed = quantize_2bit(t, res, self.threshold)
         allp = dist.all_gather(packed)
         total = torch.zeros(t.numel(), dtype=torch.float32, device=t.device)
         for i in range(allp.shape[0]):
             total.add_(dequantize_2bit(allp[i], t.numel(), self.threshold))
         t.copy_(total.view(t.shape).to(t.dtype))
+
+
+def _hip(t):
+    if not t.is_cuda or t.dtype not in (torch.float32, torch.float16, torch.bfloat16):
+        return None
+    from ..ops import kernels as _K
+    if _K.enabled() and _K.available():
+        return _K.lib()
+    return None

@@ -73,6 +73,9 @@ void multibox_target(int dtype, const float* anchors, const float* labels, const
                      int L, int W, int C, float thr, float ignore_label, float neg_ratio, float neg_thresh,
                      int min_neg, float v0, float v1, float v2, float v3, hipStream_t s);
 void slab_reduce(int out_dtype, float* slab, int splits, int64_t n, void* out, int accum, hipStream_t s);
+void twobit_quantize(int dtype, const void* g, float* res, void* packed, int64_t n, float thr, hipStream_t s);
+void twobit_dequantize_sum(const void* packed, int64_t row_bytes, int nrows, int64_t n, float thr, float* out,
+                           hipStream_t s);
 }  // namespace mxamd
 
 using namespace mxamd;
@@ -93,6 +96,16 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.attr("arch") = "gfx950";
 
   m.def("bn_partials_rows", &bn_partials_rows);
+  m.def("twobit_quantize", [](int dt, uintptr_t g, uintptr_t res, uintptr_t packed, int64_t n, float thr,
+                              uintptr_t s) {
+    twobit_quantize(dt, P<void>(g), P<float>(res), P<void>(packed), n, thr, S(s));
+    check_launch("twobit_quantize");
+  });
+  m.def("twobit_dequantize_sum", [](uintptr_t packed, int64_t row_bytes, int nrows, int64_t n, float thr,
+                                    uintptr_t out, uintptr_t s) {
+    twobit_dequantize_sum(P<void>(packed), row_bytes, nrows, n, thr, P<float>(out), S(s));
+    check_launch("twobit_dequantize_sum");
+  });
   m.def("slab_reduce", [](int odt, uintptr_t slab, int splits, int64_t n, uintptr_t out, int accum, uintptr_t s) {
     slab_reduce(odt, P<float>(slab), splits, n, P<void>(out), accum, S(s));
     check_launch("slab_reduce");

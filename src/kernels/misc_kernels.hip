@@ -242,4 +242,72 @@ void flat_sgd(int dtype, void* w, const void* g, float* mom, float* w32, int64_t
 #undef L
 }
 
+// --------------------------------------------------------------------------
+// 2-bit gradient compression with error feedback (parity: src/kvstore/
+// gradient_compression-inl.h quantize_2bit / dequantize_2bit).  Code per
+// element: 3 = +threshold, 2 = -threshold, 0 = zero; 4 codes per byte, element
+// 4j+k at bits 2k of byte j.  One thread quantises 16 elements into one 32-bit
+// word; the decode kernel sums the codes of all ranks (the all-gathered
+// buffer) in one pass.
+// --------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) twobit_quantize_kernel(const T* __restrict__ g, float* __restrict__ res,
+                                                              uint32_t* __restrict__ packed, int64_t n, float thr) {
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t base = w * 16;
+  if (base >= n) return;
+  uint32_t word = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int64_t i = base + k;
+    if (i < n) {
+      float r = res[i] + static_cast<float>(g[i]);
+      uint32_t code = 0;
+      if (r >= thr) { code = 3; r -= thr; }
+      else if (r <= -thr) { code = 2; r += thr; }
+      res[i] = r;
+      word |= code << (2 * k);
+    }
+  }
+  packed[w] = word;
+}
+
+__global__ void __launch_bounds__(256) twobit_dequantize_sum_kernel(const uint8_t* __restrict__ packed,
+                                                                    int64_t row_bytes, int nrows, int64_t n,
+                                                                    float thr, float* __restrict__ out) {
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;   // byte index
+  if (j * 4 >= n) return;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int r = 0; r < nrows; ++r) {
+    const uint32_t b = packed[r * row_bytes + j];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t c = (b >> (2 * k)) & 3u;
+      acc[k] += c == 3u ? thr : (c == 2u ? -thr : 0.f);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (j * 4 + k < n) out[j * 4 + k] = acc[k];
+}
+
+void twobit_quantize(int dtype, const void* g, float* res, void* packed, int64_t n, float thr, hipStream_t s) {
+  MXAMD_HOST_CHECK((reinterpret_cast<uintptr_t>(packed) & 3) == 0, "twobit_quantize: packed must be 4-byte aligned");
+  const unsigned blocks = static_cast<unsigned>(((n + 15) / 16 + 255) / 256);
+  uint32_t* p = static_cast<uint32_t*>(packed);
+  if (dtype == kF32) twobit_quantize_kernel<float><<<blocks, 256, 0, s>>>(static_cast<const float*>(g), res, p, n, thr);
+  else if (dtype == kF16)
+    twobit_quantize_kernel<__half><<<blocks, 256, 0, s>>>(static_cast<const __half*>(g), res, p, n, thr);
+  else twobit_quantize_kernel<__hip_bfloat16><<<blocks, 256, 0, s>>>(static_cast<const __hip_bfloat16*>(g), res, p, n,
+                                                                      thr);
+}
+
+void twobit_dequantize_sum(const void* packed, int64_t row_bytes, int nrows, int64_t n, float thr, float* out,
+                           hipStream_t s) {
+  MXAMD_HOST_CHECK(row_bytes * 4 >= n && nrows >= 1, "twobit_dequantize_sum: row too short");
+  const unsigned blocks = static_cast<unsigned>(((n + 3) / 4 + 255) / 256);
+  twobit_dequantize_sum_kernel<<<blocks, 256, 0, s>>>(static_cast<const uint8_t*>(packed), row_bytes, nrows, n, thr,
+                                                      out);
+}
+
 }  // namespace mxamd

@@ -609,3 +609,25 @@ def test_splitk_wgrad_slab_reduce(chunks, dtype):
     g0 = g.float().clone()
     assert kf._splitk_wgrad(dy.view(16, 64, 64, K), x.view(16, 64, 64, C), chunks, out=g) is None
     torch.testing.assert_close(g.float().view(K, C), g0.view(K, C) + ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float16])
+@pytest.mark.parametrize('n', [1, 37, 4096 + 5])
+def test_twobit_compression_kernels_match_reference(dtype, n):
+    K = _lib()
+    from mxnet_maintenance_amd.kvstore.compression import quantize_2bit, dequantize_2bit
+    from mxnet_maintenance_amd.ops.kernel_fns import _DT, _stream
+    torch.manual_seed(0)
+    lib = K.lib()
+    g = (torch.randn(n, device='cuda') * 0.8).to(dtype)
+    res_ref = (torch.randn(n, device='cuda') * 0.3)
+    res_hip = res_ref.clone()
+    ref_packed = quantize_2bit(g, res_ref, 0.5)
+    packed = torch.empty(((n + 15) // 16) * 4, dtype=torch.uint8, device='cuda')
+    lib.twobit_quantize(_DT[dtype], g.data_ptr(), res_hip.data_ptr(), packed.data_ptr(), n, 0.5, _stream())
+    torch.testing.assert_close(res_hip, res_ref, rtol=0, atol=1e-6)
+    assert torch.equal(packed[:ref_packed.numel()], ref_packed)
+    two = torch.stack([packed, packed])
+    out = torch.empty(n, device='cuda')
+    lib.twobit_dequantize_sum(two.data_ptr(), packed.numel(), 2, n, 0.5, out.data_ptr(), _stream())
+    torch.testing.assert_close(out, 2 * dequantize_2bit(ref_packed, n, 0.5), rtol=0, atol=0)
