@@ -42,9 +42,11 @@ def main():
     if int(os.environ.get('WORLD_SIZE', '1')) > 1:
         dist.init()
     rank = dist.rank()
-    ctx = mx.gpu(dist.local_rank()) if torch.cuda.is_available() else mx.cpu()
+    # one process per GPU; ranks beyond the visible devices share them (single-GPU rehearsals)
+    dev = dist.local_rank() % max(1, torch.cuda.device_count()) if torch.cuda.is_available() else 0
+    ctx = mx.gpu(dev) if torch.cuda.is_available() else mx.cpu()
     if torch.cuda.is_available():
-        torch.cuda.set_device(dist.local_rank())
+        torch.cuda.set_device(dev)
     mx.random.seed(4321 + rank)
     B, S, P = args.batch, args.seq, args.masked
     net = bert_mod.get_bert_model(args.model, vocab_size=args.vocab)
@@ -69,7 +71,7 @@ def main():
             _seq, _pooled, nsp, mlm = net(tokens, types, valid, pos)
             loss = ce(mlm.reshape((-1, args.vocab)), mlm_label.reshape((-1,))).mean() + ce(nsp, nsp_label).mean()
         loss.backward()
-        trainer.step(1)
+        trainer.step(dist.world_size())   # per-rank mean loss; RCCL sums the ranks
         return loss
 
     def sync():
