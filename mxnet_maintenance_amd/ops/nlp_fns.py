@@ -295,7 +295,6 @@ class Linear(torch.autograd.Function):
         key = ('fc_fwd', tuple(x2.shape), tuple(w.shape), x.dtype, b is not None)
         y = _KF._select(key, _fc_fwd_cands(x2, w.contiguous(), b), 'mm')
         ctx.save_for_backward(x2, w)
-        ctx.w_ref = w
         ctx.has_b = b is not None
         ctx.bdt = b.dtype if b is not None else None
         ctx.xshape = x.shape
@@ -312,15 +311,7 @@ class Linear(torch.autograd.Function):
             dx = _KF._select(key, _fc_dgrad_cands(dy2, w.contiguous()), 'mm').view(ctx.xshape)
         if ctx.needs_input_grad[1]:
             key = ('fc_wgrad', tuple(dy2.shape), tuple(x2.shape), dy.dtype)
-            algo = _KF._ALGO.get(key)
-            tgt = _KF._leaf_grad(ctx.w_ref, dtype=w.dtype) if algo is not None else None
-            if tgt is not None and algo == 'mm':
-                tgt.addmm_(dy2.t(), x2)          # one GEMM with beta=1 straight into .grad (no add kernel)
-            elif tgt is not None and algo == 'hip':
-                _KF.conv_wgrad(x2.view(-1, 1, 1, x2.shape[1]), dy2.view(-1, 1, 1, N), (N, 1, 1, x2.shape[1]),
-                               (1, 1), (0, 0), out=tgt.view(N, 1, 1, x2.shape[1]), accum=True)
-            else:
-                dw = _KF._select(key, _fc_wgrad_cands(dy2, x2, w), 'mm').to(w.dtype)
+            dw = _KF._select(key, _fc_wgrad_cands(dy2, x2, w), 'mm').to(w.dtype)
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = torch.sum(dy2, 0, dtype=torch.float32).to(ctx.bdt)
         return dx, dw, db
