@@ -21,6 +21,16 @@ import time
 BASELINE_IMG_S = 363.69   # reference's published ResNet-50 training number (V100, perf.md)
 
 
+def _load_launcher():
+    """parallel/launch.py loaded by path: importing the package would import torch + HIP extensions."""
+    import importlib.util
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'mxnet_maintenance_amd', 'parallel', 'launch.py')
+    spec = importlib.util.spec_from_file_location('_mxamd_launch', path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -33,6 +43,12 @@ def main():
     ap.add_argument('--image-size', type=int, default=224)
     args = ap.parse_args()
 
+    # `bench.py --gpus N` without a launcher: start N fresh worker processes (one per GPU) and exit
+    # with their status.  This happens before anything in this process touches the GPU.
+    launch = _load_launcher()
+    if launch.needs_launch(args.gpus):
+        sys.exit(launch.relaunch_self(args.gpus))
+
     import torch
     import mxnet_maintenance_amd as mx
     from mxnet_maintenance_amd import gluon, autograd, nd
@@ -41,6 +57,8 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     if world > 1:
         dist.init()
+    if dist.world_size() != args.gpus:
+        raise SystemExit('bench.py: --gpus %d but the process group has %d ranks' % (args.gpus, dist.world_size()))
     rank = dist.rank()
     local_rank = dist.local_rank()
     # one process per GPU; ranks beyond the visible devices share them (single-GPU rehearsals)

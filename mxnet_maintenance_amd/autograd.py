@@ -117,12 +117,15 @@ def _prepare_leaves(leaves):
         if v._grad_req == 'write':
             a = v._arena
             if a is not None and a.all_write:
-                arenas[id(a)] = a      # whole flat gradient arena: one memset
+                arenas.setdefault(id(a), (a, []))[1].append(gbuf)
             else:
                 zero.append(gbuf)
     with torch.no_grad():
-        for a in arenas.values():
-            a.g.zero_()
+        for a, bufs in arenas.values():
+            if len(bufs) == len(a.params):
+                a.g.zero_()            # every parameter of the flat arena is on the tape: one memset
+            else:
+                zero.extend(bufs)      # others keep their gradients ('write' is per parameter)
         if zero:
             torch._foreach_zero_(zero)
 

@@ -171,10 +171,15 @@ class Executor:
             src = v._data if isinstance(v, NDArray) else torch.as_tensor(np.asarray(v))
             with torch.no_grad():
                 ad[k]._data.copy_(src.reshape(ad[k].shape))
+        need_grad = is_train and any(r != 'null' for r in self._grad_req.values())
+        self._last_is_train = bool(is_train)
+        return self._run(is_train, need_grad)
+
+    def _run(self, is_train, need_grad):
+        from .ndarray.ndarray import NDArray
         arg_names = self._symbol.list_arguments()
         feed = {}
         leaves = []
-        need_grad = is_train and any(r != 'null' for r in self._grad_req.values())
         for n, a in zip(arg_names, self.arg_arrays):
             t = a._data.detach()
             if need_grad and self._grad_req[n] != 'null':
@@ -204,7 +209,12 @@ class Executor:
     def backward(self, out_grads=None, is_train=True):
         from .ndarray.ndarray import NDArray
         if not self._leaves:
-            return
+            if not any(r != 'null' for r in self._grad_req.values()) or not self.grad_arrays:
+                return
+            # forward() ran without recording (is_train=False, the default): the reference still
+            # computes gradients here (python/mxnet/executor.py:156), so replay the program with the
+            # tape on, in the same train/predict mode as that forward
+            self._run(getattr(self, '_last_is_train', False), True)
         if out_grads is None:
             out_grads = [None] * len(self._out_tensors)
         elif isinstance(out_grads, NDArray):

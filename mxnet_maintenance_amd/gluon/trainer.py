@@ -399,7 +399,7 @@ class Trainer:
     def _update(self, ignore_stale_grad=False):
         if self._arenas is not None:
             self._check_stale(ignore_stale_grad)
-            self._fused_update()
+            self._fused_update(ignore_stale_grad)
             for p in self._params:
                 if p._data is not None:
                     for d in p._data:
@@ -434,12 +434,13 @@ class Trainer:
                 for d in (param._data or []):
                     d._fresh_grad = False
 
-    def _fused_update(self):
+    def _fused_update(self, ignore_stale_grad=False):
         import math
         o = self._optimizer
         clip = -1.0 if o.clip_gradient is None else o.clip_gradient
         kind = getattr(self, '_arena_kind', 'sgd')
         for a in self._arenas:
+            saved = self._save_stale(a) if ignore_stale_grad else None
             o._update_count(a.indices)
             lr = o._get_lrs(a.indices[:1])[0]
             wd = o._get_wds(a.indices[:1])[0]
@@ -452,6 +453,32 @@ class Trainer:
                 flat_adam_update(a, lr, o.beta1, o.beta2, o.epsilon, wd, o.rescale_grad, clip, kind == 'adamw')
             else:
                 lamb_flat_update(a, lr, o, t, wd, clip)
+            if saved:
+                self._restore_stale(saved)
+
+    @staticmethod
+    @torch.no_grad()
+    def _save_stale(a):
+        """Copies of the weight/state slices of ``a``'s parameters without a fresh gradient.
+
+        The fused kernels update a whole arena; with ``ignore_stale_grad`` the
+        reference leaves stale parameters (and their optimizer state) untouched,
+        so their slices are snapshotted here and written back after the update.
+        """
+        saved = []
+        for p, (off, n, _shape) in zip(a.params, a.views):
+            if p.list_data()[0]._fresh_grad:
+                continue
+            for buf in (a.w, a.w32, a.mom, a.mean, a.var):
+                if buf is not None:
+                    saved.append((buf, off, buf[off:off + n].clone()))
+        return saved
+
+    @staticmethod
+    @torch.no_grad()
+    def _restore_stale(saved):
+        for buf, off, val in saved:
+            buf[off:off + val.numel()].copy_(val)
 
     def save_states(self, fname):
         assert self._optimizer is not None

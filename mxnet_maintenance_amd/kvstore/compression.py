@@ -53,12 +53,19 @@ class GradientCompression:
     def get_params(self):
         return {'type': self.type, 'threshold': self.threshold}
 
-    def allreduce(self, t):
-        key = (t.data_ptr(), t.numel())
+    def residual(self, key, t):
+        """The error-feedback residual of kvstore key ``key`` (one per key, like comm.h buf.residual)."""
         res = self._residuals.get(key)
-        if res is None:
+        if res is None or res.numel() != t.numel() or res.device != t.device:
             res = torch.zeros(t.numel(), dtype=torch.float32, device=t.device)
             self._residuals[key] = res
+        return res
+
+    def allreduce(self, t, key=None):
+        """Sum ``t`` over workers through 2-bit codes; ``key`` selects the residual."""
+        if key is None:
+            key = ('anon', tuple(t.shape), t.dtype)
+        res = self.residual(key, t)
         lib = _hip(t)
         if lib is not None:
             # gfx950 kernels: quantise (+ residual update) and decode-and-sum of all ranks in one pass each

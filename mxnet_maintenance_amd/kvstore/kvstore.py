@@ -179,13 +179,18 @@ class KVStore(KVStoreBase):
             acc.add_(v._data.to(dev))
         return acc
 
-    def _allreduce_many(self, tensors):
-        """All-reduce a list of tensors with one fused collective per (dtype, device)."""
+    def _allreduce_many(self, tensors, keys=None):
+        """All-reduce a list of tensors with one fused collective per (dtype, device).
+
+        ``keys`` name the kvstore keys the tensors belong to: gradient compression
+        keeps one error-feedback residual per key (reference comm.h ``buf.residual``).
+        """
         if dist.world_size() <= 1 or not tensors:
             return
         if self._compression is not None:
-            for t in tensors:
-                self._compression.allreduce(t)
+            keys = keys if keys is not None else list(range(len(tensors)))
+            for k, t in zip(keys, tensors):
+                self._compression.allreduce(t, key=k)
             return
         groups = {}
         for t in tensors:
@@ -220,7 +225,7 @@ class KVStore(KVStoreBase):
         with torch.no_grad():
             for k, v in zip(keys, vals):
                 merged.append(self._local_sum(_as_list(v)).clone())
-            self._allreduce_many(merged)
+            self._allreduce_many(merged, keys)
             for k, m in zip(keys, merged):
                 if k not in self._store:
                     raise MXNetError('key %s has not been initialized' % str(k))
@@ -262,7 +267,7 @@ class KVStore(KVStoreBase):
             sums = [self._local_sum(_as_list(v)) for v in vals]
             # make sure we do not all-reduce into a caller buffer that is read later as input
             sums = [s if len(_as_list(v)) > 1 else s for s, v in zip(sums, vals)]
-            self._allreduce_many(sums)
+            self._allreduce_many(sums, keys)
             for s, o in zip(sums, outs):
                 for oo in _as_list(o):
                     if oo._data.data_ptr() != s.data_ptr():

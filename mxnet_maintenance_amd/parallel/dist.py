@@ -5,8 +5,10 @@ num_workers, barrier) and kvstore_nccl.h (NCCL communicator setup), re-done
 as a ``torch.distributed`` process group: backend ``nccl`` (= RCCL on ROCm) for
 GPU tensors, ``gloo`` for CPU tensors/tests.  Launch with
 ``python -m torch.distributed.run --nproc-per-node N ...`` (or
-``tools/launch.py``); RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT
-come from the environment.
+``tools/launch.py -n N``, ``parallel/launch.py``); RANK / WORLD_SIZE /
+LOCAL_RANK / MASTER_ADDR / MASTER_PORT come from the environment.  When more
+local ranks than visible GPUs are started (a one-GPU rehearsal of a multi-GPU
+job) the group falls back to gloo, since RCCL needs a distinct GPU per rank.
 """
 import datetime
 import os
@@ -35,8 +37,13 @@ def init(backend=None, timeout_s=1800):
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
     os.environ.setdefault('MASTER_PORT', '29500')
     if backend is None:
-        backend = 'nccl' if (torch.cuda.is_available() and os.environ.get('MXAMD_DIST_BACKEND', '') != 'gloo') \
-            else 'gloo'
+        backend = os.environ.get('MXAMD_DIST_BACKEND', '') or None
+    if backend is None:
+        backend = 'nccl' if torch.cuda.is_available() else 'gloo'
+        # RCCL needs one GPU per rank; more local ranks than visible GPUs is a single-GPU rehearsal
+        local_ws = int(os.environ.get('LOCAL_WORLD_SIZE', ws))
+        if backend == 'nccl' and local_ws > torch.cuda.device_count():
+            backend = 'gloo'
     if backend == 'nccl':
         torch.cuda.set_device(local_device())
     kw = {}
@@ -106,9 +113,10 @@ def all_gather(t):
     ws = world_size()
     if ws <= 1:
         return t.unsqueeze(0)
-    out = torch.empty((ws,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-    dist.all_gather_into_tensor(out, t.contiguous(), group=_group_for(t))
-    return out
+    # flat (world*numel,) output: gloo's all_gather_into_tensor rejects a (world, ...) shaped one
+    flat = torch.empty(ws * t.numel(), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(flat, t.contiguous().view(-1), group=_group_for(t))
+    return flat.view((ws,) + tuple(t.shape))
 
 
 def reduce_scatter(t):
@@ -116,9 +124,10 @@ def reduce_scatter(t):
     ws = world_size()
     if ws <= 1:
         return t
-    out = torch.empty((t.shape[0] // ws,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    dist.reduce_scatter_tensor(out, t.contiguous(), group=_group_for(t))
-    return out
+    shard = (t.shape[0] // ws,) + tuple(t.shape[1:])
+    out = torch.empty(t.numel() // ws, dtype=t.dtype, device=t.device)
+    dist.reduce_scatter_tensor(out, t.contiguous().view(-1), group=_group_for(t))
+    return out.view(shard)
 
 
 def all_to_all(t):

@@ -340,3 +340,82 @@ def test_data_parallel_bucketed_overlap_matches_single_process():
     for a, b, c in zip(res[0][1], res[1][1], ref):
         np.testing.assert_array_equal(a, b)
         np.testing.assert_allclose(a, c, rtol=1e-4, atol=1e-5)
+
+
+def _compression_worker(rank, world, port, q, pushes):
+    os.environ.update({'RANK': str(rank), 'WORLD_SIZE': str(world), 'LOCAL_RANK': str(rank),
+                       'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port), 'MXAMD_DIST_BACKEND': 'gloo'})
+    try:
+        import mxnet_maintenance_amd as mx
+        from mxnet_maintenance_amd import nd
+        kv = mx.kv.create('dist_sync')
+        kv.set_gradient_compression({'type': '2bit', 'threshold': 0.5})
+        keys = ['a', 'b', 'c']
+        grads = {'a': 0.25, 'b': 0.75, 'c': -0.125}
+        for k in keys:
+            kv.init(k, nd.zeros((4,)))
+        outs = []
+        for _ in range(pushes):
+            vals = [nd.ones((4,)) * grads[k] for k in keys]
+            res = [nd.zeros((4,)) for _ in keys]
+            kv.pushpull(keys, vals, out=res)
+            outs.append([float(r.asnumpy()[0]) for r in res])
+        q.put((rank, outs, len(kv._compression._residuals)))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, 'ERR', traceback.format_exc()))
+    finally:
+        import torch.distributed as d
+        if d.is_initialized():
+            d.destroy_process_group()
+
+
+def test_gradient_compression_residual_per_key_two_processes():
+    """2-bit compression keeps ONE error-feedback residual per kvstore key, even for same-size keys
+    pushed through fresh buffers (reference comm.h buf.residual), and sums the quantised codes."""
+    world, pushes, thr = 2, 5, 0.5
+    ctx = tmp.get_context('spawn')
+    q = ctx.Queue()
+    port = 31000 + os.getpid() % 1000
+    procs = [ctx.Process(target=_compression_worker, args=(r, world, port, q, pushes)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        item = q.get(timeout=240)
+        res[item[0]] = item
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert res[r][1] != 'ERR', res[r][2]
+        assert res[r][2] == 3
+    # host model of error feedback, per key; both ranks push the same gradient so the sum is 2x
+    expect = []
+    resid = {'a': 0.0, 'b': 0.0, 'c': 0.0}
+    for _ in range(pushes):
+        row = []
+        for k, g in (('a', 0.25), ('b', 0.75), ('c', -0.125)):  # exact in fp32
+            resid[k] += g
+            q_ = thr if resid[k] >= thr else (-thr if resid[k] <= -thr else 0.0)
+            resid[k] -= q_
+            row.append(world * q_)
+        expect.append(row)
+    np.testing.assert_allclose(res[0][1], expect, atol=1e-6)
+    assert res[0][1] == res[1][1]
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`bench.py --gpus 2` without a launcher starts 2 worker processes (gloo on CPU) and reports n_gpus=2."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK')}
+    out = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--steps', '1',
+                          '--warmup', '1', '--batch', '2', '--image-size', '32', '--dtype', 'float32',
+                          '--model', 'resnet18_v1b'], capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec['n_gpus'] == 2 and rec['config']['parallelism'] == 'dp2' and rec['config']['global_batch'] == 4

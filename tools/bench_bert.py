@@ -20,6 +20,17 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def _load_launcher():
+    """parallel/launch.py by path (no package import, so no GPU initialisation before the fork)."""
+    import importlib.util
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        'mxnet_maintenance_amd', 'parallel', 'launch.py')
+    spec = importlib.util.spec_from_file_location('_mxamd_launch', path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--batch', type=int, default=32, help='per-GPU sequences')
@@ -31,7 +42,11 @@ def main():
     ap.add_argument('--optimizer', default='lamb', choices=['lamb', 'adamw', 'adam'])
     ap.add_argument('--dtype', default='bfloat16', choices=['bfloat16', 'float16', 'float32'])
     ap.add_argument('--vocab', type=int, default=30528, help='30522 padded to a multiple of 64')
+    ap.add_argument('--gpus', type=int, default=1, help='worker processes (one per GPU)')
     args = ap.parse_args()
+    launch = _load_launcher()
+    if launch.needs_launch(args.gpus):
+        sys.exit(launch.relaunch_self(args.gpus))
 
     import torch
     import mxnet_maintenance_amd as mx

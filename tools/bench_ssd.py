@@ -32,6 +32,17 @@ def synthetic_labels(B, max_obj, classes, gen):
     return lab
 
 
+def _load_launcher():
+    """parallel/launch.py by path (no package import, so no GPU initialisation before the fork)."""
+    import importlib.util
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        'mxnet_maintenance_amd', 'parallel', 'launch.py')
+    spec = importlib.util.spec_from_file_location('_mxamd_launch', path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--batch', type=int, default=32, help='per-GPU batch')
@@ -40,7 +51,11 @@ def main():
     ap.add_argument('--size', type=int, default=512)
     ap.add_argument('--classes', type=int, default=20)
     ap.add_argument('--dtype', default='float16', choices=['float16', 'bfloat16', 'float32'])
+    ap.add_argument('--gpus', type=int, default=1, help='worker processes (one per GPU)')
     args = ap.parse_args()
+    launch = _load_launcher()
+    if launch.needs_launch(args.gpus):
+        sys.exit(launch.relaunch_self(args.gpus))
 
     import torch
     import mxnet_maintenance_amd as mx
