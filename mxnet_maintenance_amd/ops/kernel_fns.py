@@ -65,6 +65,15 @@ def _leaf_grad(t, numel=None, dtype=torch.float32):
 
 
 _RELU_FROM_X = [True]    # BN+ReLU backward recomputes the mask from x (debug switch)
+_ZEROS = {}
+
+
+def _zeros_f32(n, dev):
+    """A cached all-zero fp32 vector (statistics centre for conv-epilogue BN partials)."""
+    z = _ZEROS.get((n, dev))
+    if z is None:
+        z = _ZEROS[(n, dev)] = torch.zeros(n, dtype=torch.float32, device=dev)
+    return z
 
 
 class BatchNormNHWC(torch.autograd.Function):
@@ -83,9 +92,17 @@ class BatchNormNHWC(torch.autograd.Function):
         if addend is not None:
             assert addend.shape == x.shape and addend.dtype == x.dtype
             addend = addend.contiguous()
+        ext_nblk = 0
+        center = mm
         if training:
-            nblk = lib.bn_partials_rows(R, C)
-            part = torch.empty(2 * nblk * C, dtype=torch.float32, device=dev)
+            ext = getattr(x, '_mxamd_bn_part', None)
+            if ext is not None and ext[0].numel() == 2 * C * ext[1] and ext[0].device == dev:
+                # per-channel sum / sum-of-squares partials written by the producing conv's epilogue
+                part, ext_nblk = ext
+                center = _zeros_f32(C, dev)
+            else:
+                nblk = lib.bn_partials_rows(R, C)
+                part = torch.empty(2 * nblk * C, dtype=torch.float32, device=dev)
             stats = torch.empty(5, C, dtype=torch.float32, device=dev)
             mean, invstd, var, scale, shift = stats.unbind(0)
         else:
@@ -105,10 +122,10 @@ class BatchNormNHWC(torch.autograd.Function):
                 if (addend is not None and relu and _RELU_FROM_X[0]) else None)
         lib.bn_nhwc_forward(_DT[x.dtype], x.data_ptr(), _p(addend), y.data_ptr(), _p(mask), g.data_ptr(),
                             b.data_ptr(),
-                            mm.data_ptr(), _p(part), mean.data_ptr(), invstd.data_ptr(), var.data_ptr(),
+                            center.data_ptr(), _p(part), mean.data_ptr(), invstd.data_ptr(), var.data_ptr(),
                             scale.data_ptr(), shift.data_ptr(), R, C, float(eps), int(bool(training)),
                             int(bool(relu)), 0, float(momentum or 0.0), moving_mean.data_ptr() if upd else 0,
-                            moving_var.data_ptr() if upd else 0, _stream())
+                            moving_var.data_ptr() if upd else 0, int(ext_nblk), _stream())
         if training and momentum is not None and not upd:
             with torch.no_grad():
                 moving_mean.mul_(momentum).add_(mean.to(moving_mean.dtype), alpha=1 - momentum)
@@ -261,11 +278,19 @@ def conv_ok_shape(x, w, stride, pad, dilate=(1, 1), groups=1):
             and w.data_ptr() % 16 == 0)
 
 
-def conv_fwd(x, w, stride, pad, bias=None, variant=0):
+# 512-thread big-tile LDS-DMA kernel (conv_big.hip): variant -> (BCO, BPIX)
+_BIG_VARIANTS = {10: (256, 256), 11: (128, 256), 12: (64, 512), 13: (256, 128)}
+
+
+def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=None):
     """y[N,Ho,Wo,K] = conv(x[N,H,W,C], w[K,R,S,C]) on the MFMA implicit-GEMM kernel.
 
     ``variant``: 0 = heuristic tile, 1..4 = (BCO, BK) in (128,64) (128,32) (64,64) (64,32),
-    5 / 6 = LDS-DMA pipelined kernel with a 128x128 / 64x256 tile (Cin % 64 == 0)."""
+    5 / 6 = LDS-DMA pipelined kernel with a 128x128 / 64x256 tile (Cin % 64 == 0),
+    10..13 = 512-thread LDS-DMA kernel with 256x256 / 128x256 / 64x512 / 256x128 tiles and a
+    row-contiguous epilogue.  ``bn_stats`` (big kernel only): also emit per-channel BatchNorm
+    sum / sum-of-squares partials of y, attached to y as ``y._mxamd_bn_part``; ``addend`` (big kernel
+    only, same shape/dtype as y): y = conv + addend."""
     N, H, W, C = x.shape
     K, R, S, _ = w.shape
     Ho = (H + 2 * pad[0] - R) // stride[0] + 1
@@ -274,6 +299,23 @@ def conv_fwd(x, w, stride, pad, bias=None, variant=0):
     if N * Ho * Wo * K >= 2 ** 31:
         raise ValueError('conv_fwd: output too large for 32-bit indexing')
     b = _f32(bias) if bias is not None else None
+    if addend is not None:
+        assert variant in _BIG_VARIANTS and addend.shape == y.shape and addend.dtype == y.dtype
+        addend = addend.contiguous()
+    if variant in _BIG_VARIANTS:
+        lib = _K.lib()
+        v = variant - 10
+        part, nparts = None, 0
+        if bn_stats:
+            nparts = lib.conv_nhwc_fwd_big_nparts(N, H, W, R, S, stride[0], stride[1], pad[0], pad[1], v)
+            part = torch.empty(2 * K * nparts, dtype=torch.float32, device=x.device)
+        lib.conv_nhwc_fwd_big(_DT[x.dtype], x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(),
+                              _zero_page(x.device).data_ptr(), N, H, W, C, K, R, S, stride[0], stride[1],
+                              pad[0], pad[1], v, _p(part), nparts, _p(addend), _stream())
+        if part is not None:
+            # consumed by a following BatchNormNHWC (training): its statistics pass over y is skipped
+            y._mxamd_bn_part = (part, nparts)
+        return y
     if variant in (5, 6):
         _K.lib().conv_nhwc_fwd_glds(_DT[x.dtype], x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(),
                                     _zero_page(x.device).data_ptr(), N, H, W, C, K, R, S, stride[0], stride[1],
@@ -299,8 +341,11 @@ def _fwd_variants(C, K):
     """Tile variants of conv_fwd valid for Cin=C, Cout=K.
 
     1..4: register-staged kernel (conv_igemm.hip) with (BCO, BK) = (128,64) (128,32) (64,64) (64,32);
-    5, 6: LDS-DMA kernel (conv_glds.hip) with 128x128 / 64x256 tiles."""
+    5, 6: LDS-DMA kernel (conv_glds.hip) with 128x128 / 64x256 tiles;
+    10..13: 512-thread LDS-DMA kernel (conv_big.hip), see _BIG_VARIANTS."""
     v = []
+    if C % 64 == 0:
+        v.extend(b for b, (bco, _bpix) in sorted(_BIG_VARIANTS.items()) if K % bco == 0)
     if C % 64 == 0 and K % 128 == 0:
         v.append(5)
     if C % 64 == 0:
@@ -380,9 +425,43 @@ _ALGO = {}
 _TIMES = {}   # key -> {candidate: ms per call} from the autotuning run
 
 
-def _time_candidates(cands, reps=3, key=None):
-    best, best_t, out = None, None, None
+_REJECTED = {}   # key -> {candidate: relative error} of candidates that failed the numerics check
+
+
+def _rel_err(a, b):
+    a = a.float()
+    b = b.float()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-6))
+
+
+def _time_candidates(cands, reps=3, key=None, tol=2e-2):
+    """Time each candidate and return (fastest name, its output).
+
+    Before timing, every in-tree candidate's output is compared with the vendor
+    library's ('mm' / 'miopen', when present) on the live inputs; a candidate
+    whose relative max error exceeds ``tol`` is rejected (recorded in
+    ``_REJECTED``) so a wrong-but-fast kernel variant can never be selected.
+    """
+    ref = None
+    ref_name = next((n for n, _ in cands if n in ('mm', 'miopen')), None)
+    if ref_name is not None:
+        ref = dict(cands)[ref_name]()
+        if isinstance(ref, torch.Tensor):
+            ref = ref.detach().clone()
+        else:
+            ref = None
+    ok = []
     for name, fn in cands:
+        if ref is not None and name != ref_name:
+            r = fn()
+            if isinstance(r, torch.Tensor) and r.shape == ref.shape:
+                err = _rel_err(r, ref)
+                if not err <= tol:      # also rejects NaN
+                    _REJECTED.setdefault(key, {})[name] = err
+                    continue
+        ok.append((name, fn))
+    best, best_t, out = None, None, None
+    for name, fn in ok:
         fn()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
@@ -416,8 +495,9 @@ def _fwd_candidates(x, w, stride, pad, bias):
     K, R, S, C = w.shape
     if conv_ok_shape(x, w, stride, pad):
         c.append(('hip', lambda: conv_fwd(x, w, stride, pad, bias)))
+        stats = bool(_state.STATE.training)
         for v in _fwd_variants(C, K):
-            c.append(('hip%d' % v, lambda v=v: conv_fwd(x, w, stride, pad, bias, v)))
+            c.append(('hip%d' % v, lambda v=v: conv_fwd(x, w, stride, pad, bias, v, bn_stats=stats)))
     if R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0):
         def mm():
             y = torch.mm(x.reshape(-1, C), w.reshape(K, C).t())
@@ -607,19 +687,49 @@ class ConvTeeNHWC(torch.autograd.Function):
             return gpass, None, None
         gy = gy.contiguous()
         if ctx.needs_input_grad[0]:
-            g2 = gy.reshape(-1, K)
-            w2 = w.reshape(K, C)
-            if gpass is not None and ctx.inplace_grad and gpass.is_contiguous():
-                # the shortcut's gradient buffer is private to this edge (the fused residual tail
-                # returns a fresh d_addend): accumulate the GEMM into it, beta = 1, no copy
-                dx = gpass.view(-1, C).addmm_(g2, w2).view(x.shape)
-            elif gpass is not None:
-                dx = torch.addmm(gpass.contiguous().reshape(-1, C), g2, w2).view(x.shape)
-            else:
-                dx = torch.mm(g2, w2).view(x.shape)
+            dx = _tee_dgrad(gy, x, w, gpass, ctx.inplace_grad)
         if ctx.needs_input_grad[1]:
             dw = _wgrad(gy, x, w, ctx.w_ref, (1, 1), (0, 0))
         return dx, dw, None
+
+
+def _tee_dgrad(gy, x, w, gpass, inplace):
+    """dX = dY . W (+ dShortcut) of a 1x1 stride-1 conv: the in-tree big-tile MFMA kernel with the
+    shortcut gradient read in its epilogue (beta = 1), or hipBLASLt addmm -- autotuned per shape."""
+    K, C = w.shape[0], w.shape[3]
+    g2 = gy.reshape(-1, K)
+    w2 = w.reshape(K, C)
+
+    def mm():
+        if gpass is not None and inplace and gpass.is_contiguous():
+            # the shortcut's gradient buffer is private to this edge (the fused residual tail
+            # returns a fresh d_addend): accumulate the GEMM into it, beta = 1, no copy
+            return gpass.view(-1, C).addmm_(g2, w2).view(x.shape)
+        if gpass is not None:
+            return torch.addmm(gpass.contiguous().reshape(-1, C), g2, w2).view(x.shape)
+        return torch.mm(g2, w2).view(x.shape)
+
+    cands = []
+    if _CONV_HIP and K % 64 == 0 and gy.dtype in (torch.float16, torch.bfloat16) and gy.numel() < 2 ** 31:
+        wt = None
+        for v, (bco, _bpix) in sorted(_BIG_VARIANTS.items()):
+            if C % bco:
+                continue
+            if wt is None:
+                wt = w2.t().contiguous().view(C, 1, 1, K)
+
+            def big(v=v, wt=wt):
+                add = gpass.contiguous() if gpass is not None else None
+                return conv_fwd(gy, wt, (1, 1), (0, 0), None, v, addend=add)
+            cands.append(('hip%d' % v, big))
+    # autotuning runs every candidate: use an out-of-place GEMM there (the in-place one would
+    # accumulate into gpass once per timing repetition)
+    cands.append(('mm', lambda: mm() if not (gpass is not None and inplace) else
+                  torch.addmm(gpass.reshape(-1, C), g2, w2).view(x.shape)))
+    key = ('teedgrad', tuple(x.shape), tuple(w.shape), x.dtype)
+    if _ALGO.get(key) == 'mm':
+        return mm()
+    return _select(key, cands, 'mm')
 
 
 def conv_tee_ok(x, w):

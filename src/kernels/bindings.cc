@@ -18,7 +18,7 @@ void bn_nhwc_forward(int dtype, const void* x, const void* addend, void* y, uint
                      const float* beta,
                      const float* center, float* part, float* mean, float* invstd, float* var, float* scale,
                      float* shift, int64_t R, int C, float eps, int training, int relu, int fix_gamma,
-                     float momentum, float* mm_upd, float* mv_upd, hipStream_t s);
+                     float momentum, float* mm_upd, float* mv_upd, int ext_nblk, hipStream_t s);
 void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, const uint8_t* mask, void* dx,
                       void* dz,
                       const float* gamma, const float* mean, const float* invstd, const float* fscale,
@@ -35,6 +35,10 @@ void flat_sgd(int dtype, void* w, const void* g, float* mom, float* w32, int64_t
               float momentum, float rescale, float clip, hipStream_t s);
 void conv_nhwc_fwd(int dtype, const void* x, const void* w, const float* bias, void* y, int N, int H, int W, int C,
                    int K, int R, int S, int sh, int sw, int ph, int pw, int variant, hipStream_t s);
+int conv_nhwc_fwd_big_nparts(int N, int H, int W, int R, int S, int sh, int sw, int ph, int pw, int variant);
+void conv_nhwc_fwd_big(int dtype, const void* x, const void* w, const float* bias, void* y, const void* zero, int N,
+                       int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int variant,
+                       float* part, int nparts, const void* addend, hipStream_t s);
 void conv_nhwc_fwd_glds(int dtype, const void* x, const void* w, const float* bias, void* y, const void* zero, int N,
                         int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int bco,
                         hipStream_t s);
@@ -125,10 +129,11 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("bn_nhwc_forward", [](int dt, uintptr_t x, uintptr_t add, uintptr_t y, uintptr_t mask, uintptr_t g, uintptr_t b,
                               uintptr_t center, uintptr_t part, uintptr_t mean, uintptr_t inv, uintptr_t var,
                               uintptr_t scale, uintptr_t shift, int64_t R, int C, float eps, int training, int relu,
-                              int fix_gamma, float momentum, uintptr_t mm_upd, uintptr_t mv_upd, uintptr_t s) {
+                              int fix_gamma, float momentum, uintptr_t mm_upd, uintptr_t mv_upd, int ext_nblk,
+                              uintptr_t s) {
     bn_nhwc_forward(dt, P<void>(x), P<void>(add), P<void>(y), P<uint8_t>(mask), P<float>(g), P<float>(b), P<float>(center),
                     P<float>(part), P<float>(mean), P<float>(inv), P<float>(var), P<float>(scale), P<float>(shift), R,
-                    C, eps, training, relu, fix_gamma, momentum, P<float>(mm_upd), P<float>(mv_upd), S(s));
+                    C, eps, training, relu, fix_gamma, momentum, P<float>(mm_upd), P<float>(mv_upd), ext_nblk, S(s));
     check_launch("bn_nhwc_forward");
   });
   // relu_mode: 0 none, 1 mask from y, 2 mask recomputed from x*fscale+fshift, 3 from the forward's bitmask;
@@ -180,6 +185,16 @@ PYBIND11_MODULE(_hip_kernels, m) {
     conv_nhwc_fwd_glds(dt, P<void>(x), P<void>(w), P<float>(bias), P<void>(y), P<void>(zero), N, H, W, C, K, R, Sf,
                        sh, sw, ph, pw, bco, S(s));
     check_launch("conv_nhwc_fwd_glds");
+  });
+  // 512-thread big-tile kernel: variant 0..3 = 256x256, 128x256, 64x512, 256x128 (co x pix);
+  // part (optional): channel-major [2][K][nparts] BatchNorm sum / sum-of-squares partials of y
+  m.def("conv_nhwc_fwd_big_nparts", &conv_nhwc_fwd_big_nparts);
+  m.def("conv_nhwc_fwd_big", [](int dt, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, uintptr_t zero, int N,
+                                int H, int W, int C, int K, int R, int Sf, int sh, int sw, int ph, int pw, int variant,
+                                uintptr_t part, int nparts, uintptr_t addend, uintptr_t s) {
+    conv_nhwc_fwd_big(dt, P<void>(x), P<void>(w), P<float>(bias), P<void>(y), P<void>(zero), N, H, W, C, K, R, Sf, sh,
+                      sw, ph, pw, variant, P<float>(part), nparts, P<void>(addend), S(s));
+    check_launch("conv_nhwc_fwd_big");
   });
   m.def("conv_nhwc_wgrad_workspace", &conv_nhwc_wgrad_workspace);
   // zero: 0 -> register-staged kernel, else a >=128-byte zero page -> LDS-DMA kernel

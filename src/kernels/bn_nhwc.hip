@@ -337,19 +337,27 @@ template <typename T>
 static void bn_forward_impl(const void* x, const void* addend, void* y, uint8_t* mask, const float* gamma,
                             const float* beta, const float* center, float* part, float* mean, float* invstd,
                             float* var, float* scale, float* shift, int64_t R, int C, float eps, int training,
-                            int relu, int fix_gamma, float momentum, float* mm_upd, float* mv_upd, hipStream_t s) {
+                            int relu, int fix_gamma, float momentum, float* mm_upd, float* mv_upd, int ext_nblk,
+                            hipStream_t s) {
   MXAMD_HOST_CHECK(C % 8 == 0, "bn_nhwc: channels must be a multiple of 8");
   BnGeom g = bn_geom(C);
   MXAMD_HOST_CHECK(C % g.cb == 0, "bn_nhwc: unsupported channel count");
   if (training) {
     int nblk;
-    int64_t rpb = bn_rows_per_block(R, C, g, &nblk);
-    dim3 grid(nblk, C / g.cb);
     float* p1 = part;
+    if (ext_nblk > 0) {
+      // statistics partials already produced by the convolution epilogue (conv_big.hip):
+      // channel-major sum(x) / sum(x^2), center must be zero
+      nblk = ext_nblk;
+    } else {
+      int64_t rpb = bn_rows_per_block(R, C, g, &nblk);
+      dim3 grid(nblk, C / g.cb);
+      float* p2r = part + static_cast<int64_t>(nblk) * C;
+      hipLaunchKernelGGL((bn_reduce_kernel<T, 0, kReluNone>), grid, dim3(kBnThreads), 0, s,
+                         static_cast<const T*>(x), nullptr, nullptr, nullptr, center, nullptr, nullptr, p1, p2r, R, C,
+                         g.tpr, g.rpi, rpb);
+    }
     float* p2 = part + static_cast<int64_t>(nblk) * C;
-    hipLaunchKernelGGL((bn_reduce_kernel<T, 0, kReluNone>), grid, dim3(kBnThreads), 0, s,
-                       static_cast<const T*>(x), nullptr, nullptr, nullptr, center, nullptr, nullptr, p1, p2, R, C, g.tpr,
-                       g.rpi, rpb);
     hipLaunchKernelGGL((bn_finalize_kernel<0>), dim3(C), dim3(kFinThreads), 0, s, p1, p2, nblk, C, R, center, gamma,
                        beta, nullptr, eps, mean, invstd, var, scale, shift, nullptr, fix_gamma, 1, momentum, mm_upd,
                        mv_upd, 0);
@@ -432,19 +440,19 @@ void bn_nhwc_forward(int dtype, const void* x, const void* addend, void* y, uint
                      const float* beta,
                      const float* center, float* part, float* mean, float* invstd, float* var, float* scale,
                      float* shift, int64_t R, int C, float eps, int training, int relu, int fix_gamma,
-                     float momentum, float* mm_upd, float* mv_upd, hipStream_t s) {
+                     float momentum, float* mm_upd, float* mv_upd, int ext_nblk, hipStream_t s) {
   switch (dtype) {
     case kF16:
       bn_forward_impl<__half>(x, addend, y, mask, gamma, beta, center, part, mean, invstd, var, scale, shift, R, C, eps,
-                              training, relu, fix_gamma, momentum, mm_upd, mv_upd, s);
+                              training, relu, fix_gamma, momentum, mm_upd, mv_upd, ext_nblk, s);
       break;
     case kBF16:
       bn_forward_impl<__hip_bfloat16>(x, addend, y, mask, gamma, beta, center, part, mean, invstd, var, scale, shift, R,
-                                      C, eps, training, relu, fix_gamma, momentum, mm_upd, mv_upd, s);
+                                      C, eps, training, relu, fix_gamma, momentum, mm_upd, mv_upd, ext_nblk, s);
       break;
     default:
       bn_forward_impl<float>(x, addend, y, mask, gamma, beta, center, part, mean, invstd, var, scale, shift, R, C, eps,
-                             training, relu, fix_gamma, momentum, mm_upd, mv_upd, s);
+                             training, relu, fix_gamma, momentum, mm_upd, mv_upd, ext_nblk, s);
   }
 }
 

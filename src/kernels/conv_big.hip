@@ -1,0 +1,367 @@
+// NHWC implicit-GEMM convolution with 512-thread, up to 256x256 output tiles
+// and an LDS-staged epilogue (gfx950).
+//
+// Why another forward kernel: the 128x128 LDS-DMA kernel (conv_glds.hip)
+// moves (128+128) x 128 B of operands through L2 per 2 MFLOP of K-tile, i.e.
+// it needs ~34 TB/s of L2 bandwidth to keep the matrix cores busy -- the
+// whole per-XCD L2 budget -- so it tops out near 700 TF/s.  A 256x256 tile
+// halves operand traffic per FLOP.  Eight waves (2 per SIMD) each own a
+// 64(co) x FJ*16(pix) sub-tile of v_mfma_f32_16x16x32 accumulators.
+//
+//   * operands: global -> LDS by global_load_lds_dwordx4 (LDS-DMA), 128-byte
+//     rows (BK = 64 halves), XOR-swizzled 16-byte chunks (chunk ^ (row & 7)),
+//     halo / out-of-range pixels fetched from a zero page, 2 stages;
+//   * epilogue: the fp32 accumulators (+bias) are rounded and written to LDS as
+//     a [pix][co] image (row pitch BCO*2+16 B: conflict-free ds_write_b64), then
+//     re-read as 16-byte chunks and stored as whole contiguous pixel rows
+//     (BCO*2 bytes per pixel), instead of 16 scattered 32-byte pieces per
+//     store instruction;
+//   * optional BatchNorm statistics: when `part` is given, each wave writes
+//     per-channel partial sum(y) and sum(y^2) over its pixels (channel-major
+//     [K][nparts]), which the BN finalize kernel consumes directly -- the
+//     separate BN statistics pass over y (a full HBM read) disappears;
+//   * optional addend (beta = 1): y = conv(x) + addend, read in the row-store
+//     loop (used to fold a residual gradient into a 1x1 dgrad).
+//
+// Requirements (host-checked): Cin % 64 == 0, Cout % BCO == 0, dilation 1.
+#include <stdexcept>
+
+#include "common.h"
+
+namespace mxamd {
+
+namespace {
+
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void gbl_void;
+
+template <typename T>
+struct MfmaB;
+template <>
+struct MfmaB<__half> {
+  static __device__ __forceinline__ f4_t run(const u32x4& a, const u32x4& b, f4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8_t, a), __builtin_bit_cast(half8_t, b), c,
+                                                  0, 0, 0);
+  }
+  static __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
+    __half2 lo = __floats2half2_rn(a, b), hi = __floats2half2_rn(c, d);
+    uint2 r;
+    r.x = *reinterpret_cast<uint32_t*>(&lo);
+    r.y = *reinterpret_cast<uint32_t*>(&hi);
+    return r;
+  }
+};
+template <>
+struct MfmaB<__hip_bfloat16> {
+  static __device__ __forceinline__ f4_t run(const u32x4& a, const u32x4& b, f4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                   c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
+    // plain conversions (v_cvt_pk_bf16_f32): round-to-nearest-even, NaN stays NaN
+    __hip_bfloat16 h0 = __float2bfloat16(a), h1 = __float2bfloat16(b), h2 = __float2bfloat16(c),
+                   h3 = __float2bfloat16(d);
+    uint2 r;
+    r.x = static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h0)) |
+          (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h1)) << 16);
+    r.y = static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h2)) |
+          (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h3)) << 16);
+    return r;
+  }
+};
+
+struct GeomB {
+  int N, H, W, C, K, R, S;
+  int Ho, Wo;
+  int sh, sw, ph, pw;
+  int M;     // N*Ho*Wo
+  int Ktot;  // R*S*C
+};
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)lds_base, 16, 0, 0);
+}
+
+// sum over the 16 lanes of a row group (lanes sharing lane >> 4)
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  return v;
+}
+
+template <int BCO, int BPIX>
+struct BigCfg {
+  static constexpr int STAGE = (BCO + BPIX) * 128;
+  static constexpr int PITCH = BCO * 2 + 16;
+  static constexpr int EPI = BPIX * PITCH;
+  static constexpr int SMEM = (2 * STAGE > EPI ? 2 * STAGE : EPI);
+};
+
+// BCO = WCO * 64 output channels, BPIX = (8 / WCO) * FJ * 16 pixels per block
+template <typename T, int WCO, int FJ>
+__global__ void __launch_bounds__(512) conv_fwd_big_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                           const float* __restrict__ bias, T* __restrict__ y,
+                                                           const T* __restrict__ zero, GeomB g, int tiles_co,
+                                                           float* __restrict__ part, int nparts,
+                                                           const T* __restrict__ addend) {
+  constexpr int WPIX = 8 / WCO;
+  constexpr int BCO = WCO * 64;
+  constexpr int BPIX = WPIX * FJ * 16;
+  constexpr int BK = 64;
+  constexpr int A_BYTES = BCO * 128;
+  constexpr int STAGE = BigCfg<BCO, BPIX>::STAGE;
+  constexpr int PITCH = BigCfg<BCO, BPIX>::PITCH;
+  constexpr int A_INS = BCO / 64;  // wave-instructions (8 rows each) per wave for A
+  constexpr int B_INS = BPIX / 64;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+
+  // XCD-aware bijective remap: consecutive tiles (same pixel tile, neighbouring co tiles) share an XCD's L2
+  const int nblk = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7;
+  const int q = nblk >> 3, rr = nblk & 7;
+  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
+  const int tco = wgid % tiles_co;
+  const int tpix = wgid / tiles_co;
+  const int co0 = tco * BCO;
+  const int pix0 = tpix * BPIX;
+
+  const int lrow = lane >> 3;
+  const int gch = (lane & 7) ^ lrow;
+
+  int a_off[A_INS];
+#pragma unroll
+  for (int i = 0; i < A_INS; ++i) a_off[i] = (co0 + (i * 8 + wid) * 8 + lrow) * g.Ktot + gch * 8;
+  int b_base[B_INS], b_hi[B_INS], b_wi[B_INS];
+#pragma unroll
+  for (int i = 0; i < B_INS; ++i) {
+    const int p = pix0 + (i * 8 + wid) * 8 + lrow;
+    if (p < g.M) {
+      const int n = p / (g.Ho * g.Wo);
+      const int rem = p - n * g.Ho * g.Wo;
+      const int ho = rem / g.Wo;
+      const int wo = rem - ho * g.Wo;
+      b_hi[i] = ho * g.sh - g.ph;
+      b_wi[i] = wo * g.sw - g.pw;
+      b_base[i] = ((n * g.H + b_hi[i]) * g.W + b_wi[i]) * g.C + gch * 8;
+    } else {
+      b_hi[i] = -(1 << 20);  // never in range -> zero page
+      b_wi[i] = 0;
+      b_base[i] = 0;
+    }
+  }
+  const T* zsrc = zero + gch * 8;
+
+  const int KT = g.Ktot / BK;
+  auto issue = [&](int kt, int stage) {
+    const int k0 = kt * BK;
+    const int rs = k0 / g.C;
+    const int c0 = k0 - rs * g.C;
+    const int r = rs / g.S;
+    const int s = rs - r * g.S;
+    char* sbase = smem + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < A_INS; ++i) glds16(w + a_off[i] + k0, sbase + (i * 8 + wid) * 1024);
+    const int doff = (r * g.W + s) * g.C + c0;
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i) {
+      const int hi = b_hi[i] + r, wi = b_wi[i] + s;
+      const bool ok = (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+      const T* src = ok ? x + b_base[i] + doff : zsrc;
+      glds16(src, sbase + A_BYTES + (i * 8 + wid) * 1024);
+    }
+  };
+
+  f4_t acc[4][FJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int wco = wid % WCO;
+  const int wpix = wid / WCO;
+  const int frag_r = lane & 15;
+  const int fchunk = lane >> 4;
+  const int a_row0 = (wco * 64 + frag_r) * 128;
+  const int b_row0 = A_BYTES + (wpix * FJ * 16 + frag_r) * 128;
+  const int sw = frag_r & 7;
+
+  issue(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int stage = kt & 1;
+    if (kt + 1 < KT) issue(kt + 1, stage ^ 1);
+    const char* sb = smem + stage * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = ((kk * 4 + fchunk) ^ sw) * 16;
+      u32x4 af[4], bf[FJ];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u32x4*>(sb + a_row0 + i * 16 * 128 + ch);
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) bf[j] = *reinterpret_cast<const u32x4*>(sb + b_row0 + j * 16 * 128 + ch);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = MfmaB<T>::run(af[i], bf[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue. Lane holds co = wco*64 + i*16 + 4*(lane>>4) + {0..3} for pixel wpix*FJ*16 + j*16 + (lane&15)
+  const int co_l = (lane >> 4) * 4;
+  const int pw0 = wpix * FJ * 16;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int cl = wco * 64 + i * 16 + co_l;  // channel within the block tile
+    float b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
+    if (bias) {
+      b0 = bias[co0 + cl];
+      b1 = bias[co0 + cl + 1];
+      b2 = bias[co0 + cl + 2];
+      b3 = bias[co0 + cl + 3];
+    }
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, q0 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const int pl = pw0 + j * 16 + frag_r;
+      const float v0 = acc[i][j][0] + b0, v1 = acc[i][j][1] + b1, v2 = acc[i][j][2] + b2, v3 = acc[i][j][3] + b3;
+      *reinterpret_cast<uint2*>(smem + pl * PITCH + cl * 2) = MfmaB<T>::pack4(v0, v1, v2, v3);
+      if (part != nullptr && pix0 + pl < g.M) {
+        s0 += v0; s1 += v1; s2 += v2; s3 += v3;
+        q0 += v0 * v0; q1 += v1 * v1; q2 += v2 * v2; q3 += v3 * v3;
+      }
+    }
+    if (part != nullptr) {
+      s0 = row16_sum(s0); s1 = row16_sum(s1); s2 = row16_sum(s2); s3 = row16_sum(s3);
+      q0 = row16_sum(q0); q1 = row16_sum(q1); q2 = row16_sum(q2); q3 = row16_sum(q3);
+      if (frag_r == 0) {
+        const int pid = tpix * WPIX + wpix;
+        const int64_t c = co0 + cl;
+        float* p1 = part;
+        float* p2 = part + static_cast<int64_t>(g.K) * nparts;
+        p1[(c + 0) * nparts + pid] = s0;
+        p1[(c + 1) * nparts + pid] = s1;
+        p1[(c + 2) * nparts + pid] = s2;
+        p1[(c + 3) * nparts + pid] = s3;
+        p2[(c + 0) * nparts + pid] = q0;
+        p2[(c + 1) * nparts + pid] = q1;
+        p2[(c + 2) * nparts + pid] = q2;
+        p2[(c + 3) * nparts + pid] = q3;
+      }
+    }
+  }
+  __syncthreads();
+  // whole pixel rows: BCO*2 bytes = BCO/8 16-byte chunks per pixel
+  constexpr int CPR = BCO / 8;
+  constexpr int TOTAL = BPIX * CPR;
+#pragma unroll 4
+  for (int e = tid; e < TOTAL; e += 512) {
+    const int pl = e / CPR;
+    const int c8 = e - pl * CPR;
+    const int p = pix0 + pl;
+    if (p < g.M) {
+      const int64_t off = (int64_t)p * g.K + co0 + c8 * 8;
+      Vec8<T> v;
+      v.raw = *reinterpret_cast<const uint4*>(smem + pl * PITCH + c8 * 16);
+      if (addend != nullptr) {
+        // y = conv + addend (beta = 1): e.g. the identity shortcut's gradient folded into a 1x1 dgrad
+        Vec8<T> a;
+        a.load(addend + off);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v.set(t, v.get(t) + a.get(t));
+      }
+      v.store(y + off);
+    }
+  }
+}
+
+template <typename T, int WCO, int FJ>
+void launch_big(const void* x, const void* w, const float* bias, void* y, const void* zero, const GeomB& g,
+                float* part, int nparts, const void* addend, hipStream_t s) {
+  constexpr int BCO = WCO * 64;
+  constexpr int BPIX = (8 / WCO) * FJ * 16;
+  constexpr int SMEM = BigCfg<BCO, BPIX>::SMEM;
+  static_assert(SMEM <= 160 * 1024, "conv_big: LDS budget");
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_fwd_big_kernel<T, WCO, FJ>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    attr_set = true;
+  }
+  const int tiles_co = g.K / BCO;
+  const int tiles_pix = (g.M + BPIX - 1) / BPIX;
+  hipLaunchKernelGGL((conv_fwd_big_kernel<T, WCO, FJ>), dim3(tiles_co * tiles_pix), dim3(512), SMEM, s,
+                     static_cast<const T*>(x), static_cast<const T*>(w), bias, static_cast<T*>(y),
+                     static_cast<const T*>(zero), g, tiles_co, part, nparts, static_cast<const T*>(addend));
+}
+
+// variant -> (WCO, FJ): tile BCO x BPIX
+//   0: 256 x 256   1: 128 x 256   2: 64 x 512   3: 256 x 128
+static void big_tile(int variant, int* bco, int* bpix) {
+  switch (variant) {
+    case 0: *bco = 256; *bpix = 256; break;
+    case 1: *bco = 128; *bpix = 256; break;
+    case 2: *bco = 64; *bpix = 512; break;
+    case 3: *bco = 256; *bpix = 128; break;
+    default: throw std::runtime_error("conv_nhwc_fwd_big: unknown variant");
+  }
+}
+
+template <typename T>
+void dispatch_big(int variant, const void* x, const void* w, const float* bias, void* y, const void* zero,
+                  const GeomB& g, float* part, int nparts, const void* addend, hipStream_t s) {
+  switch (variant) {
+    case 0: launch_big<T, 4, 8>(x, w, bias, y, zero, g, part, nparts, addend, s); break;
+    case 1: launch_big<T, 2, 4>(x, w, bias, y, zero, g, part, nparts, addend, s); break;
+    case 2: launch_big<T, 1, 4>(x, w, bias, y, zero, g, part, nparts, addend, s); break;
+    case 3: launch_big<T, 4, 4>(x, w, bias, y, zero, g, part, nparts, addend, s); break;
+  }
+}
+
+}  // namespace
+
+// Number of BN-statistics partials per channel the big kernel writes for this conv/variant.
+int conv_nhwc_fwd_big_nparts(int N, int H, int W, int R, int S, int sh, int sw, int ph, int pw, int variant) {
+  int bco, bpix;
+  big_tile(variant, &bco, &bpix);
+  const int Ho = (H + 2 * ph - R) / sh + 1;
+  const int Wo = (W + 2 * pw - S) / sw + 1;
+  const int M = N * Ho * Wo;
+  return ((M + bpix - 1) / bpix) * (8 / (bco / 64));
+}
+
+void conv_nhwc_fwd_big(int dtype, const void* x, const void* w, const float* bias, void* y, const void* zero, int N,
+                       int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int variant,
+                       float* part, int nparts, const void* addend, hipStream_t s) {
+  GeomB g;
+  g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S;
+  g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw;
+  g.Ho = (H + 2 * ph - R) / sh + 1;
+  g.Wo = (W + 2 * pw - S) / sw + 1;
+  g.M = N * g.Ho * g.Wo;
+  g.Ktot = R * S * C;
+  int bco, bpix;
+  big_tile(variant, &bco, &bpix);
+  MXAMD_HOST_CHECK(C % 64 == 0 && K % bco == 0, "conv_nhwc_fwd_big: need Cin % 64 == 0 and Cout % BCO == 0");
+  MXAMD_HOST_CHECK((int64_t)N * H * W * C < (1ll << 31) && (int64_t)g.M * K < (1ll << 31) &&
+                       (int64_t)K * g.Ktot < (1ll << 31),
+                   "conv_nhwc_fwd_big: tensor too large for 32-bit indexing");
+  MXAMD_HOST_CHECK(part == nullptr || nparts == conv_nhwc_fwd_big_nparts(N, H, W, R, S, sh, sw, ph, pw, variant),
+                   "conv_nhwc_fwd_big: wrong BN partials count");
+  if (dtype == kF16) dispatch_big<__half>(variant, x, w, bias, y, zero, g, part, nparts, addend, s);
+  else if (dtype == kBF16) dispatch_big<__hip_bfloat16>(variant, x, w, bias, y, zero, g, part, nparts, addend, s);
+  else throw std::runtime_error("conv_nhwc_fwd_big: dtype must be f16 or bf16");
+}
+
+}  // namespace mxamd

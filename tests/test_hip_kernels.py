@@ -631,3 +631,57 @@ def test_twobit_compression_kernels_match_reference(dtype, n):
     out = torch.empty(n, device='cuda')
     lib.twobit_dequantize_sum(two.data_ptr(), packed.numel(), 2, n, 0.5, out.data_ptr(), _stream())
     torch.testing.assert_close(out, 2 * dequantize_2bit(ref_packed, n, 0.5), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('cfg', [(3, 13, 128, 256, 3, 1), (2, 9, 64, 128, 1, 1), (4, 17, 64, 64, 3, 2)])
+def test_conv_big_bn_stats_addend(dtype, cfg):
+    """512-thread big-tile conv: BN sum/sum-sq partials from the epilogue, beta=1 addend, and a
+    BatchNorm consuming those partials matches torch batch statistics."""
+    from mxnet_maintenance_amd.ops import kernel_fns as KF
+    _lib()
+    N, H, Cin, Cout, k, s = cfg
+    pad = k // 2
+    torch.manual_seed(4)
+    x = torch.randn(N, H, H, Cin, device='cuda').to(dtype)
+    w = (torch.randn(Cout, k, k, Cin, device='cuda') / (k * k * Cin) ** 0.5).to(dtype)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, s, pad).permute(0, 2, 3, 1)
+    tol = 2e-2 if dtype == torch.float16 else 6e-2
+    variants = [v for v, (bco, _) in sorted(KF._BIG_VARIANTS.items()) if Cout % bco == 0]
+    assert variants
+    for v in variants:
+        y = KF.conv_fwd(x, w, (s, s), (pad, pad), None, v, bn_stats=True)
+        torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+        part, nparts = y._mxamd_bn_part
+        p = part.view(2, Cout, nparts)
+        torch.testing.assert_close(p[0].sum(1), ref.sum((0, 1, 2)), rtol=1e-2, atol=0.5)
+        torch.testing.assert_close(p[1].sum(1), (ref * ref).sum((0, 1, 2)), rtol=1e-2, atol=0.5)
+        add = torch.randn_like(y)
+        y2 = KF.conv_fwd(x, w, (s, s), (pad, pad), None, v, addend=add)
+        torch.testing.assert_close(y2.float(), ref + add.float(), rtol=tol, atol=2 * tol)
+        # BatchNorm(+ReLU) fed by the epilogue partials == torch batch-norm on the same y
+        g = torch.rand(Cout, device='cuda') + 0.5
+        b = torch.randn(Cout, device='cuda')
+        out, mean, var = KF.BatchNormNHWC.apply(y, g, b, None, 1e-5, True, True, torch.zeros(Cout, device='cuda'),
+                                                torch.ones(Cout, device='cuda'))
+        yf = y.float()
+        m_ref = yf.mean((0, 1, 2))
+        v_ref = yf.var((0, 1, 2), unbiased=False)
+        torch.testing.assert_close(mean, m_ref, rtol=1e-3, atol=2e-3)
+        torch.testing.assert_close(var, v_ref, rtol=2e-3, atol=2e-3)
+        o_ref = torch.relu((yf - m_ref) / torch.sqrt(v_ref + 1e-5) * g + b)
+        torch.testing.assert_close(out.float(), o_ref, rtol=tol, atol=tol)
+
+
+def test_conv_autotune_rejects_wrong_candidate():
+    """The autotuner compares every candidate with the vendor result on the live inputs and never
+    selects one whose numerics are off, however fast it is."""
+    from mxnet_maintenance_amd.ops import kernel_fns as KF
+    _lib()
+    x = torch.randn(64, 32, device='cuda')
+    good = lambda: x * 2                      # noqa: E731
+    bad = lambda: x * 2 + 1                   # noqa: E731  (fast and wrong)
+    key = ('test-reject',)
+    name, out = KF._time_candidates([('bad', bad), ('miopen', good)], key=key)
+    assert name == 'miopen' and 'bad' in KF._REJECTED[key]
+    torch.testing.assert_close(out, x * 2)
