@@ -1,8 +1,12 @@
-"""Training callbacks (parity: python/mxnet/callback.py).
+"""Training-loop callbacks (API parity: python/mxnet/callback.py).
 
-Batch-end callbacks receive a ``BatchEndParam(epoch, nbatch, eval_metric,
-locals)``; epoch-end callbacks receive ``(epoch, symbol, arg_params,
-aux_params)``.
+Two callback shapes exist, as in the reference:
+
+* batch-end: ``cb(param)`` with ``param`` a ``BatchEndParam(epoch, nbatch,
+  eval_metric, locals)``;
+* epoch-end: ``cb(epoch, symbol, arg_params, aux_params)``.
+
+Periodic behaviour ("every N epochs / batches") is factored into ``_every``.
 """
 import logging
 import math
@@ -12,99 +16,117 @@ __all__ = ['module_checkpoint', 'do_checkpoint', 'log_train_metric', 'Speedomete
            'LogValidationMetricsCallback']
 
 
-def module_checkpoint(mod, prefix, period=1, save_optimizer_states=False):
-    """Epoch-end callback saving ``mod``'s checkpoint every ``period`` epochs."""
-    period = int(max(1, period))
+def _every(period):
+    """Predicate on a 0-based epoch index: true on epochs period-1, 2*period-1, ..."""
+    period = max(1, int(period))
+    return lambda idx: (idx + 1) % period == 0
 
-    def _callback(iter_no, sym=None, arg=None, aux=None):
-        if (iter_no + 1) % period == 0:
-            mod.save_checkpoint(prefix, iter_no + 1, save_optimizer_states)
-    return _callback
+
+def module_checkpoint(mod, prefix, period=1, save_optimizer_states=False):
+    """Epoch-end callback: ``mod.save_checkpoint(prefix, epoch+1)`` every ``period`` epochs."""
+    due = _every(period)
+
+    def on_epoch_end(epoch, sym=None, arg=None, aux=None):
+        if due(epoch):
+            mod.save_checkpoint(prefix, epoch + 1, save_optimizer_states)
+    return on_epoch_end
 
 
 def do_checkpoint(prefix, period=1):
-    """Epoch-end callback writing ``prefix-symbol.json`` and ``prefix-%04d.params``."""
-    from .model import save_checkpoint
-    period = int(max(1, period))
+    """Epoch-end callback: write ``prefix-symbol.json`` + ``prefix-%04d.params`` every ``period`` epochs."""
+    due = _every(period)
 
-    def _callback(iter_no, sym, arg, aux):
-        if (iter_no + 1) % period == 0:
-            save_checkpoint(prefix, iter_no + 1, sym, arg, aux)
-    return _callback
+    def on_epoch_end(epoch, sym, arg, aux):
+        if due(epoch):
+            from .model import save_checkpoint
+            save_checkpoint(prefix, epoch + 1, sym, arg, aux)
+    return on_epoch_end
+
+
+def _metric_pairs(metric):
+    return list(metric.get_name_value()) if metric is not None else []
 
 
 def log_train_metric(period, auto_reset=False):
-    """Batch-end callback logging the training metric every ``period`` batches."""
-    def _callback(param):
-        if param.nbatch % period == 0 and param.eval_metric is not None:
-            name_value = param.eval_metric.get_name_value()
-            for name, value in name_value:
-                logging.info('Iter[%d] Batch[%d] Train-%s=%f', param.epoch, param.nbatch, name, value)
-            if auto_reset:
-                param.eval_metric.reset_local()
-    return _callback
+    """Batch-end callback: log the training metric every ``period`` batches."""
+    def on_batch_end(param):
+        if param.nbatch % period or param.eval_metric is None:
+            return
+        for name, value in _metric_pairs(param.eval_metric):
+            logging.info('Iter[%d] Batch[%d] Train-%s=%f', param.epoch, param.nbatch, name, value)
+        if auto_reset:
+            param.eval_metric.reset_local()
+    return on_batch_end
 
 
 class Speedometer:
-    """Log throughput (samples/sec) and the training metric every ``frequent`` batches."""
+    """Batch-end callback: samples/sec (and the metric) over each window of ``frequent`` batches.
+
+    A window starts at the first batch seen (or when the batch counter goes
+    backwards, i.e. a new epoch); with ``auto_reset`` the metric's local state
+    is cleared after each report so it covers only that window.
+    """
 
     def __init__(self, batch_size, frequent=50, auto_reset=True):
         self.batch_size = batch_size
         self.frequent = frequent
-        self.init = False
-        self.tic = 0
-        self.last_count = 0
         self.auto_reset = auto_reset
+        self._t0 = None
+        self._last = -1
+
+    # reference attribute names, kept for code that inspects them
+    @property
+    def init(self):
+        return self._t0 is not None
+
+    @property
+    def tic(self):
+        return self._t0 or 0
+
+    @property
+    def last_count(self):
+        return max(self._last, 0)
 
     def __call__(self, param):
-        count = param.nbatch
-        if self.last_count > count:
-            self.init = False
-        self.last_count = count
-        if not self.init:
-            self.init = True
-            self.tic = time.time()
+        n = param.nbatch
+        if n < self._last:
+            self._t0 = None           # new epoch
+        self._last = n
+        if self._t0 is None:
+            self._t0 = time.time()
             return
-        if count % self.frequent != 0:
+        if n % self.frequent:
             return
-        try:
-            speed = self.frequent * self.batch_size / (time.time() - self.tic)
-        except ZeroDivisionError:
-            speed = float('inf')
-        if param.eval_metric is not None:
-            name_value = param.eval_metric.get_name_value()
+        elapsed = time.time() - self._t0
+        speed = self.frequent * self.batch_size / elapsed if elapsed > 0 else float('inf')
+        pairs = _metric_pairs(param.eval_metric)
+        if param.eval_metric is None:
+            logging.info('Iter[%d] Batch [%d]\tSpeed: %.2f samples/sec', param.epoch, n, speed)
+        else:
+            first = n - self.frequent if self.auto_reset else 0
+            text = ''.join('\t%s=%f' % kv for kv in pairs)
+            logging.info('Epoch[%d] Batch [%d-%d]\tSpeed: %.2f samples/sec%s', param.epoch, first, n, speed, text)
             if self.auto_reset:
                 param.eval_metric.reset_local()
-                msg = 'Epoch[%d] Batch [%d-%d]\tSpeed: %.2f samples/sec' + '\t%s=%f' * len(name_value)
-                logging.info(msg, param.epoch, count - self.frequent, count, speed, *sum(name_value, ()))
-            else:
-                msg = 'Epoch[%d] Batch [0-%d]\tSpeed: %.2f samples/sec' + '\t%s=%f' * len(name_value)
-                logging.info(msg, param.epoch, count, speed, *sum(name_value, ()))
-        else:
-            logging.info('Iter[%d] Batch [%d]\tSpeed: %.2f samples/sec', param.epoch, count, speed)
-        self.tic = time.time()
+        self._t0 = time.time()
 
 
 class ProgressBar:
-    """Log a text progress bar of the epoch's batches."""
+    """Batch-end callback drawing a text progress bar of ``total`` batches."""
 
     def __init__(self, total, length=80):
-        self.bar_len = length
         self.total = total
+        self.bar_len = length
 
     def __call__(self, param):
-        count = param.nbatch
-        filled_len = int(round(self.bar_len * count / float(self.total)))
-        percents = math.ceil(100.0 * count / float(self.total))
-        prog_bar = '=' * filled_len + '-' * (self.bar_len - filled_len)
-        logging.info('[%s] %s%s\r', prog_bar, percents, '%')
+        frac = param.nbatch / float(self.total)
+        done = int(round(self.bar_len * frac))
+        logging.info('[%s] %s%s\r', '=' * done + '-' * (self.bar_len - done), math.ceil(100.0 * frac), '%')
 
 
 class LogValidationMetricsCallback:
-    """Log the validation metric at the end of an epoch."""
+    """Epoch-end (validation) callback logging every metric value."""
 
     def __call__(self, param):
-        if not param.eval_metric:
-            return
-        for name, value in param.eval_metric.get_name_value():
+        for name, value in _metric_pairs(param.eval_metric or None):
             logging.info('Epoch[%d] Validation-%s=%f', param.epoch, name, value)

@@ -1,106 +1,126 @@
-"""Samplers (parity: python/mxnet/gluon/data/sampler.py)."""
+"""Index samplers for DataLoader (API parity: python/mxnet/gluon/data/sampler.py).
+
+Each sampler is an iterable of dataset indices with a known length.  Index
+sequences are produced as numpy arrays (``_indices``) and converted to Python
+ints on iteration; ``BatchSampler`` groups any sampler into lists.
+"""
 import numpy as np
 
 __all__ = ['Sampler', 'SequentialSampler', 'RandomSampler', 'FilterSampler', 'BatchSampler', 'IntervalSampler']
 
+_LAST_BATCH = ('keep', 'discard', 'rollover')
+
 
 class Sampler:
-    def __iter__(self):
+    """Base class: subclasses define ``_indices()`` (numpy int array) or override ``__iter__``."""
+
+    def _indices(self):
         raise NotImplementedError
+
+    def __iter__(self):
+        return iter(self._indices().tolist())
 
     def __len__(self):
         raise NotImplementedError
 
 
 class SequentialSampler(Sampler):
+    """``start, start+1, ..., start+length-1``."""
+
     def __init__(self, length, start=0):
         self._length = length
         self._start = start
 
-    def __iter__(self):
-        return iter(range(self._start, self._start + self._length))
+    def _indices(self):
+        return np.arange(self._start, self._start + self._length)
 
     def __len__(self):
         return self._length
 
 
 class RandomSampler(Sampler):
+    """A fresh random permutation of ``range(length)`` per epoch (numpy global RNG)."""
+
     def __init__(self, length):
         self._length = length
 
-    def __iter__(self):
-        indices = np.arange(self._length)
-        np.random.shuffle(indices)
-        return iter(indices.tolist())
+    def _indices(self):
+        return np.random.permutation(self._length)
 
     def __len__(self):
         return self._length
 
 
 class FilterSampler(Sampler):
+    """Indices of the samples of ``dataset`` for which ``fn(sample)`` holds (evaluated once)."""
+
     def __init__(self, fn, dataset):
         self._fn = fn
         self._dataset = dataset
-        self._indices = [i for i, sample in enumerate(dataset) if fn(sample)]
+        self._keep = np.array([i for i in range(len(dataset)) if fn(dataset[i])], dtype=np.int64)
 
-    def __iter__(self):
-        return iter(self._indices)
+    def _indices(self):
+        return self._keep
 
     def __len__(self):
-        return len(self._indices)
+        return len(self._keep)
 
 
 class IntervalSampler(Sampler):
-    """Samples ``i, i+interval, i+2*interval, ...`` for each offset ``i`` (rollover=True) or offset 0 only."""
+    """Strided passes: ``0, k, 2k, ...`` then (with ``rollover``) ``1, 1+k, ...`` up to offset k-1."""
 
     def __init__(self, length, interval, rollover=True):
-        assert interval < length, 'Interval {} must be smaller than length {}'.format(interval, length)
+        if not interval < length:
+            raise AssertionError('interval %d must be smaller than length %d' % (interval, length))
         self._length = length
         self._interval = interval
         self._rollover = rollover
 
-    def __iter__(self):
-        for i in range(self._interval if self._rollover else 1):
-            for j in range(i, self._length, self._interval):
-                yield j
+    def _indices(self):
+        offsets = range(self._interval) if self._rollover else range(1)
+        return np.concatenate([np.arange(o, self._length, self._interval) for o in offsets])
 
     def __len__(self):
         return self._length
 
 
 class BatchSampler(Sampler):
-    """Wrap a sampler into mini-batches; last_batch in {'keep', 'discard', 'rollover'}."""
+    """Group the indices of ``sampler`` into lists of ``batch_size``.
+
+    ``last_batch``: 'keep' yields a short final batch, 'discard' drops it,
+    'rollover' carries its indices into the first batch of the next epoch.
+    """
 
     def __init__(self, sampler, batch_size, last_batch='keep'):
         self._sampler = sampler
         self._batch_size = batch_size
         self._last_batch = last_batch
-        self._prev = []
+        self._carry = []
+
+    def _check_mode(self):
+        if self._last_batch not in _LAST_BATCH:
+            raise ValueError('last_batch must be one of %s, got %r' % (_LAST_BATCH, self._last_batch))
 
     def __iter__(self):
-        batch, self._prev = self._prev, []
-        for i in self._sampler:
-            batch.append(i)
-            if len(batch) == self._batch_size:
-                yield batch
-                batch = []
-        if batch:
-            if self._last_batch == 'keep':
-                yield batch
-            elif self._last_batch == 'discard':
-                return
-            elif self._last_batch == 'rollover':
-                self._prev = batch
-            else:
-                raise ValueError("last_batch must be one of 'keep', 'discard', or 'rollover', but got %s"
-                                 % self._last_batch)
+        self._check_mode()
+        pending, self._carry = list(self._carry), []
+        for idx in self._sampler:
+            pending.append(idx)
+            if len(pending) == self._batch_size:
+                yield pending
+                pending = []
+        if not pending:
+            return
+        if self._last_batch == 'keep':
+            yield pending
+        elif self._last_batch == 'rollover':
+            self._carry = pending
 
     def __len__(self):
+        self._check_mode()
+        n, b = len(self._sampler), self._batch_size
         if self._last_batch == 'keep':
-            return (len(self._sampler) + self._batch_size - 1) // self._batch_size
+            return -(-n // b)
         if self._last_batch == 'discard':
-            return len(self._sampler) // self._batch_size
-        if self._last_batch == 'rollover':
-            return (len(self._prev) + len(self._sampler)) // self._batch_size
-        raise ValueError("last_batch must be one of 'keep', 'discard', or 'rollover', but got %s"
-                         % self._last_batch)
+            return n // b
+        return (n + len(self._carry)) // b
