@@ -1,23 +1,27 @@
-"""BaseModule: the intermediate-level training interface (parity: python/mxnet/module/base_module.py).
+"""BaseModule: the intermediate-level (symbolic) training interface.
 
-Subclasses implement ``bind``, ``init_params``, ``init_optimizer``,
-``forward``, ``backward``, ``update``, ``get_outputs``, ``update_metric``;
-this class provides ``fit``, ``score``, ``predict``, ``iter_predict``,
-``forward_backward`` and parameter save/load on top of them.
+API parity: python/mxnet/module/base_module.py.  A concrete module provides the
+primitive operations (``bind``, ``init_params``, ``init_optimizer``,
+``forward``, ``backward``, ``update``, ``get_outputs``, ``update_metric``, ...);
+this base class builds the driver loops on top of them:
+
+* ``_walk`` -- the shared "iterate an eval iterator for at most N batches,
+  preparing and forwarding each" generator behind ``score``,
+  ``iter_predict`` and ``predict``;
+* ``fit`` -- bind / init / optimizer set-up, then ``_train_epoch`` per epoch
+  (which prefetches the next batch and calls ``prepare`` on it while the
+  current one is being consumed) and the epoch-end bookkeeping.
 """
 import logging
 import time
-from collections import namedtuple
 
 import numpy as np
 
 from .. import metric
 from .. import ndarray as nd
-from ..base import MXNetError
 from ..initializer import Uniform
+from ..model import BatchEndParam
 from ..ndarray.ndarray import NDArray
-
-BatchEndParam = namedtuple('BatchEndParams', ['epoch', 'nbatch', 'eval_metric', 'locals'])
 
 __all__ = ['BaseModule', 'BatchEndParam']
 
@@ -26,44 +30,74 @@ def _as_list(obj):
     return obj if isinstance(obj, list) else [obj]
 
 
+def _fire(callbacks, *args):
+    for cb in _as_list(callbacks) if callbacks is not None else ():
+        cb(*args)
+
+
+def _warn_or_raise(msg, throw):
+    if throw:
+        raise ValueError(msg)
+    logging.warning(msg)
+
+
+def _looks_like_param(name):
+    return name.endswith(('_weight', '_bias', '_gamma', '_beta'))
+
+
 def _check_input_names(symbol, names, typename, throw):
+    """Every declared input name must be an argument of ``symbol``; suggest the plausible ones."""
     args = symbol.list_arguments()
     for name in names:
-        if name in args:
-            continue
-        candidates = [arg for arg in args if not arg.endswith('_weight') and not arg.endswith('_bias')
-                      and not arg.endswith('_gamma') and not arg.endswith('_beta')]
-        msg = ('You created Module with Module(..., %s_names=%s) but input with name \'%s\' is not found in '
-               'symbol.list_arguments(). Did you mean one of:\n\t%s' % (typename, str(names), name,
-                                                                         '\n\t'.join(candidates)))
-        if throw:
-            raise ValueError(msg)
-        logging.warning(msg)
+        if name not in args:
+            hints = '\n\t'.join(a for a in args if not _looks_like_param(a))
+            _warn_or_raise("Module(..., %s_names=%s): input '%s' is not an argument of the symbol. "
+                           'Did you mean one of:\n\t%s' % (typename, list(names), name, hints), throw)
 
 
-def _check_names_match(data_names, data_shapes, name, throw):
-    actual = [x[0] for x in data_shapes]
-    if sorted(data_names) != sorted(actual):
-        msg = 'Data provided by %s_shapes don\'t match names specified by %s_names (%s vs. %s)' % (
-            name, name, str(data_shapes), str(data_names))
-        if throw:
-            raise ValueError(msg)
-        logging.warning(msg)
+def _check_names_match(expected, descs, kind, throw):
+    got = [d[0] for d in descs]
+    if sorted(expected) != sorted(got):
+        _warn_or_raise('%s_shapes %s do not match the declared %s_names %s' % (kind, descs, kind, list(expected)),
+                       throw)
+
+
+def _as_descs(shapes):
+    from ..io import DataDesc
+    return None if shapes is None else [s if isinstance(s, DataDesc) else DataDesc(*s) for s in shapes]
 
 
 def _parse_data_desc(data_names, label_names, data_shapes, label_shapes):
-    from ..io import DataDesc
-    data_shapes = [x if isinstance(x, DataDesc) else DataDesc(*x) for x in data_shapes]
+    """Normalise (name, shape) pairs to DataDesc and validate them against the declared names."""
+    data_shapes = _as_descs(data_shapes)
+    label_shapes = _as_descs(label_shapes)
     _check_names_match(data_names, data_shapes, 'data', True)
-    if label_shapes is not None:
-        label_shapes = [x if isinstance(x, DataDesc) else DataDesc(*x) for x in label_shapes]
-        _check_names_match(label_names, label_shapes, 'label', False)
-    else:
-        _check_names_match(label_names, [], 'label', False)
+    _check_names_match(label_names, label_shapes or [], 'label', False)
     return data_shapes, label_shapes
 
 
+def _batch_labels(batch):
+    """(labels, pre_sliced) of a batch, or of a list of per-device batches."""
+    if isinstance(batch, list):
+        return [b.label for b in batch], True
+    return batch.label, False
+
+
+class _SimpleBatch:
+    """Minimal DataBatch used by ``predict`` on a bare array."""
+
+    def __init__(self, data, label=None):
+        self.data = data
+        self.label = label
+        self.pad = 0
+        self.bucket_key = None
+        self.provide_data = None
+        self.provide_label = None
+
+
 class BaseModule:
+    """Abstract module; see the module docstring for the split of responsibilities."""
+
     def __init__(self, logger=logging):
         self.logger = logger
         self.binded = False
@@ -74,91 +108,79 @@ class BaseModule:
         self._symbol = None
         self._total_exec_bytes = 0
 
-    # ------------------------------------------------------------ high level
+    def _require(self, *flags):
+        for f in flags:
+            if not getattr(self, f):
+                raise AssertionError('%s: module is not %s' % (type(self).__name__, f.replace('_', ' ')))
+
+    # ---------------------------------------------------------------- evaluation loops
+    def _walk(self, data_iter, num_batch, reset, sparse_row_id_fn):
+        self._require('binded', 'params_initialized')
+        if reset:
+            data_iter.reset()
+        for nbatch, batch in enumerate(data_iter):
+            if num_batch is not None and nbatch >= num_batch:
+                return
+            self.prepare(batch, sparse_row_id_fn=sparse_row_id_fn)
+            self.forward(batch, is_train=False)
+            yield nbatch, batch
+
+    def _unpadded_outputs(self, batch, copy):
+        outs = self.get_outputs()
+        n = lambda o: o.shape[0] - batch.pad    # noqa: E731
+        return [o[0:n(o)].copy() if copy else o[0:n(o)] for o in outs]
+
     def forward_backward(self, data_batch):
         self.forward(data_batch, is_train=True)
         self.backward()
 
     def score(self, eval_data, eval_metric, num_batch=None, batch_end_callback=None, score_end_callback=None,
               reset=True, epoch=0, sparse_row_id_fn=None):
-        assert self.binded and self.params_initialized
-        if reset:
-            eval_data.reset()
+        """Run ``eval_data`` through the model and return ``eval_metric``'s (name, value) pairs."""
         if not isinstance(eval_metric, metric.EvalMetric):
             eval_metric = metric.create(eval_metric)
         eval_metric.reset()
-        actual_num_batch = 0
-        for nbatch, eval_batch in enumerate(eval_data):
-            if num_batch is not None and nbatch == num_batch:
-                break
-            self.prepare(eval_batch, sparse_row_id_fn=sparse_row_id_fn)
-            self.forward(eval_batch, is_train=False)
-            if isinstance(eval_batch, list):
-                self.update_metric(eval_metric, [eb.label for eb in eval_batch], pre_sliced=True)
-            else:
-                self.update_metric(eval_metric, eval_batch.label)
-            if batch_end_callback is not None:
-                params = BatchEndParam(epoch=epoch, nbatch=nbatch, eval_metric=eval_metric, locals=locals())
-                for callback in _as_list(batch_end_callback):
-                    callback(params)
-            actual_num_batch += 1
-        if score_end_callback:
-            params = BatchEndParam(epoch=epoch, nbatch=actual_num_batch, eval_metric=eval_metric, locals=locals())
-            for callback in _as_list(score_end_callback):
-                callback(params)
+        seen = 0
+        for nbatch, batch in self._walk(eval_data, num_batch, reset, sparse_row_id_fn):
+            labels, pre_sliced = _batch_labels(batch)
+            self.update_metric(eval_metric, labels, pre_sliced=pre_sliced)
+            _fire(batch_end_callback, BatchEndParam(epoch, nbatch, eval_metric, locals()))
+            seen += 1
+        _fire(score_end_callback, BatchEndParam(epoch, seen, eval_metric, locals()))
         return eval_metric.get_name_value()
 
     def iter_predict(self, eval_data, num_batch=None, reset=True, sparse_row_id_fn=None):
-        assert self.binded and self.params_initialized
-        if reset:
-            eval_data.reset()
-        for nbatch, eval_batch in enumerate(eval_data):
-            if num_batch is not None and nbatch == num_batch:
-                break
-            self.prepare(eval_batch, sparse_row_id_fn=sparse_row_id_fn)
-            self.forward(eval_batch, is_train=False)
-            pad = eval_batch.pad
-            outputs = [out[0:out.shape[0] - pad] for out in self.get_outputs()]
-            yield (outputs, nbatch, eval_batch)
+        """Yield ``(outputs, batch_index, batch)`` with padding rows removed."""
+        for nbatch, batch in self._walk(eval_data, num_batch, reset, sparse_row_id_fn):
+            yield self._unpadded_outputs(batch, copy=False), nbatch, batch
 
     def predict(self, eval_data, num_batch=None, merge_batches=True, reset=True, always_output_list=False,
                 sparse_row_id_fn=None):
-        assert self.binded and self.params_initialized
+        """Outputs for a data iterator (concatenated over batches), or for one array."""
+        self._require('binded', 'params_initialized')
         if isinstance(eval_data, (NDArray, np.ndarray)):
-            if isinstance(eval_data, np.ndarray):
-                eval_data = nd.array(eval_data)
-            self.forward(_SimpleBatch([eval_data]))
+            arr = eval_data if isinstance(eval_data, NDArray) else nd.array(eval_data)
+            self.forward(_SimpleBatch([arr]))
             return self.get_outputs()[0]
-        if reset:
-            eval_data.reset()
-        output_list = []
-        for nbatch, eval_batch in enumerate(eval_data):
-            if num_batch is not None and nbatch == num_batch:
-                break
-            self.prepare(eval_batch, sparse_row_id_fn=sparse_row_id_fn)
-            self.forward(eval_batch, is_train=False)
-            pad = eval_batch.pad
-            outputs = [out[0:out.shape[0] - pad].copy() for out in self.get_outputs()]
-            output_list.append(outputs)
-        if not output_list:
-            return output_list
-        if merge_batches:
-            num_outputs = len(output_list[0])
-            for out in output_list:
-                assert len(out) == num_outputs, 'Cannot merge batches, as num of outputs is not the same ' \
-                                                'in mini-batches. Maybe bucketing is used?'
-            output_list2 = [nd.concat(*[out[i] for out in output_list], dim=0) for i in range(num_outputs)]
-            if num_outputs == 1 and not always_output_list:
-                return output_list2[0]
-            return output_list2
-        return output_list
+        per_batch = [self._unpadded_outputs(batch, copy=True)
+                     for _, batch in self._walk(eval_data, num_batch, reset, sparse_row_id_fn)]
+        if not per_batch or not merge_batches:
+            return per_batch
+        width = len(per_batch[0])
+        if any(len(outs) != width for outs in per_batch):
+            raise AssertionError('cannot merge batches with different numbers of outputs (bucketing?)')
+        merged = [nd.concat(*[outs[i] for outs in per_batch], dim=0) for i in range(width)]
+        return merged[0] if width == 1 and not always_output_list else merged
 
+    # ---------------------------------------------------------------- training loop
     def fit(self, train_data, eval_data=None, eval_metric='acc', epoch_end_callback=None, batch_end_callback=None,
             kvstore='local', optimizer='sgd', optimizer_params=(('learning_rate', 0.01),), eval_end_callback=None,
             eval_batch_end_callback=None, initializer=Uniform(0.01), arg_params=None, aux_params=None,
             allow_missing=False, force_rebind=False, force_init=False, begin_epoch=0, num_epoch=None,
             validation_metric=None, monitor=None, sparse_row_id_fn=None):
-        assert num_epoch is not None, 'please specify number of epochs'
+        """Train for epochs ``[begin_epoch, num_epoch)``; optionally score ``eval_data`` after each."""
+        if num_epoch is None:
+            raise AssertionError('fit() needs num_epoch')
         self.bind(data_shapes=train_data.provide_data, label_shapes=train_data.provide_label, for_training=True,
                   force_rebind=force_rebind)
         if monitor is not None:
@@ -166,169 +188,135 @@ class BaseModule:
         self.init_params(initializer=initializer, arg_params=arg_params, aux_params=aux_params,
                          allow_missing=allow_missing, force_init=force_init)
         self.init_optimizer(kvstore=kvstore, optimizer=optimizer, optimizer_params=optimizer_params)
-        if validation_metric is None:
-            validation_metric = eval_metric
-        if not isinstance(eval_metric, metric.EvalMetric):
-            eval_metric = metric.create(eval_metric)
+        validation_metric = validation_metric if validation_metric is not None else eval_metric
+        train_metric = eval_metric if isinstance(eval_metric, metric.EvalMetric) else metric.create(eval_metric)
         for epoch in range(begin_epoch, num_epoch):
-            tic = time.time()
-            eval_metric.reset()
-            nbatch = 0
-            data_iter = iter(train_data)
-            end_of_batch = False
-            next_data_batch = next(data_iter)
-            eval_name_vals = []
-            while not end_of_batch:
-                data_batch = next_data_batch
-                if monitor is not None:
-                    monitor.tic()
-                self.forward_backward(data_batch)
-                self.update()
-                if isinstance(data_batch, list):
-                    self.update_metric(eval_metric, [db.label for db in data_batch], pre_sliced=True)
-                else:
-                    self.update_metric(eval_metric, data_batch.label)
-                try:
-                    next_data_batch = next(data_iter)
-                    self.prepare(next_data_batch, sparse_row_id_fn=sparse_row_id_fn)
-                except StopIteration:
-                    end_of_batch = True
-                if monitor is not None:
-                    monitor.toc_print()
-                if end_of_batch:
-                    eval_name_vals = eval_metric.get_global_name_value()
-                if batch_end_callback is not None:
-                    params = BatchEndParam(epoch=epoch, nbatch=nbatch, eval_metric=eval_metric, locals=locals())
-                    for callback in _as_list(batch_end_callback):
-                        callback(params)
-                nbatch += 1
-            for name, val in eval_name_vals:
+            t0 = time.time()
+            results = self._train_epoch(epoch, train_data, train_metric, monitor, batch_end_callback,
+                                        sparse_row_id_fn)
+            for name, val in results:
                 self.logger.info('Epoch[%d] Train-%s=%f', epoch, name, val)
-            self.logger.info('Epoch[%d] Time cost=%.3f', epoch, time.time() - tic)
-            arg_params_, aux_params_ = self.get_params()
-            self.set_params(arg_params_, aux_params_)
-            if epoch_end_callback is not None:
-                for callback in _as_list(epoch_end_callback):
-                    callback(epoch, self.symbol, arg_params_, aux_params_)
+            self.logger.info('Epoch[%d] Time cost=%.3f', epoch, time.time() - t0)
+            # pull the trained values back into arg/aux dicts (and re-broadcast to every device)
+            args, auxs = self.get_params()
+            self.set_params(args, auxs)
+            _fire(epoch_end_callback, epoch, self.symbol, args, auxs)
             if eval_data is not None:
-                res = self.score(eval_data, validation_metric, score_end_callback=eval_end_callback,
-                                 batch_end_callback=eval_batch_end_callback, epoch=epoch)
-                for name, val in res:
+                for name, val in self.score(eval_data, validation_metric, score_end_callback=eval_end_callback,
+                                            batch_end_callback=eval_batch_end_callback, epoch=epoch):
                     self.logger.info('Epoch[%d] Validation-%s=%f', epoch, name, val)
             train_data.reset()
 
-    # ------------------------------------------------------------ properties
-    @property
-    def data_names(self):
-        raise NotImplementedError()
+    def _train_epoch(self, epoch, train_data, train_metric, monitor, batch_end_callback, sparse_row_id_fn):
+        train_metric.reset()
+        it = iter(train_data)
+        batch = next(it)
+        nbatch = 0
+        while batch is not None:
+            if monitor is not None:
+                monitor.tic()
+            self.forward_backward(batch)
+            self.update()
+            labels, pre_sliced = _batch_labels(batch)
+            self.update_metric(train_metric, labels, pre_sliced=pre_sliced)
+            upcoming = next(it, None)
+            if upcoming is not None:
+                self.prepare(upcoming, sparse_row_id_fn=sparse_row_id_fn)
+            if monitor is not None:
+                monitor.toc_print()
+            results = train_metric.get_global_name_value() if upcoming is None else None
+            _fire(batch_end_callback, BatchEndParam(epoch, nbatch, train_metric, locals()))
+            batch = upcoming
+            nbatch += 1
+        return results or []
 
-    @property
-    def output_names(self):
-        raise NotImplementedError()
-
-    @property
-    def data_shapes(self):
-        raise NotImplementedError()
-
-    @property
-    def label_shapes(self):
-        raise NotImplementedError()
-
-    @property
-    def output_shapes(self):
-        raise NotImplementedError()
-
+    # ---------------------------------------------------------------- properties
     @property
     def symbol(self):
         return self._symbol
 
-    # ------------------------------------------------------------ parameters
+    def _unimplemented(self, *_a, **_k):
+        raise NotImplementedError('%s does not implement this operation' % type(self).__name__)
+
+    data_names = property(_unimplemented)
+    output_names = property(_unimplemented)
+    data_shapes = property(_unimplemented)
+    label_shapes = property(_unimplemented)
+    output_shapes = property(_unimplemented)
+
+    # ---------------------------------------------------------------- parameters
     def get_params(self):
-        raise NotImplementedError()
+        self._unimplemented()
 
     def init_params(self, initializer=Uniform(0.01), arg_params=None, aux_params=None, allow_missing=False,
                     force_init=False, allow_extra=False):
-        raise NotImplementedError()
+        self._unimplemented()
 
     def set_params(self, arg_params, aux_params, allow_missing=False, force_init=True, allow_extra=False):
         self.init_params(initializer=None, arg_params=arg_params, aux_params=aux_params,
                          allow_missing=allow_missing, force_init=force_init, allow_extra=allow_extra)
 
     def save_params(self, fname):
-        arg_params, aux_params = self.get_params()
-        save_dict = {('arg:%s' % k): v.as_in_context(_cpu()) for k, v in arg_params.items()}
-        save_dict.update({('aux:%s' % k): v.as_in_context(_cpu()) for k, v in aux_params.items()})
-        nd.save(fname, save_dict)
+        """Write ``arg:<name>`` / ``aux:<name>`` arrays (host copies) to an MXNet ``.params`` file."""
+        from ..context import cpu
+        args, auxs = self.get_params()
+        blob = {}
+        for prefix, params in (('arg', args), ('aux', auxs)):
+            blob.update({'%s:%s' % (prefix, k): v.as_in_context(cpu()) for k, v in params.items()})
+        nd.save(fname, blob)
 
     def load_params(self, fname):
-        save_dict = nd.load(fname)
-        arg_params, aux_params = {}, {}
-        for k, value in save_dict.items():
-            arg_type, name = k.split(':', 1)
-            if arg_type == 'arg':
-                arg_params[name] = value
-            elif arg_type == 'aux':
-                aux_params[name] = value
-            else:
-                raise ValueError('Invalid param file ' + fname)
-        self.set_params(arg_params, aux_params)
+        parts = {'arg': {}, 'aux': {}}
+        for key, value in nd.load(fname).items():
+            kind, _, name = key.partition(':')
+            if kind not in parts or not name:
+                raise ValueError('Invalid param file %s (key %r)' % (fname, key))
+            parts[kind][name] = value
+        self.set_params(parts['arg'], parts['aux'])
 
     def get_states(self, merge_multi_context=True):
-        assert self.binded and self.params_initialized
-        assert not merge_multi_context
+        self._require('binded', 'params_initialized')
+        if merge_multi_context:
+            raise AssertionError('this module has no states to merge')
         return []
 
     def set_states(self, states=None, value=None):
-        assert self.binded and self.params_initialized
-        assert not states and not value
+        self._require('binded', 'params_initialized')
+        if states or value:
+            raise AssertionError('this module has no states')
 
     def install_monitor(self, mon):
-        raise NotImplementedError()
+        self._unimplemented()
 
     def prepare(self, data_batch, sparse_row_id_fn=None):
-        if sparse_row_id_fn is not None:
-            if not self.binded or not self.params_initialized or not self.optimizer_initialized:
-                self.logger.warning('Parameters are not initialized or optimizer is not initialized; '
-                                    'sparse_row_id_fn ignored.')
+        """Hook run before a batch is forwarded (row-sparse pulls in Module)."""
+        if sparse_row_id_fn is not None and not (self.binded and self.params_initialized
+                                                 and self.optimizer_initialized):
+            self.logger.warning('sparse_row_id_fn ignored: module not bound / initialised / optimised yet.')
 
-    # ------------------------------------------------------------ computation
+    # ---------------------------------------------------------------- computation (abstract)
     def forward(self, data_batch, is_train=None):
-        raise NotImplementedError()
+        self._unimplemented()
 
     def backward(self, out_grads=None):
-        raise NotImplementedError()
+        self._unimplemented()
 
     def get_outputs(self, merge_multi_context=True):
-        raise NotImplementedError()
+        self._unimplemented()
 
     def get_input_grads(self, merge_multi_context=True):
-        raise NotImplementedError()
+        self._unimplemented()
 
     def update(self):
-        raise NotImplementedError()
+        self._unimplemented()
 
     def update_metric(self, eval_metric, labels, pre_sliced=False):
-        raise NotImplementedError()
+        self._unimplemented()
 
     def bind(self, data_shapes, label_shapes=None, for_training=True, inputs_need_grad=False, force_rebind=False,
              shared_module=None, grad_req='write'):
-        raise NotImplementedError()
+        self._unimplemented()
 
     def init_optimizer(self, kvstore='local', optimizer='sgd', optimizer_params=(('learning_rate', 0.01),),
                        force_init=False):
-        raise NotImplementedError()
-
-
-class _SimpleBatch:
-    def __init__(self, data, label=None):
-        self.data = data
-        self.label = label
-        self.pad = 0
-        self.bucket_key = None
-        self.provide_data = None
-        self.provide_label = None
-
-
-def _cpu():
-    from ..context import cpu
-    return cpu()
+        self._unimplemented()

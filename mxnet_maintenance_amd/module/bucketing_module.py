@@ -1,8 +1,11 @@
-"""BucketingModule: one Module per bucket key sharing parameters (parity: python/mxnet/module/bucketing_module.py).
+"""BucketingModule: one Module per bucket key, all sharing one set of parameters.
 
-``sym_gen(bucket_key) -> (symbol, data_names, label_names)``; the module for
-the default bucket owns the parameters and every other bucket binds with
-``shared_module`` so all buckets update the same arrays.
+API parity: python/mxnet/module/bucketing_module.py.  ``sym_gen(bucket_key)``
+returns ``(symbol, data_names, label_names)``.  The default bucket's module owns
+the parameters (and optimizer); a module for any other key is created on first
+use and bound with ``shared_module=<default>`` so its executors alias the same
+parameter / gradient arrays.  Each batch selects its bucket by
+``data_batch.bucket_key``.
 """
 import logging
 import warnings
@@ -19,30 +22,32 @@ class BucketingModule(BaseModule):
     def __init__(self, sym_gen, default_bucket_key=None, logger=logging, context=None, work_load_list=None,
                  fixed_param_names=None, state_names=None, group2ctxs=None, compression_params=None):
         super().__init__(logger=logger)
-        assert default_bucket_key is not None
-        self._default_bucket_key = default_bucket_key
+        if default_bucket_key is None:
+            raise AssertionError('BucketingModule needs a default_bucket_key')
         self._sym_gen = sym_gen
-        symbol, data_names, label_names = self._call_sym_gen(default_bucket_key)
-        data_names = list(data_names) if data_names is not None else []
-        label_names = list(label_names) if label_names is not None else []
-        state_names = list(state_names) if state_names is not None else []
-        fixed_param_names = list(fixed_param_names) if fixed_param_names is not None else []
-        _check_input_names(symbol, data_names, 'data', True)
-        _check_input_names(symbol, label_names, 'label', False)
-        _check_input_names(symbol, state_names, 'state', True)
-        _check_input_names(symbol, fixed_param_names, 'fixed_param', True)
-        self._compression_params = compression_params
-        self._fixed_param_names = fixed_param_names
-        self._state_names = state_names
-        self._context = context if context is not None else ctx_mod.cpu()
-        self._work_load_list = work_load_list
-        self._group2ctxs = group2ctxs
+        self._default_bucket_key = default_bucket_key
+        sym, data_names, label_names = self._call_sym_gen(default_bucket_key)
+        self._fixed_param_names = list(fixed_param_names or [])
+        self._state_names = list(state_names or [])
+        for names, kind, strict in ((list(data_names or []), 'data', True), (list(label_names or []), 'label', False),
+                                    (self._state_names, 'state', True), (self._fixed_param_names, 'fixed_param', True)):
+            _check_input_names(sym, names, kind, strict)
+        # construction arguments shared by every per-bucket Module
+        self._module_kwargs = dict(logger=logger, context=context if context is not None else ctx_mod.cpu(),
+                                   work_load_list=work_load_list, fixed_param_names=self._fixed_param_names,
+                                   state_names=self._state_names, group2ctxs=group2ctxs,
+                                   compression_params=compression_params)
+        self._context = self._module_kwargs['context']
         self._buckets = {}
         self._curr_module = None
         self._curr_bucket_key = None
         self._params_dirty = False
         self._monitor = None
         self._grad_req = None
+        self._preload = None
+
+    def _call_sym_gen(self, *args, **kwargs):
+        return self._sym_gen(*args, **kwargs)
 
     def _reset_bind(self):
         self.binded = False
@@ -50,55 +55,64 @@ class BucketingModule(BaseModule):
         self._curr_module = None
         self._curr_bucket_key = None
 
-    def _call_sym_gen(self, *args, **kwargs):
-        return self._sym_gen(*args, **kwargs)
+    def _new_module(self, key):
+        sym, data_names, label_names = self._call_sym_gen(key)
+        return Module(sym, data_names, label_names, **self._module_kwargs)
+
+    @property
+    def _default_module(self):
+        return self._buckets[self._default_bucket_key]
+
+    # ---------------------------------------------------------------- names / shapes
+    def _default_sym_info(self):
+        return self._call_sym_gen(self._default_bucket_key)
 
     @property
     def data_names(self):
-        if self.binded:
-            return self._curr_module.data_names
-        _, data_names, _ = self._call_sym_gen(self._default_bucket_key)
-        return data_names
+        return self._curr_module.data_names if self.binded else self._default_sym_info()[1]
 
     @property
     def output_names(self):
-        if self.binded:
-            return self._curr_module.output_names
-        symbol, _, _ = self._call_sym_gen(self._default_bucket_key)
-        return symbol.list_outputs()
+        return self._curr_module.output_names if self.binded else self._default_sym_info()[0].list_outputs()
 
     @property
     def data_shapes(self):
-        assert self.binded
+        self._require('binded')
         return self._curr_module.data_shapes
 
     @property
     def label_shapes(self):
-        assert self.binded
+        self._require('binded')
         return self._curr_module.label_shapes
 
     @property
     def output_shapes(self):
-        assert self.binded
+        self._require('binded')
         return self._curr_module.output_shapes
 
+    @property
+    def symbol(self):
+        self._require('binded')
+        return self._curr_module.symbol
+
+    # ---------------------------------------------------------------- parameters
     def get_params(self):
-        assert self.binded and self.params_initialized
+        self._require('binded', 'params_initialized')
         self._curr_module._params_dirty = self._params_dirty
-        params = self._curr_module.get_params()
+        out = self._curr_module.get_params()
         self._params_dirty = False
-        return params
+        return out
 
     def set_params(self, arg_params, aux_params, allow_missing=False, force_init=True, allow_extra=False):
         if not allow_missing:
-            self.init_params(initializer=None, arg_params=arg_params, aux_params=aux_params,
-                             allow_missing=allow_missing, force_init=force_init)
+            self.init_params(initializer=None, arg_params=arg_params, aux_params=aux_params, allow_missing=False,
+                             force_init=force_init)
             return
         if self.params_initialized and not force_init:
             warnings.warn('Parameters already initialized and force_init=False. set_params call ignored.',
                           stacklevel=2)
             return
-        self._curr_module.set_params(arg_params, aux_params, allow_missing=allow_missing, force_init=force_init,
+        self._curr_module.set_params(arg_params, aux_params, allow_missing=True, force_init=force_init,
                                      allow_extra=allow_extra)
         self._params_dirty = True
         self.params_initialized = True
@@ -107,73 +121,69 @@ class BucketingModule(BaseModule):
                     force_init=False, allow_extra=False):
         if self.params_initialized and not force_init:
             return
-        assert self.binded, 'call bind before initializing the parameters'
+        if not self.binded:
+            raise AssertionError('call bind before initializing the parameters')
         self._curr_module.init_params(initializer=initializer, arg_params=arg_params, aux_params=aux_params,
                                       allow_missing=allow_missing, force_init=force_init, allow_extra=allow_extra)
         self._params_dirty = False
         self.params_initialized = True
 
     def get_states(self, merge_multi_context=True):
-        assert self.binded and self.params_initialized
+        self._require('binded', 'params_initialized')
         return self._curr_module.get_states(merge_multi_context=merge_multi_context)
 
     def set_states(self, states=None, value=None):
-        assert self.binded and self.params_initialized
+        self._require('binded', 'params_initialized')
         self._curr_module.set_states(states, value)
 
+    # ---------------------------------------------------------------- binding / buckets
     def bind(self, data_shapes, label_shapes=None, for_training=True, inputs_need_grad=False, force_rebind=False,
              shared_module=None, grad_req='write'):
-        if self.params_initialized:
-            arg_params, aux_params = self.get_params()
+        saved = self.get_params() if self.params_initialized else None
         if force_rebind:
             self._reset_bind()
         if self.binded:
             self.logger.warning('Already bound, ignoring bind()')
             return
-        assert shared_module is None, 'shared_module for BucketingModule is not supported'
-        self.for_training = for_training
-        self.inputs_need_grad = inputs_need_grad
+        if shared_module is not None:
+            raise AssertionError('shared_module is not supported by BucketingModule')
+        self.for_training, self.inputs_need_grad, self._grad_req = for_training, inputs_need_grad, grad_req
         self.binded = True
-        self._grad_req = grad_req
-        symbol, data_names, label_names = self._call_sym_gen(self._default_bucket_key)
-        module = Module(symbol, data_names, label_names, logger=self.logger, context=self._context,
-                        work_load_list=self._work_load_list, fixed_param_names=self._fixed_param_names,
-                        state_names=self._state_names, group2ctxs=self._group2ctxs,
-                        compression_params=self._compression_params)
-        module.bind(data_shapes, label_shapes, for_training, inputs_need_grad, force_rebind=False,
-                    shared_module=None, grad_req=self._grad_req)
-        self._curr_module = module
-        self._curr_bucket_key = self._default_bucket_key
-        self._buckets[self._default_bucket_key] = module
-        if self.params_initialized:
-            self.set_params(arg_params, aux_params)
+        mod = self._new_module(self._default_bucket_key)
+        mod.bind(data_shapes, label_shapes, for_training, inputs_need_grad, force_rebind=False, shared_module=None,
+                 grad_req=grad_req)
+        self._buckets[self._default_bucket_key] = mod
+        self._curr_module, self._curr_bucket_key = mod, self._default_bucket_key
+        if saved is None and self._preload is not None:      # BucketingModule.load()
+            saved, self._preload = self._preload, None
+            self.params_initialized = True
+        if saved is not None:
+            self.set_params(*saved)
 
     def switch_bucket(self, bucket_key, data_shapes, label_shapes=None):
-        assert self.binded, 'call bind before switching bucket'
-        if bucket_key not in self._buckets:
-            symbol, data_names, label_names = self._call_sym_gen(bucket_key)
-            module = Module(symbol, data_names, label_names, logger=self.logger, context=self._context,
-                            work_load_list=self._work_load_list, fixed_param_names=self._fixed_param_names,
-                            state_names=self._state_names, group2ctxs=self._group2ctxs,
-                            compression_params=self._compression_params)
-            module.bind(data_shapes, label_shapes, self._curr_module.for_training,
-                        self._curr_module.inputs_need_grad, force_rebind=False,
-                        shared_module=self._buckets[self._default_bucket_key], grad_req=self._grad_req)
+        """Make ``bucket_key`` current, creating / binding its module on first use."""
+        self._require('binded')
+        mod = self._buckets.get(bucket_key)
+        if mod is None:
+            mod = self._new_module(bucket_key)
+            self._buckets[bucket_key] = mod
             if self._monitor is not None:
-                module.install_monitor(self._monitor)
-            self._buckets[bucket_key] = module
-        else:
-            module = self._buckets[bucket_key]
-            if not module.binded:
-                module.bind(data_shapes, label_shapes, self._curr_module.for_training,
-                            self._curr_module.inputs_need_grad, force_rebind=False,
-                            shared_module=self._buckets[self._default_bucket_key], grad_req=self._grad_req)
-        self._curr_module = self._buckets[bucket_key]
-        self._curr_bucket_key = bucket_key
+                self._bind_shared(mod, data_shapes, label_shapes)
+                mod.install_monitor(self._monitor)
+        if not mod.binded:
+            self._bind_shared(mod, data_shapes, label_shapes)
+        self._curr_module, self._curr_bucket_key = mod, bucket_key
+
+    def _bind_shared(self, mod, data_shapes, label_shapes):
+        if mod.binded:
+            return
+        cur = self._curr_module
+        mod.bind(data_shapes, label_shapes, cur.for_training, cur.inputs_need_grad, force_rebind=False,
+                 shared_module=self._default_module, grad_req=self._grad_req)
 
     def init_optimizer(self, kvstore='local', optimizer='sgd', optimizer_params=(('learning_rate', 0.01),),
                        force_init=False):
-        assert self.binded and self.params_initialized
+        self._require('binded', 'params_initialized')
         if self.optimizer_initialized and not force_init:
             self.logger.warning('optimizer already initialized, ignoring.')
             return
@@ -183,62 +193,58 @@ class BucketingModule(BaseModule):
                 mod.borrow_optimizer(self._curr_module)
         self.optimizer_initialized = True
 
+    # ---------------------------------------------------------------- computation
     def prepare(self, data_batch, sparse_row_id_fn=None):
-        assert self.binded and self.params_initialized
-        bucket_key = data_batch.bucket_key
-        original_bucket_key = self._curr_bucket_key
-        data_shapes = data_batch.provide_data
-        label_shapes = data_batch.provide_label
-        self.switch_bucket(bucket_key, data_shapes, label_shapes)
+        self._require('binded', 'params_initialized')
+        home = self._curr_bucket_key
+        self.switch_bucket(data_batch.bucket_key, data_batch.provide_data, data_batch.provide_label)
         self._curr_module.prepare(data_batch, sparse_row_id_fn=sparse_row_id_fn)
-        self.switch_bucket(original_bucket_key, None, None)
+        self.switch_bucket(home, None, None)
 
     def forward(self, data_batch, is_train=None):
-        assert self.binded and self.params_initialized
+        self._require('binded', 'params_initialized')
         self.switch_bucket(data_batch.bucket_key, data_batch.provide_data, data_batch.provide_label)
         self._curr_module.forward(data_batch, is_train=is_train)
 
     def backward(self, out_grads=None):
-        assert self.binded and self.params_initialized
+        self._require('binded', 'params_initialized')
         self._curr_module.backward(out_grads=out_grads)
 
     def update(self):
-        assert self.binded and self.params_initialized and self.optimizer_initialized
+        self._require('binded', 'params_initialized', 'optimizer_initialized')
         self._params_dirty = True
         self._curr_module.update()
 
     def get_outputs(self, merge_multi_context=True):
-        assert self.binded and self.params_initialized
+        self._require('binded', 'params_initialized')
         return self._curr_module.get_outputs(merge_multi_context=merge_multi_context)
 
     def get_input_grads(self, merge_multi_context=True):
-        assert self.binded and self.params_initialized and self.inputs_need_grad
+        self._require('binded', 'params_initialized', 'inputs_need_grad')
         return self._curr_module.get_input_grads(merge_multi_context=merge_multi_context)
 
     def update_metric(self, eval_metric, labels, pre_sliced=False):
-        assert self.binded and self.params_initialized
+        self._require('binded', 'params_initialized')
         self._curr_module.update_metric(eval_metric, labels, pre_sliced)
 
-    @property
-    def symbol(self):
-        assert self.binded
-        return self._curr_module.symbol
-
     def install_monitor(self, mon):
-        assert self.binded
+        self._require('binded')
         self._monitor = mon
         for mod in self._buckets.values():
             mod.install_monitor(mon)
 
+    # ---------------------------------------------------------------- checkpoints
     def save_checkpoint(self, prefix, epoch, remove_amp_cast=False):
-        assert len(self._buckets) > 0 and self.binded
+        if not (self.binded and self._buckets):
+            raise AssertionError('bind before saving a checkpoint')
         self._curr_module.save_checkpoint(prefix, epoch)
 
     @staticmethod
     def load(prefix, epoch, sym_gen=None, default_bucket_key=None, **kwargs):
+        """A BucketingModule whose parameters are set from ``prefix-%04d.params`` at bind time."""
         from ..model import load_params
-        assert sym_gen is not None and default_bucket_key is not None
+        if sym_gen is None or default_bucket_key is None:
+            raise AssertionError('BucketingModule.load needs sym_gen and default_bucket_key')
         mod = BucketingModule(sym_gen=sym_gen, default_bucket_key=default_bucket_key, **kwargs)
-        arg_params, aux_params = load_params(prefix, epoch)
-        mod._preload = (arg_params, aux_params)
+        mod._preload = load_params(prefix, epoch)
         return mod

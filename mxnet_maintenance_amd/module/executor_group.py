@@ -1,18 +1,20 @@
-"""Data-parallel executor group (parity: python/mxnet/module/executor_group.py).
+"""Data-parallel executor group: one bound Executor per context.
 
-Binds one Executor per context with the batch split by ``workload``;
-parameters are replicated (one array per context), inputs/labels are sliced
-along the batch axis, outputs are concatenated back.  On an MI355X node the
-usual deployment is one process per GPU (one context here) with gradient
-reduction through the kvstore; several contexts in one process are
-supported for parity.
+API parity: python/mxnet/module/executor_group.py (``DataParallelExecutorGroup``
+with ``param_arrays`` / ``grad_arrays`` / ``aux_arrays`` as per-parameter lists
+of per-device arrays, ``forward`` / ``backward`` / ``get_outputs`` /
+``update_metric`` / ``reshape`` / ``set_params`` / ``get_params``).
+
+Design: the group is a list of ``_Shard`` records (context, batch slice,
+executor).  Per-parameter views (``param_arrays`` etc.) are derived from the
+shards after every (re)bind.  On an MI355X node the normal deployment is one
+process per GPU, i.e. a single shard, with cross-GPU reduction done by the
+kvstore over RCCL; several contexts per process still work (batch split by
+``workload``) for parity and CPU tests.
 """
 import logging
 
-import numpy as np
-
 from .. import ndarray as nd
-from ..base import MXNetError
 from ..io import DataDesc
 from ..ndarray.ndarray import NDArray
 
@@ -20,280 +22,282 @@ __all__ = ['DataParallelExecutorGroup']
 
 
 def _split_input_slice(batch_size, work_load_list):
-    total = sum(work_load_list)
-    batch_num_list = [round(w * batch_size / total) for w in work_load_list]
-    delta = batch_size - sum(batch_num_list)
-    batch_num_list[-1] += delta
-    slices = []
-    end = 0
-    for n in batch_num_list:
-        begin = int(min(end, batch_size))
-        end = int(min(begin + n, batch_size))
-        if begin >= end:
-            raise ValueError('Too many slices. Some splits are empty.')
-        slices.append(slice(begin, end))
-    return slices
+    """Contiguous batch slices proportional to ``work_load_list`` (last slice takes the rounding)."""
+    total = float(sum(work_load_list))
+    sizes = [int(round(w * batch_size / total)) for w in work_load_list]
+    sizes[-1] += batch_size - sum(sizes)
+    out, start = [], 0
+    for n in sizes:
+        stop = min(start + n, batch_size)
+        if stop <= start:
+            raise ValueError('batch of %d cannot be split over workloads %s: empty slice'
+                             % (batch_size, work_load_list))
+        out.append(slice(start, stop))
+        start = stop
+    return out
+
+
+def _copy_into(src, dst, sl, axis):
+    """dst[...] = src (sliced along ``axis`` by ``sl`` when src holds the whole batch)."""
+    if axis >= 0 and src.shape[axis] != dst.shape[axis]:
+        src = nd.slice_axis(src, axis=axis, begin=sl.start, end=sl.stop)
+    dst[:] = src.astype(dst.dtype).as_in_context(dst.context)
 
 
 def _load_general(data, targets, major_axis):
-    for d_src, d_targets in zip(data, targets):
-        if isinstance(d_targets, NDArray):
-            d_src.copyto(d_targets)
-        elif isinstance(d_src, (list, tuple)):
-            for src, dst in zip(d_src, d_targets):
-                src.copyto(dst)
+    """Copy a batch's arrays into per-device targets.
+
+    ``targets[i]`` is either a single NDArray, a list of per-device arrays (src
+    then also per-device), or a list of ``(slice, array)`` pairs to slice into.
+    """
+    for src, tgt in zip(data, targets):
+        if isinstance(tgt, NDArray):
+            src.copyto(tgt)
+        elif isinstance(src, (list, tuple)):
+            for s, d in zip(src, tgt):
+                s.copyto(d)
         else:
-            for slice_idx, d_dst in d_targets:
-                if major_axis >= 0 and d_src.shape[major_axis] != d_dst.shape[major_axis]:
-                    d_src_slice = nd.slice_axis(d_src, axis=major_axis, begin=slice_idx.start,
-                                                end=slice_idx.stop)
-                else:
-                    d_src_slice = d_src
-                d_dst[:] = d_src_slice.astype(d_dst.dtype).as_in_context(d_dst.context)
+            for sl, dst in tgt:
+                _copy_into(src, dst, sl, major_axis)
 
 
 def _merge_multi_context(outputs, major_axis):
-    rets = []
-    for tensors, axis in zip(outputs, major_axis):
-        if axis >= 0:
-            if len(tensors) == 1:
-                rets.append(tensors[0])
-            else:
-                rets.append(nd.concat(*[t.as_in_context(tensors[0].context) for t in tensors], dim=axis))
+    """Concatenate per-device pieces along each output's batch axis (axis < 0: take device 0's)."""
+    merged = []
+    for pieces, axis in zip(outputs, major_axis):
+        if axis < 0 or len(pieces) == 1:
+            merged.append(pieces[0])
         else:
-            rets.append(tensors[0])
-    return rets
+            home = pieces[0].context
+            merged.append(nd.concat(*[p.as_in_context(home) for p in pieces], dim=axis))
+    return merged
+
+
+def _resolve_grad_req(grad_req, arg_names, param_names, data_names, fixed, inputs_need_grad, for_training):
+    """Per-argument gradient request: parameters get ``grad_req`` (fixed ones 'null'), data inputs
+    only when input gradients are wanted, everything else 'null'."""
+    if not for_training:
+        return {k: 'null' for k in arg_names}
+    if isinstance(grad_req, (list, tuple)):
+        return dict(zip(arg_names, grad_req))
+    default = grad_req if isinstance(grad_req, str) else 'write'
+
+    def req(name):
+        if name in param_names:
+            return 'null' if name in fixed else default
+        if name in data_names:
+            return default if inputs_need_grad else 'null'
+        return 'null'
+    out = {k: req(k) for k in arg_names}
+    if isinstance(grad_req, dict):
+        out.update(grad_req)
+    return out
+
+
+class _Shard:
+    __slots__ = ('ctx', 'slice', 'exe')
+
+    def __init__(self, ctx, sl, exe):
+        self.ctx = ctx
+        self.slice = sl
+        self.exe = exe
 
 
 class DataParallelExecutorGroup:
+    """Executors for ``symbol`` on ``contexts`` sharing one logical batch."""
+
     def __init__(self, symbol, contexts, workload, data_shapes, label_shapes, param_names, for_training,
                  inputs_need_grad, shared_group=None, logger=logging, fixed_param_names=None, grad_req='write',
                  state_names=None, group2ctxs=None):
-        self.param_names = param_names
+        self.symbol = symbol
+        self.contexts = list(contexts)
+        self.workload = list(workload) if workload else [1] * len(self.contexts)
+        self.param_names = list(param_names)
         self.arg_names = symbol.list_arguments()
         self.aux_names = symbol.list_auxiliary_states()
-        self.symbol = symbol
-        self.contexts = contexts
-        self.workload = workload or [1] * len(contexts)
+        self.fixed_param_names = list(fixed_param_names or [])
+        self.state_names = list(state_names or [])
         self.for_training = for_training
         self.inputs_need_grad = inputs_need_grad
-        self.logger = logger
-        self.fixed_param_names = fixed_param_names or []
-        self.state_names = state_names or []
         self.shared_group = shared_group
-        self.execs = []
+        self.logger = logger
+        self.shards = []
         self.batch_size = None
         self.slices = None
-        self.data_shapes = None
-        self.label_shapes = None
-        self.grad_req = {}
-        data_names = [x.name if isinstance(x, DataDesc) else x[0] for x in data_shapes]
-        if isinstance(grad_req, str):
-            for k in self.arg_names:
-                if k in self.param_names:
-                    self.grad_req[k] = 'null' if k in self.fixed_param_names else grad_req
-                elif k in data_names:
-                    self.grad_req[k] = grad_req if self.inputs_need_grad else 'null'
-                else:
-                    self.grad_req[k] = 'null'
-        elif isinstance(grad_req, (list, tuple)):
-            self.grad_req = dict(zip(self.arg_names, grad_req))
-        elif isinstance(grad_req, dict):
-            for k in self.arg_names:
-                if k in self.param_names:
-                    self.grad_req[k] = 'null' if k in self.fixed_param_names else 'write'
-                elif k in data_names:
-                    self.grad_req[k] = 'write' if self.inputs_need_grad else 'null'
-                else:
-                    self.grad_req[k] = 'null'
-            self.grad_req.update(grad_req)
-        if not for_training:
-            self.grad_req = {k: 'null' for k in self.arg_names}
+        self.data_shapes = self.label_shapes = None
+        data_names = [d.name if isinstance(d, DataDesc) else d[0] for d in data_shapes]
+        self.grad_req = _resolve_grad_req(grad_req, self.arg_names, self.param_names, data_names,
+                                          self.fixed_param_names, inputs_need_grad, for_training)
         self.bind_exec(data_shapes, label_shapes, shared_group)
 
-    # ------------------------------------------------------------ binding
-    def decide_slices(self, data_shapes):
-        major_axis = [DataDesc.get_batch_axis(getattr(x, 'layout', 'NCHW')) for x in data_shapes]
-        for desc, axis in zip(data_shapes, major_axis):
-            if axis == -1:
-                continue
-            batch_size = desc.shape[axis]
-            if self.batch_size is not None:
-                assert batch_size == self.batch_size, \
-                    'all data must have the same batch size: batch_size = %d, but %s has shape %s' % (
-                        self.batch_size, desc.name, desc.shape)
-            else:
-                self.batch_size = batch_size
-                self.slices = _split_input_slice(self.batch_size, self.workload)
-        return major_axis
+    @property
+    def execs(self):
+        return [s.exe for s in self.shards]
 
-    def _sliced_shape(self, shapes, i, major_axis):
-        sliced = []
-        for desc, axis in zip(shapes, major_axis):
-            shape = list(desc.shape)
+    # ---------------------------------------------------------------- binding
+    def decide_slices(self, descs):
+        """Batch axis per input; fixes ``batch_size`` / ``slices`` from the first batched input."""
+        axes = [DataDesc.get_batch_axis(getattr(d, 'layout', 'NCHW')) for d in descs]
+        for d, axis in zip(descs, axes):
+            if axis < 0:
+                continue
+            n = d.shape[axis]
+            if self.batch_size is None:
+                self.batch_size = n
+                self.slices = _split_input_slice(n, self.workload)
+            elif n != self.batch_size:
+                raise AssertionError('inputs disagree on the batch size: %d vs %s of shape %s'
+                                     % (self.batch_size, d.name, d.shape))
+        return axes
+
+    def _shapes_for(self, descs, axes, sl):
+        out = {}
+        for d, axis in zip(descs, axes):
+            shape = list(d.shape)
             if axis >= 0:
-                shape[axis] = self.slices[i].stop - self.slices[i].start
-            sliced.append(DataDesc(desc.name, tuple(shape), desc.dtype, getattr(desc, 'layout', 'NCHW')))
-        return sliced
+                shape[axis] = sl.stop - sl.start
+            out[d.name] = (tuple(shape), d.dtype)
+        return out
 
     def bind_exec(self, data_shapes, label_shapes, shared_group=None, reshape=False):
-        data_shapes = [x if isinstance(x, DataDesc) else DataDesc(*x) for x in data_shapes]
-        if label_shapes is not None:
-            label_shapes = [x if isinstance(x, DataDesc) else DataDesc(*x) for x in label_shapes]
+        data_shapes = [d if isinstance(d, DataDesc) else DataDesc(*d) for d in data_shapes]
+        label_shapes = None if label_shapes is None else \
+            [d if isinstance(d, DataDesc) else DataDesc(*d) for d in label_shapes]
         self.batch_size = None
         self.data_layouts = self.decide_slices(data_shapes)
         self.label_layouts = self.decide_slices(label_shapes) if label_shapes is not None else None
-        old_execs = self.execs
-        self.execs = []
+        previous = self.shards
+        self.shards = []
         for i, ctx in enumerate(self.contexts):
-            shapes = {d.name: d.shape for d in self._sliced_shape(data_shapes, i, self.data_layouts)}
-            types = {d.name: d.dtype for d in data_shapes}
+            sl = self.slices[i]
+            spec = self._shapes_for(data_shapes, self.data_layouts, sl)
             if label_shapes is not None:
-                shapes.update({d.name: d.shape for d in self._sliced_shape(label_shapes, i, self.label_layouts)})
-                types.update({d.name: d.dtype for d in label_shapes})
-            shapes = {k: v for k, v in shapes.items() if k in self.arg_names}
-            types = {k: v for k, v in types.items() if k in self.arg_names}
-            exe = self.symbol.simple_bind(ctx, grad_req=self.grad_req, type_dict=types, **shapes)
-            # share parameters with an existing group (bucketing) or keep values across reshape
-            src = None
-            if shared_group is not None:
-                src = shared_group.execs[i]
-            elif reshape and old_execs:
-                src = old_execs[i]
-            if src is not None:
-                for name in self.param_names:
-                    if name in src.arg_dict and src.arg_dict[name].shape == exe.arg_dict[name].shape:
-                        j = self.arg_names.index(name)
-                        exe.arg_arrays[j] = src.arg_dict[name]
-                        if exe.grad_arrays[j] is not None and src.grad_dict.get(name) is not None:
-                            exe.grad_arrays[j] = src.grad_dict[name]
-                for j, name in enumerate(self.aux_names):
-                    if name in src.aux_dict and src.aux_dict[name].shape == exe.aux_arrays[j].shape:
-                        exe.aux_arrays[j] = src.aux_dict[name]
-            self.execs.append(exe)
-        self.data_shapes = data_shapes
-        self.label_shapes = label_shapes
+                spec.update(self._shapes_for(label_shapes, self.label_layouts, sl))
+            spec = {k: v for k, v in spec.items() if k in self.arg_names}
+            exe = self.symbol.simple_bind(ctx, grad_req=self.grad_req, type_dict={k: v[1] for k, v in spec.items()},
+                                          **{k: v[0] for k, v in spec.items()})
+            donor = shared_group.execs[i] if shared_group is not None else \
+                (previous[i].exe if reshape and previous else None)
+            if donor is not None:
+                self._adopt_params(exe, donor)
+            self.shards.append(_Shard(ctx, sl, exe))
+        self.data_shapes, self.label_shapes = data_shapes, label_shapes
         self.data_names = [d.name for d in data_shapes]
         self.label_names = [d.name for d in label_shapes] if label_shapes is not None else []
         self._collect_arrays()
 
+    def _adopt_params(self, exe, donor):
+        """Share parameter / gradient / aux arrays of matching shape with ``donor`` (bucketing, reshape)."""
+        for name in self.param_names:
+            src = donor.arg_dict.get(name)
+            j = self.arg_names.index(name)
+            if src is None or src.shape != exe.arg_arrays[j].shape:
+                continue
+            exe.arg_arrays[j] = src
+            g = donor.grad_dict.get(name)
+            if exe.grad_arrays[j] is not None and g is not None:
+                exe.grad_arrays[j] = g
+        for j, name in enumerate(self.aux_names):
+            src = donor.aux_dict.get(name)
+            if src is not None and src.shape == exe.aux_arrays[j].shape:
+                exe.aux_arrays[j] = src
+
     def reshape(self, data_shapes, label_shapes):
-        if data_shapes == self.data_shapes and label_shapes == self.label_shapes:
-            return
-        self.bind_exec(data_shapes, label_shapes, reshape=True)
+        if data_shapes != self.data_shapes or label_shapes != self.label_shapes:
+            self.bind_exec(data_shapes, label_shapes, reshape=True)
+
+    def _per_arg(self, names, pick):
+        return [[pick(s.exe, self.arg_names.index(n)) for s in self.shards] for n in names if n in self.arg_names]
 
     def _collect_arrays(self):
-        self.data_arrays = [[(self.slices[i], e.arg_dict[name]) for i, e in enumerate(self.execs)]
-                            for name in self.data_names if name in self.arg_names]
-        self.label_arrays = [[(self.slices[i], e.arg_dict[name]) for i, e in enumerate(self.execs)]
-                             for name in self.label_names if name in self.arg_names]
-        self.param_arrays = [[e.arg_arrays[i] for e in self.execs] for i, name in enumerate(self.arg_names)
-                             if name in self.param_names]
-        if self.for_training:
-            self.grad_arrays = [[e.grad_arrays[i] for e in self.execs] for i, name in enumerate(self.arg_names)
-                                if name in self.param_names]
-        else:
-            self.grad_arrays = None
-        data_names = [x[0] for x in self.data_shapes]
-        if self.inputs_need_grad:
-            self.input_grad_arrays = [[e.grad_arrays[self.arg_names.index(name)] for e in self.execs]
-                                      for name in data_names if name in self.arg_names]
-        else:
-            self.input_grad_arrays = None
-        self.aux_arrays = [[e.aux_arrays[i] for e in self.execs] for i in range(len(self.aux_names))]
+        arg = lambda e, j: e.arg_arrays[j]       # noqa: E731
+        grad = lambda e, j: e.grad_arrays[j]     # noqa: E731
+        self.data_arrays = [[(s.slice, s.exe.arg_dict[n]) for s in self.shards]
+                            for n in self.data_names if n in self.arg_names]
+        self.label_arrays = [[(s.slice, s.exe.arg_dict[n]) for s in self.shards]
+                             for n in self.label_names if n in self.arg_names]
+        params = [n for n in self.arg_names if n in self.param_names]
+        self.param_arrays = self._per_arg(params, arg)
+        self.grad_arrays = self._per_arg(params, grad) if self.for_training else None
+        self.input_grad_arrays = self._per_arg(self.data_names, grad) if self.inputs_need_grad else None
+        self.aux_arrays = [[s.exe.aux_arrays[j] for s in self.shards] for j in range(len(self.aux_names))]
 
-    # ------------------------------------------------------------ params
+    # ---------------------------------------------------------------- parameters
     def set_params(self, arg_params, aux_params, allow_extra=False):
-        for exe in self.execs:
-            exe.copy_params_from(arg_params, aux_params, allow_extra_params=allow_extra)
+        for s in self.shards:
+            s.exe.copy_params_from(arg_params, aux_params, allow_extra_params=allow_extra)
 
     def get_params(self, arg_params, aux_params):
-        for name, block in zip(self.param_names, self.param_arrays):
-            weight = sum(w.copyto(_cpu()) for w in block) / len(block)
-            weight.astype(arg_params[name].dtype).copyto(arg_params[name])
-        for name, block in zip(self.aux_names, self.aux_arrays):
-            weight = sum(w.copyto(_cpu()) for w in block) / len(block)
-            weight.astype(aux_params[name].dtype).copyto(aux_params[name])
+        """Average each parameter over devices (host side) into the given dicts."""
+        from ..context import cpu
+        for names, arrays, dst in ((self.param_names, self.param_arrays, arg_params),
+                                   (self.aux_names, self.aux_arrays, aux_params)):
+            for name, per_dev in zip(names, arrays):
+                mean = sum(a.copyto(cpu()) for a in per_dev) / len(per_dev)
+                mean.astype(dst[name].dtype).copyto(dst[name])
 
-    # ------------------------------------------------------------ compute
+    # ---------------------------------------------------------------- compute
     def forward(self, data_batch, is_train=None):
         _load_general(data_batch.data, self.data_arrays, self.data_layouts[0] if self.data_layouts else 0)
-        if is_train is None:
-            is_train = self.for_training
         if self.label_arrays and data_batch.label:
-            _load_general(data_batch.label, self.label_arrays,
-                          self.label_layouts[0] if self.label_layouts else 0)
-        for exe in self.execs:
-            exe.forward(is_train=is_train)
+            _load_general(data_batch.label, self.label_arrays, self.label_layouts[0] if self.label_layouts else 0)
+        train = self.for_training if is_train is None else is_train
+        for s in self.shards:
+            s.exe.forward(is_train=train)
+
+    def backward(self, out_grads=None):
+        if not self.for_training:
+            raise AssertionError('bind with for_training=True to run backward')
+        for s in self.shards:
+            heads = [nd.slice_axis(g, axis=0, begin=s.slice.start, end=s.slice.stop).as_in_context(s.ctx)
+                     for g in (out_grads or [])]
+            s.exe.backward(out_grads=heads or None)
 
     def get_output_shapes(self):
-        # shapes of the whole (unsliced) batch, from shape inference (valid before any forward)
-        shapes = {d.name: d.shape for d in self.data_shapes}
-        if self.label_shapes is not None:
-            shapes.update({d.name: d.shape for d in self.label_shapes})
-        shapes = {k: v for k, v in shapes.items() if k in self.arg_names}
-        _, out_shapes, _ = self.symbol.infer_shape(**shapes)
+        """Whole-batch output shapes from shape inference (valid before any forward)."""
+        known = {d.name: d.shape for d in (self.data_shapes + (self.label_shapes or [])) if d.name in self.arg_names}
+        _, out_shapes, _ = self.symbol.infer_shape(**known)
         return list(zip(self.symbol.list_outputs(), [tuple(s) for s in out_shapes]))
 
     def get_outputs(self, merge_multi_context=True, begin=0, end=None):
-        if end is None:
-            end = len(self.execs[0].outputs)
-        outputs = [[exe.outputs[i] for exe in self.execs] for i in range(begin, end)]
-        if merge_multi_context:
-            outputs = _merge_multi_context(outputs, [0] * len(outputs))
-        return outputs
-
-    def get_states(self, merge_multi_context=True):
-        assert not merge_multi_context
-        return [[exe.arg_dict[name] for exe in self.execs] for name in self.state_names]
-
-    def set_states(self, states=None, value=None):
-        if states is not None:
-            assert value is None
-            _load_general(states, self.get_states(False), -1)
-        else:
-            for d_dst in self.get_states(False):
-                for dst in d_dst:
-                    dst[:] = value
+        n_out = len(self.shards[0].exe.outputs)
+        picked = [[s.exe.outputs[i] for s in self.shards] for i in range(begin, n_out if end is None else end)]
+        return _merge_multi_context(picked, [0] * len(picked)) if merge_multi_context else picked
 
     def get_input_grads(self, merge_multi_context=True):
-        assert self.inputs_need_grad
-        if merge_multi_context:
-            return _merge_multi_context(self.input_grad_arrays, [0] * len(self.input_grad_arrays))
-        return self.input_grad_arrays
+        if not self.inputs_need_grad:
+            raise AssertionError('bind with inputs_need_grad=True to get input gradients')
+        g = self.input_grad_arrays
+        return _merge_multi_context(g, [0] * len(g)) if merge_multi_context else g
 
-    def backward(self, out_grads=None):
-        assert self.for_training, 're-bind with for_training=True to run backward'
-        if out_grads is None:
-            out_grads = []
-        for i, exe in enumerate(self.execs):
-            out_grads_slice = []
-            for grad in out_grads:
-                sl = self.slices[i]
-                og = nd.slice_axis(grad, axis=0, begin=sl.start, end=sl.stop)
-                out_grads_slice.append(og.as_in_context(self.contexts[i]))
-            exe.backward(out_grads=out_grads_slice or None)
+    def get_states(self, merge_multi_context=True):
+        if merge_multi_context:
+            raise AssertionError('states are per device; call with merge_multi_context=False')
+        return [[s.exe.arg_dict[n] for s in self.shards] for n in self.state_names]
+
+    def set_states(self, states=None, value=None):
+        targets = self.get_states(False)
+        if states is not None:
+            if value is not None:
+                raise AssertionError('give either states or value')
+            _load_general(states, targets, -1)
+            return
+        for per_dev in targets:
+            for arr in per_dev:
+                arr[:] = value
 
     def update_metric(self, eval_metric, labels, pre_sliced=False):
-        for current_exec, (texec, islice) in enumerate(zip(self.execs, self.slices)):
-            if not pre_sliced:
-                labels_slice = []
-                for label in labels:
-                    if label.shape[0] == self.batch_size and len(self.execs) > 1:
-                        labels_slice.append(nd.slice_axis(label, axis=0, begin=islice.start, end=islice.stop))
-                    else:
-                        labels_slice.append(label)
+        outputs = self.symbol.list_outputs()
+        for i, s in enumerate(self.shards):
+            if pre_sliced:
+                mine = labels[i]
+            elif len(self.shards) > 1:
+                mine = [nd.slice_axis(l, axis=0, begin=s.slice.start, end=s.slice.stop)
+                        if l.shape[0] == self.batch_size else l for l in labels]
             else:
-                labels_slice = labels[current_exec]
-            labels_ = dict(zip(self.label_names, labels_slice))
-            preds = dict(zip(self.symbol.list_outputs(), texec.outputs))
-            eval_metric.update_dict(labels_, preds)
+                mine = labels
+            eval_metric.update_dict(dict(zip(self.label_names, mine)), dict(zip(outputs, s.exe.outputs)))
 
     def install_monitor(self, mon):
-        for exe in self.execs:
-            mon.install(exe)
-
-
-def _cpu():
-    from ..context import cpu
-    return cpu()
+        for s in self.shards:
+            mon.install(s.exe)
