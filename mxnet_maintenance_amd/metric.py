@@ -1,10 +1,23 @@
-"""Evaluation metrics.
+"""Evaluation metrics (API parity: python/mxnet/metric.py).
 
-Parity: python/mxnet/metric.py (EvalMetric, CompositeEvalMetric, Accuracy,
-TopKAccuracy, F1, MCC, Perplexity, MAE, MSE, RMSE, CrossEntropy,
-NegativeLogLikelihood, PearsonCorrelation, PCC, Loss, Torch, Caffe,
-CustomMetric, np, create, register, check_label_shapes).
-Accuracy/TopK reduce on the device and transfer one scalar per update.
+Public surface as in the reference: ``EvalMetric`` (update / update_dict /
+reset / reset_local / get / get_global / get_name_value /
+get_global_name_value / get_config), ``CompositeEvalMetric``, ``Accuracy``,
+``TopKAccuracy``, ``F1``, ``MCC``, ``Perplexity``, ``MAE``, ``MSE``, ``RMSE``,
+``CrossEntropy``, ``NegativeLogLikelihood``, ``PearsonCorrelation``, ``PCC``,
+``Loss`` (+ ``Torch`` / ``Caffe``), ``CustomMetric``, ``np``, ``create``,
+``register``, ``check_label_shapes``.
+
+Design notes:
+
+* every metric keeps two running (sum, count) pairs -- *local* (since the last
+  ``reset_local``) and *global* (since ``reset``) -- updated together by
+  ``_accumulate``;
+* classification metrics over device tensors reduce ON the device and
+  transfer one scalar per batch (argmax / top-k / gather run in torch);
+* F1, MCC and PCC share one ``_Confusion`` matrix accumulator (binary F1 /
+  MCC use its 2x2 form), with per-batch ("macro") or running ("micro")
+  averaging.
 """
 import math
 from collections import OrderedDict
@@ -21,28 +34,35 @@ __all__ = ['EvalMetric', 'CompositeEvalMetric', 'Accuracy', 'TopKAccuracy', 'F1'
 
 
 def check_label_shapes(labels, preds, wrap=False, shape=False):
-    if not shape:
-        label_shape, pred_shape = len(labels), len(preds)
-    else:
-        label_shape, pred_shape = labels.shape, preds.shape
-    if label_shape != pred_shape:
-        raise ValueError('Shape of labels {} does not match shape of predictions {}'.format(label_shape, pred_shape))
+    """Raise ValueError unless labels and preds agree in length (or full shape); optionally wrap
+    single arrays into lists."""
+    a, b = (labels.shape, preds.shape) if shape else (len(labels), len(preds))
+    if a != b:
+        raise ValueError('Shape of labels {} does not match shape of predictions {}'.format(a, b))
     if wrap:
-        if isinstance(labels, (NDArray, numpy.ndarray)):
-            labels = [labels]
-        if isinstance(preds, (NDArray, numpy.ndarray)):
-            preds = [preds]
+        single = (NDArray, numpy.ndarray)
+        labels = [labels] if isinstance(labels, single) else labels
+        preds = [preds] if isinstance(preds, single) else preds
     return labels, preds
 
 
-def _np(x):
-    if isinstance(x, NDArray):
-        return x.asnumpy()
-    return numpy.asarray(x)
+def _host(x):
+    return x.asnumpy() if isinstance(x, NDArray) else numpy.asarray(x)
+
+
+def _dev(x):
+    """A torch tensor view of an NDArray (no copy) or of host data."""
+    return x._data if isinstance(x, NDArray) else torch.as_tensor(numpy.asarray(x))
+
+
+def _pairs(names, values):
+    names = names if isinstance(names, list) else [names]
+    values = values if isinstance(values, list) else [values]
+    return list(zip(names, values))
 
 
 class EvalMetric:
-    """Base class for all evaluation metrics."""
+    """Base metric: ``update`` adds to the running sums, ``get`` reports sum / count."""
 
     def __init__(self, name, output_names=None, label_names=None, **kwargs):
         self.name = str(name)
@@ -56,180 +76,154 @@ class EvalMetric:
         return 'EvalMetric: {}'.format(dict(self.get_name_value()))
 
     def get_config(self):
-        config = self._kwargs.copy()
-        config.update({'metric': self.__class__.__name__, 'name': self.name, 'output_names': self.output_names,
-                       'label_names': self.label_names})
-        return config
+        cfg = dict(self._kwargs)
+        cfg.update(metric=type(self).__name__, name=self.name, output_names=self.output_names,
+                   label_names=self.label_names)
+        return cfg
+
+    # ---------------------------------------------------------------- feeding
+    @staticmethod
+    def _select(mapping, names):
+        return list(mapping.values()) if names is None else [mapping[n] for n in names]
 
     def update_dict(self, label, pred):
-        if self.output_names is not None:
-            pred = [pred[name] for name in self.output_names]
-        else:
-            pred = list(pred.values())
-        if self.label_names is not None:
-            label = [label[name] for name in self.label_names]
-        else:
-            label = list(label.values())
-        self.update(label, pred)
+        """Update from ``{name: array}`` dicts, picking ``label_names`` / ``output_names``."""
+        self.update(self._select(label, self.label_names), self._select(pred, self.output_names))
 
     def update(self, labels, preds):
-        raise NotImplementedError()
+        raise NotImplementedError('%s.update' % type(self).__name__)
+
+    def _accumulate(self, total, count):
+        self.sum_metric += total
+        self.num_inst += count
+        self.global_sum_metric += total
+        self.global_num_inst += count
+
+    _add = _accumulate     # short alias used by subclasses written against the older name
+
+    # ---------------------------------------------------------------- state
+    def reset_local(self):
+        self.sum_metric, self.num_inst = 0.0, 0
 
     def reset(self):
-        self.num_inst = 0
-        self.sum_metric = 0.0
-        self.global_num_inst = 0
-        self.global_sum_metric = 0.0
+        self.reset_local()
+        self.global_sum_metric, self.global_num_inst = 0.0, 0
 
-    def reset_local(self):
-        self.num_inst = 0
-        self.sum_metric = 0.0
+    # ---------------------------------------------------------------- reporting
+    def _value(self, total, count):
+        return float('nan') if count == 0 else total / count
 
     def get(self):
-        if self.num_inst == 0:
-            return (self.name, float('nan'))
-        return (self.name, self.sum_metric / self.num_inst)
+        return self.name, self._value(self.sum_metric, self.num_inst)
 
     def get_global(self):
-        if self._has_global_stats:
-            if self.global_num_inst == 0:
-                return (self.name, float('nan'))
-            return (self.name, self.global_sum_metric / self.global_num_inst)
-        return self.get()
+        if not self._has_global_stats:
+            return self.get()
+        return self.name, self._value(self.global_sum_metric, self.global_num_inst)
 
     def get_name_value(self):
-        name, value = self.get()
-        if not isinstance(name, list):
-            name = [name]
-        if not isinstance(value, list):
-            value = [value]
-        return list(zip(name, value))
+        return _pairs(*self.get())
 
     def get_global_name_value(self):
-        if self._has_global_stats:
-            name, value = self.get_global()
-            if not isinstance(name, list):
-                name = [name]
-            if not isinstance(value, list):
-                value = [value]
-            return list(zip(name, value))
-        return self.get_name_value()
-
-    def _add(self, s, n):
-        self.sum_metric += s
-        self.global_sum_metric += s
-        self.num_inst += n
-        self.global_num_inst += n
+        return _pairs(*self.get_global()) if self._has_global_stats else self.get_name_value()
 
 
+# ------------------------------------------------------------------------ registry
 _METRICS = {}
 
 
 def register(klass):
+    """Class decorator: make ``klass`` creatable by its lower-cased name."""
     _METRICS[klass.__name__.lower()] = klass
     return klass
 
 
 def alias(*aliases):
-    def reg(klass):
-        for a in aliases:
-            _METRICS[a.lower()] = klass
+    def deco(klass):
+        _METRICS.update({a.lower(): klass for a in aliases})
         return klass
-    return reg
+    return deco
 
 
 def create(metric, *args, **kwargs):
-    if callable(metric) and not isinstance(metric, type):
-        return CustomMetric(metric, *args, **kwargs)
-    if isinstance(metric, list):
-        composite_metric = CompositeEvalMetric()
-        for child_metric in metric:
-            composite_metric.add(create(child_metric, *args, **kwargs))
-        return composite_metric
+    """Metric from a name, class, instance, callable (CustomMetric) or list (composite)."""
     if isinstance(metric, EvalMetric):
         return metric
+    if isinstance(metric, list):
+        return CompositeEvalMetric([create(m, *args, **kwargs) for m in metric])
     if isinstance(metric, type) and issubclass(metric, EvalMetric):
         return metric(*args, **kwargs)
-    return _METRICS[metric.lower()](*args, **kwargs)
+    if callable(metric):
+        return CustomMetric(metric, *args, **kwargs)
+    try:
+        return _METRICS[metric.lower()](*args, **kwargs)
+    except KeyError:
+        raise ValueError('unknown metric %r; registered: %s' % (metric, sorted(_METRICS))) from None
 
 
+# ------------------------------------------------------------------------ composite
 @register
 @alias('composite')
 class CompositeEvalMetric(EvalMetric):
+    """Several metrics updated together; ``get`` returns parallel name / value lists."""
+
     def __init__(self, metrics=None, name='composite', output_names=None, label_names=None):
+        self.metrics = []
         super().__init__(name, output_names=output_names, label_names=label_names, has_global_stats=True)
-        if metrics is None:
-            metrics = []
-        self.metrics = [create(i) for i in metrics]
+        self.metrics = [create(m) for m in (metrics or [])]
 
     def add(self, metric):
         self.metrics.append(create(metric))
 
     def get_metric(self, index):
-        try:
-            return self.metrics[index]
-        except IndexError:
+        if not -len(self.metrics) <= index < len(self.metrics):
             return ValueError('Metric index {} is out of range 0 and {}'.format(index, len(self.metrics)))
+        return self.metrics[index]
 
     def update_dict(self, labels, preds):
-        if self.label_names is not None:
-            labels = OrderedDict([i for i in labels.items() if i[0] in self.label_names])
-        if self.output_names is not None:
-            preds = OrderedDict([i for i in preds.items() if i[0] in self.output_names])
-        for metric in self.metrics:
-            metric.update_dict(labels, preds)
+        keep = lambda d, names: d if names is None else OrderedDict((k, v) for k, v in d.items() if k in names)  # noqa
+        labels, preds = keep(labels, self.label_names), keep(preds, self.output_names)
+        for m in self.metrics:
+            m.update_dict(labels, preds)
 
     def update(self, labels, preds):
-        for metric in self.metrics:
-            metric.update(labels, preds)
+        for m in self.metrics:
+            m.update(labels, preds)
 
     def reset(self):
-        try:
-            for metric in self.metrics:
-                metric.reset()
-        except AttributeError:
-            pass
+        for m in getattr(self, 'metrics', []):
+            m.reset()
 
     def reset_local(self):
-        try:
-            for metric in self.metrics:
-                metric.reset_local()
-        except AttributeError:
-            pass
+        for m in getattr(self, 'metrics', []):
+            m.reset_local()
+
+    @staticmethod
+    def _gather(results):
+        names, values = [], []
+        for n, v in results:
+            names.extend([n] if isinstance(n, string_types) else n)
+            values.extend([v] if isinstance(v, numeric_types) else v)
+        return names, values
 
     def get(self):
-        names, values = [], []
-        for metric in self.metrics:
-            name, value = metric.get()
-            if isinstance(name, string_types):
-                name = [name]
-            if isinstance(value, numeric_types):
-                value = [value]
-            names.extend(name)
-            values.extend(value)
-        return (names, values)
+        return self._gather(m.get() for m in self.metrics)
 
     def get_global(self):
-        names, values = [], []
-        for metric in self.metrics:
-            name, value = metric.get_global()
-            if isinstance(name, string_types):
-                name = [name]
-            if isinstance(value, numeric_types):
-                value = [value]
-            names.extend(name)
-            values.extend(value)
-        return (names, values)
+        return self._gather(m.get_global() for m in self.metrics)
 
     def get_config(self):
-        config = super().get_config()
-        config.update({'metrics': [i.get_config() for i in self.metrics]})
-        return config
+        cfg = super().get_config()
+        cfg['metrics'] = [m.get_config() for m in self.metrics]
+        return cfg
 
 
+# ------------------------------------------------------------------------ classification
 @register
 @alias('acc')
 class Accuracy(EvalMetric):
+    """Fraction of correct predictions; class scores are arg-maxed over ``axis``."""
+
     def __init__(self, axis=1, name='accuracy', output_names=None, label_names=None):
         super().__init__(name, axis=axis, output_names=output_names, label_names=label_names,
                          has_global_stats=True)
@@ -237,242 +231,217 @@ class Accuracy(EvalMetric):
 
     def update(self, labels, preds):
         labels, preds = check_label_shapes(labels, preds, True)
-        for label, pred_label in zip(labels, preds):
-            if isinstance(pred_label, NDArray) and isinstance(label, NDArray):
-                p = pred_label._data
-                l = label._data
-                if p.shape != l.shape:
-                    p = torch.argmax(p, dim=self.axis)
-                p = p.reshape(-1).to(torch.int64)
-                l = l.reshape(-1).to(torch.int64).to(p.device)
-                if p.numel() != l.numel():
-                    raise ValueError('Shape of labels {} does not match shape of predictions {}'.format(
-                        l.shape, p.shape))
-                correct = int((p == l).sum())
-                self._add(correct, int(l.numel()))
-                continue
-            pred_label = _np(pred_label)
-            label = _np(label)
-            if pred_label.shape != label.shape:
-                pred_label = numpy.argmax(pred_label, axis=self.axis)
-            pred_label = pred_label.astype('int64').flat
-            label = label.astype('int64').flat
-            check_label_shapes(label, pred_label)
-            num_correct = (numpy.asarray(pred_label) == numpy.asarray(label)).sum()
-            self._add(num_correct, len(pred_label))
+        for label, pred in zip(labels, preds):
+            p, l = _dev(pred), _dev(label)
+            if p.shape != l.shape:
+                p = torch.argmax(p, dim=self.axis)
+            p = p.reshape(-1).to(torch.int64)
+            l = l.reshape(-1).to(device=p.device, dtype=torch.int64)
+            if p.numel() != l.numel():
+                raise ValueError('Shape of labels {} does not match shape of predictions {}'.format(
+                    tuple(l.shape), tuple(p.shape)))
+            self._accumulate(int((p == l).sum()), int(l.numel()))
 
 
 @register
 @alias('top_k_accuracy', 'top_k_acc')
 class TopKAccuracy(EvalMetric):
+    """A prediction counts as correct when the label is among the ``top_k`` highest scores."""
+
     def __init__(self, top_k=1, name='top_k_accuracy', output_names=None, label_names=None):
-        super().__init__(name, top_k=top_k, output_names=output_names, label_names=label_names,
+        if not top_k > 1:
+            raise AssertionError('Please use Accuracy if top_k is no more than 1')
+        super().__init__('%s_%d' % (name, top_k), top_k=top_k, output_names=output_names, label_names=label_names,
                          has_global_stats=True)
         self.top_k = top_k
-        assert self.top_k > 1, 'Please use Accuracy if top_k is no more than 1'
-        self.name += '_%d' % self.top_k
 
     def update(self, labels, preds):
         labels, preds = check_label_shapes(labels, preds, True)
-        for label, pred_label in zip(labels, preds):
-            assert len(pred_label.shape) <= 2, 'Predictions should be no more than 2 dims'
-            pred_label = numpy.argpartition(_np(pred_label).astype('float32'), -self.top_k)
-            label = _np(label).astype('int32')
-            check_label_shapes(label, pred_label)
-            num_samples = pred_label.shape[0]
-            num_dims = len(pred_label.shape)
-            if num_dims == 1:
-                self._add((pred_label.flat == label.flat).sum(), num_samples)
-            elif num_dims == 2:
-                num_classes = pred_label.shape[1]
-                top_k = min(num_classes, self.top_k)
-                s = 0
-                for j in range(top_k):
-                    s += (pred_label[:, num_classes - 1 - j].flat == label.flat).sum()
-                self._add(s, num_samples)
+        for label, pred in zip(labels, preds):
+            p = _dev(pred).float()
+            if p.dim() > 2:
+                raise AssertionError('Predictions should be no more than 2 dims')
+            l = _dev(label).to(device=p.device, dtype=torch.int64).reshape(-1)
+            check_label_shapes(l, p)
+            if p.dim() == 1:
+                hits = int((p.to(torch.int64) == l).sum())
+            else:
+                k = min(self.top_k, p.shape[1])
+                top = torch.topk(p, k, dim=1).indices
+                hits = int((top == l.unsqueeze(1)).any(dim=1).sum())
+            self._accumulate(hits, p.shape[0])
 
 
-class _BinaryClassificationMetrics:
-    def __init__(self):
-        self.true_positives = 0
-        self.false_negatives = 0
-        self.false_positives = 0
-        self.true_negatives = 0
-        self.global_true_positives = 0
-        self.global_false_negatives = 0
-        self.global_false_positives = 0
-        self.global_true_negatives = 0
+class _Confusion:
+    """Running k x k confusion matrices (rows: predicted class, cols: true class), local + global."""
 
-    def update_binary_stats(self, label, pred):
-        pred = _np(pred)
-        label = _np(label).astype('int32')
-        pred_label = numpy.argmax(pred, axis=1)
-        check_label_shapes(label, pred)
-        if len(numpy.unique(label)) > 2:
-            raise ValueError('%s currently only supports binary classification.' % self.__class__.__name__)
-        pred_true = (pred_label == 1)
-        pred_false = 1 - pred_true
-        label_true = (label == 1)
-        label_false = 1 - label_true
-        tp = (pred_true * label_true).sum()
-        fp = (pred_true * label_false).sum()
-        fn = (pred_false * label_true).sum()
-        tn = (pred_false * label_false).sum()
-        self.true_positives += tp
-        self.global_true_positives += tp
-        self.false_positives += fp
-        self.global_false_positives += fp
-        self.false_negatives += fn
-        self.global_false_negatives += fn
-        self.true_negatives += tn
-        self.global_true_negatives += tn
+    def __init__(self, k=2):
+        self.k = k
+        self.local = numpy.zeros((k, k))
+        self.glob = numpy.zeros((k, k))
 
-    @property
-    def precision(self):
-        d = self.true_positives + self.false_positives
-        return float(self.true_positives) / d if d > 0 else 0.
+    def grow(self, k):
+        if k > self.k:
+            pad = ((0, k - self.k), (0, k - self.k))
+            self.local = numpy.pad(self.local, pad)
+            self.glob = numpy.pad(self.glob, pad)
+            self.k = k
 
-    @property
-    def global_precision(self):
-        d = self.global_true_positives + self.global_false_positives
-        return float(self.global_true_positives) / d if d > 0 else 0.
+    def add(self, pred, label):
+        self.grow(int(max(pred.max(initial=0), label.max(initial=0))) + 1)
+        cm = numpy.zeros((self.k, self.k))
+        numpy.add.at(cm, (pred, label), 1)
+        self.local += cm
+        self.glob += cm
 
-    @property
-    def recall(self):
-        d = self.true_positives + self.false_negatives
-        return float(self.true_positives) / d if d > 0 else 0.
+    def clear_local(self):
+        self.local = numpy.zeros((self.k, self.k))
 
-    @property
-    def global_recall(self):
-        d = self.global_true_positives + self.global_false_negatives
-        return float(self.global_true_positives) / d if d > 0 else 0.
+    def clear(self):
+        self.clear_local()
+        self.glob = numpy.zeros((self.k, self.k))
 
-    @property
-    def fscore(self):
-        if self.precision + self.recall > 0:
-            return 2 * self.precision * self.recall / (self.precision + self.recall)
-        return 0.
 
-    @property
-    def global_fscore(self):
-        if self.global_precision + self.global_recall > 0:
-            return 2 * self.global_precision * self.global_recall / (self.global_precision + self.global_recall)
-        return 0.
+def _binary_counts(cm):
+    """(tp, fp, fn, tn) of a 2x2 confusion matrix (class 1 = positive)."""
+    return cm[1, 1], cm[1, 0], cm[0, 1], cm[0, 0]
 
-    def matthewscc(self, use_global=False):
-        if use_global:
-            if not self.global_total_examples:
-                return 0.
-            tp, fp, fn, tn = map(float, (self.global_true_positives, self.global_false_positives,
-                                         self.global_false_negatives, self.global_true_negatives))
-        else:
-            if not self.total_examples:
-                return 0.
-            tp, fp, fn, tn = map(float, (self.true_positives, self.false_positives, self.false_negatives,
-                                         self.true_negatives))
-        terms = [(tp + fp), (tp + fn), (tn + fp), (tn + fn)]
-        denom = 1.
-        for t in filter(lambda t: t != 0., terms):
+
+def _f1_of(cm):
+    tp, fp, fn, _tn = _binary_counts(cm)
+    prec = tp / (tp + fp) if tp + fp > 0 else 0.0
+    rec = tp / (tp + fn) if tp + fn > 0 else 0.0
+    return 2 * prec * rec / (prec + rec) if prec + rec > 0 else 0.0
+
+
+def _mcc_binary_of(cm):
+    if cm.sum() == 0:
+        return 0.0
+    tp, fp, fn, tn = _binary_counts(cm)
+    denom = 1.0
+    for t in (tp + fp, tp + fn, tn + fp, tn + fn):
+        if t != 0:
             denom *= t
-        return ((tp * tn) - (fp * fn)) / math.sqrt(denom)
-
-    @property
-    def total_examples(self):
-        return self.false_negatives + self.false_positives + self.true_negatives + self.true_positives
-
-    @property
-    def global_total_examples(self):
-        return (self.global_false_negatives + self.global_false_positives + self.global_true_negatives +
-                self.global_true_positives)
-
-    def local_reset_stats(self):
-        self.false_positives = 0
-        self.false_negatives = 0
-        self.true_positives = 0
-        self.true_negatives = 0
-
-    def reset_stats(self):
-        self.local_reset_stats()
-        self.global_false_positives = 0
-        self.global_false_negatives = 0
-        self.global_true_positives = 0
-        self.global_true_negatives = 0
+    return (tp * tn - fp * fn) / math.sqrt(denom)
 
 
-@register
-class F1(EvalMetric):
-    def __init__(self, name='f1', output_names=None, label_names=None, average='macro'):
+def _mcc_multiclass_of(cm):
+    n = cm.sum()
+    pred_tot, true_tot = cm.sum(axis=1), cm.sum(axis=0)
+    cov_pp = numpy.sum(pred_tot * (n - pred_tot))
+    cov_tt = numpy.sum(true_tot * (n - true_tot))
+    if cov_pp == 0 or cov_tt == 0:
+        return float('nan')
+    cov_pt = numpy.sum(cm.diagonal() * n - pred_tot * true_tot)
+    return cov_pt / math.sqrt(cov_pp * cov_tt)
+
+
+class _BinaryScore(EvalMetric):
+    """F1 / MCC over a binary confusion matrix.  'macro': mean of per-batch scores; 'micro': the
+    score of all examples seen so far."""
+
+    _score = None
+
+    def __init__(self, name, output_names, label_names, average):
         self.average = average
-        self.metrics = _BinaryClassificationMetrics()
+        self._cm = _Confusion(2)
         super().__init__(name=name, output_names=output_names, label_names=label_names, has_global_stats=True)
 
     def update(self, labels, preds):
         labels, preds = check_label_shapes(labels, preds, True)
         for label, pred in zip(labels, preds):
-            self.metrics.update_binary_stats(label, pred)
+            p, l = _host(pred), _host(label).astype('int32').ravel()
+            check_label_shapes(l, p)
+            if len(numpy.unique(l)) > 2:
+                raise ValueError('%s currently only supports binary classification.' % type(self).__name__)
+            cls = numpy.argmax(p, axis=1).astype('int64')
+            self._cm.grow(2)
+            cm = numpy.zeros((2, 2))
+            numpy.add.at(cm, ((cls == 1).astype('int64'), (l == 1).astype('int64')), 1)
+            self._cm.local += cm
+            self._cm.glob += cm
+        score = type(self)._score
         if self.average == 'macro':
-            self.sum_metric += self.metrics.fscore
-            self.global_sum_metric += self.metrics.global_fscore
-            self.num_inst += 1
-            self.global_num_inst += 1
-            self.metrics.reset_stats()
+            self._accumulate(score(self._cm.local), 1)    # local == global here: both hold this batch
+            self._cm.clear()
         else:
-            self.sum_metric = self.metrics.fscore * self.metrics.total_examples
-            self.global_sum_metric = self.metrics.global_fscore * self.metrics.global_total_examples
-            self.num_inst = self.metrics.total_examples
-            self.global_num_inst = self.metrics.global_total_examples
-
-    def reset(self):
-        self.sum_metric = 0.
-        self.num_inst = 0
-        self.global_num_inst = 0
-        self.global_sum_metric = 0.0
-        self.metrics.reset_stats()
+            nl, ng = self._cm.local.sum(), self._cm.glob.sum()
+            self.sum_metric, self.num_inst = score(self._cm.local) * nl, nl
+            self.global_sum_metric, self.global_num_inst = score(self._cm.glob) * ng, ng
 
     def reset_local(self):
-        self.sum_metric = 0.
-        self.num_inst = 0
-        self.metrics.local_reset_stats()
+        super().reset_local()
+        if hasattr(self, '_cm'):
+            self._cm.clear_local()
+
+    def reset(self):
+        super().reset()
+        if hasattr(self, '_cm'):
+            self._cm.clear()
 
 
 @register
-class MCC(EvalMetric):
+class F1(_BinaryScore):
+    _score = staticmethod(_f1_of)
+
+    def __init__(self, name='f1', output_names=None, label_names=None, average='macro'):
+        super().__init__(name, output_names, label_names, average)
+
+
+@register
+class MCC(_BinaryScore):
+    _score = staticmethod(_mcc_binary_of)
+
     def __init__(self, name='mcc', output_names=None, label_names=None, average='macro'):
-        self._average = average
-        self._metrics = _BinaryClassificationMetrics()
-        super().__init__(name=name, output_names=output_names, label_names=label_names, has_global_stats=True)
+        super().__init__(name, output_names, label_names, average)
+
+
+@register
+class PCC(EvalMetric):
+    """Multi-class Matthews correlation (Gorodkin's R_K) over a growing confusion matrix."""
+
+    def __init__(self, name='pcc', output_names=None, label_names=None, has_global_stats=True):
+        self._cm = _Confusion(2)
+        super().__init__(name=name, output_names=output_names, label_names=label_names,
+                         has_global_stats=has_global_stats)
+
+    @property
+    def k(self):
+        return self._cm.k
 
     def update(self, labels, preds):
         labels, preds = check_label_shapes(labels, preds, True)
         for label, pred in zip(labels, preds):
-            self._metrics.update_binary_stats(label, pred)
-        if self._average == 'macro':
-            self.sum_metric += self._metrics.matthewscc()
-            self.global_sum_metric += self._metrics.matthewscc(use_global=True)
-            self.num_inst += 1
-            self.global_num_inst += 1
-            self._metrics.reset_stats()
-        else:
-            self.sum_metric = self._metrics.matthewscc() * self._metrics.total_examples
-            self.global_sum_metric = self._metrics.matthewscc(use_global=True) * self._metrics.global_total_examples
-            self.num_inst = self._metrics.total_examples
-            self.global_num_inst = self._metrics.global_total_examples
+            l = _host(label).astype('int32', copy=False).ravel()
+            p = _host(pred)
+            if p.shape != l.shape:
+                p = (p.ravel() > 0.5) if p.shape[-1] == 1 else p.argmax(axis=1)
+            self._cm.add(p.astype('int64').ravel(), l.astype('int64'))
+        self.num_inst += 1
+        self.global_num_inst += 1
 
-    def reset(self):
-        self.sum_metric = 0.
-        self.num_inst = 0.
-        self.global_sum_metric = 0.
-        self.global_num_inst = 0.
-        self._metrics.reset_stats()
+    # sums are derived from the confusion matrices, never assigned
+    sum_metric = property(lambda self: _mcc_multiclass_of(self._cm.local) * self.num_inst, lambda self, v: None)
+    global_sum_metric = property(lambda self: _mcc_multiclass_of(self._cm.glob) * self.global_num_inst,
+                                 lambda self, v: None)
 
     def reset_local(self):
-        self.sum_metric = 0.
-        self.num_inst = 0.
-        self._metrics.local_reset_stats()
+        self.num_inst = 0
+        if hasattr(self, '_cm'):
+            self._cm.clear_local()
+
+    def reset(self):
+        self.reset_local()
+        self.global_num_inst = 0
+        if hasattr(self, '_cm'):
+            self._cm.clear()
 
 
+# ------------------------------------------------------------------------ probabilistic
 @register
 class Perplexity(EvalMetric):
+    """exp(mean negative log-likelihood of the labels), ignoring ``ignore_label`` positions."""
+
     def __init__(self, ignore_label, axis=-1, name='perplexity', output_names=None, label_names=None):
         super().__init__(name, ignore_label=ignore_label, output_names=output_names, label_names=label_names,
                          has_global_stats=True)
@@ -480,264 +449,171 @@ class Perplexity(EvalMetric):
         self.axis = axis
 
     def update(self, labels, preds):
-        assert len(labels) == len(preds)
-        loss = 0.
-        num = 0
+        if len(labels) != len(preds):
+            raise AssertionError('labels and preds differ in length')
+        nll, count = 0.0, 0
         for label, pred in zip(labels, preds):
-            assert label.size == pred.size / pred.shape[-1], \
-                'shape mismatch: %s vs. %s' % (label.shape, pred.shape)
-            p = pred._data if isinstance(pred, NDArray) else torch.as_tensor(numpy.asarray(pred))
-            l = label._data if isinstance(label, NDArray) else torch.as_tensor(numpy.asarray(label))
-            l = l.to(p.device).reshape(-1).to(torch.int64)
-            prob = torch.gather(p.reshape(-1, p.shape[-1]).float(), 1, l.clamp(min=0).unsqueeze(1)).reshape(-1)
-            if self.ignore_label is not None:
-                ignore = (l == self.ignore_label).to(prob.dtype)
-                num -= int(ignore.sum())
-                prob = prob * (1 - ignore) + ignore
-            loss -= float(torch.sum(torch.log(torch.clamp(prob, min=1e-10))))
-            num += prob.numel()
-        self._add(loss, num)
+            p = _dev(pred)
+            if label.size != p.numel() // p.shape[-1]:
+                raise AssertionError('shape mismatch: %s vs. %s' % (label.shape, tuple(p.shape)))
+            l = _dev(label).to(p.device).reshape(-1).to(torch.int64)
+            prob = p.reshape(-1, p.shape[-1]).float().gather(1, l.clamp(min=0).unsqueeze(1)).squeeze(1)
+            keep = torch.ones_like(prob, dtype=torch.bool) if self.ignore_label is None else l != self.ignore_label
+            prob = torch.where(keep, prob, torch.ones_like(prob))
+            nll -= float(torch.log(prob.clamp(min=1e-10)).sum())
+            count += int(keep.sum())
+        self._accumulate(nll, count)
 
-    def get(self):
-        if self.num_inst == 0:
-            return (self.name, float('nan'))
-        return (self.name, math.exp(self.sum_metric / self.num_inst))
-
-    def get_global(self):
-        if self.global_num_inst == 0:
-            return (self.name, float('nan'))
-        return (self.name, math.exp(self.global_sum_metric / self.global_num_inst))
+    def _value(self, total, count):
+        return float('nan') if count == 0 else math.exp(total / count)
 
 
-def _reg_metric(fn):
+class _PickedNLL(EvalMetric):
+    """Sum of -log(p[label] + eps) over examples (CrossEntropy / NLL)."""
+
+    def __init__(self, eps, name, output_names, label_names):
+        super().__init__(name, eps=eps, output_names=output_names, label_names=label_names, has_global_stats=True)
+        self.eps = eps
+
     def update(self, labels, preds):
         labels, preds = check_label_shapes(labels, preds, True)
         for label, pred in zip(labels, preds):
-            label = _np(label)
-            pred = _np(pred)
-            if len(label.shape) == 1:
-                label = label.reshape(label.shape[0], 1)
-            if len(pred.shape) == 1:
-                pred = pred.reshape(pred.shape[0], 1)
-            self._add(fn(label, pred), 1)
-    return update
-
-
-@register
-class MAE(EvalMetric):
-    def __init__(self, name='mae', output_names=None, label_names=None):
-        super().__init__(name, output_names=output_names, label_names=label_names, has_global_stats=True)
-
-    update = _reg_metric(lambda l, p: numpy.abs(l - p).mean())
-
-
-@register
-class MSE(EvalMetric):
-    def __init__(self, name='mse', output_names=None, label_names=None):
-        super().__init__(name, output_names=output_names, label_names=label_names, has_global_stats=True)
-
-    update = _reg_metric(lambda l, p: ((l - p) ** 2.0).mean())
-
-
-@register
-class RMSE(EvalMetric):
-    def __init__(self, name='rmse', output_names=None, label_names=None):
-        super().__init__(name, output_names=output_names, label_names=label_names, has_global_stats=True)
-
-    update = _reg_metric(lambda l, p: numpy.sqrt(((l - p) ** 2.0).mean()))
+            p = _dev(pred)
+            l = _dev(label).reshape(-1).to(device=p.device, dtype=torch.int64)
+            if l.shape[0] != p.shape[0]:
+                raise AssertionError('labels (%d) and predictions (%d) differ in count' % (l.shape[0], p.shape[0]))
+            picked = p.double()[torch.arange(l.shape[0], device=p.device), l]
+            self._accumulate(float(-torch.log(picked + self.eps).sum()), int(l.shape[0]))
 
 
 @register
 @alias('ce')
-class CrossEntropy(EvalMetric):
+class CrossEntropy(_PickedNLL):
     def __init__(self, eps=1e-12, name='cross-entropy', output_names=None, label_names=None):
-        super().__init__(name, eps=eps, output_names=output_names, label_names=label_names, has_global_stats=True)
-        self.eps = eps
-
-    def update(self, labels, preds):
-        labels, preds = check_label_shapes(labels, preds, True)
-        for label, pred in zip(labels, preds):
-            label = _np(label)
-            pred = _np(pred)
-            label = label.ravel()
-            assert label.shape[0] == pred.shape[0]
-            prob = pred[numpy.arange(label.shape[0]), numpy.int64(label)]
-            self._add((-numpy.log(prob + self.eps)).sum(), label.shape[0])
+        super().__init__(eps, name, output_names, label_names)
 
 
 @register
 @alias('nll_loss')
-class NegativeLogLikelihood(EvalMetric):
+class NegativeLogLikelihood(_PickedNLL):
     def __init__(self, eps=1e-12, name='nll-loss', output_names=None, label_names=None):
-        super().__init__(name, eps=eps, output_names=output_names, label_names=label_names, has_global_stats=True)
-        self.eps = eps
+        super().__init__(eps, name, output_names, label_names)
+
+
+# ------------------------------------------------------------------------ regression
+class _Regression(EvalMetric):
+    """Per-batch error statistic of (label, pred) as 2-D column arrays, averaged over batches."""
+
+    def _stat(self, diff):
+        raise NotImplementedError
+
+    def __init__(self, name, output_names, label_names):
+        super().__init__(name, output_names=output_names, label_names=label_names, has_global_stats=True)
 
     def update(self, labels, preds):
         labels, preds = check_label_shapes(labels, preds, True)
         for label, pred in zip(labels, preds):
-            label = _np(label)
-            pred = _np(pred)
-            label = label.ravel()
-            num_examples = pred.shape[0]
-            assert label.shape[0] == num_examples, (label.shape[0], num_examples)
-            prob = pred[numpy.arange(num_examples, dtype=numpy.int64), numpy.int64(label)]
-            self._add((-numpy.log(prob + self.eps)).sum(), num_examples)
+            l, p = _host(label), _host(pred)
+            l = l.reshape(l.shape[0], 1) if l.ndim == 1 else l
+            p = p.reshape(p.shape[0], 1) if p.ndim == 1 else p
+            self._accumulate(self._stat(l - p), 1)
+
+
+@register
+class MAE(_Regression):
+    def __init__(self, name='mae', output_names=None, label_names=None):
+        super().__init__(name, output_names, label_names)
+
+    def _stat(self, diff):
+        return numpy.abs(diff).mean()
+
+
+@register
+class MSE(_Regression):
+    def __init__(self, name='mse', output_names=None, label_names=None):
+        super().__init__(name, output_names, label_names)
+
+    def _stat(self, diff):
+        return numpy.square(diff).mean()
+
+
+@register
+class RMSE(_Regression):
+    def __init__(self, name='rmse', output_names=None, label_names=None):
+        super().__init__(name, output_names, label_names)
+
+    def _stat(self, diff):
+        return numpy.sqrt(numpy.square(diff).mean())
 
 
 @register
 @alias('pearsonr')
 class PearsonCorrelation(EvalMetric):
+    """Pearson r.  'macro': mean of per-batch correlations; 'micro': one correlation over all
+    values seen, from running (Welford) means / second moments and co-moment."""
+
     def __init__(self, name='pearsonr', output_names=None, label_names=None, average='macro'):
         self.average = average
         super().__init__(name, output_names=output_names, label_names=label_names, has_global_stats=True)
-        if self.average == 'micro':
-            self.reset_micro()
 
-    def reset_micro(self):
-        self._sse_p = 0
-        self._mean_p = 0
-        self._sse_l = 0
-        self._mean_l = 0
-        self._pred_nums = 0
-        self._label_nums = 0
-        self._conv = 0
+    def _reset_moments(self):
+        self._n = 0
+        self._mean_l = self._mean_p = 0.0
+        self._m2_l = self._m2_p = 0.0
+        self._co = 0.0
 
     def reset(self):
-        self.num_inst = 0
-        self.sum_metric = 0.0
-        self.global_num_inst = 0
-        self.global_sum_metric = 0.0
+        super().reset()
         if self.average == 'micro':
-            self.reset_micro()
+            self._reset_moments()
 
-    def update_variance(self, new_values, *aggregate):
-        count, mean, m_2 = aggregate
-        count += len(new_values)
-        delta = new_values - mean
-        mean += numpy.sum(delta / count)
-        delta_2 = new_values - mean
-        m_2 += numpy.sum(delta * delta_2)
-        return count, mean, m_2
+    reset_micro = _reset_moments
 
-    def update_cov(self, label, pred):
-        self._conv = self._conv + numpy.sum((label - self._mean_l) * (pred - self._mean_p))
+    @staticmethod
+    def _welford(x, n, mean, m2):
+        n2 = n + len(x)
+        d = x - mean
+        mean2 = mean + numpy.sum(d / n2)
+        return n2, mean2, m2 + numpy.sum(d * (x - mean2))
 
     def update(self, labels, preds):
         labels, preds = check_label_shapes(labels, preds, True)
         for label, pred in zip(labels, preds):
             check_label_shapes(label, pred, False, True)
-            label = _np(label).ravel().astype(numpy.float64)
-            pred = _np(pred).ravel().astype(numpy.float64)
+            l = _host(label).ravel().astype(numpy.float64)
+            p = _host(pred).ravel().astype(numpy.float64)
             if self.average == 'macro':
-                pearson_corr = numpy.corrcoef(pred, label)[0, 1]
-                self._add(pearson_corr, 1)
-            else:
-                self.global_num_inst += 1
-                self.num_inst += 1
-                self._label_nums, self._mean_l, self._sse_l = self.update_variance(
-                    label, self._label_nums, self._mean_l, self._sse_l)
-                self.update_cov(label, pred)
-                self._pred_nums, self._mean_p, self._sse_p = self.update_variance(
-                    pred, self._pred_nums, self._mean_p, self._sse_p)
+                self._accumulate(numpy.corrcoef(p, l)[0, 1], 1)
+                continue
+            self.num_inst += 1
+            self.global_num_inst += 1
+            n, self._mean_l, self._m2_l = self._welford(l, self._n, self._mean_l, self._m2_l)
+            # co-moment against the label mean AFTER this batch and the prediction mean BEFORE it
+            self._co += numpy.sum((l - self._mean_l) * (p - self._mean_p))
+            _, self._mean_p, self._m2_p = self._welford(p, self._n, self._mean_p, self._m2_p)
+            self._n = n
 
     def get(self):
         if self.num_inst == 0:
-            return (self.name, float('nan'))
+            return self.name, float('nan')
         if self.average == 'macro':
-            return (self.name, self.sum_metric / self.num_inst)
-        n = self._label_nums
-        pearsonr = self._conv / ((n - 1) * numpy.sqrt(self._sse_p / (n - 1)) * numpy.sqrt(self._sse_l / (n - 1)))
-        return (self.name, pearsonr)
+            return self.name, self.sum_metric / self.num_inst
+        dof = self._n - 1
+        return self.name, self._co / (dof * numpy.sqrt(self._m2_p / dof) * numpy.sqrt(self._m2_l / dof))
 
 
-@register
-class PCC(EvalMetric):
-    def __init__(self, name='pcc', output_names=None, label_names=None, has_global_stats=True):
-        self.k = 2
-        super().__init__(name=name, output_names=output_names, label_names=label_names,
-                         has_global_stats=has_global_stats)
-
-    def _grow(self, inc):
-        self.lcm = numpy.pad(self.lcm, ((0, inc), (0, inc)), 'constant', constant_values=(0))
-        self.gcm = numpy.pad(self.gcm, ((0, inc), (0, inc)), 'constant', constant_values=(0))
-        self.k += inc
-
-    def _calc_mcc(self, cmat):
-        n = cmat.sum()
-        x = cmat.sum(axis=1)
-        y = cmat.sum(axis=0)
-        cov_xx = numpy.sum(x * (n - x))
-        cov_yy = numpy.sum(y * (n - y))
-        if cov_xx == 0 or cov_yy == 0:
-            return float('nan')
-        i = cmat.diagonal()
-        cov_xy = numpy.sum(i * n - x * y)
-        return cov_xy / (cov_xx * cov_yy) ** 0.5
-
-    def update(self, labels, preds):
-        labels, preds = check_label_shapes(labels, preds, True)
-        for label, pred in zip(labels, preds):
-            label = _np(label).astype('int32', copy=False).ravel()
-            pred = _np(pred)
-            if pred.shape != label.shape:
-                if pred.shape[-1] == 1:
-                    pred = (pred.ravel() > 0.5).astype('int32')
-                else:
-                    pred = pred.argmax(axis=1)
-            pred = pred.astype('int32', copy=False).ravel()
-            n = max(pred.max(), label.max())
-            if n >= self.k:
-                self._grow(n + 1 - self.k)
-            bcm = numpy.zeros((self.k, self.k))
-            for i, j in zip(pred, label):
-                bcm[i, j] += 1
-            self.lcm += bcm
-            self.gcm += bcm
-        self.num_inst += 1
-        self.global_num_inst += 1
-
-    @property
-    def sum_metric(self):
-        return self._calc_mcc(self.lcm) * self.num_inst
-
-    @sum_metric.setter
-    def sum_metric(self, v):
-        pass
-
-    @property
-    def global_sum_metric(self):
-        return self._calc_mcc(self.gcm) * self.global_num_inst
-
-    @global_sum_metric.setter
-    def global_sum_metric(self, v):
-        pass
-
-    def reset(self):
-        self.global_num_inst = 0.
-        self.gcm = numpy.zeros((self.k, self.k))
-        self.reset_local()
-
-    def reset_local(self):
-        self.num_inst = 0.
-        self.lcm = numpy.zeros((self.k, self.k))
-
-
+# ------------------------------------------------------------------------ losses / custom
 @register
 class Loss(EvalMetric):
-    """Mean of the given loss values."""
+    """Mean of the loss values given as predictions (labels are ignored)."""
 
     def __init__(self, name='loss', output_names=None, label_names=None):
         super().__init__(name, output_names=output_names, label_names=label_names, has_global_stats=True)
 
     def update(self, _, preds):
-        if isinstance(preds, NDArray):
-            preds = [preds]
-        for pred in preds:
-            if isinstance(pred, NDArray):
-                loss = float(pred._data.detach().float().sum())
-            else:
-                loss = float(numpy.sum(pred))
-            self._add(loss, pred.size)
+        for pred in ([preds] if isinstance(preds, NDArray) else preds):
+            total = float(pred._data.detach().double().sum()) if isinstance(pred, NDArray) else float(numpy.sum(pred))
+            self._accumulate(total, pred.size)
 
 
 @register
@@ -754,11 +630,12 @@ class Caffe(Loss):
 
 @register
 class CustomMetric(EvalMetric):
+    """Metric from ``feval(label_np, pred_np)`` returning a value or ``(sum, count)``."""
+
     def __init__(self, feval, name=None, allow_extra_outputs=False, output_names=None, label_names=None):
         if name is None:
             name = feval.__name__
-            if name.find('<') != -1:
-                name = 'custom(%s)' % name
+            name = 'custom(%s)' % name if '<' in name else name
         super().__init__(name, feval=feval, allow_extra_outputs=allow_extra_outputs, output_names=output_names,
                          label_names=label_names, has_global_stats=True)
         self._feval = feval
@@ -768,20 +645,15 @@ class CustomMetric(EvalMetric):
         if not self._allow_extra_outputs:
             labels, preds = check_label_shapes(labels, preds, True)
         for pred, label in zip(preds, labels):
-            label = _np(label)
-            pred = _np(pred)
-            reval = self._feval(label, pred)
-            if isinstance(reval, tuple):
-                (sum_metric, num_inst) = reval
-                self._add(sum_metric, num_inst)
-            else:
-                self._add(reval, 1)
+            res = self._feval(_host(label), _host(pred))
+            self._accumulate(*(res if isinstance(res, tuple) else (res, 1)))
 
     def get_config(self):
         raise NotImplementedError('CustomMetric cannot be serialized')
 
 
 def np(numpy_feval, name=None, allow_extra_outputs=False):
+    """CustomMetric from a function of numpy arrays."""
     def feval(label, pred):
         return numpy_feval(label, pred)
     feval.__name__ = numpy_feval.__name__
