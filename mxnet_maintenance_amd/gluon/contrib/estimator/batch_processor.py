@@ -1,4 +1,8 @@
-"""Per-batch train / evaluate hooks of the Estimator (parity: gluon/contrib/estimator/batch_processor.py)."""
+"""One training / validation step of the Estimator (API parity: gluon/contrib/estimator/batch_processor.py).
+
+Subclass and override ``fit_batch`` / ``evaluate_batch`` to customise the step;
+both return ``(data, label, pred, loss)`` as per-device lists.
+"""
 from .... import autograd
 from ...utils import split_and_load
 
@@ -6,24 +10,23 @@ __all__ = ['BatchProcessor']
 
 
 class BatchProcessor:
-    """Override ``fit_batch`` / ``evaluate_batch`` to customise one training / validation step."""
-
     def _get_data_and_label(self, batch, ctx, batch_axis=0):
-        data = split_and_load(batch[0], ctx_list=ctx, batch_axis=batch_axis)
-        label = split_and_load(batch[1], ctx_list=ctx, batch_axis=batch_axis)
-        return data, label
+        """Split ``(data, label)`` of a batch across the estimator's devices."""
+        return tuple(split_and_load(part, ctx_list=ctx, batch_axis=batch_axis) for part in batch[:2])
+
+    @staticmethod
+    def _run(net, loss_fn, data, label):
+        pred = [net(x) for x in data]
+        return pred, [loss_fn(p, y) for p, y in zip(pred, label)]
 
     def evaluate_batch(self, estimator, val_batch, batch_axis=0):
         data, label = self._get_data_and_label(val_batch, estimator.context, batch_axis)
-        pred = [estimator.val_net(x) for x in data]
-        loss = [estimator.val_loss(y_hat, y) for y_hat, y in zip(pred, label)]
+        pred, loss = self._run(estimator.val_net, estimator.val_loss, data, label)
         return data, label, pred, loss
 
     def fit_batch(self, estimator, train_batch, batch_axis=0):
         data, label = self._get_data_and_label(train_batch, estimator.context, batch_axis)
         with autograd.record():
-            pred = [estimator.net(x) for x in data]
-            loss = [estimator.loss(y_hat, y) for y_hat, y in zip(pred, label)]
-        for l in loss:
-            l.backward()
+            pred, loss = self._run(estimator.net, estimator.loss, data, label)
+        autograd.backward(loss)
         return data, label, pred, loss
