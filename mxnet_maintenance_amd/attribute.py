@@ -1,41 +1,27 @@
-"""Symbol attribute scoping (parity: python/mxnet/attribute.py)."""
-import threading
+"""Symbol attribute scopes (API parity: python/mxnet/attribute.py).
+
+``with AttrScope(ctx_group='dev1', lr_mult='0.1'): ...`` attaches string
+attributes to every symbol created inside; nested scopes merge outer and inner
+attributes (inner wins), and explicit attributes passed to a symbol win over
+both.
+"""
+from ._scope import _ThreadScope
+
+__all__ = ['AttrScope']
 
 
-class AttrScope:
-    """Attach attributes (e.g. ``ctx_group``, ``lr_mult``) to symbols created in scope."""
-    _current = threading.local()
-
+class AttrScope(_ThreadScope):
     def __init__(self, **kwargs):
-        self._old_scope = None
-        for value in kwargs.values():
-            if not isinstance(value, str):
-                raise ValueError('Attributes need to be string')
-        self._attr = kwargs
+        bad = [k for k, v in kwargs.items() if not isinstance(v, str)]
+        if bad:
+            raise ValueError('Attributes need to be string (got non-string %s)' % bad)
+        self._attr = dict(kwargs)
 
     def get(self, attr):
-        if self._attr:
-            ret = self._attr.copy()
-            if attr:
-                ret.update(attr)
-            return ret
-        return attr if attr else {}
+        """Scope attributes overlaid with the explicit ``attr`` dict."""
+        merged = dict(self._attr)
+        merged.update(attr or {})
+        return merged
 
-    def __enter__(self):
-        if not hasattr(AttrScope._current, 'value'):
-            AttrScope._current.value = AttrScope()
-        self._old_scope = AttrScope._current.value
-        attr = AttrScope._current.value._attr.copy()
-        attr.update(self._attr)
-        self._attr = attr
-        AttrScope._current.value = self
-        return self
-
-    def __exit__(self, ptype, value, trace):
-        AttrScope._current.value = self._old_scope
-
-    @staticmethod
-    def current():
-        if not hasattr(AttrScope._current, 'value'):
-            AttrScope._current.value = AttrScope()
-        return AttrScope._current.value
+    def _on_enter(self, outer):
+        self._attr = dict(outer._attr, **self._attr)
