@@ -8,7 +8,7 @@ import numbers
 import numpy as np
 import torch
 
-__all__ = ['MXNetError', 'numeric_types', 'integer_types', 'string_types',
+__all__ = ['MXNetError', 'numeric_types', 'integer_types', 'string_types', 'py_str', 'mx_real_t', '_as_list',
            'np_dtype', 'torch_dtype', 'dtype_to_flag', 'flag_to_dtype']
 
 
@@ -36,6 +36,22 @@ class NotImplementedForSymbol(MXNetError):
 numeric_types = (float, int, np.generic, numbers.Number)
 integer_types = (int, np.integer)
 string_types = (str,)
+py_str = lambda x: x.decode('utf-8') if isinstance(x, bytes) else x     # noqa: E731  (bytes from C -> str)
+mx_real_t = np.float32                                                  # default real type
+mx_uint = np.uint32
+mx_int = np.int32
+
+
+def _as_list(obj):
+    """``obj`` if it is a list, else ``[obj]``."""
+    return obj if isinstance(obj, list) else [obj]
+
+
+def check_call(ret):
+    """C-API status check of the reference; here native calls raise directly, so only non-zero
+    integers are reported."""
+    if isinstance(ret, int) and ret != 0:
+        raise MXNetError('native call failed with status %d' % ret)
 
 # MXNet type flags (include/mxnet/base.h / mshadow type_flag). These values are
 # part of the on-disk .params format, so they must match the reference exactly.

@@ -140,11 +140,27 @@ class Executor:
             self.aux_arrays = list(aux_states)
         if len(self.aux_arrays) != len(aux_names):
             raise MXNetError('bind: expected %d aux states, got %d' % (len(aux_names), len(self.aux_arrays)))
-        self.outputs = []
+        self.outputs = self._preallocate_outputs()
         self._leaves = None
         self._out_tensors = None
         self._monitor_cb = None
         self._monitor_all = False
+
+    def _preallocate_outputs(self):
+        """Output arrays allocated at bind time (as the reference's graph executor does), so
+        ``outputs`` exist before the first forward and a reshaped executor can alias them."""
+        from . import ndarray as nd
+        try:
+            shapes = {n: a.shape for n, a in zip(self._symbol.list_arguments(), self.arg_arrays)}
+            _, out_shapes, _ = self._symbol.infer_shape(**shapes)
+            _, out_types, _ = self._symbol.infer_type(**{n: a.dtype for n, a in
+                                                          zip(self._symbol.list_arguments(), self.arg_arrays)})
+        except Exception:   # pylint: disable=broad-except
+            return []
+        if not out_shapes or any(s is None for s in out_shapes):
+            return []
+        return [nd.zeros(tuple(s), ctx=self._ctx, dtype=t if t is not None else 'float32')
+                for s, t in zip(out_shapes, out_types or [None] * len(out_shapes))]
 
     @property
     def arg_dict(self):
@@ -203,7 +219,14 @@ class Executor:
             _state.STATE.training = prev_train
         self._leaves = leaves
         self._out_tensors = outs
-        self.outputs = [NDArray(o.detach()) for o in outs]
+        if len(self.outputs) == len(outs) and all(
+                b.shape == tuple(o.shape) and b._data.dtype == o.dtype for b, o in zip(self.outputs, outs)):
+            # write into the bind-time output arrays (they may be views shared with a reshaped executor)
+            with torch.no_grad():
+                for b, o in zip(self.outputs, outs):
+                    b._data.copy_(o.detach())
+        else:
+            self.outputs = [NDArray(o.detach()) for o in outs]
         return self.outputs
 
     def backward(self, out_grads=None, is_train=True):
@@ -261,7 +284,56 @@ class Executor:
                     raise ValueError('Find name %s that is not in the auxiliary states' % name)
 
     def reshape(self, partial_shaping=False, allow_up_sizing=False, **kwargs):
-        return self._symbol.simple_bind(self._ctx, grad_req=self._grad_req, **kwargs)
+        """A new executor for new input shapes that shares memory with this one.
+
+        Arrays whose shape is unchanged (typically the weights) are the same
+        NDArrays; arrays that shrink become views of this executor's storage;
+        arrays that grow are freshly allocated, which needs ``allow_up_sizing``.
+        Output arrays are aliased the same way.
+        """
+        from .ndarray.ndarray import NDArray
+        from . import ndarray as nd
+        sym = self._symbol
+        known = {n: a.shape for n, a in zip(sym.list_arguments(), self.arg_arrays)}
+        for k in kwargs:
+            if k not in known:
+                raise MXNetError('reshape: %s is not an argument of the symbol' % k)
+        if not partial_shaping:
+            known = {k: v for k, v in known.items() if k not in kwargs}
+            known.update(kwargs)
+        else:
+            known.update(kwargs)
+        arg_shapes, out_shapes, aux_shapes = sym.infer_shape(**known)
+
+        def fit(old, shape, what):
+            if old is None:
+                return None
+            shape = tuple(shape)
+            if shape == tuple(old.shape):
+                return old
+            n = 1
+            for d in shape:
+                n *= d
+            if n <= old.size:
+                return NDArray(old._data.reshape(-1)[:n].view(shape))
+            if not allow_up_sizing:
+                raise MXNetError('reshape: %s grows from %s to %s; pass allow_up_sizing=True'
+                                 % (what, old.shape, shape))
+            return nd.zeros(shape, ctx=old.context, dtype=old.dtype)
+
+        names = sym.list_arguments()
+        args = [fit(a, s, n) for a, s, n in zip(self.arg_arrays, arg_shapes, names)]
+        grads = [fit(g, s, n + '_grad') for g, s, n in zip(self.grad_arrays, arg_shapes, names)]
+        auxs = [fit(a, s, n) for a, s, n in zip(self.aux_arrays, aux_shapes, sym.list_auxiliary_states())]
+        exe = Executor(sym, self._ctx, args, grads if any(g is not None for g in grads) else None,
+                       dict(self._grad_req), auxs)
+        if len(self.outputs) == len(out_shapes):
+            try:
+                exe.outputs = [fit(o, s, 'output') for o, s in zip(self.outputs, out_shapes)]
+            except MXNetError:
+                pass
+        exe._monitor_cb, exe._monitor_all = self._monitor_cb, self._monitor_all
+        return exe
 
     def debug_str(self):
         return self._symbol.debug_str()

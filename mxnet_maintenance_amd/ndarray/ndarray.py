@@ -17,7 +17,24 @@ from ..base import (MXNetError, numeric_types, integer_types, torch_dtype, np_dt
                     dtype_name)
 from ..context import Context, current_context, context_from_torch
 
-__all__ = ['NDArray', 'array', 'empty', 'zeros', 'ones', 'full', 'arange', 'linspace',
+def _shares_storage(a, b):
+    try:
+        return a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()
+    except RuntimeError:
+        return False
+
+
+# storage type ids of the reference C API (include/mxnet/ndarray.h NDArrayStorageType)
+_STORAGE_TYPE_UNDEFINED = -1
+_STORAGE_TYPE_DEFAULT = 0
+_STORAGE_TYPE_ROW_SPARSE = 1
+_STORAGE_TYPE_CSR = 2
+_STORAGE_TYPE_STR_TO_ID = {'undefined': _STORAGE_TYPE_UNDEFINED, 'default': _STORAGE_TYPE_DEFAULT,
+                           'row_sparse': _STORAGE_TYPE_ROW_SPARSE, 'csr': _STORAGE_TYPE_CSR}
+_STORAGE_TYPE_ID_TO_STR = {v: k for k, v in _STORAGE_TYPE_STR_TO_ID.items()}
+py_slice = slice       # the reference keeps the builtin under this name (``slice`` is an op there)
+
+__all__ = ['NDArray', 'CachedOp', 'array', 'empty', 'zeros', 'ones', 'full', 'arange', 'linspace',
            'concatenate', 'moveaxis', 'waitall', 'from_numpy', 'from_dlpack', 'to_dlpack_for_read',
            'to_dlpack_for_write', 'eye', 'maximum', 'minimum', 'add', 'subtract', 'multiply',
            'divide', 'modulo', 'power', 'equal', 'not_equal', 'greater', 'greater_equal',
@@ -127,7 +144,7 @@ class NDArray:
     def __bool__(self):
         n = self.size
         if n == 0:
-            raise ValueError('The truth value of an empty array is ambiguous')
+            return False            # reference: an empty NDArray is falsy
         if n == 1:
             return bool(self._data.reshape(-1)[0].item())
         raise ValueError('The truth value of an NDArray with multiple elements is ambiguous.')
@@ -313,6 +330,8 @@ class NDArray:
         key = _convert_key(key)
         if isinstance(value, NDArray):
             v = value._data
+        elif isinstance(value, np.generic):
+            v = value.item()
         elif isinstance(value, numeric_types):
             v = value
         else:
@@ -349,6 +368,11 @@ class NDArray:
         reverse = kwargs.get('reverse', False)
         from ..ops.tensor import infer_reshape
         new = infer_reshape(self.shape, shape, reverse)
+        n = 1
+        for d in new:
+            n *= d
+        if n != self.size:
+            raise ValueError('cannot reshape array of size %d into shape %s' % (self.size, tuple(new)))
         return _invoke_unary(lambda t: t.reshape(new), self)
 
     def reshape_like(self, *args, **kwargs):
@@ -366,14 +390,44 @@ class NDArray:
     def broadcast_like(self, other):
         return _op('broadcast_like', self, other)
 
+    @staticmethod
+    def _basic_indexing_slice_is_contiguous(slc_key, shape):
+        """Whether ``x[slc_key]`` (one slice per axis) of a C-contiguous ``x`` is contiguous: after
+        dropping length-1 axes, each remaining axis must step by exactly the product of the
+        lengths of the axes after it."""
+        lens, steps = [], []
+        stride = 1
+        for slc, n in reversed(list(zip(slc_key, shape))):
+            start, stop, step = slc.indices(n)
+            length = len(range(start, stop, step))
+            if length == 0:
+                return True
+            lens.append(length)
+            steps.append(stride * step)
+            stride *= n
+        expect = 1
+        for length, st in zip(lens, steps):      # innermost first
+            if length == 1:
+                continue
+            if st != expect:
+                return False
+            expect *= length
+        return True
+
+    # shape-only views: ``inplace=True`` shares storage with self, otherwise the result is a copy
+    def _maybe_copy(self, out, inplace):
+        if inplace or not _shares_storage(out._data, self._data):
+            return out
+        return _invoke_unary(lambda t: t.clone(), out)
+
     def flatten(self, inplace=False):
-        return _op('Flatten', self)
+        return self._maybe_copy(_op('Flatten', self), inplace)
 
     def expand_dims(self, axis, inplace=False):
-        return _op('expand_dims', self, axis=axis)
+        return self._maybe_copy(_op('expand_dims', self, axis=axis), inplace)
 
     def squeeze(self, axis=None, inplace=False):
-        return _op('squeeze', self, axis=axis)
+        return self._maybe_copy(_op('squeeze', self, axis=axis), inplace)
 
     def transpose(self, *axes, **kwargs):
         if len(axes) == 1 and isinstance(axes[0], (list, tuple)):
@@ -650,7 +704,14 @@ def array(source_array, ctx=None, dtype=None):
 
 
 def from_numpy(ndarray, zero_copy=True):
-    return NDArray(torch.from_numpy(ndarray))
+    """NDArray over a numpy array.  With ``zero_copy`` the memory is shared and the numpy array
+    becomes read-only (as in the reference, which takes ownership of the buffer)."""
+    if not zero_copy:
+        return NDArray(torch.from_numpy(np.array(ndarray, copy=True)))
+    src = np.ascontiguousarray(ndarray)
+    t = torch.from_numpy(src)
+    ndarray.flags.writeable = False
+    return NDArray(t)
 
 
 def from_dlpack(dlpack):
@@ -665,25 +726,33 @@ def to_dlpack_for_write(data):
     return data.to_dlpack_for_write()
 
 
+def _into(out, result):
+    """Honour an ``out=`` argument of the creation functions."""
+    if out is None:
+        return result
+    out[:] = result
+    return out
+
+
 def empty(shape, ctx=None, dtype=None, stype=None):
     if isinstance(shape, int):
         shape = (shape,)
     return NDArray(torch.empty(shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device))
 
 
-def zeros(shape, ctx=None, dtype=None, stype=None, **kwargs):
+def zeros(shape, ctx=None, dtype=None, stype=None, out=None, **kwargs):
     if isinstance(shape, int):
         shape = (shape,)
     if stype not in (None, 'default'):
         from . import sparse
         return sparse.zeros(stype, shape, ctx=ctx, dtype=dtype)
-    return NDArray(torch.zeros(shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device))
+    return _into(out, NDArray(torch.zeros(shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device)))
 
 
-def ones(shape, ctx=None, dtype=None, **kwargs):
+def ones(shape, ctx=None, dtype=None, out=None, **kwargs):
     if isinstance(shape, int):
         shape = (shape,)
-    return NDArray(torch.ones(shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device))
+    return _into(out, NDArray(torch.ones(shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device)))
 
 
 def full(shape, val, ctx=None, dtype=np.float32, out=None):
@@ -725,7 +794,10 @@ def concatenate(arrays, axis=0, always_copy=True):
 
 
 def moveaxis(tensor, source, destination):
-    return NDArray(torch.movedim(tensor._data, source, destination).contiguous())
+    """Move axes ``source`` to positions ``destination`` (ints or sequences of ints)."""
+    def norm(a):
+        return tuple(a) if isinstance(a, (list, tuple, range)) else a
+    return NDArray(torch.movedim(tensor._data, norm(source), norm(destination)).contiguous())
 
 
 def waitall():
@@ -838,3 +910,35 @@ def logical_xor(lhs, rhs):
 
 def negative(arr):
     return _op('negative', arr)
+
+
+class CachedOp:
+    """Imperative handle on a Symbol graph (reference ``mx.nd.CachedOp``, src/imperative/cached_op.cc).
+
+    ``op(*inputs, out=None)`` feeds the NDArrays in ``sym.list_inputs()`` order
+    through the graph's slot program; under ``autograd.record()`` the run is
+    taped like any imperative op, so gradients reach the inputs.
+    """
+
+    def __init__(self, sym, flags=()):
+        from ..executor import GraphProgram
+        self._sym = sym
+        self._flags = dict(flags)
+        self._prog = GraphProgram(sym)
+        self._names = sym.list_inputs()
+
+    def __call__(self, *args, **kwargs):
+        from .register import _run, _note_leaves
+        out = kwargs.pop('out', None)
+        if len(args) != len(self._names):
+            raise MXNetError('CachedOp expects %d inputs (%s), got %d' % (len(self._names), self._names, len(args)))
+        _note_leaves(list(args))
+        names = self._names
+        outs = _run(lambda *ts: self._prog.run(dict(zip(names, ts))), [a._data for a in args], {})
+        res = [NDArray(o) for o in outs]
+        if out is not None:
+            outs_l = out if isinstance(out, (list, tuple)) else [out]
+            for dst, src in zip(outs_l, res):
+                dst[:] = src
+            return out
+        return res[0] if len(res) == 1 else res

@@ -42,16 +42,16 @@ class Optimizer:
                  aggregate_num=None, use_fused_step=None, **kwargs):
         self.rescale_grad = rescale_grad
         self.lr_scheduler = lr_scheduler
-        if learning_rate is None:
-            learning_rate = 0.01
         if self.lr_scheduler is None:
-            self.lr = learning_rate
+            self.lr = 0.01 if learning_rate is None else learning_rate
         else:
-            if lr_scheduler.base_lr != learning_rate:
-                warnings.warn('learning rate from ``lr_scheduler`` has been overwritten by ``learning_rate`` in '
-                              'optimizer.', UserWarning)
-            self.lr_scheduler.base_lr = learning_rate
-            self.lr = learning_rate
+            # an explicit learning_rate overrides the scheduler's base_lr; otherwise the scheduler's is used
+            if learning_rate is not None:
+                if lr_scheduler.base_lr != learning_rate:
+                    warnings.warn('learning rate from ``lr_scheduler`` has been overwritten by ``learning_rate`` '
+                                  'in optimizer.', UserWarning)
+                self.lr_scheduler.base_lr = learning_rate
+            self.lr = self.lr_scheduler.base_lr
         self.wd = wd
         self.lr_mult = {}
         self.wd_mult = {}

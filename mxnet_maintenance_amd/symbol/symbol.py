@@ -527,7 +527,10 @@ def _create(op_name, inputs, attrs, name=None, attr=None):
     else:
         pos, named = inputs, {}
     all_names = arg_names + aux_names
-    var_attrs = {k: v for k, v in (scope_attr or {}).items() if k.startswith('__') and k.endswith('__')}
+    # hidden attributes (lr_mult, wd_mult, ctx_group, ... from the call or the AttrScope) are inherited by the
+    # variables created for missing inputs, like nnvm's Compose does for the op's auto-named arguments
+    var_attrs = {(k if k.startswith('__') and k.endswith('__') else '__%s__' % k): v
+                 for k, v in (scope_attr or {}).items()}
     for i, an in enumerate(all_names):
         s = None
         if i < len(pos):

@@ -13,12 +13,19 @@ import sys
 from contextlib import contextmanager
 
 import numpy as np
+import numpy.random as rnd            # noqa: F401  (re-exported, as the reference module does)
+import numpy.testing as npt           # noqa: F401
+from collections import OrderedDict   # noqa: F401
 
 from . import ndarray as nd
 from . import symbol as sym_mod
 from .base import MXNetError
 from .context import Context, cpu, gpu, current_context
-from .ndarray.ndarray import NDArray
+from .ndarray import array            # noqa: F401  (tests use it via ``from mxnet.test_utils import *``)
+from .ndarray.ndarray import NDArray, _STORAGE_TYPE_STR_TO_ID   # noqa: F401
+from .symbol import Symbol            # noqa: F401
+from .util import use_np, getenv, setenv   # noqa: F401
+from .runtime import Features         # noqa: F401
 
 _default_ctx = [None]
 
@@ -838,3 +845,201 @@ def assert_raises_cudnn_not_satisfied(min_version):
     def test_helper(orig_test):
         return orig_test
     return test_helper
+
+
+# ---------------------------------------------------------------------------------------------
+# small array builders / elementwise helpers used across the reference unit tests
+# ---------------------------------------------------------------------------------------------
+
+def assign_each(the_input, function):
+    """``function`` applied to every element of a numpy array (identity copy when None)."""
+    arr = np.asarray(the_input)
+    if function is None:
+        return np.array(arr)
+    return np.vectorize(function, otypes=[np.float64])(arr) if arr.size else np.zeros(arr.shape)
+
+
+def assign_each2(input1, input2, function):
+    """``function(a, b)`` over matching elements of two same-shape numpy arrays."""
+    a, b = np.asarray(input1), np.asarray(input2)
+    if function is None:
+        return np.array(a)
+    if a.shape != b.shape:
+        raise AssertionError('assign_each2: shapes differ: %s vs %s' % (a.shape, b.shape))
+    return np.vectorize(function, otypes=[np.float64])(a, b) if a.size else np.zeros(a.shape)
+
+
+def create_vector(size, dtype=np.int64):
+    """0 .. size-1 as an NDArray (large-tensor tests)."""
+    return nd.arange(0, size, dtype=dtype)
+
+
+def create_2d_tensor(rows, columns, dtype=np.int64):
+    """rows x columns NDArray whose row i is filled with i."""
+    return nd.broadcast_to(nd.arange(0, rows, dtype=dtype).reshape((rows, 1)), shape=(rows, columns))
+
+
+def get_identity_mat(size):
+    return nd.array(np.eye(size, dtype=np.float32))
+
+
+def get_identity_mat_batch(size):
+    eye = np.eye(size, dtype=np.float32)
+    return nd.array(np.stack([eye, eye]))
+
+
+def shuffle_csr_column_indices(csr):
+    """Shuffle the column indices inside every row of a CSR matrix (unordered-index validation)."""
+    indptr = np.asarray(csr.indptr.asnumpy() if hasattr(csr.indptr, 'asnumpy') else csr.indptr)
+    for row in range(len(indptr) - 1):
+        lo, hi = int(indptr[row]), int(indptr[row + 1])
+        seg = np.array(csr.indices[lo:hi].asnumpy() if hasattr(csr.indices, 'asnumpy') else csr.indices[lo:hi])
+        np.random.shuffle(seg)
+        csr.indices[lo:hi] = seg
+
+
+def create_sparse_array_zd(shape, stype, density, data_init=None, rsp_indices=None, dtype=None,
+                           modifier_func=None, shuffle_csr_indices=False):
+    """Sparse array that may have zero density (row_sparse: only ``rsp_indices`` rows)."""
+    if stype == 'row_sparse':
+        density = 0.0
+        if rsp_indices is not None and len(rsp_indices) > shape[0]:
+            raise AssertionError('more row indices than rows')
+    return create_sparse_array(shape, stype, data_init=data_init, rsp_indices=rsp_indices, dtype=dtype,
+                               modifier_func=modifier_func, density=density,
+                               shuffle_csr_indices=shuffle_csr_indices)
+
+
+# ---- matrices with controlled spectra (linalg operator tests) --------------------------------
+
+def new_orthonormal_matrix_2d(n):
+    """A random n x n orthonormal matrix (Q of a QR factorisation)."""
+    g = np.random.randn(n, n)
+    return np.linalg.qr(g.T @ g)[0]
+
+
+def new_sym_matrix_with_real_eigvals_2d(n):
+    """Q^T D Q: symmetric, eigenvalues uniform in [-10, 10]."""
+    q = new_orthonormal_matrix_2d(n)
+    return q.T @ np.diag(np.random.uniform(-10.0, 10.0, n)) @ q
+
+
+def new_sym_matrix_with_real_eigvals_nd(shape):
+    batch = int(np.prod(shape[:-2])) if len(shape) > 2 else 1
+    return np.stack([new_sym_matrix_with_real_eigvals_2d(shape[-1]) for _ in range(batch)]).reshape(shape)
+
+
+def new_matrix_with_real_eigvals_2d(n):
+    """A non-symmetric matrix with real eigenvalues: P D P^-1 with a well-conditioned P."""
+    while True:
+        house = np.eye(n) - 2 * np.outer(*(lambda v: (v, v))(
+            (lambda v: v / np.linalg.norm(v))(np.random.uniform(-1.0, 1.0, n))))
+        p = house @ np.diag(np.random.uniform(-1.0, 1.0, n))
+        if np.linalg.cond(p, 2) < 3:
+            break
+    return p @ np.diag(np.random.uniform(-10.0, 10.0, n)) @ np.linalg.inv(p)
+
+
+def new_matrix_with_real_eigvals_nd(shape):
+    batch = int(np.prod(shape[:-2])) if len(shape) > 2 else 1
+    return np.stack([new_matrix_with_real_eigvals_2d(shape[-1]) for _ in range(batch)]).reshape(shape)
+
+
+# ---- gluon hybridization consistency ---------------------------------------------------------
+
+def check_gluon_hybridize_consistency(net_builder, data_l, numpy_func=None, test_grad=True, rtol=1E-4,
+                                      atol=1E-4):
+    """Outputs (and input gradients) of a block built by ``net_builder()`` agree between eager
+    execution and ``hybridize()`` (and with ``numpy_func`` when given).  The block must be
+    deterministic; both copies share one parameter file."""
+    import tempfile
+    from . import autograd
+    saved = None
+    results = []
+    for hybrid in (False, True):
+        net = net_builder()
+        net.initialize()
+        if saved is None:
+            net(*data_l)
+            saved = os.path.join(tempfile.mkdtemp(), 'params')
+            net.save_parameters(saved)
+        else:
+            net(*data_l)
+            net.load_parameters(saved)
+        if hybrid:
+            net.hybridize()
+        inputs = [d.copy() for d in data_l]
+        for d in inputs:
+            d.attach_grad()
+        with autograd.record():
+            out = net(*inputs)
+        outs = out if isinstance(out, (list, tuple)) else [out]
+        if test_grad:
+            autograd.backward(outs)
+        results.append(([o.asnumpy() for o in outs], [d.grad.asnumpy() for d in inputs] if test_grad else []))
+    (o0, g0), (o1, g1) = results
+    for a, b in zip(o0, o1):
+        assert_almost_equal(a, b, rtol=rtol, atol=atol)
+    for a, b in zip(g0, g1):
+        assert_almost_equal(a, b, rtol=rtol, atol=atol)
+    if numpy_func is not None:
+        ref = numpy_func(*[d.asnumpy() for d in data_l])
+        for a, b in zip(o0, ref if isinstance(ref, (list, tuple)) else [ref]):
+            assert_almost_equal(a, b, rtol=rtol, atol=atol)
+
+
+# ---- environment probes / offline data ---------------------------------------------------------
+
+def is_cd_run():
+    return os.environ.get('CD_JOB', '0') == '1'
+
+
+def is_aarch64_run():
+    import platform
+    return platform.machine() == 'aarch64'
+
+
+def has_tvm_ops():
+    """No TVM-generated operators in this build (gfx950 kernels are hand-written HIP)."""
+    return False
+
+
+def get_im2rec_path(home_env='MXNET_HOME'):
+    """Path of the im2rec tool of this repository (tools/im2rec.py)."""
+    root = os.environ.get(home_env) or os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return os.path.join(root, 'tools', 'im2rec.py')
+
+
+def _offline(what):
+    raise IOError('%s: there is no network access; place the files locally and pass their path' % what)
+
+
+def download_model(model_name, dst_dir='./', meta_info=None):
+    _offline('download_model(%s)' % model_name)
+
+
+def get_zip_data(data_dir, url, data_origin_name):
+    if not os.path.exists(os.path.join(data_dir, data_origin_name)):
+        _offline('get_zip_data(%s)' % url)
+
+
+def get_bz2_data(data_dir, data_name, url, data_origin_name):
+    if not os.path.exists(os.path.join(data_dir, data_name)):
+        _offline('get_bz2_data(%s)' % url)
+
+
+def get_cifar10(path='data'):
+    if not os.path.isdir(os.path.join(path, 'cifar')):
+        _offline('get_cifar10')
+
+
+def get_mnist_pkl(path='data'):
+    if not os.path.exists(os.path.join(path, 'mnist.pkl.gz')):
+        _offline('get_mnist_pkl')
+
+
+def get_mnist_ubyte(path='data'):
+    files = ['train-images-idx3-ubyte', 'train-labels-idx1-ubyte', 't10k-images-idx3-ubyte',
+             't10k-labels-idx1-ubyte']
+    if not all(os.path.exists(os.path.join(path, f)) for f in files):
+        _offline('get_mnist_ubyte')

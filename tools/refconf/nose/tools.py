@@ -1,0 +1,50 @@
+"""nose.tools subset: raises, assert_raises, make_decorator, with_setup, nottest, assert_* aliases."""
+import functools
+import unittest
+
+import pytest
+
+_tc = unittest.TestCase('__init__')
+assert_equal = _tc.assertEqual
+assert_not_equal = _tc.assertNotEqual
+assert_true = _tc.assertTrue
+assert_false = _tc.assertFalse
+assert_almost_equal = _tc.assertAlmostEqual
+assert_in = _tc.assertIn
+assert_raises = _tc.assertRaises
+
+
+def raises(*exceptions):
+    def deco(fn):
+        @functools.wraps(fn)
+        def wrapper(*a, **k):
+            with pytest.raises(exceptions):
+                fn(*a, **k)
+        return wrapper
+    return deco
+
+
+def make_decorator(func):
+    def deco(newfunc):
+        return functools.wraps(func)(newfunc)
+    return deco
+
+
+def with_setup(setup=None, teardown=None):
+    def deco(fn):
+        @functools.wraps(fn)
+        def wrapper(*a, **k):
+            if setup:
+                setup()
+            try:
+                return fn(*a, **k)
+            finally:
+                if teardown:
+                    teardown()
+        return wrapper
+    return deco
+
+
+def nottest(fn):
+    fn.__test__ = False
+    return fn

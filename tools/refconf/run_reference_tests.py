@@ -1,0 +1,74 @@
+#!/usr/bin/env python
+"""Run selected reference unit-test files against this framework (``mxnet`` aliased).
+
+The reference tests are COPIED into a scratch directory (nothing is written
+under the reference tree) together with their ``common.py`` helpers, then run
+by pytest with the alias plugin.  Prints one JSON line per file:
+``{"file": ..., "passed": P, "failed": F, "skipped": S, "errors": E}``.
+
+    python tools/refconf/run_reference_tests.py [--ref DIR] [--timeout S] test_executor test_optimizer ...
+"""
+import argparse
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+DEFAULT_REF = '/root/reference/tests/python'
+
+
+def run_one(ref, name, timeout, workers):
+    tmp = tempfile.mkdtemp(prefix='mxref_')
+    try:
+        unit = os.path.join(tmp, 'unittest')
+        os.makedirs(unit)
+        for f in ('common.py', name + '.py', 'legacy_ndarray.v0', 'save_000800.json'):
+            src = os.path.join(ref, 'unittest', f)
+            if os.path.exists(src):
+                shutil.copy(src, unit)
+        if os.path.isdir(os.path.join(ref, 'common')):
+            shutil.copytree(os.path.join(ref, 'common'), os.path.join(tmp, 'common'))
+        env = dict(os.environ)
+        env['PYTHONPATH'] = os.pathsep.join([HERE, unit, os.path.join(tmp, 'common')] +
+                                            ([env['PYTHONPATH']] if env.get('PYTHONPATH') else []))
+        env['PYTHONDONTWRITEBYTECODE'] = '1'
+        env.setdefault('MXNET_TEST_SEED', '42')
+        cmd = [sys.executable, '-m', 'pytest', '-q', '-p', 'mxalias', '-p', 'no:cacheprovider', '--noconftest',
+               '--timeout', str(timeout), '-o', 'addopts=', '--rootdir', tmp, os.path.join(unit, name + '.py')]
+        if workers > 1:
+            cmd[3:3] = ['-n', str(workers)]
+        r = subprocess.run(cmd, cwd=unit, env=env, capture_output=True, text=True)
+        tail = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr[-500:]
+        counts = {k: 0 for k in ('passed', 'failed', 'skipped', 'errors', 'error', 'xfailed', 'xpassed')}
+        for n, k in re.findall(r'(\d+) (passed|failed|skipped|errors?|xfailed|xpassed)', tail):
+            counts[k] += int(n)
+        counts['errors'] += counts.pop('error')
+        return {'file': name, **counts, 'summary': tail, 'output': r.stdout[-20000:]}
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('names', nargs='+')
+    ap.add_argument('--ref', default=DEFAULT_REF)
+    ap.add_argument('--timeout', type=int, default=120)
+    ap.add_argument('-n', '--workers', type=int, default=1)
+    ap.add_argument('--show-failures', action='store_true')
+    a = ap.parse_args()
+    for name in a.names:
+        res = run_one(a.ref, name, a.timeout, a.workers)
+        out = res.pop('output')
+        print(json.dumps(res), flush=True)
+        if a.show_failures:
+            for line in out.splitlines():
+                if line.startswith(('FAILED', 'ERROR')):
+                    print('   ', line[:300])
+
+
+if __name__ == '__main__':
+    main()
