@@ -45,6 +45,7 @@ from . import callback
 from . import model
 from . import module
 from . import module as mod
+from . import rnn
 from . import monitor
 from . import monitor as mon
 from . import profiler
