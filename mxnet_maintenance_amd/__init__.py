@@ -46,6 +46,7 @@ from . import model
 from . import module
 from . import module as mod
 from . import rnn
+from . import library
 from . import monitor
 from . import monitor as mon
 from . import profiler
