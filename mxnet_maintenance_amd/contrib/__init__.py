@@ -1,6 +1,7 @@
 """Experimental / contributed APIs (mx.contrib).  Parity: python/mxnet/contrib/__init__.py."""
 from . import amp  # noqa: F401
 from . import quantization  # noqa: F401
+from . import text  # noqa: F401
 from .. import ndarray as _nd
 from .. import symbol as _sym
 ndarray = _nd.contrib
