@@ -1,0 +1,6 @@
+"""Stochastic variance-reduced gradient training (``mx.contrib.svrg_optimization``).
+
+API parity: python/mxnet/contrib/svrg_optimization/ (``SVRGModule``).
+"""
+from .svrg_module import SVRGModule  # noqa: F401
+from . import svrg_module  # noqa: F401
