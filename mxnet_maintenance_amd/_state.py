@@ -33,3 +33,7 @@ def is_recording():
 
 def is_training():
     return STATE.training
+
+# HIP-graph capture of a training step (gluon.GraphStep): a device uint64 counter mixed into the seeds of
+# captured dropout kernels, advanced before every replay so masks differ between replays
+GRAPH_RNG = [None]

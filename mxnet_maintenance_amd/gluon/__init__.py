@@ -10,3 +10,4 @@ from . import utils  # noqa: F401
 from . import data  # noqa: F401
 from . import model_zoo  # noqa: F401
 from . import contrib  # noqa: F401
+from .graph_step import GraphStep  # noqa: F401

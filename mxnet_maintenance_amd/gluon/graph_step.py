@@ -1,0 +1,160 @@
+"""HIP-graph capture of a whole training (or inference) step.
+
+The reference amortises per-operator launch cost with a static computation
+graph executed by its C++ engine (``hybridize(static_alloc=True,
+static_shape=True)``, CachedOp: src/imperative/cached_op.cc) and, on NVIDIA,
+with CUDA graphs inside that executor (src/imperative/cuda_graphs.h).  On
+MI355X the same effect comes from capturing the *entire* step -- forward,
+backward, gradient reduction and the fused optimizer update -- into one HIP
+graph and replaying it: one host call launches thousands of kernels, so a
+launch-bound model (BERT at small per-GPU batch) runs at kernel speed.
+
+What changes between replays lives on the device:
+
+* optimizer hyper-parameters (learning rate from the scheduler, Adam/LAMB
+  bias corrections) -- the trainer writes them into a small device table
+  before every replay (``Trainer._stage_hyper``) and the fused kernels read
+  them through a pointer captured in the graph;
+* dropout masks -- captured dropout kernels add a device counter, bumped
+  before each replay, to their Philox key;
+* torch's own generator (``nd.random`` ops) is graph-safe by construction.
+
+Usage::
+
+    def train_step(data, label):
+        with autograd.record():
+            loss = loss_fn(net(data), label)
+        loss.backward()
+        trainer.step(batch_size)
+        return loss
+
+    step = gluon.GraphStep(train_step, trainer, warmup=3)
+    for data, label in loader:
+        loss = step(data, label)      # same shapes every call
+
+The first ``warmup`` calls run eagerly (kernel autotuning, lazy parameter
+initialisation and gradient-arena construction happen there), the next call
+captures and replays.  Inputs are copied into static buffers; returned
+arrays are the graph's static outputs and are overwritten by the next call.
+The step function must not read device values on the host (``asnumpy``,
+``asscalar``) and must be shape-stable; AMP dynamic loss scaling (a host-side
+overflow check) is not supported inside a captured step.
+"""
+import torch
+
+from .. import _state
+from ..ndarray.ndarray import NDArray
+
+__all__ = ['GraphStep']
+
+
+def _tensor_of(x):
+    return x._data if isinstance(x, NDArray) else x
+
+
+class GraphStep:
+    """Capture ``fn(*inputs)`` into a HIP graph after ``warmup`` eager calls, then replay it."""
+
+    def __init__(self, fn, trainer=None, warmup=3):
+        if warmup < 1:
+            raise ValueError('GraphStep needs at least one eager warm-up call')
+        self._fn = fn
+        self._trainer = trainer
+        self._warmup = int(warmup)
+        self._calls = 0
+        self._graph = None
+        self._static_in = None
+        self._static_out = None
+        self._stream = None
+        self._rng = None
+
+    @property
+    def captured(self):
+        return self._graph is not None
+
+    def _side_stream(self, device):
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(device=device)
+        return self._stream
+
+    @staticmethod
+    def _device(inputs):
+        dev = next((_tensor_of(x).device for x in inputs if _tensor_of(x) is not None), None)
+        if dev is None and torch.cuda.is_available():      # closure-only step: the current device
+            dev = torch.device('cuda', torch.cuda.current_device())
+        return dev
+
+    def _run_eager(self, inputs):
+        dev = self._device(inputs)
+        if dev is None or dev.type != 'cuda':
+            return self._fn(*inputs)
+        s = self._side_stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            out = self._fn(*inputs)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        return out
+
+    def _capture(self, inputs):
+        tin = [_tensor_of(x) for x in inputs]
+        dev = self._device(inputs)
+        if dev is None or dev.type != 'cuda':
+            raise RuntimeError('GraphStep captures HIP work: inputs must live on a GPU context')
+        self._static_in = [NDArray(t.clone()) if isinstance(x, NDArray) else t.clone()
+                           for x, t in zip(inputs, tin)]
+        self._rng = torch.zeros(1, dtype=torch.int64, device=dev)
+        if self._trainer is not None:
+            self._trainer._enter_graph_mode()
+        s = self._side_stream(dev)
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        _state.GRAPH_RNG[0] = self._rng
+        try:
+            with torch.cuda.graph(graph, stream=s):
+                self._static_out = self._fn(*self._static_in)
+        except Exception:
+            if self._trainer is not None:
+                self._trainer._exit_graph_mode()
+            raise
+        finally:
+            _state.GRAPH_RNG[0] = None
+        self._graph = graph
+
+    def _load_inputs(self, inputs):
+        if len(inputs) != len(self._static_in):
+            raise ValueError('GraphStep: expected %d inputs, got %d' % (len(self._static_in), len(inputs)))
+        for dst, src in zip(self._static_in, inputs):
+            d, t = _tensor_of(dst), _tensor_of(src)
+            if d.shape != t.shape or d.dtype != t.dtype:
+                raise ValueError('GraphStep: input %s/%s differs from the captured %s/%s'
+                                 % (tuple(t.shape), t.dtype, tuple(d.shape), d.dtype))
+            if d.data_ptr() != t.data_ptr():
+                d.copy_(t, non_blocking=True)
+
+    @property
+    def static_inputs(self):
+        """The captured input buffers: fill them in place to skip the copy in ``__call__``."""
+        return self._static_in
+
+    def __call__(self, *inputs):
+        self._calls += 1
+        if self._graph is None:
+            if self._calls <= self._warmup:
+                return self._run_eager(inputs)
+            self._capture(inputs)
+        else:
+            self._load_inputs(inputs)
+        if self._trainer is not None:
+            self._trainer._stage_hyper()
+        self._rng.add_(1)
+        self._graph.replay()
+        return self._static_out
+
+    def reset(self):
+        """Drop the captured graph (e.g. after a shape change); the next call re-captures."""
+        if self._trainer is not None and self._graph is not None:
+            self._trainer._exit_graph_mode()
+        self._graph = None
+        self._static_out = None
+        self._static_in = None
+        self._calls = self._warmup

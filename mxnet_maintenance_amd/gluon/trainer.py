@@ -120,6 +120,7 @@ class Trainer:
         self._params_to_init = []
         self._arenas = None
         self._buckets = None
+        self._hyper = None          # device hyper-parameters while a GraphStep is captured
         self._reset_kvstore()
 
     def _check_contexts(self):
@@ -434,27 +435,80 @@ class Trainer:
                 for d in (param._data or []):
                     d._fresh_grad = False
 
-    def _fused_update(self, ignore_stale_grad=False):
+    def _arena_hparams(self, a, advance=True):
+        """(lr, wd, t, bc1, bc2) for arena ``a``; advances the update count unless ``advance`` is False.
+
+        ``lr`` is the value the kernel consumes: for Adam it already carries the
+        bias correction ``sqrt(1 - beta2^t) / (1 - beta1^t)``.
+        """
         import math
+        o = self._optimizer
+        if advance:
+            o._update_count(a.indices)
+        lr = o._get_lrs(a.indices[:1])[0]
+        wd = o._get_wds(a.indices[:1])[0]
+        t = o._index_update_count.get(a.indices[0], 1) or 1
+        kind = getattr(self, '_arena_kind', 'sgd')
+        bc1 = bc2 = 1.0
+        if kind in ('adam', 'adamw') and (kind == 'adam' or o.correct_bias):
+            lr *= math.sqrt(1. - o.beta2 ** t) / (1. - o.beta1 ** t)
+        elif kind == 'lamb' and o.bias_correction:
+            bc1, bc2 = 1.0 - o.beta1 ** t, 1.0 - o.beta2 ** t
+        return lr, wd, t, bc1, bc2
+
+    def _fused_update(self, ignore_stale_grad=False):
         o = self._optimizer
         clip = -1.0 if o.clip_gradient is None else o.clip_gradient
         kind = getattr(self, '_arena_kind', 'sgd')
-        for a in self._arenas:
+        graph = self._hyper is not None
+        for i, a in enumerate(self._arenas):
             saved = self._save_stale(a) if ignore_stale_grad else None
-            o._update_count(a.indices)
-            lr = o._get_lrs(a.indices[:1])[0]
-            wd = o._get_wds(a.indices[:1])[0]
-            t = o._index_update_count[a.indices[0]]
+            # graph mode: counts advance (and lr / bias corrections reach the device) in _stage_hyper,
+            # before every replay; the kernels read them from self._hyper[i]
+            lr, wd, t, _bc1, _bc2 = self._arena_hparams(a, advance=not graph)
+            hp = self._hyper[i] if graph else None
             if kind == 'sgd':
-                flat_sgd_update(a.w, a.g, a.mom, a.w32, lr, wd, o.momentum, o.rescale_grad, clip)
+                flat_sgd_update(a.w, a.g, a.mom, a.w32, lr, wd, o.momentum, o.rescale_grad, clip, hp=hp)
             elif kind in ('adam', 'adamw'):
-                if kind == 'adam' or o.correct_bias:
-                    lr *= math.sqrt(1. - o.beta2 ** t) / (1. - o.beta1 ** t)
-                flat_adam_update(a, lr, o.beta1, o.beta2, o.epsilon, wd, o.rescale_grad, clip, kind == 'adamw')
+                flat_adam_update(a, lr, o.beta1, o.beta2, o.epsilon, wd, o.rescale_grad, clip, kind == 'adamw',
+                                 hp=hp)
             else:
-                lamb_flat_update(a, lr, o, t, wd, clip)
+                lamb_flat_update(a, lr, o, t, wd, clip, hp=hp)
             if saved:
                 self._restore_stale(saved)
+
+    # ------------------------------------------------------------------ HIP-graph capture support
+    def _enter_graph_mode(self):
+        """Switch the fused update to device-resident hyper-parameters (see gluon.GraphStep).
+
+        Requirements: flat arenas on a HIP device, no AMP dynamic loss scaling
+        (its overflow check reads the device), no update on kvstore.
+        """
+        self._prepare()
+        if self._arenas is None or not self._arenas[0].w.is_cuda:
+            raise RuntimeError('graph capture needs the fused flat-arena update on a HIP device')
+        if getattr(self, '_amp_loss_scaler', None) is not None:
+            raise RuntimeError('graph capture does not support AMP dynamic loss scaling')
+        if self._update_on_kvstore and self._kvstore is not None:
+            raise RuntimeError('graph capture does not support update_on_kvstore')
+        dev = self._arenas[0].w.device
+        self._hyper = torch.zeros((len(self._arenas), 4), dtype=torch.float32, device=dev)
+        self._hyper_host = torch.zeros((len(self._arenas), 4), dtype=torch.float32)
+
+    def _exit_graph_mode(self):
+        self._hyper = None
+        self._hyper_host = None
+
+    def _stage_hyper(self, batch_size=None):
+        """Advance update counts and upload this step's lr / bias corrections (before a graph replay)."""
+        if batch_size is not None and self._scale / batch_size != self._optimizer.rescale_grad:
+            raise RuntimeError('graph-captured step: rescale_grad is baked into the graph; batch_size changed')
+        for i, a in enumerate(self._arenas):
+            lr, _wd, _t, bc1, bc2 = self._arena_hparams(a, advance=True)
+            self._hyper_host[i, 0] = lr
+            self._hyper_host[i, 1] = bc1
+            self._hyper_host[i, 2] = bc2
+        self._hyper.copy_(self._hyper_host)
 
     @staticmethod
     @torch.no_grad()
@@ -594,11 +648,13 @@ class _ArenaBuckets(GradBuckets):
 
 
 @torch.no_grad()
-def flat_sgd_update(w, g, mom, w32, lr, wd, momentum, rescale, clip):
-    """SGD(-momentum) over flat buffers; fused HIP kernel on gfx950."""
+def flat_sgd_update(w, g, mom, w32, lr, wd, momentum, rescale, clip, hp=None):
+    """SGD(-momentum) over flat buffers; fused HIP kernel on gfx950 (``hp``: device lr, graph mode)."""
     if w.is_cuda and _K.available() and _K.enabled() and hasattr(_K, 'flat_sgd'):
-        _K.flat_sgd(w, g, mom, w32, lr, wd, momentum, rescale, clip)
+        _K.flat_sgd(w, g, mom, w32, lr, wd, momentum, rescale, clip, hp=hp)
         return
+    if hp is not None:
+        raise RuntimeError('graph-captured updates need the HIP optimizer kernels')
     tgt = w32 if w32 is not None else w
     gg = g.to(tgt.dtype) if g.dtype != tgt.dtype else g.clone()
     if rescale != 1.0:
@@ -617,11 +673,13 @@ def flat_sgd_update(w, g, mom, w32, lr, wd, momentum, rescale, clip):
 
 
 @torch.no_grad()
-def flat_adam_update(a, lr, beta1, beta2, eps, wd, rescale, clip, adamw):
+def flat_adam_update(a, lr, beta1, beta2, eps, wd, rescale, clip, adamw, hp=None):
     """Adam / AdamW over one arena: fused HIP kernel on gfx950, torch ops elsewhere (same math)."""
     if a.w.is_cuda and _K.available() and _K.enabled() and hasattr(_K, 'flat_adam'):
-        _K.flat_adam(a.w, a.g, a.mean, a.var, a.w32, lr, beta1, beta2, eps, wd, rescale, clip, adamw=adamw)
+        _K.flat_adam(a.w, a.g, a.mean, a.var, a.w32, lr, beta1, beta2, eps, wd, rescale, clip, adamw=adamw, hp=hp)
         return
+    if hp is not None:
+        raise RuntimeError('graph-captured updates need the HIP optimizer kernels')
     w = a.w32 if a.w32 is not None else a.w
     g = a.g.float() * rescale
     if not adamw and wd:
@@ -639,14 +697,16 @@ def flat_adam_update(a, lr, beta1, beta2, eps, wd, rescale, clip, adamw):
 
 
 @torch.no_grad()
-def lamb_flat_update(a, lr, o, t, wd, clip):
+def lamb_flat_update(a, lr, o, t, wd, clip, hp=None):
     """LAMB (phase 1 + per-parameter trust ratio + phase 2) over one arena."""
     lb = -1.0 if o.lower_bound is None else o.lower_bound
     ub = -1.0 if o.upper_bound is None else o.upper_bound
     if a.w.is_cuda and _K.available() and _K.enabled() and hasattr(_K, 'lamb_update'):
         _K.lamb_update(a.w, a.g, a.mean, a.var, a.w32, a.upd, a.table, a.nrm, lr, o.beta1, o.beta2, o.epsilon, t,
-                       o.bias_correction, wd, o.rescale_grad, clip, lb, ub)
+                       o.bias_correction, wd, o.rescale_grad, clip, lb, ub, hp=hp)
         return
+    if hp is not None:
+        raise RuntimeError('graph-captured updates need the HIP optimizer kernels')
     from ..ops import optimizer_ops as _oo
     for off, n, _shape in a.views:
         w = a.w[off:off + n]

@@ -247,8 +247,9 @@ def gap_ok(x):
 _K.gap_ok = gap_ok
 
 
-def flat_sgd(w, g, mom, w32, lr, wd, momentum, rescale, clip):
-    """Fused (mp-)SGD-momentum over flat arenas (numel % 8 == 0, 16-byte aligned)."""
+def flat_sgd(w, g, mom, w32, lr, wd, momentum, rescale, clip, hp=None):
+    """Fused (mp-)SGD-momentum over flat arenas (numel % 8 == 0, 16-byte aligned); ``hp`` (optional
+    device tensor): hp[0] replaces ``lr`` at run time (graph-captured steps)."""
     lib = _K.lib()
     n = w.numel()
     assert n % 8 == 0 and g.numel() == n and w.dtype == g.dtype and w.dtype in _DT
@@ -256,8 +257,9 @@ def flat_sgd(w, g, mom, w32, lr, wd, momentum, rescale, clip):
     assert w32 is None or (w32.dtype == torch.float32 and w32.numel() == n)
     if momentum == 0.0:
         mom = None
-    lib.flat_sgd(_DT[w.dtype], w.data_ptr(), g.data_ptr(), _p(mom), _p(w32), n, float(lr), float(wd),
-                 float(momentum), float(rescale), float(clip), _stream())
+    args = (_DT[w.dtype], w.data_ptr(), g.data_ptr(), _p(mom), _p(w32), n, float(lr), float(wd),
+            float(momentum), float(rescale), float(clip), _stream())
+    lib.flat_sgd(*args) if hp is None else lib.flat_sgd(*args, hp.data_ptr())
 
 
 # ---------------------------------------------------------------------------

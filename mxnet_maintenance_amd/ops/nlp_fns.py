@@ -9,6 +9,7 @@ tests/test_hip_kernels.py.
 import torch
 
 from . import kernels as _K
+from .. import _state
 from .kernel_fns import _DT, _stream, _p, _f32, _leaf_grad
 
 __all__ = ['LayerNorm', 'GELU', 'Softmax', 'Dropout', 'ln_ok', 'ew_ok', 'softmax_ok',
@@ -152,8 +153,13 @@ class Dropout(torch.autograd.Function):
     def forward(ctx, x, p):
         y = torch.empty_like(x)
         mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device)
-        _K.lib().dropout_forward(_DT[x.dtype], x.data_ptr(), y.data_ptr(), mask.data_ptr(), x.numel(), float(p),
-                                 _seed(), _stream())
+        ctr = _state.GRAPH_RNG[0]
+        if ctr is not None and torch.cuda.is_current_stream_capturing():
+            _K.lib().dropout_forward(_DT[x.dtype], x.data_ptr(), y.data_ptr(), mask.data_ptr(), x.numel(),
+                                     float(p), _seed(), _stream(), ctr.data_ptr())
+        else:
+            _K.lib().dropout_forward(_DT[x.dtype], x.data_ptr(), y.data_ptr(), mask.data_ptr(), x.numel(),
+                                     float(p), _seed(), _stream())
         ctx.save_for_backward(mask)
         ctx.p = float(p)
         ctx.mark_non_differentiable(mask)
@@ -196,23 +202,27 @@ class ChunkTable:
         self.table = torch.from_numpy(arr.view(np.uint8).copy()).to(device)
 
 
-def flat_adam(w, g, mean, var, w32, lr, beta1, beta2, eps, wd, rescale, clip, adamw=False, eta=1.0):
+def flat_adam(w, g, mean, var, w32, lr, beta1, beta2, eps, wd, rescale, clip, adamw=False, eta=1.0, hp=None):
+    """``hp``: optional device float tensor; hp[0] replaces ``lr`` at run time (graph-captured steps)."""
     lib = _K.lib()
     n = w.numel()
     assert n % 8 == 0 and g.numel() == n and mean.numel() == n and var.numel() == n
-    lib.flat_adam(_DT[w.dtype], int(bool(adamw)), w.data_ptr(), g.data_ptr(), mean.data_ptr(), var.data_ptr(), _p(w32),
-                  n, float(lr), float(beta1), float(beta2), float(eps), float(wd), float(eta), float(rescale),
-                  float(clip), _stream())
+    args = (_DT[w.dtype], int(bool(adamw)), w.data_ptr(), g.data_ptr(), mean.data_ptr(), var.data_ptr(), _p(w32),
+            n, float(lr), float(beta1), float(beta2), float(eps), float(wd), float(eta), float(rescale),
+            float(clip), _stream())
+    lib.flat_adam(*args) if hp is None else lib.flat_adam(*args, hp.data_ptr())
 
 
 def lamb_update(w, g, mean, var, w32, upd, table, nrm, lr, beta1, beta2, eps, t, bias_correction, wd, rescale, clip,
-                lower_bound=-1.0, upper_bound=-1.0):
+                lower_bound=-1.0, upper_bound=-1.0, hp=None):
+    """``hp``: optional device float tensor {lr, bc1, bc2} read at run time (graph-captured steps)."""
     bc1 = 1.0 - beta1 ** t if bias_correction else 1.0
     bc2 = 1.0 - beta2 ** t if bias_correction else 1.0
-    _K.lib().lamb_update(_DT[w.dtype], w.data_ptr(), g.data_ptr(), mean.data_ptr(), var.data_ptr(), _p(w32),
-                         upd.data_ptr(), table.table.data_ptr(), table.n, nrm.data_ptr(), table.nseg, float(lr),
-                         float(beta1), float(beta2), float(eps), float(bc1), float(bc2), float(wd), float(rescale),
-                         float(clip), float(lower_bound), float(upper_bound), _stream())
+    args = (_DT[w.dtype], w.data_ptr(), g.data_ptr(), mean.data_ptr(), var.data_ptr(), _p(w32),
+            upd.data_ptr(), table.table.data_ptr(), table.n, nrm.data_ptr(), table.nseg, float(lr),
+            float(beta1), float(beta2), float(eps), float(bc1), float(bc2), float(wd), float(rescale),
+            float(clip), float(lower_bound), float(upper_bound), _stream())
+    _K.lib().lamb_update(*args) if hp is None else _K.lib().lamb_update(*args, hp.data_ptr())
 
 
 def seg_sumsq(x, table):

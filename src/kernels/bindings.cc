@@ -32,7 +32,7 @@ void softmax_ce_backward(int dtype, int label_is_int, const void* logits, const 
 void gap_nhwc_forward(int dtype, const void* x, void* y, int N, int HW, int C, hipStream_t s);
 void gap_nhwc_backward(int dtype, const void* dy, void* dx, int N, int HW, int C, hipStream_t s);
 void flat_sgd(int dtype, void* w, const void* g, float* mom, float* w32, int64_t n, float lr, float wd,
-              float momentum, float rescale, float clip, hipStream_t s);
+              float momentum, float rescale, float clip, const float* hp, hipStream_t s);
 void conv_nhwc_fwd(int dtype, const void* x, const void* w, const float* bias, void* y, int N, int H, int W, int C,
                    int K, int R, int S, int sh, int sw, int ph, int pw, int variant, hipStream_t s);
 int conv_nhwc_fwd_big_nparts(int N, int H, int W, int R, int S, int sh, int sw, int ph, int pw, int variant);
@@ -58,13 +58,15 @@ void softmax_forward(int dtype, int log, const void* x, void* y, int M, int L, f
 void softmax_backward(int dtype, int log, const void* y, const void* dy, void* dx, int M, int L, float scale,
                       hipStream_t s);
 void dropout_forward(int dtype, const void* x, void* y, uint8_t* mask, int64_t n, float p, uint64_t seed,
-                     hipStream_t s);
+                     const uint64_t* seed_base, hipStream_t s);
 void dropout_backward(int dtype, const void* dy, const uint8_t* mask, void* dx, int64_t n, float p, hipStream_t s);
 void flat_adam(int dtype, int mode, void* w, const void* g, float* mean, float* var, float* w32, int64_t n, float lr,
-               float beta1, float beta2, float eps, float wd, float eta, float rescale, float clip, hipStream_t s);
+               float beta1, float beta2, float eps, float wd, float eta, float rescale, float clip, const float* hp,
+               hipStream_t s);
 void lamb_update(int dtype, void* w, const void* g, float* mean, float* var, float* w32, float* upd,
                  const void* chunks, int nchunks, float* nrm, int nseg, float lr, float beta1, float beta2, float eps,
-                 float bc1, float bc2, float wd, float rescale, float clip, float lb, float ub, hipStream_t s);
+                 float bc1, float bc2, float wd, float rescale, float clip, float lb, float ub, const float* hp,
+                 hipStream_t s);
 void seg_sumsq(int dtype, const void* x, const void* chunks, int nchunks, float* out, int nseg, hipStream_t s);
 void all_finite(int dtype, const void* x, int64_t n, float scale, int* flag, int init, hipStream_t s);
 void pool_nhwc_forward(int dtype, int is_max, const void* x, void* y, uint8_t* arg, int N, int H, int W, int C,
@@ -169,7 +171,15 @@ PYBIND11_MODULE(_hip_kernels, m) {
   });
   m.def("flat_sgd", [](int dt, uintptr_t w, uintptr_t g, uintptr_t mom, uintptr_t w32, int64_t n, float lr,
                        float wd, float momentum, float rescale, float clip, uintptr_t s) {
-    flat_sgd(dt, P<void>(w), P<void>(g), P<float>(mom), P<float>(w32), n, lr, wd, momentum, rescale, clip, S(s));
+    flat_sgd(dt, P<void>(w), P<void>(g), P<float>(mom), P<float>(w32), n, lr, wd, momentum, rescale, clip, nullptr,
+             S(s));
+    check_launch("flat_sgd");
+  });
+  // overload with a trailing device hyper-parameter pointer (hp[0] = lr), for HIP-graph-captured steps
+  m.def("flat_sgd", [](int dt, uintptr_t w, uintptr_t g, uintptr_t mom, uintptr_t w32, int64_t n, float lr,
+                       float wd, float momentum, float rescale, float clip, uintptr_t s, uintptr_t hp) {
+    flat_sgd(dt, P<void>(w), P<void>(g), P<float>(mom), P<float>(w32), n, lr, wd, momentum, rescale, clip,
+             P<float>(hp), S(s));
     check_launch("flat_sgd");
   });
   // variant: 0 heuristic tile, 1..4 = (BCO, BK) in (128,64) (128,32) (64,64) (64,32)
@@ -238,7 +248,13 @@ PYBIND11_MODULE(_hip_kernels, m) {
   });
   m.def("dropout_forward", [](int dt, uintptr_t x, uintptr_t y, uintptr_t mask, int64_t n, float p, uint64_t seed,
                               uintptr_t s) {
-    dropout_forward(dt, P<void>(x), P<void>(y), P<uint8_t>(mask), n, p, seed, S(s));
+    dropout_forward(dt, P<void>(x), P<void>(y), P<uint8_t>(mask), n, p, seed, nullptr, S(s));
+    check_launch("dropout_forward");
+  });
+  // overload: seed_base = device uint64 counter mixed into the seed (fresh masks on every graph replay)
+  m.def("dropout_forward", [](int dt, uintptr_t x, uintptr_t y, uintptr_t mask, int64_t n, float p, uint64_t seed,
+                              uintptr_t s, uintptr_t seed_base) {
+    dropout_forward(dt, P<void>(x), P<void>(y), P<uint8_t>(mask), n, p, seed, P<uint64_t>(seed_base), S(s));
     check_launch("dropout_forward");
   });
   m.def("dropout_backward", [](int dt, uintptr_t dy, uintptr_t mask, uintptr_t dx, int64_t n, float p, uintptr_t s) {
@@ -250,7 +266,14 @@ PYBIND11_MODULE(_hip_kernels, m) {
                         int64_t n, float lr, float b1, float b2, float eps, float wd, float eta, float rescale,
                         float clip, uintptr_t s) {
     flat_adam(dt, mode, P<void>(w), P<void>(g), P<float>(mean), P<float>(var), P<float>(w32), n, lr, b1, b2, eps, wd,
-              eta, rescale, clip, S(s));
+              eta, rescale, clip, nullptr, S(s));
+    check_launch("flat_adam");
+  });
+  m.def("flat_adam", [](int dt, int mode, uintptr_t w, uintptr_t g, uintptr_t mean, uintptr_t var, uintptr_t w32,
+                        int64_t n, float lr, float b1, float b2, float eps, float wd, float eta, float rescale,
+                        float clip, uintptr_t s, uintptr_t hp) {
+    flat_adam(dt, mode, P<void>(w), P<void>(g), P<float>(mean), P<float>(var), P<float>(w32), n, lr, b1, b2, eps, wd,
+              eta, rescale, clip, P<float>(hp), S(s));
     check_launch("flat_adam");
   });
   m.def("lamb_update", [](int dt, uintptr_t w, uintptr_t g, uintptr_t mean, uintptr_t var, uintptr_t w32,
@@ -259,7 +282,16 @@ PYBIND11_MODULE(_hip_kernels, m) {
                           float ub, uintptr_t s) {
     lamb_update(dt, P<void>(w), P<void>(g), P<float>(mean), P<float>(var), P<float>(w32), P<float>(upd),
                 P<void>(chunks), nchunks, P<float>(nrm), nseg, lr, b1, b2, eps, bc1, bc2, wd, rescale, clip, lb, ub,
-                S(s));
+                nullptr, S(s));
+    check_launch("lamb_update");
+  });
+  m.def("lamb_update", [](int dt, uintptr_t w, uintptr_t g, uintptr_t mean, uintptr_t var, uintptr_t w32,
+                          uintptr_t upd, uintptr_t chunks, int nchunks, uintptr_t nrm, int nseg, float lr, float b1,
+                          float b2, float eps, float bc1, float bc2, float wd, float rescale, float clip, float lb,
+                          float ub, uintptr_t s, uintptr_t hp) {
+    lamb_update(dt, P<void>(w), P<void>(g), P<float>(mean), P<float>(var), P<float>(w32), P<float>(upd),
+                P<void>(chunks), nchunks, P<float>(nrm), nseg, lr, b1, b2, eps, bc1, bc2, wd, rescale, clip, lb, ub,
+                P<float>(hp), S(s));
     check_launch("lamb_update");
   });
   m.def("seg_sumsq", [](int dt, uintptr_t x, uintptr_t chunks, int nchunks, uintptr_t out, int nseg, uintptr_t s) {

@@ -106,7 +106,9 @@ template <typename T, bool MP, bool MOM>
 __global__ void __launch_bounds__(256) flat_sgd_kernel(T* __restrict__ w, const T* __restrict__ grad,
                                                        float* __restrict__ mom, float* __restrict__ w32,
                                                        int64_t nvec, float lr, float wd, float momentum,
-                                                       float rescale, float clip) {
+                                                       float rescale, float clip, const float* __restrict__ hp) {
+  // hp (optional, device): per-step hyper-parameters written before a HIP-graph replay; hp[0] = lr
+  if (hp != nullptr) lr = hp[0];
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec; v += stride) {
     const int64_t off = v * 8;
@@ -217,14 +219,14 @@ void gap_nhwc_backward(int dtype, const void* dy, void* dx, int N, int HW, int C
 }
 
 void flat_sgd(int dtype, void* w, const void* g, float* mom, float* w32, int64_t n, float lr, float wd,
-              float momentum, float rescale, float clip, hipStream_t s) {
+              float momentum, float rescale, float clip, const float* hp, hipStream_t s) {
   MXAMD_HOST_CHECK(n % 8 == 0, "flat_sgd: arena length must be a multiple of 8");
   const int64_t nvec = n / 8;
   int blocks = static_cast<int>((nvec + 255) / 256);
   if (blocks > 8192) blocks = 8192;
 #define L(T, MP, MOM) hipLaunchKernelGGL((flat_sgd_kernel<T, MP, MOM>), dim3(blocks), dim3(256), 0, s, \
                                          static_cast<T*>(w), static_cast<const T*>(g), mom, w32, nvec, lr, wd, \
-                                         momentum, rescale, clip)
+                                         momentum, rescale, clip, hp)
 #define DISPATCH(T)                           \
   if (w32) {                                  \
     if (mom) L(T, true, true); else L(T, true, false);   \

@@ -345,7 +345,9 @@ struct Philox {
 template <typename T>
 __global__ void __launch_bounds__(256) dropout_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                           uint8_t* __restrict__ mask, int64_t nvec, float p,
-                                                          uint64_t seed) {
+                                                          uint64_t seed, const uint64_t* __restrict__ seed_base) {
+  // seed_base (optional, device): a per-replay counter so a HIP-graph-captured dropout draws fresh masks
+  if (seed_base != nullptr) seed += seed_base[0] * 0x9E3779B97F4A7C15ull;
   const uint32_t thresh = (uint32_t)fminf(p * 4294967296.f, 4294967295.f);
   const float sc = p < 1.f ? 1.f / (1.f - p) : 0.f;
   const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
@@ -494,10 +496,11 @@ void softmax_backward(int dtype, int log, const void* y, const void* dy, void* d
 }
 
 void dropout_forward(int dtype, const void* x, void* y, uint8_t* mask, int64_t n, float p, uint64_t seed,
-                     hipStream_t s) {
+                     const uint64_t* seed_base, hipStream_t s) {
   MXAMD_HOST_CHECK(n % 8 == 0, "dropout: numel must be a multiple of 8");
   MXAMD_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((dropout_fwd_kernel<T>), dim3(ew_blocks(n / 8)), dim3(256), 0, s,
-                                               static_cast<const T*>(x), static_cast<T*>(y), mask, n / 8, p, seed))
+                                               static_cast<const T*>(x), static_cast<T*>(y), mask, n / 8, p, seed,
+                                               seed_base))
 }
 
 void dropout_backward(int dtype, const void* dy, const uint8_t* mask, void* dx, int64_t n, float p, hipStream_t s) {

@@ -45,7 +45,8 @@ __global__ void __launch_bounds__(256) flat_adam_kernel(T* __restrict__ w, const
                                                         float* __restrict__ mean, float* __restrict__ var,
                                                         float* __restrict__ w32, int64_t nvec, float lr, float beta1,
                                                         float beta2, float eps, float wd, float eta, float rescale,
-                                                        float clip) {
+                                                        float clip, const float* __restrict__ hp) {
+  if (hp != nullptr) lr = hp[0];   // device hyper-parameters (HIP-graph replay): bias-corrected lr
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
     const int64_t off = v * 8;
@@ -87,7 +88,12 @@ __global__ void __launch_bounds__(256) lamb_phase1_kernel(const T* __restrict__ 
                                                           const float* __restrict__ w32, float* __restrict__ upd,
                                                           const Chunk* __restrict__ chunks, float* __restrict__ nrm,
                                                           float beta1, float beta2, float eps, float bc1, float bc2,
-                                                          float wd, float rescale, float clip) {
+                                                          float wd, float rescale, float clip,
+                                                          const float* __restrict__ hp) {
+  if (hp != nullptr) {   // hp = {lr, bc1, bc2} written before a HIP-graph replay
+    bc1 = hp[1];
+    bc2 = hp[2];
+  }
   const Chunk ck = chunks[blockIdx.x];
   float sw = 0.f, sr = 0.f;
   for (int i8 = threadIdx.x * 8; i8 < ck.len; i8 += 256 * 8) {
@@ -133,7 +139,8 @@ __global__ void __launch_bounds__(256) lamb_phase2_kernel(T* __restrict__ w, flo
                                                           const float* __restrict__ upd,
                                                           const Chunk* __restrict__ chunks,
                                                           const float* __restrict__ nrm, float lr, float lb,
-                                                          float ub) {
+                                                          float ub, const float* __restrict__ hp) {
+  if (hp != nullptr) lr = hp[0];
   const Chunk ck = chunks[blockIdx.x];
   float r1 = sqrtf(nrm[2 * ck.seg]);
   const float r2 = sqrtf(nrm[2 * ck.seg + 1]);
@@ -201,13 +208,14 @@ inline int flat_blocks(int64_t nvec) {
 }  // namespace
 
 void flat_adam(int dtype, int mode, void* w, const void* g, float* mean, float* var, float* w32, int64_t n, float lr,
-               float beta1, float beta2, float eps, float wd, float eta, float rescale, float clip, hipStream_t s) {
+               float beta1, float beta2, float eps, float wd, float eta, float rescale, float clip, const float* hp,
+               hipStream_t s) {
   MXAMD_HOST_CHECK(n % 8 == 0, "flat_adam: arena length must be a multiple of 8");
   const int64_t nvec = n / 8;
   dim3 grid(flat_blocks(nvec));
 #define L(MODE, MP) hipLaunchKernelGGL((flat_adam_kernel<T, MODE, MP>), grid, dim3(256), 0, s, static_cast<T*>(w), \
                                        static_cast<const T*>(g), mean, var, w32, nvec, lr, beta1, beta2, eps, wd, eta, \
-                                       rescale, clip)
+                                       rescale, clip, hp)
   MXAMD_OPT_DTYPE(dtype, {
     if (mode == kAdam) {
       if (w32) L(kAdam, true); else L(kAdam, false);
@@ -221,22 +229,23 @@ void flat_adam(int dtype, int mode, void* w, const void* g, float* mean, float* 
 // chunks: device array of (start, len, seg) triples (int64, int32, int32 -> 16 bytes each)
 void lamb_update(int dtype, void* w, const void* g, float* mean, float* var, float* w32, float* upd,
                  const void* chunks, int nchunks, float* nrm, int nseg, float lr, float beta1, float beta2, float eps,
-                 float bc1, float bc2, float wd, float rescale, float clip, float lb, float ub, hipStream_t s) {
+                 float bc1, float bc2, float wd, float rescale, float clip, float lb, float ub, const float* hp,
+                 hipStream_t s) {
   const Chunk* ck = static_cast<const Chunk*>(chunks);
   (void)hipMemsetAsync(nrm, 0, sizeof(float) * 2 * nseg, s);
   MXAMD_OPT_DTYPE(dtype, {
     if (w32) {
       hipLaunchKernelGGL((lamb_phase1_kernel<T, true>), dim3(nchunks), dim3(256), 0, s, static_cast<const T*>(w),
                          static_cast<const T*>(g), mean, var, w32, upd, ck, nrm, beta1, beta2, eps, bc1, bc2, wd,
-                         rescale, clip);
+                         rescale, clip, hp);
       hipLaunchKernelGGL((lamb_phase2_kernel<T, true>), dim3(nchunks), dim3(256), 0, s, static_cast<T*>(w), w32, upd,
-                         ck, nrm, lr, lb, ub);
+                         ck, nrm, lr, lb, ub, hp);
     } else {
       hipLaunchKernelGGL((lamb_phase1_kernel<T, false>), dim3(nchunks), dim3(256), 0, s, static_cast<const T*>(w),
                          static_cast<const T*>(g), mean, var, w32, upd, ck, nrm, beta1, beta2, eps, bc1, bc2, wd,
-                         rescale, clip);
+                         rescale, clip, hp);
       hipLaunchKernelGGL((lamb_phase2_kernel<T, false>), dim3(nchunks), dim3(256), 0, s, static_cast<T*>(w), w32, upd,
-                         ck, nrm, lr, lb, ub);
+                         ck, nrm, lr, lb, ub, hp);
     }
   })
 }

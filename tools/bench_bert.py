@@ -8,7 +8,7 @@ gradient all-reduce (N > 1, torch.distributed.run) and a fused flat-arena
 LAMB (default) or AdamW update.  Synthetic token ids / random-init weights.
 
 Usage: python tools/bench_bert.py [--batch 32] [--seq 128] [--steps 20] [--warmup 5]
-       [--model bert_12_768_12] [--optimizer lamb|adamw] [--dtype bfloat16]
+       [--model bert_12_768_12] [--optimizer lamb|adamw] [--dtype bfloat16] [--graph]
 Prints one JSON line (tokens/s and sequences/s for the whole job).
 """
 import argparse
@@ -43,6 +43,7 @@ def main():
     ap.add_argument('--dtype', default='bfloat16', choices=['bfloat16', 'float16', 'float32'])
     ap.add_argument('--vocab', type=int, default=30528, help='30522 padded to a multiple of 64')
     ap.add_argument('--gpus', type=int, default=1, help='worker processes (one per GPU)')
+    ap.add_argument('--graph', action='store_true', help='capture the whole step in a HIP graph (GraphStep)')
     args = ap.parse_args()
     launch = _load_launcher()
     if launch.needs_launch(args.gpus):
@@ -94,6 +95,8 @@ def main():
             torch.cuda.synchronize()
         dist.barrier()
 
+    if args.graph:
+        step = gluon.GraphStep(step, trainer, warmup=max(1, args.warmup - 1))
     for _ in range(args.warmup):
         step()
     sync()
@@ -115,7 +118,7 @@ def main():
             'dtype': {'bfloat16': 'bf16', 'float16': 'fp16', 'float32': 'fp32'}[args.dtype],
             'data': 'synthetic token ids, random-init weights',
             'config': {'model': args.model, 'per_gpu_batch': B, 'seq_len': S, 'masked_positions': P,
-                       'optimizer': args.optimizer, 'parallelism': 'dp%d' % n,
+                       'optimizer': args.optimizer, 'parallelism': 'dp%d' % n, 'hip_graph': args.graph,
                        'final_loss': round(float(last.asscalar()), 4)}}), flush=True)
     if dist.world_size() > 1:
         torch.distributed.destroy_process_group()
