@@ -430,7 +430,8 @@ class CachedOp:
 
     def __call__(self, feed, ctx_dev):
         static = self.flags.get('static_alloc') and self.flags.get('static_shape')
-        if static and not _state.STATE.recording and ctx_dev.type == 'cuda':
+        if static and not _state.STATE.recording and ctx_dev.type == 'cuda' and \
+                not torch.cuda.is_current_stream_capturing():     # inside a GraphStep capture: just run
             return self._replay(feed)
         return self.prog.run(feed)
 
@@ -447,14 +448,20 @@ class CachedOp:
                     self.prog.run(static_in)
             torch.cuda.current_stream().wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                outs = self.prog.run(static_in)
-            ent = (g, static_in, outs)
+            rng = torch.zeros(1, dtype=torch.int64, device=torch.cuda.current_device())
+            _state.GRAPH_RNG[0] = rng      # captured dropout (train_mode inference) re-keys per replay
+            try:
+                with torch.cuda.graph(g):
+                    outs = self.prog.run(static_in)
+            finally:
+                _state.GRAPH_RNG[0] = None
+            ent = (g, static_in, outs, rng)
             self._graphs[key] = ent
-        g, static_in, outs = ent
+        g, static_in, outs, rng = ent
         for k, v in feed.items():
             if v is not None and static_in[k].data_ptr() != v.data_ptr():
                 static_in[k].copy_(v)
+        rng.add_(1)
         g.replay()
         return [o.clone() for o in outs]
 
