@@ -479,12 +479,15 @@ def _time_candidates(cands, reps=3, key=None, tol=2e-2):
     return best, out
 
 
-def _select(key, cands, default):
-    """Run the cached / autotuned / default candidate and return its result."""
+def _select(key, cands, default, timing=None):
+    """Run the cached / autotuned / default candidate and return its result.
+
+    ``timing`` (optional, same names as ``cands``): the closures to time instead, e.g. with the
+    cost of work a candidate leaves to the next operator included."""
     name = _ALGO.get(key)
     if name is None:
         if _AUTOTUNE and not torch.cuda.is_current_stream_capturing() and len(cands) > 1:
-            name, out = _time_candidates(cands, key=key)
+            name, out = _time_candidates(timing or cands, key=key)
             _ALGO[key] = name
             return out
         name = default
@@ -513,6 +516,39 @@ def _fwd_candidates(x, w, stride, pad, bias):
         return y.permute(0, 2, 3, 1).contiguous()
     c.append(('miopen', miopen))
     return c
+
+
+_STATS_SCRATCH = {}
+
+
+def _bn_stats_pass(y):
+    """The BatchNorm statistics pass over ``y`` (what a following training-mode BN runs itself when
+    the conv epilogue did not emit partials)."""
+    C = y.shape[-1]
+    R = y.numel() // C
+    lib = _K.lib()
+    n = 2 * lib.bn_partials_rows(R, C) * C
+    buf = _STATS_SCRATCH.get(y.device)
+    if buf is None or buf.numel() < n:
+        buf = _STATS_SCRATCH[y.device] = torch.empty(n, dtype=torch.float32, device=y.device)
+    lib.bn_nhwc_stats(_DT[y.dtype], y.data_ptr(), _zeros_f32(C, y.device).data_ptr(), buf.data_ptr(), R, C,
+                      _stream())
+
+
+def _fwd_timing(cands):
+    """Timing closures for a training-mode conv feeding BatchNorm: candidates that do not emit BN
+    partials from their epilogue are charged the statistics pass the BN then runs over their output."""
+    if not _state.STATE.training:
+        return None
+
+    def charged(fn):
+        def run():
+            y = fn()
+            if getattr(y, '_mxamd_bn_part', None) is None and y.shape[-1] % 8 == 0 and y.is_contiguous():
+                _bn_stats_pass(y)
+            return y
+        return run
+    return [(n, charged(fn)) for n, fn in cands]
 
 
 def _fwd_default(x, w, stride):
@@ -637,7 +673,8 @@ class ConvNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, bias, stride, pad, dilate):
         key = ('fwd', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype, bias is not None)
-        y = _select(key, _fwd_candidates(x, w, stride, pad, bias), _fwd_default(x, w, stride))
+        cands = _fwd_candidates(x, w, stride, pad, bias)
+        y = _select(key, cands, _fwd_default(x, w, stride), timing=_fwd_timing(cands))
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.pad = stride, pad
         ctx.has_bias = bias is not None
@@ -674,7 +711,8 @@ class ConvTeeNHWC(torch.autograd.Function):
     def forward(ctx, x, w, inplace_grad=False):
         stride, pad = (1, 1), (0, 0)
         key = ('fwd', tuple(x.shape), tuple(w.shape), stride, pad, x.dtype, False)
-        y = _select(key, _fwd_candidates(x, w, stride, pad, None), _fwd_default(x, w, stride))
+        cands = _fwd_candidates(x, w, stride, pad, None)
+        y = _select(key, cands, _fwd_default(x, w, stride), timing=_fwd_timing(cands))
         ctx.save_for_backward(x, w)
         ctx.w_ref = w
         ctx.inplace_grad = inplace_grad

@@ -25,6 +25,7 @@ void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, c
                       const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R, int C,
                       int relu_mode, int fix_gamma, int training, int accum, hipStream_t s);
 int bn_partials_rows(int64_t R, int C);
+int bn_nhwc_stats(int dtype, const void* x, const float* center, float* part, int64_t R, int C, hipStream_t s);
 void softmax_ce_forward(int dtype, int label_is_int, const void* logits, const void* label, float* loss, float* lse,
                         int N, int K, hipStream_t s);
 void softmax_ce_backward(int dtype, int label_is_int, const void* logits, const void* label, const float* lse,
@@ -102,6 +103,11 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.attr("arch") = "gfx950";
 
   m.def("bn_partials_rows", &bn_partials_rows);
+  m.def("bn_nhwc_stats", [](int dt, uintptr_t x, uintptr_t center, uintptr_t part, int64_t R, int C, uintptr_t s) {
+    int nblk = bn_nhwc_stats(dt, P<const void>(x), P<const float>(center), P<float>(part), R, C, S(s));
+    check_launch("bn_nhwc_stats");
+    return nblk;
+  });
   m.def("twobit_quantize", [](int dt, uintptr_t g, uintptr_t res, uintptr_t packed, int64_t n, float thr,
                               uintptr_t s) {
     twobit_quantize(dt, P<void>(g), P<float>(res), P<void>(packed), n, thr, S(s));

@@ -436,6 +436,24 @@ static void bn_backward_impl(const void* x, const void* dy, const void* y, const
 #undef BWD
 }
 
+// Statistics pass only (per-channel partial sums of x - center): lets the conv autotuner charge a
+// candidate that cannot emit BN partials from its epilogue with the pass it leaves to BatchNorm.
+int bn_nhwc_stats(int dtype, const void* x, const float* center, float* part, int64_t R, int C, hipStream_t s) {
+  MXAMD_HOST_CHECK(C % 8 == 0, "bn_nhwc: channels must be a multiple of 8");
+  BnGeom g = bn_geom(C);
+  MXAMD_HOST_CHECK(C % g.cb == 0, "bn_nhwc: unsupported channel count");
+  int nblk;
+  int64_t rpb = bn_rows_per_block(R, C, g, &nblk);
+  dim3 grid(nblk, C / g.cb);
+  float* p2 = part + static_cast<int64_t>(nblk) * C;
+#define STATS(T)                                                                                              \
+  hipLaunchKernelGGL((bn_reduce_kernel<T, 0, kReluNone>), grid, dim3(kBnThreads), 0, s, static_cast<const T*>(x), \
+                     nullptr, nullptr, nullptr, center, nullptr, nullptr, part, p2, R, C, g.tpr, g.rpi, rpb)
+  if (dtype == kF16) STATS(__half); else if (dtype == kBF16) STATS(__hip_bfloat16); else STATS(float);
+#undef STATS
+  return nblk;
+}
+
 void bn_nhwc_forward(int dtype, const void* x, const void* addend, void* y, uint8_t* mask, const float* gamma,
                      const float* beta,
                      const float* center, float* part, float* mean, float* invstd, float* var, float* scale,
