@@ -62,6 +62,13 @@ def linear(data, weight, bias):
     return F.linear(data, weight, bias)
 
 
+def embedding(data, weight):
+    """Embedding lookup on the HIP gather / scatter-add kernels, or None (caller falls back)."""
+    if _use_hip(weight) and _K.embedding_ok(data, weight):
+        return _K.Embedding.apply(data, weight)
+    return None
+
+
 def conv(data, weight, bias, stride, pad, dilate, groups, channel_last):
     nsp = data.dim() - 2
     if channel_last:

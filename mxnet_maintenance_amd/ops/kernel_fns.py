@@ -33,7 +33,8 @@ def _f32(t):
 # ---------------------------------------------------------------------------
 
 def bn_ok(x):
-    return (x.dtype in _DT and x.dim() >= 2 and x.is_contiguous() and x.shape[-1] % 8 == 0
+    C = x.shape[-1] if x.dim() else 0
+    return (x.dtype in _DT and x.dim() >= 2 and x.is_contiguous() and C % 8 == 0
             and x.numel() > 0 and x.data_ptr() % 16 == 0)
 
 
@@ -41,8 +42,6 @@ def ce_ok(x):
     return x.dim() == 2 and x.dtype in _DT and x.is_contiguous()
 
 
-_K.bn_ok = bn_ok
-_K.ce_ok = ce_ok
 
 
 def _leaf_grad(t, numel=None, dtype=torch.float32):
@@ -244,7 +243,6 @@ def gap_ok(x):
     return x.dtype in _DT and x.is_contiguous() and x.shape[-1] % 8 == 0
 
 
-_K.gap_ok = gap_ok
 
 
 def flat_sgd(w, g, mom, w32, lr, wd, momentum, rescale, clip, hp=None):
@@ -777,7 +775,6 @@ def conv_tee_ok(x, w):
             and x.shape[3] == w.shape[3])
 
 
-_K.conv_tee_ok = conv_tee_ok
 
 
 def conv_algos():
@@ -796,7 +793,6 @@ def conv_ok(x, w, stride, pad, dilate, groups):
             and w.is_contiguous() and x.dtype in (torch.float16, torch.bfloat16) and w.dtype == x.dtype)
 
 
-_K.conv_ok = conv_ok
 __all__ += ['ConvNHWC', 'ConvTeeNHWC', 'conv_fwd', 'conv_ok_shape', 'conv_wgrad', 'conv_wgrad_ok']
 
 
@@ -847,5 +843,4 @@ class PoolNHWC(torch.autograd.Function):
         return dx, None, None, None, None, None, None
 
 
-_K.pool_ok = pool_ok
 __all__ += ['PoolNHWC']

@@ -46,39 +46,9 @@ def lib():
     return m
 
 
-# Shape/dtype predicates: which calls the kernels support.  Anything else
-# takes the torch path (which on ROCm is itself MIOpen/hipBLASLt).
-def gemm_ok(x, w):
-    return False
-
-
-def conv_ok(x, w, stride, pad, dilate, groups):
-    return False
-
-
-def pool_ok(x, kernel, stride, pad):
-    return False
-
-
-def ew_ok(x):
-    return False
-
-
-def ln_ok(x):
-    return False
-
-
-def ce_ok(x):
-    return False
-
-
-def bn_ok(x):
-    return False
-
-
-def gap_ok(x):
-    return False
-
-
+# Operator wrappers and their shape/dtype predicates (which calls the kernels support; anything
+# else takes the torch path, itself MIOpen / hipBLASLt on ROCm) live next to the kernels they drive.
 from .kernel_fns import *  # noqa: E402,F401,F403
+from .kernel_fns import bn_ok, ce_ok, gap_ok, conv_ok, conv_tee_ok, pool_ok  # noqa: E402,F401
 from .nlp_fns import *  # noqa: E402,F401,F403
+from .nlp_fns import ln_ok, ew_ok, gemm_ok, embedding_ok  # noqa: E402,F401

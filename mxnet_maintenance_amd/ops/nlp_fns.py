@@ -33,8 +33,6 @@ def softmax_ok(x, axis):
             and x.shape[-1] % 8 == 0 and 8 <= x.shape[-1] <= 8192 and x.numel() > 0)
 
 
-_K.ln_ok = ln_ok
-_K.ew_ok = ew_ok
 
 
 class LayerNorm(torch.autograd.Function):
@@ -241,8 +239,6 @@ def all_finite(x, scale=1.0, flag=None):
     return flag
 
 
-_K.LayerNorm = LayerNorm
-_K.GELU = GELU
 
 
 # ---------------------------------------------------------------------------
@@ -308,11 +304,13 @@ class Linear(torch.autograd.Function):
         ctx.has_b = b is not None
         ctx.bdt = b.dtype if b is not None else None
         ctx.xshape = x.shape
+        ctx.refs = (w, b)
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         x2, w = ctx.saved_tensors
+        w_ref, b_ref = ctx.refs
         N = w.shape[0]
         dy2 = dy.reshape(-1, N).contiguous()
         dx = dw = db = None
@@ -320,13 +318,100 @@ class Linear(torch.autograd.Function):
             key = ('fc_dgrad', tuple(dy2.shape), tuple(w.shape), dy.dtype)
             dx = _KF._select(key, _fc_dgrad_cands(dy2, w.contiguous()), 'mm').view(ctx.xshape)
         if ctx.needs_input_grad[1]:
-            key = ('fc_wgrad', tuple(dy2.shape), tuple(x2.shape), dy.dtype)
-            dw = _KF._select(key, _fc_wgrad_cands(dy2, x2, w), 'mm').to(w.dtype)
+            dw = _fc_wgrad(dy2, x2, w, w_ref)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = torch.sum(dy2, 0, dtype=torch.float32).to(ctx.bdt)
+            db = bias_grad(dy2, b_ref, ctx.bdt)
         return dx, dw, db
 
 
-_K.gemm_ok = gemm_ok
-_K.Linear = Linear
-__all__ += ['Linear', 'gemm_ok']
+def _fc_wgrad(dy2, x2, w, w_ref):
+    """dW = dY^T X; accumulated straight into the weight's .grad buffer when possible (GEMM with
+    beta = 1 / the MFMA kernel's accumulating reduce) so no separate dW tensor and add kernel."""
+    key = ('fc_wgrad', tuple(dy2.shape), tuple(x2.shape), dy2.dtype)
+    algo = _KF._ALGO.get(key)
+    tgt = _leaf_grad(w_ref, dtype=w.dtype) if algo is not None else None
+    if tgt is not None:
+        N, K = w.shape
+        if algo == 'hip':
+            _KF.conv_wgrad(x2.view(-1, 1, 1, K), dy2.view(-1, 1, 1, N), (N, 1, 1, K), (1, 1), (0, 0),
+                           out=tgt.view(N, 1, 1, K), accum=True)
+        else:
+            tgt.addmm_(dy2.t(), x2)
+        return None
+    return _KF._select(key, _fc_wgrad_cands(dy2, x2, w), 'mm').to(w.dtype)
+
+
+_COLSUM_PART = {}
+
+
+def bias_grad(dy2, b_ref, bdt):
+    """db = column sums of dY [M, N] in fp32 on the HIP reduce kernels, accumulated into the bias's
+    .grad buffer when possible (returns None then)."""
+    M, N = dy2.shape
+    if not (dy2.is_cuda and _K.available() and dy2.dtype in _DT and N % 8 == 0 and _aligned(dy2)):
+        return torch.sum(dy2, 0, dtype=torch.float32).to(bdt)
+    lib = _K.lib()
+    n = 2 * lib.bn_partials_rows(M, N) * N
+    part = _COLSUM_PART.get(dy2.device)
+    if part is None or part.numel() < n:
+        part = _COLSUM_PART[dy2.device] = torch.empty(n, dtype=torch.float32, device=dy2.device)
+    tgt = _leaf_grad(b_ref, N, dtype=bdt) if bdt in _DT else None
+    out = tgt if tgt is not None else torch.empty(N, dtype=torch.float32, device=dy2.device)
+    lib.colsum_rows(_DT[dy2.dtype], dy2.data_ptr(), _KF._zeros_f32(N, dy2.device).data_ptr(), part.data_ptr(), M, N,
+                    _DT[out.dtype], out.data_ptr(), int(tgt is not None), _stream())
+    if tgt is not None:
+        return None
+    return out.to(bdt)
+
+
+_IDX_T = {torch.float32: 0, torch.int64: 1, torch.int32: 2}
+_EMB_SCRATCH = {}
+
+
+def embedding_ok(idx, w):
+    return (w.is_cuda and w.dtype in _DT and w.dim() == 2 and w.shape[1] % 8 == 0 and _aligned(w)
+            and idx.device == w.device and idx.numel() > 0 and w.shape[0] < 2 ** 31)
+
+
+class Embedding(torch.autograd.Function):
+    """Row gather ``y[..., :] = W[idx[...], :]`` (indices clamped to [0, V), any of float32 / int64 /
+    int32) and its scatter-add backward on HIP kernels: fp32 hardware atomics into a persistent,
+    always-zero [V, C] scratch, then one pass that adds the touched rows into the weight's .grad
+    buffer (or a fresh gradient) and re-zeroes them.  No sort / unique, nothing data-dependent on
+    the host, so the backward is HIP-graph capturable."""
+
+    @staticmethod
+    def forward(ctx, idx, w):
+        if idx.dtype not in _IDX_T:
+            idx = idx.to(torch.int64)
+        idx = idx.contiguous()
+        V, C = w.shape
+        n = idx.numel()
+        y = torch.empty(tuple(idx.shape) + (C,), dtype=w.dtype, device=w.device)
+        _K.lib().embedding_forward(_DT[w.dtype], _IDX_T[idx.dtype], idx.data_ptr(), w.contiguous().data_ptr(),
+                                   y.data_ptr(), n, V, C, _stream())
+        ctx.save_for_backward(idx)
+        ctx.w_ref = w
+        ctx.vc = (V, C, w.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        idx, = ctx.saved_tensors
+        V, C, wdt = ctx.vc
+        dy = dy.contiguous()
+        dev = dy.device
+        key = (V, C, dev)
+        sc = _EMB_SCRATCH.get(key)
+        if sc is None:
+            sc = _EMB_SCRATCH[key] = (torch.zeros(V * C, dtype=torch.float32, device=dev),
+                                      torch.zeros(V, dtype=torch.uint8, device=dev))
+        tgt = _leaf_grad(ctx.w_ref, V * C, dtype=wdt) if ctx.needs_input_grad[1] else None
+        out = tgt if tgt is not None else torch.empty((V, C), dtype=wdt, device=dev)
+        _K.lib().embedding_backward(_DT[dy.dtype], _IDX_T[idx.dtype], idx.data_ptr(), dy.data_ptr(),
+                                    sc[0].data_ptr(), sc[1].data_ptr(), _DT[out.dtype], out.data_ptr(),
+                                    int(tgt is not None), idx.numel(), V, C, _stream())
+        return None, (None if tgt is not None else out)
+
+
+__all__ += ['Linear', 'gemm_ok', 'Embedding', 'embedding_ok']

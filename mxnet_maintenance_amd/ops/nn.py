@@ -615,6 +615,9 @@ def dropout(data, p=0.5, mode='training', axes=(), cudnn_off=False):
           params={'input_dim': ('int', 0), 'output_dim': ('int', 0), 'dtype': ('str', 'float32'),
                   'sparse_grad': ('bool', False)})
 def embedding(data, weight, input_dim=0, output_dim=0, dtype='float32', sparse_grad=False):
+    r = hip_ops.embedding(data, weight)
+    if r is not None:
+        return r
     idx = torch.clamp(data.to(torch.int64), 0, weight.shape[0] - 1)
     return F.embedding(idx, weight)
 

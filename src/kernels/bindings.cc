@@ -25,7 +25,13 @@ void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, c
                       const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R, int C,
                       int relu_mode, int fix_gamma, int training, int accum, hipStream_t s);
 int bn_partials_rows(int64_t R, int C);
+void embedding_forward(int dtype, int itype, const void* idx, const void* w, void* y, int64_t n, int V, int C,
+                       hipStream_t s);
+void embedding_backward(int dtype, int itype, const void* idx, const void* dy, float* acc, uint8_t* touched,
+                        int out_dtype, void* grad, int accum, int64_t n, int V, int C, hipStream_t s);
 int bn_nhwc_stats(int dtype, const void* x, const float* center, float* part, int64_t R, int C, hipStream_t s);
+void colsum_rows(int dtype, const void* x, const float* zeros, float* part, int64_t R, int C, int out_dtype,
+                 void* out, int accum, hipStream_t s);
 void softmax_ce_forward(int dtype, int label_is_int, const void* logits, const void* label, float* loss, float* lse,
                         int N, int K, hipStream_t s);
 void softmax_ce_backward(int dtype, int label_is_int, const void* logits, const void* label, const float* lse,
@@ -107,6 +113,22 @@ PYBIND11_MODULE(_hip_kernels, m) {
     int nblk = bn_nhwc_stats(dt, P<const void>(x), P<const float>(center), P<float>(part), R, C, S(s));
     check_launch("bn_nhwc_stats");
     return nblk;
+  });
+  m.def("embedding_forward", [](int dt, int it, uintptr_t idx, uintptr_t w, uintptr_t y, int64_t n, int V, int C,
+                                uintptr_t s) {
+    embedding_forward(dt, it, P<const void>(idx), P<const void>(w), P<void>(y), n, V, C, S(s));
+    check_launch("embedding_forward");
+  });
+  m.def("embedding_backward", [](int dt, int it, uintptr_t idx, uintptr_t dy, uintptr_t acc, uintptr_t touched,
+                                 int odt, uintptr_t grad, int accum, int64_t n, int V, int C, uintptr_t s) {
+    embedding_backward(dt, it, P<const void>(idx), P<const void>(dy), P<float>(acc), P<uint8_t>(touched), odt,
+                       P<void>(grad), accum, n, V, C, S(s));
+    check_launch("embedding_backward");
+  });
+  m.def("colsum_rows", [](int dt, uintptr_t x, uintptr_t zeros, uintptr_t part, int64_t R, int C, int odt,
+                          uintptr_t out, int accum, uintptr_t s) {
+    colsum_rows(dt, P<const void>(x), P<const float>(zeros), P<float>(part), R, C, odt, P<void>(out), accum, S(s));
+    check_launch("colsum_rows");
   });
   m.def("twobit_quantize", [](int dt, uintptr_t g, uintptr_t res, uintptr_t packed, int64_t n, float thr,
                               uintptr_t s) {

@@ -38,7 +38,13 @@ struct BnGeom {
 
 static inline BnGeom bn_geom(int C) {
   BnGeom g;
-  g.tpr = C / 8 < kBnThreads ? C / 8 : kBnThreads;
+  // threads per row: all C/8 channel groups when they fit in a block, else the largest divisor of
+  // C/8 that does (C = 3072 -> 192), so every block covers whole channel groups
+  int v = C / 8;
+  g.tpr = v;
+  if (v > kBnThreads)
+    for (g.tpr = kBnThreads; v % g.tpr != 0; --g.tpr) {
+    }
   g.cb = g.tpr * 8;
   g.rpi = kBnThreads / g.tpr;
   return g;
@@ -76,6 +82,10 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   int64_t r1 = r0 + rows_per_block;
   if (r1 > R) r1 = R;
+  // when tpr does not divide the block (C/8 not a power of two, e.g. C = 96 or 768) the last
+  // tid / tpr == rpi lanes are spare: they load nothing and stay out of the LDS reduction
+  const bool spare = lane_r >= rpi;
+  if (spare) r1 = r0;
   // rows are consumed UNR at a time: all loads of a batch are issued before any
   // accumulation, so each thread keeps UNR (x3 in backward) 16-byte loads in flight
   constexpr int UNR = 4;
@@ -124,10 +134,12 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(
   __shared__ float sh1[kBnThreads * 8];
   __shared__ float sh2[kBnThreads * 8];
   const int cb = tpr * 8;
+  if (!spare) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    sh1[lane_r * cb + lane_c * 8 + i] = s1[i];
-    sh2[lane_r * cb + lane_c * 8 + i] = s2[i];
+    for (int i = 0; i < 8; ++i) {
+      sh1[lane_r * cb + lane_c * 8 + i] = s1[i];
+      sh2[lane_r * cb + lane_c * 8 + i] = s2[i];
+    }
   }
   __syncthreads();
   for (int c = tid; c < cb; c += kBnThreads) {
@@ -452,6 +464,42 @@ int bn_nhwc_stats(int dtype, const void* x, const float* center, float* part, in
   if (dtype == kF16) STATS(__half); else if (dtype == kBF16) STATS(__hip_bfloat16); else STATS(float);
 #undef STATS
   return nblk;
+}
+
+// out[c] (+)= sum_r x[r][c] from the channel-major partials of the statistics pass
+template <typename TO>
+__global__ void __launch_bounds__(256) colsum_finalize_kernel(const float* __restrict__ part, int nblk, int C,
+                                                             TO* __restrict__ out, int accum) {
+  // one wave per column
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (c >= C) return;
+  const float* p = part + static_cast<int64_t>(c) * nblk;
+  float a = 0.f;
+  for (int i = lane; i < nblk; i += 64) a += p[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+  if (lane == 0) {
+    if (accum) a += static_cast<float>(out[c]);
+    out[c] = static_cast<TO>(a);
+  }
+}
+
+// Column sums of a row-major [R][C] matrix (bias gradient of a FullyConnected layer): the BN
+// statistics reduce (zero centre) + one wave per column.  ``part`` holds 2 * bn_partials_rows(R, C) * C floats.
+void colsum_rows(int dtype, const void* x, const float* zeros, float* part, int64_t R, int C, int out_dtype,
+                 void* out, int accum, hipStream_t s) {
+  const int nblk = bn_nhwc_stats(dtype, x, zeros, part, R, C, s);
+  const dim3 grid((C + 3) / 4);
+  if (out_dtype == kF16)
+    hipLaunchKernelGGL(colsum_finalize_kernel<__half>, grid, dim3(256), 0, s, part, nblk, C,
+                       static_cast<__half*>(out), accum);
+  else if (out_dtype == kBF16)
+    hipLaunchKernelGGL(colsum_finalize_kernel<__hip_bfloat16>, grid, dim3(256), 0, s, part, nblk, C,
+                       static_cast<__hip_bfloat16*>(out), accum);
+  else
+    hipLaunchKernelGGL(colsum_finalize_kernel<float>, grid, dim3(256), 0, s, part, nblk, C,
+                       static_cast<float*>(out), accum);
 }
 
 void bn_nhwc_forward(int dtype, const void* x, const void* addend, void* y, uint8_t* mask, const float* gamma,

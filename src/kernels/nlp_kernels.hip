@@ -509,4 +509,159 @@ void dropout_backward(int dtype, const void* dy, const uint8_t* mask, void* dx, 
                                                static_cast<const T*>(dy), mask, static_cast<T*>(dx), n / 8, p))
 }
 
+// ---------------------------------------------------------------- Embedding (gather / scatter-add)
+// Index dtypes: 0 float32 (MXNet's default index arrays), 1 int64, 2 int32; indices are clamped to [0, V).
+namespace {
+
+template <typename I>
+__device__ __forceinline__ int64_t emb_row(const void* idx, int64_t i, int V) {
+  int64_t k = static_cast<int64_t>(static_cast<const I*>(idx)[i]);
+  return k < 0 ? 0 : (k >= V ? V - 1 : k);
+}
+
+template <typename T, typename I>
+__global__ void __launch_bounds__(256) embedding_fwd_kernel(const void* __restrict__ idx, const T* __restrict__ w,
+                                                            T* __restrict__ y, int64_t n, int V, int C) {
+  const int c8 = C / 8;
+  const int64_t total = n * c8;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < total;
+       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t row = t / c8;
+    const int v = static_cast<int>(t - row * c8);
+    Vec8<T> val;
+    val.load(w + emb_row<I>(idx, row, V) * C + v * 8);
+    val.store(y + row * C + v * 8);
+  }
+}
+
+// acc[k] += dy[i] for every looked-up row k = idx[i] (fp32 hardware atomics), touched[k] = 1
+template <typename T, typename I>
+__global__ void __launch_bounds__(256) embedding_scatter_kernel(const void* __restrict__ idx,
+                                                                const T* __restrict__ dy, float* __restrict__ acc,
+                                                                uint8_t* __restrict__ touched, int64_t n, int V,
+                                                                int C) {
+  const int c8 = C / 8;
+  const int64_t total = n * c8;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < total;
+       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t row = t / c8;
+    const int v = static_cast<int>(t - row * c8);
+    const int64_t k = emb_row<I>(idx, row, V);
+    Vec8<T> g;
+    g.load(dy + row * C + v * 8);
+    float* a = acc + k * C + v * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) unsafeAtomicAdd(a + j, g.get(j));
+    if (v == 0) touched[k] = 1;
+  }
+}
+
+// Small tables (V*C fp32 fits in LDS, e.g. BERT's 2-row token-type embedding): every block
+// pre-reduces a chunk of rows in LDS and flushes one global atomic per non-zero entry, so thousands
+// of lookups of the same few rows do not serialise on the same global addresses.
+constexpr int kEmbSmallFloats = 16384;
+template <typename T, typename I>
+__global__ void __launch_bounds__(256) embedding_scatter_small_kernel(const void* __restrict__ idx,
+                                                                      const T* __restrict__ dy,
+                                                                      float* __restrict__ acc,
+                                                                      uint8_t* __restrict__ touched, int64_t n,
+                                                                      int V, int C, int64_t rows_per_block) {
+  __shared__ float lds[kEmbSmallFloats];
+  const int vc = V * C;
+  for (int i = threadIdx.x; i < vc; i += 256) lds[i] = 0.f;
+  __syncthreads();
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  int64_t r1 = r0 + rows_per_block;
+  if (r1 > n) r1 = n;
+  const int c8 = C / 8;
+  const int64_t work = (r1 - r0) * c8;
+  for (int64_t t = threadIdx.x; t < work; t += 256) {
+    const int64_t row = r0 + t / c8;
+    const int v = static_cast<int>(t % c8);
+    const int64_t k = emb_row<I>(idx, row, V);
+    Vec8<T> g;
+    g.load(dy + row * C + v * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(&lds[k * C + v * 8 + j], g.get(j));
+    if (v == 0) touched[k] = 1;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < vc; i += 256) {
+    const float a = lds[i];
+    if (a != 0.f) unsafeAtomicAdd(acc + i, a);
+  }
+}
+
+// grad[k] (+)= acc[k] for touched rows (then acc[k] = 0, touched[k] = 0: the scratch is left all-zero
+// for the next call); untouched rows are zero-filled unless accumulating.  One wave per row.
+template <typename TO>
+__global__ void __launch_bounds__(256) embedding_finalize_kernel(float* __restrict__ acc,
+                                                                 uint8_t* __restrict__ touched,
+                                                                 TO* __restrict__ grad, int V, int C, int accum) {
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (k >= V) return;
+  const bool hit = touched[k] != 0;
+  if (!hit && accum) return;
+  const int c8 = C / 8;
+  for (int v = lane; v < c8; v += 64) {
+    Vec8<TO> out;
+    float* a = acc + k * C + v * 8;
+    if (accum) out.load(grad + k * C + v * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float add = hit ? a[j] : 0.f;
+      out.set(j, (accum ? out.get(j) : 0.f) + add);
+    }
+    out.store(grad + k * C + v * 8);
+    if (hit) {
+      float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(a) = z;
+      *reinterpret_cast<float4*>(a + 4) = z;
+    }
+  }
+  if (hit && lane == 0) touched[k] = 0;
+}
+
+#define MXAMD_INDEX_SWITCH(itype, ...)                  \
+  if (itype == 0) { typedef float I; __VA_ARGS__; }     \
+  else if (itype == 1) { typedef int64_t I; __VA_ARGS__; } \
+  else { typedef int32_t I; __VA_ARGS__; }
+
+}  // namespace
+
+void embedding_forward(int dtype, int itype, const void* idx, const void* w, void* y, int64_t n, int V, int C,
+                       hipStream_t s) {
+  MXAMD_HOST_CHECK(C % 8 == 0, "embedding: output_dim must be a multiple of 8");
+  const int blocks = ew_blocks(n * (C / 8));
+  MXAMD_DTYPE_SWITCH(dtype, MXAMD_INDEX_SWITCH(itype, hipLaunchKernelGGL((embedding_fwd_kernel<T, I>), dim3(blocks),
+                                                                         dim3(256), 0, s, idx,
+                                                                         static_cast<const T*>(w),
+                                                                         static_cast<T*>(y), n, V, C)))
+}
+
+// acc: V*C fp32 and touched: V bytes, both all-zero on entry (and on exit)
+void embedding_backward(int dtype, int itype, const void* idx, const void* dy, float* acc, uint8_t* touched,
+                        int out_dtype, void* grad, int accum, int64_t n, int V, int C, hipStream_t s) {
+  MXAMD_HOST_CHECK(C % 8 == 0, "embedding: output_dim must be a multiple of 8");
+  if (static_cast<int64_t>(V) * C <= kEmbSmallFloats) {
+    int64_t rpb = 64;
+    while ((n + rpb - 1) / rpb > 512) rpb *= 2;
+    const int blocks = static_cast<int>((n + rpb - 1) / rpb);
+    MXAMD_DTYPE_SWITCH(dtype, MXAMD_INDEX_SWITCH(itype, hipLaunchKernelGGL((embedding_scatter_small_kernel<T, I>),
+                                                                           dim3(blocks), dim3(256), 0, s, idx,
+                                                                           static_cast<const T*>(dy), acc, touched,
+                                                                           n, V, C, rpb)))
+  } else {
+    const int blocks = ew_blocks(n * (C / 8));
+    MXAMD_DTYPE_SWITCH(dtype, MXAMD_INDEX_SWITCH(itype, hipLaunchKernelGGL((embedding_scatter_kernel<T, I>),
+                                                                           dim3(blocks), dim3(256), 0, s, idx,
+                                                                           static_cast<const T*>(dy), acc, touched,
+                                                                           n, V, C)))
+  }
+  const dim3 grid((V + 3) / 4);
+  MXAMD_DTYPE_SWITCH(out_dtype, hipLaunchKernelGGL((embedding_finalize_kernel<T>), grid, dim3(256), 0, s, acc,
+                                                   touched, static_cast<T*>(grad), V, C, accum))
+}
+
 }  // namespace mxamd

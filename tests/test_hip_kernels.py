@@ -26,7 +26,8 @@ def _bn_ref(x, g, b, eps, addend=None, relu=False):
 
 
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16, torch.float32])
-@pytest.mark.parametrize('shape', [(4, 7, 7, 64), (2, 14, 14, 256), (3, 5, 5, 2048), (8, 3, 3, 24)])
+@pytest.mark.parametrize('shape', [(4, 7, 7, 64), (2, 14, 14, 256), (3, 5, 5, 2048), (8, 3, 3, 24), (4, 5, 5, 96),
+                                   (2, 9, 9, 768), (2, 5, 5, 3072)])
 @pytest.mark.parametrize('mode', ['plain', 'relu', 'add_relu'])
 def test_bn_nhwc_forward_backward(dtype, shape, mode):
     K = _lib()
@@ -685,3 +686,66 @@ def test_conv_autotune_rejects_wrong_candidate():
     name, out = KF._time_candidates([('bad', bad), ('miopen', good)], key=key)
     assert name == 'miopen' and 'bad' in KF._REJECTED[key]
     torch.testing.assert_close(out, x * 2)
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('mn', [(4096, 768), (333, 96), (8192, 3072), (7, 8)])
+@pytest.mark.parametrize('out_dtype', [torch.float32, torch.bfloat16])
+def test_colsum_rows_bias_grad(dtype, mn, out_dtype):
+    K = _lib()
+    from mxnet_maintenance_amd.ops import kernel_fns as KF
+    M, N = mn
+    torch.manual_seed(1)
+    x = torch.randn(M, N, device='cuda').to(dtype)
+    lib = K.lib()
+    part = torch.empty(2 * lib.bn_partials_rows(M, N) * N, dtype=torch.float32, device='cuda')
+    out = torch.randn(N, device='cuda').to(out_dtype)
+    base = out.float().clone()
+    lib.colsum_rows(KF._DT[dtype], x.data_ptr(), KF._zeros_f32(N, x.device).data_ptr(), part.data_ptr(), M, N,
+                    KF._DT[out_dtype], out.data_ptr(), 1, torch.cuda.current_stream().cuda_stream)
+    ref = base + x.float().sum(0)
+    tol = 2e-2 if out_dtype == torch.bfloat16 else 1e-3
+    torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol * max(1.0, M ** 0.5))
+
+
+def test_linear_direct_weight_and_bias_grads():
+    import numpy as np
+    import mxnet_maintenance_amd as mx
+    from mxnet_maintenance_amd import autograd, gluon, nd
+    mx.random.seed(0)
+    net = gluon.nn.Dense(256, flatten=False, in_units=128)
+    net.initialize(mx.init.Xavier(), ctx=mx.gpu(0))
+    net.cast('bfloat16')
+    x = nd.array(np.random.RandomState(0).randn(4, 64, 128), ctx=mx.gpu(0), dtype='bfloat16')
+    w = net.weight.data().asnumpy().astype(np.float32)
+    xs = x.asnumpy().astype(np.float32).reshape(-1, 128)
+    for _ in range(3):     # first call autotunes, later ones accumulate straight into .grad
+        with autograd.record():
+            y = net(x)
+        y.backward()
+    dy = np.ones((xs.shape[0], 256), np.float32)
+    np.testing.assert_allclose(net.weight.grad().asnumpy().astype(np.float32), dy.T @ xs, rtol=3e-2, atol=0.5)
+    np.testing.assert_allclose(net.bias.grad().asnumpy().astype(np.float32), dy.sum(0), rtol=2e-2)
+    assert w.shape == (256, 128)
+
+
+@pytest.mark.parametrize('wdt', [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize('idt', [torch.float32, torch.int64, torch.int32])
+@pytest.mark.parametrize('vc', [(1000, 96), (2, 768)])     # global-atomic and LDS-privatised scatter
+def test_embedding_gather_scatter_matches_torch(wdt, idt, vc):
+    _lib()
+    from mxnet_maintenance_amd.ops import nlp_fns
+    torch.manual_seed(0)
+    V, C = vc
+    idx = torch.randint(-3, V + 3, (7, 33), device='cuda')     # out-of-range ids clamp, repeats accumulate
+    w = torch.randn(V, C, device='cuda').to(wdt).requires_grad_()
+    wr = w.detach().float().clone().requires_grad_()
+    for _ in range(2):      # the second call checks the scratch was left zeroed
+        y = nlp_fns.Embedding.apply(idx.to(idt), w)
+        dy = torch.randn_like(y)
+        y.backward(dy)
+        yr = torch.nn.functional.embedding(idx.clamp(0, V - 1), wr)
+        yr.backward(dy.float())
+        torch.testing.assert_close(y.float(), yr, rtol=0, atol=0)
+        tol = 1e-5 if wdt == torch.float32 else 3e-2
+        torch.testing.assert_close(w.grad.float(), wr.grad, rtol=tol, atol=tol)
