@@ -212,7 +212,7 @@ class Trainer:
         if self._kvstore is not None and self._kvstore._compression is not None:
             return False
         for p in self._params:
-            if p._data is None or p._stype != 'default':
+            if p._data is None or p._stype != 'default' or getattr(p, '_grad_stype', 'default') != 'default':
                 return False
         return True
 

@@ -282,14 +282,25 @@ class KVStore(KVStoreBase):
         keys = _as_list(key)
         outs = out if isinstance(key, (list, tuple)) else [out]
         rids = row_ids if isinstance(row_ids, (list, tuple)) and isinstance(key, (list, tuple)) else [row_ids]
+        from ..ndarray.sparse import RowSparseNDArray
         with torch.no_grad():
             for k, o, r in zip(keys, outs, rids):
-                src = self._store[k]._data
+                st = self._store[k]
+                src = st._data if not isinstance(st, RowSparseNDArray) else None
                 for oo, rr in zip(_as_list(o), _as_list(r) * len(_as_list(o))):
-                    idx = rr._data.to(torch.int64).to(src.device)
-                    res = torch.zeros_like(src)
-                    res[idx] = src[idx]
-                    oo._data.copy_(res.to(oo._data.device))
+                    dev = (src.device if src is not None else st._values().device)
+                    idx = torch.unique(rr._data.to(torch.int64).reshape(-1).to(dev))   # sorted, no duplicates
+                    # only the requested rows move: no dense zeros tensor of the full weight
+                    rows = src.index_select(0, idx) if src is not None else \
+                        _rsp_rows(st, idx)
+                    if isinstance(oo, RowSparseNDArray):
+                        odev = oo.context.torch_device
+                        oo._vals, oo._aux, oo._shp = rows.to(odev), (idx.to(odev),), tuple(st.shape)
+                        oo._dense, oo._stale = None, False
+                    else:
+                        res = torch.zeros_like(oo._data)
+                        res.index_copy_(0, idx.to(res.device), rows.to(res.device, res.dtype))
+                        oo._data.copy_(res)
 
     def set_gradient_compression(self, compression_params):
         if 'device' in self._type or 'dist' in self._type or self._type in ('local', 'nccl'):
@@ -331,3 +342,14 @@ def create(name='local'):
     if name not in valid:
         raise MXNetError('Unknown KVStore type %s' % name)
     return KVStore(name)
+
+
+def _rsp_rows(st, idx):
+    """Rows ``idx`` of a row_sparse stored value (zeros for rows it does not hold)."""
+    st._sync()
+    have = st._aux[0]
+    out = torch.zeros((idx.numel(),) + tuple(st.shape[1:]), dtype=st._vals.dtype, device=st._vals.device)
+    hit = torch.isin(idx, have)
+    if bool(hit.any()):
+        out[hit] = st._vals.index_select(0, torch.searchsorted(have, idx[hit]))
+    return out

@@ -257,6 +257,12 @@ class SGD(Optimizer):
         lrs = self._get_lrs(indices)
         wds = self._get_wds(indices)
         clip = self._clip()
+        if self.lazy_update and any(_is_rsp(g) for g in grads):
+            for w, g, st, lr, wd in zip(weights, grads, states, lrs, wds):
+                mom, w32 = (st if multi_precision else (st, None))
+                _lazy_sgd_rows(w._data, g, None if mom is None else mom._data,
+                               None if w32 is None else w32._data, lr, wd, self.momentum, self.rescale_grad, clip)
+            return
         W = [w._data for w in weights]
         G = [g._data for g in grads]
         if multi_precision:
@@ -274,6 +280,59 @@ class SGD(Optimizer):
         ws = _as_list(weight)
         use_mp = self.multi_precision and ws[0]._data.dtype in (torch.float16, torch.bfloat16)
         self._update_impl(index, weight, grad, state, multi_precision=use_mp)
+
+
+def _is_rsp(g):
+    return getattr(g, 'stype', 'default') == 'row_sparse'
+
+
+def _rsp_rows_of(g, device):
+    """(row ids, fp32 row values) of a row_sparse gradient (compressed storage, no densify)."""
+    idx = g._aux_arrays()[0].to(device)
+    return idx, g._values().to(device).float()
+
+
+def _prep_grad(gr, w_rows, wd, rescale, clip):
+    gr = gr * rescale
+    if clip is not None and clip >= 0:
+        gr = gr.clamp(-clip, clip)
+    return gr + wd * w_rows if wd else gr
+
+
+@torch.no_grad()
+def _lazy_sgd_rows(w, g, mom, w32, lr, wd, momentum, rescale, clip):
+    """SGD(-momentum) touching only the rows a row_sparse gradient holds (reference: lazy_update=True,
+    src/operator/optimizer_op-inl.h SGDMomLazyUpdateRspImpl)."""
+    idx, gr = _rsp_rows_of(g, w.device)
+    if idx.numel() == 0:
+        return
+    tgt = w32 if w32 is not None else w
+    rows = tgt.index_select(0, idx).float()
+    step = _prep_grad(gr, rows, wd, rescale, clip)
+    if momentum != 0.0 and mom is not None:
+        m = mom.index_select(0, idx).float().mul_(momentum).sub_(lr * step)
+        mom.index_copy_(0, idx, m.to(mom.dtype))
+        rows = rows + m
+    else:
+        rows = rows - lr * step
+    tgt.index_copy_(0, idx, rows.to(tgt.dtype))
+    if w32 is not None:
+        w.index_copy_(0, idx, rows.to(w.dtype))
+
+
+@torch.no_grad()
+def _lazy_adam_rows(w, g, mean, var, lr, beta1, beta2, eps, wd, rescale, clip):
+    """Adam over the rows of a row_sparse gradient only (AdamLazyUpdateRspImpl)."""
+    idx, gr = _rsp_rows_of(g, w.device)
+    if idx.numel() == 0:
+        return
+    rows = w.index_select(0, idx).float()
+    step = _prep_grad(gr, rows, wd, rescale, clip)
+    m = mean.index_select(0, idx).float().mul_(beta1).add_(step, alpha=1 - beta1)
+    v = var.index_select(0, idx).float().mul_(beta2).addcmul_(step, step, value=1 - beta2)
+    mean.index_copy_(0, idx, m.to(mean.dtype))
+    var.index_copy_(0, idx, v.to(var.dtype))
+    w.index_copy_(0, idx, (rows - lr * m / (v.sqrt() + eps)).to(w.dtype))
 
 
 @torch.no_grad()
@@ -620,6 +679,10 @@ class Adam(Optimizer):
         coef2 = 1. - self.beta2 ** t
         lr *= math.sqrt(coef2) / coef1
         mean, var = state
+        if self.lazy_update and _is_rsp(grad):
+            _lazy_adam_rows(weight._data, grad, mean._data, var._data, lr, self.beta1, self.beta2, self.epsilon, wd,
+                            self.rescale_grad, self._clip())
+            return
         _oo.adam_update(weight._data, grad._data, mean._data, var._data, lr=lr, beta1=self.beta1,
                         beta2=self.beta2, epsilon=self.epsilon, wd=wd, rescale_grad=self.rescale_grad,
                         clip_gradient=self._clip())

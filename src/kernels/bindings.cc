@@ -25,6 +25,10 @@ void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, c
                       const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R, int C,
                       int relu_mode, int fix_gamma, int training, int accum, hipStream_t s);
 int bn_partials_rows(int64_t R, int C);
+void csr_dot_dense(int dtype, const int64_t* indptr, const int64_t* indices, const void* vals, const void* rhs,
+                   void* out, int64_t M, int64_t K, int N, hipStream_t s);
+void csrT_dot_dense(int dtype, const int64_t* indptr, const int64_t* indices, const void* vals, const void* rhs,
+                    const int64_t* slot, float* out32, int64_t M, int64_t K, int N, hipStream_t s);
 void embedding_forward(int dtype, int itype, const void* idx, const void* w, void* y, int64_t n, int V, int C,
                        hipStream_t s);
 void embedding_backward(int dtype, int itype, const void* idx, const void* dy, float* acc, uint8_t* touched,
@@ -124,6 +128,18 @@ PYBIND11_MODULE(_hip_kernels, m) {
     embedding_backward(dt, it, P<const void>(idx), P<const void>(dy), P<float>(acc), P<uint8_t>(touched), odt,
                        P<void>(grad), accum, n, V, C, S(s));
     check_launch("embedding_backward");
+  });
+  m.def("csr_dot_dense", [](int dt, uintptr_t indptr, uintptr_t indices, uintptr_t vals, uintptr_t rhs, uintptr_t out,
+                            int64_t M, int64_t K, int N, uintptr_t s) {
+    csr_dot_dense(dt, P<const int64_t>(indptr), P<const int64_t>(indices), P<const void>(vals), P<const void>(rhs),
+                  P<void>(out), M, K, N, S(s));
+    check_launch("csr_dot_dense");
+  });
+  m.def("csrT_dot_dense", [](int dt, uintptr_t indptr, uintptr_t indices, uintptr_t vals, uintptr_t rhs,
+                             uintptr_t slot, uintptr_t out32, int64_t M, int64_t K, int N, uintptr_t s) {
+    csrT_dot_dense(dt, P<const int64_t>(indptr), P<const int64_t>(indices), P<const void>(vals), P<const void>(rhs),
+                   P<const int64_t>(slot), P<float>(out32), M, K, N, S(s));
+    check_launch("csrT_dot_dense");
   });
   m.def("colsum_rows", [](int dt, uintptr_t x, uintptr_t zeros, uintptr_t part, int64_t R, int C, int odt,
                           uintptr_t out, int accum, uintptr_t s) {
