@@ -26,7 +26,10 @@ class _ThreadScope:
 
     @classmethod
     def _default(cls):
-        return cls()
+        # the default lives on the class that owns the stack (NameManager, not its Prefix subclass,
+        # whose constructor needs arguments)
+        owner = next(c for c in cls.__mro__ if '_tls' in c.__dict__ and c is not _ThreadScope)
+        return owner()
 
     @classmethod
     def current(cls):

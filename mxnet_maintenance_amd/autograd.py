@@ -13,6 +13,8 @@ record/train scopes.
 """
 from contextlib import contextmanager
 
+import weakref
+
 import torch
 
 from . import _state
@@ -96,6 +98,11 @@ def mark_variables(variables, gradients, grad_reqs='write'):
         v._grad = g
 
 
+# heads whose recorded graph a backward without retain_graph released (reference: the engine frees
+# the graph nodes; differentiating through them again is an error even when torch could replay them)
+_RELEASED = weakref.WeakKeyDictionary()
+
+
 def _collect_leaves(retain):
     leaves = list(_state.STATE.tape_leaves.values())
     if not retain:
@@ -165,6 +172,13 @@ def backward(heads, head_grads=None, retain_graph=False, train_mode=True, create
         raise MXNetError('Cannot differentiate node because it is not in a computational graph. '
                          'You need to set is_recording to true or use autograd.record() to save '
                          'computational graphs for backward.')
+    for h in heads:
+        if h in _RELEASED:
+            raise MXNetError('Check failed: the graph of this output was already freed by a backward pass '
+                             'without retain_graph=True; record it again or pass retain_graph=True')
+    if not (retain_graph or create_graph):
+        for h in heads:
+            _RELEASED[h] = True
     leaves = _collect_leaves(retain_graph)
     _prepare_leaves(leaves)
     prev_train = set_training(train_mode)

@@ -113,6 +113,14 @@ class Parameter:
             "Expected shape %s is incompatible with given shape %s." % (str(new_shape), str(self._shape))
         self._shape = tuple(new_shape)
 
+    def _set_trainer(self, trainer):
+        """Attach the Trainer that updates this parameter (a sparse parameter allows only one)."""
+        if self._stype != 'default' and getattr(self, '_trainer', None) is not None and trainer is not None \
+                and self._trainer is not trainer:
+            raise RuntimeError("Failed to set the trainer for Parameter '%s' because it was already set. More "
+                               "than one trainers for a %s Parameter is not supported." % (self.name, self._stype))
+        self._trainer = trainer
+
     @property
     def stype(self):
         return self._stype
@@ -186,6 +194,11 @@ class Parameter:
                     self.name, str(ctx), str(self.list_ctx()))
             self.set_data(data)
         self._deferred_init = ()
+        # weights held by the kvstore are stale now: the trainer re-initialises its store
+        tr = getattr(self, '_trainer', None)
+        if tr is not None and getattr(tr, '_kv_initialized', False) and getattr(tr, '_update_on_kvstore', False) \
+                and self not in tr._params_to_init:
+            tr._reset_kvstore()
 
     def _finish_deferred_init(self):
         if not self._deferred_init:
@@ -220,7 +233,7 @@ class Parameter:
             self._grad = None
             return
         for d in self._data:
-            d.attach_grad(self.grad_req)
+            d.attach_grad(self.grad_req, stype=None if self._grad_stype == 'default' else self._grad_stype)
         self._grad = [d._grad for d in self._data]
         if self._trainer is not None and hasattr(self._trainer, '_on_param_grad_reset'):
             self._trainer._on_param_grad_reset(self)
@@ -285,11 +298,30 @@ class Parameter:
             for arr in self._check_and_get(self._data, list):
                 arr._data.copy_(src.to(arr._data.device, arr._data.dtype))
 
+    def _get_row_sparse(self, ctx, row_id):
+        if not isinstance(row_id, NDArray):
+            raise TypeError('row_id must have NDArray type, but %s is given' % type(row_id))
+        if self._trainer is None:
+            raise RuntimeError("Cannot get row_sparse data for Parameter '%s' when no Trainer is created with "
+                               "it." % self.name)
+        results = self._check_and_get(self._data, ctx)
+        # only the requested rows are fetched from the kvstore into the local copies
+        self._trainer._row_sparse_pull(self, results, row_id)
+        return results
+
     def row_sparse_data(self, row_id):
-        return self.data(row_id.context)
+        """The rows ``row_id`` of a row_sparse parameter, on ``row_id``'s context."""
+        if self._stype != 'row_sparse':
+            raise RuntimeError("Cannot return a copy of Parameter %s via row_sparse_data() because its storage "
+                               "type is %s. Please use data() instead." % (self.name, self._stype))
+        return self._get_row_sparse(row_id.context, row_id)
 
     def list_row_sparse_data(self, row_id):
-        return self.list_data()
+        if self._stype != 'row_sparse':
+            raise RuntimeError("Cannot return copies of Parameter '%s' on all contexts via "
+                               "list_row_sparse_data() because its storage type is %s. Please use data() "
+                               "instead." % (self.name, self._stype))
+        return self._get_row_sparse(list, row_id)
 
     def data(self, ctx=None):
         if self._stype != 'default':

@@ -106,7 +106,7 @@ class Trainer:
                                  % (type(param)))
             self._param2idx[param.name] = i
             self._params.append(param)
-            param._trainer = self
+            param._set_trainer(self)
         self._compression_params = compression_params
         self._contexts = self._check_contexts()
         optimizer_params = optimizer_params if optimizer_params else {}
@@ -146,6 +146,8 @@ class Trainer:
         else:
             self._optimizer = opt.create(optimizer, param_dict=param_dict, **optimizer_params)
         self._updaters = [opt.get_updater(self._optimizer) for _ in (self._contexts or [None])]
+        for i, u in enumerate(self._updaters):
+            u.device_slot = i
 
     def _init_params(self):
         assert self._kv_initialized, 'Cannot initialize parameters in KVStore when KVStore is not initialized.'
@@ -178,25 +180,48 @@ class Trainer:
         update_on_kvstore = config['update_on_kvstore']
         self._contexts = self._check_contexts()
         multi_ctx = self._contexts is not None and len(self._contexts) > 1
+        ranks = max(dist.world_size(), int(os.environ.get('WORLD_SIZE', '1')))
+        sparse_weight = any(p._stype != 'default' for p in self._params)
+        sparse_grad = any(getattr(p, '_grad_stype', 'default') != 'default' for p in self._params)
         if isinstance(kvstore, (_kvs.KVStoreBase,)):
             kv = kvstore
         elif kvstore is None or kvstore is False:
             kv = None
         else:
-            need = multi_ctx or ('dist' in str(kvstore)) or dist.world_size() > 1 or \
-                int(os.environ.get('WORLD_SIZE', '1')) > 1
+            # reference: no kvstore for one device on one machine unless the weights are sparse
+            need = multi_ctx or ('dist' in str(kvstore)) or ranks > 1 or sparse_weight
             kv = _kvs.create(kvstore) if need else None
         if kv is not None and self._compression_params:
             kv.set_gradient_compression(self._compression_params)
-        self._distributed = kv is not None and (kv.num_workers > 1 if hasattr(kv, 'num_workers') else False)
-        if update_on_kvstore is None:
-            update_on_kvstore = False
+        self._distributed = kv is not None and ('dist' in kv.type or ranks > 1)
+        if sparse_weight:
+            # sparse weights live (and are updated) on the kvstore
+            if update_on_kvstore is False:
+                raise ValueError('Cannot set update_on_kvstore=False when sparse weights are present.')
+            update_on_kvstore = True
+        elif update_on_kvstore is None:
+            if sparse_grad or ranks > 1:
+                # dense weight + sparse grad: update locally; one process per GPU (RCCL): all-reduce the
+                # gradients and run the fused local update on every rank (no parameter server round trip)
+                update_on_kvstore = self._distributed and 'async' in getattr(kv, 'type', '')
+            else:
+                # in-process multi-device: MXNET_UPDATE_ON_KVSTORE (default 1) like the reference, when
+                # the store can run the optimizer and (for 'local') no weight exceeds 16M elements
+                update_on_kvstore = bool(int(os.environ.get('MXNET_UPDATE_ON_KVSTORE', '1'))) and \
+                    kv is not None and kv.is_capable(_kvs.KVStoreBase.OPTIMIZER)
+                if update_on_kvstore and kvstore == 'local' and \
+                        max(int(np.prod(p.shape)) for p in self._params) > 1024 * 1024 * 16:
+                    update_on_kvstore = False
         if kv is not None and update_on_kvstore and not kv.is_capable(_kvs.KVStoreBase.OPTIMIZER):
             raise ValueError('Please set update_on_kvstore=False when training with {}'.format(type(kv)))
-        self._kvstore = kv
-        self._update_on_kvstore = bool(kv is not None and update_on_kvstore)
-        if self._update_on_kvstore:
-            kv.set_optimizer(self._optimizer)
+        if kv is None:
+            self._kvstore = None
+            self._update_on_kvstore = None
+        else:
+            self._kvstore = kv
+            self._update_on_kvstore = bool(update_on_kvstore)
+            if self._update_on_kvstore:
+                kv.set_optimizer(self._optimizer)
         self._kv_initialized = True
 
     # ------------------------------------------------------------ fast path
@@ -367,6 +392,14 @@ class Trainer:
                 keys.append(i)
                 vals.append(param.list_grad())
         if not keys:
+            return
+        if not isinstance(self._kvstore, _kvs.KVStore):
+            # a user-registered KVStoreBase: one key per call, like the reference trainer
+            for k, v in zip(keys, vals):
+                if self._update_on_kvstore:
+                    self._kvstore.pushpull(k, v, out=self._params[k].list_data(), priority=-k)
+                else:
+                    self._kvstore.pushpull(k, v, priority=-k)
             return
         if self._update_on_kvstore:
             self._kvstore.pushpull(keys, vals, [p.list_data() for p in self._params if p.grad_req != 'null'])

@@ -63,6 +63,14 @@ class LRScheduler:
         return '%s(base_lr=%g, warmup_steps=%d)' % (type(self).__name__, self.base_lr, self.warmup_steps)
 
 
+def _repeat_mul(lr, factor, n):
+    """``lr * factor ** n`` as n successive multiplications: bit-identical to a schedule that decays
+    its learning rate in place once per period (what user code comparing lr values expects)."""
+    for _ in range(n):
+        lr *= factor
+    return lr
+
+
 class FactorScheduler(LRScheduler):
     """``base_lr * factor ** k`` after ``k`` completed periods of ``step`` updates, floored at
     ``stop_factor_lr`` (the k-th decay applies once ``num_update > k * step``)."""
@@ -80,7 +88,7 @@ class FactorScheduler(LRScheduler):
 
     def _decayed(self, num_update):
         periods = max(0, -(-num_update // self.step) - 1)     # ceil(t / step) - 1, never negative
-        return max(self.base_lr * self.factor ** periods, self.stop_factor_lr)
+        return max(_repeat_mul(self.base_lr, self.factor, periods), self.stop_factor_lr)
 
 
 class MultiFactorScheduler(LRScheduler):
@@ -101,7 +109,7 @@ class MultiFactorScheduler(LRScheduler):
 
     def _decayed(self, num_update):
         passed = bisect.bisect_left(self.step, num_update)      # marks strictly below num_update
-        return self.base_lr * self.factor ** passed
+        return _repeat_mul(self.base_lr, self.factor, passed)
 
 
 class _AnnealTo(LRScheduler):

@@ -291,10 +291,18 @@ class NDArray:
         t.requires_grad_(True)
         self._data = t
         g = torch.zeros_like(t)
+        gstype = stype or self._stype
+        if gstype != 'default':
+            # sparse gradient buffer (reference: attach_grad(stype=...)); its dense view is the tensor
+            # autograd accumulates into, the compressed form is derived on access
+            from . import sparse
+            self._grad = {'row_sparse': sparse.RowSparseNDArray, 'csr': sparse.CSRNDArray}[gstype](g)
+            g = self._grad._data
+        else:
+            self._grad = NDArray(g)
+            if self.__class__ is not NDArray and self._stype == 'default':
+                self._grad.__class__ = self.__class__
         t.grad = g
-        self._grad = NDArray(g)
-        if self.__class__ is not NDArray and self._stype == 'default':
-            self._grad.__class__ = self.__class__
         self._grad_req = grad_req
 
     def _set_grad_buffer(self, gbuf, grad_req='write'):

@@ -202,6 +202,10 @@ class BaseSparseNDArray(NDArray):
     def __deepcopy__(self, memo):
         return self.copy()
 
+    def detach(self):
+        self._sync()
+        return type(self)._make(self._vals.detach(), list(self._aux), self._shp)
+
     def astype(self, dtype, copy=True):
         self._sync()
         td = torch_dtype(dtype)
@@ -573,7 +577,10 @@ def _csr_dot_dense(a, rhs, transpose_a):
 def dot(lhs, rhs, transpose_a=False, transpose_b=False, forward_stype=None):
     """Sparse-aware dot: csr . dense (and csr^T . dense -> row_sparse) on compressed storage."""
     from .ndarray import _op
-    if isinstance(lhs, CSRNDArray) and not isinstance(rhs, BaseSparseNDArray) and not transpose_b:
+    from .. import _state
+    if _state.STATE.recording:
+        r = _op('dot', NDArray(lhs._data), NDArray(rhs._data), transpose_a=transpose_a, transpose_b=transpose_b)
+    elif isinstance(lhs, CSRNDArray) and not isinstance(rhs, BaseSparseNDArray) and not transpose_b:
         r = _csr_dot_dense(lhs, rhs._data.detach(), transpose_a)
     elif isinstance(lhs, CSRNDArray) and isinstance(rhs, RowSparseNDArray) and not transpose_b:
         r = _csr_dot_dense(lhs, rhs._densify(), transpose_a)
@@ -602,6 +609,14 @@ def _rsp_union(a, b, fn):
 def _elem(op, torch_fn, zero_preserving_scalar):
     def f(lhs, rhs):
         from .ndarray import _op
+        from .. import _state
+        if _state.STATE.recording:
+            # autograd: the dense views carry the graph (compressed values are not differentiable leaves)
+            lt = lhs._data if isinstance(lhs, NDArray) else torch.as_tensor(lhs)
+            rt = rhs._data if isinstance(rhs, NDArray) else rhs
+            if isinstance(rt, torch.Tensor):
+                return _op(op, NDArray(lt), NDArray(rt))
+            return NDArray(torch_fn(lt, rt))
         if isinstance(lhs, RowSparseNDArray) and isinstance(rhs, RowSparseNDArray) and lhs.shape == rhs.shape \
                 and op in ('broadcast_add', 'broadcast_sub'):
             return _rsp_union(lhs, rhs, torch_fn)

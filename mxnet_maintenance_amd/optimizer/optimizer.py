@@ -945,6 +945,11 @@ class Updater:
             indices, grads, weights = [index], [grad], [weight]
         else:
             indices, grads, weights = index, grad, weight
+        if weights:
+            # one update-count table per device: updaters of different contexts advance it independently
+            # (the Trainer numbers its per-context updaters; CPU contexts share one torch device)
+            slot = getattr(self, 'device_slot', None)
+            self.optimizer._set_current_context(slot if slot is not None else weights[0].context.device_id)
         for i, idx in enumerate(indices):
             if idx not in self.states:
                 self.states[idx] = self.optimizer.create_state_multi_precision(idx, weights[i])

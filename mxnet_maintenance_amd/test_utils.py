@@ -17,8 +17,16 @@ import numpy.random as rnd            # noqa: F401  (re-exported, as the referen
 import numpy.testing as npt           # noqa: F401
 from collections import OrderedDict   # noqa: F401
 
+import gzip                           # noqa: F401  (the reference module's imports are part of
+import json                           # noqa: F401   its ``from mxnet.test_utils import *`` surface)
+import logging                        # noqa: F401
+import numbers                        # noqa: F401
+import time                           # noqa: F401
+import traceback                      # noqa: F401
+
 from . import ndarray as nd
 from . import symbol as sym_mod
+mx = sys.modules[__package__]   # the framework package: tests reach ``mx`` through the star import
 from .base import MXNetError
 from .context import Context, cpu, gpu, current_context
 from .ndarray import array            # noqa: F401  (tests use it via ``from mxnet.test_utils import *``)

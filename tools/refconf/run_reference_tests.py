@@ -21,7 +21,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_REF = '/root/reference/tests/python'
 
 
-def run_one(ref, name, timeout, workers):
+def run_one(ref, name, timeout, workers, select=None, tb=None):
     tmp = tempfile.mkdtemp(prefix='mxref_')
     try:
         unit = os.path.join(tmp, 'unittest')
@@ -41,6 +41,10 @@ def run_one(ref, name, timeout, workers):
                '--timeout', str(timeout), '-o', 'addopts=', '--rootdir', tmp, os.path.join(unit, name + '.py')]
         if workers > 1:
             cmd[3:3] = ['-n', str(workers)]
+        if select:
+            cmd[3:3] = ['-k', select]
+        if tb:
+            cmd[3:3] = ['--tb', tb]
         r = subprocess.run(cmd, cwd=unit, env=env, capture_output=True, text=True)
         tail = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr[-500:]
         counts = {k: 0 for k in ('passed', 'failed', 'skipped', 'errors', 'error', 'xfailed', 'xpassed')}
@@ -59,10 +63,14 @@ def main():
     ap.add_argument('--timeout', type=int, default=120)
     ap.add_argument('-n', '--workers', type=int, default=1)
     ap.add_argument('--show-failures', action='store_true')
+    ap.add_argument('-k', dest='select', default=None, help='pytest -k expression')
+    ap.add_argument('--tb', default=None, help='pytest traceback style; prints the full output')
     a = ap.parse_args()
     for name in a.names:
-        res = run_one(a.ref, name, a.timeout, a.workers)
+        res = run_one(a.ref, name, a.timeout, a.workers, a.select, a.tb)
         out = res.pop('output')
+        if a.tb:
+            print(out)
         print(json.dumps(res), flush=True)
         if a.show_failures:
             for line in out.splitlines():
