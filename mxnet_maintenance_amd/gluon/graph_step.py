@@ -40,6 +40,9 @@ The step function must not read device values on the host (``asnumpy``,
 ``asscalar``) and must be shape-stable; AMP dynamic loss scaling (a host-side
 overflow check) is not supported inside a captured step.
 """
+import gc
+import os
+
 import torch
 
 from .. import _state
@@ -106,6 +109,8 @@ class GraphStep:
         if self._trainer is not None:
             self._trainer._enter_graph_mode()
         s = self._side_stream(dev)
+        if os.environ.get('MXAMD_GRAPH_GC', '1') == '1':
+            gc.collect()
         torch.cuda.synchronize(dev)
         graph = torch.cuda.CUDAGraph()
         _state.GRAPH_RNG[0] = self._rng

@@ -324,12 +324,16 @@ class Linear(torch.autograd.Function):
         return dx, dw, db
 
 
+import os as _os                       # noqa: E402
+_FC_DIRECT = _os.environ.get('MXAMD_FC_DIRECT', '1') == '1'
+
+
 def _fc_wgrad(dy2, x2, w, w_ref):
     """dW = dY^T X; accumulated straight into the weight's .grad buffer when possible (GEMM with
     beta = 1 / the MFMA kernel's accumulating reduce) so no separate dW tensor and add kernel."""
     key = ('fc_wgrad', tuple(dy2.shape), tuple(x2.shape), dy2.dtype)
     algo = _KF._ALGO.get(key)
-    tgt = _leaf_grad(w_ref, dtype=w.dtype) if algo is not None else None
+    tgt = _leaf_grad(w_ref, dtype=w.dtype) if (algo is not None and _FC_DIRECT) else None
     if tgt is not None:
         N, K = w.shape
         if algo == 'hip':
@@ -355,7 +359,7 @@ def bias_grad(dy2, b_ref, bdt):
     part = _COLSUM_PART.get(dy2.device)
     if part is None or part.numel() < n:
         part = _COLSUM_PART[dy2.device] = torch.empty(n, dtype=torch.float32, device=dy2.device)
-    tgt = _leaf_grad(b_ref, N, dtype=bdt) if bdt in _DT else None
+    tgt = _leaf_grad(b_ref, N, dtype=bdt) if (bdt in _DT and _FC_DIRECT) else None
     out = tgt if tgt is not None else torch.empty(N, dtype=torch.float32, device=dy2.device)
     lib.colsum_rows(_DT[dy2.dtype], dy2.data_ptr(), _KF._zeros_f32(N, dy2.device).data_ptr(), part.data_ptr(), M, N,
                     _DT[out.dtype], out.data_ptr(), int(tgt is not None), _stream())
@@ -365,11 +369,12 @@ def bias_grad(dy2, b_ref, bdt):
 
 
 _IDX_T = {torch.float32: 0, torch.int64: 1, torch.int32: 2}
+_EMB_DIRECT = _os.environ.get('MXAMD_EMB_DIRECT', '1') == '1'
 _EMB_SCRATCH = {}
 
 
 def embedding_ok(idx, w):
-    return (w.is_cuda and w.dtype in _DT and w.dim() == 2 and w.shape[1] % 8 == 0 and _aligned(w)
+    return (_os.environ.get('MXAMD_EMB_HIP', '1') == '1' and w.is_cuda and w.dtype in _DT and w.dim() == 2 and w.shape[1] % 8 == 0 and _aligned(w)
             and idx.device == w.device and idx.numel() > 0 and w.shape[0] < 2 ** 31)
 
 
@@ -406,7 +411,7 @@ class Embedding(torch.autograd.Function):
         if sc is None:
             sc = _EMB_SCRATCH[key] = (torch.zeros(V * C, dtype=torch.float32, device=dev),
                                       torch.zeros(V, dtype=torch.uint8, device=dev))
-        tgt = _leaf_grad(ctx.w_ref, V * C, dtype=wdt) if ctx.needs_input_grad[1] else None
+        tgt = _leaf_grad(ctx.w_ref, V * C, dtype=wdt) if (ctx.needs_input_grad[1] and _EMB_DIRECT) else None
         out = tgt if tgt is not None else torch.empty((V, C), dtype=wdt, device=dev)
         _K.lib().embedding_backward(_DT[dy.dtype], _IDX_T[idx.dtype], idx.data_ptr(), dy.data_ptr(),
                                     sc[0].data_ptr(), sc[1].data_ptr(), _DT[out.dtype], out.data_ptr(),

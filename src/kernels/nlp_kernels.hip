@@ -17,6 +17,8 @@
 //   mask is reproducible from the seed and is stored as 1 bit per element.
 #include <stdexcept>
 
+#include <cstdlib>
+
 #include "common.h"
 
 namespace mxamd {
@@ -644,7 +646,11 @@ void embedding_forward(int dtype, int itype, const void* idx, const void* w, voi
 void embedding_backward(int dtype, int itype, const void* idx, const void* dy, float* acc, uint8_t* touched,
                         int out_dtype, void* grad, int accum, int64_t n, int V, int C, hipStream_t s) {
   MXAMD_HOST_CHECK(C % 8 == 0, "embedding: output_dim must be a multiple of 8");
-  if (static_cast<int64_t>(V) * C <= kEmbSmallFloats) {
+  static const bool small_ok = [] {
+    const char* e = getenv("MXAMD_EMB_SMALL");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (small_ok && static_cast<int64_t>(V) * C <= kEmbSmallFloats) {
     int64_t rpb = 64;
     while ((n + rpb - 1) / rpb > 512) rpb *= 2;
     const int blocks = static_cast<int>((n + rpb - 1) / rpb);

@@ -226,13 +226,24 @@ void flat_adam(int dtype, int mode, void* w, const void* g, float* mean, float* 
 #undef L
 }
 
+// zero a small fp32 buffer with a kernel (a plain kernel node when the launch is HIP-graph captured)
+__global__ void __launch_bounds__(256) zero_f32_kernel(float* __restrict__ p, int n) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) p[i] = 0.f;
+}
+
+static void zero_f32(float* p, int n, hipStream_t s) {
+  int blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  if (blocks > 0) hipLaunchKernelGGL(zero_f32_kernel, dim3(blocks), dim3(256), 0, s, p, n);
+}
+
 // chunks: device array of (start, len, seg) triples (int64, int32, int32 -> 16 bytes each)
 void lamb_update(int dtype, void* w, const void* g, float* mean, float* var, float* w32, float* upd,
                  const void* chunks, int nchunks, float* nrm, int nseg, float lr, float beta1, float beta2, float eps,
                  float bc1, float bc2, float wd, float rescale, float clip, float lb, float ub, const float* hp,
                  hipStream_t s) {
   const Chunk* ck = static_cast<const Chunk*>(chunks);
-  (void)hipMemsetAsync(nrm, 0, sizeof(float) * 2 * nseg, s);
+  zero_f32(nrm, 2 * nseg, s);
   MXAMD_OPT_DTYPE(dtype, {
     if (w32) {
       hipLaunchKernelGGL((lamb_phase1_kernel<T, true>), dim3(nchunks), dim3(256), 0, s, static_cast<const T*>(w),
@@ -251,7 +262,7 @@ void lamb_update(int dtype, void* w, const void* g, float* mean, float* var, flo
 }
 
 void seg_sumsq(int dtype, const void* x, const void* chunks, int nchunks, float* out, int nseg, hipStream_t s) {
-  (void)hipMemsetAsync(out, 0, sizeof(float) * nseg, s);
+  zero_f32(out, nseg, s);
   MXAMD_OPT_DTYPE(dtype, hipLaunchKernelGGL((seg_sumsq_kernel<T>), dim3(nchunks), dim3(256), 0, s,
                                             static_cast<const T*>(x), static_cast<const Chunk*>(chunks), out))
 }

@@ -60,10 +60,11 @@ def test_graph_step_matches_eager(optimizer, params):
 
 
 @pytest.mark.gpu
-def test_graph_step_multi_precision_bf16():
+@pytest.mark.parametrize('optimizer', ['adam', 'lamb', 'sgd'])
+def test_graph_step_multi_precision_bf16(optimizer):
     params = {'learning_rate': 1e-3, 'multi_precision': True}
-    le, we = _train('adam', params, graph=False, dtype='bfloat16')
-    lg, wg = _train('adam', params, graph=True, dtype='bfloat16')
+    le, we = _train(optimizer, params, graph=False, dtype='bfloat16')
+    lg, wg = _train(optimizer, params, graph=True, dtype='bfloat16')
     np.testing.assert_allclose(lg, le, rtol=2e-2, atol=1e-3)
     for a, b in zip(wg, we):
         np.testing.assert_allclose(a, b, rtol=2e-2, atol=2e-3)

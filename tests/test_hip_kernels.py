@@ -747,5 +747,6 @@ def test_embedding_gather_scatter_matches_torch(wdt, idt, vc):
         yr = torch.nn.functional.embedding(idx.clamp(0, V - 1), wr)
         yr.backward(dy.float())
         torch.testing.assert_close(y.float(), yr, rtol=0, atol=0)
-        tol = 1e-5 if wdt == torch.float32 else 3e-2
-        torch.testing.assert_close(w.grad.float(), wr.grad, rtol=tol, atol=tol)
+        # gradients of the 2-row table sum ~100 lookups: compare relative to their magnitude
+        tol = 1e-5 if wdt == torch.float32 else 1e-2
+        torch.testing.assert_close(w.grad.float(), wr.grad, rtol=tol, atol=tol * float(wr.grad.abs().max()))

@@ -44,12 +44,17 @@ def main():
     ap.add_argument('--vocab', type=int, default=30528, help='30522 padded to a multiple of 64')
     ap.add_argument('--gpus', type=int, default=1, help='worker processes (one per GPU)')
     ap.add_argument('--graph', action='store_true', help='capture the whole step in a HIP graph (GraphStep)')
+    ap.add_argument('--trace-loss', action='store_true', help='print every step\'s loss (debugging; syncs)')
     args = ap.parse_args()
     launch = _load_launcher()
     if launch.needs_launch(args.gpus):
         sys.exit(launch.relaunch_self(args.gpus))
 
     import torch
+    if os.environ.get('MXAMD_FILL_UNINIT'):
+        # debugging: torch.empty returns NaN-filled memory, exposing reads of unwritten buffers
+        torch.use_deterministic_algorithms(True, warn_only=True)
+        torch.utils.deterministic.fill_uninitialized_memory = True
     import mxnet_maintenance_amd as mx
     from mxnet_maintenance_amd import gluon, autograd, nd
     from mxnet_maintenance_amd.models import bert as bert_mod
@@ -97,12 +102,16 @@ def main():
 
     if args.graph:
         step = gluon.GraphStep(step, trainer, warmup=max(1, args.warmup - 1))
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        r = step()
+        if args.trace_loss:
+            print('warmup step %d loss %.5f' % (i, float(r.asscalar())), flush=True)
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         last = step()
+        if args.trace_loss:
+            print('step %d loss %.5f' % (i, float(last.asscalar())), flush=True)
     sync()
     dt = time.perf_counter() - t0
     if dist.world_size() > 1:
@@ -120,6 +129,10 @@ def main():
             'config': {'model': args.model, 'per_gpu_batch': B, 'seq_len': S, 'masked_positions': P,
                        'optimizer': args.optimizer, 'parallelism': 'dp%d' % n, 'hip_graph': args.graph,
                        'final_loss': round(float(last.asscalar()), 4)}}), flush=True)
+    if args.trace_loss:
+        from mxnet_maintenance_amd.ops import kernel_fns
+        for k, v in sorted(kernel_fns._ALGO.items(), key=str):
+            print('algo', v, k, file=sys.stderr)
     if dist.world_size() > 1:
         torch.distributed.destroy_process_group()
 

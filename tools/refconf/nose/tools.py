@@ -48,3 +48,21 @@ def with_setup(setup=None, teardown=None):
 def nottest(fn):
     fn.__test__ = False
     return fn
+
+
+def ok_(expr, msg=None):
+    """nose.tools.ok_: assert ``expr`` is truthy."""
+    if not expr:
+        raise AssertionError(msg)
+
+
+def eq_(a, b, msg=None):
+    """nose.tools.eq_: assert ``a == b``."""
+    if not a == b:
+        raise AssertionError(msg or '%r != %r' % (a, b))
+
+
+assert_is_instance = _tc.assertIsInstance
+assert_is_none = _tc.assertIsNone
+assert_greater = _tc.assertGreater
+assert_less = _tc.assertLess

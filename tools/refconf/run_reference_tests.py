@@ -26,9 +26,11 @@ def run_one(ref, name, timeout, workers, select=None, tb=None):
     try:
         unit = os.path.join(tmp, 'unittest')
         os.makedirs(unit)
-        for f in ('common.py', name + '.py', 'legacy_ndarray.v0', 'save_000800.json'):
-            src = os.path.join(ref, 'unittest', f)
-            if os.path.exists(src):
+        # the whole unittest directory: test files import each other (test_module -> test_bucketing)
+        src_dir = os.path.join(ref, 'unittest')
+        for f in os.listdir(src_dir):
+            src = os.path.join(src_dir, f)
+            if os.path.isfile(src) and (f.endswith('.py') or f in ('legacy_ndarray.v0', 'save_000800.json')):
                 shutil.copy(src, unit)
         if os.path.isdir(os.path.join(ref, 'common')):
             shutil.copytree(os.path.join(ref, 'common'), os.path.join(tmp, 'common'))
