@@ -66,4 +66,4 @@ from . import numpy as np
 from . import numpy_extension
 from . import numpy_extension as npx
 from . import rtc
-from .util import is_np_array, is_np_shape, set_np, reset_np, use_np, np_shape, np_array
+from .util import is_np_array, is_np_shape, set_np, reset_np, use_np, np_shape, np_array, set_np_shape, use_np_shape, use_np_array

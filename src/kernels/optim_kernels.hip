@@ -267,9 +267,13 @@ void seg_sumsq(int dtype, const void* x, const void* chunks, int nchunks, float*
                                             static_cast<const T*>(x), static_cast<const Chunk*>(chunks), out))
 }
 
+__global__ void set_flag_kernel(int* __restrict__ flag) {
+  if (threadIdx.x == 0) *flag = 1;
+}
+
 void all_finite(int dtype, const void* x, int64_t n, float scale, int* flag, int init, hipStream_t s) {
   MXAMD_HOST_CHECK(n % 8 == 0, "all_finite: length must be a multiple of 8");
-  if (init) (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flag), 1, 1, s);
+  if (init) hipLaunchKernelGGL(set_flag_kernel, dim3(1), dim3(64), 0, s, flag);   // no memset node (graphs)
   MXAMD_OPT_DTYPE(dtype, hipLaunchKernelGGL((all_finite_kernel<T>), dim3(flat_blocks(n / 8)), dim3(256), 0, s,
                                             static_cast<const T*>(x), n / 8, scale, flag))
 }

@@ -35,7 +35,7 @@ def run_one(ref, name, timeout, workers, select=None, tb=None):
         if os.path.isdir(os.path.join(ref, 'common')):
             shutil.copytree(os.path.join(ref, 'common'), os.path.join(tmp, 'common'))
         env = dict(os.environ)
-        env['PYTHONPATH'] = os.pathsep.join([HERE, unit, os.path.join(tmp, 'common')] +
+        env['PYTHONPATH'] = os.pathsep.join([HERE, unit, os.path.join(tmp, 'common'), os.path.join(ref, 'train')] +
                                             ([env['PYTHONPATH']] if env.get('PYTHONPATH') else []))
         env['PYTHONDONTWRITEBYTECODE'] = '1'
         env.setdefault('MXNET_TEST_SEED', '42')
