@@ -41,6 +41,8 @@ def main():
     ap.add_argument('--model', default='resnet50_v1b')
     ap.add_argument('--no-fuse', action='store_true')
     ap.add_argument('--image-size', type=int, default=224)
+    ap.add_argument('--graph', default='auto', choices=['auto', 'on', 'off'],
+                    help='capture the whole training step in one HIP graph (gluon.GraphStep); auto = on for 1 GPU')
     args = ap.parse_args()
 
     # `bench.py --gpus N` without a launcher: start N fresh worker processes (one per GPU) and exit
@@ -106,6 +108,11 @@ def main():
             torch.cuda.synchronize()
         dist.barrier()
 
+    use_graph = args.graph == 'on' or (args.graph == 'auto' and dist.world_size() == 1 and torch.cuda.is_available())
+    if use_graph:
+        # forward + backward + fused mp-SGD replayed as one graph; the first warm-up calls run eagerly
+        # (kernel autotuning, arena construction) and the last one captures
+        step = gluon.GraphStep(step, trainer, warmup=max(1, args.warmup - 1), fallback=args.graph == 'auto')
     for _ in range(args.warmup):
         step()
     sync()
@@ -132,7 +139,8 @@ def main():
             'data': 'synthetic (random-init weights, uniform images, random labels)',
             'config': {'model': args.model.replace('resnet50_v1b', 'ResNet-50 v1b'), 'global_batch': B * n,
                        'per_gpu_batch': B, 'seq_len': None, 'image_size': S, 'parallelism': 'dp%d' % n,
-                       'layout': 'NHWC', 'optimizer': 'mp-SGD momentum 0.9', 'final_loss': round(loss_val, 4)},
+                       'layout': 'NHWC', 'optimizer': 'mp-SGD momentum 0.9', 'final_loss': round(loss_val, 4),
+                       'hip_graph': bool(use_graph and getattr(step, 'captured', False))},
         }), flush=True)
     if os.environ.get('MXAMD_BENCH_VERBOSE', '0') == '1' and rank == 0:
         try:

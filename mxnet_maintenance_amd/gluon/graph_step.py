@@ -58,7 +58,7 @@ def _tensor_of(x):
 class GraphStep:
     """Capture ``fn(*inputs)`` into a HIP graph after ``warmup`` eager calls, then replay it."""
 
-    def __init__(self, fn, trainer=None, warmup=3):
+    def __init__(self, fn, trainer=None, warmup=3, fallback=False):
         if warmup < 1:
             raise ValueError('GraphStep needs at least one eager warm-up call')
         self._fn = fn
@@ -70,6 +70,8 @@ class GraphStep:
         self._static_out = None
         self._stream = None
         self._rng = None
+        self._fallback = fallback     # capture failure -> keep running eagerly (with a warning)
+        self._eager_only = False
 
     @property
     def captured(self):
@@ -143,10 +145,21 @@ class GraphStep:
 
     def __call__(self, *inputs):
         self._calls += 1
+        if self._eager_only:
+            return self._run_eager(inputs)
         if self._graph is None:
             if self._calls <= self._warmup:
                 return self._run_eager(inputs)
-            self._capture(inputs)
+            try:
+                self._capture(inputs)
+            except Exception as e:      # pylint: disable=broad-except
+                if not self._fallback:
+                    raise
+                import warnings
+                warnings.warn('GraphStep: capture failed (%s); running the step eagerly' % e)
+                self._eager_only = True
+                torch.cuda.synchronize()
+                return self._run_eager(inputs)
         else:
             self._load_inputs(inputs)
         if self._trainer is not None:
