@@ -15,7 +15,8 @@ MI355X design:
   summed locally first;
 * a list of keys is reduced as ONE flattened collective per dtype (bucket
   fusion), so per-key launch latency does not dominate on ResNet-sized models;
-* ``dist_async`` is emulated with synchronous all-reduce (no parameter server).
+* ``dist_async`` is an asynchronous parameter server over torch.distributed.rpc
+  (kvstore/dist_async.py): pushes are applied by the server as they arrive.
 """
 import os
 import pickle
@@ -341,6 +342,9 @@ def create(name='local'):
              'dist_sync_allreduce')
     if name not in valid:
         raise MXNetError('Unknown KVStore type %s' % name)
+    if name == 'dist_async':
+        from .dist_async import KVStoreDistAsync
+        return KVStoreDistAsync()
     return KVStore(name)
 
 
