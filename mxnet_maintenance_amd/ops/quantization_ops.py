@@ -96,6 +96,56 @@ def _exact_int(fn, *args):
     return torch.round(fn(*[a.double() for a in args])).to(torch.int32)
 
 
+def _hip_int8():
+    from . import kernels as K
+    return K.lib() if (K.available() and K.enabled()) else None
+
+
+def _int8_matmul(x, w):
+    """int32 ``x @ w.T`` for integer-valued x [M, K] (int8 or uint8) and w [N, K] (int8).
+
+    On a GPU: the gfx950 i8 MFMA GEMM (src/kernels/int8_gemm.hip) -- uint8 data is
+    re-centred to int8 (x - 128) and the 128 * sum_k w[n, k] term added back; K is
+    zero-padded to a multiple of 64.  Elsewhere: exact fp64 matmul.
+    """
+    lib = _hip_int8() if x.is_cuda else None
+    if lib is None or w.dtype != torch.int8 or x.dtype not in (torch.int8, torch.uint8):
+        return _exact_int(lambda a, b: a @ b.t(), x, w)
+    M, K = x.shape
+    N = w.shape[0]
+    shift = x.dtype == torch.uint8
+    xa = (x.to(torch.int16) - 128).to(torch.int8) if shift else x
+    pad = (-K) % 64
+    if pad:
+        xa = torch.nn.functional.pad(xa, (0, pad))
+        w = torch.nn.functional.pad(w, (0, pad))
+    xa = xa.contiguous()
+    w = w.contiguous()
+    out = torch.empty((M, N), dtype=torch.int32, device=x.device)
+    lib.int8_gemm(xa.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K + pad,
+                  torch.cuda.current_stream(x.device).cuda_stream)
+    if shift:
+        out += 128 * w.to(torch.int32).sum(1).reshape(1, -1)
+    return out
+
+
+def _im2col_nhwc(x, kernel, stride, pad, dilate):
+    """[N, H, W, C] -> ([N*Ho*Wo, kh*kw*C], (N, Ho, Wo)) with the (kh, kw, C) order of an NHWC weight."""
+    n, h, w_, c = x.shape
+    kh, kw = kernel
+    sh, sw = stride
+    ph, pw = pad
+    dh, dw = dilate
+    xp = torch.nn.functional.pad(x, (0, 0, pw, pw, ph, ph))
+    ho = (h + 2 * ph - dh * (kh - 1) - 1) // sh + 1
+    wo = (w_ + 2 * pw - dw * (kw - 1) - 1) // sw + 1
+    cols = []
+    for i in range(kh):
+        for j in range(kw):
+            cols.append(xp[:, i * dh:i * dh + sh * (ho - 1) + 1:sh, j * dw:j * dw + sw * (wo - 1) + 1:sw, :])
+    return torch.cat(cols, dim=-1).reshape(n * ho * wo, kh * kw * c), (n, ho, wo)
+
+
 def _qconv_args(a):
     names = ['data', 'weight']
     if not (str(a.get('no_bias', False)) in ('True', 'true', '1')):
@@ -128,8 +178,16 @@ def quantized_conv(data, weight, *rest, kernel=(), stride=(), dilate=(), pad=(),
     if channel_last:
         x = x.permute(0, nsp + 1, *range(1, nsp + 1))
         w = w.permute(0, nsp + 1, *range(1, nsp + 1))
-    conv = {1: F.conv1d, 2: F.conv2d, 3: F.conv3d}[nsp]
-    out = _exact_int(lambda a, b: conv(a, b, None, stride, pad, dilate, num_group), x, w)
+    if data.is_cuda and nsp == 2 and num_group == 1 and weight.dtype == torch.int8 and _hip_int8() is not None:
+        # implicit GEMM on the i8 matrix cores: NHWC im2col view x NHWC weight
+        xn = data if channel_last else data.permute(0, 2, 3, 1)
+        wn = weight if channel_last else weight.permute(0, 2, 3, 1)
+        cols, (n_, ho, wo) = _im2col_nhwc(xn, tuple(wn.shape[1:3]), stride, pad, dilate)
+        out = _int8_matmul(cols, wn.reshape(wn.shape[0], -1)).reshape(n_, ho, wo, -1)
+        out = out.permute(0, 3, 1, 2)        # NCHW view; the channel_last branch below permutes back
+    else:
+        conv = {1: F.conv1d, 2: F.conv2d, 3: F.conv3d}[nsp]
+        out = _exact_int(lambda a, b: conv(a, b, None, stride, pad, dilate, num_group), x, w)
     omin, omax = _int_range(_range_scalar(mn_d), _range_scalar(mx_d), _range_scalar(mn_w), _range_scalar(mx_w))
     if bias is not None:
         # int8 bias rescaled into the int32 output scale
@@ -138,6 +196,8 @@ def quantized_conv(data, weight, *rest, kernel=(), stride=(), dilate=(), pad=(),
         out = out + b.reshape((1, -1) + (1,) * nsp)
     if channel_last:
         out = out.permute(0, *range(2, nsp + 2), 1).contiguous()
+    else:
+        out = out.contiguous()
     return out, omin, omax
 
 
@@ -162,7 +222,8 @@ def quantized_fully_connected(data, weight, *rest, num_hidden=1, no_bias=False, 
         bias = rest[0]
         mn_d, mx_d, mn_w, mx_w, mn_b, mx_b = rest[1:7]
     x = data.reshape(data.shape[0], -1) if flatten else data
-    out = _exact_int(lambda a, b: a @ b.t(), x, weight)
+    lead = x.shape[:-1]
+    out = _int8_matmul(x.reshape(-1, x.shape[-1]), weight).reshape(*lead, weight.shape[0])
     omin, omax = _int_range(_range_scalar(mn_d), _range_scalar(mx_d), _range_scalar(mn_w), _range_scalar(mx_w))
     if bias is not None:
         rb = torch.maximum(_range_scalar(mn_b).abs(), _range_scalar(mx_b).abs()) / INT8_MAX

@@ -25,6 +25,7 @@ void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, c
                       const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R, int C,
                       int relu_mode, int fix_gamma, int training, int accum, hipStream_t s);
 int bn_partials_rows(int64_t R, int C);
+void int8_gemm(const int8_t* A, const int8_t* B, int32_t* C, int M, int N, int K, hipStream_t s);
 void csr_dot_dense(int dtype, const int64_t* indptr, const int64_t* indices, const void* vals, const void* rhs,
                    void* out, int64_t M, int64_t K, int N, hipStream_t s);
 void csrT_dot_dense(int dtype, const int64_t* indptr, const int64_t* indices, const void* vals, const void* rhs,
@@ -140,6 +141,10 @@ PYBIND11_MODULE(_hip_kernels, m) {
     csrT_dot_dense(dt, P<const int64_t>(indptr), P<const int64_t>(indices), P<const void>(vals), P<const void>(rhs),
                    P<const int64_t>(slot), P<float>(out32), M, K, N, S(s));
     check_launch("csrT_dot_dense");
+  });
+  m.def("int8_gemm", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K, uintptr_t s) {
+    int8_gemm(P<const int8_t>(a), P<const int8_t>(b), P<int32_t>(c), M, N, K, S(s));
+    check_launch("int8_gemm");
   });
   m.def("colsum_rows", [](int dt, uintptr_t x, uintptr_t zeros, uintptr_t part, int64_t R, int C, int odt,
                           uintptr_t out, int accum, uintptr_t s) {

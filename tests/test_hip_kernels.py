@@ -750,3 +750,37 @@ def test_embedding_gather_scatter_matches_torch(wdt, idt, vc):
         # gradients of the 2-row table sum ~100 lookups: compare relative to their magnitude
         tol = 1e-5 if wdt == torch.float32 else 1e-2
         torch.testing.assert_close(w.grad.float(), wr.grad, rtol=tol, atol=tol * float(wr.grad.abs().max()))
+
+
+@pytest.mark.parametrize('mnk', [(64, 64, 64), (100, 37, 200), (257, 130, 1024), (3, 1000, 64)])
+@pytest.mark.parametrize('udata', [False, True])
+def test_int8_gemm_mfma_exact(mnk, udata):
+    _lib()
+    from mxnet_maintenance_amd.ops import quantization_ops as Q
+    M, N, K = mnk
+    g = torch.Generator().manual_seed(M + N + K)
+    if udata:
+        x = torch.randint(0, 256, (M, K), generator=g, dtype=torch.int32).to(torch.uint8)
+    else:
+        x = torch.randint(-128, 128, (M, K), generator=g, dtype=torch.int32).to(torch.int8)
+    w = torch.randint(-127, 128, (N, K), generator=g, dtype=torch.int32).to(torch.int8)
+    ref = x.to(torch.int64) @ w.to(torch.int64).t()
+    out = Q._int8_matmul(x.cuda(), w.cuda())
+    assert out.dtype == torch.int32
+    assert torch.equal(out.cpu().to(torch.int64), ref)
+
+
+@pytest.mark.parametrize('cfg', [((2, 9, 9, 16), (8, 3, 3, 16), (1, 1), (1, 1)),
+                                 ((1, 12, 12, 32), (24, 1, 1, 32), (2, 2), (0, 0))])
+def test_quantized_conv_nhwc_on_int8_mfma(cfg):
+    _lib()
+    from mxnet_maintenance_amd.ops import quantization_ops as Q
+    xs, ws, stride, pad = cfg
+    g = torch.Generator().manual_seed(5)
+    x = torch.randint(-100, 100, xs, generator=g, dtype=torch.int32).to(torch.int8)
+    w = torch.randint(-100, 100, ws, generator=g, dtype=torch.int32).to(torch.int8)
+    rng = [torch.tensor([-1.0]), torch.tensor([1.0]), torch.tensor([-0.5]), torch.tensor([0.5])]
+    kw = dict(kernel=ws[1:3], stride=stride, pad=pad, num_filter=ws[0], no_bias=True, layout='NHWC')
+    ref, _, _ = Q.quantized_conv(x, w, *rng, **kw)                                     # CPU exact path
+    out, _, _ = Q.quantized_conv(x.cuda(), w.cuda(), *[r.cuda() for r in rng], **kw)  # i8 MFMA
+    assert torch.equal(out.cpu(), ref)
