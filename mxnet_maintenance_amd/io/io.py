@@ -554,11 +554,17 @@ class ImageRecordIter(DataIter):
         self.provide_data = [DataDesc(data_name, shape, np.float32, layout)]
         lshape = (batch_size,) if label_width == 1 else (batch_size, label_width)
         self.provide_label = [DataDesc(label_name, lshape, np.float32)]
-        from concurrent.futures import ThreadPoolExecutor
-        self._pool = ThreadPoolExecutor(self.threads)
+        # decode + augmentation run as dependency-engine tasks (src/native/engine.cc worker threads; PIL
+        # releases the GIL while decoding): one engine variable per batch slot, and the next batch is
+        # pushed as soon as the current one is handed out, so decoding overlaps the training step
+        from .. import engine
+        self._engine = engine
+        self._slot_vars = [engine.new_var('imrec_slot%d' % i) for i in range(batch_size)]
+        self._inflight = None
         self.reset()
 
     def reset(self):
+        self._drain()
         order = list(self.offsets)
         if self.shuffle:
             self.rng.shuffle(order)
@@ -612,21 +618,48 @@ class ImageRecordIter(DataIter):
         label = header.label
         return np.ascontiguousarray(a), label
 
-    def next(self):
+    def _launch(self):
+        """Read the next batch's records and push their decode tasks; None at the end of the epoch."""
         n = len(self._order)
         if self._cursor >= n:
-            raise StopIteration
+            return None
         bs = self.batch_size
         take = min(bs, n - self._cursor)
         if take < bs and not self.round_batch:
-            raise StopIteration
+            return None
         recs = [self._read_one(self._order[self._cursor + i]) for i in range(take)]
         pad = bs - take
         if pad:
             recs += [recs[i % take] for i in range(pad)]
         self._cursor += bs
         seeds = self.rng.randint(0, 2 ** 31 - 1, size=len(recs))
-        out = list(self._pool.map(self._decode, recs, seeds))
+        out = [None] * len(recs)
+
+        def task(i, rec, seed):
+            out[i] = self._decode(rec, seed)
+        for i, (rec, seed) in enumerate(zip(recs, seeds)):
+            self._engine.push(lambda i=i, rec=rec, seed=int(seed): task(i, rec, seed),
+                              mutable_vars=[self._slot_vars[i]], name='imrec_decode')
+        return out, pad
+
+    def _drain(self):
+        if getattr(self, '_inflight', None) is not None:
+            for v in self._slot_vars:
+                try:
+                    self._engine.wait_for_var(v)
+                except Exception:     # pylint: disable=broad-except
+                    pass
+        self._inflight = None
+
+    def next(self):
+        job = self._inflight if self._inflight is not None else self._launch()
+        self._inflight = None
+        if job is None:
+            raise StopIteration
+        out, pad = job
+        for v in self._slot_vars[:len(out)]:
+            self._engine.wait_for_var(v)      # re-raises a decode task's exception here
+        self._inflight = self._launch()       # prefetch: decode the next batch while this one trains
         data = np.stack([o[0] for o in out])
         labels = np.array([np.asarray(o[1], dtype=np.float32).reshape(-1)[:self.label_width] for o in out],
                           dtype=np.float32)
