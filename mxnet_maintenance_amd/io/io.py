@@ -283,14 +283,31 @@ def _init_data(data, allow_empty, default_name):
         list(data.items())
 
 
+def _scipy_csr_to_nd(data):
+    """scipy.sparse CSR inputs (alone, in a list or dict) become CSRNDArrays."""
+    def conv(v):
+        if hasattr(v, 'tocsr') and not isinstance(v, nd.NDArray):
+            return nd.sparse.csr_matrix(v)
+        return v
+    if isinstance(data, dict):
+        return {k: conv(v) for k, v in data.items()}
+    if isinstance(data, (list, tuple)):
+        return [conv(v) for v in data]
+    return conv(data)
+
+
 class NDArrayIter(DataIter):
     """Iterate over in-memory NDArrays/numpy arrays (shuffle, pad/discard/roll_over last batch)."""
 
     def __init__(self, data, label=None, batch_size=1, shuffle=False, last_batch_handle='pad', data_name='data',
                  label_name='softmax_label'):
         super().__init__(batch_size)
+        data = _scipy_csr_to_nd(data)
         self.data = _init_data(data, allow_empty=False, default_name=data_name)
         self.label = _init_data(label, allow_empty=True, default_name=label_name)
+        if last_batch_handle != 'discard' and any(getattr(v, 'stype', 'default') == 'csr' for _, v in self.data):
+            raise NotImplementedError("`NDArrayIter` only supports ``CSRNDArray`` with `last_batch_handle` set to "
+                                      "`discard`.")
         self.idx = np.arange(self.data[0][1].shape[0])
         self.shuffle = shuffle
         self.last_batch_handle = last_batch_handle
@@ -333,8 +350,8 @@ class NDArrayIter(DataIter):
     def next(self):
         if not self.iter_next():
             raise StopIteration
-        data = self.getdata()
-        label = self.getlabel()
+        data = self._batchify(self.data)
+        label = self._batchify(self.label)
         if data[0].shape[0] != self.batch_size:
             self._cache_data = data
             self._cache_label = label
@@ -368,10 +385,11 @@ class NDArrayIter(DataIter):
                 self._cache_label = None
             return self._concat(cache_data, second_data)
         if self.last_batch_handle == 'pad' and self.cursor + self.batch_size > self.num_data:
-            pad = self.batch_size - self.num_data + self.cursor
-            first_data = self._getdata(data_source, start=self.cursor)
-            second_data = self._getdata(data_source, end=pad)
-            return self._concat(first_data, second_data)
+            # wrap around (several times when the batch is larger than the data set)
+            pos = np.arange(self.cursor, self.cursor + self.batch_size) % self.num_data
+            if self.shuffle:
+                pos = self.idx[pos]
+            return [x[1][pos] for x in data_source]
         end_idx = self.cursor + self.batch_size if self.cursor + self.batch_size < self.num_data else self.num_data
         return self._getdata(data_source, self.cursor, end_idx)
 
@@ -418,7 +436,8 @@ class CSVIter(NDArrayIter):
 
     def __init__(self, data_csv, data_shape, label_csv=None, label_shape=(1,), batch_size=1, round_batch=True,
                  dtype='float32', **kwargs):
-        data = np.loadtxt(data_csv, delimiter=',', dtype=np.float32, ndmin=2).reshape((-1,) + tuple(data_shape))
+        ldt = np.dtype(dtype) if np.dtype(dtype).kind in 'iu' else np.float32
+        data = np.loadtxt(data_csv, delimiter=',', dtype=ldt, ndmin=2).reshape((-1,) + tuple(data_shape))
         if label_csv is not None:
             label = np.loadtxt(label_csv, delimiter=',', dtype=np.float32, ndmin=2).reshape(
                 (-1,) + tuple(label_shape))
@@ -428,6 +447,13 @@ class CSVIter(NDArrayIter):
             label = label.reshape(-1)
         super().__init__(nd.array(data, dtype=dtype), nd.array(label), batch_size=batch_size, shuffle=False,
                          last_batch_handle='pad' if round_batch else 'discard')
+
+    # like the reference's native CSVIter: getdata()/getlabel() give the current batch's arrays
+    def getdata(self):
+        return self._batchify(self.data)[0]
+
+    def getlabel(self):
+        return self._batchify(self.label)[0]
 
 
 def _read_idx(path):
@@ -457,31 +483,55 @@ class MNISTIter(NDArrayIter):
         super().__init__(img, lab, batch_size=batch_size, shuffle=False, last_batch_handle='discard')
 
 
+def _read_libsvm(path, ncol):
+    """(dense rows [n, ncol], leading labels) of a LibSVM text file; malformed ids raise MXNetError."""
+    from ..base import MXNetError
+    rows, labels = [], []
+    with open(path) as f:
+        for ln, line in enumerate(f, 1):
+            parts = line.strip().split()
+            if not parts:
+                continue
+            labels.append(float(parts[0]))
+            row = np.zeros(ncol, dtype=np.float32)
+            for p in parts[1:]:
+                k, v = p.split(':')
+                k = int(k)
+                if k < 0 or k >= ncol:
+                    raise MXNetError('%s:%d: feature index %d out of range [0, %d)' % (path, ln, k, ncol))
+                row[k] = float(v)
+            rows.append(row)
+    return np.stack(rows) if rows else np.zeros((0, ncol), np.float32), labels
+
+
 class LibSVMIter(DataIter):
     """LibSVM text format -> CSR data batches (src/io/iter_libsvm.cc)."""
 
     def __init__(self, data_libsvm, data_shape, label_libsvm=None, label_shape=(1,), batch_size=1,
                  round_batch=True, **kwargs):
         super().__init__(batch_size)
-        rows, labels = [], []
         ncol = int(np.prod(data_shape))
-        with open(data_libsvm) as f:
-            for line in f:
-                parts = line.strip().split()
-                if not parts:
-                    continue
-                labels.append(float(parts[0]))
-                row = np.zeros(ncol, dtype=np.float32)
-                for p in parts[1:]:
-                    k, v = p.split(':')
-                    row[int(k)] = float(v)
-                rows.append(row)
-        self._data = np.stack(rows)
-        self._label = np.array(labels, dtype=np.float32)
+        self._data, labels = _read_libsvm(data_libsvm, ncol)
+        if label_libsvm is not None:
+            lcol = int(np.prod(label_shape))
+            self._label, _ = _read_libsvm(label_libsvm, lcol)
+            if tuple(label_shape) == (1,):
+                self._label = self._label.reshape(-1)
+        else:
+            self._label = np.array(labels, dtype=np.float32)
         self._cursor = 0
+        self._batch = None
         self.provide_data = [DataDesc('data', (batch_size, ncol))]
-        self.provide_label = [DataDesc('softmax_label', (batch_size,))]
+        self.provide_label = [DataDesc('softmax_label', (batch_size,) + tuple(self._label.shape[1:]))]
         self._round = round_batch
+
+    def getdata(self):
+        return self._batch.data[0] if self._batch is not None else None
+
+    get_data = getdata
+
+    def getlabel(self):
+        return self._batch.label[0] if self._batch is not None else None
 
     def reset(self):
         self._cursor = 0
@@ -497,7 +547,8 @@ class LibSVMIter(DataIter):
         idx = idx % n
         self._cursor += self.batch_size
         data = nd.sparse.csr_matrix(self._data[idx])
-        return DataBatch([data], [nd.array(self._label[idx])], pad=pad)
+        self._batch = DataBatch([data], [nd.array(self._label[idx])], pad=pad)
+        return self._batch
 
 
 # ---------------------------------------------------------------------------
