@@ -160,6 +160,13 @@ def _discard_pending(results):
             _release(payload)
 
 
+def _export_package_path():
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+    parts = [p for p in os.environ.get('PYTHONPATH', '').split(os.pathsep) if p]
+    if root not in parts:
+        os.environ['PYTHONPATH'] = os.pathsep.join([root] + parts)
+
+
 class _ProcessPool:
     """Fixed set of dataset-holding worker processes fed round-robin."""
 
@@ -170,7 +177,10 @@ class _ProcessPool:
         method = os.environ.get('MXAMD_DATALOADER_START_METHOD', 'forkserver')
         ctx = multiprocessing.get_context(method)
         if method == 'forkserver':
-            # the server imports the framework (torch included) once; every worker forks with it loaded
+            # the server imports the framework (torch included) once; every worker forks with it loaded.
+            # It is a fresh interpreter: make the package importable there even when this process found
+            # it through a runtime sys.path insertion (scripts run from a checkout)
+            _export_package_path()
             ctx.set_forkserver_preload(['numpy', 'mxnet_maintenance_amd'])
         self._results = ctx.Queue()
         self._tasks = []
@@ -217,6 +227,7 @@ class _ProcessIter:
     _tags = iter(range(1 << 62))
 
     def __init__(self, pool, batch_sampler, pin_memory, prefetch, timeout):
+        self._loader = None
         self._pool = pool
         self._tag = next(_ProcessIter._tags)
         self._sampler_iter = iter(batch_sampler)
@@ -373,10 +384,14 @@ class DataLoader:
             if self._worker_pool is None:
                 self.refresh()
         if self._thread_pool:
-            return _ThreadIter(self._worker_pool, self._dataset, self._batchify_fn, self._batch_sampler,
-                               self._pin_memory, self._prefetch, self._timeout)
-        return _ProcessIter(self._worker_pool, self._batch_sampler, self._pin_memory, self._prefetch,
-                            self._timeout)
+            it = _ThreadIter(self._worker_pool, self._dataset, self._batchify_fn, self._batch_sampler,
+                             self._pin_memory, self._prefetch, self._timeout)
+            it._loader = self
+            return it
+        it = _ProcessIter(self._worker_pool, self._batch_sampler, self._pin_memory, self._prefetch,
+                          self._timeout)
+        it._loader = self          # the loader (and its worker pool) lives as long as the iterator
+        return it
 
     def __len__(self):
         return len(self._batch_sampler)

@@ -96,7 +96,11 @@ class NDArray:
 
     @property
     def context(self):
-        return context_from_torch(self._data.device)
+        t = self._data
+        if t.device.type == 'cpu' and t.is_pinned():
+            from ..context import cpu_pinned
+            return cpu_pinned(0)
+        return context_from_torch(t.device)
 
     ctx = context
 
