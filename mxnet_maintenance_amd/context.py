@@ -119,3 +119,7 @@ def context_from_torch(dev):
     if dev.type == 'cuda':
         return Context('gpu', dev.index if dev.index is not None else torch.cuda.current_device())
     return Context('cpu', 0)
+
+
+# reference: the class attribute holding the process default context
+Context.default_ctx = Context('cpu', 0)

@@ -749,6 +749,9 @@ def _into(out, result):
 def empty(shape, ctx=None, dtype=None, stype=None):
     if isinstance(shape, int):
         shape = (shape,)
+    if stype not in (None, 'default'):
+        from . import sparse
+        return sparse.empty(stype, shape, ctx=ctx, dtype=dtype)
     return NDArray(torch.empty(shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device))
 
 

@@ -268,6 +268,57 @@ class BaseSparseNDArray(NDArray):
     def __neg__(self):
         return multiply(self, -1.0)
 
+    # comparisons / arithmetic with a scalar: the result stays sparse when the op maps 0 to 0
+    # (reference: FInferStorageType of the *_scalar operators), dense otherwise
+    def _scalar_op(self, scalar, fn):
+        from .. import _state
+        if not isinstance(scalar, (int, float, np.number)) or _state.STATE.recording:
+            return None
+        self._sync()
+        dt = self._vals.dtype
+        zero = fn(torch.zeros((), dtype=dt), scalar)
+        if float(zero) == 0.0:
+            return type(self)._make(fn(self._vals, scalar).to(dt), [a.clone() for a in self._aux], self._shp)
+        return NDArray(fn(self._densify(), scalar).to(dt))
+
+    def _cmp(self, other, fn, name):
+        r = self._scalar_op(other, fn)
+        if r is not None:
+            return r
+        return getattr(NDArray, name)(NDArray(self._data), NDArray(other._data) if isinstance(other, NDArray)
+                                      else other)
+
+    @property
+    def _num_aux(self):
+        return len(self._aux) if self._aux else (2 if self._STYPE == 'csr' else 1)
+
+    def __reduce__(self):
+        self._sync()
+        return (_rebuild_sparse, (self._STYPE, _np_of(self._vals), [_np_of(a) for a in self._aux], self._shp))
+
+    def __getstate__(self):
+        return None
+
+    def __eq__(self, other):
+        return self._cmp(other, torch.eq, '__eq__')
+
+    def __ne__(self, other):
+        return self._cmp(other, torch.ne, '__ne__')
+
+    def __gt__(self, other):
+        return self._cmp(other, torch.gt, '__gt__')
+
+    def __ge__(self, other):
+        return self._cmp(other, torch.ge, '__ge__')
+
+    def __lt__(self, other):
+        return self._cmp(other, torch.lt, '__lt__')
+
+    def __le__(self, other):
+        return self._cmp(other, torch.le, '__le__')
+
+    __hash__ = NDArray.__hash__
+
     def __iadd__(self, other):
         return self._assign(add(self, other))
 
@@ -312,6 +363,13 @@ class CSRNDArray(BaseSparseNDArray):
                 raise MXNetError('csr: indptr must start at 0, be non-decreasing and end at nnz')
             if idx.numel() and (bool((idx < 0).any()) or bool((idx >= self._shp[1]).any())):
                 raise MXNetError('csr: column index out of range')
+            if idx.numel() > 1:
+                # column indices strictly increasing inside every row
+                counts = ptr[1:] - ptr[:-1]
+                rows = torch.repeat_interleave(torch.arange(self._shp[0], device=idx.device), counts)
+                same_row = rows[1:] == rows[:-1]
+                if bool(((idx[1:] <= idx[:-1]) & same_row).any()):
+                    raise MXNetError('csr: column indices must be sorted and unique within each row')
 
     @property
     def indices(self):
@@ -382,6 +440,16 @@ class RowSparseNDArray(BaseSparseNDArray):
         return NDArray.__getitem__(NDArray(self._densify()), key)
 
 
+def _np_of(t):
+    t = t.detach().cpu()
+    return (t.float() if t.dtype == torch.bfloat16 else t).numpy()
+
+
+def _rebuild_sparse(stype, vals, aux, shape):
+    cls = CSRNDArray if stype == 'csr' else RowSparseNDArray
+    return cls._make(torch.from_numpy(np.array(vals)), [torch.from_numpy(np.array(a)) for a in aux], shape)
+
+
 # ------------------------------------------------------------------ constructors
 def _dev(ctx):
     return (ctx or current_context()).torch_device
@@ -407,6 +475,8 @@ def csr_matrix(arg1, shape=None, ctx=None, dtype=None):
         r._check(False)
         return r
     if isinstance(arg1, tuple) and len(arg1) == 2 and all(isinstance(s, (int, np.integer)) for s in arg1):
+        if shape is not None and tuple(shape) != tuple(arg1):
+            raise ValueError('csr_matrix: shape %s does not match %s' % (shape, arg1))
         return zeros('csr', arg1, ctx=ctx, dtype=dtype)
     if isinstance(arg1, tuple) and len(arg1) == 2:
         # scipy-style (data, (row, col)) COO definition
@@ -416,8 +486,11 @@ def csr_matrix(arg1, shape=None, ctx=None, dtype=None):
         dense = torch.zeros(shape, dtype=d.dtype, device=dev)
         dense.index_put_((_t(row, _I64, dev), _t(col, _I64, dev)), d, accumulate=True)
         return cast_storage(NDArray(dense), 'csr')
+    if shape is not None and hasattr(arg1, 'shape') and tuple(arg1.shape) != tuple(shape):
+        raise ValueError('csr_matrix: shape %s does not match the source array %s' % (shape, tuple(arg1.shape)))
     if isinstance(arg1, CSRNDArray):
-        return arg1.copy().as_in_context(ctx) if ctx is not None else arg1.copy()
+        r = arg1.astype(dtype) if dtype is not None else arg1.copy()
+        return r.as_in_context(ctx) if ctx is not None else r
     if hasattr(arg1, 'tocsr') and not isinstance(arg1, NDArray):
         m = arg1.tocsr()
         m.sort_indices()
@@ -445,15 +518,23 @@ def row_sparse_array(arg1, shape=None, ctx=None, dtype=None):
             data = data.index_select(0, order)
         return RowSparseNDArray._make(data.clone(), [indices.clone()], shape)
     if isinstance(arg1, tuple):
+        if shape is not None and tuple(shape) != tuple(arg1):
+            raise ValueError('row_sparse_array: shape %s does not match %s' % (shape, arg1))
         return zeros('row_sparse', arg1, ctx=ctx, dtype=dtype)
+    if shape is not None and hasattr(arg1, 'shape') and tuple(arg1.shape) != tuple(shape):
+        raise ValueError('row_sparse_array: shape %s does not match the source array %s'
+                         % (shape, tuple(arg1.shape)))
     if isinstance(arg1, RowSparseNDArray):
-        return arg1.copy().as_in_context(ctx) if ctx is not None else arg1.copy()
+        r = arg1.astype(dtype) if dtype is not None else arg1.copy()
+        return r.as_in_context(ctx) if ctx is not None else r
     d = _t(arg1, device=dev)
     d = d.to(_default_dtype(d, dtype))
     return cast_storage(NDArray(d), 'row_sparse')
 
 
 def zeros(stype, shape, ctx=None, dtype=None, **kwargs):
+    if stype not in ('csr', 'row_sparse', 'default'):
+        raise ValueError('unknown storage type %s' % stype)
     dev = _dev(ctx)
     dt = torch_dtype(dtype) if dtype is not None else torch.float32
     shape = (shape,) if isinstance(shape, int) else tuple(shape)
@@ -505,10 +586,12 @@ def cast_storage(data, stype):
     raise MXNetError('unknown storage type %s' % stype)
 
 
-def retain(data, indices):
+def retain(data, indices=None, **kwargs):
     """Keep only the rows of a row_sparse array whose ids are in ``indices`` (compressed in, compressed out)."""
-    if not isinstance(data, RowSparseNDArray):
-        raise MXNetError('retain expects a row_sparse array')
+    if kwargs:
+        raise MXNetError('retain: unknown argument(s) %s' % sorted(kwargs))
+    if not isinstance(data, RowSparseNDArray) or indices is None:
+        raise MXNetError('retain expects a row_sparse array and the row indices to keep')
     data._sync()
     idx, = data._aux
     want = _t(indices, _I64, idx.device).reshape(-1)

@@ -154,24 +154,63 @@ def rand_coord_2d(x_low, x_high, y_low, y_high):
     return _pyrandom.randint(x_low, x_high), _pyrandom.randint(y_low, y_high)
 
 
+def _powerlaw_csr_parts(num_rows, num_cols, density, dtype):
+    """Row r stores min(2**r, num_cols) leading columns until int(density * size) values are placed
+    (the "powerlaw" layout of the reference generator: every row twice as dense as the previous one)."""
+    total = int(num_rows * num_cols * density)
+    counts = []
+    left, k = total, 1
+    for _ in range(num_rows):
+        c = min(k, num_cols, left)
+        counts.append(c)
+        left -= c
+        k *= 2
+    indptr = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    indices = np.concatenate([np.arange(c, dtype=np.int64) for c in counts]) if total else np.zeros(0, np.int64)
+    data = np.random.uniform(-1, 1, size=int(indptr[-1])).astype(dtype)
+    return data, indices, indptr
+
+
 def rand_sparse_ndarray(shape, stype, density=None, dtype=None, distribution=None, data_init=None,
                         rsp_indices=None, modifier_func=None, shuffle_csr_indices=False, ctx=None):
+    """Random sparse array built directly in compressed form.
+
+    Returns ``(array, (values, indices))`` for row_sparse and ``(array, (indptr, indices, data))`` for
+    csr, like the reference helper.  ``distribution``: 'uniform' (default) or 'powerlaw' (csr only).
+    """
     density = np.random.rand() if density is None else density
     dtype = default_dtype() if dtype is None else dtype
-    dense = np.random.uniform(-1, 1, size=shape).astype(dtype)
-    mask = np.random.rand(*shape) < density
     if stype == 'row_sparse':
         if rsp_indices is not None:
-            rows = np.zeros(shape[0], dtype=bool)
-            rows[np.asarray(rsp_indices, dtype=np.int64)] = True
+            idx = np.unique(np.asarray(rsp_indices, dtype=np.int64))
         else:
-            rows = np.random.rand(shape[0]) < density
-        mask = np.broadcast_to(rows.reshape((-1,) + (1,) * (len(shape) - 1)), shape)
-    arr = np.where(mask, dense if data_init is None else np.full(shape, data_init, dtype), 0).astype(dtype)
-    if modifier_func is not None:
-        arr = np.vectorize(modifier_func)(arr).astype(dtype)
-    res = nd.array(arr, ctx=ctx, dtype=dtype).tostype(stype)
-    return res, (arr,)
+            idx = np.argwhere(np.random.rand(shape[0]) < density).flatten().astype(np.int64)
+        vshape = (len(idx),) + tuple(shape[1:])
+        val = np.full(vshape, data_init, dtype=dtype) if data_init is not None else \
+            np.random.rand(*vshape).astype(dtype)
+        if modifier_func is not None and val.size:
+            val = np.vectorize(modifier_func)(val).astype(dtype)
+        arr = nd.sparse.row_sparse_array((val, idx), shape=shape, ctx=ctx, dtype=dtype)
+        return arr, (val, idx)
+    if stype == 'csr':
+        assert len(shape) == 2, 'csr arrays are 2-D'
+        if distribution == 'powerlaw':
+            data, indices, indptr = _powerlaw_csr_parts(shape[0], shape[1], density, dtype)
+        else:
+            mask = np.random.rand(*shape) < density
+            counts = mask.sum(1)
+            indptr = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+            indices = np.nonzero(mask)[1].astype(np.int64)
+            if shuffle_csr_indices:
+                for r in range(shape[0]):
+                    np.random.shuffle(indices[indptr[r]:indptr[r + 1]])
+            data = np.full(len(indices), data_init, dtype=dtype) if data_init is not None else \
+                np.random.rand(len(indices)).astype(dtype)
+        if modifier_func is not None and data.size:
+            data = np.vectorize(modifier_func)(data).astype(dtype)
+        arr = nd.sparse.csr_matrix((data, indices, indptr), shape=shape, ctx=ctx, dtype=dtype)
+        return arr, (indptr, indices, data)
+    raise ValueError('unknown storage type %s' % stype)
 
 
 def rand_ndarray(shape, stype='default', density=None, dtype=None, modifier_func=None,
@@ -182,7 +221,7 @@ def rand_ndarray(shape, stype='default', density=None, dtype=None, modifier_func
         return nd.array(arr if modifier_func is None else np.vectorize(modifier_func)(arr), ctx=ctx,
                         dtype=dtype or default_dtype())
     return rand_sparse_ndarray(shape, stype, density=density, dtype=dtype, modifier_func=modifier_func,
-                               ctx=ctx)[0]
+                               shuffle_csr_indices=shuffle_csr_indices, distribution=distribution, ctx=ctx)[0]
 
 
 def create_sparse_array(shape, stype, data_init=None, rsp_indices=None, dtype=None, modifier_func=None,
