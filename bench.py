@@ -41,6 +41,8 @@ def main():
     ap.add_argument('--model', default='resnet50_v1b')
     ap.add_argument('--no-fuse', action='store_true')
     ap.add_argument('--image-size', type=int, default=224)
+    ap.add_argument('--layout', default='NHWC', choices=['NHWC', 'NCHW'],
+                    help='model layout (NCHW = default Gluon layout, executed channels-last on the HIP kernels)')
     ap.add_argument('--graph', default='auto', choices=['auto', 'on', 'off'],
                     help='capture the whole training step in one HIP graph (gluon.GraphStep); auto = on for 1 GPU')
     args = ap.parse_args()
@@ -72,7 +74,7 @@ def main():
 
     B = args.batch
     S = args.image_size
-    net = gluon.model_zoo.vision.get_model(args.model, layout='NHWC', fuse=not args.no_fuse, classes=1000)
+    net = gluon.model_zoo.vision.get_model(args.model, layout=args.layout, fuse=not args.no_fuse, classes=1000)
     net.initialize(mx.init.Xavier(rnd_type='gaussian', factor_type='in', magnitude=2), ctx=ctx)
     if args.dtype != 'float32':
         net.cast(args.dtype)
@@ -86,7 +88,8 @@ def main():
                             kvstore='device')
     loss_fn = gluon.loss.SoftmaxCrossEntropyLoss()
 
-    x = nd.random.uniform(-1, 1, shape=(B, S, S, 3), ctx=ctx).astype(args.dtype)
+    shape = (B, S, S, 3) if args.layout == 'NHWC' else (B, 3, S, S)
+    x = nd.random.uniform(-1, 1, shape=shape, ctx=ctx).astype(args.dtype)
     y = nd.array(torch.randint(0, 1000, (B,)).numpy(), ctx=ctx)
 
     n_ranks = dist.world_size()
@@ -139,7 +142,7 @@ def main():
             'data': 'synthetic (random-init weights, uniform images, random labels)',
             'config': {'model': args.model.replace('resnet50_v1b', 'ResNet-50 v1b'), 'global_batch': B * n,
                        'per_gpu_batch': B, 'seq_len': None, 'image_size': S, 'parallelism': 'dp%d' % n,
-                       'layout': 'NHWC', 'optimizer': 'mp-SGD momentum 0.9', 'final_loss': round(loss_val, 4),
+                       'layout': args.layout, 'optimizer': 'mp-SGD momentum 0.9', 'final_loss': round(loss_val, 4),
                        'hip_graph': bool(use_graph and getattr(step, 'captured', False))},
         }), flush=True)
     if os.environ.get('MXAMD_BENCH_VERBOSE', '0') == '1' and rank == 0:

@@ -69,8 +69,31 @@ def embedding(data, weight):
     return None
 
 
+def _as_nhwc_view(t):
+    """NHWC view of a 4-D NCHW-shaped tensor: free when its memory is channels-last (the output of a
+    HIP conv/BN/pool below), one transpose copy otherwise (the network input)."""
+    v = t.permute(0, 2, 3, 1)
+    return v if v.is_contiguous() else v.contiguous()
+
+
+def _nchw_on_hip(data):
+    """The NCHW (default Gluon layout) fast path: HIP NHWC kernels over channels-last memory."""
+    return (data.dim() == 4 and data.dtype in (torch.float16, torch.bfloat16) and _use_hip(data)
+            and _NCHW_VIA_NHWC)
+
+
+_NCHW_VIA_NHWC = os.environ.get('MXAMD_NCHW_VIA_NHWC', '1') == '1'
+
+
 def conv(data, weight, bias, stride, pad, dilate, groups, channel_last):
     nsp = data.dim() - 2
+    if not channel_last and nsp == 2 and _nchw_on_hip(data):
+        # NCHW API, channels-last execution: activations stay NHWC in memory between HIP kernels
+        # (NCHW-shaped permuted views), so the default layout runs on the same MFMA kernels
+        xl = _as_nhwc_view(data)
+        wl = weight.permute(0, 2, 3, 1).contiguous()
+        if _K.conv_ok(xl, wl, stride, pad, dilate, groups):
+            return _K.ConvNHWC.apply(xl, wl, bias, tuple(stride), tuple(pad), tuple(dilate)).permute(0, 3, 1, 2)
     if channel_last:
         if _use_hip(data) and _K.conv_ok(data, weight, stride, pad, dilate, groups):
             return _K.ConvNHWC.apply(data, weight, bias, tuple(stride), tuple(pad), tuple(dilate))
@@ -106,6 +129,14 @@ def batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_ga
     axis = axis % nd
     channel_last = (axis == nd - 1) and nd > 2
     g = torch.ones_like(gamma) if fix_gamma else gamma
+    if axis == 1 and _nchw_on_hip(data) and data.permute(0, 2, 3, 1).is_contiguous():
+        # channels-last memory behind an NCHW shape (a HIP conv's output): the NHWC kernel applies
+        xl = data.permute(0, 2, 3, 1)
+        al = _as_nhwc_view(addend) if addend is not None else None
+        if _K.bn_ok(xl):
+            out, m, v = _K.BatchNormNHWC.apply(xl, g, beta, al, eps, training, act_type == 'relu',
+                                                moving_mean, moving_var, momentum)
+            return out.permute(0, 3, 1, 2), m, v
     if channel_last and _use_hip(data) and _K.bn_ok(data):
         return _K.BatchNormNHWC.apply(data, g, beta, addend, eps, training, act_type == 'relu',
                                       moving_mean, moving_var, momentum)
@@ -147,6 +178,10 @@ def batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_ga
 
 def global_pool(data, pool_type, channel_last):
     nsp = data.dim() - 2
+    if not channel_last and pool_type == 'avg' and _nchw_on_hip(data) and data.permute(0, 2, 3, 1).is_contiguous():
+        xl = data.permute(0, 2, 3, 1)
+        if _K.gap_ok(xl):
+            return _K.GlobalAvgPoolNHWC.apply(xl).permute(0, 3, 1, 2)
     if channel_last:
         if _use_hip(data) and nsp == 2 and pool_type == 'avg' and _K.gap_ok(data):
             return _K.GlobalAvgPoolNHWC.apply(data)
@@ -170,6 +205,12 @@ def _pool_out(n, k, s, p, conv):
 
 def pool(data, pool_type, kernel, stride, pad, convention, count_include_pad, channel_last, p_value=None):
     nsp = data.dim() - 2
+    if not channel_last and nsp == 2 and pool_type in ('max', 'avg') and convention != 'same' \
+            and _nchw_on_hip(data) and data.permute(0, 2, 3, 1).is_contiguous():
+        xl = data.permute(0, 2, 3, 1)
+        if _K.pool_ok(xl, kernel, stride, pad):
+            return _K.PoolNHWC.apply(xl, pool_type, tuple(kernel), tuple(stride), tuple(pad),
+                                     convention == 'full', bool(count_include_pad)).permute(0, 3, 1, 2)
     if channel_last and _use_hip(data) and nsp == 2 and pool_type in ('max', 'avg') \
             and _K.pool_ok(data, kernel, stride, pad):
         return _K.PoolNHWC.apply(data, pool_type, tuple(kernel), tuple(stride), tuple(pad),
