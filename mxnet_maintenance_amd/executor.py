@@ -198,7 +198,8 @@ class Executor:
         leaves = []
         for n, a in zip(arg_names, self.arg_arrays):
             t = a._data.detach()
-            if need_grad and self._grad_req[n] != 'null':
+            if need_grad and self._grad_req[n] != 'null' and (t.is_floating_point() or t.is_complex()):
+                # integer inputs (indices, labels) are not differentiable: their gradient stays zero
                 t = t.requires_grad_(True)
                 leaves.append((n, t))
             feed[n] = t
