@@ -273,8 +273,14 @@ class Trainer:
                     a.upd = torch.empty(a.numel, dtype=torch.float32, device=a.device)
                     a.table = ChunkTable([(off, n) for (off, n, _shape) in a.views], a.device)
                     a.nrm = torch.zeros(2 * len(a.views), dtype=torch.float32, device=a.device)
-            for (off, n, shape), idx in zip(a.views, a.indices):
+            for p, (off, n, shape), idx in zip(a.params, a.views, a.indices):
                 w32v = NDArray(a.w32[off:off + n].view(shape)) if a.w32 is not None else None
+                if w32v is not None:
+                    # fp32 master visible to kernels that want fp32 parameters (LayerNorm/BN gamma, beta):
+                    # valid while the half tensor is only written by the fused update (whose raw-pointer
+                    # writes keep its version counter); any torch in-place write invalidates it
+                    t = p.list_data()[0]._data
+                    t._mxamd_master = (w32v._data, t._version)
                 if kind == 'sgd':
                     mom = NDArray(a.mom[off:off + n].view(shape)) if a.mom is not None else None
                     st = (mom, w32v) if w32v is not None else mom

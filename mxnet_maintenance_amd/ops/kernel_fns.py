@@ -25,7 +25,14 @@ def _p(t):
 
 
 def _f32(t):
-    return t if t.dtype == torch.float32 and t.is_contiguous() else t.float().contiguous()
+    """fp32 view of a (small, per-channel) parameter: itself, its multi-precision fp32 master copy when
+    the trainer's flat arena registered one (no conversion kernel), or a converted copy."""
+    if t.dtype == torch.float32 and t.is_contiguous():
+        return t
+    m = getattr(t, '_mxamd_master', None)
+    if m is not None and m[1] == t._version and m[0].shape == t.shape:
+        return m[0]
+    return t.float().contiguous()
 
 
 # ---------------------------------------------------------------------------

@@ -77,16 +77,18 @@ class LayerNorm(torch.autograd.Function):
         nb = lib.layernorm_bwd_partials(M)
         part = torch.empty(nb * 2 * D, dtype=torch.float32, device=x.device)
         need_g, need_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
-        tg = _leaf_grad(gamma, D) if need_g else None
-        tb = _leaf_grad(beta, D) if need_b else None
+        # accumulate straight into the parameters' gradient buffers, in their dtype (no conversion/add kernels)
+        same = gamma.dtype == beta.dtype and gamma.dtype in _DT
+        tg = _leaf_grad(gamma, D, dtype=gamma.dtype) if (need_g and same) else None
+        tb = _leaf_grad(beta, D, dtype=beta.dtype) if (need_b and same) else None
         if tg is not None and tb is not None:
-            dg, db, accum = tg, tb, 1
+            dg, db, accum, gdt = tg, tb, 1, _DT[gamma.dtype]
         else:
             out = torch.empty(2, D, dtype=torch.float32, device=x.device)
-            dg, db, accum = out[0], out[1], 0
+            dg, db, accum, gdt = out[0], out[1], 0, _DT[torch.float32]
         lib.layernorm_backward(_DT[x.dtype], x.data_ptr(), gy.data_ptr(), g.data_ptr(), mean.data_ptr(),
-                               rstd.data_ptr(), dx.data_ptr(), part.data_ptr(), dg.data_ptr(), db.data_ptr(), accum,
-                               M, D, _stream())
+                               rstd.data_ptr(), dx.data_ptr(), part.data_ptr(), dg.data_ptr(), db.data_ptr(), gdt,
+                               accum, M, D, _stream())
         if accum:
             return dx, None, None, None, None
         return (dx, dg.view(gamma.shape).to(gamma.dtype) if need_g else None,
@@ -161,10 +163,13 @@ class Dropout(torch.autograd.Function):
         ctx.save_for_backward(mask)
         ctx.p = float(p)
         ctx.mark_non_differentiable(mask)
+        ctx.set_materialize_grads(False)      # no zero-filled gradient for the mask output
         return y, mask
 
     @staticmethod
     def backward(ctx, gy, _gm):
+        if gy is None:
+            return None, None
         mask, = ctx.saved_tensors
         gy = gy.contiguous()
         dx = torch.empty_like(gy)

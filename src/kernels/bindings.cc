@@ -34,7 +34,8 @@ void embedding_forward(int dtype, int itype, const void* idx, const void* w, voi
                        hipStream_t s);
 void embedding_backward(int dtype, int itype, const void* idx, const void* dy, float* acc, uint8_t* touched,
                         int out_dtype, void* grad, int accum, int64_t n, int V, int C, hipStream_t s);
-int bn_nhwc_stats(int dtype, const void* x, const float* center, float* part, int64_t R, int C, hipStream_t s);
+int bn_nhwc_stats(int dtype, const void* x, const float* center, float* part, int64_t R, int C, hipStream_t s,
+                  int total_blocks);
 void colsum_rows(int dtype, const void* x, const float* zeros, float* part, int64_t R, int C, int out_dtype,
                  void* out, int accum, hipStream_t s);
 void softmax_ce_forward(int dtype, int label_is_int, const void* logits, const void* label, float* loss, float* lse,
@@ -62,8 +63,8 @@ int layernorm_bwd_partials(int M);
 void layernorm_forward(int dtype, const void* x, const float* gamma, const float* beta, void* y, float* mean,
                        float* rstd, int M, int D, float eps, hipStream_t s);
 void layernorm_backward(int dtype, const void* x, const void* dy, const float* gamma, const float* mean,
-                        const float* rstd, void* dx, float* part, float* dgamma, float* dbeta, int accum, int M, int D,
-                        hipStream_t s);
+                        const float* rstd, void* dx, float* part, void* dgamma, void* dbeta, int gdtype, int accum,
+                        int M, int D, hipStream_t s);
 void gelu_forward(int dtype, const void* x, void* y, int64_t n, hipStream_t s);
 void gelu_backward(int dtype, const void* x, const void* dy, void* dx, int64_t n, hipStream_t s);
 void softmax_forward(int dtype, int log, const void* x, void* y, int M, int L, float scale, hipStream_t s);
@@ -115,7 +116,7 @@ PYBIND11_MODULE(_hip_kernels, m) {
 
   m.def("bn_partials_rows", &bn_partials_rows);
   m.def("bn_nhwc_stats", [](int dt, uintptr_t x, uintptr_t center, uintptr_t part, int64_t R, int C, uintptr_t s) {
-    int nblk = bn_nhwc_stats(dt, P<const void>(x), P<const float>(center), P<float>(part), R, C, S(s));
+    int nblk = bn_nhwc_stats(dt, P<const void>(x), P<const float>(center), P<float>(part), R, C, S(s), 512);
     check_launch("bn_nhwc_stats");
     return nblk;
   });
@@ -272,10 +273,10 @@ PYBIND11_MODULE(_hip_kernels, m) {
     check_launch("layernorm_forward");
   });
   m.def("layernorm_backward", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t g, uintptr_t mean, uintptr_t rstd,
-                                 uintptr_t dx, uintptr_t part, uintptr_t dg, uintptr_t db, int accum, int M, int D,
-                                 uintptr_t s) {
+                                 uintptr_t dx, uintptr_t part, uintptr_t dg, uintptr_t db, int gdt, int accum, int M,
+                                 int D, uintptr_t s) {
     layernorm_backward(dt, P<void>(x), P<void>(dy), P<float>(g), P<float>(mean), P<float>(rstd), P<void>(dx),
-                       P<float>(part), P<float>(dg), P<float>(db), accum, M, D, S(s));
+                       P<float>(part), P<void>(dg), P<void>(db), gdt, accum, M, D, S(s));
     check_launch("layernorm_backward");
   });
   m.def("gelu_forward", [](int dt, uintptr_t x, uintptr_t y, int64_t n, uintptr_t s) {

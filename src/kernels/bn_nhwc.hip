@@ -327,9 +327,9 @@ __global__ void __launch_bounds__(kBnThreads) bn_bwd_apply_kernel(
 
 // ---------------------------------------------------------------- launchers
 
-static inline int64_t bn_rows_per_block(int64_t R, int C, const BnGeom& g, int* nblk) {
+static inline int64_t bn_rows_per_block(int64_t R, int C, const BnGeom& g, int* nblk, int total_blocks = 512) {
   const int cblocks = C / g.cb;
-  int64_t target = 512 / cblocks;   // ~2 blocks per CU; partial rows stay few
+  int64_t target = total_blocks / cblocks;   // default ~2 blocks per CU; partial rows stay few
   if (target < 8) target = 8;
   int64_t rpb = (R + target - 1) / target;
   rpb = (rpb + g.rpi - 1) / g.rpi * g.rpi;
@@ -450,12 +450,13 @@ static void bn_backward_impl(const void* x, const void* dy, const void* y, const
 
 // Statistics pass only (per-channel partial sums of x - center): lets the conv autotuner charge a
 // candidate that cannot emit BN partials from its epilogue with the pass it leaves to BatchNorm.
-int bn_nhwc_stats(int dtype, const void* x, const float* center, float* part, int64_t R, int C, hipStream_t s) {
+int bn_nhwc_stats(int dtype, const void* x, const float* center, float* part, int64_t R, int C, hipStream_t s,
+                  int total_blocks) {
   MXAMD_HOST_CHECK(C % 8 == 0, "bn_nhwc: channels must be a multiple of 8");
   BnGeom g = bn_geom(C);
   MXAMD_HOST_CHECK(C % g.cb == 0, "bn_nhwc: unsupported channel count");
   int nblk;
-  int64_t rpb = bn_rows_per_block(R, C, g, &nblk);
+  int64_t rpb = bn_rows_per_block(R, C, g, &nblk, total_blocks);
   dim3 grid(nblk, C / g.cb);
   float* p2 = part + static_cast<int64_t>(nblk) * C;
 #define STATS(T)                                                                                              \
@@ -489,7 +490,8 @@ __global__ void __launch_bounds__(256) colsum_finalize_kernel(const float* __res
 // statistics reduce (zero centre) + one wave per column.  ``part`` holds 2 * bn_partials_rows(R, C) * C floats.
 void colsum_rows(int dtype, const void* x, const float* zeros, float* part, int64_t R, int C, int out_dtype,
                  void* out, int accum, hipStream_t s) {
-  const int nblk = bn_nhwc_stats(dtype, x, zeros, part, R, C, s);
+  // small matrices (bias gradients): fewer, fatter blocks -- the partials pass and the finalize stay cheap
+  const int nblk = bn_nhwc_stats(dtype, x, zeros, part, R, C, s, R * C <= (int64_t)(1 << 24) ? 64 : 512);
   const dim3 grid((C + 3) / 4);
   if (out_dtype == kF16)
     hipLaunchKernelGGL(colsum_finalize_kernel<__half>, grid, dim3(256), 0, s, part, nblk, C,

@@ -185,8 +185,9 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const T* __restrict_
 
 // out[c] (+)= sum_b part[b][c] for the 2*D columns (dgamma then dbeta):
 // 32 columns x 8 row-groups per block, LDS combine of the 8 partial sums
+template <typename TO>
 __global__ void __launch_bounds__(256) column_sum_kernel(const float* __restrict__ part, int nb, int ncol,
-                                                         float* __restrict__ out0, float* __restrict__ out1, int D,
+                                                         TO* __restrict__ out0, TO* __restrict__ out1, int D,
                                                          int accum) {
   const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
   const int col = blockIdx.x * 32 + cl;
@@ -206,9 +207,9 @@ __global__ void __launch_bounds__(256) column_sum_kernel(const float* __restrict
     float s = 0.f;
 #pragma unroll
     for (int g = 0; g < 8; ++g) s += red[g][cl];
-    float* o = col < D ? out0 + col : out1 + (col - D);
-    if (accum) *o += s;
-    else *o = s;
+    TO* o = col < D ? out0 + col : out1 + (col - D);
+    if (accum) s += static_cast<float>(*o);
+    *o = static_cast<TO>(s);
   }
 }
 
@@ -438,8 +439,8 @@ void layernorm_forward(int dtype, const void* x, const float* gamma, const float
 
 // part: fp32 workspace of layernorm_bwd_partials(M) * 2 * D; dgamma/dbeta fp32 [D] (written or accumulated)
 void layernorm_backward(int dtype, const void* x, const void* dy, const float* gamma, const float* mean,
-                        const float* rstd, void* dx, float* part, float* dgamma, float* dbeta, int accum, int M, int D,
-                        hipStream_t s) {
+                        const float* rstd, void* dx, float* part, void* dgamma, void* dbeta, int gdtype, int accum,
+                        int M, int D, hipStream_t s) {
   MXAMD_HOST_CHECK(D % 8 == 0, "layernorm: D must be a multiple of 8");
   const int vpl = pick_vpl(D);
   const int nb = layernorm_bwd_partials(M);
@@ -447,8 +448,10 @@ void layernorm_backward(int dtype, const void* x, const void* dy, const float* g
                                                                      dim3(256), 0, s, static_cast<const T*>(x),
                                                                      static_cast<const T*>(dy), gamma, mean, rstd,
                                                                      static_cast<T*>(dx), part, M, D)))
-  hipLaunchKernelGGL(column_sum_kernel, dim3((2 * D + 31) / 32), dim3(256), 0, s, part, nb, 2 * D, dgamma, dbeta, D,
-                     accum);
+  // dgamma / dbeta straight into the parameters' gradient buffers in their own dtype (fp32 / bf16 / fp16)
+  MXAMD_DTYPE_SWITCH(gdtype, hipLaunchKernelGGL((column_sum_kernel<T>), dim3((2 * D + 31) / 32), dim3(256), 0, s,
+                                                part, nb, 2 * D, static_cast<T*>(dgamma), static_cast<T*>(dbeta), D,
+                                                accum))
 }
 
 void gelu_forward(int dtype, const void* x, void* y, int64_t n, hipStream_t s) {
