@@ -360,7 +360,7 @@ def bias_grad(dy2, b_ref, bdt):
     if not (dy2.is_cuda and _K.available() and dy2.dtype in _DT and N % 8 == 0 and _aligned(dy2)):
         return torch.sum(dy2, 0, dtype=torch.float32).to(bdt)
     lib = _K.lib()
-    n = 2 * lib.bn_partials_rows(M, N) * N
+    n = lib.colsum_partials(M, N)
     part = _COLSUM_PART.get(dy2.device)
     if part is None or part.numel() < n:
         part = _COLSUM_PART[dy2.device] = torch.empty(n, dtype=torch.float32, device=dy2.device)

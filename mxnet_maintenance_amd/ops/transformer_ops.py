@@ -76,7 +76,14 @@ def sdp_attention(queries_keys_values, mask=None, heads=1, dropout=0.0, causal=F
 
     ``mask`` (B, S_k) with 1 = attend, 0 = padding (valid-length masking)."""
     from .. import _state
+    from .hip_ops import _use_hip
     x = queries_keys_values
+    p = dropout if _state.STATE.training else 0.0
+    if _use_hip(x):
+        from .attention_fns import SelfAttention, attention_ok
+        if attention_ok(x, heads, causal):
+            # hand-written gfx950 kernels: no (B*H, S, S) scores, gradient straight into the qkv layout
+            return SelfAttention.apply(x, mask, heads, float(p))
     S, B, C = x.shape
     D = C // (heads * 3)
     t = x.reshape(S, B, heads, 3, D).permute(3, 1, 2, 0, 4)     # (3, B, H, S, D)
@@ -84,6 +91,5 @@ def sdp_attention(queries_keys_values, mask=None, heads=1, dropout=0.0, causal=F
     am = None
     if mask is not None:
         am = mask.bool().reshape(B, 1, 1, -1)
-    p = dropout if _state.STATE.training else 0.0
     o = F.scaled_dot_product_attention(q, k, v, attn_mask=am, dropout_p=p, is_causal=causal and am is None)
     return o.permute(2, 0, 1, 3).reshape(S, B, heads * D)

@@ -21,7 +21,7 @@ import numpy as np
 import torch
 
 from ..attribute import AttrScope
-from ..base import MXNetError, numeric_types, torch_dtype, np_dtype, dtype_name
+from ..base import NotImplementedForSymbol, MXNetError, numeric_types, torch_dtype, np_dtype, dtype_name
 from ..name import NameManager
 from ..ops import registry
 
@@ -203,12 +203,18 @@ class Symbol:
         return Symbol(outs)
 
     def get_children(self):
-        if len(self._outputs) != 1:
-            return None
-        node, _ = self._outputs[0]
-        if not node.inputs:
-            return None
-        return Symbol(list(node.inputs))
+        """Inputs of every output node, in order (None when there are none: variables)."""
+        kids, seen = [], set()
+        for node, _ in self._outputs:
+            if id(node) not in seen:
+                seen.add(id(node))
+                kids.extend(node.inputs)
+        return Symbol(kids) if kids else None
+
+    def __bool__(self):
+        raise NotImplementedForSymbol(self.__bool__, 'bool')
+
+    __nonzero__ = __bool__
 
     def _var_nodes(self):
         return {n.name: n for n in self._topo() if n.op is None}
@@ -392,7 +398,7 @@ class Symbol:
             shapes, dtypes = {k: tuple(v) for k, v in known.items()}, {}
         else:
             shapes, dtypes = {}, {k: torch_dtype(v) for k, v in known.items()}
-        res = infer_graph(self, shapes, dtypes, what=what)
+        res = infer_graph(self, shapes, dtypes, what=what, partial=partial)
         arg_res, out_res, aux_res = res
         if what == 'shape':
             complete = all(s is not None for s in arg_res + out_res + aux_res)
@@ -422,9 +428,12 @@ class Symbol:
                 arg_nodes.append(i)
             row_ptr.append(row_ptr[-1] + (n.num_outputs() if n.op is not None else 1))
         heads = [[index[id(n)], j, 0] for n, j in self._outputs]
+        from ..util import is_np_shape
+        gattrs = {'mxnet_version': ['int', _MXNET_VERSION]}
+        if is_np_shape():
+            gattrs['is_np_shape'] = ['int', 1]
         return json.dumps({'nodes': nodes, 'arg_nodes': arg_nodes, 'node_row_ptr': row_ptr,
-                           'heads': heads, 'attrs': {'mxnet_version': ['int', _MXNET_VERSION]}},
-                          indent=2)
+                           'heads': heads, 'attrs': gattrs}, indent=2)
 
     def save(self, fname, remove_amp_cast=True):
         with open(fname, 'w') as f:
@@ -726,6 +735,12 @@ def _run_meta(op, parsed, shapes, dtypes):
 _SHAPE_PRESERVING = ('Cast', 'cast', 'amp_cast', 'amp_multicast', '_copy', 'identity', 'BlockGrad',
                      'stop_gradient')
 
+_SAME_SHAPE = frozenset(['elemwise_add', 'elemwise_sub', 'elemwise_mul', 'elemwise_div', '_grad_add', '_plus',
+                         '_minus', '_mul', '_div', '_add', '_sub', 'add_n', 'ElementWiseSum', '_maximum', '_minimum',
+                         '_power', '_hypot', 'Activation', 'relu', 'sigmoid', 'tanh', 'softsign', 'Dropout',
+                         'BlockGrad', 'stop_gradient', 'identity', '_copy', 'make_loss', 'MakeLoss', 'negative',
+                         'abs', 'exp', 'log', 'sqrt', 'square'])
+
 _INIT_OPS = ('_zeros', '_ones', '_full', '_empty', 'zeros', 'ones', 'full')
 
 
@@ -760,7 +775,7 @@ def _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what):
     return None
 
 
-def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True):
+def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True, partial=False):
     """Propagate shapes and dtypes through the graph.
 
     Returns (arg_list, out_list, aux_list) of shapes (or dtypes), None for unknown.
@@ -811,6 +826,16 @@ def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True):
                             if (id(a), j) in shape:
                                 break
                             shape[(id(a), j)] = tuple(s)
+            if any(s is None for s in in_shapes) and n.op in _SAME_SHAPE:
+                # elementwise ops (nnvm ElemwiseShape): every input and output has one shape, so a
+                # known one fills the others (backward inference into unknown producers)
+                ref = next((s for s in in_shapes + [shape.get((id(n), 0))] if s is not None), None)
+                if ref is not None:
+                    for idx, (a, j) in enumerate(n.inputs):
+                        if in_shapes[idx] is None:
+                            shape[(id(a), j)] = ref
+                            in_shapes[idx] = ref
+                            progress = True
             if any(s is None for s in in_shapes):
                 if what == 'type':
                     # dtype-only propagation: parameters follow the data dtype, outputs
@@ -847,11 +872,15 @@ def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True):
             except Exception as e:
                 raise MXNetError('Error in operator %s (%s): %s' % (n.name, n.op, e))
             for i, (s, d) in enumerate(outs):
+                prev = shape.get((id(n), i))
+                if prev is not None and tuple(prev) != tuple(s):
+                    raise MXNetError('Error in operator %s (%s): inferred output shape %s conflicts with %s '
+                                     'required by its consumers' % (n.name, n.op, tuple(s), tuple(prev)))
                 shape[(id(n), i)] = s
                 dtype[(id(n), i)] = d
             done.add(id(n))
             progress = True
-    if what == 'type':
+    if what == 'type' and not partial:
         # variables only consumed through explicit casts (AMP graphs) default to fp32 storage
         consumers = {}
         for n in order:

@@ -36,6 +36,7 @@ void embedding_backward(int dtype, int itype, const void* idx, const void* dy, f
                         int out_dtype, void* grad, int accum, int64_t n, int V, int C, hipStream_t s);
 int bn_nhwc_stats(int dtype, const void* x, const float* center, float* part, int64_t R, int C, hipStream_t s,
                   int total_blocks);
+int64_t colsum_partials(int64_t R, int C);
 void colsum_rows(int dtype, const void* x, const float* zeros, float* part, int64_t R, int C, int out_dtype,
                  void* out, int accum, hipStream_t s);
 void softmax_ce_forward(int dtype, int label_is_int, const void* logits, const void* label, float* loss, float* lse,
@@ -73,6 +74,12 @@ void softmax_backward(int dtype, int log, const void* y, const void* dy, void* d
 void dropout_forward(int dtype, const void* x, void* y, uint8_t* mask, int64_t n, float p, uint64_t seed,
                      const uint64_t* seed_base, hipStream_t s);
 void dropout_backward(int dtype, const void* dy, const uint8_t* mask, void* dx, int64_t n, float p, hipStream_t s);
+int attention_max_seq();
+void attention_forward(int dtype, const void* qkv, const float* kmask, void* out, float* lse, int S, int B, int H,
+                       int D, float scale, float p, uint64_t seed, const uint64_t* seed_base, hipStream_t s);
+void attention_backward(int dtype, const void* qkv, const float* kmask, const void* out, const void* dout,
+                        const float* lse, float* delta, void* dqkv, int S, int B, int H, int D, float scale, float p,
+                        uint64_t seed, const uint64_t* seed_base, hipStream_t s);
 void flat_adam(int dtype, int mode, void* w, const void* g, float* mean, float* var, float* w32, int64_t n, float lr,
                float beta1, float beta2, float eps, float wd, float eta, float rescale, float clip, const float* hp,
                hipStream_t s);
@@ -104,6 +111,7 @@ static inline T* P(uintptr_t p) {
   return reinterpret_cast<T*>(p);
 }
 static inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+static inline hipStream_t S_(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 static void check_launch(const char* name) {
   hipError_t e = hipGetLastError();
@@ -147,6 +155,7 @@ PYBIND11_MODULE(_hip_kernels, m) {
     int8_gemm(P<const int8_t>(a), P<const int8_t>(b), P<int32_t>(c), M, N, K, S(s));
     check_launch("int8_gemm");
   });
+  m.def("colsum_partials", [](int64_t R, int C) { return colsum_partials(R, C); });
   m.def("colsum_rows", [](int dt, uintptr_t x, uintptr_t zeros, uintptr_t part, int64_t R, int C, int odt,
                           uintptr_t out, int accum, uintptr_t s) {
     colsum_rows(dt, P<const void>(x), P<const float>(zeros), P<float>(part), R, C, odt, P<void>(out), accum, S(s));
@@ -306,6 +315,21 @@ PYBIND11_MODULE(_hip_kernels, m) {
                               uintptr_t s, uintptr_t seed_base) {
     dropout_forward(dt, P<void>(x), P<void>(y), P<uint8_t>(mask), n, p, seed, P<uint64_t>(seed_base), S(s));
     check_launch("dropout_forward");
+  });
+  m.def("attention_max_seq", []() { return attention_max_seq(); });
+  m.def("attention_forward", [](int dt, uintptr_t qkv, uintptr_t kmask, uintptr_t out, uintptr_t lse, int S, int B,
+                                int H, int D, float scale, float p, uint64_t seed, uintptr_t seed_base, uintptr_t s) {
+    attention_forward(dt, P<const void>(qkv), P<const float>(kmask), P<void>(out), P<float>(lse), S, B, H, D, scale, p,
+                      seed, P<const uint64_t>(seed_base), S_(s));
+    check_launch("attention_forward");
+  });
+  m.def("attention_backward", [](int dt, uintptr_t qkv, uintptr_t kmask, uintptr_t out, uintptr_t dout, uintptr_t lse,
+                                 uintptr_t delta, uintptr_t dqkv, int S, int B, int H, int D, float scale, float p,
+                                 uint64_t seed, uintptr_t seed_base, uintptr_t s) {
+    attention_backward(dt, P<const void>(qkv), P<const float>(kmask), P<const void>(out), P<const void>(dout),
+                       P<const float>(lse), P<float>(delta), P<void>(dqkv), S, B, H, D, scale, p, seed,
+                       P<const uint64_t>(seed_base), S_(s));
+    check_launch("attention_backward");
   });
   m.def("dropout_backward", [](int dt, uintptr_t dy, uintptr_t mask, uintptr_t dx, int64_t n, float p, uintptr_t s) {
     dropout_backward(dt, P<void>(dy), P<uint8_t>(mask), P<void>(dx), n, p, S(s));

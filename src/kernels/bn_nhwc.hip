@@ -24,6 +24,8 @@
 // one block per channel combines the (channel-major) partials in fp64.
 #include <stdexcept>
 
+#include <algorithm>
+
 #include "common.h"
 
 namespace mxamd {
@@ -467,41 +469,105 @@ int bn_nhwc_stats(int dtype, const void* x, const float* center, float* part, in
   return nblk;
 }
 
-// out[c] (+)= sum_r x[r][c] from the channel-major partials of the statistics pass
-template <typename TO>
-__global__ void __launch_bounds__(256) colsum_finalize_kernel(const float* __restrict__ part, int nblk, int C,
-                                                             TO* __restrict__ out, int accum) {
-  // one wave per column
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (c >= C) return;
-  const float* p = part + static_cast<int64_t>(c) * nblk;
-  float a = 0.f;
-  for (int i = lane; i < nblk; i += 64) a += p[i];
+// Column sums of a row-major [R][C] matrix (bias gradient of a FullyConnected layer).
+// Pass 1: grid (C/64 column strips) x (row chunks), ~768 blocks even for a 4096 x 768 gradient;
+// each block = 8 column vectors (16-byte loads, 64 columns) x 32 row lanes, LDS combine of the row
+// lanes, one fp32 partial row per chunk.  Pass 2: per 64 columns, 4 lanes per column sum the chunks
+// (coalesced rows of the partials) and write / accumulate the parameter gradient in its dtype.
+namespace {
+constexpr int kColsumTargetBlocks = 768;
+
+inline void colsum_geom(int64_t R, int C, int* nchunk, int* rows_per) {
+  const int strips = (C + 63) / 64;
+  int64_t n = (kColsumTargetBlocks + strips - 1) / strips;
+  n = std::max<int64_t>(1, std::min<int64_t>(n, (R + 31) / 32));
+  int64_t rp = (R + n - 1) / n;
+  rp = (rp + 31) / 32 * 32;
+  *rows_per = static_cast<int>(rp);
+  *nchunk = static_cast<int>((R + rp - 1) / rp);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_part_kernel(const T* __restrict__ x, int64_t R, int C, int rows_per,
+                                                          float* __restrict__ part) {
+  __shared__ float red[32][64 + 1];
+  const int cv = threadIdx.x & 7, ty = threadIdx.x >> 3;
+  const int c0 = (blockIdx.x * 8 + cv) * 8;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * rows_per;
+  const int64_t r1 = r0 + rows_per < R ? r0 + rows_per : R;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < C) {
+    for (int64_t r = r0 + ty; r < r1; r += 32) {
+      Vec8<T> v;
+      v.load(x + r * C + c0);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
-  if (lane == 0) {
-    if (accum) a += static_cast<float>(out[c]);
-    out[c] = static_cast<TO>(a);
+      for (int i = 0; i < 8; ++i) a[i] += v.get(i);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[ty][cv * 8 + i] = a[i];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int col = threadIdx.x;
+    float t = 0.f;
+#pragma unroll 8
+    for (int j = 0; j < 32; ++j) t += red[j][col];
+    const int c = blockIdx.x * 64 + col;
+    if (c < C) part[static_cast<int64_t>(blockIdx.y) * C + c] = t;
   }
 }
 
-// Column sums of a row-major [R][C] matrix (bias gradient of a FullyConnected layer): the BN
-// statistics reduce (zero centre) + one wave per column.  ``part`` holds 2 * bn_partials_rows(R, C) * C floats.
+template <typename TO>
+__global__ void __launch_bounds__(256) colsum_fin_kernel(const float* __restrict__ part, int nchunk, int C,
+                                                         TO* __restrict__ out, int accum) {
+  __shared__ float red[4][64];
+  const int col = threadIdx.x & 63, l4 = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + col;
+  float t = 0.f;
+  if (c < C)
+    for (int i = l4; i < nchunk; i += 4) t += part[static_cast<int64_t>(i) * C + c];
+  red[l4][col] = t;
+  __syncthreads();
+  if (l4 == 0 && c < C) {
+    t = red[0][col] + red[1][col] + red[2][col] + red[3][col];
+    if (accum) t += static_cast<float>(out[c]);
+    out[c] = static_cast<TO>(t);
+  }
+}
+}  // namespace
+
+int64_t colsum_partials(int64_t R, int C) {
+  int nchunk, rows_per;
+  colsum_geom(R, C, &nchunk, &rows_per);
+  return static_cast<int64_t>(nchunk) * C;
+}
+
 void colsum_rows(int dtype, const void* x, const float* zeros, float* part, int64_t R, int C, int out_dtype,
                  void* out, int accum, hipStream_t s) {
-  // small matrices (bias gradients): fewer, fatter blocks -- the partials pass and the finalize stay cheap
-  const int nblk = bn_nhwc_stats(dtype, x, zeros, part, R, C, s, R * C <= (int64_t)(1 << 24) ? 64 : 512);
-  const dim3 grid((C + 3) / 4);
+  (void)zeros;
+  MXAMD_HOST_CHECK(C % 8 == 0, "colsum_rows: columns must be a multiple of 8");
+  int nchunk, rows_per;
+  colsum_geom(R, C, &nchunk, &rows_per);
+  const dim3 grid((C + 63) / 64, nchunk);
+  if (dtype == kF16)
+    hipLaunchKernelGGL(colsum_part_kernel<__half>, grid, dim3(256), 0, s, static_cast<const __half*>(x), R, C,
+                       rows_per, part);
+  else if (dtype == kBF16)
+    hipLaunchKernelGGL(colsum_part_kernel<__hip_bfloat16>, grid, dim3(256), 0, s,
+                       static_cast<const __hip_bfloat16*>(x), R, C, rows_per, part);
+  else
+    hipLaunchKernelGGL(colsum_part_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(x), R, C,
+                       rows_per, part);
+  const dim3 g2((C + 63) / 64);
   if (out_dtype == kF16)
-    hipLaunchKernelGGL(colsum_finalize_kernel<__half>, grid, dim3(256), 0, s, part, nblk, C,
-                       static_cast<__half*>(out), accum);
+    hipLaunchKernelGGL(colsum_fin_kernel<__half>, g2, dim3(256), 0, s, part, nchunk, C, static_cast<__half*>(out),
+                       accum);
   else if (out_dtype == kBF16)
-    hipLaunchKernelGGL(colsum_finalize_kernel<__hip_bfloat16>, grid, dim3(256), 0, s, part, nblk, C,
+    hipLaunchKernelGGL(colsum_fin_kernel<__hip_bfloat16>, g2, dim3(256), 0, s, part, nchunk, C,
                        static_cast<__hip_bfloat16*>(out), accum);
   else
-    hipLaunchKernelGGL(colsum_finalize_kernel<float>, grid, dim3(256), 0, s, part, nblk, C,
-                       static_cast<float*>(out), accum);
+    hipLaunchKernelGGL(colsum_fin_kernel<float>, g2, dim3(256), 0, s, part, nchunk, C, static_cast<float*>(out),
+                       accum);
 }
 
 void bn_nhwc_forward(int dtype, const void* x, const void* addend, void* y, uint8_t* mask, const float* gamma,

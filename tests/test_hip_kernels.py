@@ -698,7 +698,7 @@ def test_colsum_rows_bias_grad(dtype, mn, out_dtype):
     torch.manual_seed(1)
     x = torch.randn(M, N, device='cuda').to(dtype)
     lib = K.lib()
-    part = torch.empty(2 * lib.bn_partials_rows(M, N) * N, dtype=torch.float32, device='cuda')
+    part = torch.empty(lib.colsum_partials(M, N), dtype=torch.float32, device="cuda")
     out = torch.randn(N, device='cuda').to(out_dtype)
     base = out.float().clone()
     lib.colsum_rows(KF._DT[dtype], x.data_ptr(), KF._zeros_f32(N, x.device).data_ptr(), part.data_ptr(), M, N,

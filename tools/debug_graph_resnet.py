@@ -39,9 +39,17 @@ def run(graph, model='resnet50_v1b', B=32, S=112, steps=6, lr=0.001):
 
 
 if __name__ == '__main__':
-    e0 = run(False)      # autotunes
-    e = run(False)       # same kernels as the graph run
-    g = run(True)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--lr', type=float, default=0.001)
+    ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--size', type=int, default=112)
+    ap.add_argument('--steps', type=int, default=6)
+    a = ap.parse_args()
+    kw = dict(B=a.batch, S=a.size, steps=a.steps, lr=a.lr)
+    e0 = run(False, **kw)      # autotunes
+    e = run(False, **kw)       # same kernels as the graph run
+    g = run(True, **kw)
     for i, ((le0, pe0), (le, pe), (lg, pg)) in enumerate(zip(e0, e, g)):
         d_ee = max(float(np.abs(a - b).max()) for a, b in zip(pe0, pe))
         d = max(float(np.abs(a - b).max()) for a, b in zip(pe, pg))
