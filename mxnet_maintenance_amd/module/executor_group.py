@@ -248,9 +248,10 @@ class DataParallelExecutorGroup:
     def backward(self, out_grads=None):
         if not self.for_training:
             raise AssertionError('bind with for_training=True to run backward')
+        axes = self._output_axes()
         for s in self.shards:
-            heads = [nd.slice_axis(g, axis=0, begin=s.slice.start, end=s.slice.stop).as_in_context(s.ctx)
-                     for g in (out_grads or [])]
+            heads = [(nd.slice_axis(g, axis=ax, begin=s.slice.start, end=s.slice.stop) if ax >= 0 else g)
+                     .as_in_context(s.ctx) for g, ax in zip(out_grads or [], axes)]
             s.exe.backward(out_grads=heads or None)
 
     def get_output_shapes(self):
@@ -259,16 +260,28 @@ class DataParallelExecutorGroup:
         _, out_shapes, _ = self.symbol.infer_shape(**known)
         return list(zip(self.symbol.list_outputs(), [tuple(s) for s in out_shapes]))
 
+    def _output_axes(self):
+        """Batch axis of every output, from its ``__layout__`` attribute (default N first)."""
+        axes = []
+        for name in self.symbol.list_outputs():
+            try:
+                layout = self.symbol[name].attr('__layout__')
+            except Exception:       # pylint: disable=broad-except
+                layout = None
+            axes.append(DataDesc.get_batch_axis(layout))
+        return axes
+
     def get_outputs(self, merge_multi_context=True, begin=0, end=None):
         n_out = len(self.shards[0].exe.outputs)
-        picked = [[s.exe.outputs[i] for s in self.shards] for i in range(begin, n_out if end is None else end)]
-        return _merge_multi_context(picked, [0] * len(picked)) if merge_multi_context else picked
+        end = n_out if end is None else end
+        picked = [[s.exe.outputs[i] for s in self.shards] for i in range(begin, end)]
+        return _merge_multi_context(picked, self._output_axes()[begin:end]) if merge_multi_context else picked
 
     def get_input_grads(self, merge_multi_context=True):
         if not self.inputs_need_grad:
             raise AssertionError('bind with inputs_need_grad=True to get input gradients')
         g = self.input_grad_arrays
-        return _merge_multi_context(g, [0] * len(g)) if merge_multi_context else g
+        return _merge_multi_context(g, list(self.data_layouts)) if merge_multi_context else g
 
     def get_states(self, merge_multi_context=True):
         if merge_multi_context:

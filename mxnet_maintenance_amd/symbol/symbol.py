@@ -753,22 +753,44 @@ def _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what):
     back into the node's ``shape`` attribute (so executors allocate it).
     """
     zero_nodes = []
+    zero_vars = []      # variables declared with unknown (0) dims, e.g. RNN begin_state(func=Variable)
     for n in order:
         if n.op in _INIT_OPS and 'shape' in n.attrs:
             shp = n.parsed().get('shape')
             if shp and any(int(d) == 0 for d in shp):
                 zero_nodes.append((n, tuple(int(d) for d in shp)))
-    if not zero_nodes:
+        elif n.op is None and n.name not in known_shapes and n.attrs.get('__shape__'):
+            shp = registry.parse_value('shape', n.attrs['__shape__'])
+            if shp and any(int(d) == 0 for d in shp) and not all(int(d) == 0 for d in shp):
+                zero_vars.append((n, tuple(int(d) for d in shp)))
+    if not zero_nodes and not zero_vars:
         return None
     cands = sorted({int(d) for s in known_shapes.values() if s for d in s if int(d) > 1})
+    aux = _aux_var_ids(order)
+    arg_nodes = [n for n in order if n.op is None and id(n) not in aux]
+    complete = lambda r: all(x is not None for part in r for x in part)     # noqa: E731
     for v in cands:
         for n, shp in zero_nodes:
             n.attrs['shape'] = str(tuple(d if d else v for d in shp))
             n._parsed = None
         try:
-            return infer_graph(sym, known_shapes, known_dtypes, what, _resolve=False)
+            res = infer_graph(sym, known_shapes, known_dtypes, what, _resolve=False)
         except MXNetError:
             continue
+        if not zero_vars or complete(res):
+            return res
+        # only variables the graph could not size itself (e.g. RNN states) take the candidate
+        unresolved = {n.name for n, r in zip(arg_nodes, res[0]) if r is None}
+        ks = dict(known_shapes)
+        for n, shp in zero_vars:
+            if n.name in unresolved:
+                ks[n.name] = tuple(d if d else v for d in shp)
+        try:
+            res = infer_graph(sym, ks, known_dtypes, what, _resolve=False)
+        except MXNetError:
+            continue
+        if complete(res):
+            return res
     for n, shp in zero_nodes:
         n.attrs['shape'] = str(shp)
         n._parsed = None

@@ -176,7 +176,15 @@ __global__ void __launch_bounds__(kFinThreads) bn_finalize_kernel(
   const float* p1 = part1 + static_cast<int64_t>(c) * nblk;
   const float* p2 = part2 + static_cast<int64_t>(c) * nblk;
   double a = 0.0, b = 0.0;
-  for (int i = tid; i < nblk; i += kFinThreads) {
+  // 16-byte loads where the channel's partial row is aligned: 4x fewer dependent load rounds
+  const int nv = ((reinterpret_cast<uintptr_t>(p1) | reinterpret_cast<uintptr_t>(p2)) & 15) == 0 ? nblk / 4 : 0;
+  for (int i = tid; i < nv; i += kFinThreads) {
+    const float4 x = reinterpret_cast<const float4*>(p1)[i];
+    const float4 y = reinterpret_cast<const float4*>(p2)[i];
+    a += static_cast<double>(x.x) + static_cast<double>(x.y) + static_cast<double>(x.z) + static_cast<double>(x.w);
+    b += static_cast<double>(y.x) + static_cast<double>(y.y) + static_cast<double>(y.z) + static_cast<double>(y.w);
+  }
+  for (int i = nv * 4 + tid; i < nblk; i += kFinThreads) {
     a += p1[i];
     b += p2[i];
   }
