@@ -77,11 +77,16 @@ class GraphProgram:
                 for j, a in enumerate(args):
                     if a is not None:
                         monitor('%s_input%d' % (name, j), a)
-            if _profiler.active_symbolic:
-                with _profiler.op_span(_profiler.current_scope() + opname, symbolic=True):
+            try:
+                if _profiler.active_symbolic:
+                    with _profiler.op_span(_profiler.current_scope() + opname, symbolic=True):
+                        r = fn(*args, **attrs)
+                else:
                     r = fn(*args, **attrs)
-            else:
-                r = fn(*args, **attrs)
+            except MXNetError:
+                raise
+            except RuntimeError as e:
+                raise MXNetError('Error in operator %s (%s): %s' % (name, opname, e)) from e
             if len(outs) == 1:
                 vals[outs[0]] = r[0] if isinstance(r, (tuple, list)) else r
             else:

@@ -674,7 +674,16 @@ class HybridBlock(Block):
             cld._monitor_all = monitor_all
 
     def forward(self, x, *args):
-        has_symbol = isinstance(x, Symbol) or any(isinstance(a, Symbol) for a in args)
+        flat, _ = _flatten([x] + list(args), 'input')
+        kinds = {type(a) is not None and (isinstance(a, Symbol) and 'sym' or isinstance(a, NDArray) and 'nd')
+                 for a in flat if a is not None}
+        kinds.discard(False)
+        if not kinds:
+            raise ValueError('In HybridBlock, there must be one NDArray or one Symbol in the input. '
+                             'Please check the type of the args.')
+        if len(kinds) > 1:
+            raise ValueError('In HybridBlock, we do not support mixed NDArrays and Symbols types for the input.')
+        has_symbol = 'sym' in kinds
         if not has_symbol and (isinstance(x, NDArray) or any(isinstance(a, NDArray) for a in args)):
             first = x if isinstance(x, NDArray) else next(a for a in args if isinstance(a, NDArray))
             ctx = first.context

@@ -63,6 +63,10 @@ class Parameter:
         self.wd_mult = wd_mult
         self.grad_req = grad_req
         self.init = init
+        valid = ('default', 'row_sparse', 'csr')
+        assert stype in valid, "Invalid stype '%s' for Parameter '%s', expected one of %s" % (stype, name, valid)
+        assert grad_stype in valid, \
+            "Invalid grad_stype '%s' for Parameter '%s', expected one of %s" % (grad_stype, name, valid)
         self._stype = stype
         self._grad_stype = grad_stype
 
@@ -330,6 +334,9 @@ class Parameter:
         return self._check_and_get(self._data, ctx)
 
     def list_data(self):
+        if self._stype != 'default':
+            raise RuntimeError("Cannot return copies of Parameter '%s' on all contexts via list_data() because its "
+                               "storage type is %s. Please use row_sparse_data() instead." % (self.name, self._stype))
         return self._check_and_get(self._data, list)
 
     def grad(self, ctx=None):

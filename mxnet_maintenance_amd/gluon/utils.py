@@ -37,6 +37,11 @@ def split_data(data, num_slice, batch_axis=0, even_split=True):
         num_slice = size
         div_points = list(range(size + 1))
     slices = []
+    if getattr(data, 'stype', 'default') == 'csr':
+        # compressed row slices keep the CSR storage
+        if batch_axis != 0:
+            raise ValueError('CSRNDArray can only be split along axis 0, got %d' % batch_axis)
+        return [data[int(div_points[i]):int(div_points[i + 1])] for i in range(num_slice)]
     for i in range(num_slice):
         st, end = int(div_points[i]), int(div_points[i + 1])
         idx = [slice(None)] * data.ndim

@@ -102,11 +102,17 @@ def invoke(op, inputs, attrs, out=None):
     _note_leaves(inputs)
     if _amp.active:
         tin = _amp.cast_inputs(op.name, tin, attrs)
-    if _profiler.active_imperative:
-        with _profiler.op_span(_profiler.current_scope() + op.name):
+    try:
+        if _profiler.active_imperative:
+            with _profiler.op_span(_profiler.current_scope() + op.name):
+                res = _run(op.fn, tin, attrs)
+        else:
             res = _run(op.fn, tin, attrs)
-    else:
-        res = _run(op.fn, tin, attrs)
+    except MXNetError:
+        raise
+    except RuntimeError as e:
+        # operator failures surface as MXNetError (a RuntimeError), as from the reference's C API
+        raise MXNetError('Error in operator %s: %s' % (op.name, e)) from e
     nvis = op.get_num_visible_outputs(attrs)
     if isinstance(res, (tuple, list)):
         outs = [NDArray(r) for r in res[:nvis]]

@@ -21,6 +21,26 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_REF = '/root/reference/tests/python'
 
 
+_STORE_CACHE = os.path.join(tempfile.gettempdir(), 'mxref_model_store')
+_SYNTHETIC_MODELS = ('resnet18_v1',)
+
+
+def _synthetic_model_store(dst, env):
+    """Random-init ``<name>-<hash>.params`` files for the model-zoo names the reference tests load."""
+    os.makedirs(dst, exist_ok=True)
+    os.makedirs(_STORE_CACHE, exist_ok=True)
+    for name in _SYNTHETIC_MODELS:
+        fname = '%s-%s.params' % (name, '0' * 40)
+        cached = os.path.join(_STORE_CACHE, fname)
+        if not os.path.exists(cached):
+            code = ('import sys; sys.path.insert(0, %r); import mxnet_maintenance_amd as mx; '
+                    'net = mx.gluon.model_zoo.vision.get_model(%r); net.initialize(); '
+                    'net(mx.nd.ones((1, 3, 32, 32))); net.save_parameters(%r)'
+                    % (os.path.dirname(os.path.dirname(HERE)), name, cached))
+            subprocess.run([sys.executable, '-c', code], env=env, check=True, capture_output=True)
+        shutil.copy(cached, os.path.join(dst, fname))
+
+
 def run_one(ref, name, timeout, workers, select=None, tb=None):
     tmp = tempfile.mkdtemp(prefix='mxref_')
     try:
@@ -38,6 +58,11 @@ def run_one(ref, name, timeout, workers, select=None, tb=None):
         env['PYTHONPATH'] = os.pathsep.join([HERE, unit, os.path.join(tmp, 'common'), os.path.join(ref, 'train')] +
                                             ([env['PYTHONPATH']] if env.get('PYTHONPATH') else []))
         env['PYTHONDONTWRITEBYTECODE'] = '1'
+        # no network: "pretrained" model-zoo weights are random-init files of the same architecture in a
+        # scratch HOME (the tests only check save/export/import round trips with them)
+        home = os.path.join(tmp, 'home')
+        _synthetic_model_store(os.path.join(home, '.mxnet', 'models'), env)
+        env['HOME'] = home
         env.setdefault('MXNET_TEST_SEED', '42')
         cmd = [sys.executable, '-m', 'pytest', '-q', '-p', 'mxalias', '-p', 'no:cacheprovider', '--noconftest',
                '--timeout', str(timeout), '-o', 'addopts=', '--rootdir', tmp, os.path.join(unit, name + '.py')]
