@@ -407,13 +407,15 @@ class FusedRNN(Initializer):
         first = total - per_rest
         ni = (first // d - g * h * h - 2 * g * h) // (g * h)
         off = 0
+        # FusedRNN(None, ...): the pieces take the global initializer (the reference's desc.global_init)
+        sub = self._init if self._init is not None else (getattr(desc, 'global_init', None) or Uniform())
         with torch.no_grad():
             for layer in range(self._num_layers):
                 nin = ni if layer == 0 else h * d
                 for _ in range(d):
                     for n in (g * h * nin, g * h * h):
                         piece = NDArray(arr._data[off:off + n].view(g * h, -1))
-                        self._init._init_weight(InitDesc('weight'), piece)
+                        sub._init_weight(InitDesc('weight'), piece)
                         off += n
             for layer in range(self._num_layers):
                 for _ in range(d):

@@ -248,7 +248,7 @@ class DataParallelExecutorGroup:
     def backward(self, out_grads=None):
         if not self.for_training:
             raise AssertionError('bind with for_training=True to run backward')
-        axes = self._output_axes()
+        axes = self._output_axes() if len(self.shards) > 1 else [-1] * len(out_grads or [])
         for s in self.shards:
             heads = [(nd.slice_axis(g, axis=ax, begin=s.slice.start, end=s.slice.stop) if ax >= 0 else g)
                      .as_in_context(s.ctx) for g, ax in zip(out_grads or [], axes)]

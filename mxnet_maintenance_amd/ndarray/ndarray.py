@@ -747,8 +747,10 @@ def _into(out, result):
 
 
 def empty(shape, ctx=None, dtype=None, stype=None):
-    if isinstance(shape, int):
-        shape = (shape,)
+    if isinstance(shape, (int, np.integer)):
+        shape = (int(shape),)
+    else:
+        shape = tuple(int(d) for d in shape)
     if stype not in (None, 'default'):
         from . import sparse
         return sparse.empty(stype, shape, ctx=ctx, dtype=dtype)

@@ -449,7 +449,7 @@ class Symbol:
         return self.bind(*a, **k)
 
     def simple_bind(self, ctx, grad_req='write', type_dict=None, stype_dict=None, group2ctx=None,
-                    shared_arg_names=None, shared_exec=None, shared_buffer=None, **kwargs):
+                    shared_arg_names=None, shared_exec=None, shared_buffer=None, force_rebind=False, **kwargs):
         from ..executor import Executor
         from .. import ndarray as nd
         arg_shapes, _, aux_shapes = self.infer_shape(**kwargs)

@@ -358,6 +358,13 @@ def simple_forward(sym, ctx=None, is_train=False, **inputs):
     return outputs
 
 
+def _arg_dtype(v, dtype):
+    """dtype='asnumpy' (reference convention): every array keeps its own dtype."""
+    if isinstance(dtype, str) and dtype == 'asnumpy':
+        return v.dtype if hasattr(v, 'dtype') else default_dtype()
+    return dtype
+
+
 def _parse_location(sym, location, ctx, dtype=default_dtype()):
     if isinstance(location, dict):
         if set(location.keys()) != set(sym.list_arguments()):
@@ -378,7 +385,7 @@ def _parse_aux_states(sym, aux_states, ctx, dtype=default_dtype()):
             raise ValueError('Symbol aux_states names and given aux_states do not match.')
     elif isinstance(aux_states, (list, tuple)):
         aux_states = {k: v for k, v in zip(sym.list_auxiliary_states(), aux_states)}
-    return {k: nd.array(v, ctx=ctx, dtype=dtype) if not isinstance(v, NDArray) else v.as_in_context(ctx)
+    return {k: nd.array(v, ctx=ctx, dtype=_arg_dtype(v, dtype)) if not isinstance(v, NDArray) else v.as_in_context(ctx)
             for k, v in aux_states.items()}
 
 
@@ -484,7 +491,7 @@ def check_symbolic_forward(sym, location, expected, rtol=None, atol=None, aux_st
     aux_states = _parse_aux_states(sym, aux_states, ctx, dtype)
     if isinstance(expected, dict):
         expected = [expected[k] for k in sym.list_outputs()]
-    args_grad_data = {k: nd.empty(v.shape, ctx=ctx, dtype=dtype) for k, v in location.items()}
+    args_grad_data = {k: nd.empty(v.shape, ctx=ctx, dtype=_arg_dtype(v, dtype)) for k, v in location.items()}
     executor = sym.bind(ctx=ctx, args=location, args_grad=args_grad_data, aux_states=aux_states)
     for g in executor.grad_arrays:
         if g is not None:
@@ -505,7 +512,7 @@ def check_symbolic_backward(sym, location, out_grads, expected, rtol=None, atol=
     if isinstance(expected, (list, tuple)):
         expected = {k: v for k, v in zip(sym.list_arguments(), expected)}
     args_grad_npy = {k: np.random.normal(size=v.shape) for k, v in expected.items()}
-    args_grad_data = {k: nd.array(v, ctx=ctx, dtype=dtype) for k, v in args_grad_npy.items()}
+    args_grad_data = {k: nd.array(v, ctx=ctx, dtype=_arg_dtype(location[k], dtype)) for k, v in args_grad_npy.items()}
     if isinstance(grad_req, str):
         grad_req = {k: grad_req for k in sym.list_arguments()}
     elif isinstance(grad_req, (list, tuple)):
@@ -514,9 +521,9 @@ def check_symbolic_backward(sym, location, out_grads, expected, rtol=None, atol=
                         grad_req=grad_req)
     executor.forward(is_train=True)
     if isinstance(out_grads, (tuple, list)):
-        outg = [nd.array(v, ctx=ctx, dtype=dtype) if not isinstance(v, NDArray) else v for v in out_grads]
+        outg = [nd.array(v, ctx=ctx, dtype=_arg_dtype(v, dtype)) if not isinstance(v, NDArray) else v for v in out_grads]
     elif isinstance(out_grads, dict):
-        outg = [nd.array(out_grads[k], ctx=ctx, dtype=dtype) for k in sym.list_outputs()]
+        outg = [nd.array(out_grads[k], ctx=ctx, dtype=_arg_dtype(out_grads[k], dtype)) for k in sym.list_outputs()]
     else:
         outg = out_grads
     executor.backward(outg)
