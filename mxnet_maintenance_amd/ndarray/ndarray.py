@@ -720,7 +720,9 @@ def from_numpy(ndarray, zero_copy=True):
     becomes read-only (as in the reference, which takes ownership of the buffer)."""
     if not zero_copy:
         return NDArray(torch.from_numpy(np.array(ndarray, copy=True)))
-    src = np.ascontiguousarray(ndarray)
+    if not ndarray.flags['C_CONTIGUOUS']:
+        raise ValueError('from_numpy with zero_copy=True needs a C-contiguous array; use zero_copy=False')
+    src = ndarray
     t = torch.from_numpy(src)
     ndarray.flags.writeable = False
     return NDArray(t)
@@ -813,6 +815,10 @@ def concatenate(arrays, axis=0, always_copy=True):
 def moveaxis(tensor, source, destination):
     """Move axes ``source`` to positions ``destination`` (ints or sequences of ints)."""
     def norm(a):
+        axes = tuple(a) if isinstance(a, (list, tuple, range)) else (a,)
+        for ax in axes:
+            if not -tensor.ndim <= ax < tensor.ndim:
+                raise ValueError('moveaxis: axis %d is out of bounds for an array of dimension %d' % (ax, tensor.ndim))
         return tuple(a) if isinstance(a, (list, tuple, range)) else a
     return NDArray(torch.movedim(tensor._data, norm(source), norm(destination)).contiguous())
 

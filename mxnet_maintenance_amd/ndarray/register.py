@@ -50,6 +50,9 @@ def _split_args(op, args, kwargs):
         if isinstance(v, NDArray):
             named_inputs[k] = v
         elif v is None:
+            spec = op.params.get(k)
+            if spec is not None and isinstance(spec[0], str) and spec[0].endswith('?'):
+                attrs[k] = None         # explicit None for an optional parameter (e.g. topk axis=None)
             continue
         else:
             attrs[k] = v

@@ -69,6 +69,9 @@ class OpDef:
         spec = self.params
         for k, v in attrs.items():
             if v is None:
+                s = spec.get(k)
+                if s is not None and isinstance(s[0], str) and s[0].endswith('?'):
+                    out[k] = None       # an optional parameter explicitly set to None
                 continue
             if k.startswith('__') and k.endswith('__'):
                 continue
