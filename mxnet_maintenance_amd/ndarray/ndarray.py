@@ -50,7 +50,7 @@ def _wrap(t):
 
 class NDArray:
     """An n-dimensional array on a :class:`Context`."""
-    __slots__ = ('_data', '_grad', '_grad_req', '_stype', '__weakref__', '_fresh_grad', '_arena')
+    __slots__ = ('_data', '_grad', '_grad_req', '_stype', '__weakref__', '_fresh_grad', '_arena', '_host_ctx')
     __array_priority__ = 1000.0
 
     def __init__(self, data, ctx=None, dtype=None, stype='default'):
@@ -97,6 +97,8 @@ class NDArray:
     @property
     def context(self):
         t = self._data
+        if t.device.type == 'cpu' and getattr(self, '_host_ctx', None) is not None:
+            return self._host_ctx       # cpu_pinned requested on a host without a GPU runtime to pin with
         if t.device.type == 'cpu' and t.is_pinned():
             from ..context import cpu_pinned
             return cpu_pinned(0)
@@ -246,6 +248,13 @@ class NDArray:
     def as_in_context(self, context):
         if self.context == context:
             return self
+        if context.device_typeid == 3:
+            t = self._data.detach().cpu()
+            if torch.cuda.is_available():
+                return NDArray(t.pin_memory())
+            out = NDArray(t.clone() if t.data_ptr() == self._data.data_ptr() else t)
+            out._host_ctx = context
+            return out
         return _invoke_unary(lambda t: t.to(context.torch_device), self)
 
     as_in_ctx = as_in_context
@@ -711,7 +720,12 @@ def array(source_array, ctx=None, dtype=None):
         npd = np.dtype(np_dtype(td)) if td != torch.bfloat16 else np.float32
         t = torch.from_numpy(np.array(source_array, dtype=npd, copy=True))
     if ctx.device_typeid == 3:
-        t = t.pin_memory() if torch.cuda.is_available() else t
+        if torch.cuda.is_available():
+            t = t.pin_memory()
+        else:
+            out = NDArray(t)
+            out._host_ctx = ctx
+            return out
     return NDArray(t.to(ctx.torch_device) if ctx.device_typeid == 2 else t)
 
 

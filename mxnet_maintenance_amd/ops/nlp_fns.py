@@ -285,10 +285,28 @@ def _fc_dgrad_cands(dy2, w):
     return c
 
 
+def _splitk_wgrad(dy2, x2, splits, out, accum):
+    """dW = dY^T X as ``splits`` batched GEMMs over row blocks of M (fp32 partials, so a small N x K
+    output still covers all 256 CUs) summed -- and accumulated into ``out`` when ``accum`` -- by the
+    in-tree slab_reduce kernel."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    slab = torch.empty(splits, N, K, dtype=torch.float32, device=dy2.device)
+    torch.bmm(dy2.view(splits, M // splits, N).transpose(1, 2), x2.view(splits, M // splits, K),
+              out_dtype=torch.float32, out=slab)
+    _K.lib().slab_reduce(_DT[out.dtype], slab.data_ptr(), splits, N * K, out.data_ptr(), int(accum), _stream())
+    return out
+
+
 def _fc_wgrad_cands(dy2, x2, w):
     M, N = dy2.shape
     K = x2.shape[1]
     c = []
+    if (N * K) % 4 == 0 and dy2.is_contiguous() and x2.is_contiguous():
+        for S in (2, 4):
+            if M % S == 0 and (M // S) >= 256:
+                c.append(('sk%d' % S, lambda S=S: _splitk_wgrad(dy2, x2, S, torch.empty(N, K, dtype=w.dtype,
+                                                                                         device=w.device), False)))
     if K % 64 == 0 and N % 64 == 0 and x2.data_ptr() % 16 == 0:
         c.append(('hip', lambda: _KF.conv_wgrad(x2.view(M, 1, 1, K), dy2.view(M, 1, 1, N), (N, 1, 1, K), (1, 1),
                                                 (0, 0)).view(N, K)))
@@ -344,6 +362,8 @@ def _fc_wgrad(dy2, x2, w, w_ref):
         if algo == 'hip':
             _KF.conv_wgrad(x2.view(-1, 1, 1, K), dy2.view(-1, 1, 1, N), (N, 1, 1, K), (1, 1), (0, 0),
                            out=tgt.view(N, 1, 1, K), accum=True)
+        elif algo.startswith('sk'):
+            _splitk_wgrad(dy2, x2, int(algo[2:]), tgt.view(N, K), True)
         else:
             tgt.addmm_(dy2.t(), x2)
         return None

@@ -825,3 +825,20 @@ def test_nchw_network_runs_on_hip_nhwc_kernels():
     np.testing.assert_allclose(o_hip, o_ref, rtol=3e-2, atol=3e-2)
     for a, b in zip(g_hip, g_ref):
         np.testing.assert_allclose(a, b, rtol=5e-2, atol=5e-2 * max(1.0, float(np.abs(b).max())))
+
+
+@pytest.mark.parametrize('splits', [2, 4])
+@pytest.mark.parametrize('nk', [(768, 768), (3072, 768), (96, 40)])
+def test_splitk_fc_wgrad_accumulates_into_grad(splits, nk):
+    _lib()
+    from mxnet_maintenance_amd.ops import nlp_fns
+    N, K = nk
+    M = 1024
+    torch.manual_seed(2)
+    dy = torch.randn(M, N, device='cuda').to(torch.bfloat16)
+    x = torch.randn(M, K, device='cuda').to(torch.bfloat16)
+    g = torch.randn(N, K, device='cuda').to(torch.bfloat16)
+    base = g.float().clone()
+    nlp_fns._splitk_wgrad(dy, x, splits, g, True)
+    ref = base + dy.float().t() @ x.float()
+    torch.testing.assert_close(g.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
