@@ -245,7 +245,7 @@ class Parameter:
     def _reduce(self):
         ctx = cpu()
         if self._stype == 'default':
-            block = self.list_data()
+            block = self._all_data()
             if len(block) > 1:
                 data = nd.add_n(*[w.copyto(ctx) for w in block]) / len(block)
             else:
@@ -332,6 +332,10 @@ class Parameter:
             raise RuntimeError("Cannot return a copy of Parameter '%s' on ctx %s via data() because its storage "
                                "type is %s. Please use row_sparse_data() instead." % (self.name, str(ctx), self._stype))
         return self._check_and_get(self._data, ctx)
+
+    def _all_data(self):
+        """Per-context data arrays whatever the storage type (framework-internal accessor)."""
+        return self._check_and_get(self._data, list)
 
     def list_data(self):
         if self._stype != 'default':

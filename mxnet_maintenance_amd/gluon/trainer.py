@@ -48,7 +48,7 @@ class _Arena:
         self.indices = indices
         self.lr_mult = lr_mult
         self.wd_mult = wd_mult
-        d0 = params[0].list_data()[0]._data
+        d0 = params[0]._all_data()[0]._data
         self.dtype = d0.dtype
         self.device = d0.device
         align = 64   # every parameter starts on a 64-element (>=128 B) boundary
@@ -56,13 +56,13 @@ class _Arena:
         off = 0
         for p in params:
             offs.append(off)
-            off += (p.list_data()[0]._data.numel() + align - 1) // align * align
+            off += (p._all_data()[0]._data.numel() + align - 1) // align * align
         self.numel = off
         self.w = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
         self.g = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
         self.views = []
         for p, off in zip(params, offs):
-            arr = p.list_data()[0]
+            arr = p._all_data()[0]
             t = arr._data
             n = t.numel()
             wv = self.w[off:off + n].view(t.shape)
@@ -247,7 +247,7 @@ class Trainer:
         for i, p in enumerate(self._params):
             if p.grad_req == 'null':
                 continue
-            key = (p.list_data()[0]._data.dtype, float(p.lr_mult), float(p.wd_mult))
+            key = (p._all_data()[0]._data.dtype, float(p.lr_mult), float(p.wd_mult))
             if key not in groups:
                 groups[key] = ([], [])
                 order.append(key)
@@ -279,7 +279,7 @@ class Trainer:
                     # fp32 master visible to kernels that want fp32 parameters (LayerNorm/BN gamma, beta):
                     # valid while the half tensor is only written by the fused update (whose raw-pointer
                     # writes keep its version counter); any torch in-place write invalidates it
-                    t = p.list_data()[0]._data
+                    t = p._all_data()[0]._data
                     t._mxamd_master = (w32v._data, t._version)
                 if kind == 'sgd':
                     mom = NDArray(a.mom[off:off + n].view(shape)) if a.mom is not None else None
@@ -300,7 +300,7 @@ class Trainer:
             reqs = []
             for a in self._arenas:
                 for p in a.params:
-                    arrays.append(p.list_data()[0])
+                    arrays.append(p._all_data()[0])
                     reqs.append(p.grad_req)
             self._buckets = _ArenaBuckets(self._arenas)
 
@@ -403,12 +403,12 @@ class Trainer:
             # a user-registered KVStoreBase: one key per call, like the reference trainer
             for k, v in zip(keys, vals):
                 if self._update_on_kvstore:
-                    self._kvstore.pushpull(k, v, out=self._params[k].list_data(), priority=-k)
+                    self._kvstore.pushpull(k, v, out=self._params[k]._all_data(), priority=-k)
                 else:
                     self._kvstore.pushpull(k, v, priority=-k)
             return
         if self._update_on_kvstore:
-            self._kvstore.pushpull(keys, vals, [p.list_data() for p in self._params if p.grad_req != 'null'])
+            self._kvstore.pushpull(keys, vals, [p._all_data() for p in self._params if p.grad_req != 'null'])
         else:
             self._kvstore.pushpull(keys, vals, vals)
 
@@ -460,7 +460,7 @@ class Trainer:
                             'Parameters with stale gradient' % (param.name, str(data.context)))
             if self._kvstore and self._update_on_kvstore:
                 continue
-            for upd, arr, grad in zip(updates, param.list_data(), param.list_grad()):
+            for upd, arr, grad in zip(updates, param._all_data(), param.list_grad()):
                 if not ignore_stale_grad or arr._fresh_grad:
                     upd.append((i, grad, arr))
                     arr._fresh_grad = False
@@ -560,7 +560,7 @@ class Trainer:
         """
         saved = []
         for p, (off, n, _shape) in zip(a.params, a.views):
-            if p.list_data()[0]._fresh_grad:
+            if p._all_data()[0]._fresh_grad:
                 continue
             for buf in (a.w, a.w32, a.mom, a.mean, a.var):
                 if buf is not None:
@@ -674,7 +674,7 @@ class _ArenaBuckets(GradBuckets):
                     self.buckets.append(cur)
                     cur_hi = off + n
                 cur_lo = off
-                cur.params.append(p.list_data()[0])
+                cur.params.append(p._all_data()[0])
                 cur.count += 1
             if cur is not None:
                 cur.flat = a.g[cur_lo:cur_hi]
