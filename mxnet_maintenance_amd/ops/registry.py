@@ -24,6 +24,23 @@ from ..base import MXNetError
 _OPS = {}
 
 
+_ACCEPTS = {}
+
+
+def _fn_accepts(fn, key):
+    """Whether ``fn`` takes keyword ``key`` (True for functions with ``**kwargs``)."""
+    acc = _ACCEPTS.get(fn)
+    if acc is None:
+        import inspect
+        try:
+            ps = inspect.signature(fn).parameters.values()
+            acc = True if any(p.kind == p.VAR_KEYWORD for p in ps) else frozenset(p.name for p in ps)
+        except (TypeError, ValueError):
+            acc = True
+        _ACCEPTS[fn] = acc
+    return acc is True or key in acc
+
+
 class OpDef:
     __slots__ = ('name', 'fn', 'arg_names', 'aux_names', 'params', 'num_outputs',
                  'infer_params', 'key_var_num_args', 'doc', 'num_visible_outputs',
@@ -77,6 +94,8 @@ class OpDef:
                 continue
             s = spec.get(k)
             if s is None:
+                if not self.extra_params and not _fn_accepts(self.fn, k):
+                    continue        # an attribute the operator does not take is ignored (as by nnvm)
                 out[k] = _auto_parse(v) if isinstance(v, str) else v
             else:
                 out[k] = parse_value(s[0], v)

@@ -253,6 +253,8 @@ def test_arena_bucket_layout_small_tail():
         def list_data(self):
             return [self._t]
 
+        _all_data = list_data
+
     sizes = [3000, 500, 800, 12000, 9000, 7000, 100]
     offs = np.cumsum([0] + sizes[:-1]).tolist()
 
