@@ -528,16 +528,27 @@ __global__ void __launch_bounds__(256) colsum_part_kernel(const T* __restrict__ 
 template <typename TO>
 __global__ void __launch_bounds__(256) colsum_fin_kernel(const float* __restrict__ part, int nchunk, int C,
                                                          TO* __restrict__ out, int accum) {
-  __shared__ float red[4][64];
-  const int col = threadIdx.x & 63, l4 = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + col;
-  float t = 0.f;
-  if (c < C)
-    for (int i = l4; i < nchunk; i += 4) t += part[static_cast<int64_t>(i) * C + c];
-  red[l4][col] = t;
+  // 16 columns x 16 lanes: each lane sums every 16th chunk (4 independent loads in flight per step)
+  __shared__ float red[16][17];
+  const int col = threadIdx.x & 15, l16 = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + col;
+  float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
+  if (c < C) {
+    int i = l16;
+    for (; i + 48 < nchunk; i += 64) {
+      t0 += part[static_cast<int64_t>(i) * C + c];
+      t1 += part[static_cast<int64_t>(i + 16) * C + c];
+      t2 += part[static_cast<int64_t>(i + 32) * C + c];
+      t3 += part[static_cast<int64_t>(i + 48) * C + c];
+    }
+    for (; i < nchunk; i += 16) t0 += part[static_cast<int64_t>(i) * C + c];
+  }
+  red[l16][col] = (t0 + t1) + (t2 + t3);
   __syncthreads();
-  if (l4 == 0 && c < C) {
-    t = red[0][col] + red[1][col] + red[2][col] + red[3][col];
+  if (l16 == 0 && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t += red[j][col];
     if (accum) t += static_cast<float>(out[c]);
     out[c] = static_cast<TO>(t);
   }
@@ -566,7 +577,7 @@ void colsum_rows(int dtype, const void* x, const float* zeros, float* part, int6
   else
     hipLaunchKernelGGL(colsum_part_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(x), R, C,
                        rows_per, part);
-  const dim3 g2((C + 63) / 64);
+  const dim3 g2((C + 15) / 16);
   if (out_dtype == kF16)
     hipLaunchKernelGGL(colsum_fin_kernel<__half>, g2, dim3(256), 0, s, part, nchunk, C, static_cast<__half*>(out),
                        accum);

@@ -184,29 +184,30 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const T* __restrict_
 }
 
 // out[c] (+)= sum_b part[b][c] for the 2*D columns (dgamma then dbeta):
-// 32 columns x 8 row-groups per block, LDS combine of the 8 partial sums
+// 8 columns x 32 row-groups per block (2*768 columns -> 192 blocks: the reduce of the 512 row partials
+// covers the chip instead of 48 blocks), LDS combine of the 32 partial sums
 template <typename TO>
 __global__ void __launch_bounds__(256) column_sum_kernel(const float* __restrict__ part, int nb, int ncol,
                                                          TO* __restrict__ out0, TO* __restrict__ out1, int D,
                                                          int accum) {
-  const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
-  const int col = blockIdx.x * 32 + cl;
+  const int cl = threadIdx.x & 7, grp = threadIdx.x >> 3;
+  const int col = blockIdx.x * 8 + cl;
   float s0 = 0.f, s1 = 0.f;
   if (col < ncol) {
     int b = grp;
-    for (; b + 8 < nb; b += 16) {
+    for (; b + 32 < nb; b += 64) {
       s0 += part[(int64_t)b * ncol + col];
-      s1 += part[(int64_t)(b + 8) * ncol + col];
+      s1 += part[(int64_t)(b + 32) * ncol + col];
     }
     if (b < nb) s0 += part[(int64_t)b * ncol + col];
   }
-  __shared__ float red[8][32];
+  __shared__ float red[32][8];
   red[grp][cl] = s0 + s1;
   __syncthreads();
   if (grp == 0 && col < ncol) {
     float s = 0.f;
 #pragma unroll
-    for (int g = 0; g < 8; ++g) s += red[g][cl];
+    for (int g = 0; g < 32; ++g) s += red[g][cl];
     TO* o = col < D ? out0 + col : out1 + (col - D);
     if (accum) s += static_cast<float>(*o);
     *o = static_cast<TO>(s);
@@ -449,7 +450,7 @@ void layernorm_backward(int dtype, const void* x, const void* dy, const float* g
                                                                      static_cast<const T*>(dy), gamma, mean, rstd,
                                                                      static_cast<T*>(dx), part, M, D)))
   // dgamma / dbeta straight into the parameters' gradient buffers in their own dtype (fp32 / bf16 / fp16)
-  MXAMD_DTYPE_SWITCH(gdtype, hipLaunchKernelGGL((column_sum_kernel<T>), dim3((2 * D + 31) / 32), dim3(256), 0, s,
+  MXAMD_DTYPE_SWITCH(gdtype, hipLaunchKernelGGL((column_sum_kernel<T>), dim3((2 * D + 7) / 8), dim3(256), 0, s,
                                                 part, nb, 2 * D, static_cast<T*>(dgamma), static_cast<T*>(dbeta), D,
                                                 accum))
 }
