@@ -3,6 +3,7 @@ from . import amp  # noqa: F401
 from . import quantization  # noqa: F401
 from . import text  # noqa: F401
 from . import svrg_optimization  # noqa: F401
+from . import autograd  # noqa: F401
 from .. import ndarray as _nd
 from .. import symbol as _sym
 ndarray = _nd.contrib

@@ -92,3 +92,19 @@ def cond(pred, then_func, else_func, name='cond'):
     node = _create('_cond', {'_pos': [pred] + inputs}, attrs, name=name)
     res = list(node)
     return res if t_is_list else res[0]
+
+
+def rand_zipfian(true_classes, num_sampled, range_max):
+    """Symbolic log-uniform (Zipfian) candidate sampler: ``(sampled_classes, expected_count_true,
+    expected_count_sampled)``, P(k) = log((k+2)/(k+1)) / log(range_max+1) (parity:
+    python/mxnet/symbol/contrib.py rand_zipfian; the NDArray twin is ndarray/contrib.py)."""
+    import math
+    log_range = math.log(range_max + 1)
+    rand = _op_func('_random_uniform')(low=0.0, high=log_range, shape=(num_sampled,), dtype='float64')
+    sampled = _op_func('_mod_scalar')(_op_func('Cast')(_op_func('exp')(rand) - 1.0, dtype='int64'),
+                                      scalar=float(range_max))
+
+    def expected_count(classes):
+        c = _op_func('Cast')(classes, dtype='float64')
+        return _op_func('log')((c + 2.0) / (c + 1.0)) / log_range * num_sampled
+    return sampled, expected_count(true_classes), expected_count(sampled)

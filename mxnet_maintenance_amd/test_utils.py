@@ -776,7 +776,7 @@ def chi_square_check(generator, buckets, probs, nsamples=1000000):
     if not isinstance(buckets, list):
         raise ValueError('buckets must be a list')
     samples = np.array(generator(nsamples)).reshape(-1)
-    continuous_dist = isinstance(buckets[0], tuple)
+    continuous_dist = isinstance(buckets[0], (tuple, list))
     if continuous_dist:
         buckets_npy = np.array([b for bucket in buckets for b in bucket])
         sample_bucket_ids = np.searchsorted(buckets_npy, samples, side='right')
