@@ -871,7 +871,17 @@ def _binary_helper(lhs, rhs, bop, sop, rsop=None):
         if rsop is None:
             return _ufunc(rhs, lhs, bop, sop)
         return _ufunc(rhs, lhs, bop, rsop, reverse=True)
-    return {'broadcast_add': lambda a, b: a + b}.get(bop, lambda a, b: None)(lhs, rhs)
+    # two python scalars: the plain scalar result (reference _ufunc_helper's lfn_scalar)
+    import operator
+    fn = {'broadcast_add': operator.add, 'broadcast_sub': operator.sub, 'broadcast_mul': operator.mul,
+          'broadcast_div': operator.truediv, 'broadcast_mod': operator.mod, 'broadcast_power': operator.pow,
+          'broadcast_maximum': max, 'broadcast_minimum': min, 'broadcast_hypot': lambda a, b: (a * a + b * b) ** 0.5,
+          'broadcast_equal': lambda a, b: float(a == b), 'broadcast_not_equal': lambda a, b: float(a != b),
+          'broadcast_greater': lambda a, b: float(a > b), 'broadcast_greater_equal': lambda a, b: float(a >= b),
+          'broadcast_lesser': lambda a, b: float(a < b), 'broadcast_lesser_equal': lambda a, b: float(a <= b)}.get(bop)
+    if fn is None:
+        raise TypeError('%s: at least one operand must be an NDArray' % bop)
+    return fn(lhs, rhs)
 
 
 def add(lhs, rhs):

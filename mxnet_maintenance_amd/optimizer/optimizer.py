@@ -113,6 +113,11 @@ class Optimizer:
         raise NotImplementedError()
 
     def update_multi_precision(self, index, weight, grad, state):
+        if isinstance(index, (list, tuple)):
+            # aggregated call (lists of indices / weights / grads / states): one update per tensor
+            for i, w, g, st in zip(index, weight, grad, state):
+                self.update_multi_precision(i, w, g, st)
+            return
         if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
             weight_master_copy = state[0]
             original_state = state[1]

@@ -835,8 +835,21 @@ def compare_optimizer(opt1, opt2, shape, dtype, w_stype='default', g_stype='defa
             compare_ndarray_tuple(state1, state2, rtol=rtol, atol=atol)
         assert_almost_equal(w1, w2, rtol=rtol, atol=atol)
     else:
+        # ``shape`` is a list of per-tensor shapes: opt1 updates tensor by tensor, opt2 takes the whole
+        # list in one (aggregated / multi-tensor) update call
+        shapes = list(shape)
+        w1 = [rand_ndarray(s, w_stype, dtype=dtype) for s in shapes]
+        g1 = [rand_ndarray(s, g_stype, dtype=dtype) for s in shapes]
+        w2 = [w.copy() for w in w1]
+        g2 = [g.copy() for g in g1]
+        state2 = [opt2.create_state_multi_precision(i, w2[i]) for i in range(ntensors)]
+        opt2.update_multi_precision(list(range(ntensors)), w2, g2, state2)
         for i in range(ntensors):
-            compare_optimizer(opt1, opt2, shape, dtype, w_stype, g_stype, rtol, atol, compare_states, 1)
+            state1 = opt1.create_state_multi_precision(i, w1[i])
+            opt1.update_multi_precision(i, w1[i], g1[i], state1)
+            if compare_states:
+                compare_ndarray_tuple(state1, state2[i], rtol=rtol, atol=atol)
+            assert_almost_equal(w1[i], w2[i], rtol=rtol, atol=atol)
 
 
 def same_symbol_structure(sym1, sym2):
