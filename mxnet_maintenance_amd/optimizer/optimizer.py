@@ -121,7 +121,9 @@ class Optimizer:
         if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
             weight_master_copy = state[0]
             original_state = state[1]
-            grad32 = NDArray(grad._data.float())
+            # sparse gradients keep their storage (lazy row updates need the row indices)
+            grad32 = grad.astype('float32') if getattr(grad, 'stype', 'default') != 'default' \
+                else NDArray(grad._data.float())
             self.update(index, weight_master_copy, grad32, original_state)
             with torch.no_grad():
                 weight._data.copy_(weight_master_copy._data)
