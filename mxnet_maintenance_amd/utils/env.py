@@ -35,6 +35,8 @@ KNOBS = {
                          'zero-copy all-reduce buckets)', ''),
     'MXAMD_DIST_BACKEND': (str, '', 'force torch.distributed backend (gloo for CPU runs); default nccl(=RCCL) on GPU',
                            ''),
+    'MXAMD_VENDOR_MARGIN': (float, 0.05, 'autotuner: a MIOpen / hipBLASLt candidate must beat the fastest in-tree '
+                            'kernel by this fraction to be chosen (near-ties within timing noise go in-tree)', ''),
     'MXAMD_DISABLE_HIP': (int, 0, 'do not load the gfx950 HIP kernel extension (debug only)', ''),
     'MXAMD_ALLOW_TORCH_FALLBACK': (int, 0, 'allow silent torch fallbacks when the HIP extension is missing on a GPU',
                                    ''),
