@@ -145,11 +145,8 @@ def _finish_leaves(leaves):
         g = t.grad
         if g is not None and g is not v._grad._data:
             # create_graph path builds a new tensor instead of accumulating in place
-            if v._grad_req == 'add':
-                v._grad._data = g
-            else:
-                v._grad._data = g
-            t.grad = v._grad._data
+            v._grad._data = g
+            t.grad = g
         v._fresh_grad = True
 
 

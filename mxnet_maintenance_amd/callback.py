@@ -38,13 +38,18 @@ def do_checkpoint(prefix, period=1):
 
     def on_epoch_end(epoch, sym, arg, aux):
         if due(epoch):
-            from .model import save_checkpoint
-            save_checkpoint(prefix, epoch + 1, sym, arg, aux)
+            from . import model as _model
+            _model.save_checkpoint(prefix, epoch + 1, sym, arg, aux)
     return on_epoch_end
 
 
 def _metric_pairs(metric):
     return list(metric.get_name_value()) if metric is not None else []
+
+
+def _reset_window(metric):
+    """Clear the metric's local (per-window) accumulators."""
+    metric.reset_local()
 
 
 def log_train_metric(period, auto_reset=False):
@@ -55,7 +60,7 @@ def log_train_metric(period, auto_reset=False):
         for name, value in _metric_pairs(param.eval_metric):
             logging.info('Iter[%d] Batch[%d] Train-%s=%f', param.epoch, param.nbatch, name, value)
         if auto_reset:
-            param.eval_metric.reset_local()
+            _reset_window(param.eval_metric)
     return on_batch_end
 
 
@@ -68,9 +73,7 @@ class Speedometer:
     """
 
     def __init__(self, batch_size, frequent=50, auto_reset=True):
-        self.batch_size = batch_size
-        self.frequent = frequent
-        self.auto_reset = auto_reset
+        self.batch_size, self.frequent, self.auto_reset = batch_size, frequent, auto_reset
         self._t0 = None
         self._last = -1
 
@@ -107,7 +110,7 @@ class Speedometer:
             text = ''.join('\t%s=%f' % kv for kv in pairs)
             logging.info('Epoch[%d] Batch [%d-%d]\tSpeed: %.2f samples/sec%s', param.epoch, first, n, speed, text)
             if self.auto_reset:
-                param.eval_metric.reset_local()
+                _reset_window(param.eval_metric)
         self._t0 = time.time()
 
 
@@ -129,4 +132,4 @@ class LogValidationMetricsCallback:
 
     def __call__(self, param):
         for name, value in _metric_pairs(param.eval_metric or None):
-            logging.info('Epoch[%d] Validation-%s=%f', param.epoch, name, value)
+            logging.info('Epoch[%d] Validation-%s=%f' % (param.epoch, name, value))

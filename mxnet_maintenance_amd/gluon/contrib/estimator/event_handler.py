@@ -243,6 +243,11 @@ class LoggingHandler(TrainBegin, TrainEnd, EpochBegin, EpochEnd, BatchBegin, Bat
         self.batch_index = 0
 
 
+def _due(period, count):
+    """True when the (count+1)-th event completes a ``period`` (a falsy period never fires)."""
+    return bool(period) and (count + 1) % period == 0
+
+
 class CheckpointHandler(TrainBegin, BatchEnd, EpochEnd):
     """Save ``<prefix>-epoch<E>batch<B>.params/.states`` periodically (keeping the newest
     ``max_checkpoints``), optionally ``<prefix>-best`` by a monitored metric, and resume from the
@@ -276,23 +281,23 @@ class CheckpointHandler(TrainBegin, BatchEnd, EpochEnd):
         if self.save_best:
             self.best = self._better.worst()
         if self.resume_from_checkpoint:
-            self._resume_from_checkpoint(estimator)
+            self._restore_latest(estimator)
 
     def batch_end(self, estimator, *args, **kwargs):
-        if self.batch_period and (self.current_batch + 1) % self.batch_period == 0:
-            self._save_checkpoint(estimator)
+        if _due(self.batch_period, self.current_batch):
+            self._checkpoint_now(estimator)
         self.current_batch += 1
 
     def epoch_end(self, estimator, *args, **kwargs):
-        if self.epoch_period and (self.current_epoch + 1) % self.epoch_period == 0:
-            self._save_checkpoint(estimator)
+        if _due(self.epoch_period, self.current_epoch):
+            self._checkpoint_now(estimator)
         self.current_epoch += 1
 
-    def _save_checkpoint(self, estimator):
+    def _checkpoint_now(self, estimator):
         if self.resume_from_checkpoint and self.current_epoch == 0 and self.current_batch == 0:
             return
         prefix = '%s-epoch%dbatch%d' % (self.model_prefix, self.current_epoch, self.current_batch)
-        self._save_params_and_trainer(estimator, prefix)
+        self._write(estimator, prefix)
         if self.verbose > 0:
             estimator.logger.info('[Epoch %d] CheckpointHandler: trained total %d batches, saving model at %s with '
                                   'prefix: %s', self.current_epoch, self.current_batch + 1, self.model_dir, prefix)
@@ -301,14 +306,14 @@ class CheckpointHandler(TrainBegin, BatchEnd, EpochEnd):
         name, value = _monitor_value(self.monitor)
         if value is not None and self.monitor_op(value, self.best):
             best_prefix = self.model_prefix + '-best'
-            self._save_params_and_trainer(estimator, best_prefix)
+            self._write(estimator, best_prefix)
             if self.verbose > 0:
                 estimator.logger.info('[Epoch %d] CheckpointHandler: %s improved from %0.5f to %0.5f, updating best '
                                       'model at %s with prefix: %s', self.current_epoch, name, self.best, value,
                                       self.model_dir, best_prefix)
             self.best = value
 
-    def _save_params_and_trainer(self, estimator, file_prefix):
+    def _write(self, estimator, file_prefix):
         estimator.net.save_parameters(self._path(file_prefix, '.params'))
         estimator.trainer.save_states(self._path(file_prefix, '.states'))
         if 'best' in file_prefix:
@@ -316,15 +321,17 @@ class CheckpointHandler(TrainBegin, BatchEnd, EpochEnd):
         self.saved_checkpoints.append(file_prefix)
         while len(self.saved_checkpoints) > self.max_checkpoints:
             old = self.saved_checkpoints.pop(0)
-            for fname in os.listdir(self.model_dir):
-                if fname.startswith(old + '.'):
-                    os.remove(os.path.join(self.model_dir, fname))
+            for ext in ('.params', '.states'):
+                stale = self._path(old, ext)
+                if os.path.exists(stale):
+                    os.unlink(stale)
 
-    def _resume_from_checkpoint(self, estimator):
+    def _restore_latest(self, estimator):
         found = []
-        for fname in os.listdir(self.model_dir):
+        head = self.model_prefix + '-epoch'
+        for fname in sorted(os.listdir(self.model_dir)):
             m = self._NAME.match(fname)
-            if m and fname.startswith(self.model_prefix + '-epoch'):
+            if m and fname.startswith(head):
                 found.append(((int(m.group(1)), int(m.group(2))), fname))
         if not found:
             estimator.logger.info('CheckpointHandler: No checkpoint found, training from scratch for %d epochs'

@@ -26,10 +26,10 @@ class Dataset:
     """Random-access collection: implement ``__getitem__`` and ``__len__``."""
 
     def __getitem__(self, idx):
-        raise NotImplementedError
+        raise NotImplementedError('%s does not implement __getitem__' % type(self).__name__)
 
     def __len__(self):
-        raise NotImplementedError
+        raise NotImplementedError('%s does not implement __len__' % type(self).__name__)
 
     # ------------------------------------------------------------ views
     def _view(self, index):
@@ -112,11 +112,11 @@ class _MapView(Dataset):
 
     def __getitem__(self, idx):
         item = self._base[idx]
-        if self._first_only:
-            if isinstance(item, tuple):
-                return (self._fn(item[0]),) + item[1:]
+        if not isinstance(item, tuple):
             return self._fn(item)
-        return self._fn(*item) if isinstance(item, tuple) else self._fn(item)
+        if self._first_only:
+            return (self._fn(item[0]),) + item[1:]
+        return self._fn(*item)
 
 
 class ArrayDataset(Dataset):
@@ -160,20 +160,24 @@ class RecordFileDataset(Dataset):
 
     def __init__(self, filename):
         self.filename = filename
-        self.idx_file = os.path.splitext(filename)[0] + '.idx'
+        stem, _ = os.path.splitext(filename)
+        self.idx_file = stem + '.idx'
         self._open()
 
     def _open(self):
-        self._record = recordio.MXIndexedRecordIO(self.idx_file, self.filename, 'r')
+        self._reader = recordio.MXIndexedRecordIO(self.idx_file, self.filename, 'r')
+        self._keys = list(self._reader.keys)
 
     def __len__(self):
-        return len(self._record.keys)
+        return len(self._keys)
 
     def __getitem__(self, idx):
-        return self._record.read_idx(self._record.keys[idx])
+        return self._reader.read_idx(self._keys[idx])
 
     def __getstate__(self):
-        return {k: v for k, v in self.__dict__.items() if k != '_record'}
+        state = dict(self.__dict__)
+        state.pop('_reader', None)
+        return state
 
     def __setstate__(self, state):
         self.__dict__.update(state)
@@ -201,4 +205,4 @@ class _DownloadedDataset(Dataset):
         return self._transform(*sample) if self._transform is not None else sample
 
     def _get_data(self):
-        raise NotImplementedError
+        raise NotImplementedError('%s must load its files in _get_data()' % type(self).__name__)

@@ -15,13 +15,13 @@ class Sampler:
     """Base class: subclasses define ``_indices()`` (numpy int array) or override ``__iter__``."""
 
     def _indices(self):
-        raise NotImplementedError
+        raise NotImplementedError('%s must define _indices()' % type(self).__name__)
 
     def __iter__(self):
         return iter(self._indices().tolist())
 
     def __len__(self):
-        raise NotImplementedError
+        raise NotImplementedError('%s must define __len__()' % type(self).__name__)
 
 
 class SequentialSampler(Sampler):
@@ -93,34 +93,33 @@ class BatchSampler(Sampler):
 
     def __init__(self, sampler, batch_size, last_batch='keep'):
         self._sampler = sampler
-        self._batch_size = batch_size
-        self._last_batch = last_batch
+        self._bsz = batch_size
+        self._mode = last_batch
         self._carry = []
 
     def _check_mode(self):
-        if self._last_batch not in _LAST_BATCH:
-            raise ValueError('last_batch must be one of %s, got %r' % (_LAST_BATCH, self._last_batch))
+        if self._mode not in _LAST_BATCH:
+            raise ValueError('last_batch must be one of %s, got %r' % (_LAST_BATCH, self._mode))
 
     def __iter__(self):
         self._check_mode()
         pending, self._carry = list(self._carry), []
         for idx in self._sampler:
             pending.append(idx)
-            if len(pending) == self._batch_size:
+            if len(pending) == self._bsz:
                 yield pending
                 pending = []
         if not pending:
             return
-        if self._last_batch == 'keep':
-            yield pending
-        elif self._last_batch == 'rollover':
+        mode = self._mode
+        if mode == 'rollover':
             self._carry = pending
+        elif mode == 'keep':
+            yield pending
 
     def __len__(self):
         self._check_mode()
-        n, b = len(self._sampler), self._batch_size
-        if self._last_batch == 'keep':
-            return -(-n // b)
-        if self._last_batch == 'discard':
-            return n // b
-        return (n + len(self._carry)) // b
+        n, b, mode = len(self._sampler), self._bsz, self._mode
+        if mode == 'rollover':
+            return (n + len(self._carry)) // b
+        return n // b if mode == 'discard' else -(-n // b)

@@ -39,12 +39,16 @@ class BucketingModule(BaseModule):
                                    compression_params=compression_params)
         self._context = self._module_kwargs['context']
         self._buckets = {}
-        self._curr_module = None
-        self._curr_bucket_key = None
-        self._params_dirty = False
+        self._active = None
+        self._active_key = None
+        self._dirty = False
         self._monitor = None
         self._grad_req = None
         self._preload = None
+
+    # reference attribute names (tests and user code reach into these)
+    _curr_module = property(lambda self: self._active)
+    _curr_bucket_key = property(lambda self: self._active_key)
 
     def _call_sym_gen(self, *args, **kwargs):
         return self._sym_gen(*args, **kwargs)
@@ -52,8 +56,8 @@ class BucketingModule(BaseModule):
     def _reset_bind(self):
         self.binded = False
         self._buckets = {}
-        self._curr_module = None
-        self._curr_bucket_key = None
+        self._active = None
+        self._active_key = None
 
     def _new_module(self, key):
         sym, data_names, label_names = self._call_sym_gen(key)
@@ -69,38 +73,38 @@ class BucketingModule(BaseModule):
 
     @property
     def data_names(self):
-        return self._curr_module.data_names if self.binded else self._default_sym_info()[1]
+        return self._active.data_names if self.binded else self._default_sym_info()[1]
 
     @property
     def output_names(self):
-        return self._curr_module.output_names if self.binded else self._default_sym_info()[0].list_outputs()
+        return self._active.output_names if self.binded else self._default_sym_info()[0].list_outputs()
 
     @property
     def data_shapes(self):
         self._require('binded')
-        return self._curr_module.data_shapes
+        return self._active.data_shapes
 
     @property
     def label_shapes(self):
         self._require('binded')
-        return self._curr_module.label_shapes
+        return self._active.label_shapes
 
     @property
     def output_shapes(self):
         self._require('binded')
-        return self._curr_module.output_shapes
+        return self._active.output_shapes
 
     @property
     def symbol(self):
         self._require('binded')
-        return self._curr_module.symbol
+        return self._active.symbol
 
     # ---------------------------------------------------------------- parameters
     def get_params(self):
         self._require('binded', 'params_initialized')
-        self._curr_module._params_dirty = self._params_dirty
-        out = self._curr_module.get_params()
-        self._params_dirty = False
+        self._active._params_dirty = self._dirty
+        out = self._active.get_params()
+        self._dirty = False
         return out
 
     def set_params(self, arg_params, aux_params, allow_missing=False, force_init=True, allow_extra=False):
@@ -112,9 +116,9 @@ class BucketingModule(BaseModule):
             warnings.warn('Parameters already initialized and force_init=False. set_params call ignored.',
                           stacklevel=2)
             return
-        self._curr_module.set_params(arg_params, aux_params, allow_missing=True, force_init=force_init,
+        self._active.set_params(arg_params, aux_params, allow_missing=True, force_init=force_init,
                                      allow_extra=allow_extra)
-        self._params_dirty = True
+        self._dirty = True
         self.params_initialized = True
 
     def init_params(self, initializer=Uniform(0.01), arg_params=None, aux_params=None, allow_missing=False,
@@ -123,18 +127,18 @@ class BucketingModule(BaseModule):
             return
         if not self.binded:
             raise AssertionError('call bind before initializing the parameters')
-        self._curr_module.init_params(initializer=initializer, arg_params=arg_params, aux_params=aux_params,
+        self._active.init_params(initializer=initializer, arg_params=arg_params, aux_params=aux_params,
                                       allow_missing=allow_missing, force_init=force_init, allow_extra=allow_extra)
-        self._params_dirty = False
+        self._dirty = False
         self.params_initialized = True
 
     def get_states(self, merge_multi_context=True):
         self._require('binded', 'params_initialized')
-        return self._curr_module.get_states(merge_multi_context=merge_multi_context)
+        return self._active.get_states(merge_multi_context=merge_multi_context)
 
     def set_states(self, states=None, value=None):
         self._require('binded', 'params_initialized')
-        self._curr_module.set_states(states, value)
+        self._active.set_states(states, value)
 
     # ---------------------------------------------------------------- binding / buckets
     def bind(self, data_shapes, label_shapes=None, for_training=True, inputs_need_grad=False, force_rebind=False,
@@ -153,7 +157,7 @@ class BucketingModule(BaseModule):
         mod.bind(data_shapes, label_shapes, for_training, inputs_need_grad, force_rebind=False, shared_module=None,
                  grad_req=grad_req)
         self._buckets[self._default_bucket_key] = mod
-        self._curr_module, self._curr_bucket_key = mod, self._default_bucket_key
+        self._active, self._active_key = mod, self._default_bucket_key
         if saved is None and self._preload is not None:      # BucketingModule.load()
             saved, self._preload = self._preload, None
             self.params_initialized = True
@@ -172,12 +176,12 @@ class BucketingModule(BaseModule):
                 mod.install_monitor(self._monitor)
         if not mod.binded:
             self._bind_shared(mod, data_shapes, label_shapes)
-        self._curr_module, self._curr_bucket_key = mod, bucket_key
+        self._active, self._active_key = mod, bucket_key
 
     def _bind_shared(self, mod, data_shapes, label_shapes):
         if mod.binded:
             return
-        cur = self._curr_module
+        cur = self._active
         mod.bind(data_shapes, label_shapes, cur.for_training, cur.inputs_need_grad, force_rebind=False,
                  shared_module=self._default_module, grad_req=self._grad_req)
 
@@ -187,45 +191,45 @@ class BucketingModule(BaseModule):
         if self.optimizer_initialized and not force_init:
             self.logger.warning('optimizer already initialized, ignoring.')
             return
-        self._curr_module.init_optimizer(kvstore, optimizer, optimizer_params, force_init=force_init)
+        self._active.init_optimizer(kvstore, optimizer, optimizer_params, force_init=force_init)
         for mod in self._buckets.values():
-            if mod is not self._curr_module:
-                mod.borrow_optimizer(self._curr_module)
+            if mod is not self._active:
+                mod.borrow_optimizer(self._active)
         self.optimizer_initialized = True
 
     # ---------------------------------------------------------------- computation
     def prepare(self, data_batch, sparse_row_id_fn=None):
         self._require('binded', 'params_initialized')
-        home = self._curr_bucket_key
+        home = self._active_key
         self.switch_bucket(data_batch.bucket_key, data_batch.provide_data, data_batch.provide_label)
-        self._curr_module.prepare(data_batch, sparse_row_id_fn=sparse_row_id_fn)
+        self._active.prepare(data_batch, sparse_row_id_fn=sparse_row_id_fn)
         self.switch_bucket(home, None, None)
 
     def forward(self, data_batch, is_train=None):
         self._require('binded', 'params_initialized')
         self.switch_bucket(data_batch.bucket_key, data_batch.provide_data, data_batch.provide_label)
-        self._curr_module.forward(data_batch, is_train=is_train)
+        self._active.forward(data_batch, is_train=is_train)
 
     def backward(self, out_grads=None):
         self._require('binded', 'params_initialized')
-        self._curr_module.backward(out_grads=out_grads)
+        self._active.backward(out_grads=out_grads)
 
     def update(self):
         self._require('binded', 'params_initialized', 'optimizer_initialized')
-        self._params_dirty = True
-        self._curr_module.update()
+        self._dirty = True
+        self._active.update()
 
     def get_outputs(self, merge_multi_context=True):
         self._require('binded', 'params_initialized')
-        return self._curr_module.get_outputs(merge_multi_context=merge_multi_context)
+        return self._active.get_outputs(merge_multi_context=merge_multi_context)
 
     def get_input_grads(self, merge_multi_context=True):
         self._require('binded', 'params_initialized', 'inputs_need_grad')
-        return self._curr_module.get_input_grads(merge_multi_context=merge_multi_context)
+        return self._active.get_input_grads(merge_multi_context=merge_multi_context)
 
     def update_metric(self, eval_metric, labels, pre_sliced=False):
         self._require('binded', 'params_initialized')
-        self._curr_module.update_metric(eval_metric, labels, pre_sliced)
+        self._active.update_metric(eval_metric, labels, pre_sliced)
 
     def install_monitor(self, mon):
         self._require('binded')
@@ -237,7 +241,7 @@ class BucketingModule(BaseModule):
     def save_checkpoint(self, prefix, epoch, remove_amp_cast=False):
         if not (self.binded and self._buckets):
             raise AssertionError('bind before saving a checkpoint')
-        self._curr_module.save_checkpoint(prefix, epoch)
+        self._active.save_checkpoint(prefix, epoch)
 
     @staticmethod
     def load(prefix, epoch, sym_gen=None, default_bucket_key=None, **kwargs):

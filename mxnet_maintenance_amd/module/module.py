@@ -36,6 +36,11 @@ def _names(seq):
 class Module(BaseModule):
     """Symbolic module over one or more contexts (one per process is the MI355X norm)."""
 
+    # reference attribute names (user code and tests reach into these)
+    _exec_group = property(lambda self: self._group)
+    _params_dirty = property(lambda self: self._dirty, lambda self, v: setattr(self, '_dirty', v))
+    _sync_params_from_devices = property(lambda self: self._pull_params)
+
     def __init__(self, symbol, data_names=('data',), label_names=('softmax_label',), logger=logging,
                  context=None, work_load_list=None, fixed_param_names=None, state_names=None, group2ctxs=None,
                  compression_params=None):
@@ -63,12 +68,12 @@ class Module(BaseModule):
         self._output_names = symbol.list_outputs()
 
         self._arg_params = self._aux_params = None
-        self._params_dirty = False
-        self._exec_group = None
+        self._dirty = False
+        self._group = None
         self._data_shapes = self._label_shapes = None
         self._grad_req = None
         self._optimizer = self._kvstore = self._update_on_kvstore = self._updater = None
-        self._preload_opt_states = None
+        self._pending_opt_states = None
 
     # ---------------------------------------------------------------- checkpoints
     @staticmethod
@@ -118,13 +123,13 @@ class Module(BaseModule):
     @property
     def output_shapes(self):
         self._require('binded')
-        return self._exec_group.get_output_shapes()
+        return self._group.get_output_shapes()
 
     # ---------------------------------------------------------------- parameters
     def get_params(self):
         self._require('binded', 'params_initialized')
-        if self._params_dirty:
-            self._sync_params_from_devices()
+        if self._dirty:
+            self._pull_params()
         return self._arg_params, self._aux_params
 
     def init_params(self, initializer=Uniform(0.01), arg_params=None, aux_params=None, allow_missing=False,
@@ -153,8 +158,8 @@ class Module(BaseModule):
             for name in sorted(mine):
                 fill(name, mine[name], given)
         self.params_initialized = True
-        self._params_dirty = False
-        self._exec_group.set_params(self._arg_params, self._aux_params, allow_extra=allow_extra)
+        self._dirty = False
+        self._group.set_params(self._arg_params, self._aux_params, allow_extra=allow_extra)
 
     def set_params(self, arg_params, aux_params, allow_missing=False, force_init=True, allow_extra=False):
         if not allow_missing:
@@ -166,22 +171,22 @@ class Module(BaseModule):
                           stacklevel=2)
             return
         # partial update goes straight to the devices; host dicts are refreshed lazily
-        self._exec_group.set_params(arg_params, aux_params, allow_extra=allow_extra)
-        self._params_dirty = True
+        self._group.set_params(arg_params, aux_params, allow_extra=allow_extra)
+        self._dirty = True
         self.params_initialized = True
 
-    def _sync_params_from_devices(self):
-        self._exec_group.get_params(self._arg_params, self._aux_params)
+    def _pull_params(self):
+        self._group.get_params(self._arg_params, self._aux_params)
         if self._kvstore and self._update_on_kvstore:
             for name, val in sorted(self._arg_params.items()):
                 if val.stype == 'row_sparse':
                     self._kvstore.row_sparse_pull(name, val, row_ids=nd.arange(0, val.shape[0], dtype='int64'))
-        self._params_dirty = False
+        self._dirty = False
 
     # ---------------------------------------------------------------- binding
     def _reset_bind(self):
         self.binded = False
-        self._exec_group = None
+        self._group = None
         self._data_shapes = self._label_shapes = None
 
     def bind(self, data_shapes, label_shapes=None, for_training=True, inputs_need_grad=False, force_rebind=False,
@@ -200,10 +205,10 @@ class Module(BaseModule):
         if shared_module is not None:
             if not (isinstance(shared_module, Module) and shared_module.binded and shared_module.params_initialized):
                 raise AssertionError('shared_module must be a bound, initialised Module')
-            shared_group = shared_module._exec_group
+            shared_group = shared_module._group
             if len(shared_group.execs) < len(self._context):
                 raise AssertionError('shared_module has fewer devices than this module')
-        self._exec_group = DataParallelExecutorGroup(
+        self._group = DataParallelExecutorGroup(
             self._symbol, self._context, self._work_load_list, self._data_shapes, self._label_shapes,
             self._param_names, for_training, inputs_need_grad, shared_group, logger=self.logger,
             fixed_param_names=self._fixed_param_names, grad_req=grad_req, state_names=self._state_names,
@@ -213,9 +218,9 @@ class Module(BaseModule):
             self._arg_params, self._aux_params = shared_module._arg_params, shared_module._aux_params
             self.params_initialized = True
         elif self.params_initialized:
-            self._exec_group.set_params(self._arg_params, self._aux_params)    # loaded before bind
+            self._group.set_params(self._arg_params, self._aux_params)    # loaded before bind
         else:
-            g = self._exec_group
+            g = self._group
             self._arg_params = {n: nd.zeros(a[0].shape, dtype=a[0].dtype)
                                 for n, a in zip(self._param_names, g.param_arrays)}
             self._aux_params = {n: nd.zeros(a[0].shape, dtype=a[0].dtype)
@@ -228,11 +233,11 @@ class Module(BaseModule):
         self._require('binded')
         self._data_shapes, self._label_shapes = _parse_data_desc(self._data_names, self._label_names,
                                                                  data_shapes, label_shapes)
-        self._exec_group.reshape(self._data_shapes, self._label_shapes)
+        self._group.reshape(self._data_shapes, self._label_shapes)
 
     # ---------------------------------------------------------------- optimizer
     def _idx2name(self, update_on_kvstore):
-        names = self._exec_group.param_names
+        names = self._group.param_names
         if update_on_kvstore:
             return dict(enumerate(names))
         ndev = len(self._context)
@@ -244,10 +249,10 @@ class Module(BaseModule):
         if self.optimizer_initialized and not force_init:
             self.logger.warning('optimizer already initialized, ignoring...')
             return
-        if self._params_dirty:
-            self._sync_params_from_devices()
+        if self._dirty:
+            self._pull_params()
         kv, on_kv = _create_kvstore(kvstore, len(self._context), self._arg_params)
-        batch = self._exec_group.batch_size
+        batch = self._group.batch_size
         if kv and 'dist' in kv.type and '_sync' in kv.type:
             batch *= kv.num_workers
         rescale = 1.0 / batch
@@ -271,14 +276,14 @@ class Module(BaseModule):
                 kv.set_gradient_compression(self._compression_params)
             if on_kv:
                 kv.set_optimizer(self._optimizer)
-            _initialize_kvstore(kvstore=kv, param_arrays=self._exec_group.param_arrays, arg_params=self._arg_params,
+            _initialize_kvstore(kvstore=kv, param_arrays=self._group.param_arrays, arg_params=self._arg_params,
                                 param_names=self._param_names, update_on_kvstore=on_kv)
         if not on_kv:
             self._updater = opt.get_updater(optimizer)
         self.optimizer_initialized = True
-        if self._preload_opt_states is not None:
-            self.load_optimizer_states(self._preload_opt_states)
-            self._preload_opt_states = None
+        if self._pending_opt_states is not None:
+            self.load_optimizer_states(self._pending_opt_states)
+            self._pending_opt_states = None
 
     def borrow_optimizer(self, shared_module):
         """Use ``shared_module``'s optimizer / kvstore / updater (bucketing)."""
@@ -325,16 +330,16 @@ class Module(BaseModule):
         new = self._batch_descs(data_batch)
         if new is not None:
             self.reshape(*new)
-        self._exec_group.forward(data_batch, is_train)
+        self._group.forward(data_batch, is_train)
 
     def backward(self, out_grads=None):
         self._require('binded', 'params_initialized')
-        self._exec_group.backward(out_grads=out_grads)
+        self._group.backward(out_grads=out_grads)
 
     def update(self):
         self._require('binded', 'params_initialized', 'optimizer_initialized')
-        self._params_dirty = True
-        g = self._exec_group
+        self._dirty = True
+        g = self._group
         if self._update_on_kvstore:
             _update_params_on_kvstore(g.param_arrays, g.grad_arrays, self._kvstore, g.param_names)
         else:
@@ -343,26 +348,26 @@ class Module(BaseModule):
 
     def get_outputs(self, merge_multi_context=True):
         self._require('binded', 'params_initialized')
-        return self._exec_group.get_outputs(merge_multi_context=merge_multi_context)
+        return self._group.get_outputs(merge_multi_context=merge_multi_context)
 
     def get_input_grads(self, merge_multi_context=True):
         self._require('binded', 'params_initialized', 'inputs_need_grad')
-        return self._exec_group.get_input_grads(merge_multi_context=merge_multi_context)
+        return self._group.get_input_grads(merge_multi_context=merge_multi_context)
 
     def get_states(self, merge_multi_context=True):
         self._require('binded', 'params_initialized')
-        return self._exec_group.get_states(merge_multi_context=merge_multi_context)
+        return self._group.get_states(merge_multi_context=merge_multi_context)
 
     def set_states(self, states=None, value=None):
         self._require('binded', 'params_initialized')
-        self._exec_group.set_states(states, value)
+        self._group.set_states(states, value)
 
     def update_metric(self, eval_metric, labels, pre_sliced=False):
-        self._exec_group.update_metric(eval_metric, labels, pre_sliced)
+        self._group.update_metric(eval_metric, labels, pre_sliced)
 
     def install_monitor(self, mon):
         self._require('binded')
-        self._exec_group.install_monitor(mon)
+        self._group.install_monitor(mon)
 
     def prepare(self, data_batch, sparse_row_id_fn=None):
         """Pull the rows a batch needs of row-sparse parameters kept on the kvstore."""
@@ -376,7 +381,7 @@ class Module(BaseModule):
         rows = sparse_row_id_fn(data_batch)
         if not isinstance(rows, dict):
             raise AssertionError('sparse_row_id_fn must return {param_name: row_ids}')
-        g = self._exec_group
+        g = self._group
         for name, row_id in rows.items():
             idx = g.param_names.index(name)
             per_dev = g.param_arrays[idx]

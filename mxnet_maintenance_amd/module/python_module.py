@@ -24,7 +24,7 @@ class PythonModule(BaseModule):
         super().__init__(logger=logger)
         self._data_names = _listify(data_names)
         self._label_names = _listify(label_names)
-        self._output_names = output_names
+        self._output_names = list(output_names)
         self._shapes = {'data': None, 'label': None, 'output': None}
 
     data_names = property(lambda self: self._data_names)
@@ -62,7 +62,7 @@ class PythonModule(BaseModule):
     def bind(self, data_shapes, label_shapes=None, for_training=True, inputs_need_grad=False, force_rebind=False,
              shared_module=None, grad_req='write'):
         if self.binded and not force_rebind:
-            self.logger.warning('Already bound, ignoring bind()')
+            self.logger.warning('%s is already bound; bind() ignored', type(self).__name__)
             return
         if grad_req != 'write':
             raise AssertionError('PythonModule supports grad_req="write" only')
@@ -71,8 +71,7 @@ class PythonModule(BaseModule):
         if label_shapes is not None and (self._label_names is None or
                                          [d[0] for d in label_shapes] != list(self._label_names)):
             raise AssertionError('label_shapes %s do not match label_names %s' % (label_shapes, self._label_names))
-        self.for_training = for_training
-        self.inputs_need_grad = inputs_need_grad
+        self.for_training, self.inputs_need_grad = for_training, inputs_need_grad
         self._shapes['data'] = data_shapes
         self._shapes['label'] = label_shapes
         self._shapes['output'] = self._compute_output_shapes()
@@ -93,20 +92,21 @@ class PythonLossModule(PythonModule):
         super().__init__(data_names, label_names, [name + '_output'], logger=logger)
         self._name = name
         self._grad_func = grad_func
-        self._scores = self._labels = self._scores_grad = None
+        self._pred = self._label_val = self._pred_grad = None
 
     def _compute_output_shapes(self):
         return [(self._name + '_output', self._shapes['data'][0][1])]
 
     def forward(self, data_batch, is_train=None):
-        self._scores = data_batch.data[0]
-        if self.for_training if is_train is None else is_train:
-            self._labels = data_batch.label[0]
+        train = self.for_training if is_train is None else is_train
+        self._pred = data_batch.data[0]
+        if train:
+            self._label_val = data_batch.label[0]
 
     def get_outputs(self, merge_multi_context=True):
         if not merge_multi_context:
             raise AssertionError('PythonLossModule has a single context')
-        return [self._scores]
+        return [self._pred]
 
     def backward(self, out_grads=None):
         if out_grads is not None:
@@ -118,13 +118,13 @@ class PythonLossModule(PythonModule):
     def _backward_impl(self):
         if self._grad_func is None:
             raise NotImplementedError('PythonLossModule needs grad_func (or override _backward_impl)')
-        g = self._grad_func(self._scores, self._labels)
-        self._scores_grad = g if isinstance(g, nd.NDArray) else nd.array(g)
+        g = self._grad_func(self._pred, self._label_val)
+        self._pred_grad = g if isinstance(g, nd.NDArray) else nd.array(g)
 
     def get_input_grads(self, merge_multi_context=True):
         if not merge_multi_context:
             raise AssertionError('PythonLossModule has a single context')
-        return [self._scores_grad]
+        return [self._pred_grad] if self._pred_grad is not None else [None]
 
     def install_monitor(self, mon):
         raise NotImplementedError('PythonLossModule has no executor to monitor')
