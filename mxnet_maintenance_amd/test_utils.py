@@ -122,32 +122,34 @@ def random_arrays(*shapes):
 
 
 def random_uniform_arrays(*shapes, **kwargs):
-    low = kwargs.pop('low', 0.0)
-    high = kwargs.pop('high', 1.0)
-    dtype = kwargs.pop('dtype', default_dtype())
-    arrays = [np.random.uniform(low, high, size=s).astype(dtype) for s in shapes]
-    return arrays
+    """Uniform [low, high) numpy arrays (keyword args ``low``, ``high``, ``dtype``)."""
+    lo, hi = kwargs.pop('low', 0.0), kwargs.pop('high', 1.0)
+    out_dtype = kwargs.pop('dtype', default_dtype())
+    return [np.random.uniform(lo, hi, size=s).astype(out_dtype) for s in shapes]
 
 
 def random_sample(population, k):
-    population_copy = population[:]
-    np.random.shuffle(population_copy)
-    return population_copy[0:k]
+    """``k`` distinct elements of ``population`` in random order."""
+    picked = list(population)
+    np.random.shuffle(picked)
+    return picked[:k]
+
+
+def _rand_dims(limits, allow_zero_size):
+    first = 0 if allow_zero_size else 1
+    return tuple(int(np.random.randint(first, d + 1)) for d in limits)
 
 
 def rand_shape_2d(dim0=10, dim1=10, allow_zero_size=False):
-    low = 0 if allow_zero_size else 1
-    return np.random.randint(low, dim0 + 1), np.random.randint(low, dim1 + 1)
+    return _rand_dims((dim0, dim1), allow_zero_size)
 
 
 def rand_shape_3d(dim0=10, dim1=10, dim2=10, allow_zero_size=False):
-    low = 0 if allow_zero_size else 1
-    return np.random.randint(low, dim0 + 1), np.random.randint(low, dim1 + 1), np.random.randint(low, dim2 + 1)
+    return _rand_dims((dim0, dim1, dim2), allow_zero_size)
 
 
 def rand_shape_nd(num_dim, dim=10, allow_zero_size=False):
-    low = 0 if allow_zero_size else 1
-    return tuple(np.random.randint(low, dim + 1, size=num_dim))
+    return _rand_dims((dim,) * num_dim, allow_zero_size)
 
 
 def rand_coord_2d(x_low, x_high, y_low, y_high):
@@ -231,28 +233,25 @@ def create_sparse_array(shape, stype, data_init=None, rsp_indices=None, dtype=No
 
 
 def np_reduce(dat, axis, keepdims, numpy_reduce_func):
-    if isinstance(axis, int):
-        axis = [axis]
+    """Apply a single-axis numpy reduction over several axes (highest axis first)."""
+    if axis is None:
+        axes = list(range(dat.ndim))
     else:
-        axis = list(axis) if axis is not None else range(len(dat.shape))
-    ret = dat
-    for i in reversed(sorted(axis)):
-        ret = numpy_reduce_func(ret, axis=i)
-    if keepdims:
-        keepdims_shape = list(dat.shape)
-        for i in axis:
-            keepdims_shape[i] = 1
-        ret = ret.reshape(tuple(keepdims_shape))
-    return ret
+        axes = [a % max(dat.ndim, 1) for a in ([axis] if isinstance(axis, int) else axis)]
+    out = dat
+    for ax in sorted(axes, reverse=True):
+        out = numpy_reduce_func(out, axis=ax)
+    if not keepdims:
+        return out
+    kept = [1 if d in axes else n for d, n in enumerate(dat.shape)]
+    return out.reshape(kept)
 
 
 def _find_max_violation(a, b, rtol, atol):
-    diff = np.abs(a - b)
-    tol = atol + rtol * np.abs(b)
-    violation = diff / (tol + 1e-20)
-    loc = np.argmax(violation)
-    idx = np.unravel_index(loc, violation.shape)
-    return idx, np.max(violation)
+    """(index, ratio) of the element whose |a-b| most exceeds atol + rtol*|b|."""
+    ratio = np.abs(a - b) / (atol + rtol * np.abs(b) + 1e-20)
+    flat = int(np.argmax(ratio))
+    return np.unravel_index(flat, ratio.shape), ratio.reshape(-1)[flat]
 
 
 def same(a, b):
@@ -365,63 +364,64 @@ def _arg_dtype(v, dtype):
     return dtype
 
 
+def _named_inputs(names, given, what):
+    """Map ``given`` (dict, or a sequence in ``names`` order) to a dict keyed by ``names``."""
+    if isinstance(given, dict):
+        if set(given) != set(names):
+            raise ValueError('%s names %s do not match the symbol\'s %s' % (what, sorted(given), sorted(names)))
+        return dict(given)
+    return dict(zip(names, given))
+
+
+def _to_ctx(v, ctx, dtype):
+    if isinstance(v, NDArray):
+        return v.as_in_context(ctx)
+    return nd.array(v, ctx=ctx, dtype=_arg_dtype(v, dtype) if not hasattr(v, 'dtype') else v.dtype)
+
+
 def _parse_location(sym, location, ctx, dtype=default_dtype()):
-    if isinstance(location, dict):
-        if set(location.keys()) != set(sym.list_arguments()):
-            raise ValueError('Symbol arguments and keys of the given location do not match. symbol args:%s, '
-                             'location.keys():%s' % (str(set(sym.list_arguments())), str(set(location.keys()))))
-    else:
-        location = {k: v for k, v in zip(sym.list_arguments(), location)}
-    return {k: v.as_in_context(ctx) if isinstance(v, NDArray) else nd.array(v, ctx=ctx, dtype=v.dtype
-                                                                               if hasattr(v, 'dtype') else dtype)
-            for k, v in location.items()}
+    named = _named_inputs(sym.list_arguments(), location, 'location')
+    return {k: _to_ctx(v, ctx, dtype) for k, v in named.items()}
 
 
 def _parse_aux_states(sym, aux_states, ctx, dtype=default_dtype()):
     if aux_states is None:
         return None
-    if isinstance(aux_states, dict):
-        if set(aux_states.keys()) != set(sym.list_auxiliary_states()):
-            raise ValueError('Symbol aux_states names and given aux_states do not match.')
-    elif isinstance(aux_states, (list, tuple)):
-        aux_states = {k: v for k, v in zip(sym.list_auxiliary_states(), aux_states)}
-    return {k: nd.array(v, ctx=ctx, dtype=_arg_dtype(v, dtype)) if not isinstance(v, NDArray) else v.as_in_context(ctx)
-            for k, v in aux_states.items()}
+    named = _named_inputs(sym.list_auxiliary_states(), aux_states, 'aux_states')
+    return {k: _to_ctx(v, ctx, dtype) for k, v in named.items()}
 
 
 def numeric_grad(executor, location, aux_states=None, eps=1e-4, use_forward_train=True, dtype=default_dtype()):
     """Central finite differences of sum(outputs) w.r.t. every input in ``location``."""
-    def as_stype(v):
-        return v
-    approx_grads = {k: np.zeros(v.shape, dtype=dtype) for k, v in location.items()}
-    for k, v in location.items():
-        executor.arg_dict[k][:] = v
-    if aux_states is not None:
-        for k, v in aux_states.items():
-            executor.aux_dict[k][:] = v
-    for k, v in location.items():
-        old_value = _np(v).astype(np.float64).copy()
-        flat = old_value.reshape(-1)
+    def load_aux():
+        for name, val in (aux_states or {}).items():
+            executor.aux_dict[name][:] = val
+
+    def total_output(point, name):
+        executor.arg_dict[name][:] = nd.array(point.astype(dtype), dtype=dtype)
+        load_aux()
+        executor.forward(is_train=use_forward_train)
+        return sum(float(o.asnumpy().astype(np.float64).sum()) for o in executor.outputs)
+
+    for name, val in location.items():
+        executor.arg_dict[name][:] = val
+    load_aux()
+    grads = {}
+    for name, val in location.items():
+        point = _np(val).astype(np.float64).copy()
+        flat = point.reshape(-1)
+        g = np.zeros(flat.size, dtype=dtype)
         for i in range(flat.size):
-            orig = flat[i]
-            flat[i] = orig + eps / 2.0
-            executor.arg_dict[k][:] = nd.array(old_value.astype(dtype), dtype=dtype)
-            if aux_states is not None:
-                for key, val in aux_states.items():
-                    executor.aux_dict[key][:] = val
-            executor.forward(is_train=use_forward_train)
-            f_peps = sum(float(o.asnumpy().astype(np.float64).sum()) for o in executor.outputs)
-            flat[i] = orig - eps / 2.0
-            executor.arg_dict[k][:] = nd.array(old_value.astype(dtype), dtype=dtype)
-            if aux_states is not None:
-                for key, val in aux_states.items():
-                    executor.aux_dict[key][:] = val
-            executor.forward(is_train=use_forward_train)
-            f_neps = sum(float(o.asnumpy().astype(np.float64).sum()) for o in executor.outputs)
-            approx_grads[k].reshape(-1)[i] = (f_peps - f_neps) / eps
-            flat[i] = orig
-        executor.arg_dict[k][:] = nd.array(old_value.astype(dtype), dtype=dtype)
-    return approx_grads
+            x0 = flat[i]
+            flat[i] = x0 + eps / 2.0
+            up = total_output(point, name)
+            flat[i] = x0 - eps / 2.0
+            down = total_output(point, name)
+            flat[i] = x0
+            g[i] = (up - down) / eps
+        executor.arg_dict[name][:] = nd.array(point.astype(dtype), dtype=dtype)
+        grads[name] = g.reshape(point.shape)
+    return grads
 
 
 def check_numeric_gradient(sym, location, aux_states=None, numeric_eps=None, rtol=None, atol=None,
@@ -436,17 +436,13 @@ def check_numeric_gradient(sym, location, aux_states=None, numeric_eps=None, rto
     location_npy = {k: v.asnumpy() for k, v in location.items()}
     aux_states = _parse_aux_states(sym, aux_states, ctx, dtype)
     aux_npy = {k: v.asnumpy() for k, v in aux_states.items()} if aux_states is not None else None
-    if grad_nodes is None:
-        grad_nodes = sym.list_arguments()
-        grad_req = {k: 'write' for k in grad_nodes}
-    elif isinstance(grad_nodes, (list, tuple)):
-        grad_nodes = list(grad_nodes)
-        grad_req = {k: 'write' for k in grad_nodes}
-    elif isinstance(grad_nodes, dict):
-        grad_req = grad_nodes.copy()
-        grad_nodes = grad_nodes.keys()
+    if isinstance(grad_nodes, dict):
+        grad_req = dict(grad_nodes)
+    elif grad_nodes is None or isinstance(grad_nodes, (list, tuple)):
+        grad_req = dict.fromkeys(sym.list_arguments() if grad_nodes is None else grad_nodes, 'write')
     else:
-        raise ValueError
+        raise ValueError('grad_nodes must be None, a list of names or a dict of grad_req')
+    grad_nodes = list(grad_req)
     input_shape = {k: v.shape for k, v in location.items()}
     _, out_shape, _ = sym.infer_shape(**input_shape)
     proj = sym_mod.var('__random_proj')
@@ -470,18 +466,13 @@ def check_numeric_gradient(sym, location, aux_states=None, numeric_eps=None, rto
         '__random_proj': location['__random_proj'].asnumpy()}, aux_npy, eps=eps,
         use_forward_train=use_forward_train, dtype=dtype)
     for name in grad_nodes:
-        fd_grad = numeric_gradients[name]
-        orig_grad = args_grad_npy[name]
-        sym_grad = symbolic_grads[name]
-        if grad_req[name] == 'write':
-            assert_almost_equal(fd_grad, sym_grad, rtol, atol, ('NUMERICAL_%s' % name, 'BACKWARD_%s' % name))
-        elif grad_req[name] == 'add':
-            assert_almost_equal(fd_grad, sym_grad - orig_grad, rtol, atol,
-                                ('NUMERICAL_%s' % name, 'BACKWARD_%s' % name))
-        elif grad_req[name] == 'null':
-            assert_almost_equal(orig_grad, sym_grad, rtol, atol, ('NUMERICAL_%s' % name, 'BACKWARD_%s' % name))
-        else:
-            raise ValueError('Invalid grad_req %s for argument %s' % (grad_req[name], name))
+        req, labels = grad_req[name], ('NUMERICAL_%s' % name, 'BACKWARD_%s' % name)
+        if req not in ('write', 'add', 'null'):
+            raise ValueError('Invalid grad_req %s for argument %s' % (req, name))
+        got, before = symbolic_grads[name], args_grad_npy[name]
+        # 'write' overwrites, 'add' accumulates onto the random initial buffer, 'null' leaves it untouched
+        want = before if req == 'null' else numeric_gradients[name]
+        assert_almost_equal(want, got - before if req == 'add' else got, rtol, atol, labels)
 
 
 def check_symbolic_forward(sym, location, expected, rtol=None, atol=None, aux_states=None, ctx=None,
