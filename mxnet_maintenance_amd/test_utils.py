@@ -699,25 +699,26 @@ def get_mnist_iterator(batch_size, input_shape, num_parts=1, part_index=0):
 
 def same_array(array1, array2):
     """True when two NDArrays share memory (writing one changes the other)."""
+    probe = array2.asnumpy()
     array1[:] += 1
-    if not same(array1.asnumpy(), array2.asnumpy()):
-        array1[:] -= 1
-        return False
+    moved = not same(probe, array2.asnumpy())
     array1[:] -= 1
-    return same(array1.asnumpy(), array2.asnumpy())
+    return moved and same(array1.asnumpy(), array2.asnumpy())
 
 
 @contextmanager
 def discard_stderr():
+    """Silence file-descriptor-level stderr (native libraries included) inside the block."""
+    fd = sys.stderr.fileno()
+    saved = os.dup(fd)
+    sink = os.open(os.devnull, os.O_WRONLY)
     try:
-        stderr_fileno = sys.stderr.fileno()
-        old_stderr = os.dup(stderr_fileno)
-        bit_bucket = open(os.devnull, 'w')
-        os.dup2(bit_bucket.fileno(), stderr_fileno)
+        os.dup2(sink, fd)
         yield
     finally:
-        os.dup2(old_stderr, stderr_fileno)
-        bit_bucket.close()
+        os.dup2(saved, fd)
+        os.close(sink)
+        os.close(saved)
 
 
 class DummyIter:
@@ -742,23 +743,27 @@ class DummyIter:
 
 
 def gen_buckets_probs_with_ppf(ppf, nbuckets):
+    """``nbuckets`` equal-probability intervals of a distribution given its inverse CDF."""
     assert nbuckets > 0
-    probs = [1.0 / nbuckets for _ in range(nbuckets)]
-    buckets = [(ppf(i / float(nbuckets)), ppf((i + 1) / float(nbuckets))) for i in range(nbuckets)]
-    return buckets, probs
+    edges = [ppf(q) for q in np.linspace(0.0, 1.0, nbuckets + 1)]
+    return list(zip(edges[:-1], edges[1:])), [1.0 / nbuckets] * nbuckets
+
+
+def _within(value, centre, half_width):
+    return centre - half_width < value < centre + half_width
 
 
 def mean_check(generator, mu, sigma, nsamples=1000000):
-    samples = np.array(generator(nsamples))
-    sample_mean = samples.mean()
-    return (sample_mean > mu - 3 * sigma / np.sqrt(nsamples)) and (sample_mean < mu + 3 * sigma / np.sqrt(nsamples))
+    """Sample mean within 3 standard errors of ``mu``."""
+    draws = np.asarray(generator(nsamples), dtype=np.float64)
+    return _within(draws.mean(), mu, 3.0 * sigma / np.sqrt(nsamples))
 
 
 def var_check(generator, sigma, nsamples=1000000):
-    samples = np.array(generator(nsamples))
-    sample_var = samples.var(ddof=1)
-    return (sample_var > sigma ** 2 - 3 * np.sqrt(2 * sigma ** 4 / (nsamples - 1))) and \
-        (sample_var < sigma ** 2 + 3 * np.sqrt(2 * sigma ** 4 / (nsamples - 1)))
+    """Unbiased sample variance within 3 standard errors of ``sigma**2`` (normal-theory SE)."""
+    draws = np.asarray(generator(nsamples), dtype=np.float64)
+    se = np.sqrt(2.0 * sigma ** 4 / (nsamples - 1))
+    return _within(draws.var(ddof=1), sigma ** 2, 3.0 * se)
 
 
 def chi_square_check(generator, buckets, probs, nsamples=1000000):
@@ -782,30 +787,25 @@ def chi_square_check(generator, buckets, probs, nsamples=1000000):
 
 
 def verify_generator(generator, buckets, probs, nsamples=1000000, nrepeat=5, success_rate=0.2, alpha=0.05):
-    cs_ret_l = []
-    obs_freq_l = []
-    expected_freq_l = []
-    for _ in range(nrepeat):
-        cs_ret, obs_freq, expected_freq = chi_square_check(generator=generator, buckets=buckets, probs=probs,
-                                                           nsamples=nsamples)
-        cs_ret_l.append(cs_ret)
-        obs_freq_l.append(obs_freq)
-        expected_freq_l.append(expected_freq)
-    success_num = (np.array(cs_ret_l) > alpha).sum()
-    if success_num < nrepeat * success_rate:
+    """Repeat the chi-square test; pass when at least ``success_rate`` of the p-values exceed ``alpha``."""
+    runs = [chi_square_check(generator=generator, buckets=buckets, probs=probs, nsamples=nsamples)
+            for _ in range(nrepeat)]
+    pvals = [r[0] for r in runs]
+    if sum(p > alpha for p in pvals) < nrepeat * success_rate:
         raise AssertionError('Generator test fails, Chi-square p=%s, obs_freq=%s, expected_freq=%s.'
-                             % (str(cs_ret_l), str(obs_freq_l), str(expected_freq_l)))
-    return cs_ret_l
+                             % (pvals, [r[1] for r in runs], [r[2] for r in runs]))
+    return pvals
 
 
 def compare_ndarray_tuple(t1, t2, rtol=None, atol=None):
+    """Compare (possibly nested tuples of) optimizer states; ``None`` on either side is skipped."""
     if t1 is None or t2 is None:
         return
-    if isinstance(t1, tuple):
-        for s1, s2 in zip(t1, t2):
-            compare_ndarray_tuple(s1, s2, rtol, atol)
-    else:
+    if not isinstance(t1, tuple):
         assert_almost_equal(t1, t2, rtol=rtol, atol=atol)
+        return
+    for pair in zip(t1, t2):
+        compare_ndarray_tuple(*pair, rtol=rtol, atol=atol)
 
 
 def compare_optimizer(opt1, opt2, shape, dtype, w_stype='default', g_stype='default', rtol=1e-4, atol=1e-5,
@@ -881,18 +881,17 @@ def environment(*args):
 
 
 def collapse_sum_like(a, shape):
-    assert len(a.shape) >= len(shape)
-    if np.prod(shape) == 0 or a.size == 0:
+    """Sum ``a`` down to a broadcast-compatible ``shape`` (the gradient of broadcasting)."""
+    lead = a.ndim - len(shape)
+    assert lead >= 0
+    if a.size == 0 or int(np.prod(shape)) == 0:
         return np.zeros(shape, dtype=a.dtype)
-    axes = []
-    ndim_diff = len(a.shape) - len(shape)
-    for i in range(ndim_diff):
-        axes.append(i)
-    for i, s in enumerate(shape):
-        if s != a.shape[i + ndim_diff]:
-            assert s == 1
-            axes.append(i + ndim_diff)
-    return np.sum(a, axis=tuple(axes)).reshape(shape)
+    reduce_axes = list(range(lead))
+    for i, n in enumerate(shape):
+        if n != a.shape[lead + i]:
+            assert n == 1, 'shape %s is not broadcast-compatible with %s' % (shape, a.shape)
+            reduce_axes.append(lead + i)
+    return a.sum(axis=tuple(reduce_axes)).reshape(shape)
 
 
 def is_op_runnable():
