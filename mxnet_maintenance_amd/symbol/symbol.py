@@ -540,6 +540,7 @@ def _create(op_name, inputs, attrs, name=None, attr=None):
     # variables created for missing inputs, like nnvm's Compose does for the op's auto-named arguments
     var_attrs = {(k if k.startswith('__') and k.endswith('__') else '__%s__' % k): v
                  for k, v in (scope_attr or {}).items()}
+    default_init = _COMPOSE_VAR_INIT.get(op.name, {})
     for i, an in enumerate(all_names):
         s = None
         if i < len(pos):
@@ -553,11 +554,24 @@ def _create(op_name, inputs, attrs, name=None, attr=None):
             if len(s._outputs) != 1:
                 raise MXNetError('Cannot compose a grouped symbol as input %s of %s' % (an, name))
             entries.append(s._outputs[0])
+        src = entries[-1][0]
+        if i in default_init and src.is_var() and '__init__' not in src.attrs:
+            src.attrs['__init__'] = default_init[i]
     for s in pos[len(all_names):]:
         entries.append(s._outputs[0])
     node.inputs = entries
     nvis = node.num_visible_outputs()
     return Symbol([(node, i) for i in range(nvis)])
+
+
+# Initializers that operators give their input variables at compose time when the variable has none
+# (nnvm FSetInputVarAttrOnCompose; reference src/operator/leaky_relu.cc:203, nn/batch_norm.cc:668,
+# nn/upsampling.cc:205): PReLU slope 0.25, BatchNorm moving mean 0 / moving var 1, bilinear upsampling kernel.
+_COMPOSE_VAR_INIT = {
+    'LeakyReLU': {1: '["Constant", {"value": 0.25}]'},
+    'BatchNorm': {3: '["zero", {}]', 4: '["one", {}]'},
+    'UpSampling': {1: '["bilinear", {}]'},
+}
 
 
 def _op_func(op_name):
