@@ -155,6 +155,16 @@ def create(metric, *args, **kwargs):
         return metric(*args, **kwargs)
     if callable(metric):
         return CustomMetric(metric, *args, **kwargs)
+    if isinstance(metric, dict) or (isinstance(metric, str) and metric.lstrip()[:1] in ('{', '[')):
+        # serialised form: get_config() (dict or JSON) {"metric": name, ...}, or JSON [name, {kwargs}]
+        import json
+        cfg = metric if isinstance(metric, dict) else json.loads(metric)
+        if isinstance(cfg, list):
+            name, extra = cfg[0], (cfg[1] if len(cfg) > 1 else {})
+        else:
+            extra = dict(cfg)
+            name = extra.pop('metric')
+        return create(name, *args, **dict(extra, **kwargs))
     try:
         return _METRICS[metric.lower()](*args, **kwargs)
     except KeyError:
