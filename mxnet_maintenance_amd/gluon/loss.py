@@ -189,7 +189,8 @@ class CTCLoss(Loss):
     def hybrid_forward(self, F, pred, label, pred_lengths=None, label_lengths=None, sample_weight=None):
         acts = F.swapaxes(pred, 0, 1) if self._layout == 'NTC' else pred          # -> TNC
         lab = F.swapaxes(label, 0, 1) if self._batch_axis == 1 else label          # -> NT
-        loss = F.CTCLoss(acts, lab, pred_lengths, label_lengths, use_data_lengths=pred_lengths is not None,
+        lengths = [t for t in (pred_lengths, label_lengths) if t is not None]   # the op takes the present ones
+        loss = F.CTCLoss(acts, lab, *lengths, use_data_lengths=pred_lengths is not None,
                          use_label_lengths=label_lengths is not None, blank_label='last')
         return _apply_weighting(F, loss, self._weight, sample_weight)
 
