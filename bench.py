@@ -33,7 +33,8 @@ def _load_launcher():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None,
+                    help='GPUs (ranks) of this node; default: WORLD_SIZE under a launcher, else 1')
     ap.add_argument('--steps', type=int, default=30)
     ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--batch', type=int, default=256, help='per-GPU batch size')
@@ -46,6 +47,9 @@ def main():
     ap.add_argument('--graph', default='auto', choices=['auto', 'on', 'off'],
                     help='capture the whole training step in one HIP graph (gluon.GraphStep); auto = on for 1 GPU')
     args = ap.parse_args()
+    gpus_given = args.gpus is not None
+    if args.gpus is None:
+        args.gpus = int(os.environ.get('WORLD_SIZE', '1'))
 
     # `bench.py --gpus N` without a launcher: start N fresh worker processes (one per GPU) and exit
     # with their status.  This happens before anything in this process touches the GPU.
@@ -61,7 +65,7 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     if world > 1:
         dist.init()
-    if dist.world_size() != args.gpus:
+    if gpus_given and dist.world_size() != args.gpus:
         raise SystemExit('bench.py: --gpus %d but the process group has %d ranks' % (args.gpus, dist.world_size()))
     rank = dist.rank()
     local_rank = dist.local_rank()
@@ -140,6 +144,10 @@ def main():
             'vs_baseline': round(value / BASELINE_IMG_S, 3), 'dtype': {'float16': 'fp16', 'bfloat16': 'bf16',
                                                                          'float32': 'fp32'}[args.dtype],
             'data': 'synthetic (random-init weights, uniform images, random labels)',
+            # the reference publishes no fp16 ResNet-50 *training* number: vs_baseline divides by its best
+            # published training number, 1x V100 fp32 batch 128 -- not a same-config ratio
+            'baseline': {'value': BASELINE_IMG_S, 'source': 'reference perf.md, 1x V100, fp32, batch 128, training',
+                         'same_config': False},
             'config': {'model': args.model.replace('resnet50_v1b', 'ResNet-50 v1b'), 'global_batch': B * n,
                        'per_gpu_batch': B, 'seq_len': None, 'image_size': S, 'parallelism': 'dp%d' % n,
                        'layout': args.layout, 'optimizer': 'mp-SGD momentum 0.9', 'final_loss': round(loss_val, 4),

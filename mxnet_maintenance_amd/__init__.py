@@ -14,6 +14,7 @@ __version__ = '1.9.1.amd0'
 
 import torch as _torch
 
+import os
 from . import base
 from .base import MXNetError
 from .context import Context, cpu, gpu, cpu_pinned, current_context, num_gpus, gpu_memory_info, Device
@@ -67,3 +68,11 @@ from . import numpy_extension
 from . import numpy_extension as npx
 from . import rtc
 from .util import is_np_array, is_np_shape, set_np, reset_np, use_np, np_shape, np_array, set_np_shape, use_np_shape, use_np_array
+
+# A process launched as a dist_async server (DMLC_ROLE=server / scheduler) serves and exits at import,
+# as the reference's kvstore_server module does.
+if os.environ.get('DMLC_ROLE') in ('server', 'scheduler'):
+    from .kvstore import kvstore_server as _kvs
+    if _kvs._init_kvstore_server_module():
+        import sys as _sys
+        _sys.exit(0)

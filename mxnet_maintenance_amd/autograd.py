@@ -13,7 +13,6 @@ record/train scopes.
 """
 from contextlib import contextmanager
 
-import weakref
 
 import torch
 
@@ -98,9 +97,13 @@ def mark_variables(variables, gradients, grad_reqs='write'):
         v._grad = g
 
 
-# heads whose recorded graph a backward without retain_graph released (reference: the engine frees
-# the graph nodes; differentiating through them again is an error even when torch could replay them)
-_RELEASED = weakref.WeakKeyDictionary()
+# recorded graphs a backward without retain_graph released (reference: the engine frees the graph
+# nodes; differentiating through them again is an error even when torch could replay them).  Keyed on
+# the head's torch tensor, i.e. on the recording: an op with out= or an in-place assignment under
+# record() rebinds the NDArray to a fresh tensor with a fresh graph, which is differentiable again.
+# The mark is an attribute on that tensor (torch tensors compare elementwise, so they cannot be keys
+# of a weak dictionary).
+_RELEASED_ATTR = '_mxamd_graph_released'
 
 
 def _collect_leaves(retain):
@@ -170,12 +173,13 @@ def backward(heads, head_grads=None, retain_graph=False, train_mode=True, create
                          'You need to set is_recording to true or use autograd.record() to save '
                          'computational graphs for backward.')
     for h in heads:
-        if h in _RELEASED:
+        if getattr(getattr(h, '_data', None), _RELEASED_ATTR, False):
             raise MXNetError('Check failed: the graph of this output was already freed by a backward pass '
                              'without retain_graph=True; record it again or pass retain_graph=True')
     if not (retain_graph or create_graph):
         for h in heads:
-            _RELEASED[h] = True
+            if getattr(h, '_data', None) is not None:
+                setattr(h._data, _RELEASED_ATTR, True)
     leaves = _collect_leaves(retain_graph)
     _prepare_leaves(leaves)
     prev_train = set_training(train_mode)

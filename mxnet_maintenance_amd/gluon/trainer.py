@@ -502,6 +502,19 @@ class Trainer:
         graph = self._hyper is not None
         for i, a in enumerate(self._arenas):
             saved = self._save_stale(a) if ignore_stale_grad else None
+            if not graph and not saved and kind != 'sgd':
+                # an earlier stale step left the arena's parameters at different update counts
+                cnt = o._index_update_count
+                c0 = cnt.get(a.indices[0], 0)
+                if any(cnt.get(j, 0) != c0 for j in a.indices):
+                    saved = [None]
+            if saved and not graph:
+                # some parameters have no fresh gradient: the reference neither updates them nor
+                # advances their update counts, so Adam/LAMB bias corrections (per-parameter t) stay
+                # exact only if each fresh parameter is updated with its own count
+                self._restore_stale([x for x in saved if x is not None])
+                self._stale_arena_update(a, kind, clip)
+                continue
             # graph mode: counts advance (and lr / bias corrections reach the device) in _stage_hyper,
             # before every replay; the kernels read them from self._hyper[i]
             lr, wd, t, _bc1, _bc2 = self._arena_hparams(a, advance=not graph)
@@ -515,6 +528,30 @@ class Trainer:
                 lamb_flat_update(a, lr, o, t, wd, clip, hp=hp)
             if saved:
                 self._restore_stale(saved)
+
+    def _stale_arena_update(self, a, kind, clip):
+        """Update only the arena's parameters with a fresh gradient, each as its own segment with its
+        own update count (torch math on the slices; the fused kernels assume one count per arena)."""
+        import math
+        o = self._optimizer
+        for idx, p, (off, n, shape) in zip(a.indices, a.params, a.views):
+            if not p._all_data()[0]._fresh_grad:
+                continue
+            o._update_count([idx])
+            lr = o._get_lrs([idx])[0]
+            wd = o._get_wds([idx])[0]
+            t = o._index_update_count.get(idx, 1) or 1
+            sl = _ArenaSlice(a, off, n, shape)
+            if kind == 'sgd':
+                flat_sgd_update(sl.w, sl.g, sl.mom, sl.w32, lr, wd, o.momentum, o.rescale_grad, clip,
+                                torch_only=True)
+            elif kind in ('adam', 'adamw'):
+                if kind == 'adam' or o.correct_bias:
+                    lr *= math.sqrt(1. - o.beta2 ** t) / (1. - o.beta1 ** t)
+                flat_adam_update(sl, lr, o.beta1, o.beta2, o.epsilon, wd, o.rescale_grad, clip, kind == 'adamw',
+                                 torch_only=True)
+            else:
+                lamb_flat_update(sl, lr, o, t, wd, clip, torch_only=True)
 
     # ------------------------------------------------------------------ HIP-graph capture support
     def _enter_graph_mode(self):
@@ -686,10 +723,22 @@ class _ArenaBuckets(GradBuckets):
                     self._hooks.append(p._data.register_post_accumulate_grad_hook(self._make_hook(b)))
 
 
+class _ArenaSlice:
+    """One parameter's segment of a flat arena, shaped like an arena for the torch update paths."""
+
+    def __init__(self, a, off, n, shape):
+        def cut(b):
+            return None if b is None else b[off:off + n]
+        self.w, self.g, self.w32 = cut(a.w), cut(a.g), cut(a.w32)
+        self.mom = cut(getattr(a, 'mom', None))
+        self.mean, self.var = cut(getattr(a, 'mean', None)), cut(getattr(a, 'var', None))
+        self.views = [(0, n, shape)]
+
+
 @torch.no_grad()
-def flat_sgd_update(w, g, mom, w32, lr, wd, momentum, rescale, clip, hp=None):
+def flat_sgd_update(w, g, mom, w32, lr, wd, momentum, rescale, clip, hp=None, torch_only=False):
     """SGD(-momentum) over flat buffers; fused HIP kernel on gfx950 (``hp``: device lr, graph mode)."""
-    if w.is_cuda and _K.available() and _K.enabled() and hasattr(_K, 'flat_sgd'):
+    if not torch_only and w.is_cuda and _K.available() and _K.enabled() and hasattr(_K, 'flat_sgd'):
         _K.flat_sgd(w, g, mom, w32, lr, wd, momentum, rescale, clip, hp=hp)
         return
     if hp is not None:
@@ -712,9 +761,9 @@ def flat_sgd_update(w, g, mom, w32, lr, wd, momentum, rescale, clip, hp=None):
 
 
 @torch.no_grad()
-def flat_adam_update(a, lr, beta1, beta2, eps, wd, rescale, clip, adamw, hp=None):
+def flat_adam_update(a, lr, beta1, beta2, eps, wd, rescale, clip, adamw, hp=None, torch_only=False):
     """Adam / AdamW over one arena: fused HIP kernel on gfx950, torch ops elsewhere (same math)."""
-    if a.w.is_cuda and _K.available() and _K.enabled() and hasattr(_K, 'flat_adam'):
+    if not torch_only and a.w.is_cuda and _K.available() and _K.enabled() and hasattr(_K, 'flat_adam'):
         _K.flat_adam(a.w, a.g, a.mean, a.var, a.w32, lr, beta1, beta2, eps, wd, rescale, clip, adamw=adamw, hp=hp)
         return
     if hp is not None:
@@ -736,11 +785,11 @@ def flat_adam_update(a, lr, beta1, beta2, eps, wd, rescale, clip, adamw, hp=None
 
 
 @torch.no_grad()
-def lamb_flat_update(a, lr, o, t, wd, clip, hp=None):
+def lamb_flat_update(a, lr, o, t, wd, clip, hp=None, torch_only=False):
     """LAMB (phase 1 + per-parameter trust ratio + phase 2) over one arena."""
     lb = -1.0 if o.lower_bound is None else o.lower_bound
     ub = -1.0 if o.upper_bound is None else o.upper_bound
-    if a.w.is_cuda and _K.available() and _K.enabled() and hasattr(_K, 'lamb_update'):
+    if not torch_only and a.w.is_cuda and _K.available() and _K.enabled() and hasattr(_K, 'lamb_update'):
         _K.lamb_update(a.w, a.g, a.mean, a.var, a.w32, a.upd, a.table, a.nrm, lr, o.beta1, o.beta2, o.epsilon, t,
                        o.bias_correction, wd, o.rescale_grad, clip, lb, ub, hp=hp)
         return

@@ -64,12 +64,13 @@ def _srv_push(key, grad):
         if key not in _SERVER.store:
             raise KeyError('dist_async: key %r pushed before init' % (key,))
         w = _SERVER.store[key]
-        if _SERVER.updater is not None:
-            wn, gn = NDArray(w), NDArray(grad.float())
-            _SERVER.updater(key, gn, wn)
-            _SERVER.store[key] = wn._data
-        else:
-            w.copy_(grad)
+        if _SERVER.updater is None:
+            # reference: kvstore_dist_server.h CHECK(updater_) 'Updater needs to be set for async mode'
+            raise MXNetError('dist_async: push before set_optimizer -- the server needs an updater '
+                             '(kv.set_optimizer(...)) to apply asynchronous pushes')
+        wn, gn = NDArray(w), NDArray(grad.float())
+        _SERVER.updater(key, gn, wn)
+        _SERVER.store[key] = wn._data
         _SERVER.pushes += 1
     return True
 
@@ -111,7 +112,18 @@ def _srv_barrier(world):
 _RPC_READY = [False]
 
 
-def _init_rpc(rank, world):
+def dedicated_server():
+    """True when a separate server process (DMLC_ROLE=server, DMLC_NUM_SERVER >= 1) hosts the store;
+    otherwise rank 0's worker process hosts it."""
+    return int(os.environ.get('DMLC_NUM_SERVER', '0') or 0) > 0
+
+
+def _server_name():
+    return 'server' if dedicated_server() else 'worker0'
+
+
+def _init_rpc(rank, world, name=None):
+    """Join the RPC world: the workers (ranks 0..W-1) plus, with a dedicated server, rank W."""
     if _RPC_READY[0]:
         return
     from torch.distributed import rpc
@@ -119,7 +131,8 @@ def _init_rpc(rank, world):
     port = int(os.environ.get('MXAMD_PS_PORT', int(os.environ.get('MASTER_PORT', '29500')) + 17))
     opts = rpc.TensorPipeRpcBackendOptions(init_method='tcp://%s:%d' % (addr, port), num_worker_threads=32,
                                            rpc_timeout=600)
-    rpc.init_rpc('worker%d' % rank, rank=rank, world_size=world, rpc_backend_options=opts)
+    total = world + (1 if dedicated_server() else 0)
+    rpc.init_rpc(name or 'worker%d' % rank, rank=rank, world_size=total, rpc_backend_options=opts)
     _RPC_READY[0] = True
     atexit.register(_shutdown_rpc)
 
@@ -156,7 +169,7 @@ class KVStoreDistAsync(KVStoreBase):
     @staticmethod
     def _call(fn, *args):
         from torch.distributed import rpc
-        return rpc.rpc_sync('worker0', fn, args=args)
+        return rpc.rpc_sync(_server_name(), fn, args=args)
 
     def _wait_key(self, key):
         for f in self._pending.pop(key, []):
@@ -199,7 +212,7 @@ class KVStoreDistAsync(KVStoreBase):
             g = self._host(parts[0])
             for p in parts[1:]:              # several local devices: sum before sending
                 g += self._host(p)
-            self._pending.setdefault(k, []).append(rpc.rpc_async('worker0', _srv_push, args=(k, g)))
+            self._pending.setdefault(k, []).append(rpc.rpc_async(_server_name(), _srv_push, args=(k, g)))
 
     def pull(self, key, out=None, priority=0, ignore_sparse=True):
         assert out is not None

@@ -289,6 +289,8 @@ def conv_ok_shape(x, w, stride, pad, dilate=(1, 1), groups=1):
 
 # 512-thread big-tile LDS-DMA kernel (conv_big.hip): variant -> (BCO, BPIX)
 _BIG_VARIANTS = {10: (256, 256), 11: (128, 256), 12: (64, 512), 13: (256, 128)}
+# persistent LDS-DMA ring kernel (conv_ring.hip): variant -> (BCO, BPIX); no bias
+_RING_VARIANTS = {20: (128, 128), 21: (256, 128), 22: (128, 256), 23: (64, 256), 24: (256, 256), 25: (64, 128)}
 
 
 def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=None):
@@ -297,7 +299,8 @@ def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=Non
     ``variant``: 0 = heuristic tile, 1..4 = (BCO, BK) in (128,64) (128,32) (64,64) (64,32),
     5 / 6 = LDS-DMA pipelined kernel with a 128x128 / 64x256 tile (Cin % 64 == 0),
     10..13 = 512-thread LDS-DMA kernel with 256x256 / 128x256 / 64x512 / 256x128 tiles and a
-    row-contiguous epilogue.  ``bn_stats`` (big kernel only): also emit per-channel BatchNorm
+    row-contiguous epilogue, 20..25 = persistent LDS-DMA ring kernel (see _RING_VARIANTS; no bias).
+    ``bn_stats`` (big / ring kernels): also emit per-channel BatchNorm
     sum / sum-of-squares partials of y, attached to y as ``y._mxamd_bn_part``; ``addend`` (big kernel
     only, same shape/dtype as y): y = conv + addend."""
     N, H, W, C = x.shape
@@ -311,6 +314,20 @@ def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=Non
     if addend is not None:
         assert variant in _BIG_VARIANTS and addend.shape == y.shape and addend.dtype == y.dtype
         addend = addend.contiguous()
+    if variant in _RING_VARIANTS:
+        assert bias is None and addend is None, 'conv ring kernel: no bias / addend'
+        lib = _K.lib()
+        v = variant - 20
+        part, nparts = None, 0
+        if bn_stats:
+            nparts = lib.conv_nhwc_fwd_ring_nparts(N, H, W, R, S, stride[0], stride[1], pad[0], pad[1], v)
+            part = torch.empty(2 * K * nparts, dtype=torch.float32, device=x.device)
+        lib.conv_nhwc_fwd_ring(_DT[x.dtype], x.data_ptr(), w.data_ptr(), y.data_ptr(), _zero_page(x.device).data_ptr(),
+                               N, H, W, C, K, R, S, stride[0], stride[1], pad[0], pad[1], v, _p(part), nparts,
+                               _stream())
+        if part is not None:
+            y._mxamd_bn_part = (part, nparts)
+        return y
     if variant in _BIG_VARIANTS:
         lib = _K.lib()
         v = variant - 10
@@ -346,13 +363,15 @@ def _zero_page(dev):
     return z
 
 
-def _fwd_variants(C, K):
+def _fwd_variants(C, K, bias=False):
     """Tile variants of conv_fwd valid for Cin=C, Cout=K.
 
     1..4: register-staged kernel (conv_igemm.hip) with (BCO, BK) = (128,64) (128,32) (64,64) (64,32);
     5, 6: LDS-DMA kernel (conv_glds.hip) with 128x128 / 64x256 tiles;
     10..13: 512-thread LDS-DMA kernel (conv_big.hip), see _BIG_VARIANTS."""
     v = []
+    if C % 64 == 0 and not bias:
+        v.extend(b for b, (bco, _bpix) in sorted(_RING_VARIANTS.items()) if K % bco == 0)
     if C % 64 == 0:
         v.extend(b for b, (bco, _bpix) in sorted(_BIG_VARIANTS.items()) if K % bco == 0)
     if C % 64 == 0 and K % 128 == 0:
@@ -376,11 +395,13 @@ def conv_wgrad_ok(x, w):
             and x.numel() < 2 ** 31 and x.data_ptr() % 16 == 0)
 
 
-def conv_wgrad(x, dy, wshape, stride, pad, out=None, accum=False, dma=True):
+def conv_wgrad(x, dy, wshape, stride, pad, out=None, accum=False, dma=True, ring=0):
     """dW[K,R,S,C] of an NHWC conv on MFMA (split-pixel fp32 slabs + reduce).
 
     ``out`` (optional, contiguous, f16/bf16/f32) receives the result; with
     ``accum`` the gradient is added to it (e.g. straight into a parameter's grad).
+    ``ring`` 1..9: the LDS-DMA ring kernel with that tile (see conv_wgrad.hip), else the planned
+    register-staged (``dma=False``) / LDS-DMA kernel.
     """
     N, H, W, C = x.shape
     K, R, S, _ = wshape
@@ -391,12 +412,20 @@ def conv_wgrad(x, dy, wshape, stride, pad, out=None, accum=False, dma=True):
     assert tuple(dy.shape[1:3]) == (Ho, Wo), 'conv_wgrad: dy shape does not match the conv geometry'
     assert dy.numel() < 2 ** 31 and dy.data_ptr() % 16 == 0
     lib = _K.lib()
-    ws = lib.conv_nhwc_wgrad_workspace(N, H, W, C, K, R, S, stride[0], stride[1], pad[0], pad[1])
+    if ring:
+        ws = lib.conv_nhwc_wgrad_ring_workspace(N, H, W, C, K, R, S, stride[0], stride[1], pad[0], pad[1], ring)
+    else:
+        ws = lib.conv_nhwc_wgrad_workspace(N, H, W, C, K, R, S, stride[0], stride[1], pad[0], pad[1])
     slab = torch.empty(ws, dtype=torch.float32, device=x.device)
     if out is None:
         out = torch.empty((K, R, S, C), dtype=x.dtype, device=x.device)
         accum = False
     assert out.is_contiguous() and out.numel() == K * R * S * C and out.dtype in _DT
+    if ring:
+        lib.conv_nhwc_wgrad_ring(_DT[x.dtype], x.data_ptr(), dy.data_ptr(), slab.data_ptr(), _DT[out.dtype],
+                                 out.data_ptr(), int(bool(accum)), N, H, W, C, K, R, S, stride[0], stride[1], pad[0],
+                                 pad[1], _zero_page(x.device).data_ptr(), int(ring), _stream())
+        return out
     lib.conv_nhwc_wgrad(_DT[x.dtype], x.data_ptr(), dy.data_ptr(), slab.data_ptr(), _DT[out.dtype], out.data_ptr(),
                         int(bool(accum)), N, H, W, C, K, R, S, stride[0], stride[1], pad[0], pad[1],
                         _zero_page(x.device).data_ptr() if dma else 0, _stream())
@@ -514,7 +543,7 @@ def _fwd_candidates(x, w, stride, pad, bias):
     if conv_ok_shape(x, w, stride, pad):
         c.append(('hip', lambda: conv_fwd(x, w, stride, pad, bias)))
         stats = bool(_state.STATE.training)
-        for v in _fwd_variants(C, K):
+        for v in _fwd_variants(C, K, bias is not None):
             c.append(('hip%d' % v, lambda v=v: conv_fwd(x, w, stride, pad, bias, v, bn_stats=stats)))
     if R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0):
         def mm():
@@ -601,6 +630,10 @@ def _wgrad_candidates(dy, x, w, stride, pad):
     if conv_wgrad_ok(x, w):
         c.insert(0, ('hip', lambda: conv_wgrad(x, dy, w.shape, stride, pad)))
         c.insert(1, ('hipreg', lambda: conv_wgrad(x, dy, w.shape, stride, pad, dma=False)))
+        lib = _K.lib()
+        for v in range(1, 10):
+            if lib.conv_nhwc_wgrad_ring_ok(C, K, R, S, v):
+                c.insert(2, ('ring%d' % v, lambda v=v: conv_wgrad(x, dy, w.shape, stride, pad, ring=v)))
     if R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0):
         P = dy.numel() // K
         for chunks in (16, 64):
@@ -660,10 +693,11 @@ def _wgrad(dy, x, w, w_ref, stride, pad):
     """
     key = ('wgrad', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype)
     algo = _ALGO.get(key)
-    if algo in ('hip', 'hipreg'):
+    if algo in ('hip', 'hipreg') or (algo or '').startswith('ring'):
         tgt = _leaf_grad(w_ref, dtype=w.dtype)
         if tgt is not None:
-            conv_wgrad(x, dy, w.shape, stride, pad, out=tgt, accum=True, dma=algo == 'hip')
+            conv_wgrad(x, dy, w.shape, stride, pad, out=tgt, accum=True, dma=algo == 'hip',
+                       ring=int(algo[4:]) if algo.startswith('ring') else 0)
             return None
     elif algo is not None and algo.startswith('splitk'):
         tgt = _leaf_grad(w_ref, dtype=w.dtype)

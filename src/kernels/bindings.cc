@@ -56,6 +56,16 @@ void conv_nhwc_fwd_big(int dtype, const void* x, const void* w, const float* bia
 void conv_nhwc_fwd_glds(int dtype, const void* x, const void* w, const float* bias, void* y, const void* zero, int N,
                         int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int bco,
                         hipStream_t s);
+int conv_nhwc_fwd_ring_nparts(int N, int H, int W, int R, int S, int sh, int sw, int ph, int pw, int variant);
+void conv_nhwc_fwd_ring(int dtype, const void* x, const void* w, void* y, const void* zero, int N, int H, int W, int C,
+                        int K, int R, int S, int sh, int sw, int ph, int pw, int variant, float* part, int nparts,
+                        hipStream_t s);
+int conv_nhwc_wgrad_ring_ok(int C, int K, int R, int S, int variant);
+int64_t conv_nhwc_wgrad_ring_workspace(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
+                                       int variant);
+void conv_nhwc_wgrad_ring(int dtype, const void* x, const void* dy, float* slab, int out_dtype, void* out, int accum,
+                          int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
+                          const void* zero, int variant, hipStream_t s);
 int64_t conv_nhwc_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw);
 void conv_nhwc_wgrad(int dtype, const void* x, const void* dy, float* slab, int out_dtype, void* out, int accum, int N,
                      int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, const void* zero,
@@ -265,7 +275,27 @@ PYBIND11_MODULE(_hip_kernels, m) {
                       sw, ph, pw, variant, P<float>(part), nparts, P<void>(addend), S(s));
     check_launch("conv_nhwc_fwd_big");
   });
+  // persistent LDS-DMA ring kernel (conv_ring.hip): variant 0..5 = 128x128x4, 256x128x3, 128x256x3, 64x256x4,
+  // 256x256x2, 64x128x4 (co x pix x stages); part as above
+  m.def("conv_nhwc_fwd_ring_nparts", &conv_nhwc_fwd_ring_nparts);
+  m.def("conv_nhwc_fwd_ring", [](int dt, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t zero, int N, int H, int W,
+                                 int C, int K, int R, int Sf, int sh, int sw, int ph, int pw, int variant, uintptr_t part,
+                                 int nparts, uintptr_t s) {
+    conv_nhwc_fwd_ring(dt, P<void>(x), P<void>(w), P<void>(y), P<void>(zero), N, H, W, C, K, R, Sf, sh, sw, ph, pw,
+                       variant, P<float>(part), nparts, S(s));
+    check_launch("conv_nhwc_fwd_ring");
+  });
   m.def("conv_nhwc_wgrad_workspace", &conv_nhwc_wgrad_workspace);
+  // weight gradient on the LDS-DMA ring (variants 1..5, see conv_wgrad.hip)
+  m.def("conv_nhwc_wgrad_ring_ok", &conv_nhwc_wgrad_ring_ok);
+  m.def("conv_nhwc_wgrad_ring_workspace", &conv_nhwc_wgrad_ring_workspace);
+  m.def("conv_nhwc_wgrad_ring", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t slab, int odt, uintptr_t out,
+                                   int accum, int N, int H, int W, int C, int K, int R, int Sf, int sh, int sw, int ph,
+                                   int pw, uintptr_t zero, int variant, uintptr_t s) {
+    conv_nhwc_wgrad_ring(dt, P<void>(x), P<void>(dy), P<float>(slab), odt, P<void>(out), accum, N, H, W, C, K, R, Sf,
+                         sh, sw, ph, pw, P<void>(zero), variant, S(s));
+    check_launch("conv_nhwc_wgrad_ring");
+  });
   // zero: 0 -> register-staged kernel, else a >=128-byte zero page -> LDS-DMA kernel
   m.def("conv_nhwc_wgrad", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t slab, int odt, uintptr_t out, int accum,
                               int N, int H, int W, int C, int K, int R, int Sf, int sh, int sw, int ph, int pw,

@@ -389,6 +389,180 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_glds_kernel(const T* 
   }
 }
 
+// s_waitcnt vmcnt(N) only (gfx9 encoding; expcnt / lgkmcnt at their maxima)
+template <int N>
+__device__ __forceinline__ void wg_vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+// wait until at most n VM ops are outstanding, n rounded DOWN to a level (always safe)
+__device__ __forceinline__ void wg_vm_wait_le(int n) {
+  if (n >= 32) wg_vm_wait<32>();
+  else if (n >= 24) wg_vm_wait<24>();
+  else if (n >= 20) wg_vm_wait<20>();
+  else if (n >= 16) wg_vm_wait<16>();
+  else if (n >= 12) wg_vm_wait<12>();
+  else if (n >= 10) wg_vm_wait<10>();
+  else if (n >= 8) wg_vm_wait<8>();
+  else if (n >= 6) wg_vm_wait<6>();
+  else if (n >= 5) wg_vm_wait<5>();
+  else if (n >= 4) wg_vm_wait<4>();
+  else if (n >= 3) wg_vm_wait<3>();
+  else if (n >= 2) wg_vm_wait<2>();
+  else if (n >= 1) wg_vm_wait<1>();
+  else wg_vm_wait<0>();
+}
+
+// Weight gradient with an NST-stage LDS-DMA ring over the pixel (reduction) stream.
+// Same sub-tile images / transposed fragment reads as conv_wgrad_glds_kernel, but D = NST-1 pixel
+// steps stay in flight across each barrier (counted vmcnt + raw s_barrier instead of
+// __syncthreads(), which would drain the DMA queue), and the host plans few, long splits (about one
+// workgroup per CU) so the fp32 slab traffic stays small next to the operand stream.
+template <typename T, int WM, int WN, int NST, int FM, bool IDENT>
+__global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_ring_kernel(const T* __restrict__ x,
+                                                                       const T* __restrict__ dy,
+                                                                       float* __restrict__ slab,
+                                                                       const T* __restrict__ zero, WgradGeom g) {
+  constexpr int NW = WM * WN;
+  constexpr int MS = FM / 4;               // X sub-tiles (64 rsc) per wave
+  constexpr int XSUB = WM * MS;            // X sub-tiles per block
+  constexpr int NSUB = XSUB + WN;
+  constexpr int SUB = 64 * 64;
+  constexpr int STAGE_B = NSUB * SUB * (int)sizeof(T);
+  constexpr int NINS = NSUB * 8;                 // wave-instructions per stage
+  constexpr int IPW = (NINS + NW - 1) / NW;      // per wave (upper bound)
+  constexpr int D = NST - 1;
+  extern __shared__ __attribute__((aligned(1024))) char wsm[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid % WM;
+  const int wn = wid / WM;
+
+  const int nblk = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7;
+  const int q8 = nblk >> 3, r8 = nblk & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tile = wgid % g.tiles;
+  const int split = wgid / g.tiles;
+  const int tm = tile % g.tiles_m;
+  const int tn = tile / g.tiles_m;
+  const int m0 = tm * 64 * XSUB;
+  const int n0 = tn * 64 * WN;
+  const int pbeg = split * g.plen;
+  const int pend = min(g.P, pbeg + g.plen);
+  const int KT = pend > pbeg ? (pend - pbeg + 63) >> 6 : 0;
+
+  const int t = lane >> 3;
+  int d_row[IPW], d_col[IPW], d_r[IPW], d_s[IPW], d_lds[IPW];
+  bool d_on[IPW], d_isx[IPW];
+  int lpt = 0;   // LDS-DMA instructions this wave issues per pixel step
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int ins = wid + i * NW;
+    d_on[i] = ins < NINS;
+    lpt += d_on[i] ? 1 : 0;
+    const int sub = d_on[i] ? ins >> 3 : 0;
+    const int row = (ins & 7) * 8 + t;
+    const int gch = (lane & 7) ^ swz(row);
+    d_row[i] = row;
+    d_lds[i] = sub * SUB * (int)sizeof(T) + (ins & 7) * 1024;
+    d_isx[i] = sub < XSUB;
+    if (d_isx[i]) {
+      const int n = m0 + sub * 64;
+      const int rs = n / g.C;
+      d_col[i] = n - rs * g.C + gch * 8;
+      d_r[i] = rs / g.S;
+      d_s[i] = rs - d_r[i] * g.S;
+    } else {
+      d_col[i] = n0 + (sub - XSUB) * 64 + gch * 8;
+      d_r[i] = d_s[i] = 0;
+    }
+  }
+  const T* zsrc = zero + ((lane & 7) << 3);
+
+  int i_kt = 0, i_stage = 0;
+  auto issue = [&]() {
+    char* sbase = wsm + i_stage * STAGE_B;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      if (!d_on[i]) continue;                 // wave-uniform
+      const int p = pbeg + i_kt * 64 + d_row[i];
+      bool ok = p < pend;
+      const T* src;
+      if (!d_isx[i]) {
+        src = dy + (int64_t)p * g.K + d_col[i];
+      } else if (IDENT) {
+        src = x + (int64_t)p * g.C + d_col[i];
+      } else {
+        const int nimg = (int)fdiv((uint32_t)p, g.fHoWo);
+        const int rem = p - nimg * (g.Ho * g.Wo);
+        const int ho = (int)fdiv((uint32_t)rem, g.fWo);
+        const int wo = rem - ho * g.Wo;
+        const int hi = ho * g.sh - g.ph + d_r[i];
+        const int wi = wo * g.sw - g.pw + d_s[i];
+        ok = ok && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+        src = x + ((int64_t)(nimg * g.H + hi) * g.W + wi) * g.C + d_col[i];
+      }
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(ok ? src : zsrc), (lds_void_t*)(sbase + d_lds[i]), 16, 0, 0);
+    }
+    ++i_kt;
+    i_stage = (i_stage + 1 == NST) ? 0 : i_stage + 1;
+  };
+
+  const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
+  const int frow = 8 * fg + fq;
+  int foff[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) foff[f] = frow * 128 + ((((2 * f) + (fp >> 1)) ^ swz(frow)) << 4) + ((fp & 1) << 3);
+
+  f4_t acc[FM][4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int npro = KT < D ? KT : D;
+  for (int p = 0; p < npro; ++p) issue();
+  int c_stage = 0;
+  for (int kt = 0; kt < KT; ++kt) {
+    const int ahead = (KT - 1 - kt) < (D - 1) ? (KT - 1 - kt) : (D - 1);
+    wg_vm_wait_le(ahead * lpt);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kt + D < KT) issue();
+    const T* sx = reinterpret_cast<const T*>(wsm + c_stage * STAGE_B) + wm * MS * SUB;
+    const T* sd = reinterpret_cast<const T*>(wsm + c_stage * STAGE_B) + (XSUB + wn) * SUB;
+#pragma unroll
+    for (int kk = 0; kk < 64; kk += 32) {
+      v8s a[FM], b[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) b[f] = tr_frag(sd, kk * 128 + foff[f]);
+#pragma unroll
+      for (int f = 0; f < FM; ++f) a[f] = tr_frag(sx + (f >> 2) * SUB, kk * 128 + foff[f & 3]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = Mfma16<T>::run(a[i], b[j], acc[i][j]);
+    }
+    c_stage = (c_stage + 1 == NST) ? 0 : c_stage + 1;
+  }
+
+  float* out = slab + (size_t)split * g.K * g.RSC;
+  const int rsc_l = (lane >> 4) * 4;
+  const int k_l = lane & 15;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int rsc = m0 + wm * MS * 64 + i * 16 + rsc_l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = n0 + wn * 64 + j * 16 + k_l;
+      *reinterpret_cast<f4_t*>(out + (size_t)k * g.RSC + rsc) = acc[i][j];
+    }
+  }
+}
+
 template <typename OutT>
 __device__ __forceinline__ void store4(OutT* p, f4_t v);
 template <>
@@ -549,7 +723,133 @@ void dispatch_wgrad(const void* x, const void* dy, float* slab, const WgradGeom&
   else launch_wgrad<T, 1, 1, 4>(x, dy, slab, g, pl.splits, ident, zero, s);
 }
 
+// ring variants: 1: 256x128 (4x2 waves, 3 stages)  2: 128x256 (2x4, 3)  3: 192x64 (3x1, 4)
+//                4: 256x64 (4x1, 4)  5: 128x128 (2x2, 4)  6: 256x256 (2x4 waves of 128x64, 2)
+//                7: 512x128 (4x2 waves of 128x64, 2)  8: 576x64 (9x1, 2: a whole 3x3x64 weight)
+//                9: 64x256 (1x4, 4)      (rsc x k)
+struct RingW {
+  int wm, wn, nst, fm;
+};
+static bool ring_wgrad_cfg(int variant, RingW* c) {
+  switch (variant) {
+    case 1: *c = {4, 2, 3, 4}; return true;
+    case 2: *c = {2, 4, 3, 4}; return true;
+    case 3: *c = {3, 1, 4, 4}; return true;
+    case 4: *c = {4, 1, 4, 4}; return true;
+    case 5: *c = {2, 2, 4, 4}; return true;
+    case 6: *c = {2, 4, 2, 8}; return true;
+    case 7: *c = {4, 2, 2, 8}; return true;
+    case 8: *c = {9, 1, 2, 4}; return true;
+    case 9: *c = {1, 4, 4, 4}; return true;
+    default: return false;
+  }
+}
+
+static WgradPlan plan_wgrad_ring(const RingW& c, int N, int H, int W, int C, int K, int R, int S, int sh, int sw,
+                                 int ph, int pw) {
+  WgradPlan pl;
+  const int Ho = (H + 2 * ph - R) / sh + 1, Wo = (W + 2 * pw - S) / sw + 1;
+  const int RSC = R * S * C;
+  const int64_t P = (int64_t)N * Ho * Wo;
+  pl.fm = 4;
+  pl.wm = c.wm;
+  pl.wn = c.wn;
+  const int64_t tiles = (int64_t)(RSC / (16 * c.fm * c.wm)) * (K / (64 * c.wn));
+  // about one workgroup per CU (the LDS ring fills the CU): whole waves of workgroups, no tail
+  int64_t splits = std::max<int64_t>(1, 256 / tiles);
+  splits = std::min<int64_t>(splits, std::max<int64_t>(1, P / 256));
+  int64_t plen = (P + splits - 1) / splits;
+  plen = (plen + 63) / 64 * 64;
+  pl.plen = (int)plen;
+  pl.splits = (int)((P + plen - 1) / plen);
+  return pl;
+}
+
+template <typename T, int WM, int WN, int NST, int FM = 4>
+static void launch_wgrad_ring(const void* x, const void* dy, float* slab, const WgradGeom& g, int splits, bool ident,
+                              const void* zero, hipStream_t s) {
+  constexpr int SMEM = NST * (WM * FM / 4 + WN) * 64 * 64 * (int)sizeof(T);
+  static_assert(SMEM <= 160 * 1024, "wgrad ring LDS budget");
+  static bool attr[2] = {false, false};
+  const void* fn = ident ? reinterpret_cast<const void*>(&conv_wgrad_ring_kernel<T, WM, WN, NST, FM, true>)
+                         : reinterpret_cast<const void*>(&conv_wgrad_ring_kernel<T, WM, WN, NST, FM, false>);
+  if (!attr[ident]) {
+    hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    attr[ident] = true;
+  }
+  dim3 grid(g.tiles * splits);
+  if (ident)
+    hipLaunchKernelGGL((conv_wgrad_ring_kernel<T, WM, WN, NST, FM, true>), grid, dim3(64 * WM * WN), SMEM, s,
+                       static_cast<const T*>(x), static_cast<const T*>(dy), slab, static_cast<const T*>(zero), g);
+  else
+    hipLaunchKernelGGL((conv_wgrad_ring_kernel<T, WM, WN, NST, FM, false>), grid, dim3(64 * WM * WN), SMEM, s,
+                       static_cast<const T*>(x), static_cast<const T*>(dy), slab, static_cast<const T*>(zero), g);
+}
+
+template <typename T>
+static void dispatch_wgrad_ring(int variant, const void* x, const void* dy, float* slab, const WgradGeom& g,
+                                int splits, bool ident, const void* zero, hipStream_t s) {
+  switch (variant) {
+    case 1: launch_wgrad_ring<T, 4, 2, 3>(x, dy, slab, g, splits, ident, zero, s); break;
+    case 2: launch_wgrad_ring<T, 2, 4, 3>(x, dy, slab, g, splits, ident, zero, s); break;
+    case 3: launch_wgrad_ring<T, 3, 1, 4>(x, dy, slab, g, splits, ident, zero, s); break;
+    case 4: launch_wgrad_ring<T, 4, 1, 4>(x, dy, slab, g, splits, ident, zero, s); break;
+    case 5: launch_wgrad_ring<T, 2, 2, 4>(x, dy, slab, g, splits, ident, zero, s); break;
+    case 6: launch_wgrad_ring<T, 2, 4, 2, 8>(x, dy, slab, g, splits, ident, zero, s); break;
+    case 7: launch_wgrad_ring<T, 4, 2, 2, 8>(x, dy, slab, g, splits, ident, zero, s); break;
+    case 8: launch_wgrad_ring<T, 9, 1, 2, 4>(x, dy, slab, g, splits, ident, zero, s); break;
+    case 9: launch_wgrad_ring<T, 1, 4, 4, 4>(x, dy, slab, g, splits, ident, zero, s); break;
+  }
+}
+
 }  // namespace
+
+// True when ring variant `variant` (1..5) tiles this weight (R*S*C x K) exactly.
+int conv_nhwc_wgrad_ring_ok(int C, int K, int R, int S, int variant) {
+  RingW c;
+  if (!ring_wgrad_cfg(variant, &c)) return 0;
+  return (C % 64 == 0 && K % (64 * c.wn) == 0 && (R * S * C) % (16 * c.fm * c.wm) == 0) ? 1 : 0;
+}
+
+int64_t conv_nhwc_wgrad_ring_workspace(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
+                                       int variant) {
+  RingW c;
+  MXAMD_HOST_CHECK(ring_wgrad_cfg(variant, &c), "conv_nhwc_wgrad_ring: unknown variant");
+  WgradPlan pl = plan_wgrad_ring(c, N, H, W, C, K, R, S, sh, sw, ph, pw);
+  return (int64_t)pl.splits * K * R * S * C;
+}
+
+void conv_nhwc_wgrad_ring(int dtype, const void* x, const void* dy, float* slab, int out_dtype, void* out, int accum,
+                          int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
+                          const void* zero, int variant, hipStream_t s) {
+  RingW c;
+  MXAMD_HOST_CHECK(ring_wgrad_cfg(variant, &c) && conv_nhwc_wgrad_ring_ok(C, K, R, S, variant) && zero != nullptr,
+                   "conv_nhwc_wgrad_ring: variant does not tile this weight");
+  WgradGeom g;
+  g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S;
+  g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw;
+  g.Ho = (H + 2 * ph - R) / sh + 1;
+  g.Wo = (W + 2 * pw - S) / sw + 1;
+  const int64_t P = (int64_t)N * g.Ho * g.Wo;
+  MXAMD_HOST_CHECK(P < (1ll << 31) && (int64_t)N * H * W * C < (1ll << 31) && P * K < (1ll << 31),
+                   "conv_nhwc_wgrad_ring: tensor too large for 32-bit indexing");
+  g.P = (int)P;
+  g.RSC = R * S * C;
+  WgradPlan pl = plan_wgrad_ring(c, N, H, W, C, K, R, S, sh, sw, ph, pw);
+  g.tiles_m = g.RSC / (16 * c.fm * c.wm);
+  g.tiles = g.tiles_m * (K / (64 * c.wn));
+  g.plen = pl.plen;
+  g.fWo = make_fastdiv(g.Wo);
+  g.fHoWo = make_fastdiv(g.Ho * g.Wo);
+  const bool ident = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
+  if (dtype == kF16) dispatch_wgrad_ring<__half>(variant, x, dy, slab, g, pl.splits, ident, zero, s);
+  else if (dtype == kBF16) dispatch_wgrad_ring<__hip_bfloat16>(variant, x, dy, slab, g, pl.splits, ident, zero, s);
+  else throw std::runtime_error("conv_nhwc_wgrad_ring: dtype must be f16 or bf16");
+  const int64_t n = (int64_t)K * g.RSC;
+  if (out_dtype == kF32) launch_reduce<float>(slab, pl.splits, n, static_cast<float*>(out), accum, s);
+  else if (out_dtype == kF16) launch_reduce<__half>(slab, pl.splits, n, static_cast<__half*>(out), accum, s);
+  else launch_reduce<__hip_bfloat16>(slab, pl.splits, n, static_cast<__hip_bfloat16*>(out), accum, s);
+}
 
 // Number of fp32 slab elements conv_nhwc_wgrad needs (splits * K * R*S*C).
 int64_t conv_nhwc_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw) {

@@ -318,6 +318,37 @@ def test_trainer_stale_param_untouched(monkeypatch, flat, optim):
     tr.step(1, ignore_stale_grad=True)
     np.testing.assert_array_equal(net[1].weight.data().asnumpy(), w1)
     assert np.abs(net[0].weight.data().asnumpy() - w0).max() > 0
+    # update counts advance only for the fresh parameters (Adam/LAMB bias corrections use them)
+    o = tr._optimizer
+    counts = {i: o._index_update_count.get(i, 0) for i in range(len(tr._params))}
+    idx1 = [i for i, p in enumerate(tr._params) if p is net[1].weight][0]
+    idx0 = [i for i, p in enumerate(tr._params) if p is net[0].weight][0]
+    assert counts[idx0] == 2 and counts[idx1] == 1, counts
+
+
+@pytest.mark.parametrize('optim', ['adam', 'lamb'])
+def test_trainer_stale_then_fresh_matches_per_parameter_path(monkeypatch, optim):
+    """After a step where one parameter was stale, the flat-arena trainer keeps per-parameter
+    update counts: a following full step gives the same weights as the per-parameter updater."""
+    out = {}
+    for flat in ('1', '0'):
+        monkeypatch.setenv('MXAMD_FLAT_ARENA', flat)
+        mx_random_seed = 3
+        np.random.seed(mx_random_seed)
+        net = nn.HybridSequential()
+        net.add(nn.Dense(3, in_units=2), nn.Dense(3, in_units=2))
+        net.initialize(mx.init.Constant(0.5))
+        tr = gluon.Trainer(net.collect_params(), optim, {'learning_rate': 0.1, 'wd': 0.01})
+        for kind in ('both', 'first', 'both'):
+            with autograd.record():
+                y = net[0](nd.ones((1, 2))).sum()
+                if kind == 'both':
+                    y = y + (net[1](nd.ones((1, 2))) * 2).sum()
+            y.backward()
+            tr.step(1, ignore_stale_grad=True)
+        out[flat] = [p.data().asnumpy().copy() for p in net.collect_params().values()]
+    for a, b in zip(out['1'], out['0']):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
 
 
 def test_model_zoo_constructs():

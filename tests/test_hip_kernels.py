@@ -213,7 +213,8 @@ def test_conv_nhwc_fwd_matches_fp32(dtype, cfg):
     # (N, H, Cin, Cout, k, stride): every (WM, WN) tile variant, identity / strided / padded paths
     (2, 14, 64, 64, 1, 1), (2, 14, 64, 64, 3, 1), (3, 9, 128, 128, 3, 1), (2, 15, 128, 128, 3, 2),
     (2, 14, 256, 512, 1, 2), (4, 7, 64, 256, 1, 1), (2, 7, 256, 64, 1, 1), (1, 5, 64, 128, 3, 1),
-    (3, 11, 128, 64, 1, 1)])
+    (3, 11, 128, 64, 1, 1), (16, 28, 256, 128, 1, 1), (8, 14, 128, 256, 3, 1), (6, 13, 64, 64, 3, 1),
+    (4, 14, 256, 256, 3, 1), (4, 10, 512, 128, 1, 1)])
 def test_conv_wgrad_matches_fp32(dtype, cfg):
     from mxnet_maintenance_amd.ops import kernel_fns as KF
     _lib()
@@ -233,6 +234,11 @@ def test_conv_wgrad_matches_fp32(dtype, cfg):
     for dma in (True, False):          # LDS-DMA kernel and register-staged kernel
         dw = KF.conv_wgrad(x, dy, w.shape, (s, s), (pad, pad), dma=dma)
         torch.testing.assert_close(dw.float(), ref, rtol=0, atol=tol)
+    lib = KF._K.lib()
+    for v in range(1, 10):              # LDS-DMA ring kernel, every tile that fits this weight
+        if lib.conv_nhwc_wgrad_ring_ok(Cin, Cout, k, k, v):
+            dw = KF.conv_wgrad(x, dy, w.shape, (s, s), (pad, pad), ring=v)
+            torch.testing.assert_close(dw.float(), ref, rtol=0, atol=tol, msg=lambda m: 'ring %d: %s' % (v, m))
     # accumulate into an fp32 buffer (the direct-to-.grad path)
     acc = torch.ones(Cout, k, k, Cin, device='cuda')
     KF.conv_wgrad(x, dy, w.shape, (s, s), (pad, pad), out=acc, accum=True)
@@ -672,6 +678,35 @@ def test_conv_big_bn_stats_addend(dtype, cfg):
         torch.testing.assert_close(var, v_ref, rtol=2e-3, atol=2e-3)
         o_ref = torch.relu((yf - m_ref) / torch.sqrt(v_ref + 1e-5) * g + b)
         torch.testing.assert_close(out.float(), o_ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('cfg', [(3, 13, 128, 256, 3, 1), (2, 9, 64, 128, 1, 1), (4, 17, 64, 64, 3, 2),
+                                 (64, 20, 64, 256, 1, 1), (200, 15, 256, 128, 3, 1)])
+def test_conv_ring_bn_stats(dtype, cfg):
+    """Persistent LDS-DMA ring conv (conv_ring.hip): every tile/stage variant matches the fp32 torch
+    conv, including workgroups that stream several tiles (the last two shapes have more tiles than
+    CUs) and a partial last pixel tile; the BN sum / sum-sq partials from its epilogue match."""
+    from mxnet_maintenance_amd.ops import kernel_fns as KF
+    _lib()
+    N, H, Cin, Cout, k, s = cfg
+    pad = k // 2
+    torch.manual_seed(5)
+    x = torch.randn(N, H, H, Cin, device='cuda').to(dtype)
+    w = (torch.randn(Cout, k, k, Cin, device='cuda') / (k * k * Cin) ** 0.5).to(dtype)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, s, pad).permute(0, 2, 3, 1)
+    tol = 2e-2 if dtype == torch.float16 else 6e-2
+    variants = [v for v, (bco, _) in sorted(KF._RING_VARIANTS.items()) if Cout % bco == 0]
+    assert variants
+    for v in variants:
+        y = KF.conv_fwd(x, w, (s, s), (pad, pad), None, v, bn_stats=True)
+        torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol, msg=lambda m: 'variant %d: %s' % (v, m))
+        part, nparts = y._mxamd_bn_part
+        p = part.view(2, Cout, nparts)
+        torch.testing.assert_close(p[0].sum(1), ref.sum((0, 1, 2)), rtol=1e-2, atol=0.5)
+        torch.testing.assert_close(p[1].sum(1), (ref * ref).sum((0, 1, 2)), rtol=1e-2, atol=0.5)
+        y2 = KF.conv_fwd(x, w, (s, s), (pad, pad), None, v)
+        assert torch.equal(y2, y)
 
 
 def test_conv_autotune_rejects_wrong_candidate():

@@ -33,8 +33,15 @@ def main():
             t_h = timeit(lambda: KF.conv_wgrad(x, dy, w.shape, (s, s), (pad, pad)))
             line += '  hip-reg %.3f ms (%4.0f TF/s)  hip-dma %.3f ms (%4.0f TF/s)' % (t_r, fl / t_r / 1e9, t_h,
                                                                                   fl / t_h / 1e9)
+            lib = KF._K.lib()
+            for v in range(1, 10):
+                if lib.conv_nhwc_wgrad_ring_ok(C, K, k, k, v):
+                    t_v = timeit(lambda: KF.conv_wgrad(x, dy, w.shape, (s, s), (pad, pad), ring=v))
+                    line += '  ring%d %.3f' % (v, t_v)
+                    t_h = min(t_h, t_v)
             t_h = min(t_h, t_r)
             tot['hip'] += t_h * cnt
+            line += '  | best-hip %.3f (%4.0f TF/s)' % (t_h, fl / t_h / 1e9)
         else:
             tot['hip'] += t_m * cnt
         print(line, flush=True)

@@ -13,9 +13,17 @@ import argparse
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from mxnet_maintenance_amd.parallel.launch import launch  # noqa: E402  (never touches the GPU)
+def _load_launch():
+    """parallel/launch.py loaded by file path: importing the package would import torch and the HIP
+    extensions into this launcher parent, which must stay GPU-free (its children are the GPU ranks)."""
+    import importlib.util
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'mxnet_maintenance_amd',
+                        'parallel', 'launch.py')
+    spec = importlib.util.spec_from_file_location('_mxamd_launch', path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.launch
 
 
 def main():
@@ -30,6 +38,7 @@ def main():
     args = ap.parse_args()
     if not args.command:
         ap.error('no command given')
+    launch = _load_launch()
     sys.exit(launch(args.command, args.num_workers, master_addr=args.master_addr,
                     master_port=args.master_port, timeout=args.timeout))
 

@@ -13,7 +13,7 @@ def classify(name):
     if 'igemm' in n or 'conv' in n or 'gemm' in n or 'ck::' in n or 'xdl' in n or 'cijk' in n:
         return 'conv/gemm (MIOpen/hipBLASLt)'
     if 'attn' in n or 'fmha' in n or 'flash' in n or 'attention' in n:
-        return 'attention (torch SDPA)'
+        return 'attention (in-tree MFMA attn_* / SDPA)'
     if 'multibox' in n:
         return 'detection (MultiBoxTarget)'
     if 'bn_' in n or 'batch_norm' in n:
