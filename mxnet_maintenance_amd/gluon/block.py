@@ -35,144 +35,169 @@ from .utils import _indent, _brief_print_list, HookHandle
 __all__ = ['Block', 'HybridBlock', 'SymbolBlock']
 
 
-class _BlockScope:
-    """Scope for collecting child Blocks and assigning name prefixes."""
-    _current = threading.local()
+# ---------------------------------------------------------------------------------------------
+# naming: a thread-local stack of the blocks whose name_scope() is open.  A block created inside
+# an open scope is named after its class (``dense0_``, ``dense1_`` ... counted per enclosing
+# block) under the enclosing block's prefix, and its ParameterDict shares the enclosing block's
+# shared-parameter table; outside any scope the global NameManager numbers it.
+# ---------------------------------------------------------------------------------------------
+_OPEN_SCOPES = threading.local()
+
+
+def _scope_stack():
+    st = getattr(_OPEN_SCOPES, 'stack', None)
+    if st is None:
+        st = _OPEN_SCOPES.stack = []
+    return st
+
+
+def _resolve_names(hint, prefix, params):
+    """(full prefix, ParameterDict) of a new block (the reference's naming rules)."""
+    stack = _scope_stack()
+    parent = stack[-1] if stack else None
+    if parent is None:
+        full = prefix if prefix is not None else _name.NameManager.current().get(None, hint) + '_'
+        shared = None if params is None else params
+        pd = ParameterDict(full) if shared is None else ParameterDict(shared.prefix, shared)
+        return full, pd
+    if prefix is None:
+        n = parent._child_counts.get(hint, 0)
+        parent._child_counts[hint] = n + 1
+        prefix = '%s%d_' % (hint, n)
+    if params is None:
+        pd = ParameterDict(parent.params.prefix + prefix, parent.params._shared)
+    else:
+        pd = ParameterDict(params.prefix, params)
+    return parent.prefix + prefix, pd
+
+
+class _NameScopeGuard:
+    """``with block.name_scope():`` -- children created inside are named under ``block``."""
 
     def __init__(self, block):
         self._block = block
-        self._counter = {}
-        self._old_scope = None
-        self._name_scope = None
-
-    @staticmethod
-    def create(prefix, params, hint):
-        current = getattr(_BlockScope._current, 'value', None)
-        if current is None:
-            if prefix is None:
-                prefix = _name.NameManager.current().get(None, hint) + '_'
-            if params is None:
-                params = ParameterDict(prefix)
-            else:
-                params = ParameterDict(params.prefix, params)
-            return prefix, params
-        if prefix is None:
-            count = current._counter.get(hint, 0)
-            prefix = '%s%d_' % (hint, count)
-            current._counter[hint] = count + 1
-        if params is None:
-            parent = current._block.params
-            params = ParameterDict(parent.prefix + prefix, parent._shared)
-        else:
-            params = ParameterDict(params.prefix, params)
-        return current._block.prefix + prefix, params
+        self._prefix_scope = None
 
     def __enter__(self):
         if self._block._empty_prefix:
             return self
-        self._old_scope = getattr(_BlockScope._current, 'value', None)
-        _BlockScope._current.value = self
-        self._name_scope = _name.Prefix(self._block.prefix)
-        self._name_scope.__enter__()
+        _scope_stack().append(self._block)
+        self._prefix_scope = _name.Prefix(self._block.prefix)
+        self._prefix_scope.__enter__()
         return self
 
     def __exit__(self, ptype, value, trace):
         if self._block._empty_prefix:
             return
-        self._name_scope.__exit__(ptype, value, trace)
-        self._name_scope = None
-        _BlockScope._current.value = self._old_scope
+        self._prefix_scope.__exit__(ptype, value, trace)
+        self._prefix_scope = None
+        stack = _scope_stack()
+        if stack and stack[-1] is self._block:
+            stack.pop()
 
 
+# ---------------------------------------------------------------------------------------------
+# nested inputs / outputs of a HybridBlock <-> a flat list of NDArray / Symbol, plus a structure
+# spec to rebuild the nesting: 'x' one array, None a None, ('n', k) a k-output Symbol, or a list
+# of specs for a list / tuple.
+# ---------------------------------------------------------------------------------------------
 def _flatten(args, inout_str):
     if isinstance(args, NDArray):
-        return [args], int(0)
+        return [args], 'x'
     if isinstance(args, Symbol):
-        length = len(args.list_outputs())
-        length = length if length > 1 else 0
-        return [args], int(length)
+        k = len(args.list_outputs())
+        return [args], ('n', k) if k > 1 else 'x'
     if args is None:
-        return [None], int(-1)
+        return [None], None
     if not isinstance(args, (list, tuple)):
         raise AssertionError('HybridBlock %s must be (nested) list of Symbol or NDArray, but got %s of type %s'
                              % (inout_str, str(args), str(type(args))))
-    flat, fmts = [], []
-    for i in args:
-        arg, fmt = _flatten(i, inout_str)
-        flat.extend(arg)
-        fmts.append(fmt)
-    return flat, fmts
+    flat, spec = [], []
+    for item in args:
+        f, sp = _flatten(item, inout_str)
+        flat += f
+        spec.append(sp)
+    return flat, spec
 
 
-def _regroup(args, fmt):
-    if isinstance(fmt, int):
-        if fmt == 0:
-            return args[0], args[1:]
-        if fmt == -1:
-            if args[0] is not None:
-                raise ValueError('We do not support passing types that are not None when the initial HybridBlock '
-                                 'has received NoneType and has been hybridized.')
-            return None, args[1:]
-        return args[:fmt], args[fmt:]
-    ret = []
-    for i in fmt:
-        res, args = _regroup(args, i)
-        ret.append(res)
-    return ret, args
+def _regroup(flat, spec):
+    """Inverse of _flatten: (rebuilt structure, the unconsumed rest of ``flat``)."""
+    if spec == 'x':
+        return flat[0], flat[1:]
+    if spec is None:
+        if flat[0] is not None:
+            raise ValueError('We do not support passing types that are not None when the initial HybridBlock '
+                             'has received NoneType and has been hybridized.')
+        return None, flat[1:]
+    if isinstance(spec, tuple):
+        return flat[:spec[1]], flat[spec[1]:]
+    out = []
+    for sp in spec:
+        item, flat = _regroup(flat, sp)
+        out.append(item)
+    return out, flat
+
+
+def _blocks_inside(obj):
+    """Blocks held (at any depth) by a list / tuple / dict attribute."""
+    if isinstance(obj, Block):
+        yield obj
+    elif isinstance(obj, dict):
+        for v in obj.values():
+            yield from _blocks_inside(v)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            yield from _blocks_inside(v)
 
 
 class Block:
-    """Base class for all neural network layers and models."""
+    """Base class for all neural network layers and models.
+
+    A block owns its directly registered Parameters (``_reg_params``, attribute name -> Parameter)
+    and child blocks (``_children``, registration name -> Block); the structural parameter names
+    used by save/load_parameters are the dotted attribute paths through that tree."""
 
     def __init__(self, prefix=None, params=None):
         self._empty_prefix = prefix == ''
-        self._prefix, self._params = _BlockScope.create(prefix, params, self._alias())
+        self._child_counts = {}
+        self._prefix, self._params = _resolve_names(self._alias(), prefix, params)
         self._name = self._prefix[:-1] if self._prefix.endswith('_') else self._prefix
-        self._scope = _BlockScope(self)
+        self._scope = _NameScopeGuard(self)
         self._children = OrderedDict()
         self._reg_params = {}
         self._forward_hooks = OrderedDict()
         self._forward_pre_hooks = OrderedDict()
 
     def __repr__(self):
-        s = '{name}(\n{modstr}\n)'
-        modstr = '\n'.join(['  ({key}): {block}'.format(key=key, block=_indent(block.__repr__(), 2))
-                            for key, block in self.__dict__.items() if isinstance(block, Block)])
-        return s.format(name=self.__class__.__name__, modstr=modstr)
+        lines = ['  ({}): {}'.format(k, _indent(repr(v), 2)) for k, v in self.__dict__.items()
+                 if isinstance(v, Block)]
+        return '{}(\n{}\n)'.format(self.__class__.__name__, '\n'.join(lines))
 
     def __setattr__(self, name, value):
-        if hasattr(self, name):
-            existing = getattr(self, name)
-            if isinstance(existing, (Parameter, Block)) and not isinstance(value, type(existing)):
-                raise TypeError('Changing attribute type for {name} from {type1} to {type2} is not allowed.'
-                                .format(name=name, type1=type(existing), type2=type(value)))
+        old = getattr(self, name, None)
+        if isinstance(old, (Parameter, Block)) and not isinstance(value, type(old)):
+            raise TypeError('Changing attribute type for {name} from {type1} to {type2} is not allowed.'
+                            .format(name=name, type1=type(old), type2=type(value)))
         if isinstance(value, Block):
             self.register_child(value, name)
         elif isinstance(value, Parameter):
-            assert name not in self._reg_params, \
-                'Overriding Parameter attribute %s is not allowed. If you want to share parameters between ' \
-                'blocks, please set \'params\' at Block construction instead.'
+            if name in self._reg_params:
+                raise AssertionError("Overriding Parameter attribute %s is not allowed. If you want to share "
+                                     "parameters between blocks, please set 'params' at Block construction "
+                                     "instead." % name)
             self._reg_params[name] = value
-        super().__setattr__(name, value)
+        object.__setattr__(self, name, value)
 
     def _check_container_with_block(self):
-        children = set(self._children.values())
-
-        def _find_unregistered_block_in_container(data):
-            if isinstance(data, (list, tuple)):
-                return any(_find_unregistered_block_in_container(e) for e in data)
-            if isinstance(data, dict):
-                return any(_find_unregistered_block_in_container(v) for v in data.values())
-            if isinstance(data, Block):
-                return data not in children
-            return False
-        for k, v in self.__dict__.items():
-            if isinstance(v, (list, tuple, dict)) and not (k.startswith('__') or k == '_children'):
-                if _find_unregistered_block_in_container(v):
-                    warnings.warn('"{name}" is an unregistered container with Blocks. Note that Blocks inside the '
-                                  'list, tuple or dict will not be registered automatically. Make sure to register '
-                                  'them using register_child() or switching to nn.Sequential/nn.HybridSequential '
-                                  'instead. '.format(name=self.__class__.__name__ + '.' + k), stacklevel=3)
+        registered = {id(b) for b in self._children.values()}
+        for attr, val in self.__dict__.items():
+            if attr.startswith('__') or attr == '_children' or not isinstance(val, (list, tuple, dict)):
+                continue
+            if any(id(b) not in registered for b in _blocks_inside(val)):
+                warnings.warn('"{name}" is an unregistered container with Blocks. Note that Blocks inside the '
+                              'list, tuple or dict will not be registered automatically. Make sure to register '
+                              'them using register_child() or switching to nn.Sequential/nn.HybridSequential '
+                              'instead. '.format(name=self.__class__.__name__ + '.' + attr), stacklevel=3)
 
     def _alias(self):
         return self.__class__.__name__.lower()
@@ -192,35 +217,40 @@ class Block:
     def params(self):
         return self._params
 
+    def _walk(self):
+        """This block and every descendant, parents first (children in registration order)."""
+        todo = [self]
+        while todo:
+            blk = todo.pop()
+            yield blk
+            todo.extend(reversed(list(blk._children.values())))
+
     def collect_params(self, select=None):
+        """ParameterDict of this block's and all descendants' Parameters (``select``: regex on names)."""
         self._check_container_with_block()
-        ret = ParameterDict(self._params.prefix)
-        if not select:
-            ret.update(self.params)
-        else:
-            pattern = re.compile(select)
-            ret.update({name: value for name, value in self.params.items() if pattern.match(name)})
-        for cld in self._children.values():
-            ret.update(cld.collect_params(select=select))
-        return ret
+        out = ParameterDict(self._params.prefix)
+        keep = re.compile(select).match if select else None
+        for blk in self._walk():
+            out.update({k: v for k, v in blk.params.items() if keep is None or keep(k)})
+        return out
 
     def _collect_params_with_prefix(self, prefix=''):
-        if prefix:
-            prefix += '.'
-        ret = {prefix + key: val for key, val in self._reg_params.items()}
-        for name, child in self._children.items():
-            ret.update(child._collect_params_with_prefix(prefix + name))
-        return ret
+        """Structural name ('child.grandchild.attr') -> Parameter."""
+        base = prefix + '.' if prefix else ''
+        found = {base + attr: p for attr, p in self._reg_params.items()}
+        for cname, child in self._children.items():
+            found.update(child._collect_params_with_prefix(base + cname))
+        return found
 
     def save_parameters(self, filename, deduplicate=False):
-        params = self._collect_params_with_prefix()
+        """Save parameters under their structural names (``deduplicate``: a shared Parameter once)."""
+        named = self._collect_params_with_prefix()
         if deduplicate:
-            reverse = {}
-            for k, v in params.items():
-                reverse.setdefault(v, []).append(k)
-            params = {v[0]: k for k, v in reverse.items()}
-        arg_dict = {key: val._reduce() for key, val in params.items()}
-        ndarray.save(filename, arg_dict)
+            first = {}
+            for key, p in named.items():
+                first.setdefault(id(p), (key, p))
+            named = dict(first.values())
+        ndarray.save(filename, {key: p._reduce() for key, p in named.items()})
 
     def save_params(self, filename):
         warnings.warn('save_params is deprecated. Please use save_parameters. Note that if you want load from '
@@ -232,31 +262,36 @@ class Block:
 
     def load_parameters(self, filename, ctx=None, allow_missing=False, ignore_extra=False, cast_dtype=False,
                         dtype_source='current'):
+        """Load a save_parameters file (structural names) or, for files with prefixed names, fall back
+        to ParameterDict.load with this block's prefix stripped."""
         loaded = ndarray.load(filename) if isinstance(filename, str) else filename
-        params = self._collect_params_with_prefix()
-        if not loaded and not params:
+        mine = self._collect_params_with_prefix()
+        if not loaded and not mine:
             return
-        if not any('.' in i for i in loaded.keys()):
-            # legacy loading (prefix-named parameters)
-            loaded = None
+        if all('.' not in key for key in loaded):
             self.collect_params().load(filename, ctx, allow_missing, ignore_extra, self.prefix,
                                        cast_dtype=cast_dtype, dtype_source=dtype_source)
             return
         if not allow_missing:
-            params_inv = {}
-            for k, v in params.items():
-                params_inv.setdefault(v, []).append(k)
-            for name, param in params.items():
-                assert any(p in loaded for p in params_inv[param]), \
-                    "Parameter '%s' is missing in file '%s', which contains parameters: %s. Set allow_missing=True " \
-                    "to ignore missing parameters." % (name, filename, _brief_print_list(loaded.keys()))
-        for name in loaded:
-            if not ignore_extra and name not in params:
+            # a shared Parameter is satisfied by any of its structural names
+            aliases = {}
+            for key, p in mine.items():
+                aliases.setdefault(id(p), []).append(key)
+            for key, p in mine.items():
+                if not any(a in loaded for a in aliases[id(p)]):
+                    raise AssertionError(
+                        "Parameter '%s' is missing in file '%s', which contains parameters: %s. Set "
+                        "allow_missing=True to ignore missing parameters." % (key, filename,
+                                                                             _brief_print_list(loaded.keys())))
+        if not ignore_extra:
+            extra = next((key for key in loaded if key not in mine), None)
+            if extra is not None:
                 raise ValueError("Parameter '%s' loaded from file '%s' is not present in ParameterDict, which "
                                  "contains parameters %s. Set ignore_extra=True to ignore. " % (
-                                     name, filename, _brief_print_list(self._params.keys())))
-            if name in params:
-                params[name]._load_init(loaded[name], ctx, cast_dtype=cast_dtype, dtype_source=dtype_source)
+                                     extra, filename, _brief_print_list(self._params.keys())))
+        for key, value in loaded.items():
+            if key in mine:
+                mine[key]._load_init(value, ctx, cast_dtype=cast_dtype, dtype_source=dtype_source)
 
     def load_params(self, filename, ctx=None, allow_missing=False, ignore_extra=False):
         warnings.warn('load_params is deprecated. Please use load_parameters.')
@@ -267,23 +302,24 @@ class Block:
         self.load_parameters(param_dict, ctx, allow_missing, ignore_extra, cast_dtype, dtype_source)
 
     def register_child(self, block, name=None):
-        if name is None:
-            name = str(len(self._children))
-        self._children[name] = block
+        self._children[str(len(self._children)) if name is None else name] = block
 
     def register_forward_pre_hook(self, hook):
-        handle = HookHandle()
-        handle.attach(self._forward_pre_hooks, hook)
-        return handle
+        """``hook(block, inputs)`` before every forward; returns a detachable handle."""
+        h = HookHandle()
+        h.attach(self._forward_pre_hooks, hook)
+        return h
 
     def register_forward_hook(self, hook):
-        handle = HookHandle()
-        handle.attach(self._forward_hooks, hook)
-        return handle
+        """``hook(block, inputs, outputs)`` after every forward; returns a detachable handle."""
+        h = HookHandle()
+        h.attach(self._forward_hooks, hook)
+        return h
 
     def apply(self, fn):
-        for cld in self._children.values():
-            cld.apply(fn)
+        """``fn(block)`` on every descendant (children first) and then on this block."""
+        for child in self._children.values():
+            child.apply(fn)
         fn(self)
         return self
 
@@ -291,14 +327,14 @@ class Block:
         self.collect_params().initialize(init, ctx, verbose, force_reinit)
 
     def hybridize(self, active=True, **kwargs):
-        for cld in self._children.values():
-            cld.hybridize(active, **kwargs)
+        for child in self._children.values():
+            child.hybridize(active, **kwargs)
 
     def cast(self, dtype):
         for child in self._children.values():
             child.cast(dtype)
-        for _, param in self.params.items():
-            param.cast(dtype)
+        for p in self.params.values():
+            p.cast(dtype)
 
     def zero_grad(self):
         self.collect_params().zero_grad()
@@ -307,110 +343,87 @@ class Block:
         self.collect_params().reset_ctx(ctx)
 
     def __call__(self, *args):
-        for hook in self._forward_pre_hooks.values():
-            hook(self, args)
+        for pre in list(self._forward_pre_hooks.values()):
+            pre(self, args)
         out = self.forward(*args)
-        for hook in self._forward_hooks.values():
-            hook(self, args, out)
+        for post in list(self._forward_hooks.values()):
+            post(self, args, out)
         return out
 
     def forward(self, *args):
         raise NotImplementedError
 
     def register_op_hook(self, callback, monitor_all=False):
-        for cld in self._children.values():
-            cld.register_op_hook(callback, monitor_all)
+        for child in self._children.values():
+            child.register_op_hook(callback, monitor_all)
 
     def summary(self, *inputs):
-        summary = OrderedDict()
-        seen = set()
-        hooks = []
+        """Print a per-layer table (output shapes, parameter counts) from one forward on ``inputs``."""
+        _LayerTable(self).run(inputs)
 
-        def _get_shape_str(args):
-            def flatten(args):
-                if not isinstance(args, (list, tuple)):
-                    return [args], int(0)
-                flat, fmts = [], []
-                for i in args:
-                    arg, fmt = flatten(i)
-                    flat.extend(arg)
-                    fmts.append(fmt)
-                return flat, fmts
 
-            def regroup(args, fmt):
-                if isinstance(fmt, int):
-                    if fmt == 0:
-                        return args[0], args[1:]
-                    return args[:fmt], args[fmt:]
-                ret = []
-                for i in fmt:
-                    res, args = regroup(args, i)
-                    ret.append(res)
-                return ret, args
-            flat_args, fmts = flatten(args)
-            flat_arg_shapes = [x.shape if isinstance(x, NDArray) else x for x in flat_args]
-            shapes = regroup(flat_arg_shapes, fmts)[0]
-            if isinstance(shapes, list):
-                shape_str = str(shapes)[1:-1]
-            else:
-                shape_str = str(shapes)
-            return shape_str.replace('L', '')
+def _shape_text(value):
+    """Shapes of a (nested) output, printed like the reference summary."""
+    def shapes(v):
+        if isinstance(v, (list, tuple)):
+            return [shapes(e) for e in v]
+        return v.shape if isinstance(v, NDArray) else v
+    s = shapes(value)
+    return (str(s)[1:-1] if isinstance(s, list) else str(s)).replace('L', '')
 
-        def _register_summary_hook(block):
-            assert not isinstance(block, HybridBlock) or not block._active, \
-                '"{}" must not be hybridized to print summary.'.format(block.name)
 
-            def _summary_hook(block, _, outputs):
-                class_name = block.__class__.__name__
-                block_idx = len(summary) - 1
-                m_key = '%s-%i' % (class_name, block_idx + 1)
-                summary[m_key] = OrderedDict()
-                summary[m_key]['output_shape'] = _get_shape_str(outputs)
-                params = 0
-                summary[m_key]['trainable'] = 0
-                summary[m_key]['shared'] = 0
-                for p in block.params.values():
-                    params += p.data().size
-                    summary[m_key]['trainable'] += 0 if p.grad_req == 'null' else p.data().size
-                    if p in seen:
-                        summary[m_key]['shared'] += p.data().size
-                    else:
-                        seen.add(p)
-                summary[m_key]['n_params'] = params
-            from .nn.basic_layers import Sequential, HybridSequential
-            if not isinstance(block, (Sequential, HybridSequential)):
-                hooks.append(block.register_forward_hook(_summary_hook))
+class _LayerTable:
+    """Collects one row per non-container block through forward hooks, then prints the table."""
 
-        summary['Input'] = OrderedDict()
-        summary['Input']['output_shape'] = _get_shape_str(inputs)
-        summary['Input']['n_params'] = 0
-        summary['Input']['trainable'] = 0
-        summary['Input']['shared'] = 0
+    def __init__(self, root):
+        self.root = root
+        self.rows = []            # (label, output shape text, #params, #trainable, #shared)
+        self.seen = set()
+        self.handles = []
+
+    def _on_forward(self, block, _inputs, outputs):
+        total = trainable = shared = 0
+        for p in block.params.values():
+            n = p.data().size
+            total += n
+            trainable += 0 if p.grad_req == 'null' else n
+            if id(p) in self.seen:
+                shared += n
+            self.seen.add(id(p))
+        label = '%s-%i' % (block.__class__.__name__, len(self.rows))
+        self.rows.append((label, _shape_text(outputs), total, trainable, shared))
+
+    def _attach(self, block):
+        if isinstance(block, HybridBlock) and block._active:
+            raise AssertionError('"{}" must not be hybridized to print summary.'.format(block.name))
+        from .nn.basic_layers import Sequential, HybridSequential
+        if not isinstance(block, (Sequential, HybridSequential)):
+            self.handles.append(block.register_forward_hook(self._on_forward))
+
+    def run(self, inputs):
+        self.rows.append(('Input', _shape_text(inputs), 0, 0, 0))
         try:
-            self.apply(_register_summary_hook)
-            self(*inputs)
-            line_format = '{:>20}  {:>42} {:>15}'
+            self.root.apply(self._attach)
+            self.root(*inputs)
+            fmt = '{:>20}  {:>42} {:>15}'
             print('-' * 80)
-            print(line_format.format('Layer (type)', 'Output Shape', 'Param #'))
+            print(fmt.format('Layer (type)', 'Output Shape', 'Param #'))
             print('=' * 80)
-            total_params = 0
-            trainable_params = 0
-            shared_params = 0
-            for layer in summary:
-                print(line_format.format(layer, str(summary[layer]['output_shape']), summary[layer]['n_params']))
-                total_params += summary[layer]['n_params']
-                trainable_params += summary[layer]['trainable']
-                shared_params += summary[layer]['shared']
+            for label, shape, n, _t, _s in self.rows:
+                print(fmt.format(label, str(shape), n))
+            total = sum(r[2] for r in self.rows)
+            trainable = sum(r[3] for r in self.rows)
+            shared = sum(r[4] for r in self.rows)
             print('=' * 80)
             print('Parameters in forward computation graph, duplicate included')
-            print('   Total params: ' + str(total_params))
-            print('   Trainable params: ' + str(trainable_params))
-            print('   Non-trainable params: ' + str(total_params - trainable_params))
-            print('Shared params in forward computation graph: ' + str(shared_params))
-            print('Unique parameters in model: ' + str(total_params - shared_params))
+            print('   Total params: ' + str(total))
+            print('   Trainable params: ' + str(trainable))
+            print('   Non-trainable params: ' + str(total - trainable))
+            print('Shared params in forward computation graph: ' + str(shared))
+            print('Unique parameters in model: ' + str(total - shared))
             print('-' * 80)
         finally:
-            for h in hooks:
+            for h in self.handles:
                 h.detach()
 
 
@@ -547,10 +560,10 @@ class HybridBlock(Block):
         args, fmt = _flatten(args, 'input')
         if fmt != self._in_format:
             if len(self._in_format) > len(fmt):
-                valid = all([self._in_format[i] == -1 for i in range(len(fmt), len(self._in_format))])
+                valid = all([self._in_format[i] is None for i in range(len(fmt), len(self._in_format))])
                 valid = valid and (fmt == self._in_format[:len(fmt)])
             elif len(self._in_format) < len(fmt):
-                valid = all([fmt[i] == -1 for i in range(len(self._in_format), len(fmt))])
+                valid = all([fmt[i] is None for i in range(len(self._in_format), len(fmt))])
                 valid = valid and (fmt[:len(self._in_format)] == self._in_format)
             else:
                 valid = False

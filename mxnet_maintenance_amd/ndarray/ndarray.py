@@ -255,7 +255,7 @@ class NDArray:
             out = NDArray(t.clone() if t.data_ptr() == self._data.data_ptr() else t)
             out._host_ctx = context
             return out
-        return _invoke_unary(lambda t: t.to(context.torch_device), self)
+        return _tag_host_ctx(_invoke_unary(lambda t: t.to(context.torch_device), self), context)
 
     as_in_ctx = as_in_context
 
@@ -698,6 +698,18 @@ def _ctx(ctx):
     return ctx if ctx is not None else current_context()
 
 
+def _tag_host_ctx(arr, ctx):
+    """Label a host array with a virtual CPU context (``cpu(k)``, k > 0): every CPU context is the same
+    host memory here, but an array created or placed on ``cpu(k)`` reports that context, as in the
+    reference, which keeps one storage pool per CPU device id."""
+    if isinstance(ctx, str):
+        ctx = Context(ctx)
+    if (isinstance(ctx, Context) and ctx.device_typeid == 1 and ctx.device_id != 0
+            and arr._data.device.type == 'cpu'):
+        arr._host_ctx = ctx
+    return arr
+
+
 def array(source_array, ctx=None, dtype=None):
     """Create an NDArray from any array-like (float32 by default, like MXNet)."""
     ctx = _ctx(ctx)
@@ -726,7 +738,7 @@ def array(source_array, ctx=None, dtype=None):
             out = NDArray(t)
             out._host_ctx = ctx
             return out
-    return NDArray(t.to(ctx.torch_device) if ctx.device_typeid == 2 else t)
+    return _tag_host_ctx(NDArray(t.to(ctx.torch_device) if ctx.device_typeid == 2 else t), ctx)
 
 
 def from_numpy(ndarray, zero_copy=True):

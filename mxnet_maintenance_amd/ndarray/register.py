@@ -122,6 +122,12 @@ def invoke(op, inputs, attrs, out=None):
     else:
         outs = [NDArray(res)]
     _np_wrap(inputs, outs)
+    hctx = attrs.get('ctx') if 'ctx' in attrs else next(
+        (x._host_ctx for x in inputs if x is not None and getattr(x, '_host_ctx', None) is not None), None)
+    if hctx is not None:
+        from .ndarray import _tag_host_ctx
+        for o in outs:
+            _tag_host_ctx(o, hctx)
     if out is not None:
         targets = out if isinstance(out, (list, tuple)) else [out]
         for t, o in zip(targets, outs):
