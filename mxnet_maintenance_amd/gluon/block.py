@@ -138,6 +138,15 @@ def _regroup(flat, spec):
     return out, flat
 
 
+def _leaves(obj):
+    """Non-container items of a nested list / tuple of call arguments."""
+    if isinstance(obj, (list, tuple)):
+        for v in obj:
+            yield from _leaves(v)
+    else:
+        yield obj
+
+
 def _blocks_inside(obj):
     """Blocks held (at any depth) by a list / tuple / dict attribute."""
     if isinstance(obj, Block):
@@ -687,32 +696,40 @@ class HybridBlock(Block):
             cld._monitor_all = monitor_all
 
     def forward(self, x, *args):
-        flat, _ = _flatten([x] + list(args), 'input')
-        kinds = {type(a) is not None and (isinstance(a, Symbol) and 'sym' or isinstance(a, NDArray) and 'nd')
-                 for a in flat if a is not None}
-        kinds.discard(False)
-        if not kinds:
+        leaves = list(_leaves([x] + list(args)))
+        arrays = [a for a in leaves if isinstance(a, NDArray)]
+        syms = [a for a in leaves if isinstance(a, Symbol)]
+        if not arrays and not syms:
             raise ValueError('In HybridBlock, there must be one NDArray or one Symbol in the input. '
                              'Please check the type of the args.')
-        if len(kinds) > 1:
+        if arrays and syms:
             raise ValueError('In HybridBlock, we do not support mixed NDArrays and Symbols types for the input.')
-        has_symbol = 'sym' in kinds
-        if not has_symbol and (isinstance(x, NDArray) or any(isinstance(a, NDArray) for a in args)):
-            first = x if isinstance(x, NDArray) else next(a for a in args if isinstance(a, NDArray))
-            ctx = first.context
-            if self._active:
-                return self._call_cached_op(x, *args)
-            try:
-                params = {k: v.data(ctx) for k, v in self._reg_params.items()}
-            except DeferredInitializationError:
-                self._deferred_infer_shape(x, *args)
-                for _, v in self.params.items():
-                    v._finish_deferred_init()
-                params = {k: v.data(ctx) for k, v in self._reg_params.items()}
-            return self.hybrid_forward(ndarray, x, *args, **params)
-        params = {i: j.var() for i, j in self._reg_params.items()}
-        with self.name_scope():
-            return self.hybrid_forward(symbol, x, *args, **params)
+        if syms:
+            params = {i: j.var() for i, j in self._reg_params.items()}
+            with self.name_scope():
+                return self.hybrid_forward(symbol, x, *args, **params)
+        ctx = arrays[0].context
+        if self._active:
+            # a cached graph takes only arrays (or None) and runs on one device
+            odd = next((a for a in leaves if a is not None and not isinstance(a, NDArray)), None)
+            if odd is not None:
+                raise ValueError('A hybridized HybridBlock only takes NDArray (or None) inputs, but got %r of type '
+                                 '%s. Use a non-hybridized block for scalar arguments.' % (odd, type(odd)))
+            host = {1, 3, 5}
+            devs = {(1, 0) if a.context.device_typeid in host and a.context.device_typeid != 1 else
+                    (a.context.device_typeid, a.context.device_id) for a in arrays}
+            if len(devs) > 1:
+                raise ValueError('A hybridized HybridBlock needs all input arrays on one context, got %s'
+                                 % sorted({str(a.context) for a in arrays}))
+            return self._call_cached_op(x, *args)
+        try:
+            params = {k: v.data(ctx) for k, v in self._reg_params.items()}
+        except DeferredInitializationError:
+            self._deferred_infer_shape(x, *args)
+            for _, v in self.params.items():
+                v._finish_deferred_init()
+            params = {k: v.data(ctx) for k, v in self._reg_params.items()}
+        return self.hybrid_forward(ndarray, x, *args, **params)
 
     def hybrid_forward(self, F, x, *args, **kwargs):
         raise NotImplementedError

@@ -38,7 +38,10 @@ def _bn(layout, relu=False, fuse=False, **kw):
 
 
 class _ResidualTail(_BatchNorm):
-    """relu(BN(x) + shortcut) of a residual block; one fused HIP kernel when ``fuse``."""
+    """relu(BN(x) + shortcut) of a residual block: one fused HIP kernel when ``fuse``; otherwise this
+    block is the plain BN and the owning residual block adds and activates (``_finish``), so the
+    add / relu symbols are named in the stage's scope as in the reference model zoo
+    (``..._stage1_activation0``)."""
 
     def __init__(self, layout, fuse, **kwargs):
         super().__init__(axis=_bn_axis(layout), **kwargs)
@@ -51,8 +54,12 @@ class _ResidualTail(_BatchNorm):
         if self._fuse_add:
             return F.contrib.BatchNormAddReLU(x, shortcut, gamma, beta, running_mean, running_var, name='fwd',
                                               **self._kwargs)
-        y = F.BatchNorm(x, gamma, beta, running_mean, running_var, name='fwd', **self._kwargs)
-        return F.Activation(y + shortcut, act_type='relu')
+        return F.BatchNorm(x, gamma, beta, running_mean, running_var, name='fwd', **self._kwargs)
+
+
+def _finish(F, tail, out, shortcut):
+    y = tail(out, shortcut)
+    return y if tail._fuse_add else F.Activation(y + shortcut, act_type='relu')
 
 
 class BasicBlockV1(HybridBlock):
@@ -74,7 +81,7 @@ class BasicBlockV1(HybridBlock):
 
     def hybrid_forward(self, F, x):
         shortcut = self.downsample(x) if self.downsample is not None else x
-        return self.tail(self.body(x), shortcut)
+        return _finish(F, self.tail, self.body(x), shortcut)
 
 
 class BottleneckV1(HybridBlock):
@@ -113,9 +120,9 @@ class BottleneckV1(HybridBlock):
             for b in blocks[1:]:
                 out = b(out)
             shortcut = self.downsample(passthrough) if self.downsample is not None else passthrough
-            return self.tail(out, shortcut)
+            return _finish(F, self.tail, out, shortcut)
         shortcut = self.downsample(x) if self.downsample is not None else x
-        return self.tail(self.body(x), shortcut)
+        return _finish(F, self.tail, self.body(x), shortcut)
 
 
 class BottleneckV1b(BottleneckV1):

@@ -236,18 +236,27 @@ class Parameter:
             self._slot.setdefault(_ctx_key(c), i)
         src = data._data.detach() if isinstance(data, NDArray) else torch.as_tensor(np.asarray(data))
         td = torch_dtype(self.dtype)
+        # replicas are dense tensors (autograd and the kvstore work on them); a sparse parameter's
+        # replicas carry its storage type
         self._data = [_tag_host_ctx(NDArray(src.to(device=c.torch_device, dtype=td, copy=True)), c)
                       for c in self._ctx_list]
+        for arr in self._data:
+            arr._stype = self._stype
         self._init_grad()
 
     def _init_grad(self):
         if self._grad_req == 'null':
             self._grad = None
             return
-        gst = None if self._grad_stype == 'default' else self._grad_stype
-        for arr in self._data:
-            arr.attach_grad(self._grad_req, stype=gst)
-        self._grad = [arr._grad for arr in self._data]
+        gst = self._grad_stype
+        if not self._data[0]._data.is_floating_point():
+            # integer parameters (e.g. quantized weights) have a gradient buffer that autograd never
+            # writes (torch cannot differentiate integer tensors)
+            self._grad = [NDArray(torch.zeros_like(arr._data)) for arr in self._data]
+        else:
+            for arr in self._data:
+                arr.attach_grad(self._grad_req, stype=gst)
+            self._grad = [arr._grad for arr in self._data]
         for arr, c in zip(self._grad, self._ctx_list):
             if arr is not None:
                 _tag_host_ctx(arr, c)
@@ -297,14 +306,18 @@ class Parameter:
             tr._reset_kvstore()
 
     def _reduce(self):
-        """One host copy of the value (replicas averaged; every row of a row_sparse parameter)."""
+        """One host copy of the value (replicas averaged; a row_sparse parameter as a RowSparseNDArray
+        holding every row)."""
         host = cpu()
-        if self._stype != 'default':
-            return self.row_sparse_data(nd.arange(self.shape[0], ctx=host))
         reps = self._all_data()
         if len(reps) == 1:
-            return self.data().copyto(host)
-        return nd.add_n(*[r.copyto(host) for r in reps]) / len(reps)
+            val = NDArray(reps[0]._data.detach().to('cpu', copy=True))
+        else:
+            val = nd.add_n(*[NDArray(r._data.detach().to('cpu', copy=True)) for r in reps]) / len(reps)
+        if self._stype == 'row_sparse':
+            from ..ndarray import sparse as _sp
+            return _sp.RowSparseNDArray(val._data, ctx=host)
+        return val
 
     def reset_ctx(self, ctx):
         """Move the replicas (or the pending initialisation) to ``ctx``."""
@@ -342,7 +355,25 @@ class Parameter:
         got = self._check_and_get(self._data, ctx)
         # only the requested rows are fetched from the kvstore into the local copies
         self._trainer._row_sparse_pull(self, got, row_id)
-        return got
+        if _state.STATE.recording:
+            # inside autograd.record() the replica itself (the leaf whose gradient the trainer reads)
+            return got
+        return [self._rows_view(a, row_id) for a in got] if isinstance(got, list) else self._rows_view(got, row_id)
+
+    @staticmethod
+    def _rows_view(arr, row_id):
+        """The requested rows of replica ``arr`` (others read as zero), as the reference's pulled
+        row_sparse copy holds only them."""
+        t = arr._data
+        rows = row_id._data.to(device=t.device, dtype=torch.int64).reshape(-1)
+        keep = torch.zeros(t.shape[0], dtype=t.dtype, device=t.device)
+        keep[rows] = 1
+        view = NDArray((t * keep.reshape((-1,) + (1,) * (t.dim() - 1))).detach())
+        view._stype = 'row_sparse'
+        hctx = getattr(arr, '_host_ctx', None)
+        if hctx is not None:
+            view._host_ctx = hctx
+        return view
 
     def row_sparse_data(self, row_id):
         """The rows ``row_id`` of a row_sparse parameter, on ``row_id``'s context."""

@@ -249,7 +249,10 @@ class KVStore(KVStoreBase):
             for k, o in zip(keys, outs):
                 src = self._store[k]._data
                 for oo in _as_list(o):
-                    oo._data.copy_(src.to(oo._data.device, oo._data.dtype))
+                    # written through .data: a pull into a parameter is an engine-ordered write in the
+                    # reference, not an autograd-visible in-place op on a recorded leaf
+                    if oo._data.data_ptr() != src.data_ptr():
+                        oo._data.data.copy_(src.to(oo._data.device, oo._data.dtype))
 
     def pushpull(self, key, value, out=None, priority=0):
         """Sum ``value`` over devices and workers and write the result to ``out``.
@@ -301,7 +304,7 @@ class KVStore(KVStoreBase):
                     else:
                         res = torch.zeros_like(oo._data)
                         res.index_copy_(0, idx.to(res.device), rows.to(res.device, res.dtype))
-                        oo._data.copy_(res)
+                        oo._data.data.copy_(res)
 
     def set_gradient_compression(self, compression_params):
         if 'device' in self._type or 'dist' in self._type or self._type in ('local', 'nccl'):

@@ -223,6 +223,12 @@ class NDArray:
         return _invoke_unary(lambda t: t.to(td) if t.dtype != td else t.clone(), self)
 
     def copy(self):
+        if self._stype != 'default' and type(self) is NDArray:
+            # a dense array tagged with a sparse storage type (a sparse Parameter's replica): its copy
+            # is a real sparse array of that type
+            from . import sparse
+            cls = sparse.RowSparseNDArray if self._stype == 'row_sparse' else sparse.CSRNDArray
+            return _tag_host_ctx(cls(self._data.detach().clone()), getattr(self, '_host_ctx', None))
         return _invoke_unary(lambda t: t.clone(), self)
 
     def __copy__(self):
@@ -782,7 +788,7 @@ def empty(shape, ctx=None, dtype=None, stype=None):
     if stype not in (None, 'default'):
         from . import sparse
         return sparse.empty(stype, shape, ctx=ctx, dtype=dtype)
-    return NDArray(torch.empty(shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device))
+    return _tag_host_ctx(NDArray(torch.empty(shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device)), ctx)
 
 
 def zeros(shape, ctx=None, dtype=None, stype=None, out=None, **kwargs):
@@ -791,19 +797,21 @@ def zeros(shape, ctx=None, dtype=None, stype=None, out=None, **kwargs):
     if stype not in (None, 'default'):
         from . import sparse
         return sparse.zeros(stype, shape, ctx=ctx, dtype=dtype)
-    return _into(out, NDArray(torch.zeros(shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device)))
+    return _into(out, _tag_host_ctx(NDArray(torch.zeros(shape, dtype=torch_dtype(dtype),
+                                                        device=_ctx(ctx).torch_device)), ctx))
 
 
 def ones(shape, ctx=None, dtype=None, out=None, **kwargs):
     if isinstance(shape, int):
         shape = (shape,)
-    return _into(out, NDArray(torch.ones(shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device)))
+    return _into(out, _tag_host_ctx(NDArray(torch.ones(shape, dtype=torch_dtype(dtype),
+                                                       device=_ctx(ctx).torch_device)), ctx))
 
 
 def full(shape, val, ctx=None, dtype=np.float32, out=None):
     if isinstance(shape, int):
         shape = (shape,)
-    r = NDArray(torch.full(shape, val, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device))
+    r = _tag_host_ctx(NDArray(torch.full(shape, val, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device)), ctx)
     if out is not None:
         out[:] = r
         return out

@@ -188,16 +188,18 @@ class Symbol:
             op = node.opdef()
             if op.output_names:
                 names.append('%s_%s' % (node.name, op.output_names[idx]))
-            elif node.num_outputs() == 1:
+            elif node.num_outputs() == 1 or (idx == 0 and node.num_visible_outputs() == 1):
+                # one (visible) output: BatchNorm's mean / var and Dropout's mask are hidden
                 names.append(node.name + '_output')
             else:
                 names.append('%s_output%d' % (node.name, idx))
         return names
 
     def get_internals(self):
+        """Every visible output of every node (nnvm GetInternals honours FNumVisibleOutputs)."""
         outs = []
         for n in self._topo():
-            k = n.num_outputs() if n.op is not None else 1
+            k = n.num_visible_outputs() if n.op is not None else 1
             for i in range(k):
                 outs.append((n, i))
         return Symbol(outs)
@@ -637,13 +639,16 @@ def var(name, attr=None, shape=None, lr_mult=None, wd_mult=None, dtype=None, ini
     if wd_mult is not None:
         attrs['__wd_mult__'] = str(wd_mult)
     if dtype is not None:
-        attrs['__dtype__'] = str(np.dtype(dtype).name if dtype != 'bfloat16' else 'bfloat16')
+        # the reference stores the mshadow type flag (python/mxnet/symbol/symbol.py var())
+        from ..base import dtype_to_flag
+        attrs['__dtype__'] = str(dtype_to_flag(dtype))
     if init is not None:
         if not isinstance(init, str):
             init = init.dumps()
         attrs['__init__'] = init
     if stype is not None:
-        attrs['__storage_type__'] = str(stype)
+        from ..ndarray.ndarray import _STORAGE_TYPE_STR_TO_ID
+        attrs['__storage_type__'] = str(_STORAGE_TYPE_STR_TO_ID.get(stype, stype))
     for k, v in kwargs.items():
         if k.startswith('__') and k.endswith('__'):
             attrs[k] = str(v)
@@ -715,6 +720,9 @@ def _attr_dtype(node):
     if d is None:
         return None
     try:
+        if isinstance(d, str) and d.lstrip('-').isdigit():
+            from ..base import flag_to_dtype
+            return flag_to_dtype(int(d)) if int(d) >= 0 else None
         return torch_dtype(d)
     except Exception:
         return None
