@@ -795,6 +795,13 @@ class SymbolBlock(HybridBlock):
         arg_params = out.list_arguments()
         aux_params = out.list_auxiliary_states()
         arg_types, aux_types = _infer_param_types(syms, out, arg_params, aux_params)
+        # a SymbolBlock holds dense Parameters only (reference: 'SymbolBlock doesn't support Parameter ...')
+        sparse_ids = ('1', '2', 'row_sparse', 'csr')
+        for node in out._topo():
+            if node.op is None and node.name not in input_names and \
+                    str(node.attrs.get('__storage_type__', '0')) in sparse_ids:
+                raise AssertionError("SymbolBlock doesn't support Parameter '%s' because its storage type is "
+                                     "not default." % node.name)
         for i, arg in enumerate(arg_params):
             if arg not in input_names:
                 self.params.get(arg, allow_deferred_init=True, dtype=arg_types[i])

@@ -283,7 +283,7 @@ class Parameter:
             if dtype_source == 'current':
                 data = data.astype(self.dtype, copy=False)
             else:
-                self._dtype = data.dtype
+                self.cast(data.dtype)      # the replicas take the saved dtype too
         want = None if ctx is None else _as_ctx_list(ctx)
         if self._data is None:
             if self._deferred_init is not None:

@@ -22,7 +22,7 @@ DEFAULT_REF = '/root/reference/tests/python'
 
 
 _STORE_CACHE = os.path.join(tempfile.gettempdir(), 'mxref_model_store')
-_SYNTHETIC_MODELS = ('resnet18_v1',)
+_SYNTHETIC_MODELS = ('resnet18_v1', 'resnet34_v2')   # random-init weights (no network): structure only
 
 
 def _synthetic_model_store(dst, env):
