@@ -16,6 +16,13 @@ class MXNetError(RuntimeError):
     """Error raised by the framework (mirrors mxnet.base.MXNetError)."""
 
 
+class AsyncOpError(MXNetError):
+    """Failure inside an operator's *execution* (not its argument / shape checks).  As with the
+    reference's threaded engine, the imperative layer does not raise it at the call: the outputs are
+    marked failed and the error surfaces at the next synchronisation point that touches them
+    (``wait_to_read`` / ``asnumpy`` / ``mx.nd.waitall``)."""
+
+
 class NotImplementedForSymbol(MXNetError):
     def __init__(self, function, alias, *args):
         super().__init__()

@@ -107,6 +107,69 @@ def wait_all():
         _engine.wait_for_all()
 
 
+# ------------------------------------------------------------------ deferred operator failures
+# Reference semantics (src/engine/threaded_engine.cc): an operator that fails on a worker stores
+# the exception on its output variables; any operator reading such a variable fails the same way;
+# WaitForVar rethrows (and clears) a variable's exception, WaitForAll rethrows the first one and
+# clears them all.  Here a failed output carries a shared one-slot "box" holding the exception
+# (views of an array share it, like the reference's shared variable).
+_failed = []          # boxes whose exception has not been rethrown yet
+_failed_lock = threading.Lock()
+
+
+def record_failure(exc):
+    """A new failure box for ``exc``, registered for the next ``waitall``."""
+    box = [exc]
+    with _failed_lock:
+        _failed.append(box)
+    return box
+
+
+# Every sampler writes the shared random-number resource (the reference's kRandom resource
+# variable), so a sampler that fails leaves its failure on that resource and the samplers after it
+# fail the same way (sharing the box) until the failure is rethrown somewhere.
+_rng_box = [None]
+
+
+def rng_failure():
+    """The failure box held by the random resource, if still pending."""
+    b = _rng_box[0]
+    return b if b is not None and b[0] is not None else None
+
+
+def set_rng_failure(box):
+    _rng_box[0] = box
+
+
+def rethrow(box):
+    """Raise (once) the failure held by ``box``; it is cleared so later reads succeed."""
+    if box is None or box[0] is None:
+        return
+    exc, box[0] = box[0], None
+    with _failed_lock:
+        try:
+            _failed.remove(box)
+        except ValueError:
+            pass
+    from .base import MXNetError
+    raise MXNetError(str(exc)) from exc
+
+
+def rethrow_all():
+    """WaitForAll: raise the oldest pending failure and clear every pending one."""
+    with _failed_lock:
+        boxes = list(_failed)
+        del _failed[:]
+    first = None
+    for b in boxes:
+        if b[0] is not None and first is None:
+            first = b[0]
+        b[0] = None
+    if first is not None:
+        from .base import MXNetError
+        raise MXNetError(str(first)) from first
+
+
 def set_bulk_size(size):
     """Set the op bulking size; returns the previous value.  Device work is
     already batched on the HIP stream (and HIP graphs), so this only records

@@ -16,7 +16,7 @@ import torch
 from . import _state
 from . import profiler as _profiler
 from .ops import amp_dispatch as _amp
-from .base import MXNetError
+from .base import MXNetError, AsyncOpError
 from .ops import registry
 
 
@@ -69,6 +69,7 @@ class GraphProgram:
         vals = [None] * self.nslots
         for name, s in self.name_to_slot.items():
             vals[s] = feed.get(name)
+        self.failure = None       # first operator execution failure of this run (deferred to sync)
         for fn, ins, attrs, outs, name, opname in self.steps:
             args = [vals[i] for i in ins]
             if _amp.active:
@@ -83,10 +84,23 @@ class GraphProgram:
                         r = fn(*args, **attrs)
                 else:
                     r = fn(*args, **attrs)
+            except AsyncOpError as e:
+                # the graph keeps running on a zero stand-in; the outputs carry the failure
+                from .ndarray.register import _placeholder
+                if self.failure is None:
+                    self.failure = AsyncOpError('Error in operator %s (%s): %s' % (name, opname, e))
+                r = _placeholder(attrs, [])
             except MXNetError:
-                raise
+                if self.failure is None:
+                    raise
+                from .ndarray.register import _placeholder
+                r = _placeholder(attrs, [])
             except RuntimeError as e:
-                raise MXNetError('Error in operator %s (%s): %s' % (name, opname, e)) from e
+                if self.failure is not None:
+                    from .ndarray.register import _placeholder
+                    r = _placeholder(attrs, [])
+                else:
+                    raise MXNetError('Error in operator %s (%s): %s' % (name, opname, e)) from e
             if len(outs) == 1:
                 vals[outs[0]] = r[0] if isinstance(r, (tuple, list)) else r
             else:
@@ -233,6 +247,13 @@ class Executor:
                     b._data.copy_(o.detach())
         else:
             self.outputs = [NDArray(o.detach()) for o in outs]
+        self._failure = getattr(self._prog, 'failure', None)
+        self._failure_box = None
+        if self._failure is not None:
+            from . import engine
+            box = self._failure_box = engine.record_failure(self._failure)
+            for o in self.outputs:
+                o._exc = box
         return self.outputs
 
     def backward(self, out_grads=None, is_train=True):
@@ -269,6 +290,11 @@ class Executor:
                     buf._data.add_(g.to(buf._data.dtype))
                 else:
                     buf._data.copy_(g)
+        box = getattr(self, '_failure_box', None)
+        if box is not None and box[0] is not None:
+            # gradients of a failed forward carry its (shared) failure
+            for n in names:
+                gd[n]._exc = box
         self._leaves = None
 
     def set_monitor_callback(self, callback, monitor_all=False):

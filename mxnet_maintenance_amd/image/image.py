@@ -121,6 +121,10 @@ def _resize_np(a, w, h, interp=1):
 
 
 def imresize(src, w, h, interp=1, out=None):
+    # OpenCV interpolation codes (src/io/image_io.cc: 0 nearest .. 4 lanczos, 9 auto, 10 random)
+    if int(interp) not in (0, 1, 2, 3, 4, 9, 10):
+        from ..base import MXNetError
+        raise MXNetError('imresize: invalid interpolation method %r (OpenCV error: Bad flag)' % (interp,))
     r = _wrap(_resize_np(_np(src), int(w), int(h), interp), src)
     if out is not None:
         out[:] = r

@@ -50,7 +50,8 @@ def _wrap(t):
 
 class NDArray:
     """An n-dimensional array on a :class:`Context`."""
-    __slots__ = ('_data', '_grad', '_grad_req', '_stype', '__weakref__', '_fresh_grad', '_arena', '_host_ctx')
+    __slots__ = ('_data', '_grad', '_grad_req', '_stype', '__weakref__', '_fresh_grad', '_arena', '_host_ctx',
+                 '_exc')
     __array_priority__ = 1000.0
 
     def __init__(self, data, ctx=None, dtype=None, stype='default'):
@@ -171,8 +172,12 @@ class NDArray:
             for i in range(self.shape[0]):
                 yield self[i]
         else:
+            box = getattr(self, '_exc', None)
             for i in range(self.shape[0]):
-                yield NDArray(self._data[i])
+                v = NDArray(self._data[i])
+                if box is not None:
+                    v._exc = box
+                yield v
 
     def __array__(self, dtype=None, copy=None):
         a = self.asnumpy()
@@ -193,13 +198,22 @@ class NDArray:
         return (_rebuild, (self.asnumpy(),))
 
     # ---------------------------------------------------------------- sync/io
+    def _rethrow(self):
+        """Raise the deferred failure of the operator that produced this array (once)."""
+        box = getattr(self, '_exc', None)
+        if box is not None and box[0] is not None:
+            from .. import engine
+            engine.rethrow(box)
+
     def wait_to_read(self):
         if self._data.is_cuda:
             torch.cuda.current_stream(self._data.device).synchronize()
+        self._rethrow()
 
     wait_to_write = wait_to_read
 
     def asnumpy(self):
+        self._rethrow()
         t = self._data.detach()
         if t.dtype == torch.bfloat16:
             t = t.float()
@@ -246,9 +260,10 @@ class NDArray:
                 raise MXNetError('copyto: shape mismatch %s vs %s' % (self.shape, other.shape))
             with torch.no_grad():
                 other._data.copy_(src)
+            _share_failure(self, other)
             return other
         if isinstance(other, Context):
-            return NDArray(self._data.to(other.torch_device, copy=True))
+            return _share_failure(self, _tag_host_ctx(NDArray(self._data.to(other.torch_device, copy=True)), other))
         raise TypeError('copyto does not support type ' + str(type(other)))
 
     def as_in_context(self, context):
@@ -351,7 +366,11 @@ class NDArray:
         r = _index_fn(t, key)
         if r.dim() == 0 and not _state.STATE.np_shape:
             r = r.reshape(1)
-        return NDArray(r)
+        out = NDArray(r)
+        box = getattr(self, '_exc', None)
+        if box is not None:
+            out._exc = box
+        return out
 
     def __setitem__(self, key, value):
         key = _convert_key(key)
@@ -704,6 +723,14 @@ def _ctx(ctx):
     return ctx if ctx is not None else current_context()
 
 
+def _share_failure(src, dst):
+    """``dst`` was computed from ``src``: it carries ``src``'s pending operator failure."""
+    box = getattr(src, '_exc', None)
+    if box is not None and box[0] is not None:
+        dst._exc = box
+    return dst
+
+
 def _tag_host_ctx(arr, ctx):
     """Label a host array with a virtual CPU context (``cpu(k)``, k > 0): every CPU context is the same
     host memory here, but an array created or placed on ``cpu(k)`` reports that context, as in the
@@ -858,11 +885,13 @@ def moveaxis(tensor, source, destination):
 
 
 def waitall():
-    """Block until all pending device work and engine work has completed."""
+    """Block until all pending device work and engine work has completed; then raise the oldest
+    deferred operator failure, if any (every pending failure is cleared)."""
     if torch.cuda.is_available() and torch.cuda.is_initialized():
         torch.cuda.synchronize()
     from .. import engine
     engine.wait_all()
+    engine.rethrow_all()
 
 
 def onehot_encode(indices, out):

@@ -31,8 +31,14 @@ def _dev(ctx):
 def _out(t, out):
     if out is not None:
         out._data.copy_(t.reshape(out.shape))
-        return out
-    return NDArray(t)
+        r = out
+    else:
+        r = NDArray(t)
+    from .. import engine
+    box = engine.rng_failure()      # an earlier sampler failed on the shared random resource
+    if box is not None:
+        r._exc = box
+    return r
 
 
 def _param(p, dev):
@@ -48,11 +54,29 @@ def uniform(low=0, high=1, shape=None, dtype=None, ctx=None, out=None, **kwargs)
         lo = lo.reshape(tuple(lo.shape) + (1,) * len(s))
         hi = hi.reshape(tuple(hi.shape) + (1,) * len(s))
         return _out(lo + (hi - lo) * base, out)
+    if high < low:
+        return _deferred_failure('Check failed: low <= high (uniform sampler: low=%s high=%s)' % (low, high), shape,
+                                 dtype, ctx, out)
     dev = _dev(ctx) if out is None else out._data.device
     s = _shape(shape) if out is None else out.shape
     dt = torch_dtype(dtype) if dtype is not None else (out._data.dtype if out is not None else torch.float32)
     t = torch.empty(s, dtype=dt, device=dev).uniform_(low, high)
     return _out(t, out)
+
+
+def _deferred_failure(msg, shape, dtype, ctx, out):
+    """A sampler whose parameter check failed inside the operator: the failure is deferred to the
+    next sync point (reference: CHECKs in the sampler kernels run on the engine's workers)."""
+    from .. import engine
+    from ..base import AsyncOpError
+    dev = _dev(ctx) if out is None else out._data.device
+    s = _shape(shape) if out is None else out.shape
+    dt = torch_dtype(dtype) if dtype is not None else torch.float32
+    box = engine.rng_failure() or engine.record_failure(AsyncOpError(msg))
+    engine.set_rng_failure(box)
+    r = _out(torch.zeros(s, dtype=dt, device=dev), out)
+    r._exc = box
+    return r
 
 
 def normal(loc=0, scale=1, shape=None, dtype=None, ctx=None, out=None, **kwargs):
@@ -64,6 +88,9 @@ def normal(loc=0, scale=1, shape=None, dtype=None, ctx=None, out=None, **kwargs)
         mu = mu.reshape(tuple(mu.shape) + (1,) * len(s))
         sd = sd.reshape(tuple(sd.shape) + (1,) * len(s))
         return _out(mu + sd * base, out)
+    if scale < 0:
+        return _deferred_failure('Check failed: scale >= 0 (normal sampler: scale=%s)' % scale, shape, dtype, ctx,
+                                 out)
     dev = _dev(ctx) if out is None else out._data.device
     s = _shape(shape) if out is None else out.shape
     dt = torch_dtype(dtype) if dtype is not None else (out._data.dtype if out is not None else torch.float32)

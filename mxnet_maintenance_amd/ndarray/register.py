@@ -10,7 +10,7 @@ import torch
 from .. import _state
 from .. import profiler as _profiler
 from ..ops import amp_dispatch as _amp
-from ..base import MXNetError
+from ..base import MXNetError, AsyncOpError
 from ..ops import registry
 from .ndarray import NDArray
 
@@ -99,20 +99,70 @@ def _note_leaves(inputs):
                 tl[id(x)] = x
 
 
+def _failed_input(inputs):
+    """The pending failure box of the first input produced by a failed operator, if any (the
+    reference shares one exception slot along a chain of dependent operators)."""
+    for x in inputs:
+        box = getattr(x, '_exc', None) if x is not None else None
+        if box is not None and box[0] is not None:
+            return box
+    return None
+
+
+def _is_sampler(name):
+    return name.startswith(('_random_', '_sample_', '_npi_random', 'random_', 'sample_')) or name in (
+        '_npi_normal', '_npi_uniform', '_npi_gamma', '_npi_exponential', '_npi_multinomial', '_shuffle')
+
+
+def _placeholder(attrs, inputs):
+    """Output stand-in of an operator whose execution failed: zeros of the declared shape, so that
+    dependent Python code (unpacking, shape arithmetic) keeps working until the error surfaces."""
+    from ..base import torch_dtype
+    shape = attrs.get('shape') or attrs.get('size') or (1,)
+    shape = (shape,) if isinstance(shape, int) else tuple(shape)
+    dt = attrs.get('dtype')
+    try:
+        td = torch_dtype(dt if dt not in (None, 'None') else 'float32')
+    except Exception:   # pylint: disable=broad-except
+        td = torch.float32
+    ctx = attrs.get('ctx')
+    dev = getattr(ctx, 'torch_device', None)
+    if dev is None:
+        dev = next((x._data.device for x in inputs if x is not None), torch.device('cpu'))
+    return torch.zeros(shape, dtype=td, device=dev)
+
+
 def invoke(op, inputs, attrs, out=None):
-    """Run ``op`` on NDArray ``inputs`` with parsed ``attrs``."""
+    """Run ``op`` on NDArray ``inputs`` with parsed ``attrs``.
+
+    Failures of the operator's execution (AsyncOpError) and failed inputs do not raise here: the
+    outputs carry the failure to the next synchronisation point (engine.rethrow / rethrow_all)."""
     tin = [None if x is None else x._data for x in inputs]
     _note_leaves(inputs)
     if _amp.active:
         tin = _amp.cast_inputs(op.name, tin, attrs)
+    box = _failed_input(inputs)
+    sampler = _is_sampler(op.name)
+    if sampler and box is None:
+        from .. import engine
+        box = engine.rng_failure()
     try:
         if _profiler.active_imperative:
             with _profiler.op_span(_profiler.current_scope() + op.name):
                 res = _run(op.fn, tin, attrs)
         else:
             res = _run(op.fn, tin, attrs)
+    except AsyncOpError as e:
+        from .. import engine
+        if box is None:
+            box = engine.record_failure(e)
+        if sampler:
+            engine.set_rng_failure(box)
+        res = _placeholder(attrs, inputs)
     except MXNetError:
-        raise
+        if box is None:
+            raise
+        res = _placeholder(attrs, inputs)    # an op fed garbage by a failed input: the input's error wins
     except RuntimeError as e:
         # operator failures surface as MXNetError (a RuntimeError), as from the reference's C API
         raise MXNetError('Error in operator %s: %s' % (op.name, e)) from e
@@ -122,6 +172,9 @@ def invoke(op, inputs, attrs, out=None):
     else:
         outs = [NDArray(res)]
     _np_wrap(inputs, outs)
+    if box is not None:
+        for o in outs:
+            o._exc = box
     hctx = attrs.get('ctx') if 'ctx' in attrs else next(
         (x._host_ctx for x in inputs if x is not None and getattr(x, '_host_ctx', None) is not None), None)
     if hctx is not None:
@@ -152,7 +205,11 @@ def invoke_fn(fn, arrays):
     """Run an ad-hoc torch function (reshape, astype, ...) with autograd semantics."""
     _note_leaves(arrays)
     res = _run(fn, [a._data for a in arrays], {})
-    return _np_wrap(arrays, [NDArray(res)])[0]
+    out = _np_wrap(arrays, [NDArray(res)])[0]
+    box = _failed_input(arrays)
+    if box is not None:
+        out._exc = box
+    return out
 
 
 def make_op_function(name):

@@ -8,7 +8,7 @@ import math
 import torch
 import torch.nn.functional as F
 
-from ..base import torch_dtype
+from ..base import AsyncOpError, torch_dtype
 from .registry import register
 from .tensor import _dev
 
@@ -23,48 +23,61 @@ def _s(shape):
     return tuple(shape) if shape else (1,)
 
 
+def _check(cond, msg):
+    # a sampler's parameter check runs inside the operator (reference: CHECKs in the sampler
+    # kernels), so its failure is deferred to the next sync point like any execution error
+    if not cond:
+        raise AsyncOpError(msg)
+
+
 @register('_random_uniform', aliases=('uniform', 'random_uniform'), arg_names=(),
-          params=dict(_RP, low=('float', 0.0), high=('float', 1.0)))
+          params=dict(low=('float', 0.0), high=('float', 1.0), **_RP))
 def random_uniform(low=0.0, high=1.0, shape=(), ctx=None, dtype='float32'):
+    _check(high >= low, 'Check failed: low <= high (uniform sampler: low=%s high=%s)' % (low, high))
     return torch.empty(_s(shape), dtype=torch_dtype(dtype if dtype != 'None' else 'float32'),
                        device=_dev(ctx)).uniform_(low, high)
 
 
 @register('_random_normal', aliases=('normal', 'random_normal'), arg_names=(),
-          params=dict(_RP, loc=('float', 0.0), scale=('float', 1.0)))
+          params=dict(loc=('float', 0.0), scale=('float', 1.0), **_RP))
 def random_normal(loc=0.0, scale=1.0, shape=(), ctx=None, dtype='float32'):
+    _check(scale >= 0, 'Check failed: scale >= 0 (normal sampler: scale=%s)' % scale)
     return torch.empty(_s(shape), dtype=torch_dtype(dtype if dtype != 'None' else 'float32'),
                        device=_dev(ctx)).normal_(loc, scale)
 
 
-@register('_random_gamma', arg_names=(), params=dict(_RP, alpha=('float', 1.0), beta=('float', 1.0)))
+@register('_random_gamma', arg_names=(), params=dict(alpha=('float', 1.0), beta=('float', 1.0), **_RP))
 def random_gamma(alpha=1.0, beta=1.0, shape=(), ctx=None, dtype='float32'):
+    _check(alpha > 0 and beta > 0, 'Check failed: alpha > 0 && beta > 0 (gamma sampler)')
     return (torch._standard_gamma(torch.full(_s(shape), alpha, device=_dev(ctx))) * beta).to(torch_dtype(dtype))
 
 
-@register('_random_exponential', arg_names=(), params=dict(_RP, lam=('float', 1.0)))
+@register('_random_exponential', arg_names=(), params=dict(lam=('float', 1.0), **_RP))
 def random_exponential(lam=1.0, shape=(), ctx=None, dtype='float32'):
+    _check(lam > 0, 'Check failed: lambda > 0 (exponential sampler)')
     return torch.empty(_s(shape), device=_dev(ctx)).exponential_(lam).to(torch_dtype(dtype))
 
 
-@register('_random_poisson', arg_names=(), params=dict(_RP, lam=('float', 1.0)))
+@register('_random_poisson', arg_names=(), params=dict(lam=('float', 1.0), **_RP))
 def random_poisson(lam=1.0, shape=(), ctx=None, dtype='float32'):
+    _check(lam >= 0, 'Check failed: lambda >= 0 (poisson sampler)')
     return torch.poisson(torch.full(_s(shape), lam, device=_dev(ctx))).to(torch_dtype(dtype))
 
 
-@register('_random_randint', arg_names=(), params=dict(_RP, low=('int', 0), high=('int', 1), dtype=('str', 'int32')))
+@register('_random_randint', arg_names=(),
+          params=dict(dict(low=('int', 0), high=('int', 1)), **dict(_RP, dtype=('str', 'int32'))))
 def random_randint(low=0, high=1, shape=(), ctx=None, dtype='int32'):
     return torch.randint(low, high, _s(shape), device=_dev(ctx)).to(torch_dtype(dtype))
 
 
-@register('_random_negative_binomial', arg_names=(), params=dict(_RP, k=('int', 1), p=('float', 1.0)))
+@register('_random_negative_binomial', arg_names=(), params=dict(k=('int', 1), p=('float', 1.0), **_RP))
 def random_negative_binomial(k=1, p=1.0, shape=(), ctx=None, dtype='float32'):
     g = torch._standard_gamma(torch.full(_s(shape), float(k), device=_dev(ctx))) * ((1 - p) / p)
     return torch.poisson(g).to(torch_dtype(dtype))
 
 
 @register('_random_generalized_negative_binomial', arg_names=(),
-          params=dict(_RP, mu=('float', 1.0), alpha=('float', 1.0)))
+          params=dict(mu=('float', 1.0), alpha=('float', 1.0), **_RP))
 def random_gen_neg_binomial(mu=1.0, alpha=1.0, shape=(), ctx=None, dtype='float32'):
     g = torch._standard_gamma(torch.full(_s(shape), 1.0 / alpha, device=_dev(ctx))) * (mu * alpha)
     return torch.poisson(g).to(torch_dtype(dtype))

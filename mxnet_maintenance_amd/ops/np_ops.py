@@ -988,6 +988,9 @@ def _uniform(low=0.0, high=1.0, size=None, ctx=None, dtype='float32'):
 
 @register('_npi_normal', arg_names=(), params=dict(_RND, loc=('float', 0.0), scale=('float', 1.0)))
 def _normal(loc=0.0, scale=1.0, size=None, ctx=None, dtype='float32'):
+    if scale < 0:
+        from ..base import AsyncOpError
+        raise AsyncOpError('Check failed: scale >= 0 (normal sampler: scale=%s)' % scale)
     return torch.randn(_size(size), dtype=_td(dtype, _FLOAT), device=_dev(ctx)) * scale + loc
 
 
