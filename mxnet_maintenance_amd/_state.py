@@ -37,3 +37,8 @@ def is_training():
 # HIP-graph capture of a training step (gluon.GraphStep): a device uint64 counter mixed into the seeds of
 # captured dropout kernels, advanced before every replay so masks differ between replays
 GRAPH_RNG = [None]
+
+
+# ids of NDArray leaves whose gradient buffer a backward pass actually reached (filled by the
+# post-accumulate hook NDArray.attach_grad registers; read when marking gradients fresh)
+GRAD_TOUCHED = set()

@@ -113,6 +113,20 @@ def _collect_leaves(retain):
     return leaves
 
 
+def _add_touch_hook(v, t):
+    """Record (in _state.GRAD_TOUCHED) that a backward pass reached leaf ``v`` -- a leaf used only
+    through a detached path keeps a stale gradient, as in the reference."""
+    import weakref
+    ref = weakref.ref(v)
+
+    def touched(_t, ref=ref):
+        a = ref()
+        if a is not None:
+            _state.GRAD_TOUCHED.add(id(a))
+    t.register_post_accumulate_grad_hook(touched)
+    t._mxamd_touch_hook = True
+
+
 def _prepare_leaves(leaves):
     """Zero 'write' buffers (grouped in one multi-tensor launch) and rebind stale .grad."""
     zero = []
@@ -121,6 +135,8 @@ def _prepare_leaves(leaves):
         t = v._data
         if not t.requires_grad or v._grad is None:
             continue
+        if not getattr(t, '_mxamd_touch_hook', False):
+            _add_touch_hook(v, t)
         gbuf = v._grad._data
         if t.grad is not gbuf:
             t.grad = gbuf
@@ -141,6 +157,7 @@ def _prepare_leaves(leaves):
 
 
 def _finish_leaves(leaves):
+    touched = _state.GRAD_TOUCHED
     for v in leaves:
         t = v._data
         if v._grad is None:
@@ -150,7 +167,13 @@ def _finish_leaves(leaves):
             # create_graph path builds a new tensor instead of accumulating in place
             v._grad._data = g
             t.grad = g
-        v._fresh_grad = True
+        if id(v) in touched or not getattr(t, '_mxamd_touch_hook', False):
+            v._fresh_grad = True
+        else:
+            # not reached by this backward (another head's graph, or a detached path): it stays on
+            # the tape for a later backward of the same recording
+            _state.STATE.tape_leaves.setdefault(id(v), v)
+    touched.clear()
 
 
 def backward(heads, head_grads=None, retain_graph=False, train_mode=True, create_graph=False):  # pylint: disable=redefined-outer-name
@@ -178,7 +201,8 @@ def backward(heads, head_grads=None, retain_graph=False, train_mode=True, create
                              'without retain_graph=True; record it again or pass retain_graph=True')
     if not (retain_graph or create_graph):
         for h in heads:
-            if getattr(h, '_data', None) is not None:
+            # only a recorded result owns a graph to free (an identity op may hand back its leaf input)
+            if getattr(h, '_data', None) is not None and h._data.grad_fn is not None:
                 setattr(h._data, _RELEASED_ATTR, True)
     leaves = _collect_leaves(retain_graph)
     _prepare_leaves(leaves)

@@ -202,7 +202,7 @@ def test_conv_nhwc_fwd_matches_fp32(dtype, cfg):
     assert KF.conv_ok_shape(x, w, (s, s), (pad, pad))
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), bias, s, pad).permute(0, 2, 3, 1)
     tol = 2e-2 if dtype == torch.float16 else 6e-2
-    for v in [0] + KF._fwd_variants(Cin, Cout):     # heuristic tile + every forced (BCO, BK) tile
+    for v in [0] + KF._fwd_variants(Cin, Cout, bias=True):     # heuristic tile + every tile taking a bias
         y = KF.conv_fwd(x, w, (s, s), (pad, pad), bias, v)
         assert y.shape == ref.shape
         torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol, msg=lambda m: 'variant %d: %s' % (v, m))
