@@ -67,6 +67,7 @@ from . import numpy as np
 from . import numpy_extension
 from . import numpy_extension as npx
 from . import rtc
+from . import numpy_op_signature
 from .util import is_np_array, is_np_shape, set_np, reset_np, use_np, np_shape, np_array, set_np_shape, use_np_shape, use_np_array
 
 # A process launched as a dist_async server (DMLC_ROLE=server / scheduler) serves and exits at import,

@@ -23,6 +23,15 @@ class AsyncOpError(MXNetError):
     (``wait_to_read`` / ``asnumpy`` / ``mx.nd.waitall``)."""
 
 
+class MXNetValueError(MXNetError, ValueError):
+    """An MXNetError that is also a ValueError (the reference maps C++ errors whose message starts
+    with ``ValueError:`` to this Python type)."""
+
+
+class AsyncValueError(AsyncOpError, ValueError):
+    """A deferred operator failure rethrown as a ValueError (invalid parameter values)."""
+
+
 class NotImplementedForSymbol(MXNetError):
     def __init__(self, function, alias, *args):
         super().__init__()

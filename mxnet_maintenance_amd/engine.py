@@ -151,8 +151,12 @@ def rethrow(box):
             _failed.remove(box)
         except ValueError:
             pass
-    from .base import MXNetError
-    raise MXNetError(str(exc)) from exc
+    raise _as_mxnet_error(exc) from exc
+
+
+def _as_mxnet_error(exc):
+    from .base import MXNetError, MXNetValueError
+    return (MXNetValueError if isinstance(exc, ValueError) else MXNetError)(str(exc))
 
 
 def rethrow_all():
@@ -166,8 +170,7 @@ def rethrow_all():
             first = b[0]
         b[0] = None
     if first is not None:
-        from .base import MXNetError
-        raise MXNetError(str(first)) from first
+        raise _as_mxnet_error(first) from first
 
 
 def set_bulk_size(size):

@@ -321,7 +321,12 @@ class NDArray:
             self._grad_req = None
             return
         if not t.is_floating_point():
-            raise MXNetError('attach_grad requires a floating point array')
+            # integer arrays get a gradient buffer too (as in the reference); autograd cannot flow
+            # into them, so it stays zero
+            self._data = t
+            self._grad = NDArray(torch.zeros_like(t))
+            self._grad_req = grad_req
+            return
         t.requires_grad_(True)
         self._data = t
         g = torch.zeros_like(t)
@@ -387,6 +392,12 @@ class NDArray:
             new = t.clone()
             new[key] = v.to(new.device, new.dtype) if torch.is_tensor(v) else v
             self._data = new
+            return
+        whole = (isinstance(key, slice) and key == slice(None)) or key is Ellipsis or key == ()
+        if t.dim() == 0 and whole:
+            # x[:] = v on a 0-d array (NumPy semantics: assign the scalar)
+            with torch.no_grad():
+                t.copy_(v.to(t.device, t.dtype).reshape(()) if torch.is_tensor(v) else torch.as_tensor(v, dtype=t.dtype))
             return
         with torch.no_grad():
             if torch.is_tensor(v):

@@ -1413,9 +1413,13 @@ dtype = onp.dtype
 float16, float32, float64 = onp.float16, onp.float32, onp.float64
 int8, int16, int32, int64, uint8 = onp.int8, onp.int16, onp.int32, onp.int64, onp.uint8
 bool_ = onp.bool_
+bool = onp.bool_          # noqa: A001  (mx.np.bool exists in the reference; NumPy 2 dropped np.bool)
+uint16, uint32, uint64 = onp.uint16, onp.uint32, onp.uint64
+complex64, complex128 = onp.complex64, onp.complex128
 pi, e, inf, nan, newaxis, euler_gamma = onp.pi, onp.e, onp.inf, onp.nan, None, onp.euler_gamma
 PZERO, NZERO = 0.0, -0.0
-__all__ += ['dtype', 'float16', 'float32', 'float64', 'int8', 'int16', 'int32', 'int64', 'uint8', 'bool_',
+__all__ += ['dtype', 'float16', 'float32', 'float64', 'int8', 'int16', 'int32', 'int64', 'uint8', 'bool_', 'bool',
+            'uint16', 'uint32', 'uint64', 'complex64', 'complex128',
             'pi', 'e', 'inf', 'nan', 'newaxis', 'euler_gamma', 'PZERO', 'NZERO']
 
 

@@ -16,9 +16,9 @@ __all__ = ['randint', 'uniform', 'normal', 'lognormal', 'logistic', 'gumbel', 'm
            'chisquare', 'randn', 'laplace', 'permutation', 'seed']
 
 
-def seed(s, ctx='all'):
+def seed(seed=None, ctx='all', **kwargs):  # pylint: disable=redefined-outer-name
     from .. import random as _r
-    _r.seed(s, ctx)
+    _r.seed(seed if seed is not None else kwargs.get('s'), ctx)
 
 
 def _size(size):
@@ -52,23 +52,47 @@ def _wrap(t, dtype=None):
     return ndarray(t)
 
 
+# parameter positions that must be > 0 (strict) or >= 0, per distribution
+_POSITIVE = {'normal': ((1, False),), 'lognormal': ((1, False),), 'logistic': ((1, False),),
+             'gumbel': ((1, False),), 'laplace': ((1, False),), 'exponential': ((0, False),),
+             'rayleigh': ((0, False),), 'weibull': ((0, True),), 'pareto': ((0, True),), 'power': ((0, True),),
+             'gamma': ((0, True), (1, True)), 'beta': ((0, True), (1, True)), 'chisquare': ((0, True),)}
+
+
+def _check_scalars(kind, params):
+    """Scalar parameters are validated in Python, at the call (reference numpy/random.py raises
+    ValueError); array parameters are checked inside the operator."""
+    for i, strict in _POSITIVE.get(kind, ()):
+        p = params[i]
+        if _is_scalar(p) and (p <= 0 if strict else p < 0):
+            raise ValueError('%s: parameter %d must be %s 0, got %r' % (kind, i, '>' if strict else '>=', p))
+
+
+def _sample(kind, params, size, dtype=None, ctx=None, out=None, batch=False):
+    """Draw from ``kind`` through the registered sampler op (array or Symbol parameters become op
+    inputs; scalars ride along as attributes)."""
+    from .multiarray import _is_sym
+    _check_scalars(kind, params)
+    arrays = [p for p in params if isinstance(p, NDArray) or _is_sym(p)]
+    pscal = tuple(None if (isinstance(p, NDArray) or _is_sym(p)) else float(p) for p in params)
+    kw = dict(kind=kind, pscal=pscal, size=_size(size), dtype=dtype or 'float32', out=out, batch=bool(batch))
+    if not arrays:
+        kw['ctx'] = ctx or current_context()
+    return _call('_npi_sampler', *arrays, **kw)
+
+
 def uniform(low=0.0, high=1.0, size=None, dtype=None, ctx=None, out=None):
     if _is_scalar(low) and _is_scalar(high):
         return _call('_npi_uniform', low=float(low), high=float(high), size=_size(size) or (),
                      ctx=ctx or current_context(), dtype=dtype or 'float32', out=out)
-    dev = _dev(ctx)
-    lo, hi = _t(low, dev), _t(high, dev)
-    shp = _bshape(size, low, high)
-    return _wrap(torch.rand(shp, device=dev) * (hi - lo) + lo, dtype)
+    return _sample('uniform', (low, high), size, dtype, ctx, out)
 
 
 def normal(loc=0.0, scale=1.0, size=None, dtype=None, ctx=None, out=None):
     if _is_scalar(loc) and _is_scalar(scale):
         return _call('_npi_normal', loc=float(loc), scale=float(scale), size=_size(size) or (),
                      ctx=ctx or current_context(), dtype=dtype or 'float32', out=out)
-    dev = _dev(ctx)
-    mu, sd = _t(loc, dev), _t(scale, dev)
-    return _wrap(torch.randn(_bshape(size, loc, scale), device=dev) * sd + mu, dtype)
+    return _sample('normal', (loc, scale), size, dtype, ctx, out)
 
 
 def randint(low, high=None, size=None, dtype=None, ctx=None, out=None):
@@ -85,75 +109,51 @@ def randn(*size, **kwargs):
 
 
 def lognormal(mean=0.0, sigma=1.0, size=None, dtype=None, ctx=None, out=None):
-    return _wrap(torch.exp(normal(mean, sigma, size, None, ctx)._data), dtype)
+    return _sample('lognormal', (mean, sigma), size, dtype, ctx, out)
 
 
 def logistic(loc=0.0, scale=1.0, size=None, ctx=None, out=None):
-    u = uniform(1e-7, 1 - 1e-7, _bshape(size, loc, scale), ctx=ctx)._data
-    dev = u.device
-    return _wrap(_t(loc, dev) + _t(scale, dev) * torch.log(u / (1 - u)))
+    return _sample('logistic', (loc, scale), size, None, ctx, out)
 
 
 def gumbel(loc=0.0, scale=1.0, size=None, ctx=None, out=None):
-    u = uniform(1e-7, 1 - 1e-7, _bshape(size, loc, scale), ctx=ctx)._data
-    dev = u.device
-    return _wrap(_t(loc, dev) - _t(scale, dev) * torch.log(-torch.log(u)))
+    return _sample('gumbel', (loc, scale), size, None, ctx, out)
 
 
 def laplace(loc=0.0, scale=1.0, size=None, dtype=None, ctx=None, out=None):
-    dev = _dev(ctx)
-    d = torch.distributions.Laplace(_t(loc, dev), _t(scale, dev))
-    return _wrap(d.sample(_bshape(size, loc, scale) if size is not None else ()), dtype)
+    return _sample('laplace', (loc, scale), size, dtype, ctx, out)
 
 
 def exponential(scale=1.0, size=None, ctx=None, out=None):
-    dev = _dev(ctx)
-    u = torch.rand(_bshape(size, scale), device=dev)
-    return _wrap(-torch.log1p(-u) * _t(scale, dev))
+    return _sample('exponential', (scale,), size, None, ctx, out)
 
 
 def rayleigh(scale=1.0, size=None, ctx=None, out=None):
-    dev = _dev(ctx)
-    u = torch.rand(_bshape(size, scale), device=dev)
-    return _wrap(_t(scale, dev) * torch.sqrt(-2.0 * torch.log1p(-u)))
+    return _sample('rayleigh', (scale,), size, None, ctx, out)
 
 
 def weibull(a, size=None, ctx=None, out=None):
-    dev = _dev(ctx)
-    u = torch.rand(_bshape(size, a), device=dev)
-    return _wrap(torch.pow(-torch.log1p(-u), 1.0 / _t(a, dev)))
+    return _sample('weibull', (a,), size, None, ctx, out)
 
 
 def pareto(a, size=None, ctx=None, out=None):
-    dev = _dev(ctx)
-    u = torch.rand(_bshape(size, a), device=dev)
-    return _wrap(torch.pow(1 - u, -1.0 / _t(a, dev)) - 1)
+    return _sample('pareto', (a,), size, None, ctx, out)
 
 
 def power(a, size=None, ctx=None, out=None):
-    dev = _dev(ctx)
-    u = torch.rand(_bshape(size, a), device=dev)
-    return _wrap(torch.pow(u, 1.0 / _t(a, dev)))
+    return _sample('power', (a,), size, None, ctx, out)
 
 
 def gamma(shape=1.0, scale=1.0, size=None, dtype=None, ctx=None, out=None):
-    dev = _dev(ctx)
-    k, th = _t(shape, dev), _t(scale, dev)
-    shp = _bshape(size, shape, scale)
-    d = torch.distributions.Gamma(k.expand(shp) if k.dim() or shp else k, torch.ones((), device=dev))
-    return _wrap(d.sample() * th, dtype)
+    return _sample('gamma', (shape, scale), size, dtype, ctx, out)
 
 
 def beta(a, b, size=None, dtype=None, ctx=None):
-    dev = _dev(ctx)
-    shp = _bshape(size, a, b)
-    d = torch.distributions.Beta(_t(a, dev).expand(shp), _t(b, dev).expand(shp))
-    return _wrap(d.sample(), dtype)
+    return _sample('beta', (a, b), size, dtype, ctx)
 
 
 def chisquare(df, size=None, dtype=None, ctx=None):
-    return _wrap(gamma(_t(df, _dev(ctx)) / 2 if isinstance(df, NDArray) else df / 2.0, 2.0, size, None, ctx)._data,
-                 dtype)
+    return _sample('chisquare', (df,), size, dtype, ctx)
 
 
 def multinomial(n, pvals, size=None):

@@ -85,9 +85,9 @@ def nonzero(a):
     return ndarray(torch.nonzero(a._data))
 
 
-def seed(s, ctx='all'):
+def seed(seed=None, ctx='all', **kwargs):  # pylint: disable=redefined-outer-name
     from .. import random as _r
-    _r.seed(s, ctx)
+    _r.seed(seed if seed is not None else kwargs.get('s'), ctx)
 
 
 def save(file, arr):
@@ -132,10 +132,11 @@ def _random_ns():
                      ctx=ctx or current_context(), dtype=dtype or 'float32')
 
     def uniform_n(low=0.0, high=1.0, batch_shape=None, dtype=None, ctx=None):
-        return nprand.uniform(low, high, size=batch_shape, dtype=dtype, ctx=ctx)
+        # output shape = batch_shape + the parameters' broadcast shape (reference: np_random_n ops)
+        return nprand._sample('uniform', (low, high), batch_shape, dtype, ctx, batch=True)
 
     def normal_n(loc=0.0, scale=1.0, batch_shape=None, dtype=None, ctx=None):
-        return nprand.normal(loc, scale, size=batch_shape, dtype=dtype, ctx=ctx)
+        return nprand._sample('normal', (loc, scale), batch_shape, dtype, ctx, batch=True)
     return _Namespace('mxnet.numpy_extension.random', {'seed': seed, 'bernoulli': bernoulli,
                                                        'uniform_n': uniform_n, 'normal_n': normal_n})
 

@@ -73,6 +73,7 @@ def _leaf_grad(t, numel=None, dtype=torch.float32):
 
 
 _RELU_FROM_X = [True]    # BN+ReLU backward recomputes the mask from x (debug switch)
+_BN_BWD_FUSE = [os.environ.get('MXAMD_BN_BWD_FUSE', '1') != '0']   # BN-backward stats in dgrad epilogues
 _ZEROS = {}
 
 
@@ -144,6 +145,14 @@ class BatchNormNHWC(torch.autograd.Function):
         ctx.save_for_backward(x, y if relu_mode == 1 else mask, g, mean, invstd,
                               scale if relu_mode == 2 else None, shift if relu_mode == 2 else None)
         ctx.cfg = (relu_mode, bool(training), addend is not None, gamma.dtype, beta.dtype)
+        ctx.bn_token = None
+        if training and relu_mode in (0, 2, 3) and _BN_BWD_FUSE[0]:
+            # a consumer convolution's dgrad (big-tile kernel) may emit this BN's backward statistics
+            # from its epilogue: it needs z (= x here), mean, the ReLU mask source, and a token that
+            # identifies this BN call (checked in backward)
+            ctx.bn_token = object()
+            y._mxamd_bn_src = (x, mean, scale if relu_mode == 2 else None, shift if relu_mode == 2 else None,
+                               mask if relu_mode == 3 else None, relu_mode, ctx.bn_token)
         ctx.refs = (gamma, beta)
         ctx.mark_non_differentiable(mean, var)
         # mean/var never receive gradients: skip materialising two zero tensors per call
@@ -164,8 +173,13 @@ class BatchNormNHWC(torch.autograd.Function):
         dev = x.device
         dx = torch.empty_like(x)
         dz = torch.empty_like(x) if has_add else None
-        nblk = lib.bn_partials_rows(R, C)
-        part = torch.empty(2 * nblk * C, dtype=torch.float32, device=dev)
+        ext = getattr(gy, '_mxamd_bn_bwd', None)
+        ext_nblk = 0
+        if ext is not None and ctx.bn_token is not None and ext[2] is ctx.bn_token:
+            part, ext_nblk = ext[0], ext[1]      # statistics from the producing dgrad's epilogue
+        else:
+            nblk = lib.bn_partials_rows(R, C)
+            part = torch.empty(2 * nblk * C, dtype=torch.float32, device=dev)
         out = torch.empty(5, C, dtype=torch.float32, device=dev)
         need_g, need_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
         # accumulate dgamma/dbeta straight into the parameters' fp32 grad buffers (arena views)
@@ -182,7 +196,8 @@ class BatchNormNHWC(torch.autograd.Function):
         lib.bn_nhwc_backward(_DT[x.dtype], x.data_ptr(), gy.data_ptr(), _p(y), _p(ymask), dx.data_ptr(), _p(dz),
                              g.data_ptr(),
                              mean.data_ptr(), invstd.data_ptr(), _p(fscale), _p(fshift), part.data_ptr(), dg_ptr,
-                             db_ptr, out[2].data_ptr(), R, C, relu_mode, 0, int(training), accum, _stream())
+                             db_ptr, out[2].data_ptr(), R, C, relu_mode, 0, int(training), accum, _stream(),
+                             ext_nblk)
         if direct:
             # returning None: torch still runs the leaves' AccumulateGrad node with an undefined
             # gradient, which fires their post-accumulate hooks (bucketed all-reduce readiness)
@@ -293,7 +308,7 @@ _BIG_VARIANTS = {10: (256, 256), 11: (128, 256), 12: (64, 512), 13: (256, 128)}
 _RING_VARIANTS = {20: (128, 128), 21: (256, 128), 22: (128, 256), 23: (64, 256), 24: (256, 256), 25: (64, 128)}
 
 
-def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=None):
+def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=None, bn_bwd=None):
     """y[N,Ho,Wo,K] = conv(x[N,H,W,C], w[K,R,S,C]) on the MFMA implicit-GEMM kernel.
 
     ``variant``: 0 = heuristic tile, 1..4 = (BCO, BK) in (128,64) (128,32) (64,64) (64,32),
@@ -302,7 +317,9 @@ def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=Non
     row-contiguous epilogue, 20..25 = persistent LDS-DMA ring kernel (see _RING_VARIANTS; no bias).
     ``bn_stats`` (big / ring kernels): also emit per-channel BatchNorm
     sum / sum-of-squares partials of y, attached to y as ``y._mxamd_bn_part``; ``addend`` (big kernel
-    only, same shape/dtype as y): y = conv + addend."""
+    only, same shape/dtype as y): y = conv + addend.  ``bn_bwd`` (big kernel only; a BatchNorm's
+    ``_mxamd_bn_src`` record): y is that BN's incoming gradient -- also emit its backward statistics
+    (sum dz, sum dz*(z-mean)), attached to y as ``y._mxamd_bn_bwd``."""
     N, H, W, C = x.shape
     K, R, S, _ = w.shape
     Ho = (H + 2 * pad[0] - R) // stride[0] + 1
@@ -335,9 +352,19 @@ def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=Non
         if bn_stats:
             nparts = lib.conv_nhwc_fwd_big_nparts(N, H, W, R, S, stride[0], stride[1], pad[0], pad[1], v)
             part = torch.empty(2 * K * nparts, dtype=torch.float32, device=x.device)
+        bkw = {}
+        if bn_bwd is not None:
+            z, bmean, bscale, bshift, bmask, bmode, token = bn_bwd
+            assert z.shape == y.shape and z.dtype == y.dtype and z.is_contiguous()
+            bnp = lib.conv_nhwc_fwd_big_bwd_nparts(N, H, W, R, S, stride[0], stride[1], pad[0], pad[1], v)
+            bpart = torch.empty(2 * K * bnp, dtype=torch.float32, device=x.device)
+            bkw = dict(bn_z=z.data_ptr(), bn_mean=bmean.data_ptr(), bn_scale=_p(bscale), bn_shift=_p(bshift),
+                       bn_mask=_p(bmask), bn_mode=int(bmode), bn_part=bpart.data_ptr(), bn_nparts=bnp)
         lib.conv_nhwc_fwd_big(_DT[x.dtype], x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(),
                               _zero_page(x.device).data_ptr(), N, H, W, C, K, R, S, stride[0], stride[1],
-                              pad[0], pad[1], v, _p(part), nparts, _p(addend), _stream())
+                              pad[0], pad[1], v, _p(part), nparts, _p(addend), _stream(), **bkw)
+        if bkw:
+            y._mxamd_bn_bwd = (bpart, bnp, bn_bwd[6])
         if part is not None:
             # consumed by a following BatchNormNHWC (training): its statistics pass over y is skipped
             y._mxamd_bn_part = (part, nparts)
@@ -615,6 +642,29 @@ def _dgrad_candidates(dy, x, w, stride, pad):
     return c
 
 
+def _big_algo(key):
+    """The big-tile variant number autotuning picked for ``key``, else None."""
+    algo = _ALGO.get(key)
+    if algo and algo.startswith('hip') and algo[3:].isdigit() and int(algo[3:]) in _BIG_VARIANTS:
+        return int(algo[3:])
+    return None
+
+
+def _dgrad_bn_fused(key, dy, w, pad, bn_src):
+    """Stride-1 dgrad on the big-tile kernel that also emits the backward statistics of the
+    BatchNorm whose output this conv read (its gradient is exactly this dgrad) -- when autotuning
+    picked the big kernel for this shape.  None otherwise (the caller runs the normal selection)."""
+    if bn_src is None or not _BN_BWD_FUSE[0]:
+        return None
+    v = _big_algo(key)
+    if v is None:
+        return None
+    K, R, S, C = w.shape
+    if bn_src[0].shape[-1] != C:
+        return None
+    return conv_fwd(dy, _dgrad_weight(w), (1, 1), (R - 1 - pad[0], S - 1 - pad[1]), None, v, bn_bwd=bn_src)
+
+
 def _dgrad_default(w, stride):
     K, R, S, C = w.shape
     if tuple(stride) != (1, 1):
@@ -726,6 +776,7 @@ class ConvNHWC(torch.autograd.Function):
         ctx.stride, ctx.pad = stride, pad
         ctx.has_bias = bias is not None
         ctx.w_ref = w
+        ctx.bn_src = getattr(x, '_mxamd_bn_src', None)
         return y
 
     @staticmethod
@@ -736,7 +787,9 @@ class ConvNHWC(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             key = ('dgrad', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype)
-            dx = _select(key, _dgrad_candidates(dy, x, w, stride, pad), _dgrad_default(w, stride))
+            dx = _dgrad_bn_fused(key, dy, w, pad, ctx.bn_src)
+            if dx is None:
+                dx = _select(key, _dgrad_candidates(dy, x, w, stride, pad), _dgrad_default(w, stride))
         if ctx.needs_input_grad[1]:
             dw = _wgrad(dy, x, w, ctx.w_ref, stride, pad)
         if ctx.has_bias and ctx.needs_input_grad[2]:
@@ -763,6 +816,7 @@ class ConvTeeNHWC(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.w_ref = w
         ctx.inplace_grad = inplace_grad
+        ctx.bn_src = getattr(x, '_mxamd_bn_src', None)
         return y, x.view_as(x)
 
     @staticmethod
@@ -774,13 +828,13 @@ class ConvTeeNHWC(torch.autograd.Function):
             return gpass, None, None
         gy = gy.contiguous()
         if ctx.needs_input_grad[0]:
-            dx = _tee_dgrad(gy, x, w, gpass, ctx.inplace_grad)
+            dx = _tee_dgrad(gy, x, w, gpass, ctx.inplace_grad, ctx.bn_src)
         if ctx.needs_input_grad[1]:
             dw = _wgrad(gy, x, w, ctx.w_ref, (1, 1), (0, 0))
         return dx, dw, None
 
 
-def _tee_dgrad(gy, x, w, gpass, inplace):
+def _tee_dgrad(gy, x, w, gpass, inplace, bn_src=None):
     """dX = dY . W (+ dShortcut) of a 1x1 stride-1 conv: the in-tree big-tile MFMA kernel with the
     shortcut gradient read in its epilogue (beta = 1), or hipBLASLt addmm -- autotuned per shape."""
     K, C = w.shape[0], w.shape[3]
@@ -816,6 +870,13 @@ def _tee_dgrad(gy, x, w, gpass, inplace):
     key = ('teedgrad', tuple(x.shape), tuple(w.shape), x.dtype)
     if _ALGO.get(key) == 'mm':
         return mm()
+    v = _big_algo(key)
+    if v is not None and bn_src is not None and _BN_BWD_FUSE[0] and bn_src[0].shape == x.shape:
+        # the block input's BatchNorm (the residual tail of the previous block) gets its backward
+        # statistics from this dgrad's epilogue
+        add = gpass.contiguous() if gpass is not None else None
+        return conv_fwd(gy, w2.t().contiguous().view(C, 1, 1, K), (1, 1), (0, 0), None, v, addend=add,
+                        bn_bwd=bn_src)
     return _select(key, cands, 'mm')
 
 

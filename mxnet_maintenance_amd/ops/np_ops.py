@@ -15,7 +15,7 @@ import math
 import numpy as onp
 import torch
 
-from ..base import torch_dtype
+from ..base import MXNetError, torch_dtype
 from .registry import register
 
 _FLOAT = torch.float32
@@ -1111,3 +1111,110 @@ def npx_reshape(a, newshape=(), reverse=False, order='C'):
     if reverse:
         out = out[::-1]
     return a.reshape(out)
+
+
+# ---------------------------------------------------------------------------
+# mx.np.random samplers with array parameters (reference: src/operator/numpy/random/np_*_op.cc).
+# One registered op for every distribution so samplers work on NDArrays, in hybridized graphs
+# (Symbol parameters) and under autograd: the draws are reparameterised (x = f(params, u) with u
+# from a parameter-free base distribution), which gives the reference's pathwise gradients w.r.t.
+# loc / scale / shape parameters.
+# ---------------------------------------------------------------------------
+_SAMPLER_ARITY = {'normal': 2, 'uniform': 2, 'lognormal': 2, 'logistic': 2, 'gumbel': 2, 'laplace': 2,
+                  'exponential': 1, 'rayleigh': 1, 'weibull': 1, 'pareto': 1, 'power': 1, 'gamma': 2,
+                  'beta': 2, 'chisquare': 1}
+
+
+def _sampler_args(attrs):
+    return ['p%d' % i for i, s in enumerate(attrs.get('pscal') or ()) if s is None]
+
+
+def _sampler_draw(kind, ps, shape, dev, dt):
+    u = lambda: torch.rand(shape, device=dev, dtype=dt).clamp_(1e-7, 1 - 1e-7)  # noqa: E731
+    if kind == 'normal':
+        return ps[0] + ps[1] * torch.randn(shape, device=dev, dtype=dt)
+    if kind == 'uniform':
+        return ps[0] + (ps[1] - ps[0]) * torch.rand(shape, device=dev, dtype=dt)
+    if kind == 'lognormal':
+        return torch.exp(ps[0] + ps[1] * torch.randn(shape, device=dev, dtype=dt))
+    if kind == 'logistic':
+        v = u()
+        return ps[0] + ps[1] * torch.log(v / (1 - v))
+    if kind == 'gumbel':
+        return ps[0] - ps[1] * torch.log(-torch.log(u()))
+    if kind == 'laplace':
+        v = u() - 0.5
+        return ps[0] - ps[1] * torch.sign(v) * torch.log1p(-2 * v.abs())
+    if kind == 'exponential':
+        return -torch.log1p(-u()) * ps[0]
+    if kind == 'rayleigh':
+        return ps[0] * torch.sqrt(-2.0 * torch.log1p(-u()))
+    if kind == 'weibull':
+        return torch.pow(-torch.log1p(-u()), 1.0 / ps[0])
+    if kind == 'pareto':
+        return torch.pow(1 - u(), -1.0 / ps[0]) - 1
+    if kind == 'power':
+        return torch.pow(u(), 1.0 / ps[0])
+    if kind == 'gamma':
+        k = ps[0].expand(shape)
+        return torch.distributions.Gamma(k, torch.ones_like(k)).rsample() * ps[1]
+    if kind == 'beta':
+        return torch.distributions.Beta(ps[0].expand(shape), ps[1].expand(shape)).rsample()
+    if kind == 'chisquare':
+        k = (ps[0] / 2).expand(shape)
+        return torch.distributions.Gamma(k, torch.ones_like(k)).rsample() * 2
+    raise MXNetError('unknown sampler %s' % kind)
+
+
+def _sampler_check(kind, ps):
+    from ..base import AsyncValueError
+
+    def positive(t, name, strict=True):
+        bad = (t <= 0) if strict else (t < 0)
+        if bool(bad.any()):
+            # a ValueError in the reference (CHECK -> "ValueError:" prefixed MXNetError)
+            raise AsyncValueError('Check failed: %s %s 0 (%s sampler)' % (name, '>' if strict else '>=', kind))
+    if kind in ('normal', 'lognormal', 'logistic', 'gumbel', 'laplace'):
+        positive(ps[1], 'scale', strict=False)
+    elif kind in ('exponential', 'rayleigh'):
+        positive(ps[0], 'scale', strict=False)
+    elif kind in ('weibull', 'pareto', 'power', 'chisquare'):
+        positive(ps[0], 'a')
+    elif kind == 'gamma':
+        positive(ps[0], 'shape')
+        positive(ps[1], 'scale')
+    elif kind == 'beta':
+        positive(ps[0], 'a')
+        positive(ps[1], 'b')
+
+
+@register('_npi_sampler', arg_names=_sampler_args,
+          params={'kind': ('str', 'normal'), 'pscal': ('any', ()), 'size': ('any', None), 'ctx': ('any', None),
+                  'dtype': ('str', 'float32'), 'batch': ('bool', False)})
+def _np_sampler(*arrays, kind='normal', pscal=(), size=None, ctx=None, dtype='float32', batch=False):
+    """``batch``: ``size`` is a batch shape prepended to the parameters' broadcast shape (npx *_n)."""
+    dt = _td(dtype if dtype not in (None, 'None') else 'float32', _FLOAT)
+    dev = arrays[0].device if arrays else _dev(ctx)
+    it = iter(arrays)
+    ps = []
+    for s in pscal:
+        if s is None:
+            a = next(it)
+            ps.append(a.to(dt) if a.dtype != dt else a)
+        else:
+            ps.append(torch.tensor(float(s), device=dev, dtype=dt))
+    pshape = tuple(torch.broadcast_shapes(*[tuple(p.shape) for p in ps])) if ps else ()
+    if size is None or size == ():
+        shape = pshape
+    else:
+        shape = (int(size),) if isinstance(size, int) else tuple(int(d) for d in size)
+        if batch:
+            shape = shape + pshape
+    _sampler_check(kind, ps)
+    if 0 in shape:
+        z = torch.zeros(shape, device=dev, dtype=dt)
+        # keep the (empty) result on the autograd tape of the parameters
+        return z + sum(p.sum() for p in ps if p.requires_grad) * 0 if any(p.requires_grad for p in ps) else z
+    cdt = torch.float32 if dt in (torch.float16, torch.bfloat16) and dev.type == 'cpu' else dt
+    ps = [(p.expand(shape) if p.dim() else p).to(cdt) for p in ps]
+    return _sampler_draw(kind, ps, shape, dev, cdt).to(dt)

@@ -195,6 +195,14 @@ class Symbol:
                 names.append('%s_output%d' % (node.name, idx))
         return names
 
+    def as_np_ndarray(self):
+        """The same graph viewed with NumPy semantics (``mx.sym.np``); graphs here are
+        dtype/shape-polymorphic, so this is the identity."""
+        return self
+
+    def as_nd_ndarray(self):
+        return self
+
     def get_internals(self):
         """Every visible output of every node (nnvm GetInternals honours FNumVisibleOutputs)."""
         outs = []

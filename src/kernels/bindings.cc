@@ -23,7 +23,7 @@ void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, c
                       void* dz,
                       const float* gamma, const float* mean, const float* invstd, const float* fscale,
                       const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R, int C,
-                      int relu_mode, int fix_gamma, int training, int accum, hipStream_t s);
+                      int relu_mode, int fix_gamma, int training, int accum, hipStream_t s, int ext_nblk);
 int bn_partials_rows(int64_t R, int C);
 void int8_gemm(const int8_t* A, const int8_t* B, int32_t* C, int M, int N, int K, hipStream_t s);
 void csr_dot_dense(int dtype, const int64_t* indptr, const int64_t* indices, const void* vals, const void* rhs,
@@ -52,7 +52,10 @@ void conv_nhwc_fwd(int dtype, const void* x, const void* w, const float* bias, v
 int conv_nhwc_fwd_big_nparts(int N, int H, int W, int R, int S, int sh, int sw, int ph, int pw, int variant);
 void conv_nhwc_fwd_big(int dtype, const void* x, const void* w, const float* bias, void* y, const void* zero, int N,
                        int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int variant,
-                       float* part, int nparts, const void* addend, hipStream_t s);
+                       float* part, int nparts, const void* addend, hipStream_t s, const void* bn_z,
+                       const float* bn_mean, const float* bn_scale, const float* bn_shift, const uint8_t* bn_mask,
+                       int bn_mode, float* bn_part, int bn_nparts);
+int conv_nhwc_fwd_big_bwd_nparts(int N, int H, int W, int R, int S, int sh, int sw, int ph, int pw, int variant);
 void conv_nhwc_fwd_glds(int dtype, const void* x, const void* w, const float* bias, void* y, const void* zero, int N,
                         int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int bco,
                         hipStream_t s);
@@ -213,12 +216,15 @@ PYBIND11_MODULE(_hip_kernels, m) {
                                uintptr_t dz,
                                uintptr_t g, uintptr_t mean, uintptr_t inv, uintptr_t fscale, uintptr_t fshift,
                                uintptr_t part, uintptr_t dgamma, uintptr_t dbeta, uintptr_t coef, int64_t R, int C,
-                               int relu_mode, int fix_gamma, int training, int accum, uintptr_t s) {
+                               int relu_mode, int fix_gamma, int training, int accum, uintptr_t s, int ext_nblk) {
     bn_nhwc_backward(dt, P<void>(x), P<void>(dy), P<void>(y), P<uint8_t>(mask), P<void>(dx), P<void>(dz), P<float>(g), P<float>(mean),
                      P<float>(inv), P<float>(fscale), P<float>(fshift), P<float>(part), P<float>(dgamma),
-                     P<float>(dbeta), P<float>(coef), R, C, relu_mode, fix_gamma, training, accum, S(s));
+                     P<float>(dbeta), P<float>(coef), R, C, relu_mode, fix_gamma, training, accum, S(s), ext_nblk);
     check_launch("bn_nhwc_backward");
-  });
+  }, py::arg("dt"), py::arg("x"), py::arg("dy"), py::arg("y"), py::arg("mask"), py::arg("dx"), py::arg("dz"),
+     py::arg("g"), py::arg("mean"), py::arg("inv"), py::arg("fscale"), py::arg("fshift"), py::arg("part"),
+     py::arg("dgamma"), py::arg("dbeta"), py::arg("coef"), py::arg("R"), py::arg("C"), py::arg("relu_mode"),
+     py::arg("fix_gamma"), py::arg("training"), py::arg("accum"), py::arg("stream"), py::arg("ext_nblk") = 0);
   m.def("softmax_ce_forward", [](int dt, int li, uintptr_t logits, uintptr_t label, uintptr_t loss, uintptr_t lse,
                                  int N, int K, uintptr_t s) {
     softmax_ce_forward(dt, li, P<void>(logits), P<void>(label), P<float>(loss), P<float>(lse), N, K, S(s));
@@ -268,13 +274,23 @@ PYBIND11_MODULE(_hip_kernels, m) {
   // 512-thread big-tile kernel: variant 0..3 = 256x256, 128x256, 64x512, 256x128 (co x pix);
   // part (optional): channel-major [2][K][nparts] BatchNorm sum / sum-of-squares partials of y
   m.def("conv_nhwc_fwd_big_nparts", &conv_nhwc_fwd_big_nparts);
+  m.def("conv_nhwc_fwd_big_bwd_nparts", &conv_nhwc_fwd_big_bwd_nparts);
+  // bn (optional): (z, mean, scale, shift, mask, mode, part, nparts) -- BN-backward statistics of y
   m.def("conv_nhwc_fwd_big", [](int dt, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, uintptr_t zero, int N,
                                 int H, int W, int C, int K, int R, int Sf, int sh, int sw, int ph, int pw, int variant,
-                                uintptr_t part, int nparts, uintptr_t addend, uintptr_t s) {
+                                uintptr_t part, int nparts, uintptr_t addend, uintptr_t s, uintptr_t bz,
+                                uintptr_t bmean, uintptr_t bscale, uintptr_t bshift, uintptr_t bmask, int bmode,
+                                uintptr_t bpart, int bnparts) {
     conv_nhwc_fwd_big(dt, P<void>(x), P<void>(w), P<float>(bias), P<void>(y), P<void>(zero), N, H, W, C, K, R, Sf, sh,
-                      sw, ph, pw, variant, P<float>(part), nparts, P<void>(addend), S(s));
+                      sw, ph, pw, variant, P<float>(part), nparts, P<void>(addend), S(s), P<void>(bz), P<float>(bmean),
+                      P<float>(bscale), P<float>(bshift), P<uint8_t>(bmask), bmode, P<float>(bpart), bnparts);
     check_launch("conv_nhwc_fwd_big");
-  });
+  }, py::arg("dt"), py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("zero"), py::arg("N"),
+     py::arg("H"), py::arg("W"), py::arg("C"), py::arg("K"), py::arg("R"), py::arg("S"), py::arg("sh"),
+     py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("variant"), py::arg("part"), py::arg("nparts"),
+     py::arg("addend"), py::arg("stream"), py::arg("bn_z") = 0, py::arg("bn_mean") = 0, py::arg("bn_scale") = 0,
+     py::arg("bn_shift") = 0, py::arg("bn_mask") = 0, py::arg("bn_mode") = 0, py::arg("bn_part") = 0,
+     py::arg("bn_nparts") = 0);
   // persistent LDS-DMA ring kernel (conv_ring.hip): variant 0..5 = 128x128x4, 256x128x3, 128x256x3, 64x256x4,
   // 256x256x2, 64x128x4 (co x pix x stages); part as above
   m.def("conv_nhwc_fwd_ring_nparts", &conv_nhwc_fwd_ring_nparts);

@@ -410,10 +410,12 @@ template <typename T>
 static void bn_backward_impl(const void* x, const void* dy, const void* y, const uint8_t* mask, void* dx, void* dz,
                              const float* gamma, const float* mean, const float* invstd, const float* fscale,
                              const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R,
-                             int C, int relu_mode, int fix_gamma, int training, int accum, hipStream_t s) {
+                             int C, int relu_mode, int fix_gamma, int training, int accum, hipStream_t s,
+                             int ext_nblk) {
   BnGeom g = bn_geom(C);
   int nblk;
   int64_t rpb = bn_rows_per_block(R, C, g, &nblk);
+  if (ext_nblk > 0) nblk = ext_nblk;   // sum(dz) / sum(dz*(x-mean)) partials came from the dgrad epilogue
   dim3 grid(nblk, C / g.cb);
   float* p1 = part;
   float* p2 = part + static_cast<int64_t>(nblk) * C;
@@ -427,7 +429,8 @@ static void bn_backward_impl(const void* x, const void* dy, const void* y, const
   hipLaunchKernelGGL((bn_reduce_kernel<T, 1, RL>), grid, dim3(kBnThreads), 0, s, xa, dya, ya, mask, mean, fscale, \
                      fshift,                                                                                         \
                      p1, p2, R, C, g.tpr, g.rpi, rpb)
-  if (relu_mode == kReluFromY) RED(kReluFromY);
+  if (ext_nblk > 0) {
+  } else if (relu_mode == kReluFromY) RED(kReluFromY);
   else if (relu_mode == kReluFromX) RED(kReluFromX);
   else if (relu_mode == kReluFromMask) RED(kReluFromMask);
   else RED(kReluNone);
@@ -613,19 +616,19 @@ void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, c
                       void* dz,
                       const float* gamma, const float* mean, const float* invstd, const float* fscale,
                       const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R, int C,
-                      int relu_mode, int fix_gamma, int training, int accum, hipStream_t s) {
+                      int relu_mode, int fix_gamma, int training, int accum, hipStream_t s, int ext_nblk) {
   switch (dtype) {
     case kF16:
       bn_backward_impl<__half>(x, dy, y, mask, dx, dz, gamma, mean, invstd, fscale, fshift, part, dgamma, dbeta, coef, R,
-                               C, relu_mode, fix_gamma, training, accum, s);
+                               C, relu_mode, fix_gamma, training, accum, s, ext_nblk);
       break;
     case kBF16:
       bn_backward_impl<__hip_bfloat16>(x, dy, y, mask, dx, dz, gamma, mean, invstd, fscale, fshift, part, dgamma, dbeta,
-                                       coef, R, C, relu_mode, fix_gamma, training, accum, s);
+                                       coef, R, C, relu_mode, fix_gamma, training, accum, s, ext_nblk);
       break;
     default:
       bn_backward_impl<float>(x, dy, y, mask, dx, dz, gamma, mean, invstd, fscale, fshift, part, dgamma, dbeta, coef, R,
-                              C, relu_mode, fix_gamma, training, accum, s);
+                              C, relu_mode, fix_gamma, training, accum, s, ext_nblk);
   }
 }
 

@@ -74,6 +74,22 @@ struct MfmaB<__hip_bfloat16> {
   }
 };
 
+// Optional BatchNorm-backward statistics fused into the epilogue of a dgrad: y here is the gradient
+// dy arriving at a BatchNorm(+ReLU) whose input was z; per (channel, pixel tile) the kernel emits
+// sum(dz) and sum(dz * (z - mean)) with dz = dy * relu_mask (mode 2: mask = z*scale+shift > 0,
+// mode 3: the forward's 1-bit mask, mode 0: no ReLU), channel-major [2][K][nparts] like the forward
+// statistics -- the BatchNorm backward then skips its reduction pass over (dy, z).
+struct BnBwdFuse {
+  const void* z;
+  const float* mean;
+  const float* scale;
+  const float* shift;
+  const uint8_t* mask;
+  int mode;
+  float* part;
+  int nparts;
+};
+
 struct GeomB {
   int N, H, W, C, K, R, S;
   int Ho, Wo;
@@ -109,7 +125,7 @@ __global__ void __launch_bounds__(512) conv_fwd_big_kernel(const T* __restrict__
                                                            const float* __restrict__ bias, T* __restrict__ y,
                                                            const T* __restrict__ zero, GeomB g, int tiles_co,
                                                            float* __restrict__ part, int nparts,
-                                                           const T* __restrict__ addend) {
+                                                           const T* __restrict__ addend, BnBwdFuse bf) {
   constexpr int WPIX = 8 / WCO;
   constexpr int BCO = WCO * 64;
   constexpr int BPIX = WPIX * FJ * 16;
@@ -265,6 +281,24 @@ __global__ void __launch_bounds__(512) conv_fwd_big_kernel(const T* __restrict__
   // whole pixel rows: BCO*2 bytes = BCO/8 16-byte chunks per pixel
   constexpr int CPR = BCO / 8;
   constexpr int TOTAL = BPIX * CPR;
+  static_assert(512 % CPR == 0, "each thread keeps one 8-channel group");
+  const bool bnb = bf.part != nullptr;
+  // BN-backward statistics: this thread's channel group is fixed (tid % CPR)
+  float s1[8], s2[8], bm[8], bsc[8], bsh[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    s1[t] = 0.f;
+    s2[t] = 0.f;
+  }
+  if (bnb) {
+    const int cb = co0 + (tid % CPR) * 8;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      bm[t] = bf.mean[cb + t];
+      bsc[t] = bf.mode == 2 ? bf.scale[cb + t] : 0.f;
+      bsh[t] = bf.mode == 2 ? bf.shift[cb + t] : 0.f;
+    }
+  }
 #pragma unroll 4
   for (int e = tid; e < TOTAL; e += 512) {
     const int pl = e / CPR;
@@ -282,13 +316,48 @@ __global__ void __launch_bounds__(512) conv_fwd_big_kernel(const T* __restrict__
         for (int t = 0; t < 8; ++t) v.set(t, v.get(t) + a.get(t));
       }
       v.store(y + off);
+      if (bnb) {
+        Vec8<T> zv;
+        zv.load(static_cast<const T*>(bf.z) + off);
+        const uint32_t mb = bf.mode == 3 ? bf.mask[off >> 3] : 0xffu;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const float zt = zv.get(t);
+          bool keep = true;
+          if (bf.mode == 2) keep = fmaf(zt, bsc[t], bsh[t]) > 0.f;
+          if (bf.mode == 3) keep = (mb >> t) & 1u;
+          const float dz = keep ? v.get(t) : 0.f;
+          s1[t] += dz;
+          s2[t] += dz * (zt - bm[t]);
+        }
+      }
+    }
+  }
+  if (bnb) {
+    // combine the 512/CPR threads of each channel group through LDS, one partial per pixel tile
+    constexpr int ROWS = 512 / CPR;
+    float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      red[(tid / CPR) * BCO + (tid % CPR) * 8 + t] = s1[t];
+      red[ROWS * BCO + (tid / CPR) * BCO + (tid % CPR) * 8 + t] = s2[t];
+    }
+    __syncthreads();
+    for (int q = tid; q < 2 * BCO; q += 512) {
+      const int which = q / BCO, ch = q - which * BCO;
+      const float* col = red + which * ROWS * BCO + ch;
+      float acc_s = 0.f;
+#pragma unroll 8
+      for (int r = 0; r < ROWS; ++r) acc_s += col[r * BCO];
+      bf.part[(int64_t)which * g.K * bf.nparts + (int64_t)(co0 + ch) * bf.nparts + tpix] = acc_s;
     }
   }
 }
 
 template <typename T, int WCO, int FJ>
 void launch_big(const void* x, const void* w, const float* bias, void* y, const void* zero, const GeomB& g,
-                float* part, int nparts, const void* addend, hipStream_t s) {
+                float* part, int nparts, const void* addend, const BnBwdFuse& bf, hipStream_t s) {
   constexpr int BCO = WCO * 64;
   constexpr int BPIX = (8 / WCO) * FJ * 16;
   constexpr int SMEM = BigCfg<BCO, BPIX>::SMEM;
@@ -303,7 +372,7 @@ void launch_big(const void* x, const void* w, const float* bias, void* y, const 
   const int tiles_pix = (g.M + BPIX - 1) / BPIX;
   hipLaunchKernelGGL((conv_fwd_big_kernel<T, WCO, FJ>), dim3(tiles_co * tiles_pix), dim3(512), SMEM, s,
                      static_cast<const T*>(x), static_cast<const T*>(w), bias, static_cast<T*>(y),
-                     static_cast<const T*>(zero), g, tiles_co, part, nparts, static_cast<const T*>(addend));
+                     static_cast<const T*>(zero), g, tiles_co, part, nparts, static_cast<const T*>(addend), bf);
 }
 
 // variant -> (WCO, FJ): tile BCO x BPIX
@@ -320,12 +389,12 @@ static void big_tile(int variant, int* bco, int* bpix) {
 
 template <typename T>
 void dispatch_big(int variant, const void* x, const void* w, const float* bias, void* y, const void* zero,
-                  const GeomB& g, float* part, int nparts, const void* addend, hipStream_t s) {
+                  const GeomB& g, float* part, int nparts, const void* addend, const BnBwdFuse& bf, hipStream_t s) {
   switch (variant) {
-    case 0: launch_big<T, 4, 8>(x, w, bias, y, zero, g, part, nparts, addend, s); break;
-    case 1: launch_big<T, 2, 4>(x, w, bias, y, zero, g, part, nparts, addend, s); break;
-    case 2: launch_big<T, 1, 4>(x, w, bias, y, zero, g, part, nparts, addend, s); break;
-    case 3: launch_big<T, 4, 4>(x, w, bias, y, zero, g, part, nparts, addend, s); break;
+    case 0: launch_big<T, 4, 8>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
+    case 1: launch_big<T, 2, 4>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
+    case 2: launch_big<T, 1, 4>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
+    case 3: launch_big<T, 4, 4>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
   }
 }
 
@@ -341,9 +410,20 @@ int conv_nhwc_fwd_big_nparts(int N, int H, int W, int R, int S, int sh, int sw, 
   return ((M + bpix - 1) / bpix) * (8 / (bco / 64));
 }
 
+// BN-backward partials per channel the big kernel's fused epilogue writes (one per pixel tile).
+int conv_nhwc_fwd_big_bwd_nparts(int N, int H, int W, int R, int S, int sh, int sw, int ph, int pw, int variant) {
+  int bco, bpix;
+  big_tile(variant, &bco, &bpix);
+  const int Ho = (H + 2 * ph - R) / sh + 1;
+  const int Wo = (W + 2 * pw - S) / sw + 1;
+  return (N * Ho * Wo + bpix - 1) / bpix;
+}
+
 void conv_nhwc_fwd_big(int dtype, const void* x, const void* w, const float* bias, void* y, const void* zero, int N,
                        int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int variant,
-                       float* part, int nparts, const void* addend, hipStream_t s) {
+                       float* part, int nparts, const void* addend, hipStream_t s, const void* bn_z,
+                       const float* bn_mean, const float* bn_scale, const float* bn_shift, const uint8_t* bn_mask,
+                       int bn_mode, float* bn_part, int bn_nparts) {
   GeomB g;
   g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S;
   g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw;
@@ -359,8 +439,14 @@ void conv_nhwc_fwd_big(int dtype, const void* x, const void* w, const float* bia
                    "conv_nhwc_fwd_big: tensor too large for 32-bit indexing");
   MXAMD_HOST_CHECK(part == nullptr || nparts == conv_nhwc_fwd_big_nparts(N, H, W, R, S, sh, sw, ph, pw, variant),
                    "conv_nhwc_fwd_big: wrong BN partials count");
-  if (dtype == kF16) dispatch_big<__half>(variant, x, w, bias, y, zero, g, part, nparts, addend, s);
-  else if (dtype == kBF16) dispatch_big<__hip_bfloat16>(variant, x, w, bias, y, zero, g, part, nparts, addend, s);
+  BnBwdFuse bf{bn_z, bn_mean, bn_scale, bn_shift, bn_mask, bn_mode, bn_part, bn_nparts};
+  MXAMD_HOST_CHECK(bn_part == nullptr ||
+                       (bn_z && bn_mean && bn_nparts == conv_nhwc_fwd_big_bwd_nparts(N, H, W, R, S, sh, sw, ph, pw,
+                                                                                     variant) &&
+                        (bn_mode != 2 || (bn_scale && bn_shift)) && (bn_mode != 3 || bn_mask)),
+                   "conv_nhwc_fwd_big: bad BN-backward epilogue arguments");
+  if (dtype == kF16) dispatch_big<__half>(variant, x, w, bias, y, zero, g, part, nparts, addend, bf, s);
+  else if (dtype == kBF16) dispatch_big<__hip_bfloat16>(variant, x, w, bias, y, zero, g, part, nparts, addend, bf, s);
   else throw std::runtime_error("conv_nhwc_fwd_big: dtype must be f16 or bf16");
 }
 

@@ -877,3 +877,55 @@ def test_splitk_fc_wgrad_accumulates_into_grad(splits, nk):
     nlp_fns._splitk_wgrad(dy, x, splits, g, True)
     ref = base + dy.float().t() @ x.float()
     torch.testing.assert_close(g.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+def test_bn_backward_stats_fused_into_dgrad_epilogue(dtype):
+    """conv1 -> BN+ReLU -> conv2 (3x3): with the dgrad of conv2 on the big-tile kernel, its epilogue
+    emits the BN backward statistics and the BN skips its reduction; gradients match the unfused
+    path (BN reduce kernel) and an fp32 torch reference."""
+    from mxnet_maintenance_amd.ops import kernel_fns as KF
+    _lib()
+    torch.manual_seed(7)
+    N, H, C = 4, 14, 128
+    x0 = torch.randn(N, H, H, C, device='cuda').to(dtype)
+    w1 = (torch.randn(C, 1, 1, C, device='cuda') / C ** 0.5).to(dtype)
+    w2 = (torch.randn(C, 3, 3, C, device='cuda') / (9 * C) ** 0.5).to(dtype)
+    g0 = torch.rand(C, device='cuda') + 0.5
+    b0 = torch.randn(C, device='cuda') * 0.1
+
+    def run(fuse):
+        KF._BN_BWD_FUSE[0] = fuse
+        x = x0.clone().requires_grad_(True)
+        g = g0.clone().requires_grad_(True)
+        b = b0.clone().requires_grad_(True)
+        z = KF.ConvNHWC.apply(x, w1, None, (1, 1), (0, 0), (1, 1))
+        y, _m, _v = KF.BatchNormNHWC.apply(z, g, b, None, 1e-5, True, True, torch.zeros(C, device='cuda'),
+                                            torch.ones(C, device='cuda'), 0.9)
+        key = ('dgrad', tuple(y.shape), tuple(w2.shape), (1, 1), (1, 1), dtype)
+        KF._ALGO[key] = 'hip10'
+        if fuse:
+            assert getattr(y, '_mxamd_bn_src', None) is not None
+        out = KF.ConvNHWC.apply(y, w2, None, (1, 1), (1, 1), (1, 1))
+        (out.float() ** 2).mean().backward()
+        return x.grad.float(), g.grad.float(), b.grad.float()
+
+    try:
+        fused = run(True)
+        plain = run(False)
+    finally:
+        KF._BN_BWD_FUSE[0] = True
+    # fp32 reference of the same graph
+    xr = x0.float().requires_grad_(True)
+    gr = g0.clone().requires_grad_(True)
+    br = b0.clone().requires_grad_(True)
+    zr = F.conv2d(xr.permute(0, 3, 1, 2), w1.float().permute(0, 3, 1, 2))
+    yr = F.relu(F.batch_norm(zr, None, None, gr, br, training=True, eps=1e-5))
+    outr = F.conv2d(yr, w2.float().permute(0, 3, 1, 2), padding=1)
+    (outr ** 2).mean().backward()
+    refs = (xr.grad, gr.grad, br.grad)
+    for a, p, r, name in zip(fused, plain, refs, ('dx', 'dgamma', 'dbeta')):
+        scale = r.abs().max().item() + 1e-6
+        tol = (3e-2 if dtype == torch.float16 else 8e-2) * scale
+        torch.testing.assert_close(a, p, rtol=0, atol=tol, msg=lambda m: '%s fused vs unfused: %s' % (name, m))
+        torch.testing.assert_close(a, r, rtol=0, atol=tol, msg=lambda m: '%s fused vs fp32: %s' % (name, m))

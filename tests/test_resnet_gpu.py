@@ -1,0 +1,80 @@
+"""Headline-path correctness on the GPU: the NHWC fp16 ResNet with fused BN kernels trained by a
+captured gluon.GraphStep matches the eager step, and the BatchNorm-backward statistics fused into
+the dgrad epilogues give the same gradients as the separate BN reduction kernels."""
+import numpy as np
+import pytest
+import torch
+
+import mxnet_maintenance_amd as mx
+from mxnet_maintenance_amd import autograd, gluon, nd
+
+pytestmark = pytest.mark.gpu
+
+
+def _resnet(seed, name='resnet18_v1'):
+    mx.random.seed(seed)
+    net = gluon.model_zoo.vision.get_model(name, layout='NHWC', fuse=True, classes=10)
+    net.initialize(mx.init.Xavier(rnd_type='gaussian', factor_type='in', magnitude=2), ctx=mx.gpu(0))
+    net.cast('float16')
+    net.hybridize(static_alloc=True, static_shape=True)
+    return net
+
+
+def _data(steps, batch=16, size=64):
+    rs = np.random.RandomState(0)
+    xs = [nd.array(rs.uniform(-1, 1, (batch, size, size, 3)), ctx=mx.gpu(0), dtype='float16') for _ in range(steps)]
+    ys = [nd.array(rs.randint(0, 10, (batch,)), ctx=mx.gpu(0)) for _ in range(steps)]
+    return xs, ys
+
+
+def _train(graph, steps=5, name='resnet18_v1'):
+    net = _resnet(3, name)
+    trainer = gluon.Trainer(net.collect_params(), 'sgd', {'learning_rate': 1e-3, 'momentum': 0.9, 'wd': 1e-4,
+                                                          'multi_precision': True, 'rescale_grad': 1.0 / 128})
+    loss_fn = gluon.loss.SoftmaxCrossEntropyLoss()
+    xs, ys = _data(steps)
+
+    def step(x, y):
+        with autograd.record():
+            loss = loss_fn(net(x), y) * 128
+        loss.backward()
+        trainer.step(x.shape[0])
+        return loss
+
+    run = gluon.GraphStep(step, trainer, warmup=2) if graph else step
+    losses = [float(run(x, y).mean().asscalar()) / 128 for x, y in zip(xs, ys)]
+    if graph:
+        assert run.captured
+    params = [p.data().asnumpy().astype(np.float32) for p in net.collect_params().values()]
+    return losses, params
+
+
+@pytest.mark.parametrize('name', ['resnet18_v1', 'resnet50_v1b'])
+def test_resnet_graph_step_matches_eager(name):
+    le, we = _train(False, name=name)
+    lg, wg = _train(True, name=name)
+    np.testing.assert_allclose(lg, le, rtol=2e-2, atol=2e-2)
+    for a, b in zip(wg, we):
+        err = np.linalg.norm(a - b) / (np.linalg.norm(b) + 1e-6)
+        assert err < 2e-3, err
+
+
+def test_resnet_bn_backward_fusion_matches_unfused():
+    from mxnet_maintenance_amd.ops import kernel_fns as KF
+    xs, ys = _data(1)
+    loss_fn = gluon.loss.SoftmaxCrossEntropyLoss()
+    grads = {}
+    try:
+        for fuse in (False, True, True):      # the second fused pass runs with autotuned (big-kernel) dgrads
+            KF._BN_BWD_FUSE[0] = fuse
+            net = _resnet(5, 'resnet50_v1b')
+            with autograd.record():
+                loss = loss_fn(net(xs[0]), ys[0]).mean() * 128
+            loss.backward()
+            grads[fuse] = [p.grad().asnumpy().astype(np.float32) for p in net.collect_params().values()
+                           if p.grad_req != 'null']
+    finally:
+        KF._BN_BWD_FUSE[0] = True
+    for a, b in zip(grads[True], grads[False]):
+        err = np.linalg.norm(a - b) / (np.linalg.norm(b) + 1e-3)
+        assert err < 3e-2, err

@@ -78,7 +78,8 @@ def run_one(ref, name, timeout, workers, select=None, tb=None):
         for n, k in re.findall(r'(\d+) (passed|failed|skipped|errors?|xfailed|xpassed)', tail):
             counts[k] += int(n)
         counts['errors'] += counts.pop('error')
-        return {'file': name, **counts, 'summary': tail, 'output': r.stdout[-20000:]}
+        keep = int(os.environ.get('MXREF_KEEP_OUTPUT', '20000'))
+        return {'file': name, **counts, 'summary': tail, 'output': r.stdout[-keep:]}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
