@@ -92,7 +92,7 @@ def _ctx(ctx):
 
 
 def _is_scalar(x):
-    return isinstance(x, (numbers.Number, onp.generic, bool)) and not isinstance(x, onp.ndarray)
+    return isinstance(x, (numbers.Number, onp.generic, builtins.bool)) and not isinstance(x, onp.ndarray)
 
 
 def _py(x):
@@ -163,7 +163,7 @@ class ndarray(NDArray):
 
     def __bool__(self):
         if self.size == 1:
-            return bool(self._data.reshape(-1)[0].item())
+            return builtins.bool(self._data.reshape(-1)[0].item())
         if self.size == 0:
             return False
         raise ValueError('The truth value of an ndarray with more than one element is ambiguous. '
@@ -577,7 +577,7 @@ def full(shape, fill_value, dtype=None, order='C', ctx=None, out=None):
     if isinstance(fill_value, NDArray):
         return broadcast_to(fill_value.astype(dtype) if dtype else fill_value, _shape(shape))
     if dtype is None:
-        dtype = 'bool' if isinstance(fill_value, bool) else ('int64' if isinstance(fill_value, int) else 'float32')
+        dtype = 'bool' if isinstance(fill_value, builtins.bool) else ('int64' if isinstance(fill_value, int) else 'float32')
     return _call('_npi_full', shape=_shape(shape), ctx=_ctx(ctx), dtype=dtype, value=_py(fill_value), out=out)
 
 
@@ -1390,12 +1390,12 @@ __all__.append('may_share_memory')
 def array_equal(a1, a2, equal_nan=False):
     if tuple(a1.shape) != tuple(a2.shape):
         return False
-    return bool(all(equal(a1, a2)).item())
+    return builtins.bool(all(equal(a1, a2)).item())
 
 
 @_export
 def allclose(a, b, rtol=1e-05, atol=1e-08, equal_nan=False):
-    return bool(onp.allclose(_host(a), _host(b), rtol, atol, equal_nan))
+    return builtins.bool(onp.allclose(_host(a), _host(b), rtol, atol, equal_nan))
 
 
 @_export
@@ -1413,7 +1413,7 @@ dtype = onp.dtype
 float16, float32, float64 = onp.float16, onp.float32, onp.float64
 int8, int16, int32, int64, uint8 = onp.int8, onp.int16, onp.int32, onp.int64, onp.uint8
 bool_ = onp.bool_
-bool = onp.bool_          # noqa: A001  (mx.np.bool exists in the reference; NumPy 2 dropped np.bool)
+globals()['bool'] = onp.bool_   # mx.np.bool exists in the reference (NumPy 2 dropped np.bool); module code uses builtins.bool
 uint16, uint32, uint64 = onp.uint16, onp.uint32, onp.uint64
 complex64, complex128 = onp.complex64, onp.complex128
 pi, e, inf, nan, newaxis, euler_gamma = onp.pi, onp.e, onp.inf, onp.nan, None, onp.euler_gamma
