@@ -1,0 +1,412 @@
+"""ImageRecordIter family: RecordIO image batches with the reference's augmenter set.
+
+Parity:
+* src/io/iter_image_recordio_2.cc (ImageRecordIter2: record parsing, label
+  width / image list labels, partitioning, seeds, ProcessImage normalisation at
+  :376, dtype float32/uint8/int8 outputs, ctx-optimised pinned batches),
+* src/io/image_aug_default.cc:45-168 (every DefaultImageAugmentParam field),
+* src/io/image_iter_common.h:141-367 (ImageRecParserParam, ImageRecordParam,
+  ImageNormalizeParam, PrefetcherParam),
+* src/io/iter_normalize.h (mean image creation when ``mean_img`` does not exist),
+* src/io/iter_image_det_recordio.cc (detection labels: header + objects).
+
+Pipeline: the native RecordPrefetcher reads records on its own thread; for each
+image a dependency-engine task decodes it (PIL, GIL released while decoding)
+and runs the native augmenter (src/native/image_aug.cc, GIL released), which
+writes the normalised image straight into its batch slot.  Batch buffers come
+from the native pinned HostStorage pool when the iterator feeds a GPU
+(``ctx='gpu'``, the reference default) and a HIP device is present, so the
+host->device copy is a direct DMA; otherwise from ordinary host memory.  The
+next batch is decoded while the current one trains (prefetch).
+
+Arguments the reference accepts are all implemented; an argument the
+reference does not know either is reported with a warning (the reference's
+``InitAllowUnknown`` accepts it silently).
+"""
+import ctypes
+import os
+import warnings
+
+import numpy as np
+
+from ..base import MXNetError
+from .. import ndarray as nd
+from ..ndarray.ndarray import NDArray
+
+# DefaultImageAugmentParam (image_aug_default.cc:45)
+_AUG_FIELDS = dict(resize=-1, rand_crop=False, random_resized_crop=False, max_rotate_angle=0,
+                   max_aspect_ratio=0.0, min_aspect_ratio=None, max_shear_ratio=0.0, max_crop_size=-1,
+                   min_crop_size=-1, max_random_scale=1.0, min_random_scale=1.0, max_random_area=1.0,
+                   min_random_area=1.0, min_img_size=0.0, max_img_size=1e10, brightness=0.0, contrast=0.0,
+                   saturation=0.0, pca_noise=0.0, random_h=0, random_s=0, random_l=0, rotate=-1,
+                   fill_value=255, inter_method=1, pad=0, rotate_list=None)
+# ImageNormalizeParam (image_iter_common.h:247)
+_NORM_FIELDS = dict(mirror=False, rand_mirror=False, mean_img='', mean_r=0.0, mean_g=0.0, mean_b=0.0,
+                    mean_a=0.0, std_r=1.0, std_g=1.0, std_b=1.0, std_a=1.0, scale=1.0,
+                    max_random_contrast=0.0, max_random_illumination=0.0)
+# ImageRecParserParam + ImageRecordParam + BatchParam + PrefetcherParam
+_ITER_FIELDS = dict(path_imglist='', path_imgidx='', aug_seq='aug_default', label_width=1,
+                    preprocess_threads=4, verbose=True, num_parts=1, part_index=0, device_id=0,
+                    shuffle_chunk_size=0, shuffle_chunk_seed=0, seed_aug=None, round_batch=True,
+                    shuffle=False, seed=0, prefetch_buffer=4, ctx='gpu', dtype=None, data_name='data',
+                    label_name='softmax_label', layout='NCHW')
+
+_OUT_DTYPES = {None: np.float32, 'float32': np.float32, 'uint8': np.uint8, 'int8': np.int8,
+               'float16': np.float32, 'bfloat16': np.float32, 'float64': np.float32}
+
+
+def _native():
+    from .._lib import _native as n   # pylint: disable=import-outside-toplevel
+    return n
+
+
+class _PinnedRing:
+    """Batch buffers leased from the native pinned HostStorage pool (reused round-robin)."""
+
+    def __init__(self, nbytes, count):
+        self._store = _native().HostStorage(True)
+        self.pinned = self._store.pinned
+        self._ptrs = [self._store.alloc(nbytes) for _ in range(count)]
+        self._nbytes = nbytes
+        self._i = 0
+
+    def take(self, shape, dtype):
+        ptr = self._ptrs[self._i % len(self._ptrs)]
+        self._i += 1
+        raw = (ctypes.c_uint8 * self._nbytes).from_address(ptr)
+        n = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        return np.frombuffer(raw, dtype=np.uint8, count=n).view(dtype).reshape(shape)
+
+    def __del__(self):
+        try:
+            for p in self._ptrs:
+                self._store.free(p)
+            self._store.release_all()
+        except Exception:      # pylint: disable=broad-except
+            pass
+
+
+def _gpu_present():
+    try:
+        import torch     # pylint: disable=import-outside-toplevel
+        return torch.cuda.is_available()
+    except Exception:    # pylint: disable=broad-except
+        return False
+
+
+class ImageRecordPipeline:
+    """Parameter handling and the decode/augment/batch pipeline shared by the ImageRecord
+    iterators of :mod:`mxnet_maintenance_amd.io` (see the module docstring)."""
+
+    _default_dtype = None
+
+    def _setup(self, path_imgrec, data_shape, batch_size, kwargs):
+        params = dict(_AUG_FIELDS)
+        params.update(_NORM_FIELDS)
+        params.update(_ITER_FIELDS)
+        if self._default_dtype is not None:
+            params['dtype'] = self._default_dtype
+        unknown = sorted(k for k in kwargs if k not in params)
+        if unknown:
+            warnings.warn('ImageRecordIter: unknown argument(s) %s are ignored' % ', '.join(unknown),
+                          stacklevel=3)
+        params.update({k: v for k, v in kwargs.items() if k in params})
+        self._p = params
+        if not path_imgrec or not os.path.exists(path_imgrec):
+            raise MXNetError('ImageRecordIter: path_imgrec %r does not exist' % (path_imgrec,))
+        data_shape = tuple(int(d) for d in data_shape)
+        if len(data_shape) != 3:
+            raise MXNetError('ImageRecordIter: data_shape must be (channels, height, width)')
+        self.path = path_imgrec
+        self.data_shape = data_shape
+        self.label_width = int(params['label_width'])
+        self.shuffle = bool(params['shuffle'])
+        self.round_batch = bool(params['round_batch'])
+        self.layout = params['layout']
+        if self.layout not in ('NCHW', 'NHWC'):
+            raise MXNetError('ImageRecordIter: layout must be NCHW or NHWC')
+        dt = params['dtype']
+        dt = None if dt is None else np.dtype(dt).name
+        if dt not in _OUT_DTYPES:
+            raise MXNetError('ImageRecordIter: unsupported dtype %s' % dt)
+        self.dtype = dt or 'float32'
+        self._slot_dtype = _OUT_DTYPES[dt]
+        self._aug = self._make_aug_param(params)
+        msg = self._aug.check()
+        if msg:
+            raise MXNetError(msg)
+        self._rng = np.random.RandomState(int(params['seed']))
+        seed_aug = params['seed_aug']
+        self._aug_rng = np.random.RandomState(int(seed_aug) if seed_aug is not None else
+                                              int(params['seed']) + 0x5eed)
+        self._labels_by_id = self._read_imglist(params['path_imglist'])
+        self.offsets = self._index(path_imgrec, params['path_imgidx'])
+        parts, part = int(params['num_parts']), int(params['part_index'])
+        if parts > 1:
+            n = len(self.offsets) // parts
+            self.offsets = self.offsets[part * n:(part + 1) * n]
+        if params['mean_img']:
+            self._aug.mean_img = self._mean_image(params['mean_img'])
+        c, h, w = data_shape
+        self._slot_shape = (c, h, w) if self.layout == 'NCHW' else (h, w, c)
+        self._batch_shape = (batch_size,) + self._slot_shape
+        self._ring = None
+        if str(params['ctx']) == 'gpu' and _gpu_present():
+            nbytes = int(np.prod(self._batch_shape)) * np.dtype(self._slot_dtype).itemsize
+            try:
+                ring = _PinnedRing(nbytes, int(params['prefetch_buffer']) + 2)
+                self._ring = ring if ring.pinned else None
+            except Exception:      # pylint: disable=broad-except
+                self._ring = None
+        from .. import engine      # pylint: disable=import-outside-toplevel
+        self._engine = engine
+        self._slot_vars = [engine.new_var('imrec_slot%d' % i) for i in range(batch_size)]
+        self._inflight = None
+
+    # -- parameters --------------------------------------------------------------------------------------
+    def _make_aug_param(self, p):
+        a = _native().AugParam()
+        a.out_c, a.out_h, a.out_w = self.data_shape
+        for k in ('resize', 'max_rotate_angle', 'max_crop_size', 'min_crop_size', 'random_h', 'random_s',
+                  'random_l', 'rotate', 'fill_value', 'inter_method', 'pad'):
+            setattr(a, k, int(p[k]))
+        for k in ('max_aspect_ratio', 'max_shear_ratio', 'max_random_scale', 'min_random_scale',
+                  'max_random_area', 'min_random_area', 'min_img_size', 'max_img_size', 'brightness',
+                  'contrast', 'saturation', 'pca_noise', 'scale', 'max_random_contrast',
+                  'max_random_illumination'):
+            setattr(a, k, float(p[k]))
+        for k in ('rand_crop', 'random_resized_crop', 'mirror', 'rand_mirror'):
+            setattr(a, k, bool(p[k]))
+        if p['min_aspect_ratio'] is not None:
+            a.has_min_aspect_ratio = True
+            a.min_aspect_ratio = float(p['min_aspect_ratio'])
+        rl = p['rotate_list']
+        if rl:
+            a.rotate_list = [int(x) for x in (rl.split(',') if isinstance(rl, str) else rl)]
+        a.mean = [float(p['mean_r']), float(p['mean_g']), float(p['mean_b']), float(p['mean_a'])]
+        a.std = [float(p['std_r']), float(p['std_g']), float(p['std_b']), float(p['std_a'])]
+        if self.data_shape[0] == 1:
+            a.mean = [float(p['mean_r'])] * 4
+            a.std = [float(p['std_r'])] * 4
+        return a
+
+    @staticmethod
+    def _read_imglist(path):
+        """``index\\tlabel...\\tpath`` lines: labels override the record headers (ImageRecParserParam.path_imglist)."""
+        if not path:
+            return None
+        out = {}
+        with open(path) as f:
+            for line in f:
+                parts = line.strip().split('\t')
+                if len(parts) >= 3:
+                    out[int(float(parts[0]))] = np.array([float(x) for x in parts[1:-1]], dtype=np.float32)
+        return out
+
+    @staticmethod
+    def _index(path_imgrec, path_imgidx):
+        if path_imgidx and os.path.exists(path_imgidx):
+            offs = []
+            with open(path_imgidx) as f:
+                for line in f:
+                    p = line.strip().split('\t')
+                    if len(p) == 2:
+                        offs.append(int(p[1]))
+            return offs
+        from .. import recordio     # pylint: disable=import-outside-toplevel
+        offs = []
+        rd = recordio.MXRecordIO(path_imgrec, 'r')
+        while True:
+            pos = rd.handle.tell()
+            if rd.read() is None:
+                break
+            offs.append(pos)
+        rd.close()
+        return offs
+
+    def _mean_image(self, path):
+        """Load the (c, h, w) mean image, or compute it over the dataset and save it (iter_normalize.h)."""
+        c, h, w = self.data_shape
+        if os.path.exists(path):
+            loaded = nd.load(path)
+            arr = list(loaded.values())[0] if isinstance(loaded, dict) else loaded[0]
+            m = arr.asnumpy().astype(np.float32)
+            if m.shape != (c, h, w):
+                raise MXNetError('ImageRecordIter: mean_img %s has shape %s, expected %s'
+                                 % (path, m.shape, (c, h, w)))
+            return m.reshape(-1).tolist()
+        n = _native()
+        plain = n.AugParam()
+        plain.out_c, plain.out_h, plain.out_w = c, h, w
+        plain.resize = self._aug.resize
+        plain.inter_method = self._aug.inter_method if self._aug.inter_method in (0, 1, 2, 3, 4) else 1
+        acc = np.zeros((c, h, w), dtype=np.float64)
+        slot = np.empty((c, h, w), dtype=np.uint8)
+        from .. import recordio      # pylint: disable=import-outside-toplevel
+        rd = recordio.MXRecordIO(self.path, 'r')
+        cnt = 0
+        for off in self.offsets:
+            rd.handle.seek(off)
+            rec = rd.read()
+            _, img = recordio.unpack(rec)
+            n.augment_into(self._decode_img(img), plain, 0, slot, True)
+            acc += slot
+            cnt += 1
+        rd.close()
+        mean = (acc / max(cnt, 1)).astype(np.float32)
+        nd.save(path, {'mean_img': nd.array(mean)})
+        return mean.reshape(-1).tolist()
+
+    # -- decode ------------------------------------------------------------------------------------------
+    def _decode_img(self, img):
+        from ..image import imdecode_np    # pylint: disable=import-outside-toplevel
+        return imdecode_np(img, 0 if self.data_shape[0] == 1 else 1)
+
+    def _label_of(self, header):
+        if self._labels_by_id is not None:
+            lab = self._labels_by_id.get(int(header.id))
+            if lab is None:
+                raise MXNetError('ImageRecordIter: image id %d not in path_imglist' % header.id)
+            return lab
+        return np.asarray(header.label, dtype=np.float32).reshape(-1)
+
+    def _process(self, rec, seed, slot):
+        """Decode + augment one record into ``slot``; returns its label vector."""
+        from ..recordio import unpack     # pylint: disable=import-outside-toplevel
+        header, img = unpack(rec)
+        try:
+            _native().augment_into(self._decode_img(img), self._aug, int(seed), slot, self.layout == 'NCHW')
+        except ValueError as e:
+            raise MXNetError('ImageRecordIter: %s' % e)
+        return self._label_of(header)
+
+    # -- iteration ---------------------------------------------------------------------------------------
+    def _restart(self):
+        self._drain()
+        order = list(self.offsets)
+        if self.shuffle:
+            self._rng.shuffle(order)
+        self._order = order
+        self._cursor = 0
+        try:
+            self._reader = _native().RecordPrefetcher(self.path, [int(o) for o in order], 4 * self.batch_size)
+        except Exception:     # pylint: disable=broad-except
+            from .. import recordio     # pylint: disable=import-outside-toplevel
+            self._reader = None
+            self._pyreader = recordio.MXRecordIO(self.path, 'r')
+
+    def _read_one(self, off):
+        if self._reader is not None:
+            return self._reader.next()
+        self._pyreader.handle.seek(off)
+        return self._pyreader.read()
+
+    def _launch(self):
+        """Read the next batch's records and push their decode tasks; None at the end of the epoch."""
+        n = len(self._order)
+        if self._cursor >= n:
+            return None
+        bs = self.batch_size
+        take = min(bs, n - self._cursor)
+        if take < bs and not self.round_batch:
+            return None
+        recs = [self._read_one(self._order[self._cursor + i]) for i in range(take)]
+        pad = bs - take
+        if pad:
+            recs += [recs[i % take] for i in range(pad)]
+        self._cursor += bs
+        seeds = self._aug_rng.randint(0, 2 ** 31 - 1, size=len(recs))
+        data = (self._ring.take(self._batch_shape, self._slot_dtype) if self._ring is not None
+                else np.empty(self._batch_shape, dtype=self._slot_dtype))
+        labels = [None] * len(recs)
+
+        def task(i, rec, seed):
+            labels[i] = self._process(rec, seed, data[i])
+        for i, (rec, seed) in enumerate(zip(recs, seeds)):
+            self._engine.push(lambda i=i, rec=rec, seed=int(seed): task(i, rec, seed),
+                              mutable_vars=[self._slot_vars[i]], name='imrec_decode')
+        return data, labels, pad
+
+    def _drain(self):
+        if getattr(self, '_inflight', None) is not None:
+            for v in self._slot_vars:
+                try:
+                    self._engine.wait_for_var(v)
+                except Exception:     # pylint: disable=broad-except
+                    pass
+        self._inflight = None
+
+    def _next_batch(self, batch_cls):
+        job = self._inflight if self._inflight is not None else self._launch()
+        self._inflight = None
+        if job is None:
+            raise StopIteration
+        data, labels, pad = job
+        for v in self._slot_vars:
+            self._engine.wait_for_var(v)      # re-raises a decode task's exception here
+        self._inflight = self._launch()       # prefetch: decode the next batch while this one trains
+        lab = self._stack_labels(labels)
+        import torch     # pylint: disable=import-outside-toplevel
+        t = torch.from_numpy(data)
+        if self.dtype in ('float16', 'bfloat16', 'float64'):
+            t = t.to(getattr(torch, self.dtype))
+        return batch_cls([NDArray(t)], [nd.array(lab)], pad=pad)
+
+    def _stack_labels(self, labels):
+        lw = self.label_width
+        out = np.zeros((len(labels), lw), dtype=np.float32)
+        for i, l in enumerate(labels):
+            l = np.asarray(l, dtype=np.float32).reshape(-1)[:lw]
+            out[i, :len(l)] = l
+        return out.reshape(-1) if lw == 1 else out
+
+
+class DetRecordPipeline(ImageRecordPipeline):
+    """Detection records: the image is resized to data_shape (no crop, so boxes stay valid) and
+    mirrored with its boxes; labels are padded to ``label_pad_width`` with -1
+    (iter_image_det_recordio.cc, image_det_aug_default.cc)."""
+
+    def _det_setup(self, label_pad_width):
+        self.label_pad_width = int(label_pad_width)
+        self.label_width = self.label_pad_width
+        a = self._aug
+        self._det_mirror = bool(a.rand_mirror) or bool(a.mirror)
+        self._det_mirror_always = bool(a.mirror)
+        a.rand_mirror = a.mirror = False
+        # geometry is applied here (resize to data_shape, box-aware mirror); the native augmenter
+        # only does colour and normalisation, so boxes stay valid
+        a.resize, a.rotate, a.pad, a.max_rotate_angle = -1, -1, 0, 0
+        a.rand_crop = a.random_resized_crop = a.has_min_aspect_ratio = False
+        a.max_aspect_ratio = a.max_shear_ratio = 0.0
+        a.max_crop_size = a.min_crop_size = -1
+        a.max_random_scale = a.min_random_scale = a.max_random_area = a.min_random_area = 1.0
+        a.min_img_size, a.max_img_size = 0.0, 1e10
+        a.rotate_list = []
+
+    def _process(self, rec, seed, slot):
+        from ..recordio import unpack     # pylint: disable=import-outside-toplevel
+        header, img = unpack(rec)
+        im = self._decode_img(img)
+        c, h, w = self.data_shape
+        if im.shape[0] != h or im.shape[1] != w:
+            im = _native().image_resize(im, w, h, 1)
+        rng = np.random.RandomState(int(seed))
+        flip = self._det_mirror_always or (self._det_mirror and rng.rand() < 0.5)
+        lab = self._label_of(header).copy()
+        if flip:
+            im = np.ascontiguousarray(im[:, ::-1])
+            if lab.size >= 2:
+                a, b = int(lab[0]), int(lab[1])      # header width, object width
+                if a >= 2 and b >= 5:
+                    objs = lab[a:a + (lab.size - a) // b * b].reshape(-1, b)
+                    xmin = objs[:, 1].copy()
+                    objs[:, 1] = 1.0 - objs[:, 3]
+                    objs[:, 3] = 1.0 - xmin
+                    lab[a:a + objs.size] = objs.reshape(-1)
+        try:
+            _native().augment_into(im, self._aug, int(seed), slot, self.layout == 'NCHW')
+        except ValueError as e:
+            raise MXNetError('ImageDetRecordIter: %s' % e)
+        out = np.full(self.label_pad_width, -1.0, dtype=np.float32)
+        out[:min(lab.size, self.label_pad_width)] = lab[:self.label_pad_width]
+        return out

@@ -19,9 +19,11 @@ from ..base import MXNetError
 from ..context import cpu
 from .. import ndarray as nd
 from ..ndarray.ndarray import NDArray
+from .image_record import ImageRecordPipeline, DetRecordPipeline
 
 __all__ = ['DataDesc', 'DataBatch', 'DataIter', 'ResizeIter', 'PrefetchingIter', 'NDArrayIter', 'MXDataIter',
-           'CSVIter', 'MNISTIter', 'ImageRecordIter', 'ImageRecordUInt8Iter', 'LibSVMIter', 'ImageDetRecordIter']
+           'CSVIter', 'MNISTIter', 'ImageRecordIter', 'ImageRecordUInt8Iter', 'ImageRecordInt8Iter', 'LibSVMIter',
+           'ImageDetRecordIter']
 
 
 class DataDesc(namedtuple('DataDesc', ['name', 'shape'])):
@@ -482,6 +484,13 @@ class MNISTIter(NDArrayIter):
             img, lab = img[perm], lab[perm]
         super().__init__(img, lab, batch_size=batch_size, shuffle=False, last_batch_handle='discard')
 
+    # native iterator accessors: the current batch's single data / label array
+    def getdata(self):
+        return self._batchify(self.data)[0]
+
+    def getlabel(self):
+        return self._batchify(self.label)[0]
+
 
 def _read_libsvm(path, ncol):
     """(dense rows [n, ncol], leading labels) of a LibSVM text file; malformed ids raise MXNetError."""
@@ -552,190 +561,50 @@ class LibSVMIter(DataIter):
 
 
 # ---------------------------------------------------------------------------
-# ImageRecordIter (src/io/iter_image_recordio_2.cc): native RecordIO read +
-# threaded PIL decode/augment + batching, prefetched one batch ahead.
+# ImageRecordIter family (src/io/iter_image_recordio_2.cc, image_aug_default.cc):
+# native RecordIO prefetch + engine decode tasks + native augmenter (image_record.py)
 # ---------------------------------------------------------------------------
 
-class ImageRecordIter(DataIter):
-    """Iterate over an image .rec file: decode, augment, normalise, batch (NCHW float32 by default)."""
+class ImageRecordIter(DataIter, ImageRecordPipeline):
+    """Iterate over an image .rec file: decode, augment, normalise, batch (NCHW float32 by default).
 
-    def __init__(self, path_imgrec, data_shape, batch_size, path_imgidx=None, label_width=1, shuffle=False,
-                 rand_crop=False, rand_mirror=False, mean_r=0.0, mean_g=0.0, mean_b=0.0, std_r=1.0, std_g=1.0,
-                 std_b=1.0, scale=1.0, resize=-1, preprocess_threads=4, prefetch_buffer=2, round_batch=True,
-                 data_name='data', label_name='softmax_label', dtype='float32', layout='NCHW', seed=0,
-                 num_parts=1, part_index=0, max_random_scale=1.0, min_random_scale=1.0, **kwargs):
-        super().__init__(batch_size)
-        from .. import recordio
-        self.path = path_imgrec
-        self.data_shape = tuple(data_shape)
-        self.label_width = label_width
-        self.shuffle = shuffle
-        self.rand_crop = rand_crop
-        self.rand_mirror = rand_mirror
-        self.mean = np.array([mean_r, mean_g, mean_b], dtype=np.float32)
-        self.std = np.array([std_r, std_g, std_b], dtype=np.float32)
-        self.scale = scale
-        self.resize = resize
-        self.threads = max(1, preprocess_threads)
-        self.round_batch = round_batch
-        self.dtype = dtype
-        self.layout = layout
-        self.rng = np.random.RandomState(seed)
-        # index: byte offsets of every record
-        if path_imgidx and os.path.exists(path_imgidx):
-            offs = []
-            with open(path_imgidx) as f:
-                for line in f:
-                    p = line.strip().split('\t')
-                    if len(p) == 2:
-                        offs.append(int(p[1]))
-        else:
-            offs = []
-            rd = recordio.MXRecordIO(path_imgrec, 'r')
-            while True:
-                pos = rd.handle.tell()
-                if rd.read() is None:
-                    break
-                offs.append(pos)
-            rd.close()
-        n = len(offs) // num_parts
-        self.offsets = offs[part_index * n:(part_index + 1) * n] if num_parts > 1 else offs
-        c, h, w = self.data_shape
-        shape = (batch_size, c, h, w) if layout == 'NCHW' else (batch_size, h, w, c)
-        self.provide_data = [DataDesc(data_name, shape, np.float32, layout)]
-        lshape = (batch_size,) if label_width == 1 else (batch_size, label_width)
-        self.provide_label = [DataDesc(label_name, lshape, np.float32)]
-        # decode + augmentation run as dependency-engine tasks (src/native/engine.cc worker threads; PIL
-        # releases the GIL while decoding): one engine variable per batch slot, and the next batch is
-        # pushed as soon as the current one is handed out, so decoding overlaps the training step
-        from .. import engine
-        self._engine = engine
-        self._slot_vars = [engine.new_var('imrec_slot%d' % i) for i in range(batch_size)]
-        self._inflight = None
+    Accepts every ImageRecordIter argument of the reference (augmenter, normaliser, parser and
+    prefetcher fields; see io/image_record.py)."""
+
+    def __init__(self, path_imgrec=None, data_shape=None, batch_size=None, **kwargs):
+        if data_shape is None or batch_size is None:
+            raise MXNetError('ImageRecordIter: data_shape and batch_size are required')
+        super().__init__(int(batch_size))
+        self._setup(path_imgrec, data_shape, int(batch_size), kwargs)
+        p = self._p
+        self.provide_data = [DataDesc(p['data_name'], self._batch_shape, np.dtype(self.dtype), self.layout)]
+        lshape = (self.batch_size,) if self.label_width == 1 else (self.batch_size, self.label_width)
+        self.provide_label = [DataDesc(p['label_name'], lshape, np.float32)]
         self.reset()
 
     def reset(self):
-        self._drain()
-        order = list(self.offsets)
-        if self.shuffle:
-            self.rng.shuffle(order)
-        self._order = order
-        self._cursor = 0
-        try:
-            from .._lib import _native
-            self._reader = _native.RecordPrefetcher(self.path, [int(o) for o in order], 4 * self.batch_size)
-        except Exception:
-            self._reader = None
-            from .. import recordio
-            self._pyreader = recordio.MXRecordIO(self.path, 'r')
-
-    def _read_one(self, off):
-        if self._reader is not None:
-            return self._reader.next()
-        self._pyreader.handle.seek(off)
-        return self._pyreader.read()
-
-    def _decode(self, rec, seed):
-        from ..recordio import unpack
-        from ..image import imdecode_np
-        header, img = unpack(rec)
-        arr = imdecode_np(img, 1)
-        rng = np.random.RandomState(seed)
-        c, h, w = self.data_shape
-        from PIL import Image
-        im = Image.fromarray(arr)
-        if self.resize > 0:
-            W, H = im.size
-            s = self.resize / min(W, H)
-            im = im.resize((max(1, int(W * s + 0.5)), max(1, int(H * s + 0.5))), Image.BILINEAR)
-        W, H = im.size
-        if W < w or H < h:
-            im = im.resize((max(W, w), max(H, h)), Image.BILINEAR)
-            W, H = im.size
-        if self.rand_crop:
-            x0 = rng.randint(0, W - w + 1)
-            y0 = rng.randint(0, H - h + 1)
-        else:
-            x0, y0 = (W - w) // 2, (H - h) // 2
-        im = im.crop((x0, y0, x0 + w, y0 + h))
-        a = np.asarray(im, dtype=np.float32)
-        if a.ndim == 2:
-            a = a[:, :, None].repeat(3, 2)
-        if self.rand_mirror and rng.rand() < 0.5:
-            a = a[:, ::-1]
-        a = (a - self.mean[:a.shape[2]]) / self.std[:a.shape[2]] * self.scale
-        if self.layout == 'NCHW':
-            a = a.transpose(2, 0, 1)
-        label = header.label
-        return np.ascontiguousarray(a), label
-
-    def _launch(self):
-        """Read the next batch's records and push their decode tasks; None at the end of the epoch."""
-        n = len(self._order)
-        if self._cursor >= n:
-            return None
-        bs = self.batch_size
-        take = min(bs, n - self._cursor)
-        if take < bs and not self.round_batch:
-            return None
-        recs = [self._read_one(self._order[self._cursor + i]) for i in range(take)]
-        pad = bs - take
-        if pad:
-            recs += [recs[i % take] for i in range(pad)]
-        self._cursor += bs
-        seeds = self.rng.randint(0, 2 ** 31 - 1, size=len(recs))
-        out = [None] * len(recs)
-
-        def task(i, rec, seed):
-            out[i] = self._decode(rec, seed)
-        for i, (rec, seed) in enumerate(zip(recs, seeds)):
-            self._engine.push(lambda i=i, rec=rec, seed=int(seed): task(i, rec, seed),
-                              mutable_vars=[self._slot_vars[i]], name='imrec_decode')
-        return out, pad
-
-    def _drain(self):
-        if getattr(self, '_inflight', None) is not None:
-            for v in self._slot_vars:
-                try:
-                    self._engine.wait_for_var(v)
-                except Exception:     # pylint: disable=broad-except
-                    pass
-        self._inflight = None
+        self._restart()
 
     def next(self):
-        job = self._inflight if self._inflight is not None else self._launch()
-        self._inflight = None
-        if job is None:
-            raise StopIteration
-        out, pad = job
-        for v in self._slot_vars[:len(out)]:
-            self._engine.wait_for_var(v)      # re-raises a decode task's exception here
-        self._inflight = self._launch()       # prefetch: decode the next batch while this one trains
-        data = np.stack([o[0] for o in out])
-        labels = np.array([np.asarray(o[1], dtype=np.float32).reshape(-1)[:self.label_width] for o in out],
-                          dtype=np.float32)
-        if self.label_width == 1:
-            labels = labels.reshape(-1)
-        return DataBatch([nd.array(data, dtype=self.dtype)], [nd.array(labels)], pad=pad)
+        return self._next_batch(DataBatch)
 
 
 class ImageRecordUInt8Iter(ImageRecordIter):
-    def __init__(self, *args, **kwargs):
-        kwargs['dtype'] = 'uint8'
-        super().__init__(*args, **kwargs)
+    """ImageRecordIter producing raw uint8 pixels."""
+    _default_dtype = 'uint8'
 
 
-class ImageDetRecordIter(ImageRecordIter):
-    """Detection variant: labels are variable-length object lists (padded with -1)."""
+class ImageRecordInt8Iter(ImageRecordIter):
+    """ImageRecordIter producing int8 pixels (value - round(mean), saturated)."""
+    _default_dtype = 'int8'
 
-    def __init__(self, *args, label_pad_width=350, **kwargs):
+
+class ImageDetRecordIter(DetRecordPipeline, ImageRecordIter):
+    """Detection variant: labels are variable-length object lists padded with -1."""
+
+    def __init__(self, path_imgrec=None, data_shape=None, batch_size=None, label_pad_width=350, **kwargs):
         kwargs.setdefault('label_width', label_pad_width)
-        super().__init__(*args, **kwargs)
-        self.label_pad_width = label_pad_width
-
-    def _decode(self, rec, seed):
-        a, label = super()._decode(rec, seed)
-        lab = np.full(self.label_pad_width, -1.0, dtype=np.float32)
-        l = np.asarray(label, dtype=np.float32).reshape(-1)[:self.label_pad_width]
-        lab[:len(l)] = l
-        return a, lab
+        ImageRecordIter.__init__(self, path_imgrec, data_shape, batch_size, **kwargs)
+        self._det_setup(label_pad_width)
+        self.provide_label = [DataDesc(self._p['label_name'], (self.batch_size, self.label_pad_width),
+                                       np.float32)]

@@ -1080,14 +1080,100 @@ def get_zip_data(data_dir, url, data_origin_name):
         _offline('get_zip_data(%s)' % url)
 
 
+# Synthetic stand-ins for the reference's downloadable test datasets (there is no network).  Only
+# when MXNET_TEST_SYNTHETIC_DATA=1 (set by tools/refconf): same file formats, shapes and class
+# balance as the real data, random pixels.  Generated once into a cache directory and linked.
+def _synthetic_enabled():
+    return os.environ.get('MXNET_TEST_SYNTHETIC_DATA', '0') == '1'
+
+
+def _synthetic_cache(name):
+    import tempfile
+    root = os.environ.get('MXNET_TEST_DATA_CACHE', os.path.join(tempfile.gettempdir(), 'mxamd_synthetic_data'))
+    d = os.path.join(root, name)
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def _link(src, dst):
+    if os.path.lexists(dst):
+        return
+    os.makedirs(os.path.dirname(os.path.abspath(dst)), exist_ok=True)
+    os.symlink(src, dst)
+
+
+def _make_synthetic_cifar10(d):
+    import io as _io
+    from PIL import Image
+    from . import recordio
+    for name, n in (('train', 50000), ('test', 10000)):
+        rec = os.path.join(d, name + '.rec')
+        if os.path.exists(rec):
+            continue
+        rng = np.random.RandomState(7 if name == 'train' else 8)
+        tmp = rec + '.part'
+        w = recordio.MXRecordIO(tmp, 'w')
+        for i in range(n):
+            img = rng.randint(0, 256, size=(32, 32, 3), dtype=np.uint8)
+            buf = _io.BytesIO()
+            Image.fromarray(img).save(buf, format='PNG')
+            w.write(recordio.pack(recordio.IRHeader(0, float(i % 10), i, 0), buf.getvalue()))
+        w.close()
+        os.replace(tmp, rec)
+
+
+def _make_synthetic_mnist(d):
+    import struct as _struct
+    for prefix, n, seed in (('train', 60000, 1), ('t10k', 10000, 2)):
+        img, lab = os.path.join(d, prefix + '-images-idx3-ubyte'), os.path.join(d, prefix + '-labels-idx1-ubyte')
+        if os.path.exists(img) and os.path.exists(lab):
+            continue
+        rng = np.random.RandomState(seed)
+        with open(img + '.part', 'wb') as f:
+            f.write(_struct.pack('>IIII', 2051, n, 28, 28))
+            f.write(rng.randint(0, 256, size=(n, 28, 28), dtype=np.uint8).tobytes())
+        with open(lab + '.part', 'wb') as f:
+            f.write(_struct.pack('>II', 2049, n))
+            f.write((np.arange(n) % 10).astype(np.uint8).tobytes())
+        os.replace(img + '.part', img)
+        os.replace(lab + '.part', lab)
+
+
+def _make_synthetic_libsvm(path, n, dim, nclass, seed=3):
+    if os.path.exists(path):
+        return
+    rng = np.random.RandomState(seed)
+    with open(path + '.part', 'w') as f:
+        for i in range(n):
+            idx = np.sort(rng.choice(dim, size=rng.randint(1, 40), replace=False))
+            f.write('%d %s\n' % (1 + i % nclass, ' '.join('%d:%.4f' % (j, rng.rand()) for j in idx)))
+    os.replace(path + '.part', path)
+
+
+_SYNTHETIC_LIBSVM = {'news20.t': (3993, 62061, 20)}
+
+
 def get_bz2_data(data_dir, data_name, url, data_origin_name):
-    if not os.path.exists(os.path.join(data_dir, data_name)):
-        _offline('get_bz2_data(%s)' % url)
+    path = os.path.join(data_dir, data_name)
+    if os.path.exists(path):
+        return
+    if _synthetic_enabled() and data_name in _SYNTHETIC_LIBSVM:
+        cached = os.path.join(_synthetic_cache('libsvm'), data_name)
+        _make_synthetic_libsvm(cached, *_SYNTHETIC_LIBSVM[data_name])
+        _link(cached, path)
+        return
+    _offline('get_bz2_data(%s)' % url)
 
 
 def get_cifar10(path='data'):
-    if not os.path.isdir(os.path.join(path, 'cifar')):
-        _offline('get_cifar10')
+    if os.path.isdir(os.path.join(path, 'cifar')):
+        return
+    if _synthetic_enabled():
+        d = _synthetic_cache('cifar')
+        _make_synthetic_cifar10(d)
+        _link(d, os.path.join(path, 'cifar'))
+        return
+    _offline('get_cifar10')
 
 
 def get_mnist_pkl(path='data'):
@@ -1098,5 +1184,12 @@ def get_mnist_pkl(path='data'):
 def get_mnist_ubyte(path='data'):
     files = ['train-images-idx3-ubyte', 'train-labels-idx1-ubyte', 't10k-images-idx3-ubyte',
              't10k-labels-idx1-ubyte']
-    if not all(os.path.exists(os.path.join(path, f)) for f in files):
-        _offline('get_mnist_ubyte')
+    if all(os.path.exists(os.path.join(path, f)) for f in files):
+        return
+    if _synthetic_enabled():
+        d = _synthetic_cache('mnist')
+        _make_synthetic_mnist(d)
+        for f in files:
+            _link(os.path.join(d, f), os.path.join(path, f))
+        return
+    _offline('get_mnist_ubyte')

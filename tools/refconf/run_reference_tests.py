@@ -64,6 +64,7 @@ def run_one(ref, name, timeout, workers, select=None, tb=None):
         _synthetic_model_store(os.path.join(home, '.mxnet', 'models'), env)
         env['HOME'] = home
         env.setdefault('MXNET_TEST_SEED', '42')
+        env.setdefault('MXNET_TEST_SYNTHETIC_DATA', '1')   # random-pixel stand-ins for the download-only datasets
         cmd = [sys.executable, '-m', 'pytest', '-q', '-p', 'mxalias', '-p', 'no:cacheprovider', '--noconftest',
                '--timeout', str(timeout), '-o', 'addopts=', '--rootdir', tmp, os.path.join(unit, name + '.py')]
         if workers > 1:
