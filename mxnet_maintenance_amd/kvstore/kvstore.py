@@ -25,6 +25,8 @@ import warnings
 import numpy as np
 import torch
 
+from .comm import DeviceComm
+
 from ..base import MXNetError, string_types
 from ..ndarray.ndarray import NDArray
 from .. import optimizer as opt
@@ -171,14 +173,17 @@ class KVStore(KVStoreBase):
         return 0
 
     # ------------------------------------------------------------ reductions
-    def _local_sum(self, values):
-        if len(values) == 1:
-            return values[0]._data
-        dev = values[0]._data.device
-        acc = values[0]._data.clone()
-        for v in values[1:]:
-            acc.add_(v._data.to(dev))
-        return acc
+    def _local_sums(self, keys, vals):
+        """Per-key sums over the devices of this process (comm.py: in-process RCCL reduce when the
+        copies sit on distinct GPUs, balanced root placement).  A single copy is returned as is."""
+        if getattr(self, '_comm', None) is None:
+            self._comm = DeviceComm()
+        return self._comm.reduce(keys, [[v._data for v in _as_list(v)] for v in vals])
+
+    def _fan_out(self, srcs, outs):
+        if getattr(self, '_comm', None) is None:
+            self._comm = DeviceComm()
+        self._comm.broadcast(srcs, [[o._data for o in _as_list(o)] for o in outs])
 
     def _allreduce_many(self, tensors, keys=None):
         """All-reduce a list of tensors with one fused collective per (dtype, device).
@@ -224,8 +229,8 @@ class KVStore(KVStoreBase):
         vals = value if isinstance(key, (list, tuple)) else [value]
         merged = []
         with torch.no_grad():
-            for k, v in zip(keys, vals):
-                merged.append(self._local_sum(_as_list(v)).clone())
+            for v, m in zip(vals, self._local_sums(keys, vals)):
+                merged.append(m.clone() if len(_as_list(v)) == 1 else m)
             self._allreduce_many(merged, keys)
             for k, m in zip(keys, merged):
                 if k not in self._store:
@@ -246,13 +251,9 @@ class KVStore(KVStoreBase):
         keys = _as_list(key)
         outs = out if isinstance(key, (list, tuple)) else [out]
         with torch.no_grad():
-            for k, o in zip(keys, outs):
-                src = self._store[k]._data
-                for oo in _as_list(o):
-                    # written through .data: a pull into a parameter is an engine-ordered write in the
-                    # reference, not an autograd-visible in-place op on a recorded leaf
-                    if oo._data.data_ptr() != src.data_ptr():
-                        oo._data.data.copy_(src.to(oo._data.device, oo._data.dtype))
+            # written through .data: a pull into a parameter is an engine-ordered write in the
+            # reference, not an autograd-visible in-place op on a recorded leaf
+            self._fan_out([self._store[k]._data for k in keys], outs)
 
     def pushpull(self, key, value, out=None, priority=0):
         """Sum ``value`` over devices and workers and write the result to ``out``.
@@ -268,14 +269,9 @@ class KVStore(KVStoreBase):
         vals = value if isinstance(key, (list, tuple)) else [value]
         outs = vals if out is None else (out if isinstance(key, (list, tuple)) else [out])
         with torch.no_grad():
-            sums = [self._local_sum(_as_list(v)) for v in vals]
-            # make sure we do not all-reduce into a caller buffer that is read later as input
-            sums = [s if len(_as_list(v)) > 1 else s for s, v in zip(sums, vals)]
+            sums = self._local_sums(keys, vals)
             self._allreduce_many(sums, keys)
-            for s, o in zip(sums, outs):
-                for oo in _as_list(o):
-                    if oo._data.data_ptr() != s.data_ptr():
-                        oo._data.copy_(s.to(oo._data.device, oo._data.dtype))
+            self._fan_out(sums, outs)
 
     def broadcast(self, key, value, out, priority=0):
         self.init(key, value)

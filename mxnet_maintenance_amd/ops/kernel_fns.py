@@ -175,7 +175,8 @@ class BatchNormNHWC(torch.autograd.Function):
         dz = torch.empty_like(x) if has_add else None
         ext = getattr(gy, '_mxamd_bn_bwd', None)
         ext_nblk = 0
-        if ext is not None and ctx.bn_token is not None and ext[2] is ctx.bn_token:
+        if (ext is not None and ctx.bn_token is not None and ext[2] is ctx.bn_token
+                and ext[3] == gy._version):
             part, ext_nblk = ext[0], ext[1]      # statistics from the producing dgrad's epilogue
         else:
             nblk = lib.bn_partials_rows(R, C)
@@ -364,7 +365,10 @@ def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=Non
                               _zero_page(x.device).data_ptr(), N, H, W, C, K, R, S, stride[0], stride[1],
                               pad[0], pad[1], v, _p(part), nparts, _p(addend), _stream(), **bkw)
         if bkw:
-            y._mxamd_bn_bwd = (bpart, bnp, bn_bwd[6])
+            # the version pins the statistics to exactly this gradient: when y has several consumers,
+            # autograd may accumulate the others' gradients into this tensor in place (bumping its
+            # version), and then the partials no longer describe it
+            y._mxamd_bn_bwd = (bpart, bnp, bn_bwd[6], y._version)
         if part is not None:
             # consumed by a following BatchNormNHWC (training): its statistics pass over y is skipped
             y._mxamd_bn_part = (part, nparts)
