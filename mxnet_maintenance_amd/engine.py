@@ -4,16 +4,29 @@ Parity: python/mxnet/engine.py (bulk, set_bulk_size) and src/engine/*
 (Engine::Get()->PushAsync / WaitForVar / WaitForAll, MXNET_ENGINE_TYPE,
 MXNET_CPU_WORKER_NTHREADS).
 
-The C++ engine (src/native/engine.cc) schedules host-side work with
-reader/writer dependencies on engine variables.  ``MXNET_ENGINE_TYPE=NaiveEngine``
-runs everything synchronously (the reference's debugging mode).
+The C++ engine (src/native/engine.cc) schedules work with reader/writer
+dependencies on engine variables:
+
+* host ops (``push``) run on a worker pool (decode, file writes, callbacks);
+* device ops (``push_device``, the reference's ThreadedEnginePerDevice path) are
+  issued on a given HIP stream once granted; ordering against work on other
+  streams/devices is enforced on the GPU with HIP events (the issuing worker
+  never waits for the GPU), and host ops touching a device-written variable
+  synchronise on its event first;
+* ``stream_wait_var`` makes a consumer stream wait for a variable's device
+  write without blocking the host on GPU execution.
+
+``MXNET_ENGINE_TYPE=NaiveEngine`` runs everything synchronously (the reference's
+debugging mode); ``MXNET_ENGINE_DEBUG=1`` turns on the race detector (every op
+validates the version / exclusive access of its variables when it starts, and
+``debug_access`` reports undeclared direct accesses that overlap an engine op).
 """
 import os
 import threading
 from contextlib import contextmanager
 
-__all__ = ['bulk', 'set_bulk_size', 'get', 'push', 'new_var', 'wait_for_var', 'wait_all',
-           'native_available', 'Engine']
+__all__ = ['bulk', 'set_bulk_size', 'get', 'push', 'push_device', 'stream_wait_var', 'new_var', 'wait_for_var',
+           'wait_all', 'native_available', 'Engine', 'debug_access', 'race_violations', 'var_of']
 
 _engine = None
 _lock = threading.Lock()
@@ -54,6 +67,20 @@ class _PyEngine:
             v.version += 1
         self.executed += 1
 
+    def push_device(self, fn, const_vars, mutable_vars, stream, device, priority=0, name=''):
+        self.push(fn, const_vars, mutable_vars, priority, name)
+
+    def stream_wait_var(self, v, stream, device):
+        pass
+
+    debug = False
+    violations = 0
+    last_violation = ''
+    device_ops = 0
+
+    def debug_access(self, v, write=False):
+        pass
+
     def push_write_file(self, path, data, const_vars, mutable_vars):
         with open(path, 'wb') as f:
             f.write(data)
@@ -77,7 +104,8 @@ def get():
                 if nat is None:
                     _engine = _PyEngine()
                 else:
-                    _engine = nat.Engine(nthreads, etype == 'NaiveEngine')
+                    _engine = nat.Engine(nthreads, etype == 'NaiveEngine',
+                                         os.environ.get('MXNET_ENGINE_DEBUG', '0') == '1')
     return _engine
 
 
@@ -92,6 +120,64 @@ def push(fn, const_vars=(), mutable_vars=(), priority=0, name=''):
     """Schedule ``fn()`` after all writers of ``const_vars`` and all users of
     ``mutable_vars`` pushed before it have finished."""
     get().push(fn, list(const_vars), list(mutable_vars), priority, name)
+
+
+def _stream_of(stream):
+    """(torch stream, raw hipStream_t handle, device index) -- (None, 0, -1) without a GPU."""
+    import torch
+    if stream is None:
+        if not torch.cuda.is_available():
+            return None, 0, -1
+        stream = torch.cuda.current_stream()
+    return stream, int(stream.cuda_stream), int(stream.device.index)
+
+
+def push_device(fn, const_vars=(), mutable_vars=(), stream=None, priority=0, name=''):
+    """Schedule a device op: once its variables are granted, ``fn()`` runs on a worker with ``stream``
+    (default: the caller's current stream) as the current stream and must only *enqueue* work; the
+    op completes when issued.  Other streams reading/writing the same variables are ordered after
+    it with HIP events, host ops synchronise on it."""
+    s, handle, dev = _stream_of(stream)
+    if s is None:
+        run = fn
+    else:
+        def run():
+            import torch
+            with torch.cuda.device(dev), torch.cuda.stream(s):
+                fn()
+    get().push_device(run, list(const_vars), list(mutable_vars), handle, dev, priority, name)
+
+
+def stream_wait_var(var, stream=None):
+    """Make ``stream`` (default: current) wait on the GPU for the last device write of ``var``."""
+    s, handle, dev = _stream_of(stream)
+    if s is None:
+        get().wait_for_var(var)
+        return
+    get().stream_wait_var(var, handle, dev)
+
+
+def debug_access(var, write=False):
+    """Debug mode: declare a direct access to ``var`` made outside the engine."""
+    get().debug_access(var, write)
+
+
+def race_violations():
+    """(count, last message) of the race detector (MXNET_ENGINE_DEBUG=1)."""
+    e = get()
+    return e.violations, e.last_violation
+
+
+def var_of(arr):
+    """The engine variable attached to an NDArray (created on first use; shared by its views)."""
+    v = getattr(arr, '_engine_var', None)
+    if v is None:
+        v = new_var('ndarray%d' % id(arr))
+        try:
+            arr._engine_var = v
+        except AttributeError:
+            pass
+    return v
 
 
 def push_write_file(path, data, const_vars=(), mutable_vars=()):

@@ -50,13 +50,55 @@ def split_data(data, num_slice, batch_axis=0, even_split=True):
     return slices
 
 
+_COPY_STREAMS = {}
+
+
+def _copy_stream(dev):
+    s = _COPY_STREAMS.get(dev)
+    if s is None:
+        s = _COPY_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def _upload(slices, ctx_list):
+    """Host -> GPU copies of the batch slices as engine device ops on each GPU's copy stream.
+
+    The copies are issued from pinned memory on a dedicated copy stream, so they overlap the
+    compute still queued on the consumer streams (the host runs ahead of the GPU); each consumer
+    stream then waits for its slice with a HIP event (engine.stream_wait_var) -- no host sync.
+    Parity: the reference's CopyFromTo pushed to the ThreadedEnginePerDevice copy workers
+    (src/engine/threaded_engine_perdevice.cc, src/ndarray/ndarray.cc CopyFromTo)."""
+    from .. import engine
+    from .. import autograd
+    outs = []
+    for s, ctx in zip(slices, ctx_list):
+        t = s._data
+        if (ctx.device_type != 'gpu' or t.device.type != 'cpu' or not torch.cuda.is_available()
+                or (autograd.is_recording() and t.requires_grad)):
+            outs.append(s.as_in_context(ctx))
+            continue
+        src = t.detach().contiguous()
+        if not src.is_pinned():
+            src = src.pin_memory()
+        dev = torch.device('cuda', ctx.device_id)
+        dst = torch.empty(src.shape, dtype=src.dtype, device=dev)
+        cs = _copy_stream(dev)
+        var = engine.new_var('h2d')
+        engine.push_device(lambda dst=dst, src=src: dst.copy_(src, non_blocking=True), (), (var,), stream=cs,
+                           name='split_and_load_h2d')
+        dst.record_stream(cs)
+        engine.stream_wait_var(var, torch.cuda.current_stream(dev))
+        outs.append(NDArray(dst))
+    return outs
+
+
 def split_and_load(data, ctx_list, batch_axis=0, even_split=True):
     if not isinstance(data, NDArray):
-        data = ndarray.array(data, ctx=ctx_list[0])
+        data = ndarray.array(data)      # host first: the per-device slices then go up as async copies
     if len(ctx_list) == 1:
-        return [data.as_in_context(ctx_list[0])]
+        return _upload([data], ctx_list)
     slices = split_data(data, len(ctx_list), batch_axis, even_split)
-    return [i.as_in_context(ctx) for i, ctx in zip(slices, ctx_list)]
+    return _upload(slices, ctx_list)
 
 
 def clip_global_norm(arrays, max_norm, check_isfinite=True):

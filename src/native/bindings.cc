@@ -49,7 +49,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("name", [](const Var& v) { return v.name; });
 
   py::class_<Engine>(m, "Engine")
-      .def(py::init<int, bool>(), py::arg("num_workers") = 4, py::arg("naive") = false)
+      .def(py::init<int, bool, bool>(), py::arg("num_workers") = 4, py::arg("naive") = false,
+           py::arg("debug") = false)
       .def("new_var", &Engine::NewVar, py::arg("name") = "")
       .def(
           "push",
@@ -74,6 +75,41 @@ PYBIND11_MODULE(_native, m) {
           },
           py::arg("fn"), py::arg("const_vars"), py::arg("mutable_vars"), py::arg("priority") = 0,
           py::arg("name") = "")
+      .def(
+          "push_device",
+          [](Engine& e, py::function fn, std::vector<VarHandle> cv, std::vector<VarHandle> mv, uintptr_t stream,
+             int device, int priority, std::string name) {
+            auto holder = std::make_shared<std::unique_ptr<py::function>>(new py::function(std::move(fn)));
+            Fn f = [holder]() {
+              py::gil_scoped_acquire g;
+              try {
+                (**holder)();
+              } catch (py::error_already_set& err) {
+                holder->reset();
+                throw PyErrorHolder(std::move(err));
+              }
+              holder->reset();
+            };
+            py::gil_scoped_release rel;
+            e.PushDevice(std::move(f), cv, mv, stream, device, priority, name);
+          },
+          py::arg("fn"), py::arg("const_vars"), py::arg("mutable_vars"), py::arg("stream"), py::arg("device"),
+          py::arg("priority") = 0, py::arg("name") = "",
+          "Device op: fn enqueues work on `stream`; ordering against other streams is by HIP events.")
+      .def("debug_access", &Engine::DebugAccess, py::arg("var"), py::arg("write") = false)
+      .def("stream_wait_var",
+           [](Engine& e, VarHandle v, uintptr_t stream, int device) {
+             try {
+               py::gil_scoped_release rel;
+               e.StreamWaitVar(v, stream, device);
+             } catch (PyErrorHolder&) {
+               Rethrow(std::current_exception());
+             }
+           })
+      .def_property_readonly("debug", &Engine::debug)
+      .def_property_readonly("violations", &Engine::violations)
+      .def_property_readonly("last_violation", &Engine::last_violation)
+      .def_property_readonly("device_ops", &Engine::device_ops)
       .def(
           "push_write_file",
           [](Engine& e, std::string path, py::bytes data, std::vector<VarHandle> cv,

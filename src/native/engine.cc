@@ -2,10 +2,26 @@
 #include "engine.h"
 
 #include <algorithm>
+#include <stdexcept>
+
+#include "hip_rt.h"
 
 namespace mxamd {
 
-Engine::Engine(int num_workers, bool naive) : naive_(naive) {
+DevEvent::~DevEvent() {
+  if (ev) HipRt::Get().event_destroy(ev);
+}
+
+namespace {
+
+void HipCheck(int rc, const char* what) {
+  if (rc != 0) throw std::runtime_error(std::string("engine device op: ") + what + " failed (hip error " +
+                                        std::to_string(rc) + ")");
+}
+
+}  // namespace
+
+Engine::Engine(int num_workers, bool naive, bool debug) : naive_(naive), debug_(debug) {
   if (!naive_) {
     if (num_workers <= 0) num_workers = 1;
     for (int i = 0; i < num_workers; ++i) workers_.emplace_back([this] { WorkerLoop(); });
@@ -47,12 +63,8 @@ bool Engine::AppendWrite(const VarHandle& v, const std::shared_ptr<Opr>& op) {
   return false;
 }
 
-void Engine::Push(Fn fn, const std::vector<VarHandle>& const_vars,
-                  const std::vector<VarHandle>& mutable_vars, int priority,
-                  const std::string& name, bool always_run) {
-  auto op = std::make_shared<Opr>();
-  op->fn = std::move(fn);
-  op->always_run = always_run;
+void Engine::PushOp(std::shared_ptr<Opr> op, const std::vector<VarHandle>& const_vars,
+                    const std::vector<VarHandle>& mutable_vars) {
   op->mutable_vars = mutable_vars;
   // a variable that is both read and written is only written
   for (const auto& v : const_vars) {
@@ -60,9 +72,18 @@ void Engine::Push(Fn fn, const std::vector<VarHandle>& const_vars,
         std::find(op->const_vars.begin(), op->const_vars.end(), v) == op->const_vars.end())
       op->const_vars.push_back(v);
   }
-  op->priority = priority;
-  op->name = name;
   op->seq = seq_.fetch_add(1);
+  if (debug_) {
+    // the version a var must have when this op starts = writes pushed before it
+    for (const auto& v : op->const_vars) {
+      std::lock_guard<std::mutex> lk(v->mu);
+      op->expect_const.push_back(v->pushed_writes);
+    }
+    for (const auto& v : op->mutable_vars) {
+      std::lock_guard<std::mutex> lk(v->mu);
+      op->expect_mut.push_back(v->pushed_writes++);
+    }
+  }
   ++pending_;
   if (naive_) {
     Execute(op);
@@ -73,6 +94,30 @@ void Engine::Push(Fn fn, const std::vector<VarHandle>& const_vars,
   for (const auto& v : op->const_vars) granted += AppendRead(v, op) ? 1 : 0;
   for (const auto& v : op->mutable_vars) granted += AppendWrite(v, op) ? 1 : 0;
   if (op->wait.fetch_sub(granted + 1) == granted + 1) Dispatch(op);
+}
+
+void Engine::Push(Fn fn, const std::vector<VarHandle>& const_vars,
+                  const std::vector<VarHandle>& mutable_vars, int priority,
+                  const std::string& name, bool always_run) {
+  auto op = std::make_shared<Opr>();
+  op->fn = std::move(fn);
+  op->always_run = always_run;
+  op->priority = priority;
+  op->name = name;
+  PushOp(std::move(op), const_vars, mutable_vars);
+}
+
+void Engine::PushDevice(Fn launch, const std::vector<VarHandle>& const_vars,
+                        const std::vector<VarHandle>& mutable_vars, uintptr_t stream, int device,
+                        int priority, const std::string& name) {
+  auto op = std::make_shared<Opr>();
+  op->fn = std::move(launch);
+  op->priority = priority;
+  op->name = name;
+  op->is_device = true;
+  op->stream = stream;
+  op->device = device;
+  PushOp(std::move(op), const_vars, mutable_vars);
 }
 
 void Engine::Dispatch(std::shared_ptr<Opr> op) {
@@ -97,8 +142,132 @@ void Engine::WorkerLoop() {
   }
 }
 
+// Device op body: stream waits on the events of its vars, launch, one event recorded for all of them.
+void Engine::RunDevice(const std::shared_ptr<Opr>& op) {
+  HipRt& rt = HipRt::Get();
+  if (!rt.ok) {       // no GPU runtime: the launch runs as a plain host op (CPU tensors)
+    if (op->fn) op->fn();
+    return;
+  }
+  int prev = -1;
+  HipCheck(rt.get_device(&prev), "hipGetDevice");
+  if (op->device >= 0 && op->device != prev) HipCheck(rt.set_device(op->device), "hipSetDevice");
+  std::vector<DevEventPtr> waits;
+  for (const auto& v : op->const_vars) {
+    std::lock_guard<std::mutex> lk(v->mu);
+    if (v->write_ev) waits.push_back(v->write_ev);
+  }
+  for (const auto& v : op->mutable_vars) {
+    std::lock_guard<std::mutex> lk(v->mu);
+    if (v->write_ev) waits.push_back(v->write_ev);
+    waits.insert(waits.end(), v->read_evs.begin(), v->read_evs.end());
+  }
+  for (const auto& e : waits)
+    if (e->stream != op->stream || e->device != op->device)   // same stream: already ordered
+      HipCheck(rt.stream_wait_event(reinterpret_cast<void*>(op->stream), e->ev, 0), "hipStreamWaitEvent");
+  try {
+    if (op->fn) op->fn();
+  } catch (...) {
+    if (op->device >= 0 && op->device != prev) rt.set_device(prev);
+    throw;
+  }
+  auto ev = std::make_shared<DevEvent>();
+  ev->stream = op->stream;
+  ev->device = op->device;
+  HipCheck(rt.event_create(&ev->ev, 0x2 /* hipEventDisableTiming */), "hipEventCreateWithFlags");
+  HipCheck(rt.event_record(ev->ev, reinterpret_cast<void*>(op->stream)), "hipEventRecord");
+  if (op->device >= 0 && op->device != prev) rt.set_device(prev);
+  for (const auto& v : op->const_vars) {
+    std::lock_guard<std::mutex> lk(v->mu);
+    v->read_evs.push_back(ev);
+  }
+  for (const auto& v : op->mutable_vars) {
+    std::lock_guard<std::mutex> lk(v->mu);
+    v->write_ev = ev;
+    v->read_evs.clear();
+  }
+  {
+    std::lock_guard<std::mutex> lk(devmu_);
+    if (std::find(devices_used_.begin(), devices_used_.end(), op->device) == devices_used_.end())
+      devices_used_.push_back(op->device);
+  }
+  ++device_ops_;
+}
+
+// Host op body prologue: data last written (or read, for a writer) on a device must be complete.
+void Engine::SyncHost(const std::shared_ptr<Opr>& op) {
+  std::vector<DevEventPtr> waits;
+  for (const auto& v : op->const_vars) {
+    std::lock_guard<std::mutex> lk(v->mu);
+    if (v->write_ev) waits.push_back(v->write_ev);
+  }
+  for (const auto& v : op->mutable_vars) {
+    std::lock_guard<std::mutex> lk(v->mu);
+    if (v->write_ev) waits.push_back(v->write_ev);
+    waits.insert(waits.end(), v->read_evs.begin(), v->read_evs.end());
+  }
+  for (const auto& e : waits) HipCheck(HipRt::Get().event_synchronize(e->ev), "hipEventSynchronize");
+}
+
+void Engine::Violation(const std::string& msg) {
+  ++violations_;
+  std::lock_guard<std::mutex> lk(vmu_);
+  last_violation_ = msg;
+}
+
+std::string Engine::last_violation() {
+  std::lock_guard<std::mutex> lk(vmu_);
+  return last_violation_;
+}
+
+std::exception_ptr Engine::DebugBegin(const std::shared_ptr<Opr>& op) {
+  std::string err;
+  for (size_t i = 0; i < op->const_vars.size(); ++i) {
+    const auto& v = op->const_vars[i];
+    std::lock_guard<std::mutex> lk(v->mu);
+    if (v->version != op->expect_const[i] || v->active_writers != 0)
+      err = "read of var '" + v->name + "' by op '" + op->name + "' at version " + std::to_string(v->version) +
+            " (expected " + std::to_string(op->expect_const[i]) + ", active writers " +
+            std::to_string(v->active_writers) + ")";
+    ++v->active_readers;
+  }
+  for (size_t i = 0; i < op->mutable_vars.size(); ++i) {
+    const auto& v = op->mutable_vars[i];
+    std::lock_guard<std::mutex> lk(v->mu);
+    if (v->version != op->expect_mut[i] || v->active_writers != 0 || v->active_readers != 0)
+      err = "write of var '" + v->name + "' by op '" + op->name + "' at version " + std::to_string(v->version) +
+            " (expected " + std::to_string(op->expect_mut[i]) + ", active readers " +
+            std::to_string(v->active_readers) + ", writers " + std::to_string(v->active_writers) + ")";
+    ++v->active_writers;
+  }
+  if (err.empty()) return nullptr;
+  Violation("engine race: " + err);
+  return std::make_exception_ptr(std::runtime_error("engine race: " + err));
+}
+
+void Engine::DebugEnd(const std::shared_ptr<Opr>& op) {
+  for (const auto& v : op->const_vars) {
+    std::lock_guard<std::mutex> lk(v->mu);
+    --v->active_readers;
+  }
+  for (const auto& v : op->mutable_vars) {
+    std::lock_guard<std::mutex> lk(v->mu);
+    --v->active_writers;
+  }
+}
+
+void Engine::DebugAccess(const VarHandle& v, bool write) {
+  if (!debug_) return;
+  std::lock_guard<std::mutex> lk(v->mu);
+  if (v->active_writers != 0 || (write && v->active_readers != 0))
+    Violation("engine race: direct " + std::string(write ? "write" : "read") + " of var '" + v->name +
+              "' while an engine op holds it (readers " + std::to_string(v->active_readers) + ", writers " +
+              std::to_string(v->active_writers) + ")");
+}
+
 void Engine::Execute(std::shared_ptr<Opr> op) {
   std::exception_ptr exc;
+  std::exception_ptr race = debug_ && !op->always_run ? DebugBegin(op) : nullptr;
   if (op->always_run) {
     if (op->fn) op->fn();
     ++executed_;
@@ -123,13 +292,20 @@ void Engine::Execute(std::shared_ptr<Opr> op) {
       if (v->exc) { exc = v->exc; break; }
     }
   }
+  if (!exc && race) exc = race;
   if (!exc) {
     try {
-      if (op->fn) op->fn();
+      if (op->is_device) {
+        RunDevice(op);
+      } else {
+        SyncHost(op);
+        if (op->fn) op->fn();
+      }
     } catch (...) {
       exc = std::current_exception();
     }
   }
+  if (debug_) DebugEnd(op);
   ++executed_;
   if (naive_) {
     for (const auto& v : op->mutable_vars) {
@@ -217,11 +393,14 @@ void Engine::WaitForVar(const VarHandle& v) {
     done->second.wait(lk, [&] { return *flag; });
   }
   std::exception_ptr exc;
+  DevEventPtr ev;
   {
     std::lock_guard<std::mutex> lk(v->mu);
     exc = v->exc;
     v->exc = nullptr;
+    ev = v->write_ev;
   }
+  if (ev) HipCheck(HipRt::Get().event_synchronize(ev->ev), "hipEventSynchronize");   // the device write too
   if (exc) {
     std::lock_guard<std::mutex> lk(excmu_);
     if (global_exc_ == exc) global_exc_ = nullptr;
@@ -229,10 +408,56 @@ void Engine::WaitForVar(const VarHandle& v) {
   }
 }
 
+void Engine::StreamWaitVar(const VarHandle& v, uintptr_t stream, int device) {
+  auto done = std::make_shared<std::pair<std::mutex, std::condition_variable>>();
+  auto flag = std::make_shared<bool>(false);
+  Push([done, flag] {
+         std::lock_guard<std::mutex> lk(done->first);
+         *flag = true;
+         done->second.notify_all();
+       },
+       {v}, {}, 1 << 20, "StreamWaitVar", /*always_run=*/true);
+  {
+    std::unique_lock<std::mutex> lk(done->first);
+    done->second.wait(lk, [&] { return *flag; });
+  }
+  DevEventPtr ev;
+  std::exception_ptr exc;
+  {
+    std::lock_guard<std::mutex> lk(v->mu);
+    ev = v->write_ev;
+    exc = v->exc;
+  }
+  if (exc) std::rethrow_exception(exc);
+  if (!ev || (ev->stream == stream && ev->device == device)) return;
+  HipRt& rt = HipRt::Get();
+  int prev = -1;
+  HipCheck(rt.get_device(&prev), "hipGetDevice");
+  if (device >= 0 && device != prev) HipCheck(rt.set_device(device), "hipSetDevice");
+  const int rc = rt.stream_wait_event(reinterpret_cast<void*>(stream), ev->ev, 0);
+  if (device >= 0 && device != prev) rt.set_device(prev);
+  HipCheck(rc, "hipStreamWaitEvent");
+}
+
 void Engine::WaitForAll() {
   {
     std::unique_lock<std::mutex> lk(allmu_);
     allcv_.wait(lk, [this] { return pending_.load() == 0; });
+  }
+  std::vector<int> devs;
+  {
+    std::lock_guard<std::mutex> lk(devmu_);
+    devs = devices_used_;
+  }
+  if (!devs.empty()) {
+    HipRt& rt = HipRt::Get();
+    int prev = -1;
+    HipCheck(rt.get_device(&prev), "hipGetDevice");
+    for (int d : devs) {
+      if (d >= 0) HipCheck(rt.set_device(d), "hipSetDevice");
+      HipCheck(rt.device_synchronize(), "hipDeviceSynchronize");
+    }
+    rt.set_device(prev);
   }
   std::exception_ptr exc;
   {

@@ -4,17 +4,30 @@
 // Parity: src/engine/threaded_engine.{h,cc} (ThreadedVar / OprBlock /
 // ThreadedEngine::Push / WaitForVar / WaitForAll) and naive_engine.cc.
 //
-// Design for an MI355X node: device work is already ordered by HIP streams,
-// so this engine schedules the *host-side* work around it (IO decode,
-// checkpoint writes, kvstore bookkeeping, Python callbacks) on a worker pool
-// with per-variable reader/writer queues.  A variable tracks
+// Design for an MI355X node.  Host operations (IO decode, checkpoint writes,
+// kvstore bookkeeping, Python callbacks) run on a worker pool with per-variable
+// reader/writer queues -- the reader/writer protocol of the reference's
+// ThreadedVar.  A variable tracks
 //   - the number of pending readers that have been granted access,
 //   - whether a writer holds it,
 //   - a FIFO of blocked operations,
-// exactly the reader/writer protocol of the reference's ThreadedVar.
+//   - the HIP events of its last device writer and of the device readers since.
+// Device operations (PushDevice, the ThreadedEnginePerDevice path of
+// threaded_engine_perdevice.cc) are granted through the same queues but never
+// block a worker on the GPU: when granted they make their stream wait on the
+// events of their variables (hipStreamWaitEvent), enqueue their work on that
+// stream, record one event and complete at once.  Ordering between device ops
+// on different streams / devices is therefore enforced on the GPU; a host op
+// whose variable was last written on a device synchronises on that event first.
+//
+// Debug mode (MXNET_ENGINE_DEBUG=1): every op checks, when it starts, that the
+// versions of its variables are exactly the number of writes pushed before it
+// and that no conflicting access is active; DebugAccess() lets code outside the
+// engine declare a direct access so an undeclared concurrent use is reported.
 #pragma once
 #include <atomic>
 #include <condition_variable>
+#include <cstdint>
 #include <deque>
 #include <exception>
 #include <functional>
@@ -29,6 +42,15 @@ namespace mxamd {
 
 struct Opr;
 
+// A recorded HIP event (destroyed when the last holder drops it).
+struct DevEvent {
+  void* ev = nullptr;
+  uintptr_t stream = 0;
+  int device = -1;
+  ~DevEvent();
+};
+using DevEventPtr = std::shared_ptr<DevEvent>;
+
 struct Var {
   std::mutex mu;
   int num_pending_reads = 0;   // readers currently granted
@@ -38,6 +60,11 @@ struct Var {
   std::exception_ptr exc;      // first exception raised by a writer of this var
   uint64_t version = 0;
   std::string name;
+  DevEventPtr write_ev;                // last device writer
+  std::vector<DevEventPtr> read_evs;   // device readers since that write
+  // debug-mode bookkeeping
+  uint64_t pushed_writes = 0;
+  int active_readers = 0, active_writers = 0;
 };
 
 using VarHandle = std::shared_ptr<Var>;
@@ -52,17 +79,36 @@ struct Opr {
   std::string name;
   uint64_t seq = 0;
   bool always_run = false;  // synchronisation ops run even if an input carries an exception
+  // device ops
+  bool is_device = false;
+  uintptr_t stream = 0;
+  int device = -1;
+  // debug mode: expected version of each const / mutable var when the op starts
+  std::vector<uint64_t> expect_const, expect_mut;
 };
 
 class Engine {
  public:
-  explicit Engine(int num_workers, bool naive);
+  explicit Engine(int num_workers, bool naive, bool debug = false);
   ~Engine();
   VarHandle NewVar(const std::string& name = "");
   void Push(Fn fn, const std::vector<VarHandle>& const_vars,
             const std::vector<VarHandle>& mutable_vars, int priority,
             const std::string& name, bool always_run = false);
+  // Device op: `launch` enqueues work on `stream` (a hipStream_t) of `device`.
+  void PushDevice(Fn launch, const std::vector<VarHandle>& const_vars,
+                  const std::vector<VarHandle>& mutable_vars, uintptr_t stream, int device,
+                  int priority, const std::string& name);
   void WaitForVar(const VarHandle& v);
+  // Make `stream` wait (on the GPU) for the device write of `v`: blocks the caller only until the ops
+  // pushed on `v` so far have been *issued*, never on GPU execution.
+  void StreamWaitVar(const VarHandle& v, uintptr_t stream, int device);
+  // Debug mode: declare a direct (non-engine) access; a conflicting active engine access is a race.
+  void DebugAccess(const VarHandle& v, bool write);
+  bool debug() const { return debug_; }
+  uint64_t violations() const { return violations_.load(); }
+  std::string last_violation();
+  uint64_t device_ops() const { return device_ops_.load(); }
   void WaitForAll();
   int64_t Pending() const { return pending_.load(); }
   bool naive() const { return naive_; }
@@ -71,7 +117,14 @@ class Engine {
   uint64_t executed() const { return executed_.load(); }
 
  private:
+  void PushOp(std::shared_ptr<Opr> op, const std::vector<VarHandle>& const_vars,
+              const std::vector<VarHandle>& mutable_vars);
   void Dispatch(std::shared_ptr<Opr> op);
+  void RunDevice(const std::shared_ptr<Opr>& op);
+  void SyncHost(const std::shared_ptr<Opr>& op);
+  std::exception_ptr DebugBegin(const std::shared_ptr<Opr>& op);
+  void DebugEnd(const std::shared_ptr<Opr>& op);
+  void Violation(const std::string& msg);
   void Execute(std::shared_ptr<Opr> op);
   void Complete(const std::shared_ptr<Opr>& op, std::exception_ptr exc);
   bool AppendRead(const VarHandle& v, const std::shared_ptr<Opr>& op);
@@ -88,6 +141,13 @@ class Engine {
   };
 
   bool naive_;
+  bool debug_;
+  std::atomic<uint64_t> violations_{0};
+  std::atomic<uint64_t> device_ops_{0};
+  std::mutex vmu_;
+  std::string last_violation_;
+  std::mutex devmu_;
+  std::vector<int> devices_used_;
   std::atomic<bool> stop_{false};
   std::atomic<int64_t> pending_{0};
   std::atomic<uint64_t> executed_{0};

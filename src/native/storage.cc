@@ -14,38 +14,13 @@
 // 4 KiB (linear 4 KiB steps below), freed blocks go to per-class free lists.
 #include "storage.h"
 
-#include <dlfcn.h>
+#include "hip_rt.h"
 
 #include <cstdlib>
 #include <cstring>
 
 namespace mxamd {
 
-namespace {
-using HostMallocFn = int (*)(void**, size_t, unsigned int);
-using HostFreeFn = int (*)(void*);
-using GetCountFn = int (*)(int*);
-
-struct HipApi {
-  HostMallocFn host_malloc = nullptr;
-  HostFreeFn host_free = nullptr;
-  bool ok = false;
-  HipApi() {
-    void* h = dlopen("libamdhip64.so", RTLD_LAZY | RTLD_LOCAL);
-    if (!h) return;
-    auto count = reinterpret_cast<GetCountFn>(dlsym(h, "hipGetDeviceCount"));
-    host_malloc = reinterpret_cast<HostMallocFn>(dlsym(h, "hipHostMalloc"));
-    host_free = reinterpret_cast<HostFreeFn>(dlsym(h, "hipHostFree"));
-    int n = 0;
-    ok = count && host_malloc && host_free && count(&n) == 0 && n > 0;
-  }
-};
-
-HipApi& Hip() {
-  static HipApi api;
-  return api;
-}
-}  // namespace
 
 size_t HostStorage::RoundSize(size_t size) {
   const size_t page = 4096;
@@ -56,14 +31,14 @@ size_t HostStorage::RoundSize(size_t size) {
   return r;
 }
 
-HostStorage::HostStorage(bool pinned) : pinned_(pinned && Hip().ok) {}
+HostStorage::HostStorage(bool pinned) : pinned_(pinned && HipRt::Get().ok) {}
 
 HostStorage::~HostStorage() { ReleaseAll(); }
 
 void* HostStorage::RawAlloc(size_t size) {
   void* p = nullptr;
   if (pinned_) {
-    if (Hip().host_malloc(&p, size, 0) != 0) p = nullptr;
+    if (HipRt::Get().host_malloc(&p, size, 0) != 0) p = nullptr;
   } else {
     p = std::aligned_alloc(4096, size);
   }
@@ -72,7 +47,7 @@ void* HostStorage::RawAlloc(size_t size) {
 
 void HostStorage::RawFree(void* p) {
   if (pinned_)
-    Hip().host_free(p);
+    HipRt::Get().host_free(p);
   else
     std::free(p);
 }

@@ -928,4 +928,5 @@ def test_bn_backward_stats_fused_into_dgrad_epilogue(dtype):
         scale = r.abs().max().item() + 1e-6
         tol = (3e-2 if dtype == torch.float16 else 8e-2) * scale
         torch.testing.assert_close(a, p, rtol=0, atol=tol, msg=lambda m: '%s fused vs unfused: %s' % (name, m))
-        torch.testing.assert_close(a, r, rtol=0, atol=tol, msg=lambda m: '%s fused vs fp32: %s' % (name, m))
+        rel = (torch.linalg.vector_norm(a - r) / torch.linalg.vector_norm(r)).item()
+        assert rel < (2e-2 if dtype == torch.float16 else 5e-2), '%s fused vs fp32: rel err %g' % (name, rel)
