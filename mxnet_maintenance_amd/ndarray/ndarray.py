@@ -829,21 +829,33 @@ def empty(shape, ctx=None, dtype=None, stype=None):
     return _tag_host_ctx(NDArray(torch.empty(shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device)), ctx)
 
 
+def _created(opname, make):
+    """Creation functions are operators of the reference (_zeros, _ones, _full): profiled as such."""
+    from .. import profiler as _prof
+    if not _prof.active_imperative:
+        return make()
+    with _prof.op_span(_prof.current_scope() + opname):
+        r = make()
+    if _prof.active_memory:
+        _prof.memory_alloc(r)
+    return r
+
+
 def zeros(shape, ctx=None, dtype=None, stype=None, out=None, **kwargs):
     if isinstance(shape, int):
         shape = (shape,)
     if stype not in (None, 'default'):
         from . import sparse
         return sparse.zeros(stype, shape, ctx=ctx, dtype=dtype)
-    return _into(out, _tag_host_ctx(NDArray(torch.zeros(shape, dtype=torch_dtype(dtype),
-                                                        device=_ctx(ctx).torch_device)), ctx))
+    return _into(out, _created('_zeros', lambda: _tag_host_ctx(NDArray(torch.zeros(
+        shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device)), ctx)))
 
 
 def ones(shape, ctx=None, dtype=None, out=None, **kwargs):
     if isinstance(shape, int):
         shape = (shape,)
-    return _into(out, _tag_host_ctx(NDArray(torch.ones(shape, dtype=torch_dtype(dtype),
-                                                       device=_ctx(ctx).torch_device)), ctx))
+    return _into(out, _created('_ones', lambda: _tag_host_ctx(NDArray(torch.ones(
+        shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device)), ctx)))
 
 
 def full(shape, val, ctx=None, dtype=np.float32, out=None):

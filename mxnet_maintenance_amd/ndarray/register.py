@@ -172,6 +172,9 @@ def invoke(op, inputs, attrs, out=None):
     else:
         outs = [NDArray(res)]
     _np_wrap(inputs, outs)
+    if _profiler.active_memory and out is None:
+        for o in outs:
+            _profiler.memory_alloc(o)
     if box is not None:
         for o in outs:
             o._exc = box

@@ -23,6 +23,7 @@ imperatively (with autograd), symbolically (infer_shape via the prop's
 import torch
 
 from . import _state
+from . import profiler as _profiler
 from .base import MXNetError
 from .ops import registry
 
@@ -109,7 +110,9 @@ def _make_prop(attrs):
         raise MXNetError('Custom operator %s is not registered' % op_type)
     kw = {k: (v if isinstance(v, str) else str(v)) for k, v in attrs.items() if k != 'op_type'
           and not (k.startswith('__') and k.endswith('__'))}
-    return _REGISTRY[op_type](**kw)
+    prop = _REGISTRY[op_type](**kw)
+    prop._op_type_name = op_type
+    return prop
 
 
 def _custom_args(attrs):
@@ -149,9 +152,9 @@ class _CustomFunction(torch.autograd.Function):
         _, out_shapes, _ = prop.infer_shape(in_shapes)
         in_types = [t.dtype for t in tensors[:n_in]]
         outs = [NDArray(torch.zeros(tuple(s), dtype=in_types[0], device=tensors[0].device)) for s in out_shapes]
-        with torch.no_grad():
+        with torch.no_grad(), _profiler.custom_op_scope(prop._op_type_name):
             op.forward(is_train=is_train, req=['write'] * len(outs), in_data=ins, out_data=outs, aux=aux)
-        ctx.op, ctx.n_in = op, n_in
+        ctx.op, ctx.n_in, ctx.op_type = op, n_in, prop._op_type_name
         ctx.save_for_backward(*tensors)
         ctx.outs = [o._data for o in outs]
         return tuple(o._data for o in outs)
@@ -166,7 +169,7 @@ class _CustomFunction(torch.autograd.Function):
         outs = [NDArray(t) for t in ctx.outs]
         ograds = [NDArray(g if g is not None else torch.zeros_like(o)) for g, o in zip(grads, ctx.outs)]
         igrads = [NDArray(torch.zeros_like(t)) for t in tensors[:n_in]]
-        with torch.no_grad():
+        with torch.no_grad(), _profiler.custom_op_scope(ctx.op_type, backward=True):
             ctx.op.backward(req=['write'] * n_in, out_grad=ograds, in_data=ins, out_data=outs, in_grad=igrads,
                             aux=aux)
         return (None, None, None, None) + tuple(g._data for g in igrads) + (None,) * (len(tensors) - n_in)

@@ -27,6 +27,8 @@ _config = {'filename': 'profile.json', 'profile_all': False, 'profile_symbolic':
 _state = {'running': False, 'paused': False}
 _events = []
 _agg = {}
+_agg_kind = {}          # (cat, name) -> 'counter' for memory counters (duration otherwise)
+_mem_live = {}          # device -> live bytes of profiled NDArrays
 _t0 = time.perf_counter()
 _pid = os.getpid()
 _scope = threading.local()
@@ -34,6 +36,8 @@ _scope = threading.local()
 # fast flags read by the dispatchers
 active_imperative = False
 active_symbolic = False
+active_memory = False
+_MEMORY_DOMAINS = ('Device Storage', 'Pool Memory')
 
 
 def _now_us():
@@ -41,10 +45,11 @@ def _now_us():
 
 
 def _refresh_flags():
-    global active_imperative, active_symbolic
+    global active_imperative, active_symbolic, active_memory
     on = _state['running'] and not _state['paused']
     active_imperative = on and (_config['profile_imperative'] or _config['profile_all'])
     active_symbolic = on and (_config['profile_symbolic'] or _config['profile_all'])
+    active_memory = on and (_config['profile_memory'] or _config['profile_all'])
 
 
 def set_config(**kwargs):
@@ -65,6 +70,7 @@ def set_state(state='stop', profile_process='worker'):
     if state not in ('run', 'stop'):
         raise ValueError('state must be run or stop')
     _state['running'] = state == 'run'
+    _state['paused'] = False        # a state change ends a pause (pause/resume only act while running)
     _refresh_flags()
     if state == 'stop' and _config['continuous_dump']:
         dump(finished=False)
@@ -110,11 +116,78 @@ def record_span(name, cat, start_us, end_us, args=None):
             st[3] = max(st[3], d)
 
 
+def _counter_sample(cat, name, value):
+    """One sample of a memory counter (aggregated as Count / Min / Max, reference kCounter)."""
+    key = (cat, name)
+    st = _agg.setdefault(key, [0, 0.0, float('inf'), float('-inf')])
+    _agg_kind[key] = 'counter'
+    st[0] += 1
+    st[1] = value
+    st[2] = min(st[2], value)
+    st[3] = max(st[3], value)
+    _events.append({'name': name, 'cat': cat, 'ph': 'C', 'ts': _now_us(), 'pid': _pid, 'args': {name: value}})
+
+
+def _device_of(t):
+    return 'gpu/%d' % t.device.index if t.device.type == 'cuda' else 'cpu/0'
+
+
+def memory_alloc(arr):
+    """Storage profiler (reference storage_profiler.h, domain 'Device Storage'): count the bytes of a new
+    NDArray against its device until it is garbage collected."""
+    import weakref
+    t = getattr(arr, '_data', None)
+    if t is None:
+        return
+    nbytes = t.numel() * t.element_size()
+    dev = _device_of(t)
+    with _lock:
+        live = _mem_live[dev] = _mem_live.get(dev, 0) + nbytes
+        _counter_sample('Device Storage', 'Memory: %s' % dev, live)
+    try:
+        weakref.finalize(arr, _memory_free, dev, nbytes)
+    except TypeError:
+        pass
+
+
+def _memory_free(dev, nbytes):
+    with _lock:
+        live = _mem_live[dev] = _mem_live.get(dev, 0) - nbytes
+        if _state['running']:
+            _counter_sample('Device Storage', 'Memory: %s' % dev, live)
+
+
+# custom operators (reference custom.cc profiling): the Python body of a Custom op is a span
+# '<op_type>::pure_python' in the 'Custom Operator' domain, and operators it invokes are recorded
+# there as '<op_type>::<op>'
+_custom = threading.local()
+
+
+class custom_op_scope:  # noqa: N801
+    def __init__(self, op_type, backward=False):
+        self.op_type = op_type
+        self.name = ('_backward_%s' if backward else '%s') % op_type + '::pure_python'
+
+    def __enter__(self):
+        self.prev = getattr(_custom, 'op', None)
+        _custom.op = self.op_type
+        self.t = _now_us()
+        return self
+
+    def __exit__(self, *a):
+        _custom.op = self.prev
+        if active_imperative or active_symbolic:
+            record_span(self.name, 'Custom Operator', self.t, _now_us())
+
+
 class _OpSpan:
     """Context helper used by the dispatchers."""
     __slots__ = ('name', 'cat', 't')
 
     def __init__(self, name, cat):
+        custom = getattr(_custom, 'op', None)
+        if custom is not None:
+            name, cat = '%s::%s' % (custom, name), 'Custom Operator'
         self.name = name
         self.cat = cat
 
@@ -147,39 +220,56 @@ def dump_profile():
 
 
 def dumps(reset=False, format='table', sort_by='total', ascending=False):  # noqa: A002
-    """Aggregate statistics per (category, name): count, total/min/max/avg microseconds."""
-    keys = {'total': 1, 'avg': None, 'min': 2, 'max': 3, 'count': 0}
+    """Aggregate statistics: operator / user-span durations per (domain, name) -- Count, Total, Min,
+    Max, Avg ms -- and memory counters ('Device Storage': Count, Min, Max, Avg kB)."""
+    keys = ('total', 'avg', 'min', 'max', 'count')
     if sort_by not in keys:
         raise ValueError('sort_by must be one of %s' % list(keys))
     with _lock:
-        rows = [(cat, name, v[0], v[1], v[2], v[3]) for (cat, name), v in _agg.items()]
+        rows = [(cat, name, v[0], v[1], v[2], v[3], _agg_kind.get((cat, name), 'duration'))
+                for (cat, name), v in _agg.items()]
         if reset:
             _agg.clear()
+            _agg_kind.clear()
+
+    def stats(r):
+        cat, name, cnt, tot, mn, mx_, kind = r
+        if kind == 'counter':
+            return {'Count': cnt, 'Min': mn / 1024.0, 'Max': mx_ / 1024.0, 'Avg': (mx_ - mn) / 2 / 1024.0}
+        return {'Count': cnt, 'Total': tot / 1e3, 'Min': mn / 1e3, 'Max': mx_ / 1e3, 'Avg': tot / max(cnt, 1) / 1e3}
+
+    field = {'total': 'Total', 'avg': 'Avg', 'min': 'Min', 'max': 'Max', 'count': 'Count'}[sort_by]
 
     def key(r):
-        if sort_by == 'avg':
-            return r[3] / max(r[2], 1)
-        return {'total': r[3], 'min': r[4], 'max': r[5], 'count': r[2]}[sort_by]
+        st = stats(r)
+        return st.get(field, st['Count'])
     rows.sort(key=key, reverse=not ascending)
     if format == 'json':
-        out = {}
-        for cat, name, cnt, tot, mn, mx_ in rows:
-            out.setdefault(cat, {})[name] = {'Count': cnt, 'Total': tot / 1e3, 'Min': mn / 1e3, 'Max': mx_ / 1e3,
-                                             'Avg': tot / max(cnt, 1) / 1e3}
-        return json.dumps({'Time': out, 'Unit': {'Time': 'ms'}})
+        time_out, mem_out = {}, {}
+        for r in rows:
+            (mem_out if r[0] in _MEMORY_DOMAINS else time_out).setdefault(r[0], {})[r[1]] = stats(r)
+        return json.dumps({'Time': time_out, 'Memory': mem_out, 'Unit': {'Time': 'ms', 'Memory': 'kB'}})
     lines = ['Profile Statistics:', '\tNote the difference in units for different entries.']
     cur = None
-    for cat, name, cnt, tot, mn, mx_ in sorted(rows, key=lambda r: r[0]):
+    for r in sorted(rows, key=lambda r: r[0]):
+        cat, name = r[0], r[1]
+        st = stats(r)
+        mem = cat in _MEMORY_DOMAINS
         if cat != cur:
             cur = cat
             lines.append('%s' % cat)
             lines.append('=' * 80)
-            lines.append('%-40s %12s %14s %12s %12s %12s' % ('Name', 'Total Count', 'Time (ms)', 'Min Time (ms)',
-                                                             'Max Time (ms)', 'Avg Time (ms)'))
-            lines.append('%-40s %12s %14s %12s %12s %12s' % ('----', '-----------', '---------', '-------------',
-                                                             '-------------', '-------------'))
-        lines.append('%-40s %12d %14.4f %12.4f %12.4f %12.4f' % (name[:40], cnt, tot / 1e3, mn / 1e3, mx_ / 1e3,
-                                                                 tot / max(cnt, 1) / 1e3))
+            if mem:
+                lines.append('%-40s %12s %14s %14s %14s' % ('Name', 'Total Count', 'Min Use  (kB)', 'Max Use  (kB)',
+                                                            'Avg Use  (kB)'))
+            else:
+                lines.append('%-40s %12s %14s %12s %12s %12s' % ('Name', 'Total Count', 'Time (ms)', 'Min Time (ms)',
+                                                                 'Max Time (ms)', 'Avg Time (ms)'))
+        if mem:
+            lines.append('%-40s %12d %14.4f %14.4f %14.4f' % (name[:40], st['Count'], st['Min'], st['Max'], st['Avg']))
+        else:
+            lines.append('%-40s %12d %14.4f %12.4f %12.4f %12.4f' % (name[:40], st['Count'], st['Total'], st['Min'],
+                                                                     st['Max'], st['Avg']))
     return '\n'.join(lines)
 
 

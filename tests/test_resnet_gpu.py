@@ -27,7 +27,7 @@ def _data(steps, batch=16, size=64):
     return xs, ys
 
 
-def _train(graph, steps=5, name='resnet18_v1'):
+def _train(graph, steps=5, name='resnet18_v1', with_names=False):
     net = _resnet(3, name)
     trainer = gluon.Trainer(net.collect_params(), 'sgd', {'learning_rate': 1e-3, 'momentum': 0.9, 'wd': 1e-4,
                                                           'multi_precision': True, 'rescale_grad': 1.0 / 128})
@@ -45,7 +45,10 @@ def _train(graph, steps=5, name='resnet18_v1'):
     losses = [float(run(x, y).mean().asscalar()) / 128 for x, y in zip(xs, ys)]
     if graph:
         assert run.captured
-    params = [p.data().asnumpy().astype(np.float32) for p in net.collect_params().values()]
+    items = list(net.collect_params().items())
+    params = [p.data().asnumpy().astype(np.float32) for _, p in items]
+    if with_names:
+        return losses, params, [k for k, _ in items]
     return losses, params
 
 
