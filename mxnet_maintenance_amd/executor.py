@@ -290,6 +290,12 @@ class Executor:
                     buf._data.add_(g.to(buf._data.dtype))
                 else:
                     buf._data.copy_(g)
+            # inputs that cannot carry a gradient (integer arrays) get the zero gradient the
+            # reference's backward writes for them
+            got = set(names)
+            for n, buf in gd.items():
+                if n not in got and buf is not None and self._grad_req.get(n) == 'write':
+                    buf._data.zero_()
         box = getattr(self, '_failure_box', None)
         if box is not None and box[0] is not None:
             # gradients of a failed forward carry its (shared) failure

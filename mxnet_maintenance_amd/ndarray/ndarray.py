@@ -380,6 +380,7 @@ class NDArray:
     def __setitem__(self, key, value):
         key = _convert_key(key)
         if isinstance(value, NDArray):
+            _share_failure(value, self)          # writing a failed result fails the target too
             v = value._data
         elif isinstance(value, np.generic):
             v = value.item()

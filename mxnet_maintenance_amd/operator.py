@@ -134,12 +134,32 @@ def _custom_infer(in_shapes, attrs):
     n_args = len(prop.list_arguments())
     shapes = [list(s) if s is not None else None for s in in_shapes[:n_args]]
     try:
-        ins, _, auxs = prop.infer_shape(shapes)
+        ins, _, auxs = _infer3(prop, shapes)
     except Exception:
         return {}
     res = {i: tuple(s) for i, s in enumerate(ins) if s is not None}
     res.update({n_args + i: tuple(s) for i, s in enumerate(auxs)})
     return res
+
+
+def _infer3(prop, shapes):
+    """prop.infer_shape -> (in, out, aux); the aux list may be omitted by user props."""
+    res = prop.infer_shape(shapes)
+    if len(res) == 2:
+        return res[0], res[1], []
+    return res
+
+
+def _out_types(prop, in_types, n_out):
+    """Output dtypes from prop.infer_type when it is overridden, else the first input's dtype."""
+    from .base import torch_dtype
+    if type(prop).infer_type is not CustomOpProp.infer_type:
+        import numpy as _np
+        res = prop.infer_type([_np.dtype(str(t).replace('torch.', '')) for t in in_types])
+        outs = res[1] if len(res) > 1 else []
+        if len(outs) == n_out:
+            return [torch_dtype(_np.dtype(t).name) for t in outs]
+    return [in_types[0] if in_types else torch.float32] * n_out
 
 
 class _CustomFunction(torch.autograd.Function):
@@ -149,11 +169,17 @@ class _CustomFunction(torch.autograd.Function):
         ins = [NDArray(t.detach()) for t in tensors[:n_in]]
         aux = [NDArray(t) for t in tensors[n_in:]]
         in_shapes = [list(t.shape) for t in tensors[:n_in]]
-        _, out_shapes, _ = prop.infer_shape(in_shapes)
-        in_types = [t.dtype for t in tensors[:n_in]]
-        outs = [NDArray(torch.zeros(tuple(s), dtype=in_types[0], device=tensors[0].device)) for s in out_shapes]
+        _, out_shapes, _ = _infer3(prop, in_shapes)
+        out_types = _out_types(prop, [t.dtype for t in tensors[:n_in]], len(out_shapes))
+        dev = tensors[0].device if tensors else torch.device('cpu')
+        outs = [NDArray(torch.zeros(tuple(s), dtype=dt, device=dev)) for s, dt in zip(out_shapes, out_types)]
         with torch.no_grad(), _profiler.custom_op_scope(prop._op_type_name):
             op.forward(is_train=is_train, req=['write'] * len(outs), in_data=ins, out_data=outs, aux=aux)
+        for o in outs:
+            box = getattr(o, '_exc', None)
+            if box is not None and box[0] is not None:
+                from . import engine
+                engine.rethrow(box)       # an operator inside the body failed
         ctx.op, ctx.n_in, ctx.op_type = op, n_in, prop._op_type_name
         ctx.save_for_backward(*tensors)
         ctx.outs = [o._data for o in outs]
@@ -184,18 +210,25 @@ def _custom_fn(*inputs, op_type=None, **kwargs):
     n_in = len(prop.list_arguments())
     tensors = [t for t in inputs if t is not None]
     if tensors and tensors[0].device.type == 'meta':
-        _, out_shapes, _ = prop.infer_shape([list(t.shape) for t in tensors[:n_in]])
+        _, out_shapes, _ = _infer3(prop, [list(t.shape) for t in tensors[:n_in]])
         outs = [torch.empty(tuple(s), dtype=tensors[0].dtype, device='meta') for s in out_shapes]
         return outs[0] if len(outs) == 1 else tuple(outs)
     from .context import context_from_torch
+    dev = tensors[0].device if tensors else torch.device('cpu')
     key = (op_type, tuple(sorted((k, str(v)) for k, v in kwargs.items())),
-           tuple(tuple(t.shape) for t in tensors), tuple(str(t.dtype) for t in tensors), str(tensors[0].device))
+           tuple(tuple(t.shape) for t in tensors), tuple(str(t.dtype) for t in tensors), str(dev))
     op = _OP_CACHE.get(key)
     if op is None:
-        op = prop.create_operator(context_from_torch(tensors[0].device), [list(t.shape) for t in tensors[:n_in]],
+        op = prop.create_operator(context_from_torch(dev), [list(t.shape) for t in tensors[:n_in]],
                                   [t.dtype for t in tensors[:n_in]])
         _OP_CACHE[key] = op
-    outs = _CustomFunction.apply(op, prop, n_in, bool(_state.STATE.training), *tensors)
+    try:
+        outs = _CustomFunction.apply(op, prop, n_in, bool(_state.STATE.training), *tensors)
+    except MXNetError:
+        raise
+    except Exception as e:      # pylint: disable=broad-except
+        # an exception in the Python body surfaces as MXNetError, like the reference's custom op worker
+        raise MXNetError('Error in CustomOp %s: %s: %s' % (op_type, type(e).__name__, e)) from e
     return outs[0] if len(outs) == 1 else tuple(outs)
 
 

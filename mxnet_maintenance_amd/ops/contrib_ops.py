@@ -192,7 +192,8 @@ class _SyncBN(torch.autograd.Function):
 
 
 @register('_contrib_SyncBatchNorm', aliases=('SyncBatchNorm',), arg_names=('data', 'gamma', 'beta'),
-          aux_names=('moving_mean', 'moving_var'), num_outputs=3, num_visible_outputs=1,
+          aux_names=('moving_mean', 'moving_var'), num_outputs=3,
+          num_visible_outputs=lambda a: 3 if str(a.get('output_mean_var', False)) in ('True', 'true', '1') else 1,
           infer_params=lambda s, a: {} if s[0] is None else {i: (s[0][1],) for i in (1, 2, 3, 4)},
           params={'eps': ('float', 1e-3), 'momentum': ('float', 0.9), 'fix_gamma': ('bool', True),
                   'use_global_stats': ('bool', False), 'output_mean_var': ('bool', False), 'ndev': ('int', 1),

@@ -143,7 +143,8 @@ def batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_ga
     if channel_last:
         x = _nd_to_ncx(data)
     elif axis != 1:
-        perm = [0, axis] + [i for i in range(1, nd) if i != axis]
+        others = [i for i in range(nd) if i != axis]      # channel axis to position 1 (axis 0 included)
+        perm = [others[0], axis] + others[1:]
         x = data.permute(*perm)
     else:
         x = data
@@ -161,7 +162,8 @@ def batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_ga
         out = _ncx_to_nd(out)
     elif axis != 1:
         inv = [0] * nd
-        perm = [0, axis] + [i for i in range(1, nd) if i != axis]
+        others = [i for i in range(nd) if i != axis]
+        perm = [others[0], axis] + others[1:]
         for i, p in enumerate(perm):
             inv[p] = i
         out = out.permute(*inv)

@@ -142,18 +142,33 @@ def _t(x, flag):
     return x.transpose(-1, -2) if flag else x
 
 
+def _rows_to(x, axis):
+    """Matrices whose rows lie on ``axis`` (reference la_op ``axis``): move that axis to -2."""
+    a = axis % x.dim()
+    return x if a == x.dim() - 2 else x.movedim(a, -2)
+
+
+def _rows_back(y, axis, nd):
+    a = axis % nd
+    return y if a == nd - 2 else y.movedim(-2, a)
+
+
 @register('_linalg_gemm', aliases=('linalg_gemm',), arg_names=('A', 'B', 'C'),
           params={'transpose_a': ('bool', False), 'transpose_b': ('bool', False), 'alpha': ('float', 1.0),
                   'beta': ('float', 1.0), 'axis': ('int', -2)})
 def linalg_gemm(A, B, C, transpose_a=False, transpose_b=False, alpha=1.0, beta=1.0, axis=-2):
-    return alpha * torch.matmul(_t(A, transpose_a), _t(B, transpose_b)) + beta * C
+    nd = A.dim()
+    A, B, C = _rows_to(A, axis), _rows_to(B, axis), _rows_to(C, axis)
+    return _rows_back(alpha * torch.matmul(_t(A, transpose_a), _t(B, transpose_b)) + beta * C, axis, nd)
 
 
 @register('_linalg_gemm2', aliases=('linalg_gemm2',), arg_names=('A', 'B'),
           params={'transpose_a': ('bool', False), 'transpose_b': ('bool', False), 'alpha': ('float', 1.0),
                   'axis': ('int', -2)})
 def linalg_gemm2(A, B, transpose_a=False, transpose_b=False, alpha=1.0, axis=-2):
-    return alpha * torch.matmul(_t(A, transpose_a), _t(B, transpose_b))
+    nd = A.dim()
+    A, B = _rows_to(A, axis), _rows_to(B, axis)
+    return _rows_back(alpha * torch.matmul(_t(A, transpose_a), _t(B, transpose_b)), axis, nd)
 
 
 @register('_linalg_potrf', aliases=('linalg_potrf',))

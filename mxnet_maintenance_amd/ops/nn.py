@@ -231,8 +231,17 @@ def batch_norm(data, gamma, beta, moving_mean, moving_var, eps=1e-3, momentum=0.
                use_global_stats=False, output_mean_var=False, axis=1, cudnn_off=False, act_type=None,
                min_calib_range=None, max_calib_range=None):
     training = _state.STATE.training and not use_global_stats
-    return hip_ops.batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_gamma,
-                              training, axis, act_type)
+    return _bn_outputs(hip_ops.batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_gamma,
+                                          training, axis, act_type), training, eps)
+
+
+def _bn_outputs(res, training, eps):
+    """The reference's extra BatchNorm outputs in training mode are the batch mean and the batch
+    *inverse* standard deviation 1/sqrt(var + eps) (batch_norm.cc, output_mean_var)."""
+    out, mean, var = res
+    if training and torch.is_tensor(var) and var.numel():
+        var = torch.rsqrt(var.float() + eps).to(var.dtype)
+    return out, mean, var
 
 
 @register('_contrib_BatchNormWithReLU', aliases=('BatchNormWithReLU',),
@@ -242,8 +251,8 @@ def batch_norm_relu(data, gamma, beta, moving_mean, moving_var, eps=1e-3, moment
                     use_global_stats=False, output_mean_var=False, axis=1, cudnn_off=False, act_type=None,
                     min_calib_range=None, max_calib_range=None):
     training = _state.STATE.training and not use_global_stats
-    return hip_ops.batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_gamma,
-                              training, axis, 'relu')
+    return _bn_outputs(hip_ops.batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_gamma,
+                                          training, axis, 'relu'), training, eps)
 
 
 @register('_contrib_BatchNormAddReLU', aliases=('BatchNormAddReLU',),
@@ -459,6 +468,11 @@ class _SoftmaxOutputFn(torch.autograd.Function):
             if use_ignore:
                 valid = (lab != int(ignore_label)).to(p.dtype)
                 grad = grad * valid.unsqueeze(1)
+        elif tuple(label.shape) == tuple(shape):
+            # a label of the data's shape is a probability distribution (reference: no one-hot)
+            p2 = p.reshape(-1, p.shape[-1])
+            grad = p2 - label.reshape(p2.shape).to(p2.dtype)
+            valid = torch.ones(p2.shape[0], dtype=p.dtype, device=p.device)
         else:
             p2 = p.reshape(-1, p.shape[-1])
             c = p2.shape[-1]
@@ -475,6 +489,11 @@ class _SoftmaxOutputFn(torch.autograd.Function):
             grad = grad / shape[0]
         elif norm == 'valid':
             grad = grad / torch.clamp(valid.sum(), min=1.0)
+        if multi_output and norm != 'valid':
+            spatial = 1
+            for d in shape[2:]:
+                spatial *= d
+            grad = grad / spatial       # reference softmax_output-inl.h: per-position average
         grad = grad * grad_scale
         return grad.reshape(shape).to(dt), None, None, None, None, None, None, None, None
 

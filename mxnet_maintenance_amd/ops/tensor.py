@@ -129,7 +129,16 @@ def _cmp(f):
 
 
 def _mod(a, b):
-    return torch.remainder(a, b)
+    """Python-sign modulo; x % 0 is 0 (reference mshadow_op::mod), also for integers."""
+    if not torch.is_tensor(b):
+        if b == 0:
+            return torch.zeros_like(a)
+        return torch.remainder(a, b)
+    zero = b == 0
+    if not torch.is_tensor(a):
+        a = torch.full_like(b, a)
+    r = torch.remainder(a, torch.where(zero, torch.ones_like(b), b))
+    return torch.where(zero, torch.zeros_like(r), r)
 
 
 def _logical(f):
@@ -639,7 +648,11 @@ def repeat(data, repeats=1, axis=None):
 
 @register('tile', params={'reps': ('shape', ())})
 def tile(data, reps=()):
-    reps = tuple(reps)
+    reps = tuple(int(r) for r in reps)
+    from ..util import is_np_shape
+    if any(r < 0 for r in reps) or (not is_np_shape() and any(r == 0 for r in reps)):
+        # 0 means "unknown" outside numpy shape semantics (reference TileOpShape)
+        raise MXNetError('tile: reps must be positive, got %s' % (reps,))
     if len(reps) < data.dim():
         reps = (1,) * (data.dim() - len(reps)) + reps
     return data.repeat(*reps) if len(reps) == data.dim() else data.reshape((1,) * (len(reps) - data.dim()) + tuple(data.shape)).repeat(*reps)
@@ -705,6 +718,8 @@ def batch_take(a, indices):
                                                     'off_value': ('float', 0.0), 'dtype': ('str', 'float32')})
 def one_hot(indices, depth=1, on_value=1.0, off_value=0.0, dtype='float32'):
     idx = indices.to(torch.int64)
+    if depth == 0:
+        return torch.zeros(tuple(idx.shape) + (0,), dtype=torch_dtype(dtype), device=idx.device)
     valid = (idx >= 0) & (idx < depth)
     oh = torch.nn.functional.one_hot(torch.where(valid, idx, torch.zeros_like(idx)), depth)
     oh = oh * valid.unsqueeze(-1)
@@ -783,6 +798,9 @@ def dot(lhs, rhs, transpose_a=False, transpose_b=False, forward_stype=None):
         a = a.reshape(a.shape[0], -1).t() if a.dim() > 2 else a.t() if a.dim() == 2 else a
     if transpose_b:
         b = b.t() if b.dim() == 2 else b.reshape(-1, b.shape[-1]).t().reshape(b.shape[-1], *b.shape[:-1]) if b.dim() > 2 else b
+    if a.shape[-1] != b.shape[0]:
+        raise MXNetError('dot: shape mismatch, lhs %s and rhs %s do not share the contracted dimension'
+                         % (tuple(lhs.shape), tuple(rhs.shape)))
     return torch.tensordot(a, b, dims=1)
 
 

@@ -401,8 +401,11 @@ class Symbol:
             for n, v in zip(arg_names, args):
                 if v is not None:
                     known[n] = v
+        names = set(arg_names) | set(self.list_auxiliary_states())
         for k, v in kwargs.items():
-            if v is not None:
+            # names that are not inputs (e.g. op attributes passed along to simple_bind) are ignored,
+            # as by the reference's MXSymbolInferShape keyword matching
+            if v is not None and k in names:
                 known[k] = v
         if what == 'shape':
             shapes, dtypes = {k: tuple(v) for k, v in known.items()}, {}

@@ -376,7 +376,8 @@ def _named_inputs(names, given, what):
 def _to_ctx(v, ctx, dtype):
     if isinstance(v, NDArray):
         return v.as_in_context(ctx)
-    return nd.array(v, ctx=ctx, dtype=_arg_dtype(v, dtype) if not hasattr(v, 'dtype') else v.dtype)
+    # reference _parse_location: numpy inputs take ``dtype`` (float32 by default) unless dtype='asnumpy'
+    return nd.array(v, ctx=ctx, dtype=_arg_dtype(v, dtype))
 
 
 def _parse_location(sym, location, ctx, dtype=default_dtype()):
