@@ -118,8 +118,9 @@ def conv_tee(data, weight, inplace_grad=False):
 # ---------------------------------------------------------------------------
 
 def batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_gamma, training,
-               axis, act_type, addend=None):
-    """BatchNorm with MXNet semantics; returns (out, mean, var).
+               axis, act_type, addend=None, invstd_out=False):
+    """BatchNorm with MXNet semantics; returns (out, mean, var) -- (out, mean, 1/sqrt(var + eps)) in
+    training mode with ``invstd_out`` (the reference's extra outputs, batch_norm.cc).
 
     ``moving_* = moving_* * momentum + batch_* * (1 - momentum)`` (biased
     variance, src/operator/nn/batch_norm.cc).  ``act_type='relu'`` fuses
@@ -135,11 +136,11 @@ def batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_ga
         al = _as_nhwc_view(addend) if addend is not None else None
         if _K.bn_ok(xl):
             out, m, v = _K.BatchNormNHWC.apply(xl, g, beta, al, eps, training, act_type == 'relu',
-                                                moving_mean, moving_var, momentum)
+                                                moving_mean, moving_var, momentum, invstd_out)
             return out.permute(0, 3, 1, 2), m, v
     if channel_last and _use_hip(data) and _K.bn_ok(data):
         return _K.BatchNormNHWC.apply(data, g, beta, addend, eps, training, act_type == 'relu',
-                                      moving_mean, moving_var, momentum)
+                                      moving_mean, moving_var, momentum, invstd_out)
     if channel_last:
         x = _nd_to_ncx(data)
     elif axis != 1:
@@ -154,7 +155,7 @@ def batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_ga
             var = (1.0 / (sinvstd.float() ** 2) - eps).clamp_(min=0.0) if sinvstd.numel() else sinvstd
             moving_mean.mul_(momentum).add_(smean.detach().to(moving_mean.dtype), alpha=1 - momentum)
             moving_var.mul_(momentum).add_(var.to(moving_var.dtype), alpha=1 - momentum)
-        mean_out, var_out = smean, var
+        mean_out, var_out = smean, (sinvstd if invstd_out else var)
     else:
         out = F.batch_norm(x, moving_mean, moving_var, g, beta, False, 0.0, eps)
         mean_out, var_out = moving_mean, moving_var

@@ -89,7 +89,8 @@ class BatchNormNHWC(torch.autograd.Function):
     """BatchNorm over the last (channel) axis with optional fused residual add + ReLU."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, addend, eps, training, relu, moving_mean, moving_var, momentum=None):
+    def forward(ctx, x, gamma, beta, addend, eps, training, relu, moving_mean, moving_var, momentum=None,
+                invstd_out=False):
         lib = _K.lib()
         C = x.shape[-1]
         R = x.numel() // C
@@ -154,10 +155,13 @@ class BatchNormNHWC(torch.autograd.Function):
             y._mxamd_bn_src = (x, mean, scale if relu_mode == 2 else None, shift if relu_mode == 2 else None,
                                mask if relu_mode == 3 else None, relu_mode, ctx.bn_token)
         ctx.refs = (gamma, beta)
-        ctx.mark_non_differentiable(mean, var)
+        # invstd_out: the third output is the batch 1/sqrt(var + eps) the kernel already wrote (the
+        # reference's training-mode extra output) instead of the variance
+        third = invstd if (invstd_out and training) else var
+        ctx.mark_non_differentiable(mean, third)
         # mean/var never receive gradients: skip materialising two zero tensors per call
         ctx.set_materialize_grads(False)
-        return y, mean, var
+        return y, mean, third
 
     @staticmethod
     def backward(ctx, gy, _gm, _gv):
@@ -166,7 +170,7 @@ class BatchNormNHWC(torch.autograd.Function):
         relu_mode, training, has_add, gdt, bdt = ctx.cfg
         gamma_ref, beta_ref = ctx.refs
         if gy is None:
-            return (None,) * 10
+            return (None,) * 11
         gy = gy.contiguous()
         C = x.shape[-1]
         R = x.numel() // C
@@ -207,7 +211,7 @@ class BatchNormNHWC(torch.autograd.Function):
         else:
             dgamma = out[0].to(gdt) if need_g else None
             dbeta = out[1].to(bdt) if need_b else None
-        return dx, dgamma, dbeta, dz, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dz, None, None, None, None, None, None, None
 
 
 class SoftmaxCE(torch.autograd.Function):
@@ -654,19 +658,41 @@ def _big_algo(key):
     return None
 
 
-def _dgrad_bn_fused(key, dy, w, pad, bn_src):
-    """Stride-1 dgrad on the big-tile kernel that also emits the backward statistics of the
-    BatchNorm whose output this conv read (its gradient is exactly this dgrad) -- when autotuning
-    picked the big kernel for this shape.  None otherwise (the caller runs the normal selection)."""
-    if bn_src is None or not _BN_BWD_FUSE[0]:
-        return None
-    v = _big_algo(key)
-    if v is None:
-        return None
+def _bn_bwd_fusable(bn_src, out_shape):
+    return bn_src is not None and _BN_BWD_FUSE[0] and tuple(bn_src[0].shape) == tuple(out_shape)
+
+
+def _charge_bn_bwd(cands, z):
+    """Timing closures for a dgrad whose output is the gradient of a BatchNorm(+ReLU) output: a
+    candidate without the fused epilogue is charged the backward-statistics pass the BatchNorm then
+    runs itself (one read of the gradient and one of the BN input z)."""
+    def charged(fn):
+        def run():
+            r = fn()
+            if isinstance(r, torch.Tensor) and r.shape[-1] % 8 == 0 and r.is_contiguous():
+                _bn_stats_pass(r)
+                _bn_stats_pass(z)
+            return r
+        return run
+    return [(n, charged(fn)) for n, fn in cands]
+
+
+def _dgrad_bn_candidates(dy, x, w, stride, pad, bn_src):
+    """Stride-1 dgrad candidates when a BatchNorm produced x: the plain candidates plus big-tile
+    variants whose epilogue also emits that BatchNorm's backward statistics ('hipN+bn').  Returns
+    (candidates, timing closures): autotuning weighs the fused epilogue's extra cost against the
+    reduction pass it saves."""
+    cands = _dgrad_candidates(dy, x, w, stride, pad)
     K, R, S, C = w.shape
-    if bn_src[0].shape[-1] != C:
-        return None
-    return conv_fwd(dy, _dgrad_weight(w), (1, 1), (R - 1 - pad[0], S - 1 - pad[1]), None, v, bn_bwd=bn_src)
+    fused = []
+    if (_CONV_HIP and tuple(stride) == (1, 1) and 2 * pad[0] == R - 1 and 2 * pad[1] == S - 1
+            and K % 64 == 0):
+        for v in _fwd_variants(K, C):
+            if v in _BIG_VARIANTS:
+                fused.append(('hip%d+bn' % v, lambda v=v: conv_fwd(dy, _dgrad_weight(w), (1, 1),
+                                                                   (R - 1 - pad[0], S - 1 - pad[1]), None, v,
+                                                                   bn_bwd=bn_src)))
+    return cands + fused, _charge_bn_bwd(cands, bn_src[0]) + fused
 
 
 def _dgrad_default(w, stride):
@@ -791,8 +817,10 @@ class ConvNHWC(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             key = ('dgrad', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype)
-            dx = _dgrad_bn_fused(key, dy, w, pad, ctx.bn_src)
-            if dx is None:
+            if _bn_bwd_fusable(ctx.bn_src, x.shape):
+                cands, timing = _dgrad_bn_candidates(dy, x, w, stride, pad, ctx.bn_src)
+                dx = _select(key + ('bnbwd',), cands, _dgrad_default(w, stride), timing=timing)
+            else:
                 dx = _select(key, _dgrad_candidates(dy, x, w, stride, pad), _dgrad_default(w, stride))
         if ctx.needs_input_grad[1]:
             dw = _wgrad(dy, x, w, ctx.w_ref, stride, pad)
@@ -855,6 +883,8 @@ def _tee_dgrad(gy, x, w, gpass, inplace, bn_src=None):
         return torch.mm(g2, w2).view(x.shape)
 
     cands = []
+    fused = []
+    fuse_bn = _bn_bwd_fusable(bn_src, x.shape)
     if _CONV_HIP and K % 64 == 0 and gy.dtype in (torch.float16, torch.bfloat16) and gy.numel() < 2 ** 31:
         wt = None
         for v, (bco, _bpix) in sorted(_BIG_VARIANTS.items()):
@@ -863,24 +893,23 @@ def _tee_dgrad(gy, x, w, gpass, inplace, bn_src=None):
             if wt is None:
                 wt = w2.t().contiguous().view(C, 1, 1, K)
 
-            def big(v=v, wt=wt):
+            def big(v=v, wt=wt, bn=None):
                 add = gpass.contiguous() if gpass is not None else None
-                return conv_fwd(gy, wt, (1, 1), (0, 0), None, v, addend=add)
+                return conv_fwd(gy, wt, (1, 1), (0, 0), None, v, addend=add, bn_bwd=bn)
             cands.append(('hip%d' % v, big))
+            if fuse_bn:
+                # the block input's BatchNorm (the previous block's residual tail) gets its backward
+                # statistics from this dgrad's epilogue
+                fused.append(('hip%d+bn' % v, lambda big=big: big(bn=bn_src)))
     # autotuning runs every candidate: use an out-of-place GEMM there (the in-place one would
     # accumulate into gpass once per timing repetition)
     cands.append(('mm', lambda: mm() if not (gpass is not None and inplace) else
                   torch.addmm(gpass.reshape(-1, C), g2, w2).view(x.shape)))
-    key = ('teedgrad', tuple(x.shape), tuple(w.shape), x.dtype)
+    key = ('teedgrad', tuple(x.shape), tuple(w.shape), x.dtype) + (('bnbwd',) if fuse_bn else ())
     if _ALGO.get(key) == 'mm':
         return mm()
-    v = _big_algo(key)
-    if v is not None and bn_src is not None and _BN_BWD_FUSE[0] and bn_src[0].shape == x.shape:
-        # the block input's BatchNorm (the residual tail of the previous block) gets its backward
-        # statistics from this dgrad's epilogue
-        add = gpass.contiguous() if gpass is not None else None
-        return conv_fwd(gy, w2.t().contiguous().view(C, 1, 1, K), (1, 1), (0, 0), None, v, addend=add,
-                        bn_bwd=bn_src)
+    if fuse_bn:
+        return _select(key, cands + fused, 'mm', timing=_charge_bn_bwd(cands, bn_src[0]) + fused)
     return _select(key, cands, 'mm')
 
 

@@ -231,17 +231,8 @@ def batch_norm(data, gamma, beta, moving_mean, moving_var, eps=1e-3, momentum=0.
                use_global_stats=False, output_mean_var=False, axis=1, cudnn_off=False, act_type=None,
                min_calib_range=None, max_calib_range=None):
     training = _state.STATE.training and not use_global_stats
-    return _bn_outputs(hip_ops.batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_gamma,
-                                          training, axis, act_type), training, eps)
-
-
-def _bn_outputs(res, training, eps):
-    """The reference's extra BatchNorm outputs in training mode are the batch mean and the batch
-    *inverse* standard deviation 1/sqrt(var + eps) (batch_norm.cc, output_mean_var)."""
-    out, mean, var = res
-    if training and torch.is_tensor(var) and var.numel():
-        var = torch.rsqrt(var.float() + eps).to(var.dtype)
-    return out, mean, var
+    return hip_ops.batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_gamma,
+                              training, axis, act_type, invstd_out=True)
 
 
 @register('_contrib_BatchNormWithReLU', aliases=('BatchNormWithReLU',),
@@ -251,8 +242,8 @@ def batch_norm_relu(data, gamma, beta, moving_mean, moving_var, eps=1e-3, moment
                     use_global_stats=False, output_mean_var=False, axis=1, cudnn_off=False, act_type=None,
                     min_calib_range=None, max_calib_range=None):
     training = _state.STATE.training and not use_global_stats
-    return _bn_outputs(hip_ops.batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_gamma,
-                                          training, axis, 'relu'), training, eps)
+    return hip_ops.batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_gamma,
+                              training, axis, 'relu', invstd_out=True)
 
 
 @register('_contrib_BatchNormAddReLU', aliases=('BatchNormAddReLU',),

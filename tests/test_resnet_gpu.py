@@ -65,7 +65,11 @@ def test_resnet_graph_step_matches_eager(name):
     le, we = _train(False, name=name)
     le2, we2 = _train(False, name=name)
     lg, wg = _train(True, name=name)
-    np.testing.assert_allclose(lg, le, rtol=2e-2, atol=2e-2)
+    # losses: the graph run may differ from eager by at most a few times what two eager runs differ
+    # by (fp16 training of a small-batch ResNet amplifies rounding differences of the vendor split-K
+    # weight-gradient kernels, which accumulate with atomics, step over step)
+    loss_noise = float(np.abs(np.asarray(le2) - np.asarray(le)).max())
+    assert np.abs(np.asarray(lg) - np.asarray(le)).max() <= 3 * loss_noise + 2e-2, (lg, le, le2)
     noise = _global_err(we2, we)
     err = _global_err(wg, we)
     assert err <= 3 * noise + 1e-4, (err, noise)
