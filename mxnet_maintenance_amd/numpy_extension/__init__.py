@@ -58,6 +58,11 @@ _MAP = {
     'box_iou': ('_contrib_box_iou', None), 'multibox_prior': ('_contrib_MultiBoxPrior', None),
     'multibox_target': ('_contrib_MultiBoxTarget', None), 'multibox_detection': ('_contrib_MultiBoxDetection', None),
     'bipartite_matching': ('_contrib_bipartite_matching', None),
+    'intgemm_maxabsolute': ('_contrib_intgemm_maxabsolute', None),
+    'intgemm_prepare_data': ('_contrib_intgemm_prepare_data', None),
+    'intgemm_prepare_weight': ('_contrib_intgemm_prepare_weight', None),
+    'intgemm_take_weight': ('_contrib_intgemm_take_weight', None),
+    'intgemm_fully_connected': ('_contrib_intgemm_fully_connected', None),
 }
 
 __all__ = ['set_np', 'reset_np', 'is_np_array', 'is_np_shape', 'use_np', 'use_np_array', 'use_np_shape', 'np_array',

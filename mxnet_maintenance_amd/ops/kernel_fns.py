@@ -581,6 +581,10 @@ def _fwd_candidates(x, w, stride, pad, bias):
         for v in _fwd_variants(C, K, bias is not None):
             c.append(('hip%d' % v, lambda v=v: conv_fwd(x, w, stride, pad, bias, v, bn_stats=stats)))
     if R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0):
+        x2, w2 = x.reshape(-1, C), w.reshape(K, C)
+        for name, fn in _gemm().candidates(x2, w2, bias=bias):
+            c.append((name, lambda fn=fn: fn().view(x.shape[0], x.shape[1], x.shape[2], K)))
+
         def mm():
             y = torch.mm(x.reshape(-1, C), w.reshape(K, C).t())
             if bias is not None:
@@ -640,6 +644,7 @@ def _dgrad_candidates(dy, x, w, stride, pad):
     K, R, S, C = w.shape
     if R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0):
         c.append(('mm', lambda: torch.mm(dy.reshape(-1, K), w.reshape(K, C)).view(x.shape)))
+        c.extend(_gemm_dgrad_1x1(dy, w, x.shape))
     if (tuple(stride) == (1, 1) and C % 64 == 0 and K % 32 == 0 and 2 * pad[0] == R - 1 and 2 * pad[1] == S - 1
             and _CONV_HIP):
         c.append(('hip', lambda: conv_fwd(dy, _dgrad_weight(w), (1, 1), (R - 1 - pad[0], S - 1 - pad[1]))))
@@ -648,6 +653,29 @@ def _dgrad_candidates(dy, x, w, stride, pad):
                                                         None, v)))
     c.append(('miopen', lambda: _conv_bwd_torch(dy, x, w, stride, pad, (True, False))[0]))
     return c
+
+
+def _gemm():
+    from . import gemm
+    return gemm
+
+
+def _gemm_dgrad_1x1(dy, w, xshape, addend=None):
+    """GEMM-kernel candidates for dX = dY . W of a 1x1 stride-1 conv (W^T materialised per call: a
+    small copy next to the activation-sized GEMM), optionally + ``addend`` (beta = 1)."""
+    K, C = w.shape[0], w.shape[3]
+    G = _gemm()
+    d2 = dy.reshape(-1, K)
+    if not (K % 64 == 0 and C % 64 == 0 and d2.is_cuda and d2.dtype in G._DT and w.dtype == d2.dtype
+            and d2.is_contiguous() and d2.data_ptr() % 16 == 0 and _K.available()):
+        return []
+    out = []
+    for cfg in G.configs(d2.shape[0], C, K, G.AUTOTUNE_TILES):
+        def run(cfg=cfg):
+            add = addend.contiguous().view(-1, C) if addend is not None else None
+            return G.gemm_nt(d2, w.reshape(K, C).t().contiguous(), addend=add, cfg=cfg).view(xshape)
+        out.append(('gemm%ds%d' % cfg, run))
+    return out
 
 
 def _big_algo(key):
@@ -901,6 +929,7 @@ def _tee_dgrad(gy, x, w, gpass, inplace, bn_src=None):
                 # the block input's BatchNorm (the previous block's residual tail) gets its backward
                 # statistics from this dgrad's epilogue
                 fused.append(('hip%d+bn' % v, lambda big=big: big(bn=bn_src)))
+    cands.extend(_gemm_dgrad_1x1(gy, w, x.shape, addend=gpass))
     # autotuning runs every candidate: use an out-of-place GEMM there (the in-place one would
     # accumulate into gpass once per timing repetition)
     cands.append(('mm', lambda: mm() if not (gpass is not None and inplace) else

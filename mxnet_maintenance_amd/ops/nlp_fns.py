@@ -256,6 +256,7 @@ def all_finite(x, scale=1.0, flag=None):
 # keeps the faster.
 
 from . import kernel_fns as _KF  # noqa: E402
+from . import gemm as _G  # noqa: E402
 
 
 def gemm_ok(x, w):
@@ -270,6 +271,7 @@ def _fc_fwd_cands(x2, w, b):
     if K % 32 == 0 and N % 64 == 0 and x2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0:
         c.append(('hip', lambda: _KF.conv_fwd(x2.view(M, 1, 1, K), w.view(N, 1, 1, K), (1, 1), (0, 0),
                                               b).view(M, N)))
+    c.extend(_G.candidates(x2, w, bias=b))
     c.append(('mm', lambda: torch.nn.functional.linear(x2, w, None if b is None else b.to(x2.dtype))))
     return c
 
@@ -281,6 +283,12 @@ def _fc_dgrad_cands(dy2, w):
     if N % 32 == 0 and K % 64 == 0:
         c.append(('hip', lambda: _KF.conv_fwd(dy2.view(M, 1, 1, N), w.t().contiguous().view(K, 1, 1, N), (1, 1),
                                               (0, 0)).view(M, K)))
+    # dX = dY . W = dY . (W^T)^T: the GEMM kernel on a fresh W^T (a small copy; the weight may
+    # change in place between steps through the fused optimizer's raw pointers, so no caching)
+    if (N % 64 == 0 and K % 64 == 0 and dy2.is_cuda and dy2.dtype in _G._DT and w.dtype == dy2.dtype
+            and dy2.is_contiguous() and dy2.data_ptr() % 16 == 0 and _K.available()):
+        for cfg in _G.configs(M, K, N, _G.AUTOTUNE_TILES):
+            c.append(('gemm%ds%d' % cfg, lambda cfg=cfg: _G.gemm_nt(dy2, w.t().contiguous(), cfg=cfg)))
     c.append(('mm', lambda: torch.mm(dy2, w)))
     return c
 

@@ -287,3 +287,234 @@ def quantized_concat(*args, num_args=1, dim=1):
     r = max(float(torch.maximum(_range_scalar(mn).abs(), _range_scalar(mx).abs())) for mn, mx in zip(mins, maxs))
     r = torch.tensor(r)
     return _quantize_int8(torch.cat(reals, dim=dim), -r, r)
+
+
+# ---------------------------------------------------------------------------
+# quantized BatchNorm / elemwise_mul / Embedding / RNN, asymmetric quantize
+# ---------------------------------------------------------------------------
+
+def _maxabs(mn, mx):
+    return torch.maximum(_range_scalar(mn).abs(), _range_scalar(mx).abs())
+
+
+def _bn_q_infer(in_shapes, a):
+    d = in_shapes[0]
+    if d is None:
+        return {}
+    c = d[a.get('axis', 1) % len(d)]
+    return {1: (c,), 2: (c,), 3: (c,), 4: (c,), 5: (1,), 6: (1,)}
+
+
+@register('_contrib_quantized_batch_norm',
+          arg_names=('data', 'gamma', 'beta', 'moving_mean', 'moving_var', 'min_data', 'max_data'),
+          num_outputs=3, infer_params=_bn_q_infer,
+          params={'eps': ('float', 1e-3), 'momentum': ('float', 0.9), 'fix_gamma': ('bool', True),
+                  'use_global_stats': ('bool', False), 'output_mean_var': ('bool', False), 'axis': ('int', 1),
+                  'cudnn_off': ('bool', False), 'min_calib_range': ('float?', None),
+                  'max_calib_range': ('float?', None)})
+def quantized_batch_norm(data, gamma, beta, moving_mean, moving_var, min_data, max_data, eps=1e-3, momentum=0.9,
+                         fix_gamma=True, use_global_stats=False, output_mean_var=False, axis=1, cudnn_off=False,
+                         min_calib_range=None, max_calib_range=None):
+    """Inference BatchNorm on int8/uint8 data (reference quantized_batch_norm.cc): the input scale and
+    the moving statistics fold into one per-channel affine map, the result is requantized to int8 with
+    the calibrated output range (or the observed one)."""
+    real = dequantize(data, min_data, max_data)
+    nd_ = real.dim()
+    ax = axis % nd_
+    shape = [1] * nd_
+    shape[ax] = real.shape[ax]
+    g = torch.ones_like(gamma.float()) if fix_gamma else gamma.float()
+    inv = torch.rsqrt(moving_var.float() + eps)
+    scale = (g * inv).reshape(shape)
+    shift = (beta.float() - moving_mean.float() * g * inv).reshape(shape)
+    y = real * scale + shift
+    if min_calib_range is not None and max_calib_range is not None:
+        r = torch.tensor(max(abs(min_calib_range), abs(max_calib_range)), device=y.device)
+    else:
+        r = torch.maximum(y.min().abs(), y.max().abs())
+    return _quantize_int8(y, -r, r)
+
+
+def _qmul_nout(a):
+    return 1 if str(a.get('enable_float_output', False)) in ('True', 'true', '1') else 3
+
+
+@register('_contrib_quantized_elemwise_mul',
+          arg_names=('lhs', 'rhs', 'lhs_min', 'lhs_max', 'rhs_min', 'rhs_max'), num_outputs=_qmul_nout,
+          params={'min_calib_range': ('float?', None), 'max_calib_range': ('float?', None),
+                  'enable_float_output': ('bool', False)})
+def quantized_elemwise_mul(lhs, rhs, lhs_min, lhs_max, rhs_min, rhs_max, min_calib_range=None,
+                           max_calib_range=None, enable_float_output=False):
+    """int8 x int8 elementwise product (reference quantized_elemwise_mul.cc).  Output: fp32 real values
+    (enable_float_output), int8 in the calibrated range, or int32 carrying a*b*scale_l*scale_r with
+    the int32 range of an s8 x s8 product."""
+    sl = _maxabs(lhs_min, lhs_max) / INT8_MAX
+    sr = _maxabs(rhs_min, rhs_max) / INT8_MAX
+    prod = lhs.to(torch.int32).to(torch.float64) * rhs.to(torch.int32).to(torch.float64)
+    if enable_float_output:
+        return (prod * (sl * sr).double()).float()
+    if min_calib_range is not None and max_calib_range is not None:
+        r = max(abs(min_calib_range), abs(max_calib_range))
+        out_scale = (INT8_MAX / r) * (sl * sr).double()
+        q = torch.clamp(torch.trunc(prod * out_scale), -INT8_MAX, INT8_MAX).to(torch.int8)
+        t = torch.tensor([r], dtype=torch.float32, device=lhs.device)
+        return q, -t, t
+    out = torch.trunc(prod * (sl * sr).double()).to(torch.int32)
+    r = (sl * sr * INT32_MAX).reshape(1).float()
+    return out, -r, r
+
+
+@register('_contrib_quantized_embedding', arg_names=('data', 'weight', 'min_weight', 'max_weight'),
+          num_outputs=3, infer_params=lambda s, a: {1: (a['input_dim'], a['output_dim']), 2: (1,), 3: (1,)},
+          params={'input_dim': ('int', 0), 'output_dim': ('int', 0), 'dtype': ('str', 'float32'),
+                  'sparse_grad': ('bool', False)})
+def quantized_embedding(data, weight, min_weight, max_weight, input_dim=0, output_dim=0, dtype='float32',
+                        sparse_grad=False):
+    """Row gather of an int8 table (reference quantized_indexing_op.cc); the output keeps the
+    weight's range.  Out-of-range indices are clipped, as Embedding does."""
+    idx = torch.clamp(data.to(torch.int64), 0, weight.shape[0] - 1)
+    return weight[idx], _range_scalar(min_weight).reshape(1), _range_scalar(max_weight).reshape(1)
+
+
+def _qrnn_nout(a):
+    so = str(a.get('state_outputs', False)) in ('True', 'true', '1')
+    return 3 if so else 1
+
+
+@register('_contrib_quantized_rnn',
+          arg_names=('data', 'parameters', 'state', 'state_cell', 'min_data', 'max_data'),
+          num_outputs=_qrnn_nout,
+          params={'state_size': ('int', 0), 'num_layers': ('int', 1), 'bidirectional': ('bool', False),
+                  'mode': ('str', 'lstm'), 'p': ('float', 0.0), 'state_outputs': ('bool', False),
+                  'projection_size': ('int?', None), 'lstm_state_clip_min': ('float?', None),
+                  'lstm_state_clip_max': ('float?', None), 'lstm_state_clip_nan': ('bool', False),
+                  'use_sequence_length': ('bool', False)})
+def quantized_rnn(data, parameters, state, state_cell, min_data, max_data, state_size=0, num_layers=1,
+                  bidirectional=False, mode='lstm', p=0.0, state_outputs=False, projection_size=None,
+                  lstm_state_clip_min=None, lstm_state_clip_max=None, lstm_state_clip_nan=False,
+                  use_sequence_length=False):
+    """LSTM on uint8 data (reference quantized_rnn.cc).  As in the reference, the last two inputs carry
+    the asymmetric data scale and shift of quantize_asym: real = (q - shift) / scale.  The recurrence
+    then runs in fp32 (at least as accurate as the reference's int8-weight GEMMs)."""
+    if mode != 'lstm':
+        raise ValueError('quantized_rnn supports mode=lstm only')
+    from .nn import rnn
+    scale = _range_scalar(min_data)
+    shift = _range_scalar(max_data)
+    real = (data.float() - shift) / scale
+    return rnn(real, parameters.float(), state.float(), state_cell.float(), state_size=state_size,
+               num_layers=num_layers, bidirectional=bidirectional, mode='lstm', p=0.0,
+               state_outputs=state_outputs, projection_size=projection_size,
+               lstm_state_clip_min=lstm_state_clip_min, lstm_state_clip_max=lstm_state_clip_max,
+               lstm_state_clip_nan=lstm_state_clip_nan)
+
+
+@register('_contrib_quantize_asym', aliases=('quantize_asym',), num_outputs=3,
+          params={'min_calib_range': ('float?', None), 'max_calib_range': ('float?', None)})
+def quantize_asym(data, min_calib_range=None, max_calib_range=None):
+    """Asymmetric uint8 quantization (reference quantize_asym-inl.h): q = x * scale + shift + 0.5 with
+    scale = 255 / (max - min), shift = 255 - max * scale; int8 input is re-centred (+128), uint8 passes.
+    Outputs (q, scale, shift)."""
+    dev = data.device
+    if data.dtype == torch.uint8:
+        return data.clone(), torch.ones(1, device=dev), torch.zeros(1, device=dev)
+    if data.dtype == torch.int8:
+        q = (data.to(torch.int16) + 128).to(torch.uint8)
+        return q, torch.ones(1, device=dev), torch.full((1,), 128.0, device=dev)
+    x = data.float()
+    if min_calib_range is not None and max_calib_range is not None:
+        mn = torch.tensor(float(min_calib_range), device=dev)
+        mx = torch.tensor(float(max_calib_range), device=dev)
+    else:
+        mn, mx = x.min(), x.max()
+    scale = UINT8_MAX / (mx - mn)
+    shift = UINT8_MAX - mx * scale
+    q = torch.clamp(torch.floor(x * scale + shift + 0.5), 0, UINT8_MAX).to(torch.uint8)
+    return q, scale.reshape(1), shift.reshape(1)
+
+
+# ---------------------------------------------------------------------------
+# intgemm (reference src/operator/contrib/intgemm/*): int8 GEMM with -128 banned.
+# The "prepared weight" format of this framework is the plain row-major int8 [rows, inner]
+# matrix the gfx950 i8 MFMA kernel consumes (the reference's is CPU-layout dependent; its tests
+# only check consistency between the prepare / take / multiply routes).
+# ---------------------------------------------------------------------------
+
+@register('_contrib_intgemm_maxabsolute', aliases=('_npx_intgemm_maxabsolute',))
+def intgemm_maxabsolute(data):
+    return data.float().abs().max().reshape(1)
+
+
+def _intgemm_quant(x, maxabs):
+    m = _range_scalar(maxabs)
+    q = torch.round(x.float() * (INT8_MAX / m))
+    return torch.clamp(q, -INT8_MAX, INT8_MAX).to(torch.int8)
+
+
+@register('_contrib_intgemm_prepare_data', aliases=('_npx_intgemm_prepare_data',),
+          arg_names=('data', 'maxabs'))
+def intgemm_prepare_data(data, maxabs):
+    """int8 quantisation with maxabs -> 127 and -128 banned (values clipped to [-127, 127])."""
+    return _intgemm_quant(data, maxabs)
+
+
+def _pw_args(a):
+    return ['weight'] if str(a.get('already_quantized', False)) in ('True', 'true', '1') else ['weight', 'maxabs']
+
+
+@register('_contrib_intgemm_prepare_weight', aliases=('_npx_intgemm_prepare_weight',), arg_names=_pw_args,
+          params={'already_quantized': ('bool', False)})
+def intgemm_prepare_weight(weight, maxabs=None, already_quantized=False):
+    if already_quantized:
+        if weight.dtype != torch.int8:
+            raise ValueError('intgemm_prepare_weight: already_quantized weight must be int8')
+        return torch.clamp(weight, -127, 127).contiguous()
+    return _intgemm_quant(weight, maxabs).contiguous()
+
+
+@register('_contrib_intgemm_take_weight', aliases=('_npx_intgemm_take_weight',), arg_names=('weight', 'indices'))
+def intgemm_take_weight(weight, indices):
+    return weight[indices.to(torch.int64)].contiguous()
+
+
+def _ifc_args(a):
+    names = ['data', 'weight']
+    if str(a.get('out_type', 'float32')) == 'float32':
+        names.append('scaling')
+    if not (str(a.get('no_bias', False)) in ('True', 'true', '1')):
+        names.append('bias')
+    return names
+
+
+@register('_contrib_intgemm_fully_connected', aliases=('_npx_intgemm_fully_connected',), arg_names=_ifc_args,
+          params={'num_hidden': ('int', 1), 'no_bias': ('bool', False), 'flatten': ('bool', True),
+                  'out_type': ('str', 'float32')})
+def intgemm_fully_connected(data, weight, *rest, num_hidden=1, no_bias=False, flatten=True, out_type='float32'):
+    """C = data . weight^T on int8 operands (the gfx950 i8 MFMA GEMM on a GPU).  fp32 data is quantised on
+    the fly with its own max-abs (the scaling is divided by that scale); ``scaling`` multiplies the int32
+    result before the (unscaled) bias is added; out_type int32 skips the scaling."""
+    rest = list(rest)
+    scaling = rest.pop(0) if out_type == 'float32' else None
+    bias = None if no_bias else rest.pop(0)
+    x = data.reshape(data.shape[0], -1) if flatten else data
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, x.shape[-1])
+    mult = None
+    if x2.dtype != torch.int8:
+        m = x2.float().abs().max()
+        x2 = _intgemm_quant(x2, m.reshape(1))
+        mult = m / INT8_MAX
+    acc = _int8_matmul(x2, weight.reshape(weight.shape[0], -1))
+    if out_type == 'int32':
+        out = acc
+        if bias is not None:
+            out = out + bias.to(torch.int32)
+    else:
+        s = _range_scalar(scaling)
+        if mult is not None:
+            s = s * mult
+        out = acc.double() * s.double()
+        if bias is not None:
+            out = out + bias.double()
+        out = out.float()
+    return out.reshape(*lead, weight.shape[0])

@@ -25,6 +25,10 @@ void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, c
                       const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R, int C,
                       int relu_mode, int fix_gamma, int training, int accum, hipStream_t s, int ext_nblk);
 int bn_partials_rows(int64_t R, int C);
+void gemm_nt(int dtype, const void* a, const void* b, const float* bias, const void* addend, void* c, int out_f32,
+             int M, int N, int K, int lda, int ldb, int ldc, int act, int cfg, int splits, float* ws, hipStream_t s);
+int gemm_nt_tile_n(int cfg);
+int gemm_nt_tile_m(int cfg);
 void int8_gemm(const int8_t* A, const int8_t* B, int32_t* C, int M, int N, int K, hipStream_t s);
 void csr_dot_dense(int dtype, const int64_t* indptr, const int64_t* indices, const void* vals, const void* rhs,
                    void* out, int64_t M, int64_t K, int N, hipStream_t s);
@@ -184,6 +188,15 @@ PYBIND11_MODULE(_hip_kernels, m) {
     twobit_dequantize_sum(P<void>(packed), row_bytes, nrows, n, thr, P<float>(out), S(s));
     check_launch("twobit_dequantize_sum");
   });
+  m.def("gemm_nt", [](int dt, uintptr_t a, uintptr_t b, uintptr_t bias, uintptr_t addend, uintptr_t c, int out_f32,
+                      int M, int N, int K, int lda, int ldb, int ldc, int act, int cfg, int splits, uintptr_t ws,
+                      uintptr_t s) {
+    gemm_nt(dt, P<void>(a), P<void>(b), P<float>(bias), P<void>(addend), P<void>(c), out_f32, M, N, K, lda, ldb, ldc,
+            act, cfg, splits, P<float>(ws), S(s));
+    check_launch("gemm_nt");
+  });
+  m.def("gemm_nt_tile_n", &gemm_nt_tile_n);
+  m.def("gemm_nt_tile_m", &gemm_nt_tile_m);
   m.def("slab_reduce", [](int odt, uintptr_t slab, int splits, int64_t n, uintptr_t out, int accum, uintptr_t s) {
     slab_reduce(odt, P<float>(slab), splits, n, P<void>(out), accum, S(s));
     check_launch("slab_reduce");

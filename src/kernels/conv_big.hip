@@ -281,7 +281,8 @@ __global__ void __launch_bounds__(512) conv_fwd_big_kernel(const T* __restrict__
   // whole pixel rows: BCO*2 bytes = BCO/8 16-byte chunks per pixel
   constexpr int CPR = BCO / 8;
   constexpr int TOTAL = BPIX * CPR;
-  static_assert(512 % CPR == 0, "each thread keeps one 8-channel group");
+  constexpr int ITERS = TOTAL / 512;
+  static_assert(512 % CPR == 0 && TOTAL % 512 == 0, "each thread keeps one 8-channel group");
   const bool bnb = bf.part != nullptr;
   // BN-backward statistics: this thread's channel group is fixed (tid % CPR)
   float s1[8], s2[8], bm[8], bsc[8], bsh[8];
@@ -299,26 +300,56 @@ __global__ void __launch_bounds__(512) conv_fwd_big_kernel(const T* __restrict__
       bsh[t] = bf.mode == 2 ? bf.shift[cb + t] : 0.f;
     }
   }
-#pragma unroll 4
-  for (int e = tid; e < TOTAL; e += 512) {
+  // The addend / BN input z rows this thread reads are streamed through a register ring D
+  // iterations deep: all loads of the first D rows are in flight before the first store, and row
+  // e + D is requested as row e retires -- instead of one latency-bound load per row.
+  constexpr int D = ITERS < 8 ? ITERS : 8;
+  const T* zsrc_b = static_cast<const T*>(bf.z);
+  uint4 ad_ring[D], z_ring[D];
+  auto row_off = [&](int it, int64_t* off) -> bool {
+    const int e = tid + it * 512;
     const int pl = e / CPR;
     const int c8 = e - pl * CPR;
     const int p = pix0 + pl;
-    if (p < g.M) {
-      const int64_t off = (int64_t)p * g.K + co0 + c8 * 8;
+    *off = (int64_t)p * g.K + co0 + c8 * 8;
+    return p < g.M;
+  };
+#pragma unroll
+  for (int it = 0; it < D; ++it) {
+    int64_t off;
+    const bool ok = row_off(it, &off);
+    if (addend != nullptr && ok) ad_ring[it] = *reinterpret_cast<const uint4*>(addend + off);
+    if (bnb && ok) z_ring[it] = *reinterpret_cast<const uint4*>(zsrc_b + off);
+  }
+#pragma unroll
+  for (int it = 0; it < ITERS; ++it) {
+    const int e = tid + it * 512;
+    const int pl = e / CPR;
+    const int c8 = e - pl * CPR;
+    const int p = pix0 + pl;
+    int64_t off;
+    const bool ok = row_off(it, &off);
+    uint4 ad_cur = ad_ring[it % D], z_cur = z_ring[it % D];
+    if (it + D < ITERS) {
+      int64_t off2;
+      const bool ok2 = row_off(it + D, &off2);
+      if (addend != nullptr && ok2) ad_ring[it % D] = *reinterpret_cast<const uint4*>(addend + off2);
+      if (bnb && ok2) z_ring[it % D] = *reinterpret_cast<const uint4*>(zsrc_b + off2);
+    }
+    if (ok) {
       Vec8<T> v;
       v.raw = *reinterpret_cast<const uint4*>(smem + pl * PITCH + c8 * 16);
       if (addend != nullptr) {
         // y = conv + addend (beta = 1): e.g. the identity shortcut's gradient folded into a 1x1 dgrad
         Vec8<T> a;
-        a.load(addend + off);
+        a.raw = ad_cur;
 #pragma unroll
         for (int t = 0; t < 8; ++t) v.set(t, v.get(t) + a.get(t));
       }
       v.store(y + off);
       if (bnb) {
         Vec8<T> zv;
-        zv.load(static_cast<const T*>(bf.z) + off);
+        zv.raw = z_cur;
         const uint32_t mb = bf.mode == 3 ? bf.mask[off >> 3] : 0xffu;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
@@ -332,6 +363,7 @@ __global__ void __launch_bounds__(512) conv_fwd_big_kernel(const T* __restrict__
         }
       }
     }
+    (void)p;
   }
   if (bnb) {
     // combine the 512/CPR threads of each channel group through LDS, one partial per pixel tile

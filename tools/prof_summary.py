@@ -8,8 +8,8 @@ import sys
 
 def classify(name):
     n = name.lower()
-    if ('mxamd::' in n and 'conv' in n) or 'wgrad_reduce' in n:
-        return 'conv (in-tree HIP MFMA)'
+    if ('mxamd::' in n and ('conv' in n or 'gemm' in n or 'slab_reduce' in n)) or 'wgrad_reduce' in n:
+        return 'conv/gemm (in-tree HIP MFMA)'
     if 'igemm' in n or 'conv' in n or 'gemm' in n or 'ck::' in n or 'xdl' in n or 'cijk' in n:
         return 'conv/gemm (MIOpen/hipBLASLt)'
     if 'attn' in n or 'fmha' in n or 'flash' in n or 'attention' in n:
