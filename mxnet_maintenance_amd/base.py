@@ -164,3 +164,89 @@ class _NullType:
 
 
 _Null = _NullType()
+
+
+# ----------------------------------------------------------------------------------------------
+# C-API shim: the reference's tests drive a few graph-partitioning entry points through ctypes
+# (``check_call(_LIB.MXBuildSubgraphByOpNames(sym.handle, c_str(b), mx_uint(n), c_str_array(names),
+# ctypes.byref(out)))`` then ``Symbol(out)``).  ``_LIB`` implements those functions in Python over
+# symbol/subgraph.py; handles are ctypes.c_void_p values naming objects in a handle table.
+# ----------------------------------------------------------------------------------------------
+import ctypes as _ctypes
+
+SymbolHandle = _ctypes.c_void_p
+NDArrayHandle = _ctypes.c_void_p
+ExecutorHandle = _ctypes.c_void_p
+_HANDLES = {}
+
+
+def c_str(string):
+    return _ctypes.c_char_p(string.encode('utf-8'))
+
+
+def c_str_array(strings):
+    arr = (_ctypes.c_char_p * len(strings))()
+    arr[:] = [s.encode('utf-8') for s in strings]
+    return arr
+
+
+def c_array(ctype, values):
+    return (ctype * len(values))(*values)
+
+
+def _new_handle(obj):
+    key = id(obj)
+    _HANDLES[key] = obj
+    return key
+
+
+def _handle_object(h):
+    v = h.value if isinstance(h, _ctypes.c_void_p) else h
+    if v not in _HANDLES:
+        raise MXNetError('invalid handle')
+    return _HANDLES[v]
+
+
+def _cstr(v):
+    if isinstance(v, _ctypes.c_char_p):
+        v = v.value
+    return v.decode('utf-8') if isinstance(v, bytes) else str(v)
+
+
+def _names(n, arr):
+    return [_cstr(arr[i]) for i in range(int(n))]
+
+
+class _CAPI:
+    """The subset of the reference's libmxnet C API its Python tests call through ctypes."""
+
+    @staticmethod
+    def MXBuildSubgraphByOpNames(sym, backend, n, names, out):  # noqa: N802
+        from .symbol import subgraph
+        part = subgraph.partition(sym, _names(n, names))
+        target = out._obj if hasattr(out, '_obj') else out
+        target.value = _new_handle(part)
+        return 0
+
+    @staticmethod
+    def MXSetSubgraphPropertyOpNames(backend, n, names):  # noqa: N802
+        from .symbol import subgraph
+        subgraph.set_backend_op_names(_cstr(backend), _names(n, names))
+        return 0
+
+    MXSetSubgraphPropertyOpNamesV2 = MXSetSubgraphPropertyOpNames
+
+    @staticmethod
+    def MXRemoveSubgraphPropertyOpNames(backend):  # noqa: N802
+        from .symbol import subgraph
+        subgraph.remove_backend(_cstr(backend))
+        return 0
+
+    MXRemoveSubgraphPropertyOpNamesV2 = MXRemoveSubgraphPropertyOpNames
+
+    @staticmethod
+    def MXNotifyShutdown():  # noqa: N802
+        return 0
+
+
+_LIB = _CAPI()

@@ -121,9 +121,13 @@ class Executor:
 
     def __init__(self, sym, ctx, args, args_grad=None, grad_req='write', aux_states=None):
         from .ndarray.ndarray import NDArray
+        from .symbol import passes as _passes
         self._symbol = sym
         self._ctx = ctx
-        self._prog = GraphProgram(sym)
+        # bind-time graph passes (common-subexpression elimination, pointwise fusion); argument /
+        # output names and order are those of ``sym``
+        self._opt_symbol = _passes.optimize(sym, ctx)
+        self._prog = GraphProgram(self._opt_symbol)
         arg_names = sym.list_arguments()
         aux_names = sym.list_auxiliary_states()
         if isinstance(args, dict):
@@ -159,11 +163,36 @@ class Executor:
             self.aux_arrays = list(aux_states)
         if len(self.aux_arrays) != len(aux_names):
             raise MXNetError('bind: expected %d aux states, got %d' % (len(aux_names), len(self.aux_arrays)))
+        self._check_differentiable()
         self.outputs = self._preallocate_outputs()
         self._leaves = None
         self._out_tensors = None
         self._monitor_cb = None
         self._monitor_all = False
+
+    # operators the reference registers without FGradient: binding for a gradient through them fails
+    _NO_GRADIENT = ('batch_take',)
+
+    def _check_differentiable(self):
+        from .symbol import passes as _passes
+        wanting = {n for n, r in self._grad_req.items() if r != 'null'}
+        if not wanting:
+            return
+        order = self._symbol._topo()
+        live = {id(n) for n, _ in self._symbol._outputs}
+        for n in reversed(order):
+            if id(n) not in live or n.op is None:
+                continue
+            name = n.opdef().name
+            if name == 'BlockGrad':
+                continue
+            if name in self._NO_GRADIENT:
+                from .symbol.symbol import Symbol
+                if _passes.grad_reachable(Symbol([(n, 0)]), wanting):
+                    raise MXNetError('Operator %s is non-differentiable because it didn\'t register '
+                                     'FGradient attribute.' % name)
+            for a, _ in n.inputs:
+                live.add(id(a))
 
     def _preallocate_outputs(self):
         """Output arrays allocated at bind time (as the reference's graph executor does), so
@@ -373,5 +402,17 @@ class Executor:
         exe._monitor_cb, exe._monitor_all = self._monitor_cb, self._monitor_all
         return exe
 
+    def get_optimized_symbol(self):
+        """The graph this executor runs, after its bind-time passes."""
+        return self._opt_symbol
+
     def debug_str(self):
-        return self._symbol.debug_str()
+        """The optimized graph plus the intermediate-storage plan ('Total N MB allocated')."""
+        from .symbol import passes as _passes
+        names = self._symbol.list_arguments()
+        wanting = [n for n in names if self._grad_req.get(n, 'null') != 'null']
+        grad = bool(_passes.grad_reachable(self._opt_symbol, set(wanting)))
+        shapes = {n: a.shape for n, a in zip(names, self.arg_arrays)}
+        dtypes = {n: a.dtype for n, a in zip(names, self.arg_arrays)}
+        nbytes = _passes.memory_plan(self._opt_symbol, shapes, dtypes, grad)
+        return '%s\nTotal %d MB allocated\n' % (self._opt_symbol.debug_str(), nbytes // (1 << 20))

@@ -7,4 +7,4 @@ def load_all():
     if _loaded:
         return
     _loaded = True
-    from . import tensor, nn, optimizer_ops, misc_ops, detection, quantization_ops, contrib_ops, control_flow, np_ops, transformer_ops, extra_ops, pdf_ops  # noqa: F401
+    from . import tensor, nn, optimizer_ops, misc_ops, detection, quantization_ops, contrib_ops, control_flow, np_ops, transformer_ops, extra_ops, pdf_ops, fused_ops  # noqa: F401

@@ -30,3 +30,4 @@ def __getattr__(name):
         globals()[name] = fn
         return fn
     raise AttributeError("module 'mxnet_maintenance_amd.symbol' has no attribute '%s'" % name)
+from . import subgraph, passes  # noqa: E402,F401  (registers _CachedOp)

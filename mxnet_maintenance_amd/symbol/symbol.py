@@ -89,6 +89,12 @@ def _aux_var_ids(order):
     for n in order:
         if n.op is None:
             continue
+        if n.op == '_CachedOp':
+            # a partitioned subgraph keeps its auxiliary inputs at their original positions
+            for i in (int(x) for x in n.attrs.get('aux_indices', '').split(',') if x != ''):
+                if i < len(n.inputs) and n.inputs[i][0].op is None:
+                    aux.add(id(n.inputs[i][0]))
+            continue
         op = n.opdef()
         nargs = len(op.get_arg_names(n.parsed()))
         for i, (inp, _) in enumerate(n.inputs):
@@ -113,6 +119,11 @@ class Symbol:
     __array_priority__ = 1000.0
 
     def __init__(self, outputs):
+        import ctypes
+        if isinstance(outputs, ctypes.c_void_p):
+            # a handle filled in by the C-API shim (base._LIB), e.g. MXBuildSubgraphByOpNames
+            from ..base import _handle_object
+            outputs = _handle_object(outputs)._outputs
         self._outputs = list(outputs)
 
     # ------------------------------------------------------------ structure
@@ -211,6 +222,17 @@ class Symbol:
             for i in range(k):
                 outs.append((n, i))
         return Symbol(outs)
+
+    def _gen_atomic_symbol(self):
+        """A fresh single-node symbol with this (single-node) symbol's operator and attributes and new
+        variables for its inputs (reference symbol.py _gen_atomic_symbol)."""
+        node = self._outputs[0][0]
+        if node.op is None:
+            return Symbol([(_Node(None, node.name, dict(node.attrs)), 0)])
+        attrs = {k: v for k, v in node.attrs.items()}
+        fresh = _Node(node.op, node.name, attrs, [(_Node(None, '%s_in%d' % (node.name, i)), 0)
+                                                  for i in range(len(node.inputs))])
+        return Symbol([(fresh, i) for i in range(fresh.num_visible_outputs())])
 
     def get_children(self):
         """Inputs of every output node, in order (None when there are none: variables)."""
@@ -365,6 +387,8 @@ class Symbol:
                     'broadcast_to', 'broadcast_like', 'reshape_like', 'zeros_like', 'ones_like',
                     'slice', 'swapaxes', 'diag'):
             opname = {'reshape': 'Reshape', 'flatten': 'Flatten', 'astype': 'Cast', 'split': 'SliceChannel'}.get(name, name)
+            if name != 'astype' and registry.has(name) and registry.get(name) is registry.get(opname):
+                opname = name      # the alias the method is named after also names the node (split0)
 
             def f(*a, **k):
                 if name == 'reshape' and a:
@@ -456,7 +480,8 @@ class Symbol:
     def bind(self, ctx, args, args_grad=None, grad_req='write', aux_states=None, group2ctx=None,
              shared_exec=None):
         from ..executor import Executor
-        return Executor(self, ctx, args, args_grad, grad_req, aux_states)
+        from . import subgraph
+        return Executor(subgraph.env_partition(self), ctx, args, args_grad, grad_req, aux_states)
 
     def _bind(self, *a, **k):
         return self.bind(*a, **k)
@@ -492,7 +517,8 @@ class Symbol:
         grads = {n: nd.zeros(s, ctx=ctx, dtype=t or np.float32)
                  for n, s, t in zip(arg_names, arg_shapes, arg_types) if reqs.get(n, 'null') != 'null'}
         aux = [nd.zeros(s, ctx=ctx, dtype=t or np.float32) for s, t in zip(aux_shapes, aux_types)]
-        return Executor(self, ctx, args, grads, reqs, aux)
+        from . import subgraph
+        return Executor(subgraph.env_partition(self), ctx, args, grads, reqs, aux)
 
     def eval(self, ctx=None, **kwargs):
         from ..context import current_context
@@ -514,7 +540,11 @@ class Symbol:
         return '\n'.join(lines)
 
     def optimize_for(self, backend, args=None, aux=None, ctx=None, **kwargs):
-        return self
+        """Partition for a subgraph backend whose operator names were registered
+        (MXSetSubgraphPropertyOpNames[V2]); the graph is returned unchanged for unknown backends.
+        ``args`` / ``aux`` (shapes/dtypes source) and options such as ``dedup_subgraph`` are accepted."""
+        from . import subgraph
+        return subgraph.partition_for_backend(self, backend)
 
     def get_backend_symbol(self, backend):
         return self
@@ -527,7 +557,9 @@ class Symbol:
 def _create(op_name, inputs, attrs, name=None, attr=None):
     """Create a Symbol applying ``op_name`` to input Symbols (missing args become variables)."""
     op = registry.get(op_name)
-    hint = op.name.lower()
+    # the default node name follows the name the operator was called by (an alias such as flip
+    # names its node flip0, as the reference's generated functions do)
+    hint = (op_name if op_name.lower().lstrip('_') else op.name).lower()
     name = NameManager.current().get(name, hint)
     scope_attr = AttrScope.current().get(attr)
     node_attrs = {}
@@ -772,7 +804,11 @@ _SAME_SHAPE = frozenset(['elemwise_add', 'elemwise_sub', 'elemwise_mul', 'elemwi
                          '_minus', '_mul', '_div', '_add', '_sub', 'add_n', 'ElementWiseSum', '_maximum', '_minimum',
                          '_power', '_hypot', 'Activation', 'relu', 'sigmoid', 'tanh', 'softsign', 'Dropout',
                          'BlockGrad', 'stop_gradient', 'identity', '_copy', 'make_loss', 'MakeLoss', 'negative',
-                         'abs', 'exp', 'log', 'sqrt', 'square'])
+                         'abs', 'exp', 'log', 'sqrt', 'square', 'sin', 'cos', 'tan', 'arcsin', 'arccos',
+                         'arctan', 'sinh', 'cosh', 'arcsinh', 'arccosh', 'arctanh', 'degrees', 'radians',
+                         'expm1', 'log1p', 'log2', 'log10', 'rsqrt', 'cbrt', 'rcbrt', 'reciprocal', 'sign',
+                         'round', 'rint', 'ceil', 'floor', 'trunc', 'fix', 'erf', 'erfinv', 'gamma', 'gammaln',
+                         'LeakyReLU', 'softrelu', 'clip', 'zeros_like', 'ones_like', '_FusedOp'])
 
 _INIT_OPS = ('_zeros', '_ones', '_full', '_empty', 'zeros', 'ones', 'full')
 
@@ -830,6 +866,49 @@ def _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what):
     return None
 
 
+def _subgraph_same_shape(node):
+    from .subgraph import same_shape
+    return same_shape(node)
+
+
+def _partial_zero_dims(order, shape):
+    """Partial inference with unknown (0) dims: a variable declared with some 0 dims keeps that
+    partial shape, shape-preserving ops (casts, copies) pass it on, and operators with parameter
+    inference size their parameters from it (unknown dims stay 0), as nnvm's partial InferShape does."""
+    def back_fill(a, j, s):
+        while True:
+            if (id(a), j) not in shape:
+                shape[(id(a), j)] = s
+            if a.op in _SHAPE_PRESERVING and a.inputs:
+                a, j = a.inputs[0]
+                continue
+            return
+    for n in order:
+        if n.op is None:
+            if (id(n), 0) not in shape and n.attrs.get('__shape__'):
+                t = registry.parse_value('shape', n.attrs['__shape__'])
+                if t and any(int(d) == 0 for d in t):
+                    shape[(id(n), 0)] = tuple(int(d) for d in t)
+            continue
+        if n.op in _SHAPE_PRESERVING and n.inputs and (id(n), 0) not in shape:
+            src = shape.get((id(n.inputs[0][0]), n.inputs[0][1]))
+            if src is not None:
+                shape[(id(n), 0)] = src
+            continue
+        op = n.opdef()
+        in_shapes = [shape.get((id(a), j)) for a, j in n.inputs]
+        if op.infer_params is None or not in_shapes or in_shapes[0] is None or all(in_shapes):
+            continue
+        try:
+            fill = op.infer_params(in_shapes, n.parsed())
+        except Exception:   # pylint: disable=broad-except
+            continue
+        for idx, s in fill.items():
+            if idx < len(n.inputs) and in_shapes[idx] is None:
+                a, j = n.inputs[idx]
+                back_fill(a, j, tuple(int(d) for d in s))
+
+
 def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True, partial=False):
     """Propagate shapes and dtypes through the graph.
 
@@ -863,7 +942,8 @@ def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True, pa
             op = n.opdef()
             parsed = n.parsed()
             in_shapes = [shape.get((id(a), j)) for a, j in n.inputs]
-            if any(s is None for s in in_shapes) and op.infer_params is not None and in_shapes and in_shapes[0] is not None:
+            if (any(s is None for s in in_shapes) and op.infer_params is not None and in_shapes
+                    and (in_shapes[0] is not None or (n.op == '_CachedOp' and any(in_shapes)))):
                 try:
                     fill = op.infer_params(in_shapes, parsed)
                 except Exception:
@@ -881,7 +961,8 @@ def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True, pa
                             if (id(a), j) in shape:
                                 break
                             shape[(id(a), j)] = tuple(s)
-            if any(s is None for s in in_shapes) and n.op in _SAME_SHAPE:
+            if any(s is None for s in in_shapes) and (n.op in _SAME_SHAPE or (
+                    n.op == '_CachedOp' and _subgraph_same_shape(n))):
                 # elementwise ops (nnvm ElemwiseShape): every input and output has one shape, so a
                 # known one fills the others (backward inference into unknown producers)
                 ref = next((s for s in in_shapes + [shape.get((id(n), 0))] if s is not None), None)
@@ -946,6 +1027,8 @@ def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True, pa
                 ops = consumers.get(id(n), [])
                 if ops and all(o in ('Cast', 'cast', 'amp_cast', 'amp_multicast') for o in ops):
                     dtype[(id(n), 0)] = torch.float32
+    if what == 'shape' and partial:
+        _partial_zero_dims(order, shape)
     aux = _aux_var_ids(order)
     table = shape if what == 'shape' else dtype
     args = [table.get((id(n), 0)) for n in order if n.op is None and id(n) not in aux]

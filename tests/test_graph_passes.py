@@ -1,0 +1,154 @@
+"""Bind-time graph passes (symbol/passes.py): common-subexpression elimination, pointwise fusion into
+generated gfx950 kernels, the executor memory plan, partial shape inference with unknown dims."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import mxnet_maintenance_amd as mx
+from mxnet_maintenance_amd.symbol import passes
+
+
+def _nodes(sym):
+    return len(sym.get_internals().list_outputs())
+
+
+def test_cse_merges_identical_subexpressions():
+    a, b, c = mx.sym.Variable('a'), mx.sym.Variable('b'), mx.sym.Variable('c')
+    assert _nodes(passes.eliminate_common_expr((a + 1) + (a + 2))) == _nodes((a + 1) + (a + 2))
+    s = ((a + b) + c) + ((a + b) + c)
+    assert _nodes(s) - _nodes(passes.eliminate_common_expr(s)) == 2
+    d = a + 1
+    g = mx.sym.Group([a * d, a * d])
+    opt = passes.eliminate_common_expr(g)
+    assert _nodes(opt) == _nodes(g)               # merged, then a copy isolates the two outputs
+    assert len(opt.list_outputs()) == 2
+
+
+def test_cse_keeps_random_ops_apart():
+    a = mx.sym.Variable('a')
+    s = mx.sym.Dropout(a, p=0.5) + mx.sym.Dropout(a, p=0.5)
+    assert _nodes(passes.eliminate_common_expr(s)) == _nodes(s)
+
+
+def test_executor_cse_matches_unoptimised():
+    a, b = mx.sym.Variable('a'), mx.sym.Variable('b')
+    s = mx.sym.exp(a * b) + mx.sym.exp(a * b)
+    args = {'a': mx.nd.array(np.random.rand(3, 4)), 'b': mx.nd.array(np.random.rand(3, 4))}
+    ex = s.bind(mx.cpu(), args, args_grad={k: mx.nd.zeros((3, 4)) for k in args})
+    out = ex.forward(is_train=True)[0].asnumpy()
+    ex.backward(mx.nd.ones((3, 4)))
+    ref = 2 * np.exp(args['a'].asnumpy() * args['b'].asnumpy())
+    np.testing.assert_allclose(out, ref, rtol=1e-5)
+    np.testing.assert_allclose(ex.grad_dict['a'].asnumpy(), ref * args['b'].asnumpy(), rtol=1e-5)
+    assert _nodes(ex.get_optimized_symbol()) < _nodes(s)
+
+
+def test_fusion_pass_groups_chains_and_preserves_values():
+    a, b = mx.sym.Variable('a'), mx.sym.Variable('b')
+    y = mx.sym.sigmoid(mx.sym.relu(a * b + 1.5) * 2 - b) / 3
+    f = passes.fuse_pointwise(y)
+    ops = [n.op for n in f._topo() if n.op is not None]
+    assert ops == ['_FusedOp']
+    assert f.list_arguments() == y.list_arguments()
+    vals = {'a': mx.nd.array(np.random.randn(5, 6)), 'b': mx.nd.array(np.random.randn(5, 6))}
+    np.testing.assert_allclose(f.bind(mx.cpu(), vals).forward()[0].asnumpy(),
+                               y.bind(mx.cpu(), vals).forward()[0].asnumpy(), rtol=1e-6)
+
+
+def test_fusion_stops_at_shared_intermediates():
+    a = mx.sym.Variable('a')
+    t = mx.sym.exp(a) * 2
+    y = mx.sym.Group([mx.sym.relu(t) + 1, t])     # t is consumed twice: it must stay materialised
+    f = passes.fuse_pointwise(y)
+    np.testing.assert_allclose(
+        f.bind(mx.cpu(), {'a': mx.nd.ones((2, 2))}).forward()[1].asnumpy(), np.full((2, 2), 2 * np.e), rtol=1e-6)
+
+
+def test_generated_kernel_source_compiles_for_gfx950():
+    import torch
+    from mxnet_maintenance_amd.ops import fused_ops
+    from mxnet_maintenance_amd import rtc
+    a, b = mx.sym.Variable('a'), mx.sym.Variable('b')
+    f = passes.fuse_pointwise(mx.sym.tanh(a - b) * mx.sym.sqrt(mx.sym.abs(b)))
+    g = json.loads(f._outputs[0][0].attrs['subgraph'])
+    src = fused_ops.kernel_source(g, torch.bfloat16)
+    assert 'fused_pointwise' in src and 'tanhf' in src
+    if os.path.exists('/opt/rocm/bin/hipcc'):
+        assert os.path.exists(rtc.compile_source(src))
+
+
+def test_debug_str_memory_plan_zero_prop():
+    import re
+    data = mx.sym.Variable('data')
+    for _ in range(4):
+        data = data * data
+    big = data.simple_bind(mx.cpu(), data=(4, 3, 64, 64))
+    small1 = data.simple_bind(mx.cpu(), data=(4, 3, 64, 64), grad_req='null')
+    small2 = mx.sym.stop_gradient(data).simple_bind(mx.cpu(), data=(4, 3, 64, 64))
+    mb = lambda e: int(re.search(r'Total (\d+) MB allocated', e.debug_str()).group(1))  # noqa: E731
+    assert mb(big) > mb(small2) and mb(small1) == mb(small2)
+
+
+def test_partial_shape_with_unknown_dims():
+    data = mx.sym.Variable('data', shape=(1, 0, 0, 0))
+    w = mx.sym.Variable('weight')
+    conv = mx.sym.Convolution(data=mx.sym.cast(data, dtype='float16'), weight=mx.sym.cast(w, dtype='float16'),
+                              pad=(3, 3), num_filter=64, stride=(2, 2), no_bias=True, kernel=(7, 7))
+    arg, _, _ = conv.infer_shape_partial()
+    shapes = dict(zip(conv.list_arguments(), arg))
+    assert shapes['data'] == (1, 0, 0, 0) and shapes['weight'] == (64, 0, 7, 7)
+
+
+@pytest.mark.gpu
+def test_fused_kernel_runs_on_gpu_and_matches():
+    import torch
+    from mxnet_maintenance_amd.ops import fused_ops
+    a, b = mx.sym.Variable('a'), mx.sym.Variable('b')
+    y = mx.sym.sigmoid(mx.sym.relu(a * b + 1.5) * 2 - b) / 3
+    for dt in ('float32', 'float16', 'bfloat16'):
+        vals = {'a': mx.nd.array(np.random.randn(257, 129), ctx=mx.gpu(0)).astype(dt),
+                'b': mx.nd.array(np.random.randn(257, 129), ctx=mx.gpu(0)).astype(dt)}
+        ex = y.bind(mx.gpu(0), vals)
+        assert any(n.op == '_FusedOp' for n in ex.get_optimized_symbol()._topo())
+        out = ex.forward()[0].astype('float32').asnumpy()
+        av, bv = (vals[k].astype('float32').asnumpy() for k in ('a', 'b'))
+        ref = 1 / (1 + np.exp(-(np.maximum(av * bv + 1.5, 0) * 2 - bv))) / 3
+        tol = 1e-5 if dt == 'float32' else 2e-2
+        np.testing.assert_allclose(out, ref, rtol=tol, atol=tol)
+        tdt = getattr(torch, dt)
+        assert any(k[1] == tdt and v is not None for k, v in fused_ops._KERNELS.items()), 'HIP kernel not used'
+
+
+def test_subgraph_partition_keeps_io_and_values():
+    import ctypes
+    from mxnet_maintenance_amd.base import SymbolHandle, check_call, _LIB, mx_uint, c_str_array, c_str
+    from mxnet_maintenance_amd.symbol import Symbol
+    data = mx.sym.var('data', shape=(2, 3, 8, 8))
+    bn = mx.sym.BatchNorm(mx.sym.exp(data) + mx.sym.sin(data), name='bn')
+    y = mx.sym.Convolution(mx.sym.cos(bn), num_filter=4, kernel=(3, 3), name='conv')
+    out = SymbolHandle()
+    check_call(_LIB.MXBuildSubgraphByOpNames(y.handle, c_str('default'), mx_uint(4),
+                                              c_str_array(['exp', 'sin', 'elemwise_add', 'BatchNorm']),
+                                              ctypes.byref(out)))
+    part = Symbol(out)
+    assert any(n.op == '_CachedOp' for n in part._topo())
+    assert part.list_inputs() == y.list_inputs()
+    assert part.list_auxiliary_states() == y.list_auxiliary_states()
+    e1 = y.simple_bind(mx.cpu(), grad_req='null')
+    e2 = part.simple_bind(mx.cpu(), grad_req='null')
+    for name, arr in e1.arg_dict.items():
+        arr[:] = mx.nd.random.uniform(shape=arr.shape)
+        e2.arg_dict[name][:] = arr
+    for name, arr in e1.aux_dict.items():
+        arr[:] = mx.nd.random.uniform(shape=arr.shape) + 0.5
+        e2.aux_dict[name][:] = arr
+    np.testing.assert_allclose(e1.forward()[0].asnumpy(), e2.forward()[0].asnumpy(), rtol=1e-5, atol=1e-5)
+    # optimize_for with a registered backend partitions the same way
+    check_call(_LIB.MXSetSubgraphPropertyOpNamesV2(c_str('default'), mx_uint(1), c_str_array(['cos'])))
+    try:
+        assert any(n.op == '_CachedOp' for n in y.optimize_for('default')._topo())
+    finally:
+        check_call(_LIB.MXRemoveSubgraphPropertyOpNamesV2(c_str('default')))
+    assert not any(n.op == '_CachedOp' for n in y.optimize_for('default')._topo())
