@@ -59,7 +59,7 @@ class GraphProgram:
         self.nslots = nslots
         self.name_to_slot = dict(zip(self.var_names, self.var_slots))
 
-    def run(self, feed, monitor=None, monitor_all=False):
+    def run(self, feed, monitor=None, monitor_all=False, record=None):
         """``feed``: dict var name -> torch tensor.  Returns output tensors.
 
         ``monitor(name, tensor)`` is called for every operator output (and,
@@ -74,6 +74,8 @@ class GraphProgram:
             args = [vals[i] for i in ins]
             if _amp.active:
                 args = _amp.cast_inputs(opname, args, attrs)
+            if record is not None:
+                record.append((name, args))
             if monitor is not None and monitor_all:
                 for j, a in enumerate(args):
                     if a is not None:
@@ -262,8 +264,22 @@ class Executor:
 
                 def mon(name, t):
                     cb(name, NDArray(t.detach()))
+            record = [] if (mon is not None and need_grad) else None
             with torch.set_grad_enabled(need_grad):
-                outs = self._prog.run(feed, mon, self._monitor_all)
+                outs = self._prog.run(feed, mon, self._monitor_all, record)
+            self._mon_record = record
+            self._mon_grads = {}
+            if record:
+                # gradients flowing into every operator input, reported by backward() like the
+                # reference's monitor over the backward graph's nodes
+                for _name, args in record:
+                    for t in args:
+                        if isinstance(t, torch.Tensor) and t.requires_grad and id(t) not in self._mon_grads:
+                            self._mon_grads[id(t)] = None
+
+                            def hook(g, key=id(t)):
+                                self._mon_grads[key] = g.detach()
+                            t.register_hook(hook)
         finally:
             _state.STATE.training = prev_train
         self._leaves = leaves
@@ -325,6 +341,15 @@ class Executor:
             for n, buf in gd.items():
                 if n not in got and buf is not None and self._grad_req.get(n) == 'write':
                     buf._data.zero_()
+        record = getattr(self, '_mon_record', None)
+        if record and self._monitor_cb is not None:
+            for name, args in reversed(record):
+                for i, t in enumerate(args):
+                    if not isinstance(t, torch.Tensor):
+                        continue
+                    g = self._mon_grads.get(id(t))
+                    self._monitor_cb('%s_backward_in%d' % (name, i), NDArray(g if g is not None else torch.zeros_like(t)))
+            self._mon_record = None
         box = getattr(self, '_failure_box', None)
         if box is not None and box[0] is not None:
             # gradients of a failed forward carry its (shared) failure

@@ -467,7 +467,9 @@ class Perplexity(EvalMetric):
             if label.size != p.numel() // p.shape[-1]:
                 raise AssertionError('shape mismatch: %s vs. %s' % (label.shape, tuple(p.shape)))
             l = _dev(label).to(p.device).reshape(-1).to(torch.int64)
-            prob = p.reshape(-1, p.shape[-1]).float().gather(1, l.clamp(min=0).unsqueeze(1)).squeeze(1)
+            # pick() semantics of the reference (mode='clip'): out-of-range labels read the edge class
+            prob = p.reshape(-1, p.shape[-1]).float().gather(
+                1, l.clamp(min=0, max=p.shape[-1] - 1).unsqueeze(1)).squeeze(1)
             keep = torch.ones_like(prob, dtype=torch.bool) if self.ignore_label is None else l != self.ignore_label
             prob = torch.where(keep, prob, torch.ones_like(prob))
             nll -= float(torch.log(prob.clamp(min=1e-10)).sum())

@@ -51,7 +51,11 @@ class BucketingModule(BaseModule):
     _curr_bucket_key = property(lambda self: self._active_key)
 
     def _call_sym_gen(self, *args, **kwargs):
-        return self._sym_gen(*args, **kwargs)
+        # a fresh name scope per call: every bucket's graph names its auto-named nodes alike
+        # (embedding0_weight in each), so parameters are shared by name across buckets
+        from ..name import NameManager
+        with NameManager():
+            return self._sym_gen(*args, **kwargs)
 
     def _reset_bind(self):
         self.binded = False

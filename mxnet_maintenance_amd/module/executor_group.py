@@ -125,6 +125,11 @@ class DataParallelExecutorGroup:
         self.batch_size = None
         self.slices = None
         self.data_shapes = self.label_shapes = None
+        self.group2ctxs = group2ctxs
+        # per device: the non-parameter argument arrays (inputs, labels, states), shared by name
+        # with (and extended into) the shared group's, as the reference's executor group does
+        self.shared_data_arrays = (shared_group.shared_data_arrays if shared_group is not None
+                                   else [{} for _ in self.contexts])
         data_names = [d.name if isinstance(d, DataDesc) else d[0] for d in data_shapes]
         self.grad_req = _resolve_grad_req(grad_req, self.arg_names, self.param_names, data_names,
                                           self.fixed_param_names, inputs_need_grad, for_training)
@@ -174,8 +179,24 @@ class DataParallelExecutorGroup:
             if label_shapes is not None:
                 spec.update(self._shapes_for(label_shapes, self.label_layouts, sl))
             spec = {k: v for k, v in spec.items() if k in self.arg_names}
+            g2c = self.group2ctxs
+            if isinstance(g2c, (list, tuple)):
+                g2c = g2c[i] if i < len(g2c) else None
+            if isinstance(g2c, dict):
+                # a group maps to one context for every device or to a per-device list
+                g2c = {k: (v[i] if i < len(v) else v[-1]) if isinstance(v, (list, tuple)) else v
+                       for k, v in g2c.items()}
             exe = self.symbol.simple_bind(ctx, grad_req=self.grad_req, type_dict={k: v[1] for k, v in spec.items()},
-                                          **{k: v[0] for k, v in spec.items()})
+                                          group2ctx=g2c, **{k: v[0] for k, v in spec.items()})
+            shared = self.shared_data_arrays[i]
+            for j, name in enumerate(self.arg_names):
+                if name in self.param_names:
+                    continue
+                have = shared.get(name)
+                if have is not None and have.shape == exe.arg_arrays[j].shape and have.dtype == exe.arg_arrays[j].dtype:
+                    exe.arg_arrays[j] = have
+                else:
+                    shared[name] = exe.arg_arrays[j]
             donor = shared_group.execs[i] if shared_group is not None else \
                 (previous[i].exe if reshape and previous else None)
             if donor is not None:

@@ -84,7 +84,7 @@ class Module(BaseModule):
         mod._arg_params, mod._aux_params = args, auxs
         mod.params_initialized = True
         if load_optimizer_states:
-            mod._preload_opt_states = '%s-%04d.states' % (prefix, epoch)
+            mod._pending_opt_states = '%s-%04d.states' % (prefix, epoch)
         return mod
 
     def save_checkpoint(self, prefix, epoch, save_optimizer_states=False, remove_amp_cast=True):
@@ -221,7 +221,8 @@ class Module(BaseModule):
             self._group.set_params(self._arg_params, self._aux_params)    # loaded before bind
         else:
             g = self._group
-            self._arg_params = {n: nd.zeros(a[0].shape, dtype=a[0].dtype)
+            stypes = {n: v.attrs.get('__storage_type__') for n, v in self._symbol._var_nodes().items()}
+            self._arg_params = {n: nd.zeros(a[0].shape, dtype=a[0].dtype, stype=_stype_name(stypes.get(n)))
                                 for n, a in zip(self._param_names, g.param_arrays)}
             self._aux_params = {n: nd.zeros(a[0].shape, dtype=a[0].dtype)
                                 for n, a in zip(self._aux_names, g.aux_arrays)}
@@ -389,3 +390,11 @@ class Module(BaseModule):
                 warnings.warn("%s is not 'row_sparse'; no row_sparse_pull needed." % name, stacklevel=2)
                 continue
             self._kvstore.row_sparse_pull(name, per_dev, row_ids=row_id, priority=-idx)
+
+
+def _stype_name(flag):
+    """Storage type of a variable's ``__storage_type__`` attribute (stype flag or name)."""
+    if flag is None:
+        return 'default'
+    names = {'0': 'default', '1': 'row_sparse', '2': 'csr', '-1': 'default'}
+    return names.get(str(flag), str(flag) if str(flag) in ('default', 'row_sparse', 'csr') else 'default')

@@ -500,11 +500,18 @@ class Symbol:
             arg_types = [np.float32] * len(arg_names)
             aux_types = [np.float32] * len(aux_shapes)
         args = []
+        var_nodes = self._var_nodes()
+
+        def place(name):
+            # model parallelism: a variable created under AttrScope(ctx_group=g) lives on group2ctx[g]
+            va = var_nodes[name].attrs if name in var_nodes else {}
+            g = va.get('__ctx_group__', va.get('ctx_group'))
+            return group2ctx[g] if (group2ctx and g in group2ctx) else ctx
         for n, s, t in zip(arg_names, arg_shapes, arg_types):
             if shared_buffer is not None and n in shared_buffer and shared_buffer[n].shape == tuple(s):
                 args.append(shared_buffer[n])
             else:
-                a = nd.zeros(s, ctx=ctx, dtype=t or np.float32)
+                a = nd.zeros(s, ctx=place(n), dtype=t or np.float32)
                 if shared_buffer is not None:
                     shared_buffer[n] = a
                 args.append(a)
@@ -514,7 +521,7 @@ class Symbol:
             reqs = dict(zip(arg_names, grad_req))
         else:
             reqs = {n: grad_req.get(n, 'null') for n in arg_names}
-        grads = {n: nd.zeros(s, ctx=ctx, dtype=t or np.float32)
+        grads = {n: nd.zeros(s, ctx=place(n), dtype=t or np.float32)
                  for n, s, t in zip(arg_names, arg_shapes, arg_types) if reqs.get(n, 'null') != 'null'}
         aux = [nd.zeros(s, ctx=ctx, dtype=t or np.float32) for s, t in zip(aux_shapes, aux_types)]
         from . import subgraph
@@ -676,7 +683,8 @@ def var(name, attr=None, shape=None, lr_mult=None, wd_mult=None, dtype=None, ini
     for k, v in (attr or {}).items():
         attrs[k] = v
     if shape is not None:
-        attrs['__shape__'] = registry.format_value(tuple(shape))
+        attrs['__shape__'] = registry.format_value((shape,) if isinstance(shape, (int, np.integer))
+                                                   else tuple(shape))
     if lr_mult is not None:
         attrs['__lr_mult__'] = str(lr_mult)
     if wd_mult is not None:
