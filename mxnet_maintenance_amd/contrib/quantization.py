@@ -108,6 +108,19 @@ def quantize_graph(sym, excluded_sym_names=None, excluded_op_names=None, calib_r
             rq = _Node('_contrib_requantize', n.name + '_requantize', rattrs, [(qn, 0), (qn, 1), (qn, 2)])
             qmap[(id(n), 0)] = ((rq, 0), (rq, 1), (rq, 2))
             continue
+        if (n.op == 'BatchNorm' and quantize_mode == 'full' and n.name not in excluded
+                and n.op not in excluded_ops and n.num_visible_outputs() == 1):
+            # int8 BatchNorm (inference): quantized input, fp32 statistics, calibrated int8 output
+            data_q = quant_of(ins_fp[0], n.name + '_data')
+            attrs = {k: v for k, v in n.attrs.items() if not (k.startswith('__') and k.endswith('__'))}
+            rng = calib_ranges.get(_entry_name(n, 0))
+            if rng is not None:
+                attrs['min_calib_range'] = repr(float(rng[0]))
+                attrs['max_calib_range'] = repr(float(rng[1]))
+            qn = _Node('_contrib_quantized_batch_norm', 'quantized_' + n.name, attrs,
+                       [data_q[0]] + [fp32_of(e) for e in ins_fp[1:5]] + [data_q[1], data_q[2]])
+            qmap[(id(n), 0)] = ((qn, 0), (qn, 1), (qn, 2))
+            continue
         if passthrough:
             q, mn, mx = qmap[(id(ins_fp[0][0]), ins_fp[0][1])]
             attrs = {k: v for k, v in n.attrs.items() if not (k.startswith('__') and k.endswith('__'))}
@@ -201,6 +214,7 @@ def _smooth(p, eps=0.0001):
 def get_optimal_threshold(hist_data, quantized_dtype='int8', num_quantized_bins=255):
     """Threshold minimising KL(P || Q) between the clipped fp32 histogram P and its int8 quantisation Q."""
     hist, hist_edges, min_val, max_val, _ = hist_data
+    hist, hist_edges = np.asarray(hist), np.asarray(hist_edges)
     num_bins = len(hist)
     assert num_bins % 2 == 1
     if min_val >= 0 and quantized_dtype in ('auto', 'uint8'):
@@ -244,6 +258,29 @@ def get_optimal_threshold(hist_data, quantized_dtype='int8', num_quantized_bins=
     return float(best_th)
 
 
+def _smooth_distribution(p, eps=0.0001):
+    """Reference-named helper: move ``eps`` of mass onto the zero bins of a histogram (ValueError when
+    every bin is zero)."""
+    return _smooth(np.asarray(p), eps)
+
+
+def _get_optimal_threshold(hist_data, quantized_dtype, num_quantized_bins=255):
+    """(min, max, threshold, divergence) of the KL-optimal threshold (reference return layout)."""
+    th = get_optimal_threshold(hist_data, quantized_dtype, num_quantized_bins)
+    return hist_data[2], hist_data[3], th, None
+
+
+def _get_optimal_thresholds(hist_dict, quantized_dtype, num_quantized_bins=255, logger=None):
+    """{name: (-th, th)} for a dict of (hist, edges, min, max, th) histograms."""
+    out = {}
+    for name, hist in hist_dict.items():
+        th = get_optimal_threshold(hist, quantized_dtype, num_quantized_bins)
+        out[name] = (-th, th)
+        if logger is not None:
+            logger.debug('layer=%s, min_val=%f, max_val=%f, th=%f', name, hist[2], hist[3], th)
+    return out
+
+
 def calib_graph(qsym, arg_params, aux_params, collector=None, calib_mode='entropy', quantized_dtype='int8',
                 logger=logging):
     return qsym, arg_params, aux_params
@@ -264,7 +301,8 @@ def quantize_model(sym, arg_params, aux_params, data_names=('data',), label_name
         ranges = _collect_ranges(sym, arg_params, aux_params, calib_data, num_calib_examples, ctx,
                                  list(data_names), list(label_names or []), calib_mode)
         logger.info('Collected calibration ranges for %d tensors (%s)', len(ranges), calib_mode)
-    qsym = quantize_graph(sym, excluded_sym_names, excluded_op_names, ranges, quantized_dtype)
+    qsym = quantize_graph(sym, excluded_sym_names, excluded_op_names, ranges, quantized_dtype,
+                          quantize_mode=quantize_mode)
     return qsym, dict(arg_params), dict(aux_params)
 
 

@@ -109,3 +109,8 @@ def rand_zipfian(true_classes, num_sampled, range_max, ctx=None):
     expected_prob_sampled = ((sampled_cls_fp64 + 2.0) / (sampled_cls_fp64 + 1.0)).log() / log_range
     expected_count_sampled = expected_prob_sampled * num_sampled
     return sampled_classes, expected_count_true, expected_count_sampled
+
+
+# graph operators on CSR adjacency (src/operator/contrib/dgl_graph.cc), on the compressed storage
+from .dgl_graph import (dgl_csr_neighbor_uniform_sample, dgl_csr_neighbor_non_uniform_sample,  # noqa: E402,F401
+                        dgl_subgraph, edge_id, dgl_adjacency, dgl_graph_compact)

@@ -47,11 +47,17 @@ def run_one(ref, name, timeout, workers, select=None, tb=None):
         unit = os.path.join(tmp, 'unittest')
         os.makedirs(unit)
         # the whole unittest directory: test files import each other (test_module -> test_bucketing)
-        src_dir = os.path.join(ref, 'unittest')
-        for f in os.listdir(src_dir):
-            src = os.path.join(src_dir, f)
-            if os.path.isfile(src) and (f.endswith('.py') or f in ('legacy_ndarray.v0', 'save_000800.json')):
-                shutil.copy(src, unit)
+        src_dirs = [os.path.join(ref, 'unittest')]
+        if '/' in name:
+            # another reference test directory (e.g. quantization/test_quantization): its files on
+            # top of the unittest helpers it imports (common.py)
+            sub, name = name.split('/', 1)
+            src_dirs.append(os.path.join(ref, sub))
+        for src_dir in src_dirs:
+            for f in os.listdir(src_dir):
+                src = os.path.join(src_dir, f)
+                if os.path.isfile(src) and (f.endswith('.py') or f in ('legacy_ndarray.v0', 'save_000800.json')):
+                    shutil.copy(src, unit)
         if os.path.isdir(os.path.join(ref, 'common')):
             shutil.copytree(os.path.join(ref, 'common'), os.path.join(tmp, 'common'))
         env = dict(os.environ)
