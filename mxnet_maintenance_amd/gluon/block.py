@@ -101,6 +101,14 @@ class _NameScopeGuard:
 # spec to rebuild the nesting: 'x' one array, None a None, ('n', k) a k-output Symbol, or a list
 # of specs for a list / tuple.
 # ---------------------------------------------------------------------------------------------
+def _check_output_kinds(legacy_flags):
+    """A NumPy-mode block must not return legacy NDArrays next to mx.np arrays (reference
+    HybridBlock: 'mixed types of outputs')."""
+    from .. import _state as _st
+    if _st.STATE.np_array and any(legacy_flags) and not all(legacy_flags):
+        raise TypeError('Block outputs mix legacy NDArrays / Symbols with mx.np ndarrays')
+
+
 def _flatten(args, inout_str):
     if isinstance(args, NDArray):
         return [args], 'x'
@@ -535,6 +543,7 @@ class HybridBlock(Block):
             with self.name_scope():
                 out = self.hybrid_forward(symbol, *grouped_inputs, **params)
             out, self._out_format = _flatten(out, 'output')
+            _check_output_kinds([getattr(o, '_legacy', False) for o in out])
             self._cached_graph = symbol_inputs, symbol.Group(out)
         return self._cached_graph
 
@@ -729,7 +738,12 @@ class HybridBlock(Block):
             for _, v in self.params.items():
                 v._finish_deferred_init()
             params = {k: v.data(ctx) for k, v in self._reg_params.items()}
-        return self.hybrid_forward(ndarray, x, *args, **params)
+        res = self.hybrid_forward(ndarray, x, *args, **params)
+        if _state.STATE.np_array:
+            from ..numpy import ndarray as _np_ndarray
+            flat, _ = _flatten(res, 'output')
+            _check_output_kinds([isinstance(o, NDArray) and not isinstance(o, _np_ndarray) for o in flat])
+        return res
 
     def hybrid_forward(self, F, x, *args, **kwargs):
         raise NotImplementedError

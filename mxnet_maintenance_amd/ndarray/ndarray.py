@@ -647,6 +647,8 @@ def _convert_key(key):
     if isinstance(key, np.ndarray):
         return torch.as_tensor(key.astype(np.int64) if key.dtype.kind == 'f' else key)
     if isinstance(key, list):
+        if key and all(isinstance(k, (bool, np.bool_)) for k in key):
+            return torch.as_tensor(np.asarray(key, dtype=np.bool_))       # a boolean mask
         return torch.as_tensor(np.asarray(key, dtype=np.int64))
     if isinstance(key, tuple):
         return tuple(_convert_key(k) if isinstance(k, (NDArray, np.ndarray, list)) else

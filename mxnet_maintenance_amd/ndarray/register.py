@@ -19,11 +19,14 @@ _NP_CLS = [None]     # mx.np.ndarray, set when mx.numpy is imported
 
 
 def _np_wrap(inputs, outs):
-    """Outputs become mx.np.ndarray under npx.set_np() or when any input is one."""
+    """Outputs become mx.np.ndarray when any input is one (a legacy mx.nd operator on legacy arrays
+    returns legacy arrays even under npx.set_np(), as in the reference; input-less creation ops follow
+    the active mode)."""
     cls = _NP_CLS[0]
     if cls is None:
         return outs
-    if _state.STATE.np_array or any(x is not None and x.__class__ is cls for x in inputs):
+    has_inputs = any(x is not None for x in inputs)
+    if (_state.STATE.np_array and not has_inputs) or any(x is not None and x.__class__ is cls for x in inputs):
         for o in outs:
             if o.__class__ is NDArray:
                 o.__class__ = cls

@@ -84,7 +84,11 @@ def _write_str(f, s):
     f.write(b)
 
 
-def save_to_stream(f, data):
+def save_to_stream(f, data, np_shape=None):
+    if np_shape is None:
+        # NumPy-shape semantics (0-d arrays are scalars, 0-size dims are real): the V3 record
+        from ..util import is_np_shape
+        np_shape = is_np_shape()
     if isinstance(data, NDArray):
         data = [data]
     names = []
@@ -101,7 +105,7 @@ def save_to_stream(f, data):
     f.write(struct.pack('<QQ', LIST_MAGIC, 0))
     f.write(struct.pack('<Q', len(arrays)))
     for a in arrays:
-        _write_array(f, a)
+        _write_array(f, a, np_shape)
     f.write(struct.pack('<Q', len(names)))
     for n in names:
         if not isinstance(n, string_types):
@@ -109,16 +113,16 @@ def save_to_stream(f, data):
         _write_str(f, n)
 
 
-def save(fname, data):
-    """Save a list or a str->NDArray dict to ``fname`` (MXNet .params format)."""
+def save(fname, data, np_shape=None):
+    """Save a list or a str->NDArray dict to ``fname`` (MXNet .params format; V3 records under
+    NumPy-shape semantics)."""
     if isinstance(fname, str):
-        from .. import engine
         buf = io.BytesIO()
-        save_to_stream(buf, data)
+        save_to_stream(buf, data, np_shape)
         with open(fname, 'wb') as f:
             f.write(buf.getvalue())
     else:
-        save_to_stream(fname, data)
+        save_to_stream(fname, data, np_shape)
 
 
 class _Reader:

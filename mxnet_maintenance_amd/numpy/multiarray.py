@@ -224,7 +224,17 @@ class ndarray(NDArray):
         return _np_out(_reg.invoke_fn(lambda t: t.to(td) if t.dtype != td else t.clone(), [self]))
 
     def copy(self, order='C'):
+        if order != 'C':
+            raise NotImplementedError('ndarray.copy only supports order=\'C\', got %s' % order)
         return _np_out(_reg.invoke_fn(lambda t: t.clone(), [self]))
+
+    def __format__(self, spec):
+        # a 0-d array formats like its scalar; an n-d array takes only the empty format spec
+        if self.ndim == 0:
+            return format(self.item(), spec)
+        if spec:
+            raise TypeError('unsupported format string passed to ndarray.__format__')
+        return str(self.asnumpy())
 
     def detach(self):
         return ndarray(self._data.detach())
@@ -569,6 +579,8 @@ def ones(shape, dtype=None, order='C', ctx=None):
 
 @_export
 def empty(shape, dtype=None, order='C', ctx=None):
+    if order != 'C':
+        raise NotImplementedError('np.empty only supports order=\'C\', got %s' % order)
     return zeros(shape, dtype, order, ctx)
 
 

@@ -160,6 +160,8 @@ def multinomial(n, pvals, size=None):
     p = torch.as_tensor(pvals.asnumpy() if isinstance(pvals, NDArray) else onp.asarray(pvals), dtype=torch.float64)
     shp = _size(size) or ()
     cnt = int(onp.prod(shp)) if shp else 1
+    if p.numel() == 0 or cnt == 0:
+        return ndarray(torch.zeros(tuple(shp) + (p.numel(),), dtype=torch.int64))
     draws = torch.multinomial(p.expand(cnt, -1), n, replacement=True)
     counts = torch.zeros(cnt, p.numel(), dtype=torch.int64).scatter_add_(1, draws, torch.ones_like(draws))
     return ndarray(counts.reshape(tuple(shp) + (p.numel(),)))

@@ -104,7 +104,7 @@ def save(file, arr):
         arr = {k: v.as_nd_ndarray() if hasattr(v, 'as_nd_ndarray') else v for k, v in arr.items()}
     else:
         arr = [v.as_nd_ndarray() if hasattr(v, 'as_nd_ndarray') else v for v in arr]
-    _u.save(file, arr)
+    _u.save(file, arr, np_shape=True)
 
 
 def load(file):

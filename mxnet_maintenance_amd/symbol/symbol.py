@@ -208,11 +208,17 @@ class Symbol:
 
     def as_np_ndarray(self):
         """The same graph viewed with NumPy semantics (``mx.sym.np``); graphs here are
-        dtype/shape-polymorphic, so this is the identity."""
-        return self
+        dtype/shape-polymorphic, so only the array-kind mark changes."""
+        if not getattr(self, '_legacy', False):
+            return self
+        return Symbol(self._outputs)
 
     def as_nd_ndarray(self):
-        return self
+        """The same graph as a legacy (mx.sym) symbol: marked, so a NumPy-mode HybridBlock can refuse
+        outputs that mix the two array kinds, as the reference does."""
+        s = Symbol(self._outputs)
+        s._legacy = True
+        return s
 
     def get_internals(self):
         """Every visible output of every node (nnvm GetInternals honours FNumVisibleOutputs)."""
@@ -613,7 +619,10 @@ def _create(op_name, inputs, attrs, name=None, attr=None):
         entries.append(s._outputs[0])
     node.inputs = entries
     nvis = node.num_visible_outputs()
-    return Symbol([(node, i) for i in range(nvis)])
+    out = Symbol([(node, i) for i in range(nvis)])
+    if any(getattr(x, '_legacy', False) for x in list(pos) + list(named.values()) if isinstance(x, Symbol)):
+        out._legacy = True
+    return out
 
 
 # Initializers that operators give their input variables at compose time when the variable has none

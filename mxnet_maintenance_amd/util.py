@@ -99,9 +99,30 @@ def np_array(active=True):
     return _NumpyArrayScope(active)
 
 
+def _wrap_class(cls, scope):
+    """Run every method of ``cls`` (and its inherited ``__call__`` / ``forward``, where a Block turns
+    results into arrays) inside ``scope()`` -- the class form of the use_np decorators."""
+    import inspect
+    names = [n for n, v in vars(cls).items() if inspect.isfunction(v)]
+    for extra in ('__call__', 'forward'):
+        if extra not in names and callable(getattr(cls, extra, None)):
+            names.append(extra)
+    for n in names:
+        meth = getattr(cls, n)
+
+        def make(meth):
+            @functools.wraps(meth)
+            def f(*a, **k):
+                with scope():
+                    return meth(*a, **k)
+            return f
+        setattr(cls, n, make(meth))
+    return cls
+
+
 def use_np_shape(func):
     if isinstance(func, type):
-        return func
+        return _wrap_class(func, lambda: np_shape(True))
 
     @functools.wraps(func)
     def f(*a, **k):
@@ -112,7 +133,7 @@ def use_np_shape(func):
 
 def use_np_array(func):
     if isinstance(func, type):
-        return func
+        return _wrap_class(func, lambda: np_array(True))
 
     @functools.wraps(func)
     def f(*a, **k):
