@@ -148,7 +148,7 @@ def _collect_ranges(sym, arg_params, aux_params, calib_data, num_calib_examples,
     hists = {}
 
     def cb(name, arr):
-        a = arr.asnumpy()
+        a = nd.NDArray(arr).asnumpy()
         if not np.issubdtype(a.dtype, np.floating):
             return
         mn, mx = float(a.min()), float(a.max())

@@ -20,6 +20,19 @@ from .base import MXNetError, AsyncOpError
 from .ops import registry
 
 
+def _call_monitor(cb, name, arr):
+    """Executor monitor callbacks receive (name, NDArrayHandle) as from the reference's C API:
+    ``NDArray(ctypes.cast(handle, NDArrayHandle))`` recovers the array.  The handle is live for the
+    duration of the call."""
+    from .base import _HANDLES, NDArrayHandle
+    key = id(arr)
+    _HANDLES[key] = arr
+    try:
+        cb(name, NDArrayHandle(key))
+    finally:
+        _HANDLES.pop(key, None)
+
+
 class GraphProgram:
     """Topologically ordered, slot-addressed form of a Symbol."""
 
@@ -57,7 +70,19 @@ class GraphProgram:
             self.steps.append((op.fn, ins, parsed, outs, n.name, op.name))
         self.out_slots = [slot[(id(n), j)] for n, j in sym._outputs]
         self.nslots = nslots
+        self._var_of_slot = {s: n for n, s in zip(self.var_names, self.var_slots)}
         self.name_to_slot = dict(zip(self.var_names, self.var_slots))
+
+    # operators whose monitor input names are positional in the reference (no FListInputNames)
+    _POSITIONAL_INPUTS = ('SoftmaxActivation', 'Activation')
+
+    @staticmethod
+    def _input_names(opname, attrs, n):
+        op = registry.get(opname)
+        if op.name in GraphProgram._POSITIONAL_INPUTS:
+            return ['input%d' % j for j in range(n)]
+        names = op.get_arg_names(attrs) + op.get_aux_names(attrs)
+        return [names[j] if j < len(names) else 'input%d' % j for j in range(n)]
 
     def run(self, feed, monitor=None, monitor_all=False, record=None):
         """``feed``: dict var name -> torch tensor.  Returns output tensors.
@@ -77,9 +102,16 @@ class GraphProgram:
             if record is not None:
                 record.append((name, args))
             if monitor is not None and monitor_all:
+                # reference order: a variable input under its own name, then every input as
+                # <node>_<argument name>
+                argn = self._input_names(opname, attrs, len(args))
                 for j, a in enumerate(args):
-                    if a is not None:
-                        monitor('%s_input%d' % (name, j), a)
+                    if a is None:
+                        continue
+                    var = self._var_of_slot.get(ins[j])
+                    if var is not None:
+                        monitor(var, a)
+                    monitor('%s_%s' % (name, argn[j]), a)
             try:
                 if _profiler.active_symbolic:
                     with _profiler.op_span(_profiler.current_scope() + opname, symbolic=True):
@@ -263,7 +295,7 @@ class Executor:
                 cb = self._monitor_cb
 
                 def mon(name, t):
-                    cb(name, NDArray(t.detach()))
+                    _call_monitor(cb, name, NDArray(t.detach()))
             record = [] if (mon is not None and need_grad) else None
             with torch.set_grad_enabled(need_grad):
                 outs = self._prog.run(feed, mon, self._monitor_all, record)
@@ -348,7 +380,8 @@ class Executor:
                     if not isinstance(t, torch.Tensor):
                         continue
                     g = self._mon_grads.get(id(t))
-                    self._monitor_cb('%s_backward_in%d' % (name, i), NDArray(g if g is not None else torch.zeros_like(t)))
+                    _call_monitor(self._monitor_cb, '%s_backward_in%d' % (name, i),
+                                  NDArray(g if g is not None else torch.zeros_like(t)))
             self._mon_record = None
         box = getattr(self, '_failure_box', None)
         if box is not None and box[0] is not None:

@@ -201,6 +201,10 @@ class DataParallelExecutorGroup:
                 (previous[i].exe if reshape and previous else None)
             if donor is not None:
                 self._adopt_params(exe, donor)
+            if reshape and previous and i < len(previous):
+                # a monitor installed on the executor survives the rebind for new input shapes
+                old = previous[i].exe
+                exe._monitor_cb, exe._monitor_all = old._monitor_cb, old._monitor_all
             self.shards.append(_Shard(ctx, sl, exe))
         self.data_shapes, self.label_shapes = data_shapes, label_shapes
         self.data_names = [d.name for d in data_shapes]

@@ -52,6 +52,8 @@ class Monitor:
         self.stat_helper = self._observe
 
     def _observe(self, name, array):
+        if not isinstance(array, NDArray):
+            array = NDArray(array)       # an NDArrayHandle from the executor callback
         if self.activated and self.re_prog.match(name):
             self.queue.append((self.step, name, self.stat_func(array)))
 

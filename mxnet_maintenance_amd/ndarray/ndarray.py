@@ -9,6 +9,8 @@ Device work is ordered by the HIP stream, so ``wait_to_read`` is a stream
 synchronisation; host-side asynchrony (IO, kvstore) goes through the native
 dependency engine (engine.py).
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -54,7 +56,11 @@ class NDArray:
                  '_exc')
     __array_priority__ = 1000.0
 
-    def __init__(self, data, ctx=None, dtype=None, stype='default'):
+    def __init__(self, data, ctx=None, dtype=None, stype='default', writable=True):
+        if isinstance(data, ctypes.c_void_p):
+            # a handle from the C-API shim (monitor callbacks, partitioning): the array it names
+            from ..base import _handle_object
+            data = _handle_object(data)
         if isinstance(data, NDArray):
             data = data._data
         if not isinstance(data, torch.Tensor):
@@ -844,9 +850,20 @@ def _created(opname, make):
     return r
 
 
+def _check_creation_shape(shape, what):
+    """Legacy (non NumPy-shape) semantics: a 0 dim means "unknown" and () is no shape, so creating
+    such an array is an error (reference: InitNDArray shape checks); under np_shape both are real."""
+    from ..util import is_np_shape
+    if not is_np_shape() and (len(shape) == 0 or any(int(d) == 0 for d in shape)):
+        raise MXNetError('%s: shape %s has unknown (0) dimensions; use mx.np_shape() for scalar or '
+                         'zero-size arrays' % (what, tuple(shape)))
+
+
 def zeros(shape, ctx=None, dtype=None, stype=None, out=None, **kwargs):
     if isinstance(shape, int):
         shape = (shape,)
+    if stype in (None, 'default'):
+        _check_creation_shape(tuple(shape), 'zeros')
     if stype not in (None, 'default'):
         from . import sparse
         return sparse.zeros(stype, shape, ctx=ctx, dtype=dtype)
@@ -857,6 +874,7 @@ def zeros(shape, ctx=None, dtype=None, stype=None, out=None, **kwargs):
 def ones(shape, ctx=None, dtype=None, out=None, **kwargs):
     if isinstance(shape, int):
         shape = (shape,)
+    _check_creation_shape(tuple(shape), 'ones')
     return _into(out, _created('_ones', lambda: _tag_host_ctx(NDArray(torch.ones(
         shape, dtype=torch_dtype(dtype), device=_ctx(ctx).torch_device)), ctx)))
 

@@ -166,7 +166,7 @@ def invoke(op, inputs, attrs, out=None):
         if box is None:
             raise
         res = _placeholder(attrs, inputs)    # an op fed garbage by a failed input: the input's error wins
-    except RuntimeError as e:
+    except (RuntimeError, IndexError) as e:
         # operator failures surface as MXNetError (a RuntimeError), as from the reference's C API
         raise MXNetError('Error in operator %s: %s' % (op.name, e)) from e
     nvis = op.get_num_visible_outputs(attrs)

@@ -20,14 +20,18 @@ The ``Custom`` operator is registered like any other op, so it works
 imperatively (with autograd), symbolically (infer_shape via the prop's
 ``infer_shape``) and inside hybridized blocks.
 """
+import collections
+import ctypes  # noqa: F401  (part of the reference module's star-import surface)
 import torch
 
 from . import _state
 from . import profiler as _profiler
-from .base import MXNetError
+from .base import MXNetError, NDArrayHandle  # noqa: F401
+from .ndarray.ndarray import NDArray  # noqa: F401
 from .ops import registry
 
-__all__ = ['CustomOp', 'CustomOpProp', 'register', 'get_all_registered_operators', 'NDArrayOp', 'NumpyOp',
+__all__ = ['CustomOp', 'CustomOpProp', 'register', 'get_all_registered_operators', 'get_operator_arguments',
+           'OperatorArguments', 'ctypes', 'NDArrayHandle', 'NDArray', 'NDArrayOp', 'NumpyOp',
            'PythonOp']
 
 _REGISTRY = {}
@@ -101,7 +105,40 @@ def register(reg_name):
 
 
 def get_all_registered_operators():
-    return list(_REGISTRY)
+    """Names of every registered operator (built-in and Custom)."""
+    from .ops import registry as _ops_registry, load_all
+    load_all()
+    return sorted(set(_ops_registry.list_ops()) | set(_REGISTRY))
+
+
+OperatorArguments = collections.namedtuple('OperatorArguments', ['narg', 'names', 'types'])
+
+
+def _type_doc(spec):
+    kind, default = spec[0], spec[1]
+    if kind == 'str' and isinstance(default, str) and default.startswith('{'):
+        return default
+    return '%s, %s' % (kind.rstrip('?'), 'optional, default=%r' % (default,) if default is not None
+                       else 'required')
+
+
+def get_operator_arguments(op_name):
+    """OperatorArguments(narg, names, types) of a registered operator: its array inputs
+    ('NDArray-or-Symbol') followed by its parameters."""
+    from .ops import registry as _ops_registry, load_all
+    load_all()
+    op = _ops_registry.get(op_name)
+    names = list(op.get_arg_names({}) if not callable(op.arg_names) else op.get_arg_names({}))
+    types = ['NDArray-or-Symbol'] * len(names)
+    enums = _ENUM_DOCS.get(op.name, {})
+    for k, spec in op.params.items():
+        names.append(k)
+        types.append(enums.get(k) or _type_doc(spec))
+    return OperatorArguments(len(names), names, types)
+
+
+# documented choices of enumerated parameters (the reference's dmlc enum type strings)
+_ENUM_DOCS = {'Activation': {'act_type': "{'relu', 'sigmoid', 'softrelu', 'softsign', 'tanh'}, required"}}
 
 
 def _make_prop(attrs):

@@ -226,7 +226,8 @@ def _bn_nvis(a):
 
 @register('BatchNorm', aliases=('BatchNorm_v1', 'CuDNNBatchNorm'),
           arg_names=('data', 'gamma', 'beta'), aux_names=('moving_mean', 'moving_var'),
-          num_outputs=3, num_visible_outputs=_bn_nvis, infer_params=_bn_infer, params=_BN_PARAMS)
+          num_outputs=3, num_visible_outputs=_bn_nvis, infer_params=_bn_infer, params=_BN_PARAMS,
+          output_names=('output', 'mean', 'var'))
 def batch_norm(data, gamma, beta, moving_mean, moving_var, eps=1e-3, momentum=0.9, fix_gamma=True,
                use_global_stats=False, output_mean_var=False, axis=1, cudnn_off=False, act_type=None,
                min_calib_range=None, max_calib_range=None):
@@ -281,6 +282,11 @@ def pooling(data, kernel=(), pool_type='max', global_pool=False, cudnn_off=False
         return hip_ops.global_pool(data, pool_type, _is_channel_last(layout))
     kernel = _tup(kernel, nsp, 1)
     stride = _tup(stride, nsp, 1)
+    if pooling_convention == 'same':
+        # the 'same' convention derives its own padding (output = ceil(input / stride))
+        if any(int(p) != 0 for p in (pad or ())):
+            raise MXNetError('Pooling: pad must be 0 with pooling_convention=same, got %s' % (tuple(pad),))
+        pad = (0,) * nsp
     pad = _tup(pad, nsp, 0)
     return hip_ops.pool(data, pool_type, kernel, stride, pad, pooling_convention,
                         count_include_pad, _is_channel_last(layout), p_value)
@@ -601,7 +607,7 @@ def softmax_cross_entropy(data, label):
 # Dropout / Embedding
 # ---------------------------------------------------------------------------
 
-@register('Dropout', num_outputs=2, num_visible_outputs=1,
+@register('Dropout', num_outputs=2, num_visible_outputs=1, output_names=('output', 'mask'),
           params={'p': ('float', 0.5), 'mode': ('str', 'training'), 'axes': ('shape', ()),
                   'cudnn_off': ('bool?', False)})
 def dropout(data, p=0.5, mode='training', axes=(), cudnn_off=False):
@@ -700,7 +706,7 @@ def l2_normalization(data, eps=1e-10, mode='instance'):
     return data / n.reshape(data.shape[:2] + (1,) * (data.dim() - 2))
 
 
-@register('LRN', num_outputs=2, num_visible_outputs=1,
+@register('LRN', num_outputs=2, num_visible_outputs=1, output_names=('output', 'tmp_norm'),
           params={'alpha': ('float', 1e-4), 'beta': ('float', 0.75), 'knorm': ('float', 2.0), 'nsize': ('int', 5)})
 def lrn(data, alpha=1e-4, beta=0.75, knorm=2.0, nsize=5):
     sq = (data * data).unsqueeze(1)
@@ -911,6 +917,9 @@ def spatial_transformer(data, loc, target_shape=(0, 0), transform_type='affine',
 def correlation(data1, data2, kernel_size=1, max_displacement=1, stride1=1, stride2=1, pad_size=0,
                 is_multiply=True):
     n, c, h, w = data1.shape
+    if kernel_size <= 0 or kernel_size % 2 == 0 or kernel_size > min(h, w) + 2 * pad_size - 2 * max_displacement:
+        raise MXNetError('Correlation: kernel_size %d must be odd and fit the %dx%d input (pad_size %d, '
+                         'max_displacement %d)' % (kernel_size, h, w, pad_size, max_displacement))
     p1 = F.pad(data1, (pad_size,) * 4)
     p2 = F.pad(data2, (pad_size,) * 4)
     kr = (kernel_size - 1) // 2

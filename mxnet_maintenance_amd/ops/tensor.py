@@ -668,6 +668,9 @@ def reverse(data, axis=()):
 @register('depth_to_space', params={'block_size': ('int', 1)})
 def depth_to_space(data, block_size=1):
     b = block_size
+    if data.dim() != 4 or b <= 0 or data.shape[1] % (b * b) or min(data.shape) == 0:
+        raise MXNetError('depth_to_space: need a 4-D input with depth divisible by block_size^2 > 0, got %s '
+                         'with block_size %d' % (tuple(data.shape), b))
     n, c, h, w = data.shape
     x = data.reshape(n, b, b, c // (b * b), h, w).permute(0, 3, 4, 1, 5, 2)
     return x.reshape(n, c // (b * b), h * b, w * b)
@@ -676,6 +679,9 @@ def depth_to_space(data, block_size=1):
 @register('space_to_depth', params={'block_size': ('int', 1)})
 def space_to_depth(data, block_size=1):
     b = block_size
+    if data.dim() != 4 or b <= 0 or data.shape[2] % b or data.shape[3] % b or min(data.shape) == 0:
+        raise MXNetError('space_to_depth: need a 4-D input whose height and width are divisible by '
+                         'block_size > 0, got %s with block_size %d' % (tuple(data.shape), b))
     n, c, h, w = data.shape
     x = data.reshape(n, c, h // b, b, w // b, b).permute(0, 3, 5, 1, 2, 4)
     return x.reshape(n, c * b * b, h // b, w // b)
@@ -683,6 +689,10 @@ def space_to_depth(data, block_size=1):
 
 @register('diag', params={'k': ('int', 0), 'axis1': ('int', 0), 'axis2': ('int', 1)})
 def diag(data, k=0, axis1=0, axis2=1):
+    if data.dim() >= 2:
+        d1, d2 = data.shape[axis1 % data.dim()], data.shape[axis2 % data.dim()]
+        if (k > 0 and k >= d2) or (k < 0 and -k >= d1):
+            raise MXNetError('diag: k=%d out of range for a %dx%d matrix' % (k, d1, d2))
     if data.dim() == 1:
         return torch.diag(data, k)
     return torch.diagonal(data, offset=k, dim1=axis1, dim2=axis2).contiguous()
@@ -701,6 +711,11 @@ def take(a, indices, axis=0, mode='clip'):
     n = a.shape[axis]
     idx = indices.to(torch.int64)
     if mode == 'wrap':
+        idx = torch.remainder(idx, n)
+    elif mode == 'raise':
+        if idx.numel() and bool(((idx < 0) | (idx >= n)).any()):
+            from ..base import AsyncOpError
+            raise AsyncOpError('take: index out of range for axis of size %d (mode=raise)' % n)
         idx = torch.remainder(idx, n)
     else:
         idx = torch.clamp(idx, 0, n - 1)
@@ -883,19 +898,23 @@ def ravel_multi_index(data, shape=()):
 def unravel_index(data, shape=()):
     out = []
     x = data.to(torch.int64)
-    for s in reversed(shape):
+    for s in reversed(shape[1:]):
         out.append(torch.remainder(x, s))
         x = torch.div(x, s, rounding_mode='floor')
+    out.append(x)            # the leading axis takes the quotient (its extent may be -1: unknown)
     return torch.stack(out[::-1]).to(data.dtype)
 
 
-@register('_histogram', aliases=('histogram',), arg_names=('data', 'bins'), num_outputs=2,
+@register('_histogram', aliases=('histogram',),
+          arg_names=lambda a: ['data'] if a.get('bin_cnt') not in (None, 'None') else ['data', 'bins'],
+          num_outputs=2,
           params={'bin_cnt': ('int?', None), 'range': ('floats', None)})
 def histogram(data, bins=None, bin_cnt=None, range=None):
     if bin_cnt is not None:
         lo, hi = range
         cnt = torch.histc(data.to(torch.float32), bins=bin_cnt, min=lo, max=hi)
-        edges = torch.linspace(lo, hi, bin_cnt + 1, device=data.device, dtype=data.dtype)
+        # edges as numpy computes them (exact 0 at the centre of a symmetric range)
+        edges = torch.as_tensor(np.linspace(lo, hi, bin_cnt + 1), device=data.device).to(data.dtype)
         return cnt.to(torch.int64), edges
     edges = bins
     idx = torch.bucketize(data, edges, right=True) - 1
@@ -1002,6 +1021,8 @@ def index_copy(old_tensor, index_vector, new_tensor):
 
 @register('_contrib_index_array', aliases=('index_array',), params={'axes': ('shape?', None)})
 def index_array(data, axes=None):
+    if data.dim() == 0:
+        return torch.zeros((0,), dtype=torch.int64, device=data.device)
     grids = torch.meshgrid(*[torch.arange(s, device=data.device) for s in data.shape], indexing='ij')
     if axes is not None:
         grids = [grids[a % data.dim()] for a in axes]

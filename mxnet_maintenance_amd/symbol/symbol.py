@@ -26,7 +26,7 @@ from ..name import NameManager
 from ..ops import registry
 
 __all__ = ['Symbol', 'var', 'Variable', 'Group', 'load', 'load_json', 'zeros', 'ones', 'full', 'arange',
-           'pow', 'maximum', 'minimum', 'hypot', 'eye', 'linspace', 'histogram', 'split_v2']
+           'pow', 'power', 'maximum', 'minimum', 'hypot', 'eye', 'linspace', 'histogram', 'split_v2']
 
 _MXNET_VERSION = 10901
 
