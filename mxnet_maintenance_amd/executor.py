@@ -160,6 +160,8 @@ class Executor:
         self._ctx = ctx
         # bind-time graph passes (common-subexpression elimination, pointwise fusion); argument /
         # output names and order are those of ``sym``
+        from .symbol.symbol import _unify_init_shapes
+        _unify_init_shapes(sym._topo())      # init ops with unknown dims sized from their consumers
         self._opt_symbol = _passes.optimize(sym, ctx)
         self._prog = GraphProgram(self._opt_symbol)
         arg_names = sym.list_arguments()
@@ -354,7 +356,9 @@ class Executor:
             hgs.append(torch.ones_like(o) if g is None else g._data.to(o.dtype).reshape(o.shape))
         names = [n for n, _ in self._leaves]
         ts = [t for _, t in self._leaves]
-        grads = torch.autograd.grad(heads, ts, hgs, allow_unused=True, retain_graph=False)
+        # no differentiable path (e.g. a cast to an integer type): every gradient is zero
+        grads = (torch.autograd.grad(heads, ts, hgs, allow_unused=True, retain_graph=False)
+                 if heads and ts else [None] * len(ts))
         gd = self.grad_dict
         with torch.no_grad():
             for n, g in zip(names, grads):

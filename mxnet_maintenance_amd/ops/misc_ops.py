@@ -219,8 +219,13 @@ def linalg_gelqf(A):
 
 @register('_linalg_syevd', aliases=('linalg_syevd',), num_outputs=2)
 def linalg_syevd(A):
+    """(U, L): rows of U are eigenvectors, each signed so its largest-magnitude entry (first on a tie)
+    is positive -- the reference's deterministic sign rule (la_op-inl.h SyevdEigenVecSigns)."""
     w, v = torch.linalg.eigh(A)
-    return v.transpose(-1, -2), w
+    u = v.transpose(-1, -2)
+    k = torch.argmax(u.abs(), dim=-1, keepdim=True)        # argmax returns the first maximum
+    sign = torch.where(torch.gather(u, -1, k) < 0, -1.0, 1.0).to(u.dtype)
+    return u * sign, w
 
 
 @register('_linalg_inverse', aliases=('linalg_inverse',))

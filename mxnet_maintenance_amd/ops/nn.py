@@ -350,7 +350,10 @@ def leaky_relu(data, gamma=None, act_type='leaky', slope=0.25, lower_bound=0.125
     if act_type == 'leaky':
         return F.leaky_relu(data, slope)
     if act_type == 'prelu':
-        g = gamma.reshape((1, -1) + (1,) * (data.dim() - 2)) if data.dim() > 1 else gamma
+        if gamma.dim() > 1:     # a per-(batch, channel) gamma broadcast over trailing axes
+            g = gamma.reshape(tuple(gamma.shape) + (1,) * (data.dim() - gamma.dim()))
+        else:
+            g = gamma.reshape((1, -1) + (1,) * (data.dim() - 2)) if data.dim() > 1 else gamma
         return torch.where(data >= 0, data, data * g)
     if act_type == 'elu':
         return F.elu(data, slope)
@@ -729,7 +732,23 @@ def moments(data, axes=None, keepdims=False):
 # UpSampling / spatial
 # ---------------------------------------------------------------------------
 
-@register('UpSampling', arg_names=lambda a: ['arg%d' % i for i in range(int(a.get('num_args', 1)))],
+def _upsampling_args(a):
+    if a.get('sample_type', 'nearest') == 'bilinear':
+        return ['data', 'weight']
+    return ['arg%d' % i for i in range(int(a.get('num_args', 1)))]
+
+
+def _upsampling_infer(in_shapes, a):
+    """Bilinear mode: the depthwise deconvolution weight is (channels, 1, k, k), k = 2s - s%2
+    (reference src/operator/nn/upsampling-inl.h InferShape)."""
+    if a.get('sample_type', 'nearest') != 'bilinear' or not in_shapes or in_shapes[0] is None:
+        return {}
+    s = int(a.get('scale', 1))
+    k = 2 * s - s % 2
+    return {1: (in_shapes[0][1], 1, k, k)}
+
+
+@register('UpSampling', arg_names=_upsampling_args, infer_params=_upsampling_infer,
           key_var_num_args='num_args',
           params={'scale': ('int', 1), 'num_filter': ('int', 0), 'sample_type': ('str', 'nearest'),
                   'multi_input_mode': ('str', 'concat'), 'num_args': ('int', 1), 'workspace': ('int', 512)})

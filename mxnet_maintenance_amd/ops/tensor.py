@@ -461,10 +461,13 @@ def reshape(data, shape=(), reverse=False, target_shape=None, keep_highest=False
 def reshape_like(lhs, rhs, lhs_begin=None, lhs_end=None, rhs_begin=None, rhs_end=None):
     if lhs_begin is None and rhs_begin is None and lhs_end is None and rhs_end is None:
         return lhs.reshape(rhs.shape)
-    lb = 0 if lhs_begin is None else lhs_begin % (lhs.dim() + 1)
-    le = lhs.dim() if lhs_end is None else lhs_end % (lhs.dim() + 1)
-    rb = 0 if rhs_begin is None else rhs_begin % (rhs.dim() + 1)
-    re_ = rhs.dim() if rhs_end is None else rhs_end % (rhs.dim() + 1)
+    def norm(v, dim, default):
+        # negative positions count from the end (python slicing): -1 is the last axis
+        return default if v is None else (v + dim if v < 0 else v)
+    lb = norm(lhs_begin, lhs.dim(), 0)
+    le = norm(lhs_end, lhs.dim(), lhs.dim())
+    rb = norm(rhs_begin, rhs.dim(), 0)
+    re_ = norm(rhs_end, rhs.dim(), rhs.dim())
     new = list(lhs.shape[:lb]) + list(rhs.shape[rb:re_]) + list(lhs.shape[le:])
     return lhs.reshape(new)
 
@@ -963,7 +966,16 @@ def _full(shape=(), ctx=None, dtype='float32', value=0.0):
 def _arange(start=0.0, stop=None, step=1.0, repeat=1, infer_range=False, ctx=None, dtype='float32'):
     if stop is None:
         start, stop = 0.0, start
-    r = torch.arange(start, stop, step, dtype=torch.float64, device=_dev(ctx)).to(torch_dtype(dtype))
+    td = torch_dtype(dtype)
+    n = max(int(math.ceil((stop - start) / step)), 0)
+    if td.is_floating_point:
+        r = (start + step * torch.arange(n, dtype=torch.float64, device=_dev(ctx))).to(td)
+    else:
+        # integer ranges as numpy (and the reference kernel) build them: the first two values in the
+        # target type fix the step
+        first = int(start)
+        delta = int(start + step) - first
+        r = (first + delta * torch.arange(n, dtype=torch.int64, device=_dev(ctx))).to(td)
     if repeat > 1:
         r = r.repeat_interleave(repeat)
     return r

@@ -830,6 +830,75 @@ _SAME_SHAPE = frozenset(['elemwise_add', 'elemwise_sub', 'elemwise_mul', 'elemwi
 _INIT_OPS = ('_zeros', '_ones', '_full', '_empty', 'zeros', 'ones', 'full')
 
 
+def _unify_init_shapes(order):
+    """Size init ops declared with unknown dims (0, or -1) by unifying partial shapes across the graph
+    (nnvm's bidirectional InferShape): elementwise ops share one shape, transposes permute it, and
+    shape-preserving ops pass it through, in both directions, until nothing changes.  Fully resolved
+    init ops get the shape written into their ``shape`` attribute."""
+    inits = [n for n in order if n.op in _INIT_OPS and 'shape' in n.attrs and n.parsed().get('shape')
+             and any(int(d) <= 0 for d in n.parsed()['shape'])]
+    if not inits:
+        return
+    part = {}
+
+    def merge(key, s):
+        if s is None:
+            return False
+        s = tuple(int(d) if int(d) > 0 else -1 for d in s)
+        cur = part.get(key)
+        if cur is None:
+            part[key] = s
+            return True
+        if len(cur) != len(s):
+            return False
+        new = tuple(c if c > 0 else d for c, d in zip(cur, s))
+        if new != cur:
+            part[key] = new
+            return True
+        return False
+
+    for n in order:
+        if n.op in _INIT_OPS and 'shape' in n.attrs and n.parsed().get('shape'):
+            merge((id(n), 0), n.parsed()['shape'])
+        elif n.op is None and n.attrs.get('__shape__'):
+            merge((id(n), 0), registry.parse_value('shape', n.attrs['__shape__']))
+    for _ in range(len(order) + 1):
+        changed = False
+        for n in order:
+            if n.op is None or not n.inputs:
+                continue
+            keys = [(id(a), j) for a, j in n.inputs]
+            out = (id(n), 0)
+            if n.op in _SAME_SHAPE or n.op in _SHAPE_PRESERVING:
+                group = (keys if n.op in _SAME_SHAPE else keys[:1]) + [out]
+                for k in group:
+                    for k2 in group:
+                        if k2 != k and part.get(k2) is not None:
+                            changed |= merge(k, part[k2])
+            elif n.op == 'transpose' and len(keys) == 1:
+                axes = tuple(n.parsed().get('axes') or ())
+                src = part.get(keys[0])
+                dst = part.get(out)
+                nd = len(src) if src is not None else (len(dst) if dst is not None else 0)
+                if not nd:
+                    continue
+                axes = axes or tuple(range(nd - 1, -1, -1))
+                if src is not None:
+                    changed |= merge(out, tuple(src[a] for a in axes))
+                if dst is not None:
+                    inv = [0] * nd
+                    for i, a in enumerate(axes):
+                        inv[a] = dst[i]
+                    changed |= merge(keys[0], tuple(inv))
+        if not changed:
+            break
+    for n in inits:
+        s = part.get((id(n), 0))
+        if s is not None and all(d > 0 for d in s):
+            n.attrs['shape'] = str(s)
+            n._parsed = None
+
+
 def _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what):
     """Init ops declared with 0 (unknown) dims, e.g. RNN ``begin_state`` via ``sym.zeros``.
 
@@ -838,12 +907,14 @@ def _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what):
     candidate under which the whole graph infers consistently is written
     back into the node's ``shape`` attribute (so executors allocate it).
     """
+    _unify_init_shapes(order)
     zero_nodes = []
     zero_vars = []      # variables declared with unknown (0) dims, e.g. RNN begin_state(func=Variable)
     for n in order:
         if n.op in _INIT_OPS and 'shape' in n.attrs:
             shp = n.parsed().get('shape')
-            if shp and any(int(d) == 0 for d in shp):
+            if shp and any(int(d) <= 0 for d in shp):
+                shp = tuple(max(int(d), 0) for d in shp)
                 zero_nodes.append((n, tuple(int(d) for d in shp)))
         elif n.op is None and n.name not in known_shapes and n.attrs.get('__shape__'):
             shp = registry.parse_value('shape', n.attrs['__shape__'])
@@ -883,6 +954,45 @@ def _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what):
     return None
 
 
+def _unknown_dims(s):
+    """True when a shape has unknown dims (-1 under np-shape semantics, 0 in legacy mode)."""
+    from .. import util
+    unk = -1 if util.is_np_shape() else 0
+    return s is not None and any(int(d) == unk or int(d) < 0 for d in s)
+
+
+def _slice_dim(dim, b, e, st):
+    from .. import util
+    if int(dim) == (-1 if util.is_np_shape() else 0) or int(dim) < 0:
+        return int(dim)
+    return len(range(*slice(b, e, st).indices(int(dim))))
+
+
+def _partial_slice(d, a):
+    """slice on a partially known shape: sliced axes of unknown extent stay unknown
+    (reference src/operator/tensor/matrix_op-inl.h SliceOpShape)."""
+    begin, end, step = tuple(a.get('begin') or ()), tuple(a.get('end') or ()), tuple(a.get('step') or ())
+    out = []
+    for i, dim in enumerate(d):
+        if i >= len(begin):
+            out.append(int(dim))
+            continue
+        st = step[i] if i < len(step) and step[i] is not None else 1
+        out.append(_slice_dim(dim, begin[i], end[i] if i < len(end) else None, st))
+    return tuple(out)
+
+
+def _partial_slice_axis(d, a):
+    ax = int(a.get('axis', 0)) % len(d)
+    out = [int(x) for x in d]
+    out[ax] = _slice_dim(d[ax], a.get('begin', 0), a.get('end'), 1)
+    return tuple(out)
+
+
+_PARTIAL_OUT = {'slice': _partial_slice, 'crop': _partial_slice, '_slice': _partial_slice,
+                'slice_axis': _partial_slice_axis}
+
+
 def _subgraph_same_shape(node):
     from .subgraph import same_shape
     return same_shape(node)
@@ -914,6 +1024,9 @@ def _partial_zero_dims(order, shape):
             continue
         op = n.opdef()
         in_shapes = [shape.get((id(a), j)) for a, j in n.inputs]
+        if n.op in _PARTIAL_OUT and in_shapes and in_shapes[0] is not None and (id(n), 0) not in shape:
+            shape[(id(n), 0)] = _PARTIAL_OUT[n.op](in_shapes[0], n.parsed())
+            continue
         if op.infer_params is None or not in_shapes or in_shapes[0] is None or all(in_shapes):
             continue
         try:
@@ -1020,10 +1133,17 @@ def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True, pa
             for (a, j), d in zip(n.inputs, in_dt):
                 if (id(a), j) not in dtype and a.op is None:
                     dtype[(id(a), j)] = d
-            try:
-                outs = _run_meta(op, parsed, in_shapes, in_dt)
-            except Exception as e:
-                raise MXNetError('Error in operator %s (%s): %s' % (n.name, n.op, e))
+            pfn = _PARTIAL_OUT.get(n.op) if partial else None
+            if pfn is not None and any(_unknown_dims(s) for s in in_shapes):
+                outs = [(pfn(in_shapes[0], parsed), base_dt)]
+            else:
+                try:
+                    outs = _run_meta(op, parsed, in_shapes, in_dt)
+                except Exception as e:
+                    if partial and any(_unknown_dims(s) for s in in_shapes):
+                        done.add(id(n))     # output stays unknown
+                        continue
+                    raise MXNetError('Error in operator %s (%s): %s' % (n.name, n.op, e))
             for i, (s, d) in enumerate(outs):
                 prev = shape.get((id(n), i))
                 if prev is not None and tuple(prev) != tuple(s):
