@@ -472,6 +472,54 @@ def _dgrad_weight(w):
     return w.flip(1, 2).permute(3, 1, 2, 0).contiguous()
 
 
+def _phase_taps(R, P, s, ph):
+    """Taps of kernel axis R (pad P, stride s) that reach dX positions s*a + ph: [(d, r)] with
+    dX[s*a + ph] += dY[a + d] * W[r], d ascending."""
+    return sorted(((ph + P - r) // s, r) for r in range(R) if (ph + P - r) % s == 0)
+
+
+def conv_dgrad_strided_ok(dy, w, stride, pad, xshape, bco=128):
+    K, R, S, C = w.shape
+    s = tuple(stride)
+    return (_CONV_HIP and s != (1, 1) and s[0] == s[1] and dy.dtype in (torch.float16, torch.bfloat16)
+            and dy.dim() == 4 and K % 64 == 0 and C % bco == 0 and xshape[1] % s[0] == 0 and xshape[2] % s[1] == 0
+            and dy.is_cuda and all(0 <= p < k for p, k in zip(pad, (R, S))))
+
+
+def conv_dgrad_strided(dy, w, stride, pad, xshape, bco=128):
+    """Data gradient of a stride-s conv as s*s sub-pixel phases (src/kernels/conv_glds.hip
+    conv_nhwc_dgrad_phase_glds): phase (ph, pw) of dX -- rows s*a + ph, columns s*b + pw -- is a
+    stride-1 conv of dY with the taps of W that reach it, written in place; phases no tap reaches
+    are zero.  No zero-stuffed dY and no scatter pass (cf. the reference's cuDNN backward-data,
+    src/operator/nn/cudnn/cudnn_convolution-inl.h)."""
+    K, R, S, C = w.shape
+    N, H, W, _ = xshape
+    st = stride[0]
+    Ho, Wo = H // st, W // st
+    dy = dy.contiguous()
+    dx = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+    lib = _K.lib()
+    wp = w.permute(3, 1, 2, 0)      # [C][R][S][K]
+    zero = _zero_page(dy.device).data_ptr()
+    for ph in range(st):
+        th = _phase_taps(R, pad[0], st, ph)
+        for pw in range(st):
+            tw = _phase_taps(S, pad[1], st, pw)
+            if not th or not tw:
+                dx.view(N, Ho, st, Wo, st, C)[:, :, ph, :, pw, :].zero_()
+                continue
+            dh = [d for d, _ in th]
+            dw = [d for d, _ in tw]
+            if dh != list(range(dh[0], dh[0] + len(dh))) or dw != list(range(dw[0], dw[0] + len(dw))):
+                raise ValueError('conv_dgrad_strided: non-contiguous phase taps')
+            wsub = wp.index_select(1, torch.tensor([r for _, r in th], device=w.device)) \
+                     .index_select(2, torch.tensor([r for _, r in tw], device=w.device)).contiguous()
+            lib.conv_nhwc_dgrad_phase_glds(_DT[dy.dtype], dy.data_ptr(), wsub.data_ptr(), dx.data_ptr(), zero, N,
+                                           dy.shape[1], dy.shape[2], K, C, len(th), len(tw), -dh[0], -dw[0], Ho, Wo,
+                                           st, ph, pw, bco, _stream())
+    return dx
+
+
 def _conv_bwd_torch(dy, x, w, stride, pad, mask):
     xc = x.permute(0, 3, 1, 2)
     wc = w.permute(0, 3, 1, 2)
@@ -651,6 +699,9 @@ def _dgrad_candidates(dy, x, w, stride, pad):
         for v in _fwd_variants(K, C):
             c.append(('hip%d' % v, lambda v=v: conv_fwd(dy, _dgrad_weight(w), (1, 1), (R - 1 - pad[0], S - 1 - pad[1]),
                                                         None, v)))
+    for bco in (128, 64):
+        if conv_dgrad_strided_ok(dy, w, stride, pad, x.shape, bco):
+            c.append(('phase%d' % bco, lambda bco=bco: conv_dgrad_strided(dy, w, stride, pad, x.shape, bco)))
     c.append(('miopen', lambda: _conv_bwd_torch(dy, x, w, stride, pad, (True, False))[0]))
     return c
 

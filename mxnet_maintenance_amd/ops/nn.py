@@ -1169,6 +1169,12 @@ def rnn(data, parameters, state, state_cell=None, sequence_length=None, state_si
             return (out, h, c) if state_outputs else out
         return (out, h) if state_outputs else out
     flat = [t for group in ws for t in group]
+    hsz = projection_size or state_size
+    want = (num_layers * d, data.shape[1], hsz)
+    if tuple(state.shape) != want or (mode == 'lstm' and state_cell is not None
+                                      and tuple(state_cell.shape) != (num_layers * d, data.shape[1], state_size)):
+        # the fused torch kernels do not validate state shapes
+        raise MXNetError('RNN: state shape %s does not match %s' % (tuple(state.shape), want))
     if mode == 'lstm':
         out, h, c = torch._VF.lstm(data, (state, state_cell), flat, True, num_layers, p, train,
                                    bidirectional, False)

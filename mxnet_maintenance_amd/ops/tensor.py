@@ -403,13 +403,9 @@ def infer_reshape(src, shape, reverse=False):
     src = list(src)
     shape = list(shape)
     if reverse:
+        # right-to-left: the reversed codes apply to the reversed source shape (a -4 then splits
+        # into the two reversed entries after it)
         src = src[::-1]
-        # -4 consumes the next two entries: keep (-4, a, b) groups in order
-        out_rev = []
-        i = 0
-        while i < len(shape):
-            out_rev.append(shape[i])
-            i += 1
         shape = shape[::-1]
     out = []
     si = 0
@@ -427,8 +423,6 @@ def infer_reshape(src, shape, reverse=False):
             out.append(src[si] * src[si + 1]); si += 2
         elif s == -4:
             d1, d2 = shape[i + 1], shape[i + 2]
-            if reverse:
-                d1, d2 = d2, d1
             cur = src[si]
             if d1 == -1:
                 d1 = cur // d2
@@ -451,7 +445,13 @@ def infer_reshape(src, shape, reverse=False):
                                                    'target_shape': ('shape?', None), 'keep_highest': ('bool', False)})
 def reshape(data, shape=(), reverse=False, target_shape=None, keep_highest=False):
     if not shape and target_shape:
-        shape = target_shape
+        # legacy target_shape: a 0 is the inferred dim; keep_highest fixes the first dim to the input's
+        t = [int(d) for d in target_shape]
+        if keep_highest:
+            t[0] = int(data.shape[0])
+        known = int(np.prod([d for d in t if d != 0])) if t else 1
+        shape = tuple(d if d != 0 else data.numel() // max(known, 1) for d in t)
+        return data.reshape(shape)
     return data.reshape(infer_reshape(data.shape, shape, reverse))
 
 

@@ -15,6 +15,7 @@ from the operator's ``infer_params`` hook.
 """
 import copy
 import json
+import math
 import warnings
 
 import numpy as np
@@ -817,6 +818,10 @@ def _run_meta(op, parsed, shapes, dtypes):
 _SHAPE_PRESERVING = ('Cast', 'cast', 'amp_cast', 'amp_multicast', '_copy', 'identity', 'BlockGrad',
                      'stop_gradient')
 
+_ELEMWISE_BINARY = frozenset(['elemwise_add', 'elemwise_sub', 'elemwise_mul', 'elemwise_div', '_grad_add', '_plus',
+                              '_minus', '_mul', '_div', '_add', '_sub', 'add_n', 'ElementWiseSum', '_maximum',
+                              '_minimum', '_power', '_hypot'])
+
 _SAME_SHAPE = frozenset(['elemwise_add', 'elemwise_sub', 'elemwise_mul', 'elemwise_div', '_grad_add', '_plus',
                          '_minus', '_mul', '_div', '_add', '_sub', 'add_n', 'ElementWiseSum', '_maximum', '_minimum',
                          '_power', '_hypot', 'Activation', 'relu', 'sigmoid', 'tanh', 'softsign', 'Dropout',
@@ -830,15 +835,12 @@ _SAME_SHAPE = frozenset(['elemwise_add', 'elemwise_sub', 'elemwise_mul', 'elemwi
 _INIT_OPS = ('_zeros', '_ones', '_full', '_empty', 'zeros', 'ones', 'full')
 
 
-def _unify_init_shapes(order):
-    """Size init ops declared with unknown dims (0, or -1) by unifying partial shapes across the graph
-    (nnvm's bidirectional InferShape): elementwise ops share one shape, transposes permute it, and
-    shape-preserving ops pass it through, in both directions, until nothing changes.  Fully resolved
-    init ops get the shape written into their ``shape`` attribute."""
-    inits = [n for n in order if n.op in _INIT_OPS and 'shape' in n.attrs and n.parsed().get('shape')
-             and any(int(d) <= 0 for d in n.parsed()['shape'])]
-    if not inits:
-        return
+def _unify_shapes(order, seeds):
+    """Unify partial shapes across the graph (nnvm's bidirectional InferShape, unknown dims <= 0):
+    elementwise ops share one shape, transposes permute it, shape-preserving ops pass it through,
+    and a Reshape whose output is known sizes the one unknown dim of its input -- in both
+    directions, until nothing changes.  ``seeds``: (id(node), 0) -> partial shape.  Returns the
+    (id(node), out) -> partial shape map (unknown dims -1)."""
     part = {}
 
     def merge(key, s):
@@ -857,6 +859,9 @@ def _unify_init_shapes(order):
             return True
         return False
 
+    full = lambda t: t is not None and all(d > 0 for d in t)     # noqa: E731
+    for k, v in seeds.items():
+        merge(k, v)
     for n in order:
         if n.op in _INIT_OPS and 'shape' in n.attrs and n.parsed().get('shape'):
             merge((id(n), 0), n.parsed()['shape'])
@@ -890,8 +895,32 @@ def _unify_init_shapes(order):
                     for i, a in enumerate(axes):
                         inv[a] = dst[i]
                     changed |= merge(keys[0], tuple(inv))
+            elif n.op in ('Reshape', 'reshape') and len(keys) == 1:
+                src, dst = part.get(keys[0]), part.get(out)
+                if full(src) and not full(dst):
+                    try:
+                        o = _run_meta(n.opdef(), n.parsed(), [src], [torch.float32])
+                        changed |= merge(out, o[0][0])
+                    except Exception:   # pylint: disable=broad-except
+                        pass
+                elif full(dst) and src is not None and sum(1 for d in src if d <= 0) == 1:
+                    known = math.prod(d for d in src if d > 0)
+                    total = math.prod(dst)
+                    if known and total % known == 0:
+                        changed |= merge(keys[0], tuple(d if d > 0 else total // known for d in src))
         if not changed:
             break
+    return part
+
+
+def _unify_init_shapes(order):
+    """Size init ops declared with unknown dims (0, or -1) from their consumers (_unify_shapes);
+    fully resolved ones get the shape written into their ``shape`` attribute."""
+    inits = [n for n in order if n.op in _INIT_OPS and 'shape' in n.attrs and n.parsed().get('shape')
+             and any(int(d) <= 0 for d in n.parsed()['shape'])]
+    if not inits:
+        return
+    part = _unify_shapes(order, {})
     for n in inits:
         s = part.get((id(n), 0))
         if s is not None and all(d > 0 for d in s):
@@ -922,7 +951,7 @@ def _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what):
                 zero_vars.append((n, tuple(int(d) for d in shp)))
     if not zero_nodes and not zero_vars:
         return None
-    cands = sorted({int(d) for s in known_shapes.values() if s for d in s if int(d) > 1})
+    cands = sorted({int(d) for s in known_shapes.values() if s for d in s if int(d) >= 1})
     aux = _aux_var_ids(order)
     arg_nodes = [n for n in order if n.op is None and id(n) not in aux]
     complete = lambda r: all(x is not None for part in r for x in part)     # noqa: E731
@@ -1045,6 +1074,16 @@ def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True, pa
     Returns (arg_list, out_list, aux_list) of shapes (or dtypes), None for unknown.
     """
     order = sym._topo()
+    if what == 'shape' and known_shapes and any(any(int(d) <= 0 for d in v) for v in known_shapes.values() if v):
+        # arguments given with unknown dims: size them by unification when the graph determines them
+        byname = {n.name: n for n in order if n.op is None}
+        seeds = {(id(byname[k]), 0): v for k, v in known_shapes.items() if k in byname and v}
+        part = _unify_shapes(order, seeds)
+        known_shapes = dict(known_shapes)
+        for k in list(known_shapes):
+            r = part.get((id(byname[k]), 0)) if k in byname else None
+            if r is not None and all(d > 0 for d in r):
+                known_shapes[k] = r
     if _resolve and what == 'shape' and known_shapes:
         res = _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what)
         if res is not None:
@@ -1133,6 +1172,11 @@ def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True, pa
             for (a, j), d in zip(n.inputs, in_dt):
                 if (id(a), j) not in dtype and a.op is None:
                     dtype[(id(a), j)] = d
+            if (n.op in _ELEMWISE_BINARY and len({tuple(x) for x in in_shapes}) > 1
+                    and not any(int(d) == 0 for x in in_shapes for d in x)):
+                # nnvm ElemwiseShape: no broadcasting
+                raise MXNetError('Error in operator %s (%s): incompatible input shapes %s'
+                                 % (n.name, n.op, [tuple(x) for x in in_shapes]))
             pfn = _PARTIAL_OUT.get(n.op) if partial else None
             if pfn is not None and any(_unknown_dims(s) for s in in_shapes):
                 outs = [(pfn(in_shapes[0], parsed), base_dt)]

@@ -63,6 +63,9 @@ int conv_nhwc_fwd_big_bwd_nparts(int N, int H, int W, int R, int S, int sh, int 
 void conv_nhwc_fwd_glds(int dtype, const void* x, const void* w, const float* bias, void* y, const void* zero, int N,
                         int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int bco,
                         hipStream_t s);
+void conv_nhwc_dgrad_phase_glds(int dtype, const void* dy, const void* wsub, void* dx, const void* zero, int N,
+                                int Hi, int Wi, int Cin, int Cout, int R, int S, int pad_h, int pad_w, int Ho,
+                                int Wo, int stride, int ph, int pw, int bco, hipStream_t s);
 int conv_nhwc_fwd_ring_nparts(int N, int H, int W, int R, int S, int sh, int sw, int ph, int pw, int variant);
 void conv_nhwc_fwd_ring(int dtype, const void* x, const void* w, void* y, const void* zero, int N, int H, int W, int C,
                         int K, int R, int S, int sh, int sw, int ph, int pw, int variant, float* part, int nparts,
@@ -283,6 +286,14 @@ PYBIND11_MODULE(_hip_kernels, m) {
     conv_nhwc_fwd_glds(dt, P<void>(x), P<void>(w), P<float>(bias), P<void>(y), P<void>(zero), N, H, W, C, K, R, Sf,
                        sh, sw, ph, pw, bco, S(s));
     check_launch("conv_nhwc_fwd_glds");
+  });
+  // one sub-pixel phase of a strided data gradient, written in place into dX
+  m.def("conv_nhwc_dgrad_phase_glds", [](int dt, uintptr_t dy, uintptr_t wsub, uintptr_t dx, uintptr_t zero, int N,
+                                         int Hi, int Wi, int Cin, int Cout, int R, int Sf, int pad_h, int pad_w,
+                                         int Ho, int Wo, int stride, int ph, int pw, int bco, uintptr_t s) {
+    conv_nhwc_dgrad_phase_glds(dt, P<void>(dy), P<void>(wsub), P<void>(dx), P<void>(zero), N, Hi, Wi, Cin, Cout, R,
+                               Sf, pad_h, pad_w, Ho, Wo, stride, ph, pw, bco, S(s));
+    check_launch("conv_nhwc_dgrad_phase_glds");
   });
   // 512-thread big-tile kernel: variant 0..3 = 256x256, 128x256, 64x512, 256x128 (co x pix);
   // part (optional): channel-major [2][K][nparts] BatchNorm sum / sum-of-squares partials of y

@@ -75,6 +75,9 @@ struct GeomG {
   int sh, sw, ph, pw;
   int M;     // N*Ho*Wo
   int Ktot;  // R*S*C
+  // output element offset of pixel p = q*Wo + wo (q = n*Ho + ho): q*og + wo*oc + ob (dense: Wo*K, K, 0);
+  // a strided map lets a sub-pixel piece of a strided dgrad write its phase of dX in place
+  int64_t og, oc, ob;
 };
 
 __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
@@ -213,7 +216,9 @@ __global__ void __launch_bounds__(256) conv_fwd_glds_kernel(const T* __restrict_
       const int p = pix0 + wpix * 64 + j * 16 + frag_r;
       if (p < g.M) {
         uint2 v = Mfma<T>::pack4(acc[i][j][0] + b0, acc[i][j][1] + b1, acc[i][j][2] + b2, acc[i][j][3] + b3);
-        *reinterpret_cast<uint2*>(y + (int64_t)p * g.K + co) = v;
+        const int q = p / g.Wo;
+        const int64_t off = q * g.og + (p - q * g.Wo) * g.oc + g.ob;
+        *reinterpret_cast<uint2*>(y + off + co) = v;
       }
     }
   }
@@ -243,6 +248,9 @@ void conv_nhwc_fwd_glds(int dtype, const void* x, const void* w, const float* bi
   g.Wo = (W + 2 * pw - S) / sw + 1;
   g.M = N * g.Ho * g.Wo;
   g.Ktot = R * S * C;
+  g.og = (int64_t)g.Wo * K;
+  g.oc = K;
+  g.ob = 0;
   MXAMD_HOST_CHECK(C % 64 == 0 && K % bco == 0 && (bco == 64 || bco == 128),
                    "conv_nhwc_fwd_glds: need Cin % 64 == 0 and Cout % BCO == 0");
   MXAMD_HOST_CHECK((int64_t)N * H * W * C < (1ll << 31) && (int64_t)g.M * K < (1ll << 31) &&
@@ -256,6 +264,41 @@ void conv_nhwc_fwd_glds(int dtype, const void* x, const void* w, const float* bi
     else launch_glds<__hip_bfloat16, 64>(x, w, bias, y, zero, g, s);
   } else {
     throw std::runtime_error("conv_nhwc_fwd_glds: dtype must be f16 or bf16");
+  }
+}
+
+// One sub-pixel phase (ph, pw) of a stride-s data gradient: dX[n, s*a + ph, s*b + pw, :] for all (a, b),
+// as a stride-1 conv of dY (N x Hi x Wi x Cin, Cin = the conv's output channels) with the phase's taps
+// wsub [Cout][R][S][Cin] (R x S = taps of that phase, offsets -pad_h/-pad_w, possibly negative) into an
+// Ho x Wo grid written in place inside dX (Hx x Wx x Cout, Hx = s*Ho, Wx = s*Wo).
+void conv_nhwc_dgrad_phase_glds(int dtype, const void* dy, const void* wsub, void* dx, const void* zero, int N,
+                                int Hi, int Wi, int Cin, int Cout, int R, int S, int pad_h, int pad_w, int Ho,
+                                int Wo, int stride, int ph, int pw, int bco, hipStream_t s) {
+  GeomG g;
+  g.N = N; g.H = Hi; g.W = Wi; g.C = Cin; g.K = Cout; g.R = R; g.S = S;
+  g.sh = 1; g.sw = 1; g.ph = pad_h; g.pw = pad_w;
+  g.Ho = Ho;
+  g.Wo = Wo;
+  g.M = N * Ho * Wo;
+  g.Ktot = R * S * Cin;
+  const int64_t Wx = (int64_t)stride * Wo;
+  g.og = stride * Wx * Cout;
+  g.oc = (int64_t)stride * Cout;
+  g.ob = ((int64_t)ph * Wx + pw) * Cout;
+  MXAMD_HOST_CHECK(Cin % 64 == 0 && Cout % bco == 0 && (bco == 64 || bco == 128) && stride >= 1 && ph >= 0 &&
+                       ph < stride && pw >= 0 && pw < stride && Ho > 0 && Wo > 0,
+                   "conv_nhwc_dgrad_phase_glds: need Cin % 64 == 0, Cout % BCO == 0 and a valid phase");
+  MXAMD_HOST_CHECK((int64_t)N * Hi * Wi * Cin < (1ll << 31) && (int64_t)Cout * g.Ktot < (1ll << 31) &&
+                       (int64_t)N * stride * Ho * Wx * Cout < (1ll << 62),
+                   "conv_nhwc_dgrad_phase_glds: tensor too large for 32-bit indexing");
+  if (dtype == kF16) {
+    if (bco == 128) launch_glds<__half, 128>(dy, wsub, nullptr, dx, zero, g, s);
+    else launch_glds<__half, 64>(dy, wsub, nullptr, dx, zero, g, s);
+  } else if (dtype == kBF16) {
+    if (bco == 128) launch_glds<__hip_bfloat16, 128>(dy, wsub, nullptr, dx, zero, g, s);
+    else launch_glds<__hip_bfloat16, 64>(dy, wsub, nullptr, dx, zero, g, s);
+  } else {
+    throw std::runtime_error("conv_nhwc_dgrad_phase_glds: dtype must be f16 or bf16");
   }
 }
 

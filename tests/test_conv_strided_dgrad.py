@@ -1,0 +1,83 @@
+"""Strided convolution data gradient as sub-pixel phases (ops/kernel_fns.conv_dgrad_strided,
+src/kernels/conv_glds.hip conv_nhwc_dgrad_phase_glds), against the fp32 PyTorch reference."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mxnet_maintenance_amd.ops import kernel_fns as KF
+
+CASES = [  # (N, H, W, C, K, R, stride, pad)
+    (2, 8, 8, 64, 64, 3, 2, 1),
+    (2, 8, 8, 128, 64, 1, 2, 0),
+    (1, 12, 8, 64, 128, 3, 2, 0),
+    (2, 9, 9, 64, 64, 3, 3, 1),
+]
+
+
+def _ref_dx(dy, w, stride, pad, xshape):
+    """fp32 dX of an NHWC conv (w: K x R x S x C) via autograd."""
+    x = torch.zeros(xshape[0], xshape[3], xshape[1], xshape[2], dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(x, w.double().permute(0, 3, 1, 2), stride=stride, padding=pad)
+    y.backward(dy.double().permute(0, 3, 1, 2))
+    return x.grad.permute(0, 2, 3, 1)
+
+
+def _phase_emulation(dy, w, stride, pad, xshape):
+    """The phase decomposition evaluated with stride-1 torch convs on the CPU (checks the tap algebra)."""
+    K, R, S, C = w.shape
+    N, H, W, _ = xshape
+    s = stride
+    dx = torch.zeros(N, H, W, C, dtype=torch.float64)
+    d = dy.double().permute(0, 3, 1, 2)
+    for ph in range(s):
+        th = KF._phase_taps(R, pad, s, ph)
+        for pw in range(s):
+            tw = KF._phase_taps(S, pad, s, pw)
+            if not th or not tw:
+                continue
+            wsub = w.double()[:, [r for _, r in th]][:, :, [c for _, c in tw]]     # K x th x tw x C
+            wk = wsub.permute(3, 0, 1, 2)                                       # C x K x th x tw
+            dh0, dw0 = th[0][0], tw[0][0]
+            Ho, Wo = H // s, W // s
+            # rows a + dh0 + t for t < len(th): pad dY so the window starts at dh0
+            top, left = max(-dh0, 0), max(-dw0, 0)
+            dp = F.pad(d, (left, Wo + len(tw) + abs(dw0), top, Ho + len(th) + abs(dh0)))
+            out = F.conv2d(dp[:, :, top + dh0:, left + dw0:], wk)[:, :, :Ho, :Wo]
+            dx[:, ph::s, pw::s, :] = out.permute(0, 2, 3, 1)
+    return dx
+
+
+@pytest.mark.parametrize('case', CASES)
+def test_phase_taps_reproduce_conv_transpose(case):
+    N, H, W, C, K, R, s, p = case
+    torch.manual_seed(0)
+    Ho = (H + 2 * p - R) // s + 1
+    Wo = (W + 2 * p - R) // s + 1
+    dy = torch.randn(N, Ho, Wo, K)
+    w = torch.randn(K, R, R, C)
+    if H % s or W % s:
+        pytest.skip('phase grid needs H, W divisible by the stride')
+    ref = _ref_dx(dy, w, s, p, (N, H, W, C))
+    got = _phase_emulation(dy, w, s, p, (N, H, W, C))
+    torch.testing.assert_close(got, ref, rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('case', CASES + [(4, 56, 56, 128, 128, 3, 2, 1), (4, 56, 56, 256, 512, 1, 2, 0)])
+@pytest.mark.parametrize('bco', [128, 64])
+def test_strided_dgrad_kernel_matches_fp32(case, dtype, bco):
+    N, H, W, C, K, R, s, p = case
+    if H % s or W % s:
+        pytest.skip('phase grid needs H, W divisible by the stride')
+    torch.manual_seed(1)
+    Ho = (H + 2 * p - R) // s + 1
+    Wo = (W + 2 * p - R) // s + 1
+    dy = torch.randn(N, Ho, Wo, K, device='cuda').to(dtype)
+    w = (torch.randn(K, R, R, C, device='cuda') / (K * R * R) ** 0.5).to(dtype)
+    assert KF.conv_dgrad_strided_ok(dy, w, (s, s), (p, p), (N, H, W, C), bco)
+    got = KF.conv_dgrad_strided(dy, w, (s, s), (p, p), (N, H, W, C), bco)
+    torch.cuda.synchronize()
+    ref = _ref_dx(dy.cpu().float(), w.cpu().float(), s, p, (N, H, W, C))
+    err = (got.float().cpu().double() - ref).abs().max() / ref.abs().max()
+    assert err < (1e-2 if dtype == torch.float16 else 3e-2), float(err)
