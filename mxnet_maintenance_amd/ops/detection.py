@@ -375,39 +375,79 @@ def box_decode(data, anchors, std0=1.0, std1=1.0, std2=1.0, std3=1.0, clip=-1.0,
                   'position_sensitive': ('bool', False), 'aligned': ('bool', False)})
 def roi_align(data, rois, pooled_size=(), spatial_scale=1.0, sample_ratio=-1, position_sensitive=False,
               aligned=False):
+    """ROIAlign (reference src/operator/contrib/roi_align.cc): per-ROI sampling grids
+    (ceil(roi / pooled) points per bin unless sample_ratio > 0), bilinear samples that vanish beyond
+    one pixel outside the map and clamp to the border inside it, averaged per bin.  Gradients reach
+    ``data`` only (the ROI coordinates get none, as in the reference)."""
     N, C, H, W = data.shape
     ph, pw = pooled_size
     R = rois.shape[0]
+    dev, dt = data.device, data.dtype
+    r = rois.detach().to(dt)
     off = 0.5 if aligned else 0.0
-    bidx = rois[:, 0].long()
-    x1 = rois[:, 1] * spatial_scale - off
-    y1 = rois[:, 2] * spatial_scale - off
-    x2 = rois[:, 3] * spatial_scale - off
-    y2 = rois[:, 4] * spatial_scale - off
-    rw, rh = x2 - x1, y2 - y1
+    bidx = r[:, 0].long()
+    x1 = r[:, 1] * spatial_scale - off
+    y1 = r[:, 2] * spatial_scale - off
+    rw = r[:, 3] * spatial_scale - off - x1
+    rh = r[:, 4] * spatial_scale - off - y1
     if not aligned:
         rw, rh = rw.clamp(min=1.0), rh.clamp(min=1.0)
     bw, bh = rw / pw, rh / ph
     if sample_ratio > 0:
-        sy = sx = sample_ratio
+        gh = torch.full((R,), sample_ratio, device=dev, dtype=torch.long)
+        gw = gh.clone()
     else:
-        sy = max(1, int(math.ceil(float(rh.max()) / ph))) if R else 1
-        sx = max(1, int(math.ceil(float(rw.max()) / pw))) if R else 1
-    iy = (torch.arange(ph * sy, device=data.device, dtype=data.dtype) + 0.5) / sy   # in bin units
-    ix = (torch.arange(pw * sx, device=data.device, dtype=data.dtype) + 0.5) / sx
-    ys = y1[:, None] + iy[None, :] * bh[:, None]                 # [R, ph*sy]
-    xs = x1[:, None] + ix[None, :] * bw[:, None]
-    gy = 2.0 * (ys + 0.5) / H - 1.0                              # align_corners=False pixel-center mapping
-    gx = 2.0 * (xs + 0.5) / W - 1.0
-    grid = torch.stack([gx[:, None, :].expand(R, ph * sy, pw * sx), gy[:, :, None].expand(R, ph * sy, pw * sx)], -1)
-    feats = data[bidx]                                           # [R, C, H, W]
-    s = F.grid_sample(feats, grid, mode='bilinear', padding_mode='zeros', align_corners=False)
-    s = s.reshape(R, C, ph, sy, pw, sx).mean(dim=(3, 5))
+        gh = torch.ceil(rh / ph).long().clamp(min=1)
+        gw = torch.ceil(rw / pw).long().clamp(min=1)
+    GH = int(gh.max()) if R else 1
+    GW = int(gw.max()) if R else 1
+    iy = torch.arange(GH, device=dev, dtype=dt)
+    ix = torch.arange(GW, device=dev, dtype=dt)
+    # sample coordinates [R, ph, GH] / [R, pw, GW]
+    ys = (y1[:, None, None] + torch.arange(ph, device=dev, dtype=dt)[None, :, None] * bh[:, None, None]
+          + (iy[None, None, :] + 0.5) * bh[:, None, None] / gh[:, None, None].to(dt))
+    xs = (x1[:, None, None] + torch.arange(pw, device=dev, dtype=dt)[None, :, None] * bw[:, None, None]
+          + (ix[None, None, :] + 0.5) * bw[:, None, None] / gw[:, None, None].to(dt))
+    my = (iy[None, :] < gh[:, None].to(dt)).to(dt)                  # [R, GH] points in use
+    mx_ = (ix[None, :] < gw[:, None].to(dt)).to(dt)
+
+    def axis(v, size):
+        inside = ((v >= -1.0) & (v <= size)).to(dt)
+        v = v.clamp(min=0.0)
+        lo = v.floor().long()
+        top = lo >= size - 1
+        lo = torch.where(top, torch.full_like(lo, size - 1), lo)
+        hi = torch.where(top, lo, lo + 1)
+        v = torch.where(top, lo.to(dt), v)
+        frac = v - lo.to(dt)
+        return lo, hi, frac, inside
+
+    ylo, yhi, ly, yin = axis(ys, H)
+    xlo, xhi, lx, xin = axis(xs, W)
+    P = ph * GH * pw * GW
+    shp = (R, ph, GH, pw, GW)
+
+    def idx(yi, xi):
+        return (yi[:, :, :, None, None] * W + xi[:, None, None, :, :]).expand(shp).reshape(R, 1, P)
+
+    wy = {0: (1.0 - ly), 1: ly}
+    wx = {0: (1.0 - lx), 1: lx}
+    valid = (yin[:, :, :, None, None] * xin[:, None, None, :, :] * my[:, None, :, None, None]
+             * mx_[:, None, None, None, :])
+    feats = data[bidx].reshape(R, C, H * W)
+    acc = None
+    for a, yi in ((0, ylo), (1, yhi)):
+        for b_, xi in ((0, xlo), (1, xhi)):
+            wgt = (wy[a][:, :, :, None, None] * wx[b_][:, None, None, :, :] * valid).reshape(R, 1, P)
+            v = feats.gather(2, idx(yi, xi).expand(R, C, P)) * wgt
+            acc = v if acc is None else acc + v
+    cnt = (gh * gw).to(dt)
+    s = acc.reshape(R, C, ph, GH, pw, GW).sum(dim=(3, 5)) / cnt[:, None, None, None]
     if position_sensitive:
         co = C // (ph * pw)
         s = s.reshape(R, co, ph, pw, ph, pw)
-        i = torch.arange(ph, device=data.device)
-        j = torch.arange(pw, device=data.device)
+        i = torch.arange(ph, device=dev)
+        j = torch.arange(pw, device=dev)
         s = s[:, :, i[:, None], j[None, :], i[:, None], j[None, :]]
     return s
 

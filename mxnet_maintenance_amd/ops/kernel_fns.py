@@ -481,42 +481,75 @@ def _phase_taps(R, P, s, ph):
 def conv_dgrad_strided_ok(dy, w, stride, pad, xshape, bco=128):
     K, R, S, C = w.shape
     s = tuple(stride)
-    return (_CONV_HIP and s != (1, 1) and s[0] == s[1] and dy.dtype in (torch.float16, torch.bfloat16)
+    return (_CONV_HIP and s != (1, 1) and s[0] == s[1] and s[0] <= 2 and dy.dtype in (torch.float16, torch.bfloat16)
             and dy.dim() == 4 and K % 64 == 0 and C % bco == 0 and xshape[1] % s[0] == 0 and xshape[2] % s[1] == 0
             and dy.is_cuda and all(0 <= p < k for p, k in zip(pad, (R, S))))
 
 
+_PHASE_PLANS = {}
+
+
+def _phase_plan(wshape, stride, pad, device):
+    """Per (weight shape, stride, pad): the phases with taps [(ph, pw, R_i, S_i, pad_h, pad_w, w_off)], the
+    phases no tap reaches, and one gather index that builds every phase's weight slice
+    ([C][R_i][S_i][K], concatenated) from W [K][R][S][C] in a single kernel."""
+    key = (tuple(wshape), tuple(stride), tuple(pad), device)
+    plan = _PHASE_PLANS.get(key)
+    if plan is not None:
+        return plan
+    K, R, S, C = wshape
+    st = stride[0]
+    phases, empty, idx, off = [], [], [], 0
+    for ph in range(st):
+        th = _phase_taps(R, pad[0], st, ph)
+        for pw in range(st):
+            tw = _phase_taps(S, pad[1], st, pw)
+            if not th or not tw:
+                empty.append((ph, pw))
+                continue
+            dh = [d for d, _ in th]
+            dw = [d for d, _ in tw]
+            if dh != list(range(dh[0], dh[0] + len(dh))) or dw != list(range(dw[0], dw[0] + len(dw))):
+                raise ValueError('conv_dgrad_strided: non-contiguous phase taps')
+            rr = torch.tensor([r for _, r in th])
+            ss = torch.tensor([c for _, c in tw])
+            kk = torch.arange(K)
+            cc = torch.arange(C)
+            # element (c, i, j, k) of the slice <- W[k, rr[i], ss[j], c]
+            src = (((kk[None, None, None, :] * R + rr[None, :, None, None]) * S + ss[None, None, :, None]) * C
+                   + cc[:, None, None, None])
+            idx.append(src.reshape(-1))
+            phases.append((ph, pw, len(th), len(tw), -dh[0], -dw[0], off))
+            off += src.numel()
+    plan = (phases, empty, torch.cat(idx).to(device))
+    _PHASE_PLANS[key] = plan
+    return plan
+
+
 def conv_dgrad_strided(dy, w, stride, pad, xshape, bco=128):
-    """Data gradient of a stride-s conv as s*s sub-pixel phases (src/kernels/conv_glds.hip
-    conv_nhwc_dgrad_phase_glds): phase (ph, pw) of dX -- rows s*a + ph, columns s*b + pw -- is a
-    stride-1 conv of dY with the taps of W that reach it, written in place; phases no tap reaches
-    are zero.  No zero-stuffed dY and no scatter pass (cf. the reference's cuDNN backward-data,
+    """Data gradient of a stride-s conv as s*s sub-pixel phases in one launch (src/kernels/conv_glds.hip
+    conv_nhwc_dgrad_phases_glds): phase (ph, pw) of dX -- rows s*a + ph, columns s*b + pw -- is a
+    stride-1 conv of dY with the taps of W that reach it, written in place; the first phase's
+    epilogue also clears the phases no tap reaches (1x1 stride 2: 3 of 4).  No zero-stuffed dY and no scatter pass (cf. the reference's cuDNN backward-data,
     src/operator/nn/cudnn/cudnn_convolution-inl.h)."""
     K, R, S, C = w.shape
     N, H, W, _ = xshape
     st = stride[0]
     Ho, Wo = H // st, W // st
     dy = dy.contiguous()
+    phases, empty, gidx = _phase_plan(w.shape, stride, pad, w.device)
+    if len(phases) > 4:
+        raise ValueError('conv_dgrad_strided: at most 4 phases per launch')
     dx = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
-    lib = _K.lib()
-    wp = w.permute(3, 1, 2, 0)      # [C][R][S][K]
-    zero = _zero_page(dy.device).data_ptr()
-    for ph in range(st):
-        th = _phase_taps(R, pad[0], st, ph)
-        for pw in range(st):
-            tw = _phase_taps(S, pad[1], st, pw)
-            if not th or not tw:
-                dx.view(N, Ho, st, Wo, st, C)[:, :, ph, :, pw, :].zero_()
-                continue
-            dh = [d for d, _ in th]
-            dw = [d for d, _ in tw]
-            if dh != list(range(dh[0], dh[0] + len(dh))) or dw != list(range(dw[0], dw[0] + len(dw))):
-                raise ValueError('conv_dgrad_strided: non-contiguous phase taps')
-            wsub = wp.index_select(1, torch.tensor([r for _, r in th], device=w.device)) \
-                     .index_select(2, torch.tensor([r for _, r in tw], device=w.device)).contiguous()
-            lib.conv_nhwc_dgrad_phase_glds(_DT[dy.dtype], dy.data_ptr(), wsub.data_ptr(), dx.data_ptr(), zero, N,
-                                           dy.shape[1], dy.shape[2], K, C, len(th), len(tw), -dh[0], -dw[0], Ho, Wo,
-                                           st, ph, pw, bco, _stream())
+    if len(empty) > 3:
+        raise ValueError('conv_dgrad_strided: at most 3 phases without taps')
+    wsub = w.reshape(-1).index_select(0, gidx)
+    cols = list(zip(*phases))
+    _K.lib().conv_nhwc_dgrad_phases_glds(_DT[dy.dtype], dy.data_ptr(), wsub.data_ptr(), dx.data_ptr(),
+                                         _zero_page(dy.device).data_ptr(), N, dy.shape[1], dy.shape[2], K, C, Ho, Wo,
+                                         st, list(cols[0]), list(cols[1]), list(cols[2]), list(cols[3]),
+                                         list(cols[4]), list(cols[5]), list(cols[6]), [e[0] for e in empty],
+                                         [e[1] for e in empty], bco, _stream())
     return dx
 
 

@@ -930,6 +930,19 @@ def spatial_transformer(data, loc, target_shape=(0, 0), transform_type='affine',
     return out, grid, grid
 
 
+class _AbsGeZero(torch.autograd.Function):
+    """|d| with d/dd = +1 at d == 0 (the reference correlation's sign convention)."""
+    @staticmethod
+    def forward(ctx, d):
+        ctx.save_for_backward(d)
+        return d.abs()
+
+    @staticmethod
+    def backward(ctx, g):
+        d, = ctx.saved_tensors
+        return torch.where(d >= 0, g, -g)
+
+
 @register('Correlation', arg_names=('data1', 'data2'), num_outputs=3, num_visible_outputs=1,
           params={'kernel_size': ('int', 1), 'max_displacement': ('int', 1), 'stride1': ('int', 1),
                   'stride2': ('int', 1), 'pad_size': ('int', 0), 'is_multiply': ('bool', True)})
@@ -959,7 +972,7 @@ def correlation(data1, data2, kernel_size=1, max_displacement=1, stride1=1, stri
                 for kx in range(-kr, kr + 1):
                     a = p1[:, :, (ys + ky)][:, :, :, (xs + kx)]
                     b = p2[:, :, (ys + ky + s2y)][:, :, :, (xs + kx + s2x)]
-                    acc = acc + (a * b if is_multiply else torch.abs(a - b))
+                    acc = acc + (a * b if is_multiply else _AbsGeZero.apply(a - b))
             outs.append(acc.sum(1) / (kernel_size * kernel_size * c))
     out = torch.stack(outs, 1)
     return out, p1, p2

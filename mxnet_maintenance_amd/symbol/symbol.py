@@ -579,6 +579,8 @@ def _create(op_name, inputs, attrs, name=None, attr=None):
     node_attrs = {}
     for k, v in attrs.items():
         if v is None:
+            if k in op.params and str(op.params[k][0]).endswith('?') and op.params[k][1] is not None:
+                node_attrs[k] = 'None'      # explicit None overriding a non-None default (sort axis)
             continue
         node_attrs[k] = registry.format_value(v) if not isinstance(v, str) else v
     for k, v in (scope_attr or {}).items():
@@ -617,7 +619,8 @@ def _create(op_name, inputs, attrs, name=None, attr=None):
         if i in default_init and src.is_var() and '__init__' not in src.attrs:
             src.attrs['__init__'] = default_init[i]
     for s in pos[len(all_names):]:
-        entries.append(s._outputs[0])
+        if s is not None:       # e.g. an explicit None bias of a no_bias Convolution
+            entries.append(s._outputs[0])
     node.inputs = entries
     nvis = node.num_visible_outputs()
     out = Symbol([(node, i) for i in range(nvis)])
@@ -657,7 +660,10 @@ def _op_func(op_name):
             else:
                 extra_pos.append(a)
         named = {k: v for k, v in kwargs.items() if isinstance(v, Symbol)}
-        attrs = {k: v for k, v in kwargs.items() if not isinstance(v, Symbol) and v is not None}
+        # an explicit None for an optional parameter (e.g. sort axis=None: flatten) is kept
+        attrs = {k: v for k, v in kwargs.items() if not isinstance(v, Symbol) and (
+            v is not None or (k in op.params and isinstance(op.params[k][0], str) and op.params[k][0].endswith('?')
+                              and op.params[k][1] is not None))}
         if extra_pos:
             # positional attribute values follow the declared param order (as in the nd frontend)
             for p, v in zip([p for p in op.params if p not in attrs], extra_pos):

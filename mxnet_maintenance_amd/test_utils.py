@@ -402,7 +402,7 @@ def numeric_grad(executor, location, aux_states=None, eps=1e-4, use_forward_trai
         executor.arg_dict[name][:] = nd.array(point.astype(dtype), dtype=dtype)
         load_aux()
         executor.forward(is_train=use_forward_train)
-        return sum(float(o.asnumpy().astype(np.float64).sum()) for o in executor.outputs)
+        return [o.asnumpy().astype(np.float64) for o in executor.outputs]
 
     for name, val in location.items():
         executor.arg_dict[name][:] = val
@@ -419,7 +419,9 @@ def numeric_grad(executor, location, aux_states=None, eps=1e-4, use_forward_trai
             flat[i] = x0 - eps / 2.0
             down = total_output(point, name)
             flat[i] = x0
-            g[i] = (up - down) / eps
+            # elementwise differences first: unperturbed outputs cancel exactly, so the quotient
+            # does not inherit the rounding of a large sum
+            g[i] = sum(float((u - d).sum()) for u, d in zip(up, down)) / eps
         executor.arg_dict[name][:] = nd.array(point.astype(dtype), dtype=dtype)
         grads[name] = g.reshape(point.shape)
     return grads
@@ -447,7 +449,7 @@ def check_numeric_gradient(sym, location, aux_states=None, numeric_eps=None, rto
     input_shape = {k: v.shape for k, v in location.items()}
     _, out_shape, _ = sym.infer_shape(**input_shape)
     proj = sym_mod.var('__random_proj')
-    out = sym_mod.sum(sym * proj) if len(out_shape) == 1 else sym_mod.sum(sym_mod.Group(list(sym))[0] * proj)
+    out = (sym * proj) if len(out_shape) == 1 else (sym_mod.Group(list(sym))[0] * proj)
     out = sym_mod.make_loss(out)
     location = dict(list(location.items()) + [('__random_proj', nd.array(np.random.normal(0, 0.01,
                                                                                           size=out_shape[0]),

@@ -7,9 +7,11 @@
 // call; the launchers re-check the invariants they rely on.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include <cstdint>
 #include <stdexcept>
+#include <vector>
 
 namespace py = pybind11;
 
@@ -63,9 +65,11 @@ int conv_nhwc_fwd_big_bwd_nparts(int N, int H, int W, int R, int S, int sh, int 
 void conv_nhwc_fwd_glds(int dtype, const void* x, const void* w, const float* bias, void* y, const void* zero, int N,
                         int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int bco,
                         hipStream_t s);
-void conv_nhwc_dgrad_phase_glds(int dtype, const void* dy, const void* wsub, void* dx, const void* zero, int N,
-                                int Hi, int Wi, int Cin, int Cout, int R, int S, int pad_h, int pad_w, int Ho,
-                                int Wo, int stride, int ph, int pw, int bco, hipStream_t s);
+void conv_nhwc_dgrad_phases_glds(int dtype, const void* dy, const void* w, void* dx, const void* zero, int N, int Hi,
+                                 int Wi, int Cin, int Cout, int Ho, int Wo, int stride, int nph, const int* ph,
+                                 const int* pw, const int* R, const int* S, const int* pad_h, const int* pad_w,
+                                 const int64_t* w_off, int nzero, const int* zph, const int* zpw, int bco,
+                                 hipStream_t s);
 int conv_nhwc_fwd_ring_nparts(int N, int H, int W, int R, int S, int sh, int sw, int ph, int pw, int variant);
 void conv_nhwc_fwd_ring(int dtype, const void* x, const void* w, void* y, const void* zero, int N, int H, int W, int C,
                         int K, int R, int S, int sh, int sw, int ph, int pw, int variant, float* part, int nparts,
@@ -287,14 +291,22 @@ PYBIND11_MODULE(_hip_kernels, m) {
                        sh, sw, ph, pw, bco, S(s));
     check_launch("conv_nhwc_fwd_glds");
   });
-  // one sub-pixel phase of a strided data gradient, written in place into dX
-  m.def("conv_nhwc_dgrad_phase_glds", [](int dt, uintptr_t dy, uintptr_t wsub, uintptr_t dx, uintptr_t zero, int N,
-                                         int Hi, int Wi, int Cin, int Cout, int R, int Sf, int pad_h, int pad_w,
-                                         int Ho, int Wo, int stride, int ph, int pw, int bco, uintptr_t s) {
-    conv_nhwc_dgrad_phase_glds(dt, P<void>(dy), P<void>(wsub), P<void>(dx), P<void>(zero), N, Hi, Wi, Cin, Cout, R,
-                               Sf, pad_h, pad_w, Ho, Wo, stride, ph, pw, bco, S(s));
-    check_launch("conv_nhwc_dgrad_phase_glds");
-  });
+  // the sub-pixel phases of a strided data gradient, one launch, written in place into dX
+  m.def("conv_nhwc_dgrad_phases_glds",
+        [](int dt, uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t zero, int N, int Hi, int Wi, int Cin, int Cout,
+           int Ho, int Wo, int stride, std::vector<int> ph, std::vector<int> pw, std::vector<int> R,
+           std::vector<int> Sf, std::vector<int> pad_h, std::vector<int> pad_w, std::vector<int64_t> w_off,
+           std::vector<int> zph, std::vector<int> zpw, int bco, uintptr_t s) {
+          const size_t n = ph.size();
+          if (pw.size() != n || R.size() != n || Sf.size() != n || pad_h.size() != n || pad_w.size() != n ||
+              w_off.size() != n || zph.size() != zpw.size())
+            throw std::runtime_error("conv_nhwc_dgrad_phases_glds: per-phase lists differ in length");
+          conv_nhwc_dgrad_phases_glds(dt, P<void>(dy), P<void>(w), P<void>(dx), P<void>(zero), N, Hi, Wi, Cin, Cout,
+                                      Ho, Wo, stride, (int)n, ph.data(), pw.data(), R.data(), Sf.data(),
+                                      pad_h.data(), pad_w.data(), w_off.data(), (int)zph.size(), zph.data(),
+                                      zpw.data(), bco, S(s));
+          check_launch("conv_nhwc_dgrad_phases_glds");
+        });
   // 512-thread big-tile kernel: variant 0..3 = 256x256, 128x256, 64x512, 256x128 (co x pix);
   // part (optional): channel-major [2][K][nparts] BatchNorm sum / sum-of-squares partials of y
   m.def("conv_nhwc_fwd_big_nparts", &conv_nhwc_fwd_big_nparts);

@@ -78,6 +78,9 @@ struct GeomG {
   // output element offset of pixel p = q*Wo + wo (q = n*Ho + ho): q*og + wo*oc + ob (dense: Wo*K, K, 0);
   // a strided map lets a sub-pixel piece of a strided dgrad write its phase of dX in place
   int64_t og, oc, ob;
+  // phases of a strided dgrad no tap reaches: this phase also writes zeros at off - ob + zob[i]
+  int nz;
+  int64_t zob[3];
 };
 
 __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
@@ -85,9 +88,37 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
 }
 
 template <typename T, int BCO>
+__device__ __forceinline__ void glds_body(const T* __restrict__ x, const T* __restrict__ w,
+                                          const float* __restrict__ bias, T* __restrict__ y,
+                                          const T* __restrict__ zero, const GeomG& g, int tiles_co);
+
+template <typename T, int BCO>
 __global__ void __launch_bounds__(256) conv_fwd_glds_kernel(const T* __restrict__ x, const T* __restrict__ w,
                                                             const float* __restrict__ bias, T* __restrict__ y,
                                                             const T* __restrict__ zero, GeomG g, int tiles_co) {
+  glds_body<T, BCO>(x, w, bias, y, zero, g, tiles_co);
+}
+
+// All sub-pixel phases of a strided data gradient in one launch: blockIdx.y picks the phase (its
+// taps, padding, output offset and weight slice); phases share dY and the output dX.
+constexpr int kMaxPhases = 4;
+struct PhaseSet {
+  GeomG g[kMaxPhases];
+  int64_t w_off[kMaxPhases];   // element offset of the phase's weight slice
+};
+
+template <typename T, int BCO>
+__global__ void __launch_bounds__(256) conv_phase_glds_kernel(const T* __restrict__ dy, const T* __restrict__ w,
+                                                              T* __restrict__ dx, const T* __restrict__ zero,
+                                                              PhaseSet ps, int tiles_co) {
+  const int ph = blockIdx.y;
+  glds_body<T, BCO>(dy, w + ps.w_off[ph], nullptr, dx, zero, ps.g[ph], tiles_co);
+}
+
+template <typename T, int BCO>
+__device__ __forceinline__ void glds_body(const T* __restrict__ x, const T* __restrict__ w,
+                                          const float* __restrict__ bias, T* __restrict__ y,
+                                          const T* __restrict__ zero, const GeomG& g, int tiles_co) {
   constexpr int WAVES_CO = BCO / 64;
   constexpr int WAVES_PIX = 4 / WAVES_CO;
   constexpr int BPIX = WAVES_PIX * 64;
@@ -219,6 +250,7 @@ __global__ void __launch_bounds__(256) conv_fwd_glds_kernel(const T* __restrict_
         const int q = p / g.Wo;
         const int64_t off = q * g.og + (p - q * g.Wo) * g.oc + g.ob;
         *reinterpret_cast<uint2*>(y + off + co) = v;
+        for (int z = 0; z < g.nz; ++z) *reinterpret_cast<uint2*>(y + off - g.ob + g.zob[z] + co) = uint2{0u, 0u};
       }
     }
   }
@@ -251,6 +283,7 @@ void conv_nhwc_fwd_glds(int dtype, const void* x, const void* w, const float* bi
   g.og = (int64_t)g.Wo * K;
   g.oc = K;
   g.ob = 0;
+  g.nz = 0;
   MXAMD_HOST_CHECK(C % 64 == 0 && K % bco == 0 && (bco == 64 || bco == 128),
                    "conv_nhwc_fwd_glds: need Cin % 64 == 0 and Cout % BCO == 0");
   MXAMD_HOST_CHECK((int64_t)N * H * W * C < (1ll << 31) && (int64_t)g.M * K < (1ll << 31) &&
@@ -267,39 +300,62 @@ void conv_nhwc_fwd_glds(int dtype, const void* x, const void* w, const float* bi
   }
 }
 
-// One sub-pixel phase (ph, pw) of a stride-s data gradient: dX[n, s*a + ph, s*b + pw, :] for all (a, b),
-// as a stride-1 conv of dY (N x Hi x Wi x Cin, Cin = the conv's output channels) with the phase's taps
-// wsub [Cout][R][S][Cin] (R x S = taps of that phase, offsets -pad_h/-pad_w, possibly negative) into an
-// Ho x Wo grid written in place inside dX (Hx x Wx x Cout, Hx = s*Ho, Wx = s*Wo).
-void conv_nhwc_dgrad_phase_glds(int dtype, const void* dy, const void* wsub, void* dx, const void* zero, int N,
-                                int Hi, int Wi, int Cin, int Cout, int R, int S, int pad_h, int pad_w, int Ho,
-                                int Wo, int stride, int ph, int pw, int bco, hipStream_t s) {
-  GeomG g;
-  g.N = N; g.H = Hi; g.W = Wi; g.C = Cin; g.K = Cout; g.R = R; g.S = S;
-  g.sh = 1; g.sw = 1; g.ph = pad_h; g.pw = pad_w;
-  g.Ho = Ho;
-  g.Wo = Wo;
-  g.M = N * Ho * Wo;
-  g.Ktot = R * S * Cin;
+// The sub-pixel phases of a stride-s data gradient in one launch.  Phase i writes dX[n, s*a + ph_i,
+// s*b + pw_i, :] for all (a, b) (an Ho x Wo grid, Hx = s*Ho, Wx = s*Wo) as a stride-1 conv of dY
+// (N x Hi x Wi x Cin, Cin = the conv's output channels) with its taps: weight slice w + w_off[i]
+// laid out [Cout][R_i][S_i][Cin], tap offsets -pad_h[i] / -pad_w[i] (possibly negative).
+void conv_nhwc_dgrad_phases_glds(int dtype, const void* dy, const void* w, void* dx, const void* zero, int N, int Hi,
+                                 int Wi, int Cin, int Cout, int Ho, int Wo, int stride, int nph, const int* ph,
+                                 const int* pw, const int* R, const int* S, const int* pad_h, const int* pad_w,
+                                 const int64_t* w_off, int nzero, const int* zph, const int* zpw, int bco,
+                                 hipStream_t s) {
+  MXAMD_HOST_CHECK(nph >= 1 && nph <= kMaxPhases, "conv_nhwc_dgrad_phases_glds: 1..4 phases");
+  MXAMD_HOST_CHECK(nzero >= 0 && nzero <= 3, "conv_nhwc_dgrad_phases_glds: at most 3 zero phases");
+  MXAMD_HOST_CHECK(Cin % 64 == 0 && Cout % bco == 0 && (bco == 64 || bco == 128) && stride >= 1 && Ho > 0 &&
+                       Wo > 0,
+                   "conv_nhwc_dgrad_phases_glds: need Cin % 64 == 0 and Cout % BCO == 0");
+  MXAMD_HOST_CHECK((int64_t)N * Hi * Wi * Cin < (1ll << 31), "conv_nhwc_dgrad_phases_glds: dY too large");
+  PhaseSet ps;
   const int64_t Wx = (int64_t)stride * Wo;
-  g.og = stride * Wx * Cout;
-  g.oc = (int64_t)stride * Cout;
-  g.ob = ((int64_t)ph * Wx + pw) * Cout;
-  MXAMD_HOST_CHECK(Cin % 64 == 0 && Cout % bco == 0 && (bco == 64 || bco == 128) && stride >= 1 && ph >= 0 &&
-                       ph < stride && pw >= 0 && pw < stride && Ho > 0 && Wo > 0,
-                   "conv_nhwc_dgrad_phase_glds: need Cin % 64 == 0, Cout % BCO == 0 and a valid phase");
-  MXAMD_HOST_CHECK((int64_t)N * Hi * Wi * Cin < (1ll << 31) && (int64_t)Cout * g.Ktot < (1ll << 31) &&
-                       (int64_t)N * stride * Ho * Wx * Cout < (1ll << 62),
-                   "conv_nhwc_dgrad_phase_glds: tensor too large for 32-bit indexing");
-  if (dtype == kF16) {
-    if (bco == 128) launch_glds<__half, 128>(dy, wsub, nullptr, dx, zero, g, s);
-    else launch_glds<__half, 64>(dy, wsub, nullptr, dx, zero, g, s);
-  } else if (dtype == kBF16) {
-    if (bco == 128) launch_glds<__hip_bfloat16, 128>(dy, wsub, nullptr, dx, zero, g, s);
-    else launch_glds<__hip_bfloat16, 64>(dy, wsub, nullptr, dx, zero, g, s);
-  } else {
-    throw std::runtime_error("conv_nhwc_dgrad_phase_glds: dtype must be f16 or bf16");
+  for (int i = 0; i < nph; ++i) {
+    MXAMD_HOST_CHECK(ph[i] >= 0 && ph[i] < stride && pw[i] >= 0 && pw[i] < stride && R[i] > 0 && S[i] > 0,
+                     "conv_nhwc_dgrad_phases_glds: bad phase");
+    GeomG& g = ps.g[i];
+    g.N = N; g.H = Hi; g.W = Wi; g.C = Cin; g.K = Cout; g.R = R[i]; g.S = S[i];
+    g.sh = 1; g.sw = 1; g.ph = pad_h[i]; g.pw = pad_w[i];
+    g.Ho = Ho;
+    g.Wo = Wo;
+    g.M = N * Ho * Wo;
+    g.Ktot = R[i] * S[i] * Cin;
+    g.og = stride * Wx * Cout;
+    g.oc = (int64_t)stride * Cout;
+    g.ob = ((int64_t)ph[i] * Wx + pw[i]) * Cout;
+    ps.w_off[i] = w_off[i];
+    g.nz = i == 0 ? nzero : 0;    // the first phase's blocks also clear the phases no tap reaches
+    for (int z = 0; z < nzero && i == 0; ++z) {
+      MXAMD_HOST_CHECK(zph[z] >= 0 && zph[z] < stride && zpw[z] >= 0 && zpw[z] < stride,
+                       "conv_nhwc_dgrad_phases_glds: bad zero phase");
+      g.zob[z] = ((int64_t)zph[z] * Wx + zpw[z]) * Cout;
+    }
+    MXAMD_HOST_CHECK((int64_t)Cout * g.Ktot < (1ll << 31), "conv_nhwc_dgrad_phases_glds: weight too large");
   }
+  const int bpix = bco == 128 ? 128 : 256;
+  const int tiles_co = Cout / bco;
+  const int tiles_pix = (N * Ho * Wo + bpix - 1) / bpix;
+  dim3 grid(tiles_co * tiles_pix, nph);
+#define MXAMD_PHASES(T, B)                                                                                  \
+  hipLaunchKernelGGL((conv_phase_glds_kernel<T, B>), grid, dim3(256), 0, s, static_cast<const T*>(dy),     \
+                     static_cast<const T*>(w), static_cast<T*>(dx), static_cast<const T*>(zero), ps, tiles_co)
+  if (dtype == kF16) {
+    if (bco == 128) MXAMD_PHASES(__half, 128);
+    else MXAMD_PHASES(__half, 64);
+  } else if (dtype == kBF16) {
+    if (bco == 128) MXAMD_PHASES(__hip_bfloat16, 128);
+    else MXAMD_PHASES(__hip_bfloat16, 64);
+  } else {
+    throw std::runtime_error("conv_nhwc_dgrad_phases_glds: dtype must be f16 or bf16");
+  }
+#undef MXAMD_PHASES
 }
 
 }  // namespace mxamd

@@ -68,8 +68,8 @@ def test_phase_taps_reproduce_conv_transpose(case):
 @pytest.mark.parametrize('bco', [128, 64])
 def test_strided_dgrad_kernel_matches_fp32(case, dtype, bco):
     N, H, W, C, K, R, s, p = case
-    if H % s or W % s:
-        pytest.skip('phase grid needs H, W divisible by the stride')
+    if H % s or W % s or C % bco or s > 2:
+        pytest.skip('phase grid needs H, W divisible by the stride and C by the tile')
     torch.manual_seed(1)
     Ho = (H + 2 * p - R) // s + 1
     Wo = (W + 2 * p - R) // s + 1
@@ -81,3 +81,19 @@ def test_strided_dgrad_kernel_matches_fp32(case, dtype, bco):
     ref = _ref_dx(dy.cpu().float(), w.cpu().float(), s, p, (N, H, W, C))
     err = (got.float().cpu().double() - ref).abs().max() / ref.abs().max()
     assert err < (1e-2 if dtype == torch.float16 else 3e-2), float(err)
+
+
+def test_phase_plan_gather_builds_tap_slices():
+    K, R, S, C = 64, 3, 3, 32
+    w = torch.randn(K, R, S, C)
+    phases, empty, gidx = KF._phase_plan(w.shape, (2, 2), (1, 1), w.device)
+    assert not empty and len(phases) == 4
+    flat = w.reshape(-1).index_select(0, gidx)
+    wp = w.permute(3, 1, 2, 0)
+    for ph, pw, r, s, _, _, off in phases:
+        rr = [t for _, t in KF._phase_taps(R, 1, 2, ph)]
+        ss = [t for _, t in KF._phase_taps(S, 1, 2, pw)]
+        want = wp[:, rr][:, :, ss].reshape(-1)
+        torch.testing.assert_close(flat[off:off + want.numel()], want)
+    phases, empty, _ = KF._phase_plan((64, 1, 1, 32), (2, 2), (0, 0), w.device)
+    assert len(phases) == 1 and sorted(empty) == [(0, 1), (1, 0), (1, 1)]
