@@ -127,6 +127,16 @@ def _add_touch_hook(v, t):
     t._mxamd_touch_hook = True
 
 
+def _zero_marked_grads():
+    """Backward of recorded heads with no differentiable path: 'write' gradients of the recorded
+    variables become zero and each is marked fresh."""
+    leaves = _collect_leaves(False)
+    _prepare_leaves(leaves)
+    for v in leaves:
+        if v._grad is not None:
+            v._fresh_grad = True
+
+
 def _prepare_leaves(leaves):
     """Zero 'write' buffers (grouped in one multi-tensor launch) and rebind stale .grad."""
     zero = []
@@ -191,6 +201,11 @@ def backward(heads, head_grads=None, retain_graph=False, train_mode=True, create
         tensors.append(t)
         hg = None if head_grads is None else head_grads[i]
         grads.append(torch.ones_like(t) if hg is None else hg._data.to(t.dtype))
+    if not tensors and heads and all(getattr(h, '_recorded', False) for h in heads):
+        # recorded outputs without a differentiable path (integer results, constant outputs): the
+        # marked variables get zero gradients, as the reference's backward writes them
+        _zero_marked_grads()
+        return
     if not tensors:
         raise MXNetError('Cannot differentiate node because it is not in a computational graph. '
                          'You need to set is_recording to true or use autograd.record() to save '

@@ -617,6 +617,9 @@ class HybridBlock(Block):
         else:
             outs = self._cached_op(feed, ctx.torch_device)
         outs = [NDArray(o) for o in outs]
+        if _state.STATE.recording:
+            for o in outs:
+                o._recorded = True
         if _state.STATE.np_array:
             from ..numpy import _np_out
             outs = _np_out(outs)

@@ -53,7 +53,7 @@ def _wrap(t):
 class NDArray:
     """An n-dimensional array on a :class:`Context`."""
     __slots__ = ('_data', '_grad', '_grad_req', '_stype', '__weakref__', '_fresh_grad', '_arena', '_host_ctx',
-                 '_exc')
+                 '_exc', '_recorded', '_idt')
     __array_priority__ = 1000.0
 
     def __init__(self, data, ctx=None, dtype=None, stype='default', writable=True):
@@ -95,7 +95,7 @@ class NDArray:
 
     @property
     def dtype(self):
-        return np_dtype(self._data.dtype)
+        return np_dtype(getattr(self, '_idt', None) or self._data.dtype)
 
     @property
     def stype(self):
@@ -221,6 +221,9 @@ class NDArray:
     def asnumpy(self):
         self._rethrow()
         t = self._data.detach()
+        idt = getattr(self, '_idt', None)
+        if idt is not None:
+            t = t.to(idt)       # an integer variable carried in float64 for autograd
         if t.dtype == torch.bfloat16:
             t = t.float()
         return t.cpu().numpy().copy() if t.device.type == 'cpu' else t.cpu().numpy()
@@ -327,10 +330,18 @@ class NDArray:
             self._grad_req = None
             return
         if not t.is_floating_point():
-            # integer arrays get a gradient buffer too (as in the reference); autograd cannot flow
-            # into them, so it stays zero
+            # integer (and bool) variables differentiate as in the reference: the values are carried
+            # in float64 (exact for the integers tests use) with the integer dtype kept in _idt;
+            # operators on them compute the integer result and take the gradient path from the
+            # float copy (register.invoke), and the gradient reports the integer dtype too
+            idt = getattr(self, '_idt', None) or t.dtype
+            t = t.to(torch.float64).requires_grad_(True)
             self._data = t
+            self._idt = idt
             self._grad = NDArray(torch.zeros_like(t))
+            self._grad._idt = idt
+            if self.__class__ is not NDArray:
+                self._grad.__class__ = self.__class__
             self._grad_req = grad_req
             return
         t.requires_grad_(True)

@@ -135,6 +135,39 @@ def _placeholder(attrs, inputs):
     return torch.zeros(shape, dtype=td, device=dev)
 
 
+def _shadowed(arrays):
+    return any(x is not None and getattr(x, '_idt', None) is not None for x in arrays)
+
+
+def _true_inputs(arrays):
+    return [None if x is None else (x._data.detach().to(x._idt) if getattr(x, '_idt', None) is not None
+                                    else x._data) for x in arrays]
+
+
+def _merge_shadow(res_f, res_t):
+    """Outputs of an operator on integer variables (see NDArray.attach_grad): the integer-input
+    result's values and dtype, the float copy's gradient path.  Returns (tensor, int dtype or None)."""
+    if not isinstance(res_f, torch.Tensor) or not res_f.requires_grad or not res_f.is_floating_point():
+        return res_t, None
+    if res_t.is_floating_point() or res_t.is_complex():
+        return res_f.to(res_t.dtype) + (res_t - res_f.to(res_t.dtype)).detach(), None
+    return res_f + (res_t.to(res_f.dtype) - res_f).detach(), res_t.dtype
+
+
+def _run_shadow(fn, inputs, kw):
+    """Run ``fn`` on arrays some of which are integer variables carried in float64."""
+    with torch.no_grad():
+        res_t = fn(*_true_inputs(inputs), **kw)
+    if not _state.STATE.recording:
+        return res_t, None
+    res_f = _run(fn, [None if x is None else x._data for x in inputs], kw)
+    if isinstance(res_t, (tuple, list)):
+        pairs = [_merge_shadow(f, t) for f, t in zip(res_f, res_t)]
+        return type(res_t)(p[0] for p in pairs), [p[1] for p in pairs]
+    r, idt = _merge_shadow(res_f, res_t)
+    return r, idt
+
+
 def invoke(op, inputs, attrs, out=None):
     """Run ``op`` on NDArray ``inputs`` with parsed ``attrs``.
 
@@ -149,8 +182,11 @@ def invoke(op, inputs, attrs, out=None):
     if sampler and box is None:
         from .. import engine
         box = engine.rng_failure()
+    idts = None
     try:
-        if _profiler.active_imperative:
+        if _shadowed(inputs) and not _amp.active:
+            res, idts = _run_shadow(op.fn, inputs, attrs)
+        elif _profiler.active_imperative:
             with _profiler.op_span(_profiler.current_scope() + op.name):
                 res = _run(op.fn, tin, attrs)
         else:
@@ -175,6 +211,13 @@ def invoke(op, inputs, attrs, out=None):
     else:
         outs = [NDArray(res)]
     _np_wrap(inputs, outs)
+    if idts is not None:
+        for o, d in zip(outs, idts if isinstance(idts, list) else [idts]):
+            if d is not None:
+                o._idt = d
+    if _state.STATE.recording:
+        for o in outs:
+            o._recorded = True
     if _profiler.active_memory and out is None:
         for o in outs:
             _profiler.memory_alloc(o)
@@ -210,8 +253,16 @@ def invoke_by_name(name, args, kwargs):
 def invoke_fn(fn, arrays):
     """Run an ad-hoc torch function (reshape, astype, ...) with autograd semantics."""
     _note_leaves(arrays)
-    res = _run(fn, [a._data for a in arrays], {})
+    idt = None
+    if _shadowed(arrays):
+        res, idt = _run_shadow(fn, arrays, {})
+    else:
+        res = _run(fn, [a._data for a in arrays], {})
     out = _np_wrap(arrays, [NDArray(res)])[0]
+    if idt is not None:
+        out._idt = idt
+    if _state.STATE.recording:
+        out._recorded = True
     box = _failed_input(arrays)
     if box is not None:
         out._exc = box

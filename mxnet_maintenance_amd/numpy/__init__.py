@@ -31,3 +31,10 @@ def set_module(name):
         f.__module__ = name
         return f
     return deco
+
+
+def __getattr__(name):
+    if name == '_Symbol':       # mx.sym.np._Symbol: the Symbol class np-mode graphs are built from
+        from ..symbol.symbol import Symbol
+        return Symbol
+    raise AttributeError("module 'mxnet.numpy' has no attribute '%s'" % name)

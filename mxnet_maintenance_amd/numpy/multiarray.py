@@ -16,6 +16,8 @@ import numbers
 import numpy as onp
 import torch
 
+from ..base import MXNetError
+
 from .. import _state
 from ..base import numeric_types, torch_dtype
 from ..context import current_context
@@ -58,7 +60,11 @@ def _call(name, *inputs, **attrs):
     """Invoke registered op ``name`` imperatively, or build a graph node for Symbol inputs."""
     if _FORCE_SYM[0] or builtins.any(_is_sym(x) for x in inputs):
         from ..symbol.symbol import _op_func
-        attrs = {k: v for k, v in attrs.items() if v is not None}
+        spec = _registry.get(name).params
+
+        def keep(k, v):     # an explicit None overriding a non-None optional default (sort axis=None)
+            return v is not None or (k in spec and str(spec[k][0]).endswith('?') and spec[k][1] is not None)
+        attrs = {k: v for k, v in attrs.items() if keep(k, v)}
         if 'dtype' in attrs and not isinstance(attrs['dtype'], str):
             attrs['dtype'] = _dtype_name(attrs['dtype'])
         return _op_func(name)(*inputs, **attrs)
@@ -618,12 +624,16 @@ def full_like(a, fill_value, dtype=None, order='C', ctx=None, out=None):
 def arange(start, stop=None, step=1, dtype=None, ctx=None):
     if stop is None:
         start, stop = 0, start
+    if step is None:
+        step = 1
     return _call('_npi_arange', start=float(start), stop=float(stop), step=float(step), ctx=_ctx(ctx),
                  dtype=dtype or 'float32')
 
 
 @_export
 def linspace(start, stop, num=50, endpoint=True, retstep=False, dtype=None, axis=0, ctx=None):
+    if int(num) != num or num < 0:
+        raise MXNetError('linspace: num must be a non-negative integer, got %r' % (num,))
     r = _call('_npi_linspace', start=float(start), stop=float(stop), num=int(num), endpoint=endpoint,
               ctx=_ctx(ctx), dtype=dtype or 'float32')
     if retstep:
@@ -708,10 +718,34 @@ def _binary(name, x1, x2, out=None):
     return _call('_npi_' + name, _as_nd(x1, ctx), _as_nd(x2, ctx), out=out)
 
 
+def _ufunc_kwargs(kwargs):
+    """The ufunc keywords mx.np does not implement (reference numpy/multiarray.py _ufunc_helper
+    callers): where/subok/casting/order other than their defaults and any dtype raise
+    NotImplementedError; an unparseable dtype raises TypeError."""
+    if 'dtype' in kwargs and kwargs['dtype'] is not None:
+        try:
+            onp.dtype(kwargs['dtype'])
+        except TypeError:
+            raise
+        raise NotImplementedError('dtype is not supported by mx.np ufuncs')
+    if kwargs.get('where', True) is not True:
+        raise NotImplementedError('where is not supported by mx.np ufuncs')
+    if kwargs.get('subok', True) is not True:
+        raise NotImplementedError('subok is not supported by mx.np ufuncs')
+    casting = kwargs.get('casting', 'same_kind')
+    if casting not in ('no', 'equiv', 'safe', 'same_kind', 'unsafe'):
+        raise TypeError('casting must be one of no, equiv, safe, same_kind, unsafe')
+    if casting != 'same_kind':
+        raise NotImplementedError('casting other than same_kind is not supported by mx.np ufuncs')
+    if kwargs.get('order', 'K') != 'K':
+        raise NotImplementedError('order other than K is not supported by mx.np ufuncs')
+
+
 def _mk_unary(name, opname=None):
     opname = opname or name
 
     def f(x, out=None, **kwargs):
+        _ufunc_kwargs(kwargs)
         return _unary(opname, x, out)
     f.__name__ = name
     f.__doc__ = 'Element-wise ``%s`` (NumPy semantics).' % name
@@ -723,6 +757,7 @@ def _mk_binary(name, opname=None):
     opname = opname or name
 
     def f(x1, x2, out=None, **kwargs):
+        _ufunc_kwargs(kwargs)
         return _binary(opname, x1, x2, out)
     f.__name__ = name
     f.__doc__ = 'Element-wise ``%s`` with broadcasting (NumPy semantics).' % name
@@ -1093,10 +1128,17 @@ def column_stack(tup):
     return _call('_npi_column_stack', *[_as_nd(x) for x in tup])
 
 
+def _atleast_sym(n, arys):
+    r = [_call('_npi_atleast_%dd' % n, a) for a in arys]
+    return r[0] if len(r) == 1 else r
+
+
 def _split_call(name, ary, ios, axis):
     ios = ios.tolist() if isinstance(ios, NDArray) else ios
     ios = list(ios) if isinstance(ios, (list, tuple)) else int(ios)
     r = _call('_npi_' + name, ary, indices_or_sections=ios, axis=axis)
+    if _is_sym(r):
+        return [r[i] for i in range(len(r.list_outputs()))]
     return list(r) if isinstance(r, (list, tuple)) else [r]
 
 
@@ -1127,12 +1169,16 @@ def dsplit(ary, indices_or_sections):
 
 @_export
 def atleast_1d(*arys):
+    if _FORCE_SYM[0] or builtins.any(_is_sym(a) for a in arys):
+        return _atleast_sym(1, arys)
     r = [a if a.ndim >= 1 else reshape(a, (1,)) for a in map(_as_nd, arys)]
     return r[0] if len(r) == 1 else r
 
 
 @_export
 def atleast_2d(*arys):
+    if _FORCE_SYM[0] or builtins.any(_is_sym(a) for a in arys):
+        return _atleast_sym(2, arys)
     r = []
     for a in map(_as_nd, arys):
         r.append(a if a.ndim >= 2 else reshape(a, (1, -1) if a.ndim == 1 else (1, 1)))
@@ -1141,6 +1187,8 @@ def atleast_2d(*arys):
 
 @_export
 def atleast_3d(*arys):
+    if _FORCE_SYM[0] or builtins.any(_is_sym(a) for a in arys):
+        return _atleast_sym(3, arys)
     r = []
     for a in map(_as_nd, arys):
         if a.ndim == 0:

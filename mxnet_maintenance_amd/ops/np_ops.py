@@ -114,6 +114,15 @@ def _fbin(f):
     return g
 
 
+def _sub(a, b):
+    # numpy: a bool operand is promoted to the other's type (bool - bool is a TypeError there too)
+    if a.dtype == torch.bool and b.dtype != torch.bool:
+        a = a.to(b.dtype)
+    elif b.dtype == torch.bool and a.dtype != torch.bool:
+        b = b.to(a.dtype)
+    return torch.sub(a, b)
+
+
 def _floor_divide(a, b):
     return torch.floor_divide(a, b)
 
@@ -136,7 +145,7 @@ def _heaviside(a, b):
 
 
 _BINARY = {
-    'add': torch.add, 'subtract': torch.sub, 'multiply': torch.mul, 'true_divide': torch.true_divide,
+    'add': torch.add, 'subtract': _sub, 'multiply': torch.mul, 'true_divide': torch.true_divide,
     'floor_divide': _floor_divide, 'mod': _mod, 'fmod': torch.fmod, 'power': _power,
     'maximum': torch.maximum, 'minimum': torch.minimum, 'fmax': torch.fmax, 'fmin': torch.fmin,
     'arctan2': _fbin(torch.atan2), 'hypot': _fbin(torch.hypot), 'copysign': _fbin(torch.copysign),
@@ -211,7 +220,9 @@ def _prod(a, axis=None, keepdims=False, dtype=None, initial=None):
 def _mean(a, axis=None, keepdims=False, dtype=None):
     dt = _td(dtype) or (a.dtype if a.is_floating_point() else _FLOAT)
     d = _red_dims(a, axis)
-    return torch.mean(a.to(dt), dim=d, keepdim=keepdims) if d else a.to(dt).clone()
+    acc = dt if dt.is_floating_point else torch.float64     # integer dtype: float mean, then cast
+    r = torch.mean(a.to(acc), dim=d, keepdim=keepdims) if d else a.to(acc).clone()
+    return r.to(dt)
 
 
 def _std_var(fn):
@@ -390,7 +401,10 @@ def _linspace(start=0.0, stop=1.0, num=50, endpoint=True, ctx=None, dtype='float
         r = torch.linspace(start, stop, num, dtype=torch.float64)
     else:
         r = start + (stop - start) / max(num, 1) * torch.arange(num, dtype=torch.float64)
-    return r.to(_td(dtype, _FLOAT)).to(_dev(ctx))
+    dt = _td(dtype, _FLOAT)
+    if not (dt.is_floating_point or dt.is_complex):
+        r = torch.floor(r)          # numpy floors integer linspace
+    return r.to(dt).to(_dev(ctx))
 
 
 @register('_npi_logspace', arg_names=(), params={'start': ('float', 0.0), 'stop': ('float', 1.0), 'num': ('int', 50),
@@ -440,6 +454,8 @@ def _reshape(a, newshape=(), order='C'):
 
 @register('_np_transpose', aliases=('_npi_transpose',), arg_names=('a',), params={'axes': ('shape?', None)})
 def _transpose(a, axes=None):
+    if a.dim() == 0:
+        return a.clone()
     if not axes:
         axes = tuple(reversed(range(a.dim())))
     return a.permute(*[x % a.dim() for x in axes])
@@ -479,6 +495,8 @@ def _expand_dims(a, axis=0):
 def _squeeze(a, axis=None):
     if axis is None:
         return a.squeeze()
+    if a.dim() == 0:
+        return a.clone()        # numpy accepts axis 0 / -1 on a 0-d array
     for ax in sorted(_axes(axis, a.dim()), reverse=True):
         if a.shape[ax] != 1:
             raise ValueError('cannot select an axis to squeeze out which has size not equal to one')
@@ -531,11 +549,15 @@ def _ravel(a, order='C'):
 
 @register('_npi_tril', arg_names=('a',), params={'k': ('int', 0)})
 def _tril(a, k=0):
+    if a.dim() == 1:        # numpy: a vector is broadcast to its square matrix first
+        a = a.unsqueeze(0).expand(a.shape[0], a.shape[0])
     return torch.tril(a, k)
 
 
 @register('_npi_triu', arg_names=('a',), params={'k': ('int', 0)})
 def _triu(a, k=0):
+    if a.dim() == 1:
+        a = a.unsqueeze(0).expand(a.shape[0], a.shape[0])
     return torch.triu(a, k)
 
 
@@ -679,6 +701,11 @@ def _atleast(t, n):
     while t.dim() < n:
         t = t.unsqueeze(0) if n < 3 or t.dim() == 0 else (t.unsqueeze(0).unsqueeze(-1) if t.dim() == 1 else t.unsqueeze(-1))
     return t
+
+
+for _nd in (1, 2, 3):
+    register('_npi_atleast_%dd' % _nd, arg_names=('a',))(lambda a, _nd=_nd: _atleast(a, _nd).clone()
+                                                       if a.dim() >= _nd else _atleast(a, _nd))
 
 
 @register('_npi_vstack', aliases=('_npi_row_stack',), arg_names=lambda a: ['data%d' % i for i in range(int(a.get('num_args', 1)))],

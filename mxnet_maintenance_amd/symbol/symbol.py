@@ -397,6 +397,10 @@ class Symbol:
             if name != 'astype' and registry.has(name) and registry.get(name) is registry.get(opname):
                 opname = name      # the alias the method is named after also names the node (split0)
 
+            from .. import util as _util
+            if name == 'flatten' and _util.is_np_array() and not getattr(self, '_legacy', False):
+                return lambda *a, **k: _op_func('_npi_ravel')(self)     # ndarray.flatten: 1-D copy
+
             def f(*a, **k):
                 if name == 'reshape' and a:
                     k['shape'] = a[0] if len(a) == 1 and isinstance(a[0], (tuple, list)) else a
@@ -409,6 +413,15 @@ class Symbol:
                     a = ()
                 return _op_func(opname)(self, *a, **k)
             return f
+        if name.startswith('_'):
+            raise AttributeError(name)
+        if not vars(self).get('_legacy', False):
+            # np-style symbols take the mx.np functions as methods (x.cumsum(axis=...), x.clip(...))
+            from .. import numpy as _mnp
+            meth = _mnp.ndarray.__dict__.get(name)      # only ndarray *methods*, never properties
+            fn = getattr(_mnp, name, None) if callable(meth) and not isinstance(meth, property) else None
+            if callable(fn) and not isinstance(fn, type):
+                return lambda *a, **k: fn(self, *a, **k)
         raise AttributeError("'Symbol' object has no attribute '%s'" % name)
 
     # ----------------------------------------------------------- inference
