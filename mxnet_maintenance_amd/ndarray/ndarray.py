@@ -936,7 +936,15 @@ def moveaxis(tensor, source, destination):
             if not -tensor.ndim <= ax < tensor.ndim:
                 raise ValueError('moveaxis: axis %d is out of bounds for an array of dimension %d' % (ax, tensor.ndim))
         return tuple(a) if isinstance(a, (list, tuple, range)) else a
-    return NDArray(torch.movedim(tensor._data, norm(source), norm(destination)).contiguous())
+    src, dst = norm(source), norm(destination)
+    s_list = src if isinstance(src, tuple) else (src,)
+    d_list = dst if isinstance(dst, tuple) else (dst,)
+    if len(s_list) != len(d_list):
+        raise ValueError('moveaxis: source and destination must have the same number of elements')
+    for lst, what in ((s_list, 'source'), (d_list, 'destination')):
+        if len({a % tensor.ndim for a in lst}) != len(lst):
+            raise ValueError('moveaxis: repeated axis in %s' % what)
+    return NDArray(torch.movedim(tensor._data, src, dst).contiguous())
 
 
 def waitall():

@@ -866,6 +866,7 @@ def _topk_nout(a):
           params={'axis': ('int?', -1), 'k': ('int', 1), 'ret_typ': ('str', 'indices'),
                   'is_ascend': ('bool', False), 'dtype': ('str', 'float32')})
 def topk(data, axis=-1, k=1, ret_typ='indices', is_ascend=False, dtype='float32'):
+    shape = data.shape
     if axis is None:
         data, axis = data.reshape(-1), 0
     if k <= 0:
@@ -878,7 +879,7 @@ def topk(data, axis=-1, k=1, ret_typ='indices', is_ascend=False, dtype='float32'
     if ret_typ == 'mask':
         m = torch.zeros_like(data)
         m.scatter_(axis, i, 1)
-        return m
+        return m.reshape(shape)     # the mask has the input's shape (also for axis=None)
     return v, i.to(torch_dtype(dtype))
 
 
