@@ -317,8 +317,12 @@ def _average(a, weights=None, axis=None, returned=False, weighted=False):
 @register('_npi_quantile', arg_names=('a',), params={'q': ('any', 0.5), 'axis': ('axis', None),
                                                      'interpolation': ('str', 'linear'), 'keepdims': ('bool', False)})
 def _quantile(a, q=0.5, axis=None, interpolation='linear', keepdims=False):
-    qt = torch.as_tensor(q, dtype=_fl(a).dtype, device=a.device)
-    x = _fl(a)
+    if a.dtype not in (torch.float32, torch.float64):
+        # torch.quantile takes float/double only: half and integer inputs go through float64
+        out_dt = a.dtype if a.is_floating_point() else _FLOAT
+        return _quantile(a.double(), q, axis, interpolation, keepdims).to(out_dt)
+    qt = torch.as_tensor(q, dtype=a.dtype, device=a.device)
+    x = a
     if axis is None:
         r = torch.quantile(x.reshape(-1), qt, interpolation=interpolation)
         if keepdims:
@@ -326,9 +330,12 @@ def _quantile(a, q=0.5, axis=None, interpolation='linear', keepdims=False):
         return r
     if isinstance(axis, tuple):
         if len(axis) != 1:
-            keep = [i for i in range(x.dim()) if i not in _axes(axis, x.dim())]
-            x = x.permute(keep + list(_axes(axis, x.dim()))).reshape([x.shape[i] for i in keep] + [-1])
-            return torch.quantile(x, qt, dim=-1, interpolation=interpolation)
+            red = _axes(axis, x.dim())
+            keep = [i for i in range(x.dim()) if i not in red]
+            full = [1 if i in red else x.shape[i] for i in range(x.dim())]
+            x = x.permute(keep + list(red)).reshape([x.shape[i] for i in keep] + [-1])
+            r = torch.quantile(x, qt, dim=-1, interpolation=interpolation)
+            return r.reshape(tuple(qt.shape) + tuple(full)) if keepdims else r
         axis = axis[0]
     return torch.quantile(x, qt, dim=axis, keepdim=keepdims, interpolation=interpolation)
 
