@@ -273,9 +273,31 @@ def get_symbol(x):
     """Return a Symbol for the recorded history of ``x`` (only available for
     arrays produced by a hybridized block; see gluon.block)."""
     sym = getattr(x, '_symbol', None)
-    if sym is None:
-        raise MXNetError('get_symbol is only supported for outputs of hybridized blocks')
-    return sym
+    if sym is not None:
+        return sym
+    if getattr(x, '_hist', None) is None:
+        raise MXNetError('get_symbol: the array was not produced by a recorded operator')
+    # rebuild the recorded operator history (reference: Imperative::GetSymbol over the autograd
+    # entries); arrays without history become variables var0, var1, ...
+    from .symbol.symbol import _op_func, var
+    memo, nvars = {}, [0]
+
+    def build(a):
+        key = id(a)
+        if key in memo:
+            return memo[key]
+        h = getattr(a, '_hist', None)
+        if h is None:
+            s = var('var%d' % nvars[0])
+            nvars[0] += 1
+        else:
+            (opname, attrs, ins), i = h
+            kw = {k: v for k, v in attrs.items() if v is not None}
+            node = _op_func(opname)(*[build(b) for b in ins if b is not None], **kw)
+            s = node[i] if len(node.list_outputs()) > 1 else node
+        memo[key] = s
+        return s
+    return build(x)
 
 
 class Function:

@@ -53,7 +53,7 @@ def _wrap(t):
 class NDArray:
     """An n-dimensional array on a :class:`Context`."""
     __slots__ = ('_data', '_grad', '_grad_req', '_stype', '__weakref__', '_fresh_grad', '_arena', '_host_ctx',
-                 '_exc', '_recorded', '_idt')
+                 '_exc', '_recorded', '_idt', '_hist')
     __array_priority__ = 1000.0
 
     def __init__(self, data, ctx=None, dtype=None, stype='default', writable=True):

@@ -216,8 +216,10 @@ def invoke(op, inputs, attrs, out=None):
             if d is not None:
                 o._idt = d
     if _state.STATE.recording:
-        for o in outs:
+        hist = (op.name, attrs, list(inputs))       # for autograd.get_symbol
+        for i, o in enumerate(outs):
             o._recorded = True
+            o._hist = (hist, i)
     if _profiler.active_memory and out is None:
         for o in outs:
             _profiler.memory_alloc(o)
