@@ -86,6 +86,7 @@ def test_device_ops_across_streams_gpu():
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     a = torch.zeros(1 << 22, device='cuda')
     b = torch.empty_like(a)
+    torch.cuda.synchronize()    # the zero fill ran on the default stream, which s1 does not wait for
     v = engine.new_var('a')
     before = engine.get().device_ops
     # a long write on s1, then a read on s2 ordered only by the engine's event
