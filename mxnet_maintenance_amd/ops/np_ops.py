@@ -520,7 +520,13 @@ def _flip(a, axis=None):
 def _roll(a, shift=0, axis=None):
     if axis is None:
         return torch.roll(a.reshape(-1), shift).reshape(a.shape)
-    return torch.roll(a, shift, axis)
+    axes = tuple(axis) if isinstance(axis, (tuple, list)) else (axis,)
+    shifts = tuple(shift) if isinstance(shift, (tuple, list)) else (shift,)
+    if len(shifts) == 1 and len(axes) > 1:
+        shifts = shifts * len(axes)        # numpy broadcasts one shift over several axes
+    elif len(axes) == 1 and len(shifts) > 1:
+        axes = axes * len(shifts)
+    return torch.roll(a, shifts, axes)
 
 
 @register('_npi_rot90', arg_names=('a',), params={'k': ('int', 1), 'axes': ('shape', (0, 1))})
@@ -664,6 +670,7 @@ def _take(a, indices, axis=None, mode='raise'):
     idx = indices.long()
     if axis is None:
         a, axis = a.reshape(-1), 0
+    axis %= max(a.dim(), 1)
     n = a.shape[axis]
     if mode == 'wrap':
         idx = idx % n
