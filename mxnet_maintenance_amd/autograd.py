@@ -241,10 +241,9 @@ def backward(heads, head_grads=None, retain_graph=False, train_mode=True, create
 def grad(heads, variables, head_grads=None, retain_graph=None, create_graph=False, train_mode=True):  # pylint: disable=redefined-outer-name
     """Return gradients of heads w.r.t. variables (does not touch .grad buffers)."""
     from .ndarray.ndarray import NDArray
-    single = isinstance(variables, NDArray)
     if isinstance(heads, NDArray):
         heads = [heads]
-    if single:
+    if isinstance(variables, NDArray):
         variables = [variables]
     if head_grads is not None and isinstance(head_grads, NDArray):
         head_grads = [head_grads]
@@ -255,18 +254,29 @@ def grad(heads, variables, head_grads=None, retain_graph=None, create_graph=Fals
         hgs = [torch.ones_like(h) if g is None else g._data for h, g in zip(hts, head_grads)]
     if retain_graph is None:
         retain_graph = create_graph
-    prev_train = set_training(train_mode)
-    prev_rec = set_recording(create_graph)
-    try:
-        with torch.enable_grad():
-            gs = torch.autograd.grad(hts, [v._data for v in variables], grad_outputs=hgs,
-                                     retain_graph=retain_graph, create_graph=create_graph,
-                                     allow_unused=True)
-    finally:
-        set_training(prev_train)
-        set_recording(prev_rec)
-    out = [NDArray(g if g is not None else torch.zeros_like(v._data)) for g, v in zip(gs, variables)]
-    return out[0] if single else out
+    # a head without history (e.g. the constant first derivative of a linear op, differentiated
+    # again) contributes nothing: the reference's backward gives zero gradients for it
+    live = [(h, g) for h, g in zip(hts, hgs) if h.requires_grad]
+    gs = [None] * len(variables)
+    if live:
+        prev_train = set_training(train_mode)
+        prev_rec = set_recording(create_graph)
+        try:
+            with torch.enable_grad():
+                gs = torch.autograd.grad([h for h, _ in live], [v._data for v in variables],
+                                         grad_outputs=[g for _, g in live], retain_graph=retain_graph,
+                                         create_graph=create_graph, allow_unused=True)
+        finally:
+            set_training(prev_train)
+            set_recording(prev_rec)
+
+    def dense(g, v):
+        if g is None or g._is_zerotensor():      # torch's symbolic zeros (abs'' etc.) become real arrays
+            return torch.zeros_like(v._data)
+        return g
+    # always a list, even for a single variable: the reference rebinds ``variables`` to a list before
+    # its final isinstance check (python/mxnet/autograd.py:318-345), so callers index [0]
+    return [NDArray(dense(g, v)) for g, v in zip(gs, variables)]
 
 
 def get_symbol(x):

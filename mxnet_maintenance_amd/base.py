@@ -8,6 +8,22 @@ import numbers
 import numpy as np
 import torch
 
+
+def data_dir_default():
+    """Default directory for downloaded data and models: ``%APPDATA%/mxnet`` on Windows,
+    ``~/.mxnet`` elsewhere (reference python/mxnet/base.py:57)."""
+    import os
+    import platform
+    if platform.system() == 'Windows':
+        return os.path.join(os.environ.get('APPDATA'), 'mxnet')
+    return os.path.join(os.path.expanduser('~'), '.mxnet')
+
+
+def data_dir():
+    """``$MXNET_HOME`` if set, else :func:`data_dir_default`."""
+    import os
+    return os.getenv('MXNET_HOME', data_dir_default())
+
 __all__ = ['MXNetError', 'numeric_types', 'integer_types', 'string_types', 'py_str', 'mx_real_t', '_as_list',
            'np_dtype', 'torch_dtype', 'dtype_to_flag', 'flag_to_dtype']
 

@@ -5,6 +5,7 @@ from . import quantization as quant  # noqa: F401  (reference alias mx.contrib.q
 from . import text  # noqa: F401
 from . import svrg_optimization  # noqa: F401
 from . import autograd  # noqa: F401
+from . import io  # noqa: F401
 from .. import ndarray as _nd
 from .. import symbol as _sym
 ndarray = _nd.contrib

@@ -61,6 +61,24 @@ class SVRGModule(Module):
             args, auxs = self.get_params()
             self._mod_aux.init_params(initializer=None, arg_params=args, aux_params=auxs, force_init=True)
 
+    def init_optimizer(self, kvstore='local', optimizer='sgd', optimizer_params=(('learning_rate', 0.01),),
+                       force_init=False):
+        """The parent Module's optimizer, wrapped in ``_SVRGOptimizer`` so KVStore keys of full-gradient
+        slots (names containing ``full``) are stored rather than stepped."""
+        from ... import optimizer as _opt
+        from .svrg_optimizer import _SVRGOptimizer
+        super().init_optimizer(kvstore=kvstore, optimizer=optimizer, optimizer_params=optimizer_params,
+                               force_init=force_init)
+        inner = self._optimizer
+        if isinstance(inner, _SVRGOptimizer):
+            return
+        wrapped = _SVRGOptimizer(inner, param_idx2name=dict(inner.idx2name), rescale_grad=inner.rescale_grad)
+        self._optimizer = wrapped
+        if self._update_on_kvstore and self._kvstore is not None:
+            self._kvstore.set_optimizer(wrapped)
+        else:
+            self._updater = _opt.get_updater(wrapped)
+
     # ---------------------------------------------------------------- per-batch
     def forward(self, data_batch, is_train=None):
         super().forward(data_batch, is_train)

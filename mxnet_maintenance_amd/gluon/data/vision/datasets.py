@@ -49,6 +49,11 @@ class MNIST(_DownloadedDataset):
 
     def _get_data(self):
         img_name, lab_name = self._files[self._train]
+        from .... import test_utils
+        if type(self) is MNIST and test_utils._synthetic_enabled() and not any(
+                os.path.exists(os.path.join(self._root, n + e)) for n in (lab_name,) for e in ('', '.gz')):
+            # MXNET_TEST_SYNTHETIC_DATA=1 (reference-test harness only): random-pixel idx files
+            test_utils.get_mnist_ubyte(self._root)
         lab_path = _find(self._root, [lab_name + '.gz', lab_name])
         img_path = _find(self._root, [img_name + '.gz', img_name])
         with _open(lab_path) as fin:

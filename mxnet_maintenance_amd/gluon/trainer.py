@@ -272,7 +272,7 @@ class Trainer:
                     from ..ops.nlp_fns import ChunkTable
                     a.upd = torch.empty(a.numel, dtype=torch.float32, device=a.device)
                     a.table = ChunkTable([(off, n) for (off, n, _shape) in a.views], a.device)
-                    a.nrm = torch.zeros(2 * len(a.views), dtype=torch.float32, device=a.device)
+                    a.nrm = torch.zeros(2 * (len(a.views) + a.table.n), dtype=torch.float32, device=a.device)
             for p, (off, n, shape), idx in zip(a.params, a.views, a.indices):
                 w32v = NDArray(a.w32[off:off + n].view(shape)) if a.w32 is not None else None
                 if w32v is not None:

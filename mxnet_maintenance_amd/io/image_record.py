@@ -73,6 +73,9 @@ class _PinnedRing:
     def take(self, shape, dtype):
         ptr = self._ptrs[self._i % len(self._ptrs)]
         self._i += 1
+        # the slot may still be the source of an async H2D copy (split_and_load on a copy stream)
+        from ..gluon.utils import wait_host_reads     # pylint: disable=import-outside-toplevel
+        wait_host_reads(ptr, self._nbytes)
         raw = (ctypes.c_uint8 * self._nbytes).from_address(ptr)
         n = int(np.prod(shape)) * np.dtype(dtype).itemsize
         return np.frombuffer(raw, dtype=np.uint8, count=n).view(dtype).reshape(shape)

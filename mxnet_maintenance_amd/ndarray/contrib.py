@@ -114,3 +114,65 @@ def rand_zipfian(true_classes, num_sampled, range_max, ctx=None):
 # graph operators on CSR adjacency (src/operator/contrib/dgl_graph.cc), on the compressed storage
 from .dgl_graph import (dgl_csr_neighbor_uniform_sample, dgl_csr_neighbor_non_uniform_sample,  # noqa: E402,F401
                         dgl_subgraph, edge_id, dgl_adjacency, dgl_graph_compact)
+
+
+# ---------------------------------------------------------------------------
+# optimizer-update front ends taking Python lists (reference python/mxnet/ndarray/contrib.py:550-680):
+# the registered operators take a flat, interleaved argument list (w0, g0, m0, v0, w1, ...) and a
+# rescale_grad *array* (so the update can be skipped on the device for a non-finite scale)
+# ---------------------------------------------------------------------------
+def _rescale_array(rescale_grad, like):
+    from .ndarray import NDArray
+    from . import full
+    if isinstance(rescale_grad, NDArray):
+        return rescale_grad.as_in_context(like.context)
+    return full((1,), rescale_grad, ctx=like.context)
+
+
+def _interleave(*groups):
+    return [a for row in zip(*groups) for a in row]
+
+
+def _op(name):
+    return _register.make_op_function(name)
+
+
+def adamw_update(weight, grad, mean, var, rescale_grad, lr, eta, beta1=0.9, beta2=0.999, epsilon=1e-8, wd=0,
+                 clip_gradient=-1, out=None, name=None, **kwargs):
+    return _op('_adamw_update')(weight, grad, mean, var, _rescale_array(rescale_grad, weight), lr=lr, eta=eta,
+                                beta1=beta1, beta2=beta2, epsilon=epsilon, wd=wd, clip_gradient=clip_gradient,
+                                out=out, **kwargs)
+
+
+def mp_adamw_update(weight, grad, mean, var, weight32, rescale_grad, lr, eta, beta1=0.9, beta2=0.999,
+                    epsilon=1e-8, wd=0, clip_gradient=-1, out=None, name=None, **kwargs):
+    return _op('_mp_adamw_update')(weight, grad, mean, var, weight32, _rescale_array(rescale_grad, weight), lr=lr,
+                                   eta=eta, beta1=beta1, beta2=beta2, epsilon=epsilon, wd=wd,
+                                   clip_gradient=clip_gradient, out=out, **kwargs)
+
+
+def multi_adamw_update(weights, grads, mean, var, rescale_grad, lrs, wds, etas, out=None, name=None, size=0,
+                       **kwargs):
+    args = _interleave(weights, grads, mean, var) + [_rescale_array(rescale_grad, weights[0])]
+    return _op('_multi_adamw_update')(*args, out=out, num_weights=size or len(weights), lrs=lrs, wds=wds,
+                                      etas=etas, **kwargs)
+
+
+def multi_mp_adamw_update(weights, grads, mean, var, weights32, rescale_grad, lrs, wds, etas, out=None, name=None,
+                          size=0, **kwargs):
+    args = _interleave(weights, grads, mean, var, weights32) + [_rescale_array(rescale_grad, weights[0])]
+    return _op('_multi_mp_adamw_update')(*args, out=out, num_weights=size or len(weights), lrs=lrs, wds=wds,
+                                         etas=etas, **kwargs)
+
+
+def multi_lamb_update(weights, grads, mean, var, step_count, lrs, wds, out=None, num_tensors=0, **kwargs):
+    return _op('_multi_lamb_update')(*_interleave(weights, grads, mean, var), out=out,
+                                     num_tensors=num_tensors or len(weights), step_count=step_count,
+                                     learning_rates=lrs, wds=wds, **kwargs)
+
+
+def multi_mp_lamb_update(weights, grads, mean, var, weights32, step_count, lrs, wds, out=None, num_tensors=0,
+                         **kwargs):
+    return _op('_multi_mp_lamb_update')(*_interleave(weights, grads, mean, var, weights32), out=out,
+                                        num_tensors=num_tensors or len(weights), step_count=step_count,
+                                        learning_rates=lrs, wds=wds, **kwargs)

@@ -112,9 +112,17 @@ def _failed_input(inputs):
     return None
 
 
+_SAMPLER_NAMES = frozenset(('_npi_normal', '_npi_uniform', '_npi_gamma', '_npi_exponential', '_npi_multinomial',
+                            '_shuffle', '_npi_bernoulli', '_npi_sampler', '_npi_uniform_like', '_npi_normal_like',
+                            '_npi_choice', '_npi_shuffle', '_npi_laplace', '_npi_logistic', '_npi_gumbel',
+                            '_npi_pareto', '_npi_power', '_npi_rayleigh', '_npi_weibull', '_npi_chisquare',
+                            '_npi_f', '_npi_beta', '_npi_lognormal', '_npi_poisson'))
+
+
 def _is_sampler(name):
-    return name.startswith(('_random_', '_sample_', '_npi_random', 'random_', 'sample_')) or name in (
-        '_npi_normal', '_npi_uniform', '_npi_gamma', '_npi_exponential', '_npi_multinomial', '_shuffle')
+    """Operators whose output is a random draw (one predicate for the RNG failure box and for the
+    graph passes, which must never merge two of them)."""
+    return name.startswith(('_random_', '_sample_', '_npi_random', 'random_', 'sample_')) or name in _SAMPLER_NAMES
 
 
 def _placeholder(attrs, inputs):

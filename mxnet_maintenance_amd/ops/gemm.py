@@ -25,9 +25,17 @@ def _stream():
 
 
 def _workspace(n, dev):
-    buf = _WS.get(dev)
+    """Split-K fp32 partials, one buffer per (device, stream): split-K GEMMs issued on two streams of
+    one device must not share it.  It is never grown during a HIP-graph capture (a buffer from the
+    graph's private pool would be reused outside the graph): the eager warm-up sizes it first."""
+    s = torch.cuda.current_stream(dev)
+    key = (dev, s.cuda_stream)
+    buf = _WS.get(key)
     if buf is None or buf.numel() < n:
-        buf = _WS[dev] = torch.empty(n, dtype=torch.float32, device=dev)
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError('gemm split-K workspace of %d floats requested during graph capture on a '
+                               'stream without one; run the step eagerly first' % n)
+        buf = _WS[key] = torch.empty(n, dtype=torch.float32, device=dev)
     return buf
 
 

@@ -292,7 +292,10 @@ def dropout(x, p):
 
 
 def softmax_ce(logits, label, reduction='none'):
-    """Cross entropy of softmax(logits) against integer labels (fp32 accumulation)."""
+    """Cross entropy of softmax(logits) against integer labels (fp32 accumulation).  Labels may be
+    ``(N,)`` or ``(N, 1)`` (what NDArrayIter yields; the reference picks with keepdims, loss.py:390)."""
+    if label.dim() > 1 and label.numel() == logits.shape[0]:
+        label = label.reshape(-1)
     if _use_hip(logits) and _K.ce_ok(logits):
         loss = _K.SoftmaxCE.apply(logits, label)
     else:

@@ -647,11 +647,60 @@ def _time_candidates(cands, reps=3, key=None, tol=2e-2):
     return best, (outs[best] if best is not None else None)
 
 
+# ---- deterministic execution (MXNET_ENFORCE_DETERMINISM; reference: the cuDNN algorithm filter of
+# src/operator/nn/cudnn/cudnn_convolution-inl.h:627 and cudnn_pooling-inl.h:53).  The in-tree kernels
+# reduce in a fixed order (slab reductions, no float atomics); vendor candidates may pick split-K
+# solutions that accumulate with atomics, so in this mode they are only used where no in-tree kernel
+# can run, with torch's / MIOpen's deterministic algorithm selection switched on.
+_DETERMINISTIC = [_env.get('MXNET_ENFORCE_DETERMINISM') != 0]
+_NONDET = ('mm', 'miopen', 'sk', 'splitk', 'bmm', 'blaslt')
+
+
+def _apply_torch_determinism(flag):
+    torch.backends.cudnn.deterministic = bool(flag)
+    if flag:
+        torch.backends.cudnn.benchmark = False
+    try:
+        torch.use_deterministic_algorithms(bool(flag), warn_only=True)
+    except Exception:   # pylint: disable=broad-except
+        pass
+
+
+def set_deterministic(flag):
+    """Switch deterministic execution on or off at run time (the env knob sets the initial state).
+    Algorithm choices are cached per mode, so switching does not reuse a nondeterministic choice."""
+    _DETERMINISTIC[0] = bool(flag)
+    _apply_torch_determinism(flag)
+
+
+def deterministic():
+    return _DETERMINISTIC[0]
+
+
+if _DETERMINISTIC[0]:
+    _apply_torch_determinism(True)
+
+
+def _det_filter(cands):
+    if not _DETERMINISTIC[0] or cands is None:
+        return cands
+    keep = [(n, f) for n, f in cands if not n.startswith(_NONDET)]
+    return keep or cands
+
+
+def _akey(key):
+    """Algorithm-cache key: choices made in deterministic mode are kept apart."""
+    return key + ('det',) if _DETERMINISTIC[0] else key
+
+
 def _select(key, cands, default, timing=None):
     """Run the cached / autotuned / default candidate and return its result.
 
     ``timing`` (optional, same names as ``cands``): the closures to time instead, e.g. with the
     cost of work a candidate leaves to the next operator included."""
+    key = _akey(key)
+    cands = _det_filter(cands)
+    timing = _det_filter(timing)
     name = _ALGO.get(key)
     if name is None:
         if _AUTOTUNE and not torch.cuda.is_current_stream_capturing() and len(cands) > 1:
@@ -774,7 +823,7 @@ def _gemm_dgrad_1x1(dy, w, xshape, addend=None):
 
 def _big_algo(key):
     """The big-tile variant number autotuning picked for ``key``, else None."""
-    algo = _ALGO.get(key)
+    algo = _ALGO.get(_akey(key))
     if algo and algo.startswith('hip') and algo[3:].isdigit() and int(algo[3:]) in _BIG_VARIANTS:
         return int(algo[3:])
     return None
@@ -894,7 +943,7 @@ def _wgrad(dy, x, w, w_ref, stride, pad):
     split-K GEMM candidates add their fp32 sum into it).
     """
     key = ('wgrad', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype)
-    algo = _ALGO.get(key)
+    algo = _ALGO.get(_akey(key))
     if algo in ('hip', 'hipreg') or (algo or '').startswith('ring'):
         tgt = _leaf_grad(w_ref, dtype=w.dtype)
         if tgt is not None:
@@ -1029,7 +1078,7 @@ def _tee_dgrad(gy, x, w, gpass, inplace, bn_src=None):
     cands.append(('mm', lambda: mm() if not (gpass is not None and inplace) else
                   torch.addmm(gpass.reshape(-1, C), g2, w2).view(x.shape)))
     key = ('teedgrad', tuple(x.shape), tuple(w.shape), x.dtype) + (('bnbwd',) if fuse_bn else ())
-    if _ALGO.get(key) == 'mm':
+    if _ALGO.get(_akey(key)) == 'mm':
         return mm()
     if fuse_bn:
         return _select(key, cands + fused, 'mm', timing=_charge_bn_bwd(cands, bn_src[0]) + fused)

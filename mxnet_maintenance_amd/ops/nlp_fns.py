@@ -218,7 +218,9 @@ def flat_adam(w, g, mean, var, w32, lr, beta1, beta2, eps, wd, rescale, clip, ad
 
 def lamb_update(w, g, mean, var, w32, upd, table, nrm, lr, beta1, beta2, eps, t, bias_correction, wd, rescale, clip,
                 lower_bound=-1.0, upper_bound=-1.0, hp=None):
-    """``hp``: optional device float tensor {lr, bc1, bc2} read at run time (graph-captured steps)."""
+    """``hp``: optional device float tensor {lr, bc1, bc2} read at run time (graph-captured steps).
+    ``nrm``: 2 * (segments + chunks) floats -- the per-segment norms, then the per-chunk partials."""
+    assert nrm.numel() >= 2 * (table.nseg + table.n), 'lamb_update: nrm needs 2*(nseg + nchunks) floats'
     bc1 = 1.0 - beta1 ** t if bias_correction else 1.0
     bc2 = 1.0 - beta2 ** t if bias_correction else 1.0
     args = (_DT[w.dtype], w.data_ptr(), g.data_ptr(), mean.data_ptr(), var.data_ptr(), _p(w32),
@@ -229,10 +231,11 @@ def lamb_update(w, g, mean, var, w32, upd, table, nrm, lr, beta1, beta2, eps, t,
 
 
 def seg_sumsq(x, table):
-    out = torch.empty(table.nseg, dtype=torch.float32, device=x.device)
+    # per-segment sums followed by the per-chunk partials they are reduced from (workspace)
+    out = torch.empty(table.nseg + table.n, dtype=torch.float32, device=x.device)
     _K.lib().seg_sumsq(_DT[x.dtype], x.data_ptr(), table.table.data_ptr(), table.n, out.data_ptr(), table.nseg,
                        _stream())
-    return out
+    return out[:table.nseg]
 
 
 def all_finite(x, scale=1.0, flag=None):
@@ -363,7 +366,7 @@ def _fc_wgrad(dy2, x2, w, w_ref):
     """dW = dY^T X; accumulated straight into the weight's .grad buffer when possible (GEMM with
     beta = 1 / the MFMA kernel's accumulating reduce) so no separate dW tensor and add kernel."""
     key = ('fc_wgrad', tuple(dy2.shape), tuple(x2.shape), dy2.dtype)
-    algo = _KF._ALGO.get(key)
+    algo = _KF._ALGO.get(_KF._akey(key))
     tgt = _leaf_grad(w_ref, dtype=w.dtype) if (algo is not None and _FC_DIRECT) else None
     if tgt is not None:
         N, K = w.shape
@@ -439,6 +442,16 @@ class Embedding(torch.autograd.Function):
         V, C, wdt = ctx.vc
         dy = dy.contiguous()
         dev = dy.device
+        if _KF.deterministic():
+            # MXNET_ENFORCE_DETERMINISM: an ordered (sort-based) accumulation instead of float atomics
+            rows = idx.reshape(-1).to(torch.int64).clamp(0, V - 1)
+            acc = torch.zeros((V, C), dtype=torch.float32, device=dev)
+            acc.index_put_((rows,), dy.reshape(-1, C).float(), accumulate=True)
+            tgt = _leaf_grad(ctx.w_ref, V * C, dtype=wdt) if ctx.needs_input_grad[1] else None
+            if tgt is not None:
+                tgt.add_(acc.view(tgt.shape))
+                return None, None
+            return None, acc.to(wdt)
         key = (V, C, dev)
         sc = _EMB_SCRATCH.get(key)
         if sc is None:

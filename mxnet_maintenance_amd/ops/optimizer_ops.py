@@ -126,7 +126,7 @@ _ADAMW = {'lr': ('float', 0.001), 'beta1': ('float', 0.9), 'beta2': ('float', 0.
 def _adamw(weight, grad, mean, var, rescale_grad, lr, beta1, beta2, epsilon, wd, eta, clip_gradient, w32=None):
     w = weight if w32 is None else w32
     rs = float(rescale_grad.reshape(-1)[0]) if torch.is_tensor(rescale_grad) else rescale_grad
-    if not math.isfinite(rs):
+    if not math.isfinite(rs) or rs == 0:      # skipped update (adamw-inl.h: non-finite or zero scale)
         return weight
     g = grad.float() * rs
     if clip_gradient >= 0:

@@ -1130,29 +1130,45 @@ def dgl_adjacency(data):
 @register('_contrib_hawkesll', aliases=('hawkesll',), num_outputs=2,
           arg_names=('lda', 'alpha', 'beta', 'state', 'lags', 'marks', 'valid_length', 'max_time'))
 def hawkesll(lda, alpha, beta, state, lags, marks, valid_length, max_time):
-    # Univariate-mark Hawkes log-likelihood with exponential kernel
-    # (src/operator/contrib/hawkes_ll-inl.h), computed sequentially per batch.
+    """Log-likelihood of marked Hawkes processes with exponential decay kernels (one sequence per row).
+
+    Semantics of src/operator/contrib/hawkes_ll-inl.h: each mark k keeps its own excitation state
+    ``s_k`` and last event time; at an event of mark k after ``d`` time units since that mark's last
+    event, ``lambda = mu_k + alpha_k beta_k s_k e^{-beta_k d}`` contributes ``log lambda`` and the
+    compensator ``mu_k d + alpha_k s_k (1 - e^{-beta_k d})`` is subtracted, then
+    ``s_k <- 1 + s_k e^{-beta_k d}``.  Every mark's remaining compensator up to ``max_time`` closes
+    the sequence and the returned states are decayed to ``max_time``.
+
+    All N sequences advance together, one event index per step (rows past their valid length are
+    masked), as differentiable tensor ops: autograd gives the exact gradients w.r.t. mu, alpha and
+    beta (the reference's hand-written backward) and the initial state."""
     N, T = lags.shape
     K = lda.shape[1]
-    ll = torch.zeros(N, dtype=lda.dtype, device=lda.device)
-    st = state.clone()
-    for b in range(N):
-        t = 0.0
-        s = st[b].clone()
-        last = torch.zeros(K, dtype=lda.dtype, device=lda.device)
-        for j in range(int(valid_length[b])):
-            t = t + float(lags[b, j])
-            k = int(marks[b, j])
-            ed = torch.exp(-beta * (t - last))
-            s = s * ed
-            lam = lda[b, k] + alpha[k] * beta[k] * s[k]
-            ll[b] = ll[b] + torch.log(lam)
-            comp = lda[b] * lags[b, j]
-            ll[b] = ll[b] - comp.sum()
-            s = s.clone()
-            s[k] = s[k] + 1.0
-            last = torch.full_like(last, t)
-        rem = float(max_time[b]) - t
-        ll[b] = ll[b] - (lda[b] * rem).sum() - (alpha * s * (1 - torch.exp(-beta * (rem + t - last)))).sum()
-        st[b] = s * torch.exp(-beta * (float(max_time[b]) - last))
-    return ll, st
+    dt = lda.dtype
+    marks = marks.to(torch.int64)
+    vl = valid_length.to(dt)
+    rows = torch.arange(N, device=lda.device)
+    st = state.to(dt)
+    last = torch.zeros(N, K, dtype=dt, device=lda.device)
+    t = torch.zeros(N, dtype=dt, device=lda.device)
+    ll = torch.zeros(N, dtype=dt, device=lda.device)
+    steps = min(T, int(vl.max().item())) if N else 0
+    for j in range(steps):
+        active = vl > j
+        ci = marks[:, j]
+        t = t + torch.where(active, lags[:, j].to(dt), torch.zeros_like(t))
+        d = t - last[rows, ci]
+        b, a = beta[ci], alpha[ci]
+        s_c = st[rows, ci]
+        mu_c = lda[rows, ci]
+        ed = torch.exp(-b * d)
+        lam = torch.where(active, mu_c + a * b * s_c * ed, torch.ones_like(mu_c))
+        term = torch.log(lam) - (mu_c * d + a * s_c * (1 - ed))
+        ll = ll + torch.where(active, term, torch.zeros_like(term))
+        hit = torch.nn.functional.one_hot(ci, K).bool() & active[:, None]
+        st = torch.where(hit, (1 + s_c * ed)[:, None], st)
+        last = torch.where(hit, t[:, None], last)
+    d = max_time.to(dt)[:, None] - last
+    ed = torch.exp(-beta[None, :] * d)
+    ll = ll - (lda * d + alpha[None, :] * st * (1 - ed)).sum(1)
+    return ll, ed * st

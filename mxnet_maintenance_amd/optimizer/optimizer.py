@@ -903,7 +903,7 @@ class Nadam(Optimizer):
 class GroupAdaGrad(Optimizer):
     """AdaGrad with one accumulator per row (python/mxnet/optimizer/contrib.py)."""
 
-    def __init__(self, eps=1e-6, **kwargs):
+    def __init__(self, eps=1e-5, **kwargs):
         super().__init__(**kwargs)
         self.float_stable_eps = eps
 

@@ -22,17 +22,26 @@ __all__ = ['eliminate_common_expr', 'fuse_pointwise', 'memory_plan', 'optimize']
 
 # never merged: outputs are random or the op mutates state
 _NONDETERMINISTIC_PREFIX = ('_random', '_sample', 'random_', '_npi_random', '_npi_choice', '_npi_shuffle',
-                            'sample_', 'Dropout', 'Custom', '_contrib_quantize', '_shuffle', 'shuffle')
+                            'sample_', 'Dropout', '_npx_dropout', 'Custom', '_contrib_quantize', '_shuffle', 'shuffle')
 # outputs that alias their input (no storage of their own in the memory plan)
 _ALIAS_OPS = ('BlockGrad', '_copy', 'Reshape', 'Flatten', 'expand_dims', 'squeeze', 'identity',
               '_npx_reshape', 'reshape_like')
 
 
 def _cse_ok(node):
+    """Whether ``node`` may be merged with an identical node.  As in the reference
+    (eliminate_common_expr_pass.cc: nodes without inputs are never grouped, nor ops that request a
+    random resource) -- source nodes (zeros, arange, every sampler called with a ``size``) and all
+    samplers, including the NumPy ones taking array parameters, stay distinct."""
+    if not node.inputs:
+        return False
     op = node.opdef()
     if op.get_aux_names(node.parsed()):
         return False
+    from ..ndarray.register import _is_sampler
     name = op.name
+    if _is_sampler(name) or _is_sampler(node.op):
+        return False
     return not any(name.startswith(p) for p in _NONDETERMINISTIC_PREFIX)
 
 

@@ -19,6 +19,10 @@ KNOBS = {
     'MXNET_CUDNN_AUTOTUNE_DEFAULT': (int, 1, 'conv algorithm autotuning (HIP implicit-GEMM / hipBLASLt / MIOpen / '
                                      'split-K wgrad timed per shape); 0 = heuristic choice',
                                      'MXNET_CUDNN_AUTOTUNE_DEFAULT'),
+    'MXNET_ENFORCE_DETERMINISM': (int, 0, 'bitwise-reproducible training: the autotuner only admits kernels with a '
+                                  'fixed reduction order (the in-tree MFMA kernels, no vendor split-K / atomic '
+                                  'candidates), atomic accumulations switch to ordered reductions, and torch / MIOpen '
+                                  'run their deterministic algorithms', 'MXNET_ENFORCE_DETERMINISM'),
     'MXNET_UPDATE_ON_KVSTORE': (int, 1, 'Module/model API: run the optimizer inside the kvstore',
                                 'MXNET_UPDATE_ON_KVSTORE'),
     'MXNET_HOME': (str, os.path.join(os.path.expanduser('~'), '.mxnet'), 'dataset / model cache root', 'MXNET_HOME'),

@@ -11,9 +11,10 @@
 // is ONE pass over HBM: 16-byte vectors of weight/grad (f16/bf16/f32) plus the
 // fp32 optimizer state (and fp32 master weights under multi-precision).
 // LAMB's per-parameter trust ratio needs per-segment norms: a chunk table built
-// once on the host maps 2048-element chunks to segments; each block reduces its
-// chunk in registers + LDS and adds one value per segment (fp32 atomics on
-// O(#chunks) addresses).
+// once on the host maps 16K-element chunks to segments; each block reduces its
+// chunk in registers + LDS to one partial per chunk, and a finalize kernel sums
+// each segment's (contiguous) chunk partials in a fixed order -- no float
+// atomics, so the norms (and the update) are bitwise reproducible.
 #include <stdexcept>
 
 #include "common.h"
@@ -86,7 +87,7 @@ template <typename T, bool MP>
 __global__ void __launch_bounds__(256) lamb_phase1_kernel(const T* __restrict__ w, const T* __restrict__ grad,
                                                           float* __restrict__ mean, float* __restrict__ var,
                                                           const float* __restrict__ w32, float* __restrict__ upd,
-                                                          const Chunk* __restrict__ chunks, float* __restrict__ nrm,
+                                                          const Chunk* __restrict__ chunks, float* __restrict__ cpart,
                                                           float beta1, float beta2, float eps, float bc1, float bc2,
                                                           float wd, float rescale, float clip,
                                                           const float* __restrict__ hp) {
@@ -127,9 +128,40 @@ __global__ void __launch_bounds__(256) lamb_phase1_kernel(const T* __restrict__ 
     red[1][wid] = sr;
   }
   __syncthreads();
+  if (threadIdx.x == 0) {   // this chunk's partials; seg_finalize_kernel sums them per segment
+    cpart[2 * blockIdx.x] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    cpart[2 * blockIdx.x + 1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  }
+}
+
+// Per-segment totals of per-chunk partials (W values per chunk, out[W*seg + v]).  The block of a
+// segment's first chunk reduces the segment: thread t sums chunks first+t, first+t+256, ... while
+// they belong to the segment, then a fixed-order wave / LDS tree -- the result never depends on
+// scheduling.  Blocks of other chunks exit at once.
+template <int W>
+__global__ void __launch_bounds__(256) seg_finalize_kernel(const Chunk* __restrict__ chunks, int nchunks,
+                                                           const float* __restrict__ cpart, float* __restrict__ out) {
+  const int first = blockIdx.x;
+  const int seg = chunks[first].seg;
+  if (first > 0 && chunks[first - 1].seg == seg) return;
+  float acc[W];
+#pragma unroll
+  for (int v = 0; v < W; ++v) acc[v] = 0.f;
+  for (int j = first + threadIdx.x; j < nchunks && chunks[j].seg == seg; j += 256) {
+#pragma unroll
+    for (int v = 0; v < W; ++v) acc[v] += cpart[W * j + v];
+  }
+  __shared__ float red[W][4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int v = 0; v < W; ++v) {
+    const float t = wave_sum(acc[v]);
+    if (lane == 0) red[v][wid] = t;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    atomicAdd(nrm + 2 * ck.seg, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
-    atomicAdd(nrm + 2 * ck.seg + 1, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+#pragma unroll
+    for (int v = 0; v < W; ++v) out[W * seg + v] = (red[v][0] + red[v][1]) + (red[v][2] + red[v][3]);
   }
 }
 
@@ -161,10 +193,11 @@ __global__ void __launch_bounds__(256) lamb_phase2_kernel(T* __restrict__ w, flo
   }
 }
 
-// per-segment sum of squares (multi_sum_sq over an arena): out[seg] += sum(x^2)
+// per-chunk sum of squares (multi_sum_sq over an arena): cpart[chunk] = sum(x^2); totals per segment
+// by seg_finalize_kernel<1>
 template <typename T>
 __global__ void __launch_bounds__(256) seg_sumsq_kernel(const T* __restrict__ x, const Chunk* __restrict__ chunks,
-                                                        float* __restrict__ out) {
+                                                        float* __restrict__ cpart) {
   const Chunk ck = chunks[blockIdx.x];
   float s = 0.f;
   for (int i8 = threadIdx.x * 8; i8 < ck.len; i8 += 256 * 8) {
@@ -177,7 +210,7 @@ __global__ void __launch_bounds__(256) seg_sumsq_kernel(const T* __restrict__ x,
   __shared__ float red[4];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(out + ck.seg, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) cpart[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
 // flag[0] = 0 when any element is inf/nan (flag preset to 1 by the caller)
@@ -237,34 +270,43 @@ static void zero_f32(float* p, int n, hipStream_t s) {
   if (blocks > 0) hipLaunchKernelGGL(zero_f32_kernel, dim3(blocks), dim3(256), 0, s, p, n);
 }
 
-// chunks: device array of (start, len, seg) triples (int64, int32, int32 -> 16 bytes each)
+// chunks: device array of (start, len, seg) triples (int64, int32, int32 -> 16 bytes each);
+// nrm: 2*nseg per-segment norms followed by 2*nchunks per-chunk partials (workspace)
 void lamb_update(int dtype, void* w, const void* g, float* mean, float* var, float* w32, float* upd,
                  const void* chunks, int nchunks, float* nrm, int nseg, float lr, float beta1, float beta2, float eps,
                  float bc1, float bc2, float wd, float rescale, float clip, float lb, float ub, const float* hp,
                  hipStream_t s) {
   const Chunk* ck = static_cast<const Chunk*>(chunks);
-  zero_f32(nrm, 2 * nseg, s);
+  float* cpart = nrm + 2 * nseg;
+  zero_f32(nrm, 2 * nseg, s);     // segments without chunks (empty parameters) keep norm 0
   MXAMD_OPT_DTYPE(dtype, {
     if (w32) {
       hipLaunchKernelGGL((lamb_phase1_kernel<T, true>), dim3(nchunks), dim3(256), 0, s, static_cast<const T*>(w),
-                         static_cast<const T*>(g), mean, var, w32, upd, ck, nrm, beta1, beta2, eps, bc1, bc2, wd,
+                         static_cast<const T*>(g), mean, var, w32, upd, ck, cpart, beta1, beta2, eps, bc1, bc2, wd,
                          rescale, clip, hp);
+    } else {
+      hipLaunchKernelGGL((lamb_phase1_kernel<T, false>), dim3(nchunks), dim3(256), 0, s, static_cast<const T*>(w),
+                         static_cast<const T*>(g), mean, var, w32, upd, ck, cpart, beta1, beta2, eps, bc1, bc2, wd,
+                         rescale, clip, hp);
+    }
+    hipLaunchKernelGGL(seg_finalize_kernel<2>, dim3(nchunks), dim3(256), 0, s, ck, nchunks, cpart, nrm);
+    if (w32) {
       hipLaunchKernelGGL((lamb_phase2_kernel<T, true>), dim3(nchunks), dim3(256), 0, s, static_cast<T*>(w), w32, upd,
                          ck, nrm, lr, lb, ub, hp);
     } else {
-      hipLaunchKernelGGL((lamb_phase1_kernel<T, false>), dim3(nchunks), dim3(256), 0, s, static_cast<const T*>(w),
-                         static_cast<const T*>(g), mean, var, w32, upd, ck, nrm, beta1, beta2, eps, bc1, bc2, wd,
-                         rescale, clip, hp);
       hipLaunchKernelGGL((lamb_phase2_kernel<T, false>), dim3(nchunks), dim3(256), 0, s, static_cast<T*>(w), w32, upd,
                          ck, nrm, lr, lb, ub, hp);
     }
   })
 }
 
+// out: nseg per-segment sums followed by nchunks per-chunk partials (workspace)
 void seg_sumsq(int dtype, const void* x, const void* chunks, int nchunks, float* out, int nseg, hipStream_t s) {
+  const Chunk* ck = static_cast<const Chunk*>(chunks);
   zero_f32(out, nseg, s);
   MXAMD_OPT_DTYPE(dtype, hipLaunchKernelGGL((seg_sumsq_kernel<T>), dim3(nchunks), dim3(256), 0, s,
-                                            static_cast<const T*>(x), static_cast<const Chunk*>(chunks), out))
+                                            static_cast<const T*>(x), ck, out + nseg))
+  hipLaunchKernelGGL(seg_finalize_kernel<1>, dim3(nchunks), dim3(256), 0, s, ck, nchunks, out + nseg, out);
 }
 
 __global__ void set_flag_kernel(int* __restrict__ flag) {

@@ -179,7 +179,13 @@ void Engine::RunDevice(const std::shared_ptr<Opr>& op) {
   if (op->device >= 0 && op->device != prev) rt.set_device(prev);
   for (const auto& v : op->const_vars) {
     std::lock_guard<std::mutex> lk(v->mu);
-    v->read_evs.push_back(ev);
+    // one read event per (device, stream): a later event on the same stream implies the earlier ones,
+    // so a read-only variable (weights at inference) keeps a bounded list
+    auto& r = v->read_evs;
+    r.erase(std::remove_if(r.begin(), r.end(),
+                           [&](const DevEventPtr& e) { return e->stream == ev->stream && e->device == ev->device; }),
+            r.end());
+    r.push_back(ev);
   }
   for (const auto& v : op->mutable_vars) {
     std::lock_guard<std::mutex> lk(v->mu);

@@ -106,3 +106,32 @@ def test_split_and_load_async_upload_gpu():
     got = np.concatenate([p.asnumpy() for p in parts])
     np.testing.assert_array_equal(got, data.asnumpy())
     assert all(p.context == mx.gpu(0) for p in parts)
+
+
+@pytest.mark.gpu
+def test_split_and_load_does_not_overwrite_queued_compute_memory():
+    """A large tensor freed on the compute stream while its kernels are still queued must not be
+    handed to the copy stream's upload (allocation from the copy stream's pool)."""
+    dev = torch.device('cuda', 0)
+    n = 1 << 24
+    host = mx.nd.array(np.full((n,), 7.0, dtype=np.float32))
+    torch.cuda.synchronize()
+    a = torch.ones(n, device=dev)
+    acc = torch.zeros(n, device=dev)
+    for _ in range(40):           # queue a lot of work reading `a` on the compute stream
+        acc.add_(a)
+    del a                          # freed while its readers are queued
+    part = mx.gluon.utils.split_and_load(host, [mx.gpu(0)])[0]
+    torch.cuda.synchronize()
+    assert float(acc.min()) == 40.0 and float(acc.max()) == 40.0
+    assert float(part._data.min()) == 7.0
+
+
+def test_wait_host_reads_waits_only_overlapping_ranges(monkeypatch):
+    from mxnet_maintenance_amd.gluon import utils as gu
+    waited = []
+    monkeypatch.setattr(engine, 'wait_for_var', lambda v: waited.append(v))
+    monkeypatch.setattr(gu, '_HOST_READS', [(1000, 100, 'a'), (5000, 100, 'b'), (1050, 10, 'c')])
+    gu.wait_host_reads(1040, 20)
+    assert waited == ['a', 'c']
+    assert gu._HOST_READS == [(5000, 100, 'b')]

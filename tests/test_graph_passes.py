@@ -32,6 +32,19 @@ def test_cse_keeps_random_ops_apart():
     assert _nodes(passes.eliminate_common_expr(s)) == _nodes(s)
 
 
+def test_cse_keeps_numpy_samplers_and_source_nodes_apart():
+    """Two np.random draws (no inputs, or the same array parameters) stay independent, and
+    zero-input nodes are never grouped (eliminate_common_expr_pass.cc)."""
+    u = mx.sym.np.random.uniform(size=(64,)) - mx.sym.np.random.uniform(size=(64,))
+    opt = passes.eliminate_common_expr(u)
+    assert _nodes(opt) == _nodes(u)
+    out = opt.bind(mx.cpu(), {}).forward()[0].asnumpy()
+    assert np.abs(out).max() > 0
+    a = mx.sym.Variable('a')
+    z = mx.sym.np.random.normal(a, 1.0) + mx.sym.np.random.normal(a, 1.0)
+    assert _nodes(passes.eliminate_common_expr(z)) == _nodes(z)
+
+
 def test_executor_cse_matches_unoptimised():
     a, b = mx.sym.Variable('a'), mx.sym.Variable('b')
     s = mx.sym.exp(a * b) + mx.sym.exp(a * b)

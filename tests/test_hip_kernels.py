@@ -526,7 +526,7 @@ def test_flat_adam_kernel_matches_torch(adamw, mp):
 def test_lamb_arena_kernel_matches_per_segment_reference():
     K = _lib()
     torch.manual_seed(7)
-    sizes = [1000, 64, 40000, 8]
+    sizes = [1000, 64, 40000, 8, 4500000]   # the last spans > 256 chunks
     offs, off = [], 0
     for s in sizes:
         offs.append(off)
@@ -541,10 +541,16 @@ def test_lamb_arena_kernel_matches_per_segment_reference():
     v = torch.zeros(n, device='cuda')
     upd = torch.empty(n, device='cuda')
     table = K.ChunkTable(list(zip(offs, sizes)), 'cuda')
-    nrm = torch.zeros(2 * len(sizes), device='cuda')
+    nrm = torch.zeros(2 * (len(sizes) + table.n), device='cuda')
     ref_w = w.clone()
     lr, b1, b2, eps, wd, t = 0.01, 0.9, 0.999, 1e-6, 0.01, 1
+    w0, m0, v0 = w.clone(), m.clone(), v.clone()
     K.lamb_update(w, g, m, v, None, upd, table, nrm, lr, b1, b2, eps, t, True, wd, 1.0, -1.0)
+    # no float atomics: a second update from the same state is bitwise identical
+    w2, m2, v2 = w0.clone(), m0.clone(), v0.clone()
+    K.lamb_update(w2, g, m2, v2, None, torch.empty_like(upd), table, torch.zeros_like(nrm), lr, b1, b2, eps, t, True,
+                  wd, 1.0, -1.0)
+    assert torch.equal(w, w2)
     for o, s in zip(offs, sizes):
         gg = g[o:o + s]
         mm = (1 - b1) * gg
