@@ -288,10 +288,10 @@ class Trainer:
                     mv = (NDArray(a.mean[off:off + n].view(shape)), NDArray(a.var[off:off + n].view(shape)))
                     if w32v is None:
                         st = mv
-                    elif kind == 'adam':
+                    elif kind in ('adam', 'lamb'):
                         st = (w32v, mv)       # Optimizer.create_state_multi_precision layout
                     else:
-                        st = (w32v,) + mv     # AdamW / LAMB layout
+                        st = (w32v,) + mv     # AdamW layout
                 upd.states[idx] = st
                 upd.states_synced[idx] = True
         self._arena_kind = kind
@@ -660,7 +660,7 @@ class Trainer:
                             else:
                                 if a.w32 is None:
                                     mean, var = st
-                                elif kind == 'adam':
+                                elif kind in ('adam', 'lamb'):
                                     w32, (mean, var) = st
                                     cp(a.w32, w32)
                                 else:
@@ -675,7 +675,8 @@ class Trainer:
                             upd.states[idx] = (momv, w32v) if w32v is not None else momv
                         else:
                             mv = (NDArray(a.mean[off:off + n].view(shape)), NDArray(a.var[off:off + n].view(shape)))
-                            upd.states[idx] = mv if w32v is None else ((w32v, mv) if kind == 'adam' else (w32v,) + mv)
+                            upd.states[idx] = mv if w32v is None else ((w32v, mv) if kind in ('adam', 'lamb')
+                                                                       else (w32v,) + mv)
         param_dict = {i: param for i, param in enumerate(self._params)}
         self._optimizer.param_dict = param_dict
 

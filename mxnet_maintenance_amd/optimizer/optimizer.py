@@ -33,102 +33,124 @@ def _t(x):
     return x._data if isinstance(x, NDArray) else x
 
 
+class _UpdateCounts:
+    """Per-device, per-parameter update counters (the reference counts updates separately on every
+    device of a multi-device Module).  ``current`` is the table of the active device."""
+
+    def __init__(self, begin):
+        self.begin = begin
+        self.tables = {0: {}}
+        self.current = self.tables[0]
+
+    def select(self, device_id):
+        self.current = self.tables.setdefault(device_id, {})
+
+    def bump(self, indices):
+        """Advance the counters of ``indices``; returns the largest resulting count."""
+        top = 0
+        for idx in indices:
+            n = self.current.get(idx, self.begin) + 1
+            self.current[idx] = n
+            top = max(top, n)
+        return top
+
+
+def _symbol_attr_mults(sym_info, key):
+    """``{argument name: float}`` from the ``__lr_mult__`` / ``__wd_mult__`` attributes of a Symbol."""
+    if not sym_info:
+        return {}
+    attrs, names = sym_info
+    return {n: float(attrs[n][key]) for n in names if key in attrs.get(n, {})}
+
+
 class Optimizer:
-    """Base class of all optimizers."""
+    """Base class of all optimizers.
+
+    Hyper-parameters are resolved per parameter index: the learning rate comes from the scheduler
+    (at the current update count) or ``lr``, the weight decay from ``wd``; both are scaled by a
+    multiplier looked up first on the Gluon Parameter (``param_dict``), then by index, then by the
+    parameter's name (``idx2name``) in ``lr_mult`` / ``wd_mult``.  By default only ``*_weight`` and
+    ``*_gamma`` parameters are decayed.  Subclasses implement ``create_state`` and ``update``.
+    """
     opt_registry = {}
 
     def __init__(self, rescale_grad=1., param_idx2name=None, wd=0., clip_gradient=None, learning_rate=None,
                  lr_scheduler=None, sym=None, begin_num_update=0, multi_precision=False, param_dict=None,
                  aggregate_num=None, use_fused_step=None, **kwargs):
+        if param_idx2name is not None and not isinstance(param_idx2name, dict):
+            raise AssertionError('param_idx2name should be a dict of param indexes to names.')
         self.rescale_grad = rescale_grad
-        self.lr_scheduler = lr_scheduler
-        if self.lr_scheduler is None:
-            self.lr = 0.01 if learning_rate is None else learning_rate
-        else:
-            # an explicit learning_rate overrides the scheduler's base_lr; otherwise the scheduler's is used
-            if learning_rate is not None:
-                if lr_scheduler.base_lr != learning_rate:
-                    warnings.warn('learning rate from ``lr_scheduler`` has been overwritten by ``learning_rate`` '
-                                  'in optimizer.', UserWarning)
-                self.lr_scheduler.base_lr = learning_rate
-            self.lr = self.lr_scheduler.base_lr
         self.wd = wd
-        self.lr_mult = {}
-        self.wd_mult = {}
-        self.begin_num_update = begin_num_update
-        self.num_update = begin_num_update
-        self._all_index_update_counts = {0: {}}
-        self._index_update_count = self._all_index_update_counts[0]
         self.clip_gradient = clip_gradient
         self.multi_precision = multi_precision
-        self.aggregate_num = 0 if aggregate_num is None else aggregate_num
-        if param_idx2name is None:
-            param_idx2name = {}
-        assert isinstance(param_idx2name, dict), 'param_idx2name should be a dict of param indexes to names.'
-        self.idx2name = param_idx2name.copy()
-        self.sym_info = (sym.attr_dict(), sym.list_arguments()) if sym is not None else ()
-        self.param_dict = param_dict if param_dict else {}
+        self.aggregate_num = aggregate_num or 0
         self.allow_np_array = False
+        self.lr_scheduler = lr_scheduler
+        self.lr = self._initial_lr(learning_rate, lr_scheduler)
+        self.begin_num_update = begin_num_update
+        self.num_update = begin_num_update
+        self._counts = _UpdateCounts(begin_num_update)
+        self.idx2name = dict(param_idx2name or {})
+        self.sym_info = (sym.attr_dict(), sym.list_arguments()) if sym is not None else ()
+        self.param_dict = param_dict or {}
+        self.lr_mult, self.wd_mult = {}, {}
         self.set_lr_mult({})
         self.set_wd_mult({})
 
     @staticmethod
+    def _initial_lr(learning_rate, scheduler):
+        if scheduler is None:
+            return 0.01 if learning_rate is None else learning_rate
+        if learning_rate is not None:
+            # an explicit learning_rate overrides the scheduler's base_lr
+            if scheduler.base_lr != learning_rate:
+                warnings.warn('learning rate from ``lr_scheduler`` has been overwritten by ``learning_rate`` '
+                              'in optimizer.', UserWarning)
+            scheduler.base_lr = learning_rate
+        return scheduler.base_lr
+
+    # ------------------------------------------------------------------ registry
+    @staticmethod
     def register(klass):
-        assert isinstance(klass, type)
-        name = klass.__name__.lower()
-        if name in Optimizer.opt_registry:
-            warnings.warn('WARNING: New optimizer %s.%s is overriding existing optimizer %s.%s' % (
-                klass.__module__, klass.__name__, Optimizer.opt_registry[name].__module__,
-                Optimizer.opt_registry[name].__name__))
-        Optimizer.opt_registry[name] = klass
+        """Class decorator: make ``klass`` creatable by its lower-cased name."""
+        if not isinstance(klass, type):
+            raise AssertionError('register expects a class')
+        key = klass.__name__.lower()
+        old = Optimizer.opt_registry.get(key)
+        if old is not None:
+            warnings.warn('WARNING: New optimizer %s.%s is overriding existing optimizer %s.%s'
+                          % (klass.__module__, klass.__name__, old.__module__, old.__name__))
+        Optimizer.opt_registry[key] = klass
         return klass
 
     @staticmethod
     def create_optimizer(name, **kwargs):
-        if name.lower() in Optimizer.opt_registry:
-            return Optimizer.opt_registry[name.lower()](**kwargs)
-        raise ValueError('Cannot find optimizer %s' % name)
+        """Instantiate a registered optimizer by (case-insensitive) name."""
+        klass = Optimizer.opt_registry.get(name.lower())
+        if klass is None:
+            raise ValueError('Cannot find optimizer %s' % name)
+        return klass(**kwargs)
+
+    # ------------------------------------------------------------------ update-count bookkeeping
+    @property
+    def _index_update_count(self):
+        return self._counts.current
 
     @property
+    def _all_index_update_counts(self):
+        return self._counts.tables
+
+    def _set_current_context(self, device_id):
+        self._counts.select(device_id)
+
+    def _update_count(self, index):
+        top = self._counts.bump(index if isinstance(index, (list, tuple)) else [index])
+        self.num_update = max(self.num_update, top)
+
+    # ------------------------------------------------------------------ learning rate / weight decay
+    @property
     def learning_rate(self):
-        if self.lr_scheduler is not None:
-            return self.lr_scheduler(self.num_update)
-        return self.lr
-
-    def create_state(self, index, weight):
-        return None
-
-    def create_state_multi_precision(self, index, weight):
-        weight_master_copy = None
-        if self.multi_precision and weight.dtype in (np.float16,) or \
-                (self.multi_precision and weight._data.dtype == torch.bfloat16):
-            weight_master_copy = NDArray(weight._data.detach().float().clone())
-            return (weight_master_copy,) + (self.create_state(index, weight_master_copy),)
-        if weight._data.dtype in (torch.float16, torch.bfloat16) and not self.multi_precision:
-            warnings.warn('Accumulating with float16 in optimizer can lead to poor accuracy or slow convergence. '
-                          'Consider using multi_precision=True option of the optimizer')
-        return self.create_state(index, weight)
-
-    def update(self, index, weight, grad, state):
-        raise NotImplementedError()
-
-    def update_multi_precision(self, index, weight, grad, state):
-        if isinstance(index, (list, tuple)):
-            # aggregated call (lists of indices / weights / grads / states): one update per tensor
-            for i, w, g, st in zip(index, weight, grad, state):
-                self.update_multi_precision(i, w, g, st)
-            return
-        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
-            weight_master_copy = state[0]
-            original_state = state[1]
-            # sparse gradients keep their storage (lazy row updates need the row indices)
-            grad32 = grad.astype('float32') if getattr(grad, 'stype', 'default') != 'default' \
-                else NDArray(grad._data.float())
-            self.update(index, weight_master_copy, grad32, original_state)
-            with torch.no_grad():
-                weight._data.copy_(weight_master_copy._data)
-        else:
-            self.update(index, weight, grad, state)
+        return self.lr if self.lr_scheduler is None else self.lr_scheduler(self.num_update)
 
     def set_learning_rate(self, lr):
         if self.lr_scheduler is not None:
@@ -141,68 +163,34 @@ class Optimizer:
         raise DeprecationWarning
 
     def set_lr_mult(self, args_lr_mult):
-        self.lr_mult = {}
-        if self.sym_info:
-            attr, arg_names = self.sym_info
-            for name in arg_names:
-                if name in attr and '__lr_mult__' in attr[name]:
-                    self.lr_mult[name] = float(attr[name]['__lr_mult__'])
+        """Learning-rate multipliers by name or index (Symbol ``__lr_mult__`` attributes come first)."""
+        self.lr_mult = _symbol_attr_mults(self.sym_info, '__lr_mult__')
         self.lr_mult.update(args_lr_mult)
 
     def set_wd_mult(self, args_wd_mult):
-        self.wd_mult = {}
-        for n in self.idx2name.values():
-            if not (n.endswith('_weight') or n.endswith('_gamma')):
-                self.wd_mult[n] = 0.0
-        if self.sym_info:
-            attr, arg_names = self.sym_info
-            for name in arg_names:
-                if name in attr and '__wd_mult__' in attr[name]:
-                    self.wd_mult[name] = float(attr[name]['__wd_mult__'])
+        """Weight-decay multipliers; parameters not named ``*_weight`` / ``*_gamma`` default to 0."""
+        self.wd_mult = {n: 0.0 for n in self.idx2name.values() if not n.endswith(('_weight', '_gamma'))}
+        self.wd_mult.update(_symbol_attr_mults(self.sym_info, '__wd_mult__'))
         self.wd_mult.update(args_wd_mult)
 
-    def _set_current_context(self, device_id):
-        if device_id not in self._all_index_update_counts:
-            self._all_index_update_counts[device_id] = {}
-        self._index_update_count = self._all_index_update_counts[device_id]
-
-    def _update_count(self, index):
-        if not isinstance(index, (list, tuple)):
-            index = [index]
-        for idx in index:
-            if idx not in self._index_update_count:
-                self._index_update_count[idx] = self.begin_num_update
-            self._index_update_count[idx] += 1
-            self.num_update = max(self._index_update_count[idx], self.num_update)
+    def _mult(self, index, table, attr):
+        p = self.param_dict.get(index)
+        if p is not None:
+            return getattr(p, attr)
+        if index in table:
+            return table[index]
+        name = self.idx2name.get(index)
+        return table.get(name, 1.0) if name is not None else 1.0
 
     def _get_lrs(self, indices):
-        if self.lr_scheduler is not None:
-            lr = self.lr_scheduler(self.num_update)
-        else:
-            lr = self.lr
-        lrs = [lr for _ in indices]
-        for i, index in enumerate(indices):
-            if index in self.param_dict:
-                lrs[i] *= self.param_dict[index].lr_mult
-            elif index in self.lr_mult:
-                lrs[i] *= self.lr_mult[index]
-            elif index in self.idx2name:
-                lrs[i] *= self.lr_mult.get(self.idx2name[index], 1.0)
-        return lrs
+        base = self.learning_rate
+        return [base * self._mult(i, self.lr_mult, 'lr_mult') for i in indices]
 
     def _get_lr(self, index):
         return self._get_lrs([index])[0]
 
     def _get_wds(self, indices):
-        wds = [self.wd for _ in indices]
-        for i, index in enumerate(indices):
-            if index in self.param_dict:
-                wds[i] *= self.param_dict[index].wd_mult
-            elif index in self.wd_mult:
-                wds[i] *= self.wd_mult[index]
-            elif index in self.idx2name:
-                wds[i] *= self.wd_mult.get(self.idx2name[index], 1.0)
-        return wds
+        return [self.wd * self._mult(i, self.wd_mult, 'wd_mult') for i in indices]
 
     def _get_wd(self, index):
         return self._get_wds([index])[0]
@@ -210,12 +198,55 @@ class Optimizer:
     def _clip(self):
         return -1.0 if self.clip_gradient is None else self.clip_gradient
 
+    # ------------------------------------------------------------------ states and updates
+    def create_state(self, index, weight):
+        return None
+
+    def _wants_master(self, weight):
+        return self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16)
+
+    def create_state_multi_precision(self, index, weight):
+        """With ``multi_precision`` and a half-precision weight: ``(fp32 master copy, state of the
+        master)``; otherwise the plain state."""
+        if self._wants_master(weight):
+            master = NDArray(weight._data.detach().float().clone())
+            return (master, self.create_state(index, master))
+        if weight._data.dtype in (torch.float16, torch.bfloat16):
+            warnings.warn('Accumulating with float16 in optimizer can lead to poor accuracy or slow convergence. '
+                          'Consider using multi_precision=True option of the optimizer')
+        return self.create_state(index, weight)
+
+    def update(self, index, weight, grad, state):
+        raise NotImplementedError()
+
+    def update_multi_precision(self, index, weight, grad, state):
+        """``update`` on the fp32 master copy (then rounded into the weight) for half-precision weights
+        under ``multi_precision``; lists of indices are updated one by one."""
+        if isinstance(index, (list, tuple)):
+            for args in zip(index, weight, grad, state):
+                self.update_multi_precision(*args)
+            return
+        if not self._wants_master(weight):
+            self.update(index, weight, grad, state)
+            return
+        master, inner = state
+        # sparse gradients keep their storage (lazy row updates need the row indices)
+        g32 = grad.astype('float32') if getattr(grad, 'stype', 'default') != 'default' else NDArray(grad._data.float())
+        self.update(index, master, g32, inner)
+        with torch.no_grad():
+            weight._data.copy_(master._data)
+
     def __getstate__(self):
-        ret = self.__dict__.copy()
-        del ret['param_dict']
-        return ret
+        state = dict(self.__dict__)
+        state.pop('param_dict', None)      # Gluon Parameters do not travel with a pickled optimizer
+        return state
 
     def __setstate__(self, state):
+        if '_counts' not in state:        # optimizer states pickled by an older version of this class
+            counts = _UpdateCounts(state.get('begin_num_update', 0))
+            counts.tables = state.pop('_all_index_update_counts', {0: {}})
+            counts.current = state.pop('_index_update_count', counts.tables.setdefault(0, {}))
+            state['_counts'] = counts
         self.__dict__ = state
         self.param_dict = {}
 
@@ -539,12 +570,6 @@ class LAMB(Optimizer):
         z = lambda: NDArray(torch.zeros_like(weight._data, dtype=torch.float32))
         return (z(), z())
 
-    def create_state_multi_precision(self, index, weight):
-        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
-            w32 = NDArray(weight._data.float())
-            return (w32,) + self.create_state(index, w32)
-        return self.create_state(index, weight)
-
     def _step(self, index, weight, grad, mean, var, w32=None):
         self._update_count(index)
         lr = self._get_lr(index)
@@ -564,8 +589,14 @@ class LAMB(Optimizer):
         self._step(index, weight, grad, mean._data, var._data)
 
     def update_multi_precision(self, index, weight, grad, state):
-        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
-            w32, mean, var = state
+        """Multi-precision state = (fp32 master, (mean, var)) (the reference layout); lists of indices
+        (aggregated updates) are applied tensor by tensor."""
+        if isinstance(index, (list, tuple)):
+            for args in zip(index, weight, grad, state):
+                self.update_multi_precision(*args)
+            return
+        if self._wants_master(weight):
+            w32, (mean, var) = state
             self._step(index, weight, grad, mean._data, var._data, w32=w32._data)
         else:
             self.update(index, weight, grad, state)

@@ -41,7 +41,7 @@ def _synthetic_model_store(dst, env):
         shutil.copy(cached, os.path.join(dst, fname))
 
 
-def run_one(ref, name, timeout, workers, select=None, tb=None):
+def run_one(ref, name, timeout, workers, select=None, tb=None, extra=()):
     tmp = tempfile.mkdtemp(prefix='mxref_')
     try:
         unit = os.path.join(tmp, 'unittest')
@@ -79,6 +79,8 @@ def run_one(ref, name, timeout, workers, select=None, tb=None):
             cmd[3:3] = ['-k', select]
         if tb:
             cmd[3:3] = ['--tb', tb]
+        if extra:
+            cmd[3:3] = list(extra)
         r = subprocess.run(cmd, cwd=unit, env=env, capture_output=True, text=True)
         tail = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr[-500:]
         counts = {k: 0 for k in ('passed', 'failed', 'skipped', 'errors', 'error', 'xfailed', 'xpassed')}
@@ -100,9 +102,10 @@ def main():
     ap.add_argument('--show-failures', action='store_true')
     ap.add_argument('-k', dest='select', default=None, help='pytest -k expression')
     ap.add_argument('--tb', default=None, help='pytest traceback style; prints the full output')
+    ap.add_argument('--pytest-arg', action='append', default=[], help='extra pytest argument (repeatable)')
     a = ap.parse_args()
     for name in a.names:
-        res = run_one(a.ref, name, a.timeout, a.workers, a.select, a.tb)
+        res = run_one(a.ref, name, a.timeout, a.workers, a.select, a.tb, a.pytest_arg)
         out = res.pop('output')
         if a.tb:
             print(out)
