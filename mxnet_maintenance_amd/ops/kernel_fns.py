@@ -307,6 +307,53 @@ def conv_ok_shape(x, w, stride, pad, dilate=(1, 1), groups=1):
             and w.data_ptr() % 16 == 0)
 
 
+def stem_ok(x, w, stride, pad, bias=None):
+    """True when the few-channel stride-2 stem kernel (src/kernels/conv_stem.hip) handles this conv:
+    Cin <= 4, Cout = 64, kernel up to 8x8, stride 2, no bias."""
+    return (_CONV_HIP and bias is None and x.dim() == 4 and w.dim() == 4 and x.dtype in (torch.float16, torch.bfloat16)
+            and w.dtype == x.dtype and x.is_contiguous() and w.is_contiguous() and 1 <= x.shape[3] <= 4
+            and w.shape[3] == x.shape[3] and w.shape[0] == 64 and w.shape[1] <= 8 and w.shape[2] <= 8
+            and tuple(stride) == (2, 2) and all(0 <= p < 8 for p in pad) and _K.available()
+            and hasattr(_K.lib(), 'conv_stem_fwd'))
+
+
+def conv_stem_fwd(x, w, pad, bn_stats=False):
+    """y[N,Ho,Wo,64] of a stride-2 stem conv on MFMA (conv_stem.hip); ``bn_stats``: also emit the
+    BatchNorm sum / sum-of-squares partials of y (``y._mxamd_bn_part``)."""
+    N, H, W, C = x.shape
+    K, R, S, _ = w.shape
+    Ho = (H + 2 * pad[0] - R) // 2 + 1
+    Wo = (W + 2 * pad[1] - S) // 2 + 1
+    y = torch.empty((N, Ho, Wo, K), dtype=x.dtype, device=x.device)
+    lib = _K.lib()
+    part, nparts = None, 0
+    if bn_stats:
+        nparts = 4 * lib.conv_stem_grid(N, H, W, R, S, pad[0], pad[1])
+        part = torch.empty(2 * K * nparts, dtype=torch.float32, device=x.device)
+    lib.conv_stem_fwd(_DT[x.dtype], x.data_ptr(), w.data_ptr(), y.data_ptr(), N, H, W, C, K, R, S, 2, 2, pad[0],
+                      pad[1], _p(part), nparts, _stream())
+    if part is not None:
+        y._mxamd_bn_part = (part, nparts)
+    return y
+
+
+def conv_stem_wgrad(x, dy, wshape, pad, out=None, accum=False):
+    """dW[64,R,S,C] of a stride-2 stem conv: per-workgroup fp32 slabs summed in a fixed order."""
+    N, H, W, C = x.shape
+    K, R, S, _ = wshape
+    dy = dy.contiguous()
+    lib = _K.lib()
+    slab = torch.empty(lib.conv_stem_wgrad_workspace(N, H, W, R, S, pad[0], pad[1]), dtype=torch.float32,
+                       device=x.device)
+    if out is None:
+        out = torch.empty((K, R, S, C), dtype=x.dtype, device=x.device)
+        accum = False
+    assert out.is_contiguous() and out.numel() == K * R * S * C and out.dtype in _DT
+    lib.conv_stem_wgrad(_DT[x.dtype], x.data_ptr(), dy.data_ptr(), slab.data_ptr(), _DT[out.dtype], out.data_ptr(),
+                        int(bool(accum)), N, H, W, C, K, R, S, 2, 2, pad[0], pad[1], _stream())
+    return out
+
+
 # 512-thread big-tile LDS-DMA kernel (conv_big.hip): variant -> (BCO, BPIX)
 _BIG_VARIANTS = {10: (256, 256), 11: (128, 256), 12: (64, 512), 13: (256, 128)}
 # persistent LDS-DMA ring kernel (conv_ring.hip): variant -> (BCO, BPIX); no bias
@@ -715,6 +762,8 @@ def _select(key, cands, default, timing=None):
 def _fwd_candidates(x, w, stride, pad, bias):
     c = []
     K, R, S, C = w.shape
+    if stem_ok(x, w, stride, pad, bias):
+        c.append(('stem', lambda: conv_stem_fwd(x, w, pad, bn_stats=bool(_state.STATE.training))))
     if conv_ok_shape(x, w, stride, pad):
         c.append(('hip', lambda: conv_fwd(x, w, stride, pad, bias)))
         stats = bool(_state.STATE.training)
@@ -774,6 +823,8 @@ def _fwd_timing(cands):
 
 def _fwd_default(x, w, stride):
     K, R, S, C = w.shape
+    if C <= 4 and K == 64 and tuple(stride) == (2, 2) and R <= 8 and S <= 8:
+        return 'stem'
     if R == 1 and S == 1 and tuple(stride) == (1, 1) and (K >= 256 or x.shape[1] * x.shape[2] <= 784):
         return 'mm'
     return 'hip'
@@ -878,6 +929,8 @@ def _dgrad_default(w, stride):
 def _wgrad_candidates(dy, x, w, stride, pad):
     c = [('miopen', lambda: _conv_bwd_torch(dy, x, w, stride, pad, (False, True))[1])]
     K, R, S, C = w.shape
+    if stem_ok(x, w, stride, pad):
+        c.insert(0, ('stem', lambda: conv_stem_wgrad(x, dy, w.shape, pad)))
     if conv_wgrad_ok(x, w):
         c.insert(0, ('hip', lambda: conv_wgrad(x, dy, w.shape, stride, pad)))
         c.insert(1, ('hipreg', lambda: conv_wgrad(x, dy, w.shape, stride, pad, dma=False)))
@@ -944,6 +997,11 @@ def _wgrad(dy, x, w, w_ref, stride, pad):
     """
     key = ('wgrad', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype)
     algo = _ALGO.get(_akey(key))
+    if algo == 'stem':
+        tgt = _leaf_grad(w_ref, dtype=w.dtype)
+        if tgt is not None:
+            conv_stem_wgrad(x, dy, w.shape, pad, out=tgt, accum=True)
+            return None
     if algo in ('hip', 'hipreg') or (algo or '').startswith('ring'):
         tgt = _leaf_grad(w_ref, dtype=w.dtype)
         if tgt is not None:
@@ -955,7 +1013,8 @@ def _wgrad(dy, x, w, w_ref, stride, pad):
         if tgt is not None:
             _splitk_wgrad(dy, x, int(algo[6:]), out=tgt)
             return None
-    dw = _select(key, _wgrad_candidates(dy, x, w, stride, pad), 'hip' if conv_wgrad_ok(x, w) else 'miopen')
+    default = 'stem' if stem_ok(x, w, stride, pad) else ('hip' if conv_wgrad_ok(x, w) else 'miopen')
+    dw = _select(key, _wgrad_candidates(dy, x, w, stride, pad), default)
     if dw.dtype != w.dtype:
         tgt = _leaf_grad(w_ref, dtype=w.dtype)
         if tgt is not None:
@@ -1108,7 +1167,8 @@ def conv_ok(x, w, stride, pad, dilate, groups):
             and w.is_contiguous() and x.dtype in (torch.float16, torch.bfloat16) and w.dtype == x.dtype)
 
 
-__all__ += ['ConvNHWC', 'ConvTeeNHWC', 'conv_fwd', 'conv_ok_shape', 'conv_wgrad', 'conv_wgrad_ok']
+__all__ += ['ConvNHWC', 'ConvTeeNHWC', 'conv_fwd', 'conv_ok_shape', 'conv_wgrad', 'conv_wgrad_ok', 'stem_ok',
+            'conv_stem_fwd', 'conv_stem_wgrad']
 
 
 # ---------------------------------------------------------------------------

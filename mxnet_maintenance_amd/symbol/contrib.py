@@ -16,6 +16,30 @@ def _as_list(x):
     return (list(x), True) if isinstance(x, (list, tuple)) else ([x], False)
 
 
+def _flat(x):
+    """(flat list of leaves, format) of a possibly nested list of symbols; the format is None for a
+    single symbol, else the list of the items' formats (so ``[]`` and ``[[a], b]`` round-trip)."""
+    if not isinstance(x, (list, tuple)):
+        return [x], None
+    leaves, fmt = [], []
+    for item in x:
+        lv, f = _flat(item)
+        leaves.extend(lv)
+        fmt.append(f)
+    return leaves, fmt
+
+
+def _unflat(leaves, fmt):
+    """Inverse of _flat: (structure, leaves left over)."""
+    if fmt is None:
+        return leaves[0], leaves[1:]
+    out = []
+    for f in fmt:
+        item, leaves = _unflat(leaves, f)
+        out.append(item)
+    return out, leaves
+
+
 def _free_vars(g, exclude):
     from .symbol import Symbol
     out = []
@@ -26,15 +50,20 @@ def _free_vars(g, exclude):
 
 
 def foreach(body, data, init_states, name='foreach'):
-    """Run ``body(data_t, states) -> (outputs, new_states)`` over the leading axis of ``data``."""
+    """Run ``body(data_t, states) -> (outputs, new_states)`` over the leading axis of ``data``.
+
+    ``data``, ``init_states`` and the body's outputs may be (nested) lists; the results keep the
+    body's structure (an empty output list stays empty), as the reference's _flatten / _regroup do."""
     from .symbol import var, Group, _create
-    data_l, data_is_list = _as_list(data)
-    states_l, states_is_list = _as_list(init_states)
+    data_l, data_fmt = _flat(data)
+    states_l, states_fmt = _flat(init_states)
     d_ph = [var('%s_data%d' % (name, i)) for i in range(len(data_l))]
     s_ph = [var('%s_state%d' % (name, i)) for i in range(len(states_l))]
-    outs, new_states = body(d_ph if data_is_list else d_ph[0], s_ph if states_is_list else s_ph[0])
-    outs_l, outs_is_list = _as_list(outs)
-    new_l, _ = _as_list(new_states)
+    outs, new_states = body(_unflat(d_ph, data_fmt)[0], _unflat(s_ph, states_fmt)[0])
+    outs_l, outs_fmt = _flat(outs if outs is not None else [])
+    new_l, new_fmt = _flat(new_states)
+    if len(new_l) != len(states_l):
+        raise ValueError('foreach: the body returned %d states for %d initial states' % (len(new_l), len(states_l)))
     g = Group(outs_l + new_l)
     ph_names = {s.name for s in d_ph + s_ph}
     remain = _free_vars(g, ph_names)
@@ -43,23 +72,25 @@ def foreach(body, data, init_states, name='foreach'):
              'remain_names': _json.dumps([s.name for s in remain]), 'num_out_data': len(outs_l)}
     node = _create('_foreach', {'_pos': data_l + states_l + remain}, attrs, name=name)
     res = list(node)
-    o = res[:len(outs_l)]
-    st = res[len(outs_l):]
-    return (o if outs_is_list else o[0]), (st if states_is_list else st[0])
+    return _unflat(res[:len(outs_l)], outs_fmt)[0], _unflat(res[len(outs_l):], new_fmt)[0]
 
 
 def while_loop(cond, func, loop_vars, max_iterations=None, name='while_loop'):
-    """Symbolic while loop; per-step outputs are padded to ``max_iterations``."""
+    """Symbolic while loop; per-step outputs are padded to ``max_iterations``.  Loop variables and
+    step outputs may be (nested) lists; the results keep their structure."""
     from .symbol import var, Group, _create
     if max_iterations is None:
         raise ValueError('max_iterations should be specified')
-    vars_l, vars_is_list = _as_list(loop_vars)
+    vars_l, vars_fmt = _flat(loop_vars)
     ph = [var('%s_var%d' % (name, i)) for i in range(len(vars_l))]
-    arg = ph if vars_is_list else ph[0]
-    c = cond(*ph) if vars_is_list else cond(arg)
-    outs, new_vars = func(*ph) if vars_is_list else func(arg)
-    outs_l, outs_is_list = _as_list(outs) if outs is not None else ([], True)
-    new_l, _ = _as_list(new_vars)
+    arg = _unflat(ph, vars_fmt)[0]
+    as_args = isinstance(arg, list)
+    c = cond(*arg) if as_args else cond(arg)
+    outs, new_vars = func(*arg) if as_args else func(arg)
+    outs_l, outs_fmt = _flat(outs if outs is not None else [])
+    new_l, _ = _flat(new_vars)
+    if len(new_l) != len(vars_l):
+        raise ValueError('while_loop: func returned %d loop variables for %d' % (len(new_l), len(vars_l)))
     fg = Group(outs_l + new_l)
     cg = Group([c])
     ph_names = {s.name for s in ph}
@@ -70,9 +101,8 @@ def while_loop(cond, func, loop_vars, max_iterations=None, name='while_loop'):
              'max_iterations': int(max_iterations)}
     node = _create('_while_loop', {'_pos': vars_l + remain}, attrs, name=name)
     res = list(node)
-    o = res[:len(outs_l)]
-    v = res[len(outs_l):]
-    return (o if outs_is_list else (o[0] if o else [])), (v if vars_is_list else v[0])
+    # final loop variables take the structure of the initial ones (reference symbol/contrib.py)
+    return _unflat(res[:len(outs_l)], outs_fmt)[0], _unflat(res[len(outs_l):], vars_fmt)[0]
 
 
 def cond(pred, then_func, else_func, name='cond'):

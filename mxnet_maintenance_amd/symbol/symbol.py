@@ -462,7 +462,9 @@ class Symbol:
             if not complete and not partial:
                 warnings.warn('Cannot decide shape for some arguments', stacklevel=2)
                 return None, None, None
-            fix = lambda l: [s if s is not None else () for s in l]
+            from ..util import is_np_shape
+            empty = None if is_np_shape() else ()      # a completely unknown shape
+            fix = lambda l: [s if s is not None else empty for s in l]     # noqa: E731
             return fix(arg_res), fix(out_res), fix(aux_res)
         complete = all(s is not None for s in arg_res + out_res + aux_res)
         if not complete and not partial:
@@ -795,6 +797,17 @@ def _attr_shape(node):
     return t
 
 
+def _partial_attr_shape(node):
+    """A variable's declared shape when it has some (not all) unknown dims."""
+    v = node.attrs.get('__shape__')
+    if v is None:
+        return None
+    t = registry.parse_value('shape', v)
+    if not t or all(int(d) <= 0 for d in t) or all(int(d) > 0 for d in t):
+        return None
+    return t
+
+
 def _attr_dtype(node):
     d = node.attrs.get('__dtype__')
     if d is None:
@@ -849,7 +862,8 @@ _SAME_SHAPE = frozenset(['elemwise_add', 'elemwise_sub', 'elemwise_mul', 'elemwi
                          'arctan', 'sinh', 'cosh', 'arcsinh', 'arccosh', 'arctanh', 'degrees', 'radians',
                          'expm1', 'log1p', 'log2', 'log10', 'rsqrt', 'cbrt', 'rcbrt', 'reciprocal', 'sign',
                          'round', 'rint', 'ceil', 'floor', 'trunc', 'fix', 'erf', 'erfinv', 'gamma', 'gammaln',
-                         'LeakyReLU', 'softrelu', 'clip', 'zeros_like', 'ones_like', '_FusedOp'])
+                         'LeakyReLU', 'softrelu', 'clip', 'zeros_like', 'ones_like', '_FusedOp',
+                         '_identity_with_attr_like_rhs'])
 
 _INIT_OPS = ('_zeros', '_ones', '_full', '_empty', 'zeros', 'ones', 'full')
 
@@ -861,6 +875,7 @@ def _unify_shapes(order, seeds):
     directions, until nothing changes.  ``seeds``: (id(node), 0) -> partial shape.  Returns the
     (id(node), out) -> partial shape map (unknown dims -1)."""
     part = {}
+    memo = {}
 
     def merge(key, s):
         if s is None:
@@ -927,9 +942,141 @@ def _unify_shapes(order, seeds):
                     total = math.prod(dst)
                     if known and total % known == 0:
                         changed |= merge(keys[0], tuple(d if d > 0 else total // known for d in src))
+            elif n.op not in _PROBE_SKIP:
+                changed |= _probe_node(n, keys, part, merge, memo)
         if not changed:
             break
     return part
+
+
+# ---- probing: partial shape inference through any operator's own shape function ----------------
+# nnvm lets every operator infer shapes both ways with unknown dims.  Here each operator has one
+# forward shape function (its meta-tensor execution), so unknown dims are *probed*: run the function
+# with the unknown dims set to two different values; output dims that do not move are known.  The
+# inverse direction solves for an input dim: an output dim that moves linearly with it and is known
+# downstream determines it (checked by re-running the function with the solution).
+_PROBES = (509, 521)
+_PROBE_SKIP = frozenset(['where', '_npi_where'])      # the reference needs a fully known condition
+_PROBE_MAX_ELEMS = 1 << 34
+
+
+def _probe_eval(n, shapes):
+    """Output shapes of node ``n`` for fully known input shapes, or None when the op rejects them."""
+    if any(math.prod(s) > _PROBE_MAX_ELEMS for s in shapes):
+        return None
+    try:
+        return [o[0] for o in _run_meta(n.opdef(), n.parsed(), shapes, [torch.float32] * len(shapes))]
+    except Exception:   # pylint: disable=broad-except
+        return None
+
+
+def _probe_params(n, shapes):
+    """Parameter shapes an operator derives from its (fully known) data shapes, or {}."""
+    fn = n.opdef().infer_params
+    if fn is None:
+        return {}
+    try:
+        return {i: tuple(int(d) for d in v) for i, v in fn(shapes, n.parsed()).items()}
+    except Exception:   # pylint: disable=broad-except
+        return {}
+
+
+def _subst(shapes, value, only=None):
+    """Unknown dims (-1) replaced by ``value`` (``only``: just that (input, dim); others get probe 0)."""
+    out = []
+    for i, s in enumerate(shapes):
+        row = []
+        for d, v in enumerate(s):
+            if v > 0:
+                row.append(v)
+            elif only is None or only == (i, d):
+                row.append(value)
+            else:
+                row.append(_PROBES[0])
+        out.append(tuple(row))
+    return out
+
+
+def _probe_node(n, keys, part, merge, memo):
+    ins = [part.get(k) for k in keys]
+    nout = n.num_outputs()
+    outs = [part.get((id(n), i)) for i in range(nout)]
+    sig = (tuple(ins), tuple(outs))
+    if memo.get(id(n)) == sig:
+        return False
+    memo[id(n)] = sig
+    changed = False
+    # parameters (weights, biases) from partially known data: probe the data dims
+    if ins and ins[0] is not None and any(s is None for s in ins[1:]):
+        def filled(v):
+            return [None if x is None else _subst([x], v)[0] for x in ins]
+        a = _probe_params(n, filled(_PROBES[0]))
+        b = _probe_params(n, filled(_PROBES[1]))
+        for idx in a:
+            if idx < len(keys) and ins[idx] is None and idx in b and len(a[idx]) == len(b[idx]):
+                changed |= merge(keys[idx], tuple(x if x == y else -1 for x, y in zip(a[idx], b[idx])))
+        ins = [part.get(k) for k in keys]
+    if not ins or any(s is None for s in ins):
+        return changed
+    unknown = [(i, d) for i, s in enumerate(ins) for d, v in enumerate(s) if v <= 0]
+    if not unknown:
+        res = _probe_eval(n, list(ins))
+        if res is not None:
+            for i, o in enumerate(res[:nout]):
+                changed |= merge((id(n), i), o)
+        return changed
+    # forward: dims of the outputs that do not depend on the unknown input dims
+    r1 = _probe_eval(n, _subst(ins, _PROBES[0]))
+    r2 = _probe_eval(n, _subst(ins, _PROBES[1]))
+    if r1 is not None and r2 is not None and len(r1) == len(r2):
+        for i, (a, b) in enumerate(zip(r1[:nout], r2[:nout])):
+            if len(a) == len(b):
+                changed |= merge((id(n), i), tuple(x if x == y else -1 for x, y in zip(a, b)))
+    # backward: solve unknown input dims from known output dims (all together first, then one by one)
+    outs = [part.get((id(n), i)) for i in range(nout)]
+    if not any(o is not None and any(v > 0 for v in o) for o in outs):
+        return changed
+    for only in [None] + unknown:
+        sol = _solve_dim(n, ins, outs, only)
+        if sol is None:
+            continue
+        for i, s in enumerate(ins):
+            new = tuple(sol if (v <= 0 and (only is None or only == (i, d))) else v for d, v in enumerate(s))
+            changed |= merge(keys[i], new)
+        if only is None:
+            break
+        ins = [part.get(k) for k in keys]
+    return changed
+
+
+def _solve_dim(n, ins, outs, only):
+    """The value of the probed unknown dim(s) that reproduces every known output dim, or None."""
+    p0, p1 = _PROBES
+    ra = _probe_eval(n, _subst(ins, p0, only))
+    rb = _probe_eval(n, _subst(ins, p1, only))
+    if ra is None or rb is None:
+        return None
+    cands = set()
+    for o, a, b in zip(outs, ra, rb):
+        if o is None or len(o) != len(a) or len(a) != len(b):
+            continue
+        for t, x, y in zip(o, a, b):
+            if t > 0 and x != y:
+                slope = (y - x) / float(p1 - p0)
+                v = p0 + (t - x) / slope
+                for c in (math.floor(v), math.ceil(v), math.floor(v) - 1):
+                    if c >= 1:
+                        cands.add(int(c))
+    for c in sorted(cands):
+        r = _probe_eval(n, _subst(ins, c, only))
+        if r is None:
+            continue
+        # every known output dim that depends on the probed dim(s) must come out right
+        if all(o is None or (len(o) == len(x) and all(t <= 0 or xa == xb or t == v
+                                                        for t, v, xa, xb in zip(o, x, a, b)))
+               for o, x, a, b in zip(outs, r, ra, rb)):
+            return c
+    return None
 
 
 def _unify_init_shapes(order):
@@ -1093,16 +1240,20 @@ def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True, pa
     Returns (arg_list, out_list, aux_list) of shapes (or dtypes), None for unknown.
     """
     order = sym._topo()
-    if what == 'shape' and known_shapes and any(any(int(d) <= 0 for d in v) for v in known_shapes.values() if v):
-        # arguments given with unknown dims: size them by unification when the graph determines them
+    part = None
+    partial_attr = any(n.op is None and n.name not in known_shapes and _partial_attr_shape(n) for n in order)
+    if what == 'shape' and (partial_attr or (known_shapes and any(any(int(d) <= 0 for d in v)
+                                                                  for v in known_shapes.values() if v))):
+        # arguments with unknown dims (given or declared): size what the graph determines by
+        # bidirectional unification / probing; the rest stays partial
         byname = {n.name: n for n in order if n.op is None}
         seeds = {(id(byname[k]), 0): v for k, v in known_shapes.items() if k in byname and v}
         part = _unify_shapes(order, seeds)
         known_shapes = dict(known_shapes)
-        for k in list(known_shapes):
-            r = part.get((id(byname[k]), 0)) if k in byname else None
-            if r is not None and all(d > 0 for d in r):
-                known_shapes[k] = r
+        for name, node in byname.items():
+            r = part.get((id(node), 0))
+            if r is not None and len(r) and all(d > 0 for d in r):
+                known_shapes[name] = r
     if _resolve and what == 'shape' and known_shapes:
         res = _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what)
         if res is not None:
@@ -1137,6 +1288,12 @@ def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True, pa
                 except Exception:
                     fill = {}
                 for idx, s in fill.items():
+                    if (idx < len(n.inputs) and in_shapes[idx] is not None and len(s) and len(in_shapes[idx])
+                            and all(int(d) > 0 for d in in_shapes[idx]) and all(int(d) > 0 for d in s)
+                            and tuple(int(d) for d in in_shapes[idx]) != tuple(int(d) for d in s)):
+                        raise MXNetError('Error in operator %s (%s): shape inconsistent for input %d: '
+                                         'provided %s, inferred %s' % (n.name, n.op, idx, tuple(in_shapes[idx]),
+                                                                       tuple(s)))
                     if idx < len(n.inputs) and in_shapes[idx] is None:
                         a, j = n.inputs[idx]
                         shape[(id(a), j)] = tuple(s)
@@ -1197,6 +1354,9 @@ def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True, pa
                 raise MXNetError('Error in operator %s (%s): incompatible input shapes %s'
                                  % (n.name, n.op, [tuple(x) for x in in_shapes]))
             pfn = _PARTIAL_OUT.get(n.op) if partial else None
+            if partial and n.op in _PROBE_SKIP and any(_unknown_dims(s) for s in in_shapes):
+                done.add(id(n))         # e.g. where: the output is unknown until the condition is known
+                continue
             if pfn is not None and any(_unknown_dims(s) for s in in_shapes):
                 outs = [(pfn(in_shapes[0], parsed), base_dt)]
             else:
@@ -1229,6 +1389,12 @@ def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True, pa
                     dtype[(id(n), 0)] = torch.float32
     if what == 'shape' and partial:
         _partial_zero_dims(order, shape)
+        if part is not None:
+            from .. import util
+            unk = -1 if util.is_np_shape() else 0
+            for key, v in part.items():
+                if shape.get(key) is None and v:
+                    shape[key] = tuple(d if d > 0 else unk for d in v)
     aux = _aux_var_ids(order)
     table = shape if what == 'shape' else dtype
     args = [table.get((id(n), 0)) for n in order if n.op is None and id(n) not in aux]

@@ -84,6 +84,12 @@ int64_t conv_nhwc_wgrad_workspace(int N, int H, int W, int C, int K, int R, int 
 void conv_nhwc_wgrad(int dtype, const void* x, const void* dy, float* slab, int out_dtype, void* out, int accum, int N,
                      int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, const void* zero,
                      hipStream_t s);
+int conv_stem_grid(int N, int H, int W, int R, int S, int ph, int pw);
+void conv_stem_fwd(int dtype, const void* x, const void* w, void* y, int N, int H, int W, int C, int K, int R, int S,
+                   int sh, int sw, int ph, int pw, float* part, int nparts, hipStream_t s);
+int64_t conv_stem_wgrad_workspace(int N, int H, int W, int R, int S, int ph, int pw);
+void conv_stem_wgrad(int dtype, const void* x, const void* dy, float* slab, int out_dtype, void* out, int accum, int N,
+                     int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, hipStream_t s);
 int layernorm_bwd_partials(int M);
 void layernorm_forward(int dtype, const void* x, const float* gamma, const float* beta, void* y, float* mean,
                        float* rstd, int M, int D, float eps, hipStream_t s);
@@ -309,6 +315,22 @@ PYBIND11_MODULE(_hip_kernels, m) {
         });
   // 512-thread big-tile kernel: variant 0..3 = 256x256, 128x256, 64x512, 256x128 (co x pix);
   // part (optional): channel-major [2][K][nparts] BatchNorm sum / sum-of-squares partials of y
+  // few-channel stride-2 stems (conv_stem.hip): Cin <= 4, Cout = 64, kernel up to 8x8
+  m.def("conv_stem_grid", &conv_stem_grid);
+  m.def("conv_stem_wgrad_workspace", &conv_stem_wgrad_workspace);
+  m.def("conv_stem_fwd", [](int dt, uintptr_t x, uintptr_t w, uintptr_t y, int N, int H, int W, int C, int K, int R,
+                            int Sf, int sh, int sw, int ph, int pw, uintptr_t part, int nparts, uintptr_t s) {
+    conv_stem_fwd(dt, P<void>(x), P<void>(w), P<void>(y), N, H, W, C, K, R, Sf, sh, sw, ph, pw, P<float>(part),
+                  nparts, S(s));
+    check_launch("conv_stem_fwd");
+  });
+  m.def("conv_stem_wgrad", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t slab, int odt, uintptr_t out, int accum,
+                              int N, int H, int W, int C, int K, int R, int Sf, int sh, int sw, int ph, int pw,
+                              uintptr_t s) {
+    conv_stem_wgrad(dt, P<void>(x), P<void>(dy), P<float>(slab), odt, P<void>(out), accum, N, H, W, C, K, R, Sf, sh,
+                    sw, ph, pw, S(s));
+    check_launch("conv_stem_wgrad");
+  });
   m.def("conv_nhwc_fwd_big_nparts", &conv_nhwc_fwd_big_nparts);
   m.def("conv_nhwc_fwd_big_bwd_nparts", &conv_nhwc_fwd_big_bwd_nparts);
   // bn (optional): (z, mean, scale, shift, mask, mode, part, nparts) -- BN-backward statistics of y
