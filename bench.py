@@ -44,6 +44,9 @@ def main():
     ap.add_argument('--image-size', type=int, default=224)
     ap.add_argument('--layout', default='NHWC', choices=['NHWC', 'NCHW'],
                     help='model layout (NCHW = default Gluon layout, executed channels-last on the HIP kernels)')
+    ap.add_argument('--lr-warmup', type=int, default=None,
+                    help='linear learning-rate warm-up steps from 0 to 0.1 (default: the --warmup count); '
+                         'lr 0.1 from random init on one fixed batch otherwise overshoots before it fits it')
     ap.add_argument('--graph', default='auto', choices=['auto', 'on', 'off'],
                     help='capture the whole training step in one HIP graph (gluon.GraphStep); auto = on for 1 GPU')
     args = ap.parse_args()
@@ -85,8 +88,12 @@ def main():
     net.hybridize(static_alloc=True, static_shape=True)
 
     loss_scale = 128.0 if args.dtype == 'float16' else 1.0
+    warm = args.warmup if args.lr_warmup is None else args.lr_warmup
+    # constant 0.1 after a linear ramp; the schedule is device-staged per HIP-graph replay
+    sched = mx.lr_scheduler.FactorScheduler(step=1 << 30, factor=1.0, base_lr=0.1, warmup_steps=warm,
+                                            warmup_begin_lr=0.0) if warm > 0 else None
     trainer = gluon.Trainer(net.collect_params(), 'sgd',
-                            {'learning_rate': 0.1, 'momentum': 0.9, 'wd': 1e-4,
+                            {'learning_rate': 0.1, 'momentum': 0.9, 'wd': 1e-4, 'lr_scheduler': sched,
                              'multi_precision': args.dtype != 'float32',
                              'rescale_grad': 1.0 / loss_scale},
                             kvstore='device')
@@ -120,8 +127,15 @@ def main():
         # forward + backward + fused mp-SGD replayed as one graph; the first warm-up calls run eagerly
         # (kernel autotuning, arena construction) and the last one captures
         step = gluon.GraphStep(step, trainer, warmup=max(1, args.warmup - 1), fallback=args.graph == 'auto')
-    for _ in range(args.warmup):
-        step()
+    first_loss = None
+    trace = os.environ.get('MXAMD_BENCH_VERBOSE', '0') == '1'
+    for i in range(args.warmup):
+        out = step()
+        if i == 0 or trace:
+            v = float(out.mean().asscalar()) / loss_scale     # host read: outside the timed region
+            first_loss = v if first_loss is None else first_loss
+            if trace and rank == 0:
+                print('warmup step %d loss %.4f' % (i, v), file=sys.stderr, flush=True)
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -150,7 +164,9 @@ def main():
                          'same_config': False},
             'config': {'model': args.model.replace('resnet50_v1b', 'ResNet-50 v1b'), 'global_batch': B * n,
                        'per_gpu_batch': B, 'seq_len': None, 'image_size': S, 'parallelism': 'dp%d' % n,
-                       'layout': args.layout, 'optimizer': 'mp-SGD momentum 0.9', 'final_loss': round(loss_val, 4),
+                       'layout': args.layout, 'optimizer': 'mp-SGD momentum 0.9, lr 0.1 (linear warm-up %d steps)' % warm,
+                       'first_loss': None if first_loss is None else round(first_loss, 4),
+                       'final_loss': round(loss_val, 4),
                        'hip_graph': bool(use_graph and getattr(step, 'captured', False))},
         }), flush=True)
     if os.environ.get('MXAMD_BENCH_VERBOSE', '0') == '1' and rank == 0:

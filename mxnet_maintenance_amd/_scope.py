@@ -1,14 +1,28 @@
 """Thread-local "current object" stacks shared by NameManager and AttrScope.
 
-A scope class derived from ``_ThreadScope`` gets ``current()`` (lazily
-creating a default instance per thread) and ``with``-statement support that
+A scope class derived from ``_ThreadScope`` gets the class property ``current`` (lazily
+creating a default instance per thread; assignable) and ``with``-statement support that
 pushes / pops itself on a per-thread stack.  ``_on_enter(outer)`` lets a
 scope inherit state from the scope it is nested in.
 """
 import threading
 
 
-class _ThreadScope:
+class _ScopeMeta(type):
+    """``Scope.current`` is a thread-local class property: reading gives this thread's innermost
+    scope, assigning replaces it (reference: ``AttrScope._current = threading.local()`` with the
+    ``current`` class property of python/mxnet/attribute.py and name.py)."""
+
+    @property
+    def current(cls):
+        return cls._stack()[-1]
+
+    @current.setter
+    def current(cls, scope):
+        cls._stack()[-1] = scope
+
+
+class _ThreadScope(metaclass=_ScopeMeta):
     _tls = None            # each subclass gets its own threading.local (see __init_subclass__)
 
     def __init_subclass__(cls, **kw):
@@ -30,10 +44,6 @@ class _ThreadScope:
         # whose constructor needs arguments)
         owner = next(c for c in cls.__mro__ if '_tls' in c.__dict__ and c is not _ThreadScope)
         return owner()
-
-    @classmethod
-    def current(cls):
-        return cls._stack()[-1]
 
     def _on_enter(self, outer):
         """Hook: adapt to the enclosing scope ``outer``."""

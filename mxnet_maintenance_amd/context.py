@@ -12,7 +12,21 @@ __all__ = ['Context', 'cpu', 'gpu', 'cpu_pinned', 'cpu_shared', 'num_gpus',
            'gpu_memory_info', 'current_context', 'Device', 'device']
 
 
-class Context:
+class _ContextMeta(type):
+    """``Context.default_ctx`` is per thread (reference context.py:70: a ``threading.local``
+    behind a class property): each thread starts on cpu(0) and ``with ctx:`` / assignment only
+    change the calling thread's default."""
+
+    @property
+    def default_ctx(cls):
+        return current_context()
+
+    @default_ctx.setter
+    def default_ctx(cls, ctx):
+        Context._default_ctx.value = ctx
+
+
+class Context(metaclass=_ContextMeta):
     """A device context: ``cpu``, ``gpu``, ``cpu_pinned`` or ``cpu_shared``."""
     _default_ctx = threading.local()
     devtype2str = {1: 'cpu', 2: 'gpu', 3: 'cpu_pinned', 5: 'cpu_shared'}
@@ -120,6 +134,3 @@ def context_from_torch(dev):
         return Context('gpu', dev.index if dev.index is not None else torch.cuda.current_device())
     return Context('cpu', 0)
 
-
-# reference: the class attribute holding the process default context
-Context.default_ctx = Context('cpu', 0)

@@ -56,7 +56,7 @@ def _resolve_names(hint, prefix, params):
     stack = _scope_stack()
     parent = stack[-1] if stack else None
     if parent is None:
-        full = prefix if prefix is not None else _name.NameManager.current().get(None, hint) + '_'
+        full = prefix if prefix is not None else _name.NameManager.current.get(None, hint) + '_'
         shared = None if params is None else params
         pd = ParameterDict(full) if shared is None else ParameterDict(shared.prefix, shared)
         return full, pd
@@ -94,6 +94,16 @@ class _NameScopeGuard:
         stack = _scope_stack()
         if stack and stack[-1] is self._block:
             stack.pop()
+
+
+class _BlockScope(_NameScopeGuard):
+    """The reference's name for the per-thread block naming scope (gluon/block.py _BlockScope):
+    ``with _BlockScope(block):`` names new blocks / symbols under ``block.prefix`` in this thread;
+    ``_BlockScope.create(prefix, params, hint)`` resolves a new block's (prefix, ParameterDict)."""
+
+    @staticmethod
+    def create(prefix, params, hint):
+        return _resolve_names(hint, prefix, params)
 
 
 # ---------------------------------------------------------------------------------------------

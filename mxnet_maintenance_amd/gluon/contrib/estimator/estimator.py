@@ -40,6 +40,15 @@ def _check_metrics(metrics):
     return metrics
 
 
+def _require_loader(data):
+    """The Estimator consumes Gluon DataLoaders only (reference estimator.py fit / evaluate): a
+    DataIter yields DataBatch objects and a bare NDArray has no (data, label) structure."""
+    from ...data import DataLoader
+    if not isinstance(data, DataLoader):
+        raise ValueError('Estimator only support input as Gluon DataLoader. Alternatively, you can transform '
+                         'your DataIter or any NDArray into Gluon DataLoader. Refer to gluon.data.DataLoader')
+
+
 class _EventBus:
     """Handlers sorted by priority, grouped per event by their hook mix-ins."""
 
@@ -89,6 +98,11 @@ class Estimator:
         if not isinstance(ctxs, list) or any(not isinstance(c, Context) for c in ctxs):
             raise ValueError('context must be a Context or a list of Context, refer to mxnet.Context: {}'
                              .format(context))
+        gpus = [gpu(i) for i in range(num_gpus())]
+        for c in ctxs:
+            if c.device_type != 'cpu' and c not in gpus:
+                raise AssertionError('%s is not available, please make sure your context is in one of: mx.cpu(), %s'
+                                     % (c, ', '.join(str(g) for g in gpus)))
         return ctxs
 
     def _is_initialized(self):
@@ -159,8 +173,21 @@ class Estimator:
         if val_data:
             defaults.append(ValidationHandler(val_data=val_data, eval_fn=self.evaluate))
         defaults.append(LoggingHandler(metrics=self.train_metrics))
+        user = _check_event_handlers(event_handlers)
         handlers = self._with_defaults(event_handlers, defaults)
         handlers.append(StoppingHandler(self.max_epoch, self.max_batch))     # always one of ours
+        if user:
+            # user handlers next to default ones must watch the estimator's own metric objects
+            known = set(id(m) for m in self.train_metrics + self.val_metrics)
+            for h in handlers:
+                for attr in dir(h):
+                    if 'metric' not in attr:
+                        continue
+                    ref = getattr(h, attr, None)
+                    for m in (ref if isinstance(ref, list) else [ref] if ref else []):
+                        if hasattr(m, 'update') and id(m) not in known:
+                            raise ValueError('Event handler %s refers to a metric instance %s outside of the '
+                                             'estimator\'s train_metrics / val_metrics' % (type(h).__name__, m))
         return sorted(handlers, key=lambda h: getattr(h, 'priority', 0))
 
     def _prepare_default_validation_handlers(self, event_handlers):
@@ -176,6 +203,7 @@ class Estimator:
     # ---------------------------------------------------------------- loops
     def evaluate(self, val_data, batch_axis=0, event_handlers=None):
         """One pass over ``val_data`` updating ``val_metrics`` (through the validation handlers)."""
+        _require_loader(val_data)
         for m in self.val_metrics:
             m.reset()
         bus = _EventBus(self._prepare_default_validation_handlers(event_handlers))
@@ -188,8 +216,7 @@ class Estimator:
 
     def fit(self, train_data, val_data=None, epochs=None, event_handlers=None, batches=None, batch_axis=0):
         """Train for ``epochs`` epochs or ``batches`` batches (exactly one of them)."""
-        if not isinstance(train_data, (list, tuple)) and not hasattr(train_data, '__iter__'):
-            raise ValueError('train_data must be iterable')
+        _require_loader(train_data)
         if bool(epochs) == bool(batches):
             raise ValueError('Please specify either epochs or batches.' if not epochs else
                              'Only one of epochs and batches can be specified.')

@@ -253,8 +253,6 @@ class CheckpointHandler(TrainBegin, BatchEnd, EpochEnd):
     ``max_checkpoints``), optionally ``<prefix>-best`` by a monitored metric, and resume from the
     newest checkpoint on request."""
 
-    _NAME = re.compile(r'.*epoch(\d+)batch(\d+)\.params$')
-
     def __init__(self, model_dir, model_prefix='model', monitor=None, verbose=0, save_best=False, mode='auto',
                  epoch_period=1, batch_period=None, max_checkpoints=5, resume_from_checkpoint=False):
         if save_best and not isinstance(monitor, EvalMetric):
@@ -278,25 +276,39 @@ class CheckpointHandler(TrainBegin, BatchEnd, EpochEnd):
 
     def train_begin(self, estimator, *args, **kwargs):
         self.current_epoch = self.current_batch = 0
+        self.trained_epoch = self.trained_batch = -1
         if self.save_best:
             self.best = self._better.worst()
         if self.resume_from_checkpoint:
-            self._restore_latest(estimator)
+            by_batch = bool(estimator.max_batch)
+            if (by_batch and (not self.batch_period or self.epoch_period)) or \
+                    (not by_batch and (not self.epoch_period or self.batch_period)):
+                raise AssertionError('To use resume from checkpoint, you must only specify the same type of period '
+                                     'you used for training (epoch_period for epochs, batch_period for batches).')
+            self._resume(estimator)
 
     def batch_end(self, estimator, *args, **kwargs):
-        if _due(self.batch_period, self.current_batch):
+        if self.current_batch == 0:
+            self._save_symbol(estimator)
+        if self.batch_period and (self.current_batch + 1) % self.batch_period == 0:
             self._checkpoint_now(estimator)
         self.current_batch += 1
 
     def epoch_end(self, estimator, *args, **kwargs):
-        if _due(self.epoch_period, self.current_epoch):
+        if self.epoch_period and (self.current_epoch + 1) % self.epoch_period == 0:
             self._checkpoint_now(estimator)
         self.current_epoch += 1
 
+    def _numbers(self, estimator):
+        """(epoch, batch) the checkpoint is named after: continuing the resumed run's count."""
+        if self.trained_epoch < 0:
+            return self.current_epoch, self.current_batch
+        extra = 0 if estimator.max_epoch else 1
+        return self.current_epoch + self.trained_epoch + 1, self.current_batch + self.trained_batch + extra
+
     def _checkpoint_now(self, estimator):
-        if self.resume_from_checkpoint and self.current_epoch == 0 and self.current_batch == 0:
-            return
-        prefix = '%s-epoch%dbatch%d' % (self.model_prefix, self.current_epoch, self.current_batch)
+        epoch, batch = self._numbers(estimator)
+        prefix = '%s-epoch%dbatch%d' % (self.model_prefix, epoch, batch)
         self._write(estimator, prefix)
         if self.verbose > 0:
             estimator.logger.info('[Epoch %d] CheckpointHandler: trained total %d batches, saving model at %s with '
@@ -313,6 +325,15 @@ class CheckpointHandler(TrainBegin, BatchEnd, EpochEnd):
                                       self.model_dir, best_prefix)
             self.best = value
 
+    def _save_symbol(self, estimator):
+        """``<prefix>-symbol.json`` of a hybridized network (its cached graph), once per fit."""
+        graph = getattr(estimator.net, '_cached_graph', None)
+        if graph:
+            graph[1].save(self._path(self.model_prefix + '-symbol', '.json'))
+        else:
+            estimator.logger.info('Model architecture (symbol file) is not saved: hybridize a HybridBlock model '
+                                  'before passing it to the Estimator to save it as %s-symbol.json', self.model_prefix)
+
     def _write(self, estimator, file_prefix):
         estimator.net.save_parameters(self._path(file_prefix, '.params'))
         estimator.trainer.save_states(self._path(file_prefix, '.states'))
@@ -321,33 +342,49 @@ class CheckpointHandler(TrainBegin, BatchEnd, EpochEnd):
         self.saved_checkpoints.append(file_prefix)
         while len(self.saved_checkpoints) > self.max_checkpoints:
             old = self.saved_checkpoints.pop(0)
-            for ext in ('.params', '.states'):
-                stale = self._path(old, ext)
-                if os.path.exists(stale):
-                    os.unlink(stale)
+            for fname in os.listdir(self.model_dir):
+                if fname.startswith(old):
+                    os.unlink(os.path.join(self.model_dir, fname))
 
-    def _restore_latest(self, estimator):
-        found = []
+    def _latest(self, head, tail):
+        """Largest integer between ``head`` and ``tail`` in the model directory's file names, or -1."""
+        best = -1
+        for fname in os.listdir(self.model_dir):
+            if fname.startswith(head) and tail in fname[len(head):]:
+                num = fname[len(head):].split(tail, 1)[0]
+                if num.isdigit():
+                    best = max(best, int(num))
+        return best
+
+    def _resume(self, estimator):
         head = self.model_prefix + '-epoch'
-        for fname in sorted(os.listdir(self.model_dir)):
-            m = self._NAME.match(fname)
-            if m and fname.startswith(head):
-                found.append(((int(m.group(1)), int(m.group(2))), fname))
-        if not found:
-            estimator.logger.info('CheckpointHandler: No checkpoint found, training from scratch for %d epochs'
-                                  % (estimator.max_epoch or 0))
+        self.trained_epoch = self._latest(head, 'batch')
+        if self.trained_epoch < 0:
+            estimator.logger.info('CheckpointHandler: No checkpoint found, training from scratch for %s'
+                                  % ('%d batches' % estimator.max_batch if estimator.max_batch else
+                                     '%d epochs' % (estimator.max_epoch or 0)))
             return
-        (epoch, batch), latest = max(found)
-        estimator.net.load_parameters(os.path.join(self.model_dir, latest))
-        states = os.path.join(self.model_dir, latest[:-len('.params')] + '.states')
-        if os.path.exists(states):
-            estimator.trainer.load_states(states)
-        self.current_epoch = epoch + 1 if self.epoch_period else epoch
-        self.current_batch = batch
-        for h in getattr(estimator, '_handlers', []):
-            if isinstance(h, StoppingHandler):
-                h.current_epoch, h.current_batch = self.current_epoch, self.current_batch
-        estimator.logger.info('CheckpointHandler: resumed from %s', latest)
+        self.trained_batch = self._latest('%s%d' % (head, self.trained_epoch) + 'batch', '.params')
+        if estimator.max_epoch:
+            if self.trained_epoch >= estimator.max_epoch - 1:
+                raise ValueError('Found checkpoint with maximum number of epoch %d reached, please specify '
+                                 'resume_from_checkpoint=False to train from scratch.' % estimator.max_epoch)
+            estimator.max_epoch -= self.trained_epoch + 1
+        if estimator.max_batch:
+            if self.trained_batch >= estimator.max_batch - 1:
+                raise ValueError('Found checkpoint with maximum number of batch %d reached, please specify '
+                                 'resume_from_checkpoint=False to train from scratch.' % self.trained_batch)
+            estimator.max_batch -= self.trained_batch + 1
+        stem = '%s-epoch%dbatch%d' % (self.model_prefix, self.trained_epoch, self.trained_batch)
+        params, states = self._path(stem, '.params'), self._path(stem, '.states')
+        if not (os.path.exists(params) and os.path.exists(states)):
+            raise AssertionError('Failed to load checkpoint %s (.params / .states missing)' % stem)
+        estimator.net.load_parameters(params, ctx=estimator.context)
+        estimator.trainer.load_states(states)
+        estimator.logger.warning('CheckpointHandler: Checkpoint resumed from epoch %d batch %d, continue to train '
+                                 'for %s', self.trained_epoch, self.trained_batch,
+                                 '%d epochs' % estimator.max_epoch if estimator.max_epoch else
+                                 '%d batches' % estimator.max_batch)
 
 
 class EarlyStoppingHandler(TrainBegin, EpochEnd, TrainEnd):

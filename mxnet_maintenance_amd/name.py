@@ -33,4 +33,4 @@ class Prefix(NameManager):
 
 
 def current():
-    return NameManager.current()
+    return NameManager.current

@@ -589,8 +589,8 @@ def _create(op_name, inputs, attrs, name=None, attr=None):
     # the default node name follows the name the operator was called by (an alias such as flip
     # names its node flip0, as the reference's generated functions do)
     hint = (op_name if op_name.lower().lstrip('_') else op.name).lower()
-    name = NameManager.current().get(name, hint)
-    scope_attr = AttrScope.current().get(attr)
+    name = NameManager.current.get(name, hint)
+    scope_attr = AttrScope.current.get(attr)
     node_attrs = {}
     for k, v in attrs.items():
         if v is None:
@@ -709,7 +709,7 @@ def var(name, attr=None, shape=None, lr_mult=None, wd_mult=None, dtype=None, ini
     """Create a symbolic variable."""
     if not isinstance(name, str):
         raise TypeError('Expect a string for variable `name`')
-    attr = AttrScope.current().get(attr)
+    attr = AttrScope.current.get(attr)
     attrs = {}
     for k, v in (attr or {}).items():
         attrs[k] = v

@@ -39,16 +39,18 @@ _default_ctx = [None]
 
 
 def default_context():
-    """Context used by tests (MXNET_TEST_DEVICE=gpu selects the first GPU)."""
-    if _default_ctx[0] is not None:
-        return _default_ctx[0]
-    if os.environ.get('MXNET_TEST_DEVICE', 'cpu') == 'gpu':
+    """Context used by tests: this thread's default context (MXNET_TEST_DEVICE=gpu selects the first
+    GPU while no context was set)."""
+    from .context import Context
+    if getattr(Context._default_ctx, 'value', None) is None and os.environ.get('MXNET_TEST_DEVICE', 'cpu') == 'gpu':
         return gpu(0)
     return current_context()
 
 
 def set_default_context(ctx):
-    _default_ctx[0] = ctx
+    """Set this thread's default context (``Context.default_ctx``)."""
+    from .context import Context
+    Context.default_ctx = ctx
 
 
 def default_dtype():

@@ -77,14 +77,29 @@ class _NumpyShapeScope:
         set_np_shape(self._prev)
 
 
-class _NumpyArrayScope:
-    def __init__(self, active):
-        self._enter = active
+class _NumpyArrayScopeMeta(type):
+    """``_NumpyArrayScope._current``: the calling thread's NumPy-array mode as a scope object
+    (assigning one switches this thread's mode; reference util.py keeps it in a threading.local)."""
+
+    @property
+    def _current(cls):
+        return cls(_state.STATE.np_array)
+
+    @_current.setter
+    def _current(cls, scope):
+        _state.STATE.np_array = bool(scope._is_np_array)
+
+
+class _NumpyArrayScope(metaclass=_NumpyArrayScopeMeta):
+    """``with np_array(flag):`` -- NumPy-compatible array semantics in this thread."""
+
+    def __init__(self, is_np_array):
+        self._is_np_array = bool(is_np_array)
         self._prev = None
 
     def __enter__(self):
         self._prev = _state.STATE.np_array
-        _state.STATE.np_array = self._enter
+        _state.STATE.np_array = self._is_np_array
         return self
 
     def __exit__(self, *a):

@@ -43,11 +43,15 @@ def test_stem_forward_and_bn_partials(shape, dtype):
     ref = _ref_fwd(x, w, pad)
     assert y.shape == ref.shape
     assert _rel(y, ref) < (5e-3 if dtype == torch.float16 else 2e-2)
+    # the partials come from the fp32 accumulators: compare with the fp32 reference, to within the
+    # accumulated difference of the operands' rounding
     part, nparts = y._mxamd_bn_part
     p = part.view(2, 64, nparts)
-    yf = y.float().reshape(-1, 64)
-    torch.testing.assert_close(p[0].sum(1), yf.sum(0), rtol=1e-3, atol=1e-1)
-    torch.testing.assert_close(p[1].sum(1), (yf * yf).sum(0), rtol=1e-3, atol=1e-1)
+    rf = ref.float().reshape(-1, 64)
+    scale = rf.abs().sum(0) * (2e-3 if dtype == torch.float16 else 1e-2) + 1e-2
+    assert ((p[0].sum(1) - rf.sum(0)).abs() <= scale).all()
+    sq = (rf * rf).sum(0)
+    assert ((p[1].sum(1) - sq).abs() <= sq * (4e-3 if dtype == torch.float16 else 2e-2) + 1e-2).all()
 
 
 @pytest.mark.parametrize('shape', SHAPES)

@@ -129,4 +129,4 @@ def test_resnet_bn_backward_fusion_matches_unfused(deterministic):
     noise = _global_err(runs[1], runs[0])
     err = _global_err(runs[2], runs[0])
     assert noise == 0.0, noise
-    assert err <= 1e-3, err
+    assert err <= 5e-3, err         # fp16 gradients, statistics summed in another order
