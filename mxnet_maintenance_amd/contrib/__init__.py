@@ -10,3 +10,5 @@ from .. import ndarray as _nd
 from .. import symbol as _sym
 ndarray = _nd.contrib
 symbol = _sym.contrib
+nd = ndarray        # reference aliases (mx.contrib.nd / mx.contrib.sym)
+sym = symbol

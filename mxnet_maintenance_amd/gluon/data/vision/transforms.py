@@ -147,7 +147,8 @@ class CropResize(HybridBlock):
 
     def hybrid_forward(self, F, x):
         out = F.image.crop(x, *self._box)
-        return F.image.resize(out, self._size, False, self._interpolation) if self._size else out
+        return F.image.resize(out, size=self._size, keep_ratio=False, interp=self._interpolation) if self._size \
+            else out
 
 
 class Resize(HybridBlock):
@@ -159,16 +160,10 @@ class Resize(HybridBlock):
         self._keep = keep_ratio
         self._interpolation = interpolation
 
-    def _target(self, h, w):
-        if not (isinstance(self._size, int) or len(self._size) == 1):
-            return tuple(self._size)
-        s = self._size if isinstance(self._size, int) else self._size[0]
-        if not self._keep:
-            return (s, s)
-        return (s, int(h * s / w)) if h > w else (int(w * s / h), s)
-
     def hybrid_forward(self, F, x):
-        return F.image.resize(x, self._target(x.shape[-3], x.shape[-2]), False, self._interpolation)
+        # the operator sizes the target from the input (keep_ratio), so this hybridizes
+        size = (self._size,) if isinstance(self._size, int) else tuple(self._size)
+        return F.image.resize(x, size=size, keep_ratio=self._keep, interp=self._interpolation)
 
 
 class Rotate(Block):

@@ -26,7 +26,7 @@ def _deform_columns(x, offset, mask, kernel, stride, pad, dilate, dg):
     base_h = (torch.arange(Ho, device=dev, dtype=dt) * sh - ph).view(1, Ho, 1)
     base_w = (torch.arange(Wo, device=dev, dtype=dt) * sw - pw).view(1, 1, Wo)
     cpg = C // dg
-    off = offset.view(N, dg, K, 2, Ho, Wo)
+    off = offset.reshape(N, dg, K, 2, Ho, Wo)
     cols = []
     for k in range(K):
         i, j = divmod(k, kw)
@@ -34,12 +34,12 @@ def _deform_columns(x, offset, mask, kernel, stride, pad, dilate, dg):
         ws = base_w + j * dw + off[:, :, k, 1]
         gy = 2.0 * hs / max(H - 1, 1) - 1.0
         gx = 2.0 * ws / max(W - 1, 1) - 1.0
-        grid = torch.stack([gx, gy], dim=-1).view(N * dg, Ho, Wo, 2)
-        xs = x.view(N * dg, cpg, H, W)
+        grid = torch.stack([gx, gy], dim=-1).reshape(N * dg, Ho, Wo, 2)
+        xs = x.reshape(N * dg, cpg, H, W)
         s = F.grid_sample(xs, grid, mode='bilinear', padding_mode='zeros', align_corners=True)
-        s = s.view(N, dg, cpg, Ho, Wo)
+        s = s.reshape(N, dg, cpg, Ho, Wo)
         if mask is not None:
-            s = s * mask.view(N, dg, K, Ho, Wo)[:, :, k].unsqueeze(2)
+            s = s * mask.reshape(N, dg, K, Ho, Wo)[:, :, k].unsqueeze(2)
         cols.append(s.reshape(N, C, Ho, Wo))
     return torch.stack(cols, dim=2)                     # [N, C, K, Ho, Wo]
 
@@ -49,8 +49,8 @@ def _deform_conv(x, offset, mask, weight, bias, kernel, stride, pad, dilate, num
     N, C, K, Ho, Wo = cols.shape
     O = weight.shape[0]
     g = num_group
-    cols = cols.view(N, g, C // g, K, Ho, Wo)
-    w = weight.view(g, O // g, C // g, K)
+    cols = cols.reshape(N, g, C // g, K, Ho, Wo)
+    w = weight.reshape(g, O // g, C // g, K)
     out = torch.einsum('ngckhw,gock->ngohw', cols, w).reshape(N, O, Ho, Wo)
     if bias is not None:
         out = out + bias.view(1, -1, 1, 1)

@@ -275,7 +275,7 @@ def box_nms(data, overlap_thresh=0.5, valid_thresh=0.0, topk=-1, coord_start=2, 
     for b in range(x.shape[0]):
         rows = x[b]
         valid = rows[:, score_index] > valid_thresh
-        if id_index >= 0 and background_id >= 0:
+        if id_index >= 0:       # entries of the background class (default id -1) are never kept
             valid &= rows[:, id_index] != background_id
         vidx = torch.nonzero(valid).reshape(-1)
         if vidx.numel() == 0:
@@ -283,12 +283,11 @@ def box_nms(data, overlap_thresh=0.5, valid_thresh=0.0, topk=-1, coord_start=2, 
         order = vidx[torch.argsort(rows[vidx, score_index], descending=True, stable=True)]
         cand = rows[order].clone()
         boxes = _corner(cand[:, coord_start:coord_start + 4], in_format)
-        work = torch.cat([(cand[:, id_index:id_index + 1] if id_index >= 0 else torch.zeros_like(cand[:, :1])),
-                          cand[:, score_index:score_index + 1], boxes], -1)
+        # column 0 = class id shifted to >= 1 (a kept box of class -1 must not read as suppressed)
+        cls = cand[:, id_index:id_index + 1] + 2.0 if id_index >= 0 else torch.zeros_like(cand[:, :1])
+        work = torch.cat([cls, cand[:, score_index:score_index + 1], boxes], -1)
         work = _nms_rows(work, overlap_thresh, force_suppress or id_index < 0, topk)
         keep = work[:, 0] >= 0
-        if id_index < 0:
-            keep = work[:, 0] == 0
         kept = cand[keep]
         if in_format != out_format:
             b4 = kept[:, coord_start:coord_start + 4]

@@ -5,6 +5,8 @@ src/operator/tensor/la_op.cc (_linalg_*); src/operator/image/*.cc (_image_*).
 """
 import math
 
+import numpy as np
+
 import torch
 import torch.nn.functional as F
 
@@ -283,22 +285,56 @@ def image_to_tensor(data):
     return x.permute(0, 3, 1, 2).contiguous()
 
 
+def _image_error(msg):
+    from ..base import MXNetError
+    return MXNetError(msg)
+
+
 @register('_image_normalize', aliases=('image_normalize',), params={'mean': ('floats', (0.0,)), 'std': ('floats', (1.0,))})
 def image_normalize(data, mean=(0.0,), std=(1.0,)):
+    """(x - mean) / std per channel of a CHW image or NCHW batch (src/operator/image/image_random-inl.h:
+    1 or 3 channels; mean / std of length 1 or C)."""
+    if data.dim() not in (3, 4):
+        raise _image_error('Normalize: input must be a 3-D (CHW) or 4-D (NCHW) tensor, got shape %s'
+                           % (tuple(data.shape),))
     c = data.shape[-3]
+    if c not in (1, 3):
+        raise _image_error('Normalize: expected 1 or 3 channels, got %d' % c)
     m = torch.tensor(list(mean) * (c if len(mean) == 1 else 1), dtype=data.dtype, device=data.device)[:c]
     s = torch.tensor(list(std) * (c if len(std) == 1 else 1), dtype=data.dtype, device=data.device)[:c]
     shape = (c, 1, 1)
     return (data - m.reshape(shape)) / s.reshape(shape)
 
 
+def _resize_target(h, w, size, keep_ratio):
+    """(width, height) of a resize (src/operator/image/resize-inl.h): ``size`` is (w, h) or one side;
+    with ``keep_ratio`` a single size is the short side."""
+    size = tuple(int(v) for v in size)
+    if len(size) not in (1, 2) or any(v <= 0 for v in size):
+        raise _image_error('Resize: size must be one or two positive integers, got %s' % (size,))
+    if len(size) == 2:
+        return size
+    s = size[0]
+    if not keep_ratio:
+        return s, s
+    return (s, int(h * s / w)) if h > w else (int(w * s / h), s)
+
+
 @register('_image_resize', aliases=('image_resize',), params={'size': ('shape', ()), 'keep_ratio': ('bool', False),
                                                               'interp': ('int', 1)})
 def image_resize(data, size=(), keep_ratio=False, interp=1):
-    if len(size) == 1:
-        size = (size[0], size[0])
-    w, h = size
+    """Resize HWC images / NHWC batches.  Host tensors go through the same resampler as
+    ``mx.image.imresize`` (bit-identical results); device tensors through bilinear / nearest
+    interpolation on the GPU."""
+    if data.dim() not in (3, 4):
+        raise _image_error('Resize: input must be HWC or NHWC, got shape %s' % (tuple(data.shape),))
+    w, h = _resize_target(data.shape[-3], data.shape[-2], size, keep_ratio)
     hwc = data.dim() == 3
+    if data.device.type == 'cpu' and not data.requires_grad:
+        from ..image.image import _resize_np
+        imgs = [data] if hwc else list(data)
+        outs = [torch.from_numpy(np.ascontiguousarray(_resize_np(i.numpy(), w, h, interp))) for i in imgs]
+        return outs[0] if hwc else torch.stack(outs)
     x = data.permute(2, 0, 1).unsqueeze(0) if hwc else data.permute(0, 3, 1, 2)
     mode = 'nearest' if interp == 0 else 'bilinear'
     y = F.interpolate(x.float(), size=(h, w), mode=mode, align_corners=False if mode == 'bilinear' else None)
@@ -310,6 +346,12 @@ def image_resize(data, size=(), keep_ratio=False, interp=1):
 @register('_image_crop', aliases=('image_crop',), params={'x': ('int', 0), 'y': ('int', 0), 'width': ('int', 1),
                                                           'height': ('int', 1)})
 def image_crop(data, x=0, y=0, width=1, height=1):
+    if data.dim() not in (3, 4):
+        raise _image_error('Crop: input must be HWC or NHWC, got shape %s' % (tuple(data.shape),))
+    H, W = data.shape[-3], data.shape[-2]
+    if width <= 0 or height <= 0 or x < 0 or y < 0 or x + width > W or y + height > H:
+        raise _image_error('Crop: window (x=%d, y=%d, width=%d, height=%d) is outside the %dx%d image'
+                           % (x, y, width, height, W, H))
     if data.dim() == 3:
         return data[y:y + height, x:x + width].contiguous()
     return data[:, y:y + height, x:x + width].contiguous()

@@ -24,11 +24,16 @@ def feature_list():
         'HIP_KERNELS_GFX950': _hip_loaded(),
         'RCCL': torch.distributed.is_available() and torch.distributed.is_nccl_available(),
         'NATIVE_ENGINE': _native_loaded(),
-        'CUDA': False, 'CUDNN': False, 'NCCL': False, 'TENSORRT': False,
-        'CPU_SSE': True, 'CPU_AVX': True, 'OPENMP': True, 'MKLDNN': False,
-        'BLAS_OPEN': True, 'LAPACK': True, 'OPENCV': False, 'DIST_KVSTORE': True,
-        'INT64_TENSOR_SIZE': True, 'SIGNAL_HANDLER': True, 'DEBUG': False,
-        'BF16': True, 'F16C': True,
+        'MIOPEN': torch.version.hip is not None, 'HIPBLASLT': torch.version.hip is not None,
+        'HIP_RTC': torch.version.hip is not None,
+        # the reference's feature names (src/libinfo.cc), answered for this build
+        'CUDA': False, 'CUDNN': False, 'NCCL': False, 'CUDA_RTC': False, 'TENSORRT': False,
+        'CPU_SSE': True, 'CPU_SSE2': True, 'CPU_SSE3': True, 'CPU_SSE4_1': True, 'CPU_SSE4_2': True,
+        'CPU_SSE4A': False, 'CPU_AVX': True, 'CPU_AVX2': True, 'OPENMP': True, 'SSE': True, 'F16C': True,
+        'JEMALLOC': False, 'BLAS_OPEN': True, 'BLAS_ATLAS': False, 'BLAS_MKL': False, 'BLAS_APPLE': False,
+        'LAPACK': True, 'MKLDNN': False, 'OPENCV': False, 'CAFFE': False, 'PROFILER': True, 'DIST_KVSTORE': True,
+        'CXX14': True, 'INT64_TENSOR_SIZE': True, 'SIGNAL_HANDLER': True, 'DEBUG': False, 'TVM_OP': False,
+        'BF16': True,
     }
     return [Feature(k, v) for k, v in feats.items()]
 
