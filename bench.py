@@ -48,7 +48,8 @@ def main():
                     help='linear learning-rate warm-up steps from 0 to 0.1 (default: the --warmup count); '
                          'lr 0.1 from random init on one fixed batch otherwise overshoots before it fits it')
     ap.add_argument('--graph', default='auto', choices=['auto', 'on', 'off'],
-                    help='capture the whole training step in one HIP graph (gluon.GraphStep); auto = on for 1 GPU')
+                    help='capture the whole training step in one HIP graph (gluon.GraphStep); with N>1 the bucketed '
+                         'RCCL all-reduces are captured too; auto = on for 1 GPU, eager for N>1 until measured')
     args = ap.parse_args()
     gpus_given = args.gpus is not None
     if args.gpus is None:

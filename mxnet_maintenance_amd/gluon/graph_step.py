@@ -19,6 +19,14 @@ What changes between replays lives on the device:
   before each replay, to their Philox key;
 * torch's own generator (``nd.random`` ops) is graph-safe by construction.
 
+Data parallel (one process per GPU): the trainer's gradient-bucket hooks fire
+during the captured backward and issue their RCCL all-reduces from the
+capturing stream; ProcessGroupNCCL runs them on its own stream, which joins
+the capture through events, so every replay launches forward, the overlapped
+bucket all-reduces, the tail reduces and the update as one graph.  All ranks
+capture at the same call (warm-up counts are identical), and the eager
+warm-up steps have already created the communicators.
+
 Usage::
 
     def train_step(data, label):

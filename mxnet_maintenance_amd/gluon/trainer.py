@@ -687,7 +687,8 @@ class _ArenaBuckets(GradBuckets):
     def __init__(self, arenas, bucket_bytes=None, tail_bytes=None):
         from ..parallel.buckets import _Bucket
         if bucket_bytes is None:
-            bucket_bytes = int(_env.get('MXAMD_BUCKET_MB') * (1 << 20))
+            from ..parallel.buckets import bucket_bytes_for
+            bucket_bytes = bucket_bytes_for(sum(a.g.numel() * a.g.element_size() for a in arenas))
         if tail_bytes is None:
             tail_bytes = int(_env.get('MXAMD_TAIL_BUCKET_MB') * (1 << 20))
         tail_bytes = max(1, min(tail_bytes, bucket_bytes))

@@ -33,6 +33,21 @@ def _rccl_ok(ts):
         return False
 
 
+def _reduce_coalesced(inputs, destination, buffer_size):
+    """One in-process RCCL reduce per coalesced bucket (indirection point for tests)."""
+    return torch.cuda.comm.reduce_add_coalesced(inputs, destination=destination, buffer_size=buffer_size)
+
+
+def _broadcast_coalesced(tensors, devices, buffer_size):
+    """One in-process RCCL broadcast per coalesced bucket (indirection point for tests)."""
+    return torch.cuda.comm.broadcast_coalesced(tensors, devices, buffer_size=buffer_size)
+
+
+def _rccl_broadcast_ok(src, dsts):
+    devs = [d.device for d in dsts]
+    return len(dsts) > 1 and src.device in devs and _distinct_gpus(dsts)
+
+
 class DeviceComm:
     """Reduce/broadcast helper keyed by kvstore key (root placement is sticky per key)."""
 
@@ -67,7 +82,7 @@ class DeviceComm:
         for (devs, r, _), idx in groups.items():
             # inputs[d] = the tensors of device d for every key of the group
             inputs = [[value_lists[i][d].contiguous() for i in idx] for d in range(len(devs))]
-            sums = torch.cuda.comm.reduce_add_coalesced(inputs, destination=devs[r].index, buffer_size=_BUCKET)
+            sums = _reduce_coalesced(inputs, devs[r].index, _BUCKET)
             for i, s in zip(idx, sums):
                 out[i] = s
         return out
@@ -88,20 +103,19 @@ class DeviceComm:
         when the destinations are on distinct GPUs)."""
         groups = {}
         for i, (s, ds) in enumerate(zip(srcs, dst_lists)):
-            devs = [d.device for d in ds]
-            if (len(ds) > 1 and s.device.type == 'cuda' and all(x.type == 'cuda' for x in devs)
-                    and len(set(devs)) == len(devs) and s.device in devs):
-                groups.setdefault((tuple(devs), s.device, s.dtype), []).append(i)
+            if _rccl_broadcast_ok(s, ds):
+                devs = tuple(d.device for d in ds)
+                groups.setdefault((devs, devs.index(s.device), s.dtype), []).append(i)
                 continue
             for d in ds:
                 if d.data_ptr() != s.data_ptr():
                     d.data.copy_(s)
-        for (devs, sdev, _), idx in groups.items():
-            order = [sdev] + [d for d in devs if d != sdev]
-            outs = torch.cuda.comm.broadcast_coalesced([srcs[i] for i in idx], [d.index for d in order],
-                                                       buffer_size=_BUCKET)
-            for dev, copies in zip(order, outs):
+        for (devs, src_pos, _), idx in groups.items():
+            # positions in the destination list, the source's first (broadcast_coalesced's contract)
+            order = [src_pos] + [p for p in range(len(devs)) if p != src_pos]
+            outs = _broadcast_coalesced([srcs[i] for i in idx], [devs[p].index for p in order], _BUCKET)
+            for p, copies in zip(order, outs):
                 for i, c in zip(idx, copies):
-                    dst = dst_lists[i][devs.index(dev)]
+                    dst = dst_lists[i][p]
                     if dst.data_ptr() != c.data_ptr():
                         dst.data.copy_(c)

@@ -11,9 +11,9 @@ MXNET_KVSTORE_BIGARRAY_BOUND splitting).  On an MI355X node we instead:
   bucket is written during backward, an async RCCL all-reduce of that bucket
   is launched immediately, overlapping communication with the rest of the
   backward pass;
-* size buckets for xGMI's point-to-point ring: big enough that the per-call
-  latency (~tens of us) is amortised, small enough that ≥3 buckets overlap with
-  backward (default 25 MB, ``MXAMD_BUCKET_MB``).
+* size buckets for xGMI's point-to-point ring (``bucket_bytes_for``): big enough that the per-call
+  latency is amortised, small enough that several buckets overlap with backward
+  (``MXAMD_BUCKET_MB`` overrides).
 """
 import os
 
@@ -22,7 +22,32 @@ import torch
 from . import dist
 from ..utils import env as _env
 
-__all__ = ['GradBuckets']
+__all__ = ['GradBuckets', 'bucket_bytes_for']
+
+# Cost model of one bucketed all-reduce on an MI355X node (8 GPUs, each with 7 point-to-point xGMI
+# links; RCCL runs its rings over all of them): t(S) = ALPHA + S / BETA with ALPHA ~ 30 us launch +
+# synchronisation latency and BETA ~ 150 GB/s algorithm bandwidth for large messages.  A bucket of
+# S bytes then uses the links at S / (S + ALPHA * BETA): 78 % at 16 MB, 93 % at 64 MB.  Backward
+# overlap wants several buckets (the last one is exposed), so the size is a quarter of the gradient
+# bytes, clamped to [16, 64] MB: ResNet-50 fp16 (51 MB) -> 16 MB x 3-4, BERT-base bf16 (220 MB) ->
+# 55 MB x 4.  With one rank there is nothing to reduce and bucketing only shapes the arenas.
+_ALPHA_S = 30e-6
+_BETA_BPS = 150e9
+_MIN_BUCKET = 16 << 20
+_MAX_BUCKET = 64 << 20
+
+
+def bucket_bytes_for(total_bytes, world=None):
+    """Bucket size (bytes) for ``total_bytes`` of gradients; ``MXAMD_BUCKET_MB`` overrides."""
+    env = os.environ.get('MXAMD_BUCKET_MB')
+    if env:
+        return int(float(env) * (1 << 20))
+    return int(min(_MAX_BUCKET, max(_MIN_BUCKET, total_bytes // 4)))
+
+
+def link_efficiency(bucket_bytes):
+    """Fraction of the xGMI all-reduce bandwidth a bucket of this size reaches in the model above."""
+    return bucket_bytes / (bucket_bytes + _ALPHA_S * _BETA_BPS)
 
 
 class _Bucket:
@@ -43,7 +68,9 @@ class GradBuckets:
 
     def __init__(self, arrays, grad_reqs, bucket_bytes=None, overlap=True, average=False):
         if bucket_bytes is None:
-            bucket_bytes = int(_env.get('MXAMD_BUCKET_MB') * (1 << 20))
+            total = sum(a._data.numel() * a._data.element_size() for a, r in zip(arrays, grad_reqs)
+                        if r != 'null' and a._grad is not None)
+            bucket_bytes = bucket_bytes_for(total)
         self.overlap = overlap and dist.world_size() > 1
         self.average = average
         self.buckets = []

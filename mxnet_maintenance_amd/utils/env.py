@@ -29,8 +29,9 @@ KNOBS = {
     'MXNET_GLUON_REPO': (str, 'https://apache-mxnet.s3-accelerate.dualstack.amazonaws.com/',
                          'model/dataset repository URL (unused offline)', 'MXNET_GLUON_REPO'),
     'MXNET_TEST_DEVICE': (str, 'cpu', 'test_utils.default_context(): cpu or gpu', ''),
-    'MXAMD_BUCKET_MB': (float, 25.0, 'gradient bucket size for the overlapped RCCL all-reduce (MiB); larger buckets '
-                        'amortise per-collective latency on point-to-point xGMI rings',
+    'MXAMD_BUCKET_MB': (float, 0.0, 'gradient bucket size for the overlapped RCCL all-reduce (MiB); default (0): '
+                        'a quarter of the gradient bytes clamped to [16, 64] MiB (parallel/buckets.py cost model '
+                        'for 7-link xGMI rings)',
                         'MXNET_KVSTORE_BIGARRAY_BOUND'),
     'MXAMD_TAIL_BUCKET_MB': (float, 4.0, 'bucket cap for the gradients of the first layers (the last to be produced '
                              'in backward): their all-reduce cannot overlap compute, so smaller buckets shorten the '

@@ -92,3 +92,83 @@ def test_bucketed_overlap_dp_gpu_hooks_fire():
         assert n_total >= 3 and n_launched == n_total, launched
     for a, b in zip(res[0][3], res[1][3]):
         np.testing.assert_array_equal(a, b)
+
+
+def _graph_worker(port, q):
+    """One RCCL rank whose collective path is forced on (world_size patched to 2): the bucketed
+    all-reduces launched from the backward hooks are captured into the GraphStep's HIP graph."""
+    os.environ.update({'RANK': '0', 'WORLD_SIZE': '1', 'LOCAL_RANK': '0', 'LOCAL_WORLD_SIZE': '1',
+                       'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port), 'MXAMD_DIST_BACKEND': 'nccl',
+                       'MXAMD_BUCKET_MB': '4', 'MXAMD_TAIL_BUCKET_MB': '1'})
+    try:
+        import torch
+        import torch.distributed as tdist
+        import mxnet_maintenance_amd as mx
+        from mxnet_maintenance_amd import gluon, autograd, nd
+        from mxnet_maintenance_amd.parallel import dist
+        dist.init()
+        assert dist.backend() == 'nccl'
+        dist.world_size = lambda: 2          # a 1-rank RCCL sum is the identity: values stay comparable
+        calls = []
+        real = tdist.all_reduce
+
+        def counting(t, *a, **k):
+            calls.append(torch.cuda.is_current_stream_capturing())
+            return real(t, *a, **k)
+        tdist.all_reduce = counting
+        ctx = mx.gpu(0)
+        g = torch.Generator().manual_seed(3)
+        x = nd.array(torch.rand(8, 32, 32, 3, generator=g).numpy(), ctx=ctx).astype('float16')
+        y = nd.array(torch.randint(0, 10, (8,), generator=g).numpy(), ctx=ctx)
+        results = []
+        for graph in (False, True):
+            mx.random.seed(11)
+            net = gluon.model_zoo.vision.get_model('resnet18_v1b', layout='NHWC', fuse=True, classes=10)
+            net.initialize(mx.init.Xavier(), ctx=ctx)
+            net.cast('float16')
+            net.hybridize(static_alloc=True, static_shape=True)
+            tr = gluon.Trainer(net.collect_params(), 'sgd', {'learning_rate': 0.05, 'momentum': 0.9,
+                                                             'multi_precision': True}, kvstore='device')
+            loss_fn = gluon.loss.SoftmaxCrossEntropyLoss()
+
+            def step():
+                with autograd.record():
+                    loss = loss_fn(net(x), y)
+                loss.backward()
+                tr.step(16)
+                return loss
+            fn = gluon.GraphStep(step, tr, warmup=2) if graph else step
+            losses = [float(fn().mean().asscalar()) for _ in range(5)]
+            torch.cuda.synchronize()
+            w = [p.data().asnumpy().astype('float32') for p in net.collect_params().values() if p.grad_req != 'null']
+            results.append((losses, w, len(tr._buckets.buckets), getattr(fn, 'captured', False)))
+        q.put(('OK', results, calls))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put(('ERR', traceback.format_exc(), None))
+    finally:
+        import torch.distributed as d
+        if d.is_initialized():
+            d.destroy_process_group()
+
+
+def test_graph_step_captures_bucketed_rccl_allreduce():
+    """`bench.py --graph on` at N>1: forward + backward + bucketed RCCL all-reduce + fused update in
+    one HIP graph must train exactly like the eager step."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    p = ctx.Process(target=_graph_worker, args=(33000 + os.getpid() % 1000, q))
+    p.start()
+    try:
+        status, results, calls = q.get(timeout=110)
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert status == 'OK', results
+    (le, we, nb, _), (lg, wg, nbg, captured) = results
+    assert captured and nb == nbg and nb >= 3
+    assert sum(calls) == nb, 'every bucket all-reduce must be issued inside the capture: %r' % calls
+    np.testing.assert_allclose(lg, le, rtol=2e-2, atol=2e-2)
+    for a, b in zip(we, wg):
+        np.testing.assert_allclose(b, a, rtol=2e-2, atol=2e-2)

@@ -421,3 +421,29 @@ def test_bench_gpus_flag_launches_ranks():
     assert len(lines) == 1, out.stdout
     rec = json.loads(lines[0])
     assert rec['n_gpus'] == 2 and rec['config']['parallelism'] == 'dp2' and rec['config']['global_batch'] == 4
+
+
+def test_bench_eight_ranks_through_torchrun():
+    """The driver's N=8 launch (`torch.distributed.run --nproc-per-node 8 bench.py --gpus 8`) rehearsed
+    on gloo: every rank joins, gradients are reduced in buckets, and rank 0 prints one dp8 line."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK')}
+    env['OMP_NUM_THREADS'] = '1'
+    out = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '8',
+                          '--master-addr', '127.0.0.1', '--master-port', str(port), 'bench.py', '--gpus', '8',
+                          '--steps', '1', '--warmup', '1', '--batch', '2', '--image-size', '32',
+                          '--dtype', 'float32', '--model', 'resnet18_v1b'],
+                         capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec['n_gpus'] == 8 and rec['config']['parallelism'] == 'dp8' and rec['config']['global_batch'] == 16
+    assert rec['value'] > 0
