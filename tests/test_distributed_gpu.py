@@ -120,14 +120,16 @@ def _graph_worker(port, q):
         g = torch.Generator().manual_seed(3)
         x = nd.array(torch.rand(8, 32, 32, 3, generator=g).numpy(), ctx=ctx).astype('float16')
         y = nd.array(torch.randint(0, 10, (8,), generator=g).numpy(), ctx=ctx)
+        from mxnet_maintenance_amd.ops import kernel_fns as KF
+        KF.set_deterministic(True)       # eager runs repeat bitwise: graph vs eager is then exact-ish
         results = []
-        for graph in (False, True):
+        for graph in (None, False, True):          # None: autotune pass, kernel choices then fixed
             mx.random.seed(11)
             net = gluon.model_zoo.vision.get_model('resnet18_v1b', layout='NHWC', fuse=True, classes=10)
             net.initialize(mx.init.Xavier(), ctx=ctx)
             net.cast('float16')
             net.hybridize(static_alloc=True, static_shape=True)
-            tr = gluon.Trainer(net.collect_params(), 'sgd', {'learning_rate': 0.05, 'momentum': 0.9,
+            tr = gluon.Trainer(net.collect_params(), 'sgd', {'learning_rate': 0.02, 'momentum': 0.9,
                                                              'multi_precision': True}, kvstore='device')
             loss_fn = gluon.loss.SoftmaxCrossEntropyLoss()
 
@@ -138,7 +140,9 @@ def _graph_worker(port, q):
                 tr.step(16)
                 return loss
             fn = gluon.GraphStep(step, tr, warmup=2) if graph else step
-            losses = [float(fn().mean().asscalar()) for _ in range(5)]
+            losses = [float(fn().mean().asscalar()) for _ in range(1 if graph is None else 5)]
+            if graph is None:
+                continue
             torch.cuda.synchronize()
             w = [p.data().asnumpy().astype('float32') for p in net.collect_params().values() if p.grad_req != 'null']
             results.append((losses, w, len(tr._buckets.buckets), getattr(fn, 'captured', False)))
@@ -169,6 +173,6 @@ def test_graph_step_captures_bucketed_rccl_allreduce():
     (le, we, nb, _), (lg, wg, nbg, captured) = results
     assert captured and nb == nbg and nb >= 3
     assert sum(calls) == nb, 'every bucket all-reduce must be issued inside the capture: %r' % calls
-    np.testing.assert_allclose(lg, le, rtol=2e-2, atol=2e-2)
+    np.testing.assert_allclose(lg, le, rtol=1e-3, atol=1e-3)
     for a, b in zip(we, wg):
-        np.testing.assert_allclose(b, a, rtol=2e-2, atol=2e-2)
+        np.testing.assert_allclose(b, a, rtol=1e-3, atol=1e-3)
