@@ -56,6 +56,7 @@ from . import test_utils
 from . import util
 from . import operator
 from . import image
+from . import image as img
 from . import visualization
 from . import visualization as viz
 from . import contrib

@@ -1,17 +1,24 @@
-"""Image decoding, transforms, augmenters and ImageIter (mx.image).
+"""mx.image: decoding, geometric / photometric transforms, augmenter pipelines and ``ImageIter``.
 
-Parity: python/mxnet/image/image.py (imread/imdecode/imresize/resize_short/
-crops/color_normalize/random_size_crop/imrotate, the Augmenter family,
-CreateAugmenter, ImageIter).  The reference decodes with OpenCV in C++;
-here decoding is PIL (libjpeg-turbo, releases the GIL so ImageIter's thread
-pool scales) and images are HWC NDArrays exactly like the reference.
+Behavioural parity with python/mxnet/image/image.py (reference: imdecode :85, imresize :301,
+scale_down :406, copyMakeBorder :437, resize_short :523, fixed_crop :563, random_crop :594,
+center_crop :640... imrotate :618, the Augmenter family :848-1240, CreateAugmenter :1180 and
+ImageIter :1250).  The reference decodes and resizes with OpenCV inside its C++ operator library;
+this module keeps the host-side work in numpy + PIL (libjpeg-turbo, GIL released while decoding)
+and does the batched float work (rotation) with torch so it runs on the GPU when the input lives
+there.  The high-throughput training input path is the native ``io.ImageRecordIter`` (C++ decode
+pool + pinned ring, io/image_record.py); ``ImageIter`` is the flexible Python iterator.
+
+Layout conventions follow the reference: single images are HWC (uint8 after decoding, float32
+after ``CastAug``); ``imrotate`` works on CHW / NCHW float32.
 """
-import io as _io
+import io as _bytesio
 import json
 import logging
 import math
 import os
-import random as _pyrandom
+import random as _rand
+from numbers import Number
 
 import numpy as np
 
@@ -28,451 +35,511 @@ __all__ = ['imread', 'imdecode', 'imdecode_np', 'imresize', 'scale_down', 'copyM
            'SaturationJitterAug', 'HueJitterAug', 'ColorJitterAug', 'LightingAug', 'ColorNormalizeAug',
            'RandomGrayAug', 'HorizontalFlipAug', 'CastAug', 'CreateAugmenter', 'ImageIter']
 
-_GRAY = np.array([0.299, 0.587, 0.114], dtype=np.float32)
+# ITU-R 601 luma weights (RGB order), used by the contrast / saturation jitters
+_LUMA = np.array([0.299, 0.587, 0.114], dtype=np.float32)
+# ImageNet statistics used by CreateAugmenter(mean=True / std=True / pca_noise>0)
+_IMAGENET_MEAN = (123.68, 116.28, 103.53)
+_IMAGENET_STD = (58.395, 57.12, 57.375)
+_PCA_EIGVAL = np.array([55.46, 4.794, 1.148])
+_PCA_EIGVEC = np.array([[-0.5675, 0.7192, 0.4009],
+                        [-0.5808, -0.0045, -0.8140],
+                        [-0.5836, -0.6948, 0.4203]])
 
 
-def _np(src):
-    return src.asnumpy() if isinstance(src, NDArray) else np.asarray(src)
+# --------------------------------------------------------------------------- array plumbing
+def _host(img):
+    """numpy view of an image argument (NDArray or array-like)."""
+    return img.asnumpy() if isinstance(img, NDArray) else np.asarray(img)
 
 
-def _wrap(a, like):
-    return nd.array(a, dtype=a.dtype) if isinstance(like, NDArray) or like is None else a
+def _like(arr, ref):
+    """Return ``arr`` in the container type of ``ref`` (NDArray unless ``ref`` is a numpy array)."""
+    if isinstance(ref, np.ndarray):
+        return arr
+    return nd.array(arr, dtype=arr.dtype)
+
+
+def _emit(result, out):
+    """Honour the reference's optional ``out=`` argument."""
+    if out is None:
+        return result
+    out[:] = result
+    return out
+
+
+# --------------------------------------------------------------------------- decode
+def _as_bytes(buf):
+    if isinstance(buf, NDArray):
+        return buf.asnumpy().astype(np.uint8).tobytes()
+    if isinstance(buf, np.ndarray):
+        return buf.tobytes()
+    return bytes(buf)
 
 
 def imdecode_np(buf, flag=1, to_rgb=True):
-    """Decode an encoded image (bytes) to a HWC uint8 numpy array (RGB, or BGR with to_rgb=False)."""
+    """Decode encoded image bytes to a contiguous HWC uint8 numpy array.
+
+    ``flag`` 1 = 3-channel colour, 0 = one grey channel; ``to_rgb=False`` gives OpenCV's BGR order.
+    """
     from PIL import Image
-    if isinstance(buf, NDArray):
-        buf = buf.asnumpy().astype(np.uint8).tobytes()
-    elif isinstance(buf, np.ndarray):
-        buf = buf.tobytes()
+    data = _as_bytes(buf)
+    if not data:
+        raise MXNetError('Decoding failed: empty image buffer')
     try:
-        im = Image.open(_io.BytesIO(buf))
-        im = im.convert('RGB' if flag else 'L')
-    except Exception as e:
-        raise MXNetError('Decoding failed. Invalid image file: %s' % e)
-    a = np.asarray(im)
-    if not flag:
-        return a[:, :, None]
-    if not to_rgb:
-        a = a[:, :, ::-1]
-    return np.ascontiguousarray(a)
+        with Image.open(_bytesio.BytesIO(data)) as im:
+            pixels = np.asarray(im.convert('RGB' if flag else 'L'))
+    except Exception as err:       # PIL raises several unrelated exception types
+        raise MXNetError('Decoding failed. Invalid image file: %s' % err)
+    if pixels.ndim == 2:
+        return np.ascontiguousarray(pixels[:, :, None])
+    return np.ascontiguousarray(pixels if to_rgb else pixels[:, :, ::-1])
 
 
 def imdecode(buf, flag=1, to_rgb=1, out=None):
-    """Decode an image to an NDArray (HWC, uint8)."""
-    a = imdecode_np(buf, flag, bool(to_rgb))
-    r = nd.array(a, dtype='uint8')
-    if out is not None:
-        out[:] = r
-        return out
-    return r
+    """Decode an image buffer into an HWC uint8 NDArray (RGB unless ``to_rgb`` is false)."""
+    return _emit(nd.array(imdecode_np(buf, flag, bool(to_rgb)), dtype='uint8'), out)
 
 
 def imread(filename, flag=1, to_rgb=True, out=None):
-    with open(filename, 'rb') as f:
-        return imdecode(f.read(), flag, to_rgb, out)
+    """Read and decode an image file (HWC uint8 NDArray)."""
+    try:
+        with open(filename, 'rb') as fh:
+            payload = fh.read()
+    except OSError as err:
+        raise MXNetError('imread: cannot open %s (%s)' % (filename, err))
+    return imdecode(payload, flag, to_rgb, out)
 
 
-_PIL_INTERP = None
-
-
-def _interp(interp, sizes=()):
-    from PIL import Image
-    table = {0: Image.NEAREST, 1: Image.BILINEAR, 2: Image.BICUBIC, 3: Image.BOX, 4: Image.LANCZOS}
-    if interp == 9:
-        if sizes:
-            oh, ow, nh, nw = sizes
-            if nh > oh and nw > ow:
-                return Image.BICUBIC
-            if nh < oh and nw < ow:
-                return Image.BOX
-        return Image.BILINEAR
-    if interp == 10:
-        return table[_pyrandom.randint(0, 4)]
-    return table.get(interp, Image.BILINEAR)
+# --------------------------------------------------------------------------- resize
+# OpenCV interpolation codes accepted by the reference (src/io/image_io.cc): 0 nearest, 1 bilinear,
+# 2 bicubic, 3 area, 4 lanczos, 9 = pick by direction (cubic up / area down / linear), 10 = random.
+_CONCRETE_INTERP = (0, 1, 2, 3, 4)
 
 
 def _get_interp_method(interp, sizes=()):
-    if interp == 9 and sizes:
-        oh, ow, nh, nw = sizes
-        if nh > oh and nw > ow:
-            return 2
-        if nh < oh and nw < ow:
-            return 3
-        return 1
+    """Resolve the meta codes 9 / 10 into one of 0..4 for a resize ``sizes=(oh, ow, nh, nw)``."""
     if interp == 10:
-        return _pyrandom.randint(0, 4)
-    if interp not in (0, 1, 2, 3, 4):
+        return _rand.randint(0, 4)
+    if interp == 9:
+        if not sizes:
+            return 1
+        old_h, old_w, new_h, new_w = sizes
+        grow = new_h > old_h and new_w > old_w
+        shrink = new_h < old_h and new_w < old_w
+        return 2 if grow else (3 if shrink else 1)
+    if interp not in _CONCRETE_INTERP:
         raise ValueError('Unknown interp method %d' % interp)
     return interp
 
 
-def _resize_np(a, w, h, interp=1):
+def _pil_filter(code):
     from PIL import Image
-    mode = _interp(interp, (a.shape[0], a.shape[1], h, w))
-    if a.dtype == np.uint8:
-        if a.shape[2] == 1:
-            return np.asarray(Image.fromarray(a[:, :, 0]).resize((w, h), mode))[:, :, None]
-        return np.asarray(Image.fromarray(a).resize((w, h), mode))
-    chans = [np.asarray(Image.fromarray(a[:, :, c].astype(np.float32), mode='F').resize((w, h), mode))
-             for c in range(a.shape[2])]
-    return np.stack(chans, axis=2).astype(a.dtype)
+    return (Image.NEAREST, Image.BILINEAR, Image.BICUBIC, Image.BOX, Image.LANCZOS)[code]
+
+
+def _resize_np(pixels, w, h, interp=1):
+    """Resize an HWC numpy image to (h, w); uint8 keeps PIL's fast path, floats go per channel."""
+    from PIL import Image
+    code = _get_interp_method(interp, (pixels.shape[0], pixels.shape[1], h, w))
+    flt = _pil_filter(code)
+    if pixels.dtype == np.uint8:
+        if pixels.shape[2] == 1:
+            return np.asarray(Image.fromarray(pixels[:, :, 0]).resize((w, h), flt))[:, :, None]
+        return np.asarray(Image.fromarray(pixels).resize((w, h), flt))
+    planes = []
+    for ch in range(pixels.shape[2]):
+        plane = Image.fromarray(np.ascontiguousarray(pixels[:, :, ch], dtype=np.float32), mode='F')
+        planes.append(np.asarray(plane.resize((w, h), flt)))
+    return np.stack(planes, axis=2).astype(pixels.dtype)
 
 
 def imresize(src, w, h, interp=1, out=None):
-    # OpenCV interpolation codes (src/io/image_io.cc: 0 nearest .. 4 lanczos, 9 auto, 10 random)
-    if int(interp) not in (0, 1, 2, 3, 4, 9, 10):
-        from ..base import MXNetError
+    """Resize ``src`` (HWC) to exactly ``w`` x ``h``."""
+    if int(interp) not in _CONCRETE_INTERP + (9, 10):
         raise MXNetError('imresize: invalid interpolation method %r (OpenCV error: Bad flag)' % (interp,))
-    r = _wrap(_resize_np(_np(src), int(w), int(h), interp), src)
-    if out is not None:
-        out[:] = r
-        return out
-    return r
+    return _emit(_like(_resize_np(_host(src), int(w), int(h), interp), src), out)
 
 
 def scale_down(src_size, size):
-    w, h = size
-    sw, sh = src_size
-    if sh < h:
-        w, h = float(w * sh) / h, sh
-    if sw < w:
-        w, h = sw, float(h * sw) / w
-    return int(w), int(h)
+    """Shrink the crop ``size=(w, h)`` until it fits inside ``src_size=(w, h)``, keeping its aspect."""
+    crop_w, crop_h = size
+    img_w, img_h = src_size
+    if img_h < crop_h:
+        crop_w, crop_h = float(crop_w * img_h) / crop_h, img_h
+    if img_w < crop_w:
+        crop_w, crop_h = img_w, float(crop_h * img_w) / crop_w
+    return int(crop_w), int(crop_h)
+
+
+# cv2.BORDER_* -> numpy.pad mode (0 = constant is handled separately)
+_BORDER_MODES = {1: 'edge', 2: 'symmetric', 3: 'wrap', 4: 'reflect'}
 
 
 def copyMakeBorder(src, top, bot, left, right, type=0, value=0, values=None, out=None):  # noqa: A002
-    """Pad an image; type 0 = constant, 1 = replicate, 2 = reflect (cv2 BORDER_* codes)."""
-    a = _np(src)
-    pad = ((top, bot), (left, right), (0, 0))
+    """Pad an HWC image; ``type`` is an OpenCV border code (0 constant, 1 replicate, 2 reflect,
+    3 wrap, 4 reflect-101)."""
+    pixels = _host(src)
+    spatial = ((top, bot), (left, right))
     if type == 0:
-        cval = values if values is not None else value
-        if np.ndim(cval):
-            r = np.stack([np.pad(a[:, :, c], pad[:2], constant_values=cval[c]) for c in range(a.shape[2])], 2)
+        fill = value if values is None else values
+        if np.ndim(fill):
+            padded = np.stack([np.pad(pixels[:, :, c], spatial, constant_values=fill[c])
+                               for c in range(pixels.shape[2])], axis=2)
         else:
-            r = np.pad(a, pad, constant_values=cval)
+            padded = np.pad(pixels, spatial + ((0, 0),), constant_values=fill)
     else:
-        r = np.pad(a, pad, mode={1: 'edge', 2: 'symmetric', 4: 'reflect'}.get(type, 'edge'))
-    r = _wrap(r, src)
-    if out is not None:
-        out[:] = r
-        return out
-    return r
+        if type not in _BORDER_MODES:
+            raise MXNetError('copyMakeBorder: unsupported border type %r' % (type,))
+        padded = np.pad(pixels, spatial + ((0, 0),), mode=_BORDER_MODES[type])
+    return _emit(_like(padded, src), out)
 
 
 def resize_short(src, size, interp=2):
-    h, w = src.shape[0], src.shape[1]
-    if h > w:
-        new_h, new_w = size * h // w, size
+    """Resize so the shorter edge becomes ``size`` (the longer keeps the aspect ratio)."""
+    old_h, old_w = src.shape[0], src.shape[1]
+    if old_h > old_w:
+        new_w, new_h = size, size * old_h // old_w
     else:
-        new_h, new_w = size, size * w // h
-    return imresize(src, new_w, new_h, interp=_get_interp_method(interp, (h, w, new_h, new_w)))
+        new_w, new_h = size * old_w // old_h, size
+    code = _get_interp_method(interp, (old_h, old_w, new_h, new_w))
+    return imresize(src, new_w, new_h, interp=code)
 
 
+# --------------------------------------------------------------------------- crops
 def fixed_crop(src, x0, y0, w, h, size=None, interp=2):
-    out = src[y0:y0 + h, x0:x0 + w]
-    if size is not None and (w, h) != tuple(size):
-        sizes = (h, w, size[1], size[0])
-        out = imresize(out, *size, interp=_get_interp_method(interp, sizes))
-    return out
+    """Crop the (x0, y0, w, h) window, then resize it to ``size=(w, h)`` when given."""
+    window = src[y0:y0 + h, x0:x0 + w]
+    if size is None or (w, h) == tuple(size):
+        return window
+    code = _get_interp_method(interp, (h, w, size[1], size[0]))
+    return imresize(window, size[0], size[1], interp=code)
+
+
+def _crop_at(src, box, size, interp):
+    x0, y0, cw, ch = box
+    return fixed_crop(src, x0, y0, cw, ch, size, interp), box
 
 
 def random_crop(src, size, interp=2):
-    h, w = src.shape[0], src.shape[1]
-    new_w, new_h = scale_down((w, h), size)
-    x0 = _pyrandom.randint(0, w - new_w)
-    y0 = _pyrandom.randint(0, h - new_h)
-    out = fixed_crop(src, x0, y0, new_w, new_h, size, interp)
-    return out, (x0, y0, new_w, new_h)
+    """Random window of ``size`` (shrunk to fit); returns ``(image, (x0, y0, w, h))``."""
+    img_h, img_w = src.shape[0], src.shape[1]
+    cw, ch = scale_down((img_w, img_h), size)
+    box = (_rand.randint(0, img_w - cw), _rand.randint(0, img_h - ch), cw, ch)
+    return _crop_at(src, box, size, interp)
 
 
 def center_crop(src, size, interp=2):
-    h, w = src.shape[0], src.shape[1]
-    new_w, new_h = scale_down((w, h), size)
-    x0 = int((w - new_w) / 2)
-    y0 = int((h - new_h) / 2)
-    out = fixed_crop(src, x0, y0, new_w, new_h, size, interp)
-    return out, (x0, y0, new_w, new_h)
-
-
-def color_normalize(src, mean, std=None):
-    if mean is not None:
-        src = src - mean
-    if std is not None:
-        src = src / std
-    return src
+    """Central window of ``size`` (shrunk to fit); returns ``(image, (x0, y0, w, h))``."""
+    img_h, img_w = src.shape[0], src.shape[1]
+    cw, ch = scale_down((img_w, img_h), size)
+    box = (int((img_w - cw) / 2), int((img_h - ch) / 2), cw, ch)
+    return _crop_at(src, box, size, interp)
 
 
 def random_size_crop(src, size, area, ratio, interp=2, **kwargs):
-    h, w = src.shape[0], src.shape[1]
-    src_area = h * w
-    if 'min_area' in kwargs:
-        area = kwargs.pop('min_area')
-    if isinstance(area, (int, float)):
-        area = (area, 1.0)
+    """Inception-style crop: random area fraction in ``area`` and log-uniform aspect in ``ratio``
+    (10 tries, then a centre crop).  ``min_area=`` is the deprecated spelling of ``area``."""
+    img_h, img_w = src.shape[0], src.shape[1]
+    area = kwargs.pop('min_area', area)
+    lo_area, hi_area = (area, 1.0) if isinstance(area, Number) else area
+    log_lo, log_hi = math.log(ratio[0]), math.log(ratio[1])
     for _ in range(10):
-        target_area = _pyrandom.uniform(area[0], area[1]) * src_area
-        log_ratio = (np.log(ratio[0]), np.log(ratio[1]))
-        new_ratio = np.exp(_pyrandom.uniform(*log_ratio))
-        new_w = int(round(np.sqrt(target_area * new_ratio)))
-        new_h = int(round(np.sqrt(target_area / new_ratio)))
-        if new_w <= w and new_h <= h:
-            x0 = _pyrandom.randint(0, w - new_w)
-            y0 = _pyrandom.randint(0, h - new_h)
-            out = fixed_crop(src, x0, y0, new_w, new_h, size, interp)
-            return out, (x0, y0, new_w, new_h)
+        target = _rand.uniform(lo_area, hi_area) * img_h * img_w
+        aspect = math.exp(_rand.uniform(log_lo, log_hi))
+        cw = int(round(math.sqrt(target * aspect)))
+        ch = int(round(math.sqrt(target / aspect)))
+        if cw <= img_w and ch <= img_h:
+            box = (_rand.randint(0, img_w - cw), _rand.randint(0, img_h - ch), cw, ch)
+            return _crop_at(src, box, size, interp)
     return center_crop(src, size, interp)
 
 
+def color_normalize(src, mean, std=None):
+    """``(src - mean) / std`` with either term optional."""
+    shifted = src if mean is None else src - mean
+    return shifted if std is None else shifted / std
+
+
+# --------------------------------------------------------------------------- rotation
 def imrotate(src, rotation_degrees, zoom_in=False, zoom_out=False):
-    """Rotate CHW (or NCHW) float images by the given degrees (bilinear, zero fill)."""
+    """Rotate CHW / NCHW float32 image(s) about their centre (bilinear, zero outside).
+
+    ``rotation_degrees`` is a scalar or (for a batch) one angle per image.  ``zoom_in`` scales so
+    no padding is visible, ``zoom_out`` so the whole rotated image fits.
+    """
     import torch
     import torch.nn.functional as F
     if zoom_in and zoom_out:
         raise ValueError('`zoom_in` and `zoom_out` cannot be both True')
-    x = src._data if isinstance(src, NDArray) else torch.as_tensor(src)
-    if x.dtype not in (torch.float32, torch.float64, torch.float16):
-        raise TypeError('Only floating point types are supported')
-    squeeze = x.dim() == 3
-    if squeeze:
-        x = x.unsqueeze(0)
-    n, _, h, w = x.shape
-    deg = rotation_degrees._data if isinstance(rotation_degrees, NDArray) else torch.as_tensor(rotation_degrees)
-    deg = deg.to(x.dtype).reshape(-1).expand(n) if deg.numel() == 1 else deg.to(x.dtype).reshape(-1)
-    rad = deg * math.pi / 180
-    c, s = torch.cos(rad), torch.sin(rad)
-    scale = torch.ones_like(c)
+    if src.dtype != np.float32:
+        raise TypeError('Only `float32` images are supported by this function')
+    single = src.ndim == 3
+    if single and not isinstance(rotation_degrees, Number):
+        raise TypeError('When a single image is passed the rotation angle is required to be a scalar.')
+    if src.ndim not in (3, 4):
+        raise ValueError('Only 3D and 4D are supported by this function')
+    imgs = src._data if isinstance(src, NDArray) else torch.as_tensor(src)
+    if single:
+        imgs = imgs.unsqueeze(0)
+    n, _, h, w = imgs.shape
+    if isinstance(rotation_degrees, Number):
+        theta = torch.full((n,), float(rotation_degrees), dtype=torch.float32, device=imgs.device)
+    else:
+        raw = rotation_degrees._data if isinstance(rotation_degrees, NDArray) else torch.as_tensor(rotation_degrees)
+        theta = raw.reshape(-1).to(device=imgs.device, dtype=torch.float32)
+        if theta.numel() != n:
+            raise ValueError('The number of images must be equal to the number of rotation angles')
+    theta = theta * (math.pi / 180.0)
+    cos_t, sin_t = torch.cos(theta).view(n, 1, 1), torch.sin(theta).view(n, 1, 1)
+    # pixel-centred sampling grid, rotated in pixel units, then normalised (align_corners=True)
+    cy, cx = (h - 1) / 2.0, (w - 1) / 2.0
+    ys = (torch.arange(h, dtype=torch.float32, device=imgs.device) - cy).view(1, h, 1)
+    xs = (torch.arange(w, dtype=torch.float32, device=imgs.device) - cx).view(1, 1, w)
+    gx = (xs * cos_t - ys * sin_t) / cx
+    gy = (xs * sin_t + ys * cos_t) / cy
     if zoom_in or zoom_out:
-        ar = w / h
-        hw = (torch.abs(c) * w + torch.abs(s) * h) / w
-        hh = (torch.abs(s) * w + torch.abs(c) * h) / h
-        big = torch.maximum(hw, hh)
-        scale = 1 / big if zoom_in else big
-        del ar
-    theta = torch.zeros(n, 2, 3, dtype=x.dtype)
-    theta[:, 0, 0] = c * scale
-    theta[:, 0, 1] = -s * scale * h / w
-    theta[:, 1, 0] = s * scale * w / h
-    theta[:, 1, 1] = c * scale
-    grid = F.affine_grid(theta.to(x.device), list(x.shape), align_corners=False)
-    y = F.grid_sample(x, grid, align_corners=False)
-    if squeeze:
-        y = y[0]
-    return NDArray(y)
+        ac, as_ = cos_t.abs(), sin_t.abs()
+        fit = torch.maximum((ac * w + as_ * h) / w, (as_ * w + ac * h) / h)   # bounding box / image
+        scale = fit if zoom_out else 1.0 / fit
+        gx, gy = gx * scale, gy * scale
+    grid = torch.stack([gx, gy], dim=-1)
+    rotated = F.grid_sample(imgs, grid, mode='bilinear', padding_mode='zeros', align_corners=True)
+    return NDArray(rotated[0] if single else rotated)
 
 
 def random_rotate(src, angle_limits, zoom_in=False, zoom_out=False):
-    n = src.shape[0] if src.ndim == 4 else 1
-    ang = np.random.uniform(angle_limits[0], angle_limits[1], size=n)
-    return imrotate(src, nd.array(ang), zoom_in, zoom_out)
+    """``imrotate`` by angle(s) drawn uniformly from ``angle_limits`` (one per image of a batch)."""
+    if src.ndim == 3:
+        return imrotate(src, float(np.random.uniform(*angle_limits)), zoom_in, zoom_out)
+    angles = np.random.uniform(angle_limits[0], angle_limits[1], size=src.shape[0]).astype(np.float32)
+    return imrotate(src, nd.array(angles), zoom_in, zoom_out)
 
 
+# --------------------------------------------------------------------------- augmenters
 class Augmenter:
-    """Image augmenter base class (callable on HWC NDArrays)."""
+    """Callable image transform.  Constructor keyword arguments are recorded (JSON-safe) for
+    ``dumps`` and exposed as attributes, so subclasses only declare their parameters."""
 
     def __init__(self, **kwargs):
-        self._kwargs = kwargs
-        for k, v in self._kwargs.items():
-            if isinstance(v, NDArray):
-                v = v.asnumpy()
-            if isinstance(v, np.ndarray):
-                self._kwargs[k] = v.tolist()
+        self._kwargs = {}
+        for key, val in kwargs.items():
+            if isinstance(val, NDArray):
+                val = val.asnumpy()
+            self._kwargs[key] = val.tolist() if isinstance(val, np.ndarray) else val
+            self.__dict__.setdefault(key, val)
 
     def dumps(self):
-        return json.dumps([self.__class__.__name__.lower(), self._kwargs])
+        """``[name, params]`` JSON description of this augmenter."""
+        return json.dumps([type(self).__name__.lower(), self._kwargs])
 
     def __call__(self, src):
-        raise NotImplementedError
+        raise NotImplementedError('Must override implementation.')
 
 
-class SequentialAug(Augmenter):
+class _Composite(Augmenter):
+    """Augmenter holding child augmenters (dumps them recursively)."""
+
     def __init__(self, ts):
         super().__init__()
-        self.ts = ts
+        self.ts = list(ts)
 
     def dumps(self):
-        return [self.__class__.__name__.lower(), [x.dumps() for x in self.ts]]
+        return [type(self).__name__.lower(), [child.dumps() for child in self.ts]]
 
-    def __call__(self, src):
-        for aug in self.ts:
-            src = aug(src)
+    def _run(self, src, order):
+        for child in order:
+            src = child(src)
         return src
 
 
+class SequentialAug(_Composite):
+    """Apply the children in order."""
+
+    def __call__(self, src):
+        return self._run(src, self.ts)
+
+
+class RandomOrderAug(_Composite):
+    """Apply the children in a freshly shuffled order."""
+
+    def __call__(self, src):
+        order = list(self.ts)
+        _rand.shuffle(order)
+        return self._run(src, order)
+
+
 class ResizeAug(Augmenter):
+    """Shorter edge to ``size``."""
+
     def __init__(self, size, interp=2):
         super().__init__(size=size, interp=interp)
-        self.size, self.interp = size, interp
 
     def __call__(self, src):
         return resize_short(src, self.size, self.interp)
 
 
 class ForceResizeAug(Augmenter):
+    """Resize to exactly ``size=(w, h)``, ignoring the aspect ratio."""
+
     def __init__(self, size, interp=2):
         super().__init__(size=size, interp=interp)
-        self.size, self.interp = size, interp
 
     def __call__(self, src):
-        sizes = (src.shape[0], src.shape[1], self.size[1], self.size[0])
-        return imresize(src, *self.size, interp=_get_interp_method(self.interp, sizes))
+        code = _get_interp_method(self.interp, (src.shape[0], src.shape[1], self.size[1], self.size[0]))
+        return imresize(src, self.size[0], self.size[1], interp=code)
 
 
 class RandomCropAug(Augmenter):
+    """``random_crop`` to ``size``."""
+
     def __init__(self, size, interp=2):
         super().__init__(size=size, interp=interp)
-        self.size, self.interp = size, interp
 
     def __call__(self, src):
         return random_crop(src, self.size, self.interp)[0]
 
 
 class RandomSizedCropAug(Augmenter):
+    """``random_size_crop`` to ``size``."""
+
     def __init__(self, size, area, ratio, interp=2, **kwargs):
+        area = kwargs.pop('min_area', area)
         super().__init__(size=size, area=area, ratio=ratio, interp=interp)
-        self.size, self.interp, self.ratio = size, interp, ratio
-        self.area = kwargs.pop('min_area') if 'min_area' in kwargs else area
 
     def __call__(self, src):
         return random_size_crop(src, self.size, self.area, self.ratio, self.interp)[0]
 
 
 class CenterCropAug(Augmenter):
+    """``center_crop`` to ``size``."""
+
     def __init__(self, size, interp=2):
         super().__init__(size=size, interp=interp)
-        self.size, self.interp = size, interp
 
     def __call__(self, src):
         return center_crop(src, self.size, self.interp)[0]
 
 
-class RandomOrderAug(Augmenter):
-    def __init__(self, ts):
-        super().__init__()
-        self.ts = ts
-
-    def dumps(self):
-        return [self.__class__.__name__.lower(), [x.dumps() for x in self.ts]]
-
-    def __call__(self, src):
-        order = list(self.ts)
-        _pyrandom.shuffle(order)
-        for t in order:
-            src = t(src)
-        return src
+def _blend(src, alpha, base):
+    """``alpha * src + base`` in float32, keeping the container type of ``src``."""
+    return _like((_host(src).astype(np.float32) * alpha + base).astype(np.float32), src)
 
 
 class BrightnessJitterAug(Augmenter):
+    """Scale intensities by ``1 + U(-brightness, brightness)``."""
+
     def __init__(self, brightness):
         super().__init__(brightness=brightness)
-        self.brightness = brightness
 
     def __call__(self, src):
-        alpha = 1.0 + _pyrandom.uniform(-self.brightness, self.brightness)
-        return src * alpha
+        return src * (1.0 + _rand.uniform(-self.brightness, self.brightness))
 
 
 class ContrastJitterAug(Augmenter):
+    """Blend with the image's mean luma by ``1 + U(-contrast, contrast)``."""
+
     def __init__(self, contrast):
         super().__init__(contrast=contrast)
-        self.contrast = contrast
 
     def __call__(self, src):
-        alpha = 1.0 + _pyrandom.uniform(-self.contrast, self.contrast)
-        a = _np(src).astype(np.float32)
-        gray = (a * _GRAY).sum(axis=2)
-        gray = (3.0 * (1.0 - alpha) / gray.size) * gray.sum()
-        return _wrap((a * alpha + gray).astype(np.float32), src)
+        alpha = 1.0 + _rand.uniform(-self.contrast, self.contrast)
+        luma = (_host(src).astype(np.float32) @ _LUMA).mean()
+        return _blend(src, alpha, 3.0 * (1.0 - alpha) * luma)
 
 
 class SaturationJitterAug(Augmenter):
+    """Blend with the per-pixel luma by ``1 + U(-saturation, saturation)``."""
+
     def __init__(self, saturation):
         super().__init__(saturation=saturation)
-        self.saturation = saturation
 
     def __call__(self, src):
-        alpha = 1.0 + _pyrandom.uniform(-self.saturation, self.saturation)
-        a = _np(src).astype(np.float32)
-        gray = (a * _GRAY).sum(axis=2, keepdims=True) * (1.0 - alpha)
-        return _wrap((a * alpha + gray).astype(np.float32), src)
+        alpha = 1.0 + _rand.uniform(-self.saturation, self.saturation)
+        luma = (_host(src).astype(np.float32) @ _LUMA)[:, :, None]
+        return _blend(src, alpha, (1.0 - alpha) * luma)
+
+
+# RGB <-> YIQ; a hue shift is a rotation of the (I, Q) chroma plane
+_RGB2YIQ = np.array([[0.299, 0.587, 0.114], [0.596, -0.274, -0.321], [0.211, -0.523, 0.311]])
+_YIQ2RGB = np.array([[1.0, 0.956, 0.621], [1.0, -0.272, -0.647], [1.0, -1.107, 1.705]])
 
 
 class HueJitterAug(Augmenter):
+    """Rotate the chroma plane by ``U(-hue, hue) * pi``."""
+
     def __init__(self, hue):
         super().__init__(hue=hue)
-        self.hue = hue
-        self.tyiq = np.array([[0.299, 0.587, 0.114], [0.596, -0.274, -0.321], [0.211, -0.523, 0.311]])
-        self.ityiq = np.array([[1.0, 0.956, 0.621], [1.0, -0.272, -0.647], [1.0, -1.107, 1.705]])
 
     def __call__(self, src):
-        alpha = _pyrandom.uniform(-self.hue, self.hue)
-        u, w = np.cos(alpha * np.pi), np.sin(alpha * np.pi)
-        bt = np.array([[1.0, 0.0, 0.0], [0.0, u, -w], [0.0, w, u]])
-        t = np.dot(np.dot(self.ityiq, bt), self.tyiq).T
-        a = _np(src).astype(np.float32)
-        return _wrap(np.dot(a, t.astype(np.float32)), src)
+        ang = _rand.uniform(-self.hue, self.hue) * np.pi
+        rot = np.array([[1.0, 0.0, 0.0], [0.0, np.cos(ang), -np.sin(ang)], [0.0, np.sin(ang), np.cos(ang)]])
+        mix = (_YIQ2RGB @ rot @ _RGB2YIQ).T.astype(np.float32)
+        return _like(_host(src).astype(np.float32) @ mix, src)
 
 
 class ColorJitterAug(RandomOrderAug):
+    """Brightness / contrast / saturation jitters (the non-zero ones) in random order."""
+
     def __init__(self, brightness, contrast, saturation):
-        ts = []
-        if brightness > 0:
-            ts.append(BrightnessJitterAug(brightness))
-        if contrast > 0:
-            ts.append(ContrastJitterAug(contrast))
-        if saturation > 0:
-            ts.append(SaturationJitterAug(saturation))
-        super().__init__(ts)
+        parts = [(brightness, BrightnessJitterAug), (contrast, ContrastJitterAug),
+                 (saturation, SaturationJitterAug)]
+        super().__init__([cls(amount) for amount, cls in parts if amount > 0])
 
 
 class LightingAug(Augmenter):
+    """AlexNet PCA lighting noise: add ``eigvec @ (alpha * eigval)``, ``alpha ~ N(0, alphastd)``."""
+
     def __init__(self, alphastd, eigval, eigvec):
         super().__init__(alphastd=alphastd, eigval=eigval, eigvec=eigvec)
-        self.alphastd = alphastd
-        self.eigval = np.asarray(eigval)
-        self.eigvec = np.asarray(eigvec)
+        self.eigval, self.eigvec = np.asarray(eigval), np.asarray(eigvec)
 
     def __call__(self, src):
         alpha = np.random.normal(0, self.alphastd, size=(3,))
-        rgb = np.dot(self.eigvec * alpha, self.eigval)
-        return src + nd.array(rgb.astype(np.float32)) if isinstance(src, NDArray) else src + rgb
+        shift = (self.eigvec * alpha) @ self.eigval
+        return src + nd.array(shift.astype(np.float32)) if isinstance(src, NDArray) else src + shift
 
 
 class ColorNormalizeAug(Augmenter):
+    """``color_normalize`` with fixed ``mean`` / ``std``."""
+
     def __init__(self, mean, std):
         super().__init__(mean=mean, std=std)
-        self.mean = mean if mean is None or isinstance(mean, NDArray) else nd.array(mean)
-        self.std = std if std is None or isinstance(std, NDArray) else nd.array(std)
+        self.mean = None if mean is None else (mean if isinstance(mean, NDArray) else nd.array(mean))
+        self.std = None if std is None else (std if isinstance(std, NDArray) else nd.array(std))
 
     def __call__(self, src):
         return color_normalize(src, self.mean, self.std)
 
 
+# luma-ish grey projection replicated into three channels
+_GREY3 = np.repeat(np.array([[0.21], [0.72], [0.07]], dtype=np.float32), 3, axis=1)
+
+
 class RandomGrayAug(Augmenter):
+    """With probability ``p`` replace the image with its grey version."""
+
     def __init__(self, p):
         super().__init__(p=p)
-        self.p = p
-        self.mat = np.array([[0.21, 0.21, 0.21], [0.72, 0.72, 0.72], [0.07, 0.07, 0.07]], dtype=np.float32)
 
     def __call__(self, src):
-        if _pyrandom.random() < self.p:
-            src = _wrap(np.dot(_np(src).astype(np.float32), self.mat), src)
-        return src
+        if _rand.random() >= self.p:
+            return src
+        return _like(_host(src).astype(np.float32) @ _GREY3, src)
 
 
 class HorizontalFlipAug(Augmenter):
+    """With probability ``p`` mirror left-right."""
+
     def __init__(self, p):
         super().__init__(p=p)
-        self.p = p
 
     def __call__(self, src):
-        if _pyrandom.random() < self.p:
-            src = nd.flip(src, axis=1)
-        return src
+        return nd.flip(src, axis=1) if _rand.random() < self.p else src
 
 
 class CastAug(Augmenter):
+    """Cast to ``typ`` (recorded as ``type`` like the reference)."""
+
     def __init__(self, typ='float32'):
         super().__init__(type=typ)
         self.typ = typ
@@ -484,45 +551,69 @@ class CastAug(Augmenter):
 def CreateAugmenter(data_shape, resize=0, rand_crop=False, rand_resize=False, rand_mirror=False, mean=None,
                     std=None, brightness=0, contrast=0, saturation=0, hue=0, pca_noise=0, rand_gray=0,
                     inter_method=2):
-    """Standard augmenter list (resize -> crop -> flip -> cast -> color -> normalize)."""
-    auglist = []
-    if resize > 0:
-        auglist.append(ResizeAug(resize, inter_method))
-    crop_size = (data_shape[2], data_shape[1])
+    """The standard classification pipeline: resize, crop, mirror, cast, colour, normalise."""
+    crop = (data_shape[2], data_shape[1])
     if rand_resize:
         assert rand_crop
-        auglist.append(RandomSizedCropAug(crop_size, 0.08, (3.0 / 4.0, 4.0 / 3.0), inter_method))
-    elif rand_crop:
-        auglist.append(RandomCropAug(crop_size, inter_method))
+        cropper = RandomSizedCropAug(crop, 0.08, (3.0 / 4.0, 4.0 / 3.0), inter_method)
     else:
-        auglist.append(CenterCropAug(crop_size, inter_method))
-    if rand_mirror:
-        auglist.append(HorizontalFlipAug(0.5))
-    auglist.append(CastAug())
-    if brightness or contrast or saturation:
-        auglist.append(ColorJitterAug(brightness, contrast, saturation))
-    if hue:
-        auglist.append(HueJitterAug(hue))
-    if pca_noise > 0:
-        eigval = np.array([55.46, 4.794, 1.148])
-        eigvec = np.array([[-0.5675, 0.7192, 0.4009], [-0.5808, -0.0045, -0.8140], [-0.5836, -0.6948, 0.4203]])
-        auglist.append(LightingAug(pca_noise, eigval, eigvec))
-    if rand_gray > 0:
-        auglist.append(RandomGrayAug(rand_gray))
-    if mean is True:
-        mean = nd.array([123.68, 116.28, 103.53])
-    if std is True:
-        std = nd.array([58.395, 57.12, 57.375])
-    if mean is not None or std is not None:
-        auglist.append(ColorNormalizeAug(mean, std))
-    return auglist
+        cropper = (RandomCropAug if rand_crop else CenterCropAug)(crop, inter_method)
+    mean = nd.array(_IMAGENET_MEAN) if mean is True else mean
+    std = nd.array(_IMAGENET_STD) if std is True else std
+    stages = [
+        (resize > 0, lambda: ResizeAug(resize, inter_method)),
+        (True, lambda: cropper),
+        (rand_mirror, lambda: HorizontalFlipAug(0.5)),
+        (True, CastAug),
+        (brightness or contrast or saturation, lambda: ColorJitterAug(brightness, contrast, saturation)),
+        (hue, lambda: HueJitterAug(hue)),
+        (pca_noise > 0, lambda: LightingAug(pca_noise, _PCA_EIGVAL, _PCA_EIGVEC)),
+        (rand_gray > 0, lambda: RandomGrayAug(rand_gray)),
+        (mean is not None or std is not None, lambda: ColorNormalizeAug(mean, std)),
+    ]
+    return [make() for wanted, make in stages if wanted]
+
+
+# --------------------------------------------------------------------------- ImageIter
+def _read_list_file(path, dtype):
+    """``index<TAB>label...<TAB>path`` lines -> (keys, {key: (label, path)})."""
+    keys, table = [], {}
+    with open(path) as fh:
+        for line in fh:
+            cols = line.strip().split('\t')
+            if len(cols) < 2:
+                continue
+            key = int(cols[0])
+            table[key] = (nd.array([float(v) for v in cols[1:-1]], dtype=dtype), cols[-1])
+            keys.append(key)
+    return keys, table
+
+
+def _read_list_obj(items, dtype):
+    """In-memory ``[label..., path]`` entries -> (keys, {key: (label, path)}), keys '1', '2', ..."""
+    keys, table = [], {}
+    for pos, item in enumerate(items, 1):
+        key = str(pos)
+        if len(item) > 2:
+            label = nd.array(item[:-1], dtype=dtype)
+        elif isinstance(item[0], (int, float, np.number)):
+            label = nd.array([item[0]], dtype=dtype)
+        else:
+            label = nd.array(item[0], dtype=dtype)
+        table[key] = (label, item[-1])
+        keys.append(key)
+    return keys, table
 
 
 class ImageIter(mxio.DataIter):
-    """Image iterator over a .rec file, an image list file or an in-memory list, with augmenters.
+    """Batches of augmented images from a RecordIO file, a ``.lst`` file or an in-memory list.
 
-    Decoding+augmentation of a batch runs on a thread pool of
-    ``MXNET_CPU_WORKER_NTHREADS`` workers (PIL releases the GIL).
+    Samples come from ``path_imgrec`` (optionally indexed by ``path_imgidx``), from
+    ``path_imglist`` / ``imglist`` entries ``[label..., path]`` read under ``path_root``, or from a
+    record file whose labels are overridden by a list.  ``last_batch_handle`` is ``'pad'`` (fill
+    the last batch from the start of the epoch, report ``pad``), ``'discard'`` or ``'roll_over'``
+    (carry the partial batch into the next epoch).  Subclasses customise one sample through
+    ``next_sample`` / ``imdecode`` / ``augmentation_transform`` / ``postprocess_data``.
     """
 
     def __init__(self, batch_size, data_shape, label_width=1, path_imgrec=None, path_imglist=None, path_root=None,
@@ -531,55 +622,30 @@ class ImageIter(mxio.DataIter):
                  **kwargs):
         super().__init__()
         assert path_imgrec or path_imglist or isinstance(imglist, list)
-        assert dtype in ['int32', 'float32', 'int64', 'float64'], dtype + ' label not supported'
-        if path_imgrec:
-            if path_imgidx:
-                self.imgrec = recordio.MXIndexedRecordIO(path_imgidx, path_imgrec, 'r')
-                self.imgidx = list(self.imgrec.keys)
-            else:
-                self.imgrec = recordio.MXRecordIO(path_imgrec, 'r')
-                self.imgidx = None
-        else:
-            self.imgrec = None
-        imgkeys = []
+        assert dtype in ('int32', 'float32', 'int64', 'float64'), dtype + ' label not supported'
+        self.imgrec, self.imgidx = None, None
+        if path_imgrec and path_imgidx:
+            self.imgrec = recordio.MXIndexedRecordIO(path_imgidx, path_imgrec, 'r')
+            self.imgidx = list(self.imgrec.keys)
+        elif path_imgrec:
+            self.imgrec = recordio.MXRecordIO(path_imgrec, 'r')
+        keys, self.imglist = [], None
         if path_imglist:
-            with open(path_imglist) as fin:
-                imglist_d = {}
-                for line in fin:
-                    line = line.strip().split('\t')
-                    if len(line) < 2:
-                        continue
-                    label = nd.array([float(x) for x in line[1:-1]], dtype=dtype)
-                    key = int(line[0])
-                    imglist_d[key] = (label, line[-1])
-                    imgkeys.append(key)
-                self.imglist = imglist_d
+            keys, self.imglist = _read_list_file(path_imglist, dtype)
         elif isinstance(imglist, list):
-            result = {}
-            for index, img in enumerate(imglist, 1):
-                key = str(index)
-                if len(img) > 2:
-                    label = nd.array(img[:-1], dtype=dtype)
-                elif isinstance(img[0], (int, float, np.number)):
-                    label = nd.array([img[0]], dtype=dtype)
-                else:
-                    label = nd.array(img[0], dtype=dtype)
-                result[key] = (label, img[-1])
-                imgkeys.append(key)
-            self.imglist = result
-        else:
-            self.imglist = None
+            keys, self.imglist = _read_list_obj(imglist, dtype)
         self.path_root = path_root
         self.check_data_shape(data_shape)
-        self.provide_data = [(data_name, (batch_size,) + tuple(data_shape))]
-        self.provide_label = [(label_name, (batch_size, label_width) if label_width > 1 else (batch_size,))]
         self.batch_size = batch_size
         self.data_shape = tuple(data_shape)
         self.label_width = label_width
         self.shuffle = shuffle
         self.dtype = dtype
+        self.provide_data = [(data_name, (batch_size,) + self.data_shape)]
+        self.provide_label = [(label_name, (batch_size, label_width) if label_width > 1 else (batch_size,))]
+        # the visiting order: list keys, record index keys, or None = stream the record file
         if self.imgrec is None:
-            self.seq = imgkeys
+            self.seq = keys
         elif shuffle or num_parts > 1 or path_imgidx:
             assert self.imgidx is not None
             self.seq = self.imgidx
@@ -587,144 +653,95 @@ class ImageIter(mxio.DataIter):
             self.seq = None
         if num_parts > 1:
             assert part_index < num_parts
-            n = len(self.seq)
-            c = n // num_parts
-            self.seq = self.seq[part_index * c:(part_index + 1) * c]
+            share = len(self.seq) // num_parts
+            self.seq = self.seq[part_index * share:(part_index + 1) * share]
+        self.num_image = None if self.seq is None else len(self.seq)
         self.auglist = CreateAugmenter(data_shape, **kwargs) if aug_list is None else aug_list
+        self.last_batch_handle = last_batch_handle
         self.cur = 0
         self._allow_read = True
-        self.last_batch_handle = last_batch_handle
-        self.num_image = len(self.seq) if self.seq is not None else None
-        self._cache_data = None
-        self._cache_label = None
-        self._cache_idx = None
+        self._drop_carry()
         self.reset()
 
-    def reset(self):
-        if self.seq is not None and self.shuffle:
-            _pyrandom.shuffle(self.seq)
-        if self.last_batch_handle != 'roll_over' or self._cache_data is None:
-            if self.imgrec is not None:
-                self.imgrec.reset()
-            self.cur = 0
-            if self._allow_read is False:
-                self._allow_read = True
+    # ---------------------------------------------------------------- epoch control
+    def _drop_carry(self):
+        self._cache_data = self._cache_label = self._cache_idx = None
 
-    def hard_reset(self):
+    def _rewind(self):
         if self.seq is not None and self.shuffle:
-            _pyrandom.shuffle(self.seq)
+            _rand.shuffle(self.seq)
         if self.imgrec is not None:
             self.imgrec.reset()
         self.cur = 0
         self._allow_read = True
-        self._cache_data = None
-        self._cache_label = None
-        self._cache_idx = None
 
+    def reset(self):
+        """Start a new epoch (a ``roll_over`` carry keeps the read position)."""
+        if self.last_batch_handle == 'roll_over' and self._cache_data is not None:
+            if self.seq is not None and self.shuffle:
+                _rand.shuffle(self.seq)
+            return
+        self._rewind()
+
+    def hard_reset(self):
+        """Start over and forget any ``roll_over`` carry."""
+        self._rewind()
+        self._drop_carry()
+
+    # ---------------------------------------------------------------- one sample
     def next_sample(self):
-        if self._allow_read is False:
+        """``(label, encoded image bytes)`` of the next sample; StopIteration at epoch end."""
+        if not self._allow_read:
             raise StopIteration
-        if self.seq is not None:
-            if self.cur < self.num_image:
-                idx = self.seq[self.cur]
-            else:
+        if self.seq is None:
+            record = self.imgrec.read()
+            if record is None:
                 if self.last_batch_handle != 'discard':
-                    self.cur = 0
+                    self.imgrec.reset()
                 raise StopIteration
-            self.cur += 1
-            if self.imgrec is not None:
-                s = self.imgrec.read_idx(idx)
-                header, img = recordio.unpack(s)
-                if self.imglist is None:
-                    return header.label, img
-                return self.imglist[idx][0], img
-            label, fname = self.imglist[idx]
-            return label, self.read_image(fname)
-        s = self.imgrec.read()
-        if s is None:
+            header, payload = recordio.unpack(record)
+            return header.label, payload
+        if self.cur >= self.num_image:
             if self.last_batch_handle != 'discard':
-                self.imgrec.reset()
+                self.cur = 0
             raise StopIteration
-        header, img = recordio.unpack(s)
-        return header.label, img
+        key = self.seq[self.cur]
+        self.cur += 1
+        if self.imgrec is None:
+            label, fname = self.imglist[key]
+            return label, self.read_image(fname)
+        header, payload = recordio.unpack(self.imgrec.read_idx(key))
+        return (header.label if self.imglist is None else self.imglist[key][0]), payload
 
-    def _batchify(self, batch_data, batch_label, start=0):
-        i = start
-        batch_size = self.batch_size
+    def _sample_name(self):
+        """Human-readable id of the sample just read (for decode errors)."""
+        pos = (self.cur % self.num_image) - 1 if self.num_image else -1
+        key = self.seq[pos] if self.seq is not None else pos
+        if self.imglist is not None:
+            return 'Broken image filename: {}'.format(self.imglist[key][1])
+        return 'Broken image index: {}'.format(key)
+
+    def imdecode(self, s):
+        """Decode one sample's bytes (errors name the offending file / index)."""
         try:
-            while i < batch_size:
-                label, s = self.next_sample()
-                data = self.imdecode(s)
-                try:
-                    self.check_valid_image(data)
-                except RuntimeError as e:
-                    logging.debug('Invalid image, skipping:  %s', str(e))
-                    continue
-                data = self.augmentation_transform(data)
-                assert i < batch_size, 'Batch size must be multiples of augmenter output length'
-                batch_data[i] = self.postprocess_data(data)
-                batch_label[i] = label
-                i += 1
-        except StopIteration:
-            if not i:
-                raise StopIteration
-        return i
+            return imdecode(s)
+        except Exception as err:      # pylint: disable=broad-except
+            raise RuntimeError('{}, {}'.format(self._sample_name(), err))
 
-    def next(self):
-        batch_size = self.batch_size
-        c, h, w = self.data_shape
-        if self._cache_data is not None:
-            assert self._cache_label is not None
-            assert self._cache_idx is not None
-            batch_data, batch_label, i = self._cache_data, self._cache_label, self._cache_idx
-        else:
-            batch_data = nd.zeros((batch_size, c, h, w))
-            batch_label = nd.empty(self.provide_label[0][1])
-            batch_label[:] = 0
-            i = self._batchify(batch_data, batch_label)
-        pad = batch_size - i
-        if pad != 0:
-            if self.last_batch_handle == 'discard':
-                raise StopIteration
-            if self.last_batch_handle == 'roll_over' and self._cache_data is None:
-                self._cache_data, self._cache_label, self._cache_idx = batch_data, batch_label, i
-                raise StopIteration
-            _ = self._batchify(batch_data, batch_label, i)
-            if self.last_batch_handle == 'pad':
-                self._allow_read = False
-            else:
-                self._cache_data = self._cache_label = self._cache_idx = None
-        return mxio.DataBatch([batch_data], [batch_label], pad=pad)
+    def read_image(self, fname):
+        """Encoded bytes of ``fname`` relative to ``path_root``."""
+        with open(os.path.join(self.path_root or '', fname), 'rb') as fh:
+            return fh.read()
 
     def check_data_shape(self, data_shape):
-        if not len(data_shape) == 3:
+        if len(data_shape) != 3:
             raise ValueError('data_shape should have length 3, with dimensions CxHxW')
-        if not data_shape[0] == 3:
+        if data_shape[0] != 3:
             raise ValueError('This iterator expects inputs to have 3 channels.')
 
     def check_valid_image(self, data):
         if len(data[0].shape) == 0:
             raise RuntimeError('Data shape is wrong')
-
-    def imdecode(self, s):
-        def locate():
-            if self.seq is not None:
-                idx = self.seq[(self.cur % self.num_image) - 1]
-            else:
-                idx = (self.cur % self.num_image) - 1
-            if self.imglist is not None:
-                _, fname = self.imglist[idx]
-                return 'Broken image filename: {}'.format(fname)
-            return 'Broken image index: {}'.format(idx)
-        try:
-            img = imdecode(s)
-        except Exception as e:
-            raise RuntimeError('{}, {}'.format(locate(), e))
-        return img
-
-    def read_image(self, fname):
-        with open(os.path.join(self.path_root or '', fname), 'rb') as fin:
-            return fin.read()
 
     def augmentation_transform(self, data):
         for aug in self.auglist:
@@ -732,4 +749,58 @@ class ImageIter(mxio.DataIter):
         return data
 
     def postprocess_data(self, datum):
+        """HWC -> CHW."""
         return nd.transpose(datum, axes=(2, 0, 1))
+
+    def _load_one(self, label, raw):
+        """Decoded, validated and augmented ``(chw image, label)``; RuntimeError skips the sample."""
+        img = self.imdecode(raw)
+        self.check_valid_image(img)
+        return self.postprocess_data(self.augmentation_transform(img)), label
+
+    # ---------------------------------------------------------------- batches
+    def _empty_label_batch(self):
+        lab = nd.empty(self.provide_label[0][1])
+        lab[:] = 0
+        return lab
+
+    def _batchify(self, batch_data, batch_label, start=0):
+        """Fill rows ``start..`` of the batch; returns the number of filled rows."""
+        filled = start
+        try:
+            while filled < self.batch_size:
+                label, raw = self.next_sample()
+                try:
+                    datum, label = self._load_one(label, raw)
+                except RuntimeError as err:
+                    logging.debug('Invalid image, skipping:  %s', err)
+                    continue
+                batch_data[filled] = datum
+                batch_label[filled] = label
+                filled += 1
+        except StopIteration:
+            if filled == 0:
+                raise
+        return filled
+
+    def next(self):
+        if self._cache_data is not None:
+            data, label, filled = self._cache_data, self._cache_label, self._cache_idx
+        else:
+            data = nd.zeros((self.batch_size,) + self.data_shape)
+            label = self._empty_label_batch()
+            filled = self._batchify(data, label)
+        pad = self.batch_size - filled
+        if pad:
+            if self.last_batch_handle == 'discard':
+                raise StopIteration
+            if self.last_batch_handle == 'roll_over' and self._cache_data is None:
+                self._cache_data, self._cache_label, self._cache_idx = data, label, filled
+                raise StopIteration
+            # 'pad' wraps to the start of the epoch; a roll_over carry is completed the same way
+            self._batchify(data, label, filled)
+            if self.last_batch_handle == 'pad':
+                self._allow_read = False
+            else:
+                self._drop_carry()
+        return mxio.DataBatch([data], [label], pad=pad)

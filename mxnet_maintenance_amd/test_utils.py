@@ -661,7 +661,38 @@ def download(url, fname=None, dirname=None, overwrite=False, retries=5):
         fname = os.path.join(dirname, fname)
     if os.path.exists(fname) and not overwrite:
         return fname
+    maker = _SYNTHETIC_DOWNLOADS.get(os.path.basename(fname)) if _synthetic_enabled() else None
+    if maker is not None:
+        cached = os.path.join(_synthetic_cache('downloads'), os.path.basename(fname))
+        if not os.path.exists(cached):
+            maker(cached + '.part')
+            os.replace(cached + '.part', cached)
+        if os.path.dirname(os.path.abspath(fname)):
+            os.makedirs(os.path.dirname(os.path.abspath(fname)), exist_ok=True)
+        import shutil
+        shutil.copyfile(cached, fname)
+        return fname
     raise MXNetError('download(%s): no network access; place the file at %s' % (url, fname))
+
+
+def _make_synthetic_test_images(path, count=16, seed=5):
+    """Stand-in for the reference's test_images.tar.gz: ``count`` JPEGs of varied sizes under
+    ``test_images/`` (the ImageIter tests' batch arithmetic assumes 16 images)."""
+    import io as _io
+    import tarfile
+    from PIL import Image
+    rng = np.random.RandomState(seed)
+    with tarfile.open(path, 'w:gz') as tar:
+        for i in range(count):
+            h, w = int(rng.randint(180, 400)), int(rng.randint(180, 400))
+            yy, xx = np.mgrid[0:h, 0:w]
+            img = np.stack([(xx * 255 // w), (yy * 255 // h), rng.randint(0, 256, size=(h, w))], 2).astype(np.uint8)
+            buf = _io.BytesIO()
+            Image.fromarray(img).save(buf, format='JPEG', quality=90)
+            info = tarfile.TarInfo('test_images/img%02d.jpg' % i)
+            info.size = len(buf.getvalue())
+            buf.seek(0)
+            tar.addfile(info, buf)
 
 
 def get_mnist(num_train=60000, num_test=10000, seed=42):
@@ -1156,6 +1187,7 @@ def _make_synthetic_libsvm(path, n, dim, nclass, seed=3):
 
 
 _SYNTHETIC_LIBSVM = {'news20.t': (3993, 62061, 20)}
+_SYNTHETIC_DOWNLOADS = {'test_images.tar.gz': _make_synthetic_test_images}
 
 
 def get_bz2_data(data_dir, data_name, url, data_origin_name):

@@ -45,7 +45,7 @@ def run_one(ref, name, timeout, workers, select=None, tb=None, extra=()):
     tmp = tempfile.mkdtemp(prefix='mxref_')
     try:
         unit = os.path.join(tmp, 'unittest')
-        os.makedirs(unit)
+        os.makedirs(os.path.join(unit, 'data'))        # the reference CI's scratch dir for .lst/.rec files
         # the whole unittest directory: test files import each other (test_module -> test_bucketing)
         src_dirs = [os.path.join(ref, 'unittest')]
         if '/' in name:
