@@ -66,6 +66,7 @@ from . import utils
 from . import numpy
 from . import numpy as np
 from . import numpy_extension
+from . import numpy_dispatch_protocol
 from . import numpy_extension as npx
 from . import rtc
 from . import numpy_op_signature

@@ -458,7 +458,7 @@ class Constant(Parameter):
             def _init_weight(self, _, arr):
                 initializer.Initializer._set(arr, value._data)
         key = 'Constant_{}_{}'.format(name, id(self))
-        initializer._INIT_REGISTRY[key.lower()] = _ConstInit
+        initializer._REGISTRY[key.lower()] = _ConstInit
         super().__init__(name, grad_req='null', shape=value.shape, dtype=value.dtype, init=key)
 
     def __repr__(self):

@@ -10,6 +10,8 @@ from .multiarray import *  # noqa: F401,F403
 from .multiarray import ndarray, _np_out
 from . import linalg, random
 from . import fallback as _fallback
+from . import fallback
+from . import fallback_linalg
 
 _fallback.install(globals())
 _fallback.install(linalg.__dict__, _fallback._LINALG, __import__('numpy').linalg)

@@ -20,9 +20,12 @@ _NAMES = ['allclose', 'alltrue', 'apply_along_axis', 'apply_over_axes', 'argpart
           'packbits', 'poly', 'polyadd', 'polydiv', 'polyfit', 'polyint', 'polymul', 'polysub', 'positive',
           'promote_types', 'ptp', 'real', 'result_type', 'rollaxis', 'roots', 'searchsorted', 'select', 'setdiff1d',
           'setxor1d', 'signbit', 'size', 'spacing', 'take_along_axis', 'trapz', 'tril_indices_from', 'trim_zeros',
-          'triu_indices_from', 'union1d', 'unpackbits', 'unwrap', 'vander', 'nansum', 'nanmean', 'nanstd', 'nanvar',
-          'convolve', 'gradient', 'sinc', 'angle', 'conj', 'imag', 'iscomplex', 'isreal', 'fliplr', 'flipud']
+          'triu_indices_from', 'union1d', 'unpackbits', 'unwrap', 'vander']
+# host fallbacks here that the reference implements as device operators (not part of its fallback list)
+_ALSO_HOST = ['nansum', 'nanmean', 'nanstd', 'nanvar', 'convolve', 'gradient', 'sinc', 'angle', 'conj', 'imag',
+              'iscomplex', 'isreal', 'fliplr', 'flipud']
 _LINALG = ['cond', 'lstsq', 'matrix_power', 'matrix_rank', 'multi_dot', 'qr']
+__all__ = list(_NAMES)
 
 
 def _ctx_of(args):
@@ -66,7 +69,7 @@ def make(fn, name):
     return f
 
 
-def install(namespace, names=_NAMES, mod=onp):
+def install(namespace, names=tuple(_NAMES) + tuple(_ALSO_HOST), mod=onp):
     for n in names:
         if n not in namespace and hasattr(mod, n):
             namespace[n] = make(getattr(mod, n), n)

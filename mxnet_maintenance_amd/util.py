@@ -7,7 +7,7 @@ from . import _state
 __all__ = ['is_np_shape', 'is_np_array', 'set_np_shape', 'set_np', 'reset_np', 'use_np', 'use_np_shape',
            'use_np_array', 'np_shape', 'np_array', 'getenv', 'setenv', 'makedirs', 'get_gpu_count',
            'get_gpu_memory', 'set_module', 'wrap_np_unary_func', 'wrap_np_binary_func', 'default_array',
-           'get_cuda_compute_capability']
+           'get_cuda_compute_capability', 'set_flush_denorms']
 
 
 def makedirs(d):
@@ -39,6 +39,19 @@ def setenv(name, value):
         os.environ.pop(name, None)
     else:
         os.environ[name] = str(value)
+
+
+# flush-to-zero / denormals-are-zero for CPU float math (reference util.py:852; on by default there)
+_FLUSH_DENORMS = [True]
+
+
+def set_flush_denorms(value):
+    """Enable / disable flushing of denormal CPU floats to zero; returns the previous state."""
+    import torch
+    prev = _FLUSH_DENORMS[0]
+    if torch.set_flush_denormal(bool(value)) or not value:
+        _FLUSH_DENORMS[0] = bool(value)
+    return prev
 
 
 def is_np_shape():

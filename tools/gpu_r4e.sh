@@ -1,0 +1,14 @@
+# round-4: graph-captured RCCL bucket all-reduce test (deterministic), full GPU test suite
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {
+  local log=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "gpurun_out/$log" 2>&1
+  local rc=$?
+  echo "step $log rc=$rc"
+  if [ $rc -ge 124 ]; then exit $rc; fi
+  return 0
+}
+PYT="python -u -m pytest -v --timeout 300 --timeout-method thread -p no:cacheprovider"
+step r4e_dist_tests.log 300 $PYT tests/test_distributed_gpu.py
+step r4e_gpu_all.log 900 $PYT -m gpu tests -x
