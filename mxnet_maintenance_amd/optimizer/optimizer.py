@@ -259,65 +259,88 @@ def _as_list(x):
     return x if isinstance(x, (list, tuple)) else [x]
 
 
+def _zeros(weight, count=1, dtype=None):
+    """``count`` zero state arrays shaped like ``weight`` (a single array when ``count == 1``)."""
+    made = tuple(NDArray(torch.zeros_like(weight._data, dtype=dtype)) for _ in range(count))
+    return made[0] if count == 1 else made
+
+
+def _is_half(weight):
+    return weight._data.dtype in (torch.float16, torch.bfloat16)
+
+
+def _master_then(opt, weight, make_state):
+    """Multi-precision state ``(make_state(master), master)`` -- the SGD-family layout (state first)."""
+    if opt.multi_precision and _is_half(weight):
+        master = NDArray(weight._data.detach().float().clone())
+        return (make_state(master), master)
+    return make_state(weight)
+
+
+class _Stepper(Optimizer):
+    """Shared plumbing of the concrete optimizers below: hyper-parameters kept as attributes,
+    one call that counts the update and resolves (lr, wd, t), and gradient conditioning."""
+
+    def _hyper(self, **values):
+        self.__dict__.update(values)
+
+    def _begin(self, index):
+        self._update_count(index)
+        return self._get_lr(index), self._get_wd(index), self._index_update_count[index]
+
+    def _conditioned(self, grad, decay_with=None, wd=0.0):
+        """``clip(rescale * grad (+ wd * decay_with))`` (decay before clipping when given)."""
+        g = grad._data * self.rescale_grad
+        if decay_with is not None and wd:
+            g = g + wd * decay_with._data
+        if self.clip_gradient is not None:
+            g = torch.clamp(g, -self.clip_gradient, self.clip_gradient)
+        return g
+
+
 @register
-class SGD(Optimizer):
+class SGD(_Stepper):
     """SGD with optional momentum and multi-precision (fp32 master weights).
 
-    ``state = momentum * state + lr * (rescale_grad * clip(grad) + wd * weight)``;
-    ``weight -= state`` (MXNet's sign convention: mom stores -lr*update).
+    ``state = momentum * state - lr * (rescale_grad * clip(grad) + wd * weight)``; ``weight += state``.
+    Lists of indices (``aggregate_num``) run as one multi-tensor update; row_sparse gradients with
+    ``lazy_update`` touch only their rows.
     """
 
     def __init__(self, momentum=0.0, lazy_update=True, **kwargs):
         super().__init__(**kwargs)
-        self.momentum = momentum
-        self.lazy_update = lazy_update
-        self.aggregate_num = int(kwargs.get('aggregate_num') or 1 << 30)
+        self._hyper(momentum=momentum, lazy_update=lazy_update,
+                    aggregate_num=int(kwargs.get('aggregate_num') or 1 << 30))
 
     def create_state_multi_precision(self, index, weight):
-        weight_master_copy = None
-        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
-            weight_master_copy = NDArray(weight._data.detach().float().clone())
-            return (self.create_state(index, weight_master_copy), weight_master_copy)
-        if weight._data.dtype in (torch.float16, torch.bfloat16) and not self.multi_precision:
+        if _is_half(weight) and not self.multi_precision:
             warnings.warn('Accumulating with float16 in optimizer can lead to poor accuracy or slow convergence. '
                           'Consider using multi_precision=True option of the SGD optimizer')
-        return self.create_state(index, weight)
+        return _master_then(self, weight, lambda w: self.create_state(index, w))
 
     def create_state(self, index, weight):
-        if self.momentum != 0.0:
-            return NDArray(torch.zeros_like(weight._data))
-        return None
+        return _zeros(weight) if self.momentum != 0.0 else None
 
-    def _update_impl(self, indices, weights, grads, states, multi_precision=False):
-        indices, weights, grads, states = map(_as_list, (indices, weights, grads, states)) \
+    def _apply(self, indices, weights, grads, states, with_master):
+        idx, ws, gs, sts = (list(indices), list(weights), list(grads), list(states)) \
             if isinstance(indices, (list, tuple)) else ([indices], [weights], [grads], [states])
-        self._update_count(indices)
-        lrs = self._get_lrs(indices)
-        wds = self._get_wds(indices)
-        clip = self._clip()
-        if self.lazy_update and any(_is_rsp(g) for g in grads):
-            for w, g, st, lr, wd in zip(weights, grads, states, lrs, wds):
-                mom, w32 = (st if multi_precision else (st, None))
-                _lazy_sgd_rows(w._data, g, None if mom is None else mom._data,
-                               None if w32 is None else w32._data, lr, wd, self.momentum, self.rescale_grad, clip)
+        self._update_count(idx)
+        lrs, wds, clip = self._get_lrs(idx), self._get_wds(idx), self._clip()
+        split = [(st if with_master else (st, None)) for st in sts]
+        moms = [None if m is None else m._data for m, _ in split]
+        masters = [None if w32 is None else w32._data for _, w32 in split]
+        if self.lazy_update and any(_is_rsp(g) for g in gs):
+            for w, g, m, w32, lr, wd in zip(ws, gs, moms, masters, lrs, wds):
+                _lazy_sgd_rows(w._data, g, m, w32, lr, wd, self.momentum, self.rescale_grad, clip)
             return
-        W = [w._data for w in weights]
-        G = [g._data for g in grads]
-        if multi_precision:
-            M = [s[0]._data if s[0] is not None else None for s in states]
-            W32 = [s[1]._data for s in states]
-        else:
-            M = [s._data if s is not None else None for s in states]
-            W32 = None
-        multi_sgd(W, G, M, W32, lrs, wds, self.momentum, self.rescale_grad, clip)
+        multi_sgd([w._data for w in ws], [g._data for g in gs], moms, masters if with_master else None,
+                  lrs, wds, self.momentum, self.rescale_grad, clip)
 
     def update(self, index, weight, grad, state):
-        self._update_impl(index, weight, grad, state, multi_precision=False)
+        self._apply(index, weight, grad, state, False)
 
     def update_multi_precision(self, index, weight, grad, state):
-        ws = _as_list(weight)
-        use_mp = self.multi_precision and ws[0]._data.dtype in (torch.float16, torch.bfloat16)
-        self._update_impl(index, weight, grad, state, multi_precision=use_mp)
+        self._apply(index, weight, grad, state, self.multi_precision and _is_half(_as_list(weight)[0]))
 
 
 def _is_rsp(g):
@@ -409,184 +432,151 @@ def multi_sgd(W, G, M, W32, lrs, wds, momentum, rescale, clip):
 
 
 @register
-class Signum(Optimizer):
+class Signum(_Stepper):
+    """signSGD / Signum (Bernstein et al. 2018): step by the sign of the (momentum-averaged) gradient."""
+
     def __init__(self, learning_rate=0.01, momentum=0.9, wd_lh=0.0, **kwargs):
         super().__init__(learning_rate=learning_rate, **kwargs)
-        self.momentum = momentum
-        self.wd_lh = wd_lh
+        self._hyper(momentum=momentum, wd_lh=wd_lh)
 
     def create_state(self, index, weight):
-        if self.momentum != 0.0:
-            return NDArray(torch.zeros_like(weight._data))
-        return None
+        return _zeros(weight) if self.momentum != 0.0 else None
 
     def update(self, index, weight, grad, state):
-        self._update_count(index)
-        lr = self._get_lr(index)
-        wd = self._get_wd(index)
-        if state is not None:
-            _oo.signum_update(weight._data, grad._data, state._data, lr=lr, momentum=self.momentum, wd=wd,
-                              rescale_grad=self.rescale_grad, clip_gradient=self._clip(), wd_lh=self.wd_lh)
+        lr, wd, _ = self._begin(index)
+        common = dict(lr=lr, wd=wd, rescale_grad=self.rescale_grad, clip_gradient=self._clip())
+        if state is None:
+            _oo.signsgd_update(weight._data, grad._data, **common)
         else:
-            _oo.signsgd_update(weight._data, grad._data, lr=lr, wd=wd, rescale_grad=self.rescale_grad,
-                               clip_gradient=self._clip())
+            _oo.signum_update(weight._data, grad._data, state._data, momentum=self.momentum, wd_lh=self.wd_lh,
+                              **common)
 
 
 @register
-class FTML(Optimizer):
+class FTML(_Stepper):
+    """FTML (Zheng & Kwok 2017); state (d, v, z)."""
+
     def __init__(self, beta1=0.6, beta2=0.999, epsilon=1e-8, **kwargs):
         super().__init__(**kwargs)
-        self.beta1 = beta1
-        self.beta2 = beta2
-        self.epsilon = epsilon
+        self._hyper(beta1=beta1, beta2=beta2, epsilon=epsilon)
 
     def create_state(self, index, weight):
-        z = lambda: NDArray(torch.zeros_like(weight._data))
-        return (z(), z(), z())
+        return _zeros(weight, 3)
 
     def update(self, index, weight, grad, state):
-        self._update_count(index)
-        t = self._index_update_count[index]
-        d, v, z = state
-        _oo.ftml_update(weight._data, grad._data, d._data, v._data, z._data, lr=self._get_lr(index),
-                        beta1=self.beta1, beta2=self.beta2, epsilon=self.epsilon, t=t, wd=self._get_wd(index),
-                        rescale_grad=self.rescale_grad, clip_grad=self._clip())
+        lr, wd, t = self._begin(index)
+        d, v, z = (s._data for s in state)
+        _oo.ftml_update(weight._data, grad._data, d, v, z, lr=lr, beta1=self.beta1, beta2=self.beta2,
+                        epsilon=self.epsilon, t=t, wd=wd, rescale_grad=self.rescale_grad, clip_grad=self._clip())
+
+
+_NO_LARS_SUFFIXES = ('gamma', 'beta', 'bias')
 
 
 @register
-class LARS(Optimizer):
-    """SGD with layer-wise adaptive rate scaling (You et al. 2017)."""
+class LARS(_Stepper):
+    """SGD with layer-wise adaptive rate scaling (You et al. 2017): the learning rate of every
+    weight tensor is scaled by ``eta * |w| / (|g| + wd * |w| + eps)``."""
 
     def __init__(self, momentum=0.0, lazy_update=True, eta=0.001, eps=0, momentum_correction=True, **kwargs):
         super().__init__(**kwargs)
-        self.momentum = momentum
-        self.eta = eta
-        self.eps = eps
-        self.lazy_update = lazy_update
+        self._hyper(momentum=momentum, eta=eta, eps=eps, lazy_update=lazy_update)
 
     def create_state(self, index, weight):
-        if self.momentum != 0.0:
-            return NDArray(torch.zeros_like(weight._data, dtype=torch.float32))
-        return None
+        return _zeros(weight, dtype=torch.float32) if self.momentum != 0.0 else None
 
     def create_state_multi_precision(self, index, weight):
-        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
-            w32 = NDArray(weight._data.float())
-            return (self.create_state(index, w32), w32)
-        return self.create_state(index, weight)
+        return _master_then(self, weight, lambda w: self.create_state(index, w))
 
-    def _l2norm(self, v):
-        return float(torch.linalg.vector_norm(v.float()))
+    def _trust(self, index, weight, grad, lr, wd):
+        if self.idx2name.get(index, '').endswith(_NO_LARS_SUFFIXES):
+            return lr
+        w_norm = float(torch.linalg.vector_norm(weight._data.float()))
+        g_norm = float(torch.linalg.vector_norm(grad._data.float() * self.rescale_grad))
+        if w_norm > 0.0 and g_norm > 0.0:
+            return lr * self.eta * w_norm / (g_norm + wd * w_norm + self.eps)
+        return lr
 
     def update(self, index, weight, grad, state):
-        self._update_count(index)
-        lr = self._get_lr(index)
-        wd = self._get_wd(index)
-        name = self.idx2name.get(index, '')
-        if not (name.endswith('gamma') or name.endswith('beta') or name.endswith('bias')):
-            w_norm = self._l2norm(weight._data)
-            g_norm = self._l2norm(grad._data * self.rescale_grad)
-            if w_norm > 0.0 and g_norm > 0.0:
-                lr = lr * self.eta * w_norm / (g_norm + wd * w_norm + self.eps)
-        multi_sgd([weight._data], [grad._data], [state._data if state is not None else None], None, [lr], [wd],
+        lr, wd, _ = self._begin(index)
+        lr = self._trust(index, weight, grad, lr, wd)
+        multi_sgd([weight._data], [grad._data], [None if state is None else state._data], None, [lr], [wd],
                   self.momentum, self.rescale_grad, self._clip())
 
     def update_multi_precision(self, index, weight, grad, state):
-        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
-            mom, w32 = state
-            self.update(index, w32, NDArray(grad._data.float()), mom)
-            with torch.no_grad():
-                weight._data.copy_(w32._data)
-        else:
+        if not (self.multi_precision and _is_half(weight)):
             self.update(index, weight, grad, state)
+            return
+        mom, master = state
+        self.update(index, master, NDArray(grad._data.float()), mom)
+        with torch.no_grad():
+            weight._data.copy_(master._data)
+
+
+def _warmup_multiplier(strategy, done, total, peak):
+    """Large-batch warm-up factor after ``done`` of ``total`` warm-up updates (1 -> ``peak``)."""
+    if done >= total:
+        return peak
+    if total <= 1:
+        return 1.0
+    frac = {'linear': done / total, 'power2': (done * done) / (total * total),
+            'sqrt': math.sqrt(float(done) / total)}.get(strategy)
+    return 1.0 if frac is None else 1.0 + (peak - 1) * frac
 
 
 @register
-class LBSGD(Optimizer):
-    """Large-batch SGD with warmup strategies (reference optimizer.py LBSGD)."""
+class LBSGD(_Stepper):
+    """Large-batch SGD: momentum SGD whose learning rate ramps up to ``batch_scale`` x over
+    ``warmup_epochs`` (linear, power2 or sqrt)."""
 
     def __init__(self, momentum=0.0, multi_precision=False, warmup_strategy='linear', warmup_epochs=5,
                  batch_scale=1, updates_per_epoch=32, begin_epoch=0, num_epochs=60, **kwargs):
         super().__init__(multi_precision=multi_precision, **kwargs)
-        self.momentum = momentum
-        self.warmup_strategy = warmup_strategy
-        self.warmup_epochs = warmup_epochs
-        self.batch_scale = batch_scale
-        self.updates_per_epoch = updates_per_epoch
-        self.init_updates = begin_epoch * updates_per_epoch
-        self.num_epochs = num_epochs
-        self.lbmult = 1
-        self.cumgrads = {}
-        self.adaptive = False
-        self.admult = 1
+        self._hyper(momentum=momentum, warmup_strategy=warmup_strategy, warmup_epochs=warmup_epochs,
+                    batch_scale=batch_scale, updates_per_epoch=updates_per_epoch,
+                    init_updates=begin_epoch * updates_per_epoch, num_epochs=num_epochs,
+                    lbmult=1, cumgrads={}, adaptive=False, admult=1)
 
     def create_state(self, index, weight):
-        if self.momentum != 0.0:
-            return NDArray(torch.zeros_like(weight._data))
-        return None
+        return _zeros(weight) if self.momentum != 0.0 else None
 
     def _get_lbmult(self, nup):
-        nwup = self.warmup_epochs * self.updates_per_epoch
-        strategy = self.warmup_strategy
-        maxmult = float(self.batch_scale)
-        if nup >= nwup:
-            mult = maxmult
-        elif nwup <= 1:
-            mult = 1.0
-        else:
-            if strategy == 'linear':
-                mult = 1.0 + (maxmult - 1) * nup / nwup
-            elif strategy == 'power2':
-                mult = 1.0 + (maxmult - 1) * (nup * nup) / (nwup * nwup)
-            elif strategy == 'sqrt':
-                mult = 1.0 + (maxmult - 1) * math.sqrt(float(nup) / nwup)
-            else:
-                mult = 1.0
-        return mult
+        return _warmup_multiplier(self.warmup_strategy, nup, self.warmup_epochs * self.updates_per_epoch,
+                                  float(self.batch_scale))
 
     def update(self, index, weight, grad, state):
-        self._update_count(index)
-        lr = self._get_lr(index) * self._get_lbmult(self.num_update - self.init_updates)
-        wd = self._get_wd(index)
-        multi_sgd([weight._data], [grad._data], [state._data if state is not None else None], None, [lr], [wd],
+        lr, wd, _ = self._begin(index)
+        lr *= self._get_lbmult(self.num_update - self.init_updates)
+        multi_sgd([weight._data], [grad._data], [None if state is None else state._data], None, [lr], [wd],
                   self.momentum, self.rescale_grad, self._clip())
 
 
 @register
-class LAMB(Optimizer):
-    """LAMB optimizer (You et al. 2019), two-phase update as in the reference ops."""
+class LAMB(_Stepper):
+    """LAMB (You et al. 2019): Adam-style direction, per-tensor trust ratio ``|w| / |update|``
+    clamped to [lower_bound, upper_bound]; phase 1 / phase 2 as in the reference operators."""
 
     def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-6, lower_bound=None,
                  upper_bound=None, bias_correction=True, **kwargs):
         super().__init__(learning_rate=learning_rate, **kwargs)
-        self.beta1 = beta1
-        self.beta2 = beta2
-        self.epsilon = epsilon
-        self.lower_bound = lower_bound
-        self.upper_bound = upper_bound
-        self.bias_correction = bias_correction
+        self._hyper(beta1=beta1, beta2=beta2, epsilon=epsilon, lower_bound=lower_bound, upper_bound=upper_bound,
+                    bias_correction=bias_correction)
 
     def create_state(self, index, weight):
-        z = lambda: NDArray(torch.zeros_like(weight._data, dtype=torch.float32))
-        return (z(), z())
+        return _zeros(weight, 2, dtype=torch.float32)
 
     def _step(self, index, weight, grad, mean, var, w32=None):
-        self._update_count(index)
-        lr = self._get_lr(index)
-        wd = self._get_wd(index)
-        t = self._index_update_count[index]
-        tgt = w32 if w32 is not None else weight._data
-        g = _oo._lamb1(tgt, grad._data.float(), mean, var, self.beta1, self.beta2, self.epsilon, t,
-                       self.bias_correction, wd, self.rescale_grad, self._clip())
-        r1 = torch.linalg.vector_norm(tgt.float()).reshape(1)
-        r2 = torch.linalg.vector_norm(g).reshape(1)
-        lb = -1.0 if self.lower_bound is None else self.lower_bound
-        ub = -1.0 if self.upper_bound is None else self.upper_bound
-        _oo._lamb2(weight._data, g, r1, r2, lr, lb, ub, w32=w32)
+        lr, wd, t = self._begin(index)
+        target = weight._data if w32 is None else w32
+        direction = _oo._lamb1(target, grad._data.float(), mean, var, self.beta1, self.beta2, self.epsilon, t,
+                               self.bias_correction, wd, self.rescale_grad, self._clip())
+        w_norm = torch.linalg.vector_norm(target.float()).reshape(1)
+        d_norm = torch.linalg.vector_norm(direction).reshape(1)
+        bounds = [-1.0 if b is None else b for b in (self.lower_bound, self.upper_bound)]
+        _oo._lamb2(weight._data, direction, w_norm, d_norm, lr, bounds[0], bounds[1], w32=w32)
 
     def update(self, index, weight, grad, state):
-        mean, var = state
-        self._step(index, weight, grad, mean._data, var._data)
+        self._step(index, weight, grad, state[0]._data, state[1]._data)
 
     def update_multi_precision(self, index, weight, grad, state):
         """Multi-precision state = (fp32 master, (mean, var)) (the reference layout); lists of indices
@@ -595,348 +585,289 @@ class LAMB(Optimizer):
             for args in zip(index, weight, grad, state):
                 self.update_multi_precision(*args)
             return
-        if self._wants_master(weight):
-            w32, (mean, var) = state
-            self._step(index, weight, grad, mean._data, var._data, w32=w32._data)
-        else:
+        if not self._wants_master(weight):
             self.update(index, weight, grad, state)
+            return
+        master, (mean, var) = state
+        self._step(index, weight, grad, mean._data, var._data, w32=master._data)
 
 
 @register
-class DCASGD(Optimizer):
+class DCASGD(_Stepper):
+    """Delay-compensated async SGD (Zheng et al. 2016): the gradient is corrected by
+    ``lamda * g * g * (w - w_prev)``; state (momentum or None, previous weight)."""
+
     def __init__(self, momentum=0.0, lamda=0.04, **kwargs):
         super().__init__(**kwargs)
-        self.momentum = momentum
-        self.weight_previous = {}
-        self.lamda = lamda
+        self._hyper(momentum=momentum, lamda=lamda, weight_previous={})
 
     def create_state(self, index, weight):
-        if self.momentum == 0.0:
-            return (None, NDArray(weight._data.clone()))
-        return (NDArray(torch.zeros_like(weight._data)), NDArray(weight._data.clone()))
+        previous = NDArray(weight._data.clone())
+        return (_zeros(weight) if self.momentum != 0.0 else None, previous)
 
     @torch.no_grad()
     def update(self, index, weight, grad, state):
-        self._update_count(index)
-        lr = self._get_lr(index)
-        wd = self._get_wd(index)
-        g = grad._data * self.rescale_grad
-        if self.clip_gradient is not None:
-            g = torch.clamp(g, -self.clip_gradient, self.clip_gradient)
-        mom, previous_weight = state
+        lr, wd, _ = self._begin(index)
+        g = self._conditioned(grad)
+        mom, previous = state
         w = weight._data
-        delta = -lr * (g + wd * w + self.lamda * g * g * (w - previous_weight._data))
+        delta = -lr * (g + wd * w + self.lamda * g * g * (w - previous._data))
         if mom is not None:
-            mom._data.mul_(self.momentum).add_(delta)
-            delta = mom._data
-        previous_weight._data.copy_(w)
+            delta = mom._data.mul_(self.momentum).add_(delta)
+        previous._data.copy_(w)
         w.add_(delta)
 
 
 @register
-class NAG(Optimizer):
+class NAG(_Stepper):
+    """Nesterov accelerated gradient (momentum look-ahead); multi-precision like SGD."""
+
     def __init__(self, momentum=0.0, **kwargs):
         super().__init__(**kwargs)
-        self.momentum = momentum
+        self._hyper(momentum=momentum)
 
     def create_state_multi_precision(self, index, weight):
-        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
-            w32 = NDArray(weight._data.float())
-            return (self.create_state(index, w32), w32)
-        return self.create_state(index, weight)
+        return _master_then(self, weight, lambda w: self.create_state(index, w))
 
     def create_state(self, index, weight):
-        if self.momentum != 0.0:
-            return NDArray(torch.zeros_like(weight._data))
-        return None
+        return _zeros(weight) if self.momentum != 0.0 else None
 
-    def _upd(self, index, weight, grad, state, w32=None):
-        self._update_count(index)
-        lr = self._get_lr(index)
-        wd = self._get_wd(index)
-        if state is not None:
-            _oo._nag(weight._data, grad._data, state._data, lr, self.momentum, wd, self.rescale_grad,
-                     self._clip(), w32=w32)
-        else:
+    def _nesterov(self, index, weight, grad, mom, w32=None):
+        lr, wd, _ = self._begin(index)
+        if mom is None:
             _oo._sgd(weight._data, grad._data, lr, wd, self.rescale_grad, self._clip(), w32=w32)
+        else:
+            _oo._nag(weight._data, grad._data, mom._data, lr, self.momentum, wd, self.rescale_grad, self._clip(),
+                     w32=w32)
 
     def update(self, index, weight, grad, state):
-        self._upd(index, weight, grad, state)
+        self._nesterov(index, weight, grad, state)
 
     def update_multi_precision(self, index, weight, grad, state):
-        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
-            mom, w32 = state
-            self._upd(index, weight, NDArray(grad._data.float()), mom, w32=w32._data)
+        if self.multi_precision and _is_half(weight):
+            mom, master = state
+            self._nesterov(index, weight, NDArray(grad._data.float()), mom, w32=master._data)
         else:
             self.update(index, weight, grad, state)
 
 
 @register
-class SGLD(Optimizer):
+class SGLD(_Stepper):
+    """Stochastic gradient Langevin dynamics: half an SGD step plus N(0, lr) noise."""
+
     def create_state(self, index, weight):
         return None
 
     @torch.no_grad()
     def update(self, index, weight, grad, state):
-        self._update_count(index)
-        lr = self._get_lr(index)
-        wd = self._get_wd(index)
-        g = grad._data * self.rescale_grad
-        if self.clip_gradient is not None:
-            g = torch.clamp(g, -self.clip_gradient, self.clip_gradient)
+        lr, wd, _ = self._begin(index)
         w = weight._data
-        w.add_(-lr / 2 * (g + wd * w) + torch.randn_like(w) * math.sqrt(lr))
+        w.add_(-lr / 2 * (self._conditioned(grad) + wd * w) + torch.randn_like(w) * math.sqrt(lr))
 
 
 @register
 class ccSGD(SGD):
-    def __init__(self, *args, **kwargs):
-        super().__init__(*args, **kwargs)
+    """Deprecated alias of SGD kept for API compatibility."""
 
 
 @register
-class Adam(Optimizer):
+class Adam(_Stepper):
     """Adam (Kingma & Ba); bias correction folded into the learning rate like the reference."""
 
     def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8, lazy_update=True, **kwargs):
         super().__init__(learning_rate=learning_rate, **kwargs)
-        self.beta1 = beta1
-        self.beta2 = beta2
-        self.epsilon = epsilon
-        self.lazy_update = lazy_update
+        self._hyper(beta1=beta1, beta2=beta2, epsilon=epsilon, lazy_update=lazy_update)
 
     def create_state(self, index, weight):
-        return (NDArray(torch.zeros_like(weight._data)), NDArray(torch.zeros_like(weight._data)))
+        return _zeros(weight, 2)
 
     def update(self, index, weight, grad, state):
-        self._update_count(index)
-        lr = self._get_lr(index)
-        wd = self._get_wd(index)
-        t = self._index_update_count[index]
-        coef1 = 1. - self.beta1 ** t
-        coef2 = 1. - self.beta2 ** t
-        lr *= math.sqrt(coef2) / coef1
-        mean, var = state
+        lr, wd, t = self._begin(index)
+        lr *= math.sqrt(1. - self.beta2 ** t) / (1. - self.beta1 ** t)
+        mean, var = state[0]._data, state[1]._data
+        clip = self._clip()
         if self.lazy_update and _is_rsp(grad):
-            _lazy_adam_rows(weight._data, grad, mean._data, var._data, lr, self.beta1, self.beta2, self.epsilon, wd,
-                            self.rescale_grad, self._clip())
-            return
-        _oo.adam_update(weight._data, grad._data, mean._data, var._data, lr=lr, beta1=self.beta1,
-                        beta2=self.beta2, epsilon=self.epsilon, wd=wd, rescale_grad=self.rescale_grad,
-                        clip_gradient=self._clip())
+            _lazy_adam_rows(weight._data, grad, mean, var, lr, self.beta1, self.beta2, self.epsilon, wd,
+                            self.rescale_grad, clip)
+        else:
+            _oo.adam_update(weight._data, grad._data, mean, var, lr=lr, beta1=self.beta1, beta2=self.beta2,
+                            epsilon=self.epsilon, wd=wd, rescale_grad=self.rescale_grad, clip_gradient=clip)
 
 
 @register
-class AdamW(Optimizer):
-    """Adam with decoupled weight decay (contrib adamw_update)."""
+class AdamW(_Stepper):
+    """Adam with decoupled weight decay (contrib adamw_update); mp state = (master, mean, var)."""
 
     def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8, correct_bias=True, **kwargs):
         super().__init__(learning_rate=learning_rate, **kwargs)
-        self.beta1 = beta1
-        self.beta2 = beta2
-        self.epsilon = epsilon
-        self.correct_bias = correct_bias
+        self._hyper(beta1=beta1, beta2=beta2, epsilon=epsilon, correct_bias=correct_bias)
 
     def create_state(self, index, weight):
-        z = lambda: NDArray(torch.zeros_like(weight._data, dtype=torch.float32))
-        return (z(), z())
+        return _zeros(weight, 2, dtype=torch.float32)
 
     def create_state_multi_precision(self, index, weight):
-        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
-            w32 = NDArray(weight._data.float())
-            return (w32,) + self.create_state(index, w32)
+        if self.multi_precision and _is_half(weight):
+            master = NDArray(weight._data.float())
+            return (master,) + self.create_state(index, master)
         return self.create_state(index, weight)
 
-    def _upd(self, index, weight, grad, mean, var, w32=None):
-        self._update_count(index)
-        lr = self._get_lr(index)
-        wd = self._get_wd(index)
-        t = self._index_update_count[index]
+    def _decoupled(self, index, weight, grad, mean, var, w32=None):
+        lr, wd, t = self._begin(index)
         if self.correct_bias:
             lr *= math.sqrt(1. - self.beta2 ** t) / (1. - self.beta1 ** t)
         _oo._adamw(weight._data, grad._data.float(), mean._data, var._data, self.rescale_grad, lr,
-                   self.beta1, self.beta2, self.epsilon, wd, 1.0,
-                   self._clip(), w32=w32)
+                   self.beta1, self.beta2, self.epsilon, wd, 1.0, self._clip(), w32=w32)
 
     def update(self, index, weight, grad, state):
-        self._upd(index, weight, grad, state[0], state[1])
+        self._decoupled(index, weight, grad, *state)
 
     def update_multi_precision(self, index, weight, grad, state):
-        if self.multi_precision and weight._data.dtype in (torch.float16, torch.bfloat16):
-            w32, mean, var = state
-            self._upd(index, weight, grad, mean, var, w32=w32._data)
+        if self.multi_precision and _is_half(weight):
+            master, mean, var = state
+            self._decoupled(index, weight, grad, mean, var, w32=master._data)
         else:
             self.update(index, weight, grad, state)
 
 
 @register
-class AdaGrad(Optimizer):
+class AdaGrad(_Stepper):
+    """AdaGrad: per-element learning rate ``lr / sqrt(sum g^2 + eps)``."""
+
     def __init__(self, eps=1e-7, **kwargs):
         super().__init__(**kwargs)
-        self.float_stable_eps = eps
+        self._hyper(float_stable_eps=eps)
 
     def create_state(self, index, weight):
-        return NDArray(torch.zeros_like(weight._data))
+        return _zeros(weight)
 
     @torch.no_grad()
     def update(self, index, weight, grad, state):
-        self._update_count(index)
-        lr = self._get_lr(index)
-        wd = self._get_wd(index)
-        g = grad._data * self.rescale_grad
-        if self.clip_gradient is not None:
-            g = torch.clamp(g, -self.clip_gradient, self.clip_gradient)
-        h = state._data
-        h.add_(g * g)
+        lr, wd, _ = self._begin(index)
+        g = self._conditioned(grad)
+        history = state._data.add_(g * g)
         w = weight._data
-        w.add_(-lr * (g / torch.sqrt(h + self.float_stable_eps) + wd * w))
+        w.add_(-lr * (g / torch.sqrt(history + self.float_stable_eps) + wd * w))
 
 
 @register
-class RMSProp(Optimizer):
+class RMSProp(_Stepper):
+    """RMSProp (Tieleman & Hinton) and, with ``centered``, the Graves 2013 variant."""
+
     def __init__(self, learning_rate=0.001, gamma1=0.9, gamma2=0.9, epsilon=1e-8, centered=False,
                  clip_weights=None, **kwargs):
         super().__init__(learning_rate=learning_rate, **kwargs)
-        self.gamma1 = gamma1
-        self.gamma2 = gamma2
-        self.centered = centered
-        self.epsilon = epsilon
-        self.clip_weights = clip_weights
+        self._hyper(gamma1=gamma1, gamma2=gamma2, centered=centered, epsilon=epsilon, clip_weights=clip_weights)
 
     def create_state(self, index, weight):
-        z = lambda: NDArray(torch.zeros_like(weight._data))
-        if self.centered:
-            return (z(), z(), z())
-        return (z(),)
+        return _zeros(weight, 3) if self.centered else (_zeros(weight),)
 
     def update(self, index, weight, grad, state):
-        self._update_count(index)
-        lr = self._get_lr(index)
-        wd = self._get_wd(index)
-        cw = -1.0 if self.clip_weights is None else self.clip_weights
-        if not self.centered:
-            _oo.rmsprop_update(weight._data, grad._data, state[0]._data, lr=lr, gamma1=self.gamma1,
-                               epsilon=self.epsilon, wd=wd, rescale_grad=self.rescale_grad,
-                               clip_gradient=self._clip(), clip_weights=cw)
+        lr, wd, _ = self._begin(index)
+        common = dict(lr=lr, gamma1=self.gamma1, epsilon=self.epsilon, wd=wd, rescale_grad=self.rescale_grad,
+                      clip_gradient=self._clip(), clip_weights=-1.0 if self.clip_weights is None else self.clip_weights)
+        tensors = [s._data for s in state]
+        if self.centered:
+            _oo.rmspropalex_update(weight._data, grad._data, *tensors, gamma2=self.gamma2, **common)
         else:
-            n, g, delta = state
-            _oo.rmspropalex_update(weight._data, grad._data, n._data, g._data, delta._data, lr=lr,
-                                   gamma1=self.gamma1, gamma2=self.gamma2, epsilon=self.epsilon, wd=wd,
-                                   rescale_grad=self.rescale_grad, clip_gradient=self._clip(), clip_weights=cw)
+            _oo.rmsprop_update(weight._data, grad._data, tensors[0], **common)
 
 
 @register
-class AdaDelta(Optimizer):
+class AdaDelta(_Stepper):
+    """AdaDelta (Zeiler 2012): running averages of g^2 and of the squared steps."""
+
     def __init__(self, rho=0.90, epsilon=1e-5, **kwargs):
         super().__init__(**kwargs)
-        self.rho = rho
-        self.epsilon = epsilon
+        self._hyper(rho=rho, epsilon=epsilon)
 
     def create_state(self, index, weight):
-        return (NDArray(torch.zeros_like(weight._data)), NDArray(torch.zeros_like(weight._data)))
+        return _zeros(weight, 2)
 
     @torch.no_grad()
     def update(self, index, weight, grad, state):
-        self._update_count(index)
-        wd = self._get_wd(index)
-        g = grad._data * self.rescale_grad
-        if self.clip_gradient is not None:
-            g = torch.clamp(g, -self.clip_gradient, self.clip_gradient)
-        acc_g, acc_delta = state
-        acc_g._data.mul_(self.rho).add_((1. - self.rho) * g * g)
-        current_delta = torch.sqrt(acc_delta._data + self.epsilon) / torch.sqrt(acc_g._data + self.epsilon) * g
-        acc_delta._data.mul_(self.rho).add_((1. - self.rho) * current_delta * current_delta)
-        weight._data.sub_(current_delta + wd * weight._data)
+        _lr, wd, _ = self._begin(index)
+        g = self._conditioned(grad)
+        sq_grad, sq_step = state[0]._data, state[1]._data
+        keep = self.rho
+        sq_grad.mul_(keep).add_((1. - keep) * g * g)
+        step = torch.sqrt(sq_step + self.epsilon) / torch.sqrt(sq_grad + self.epsilon) * g
+        sq_step.mul_(keep).add_((1. - keep) * step * step)
+        weight._data.sub_(step + wd * weight._data)
 
 
 @register
-class Ftrl(Optimizer):
+class Ftrl(_Stepper):
+    """FTRL-proximal (McMahan et al. 2013); state (z, n)."""
+
     def __init__(self, lamda1=0.01, learning_rate=0.1, beta=1, **kwargs):
         super().__init__(learning_rate=learning_rate, **kwargs)
-        self.lamda1 = lamda1
-        self.beta = beta
+        self._hyper(lamda1=lamda1, beta=beta)
 
     def create_state(self, index, weight):
-        return (NDArray(torch.zeros_like(weight._data)), NDArray(torch.zeros_like(weight._data)))
+        return _zeros(weight, 2)
 
     def update(self, index, weight, grad, state):
-        self._update_count(index)
-        wd = self._get_wd(index)
-        lr = self._get_lr(index)
-        z, n = state
-        _oo.ftrl_update(weight._data, grad._data, z._data, n._data, lr=lr, lamda1=self.lamda1, beta=self.beta,
-                        wd=wd, rescale_grad=self.rescale_grad, clip_gradient=self._clip())
+        lr, wd, _ = self._begin(index)
+        _oo.ftrl_update(weight._data, grad._data, state[0]._data, state[1]._data, lr=lr, lamda1=self.lamda1,
+                        beta=self.beta, wd=wd, rescale_grad=self.rescale_grad, clip_gradient=self._clip())
 
 
 @register
-class Adamax(Optimizer):
+class Adamax(_Stepper):
+    """AdaMax (Adam with the infinity norm): ``u = max(beta2 * u, |g|)``."""
+
     def __init__(self, learning_rate=0.002, beta1=0.9, beta2=0.999, **kwargs):
         super().__init__(learning_rate=learning_rate, **kwargs)
-        self.beta1 = beta1
-        self.beta2 = beta2
+        self._hyper(beta1=beta1, beta2=beta2)
 
     def create_state(self, index, weight):
-        return (NDArray(torch.zeros_like(weight._data)), NDArray(torch.zeros_like(weight._data)))
+        return _zeros(weight, 2)
 
     @torch.no_grad()
     def update(self, index, weight, grad, state):
-        self._update_count(index)
-        lr = self._get_lr(index)
-        wd = self._get_wd(index)
-        t = self._index_update_count[index]
-        lr /= (1. - self.beta1 ** t)
-        g = grad._data * self.rescale_grad + wd * weight._data
-        if self.clip_gradient is not None:
-            g = torch.clamp(g, -self.clip_gradient, self.clip_gradient)
-        m_t, u_t = state
-        m_t._data.mul_(self.beta1).add_((1. - self.beta1) * g)
-        u_t._data.copy_(torch.maximum(self.beta2 * u_t._data, torch.abs(g)))
-        weight._data.sub_(lr * m_t._data / u_t._data)
+        lr, wd, t = self._begin(index)
+        g = self._conditioned(grad, decay_with=weight, wd=wd)
+        first, inf_norm = state[0]._data, state[1]._data
+        first.mul_(self.beta1).add_((1. - self.beta1) * g)
+        inf_norm.copy_(torch.maximum(self.beta2 * inf_norm, torch.abs(g)))
+        weight._data.sub_(lr / (1. - self.beta1 ** t) * first / inf_norm)
 
 
 @register
-class Nadam(Optimizer):
+class Nadam(_Stepper):
+    """Nesterov Adam (Dozat 2016) with the momentum schedule ``beta1 (1 - 0.5 * 0.96^(t * decay))``."""
+
     def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8, schedule_decay=0.004, **kwargs):
         super().__init__(learning_rate=learning_rate, **kwargs)
-        self.beta1 = beta1
-        self.beta2 = beta2
-        self.epsilon = epsilon
-        self.schedule_decay = schedule_decay
-        self.m_schedule = 1.
+        self._hyper(beta1=beta1, beta2=beta2, epsilon=epsilon, schedule_decay=schedule_decay, m_schedule=1.)
 
     def create_state(self, index, weight):
-        return (NDArray(torch.zeros_like(weight._data)), NDArray(torch.zeros_like(weight._data)))
+        return _zeros(weight, 2)
+
+    def _mu(self, step):
+        return self.beta1 * (1. - 0.5 * pow(0.96, step * self.schedule_decay))
 
     @torch.no_grad()
     def update(self, index, weight, grad, state):
-        self._update_count(index)
-        lr = self._get_lr(index)
-        wd = self._get_wd(index)
-        t = self._index_update_count[index]
-        g = grad._data * self.rescale_grad + wd * weight._data
-        if self.clip_gradient is not None:
-            g = torch.clamp(g, -self.clip_gradient, self.clip_gradient)
-        momentum_t = self.beta1 * (1. - 0.5 * (pow(0.96, t * self.schedule_decay)))
-        momentum_t_1 = self.beta1 * (1. - 0.5 * (pow(0.96, (t + 1) * self.schedule_decay)))
-        self.m_schedule = self.m_schedule * momentum_t
-        m_schedule_next = self.m_schedule * momentum_t_1
-        m_t, v_t = state
-        m_t._data.mul_(self.beta1).add_((1. - self.beta1) * g)
-        v_t._data.mul_(self.beta2).add_((1. - self.beta2) * g * g)
-        grad_prime = g / (1. - self.m_schedule)
-        m_t_prime = m_t._data / (1. - m_schedule_next)
-        v_t_prime = v_t._data / (1. - pow(self.beta2, t))
-        m_t_bar = (1. - momentum_t) * grad_prime + momentum_t_1 * m_t_prime
-        weight._data.sub_(lr * m_t_bar / (torch.sqrt(v_t_prime) + self.epsilon))
+        lr, wd, t = self._begin(index)
+        g = self._conditioned(grad, decay_with=weight, wd=wd)
+        mu_now, mu_next = self._mu(t), self._mu(t + 1)
+        self.m_schedule *= mu_now
+        first, second = state[0]._data, state[1]._data
+        first.mul_(self.beta1).add_((1. - self.beta1) * g)
+        second.mul_(self.beta2).add_((1. - self.beta2) * g * g)
+        blended = (1. - mu_now) * g / (1. - self.m_schedule) + mu_next * first / (1. - self.m_schedule * mu_next)
+        second_hat = second / (1. - pow(self.beta2, t))
+        weight._data.sub_(lr * blended / (torch.sqrt(second_hat) + self.epsilon))
 
 
 @register
-class GroupAdaGrad(Optimizer):
+class GroupAdaGrad(_Stepper):
     """AdaGrad with one accumulator per row (python/mxnet/optimizer/contrib.py)."""
 
     def __init__(self, eps=1e-5, **kwargs):
         super().__init__(**kwargs)
-        self.float_stable_eps = eps
+        self._hyper(float_stable_eps=eps)
 
     def create_state(self, index, weight):
         assert len(weight.shape) == 2
@@ -944,24 +875,19 @@ class GroupAdaGrad(Optimizer):
 
     @torch.no_grad()
     def update(self, index, weight, grad, state):
-        self._update_count(index)
-        lr = self._get_lr(index)
-        wd = self._get_wd(index)
+        lr, wd, _ = self._begin(index)
         assert wd == 0, 'Weight decay is not supported for GroupAdaGrad'
-        g = grad._data * self.rescale_grad
-        if self.clip_gradient is not None:
-            g = torch.clamp(g, -self.clip_gradient, self.clip_gradient)
+        g = self._conditioned(grad)
         state._data.add_((g * g).mean(1, keepdim=True))
         weight._data.sub_(lr * g / torch.sqrt(state._data + self.float_stable_eps))
 
 
 @register
-class Test(Optimizer):
-    def __init__(self, **kwargs):
-        super().__init__(**kwargs)
+class Test(_Stepper):
+    """Test optimizer: ``weight += rescale_grad * grad``; the state mirrors the weight."""
 
     def create_state(self, index, weight):
-        return NDArray(torch.zeros_like(weight._data))
+        return _zeros(weight)
 
     @torch.no_grad()
     def update(self, index, weight, grad, state):
