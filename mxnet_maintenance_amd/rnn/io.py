@@ -23,7 +23,14 @@ def encode_sentences(sentences, vocab=None, invalid_label=-1, invalid_key='\n', 
     grow = vocab is None
     if grow:
         vocab = {invalid_key: invalid_label}
-    next_id = start_label
+    ids_from = [start_label]
+
+    def fresh_id():
+        if ids_from[0] == invalid_label:
+            ids_from[0] += 1
+        ids_from[0] += 1
+        return ids_from[0] - 1
+
     encoded = []
     for sent in sentences:
         ids = []
@@ -31,13 +38,10 @@ def encode_sentences(sentences, vocab=None, invalid_label=-1, invalid_key='\n', 
             if tok not in vocab:
                 if not grow and unknown_token is None:
                     raise AssertionError('Unknown token %s' % tok)
-                if not grow:
-                    tok = unknown_token
-                else:
-                    if next_id == invalid_label:
-                        next_id += 1
-                    vocab[tok] = next_id
-                    next_id += 1
+                if unknown_token is not None:
+                    tok = unknown_token            # unknown words share the unknown token's id
+                if tok not in vocab:
+                    vocab[tok] = fresh_id()
             ids.append(vocab[tok])
         encoded.append(ids)
     return encoded, vocab

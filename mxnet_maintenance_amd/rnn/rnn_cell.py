@@ -557,7 +557,7 @@ class ZoneoutCell(ModifierCell):
         cell = self.base_cell
         next_output, next_states = cell(inputs, states)
         mask = lambda p, like: symbol.Dropout(symbol.ones_like(like), p=p)   # noqa: E731
-        prev = self.prev_output if self.prev_output is not None else symbol.zeros((0, 0))
+        prev = self.prev_output if self.prev_output is not None else symbol.zeros_like(next_output)
         out = symbol.where(mask(self.zoneout_outputs, next_output), next_output, prev) \
             if self.zoneout_outputs != 0. else next_output
         if self.zoneout_states != 0.:
