@@ -16,6 +16,7 @@ HIP graph and replayed (``CachedOp``), removing per-kernel launch overhead.
 import copy
 import re
 import threading
+import os
 import warnings
 from collections import OrderedDict
 
@@ -636,7 +637,21 @@ class HybridBlock(Block):
                           .format(input='data', names=unused, name=self.name), stacklevel=4)
         self._data_names = [d.name for d in data]
         self._param_map = [(n, params[n]) for n in input_names if n in param_names]
-        self._cached_op = CachedOp(out, self._flags)
+        self._cached_op = CachedOp(self._fuse_for(out, args), self._flags)
+
+    @staticmethod
+    def _fuse_for(out, args):
+        """Pointwise fusion of the cached graph when it will run on a GPU (reference: the cached op's
+        FusePointwise, MXNET_USE_FUSION=1 by default): elementwise chains become one generated forward
+        and one generated backward kernel (ops/fused_ops.py)."""
+        if os.environ.get('MXNET_USE_FUSION', '1') == '0':
+            return out
+        flat = _flatten(args, 'input')[0]
+        ctx = next((a.context for a in flat if isinstance(a, NDArray)), None)
+        if ctx is None or ctx.device_type != 'gpu':
+            return out
+        from ..symbol import passes
+        return passes.fuse_pointwise(out)
 
     def _deferred_infer_shape(self, *args):
         try:
