@@ -1,10 +1,12 @@
 """contrib operators: deformable convolution (v1 / modulated v2), SyncBatchNorm, PixelShuffle helpers.
 
 Parity: src/operator/contrib/deformable_convolution*, modulated_deformable_convolution*,
-sync_batch_norm*.  Deformable sampling is expressed as one ``grid_sample`` per
-kernel tap (bilinear, zero outside, the reference's im2col semantics) followed
-by a grouped GEMM over the gathered columns; autograd gives the gradients
-w.r.t. data, offsets, masks and weights.
+sync_batch_norm*.  On the GPU deformable convolution runs the in-tree gfx950 kernels of
+src/kernels/deform_conv.hip: a deformable im2col (bilinear sampling at the offset taps, mask
+applied) feeding one batched grouped GEMM, and for the backward col2im (data gradient, fp32
+atomics) + col2im_coord (offset / mask gradients, register reductions) around the transposed
+GEMMs.  On the CPU the same math is one ``grid_sample`` per kernel tap (bilinear, zero outside)
+followed by the grouped GEMM, differentiated by autograd.
 """
 import torch
 import torch.nn.functional as F
@@ -44,7 +46,77 @@ def _deform_columns(x, offset, mask, kernel, stride, pad, dilate, dg):
     return torch.stack(cols, dim=2)                     # [N, C, K, Ho, Wo]
 
 
+class _DeformConvHip(torch.autograd.Function):
+    """Deformable conv on the HIP kernels: columns [N, g, C/g*K, L] -> GEMM with [g, O/g, C/g*K]."""
+
+    @staticmethod
+    def forward(ctx, x, offset, mask, weight, geom, num_group):
+        from . import kernels as _K
+        from .kernel_fns import _DT, _stream
+        lib = _K.lib()
+        N, C, H, W = x.shape
+        O = weight.shape[0]
+        Ho, Wo = geom[4], geom[5]
+        K = geom[6] * geom[7]
+        x, offset = x.contiguous(), offset.contiguous()
+        mask = mask.contiguous() if mask is not None else None
+        cols = torch.empty((N, C * K, Ho * Wo), dtype=x.dtype, device=x.device)
+        lib.deform_im2col(_DT[x.dtype], x.data_ptr(), offset.data_ptr(), 0 if mask is None else mask.data_ptr(),
+                          cols.data_ptr(), list(geom), _stream())
+        g = num_group
+        wmat = weight.reshape(g, O // g, (C // g) * K)
+        out = torch.matmul(wmat, cols.view(N, g, (C // g) * K, Ho * Wo))        # [N, g, O/g, L]
+        ctx.save_for_backward(x, offset, mask, weight, cols)
+        ctx.geom, ctx.g = geom, g
+        return out.reshape(N, O, Ho, Wo)
+
+    @staticmethod
+    def backward(ctx, gout):
+        from . import kernels as _K
+        from .kernel_fns import _DT, _stream
+        lib = _K.lib()
+        x, offset, mask, weight, cols = ctx.saved_tensors
+        geom, g = ctx.geom, ctx.g
+        N, C, H, W = x.shape
+        O = weight.shape[0]
+        L = geom[4] * geom[5]
+        K = geom[6] * geom[7]
+        go = gout.contiguous().view(N, g, O // g, L)
+        wmat = weight.reshape(g, O // g, (C // g) * K)
+        gw = torch.matmul(go.permute(1, 2, 0, 3).reshape(g, O // g, N * L),
+                          cols.view(N, g, (C // g) * K, L).permute(1, 0, 3, 2).reshape(g, N * L, (C // g) * K))
+        gcols = torch.matmul(wmat.transpose(1, 2), go).reshape(N, C * K, L).contiguous()
+        gx32 = torch.zeros(x.shape, dtype=torch.float32, device=x.device)
+        mptr = 0 if mask is None else mask.data_ptr()
+        lib.deform_col2im(_DT[x.dtype], offset.data_ptr(), mptr, gcols.data_ptr(), gx32.data_ptr(), list(geom),
+                          _stream())
+        goff = torch.empty_like(offset)
+        gmask = torch.empty_like(mask) if mask is not None else None
+        lib.deform_col2im_coord(_DT[x.dtype], x.data_ptr(), offset.data_ptr(), mptr, gcols.data_ptr(),
+                                goff.data_ptr(), 0 if gmask is None else gmask.data_ptr(), list(geom), _stream())
+        return gx32.to(x.dtype), goff, gmask, gw.reshape(weight.shape).to(weight.dtype), None, None
+
+
+def _deform_hip_ok(x, offset, mask, weight):
+    from . import kernels as _K
+    from .kernel_fns import _DT
+    ts = [t for t in (x, offset, mask, weight) if t is not None]
+    if not (x.is_cuda and all(t.is_cuda and t.dtype == x.dtype for t in ts) and x.dtype in _DT):
+        return False
+    if not _K.available():
+        # fail loudly on a GPU box without the extension instead of silently using the torch path
+        raise RuntimeError('deformable convolution: HIP kernel extension not available: %s' % _K.load_error())
+    return _K.enabled()
+
+
 def _deform_conv(x, offset, mask, weight, bias, kernel, stride, pad, dilate, num_group, dg):
+    if _deform_hip_ok(x, offset, mask, weight):
+        N, C, H, W = x.shape
+        Ho, Wo = offset.shape[2], offset.shape[3]
+        geom = (N, C, H, W, Ho, Wo, kernel[0], kernel[1], stride[0], stride[1], pad[0], pad[1], dilate[0],
+                dilate[1], dg)
+        out = _DeformConvHip.apply(x, offset, mask, weight, geom, num_group)
+        return out if bias is None else out + bias.view(1, -1, 1, 1).to(out.dtype)
     cols = _deform_columns(x, offset, mask, kernel, stride, pad, dilate, dg)
     N, C, K, Ho, Wo = cols.shape
     O = weight.shape[0]

@@ -124,6 +124,15 @@ void pool_nhwc_forward(int dtype, int is_max, const void* x, void* y, uint8_t* a
 void pool_nhwc_backward(int dtype, int is_max, const void* dy, const uint8_t* arg, void* dx, int N, int H, int W,
                         int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip,
                         hipStream_t s);
+void deform_im2col(int dtype, const void* x, const void* off, const void* msk, void* cols, int N, int C, int H, int W,
+                   int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int dg,
+                   hipStream_t s);
+void deform_col2im(int dtype, const void* off, const void* msk, const void* gcols, float* gx, int N, int C, int H,
+                   int W, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int dg,
+                   hipStream_t s);
+void deform_col2im_coord(int dtype, const void* x, const void* off, const void* msk, const void* gcols, void* goff,
+                         void* gmsk, int N, int C, int H, int W, int Ho, int Wo, int kh, int kw, int sh, int sw,
+                         int ph, int pw, int dh, int dw, int dg, hipStream_t s);
 void multibox_target(int dtype, const float* anchors, const float* labels, const void* cls_pred, float* loc_target,
                      float* loc_mask, float* cls_target, float* match_iou, int* match_gt, uint32_t* key, int B, int A,
                      int L, int W, int C, float thr, float ignore_label, float neg_ratio, float neg_thresh,
@@ -213,6 +222,29 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("slab_reduce", [](int odt, uintptr_t slab, int splits, int64_t n, uintptr_t out, int accum, uintptr_t s) {
     slab_reduce(odt, P<float>(slab), splits, n, P<void>(out), accum, S(s));
     check_launch("slab_reduce");
+  });
+  // deformable convolution (NCHW): geometry g = [N, C, H, W, Ho, Wo, kh, kw, sh, sw, ph, pw, dh, dw, dg]
+  m.def("deform_im2col", [](int dt, uintptr_t x, uintptr_t off, uintptr_t msk, uintptr_t cols, std::vector<int> g,
+                            uintptr_t s) {
+    if (g.size() != 15) throw std::runtime_error("deform_im2col: geometry needs 15 ints");
+    deform_im2col(dt, P<void>(x), P<void>(off), P<void>(msk), P<void>(cols), g[0], g[1], g[2], g[3], g[4], g[5], g[6],
+                  g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14], S(s));
+    check_launch("deform_im2col");
+  });
+  m.def("deform_col2im", [](int dt, uintptr_t off, uintptr_t msk, uintptr_t gcols, uintptr_t gx, std::vector<int> g,
+                            uintptr_t s) {
+    if (g.size() != 15) throw std::runtime_error("deform_col2im: geometry needs 15 ints");
+    deform_col2im(dt, P<void>(off), P<void>(msk), P<void>(gcols), P<float>(gx), g[0], g[1], g[2], g[3], g[4], g[5],
+                  g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14], S(s));
+    check_launch("deform_col2im");
+  });
+  m.def("deform_col2im_coord", [](int dt, uintptr_t x, uintptr_t off, uintptr_t msk, uintptr_t gcols, uintptr_t goff,
+                                  uintptr_t gmsk, std::vector<int> g, uintptr_t s) {
+    if (g.size() != 15) throw std::runtime_error("deform_col2im_coord: geometry needs 15 ints");
+    deform_col2im_coord(dt, P<void>(x), P<void>(off), P<void>(msk), P<void>(gcols), P<void>(goff), P<void>(gmsk),
+                        g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14],
+                        S(s));
+    check_launch("deform_col2im_coord");
   });
   m.def("multibox_target", [](int dt, uintptr_t anchors, uintptr_t labels, uintptr_t cls_pred, uintptr_t loc_target,
                               uintptr_t loc_mask, uintptr_t cls_target, uintptr_t match_iou, uintptr_t match_gt,

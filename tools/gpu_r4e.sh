@@ -1,4 +1,4 @@
-# round-4: graph-captured RCCL bucket all-reduce test (deterministic), full GPU test suite
+# round-4: graph-captured RCCL bucket all-reduce test, fused fwd/bwd kernels, full GPU suite, bench
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() {
@@ -11,4 +11,6 @@ step() {
 }
 PYT="python -u -m pytest -v --timeout 300 --timeout-method thread -p no:cacheprovider"
 step r4e_dist_tests.log 300 $PYT tests/test_distributed_gpu.py
-step r4e_gpu_all.log 900 $PYT -m gpu tests -x
+step r4e_fused.log 300 $PYT -m gpu tests/test_graph_passes.py
+step r4e_gpu_all.log 900 $PYT -m gpu tests
+step r4e_bench.log 400 python -u bench.py --steps 30 --warmup 10
