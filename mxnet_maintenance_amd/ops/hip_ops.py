@@ -87,6 +87,14 @@ _NCHW_VIA_NHWC = os.environ.get('MXAMD_NCHW_VIA_NHWC', '1') == '1'
 
 def conv(data, weight, bias, stride, pad, dilate, groups, channel_last):
     nsp = data.dim() - 2
+    if groups > 1 and nsp == 2 and _use_hip(data):
+        # depthwise (MobileNet): in-tree NHWC kernels, NCHW shapes through channels-last views
+        from .conv_dw import dw_ok, ConvDwNHWC
+        xl = data if channel_last else (_as_nhwc_view(data) if _nchw_on_hip(data) else None)
+        if xl is not None and dw_ok(xl, weight, groups, dilate):
+            rs = tuple(weight.shape[1:3]) if channel_last else tuple(weight.shape[2:4])
+            y = ConvDwNHWC.apply(xl, weight, bias, rs, tuple(stride), tuple(pad), tuple(dilate))
+            return y if channel_last else y.permute(0, 3, 1, 2)
     if not channel_last and nsp == 2 and _nchw_on_hip(data):
         # NCHW API, channels-last execution: activations stay NHWC in memory between HIP kernels
         # (NCHW-shaped permuted views), so the default layout runs on the same MFMA kernels

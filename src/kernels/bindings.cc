@@ -133,6 +133,10 @@ void deform_col2im(int dtype, const void* off, const void* msk, const void* gcol
 void deform_col2im_coord(int dtype, const void* x, const void* off, const void* msk, const void* gcols, void* goff,
                          void* gmsk, int N, int C, int H, int W, int Ho, int Wo, int kh, int kw, int sh, int sw,
                          int ph, int pw, int dh, int dw, int dg, hipStream_t s);
+void conv_dw_fwd(int dtype, const void* x, const void* wt, const float* bias, void* y, const int* gm, hipStream_t s);
+void conv_dw_dgrad(int dtype, const void* dy, const void* wt, void* dx, const int* gm, hipStream_t s);
+void conv_dw_wgrad(int dtype, const void* x, const void* dy, float* slab, int nslice, int out_dtype, void* out,
+                   int accum, const int* gm, hipStream_t s);
 void multibox_target(int dtype, const float* anchors, const float* labels, const void* cls_pred, float* loc_target,
                      float* loc_mask, float* cls_target, float* match_iou, int* match_gt, uint32_t* key, int B, int A,
                      int L, int W, int C, float thr, float ignore_label, float neg_ratio, float neg_thresh,
@@ -245,6 +249,24 @@ PYBIND11_MODULE(_hip_kernels, m) {
                         g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14],
                         S(s));
     check_launch("deform_col2im_coord");
+  });
+  // depthwise NHWC conv; geometry g = [N, H, W, C, Ho, Wo, R, S, sh, sw, ph, pw, dh, dw]; wt = [R*S][C]
+  m.def("conv_dw_fwd", [](int dt, uintptr_t x, uintptr_t wt, uintptr_t bias, uintptr_t y, std::vector<int> g,
+                          uintptr_t s) {
+    if (g.size() != 14) throw std::runtime_error("conv_dw_fwd: geometry needs 14 ints");
+    conv_dw_fwd(dt, P<void>(x), P<void>(wt), P<float>(bias), P<void>(y), g.data(), S(s));
+    check_launch("conv_dw_fwd");
+  });
+  m.def("conv_dw_dgrad", [](int dt, uintptr_t dy, uintptr_t wt, uintptr_t dx, std::vector<int> g, uintptr_t s) {
+    if (g.size() != 14) throw std::runtime_error("conv_dw_dgrad: geometry needs 14 ints");
+    conv_dw_dgrad(dt, P<void>(dy), P<void>(wt), P<void>(dx), g.data(), S(s));
+    check_launch("conv_dw_dgrad");
+  });
+  m.def("conv_dw_wgrad", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t slab, int nslice, int out_dt, uintptr_t out,
+                            int accum, std::vector<int> g, uintptr_t s) {
+    if (g.size() != 14) throw std::runtime_error("conv_dw_wgrad: geometry needs 14 ints");
+    conv_dw_wgrad(dt, P<void>(x), P<void>(dy), P<float>(slab), nslice, out_dt, P<void>(out), accum, g.data(), S(s));
+    check_launch("conv_dw_wgrad");
   });
   m.def("multibox_target", [](int dt, uintptr_t anchors, uintptr_t labels, uintptr_t cls_pred, uintptr_t loc_target,
                               uintptr_t loc_mask, uintptr_t cls_target, uintptr_t match_iou, uintptr_t match_gt,
