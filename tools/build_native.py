@@ -104,15 +104,35 @@ def build_hip(jobs):
     return out
 
 
+def build_capi(jobs):
+    """``libmxamd_predict.so``: the C predict API (src/capi), a C ABI over an embedded CPython."""
+    import sysconfig
+    srcs = sorted(glob.glob(os.path.join(ROOT, 'src', 'capi', '*.cc')))
+    if not srcs:
+        return None
+    os.makedirs(LIB, exist_ok=True)
+    out = os.path.join(LIB, 'libmxamd_predict.so')
+    if not _newer(srcs, out):
+        return out
+    inc = sysconfig.get_paths()['include']
+    libdir = sysconfig.get_config_var('LIBDIR')
+    ver = sysconfig.get_config_var('LDVERSION') or sysconfig.get_python_version()
+    _run(['g++', '-O2', '-fPIC', '-shared', '-std=c++17', '-fvisibility=hidden', '-I' + inc] + srcs +
+         ['-o', out, '-L' + libdir, '-lpython' + ver, '-ldl', '-Wl,-rpath,' + libdir])
+    return out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument('--only', choices=['native', 'hip'], default=None)
+    ap.add_argument('--only', choices=['native', 'hip', 'capi'], default=None)
     ap.add_argument('-j', type=int, default=min(8, os.cpu_count() or 4))
     a = ap.parse_args(argv)
     if a.only in (None, 'native'):
         print('built', build_native(a.j))
     if a.only in (None, 'hip'):
         print('built', build_hip(a.j))
+    if a.only in (None, 'capi'):
+        print('built', build_capi(a.j))
 
 
 if __name__ == '__main__':
