@@ -26,7 +26,8 @@ import threading
 from contextlib import contextmanager
 
 __all__ = ['bulk', 'set_bulk_size', 'get', 'push', 'push_device', 'stream_wait_var', 'new_var', 'wait_for_var',
-           'wait_all', 'native_available', 'Engine', 'debug_access', 'race_violations', 'var_of']
+           'wait_all', 'native_available', 'Engine', 'debug_access', 'race_violations', 'var_of', 'copy_stream',
+           'host_to_device', 'wait_host_reads']
 
 _engine = None
 _lock = threading.Lock()
@@ -118,8 +119,48 @@ def new_var(name=''):
 
 def push(fn, const_vars=(), mutable_vars=(), priority=0, name=''):
     """Schedule ``fn()`` after all writers of ``const_vars`` and all users of
-    ``mutable_vars`` pushed before it have finished."""
+    ``mutable_vars`` pushed before it have finished.  Inside ``bulk(n)`` (n > 1) host ops are
+    gathered and pushed as one engine op per ``n`` ops (see ``set_bulk_size``)."""
+    if _bulk_size > 1 and _bulking.active:
+        _bulking.add(fn, const_vars, mutable_vars, priority, name)
+        return
     get().push(fn, list(const_vars), list(mutable_vars), priority, name)
+
+
+class _Bulk(threading.local):
+    """Host ops gathered by ``bulk``: flushed as ONE engine op (the reference's bulk execution,
+    threaded_engine.h BulkAppend / BulkFlush: fewer scheduling round trips for chains of small ops).
+    The bulk op reads the union of the gathered reads and writes the union of the writes; the
+    functions run in push order, so their mutual dependencies are respected."""
+
+    def __init__(self):
+        self.active = False
+        self.ops = []
+
+    def add(self, fn, const_vars, mutable_vars, priority, name):
+        self.ops.append((fn, list(const_vars), list(mutable_vars), priority, name))
+        if len(self.ops) >= _bulk_size:
+            self.flush()
+
+    def flush(self):
+        if not self.ops:
+            return
+        ops, self.ops = self.ops, []
+        writes = []
+        for _, _, m, _, _ in ops:
+            writes.extend(v for v in m if all(v is not w for w in writes))
+        reads = []
+        for _, c, _, _, _ in ops:
+            reads.extend(v for v in c if all(v is not w for w in writes + reads))
+        fns = [op[0] for op in ops]
+
+        def run_bulk():
+            for f in fns:
+                f()
+        get().push(run_bulk, reads, writes, max(op[3] for op in ops), 'bulk[%d]' % len(fns))
+
+
+_bulking = _Bulk()
 
 
 def _stream_of(stream):
@@ -260,9 +301,10 @@ def rethrow_all():
 
 
 def set_bulk_size(size):
-    """Set the op bulking size; returns the previous value.  Device work is
-    already batched on the HIP stream (and HIP graphs), so this only records
-    the value for API parity."""
+    """Set the op bulking size (MXNET_EXEC_BULK_EXEC_* in the reference); returns the previous
+    value.  Inside ``bulk(size)`` host ops pushed through ``push`` are grouped ``size`` at a time
+    into single engine ops.  Device work needs no bulking here: it is already batched on the HIP
+    stream, and whole steps are captured into HIP graphs (gluon.GraphStep)."""
     global _bulk_size
     prev = _bulk_size
     _bulk_size = int(size)
@@ -271,8 +313,91 @@ def set_bulk_size(size):
 
 @contextmanager
 def bulk(size):
+    """Group the host ops pushed in this block ``size`` at a time (flushed at exit)."""
     prev = set_bulk_size(size)
+    outer = _bulking.active
+    _bulking.active = True
     try:
         yield
     finally:
+        _bulking.flush()
+        _bulking.active = outer
         set_bulk_size(prev)
+
+
+# ------------------------------------------------------------------ host <-> device transfers
+# Reference: CopyFromTo pushed to the ThreadedEnginePerDevice copy workers / streams
+# (src/ndarray/ndarray.cc, src/engine/threaded_engine_perdevice.cc:47,95).  A host -> GPU copy is
+# an engine device op on the GPU's dedicated copy stream, reading from pinned memory; the
+# consumer stream waits for it with a HIP event (stream_wait_var), so the copy overlaps whatever
+# compute is still queued and the host never blocks on the GPU.
+_COPY_STREAMS = {}
+_ASYNC_MIN_BYTES = int(os.environ.get('MXAMD_ASYNC_COPY_MIN_BYTES', str(64 << 10)))
+
+# pinned host ranges we do not own with a pending device read: (base, nbytes, engine var of the copy)
+_HOST_READS = []
+_HOST_READS_MAX = 256
+
+
+def copy_stream(dev):
+    """The dedicated H2D copy stream of device ``dev`` (a torch.device)."""
+    import torch
+    s = _COPY_STREAMS.get(dev)
+    if s is None:
+        s = _COPY_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def _note_host_read(src, var):
+    _HOST_READS.append((src.data_ptr(), src.numel() * src.element_size(), var))
+    if len(_HOST_READS) > _HOST_READS_MAX:
+        wait_for_var(_HOST_READS.pop(0)[2])
+
+
+def wait_host_reads(ptr, nbytes):
+    """Block until every pending H2D copy reading ``[ptr, ptr + nbytes)`` has finished (producers
+    that recycle pinned buffers call this before overwriting one)."""
+    keep = []
+    for base, n, var in _HOST_READS:
+        if base < ptr + nbytes and ptr < base + n:
+            wait_for_var(var)
+        else:
+            keep.append((base, n, var))
+    _HOST_READS[:] = keep
+
+
+def host_to_device(src, dev, out=None, var=None, name='h2d'):
+    """Copy host tensor ``src`` to GPU ``dev`` as an engine device op on the copy stream.
+
+    Returns the device tensor (``out`` when given -- the copy then first waits for the work already
+    queued on the consumer stream, which may still read ``out``) and its engine variable; the
+    caller's current stream on ``dev`` is made to wait for the copy on the GPU.  Pinned sources
+    the caller does not own are registered so their producer can ``wait_host_reads``."""
+    import torch
+    src = src.detach().contiguous()
+    borrowed = src.is_pinned()
+    if not borrowed:
+        src = src.pin_memory()
+    cs = copy_stream(dev)
+    consumer = torch.cuda.current_stream(dev)
+    if out is None:
+        # from the copy stream's pool: a block the compute stream freed may still be read by its
+        # queued kernels, and the copy stream does not wait for them
+        with torch.cuda.stream(cs):
+            out = torch.empty(src.shape, dtype=src.dtype, device=dev)
+    else:
+        cs.wait_stream(consumer)       # write-after-read on an existing destination
+    var = var if var is not None else new_var(name)
+    if borrowed:
+        _note_host_read(src, var)
+    push_device(lambda dst=out, s=src: dst.copy_(s, non_blocking=True), (), (var,), stream=cs, name=name)
+    stream_wait_var(var, consumer)
+    out.record_stream(consumer)
+    return out, var
+
+
+def async_copy_ok(src, dev):
+    """Whether a host -> device copy of ``src`` takes the engine path (big enough, not recorded)."""
+    import torch
+    return (dev.type == 'cuda' and src.device.type == 'cpu' and not (src.requires_grad and torch.is_grad_enabled())
+            and src.numel() * src.element_size() >= _ASYNC_MIN_BYTES)

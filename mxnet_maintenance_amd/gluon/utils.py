@@ -50,22 +50,10 @@ def split_data(data, num_slice, batch_axis=0, even_split=True):
     return slices
 
 
-_COPY_STREAMS = {}
-
-
-def _copy_stream(dev):
-    s = _COPY_STREAMS.get(dev)
-    if s is None:
-        s = _COPY_STREAMS[dev] = torch.cuda.Stream(device=dev)
-    return s
-
-
 def _upload(slices, ctx_list):
-    """Host -> GPU copies of the batch slices as engine device ops on each GPU's copy stream.
-
-    The copies are issued from pinned memory on a dedicated copy stream, so they overlap the
-    compute still queued on the consumer streams (the host runs ahead of the GPU); each consumer
-    stream then waits for its slice with a HIP event (engine.stream_wait_var) -- no host sync.
+    """Host -> GPU copies of the batch slices as engine device ops on each GPU's copy stream
+    (engine.host_to_device): they overlap the compute still queued on the consumer streams, which
+    wait for their slice with a HIP event -- no host sync.
     Parity: the reference's CopyFromTo pushed to the ThreadedEnginePerDevice copy workers
     (src/engine/threaded_engine_perdevice.cc, src/ndarray/ndarray.cc CopyFromTo)."""
     from .. import engine
@@ -77,54 +65,18 @@ def _upload(slices, ctx_list):
                 or (autograd.is_recording() and t.requires_grad)):
             outs.append(s.as_in_context(ctx))
             continue
-        src = t.detach().contiguous()
-        borrowed = src.is_pinned()      # pinned memory we do not own (e.g. an iterator's ring slot)
-        if not borrowed:
-            src = src.pin_memory()
-        dev = torch.device('cuda', ctx.device_id)
-        cs = _copy_stream(dev)
-        consumer = torch.cuda.current_stream(dev)
-        # allocate from the copy stream's pool: a block the compute stream freed may still be in use by
-        # kernels queued there, and the copy stream does not wait for them
-        with torch.cuda.stream(cs):
-            dst = torch.empty(src.shape, dtype=src.dtype, device=dev)
-        var = engine.new_var('h2d')
-        if borrowed:
-            _note_host_read(src, var)
-        engine.push_device(lambda dst=dst, src=src: dst.copy_(src, non_blocking=True), (), (var,), stream=cs,
-                           name='split_and_load_h2d')
-        engine.stream_wait_var(var, consumer)
-        dst.record_stream(consumer)     # freeing dst is ordered after the consumer's kernels
-        outs.append(NDArray(dst))
+        dst, var = engine.host_to_device(t, torch.device('cuda', ctx.device_id), name='split_and_load_h2d')
+        out = NDArray(dst)
+        out._engine_var = var
+        outs.append(out)
     return outs
 
 
-# pinned host ranges we do not own with a pending device read: (base, nbytes, engine var of the copy)
-_HOST_READS = []
-_HOST_READS_MAX = 256
-
-
-def _note_host_read(src, var):
-    _HOST_READS.append((src.data_ptr(), src.numel() * src.element_size(), var))
-    if len(_HOST_READS) > _HOST_READS_MAX:
-        from .. import engine
-        engine.wait_for_var(_HOST_READS.pop(0)[2])
-
-
 def wait_host_reads(ptr, nbytes):
-    """Block until every pending H2D copy reading ``[ptr, ptr + nbytes)`` has finished.
-
-    Producers that recycle pinned buffers (ImageRecordIter's ring) call this before
-    overwriting a slot, so an upload still queued on a copy stream never reads a torn
-    batch (the engine's wait on the copy's variable synchronises its HIP event)."""
+    """Block until every pending H2D copy reading ``[ptr, ptr + nbytes)`` has finished (see
+    engine.wait_host_reads)."""
     from .. import engine
-    keep = []
-    for base, n, var in _HOST_READS:
-        if base < ptr + nbytes and ptr < base + n:
-            engine.wait_for_var(var)
-        else:
-            keep.append((base, n, var))
-    _HOST_READS[:] = keep
+    engine.wait_host_reads(ptr, nbytes)
 
 
 def split_and_load(data, ctx_list, batch_axis=0, even_split=True):

@@ -50,10 +50,27 @@ def _wrap(t):
     return NDArray(t)
 
 
+
+def _engine_copy(src, dev):
+    """Host -> GPU copies of plain (non-recorded, big enough) tensors go through the dependency
+    engine's copy streams (engine.host_to_device) instead of a copy on the compute stream."""
+    if not torch.cuda.is_available() or _state.STATE.recording:
+        return False
+    from .. import engine
+    return type(src) is torch.Tensor and engine.async_copy_ok(src, torch.device(dev))
+
+
+def _async_upload(src, context):
+    from .. import engine
+    dst, var = engine.host_to_device(src, context.torch_device, name='as_in_context')
+    out = NDArray(dst)
+    out._engine_var = var
+    return out
+
 class NDArray:
     """An n-dimensional array on a :class:`Context`."""
     __slots__ = ('_data', '_grad', '_grad_req', '_stype', '__weakref__', '_fresh_grad', '_arena', '_host_ctx',
-                 '_exc', '_recorded', '_idt', '_hist')
+                 '_exc', '_recorded', '_idt', '_hist', '_engine_var')
     __array_priority__ = 1000.0
 
     def __init__(self, data, ctx=None, dtype=None, stype='default', writable=True):
@@ -212,6 +229,11 @@ class NDArray:
             engine.rethrow(box)
 
     def wait_to_read(self):
+        var = getattr(self, '_engine_var', None)
+        if var is not None:
+            # an array written by an engine op (e.g. an async host -> device copy): its variable
+            from .. import engine
+            engine.wait_for_var(var)
         if self._data.is_cuda:
             torch.cuda.current_stream(self._data.device).synchronize()
         self._rethrow()
@@ -267,11 +289,19 @@ class NDArray:
             src = self._data.detach() if not _state.STATE.recording else self._data
             if other.shape != self.shape:
                 raise MXNetError('copyto: shape mismatch %s vs %s' % (self.shape, other.shape))
-            with torch.no_grad():
-                other._data.copy_(src)
+            if _engine_copy(src, other._data.device) and other._data.is_contiguous() \
+                    and other._data.dtype == src.dtype:
+                from .. import engine
+                _, other._engine_var = engine.host_to_device(src, other._data.device, out=other._data,
+                                                             var=getattr(other, '_engine_var', None), name='copyto')
+            else:
+                with torch.no_grad():
+                    other._data.copy_(src)
             _share_failure(self, other)
             return other
         if isinstance(other, Context):
+            if _engine_copy(self._data, other.torch_device):
+                return _share_failure(self, _async_upload(self._data, other))
             return _share_failure(self, _tag_host_ctx(NDArray(self._data.to(other.torch_device, copy=True)), other))
         raise TypeError('copyto does not support type ' + str(type(other)))
 
@@ -285,6 +315,8 @@ class NDArray:
             out = NDArray(t.clone() if t.data_ptr() == self._data.data_ptr() else t)
             out._host_ctx = context
             return out
+        if _engine_copy(self._data, context.torch_device):
+            return _share_failure(self, _async_upload(self._data, context))
         return _tag_host_ctx(_invoke_unary(lambda t: t.to(context.torch_device), self), context)
 
     as_in_ctx = as_in_context
