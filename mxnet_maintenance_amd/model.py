@@ -27,113 +27,104 @@ __all__ = ['BatchEndParam', 'save_checkpoint', 'load_checkpoint', 'load_params',
 
 
 def _create_kvstore(kvstore, num_device, arg_params):
-    """Create the kvstore for Module/FeedForward; returns (kvstore or None, update_on_kvstore)."""
-    update_on_kvstore = bool(int(os.getenv('MXNET_UPDATE_ON_KVSTORE', '1')))
-    if kvstore is None:
-        kv = None
-    elif isinstance(kvstore, kvs.KVStoreBase):
-        kv = kvstore
-    elif isinstance(kvstore, str):
-        if num_device == 1 and 'dist' not in kvstore:
-            # no need for a kvstore with one device in one process
-            kv = None
-        else:
-            kv = kvs.create(kvstore)
-            if kvstore == 'local':
-                max_size = max(np.prod(param.shape) for param in arg_params.values()) if arg_params else 0
-                if max_size > 1024 * 1024 * 16:
-                    update_on_kvstore = False
-    else:
+    """(kvstore or None, update_on_kvstore) for Module / FeedForward.
+
+    One device in one process needs no store; 'local' stores keep the update on the workers when a
+    parameter exceeds 16M elements (the store would serialise a huge update); a store that cannot
+    run optimizers never updates on itself.  MXNET_UPDATE_ON_KVSTORE=0 disables store updates."""
+    if kvstore is not None and not isinstance(kvstore, (kvs.KVStoreBase, str)):
         raise TypeError('kvstore must be KVStore, str or None')
-    if kv is None:
-        update_on_kvstore = False
-    elif not kv.is_capable(kvs.KVStoreBase.OPTIMIZER):
-        update_on_kvstore = False
-    return (kv, update_on_kvstore)
+    if isinstance(kvstore, str):
+        kv = kvs.create(kvstore) if (num_device > 1 or 'dist' in kvstore) else None
+    else:
+        kv = kvstore
+    if kv is None or not kv.is_capable(kvs.KVStoreBase.OPTIMIZER):
+        return kv, False
+    on_store = bool(int(os.getenv('MXNET_UPDATE_ON_KVSTORE', '1')))
+    biggest = max((int(np.prod(p.shape)) for p in arg_params.values()), default=0) if arg_params else 0
+    if kvstore == 'local' and biggest > (16 << 20):
+        on_store = False
+    return kv, on_store
 
 
 def _initialize_kvstore(kvstore, param_arrays, arg_params, param_names, update_on_kvstore):
-    for idx, param_on_devs in enumerate(param_arrays):
-        name = param_names[idx]
-        if not update_on_kvstore or arg_params[name].stype != 'default':
-            kvstore.init(name, arg_params[name])
+    """Seed the store with every parameter; with store-side updates the device copies are
+    broadcast from it (sparse parameters are only initialised)."""
+    for name, replicas in zip(param_names, param_arrays):
+        value = arg_params[name]
+        if update_on_kvstore and value.stype == 'default':
+            kvstore.broadcast(name, value, out=replicas)
         else:
-            kvstore.broadcast(name, arg_params[name], out=param_on_devs)
+            kvstore.init(name, value)
 
 
 def _update_params_on_kvstore(param_arrays, grad_arrays, kvstore, param_names):
-    for index, pair in enumerate(zip(param_arrays, grad_arrays)):
-        arg_list, grad_list = pair
-        if grad_list[0] is None:
-            continue
-        name = param_names[index]
-        kvstore.push(name, grad_list, priority=-index)
-        kvstore.pull(name, arg_list, priority=-index)
+    """Store-side update: push each gradient set, pull the updated weights (priority = -index so
+    the first layers, needed first by the next forward, are served first)."""
+    for pos, (name, replicas, grads) in enumerate(zip(param_names, param_arrays, grad_arrays)):
+        if grads[0] is not None:
+            kvstore.push(name, grads, priority=-pos)
+            kvstore.pull(name, replicas, priority=-pos)
 
 
 def _update_params(param_arrays, grad_arrays, updater, num_device, kvstore=None, param_names=None):
-    updates = [[] for _ in range(num_device)]
-    for i, pair in enumerate(zip(param_arrays, grad_arrays)):
-        arg_list, grad_list = pair
-        if grad_list[0] is None:
+    """Worker-side update: optional gradient all-reduce through the store, then ONE aggregated
+    updater call per device (updater keys ``index * num_device + device``)."""
+    per_device = [([], [], []) for _ in range(num_device)]
+    for pos, (replicas, grads) in enumerate(zip(param_arrays, grad_arrays)):
+        if grads[0] is None:
             continue
-        index = i
         if kvstore:
-            name = param_names[index]
-            kvstore.pushpull(name, grad_list, grad_list, priority=-index)
-        for k, p in enumerate(zip(arg_list, grad_list)):
-            w, g = p
-            updates[k].append((index * num_device + k, g, w))
-    for dev_updates in updates:
-        if dev_updates:
-            i, g, w = zip(*dev_updates)
-            updater(list(i), list(g), list(w))
+            kvstore.pushpull(param_names[pos], grads, grads, priority=-pos)
+        for dev, (w, g) in enumerate(zip(replicas, grads)):
+            keys, gs, ws = per_device[dev]
+            keys.append(pos * num_device + dev)
+            gs.append(g)
+            ws.append(w)
+    for keys, gs, ws in per_device:
+        if keys:
+            updater(keys, gs, ws)
 
 
 def _multiple_callbacks(callbacks, *args, **kwargs):
-    if isinstance(callbacks, list):
-        for cb in callbacks:
-            cb(*args, **kwargs)
-        return
-    if callbacks:
-        callbacks(*args, **kwargs)
+    for cb in (callbacks if isinstance(callbacks, list) else [callbacks] if callbacks else []):
+        cb(*args, **kwargs)
 
 
 def save_checkpoint_symbol(prefix, symbol, remove_amp_cast=True):
+    """Write ``prefix-symbol.json`` (nothing for ``symbol=None``)."""
     if symbol is not None:
         symbol.save('%s-symbol.json' % prefix, remove_amp_cast=remove_amp_cast)
 
 
 def save_checkpoint(prefix, epoch, symbol, arg_params, aux_params, remove_amp_cast=True):
-    """Write ``prefix-symbol.json`` and ``prefix-%04d.params``."""
+    """Write ``prefix-symbol.json`` and ``prefix-%04d.params`` (``arg:`` / ``aux:`` keyed, host copies)."""
     save_checkpoint_symbol(prefix, symbol, remove_amp_cast)
-    save_dict = {('arg:%s' % k): v.as_in_context(cpu()) for k, v in arg_params.items()}
-    save_dict.update({('aux:%s' % k): v.as_in_context(cpu()) for k, v in aux_params.items()})
-    param_name = '%s-%04d.params' % (prefix, epoch)
-    nd.save(param_name, save_dict)
-    logging.info('Saved checkpoint to "%s"', param_name)
+    tagged = {}
+    for tag, table in (('arg', arg_params), ('aux', aux_params)):
+        tagged.update({'%s:%s' % (tag, k): v.as_in_context(cpu()) for k, v in table.items()})
+    path = '%s-%04d.params' % (prefix, epoch)
+    nd.save(path, tagged)
+    logging.info('Saved checkpoint to "%s"', path)
 
 
 def load_params(prefix, epoch):
-    save_dict = nd.load('%s-%04d.params' % (prefix, epoch))
-    arg_params, aux_params = {}, {}
-    if not save_dict:
-        logging.warning('Params file "%s" is empty', '%s-%04d.params' % (prefix, epoch))
-        return (arg_params, aux_params)
-    for k, v in save_dict.items():
-        tp, name = k.split(':', 1)
-        if tp == 'arg':
-            arg_params[name] = v
-        if tp == 'aux':
-            aux_params[name] = v
-    return (arg_params, aux_params)
+    """(arg_params, aux_params) from ``prefix-%04d.params``."""
+    path = '%s-%04d.params' % (prefix, epoch)
+    saved = nd.load(path)
+    tables = {'arg': {}, 'aux': {}}
+    if not saved:
+        logging.warning('Params file "%s" is empty', path)
+    for key, value in (saved or {}).items():
+        tag, name = key.split(':', 1)
+        if tag in tables:
+            tables[tag][name] = value
+    return tables['arg'], tables['aux']
 
 
 def load_checkpoint(prefix, epoch):
-    """Returns (symbol, arg_params, aux_params)."""
-    symbol = sym_mod.load('%s-symbol.json' % prefix)
-    arg_params, aux_params = load_params(prefix, epoch)
-    return (symbol, arg_params, aux_params)
+    """(symbol, arg_params, aux_params) of a checkpoint written by ``save_checkpoint``."""
+    return (sym_mod.load('%s-symbol.json' % prefix),) + load_params(prefix, epoch)
 
 
 class FeedForward:
