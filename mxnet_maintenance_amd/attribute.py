@@ -5,12 +5,18 @@ attributes to every symbol created inside; nested scopes merge outer and inner
 attributes (inner wins), and explicit attributes passed to a symbol win over
 both.
 """
+from collections import defaultdict
+
 from ._scope import _ThreadScope
 
 __all__ = ['AttrScope']
 
 
 class AttrScope(_ThreadScope):
+    # how many control-flow subgraphs were built under each name (symbol/contrib.py numbers them
+    # <name>0, <name>1, ... like the reference's _get_unique_subgraph_name)
+    _subgraph_names = defaultdict(int)
+
     def __init__(self, **kwargs):
         bad = [k for k, v in kwargs.items() if not isinstance(v, str)]
         if bad:

@@ -39,7 +39,30 @@ def _foreach_args(a):
             ['remain%d' % i for i in range(len(_names(a.get('remain_names', '[]'))))])
 
 
-@register('_foreach', arg_names=_foreach_args, num_outputs=_foreach_nout,
+def _foreach_infer(in_shapes, a):
+    """Shapes of unknown loop states / free inputs from the body graph's (partial) shape inference,
+    given the per-step slice shapes of the data (reference control_flow.cc ForeachShape)."""
+    from ..symbol import symbol as sym_mod
+    dn, sn, rn = _names(a.get('data_names', '[]')), _names(a.get('state_names', '[]')), \
+        _names(a.get('remain_names', '[]'))
+    names = dn + sn + rn
+    known = {}
+    for i, (name, shp) in enumerate(zip(names, in_shapes)):
+        if shp is None:
+            continue
+        known[name] = tuple(shp[1:]) if i < len(dn) else tuple(shp)
+    body = sym_mod.load_json(a['subgraph'])
+    args = body.list_arguments()
+    arg_shapes, _, _ = body.infer_shape_partial(**{k: v for k, v in known.items() if k in args})
+    inferred = dict(zip(args, arg_shapes or []))
+    fill = {}
+    for i, name in enumerate(names):
+        if in_shapes[i] is None and i >= len(dn) and inferred.get(name):
+            fill[i] = tuple(inferred[name])
+    return fill
+
+
+@register('_foreach', arg_names=_foreach_args, num_outputs=_foreach_nout, infer_params=_foreach_infer,
           params={'subgraph': ('str', ''), 'data_names': ('str', '[]'), 'state_names': ('str', '[]'),
                   'remain_names': ('str', '[]'), 'num_out_data': ('int', 1)})
 def foreach_op(*inputs, subgraph='', data_names='[]', state_names='[]', remain_names='[]', num_out_data=1):

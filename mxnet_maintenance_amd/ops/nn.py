@@ -1087,6 +1087,9 @@ def unpack_rnn_params(params, mode, num_layers, input_size, state_size, bidirect
             wr = ws[k][2:] if projection_size else []
             ws[k] = ws[k][:2] + [bi, bh] + wr
             k += 1
+    if off != params.numel():
+        # a wrong-size vector would hand empty / truncated views to the fused kernels (which crash)
+        raise ValueError('RNN: parameter vector has %d elements, the layer needs %d' % (params.numel(), off))
     return ws
 
 
@@ -1182,6 +1185,9 @@ def rnn(data, parameters, state, state_cell=None, sequence_length=None, state_si
             return (out, h, c) if state_outputs else out
         return (out, h) if state_outputs else out
     flat = [t for group in ws for t in group]
+    if any(int(x) == 0 for x in tuple(data.shape) + tuple(state.shape)):
+        # the fused torch kernels crash on empty inputs (e.g. a shape probe with an unknown dim)
+        raise MXNetError('RNN: empty input %s / state %s' % (tuple(data.shape), tuple(state.shape)))
     hsz = projection_size or state_size
     want = (num_layers * d, data.shape[1], hsz)
     if tuple(state.shape) != want or (mode == 'lstm' and state_cell is not None

@@ -40,6 +40,26 @@ def _unflat(leaves, fmt):
     return out, leaves
 
 
+def _subgraph_name(base):
+    """Unique subgraph name (reference symbol/contrib.py _get_unique_subgraph_name): nested inside
+    another subgraph it is prefixed ``outer$``; the n-th subgraph of one name gets suffix n."""
+    from ..attribute import AttrScope
+    outer = AttrScope.current._attr.get('__subgraph_name__', '')
+    if outer:
+        base = outer + '$' + base
+    AttrScope._subgraph_names[base] += 1
+    return base + str(AttrScope._subgraph_names[base] - 1)
+
+
+def _in_subgraph(base, build):
+    """Run ``build()`` (the Python function that creates a subgraph's symbols) under the subgraph's
+    unique name; returns (build's result, the name)."""
+    from ..attribute import AttrScope
+    name = _subgraph_name(base)
+    with AttrScope(__subgraph_name__=name):
+        return build(), name
+
+
 def _free_vars(g, exclude):
     from .symbol import Symbol
     out = []
@@ -59,7 +79,8 @@ def foreach(body, data, init_states, name='foreach'):
     states_l, states_fmt = _flat(init_states)
     d_ph = [var('%s_data%d' % (name, i)) for i in range(len(data_l))]
     s_ph = [var('%s_state%d' % (name, i)) for i in range(len(states_l))]
-    outs, new_states = body(_unflat(d_ph, data_fmt)[0], _unflat(s_ph, states_fmt)[0])
+    (outs, new_states), _ = _in_subgraph(name, lambda: body(_unflat(d_ph, data_fmt)[0],
+                                                            _unflat(s_ph, states_fmt)[0]))
     outs_l, outs_fmt = _flat(outs if outs is not None else [])
     new_l, new_fmt = _flat(new_states)
     if len(new_l) != len(states_l):
@@ -85,8 +106,8 @@ def while_loop(cond, func, loop_vars, max_iterations=None, name='while_loop'):
     ph = [var('%s_var%d' % (name, i)) for i in range(len(vars_l))]
     arg = _unflat(ph, vars_fmt)[0]
     as_args = isinstance(arg, list)
-    c = cond(*arg) if as_args else cond(arg)
-    outs, new_vars = func(*arg) if as_args else func(arg)
+    c, _ = _in_subgraph(name + '_cond', lambda: cond(*arg) if as_args else cond(arg))
+    (outs, new_vars), _ = _in_subgraph(name + '_func', lambda: func(*arg) if as_args else func(arg))
     outs_l, outs_fmt = _flat(outs if outs is not None else [])
     new_l, _ = _flat(new_vars)
     if len(new_l) != len(vars_l):
@@ -108,8 +129,9 @@ def while_loop(cond, func, loop_vars, max_iterations=None, name='while_loop'):
 def cond(pred, then_func, else_func, name='cond'):
     """Symbolic if/else: both branches are subgraphs over the free variables they use."""
     from .symbol import Group, _create
-    then_out = then_func()
-    else_out = else_func()
+    _subgraph_name(name + '_pred')          # the predicate is a subgraph of its own in the reference
+    then_out, _ = _in_subgraph(name + '_then', then_func)
+    else_out, _ = _in_subgraph(name + '_else', else_func)
     t_l, t_is_list = _as_list(then_out)
     e_l, _ = _as_list(else_out)
     if len(t_l) != len(e_l):

@@ -1094,7 +1094,7 @@ def _unify_init_shapes(order):
             n._parsed = None
 
 
-def _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what):
+def _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what, partial=False):
     """Init ops declared with 0 (unknown) dims, e.g. RNN ``begin_state`` via ``sym.zeros``.
 
     The reference fills those dims by backward shape inference; here the
@@ -1103,6 +1103,11 @@ def _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what):
     back into the node's ``shape`` attribute (so executors allocate it).
     """
     _unify_init_shapes(order)
+    loop_data = set()
+    for n in order:
+        if n.op == '_foreach':
+            ndata = len(json.loads(n.parsed().get('data_names') or '[]'))
+            loop_data.update(id(a) for a, _ in n.inputs[:ndata])
     zero_nodes = []
     zero_vars = []      # variables declared with unknown (0) dims, e.g. RNN begin_state(func=Variable)
     for n in order:
@@ -1111,7 +1116,9 @@ def _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what):
             if shp and any(int(d) <= 0 for d in shp):
                 shp = tuple(max(int(d), 0) for d in shp)
                 zero_nodes.append((n, tuple(int(d) for d in shp)))
-        elif n.op is None and n.name not in known_shapes and n.attrs.get('__shape__'):
+        elif n.op is None and n.name not in known_shapes and n.attrs.get('__shape__') and not (
+                partial and id(n) in loop_data):
+            # (the unknown sequence length of a foreach's data stays unknown in partial inference)
             shp = registry.parse_value('shape', n.attrs['__shape__'])
             if shp and any(int(d) == 0 for d in shp) and not all(int(d) == 0 for d in shp):
                 zero_vars.append((n, tuple(int(d) for d in shp)))
@@ -1255,7 +1262,7 @@ def infer_graph(sym, known_shapes, known_dtypes, what='shape', _resolve=True, pa
             if r is not None and len(r) and all(d > 0 for d in r):
                 known_shapes[name] = r
     if _resolve and what == 'shape' and known_shapes:
-        res = _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what)
+        res = _resolve_unknown_init_shapes(sym, order, known_shapes, known_dtypes, what, partial)
         if res is not None:
             return res
     shape = {}   # (id(node), idx) -> shape
