@@ -264,5 +264,24 @@ class _CAPI:
     def MXNotifyShutdown():  # noqa: N802
         return 0
 
+    @staticmethod
+    def MXNDArrayFromDLPack(dlpack, out):  # noqa: N802
+        """Wrap a ``DLManagedTensor*`` (the pointer inside a 'dltensor' capsule) as an NDArray; the
+        new array owns the tensor (its deleter runs when the array is freed)."""
+        import torch.utils.dlpack as _tdl
+        ptr = dlpack.value if isinstance(dlpack, _ctypes.c_void_p) else dlpack
+        new_capsule = _ctypes.pythonapi.PyCapsule_New
+        new_capsule.restype = _ctypes.py_object
+        new_capsule.argtypes = [_ctypes.c_void_p, _ctypes.c_char_p, _ctypes.c_void_p]
+        capsule = new_capsule(ptr, _DLTENSOR_NAME, None)
+        from .ndarray.ndarray import NDArray
+        arr = NDArray(_tdl.from_dlpack(capsule))
+        target = out._obj if hasattr(out, '_obj') else out
+        target.value = _new_handle(arr)
+        return 0
+
+
+_DLTENSOR_NAME = b'dltensor'     # capsule names must outlive the capsules
+
 
 _LIB = _CAPI()

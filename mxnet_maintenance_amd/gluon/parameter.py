@@ -358,22 +358,21 @@ class Parameter:
         if _state.STATE.recording:
             # inside autograd.record() the replica itself (the leaf whose gradient the trainer reads)
             return got
-        return [self._rows_view(a, row_id) for a in got] if isinstance(got, list) else self._rows_view(got, row_id)
+        for a in (got if isinstance(got, list) else [got]):
+            self._keep_rows(a, row_id)
+        return got
 
     @staticmethod
-    def _rows_view(arr, row_id):
-        """The requested rows of replica ``arr`` (others read as zero), as the reference's pulled
-        row_sparse copy holds only them."""
+    def _keep_rows(arr, row_id):
+        """Zero the rows of replica ``arr`` that were not pulled: like the reference's pulled row_sparse
+        copy it then holds only the requested rows (the kvstore keeps the full weight), and it stays the
+        parameter's own array, so gradients computed from it reach the trainer."""
         t = arr._data
         rows = row_id._data.to(device=t.device, dtype=torch.int64).reshape(-1)
-        keep = torch.zeros(t.shape[0], dtype=t.dtype, device=t.device)
-        keep[rows] = 1
-        view = NDArray((t * keep.reshape((-1,) + (1,) * (t.dim() - 1))).detach())
-        view._stype = 'row_sparse'
-        hctx = getattr(arr, '_host_ctx', None)
-        if hctx is not None:
-            view._host_ctx = hctx
-        return view
+        keep = torch.zeros(t.shape[0], dtype=torch.bool, device=t.device)
+        keep[rows] = True
+        with torch.no_grad():
+            t[~keep] = 0
 
     def row_sparse_data(self, row_id):
         """The rows ``row_id`` of a row_sparse parameter, on ``row_id``'s context."""

@@ -193,8 +193,9 @@ class KVStoreDistAsync(KVStoreBase):
     def num_workers(self):
         return self._world
 
-    def is_capable(self, capability):
-        if capability.lower() == self.OPTIMIZER:
+    @staticmethod
+    def is_capable(capability):
+        if capability.lower() == KVStoreBase.OPTIMIZER:
             return True
         raise ValueError('Unknown capability: {}'.format(capability))
 

@@ -54,7 +54,8 @@ class KVStoreBase:
     def set_optimizer(self, optimizer):
         raise NotImplementedError()
 
-    def is_capable(self, capability):
+    @staticmethod
+    def is_capable(capability):
         raise NotImplementedError()
 
     def save_optimizer_states(self, fname, dump_optimizer=False):
@@ -105,7 +106,8 @@ class TestStore(KVStoreBase):
         for o in out:
             o[:] = total.as_in_context(o.context)
 
-    def is_capable(self, capability):
+    @staticmethod
+    def is_capable(capability):
         if capability.lower() == KVStoreBase.OPTIMIZER:
             return False
         raise ValueError('Unknown capability: {}'.format(capability))
@@ -144,6 +146,7 @@ class KVStore(KVStoreBase):
         self._optimizer = None
         self._compression = None
         self._str_keys = {}
+        self._key_kind = None          # int or str: a store takes one kind of key (reference KVStore)
 
     # ---------------------------------------------------------------- basics
     @property
@@ -158,7 +161,8 @@ class KVStore(KVStoreBase):
     def num_workers(self):
         return dist.world_size()
 
-    def is_capable(self, capability):
+    @staticmethod
+    def is_capable(capability):
         if capability.lower() == KVStoreBase.OPTIMIZER:
             return True
         raise ValueError('Unknown capability: {}'.format(capability))
@@ -214,8 +218,22 @@ class KVStore(KVStoreBase):
                 off += n
 
     # ------------------------------------------------------------------- API
-    def init(self, key, value):
+    def _keys(self, key):
+        """``key`` as a list, checked against the store's key kind (all int or all str)."""
         keys = _as_list(key)
+        for k in keys:
+            kind = str if isinstance(k, str) else int
+            if not isinstance(k, (str, int, np.integer)):
+                raise MXNetError('kvstore keys must be int or str, got %s' % type(k).__name__)
+            if self._key_kind is None:
+                self._key_kind = kind
+            elif kind is not self._key_kind:
+                raise MXNetError('this kvstore uses %s keys; got the %s key %r'
+                                 % (self._key_kind.__name__, kind.__name__, k))
+        return keys
+
+    def init(self, key, value):
+        keys = self._keys(key)
         vals = value if isinstance(key, (list, tuple)) else [value]
         for k, v in zip(keys, vals):
             v0 = _as_list(v)[0]
@@ -225,7 +243,7 @@ class KVStore(KVStoreBase):
             self._store[k] = NDArray(t)
 
     def push(self, key, value, priority=0):
-        keys = _as_list(key)
+        keys = self._keys(key)
         vals = value if isinstance(key, (list, tuple)) else [value]
         merged = []
         with torch.no_grad():
@@ -237,7 +255,8 @@ class KVStore(KVStoreBase):
                     raise MXNetError('key %s has not been initialized' % str(k))
                 stored = self._store[k]
                 if self._updater is not None:
-                    self._updater(k if not isinstance(k, str) else self._str_key(k), NDArray(m), stored)
+                    # string-keyed stores hand the updater the string key, like the reference's str updater
+                    self._updater(k, NDArray(m), stored)
                 else:
                     stored._data.copy_(m.to(stored._data.device, stored._data.dtype))
 
@@ -248,8 +267,15 @@ class KVStore(KVStoreBase):
 
     def pull(self, key, out=None, priority=0, ignore_sparse=True):
         assert out is not None
-        keys = _as_list(key)
+        keys = self._keys(key)
         outs = out if isinstance(key, (list, tuple)) else [out]
+        if ignore_sparse:
+            # a row_sparse destination is left untouched (reference kvstore.pull: use row_sparse_pull)
+            kept = [(k, o) for k, o in zip(keys, outs)
+                    if not all(getattr(x, 'stype', 'default') == 'row_sparse' for x in _as_list(o))]
+            if len(kept) != len(keys):
+                keys = [k for k, _ in kept]
+                outs = [o for _, o in kept]
         with torch.no_grad():
             # written through .data: a pull into a parameter is an engine-ordered write in the
             # reference, not an autograd-visible in-place op on a recorded leaf
@@ -265,7 +291,7 @@ class KVStore(KVStoreBase):
             self.push(key, value, priority)
             self.pull(key, out if out is not None else value, priority)
             return
-        keys = _as_list(key)
+        keys = self._keys(key)
         vals = value if isinstance(key, (list, tuple)) else [value]
         outs = vals if out is None else (out if isinstance(key, (list, tuple)) else [out])
         with torch.no_grad():
@@ -279,10 +305,15 @@ class KVStore(KVStoreBase):
 
     def row_sparse_pull(self, key, out=None, priority=0, row_ids=None):
         assert out is not None and row_ids is not None
-        keys = _as_list(key)
+        keys = self._keys(key)
         outs = out if isinstance(key, (list, tuple)) else [out]
         rids = row_ids if isinstance(row_ids, (list, tuple)) and isinstance(key, (list, tuple)) else [row_ids]
         from ..ndarray.sparse import RowSparseNDArray
+        for o in outs:
+            for oo in _as_list(o):
+                if getattr(oo, 'stype', 'default') != 'row_sparse':
+                    raise MXNetError('row_sparse_pull: out must be a row_sparse NDArray, got %s storage'
+                                     % getattr(oo, 'stype', type(oo).__name__))
         with torch.no_grad():
             for k, o, r in zip(keys, outs, rids):
                 st = self._store[k]

@@ -73,7 +73,9 @@ class NDArray:
                  '_exc', '_recorded', '_idt', '_hist', '_engine_var')
     __array_priority__ = 1000.0
 
-    def __init__(self, data, ctx=None, dtype=None, stype='default', writable=True):
+    def __init__(self, data=None, ctx=None, dtype=None, stype='default', writable=True, handle=None):
+        if handle is not None:
+            data = handle
         if isinstance(data, ctypes.c_void_p):
             # a handle from the C-API shim (monitor callbacks, partitioning): the array it names
             from ..base import _handle_object

@@ -149,17 +149,22 @@ def test_kvstore_local_single_process():
     out = nd.zeros((2, 3))
     kv.pull(3, out=out)
     np.testing.assert_allclose(out.asnumpy(), 5)
-    vals = [nd.ones((4,)), nd.ones((4,)) * 2]
-    kv.pushpull('g', vals, vals)
-    np.testing.assert_allclose(vals[0].asnumpy(), 3)
-    kv.set_optimizer(mx.optimizer.SGD(learning_rate=0.1))
-    kv.init('w', nd.ones((2,)))
-    kv.push('w', nd.ones((2,)))
-    o = nd.zeros((2,))
-    kv.pull('w', out=o)
-    np.testing.assert_allclose(o.asnumpy(), 0.9, rtol=1e-6)
+    out = nd.zeros((2, 3)).tostype("row_sparse")
     kv.row_sparse_pull(3, out=out, row_ids=nd.array([1]))
     np.testing.assert_allclose(out.asnumpy()[0], 0)
+    # a store takes one kind of key (the reference's restriction): string keys go to another store
+    with pytest.raises(mx.base.MXNetError):
+        kv.init('g', nd.ones((4,)))
+    skv = mx.kv.create('local')
+    vals = [nd.ones((4,)), nd.ones((4,)) * 2]
+    skv.pushpull('g', vals, vals)
+    np.testing.assert_allclose(vals[0].asnumpy(), 3)
+    skv.set_optimizer(mx.optimizer.SGD(learning_rate=0.1))
+    skv.init('w', nd.ones((2,)))
+    skv.push('w', nd.ones((2,)))
+    o = nd.zeros((2,))
+    skv.pull('w', out=o)
+    np.testing.assert_allclose(o.asnumpy(), 0.9, rtol=1e-6)
 
 
 def test_custom_kvstore_registry():
