@@ -85,7 +85,8 @@ class _DeformConvHip(torch.autograd.Function):
         wmat = weight.reshape(g, O // g, (C // g) * K)
         gw = torch.matmul(go.permute(1, 2, 0, 3).reshape(g, O // g, N * L),
                           cols.view(N, g, (C // g) * K, L).permute(1, 0, 3, 2).reshape(g, N * L, (C // g) * K))
-        gcols = torch.matmul(wmat.transpose(1, 2), go).reshape(N, C * K, L).contiguous()
+        # fp32 column gradients: the offset gradient is a difference of products, bf16 columns lose it
+        gcols = torch.matmul(wmat.transpose(1, 2).float(), go.float()).reshape(N, C * K, L).contiguous()
         gx32 = torch.zeros(x.shape, dtype=torch.float32, device=x.device)
         mptr = 0 if mask is None else mask.data_ptr()
         lib.deform_col2im(_DT[x.dtype], offset.data_ptr(), mptr, gcols.data_ptr(), gx32.data_ptr(), list(geom),

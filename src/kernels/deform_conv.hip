@@ -11,7 +11,8 @@
 //                 fixed tap the threads of a wave write 64 consecutive l -> coalesced column rows,
 //                 offsets / mask read coalesced along l, the bilinear corners are the only gathers.
 //   col2im      : one thread per (n, c, k, l); the 4 bilinear corners are scattered into an fp32
-//                 data-gradient buffer with global (vector-memory) float atomics.
+//                 data-gradient buffer with global (vector-memory) float atomics.  The column
+//                 gradients come in fp32 (the coordinate gradient is a difference of products)
 //   col2im_coord: one thread per (n, group, k, l) reduces over the group's channels in registers
 //                 and writes d(offset_h), d(offset_w) (and d(mask)) once -- no atomics.
 // All arithmetic in fp32; storage fp32 / fp16 / bf16.
@@ -97,7 +98,7 @@ __global__ void __launch_bounds__(256) deform_im2col_kernel(const T* __restrict_
 
 template <typename T, bool MASK>
 __global__ void __launch_bounds__(256) deform_col2im_kernel(const T* __restrict__ off, const T* __restrict__ msk,
-                                                            const T* __restrict__ gcols, float* __restrict__ gx,
+                                                            const float* __restrict__ gcols, float* __restrict__ gx,
                                                             DeformGeom g) {
   const int L = g.Ho * g.Wo, K = g.kh * g.kw;
   const int64_t total = (int64_t)g.N * g.C * K * L;
@@ -115,7 +116,7 @@ __global__ void __launch_bounds__(256) deform_col2im_kernel(const T* __restrict_
     const float h = ho * g.sh - g.ph + i * g.dh + ld(off + ob + (int64_t)(2 * k) * L);
     const float w = wo * g.sw - g.pw + j * g.dw + ld(off + ob + (int64_t)(2 * k + 1) * L);
     if (!(h > -1.f && w > -1.f && h < g.H && w < g.W)) continue;
-    float gv = ld(gcols + t);
+    float gv = gcols[t];
     if (MASK) gv *= ld(msk + ((int64_t)n * g.dg + grp) * K * L + (int64_t)k * L + l);
     const int hl = (int)floorf(h), wl = (int)floorf(w);
     const float lh = h - hl, lw = w - wl;
@@ -130,7 +131,7 @@ __global__ void __launch_bounds__(256) deform_col2im_kernel(const T* __restrict_
 template <typename T, bool MASK>
 __global__ void __launch_bounds__(256) deform_col2im_coord_kernel(const T* __restrict__ x, const T* __restrict__ off,
                                                                   const T* __restrict__ msk,
-                                                                  const T* __restrict__ gcols, T* __restrict__ goff,
+                                                                  const float* __restrict__ gcols, T* __restrict__ goff,
                                                                   T* __restrict__ gmsk, DeformGeom g) {
   const int L = g.Ho * g.Wo, K = g.kh * g.kw;
   const int64_t total = (int64_t)g.N * g.dg * K * L;
@@ -154,7 +155,7 @@ __global__ void __launch_bounds__(256) deform_col2im_coord_kernel(const T* __res
       for (int cc = 0; cc < cpg; ++cc) {
         const int c = grp * cpg + cc;
         const T* plane = x + ((int64_t)n * g.C + c) * g.H * g.W;
-        const float gv = ld(gcols + (((int64_t)n * g.C + c) * K + k) * L + l);
+        const float gv = gcols[(((int64_t)n * g.C + c) * K + k) * L + l];
         float v[4];
         corners(plane, g.H, g.W, hl, wl, v);
         // d(bilinear)/dh and d(bilinear)/dw
@@ -189,9 +190,10 @@ template <typename T>
 void col2im_t(const void* off, const void* msk, const void* gcols, float* gx, const DeformGeom& g, hipStream_t s) {
   const int64_t total = (int64_t)g.N * g.C * g.kh * g.kw * g.Ho * g.Wo;
   if (msk)
-    deform_col2im_kernel<T, true><<<grid_for(total), 256, 0, s>>>((const T*)off, (const T*)msk, (const T*)gcols, gx, g);
+    deform_col2im_kernel<T, true><<<grid_for(total), 256, 0, s>>>((const T*)off, (const T*)msk, (const float*)gcols, gx,
+                                                                  g);
   else
-    deform_col2im_kernel<T, false><<<grid_for(total), 256, 0, s>>>((const T*)off, nullptr, (const T*)gcols, gx, g);
+    deform_col2im_kernel<T, false><<<grid_for(total), 256, 0, s>>>((const T*)off, nullptr, (const float*)gcols, gx, g);
 }
 
 template <typename T>
@@ -200,10 +202,10 @@ void coord_t(const void* x, const void* off, const void* msk, const void* gcols,
   const int64_t total = (int64_t)g.N * g.dg * g.kh * g.kw * g.Ho * g.Wo;
   if (msk)
     deform_col2im_coord_kernel<T, true><<<grid_for(total), 256, 0, s>>>(
-        (const T*)x, (const T*)off, (const T*)msk, (const T*)gcols, (T*)goff, (T*)gmsk, g);
+        (const T*)x, (const T*)off, (const T*)msk, (const float*)gcols, (T*)goff, (T*)gmsk, g);
   else
     deform_col2im_coord_kernel<T, false><<<grid_for(total), 256, 0, s>>>(
-        (const T*)x, (const T*)off, nullptr, (const T*)gcols, (T*)goff, nullptr, g);
+        (const T*)x, (const T*)off, nullptr, (const float*)gcols, (T*)goff, nullptr, g);
 }
 
 DeformGeom geom(int N, int C, int H, int W, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int dh,
