@@ -30,6 +30,24 @@ _RESNET50_RATIOS = [[1, 2, .5], [1, 2, .5, 3, 1. / 3], [1, 2, .5, 3, 1. / 3], [1
                     [1, 2, .5], [1, 2, .5]]
 
 
+class _DeformBlock(HybridBlock):
+    """ReLU(deformable 3x3 conv) on an NHWC or NCHW feature map (the deformable op itself is NCHW)."""
+
+    def __init__(self, channels, stride, pad, layout, **kwargs):
+        super().__init__(**kwargs)
+        from ..gluon.contrib.cnn import DeformableConvolution
+        self.layout = layout
+        self._kwargs = {'kernel': (3, 3), 'stride': (stride, stride), 'pad': (pad, pad)}
+        with self.name_scope():
+            self.conv = DeformableConvolution(channels, kernel_size=(3, 3), strides=(stride, stride),
+                                              padding=(pad, pad), activation='relu')
+
+    def hybrid_forward(self, F, x):
+        if self.layout == 'NHWC':
+            return F.transpose(self.conv(F.transpose(x, axes=(0, 3, 1, 2))), axes=(0, 2, 3, 1))
+        return self.conv(x)
+
+
 class SSD(HybridBlock):
     """SSD detector.  ``forward(x)`` -> (cls_preds [B, A, C+1], loc_preds [B, A*4]).
 
@@ -37,7 +55,8 @@ class SSD(HybridBlock):
     """
 
     def __init__(self, base='resnet50_v1b', classes=20, sizes=None, ratios=None, num_filters=(512, 256, 256, 128),
-                 strides=(2, 2, 2, 2), pads=(1, 1, 1, 1), min_filter=128, layout='NHWC', fuse=True, **kwargs):
+                 strides=(2, 2, 2, 2), pads=(1, 1, 1, 1), min_filter=128, layout='NHWC', fuse=True,
+                 deformable=False, **kwargs):
         super().__init__(**kwargs)
         from ..gluon.model_zoo import vision
         self.classes = classes
@@ -58,8 +77,13 @@ class SSD(HybridBlock):
                 for k, (nf, s, p) in enumerate(zip(num_filters, strides, pads)):
                     blk = nn.HybridSequential(prefix='multi_feat_%d_' % (k + 2))
                     with blk.name_scope():
-                        blk.add(nn.Conv2D(max(min_filter, nf // 2), 1, layout=layout, activation='relu'),
-                                nn.Conv2D(nf, 3, strides=s, padding=p, layout=layout, activation='relu'))
+                        blk.add(nn.Conv2D(max(min_filter, nf // 2), 1, layout=layout, activation='relu'))
+                        if deformable:
+                            # the config's deformable / im2col conv: 3x3 taps displaced by learned offsets
+                            # (contrib DeformableConvolution, in-tree HIP sampling kernels on the GPU)
+                            blk.add(_DeformBlock(nf, s, p, layout))
+                        else:
+                            blk.add(nn.Conv2D(nf, 3, strides=s, padding=p, layout=layout, activation='relu'))
                     self.extras.add(blk)
             self.cls_preds = nn.HybridSequential(prefix='cls_')
             self.loc_preds = nn.HybridSequential(prefix='loc_')

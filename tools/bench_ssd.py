@@ -52,6 +52,8 @@ def main():
     ap.add_argument('--classes', type=int, default=20)
     ap.add_argument('--dtype', default='float16', choices=['float16', 'bfloat16', 'float32'])
     ap.add_argument('--gpus', type=int, default=1, help='worker processes (one per GPU)')
+    ap.add_argument('--deformable', type=int, default=1,
+                    help='deformable 3x3 convs in the extra feature layers (the config\'s deformable/im2col conv)')
     args = ap.parse_args()
     launch = _load_launcher()
     if launch.needs_launch(args.gpus):
@@ -74,7 +76,7 @@ def main():
     mx.random.seed(7 + rank)
 
     B, S = args.batch, args.size
-    net = ssd.ssd_512_resnet50_v1(classes=args.classes, layout='NHWC', fuse=True)
+    net = ssd.ssd_512_resnet50_v1(classes=args.classes, layout='NHWC', fuse=True, deformable=bool(args.deformable))
     net.initialize(mx.init.Xavier(magnitude=2), ctx=ctx)
     if args.dtype != 'float32':
         net.cast(args.dtype)
@@ -113,7 +115,8 @@ def main():
             'data': 'synthetic (random-init weights, uniform images, random gt boxes)',
             'config': {'model': 'SSD-ResNet50 v1b', 'image_size': S, 'per_gpu_batch': B, 'global_batch': B * n,
                        'classes': args.classes, 'anchors': int(net.anchors((S, S), ctx).shape[1]),
-                       'parallelism': 'dp%d' % n, 'final_loss': round(float(L.asscalar()), 4)},
+                       'parallelism': 'dp%d' % n, 'final_loss': round(float(L.asscalar()), 4),
+                       'deformable_extras': bool(args.deformable)},
         }), flush=True)
     if n > 1:
         torch.distributed.destroy_process_group()
