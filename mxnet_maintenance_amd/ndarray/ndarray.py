@@ -212,7 +212,13 @@ class NDArray:
         return {'data': self.asnumpy(), 'ctx': self.context}
 
     def __setstate__(self, state):
-        self._data = torch.from_numpy(np.ascontiguousarray(state['data']))
+        if 'handle' in state:
+            # the reference's pickled state: one array in the raw-bytes save format
+            # (MXNDArraySaveRawBytes); a GPU context in it loads on the CPU when no GPU is present
+            from .utils import _Reader, _read_array
+            self._data = _read_array(_Reader(bytes(state['handle'])))._data
+        else:
+            self._data = torch.from_numpy(np.ascontiguousarray(state['data']))
         self._grad = None
         self._grad_req = None
         self._stype = 'default'
@@ -433,6 +439,8 @@ class NDArray:
         if isinstance(value, NDArray):
             _share_failure(value, self)          # writing a failed result fails the target too
             v = value._data
+        elif torch.is_tensor(value):
+            v = value
         elif isinstance(value, np.generic):
             v = value.item()
         elif isinstance(value, numeric_types):
@@ -440,6 +448,16 @@ class NDArray:
         else:
             v = torch.as_tensor(np.asarray(value), dtype=self._data.dtype)
         t = self._data
+        if _state.STATE.recording and torch.is_tensor(v) and v.requires_grad and not t.requires_grad:
+            # a recorded write of a differentiable value into an untracked array: the array joins the
+            # graph (its untouched elements are constants); an integer array cannot carry gradients
+            if not t.is_floating_point():
+                raise MXNetError('Inplace operations (+=, -=, x[:]=, etc) are not supported when recording with '
+                                 'autograd: the %s target cannot carry the value\'s gradient' % t.dtype)
+            new = t.detach().clone()
+            new[key] = v.to(new.device, new.dtype)
+            self._data = new
+            return
         if _state.STATE.recording and t.requires_grad and not t.is_leaf:
             new = t.clone()
             new[key] = v.to(new.device, new.dtype) if torch.is_tensor(v) else v
@@ -451,12 +469,36 @@ class NDArray:
             with torch.no_grad():
                 t.copy_(v.to(t.device, t.dtype).reshape(()) if torch.is_tensor(v) else torch.as_tensor(v, dtype=t.dtype))
             return
+        key, flips = _positive_step_key(t, key)
+        if flips is None:
+            # key is now a tensor of flat positions
+            if not torch.is_tensor(v):
+                v = torch.as_tensor(v, dtype=t.dtype)
+            v = v.to(t.device, t.dtype)
+            while v.dim() > key.dim() and v.shape[0] == 1:
+                v = v[0]
+            with torch.no_grad():
+                t.view(-1)[key.reshape(-1)] = v.expand(key.shape).reshape(-1)
+            return
+        if flips:
+            # negative-step slices: write the mirrored positive-step slice with the value flipped
+            if not torch.is_tensor(v):
+                v = torch.as_tensor(v, dtype=t.dtype)
+            v = v.to(t.device, t.dtype)
+            tshape = t[key].shape
+            while v.dim() > len(tshape) and v.shape[0] == 1:
+                v = v[0]
+            v = v.expand(tshape).flip(flips)
         with torch.no_grad():
             if torch.is_tensor(v):
                 v = v.to(t.device, t.dtype)
                 tgt = t[key] if not (isinstance(key, slice) and key == slice(None)) else t
                 if tgt.dim() and v.dim() > tgt.dim():
-                    v = v.reshape(tgt.shape)
+                    # extra leading unit axes broadcast away (value (1, 1, 1, 9) into a (16, 9, 9) slot)
+                    while v.dim() > tgt.dim() and v.shape[0] == 1:
+                        v = v[0]
+                    if v.dim() > tgt.dim():
+                        v = v.reshape(tgt.shape)
             t[key] = v
 
     def slice(self, *args, **kwargs):
@@ -724,7 +766,7 @@ def _index_fn(t, key):
                     continue
                 if isinstance(k, slice) and k.step is not None and k.step < 0:
                     b, e, s = k.indices(t.shape[ax])
-                    t = t.index_select(ax, torch.arange(b, e, s, device=t.device))
+                    t = t.index_select(ax, torch.tensor(list(range(b, e, s)), dtype=torch.long, device=t.device))
                     newkey.append(slice(None))
                 else:
                     newkey.append(k)
@@ -796,14 +838,60 @@ def _share_failure(src, dst):
     return dst
 
 
+def _positive_step_key(t, key):
+    """A basic index with negative-step slices -> (the same elements as positive-step slices, the
+    result axes whose order those reverse).  torch has no negative-step views; assignment through
+    one writes the mirrored slice with a flipped value."""
+    items = key if isinstance(key, tuple) else (key,)
+    if not any(isinstance(k, slice) and k.step is not None and k.step < 0 for k in items):
+        return key, []
+    if any(torch.is_tensor(k) or isinstance(k, (list, np.ndarray)) for k in items):
+        # with advanced indices: the flat positions NumPy's indexing selects (one host pass)
+        nkey = tuple(k.cpu().numpy() if torch.is_tensor(k) else k for k in items)
+        flat = np.arange(t.numel()).reshape(tuple(t.shape))[nkey]
+        return torch.from_numpy(np.ascontiguousarray(flat)).to(t.device), None
+    if any(k is Ellipsis for k in items):
+        i = [j for j, k in enumerate(items) if k is Ellipsis][0]
+        used = sum(1 for k in items if k is not None and k is not Ellipsis)
+        items = items[:i] + (slice(None),) * (t.dim() - used) + items[i + 1:]
+    out, flips = [], []
+    ax = oax = 0
+    for k in items:
+        if k is None:
+            out.append(k)
+            oax += 1
+            continue
+        if isinstance(k, slice) and k.step is not None and k.step < 0:
+            b, e, s = k.indices(t.shape[ax])
+            n = len(range(b, e, s))
+            if n == 0:
+                out.append(slice(0, 0))
+            else:
+                last = b + (n - 1) * s
+                out.append(slice(last, b + 1, -s))
+                flips.append(oax)
+            oax += 1
+        else:
+            out.append(k)
+            if isinstance(k, slice):
+                oax += 1
+        ax += 1
+    return tuple(out), flips
+
+
 def _tag_host_ctx(arr, ctx):
     """Label a host array with a virtual CPU context (``cpu(k)``, k > 0): every CPU context is the same
     host memory here, but an array created or placed on ``cpu(k)`` reports that context, as in the
-    reference, which keeps one storage pool per CPU device id."""
+    reference, which keeps one storage pool per CPU device id.  ``cpu_shared`` arrays live in shared
+    memory (the storage worker processes hand to each other) and report that context."""
     if isinstance(ctx, str):
         ctx = Context(ctx)
-    if (isinstance(ctx, Context) and ctx.device_typeid == 1 and ctx.device_id != 0
-            and arr._data.device.type == 'cpu'):
+    if not isinstance(ctx, Context) or arr._data.device.type != 'cpu':
+        return arr
+    if ctx.device_typeid == 5:
+        arr._data.share_memory_()
+        arr._host_ctx = ctx
+    elif ctx.device_typeid == 1 and ctx.device_id != 0:
         arr._host_ctx = ctx
     return arr
 
@@ -811,6 +899,10 @@ def _tag_host_ctx(arr, ctx):
 def array(source_array, ctx=None, dtype=None):
     """Create an NDArray from any array-like (float32 by default, like MXNet)."""
     ctx = _ctx(ctx)
+    if getattr(source_array, 'stype', 'default') != 'default' or (
+            hasattr(source_array, 'tocsr') and not isinstance(source_array, (NDArray, torch.Tensor))):
+        from . import sparse      # sparse NDArray / scipy matrix sources stay sparse
+        return sparse.array(source_array, ctx=ctx, dtype=dtype)
     if isinstance(source_array, NDArray):
         dt = torch_dtype(dtype) if dtype is not None else source_array._data.dtype
         return NDArray(source_array._data.detach().to(device=ctx.torch_device, dtype=dt, copy=True))

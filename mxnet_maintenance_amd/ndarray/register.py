@@ -218,6 +218,10 @@ def invoke(op, inputs, attrs, out=None):
         outs = [NDArray(r) for r in res[:nvis]]
     else:
         outs = [NDArray(res)]
+    st = _kept_stype(op.name, inputs, attrs) if out is None else None
+    if st is not None and not _state.STATE.recording:
+        from . import sparse
+        outs = [sparse.cast_storage(o, st) for o in outs]
     _np_wrap(inputs, outs)
     if idts is not None:
         for o, d in zip(outs, idts if isinstance(idts, list) else [idts]):
@@ -252,6 +256,31 @@ def invoke(op, inputs, attrs, out=None):
     if len(outs) == 1:
         return outs[0]
     return outs
+
+
+# operators whose output keeps a sparse input's storage type (reference: their FInferStorageType --
+# zero-preserving unary math, row selection of a csr matrix); everything else falls back to dense
+_ZERO_PRESERVING = frozenset((
+    'abs', 'sign', 'round', 'rint', 'ceil', 'floor', 'trunc', 'fix', 'square', 'sqrt', 'sin', 'tan',
+    'arcsin', 'arctan', 'sinh', 'tanh', 'arcsinh', 'arctanh', 'expm1', 'log1p', 'relu', 'negative',
+    'degrees', 'radians', '_copy', 'identity', 'cbrt', 'Cast', 'cast', 'stop_gradient', 'BlockGrad'))
+
+
+def _kept_stype(name, inputs, attrs):
+    x = inputs[0] if inputs else None
+    st = getattr(x, 'stype', 'default') if x is not None else 'default'
+    if st == 'default':
+        return None
+    if name in _ZERO_PRESERVING:
+        return st
+    if name == 'clip' and st != 'default':
+        lo, hi = attrs.get('a_min', 0), attrs.get('a_max', 0)
+        return st if (lo is None or float(lo) <= 0) and (hi is None or float(hi) >= 0) else None
+    if st == 'csr' and name == 'take' and int(attrs.get('axis', 0)) == 0:
+        return 'csr'
+    if st == 'csr' and name in ('slice', 'crop', '_slice'):
+        return 'csr'
+    return None
 
 
 def invoke_by_name(name, args, kwargs):

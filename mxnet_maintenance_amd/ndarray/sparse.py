@@ -57,7 +57,7 @@ def _t(a, dtype=None, device=None):
 def _csr_from_dense(d):
     d = d.detach()
     if d.dim() != 2:
-        raise MXNetError('csr storage needs a 2-D array, got shape %s' % (tuple(d.shape),))
+        raise ValueError('csr storage needs a 2-D array, got shape %s' % (tuple(d.shape),))
     mask = d != 0
     counts = mask.sum(1)
     indptr = torch.zeros(d.shape[0] + 1, dtype=_I64, device=d.device)
@@ -168,6 +168,9 @@ class BaseSparseNDArray(NDArray):
     @property
     def context(self):
         self._sync()
+        hc = getattr(self, '_host_ctx', None)
+        if hc is not None and self._vals.device.type == 'cpu':
+            return hc           # cpu(k), k > 0: same host memory, reported context (see _tag_host_ctx)
         return context_from_torch(self._vals.device)
 
     ctx = context
@@ -195,9 +198,15 @@ class BaseSparseNDArray(NDArray):
         self._sync()
         return NDArray(self._densify()).asnumpy()
 
+    def _keep_ctx(self, r):
+        hc = getattr(self, '_host_ctx', None)
+        if hc is not None:
+            r._host_ctx = hc
+        return r
+
     def copy(self):
         self._sync()
-        return type(self)._make(self._vals.clone(), [a.clone() for a in self._aux], self._shp)
+        return self._keep_ctx(type(self)._make(self._vals.clone(), [a.clone() for a in self._aux], self._shp))
 
     def __deepcopy__(self, memo):
         return self.copy()
@@ -211,14 +220,17 @@ class BaseSparseNDArray(NDArray):
         td = torch_dtype(dtype)
         if not copy and td == self._vals.dtype:
             return self
-        return type(self)._make(self._vals.to(td), [a.clone() for a in self._aux], self._shp)
+        return self._keep_ctx(type(self)._make(self._vals.to(td), [a.clone() for a in self._aux], self._shp))
 
     def as_in_context(self, context):
         self._sync()
         if self.context == context:
             return self
         dev = context.torch_device
-        return type(self)._make(self._vals.to(dev), [a.to(dev) for a in self._aux], self._shp)
+        r = type(self)._make(self._vals.to(dev), [a.to(dev) for a in self._aux], self._shp)
+        if context.device_typeid == 1 and context.device_id != 0:
+            r._host_ctx = context
+        return r
 
     as_in_ctx = as_in_context
 
@@ -451,26 +463,57 @@ def _rebuild_sparse(stype, vals, aux, shape):
 
 
 # ------------------------------------------------------------------ constructors
+def _tagged(fn):
+    """Constructors report a requested ``cpu(k)`` context (k > 0) on their result."""
+    import functools
+
+    @functools.wraps(fn)
+    def f(*args, **kwargs):
+        r = fn(*args, **kwargs)
+        ctx = kwargs.get('ctx')
+        if ctx is None:
+            names = fn.__code__.co_varnames[:fn.__code__.co_argcount]
+            if 'ctx' in names and len(args) > names.index('ctx'):
+                ctx = args[names.index('ctx')]
+        if isinstance(ctx, str):
+            ctx = Context(ctx)
+        if (isinstance(r, BaseSparseNDArray) and isinstance(ctx, Context) and ctx.device_typeid == 1
+                and ctx.device_id != 0):
+            r._host_ctx = ctx
+        return r
+    return f
+
+
 def _dev(ctx):
     return (ctx or current_context()).torch_device
 
 
-def _default_dtype(t, dtype):
+def _default_dtype(t, dtype, src=None):
+    """The dtype a sparse constructor gives its values: ``dtype``, else the source's own dtype when
+    it is an NDArray / numpy array / scipy matrix, else float32 (reference: sparse.py
+    _prepare_default_dtype)."""
     if dtype is not None:
         return torch_dtype(dtype)
+    if src is not None:
+        if isinstance(src, (NDArray, np.ndarray)) or hasattr(src, 'tocsr'):
+            return t.dtype
+        return torch.float32
     return t.dtype if t.is_floating_point() else torch.float32
 
 
+@_tagged
 def csr_matrix(arg1, shape=None, ctx=None, dtype=None):
     """CSRNDArray from ``(data, indices, indptr)``, ``(M, N)`` (empty), a dense array or a scipy matrix."""
     dev = _dev(ctx)
     if isinstance(arg1, tuple) and len(arg1) == 3:
         data = _t(arg1[0], device=dev)
-        data = data.to(_default_dtype(data, dtype))
+        data = data.to(_default_dtype(data, dtype, arg1[0]))
         indices = _t(arg1[1], _I64, dev)
         indptr = _t(arg1[2], _I64, dev)
         if shape is None:
-            shape = (indptr.numel() - 1, int(indices.max()) + 1 if indices.numel() else 0)
+            if not indices.numel():
+                raise ValueError('csr_matrix: cannot infer the number of columns without indices; pass shape')
+            shape = (indptr.numel() - 1, int(indices.max()) + 1)
         r = CSRNDArray._make(data.reshape(-1).clone(), [indptr.clone(), indices.clone()], shape)
         r._check(False)
         return r
@@ -482,7 +525,7 @@ def csr_matrix(arg1, shape=None, ctx=None, dtype=None):
         # scipy-style (data, (row, col)) COO definition
         data, (row, col) = arg1
         d = _t(data, device=dev)
-        d = d.to(_default_dtype(d, dtype))
+        d = d.to(_default_dtype(d, dtype, data))
         dense = torch.zeros(shape, dtype=d.dtype, device=dev)
         dense.index_put_((_t(row, _I64, dev), _t(col, _I64, dev)), d, accumulate=True)
         return cast_storage(NDArray(dense), 'csr')
@@ -492,30 +535,31 @@ def csr_matrix(arg1, shape=None, ctx=None, dtype=None):
         r = arg1.astype(dtype) if dtype is not None else arg1.copy()
         return r.as_in_context(ctx) if ctx is not None else r
     if hasattr(arg1, 'tocsr') and not isinstance(arg1, NDArray):
-        m = arg1.tocsr()
+        m = arg1.tocsr(copy=True)
+        m.sum_duplicates()          # canonical form: duplicates summed, column indices sorted per row
         m.sort_indices()
         dt = torch_dtype(dtype) if dtype is not None else torch_dtype(m.dtype if m.dtype.kind == 'f' else np.float32)
         return CSRNDArray._make(torch.as_tensor(m.data).to(dev, dt), [torch.as_tensor(m.indptr).to(dev, _I64),
                                                                       torch.as_tensor(m.indices).to(dev, _I64)],
                                 m.shape)
     d = _t(arg1, device=dev)
-    d = d.to(_default_dtype(d, dtype))
+    d = d.to(_default_dtype(d, dtype, arg1))
     return cast_storage(NDArray(d), 'csr')
 
 
+@_tagged
 def row_sparse_array(arg1, shape=None, ctx=None, dtype=None):
     """RowSparseNDArray from ``(data, indices)``, a shape tuple (empty) or a dense array."""
     dev = _dev(ctx)
     if isinstance(arg1, tuple) and len(arg1) == 2 and not isinstance(arg1[0], (int, np.integer)):
         data = _t(arg1[0], device=dev)
-        data = data.to(_default_dtype(data, dtype))
+        data = data.to(_default_dtype(data, dtype, arg1[0]))
         indices = _t(arg1[1], _I64, dev).reshape(-1)
         if shape is None:
             shape = (int(indices.max()) + 1 if indices.numel() else 0,) + tuple(data.shape[1:])
         data = data.reshape((indices.numel(),) + tuple(shape[1:]))
-        if indices.numel() > 1 and bool((indices[1:] <= indices[:-1]).any()):
-            indices, order = torch.sort(indices)
-            data = data.index_select(0, order)
+        # kept as given: unsorted / negative / out-of-range indices are an invalid format that
+        # check_format reports (reference: RowSparseNDArray format checks)
         return RowSparseNDArray._make(data.clone(), [indices.clone()], shape)
     if isinstance(arg1, tuple):
         if shape is not None and tuple(shape) != tuple(arg1):
@@ -528,10 +572,11 @@ def row_sparse_array(arg1, shape=None, ctx=None, dtype=None):
         r = arg1.astype(dtype) if dtype is not None else arg1.copy()
         return r.as_in_context(ctx) if ctx is not None else r
     d = _t(arg1, device=dev)
-    d = d.to(_default_dtype(d, dtype))
+    d = d.to(_default_dtype(d, dtype, arg1))
     return cast_storage(NDArray(d), 'row_sparse')
 
 
+@_tagged
 def zeros(stype, shape, ctx=None, dtype=None, **kwargs):
     if stype not in ('csr', 'row_sparse', 'default'):
         raise ValueError('unknown storage type %s' % stype)
@@ -552,6 +597,7 @@ def empty(stype, shape, ctx=None, dtype=None):
     return zeros(stype, shape, ctx, dtype)
 
 
+@_tagged
 def array(source_array, ctx=None, dtype=None):
     """Sparse array from a sparse NDArray or a scipy sparse matrix (copies)."""
     if isinstance(source_array, CSRNDArray):

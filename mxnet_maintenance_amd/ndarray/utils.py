@@ -158,8 +158,23 @@ def _read_data(r, flag, shape):
     return torch.from_numpy(raw.reshape(shape))
 
 
+def _check_shape_semantics(magic):
+    """An array saved under numpy shape semantics (V3) loads only under them, and a legacy-semantics
+    array only outside them (reference: src/ndarray/ndarray.cc:1884 NDArray::Load) -- the two
+    disagree on what a 0 in a shape means."""
+    from .. import _state
+    np_shape = bool(_state.STATE.np_shape)
+    if magic == V3_MAGIC and not np_shape:
+        raise MXNetError('ndarray was saved in np shape semantics, must be loaded in the same semantics: '
+                         'use `with np_shape(True)` around the load')
+    if magic != V3_MAGIC and np_shape and not getattr(_state.STATE, 'np_shape_global', False):
+        raise MXNetError('ndarray was not saved in np shape semantics, but is being loaded in np shape '
+                         'semantics: use `with np_shape(False)` around the load')
+
+
 def _read_array(r):
     magic, = r.unpack('<I')
+    _check_shape_semantics(magic)
     if magic in (V2_MAGIC, V3_MAGIC):
         stype_id, = r.unpack('<i')
         stype = _ID_STYPE.get(stype_id, 'default')

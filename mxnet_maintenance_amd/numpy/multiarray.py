@@ -1209,7 +1209,7 @@ def _split_call(name, ary, ios, axis):
     ios = list(ios) if isinstance(ios, (list, tuple)) else int(ios)
     r = _call('_npi_' + name, ary, indices_or_sections=ios, axis=axis)
     if _is_sym(r):
-        return [r[i] for i in range(len(r.list_outputs()))]
+        return [r._output(i) for i in range(len(r.list_outputs()))]
     return list(r) if isinstance(r, (list, tuple)) else [r]
 
 

@@ -109,7 +109,9 @@ def save(file, arr):
 
 def load(file):
     from ..ndarray import utils as _u
-    r = _u.load(file)
+    from ..util import np_shape as _np_shape
+    with _np_shape(True):            # npx.save writes numpy-shape-semantics (V3) records
+        r = _u.load(file)
     if isinstance(r, dict):
         return {k: v.as_np_ndarray() for k, v in r.items()}
     return [v.as_np_ndarray() for v in r]

@@ -355,7 +355,10 @@ def conv_stem_wgrad(x, dy, wshape, pad, out=None, accum=False):
 
 
 # 512-thread big-tile LDS-DMA kernel (conv_big.hip): variant -> (BCO, BPIX)
-_BIG_VARIANTS = {10: (256, 256), 11: (128, 256), 12: (64, 512), 13: (256, 128)}
+_BIG_VARIANTS = {10: (256, 256), 11: (128, 256), 12: (64, 512), 13: (256, 128), 14: (128, 256), 15: (256, 128)}
+# 14 / 15: the 11 / 13 tiles with a 128-VGPR budget, two workgroups per CU -- only for a single
+# K-tile (reduction 64), where one LDS operand stage suffices and the epilogue's HBM streams dominate
+_BIG_SKINNY = (14, 15)
 # persistent LDS-DMA ring kernel (conv_ring.hip): variant -> (BCO, BPIX); no bias
 _RING_VARIANTS = {20: (128, 128), 21: (256, 128), 22: (128, 256), 23: (64, 256), 24: (256, 256), 25: (64, 128)}
 
@@ -445,17 +448,18 @@ def _zero_page(dev):
     return z
 
 
-def _fwd_variants(C, K, bias=False):
-    """Tile variants of conv_fwd valid for Cin=C, Cout=K.
+def _fwd_variants(C, K, bias=False, ktot=None):
+    """Tile variants of conv_fwd valid for Cin=C, Cout=K (``ktot``: the reduction R*S*C).
 
     1..4: register-staged kernel (conv_igemm.hip) with (BCO, BK) = (128,64) (128,32) (64,64) (64,32);
     5, 6: LDS-DMA kernel (conv_glds.hip) with 128x128 / 64x256 tiles;
-    10..13: 512-thread LDS-DMA kernel (conv_big.hip), see _BIG_VARIANTS."""
+    10..15: 512-thread LDS-DMA kernel (conv_big.hip), see _BIG_VARIANTS (14 / 15 only when ktot == 64)."""
     v = []
     if C % 64 == 0 and not bias:
         v.extend(b for b, (bco, _bpix) in sorted(_RING_VARIANTS.items()) if K % bco == 0)
     if C % 64 == 0:
-        v.extend(b for b, (bco, _bpix) in sorted(_BIG_VARIANTS.items()) if K % bco == 0)
+        v.extend(b for b, (bco, _bpix) in sorted(_BIG_VARIANTS.items())
+                 if K % bco == 0 and (b not in _BIG_SKINNY or ktot == 64))
     if C % 64 == 0 and K % 128 == 0:
         v.append(5)
     if C % 64 == 0:
@@ -767,7 +771,7 @@ def _fwd_candidates(x, w, stride, pad, bias):
     if conv_ok_shape(x, w, stride, pad):
         c.append(('hip', lambda: conv_fwd(x, w, stride, pad, bias)))
         stats = bool(_state.STATE.training)
-        for v in _fwd_variants(C, K, bias is not None):
+        for v in _fwd_variants(C, K, bias is not None, ktot=R * S * C):
             c.append(('hip%d' % v, lambda v=v: conv_fwd(x, w, stride, pad, bias, v, bn_stats=stats)))
     if R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0):
         x2, w2 = x.reshape(-1, C), w.reshape(K, C)
@@ -839,7 +843,7 @@ def _dgrad_candidates(dy, x, w, stride, pad):
     if (tuple(stride) == (1, 1) and C % 64 == 0 and K % 32 == 0 and 2 * pad[0] == R - 1 and 2 * pad[1] == S - 1
             and _CONV_HIP):
         c.append(('hip', lambda: conv_fwd(dy, _dgrad_weight(w), (1, 1), (R - 1 - pad[0], S - 1 - pad[1]))))
-        for v in _fwd_variants(K, C):
+        for v in _fwd_variants(K, C, ktot=R * S * K):
             c.append(('hip%d' % v, lambda v=v: conv_fwd(dy, _dgrad_weight(w), (1, 1), (R - 1 - pad[0], S - 1 - pad[1]),
                                                         None, v)))
     for bco in (128, 64):
@@ -909,7 +913,7 @@ def _dgrad_bn_candidates(dy, x, w, stride, pad, bn_src):
     fused = []
     if (_CONV_HIP and tuple(stride) == (1, 1) and 2 * pad[0] == R - 1 and 2 * pad[1] == S - 1
             and K % 64 == 0):
-        for v in _fwd_variants(K, C):
+        for v in _fwd_variants(K, C, ktot=R * S * K):
             if v in _BIG_VARIANTS:
                 fused.append(('hip%d+bn' % v, lambda v=v: conv_fwd(dy, _dgrad_weight(w), (1, 1),
                                                                    (R - 1 - pad[0], S - 1 - pad[1]), None, v,
@@ -1118,7 +1122,7 @@ def _tee_dgrad(gy, x, w, gpass, inplace, bn_src=None):
     if _CONV_HIP and K % 64 == 0 and gy.dtype in (torch.float16, torch.bfloat16) and gy.numel() < 2 ** 31:
         wt = None
         for v, (bco, _bpix) in sorted(_BIG_VARIANTS.items()):
-            if C % bco:
+            if C % bco or (v in _BIG_SKINNY and K != 64):
                 continue
             if wt is None:
                 wt = w2.t().contiguous().view(C, 1, 1, K)

@@ -87,6 +87,8 @@ def _fc_infer(in_shapes, a):
 def fully_connected(data, weight, bias=None, num_hidden=0, no_bias=False, flatten=True):
     if flatten and data.dim() != 2:
         data = data.reshape(data.shape[0], -1)
+    if bias is not None and bias.dim() != 1:
+        bias = bias.reshape(-1)          # a (num_hidden, 1) bias (e.g. row_sparse) is the same vector
     return hip_ops.linear(data, weight, bias)
 
 

@@ -39,11 +39,50 @@ def _rcbrt(x):
     return torch.sign(x) * torch.abs(x).pow(-1.0 / 3)
 
 
+class _Cbrt(torch.autograd.Function):
+    """Real cube root with the reference gradient 1 / (3 cbrt(x)^2) (inf at 0; the
+    sign * |x|^(1/3) composition gives 0 * inf = NaN there)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        y = torch.sign(x) * torch.abs(x).pow(1.0 / 3)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        y, = ctx.saved_tensors
+        return g / (3 * y * y)
+
+
+def _cbrt(x):
+    return _Cbrt.apply(x) if x.requires_grad else torch.sign(x) * torch.abs(x).pow(1.0 / 3)
+
+
+class _Relu(torch.autograd.Function):
+    """relu whose gradient propagates NaN inputs (reference: mshadow_op relu_grad returns NaN for a
+    NaN input, test_ndarray.py:test_ndarray_nan_comparison); torch's threshold gradient zeroes them."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        return torch.relu(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, = ctx.saved_tensors
+        return torch.where(x > 0, g, torch.where(torch.isnan(x), x, torch.zeros_like(g)))
+
+
+def _relu(x):
+    return _Relu.apply(x) if x.requires_grad and x.is_floating_point() else torch.relu(x)
+
+
 _UNARY = {
     'abs': torch.abs, 'sign': torch.sign, 'round': torch.round,
     'rint': torch.round, 'ceil': torch.ceil, 'floor': torch.floor, 'trunc': torch.trunc,
     'fix': torch.trunc, 'square': torch.square, 'sqrt': torch.sqrt, 'rsqrt': torch.rsqrt,
-    'cbrt': lambda x: torch.sign(x) * torch.abs(x).pow(1.0 / 3), 'rcbrt': _rcbrt,
+    'cbrt': _cbrt, 'rcbrt': _rcbrt,
     'exp': torch.exp, 'log': torch.log, 'log10': torch.log10, 'log2': torch.log2,
     'log1p': torch.log1p, 'expm1': torch.expm1, 'gamma': lambda x: torch.exp(torch.lgamma(x)),
     'gammaln': torch.lgamma, 'erf': torch.erf, 'erfinv': torch.erfinv,
@@ -51,7 +90,7 @@ _UNARY = {
     'arccos': torch.acos, 'arctan': torch.atan, 'degrees': torch.rad2deg,
     'radians': torch.deg2rad, 'sinh': torch.sinh, 'cosh': torch.cosh, 'tanh': torch.tanh,
     'arcsinh': torch.asinh, 'arccosh': torch.acosh, 'arctanh': torch.atanh,
-    'reciprocal': torch.reciprocal, 'negative': torch.neg, 'relu': torch.relu,
+    'reciprocal': torch.reciprocal, 'negative': torch.neg, 'relu': _relu,
     'sigmoid': torch.sigmoid, 'softsign': lambda x: x / (1 + torch.abs(x)),
     'logical_not': lambda x: (x == 0).to(x.dtype),
     'log_sigmoid': torch.nn.functional.logsigmoid,
@@ -62,6 +101,44 @@ _UNARY = {
 for _n, _f in _UNARY.items():
     register(_n, (lambda f: lambda data: f(data))(_f))
 alias('negative', '_np_negative')
+
+
+def encode_basic_index(key):
+    """A basic (view) index -- ints, slices, None, Ellipsis, or a tuple of them -- as a JSON string,
+    the ``key`` attribute of ``_npi_basic_index``."""
+    import json
+    items = key if isinstance(key, tuple) else (key,)
+    enc = []
+    for k in items:
+        if isinstance(k, slice):
+            enc.append(['s', k.start, k.stop, k.step])
+        elif k is None:
+            enc.append(['n'])
+        elif k is Ellipsis:
+            enc.append(['e'])
+        elif isinstance(k, (int, np.integer)) and not isinstance(k, bool):
+            enc.append(['i', int(k)])
+        else:
+            raise TypeError('symbolic numpy indexing supports ints, slices, None and Ellipsis, got %r' % (k,))
+    return json.dumps(enc)
+
+
+def _decode_basic_index(enc):
+    import json
+    out = []
+    for item in json.loads(enc):
+        tag = item[0]
+        out.append(slice(*item[1:]) if tag == 's' else None if tag == 'n' else Ellipsis if tag == 'e'
+                   else item[1])
+    return tuple(out)
+
+
+@register('_npi_basic_index', params={'key': ('str', '[]')})
+def _npi_basic_index(data, key='[]'):
+    """x[key] for a basic index in a numpy-mode symbol graph (reference: numpy _Symbol.__getitem__,
+    python/mxnet/symbol/numpy/_symbol.py, lowered there to slice / reshape / expand_dims ops)."""
+    from ..ndarray.ndarray import _index_fn
+    return _index_fn(data, _decode_basic_index(key)).contiguous()
 
 
 @register('hard_sigmoid', params={'alpha': ('float', 0.2), 'beta': ('float', 0.5)})
@@ -388,6 +465,9 @@ def broadcast_axis(data, axis=(), size=()):
 def broadcast_like(lhs, rhs, lhs_axes=None, rhs_axes=None):
     if lhs_axes is None:
         return lhs.expand_as(rhs).contiguous()
+    if len(lhs_axes) == 0 or len(lhs_axes) != len(rhs_axes):
+        raise MXNetError('broadcast_like: lhs_axes and rhs_axes must be non-empty and of equal length, got %s / %s'
+                         % (tuple(lhs_axes), tuple(rhs_axes)))
     tgt = list(lhs.shape)
     for la, ra in zip(lhs_axes, rhs_axes):
         tgt[la] = rhs.shape[ra]
@@ -524,7 +604,7 @@ def _neg_step_slice(data, idx):
         if sl.step is not None and sl.step < 0:
             n = out.shape[ax]
             b, e, s = sl.indices(n)
-            ids = torch.arange(b, e, s, device=out.device)
+            ids = torch.tensor(list(range(b, e, s)), dtype=torch.long, device=out.device)
             out = out.index_select(ax, ids)
         else:
             out = out[(slice(None),) * ax + (sl,)]

@@ -163,6 +163,10 @@ class Symbol:
     def __setstate__(self, state):
         self._outputs = load_json(state['json'])._outputs
 
+    def _output(self, i):
+        """Output ``i`` as its own Symbol (output selection whatever the indexing mode)."""
+        return Symbol([self._outputs[i]])
+
     def __getitem__(self, index):
         if isinstance(index, str):
             names = self.list_outputs()
@@ -171,6 +175,12 @@ class Symbol:
                 raise ValueError('There are multiple outputs with name "%s"' % index if idx else
                                  'Cannot find output that matches name "%s"' % index)
             index = idx[0]
+        from .. import util as _util
+        if (_util.is_np_array() and not getattr(self, '_legacy', False)
+                and (not isinstance(index, (int, np.integer)) or len(self._outputs) == 1)):
+            # numpy semantics: basic indexing of the (single) output, not output selection
+            from ..ops.tensor import encode_basic_index
+            return _create('_npi_basic_index', [self], {'key': encode_basic_index(index)})
         if isinstance(index, slice):
             return Symbol(self._outputs[index])
         return Symbol([self._outputs[index]])
@@ -359,23 +369,31 @@ class Symbol:
     def __neg__(self):
         return self.__mul__(-1.0)
 
+    def _cmp(self, o, bop, sop):
+        out = self._bin(o, bop, sop)
+        from .. import util as _util
+        if _util.is_np_array() and not getattr(self, '_legacy', False):
+            # numpy semantics: comparisons produce booleans (the legacy ops produce 0 / 1 floats)
+            out = _create('Cast', [out], {'dtype': 'bool'})
+        return out
+
     def __eq__(self, o):
-        return self._bin(o, '_equal', '_equal_scalar')
+        return self._cmp(o, '_equal', '_equal_scalar')
 
     def __ne__(self, o):
-        return self._bin(o, '_not_equal', '_not_equal_scalar')
+        return self._cmp(o, '_not_equal', '_not_equal_scalar')
 
     def __gt__(self, o):
-        return self._bin(o, '_greater', '_greater_scalar')
+        return self._cmp(o, '_greater', '_greater_scalar')
 
     def __ge__(self, o):
-        return self._bin(o, '_greater_equal', '_greater_equal_scalar')
+        return self._cmp(o, '_greater_equal', '_greater_equal_scalar')
 
     def __lt__(self, o):
-        return self._bin(o, '_lesser', '_lesser_scalar')
+        return self._cmp(o, '_lesser', '_lesser_scalar')
 
     def __le__(self, o):
-        return self._bin(o, '_lesser_equal', '_lesser_equal_scalar')
+        return self._cmp(o, '_lesser_equal', '_lesser_equal_scalar')
 
     def __hash__(self):
         return id(self)

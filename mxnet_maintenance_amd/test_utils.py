@@ -508,7 +508,14 @@ def check_symbolic_backward(sym, location, out_grads, expected, rtol=None, atol=
     if isinstance(expected, (list, tuple)):
         expected = {k: v for k, v in zip(sym.list_arguments(), expected)}
     args_grad_npy = {k: np.random.normal(size=v.shape) for k, v in expected.items()}
-    args_grad_data = {k: nd.array(v, ctx=ctx, dtype=_arg_dtype(location[k], dtype)) for k, v in args_grad_npy.items()}
+    args_grad_data = {}
+    for k, v in args_grad_npy.items():
+        st = (grad_stypes or {}).get(k)
+        if st is not None and st != 'default':
+            # a sparse gradient buffer: the executor writes the gradient in that storage type
+            args_grad_data[k] = nd.sparse.zeros(st, v.shape, ctx=ctx, dtype=_arg_dtype(location[k], dtype))
+        else:
+            args_grad_data[k] = nd.array(v, ctx=ctx, dtype=_arg_dtype(location[k], dtype))
     if isinstance(grad_req, str):
         grad_req = {k: grad_req for k in sym.list_arguments()}
     elif isinstance(grad_req, (list, tuple)):
@@ -523,7 +530,8 @@ def check_symbolic_backward(sym, location, out_grads, expected, rtol=None, atol=
     else:
         outg = out_grads
     executor.backward(outg)
-    grads = {k: v.asnumpy() for k, v in executor.grad_dict.items() if v is not None}
+    grad_arrays = {k: v for k, v in executor.grad_dict.items() if v is not None}
+    grads = {k: v.asnumpy() for k, v in grad_arrays.items()}
     for name in expected:
         if grad_req[name] == 'write':
             assert_almost_equal(expected[name], grads[name], rtol, atol,
@@ -534,7 +542,7 @@ def check_symbolic_backward(sym, location, out_grads, expected, rtol=None, atol=
         elif grad_req[name] == 'null':
             assert_almost_equal(args_grad_npy[name], grads[name], rtol, atol,
                                 ('EXPECTED_%s' % name, 'BACKWARD_%s' % name), equal_nan=equal_nan)
-    return grads
+    return grad_arrays
 
 
 def check_speed(sym, location=None, ctx=None, N=20, grad_req=None, typ='whole', **kwargs):

@@ -367,7 +367,8 @@ PYBIND11_MODULE(_hip_kernels, m) {
                                       zpw.data(), bco, S(s));
           check_launch("conv_nhwc_dgrad_phases_glds");
         });
-  // 512-thread big-tile kernel: variant 0..3 = 256x256, 128x256, 64x512, 256x128 (co x pix);
+  // 512-thread big-tile kernel: variant 0..3 = 256x256, 128x256, 64x512, 256x128 (co x pix), 4 / 5 =
+  // 128x256 / 256x128 at two workgroups per CU;
   // part (optional): channel-major [2][K][nparts] BatchNorm sum / sum-of-squares partials of y
   // few-channel stride-2 stems (conv_stem.hip): Cin <= 4, Cout = 64, kernel up to 8x8
   m.def("conv_stem_grid", &conv_stem_grid);

@@ -119,9 +119,12 @@ struct BigCfg {
   static constexpr int SMEM = (2 * STAGE > EPI ? 2 * STAGE : EPI);
 };
 
-// BCO = WCO * 64 output channels, BPIX = (8 / WCO) * FJ * 16 pixels per block
-template <typename T, int WCO, int FJ>
-__global__ void __launch_bounds__(512) conv_fwd_big_kernel(const T* __restrict__ x, const T* __restrict__ w,
+// BCO = WCO * 64 output channels, BPIX = (8 / WCO) * FJ * 16 pixels per block.
+// MINB = workgroups per CU the register budget is sized for: MINB 2 caps a wave at 128 VGPRs
+// (4 waves per SIMD) and halves the epilogue's register ring -- the variant for single-K-tile
+// (reduction 64) convs, whose time is the epilogue's HBM traffic, not MFMA.
+template <typename T, int WCO, int FJ, int MINB>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * MINB))) conv_fwd_big_kernel(const T* __restrict__ x, const T* __restrict__ w,
                                                            const float* __restrict__ bias, T* __restrict__ y,
                                                            const T* __restrict__ zero, GeomB g, int tiles_co,
                                                            float* __restrict__ part, int nparts,
@@ -303,7 +306,8 @@ __global__ void __launch_bounds__(512) conv_fwd_big_kernel(const T* __restrict__
   // The addend / BN input z rows this thread reads are streamed through a register ring D
   // iterations deep: all loads of the first D rows are in flight before the first store, and row
   // e + D is requested as row e retires -- instead of one latency-bound load per row.
-  constexpr int D = ITERS < 8 ? ITERS : 8;
+  constexpr int DMAX = MINB > 1 ? 4 : 8;
+  constexpr int D = ITERS < DMAX ? ITERS : DMAX;
   const T* zsrc_b = static_cast<const T*>(bf.z);
   uint4 ad_ring[D], z_ring[D];
   auto row_off = [&](int it, int64_t* off) -> bool {
@@ -387,7 +391,7 @@ __global__ void __launch_bounds__(512) conv_fwd_big_kernel(const T* __restrict__
   }
 }
 
-template <typename T, int WCO, int FJ>
+template <typename T, int WCO, int FJ, int MINB>
 void launch_big(const void* x, const void* w, const float* bias, void* y, const void* zero, const GeomB& g,
                 float* part, int nparts, const void* addend, const BnBwdFuse& bf, hipStream_t s) {
   constexpr int BCO = WCO * 64;
@@ -396,20 +400,31 @@ void launch_big(const void* x, const void* w, const float* bias, void* y, const 
   static_assert(SMEM <= 160 * 1024, "conv_big: LDS budget");
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_fwd_big_kernel<T, WCO, FJ>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_fwd_big_kernel<T, WCO, FJ, MINB>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     attr_set = true;
   }
   const int tiles_co = g.K / BCO;
   const int tiles_pix = (g.M + BPIX - 1) / BPIX;
-  hipLaunchKernelGGL((conv_fwd_big_kernel<T, WCO, FJ>), dim3(tiles_co * tiles_pix), dim3(512), SMEM, s,
+  // a single K-tile (reduction 64: skinny 1x1 convs, the tee dgrads of the bottleneck's first conv)
+  // never touches the second operand stage: launching with only stage 0 + the epilogue image lets
+  // two workgroups share a CU for the 128x256 / 256x128 / 64x512 tiles (with the MINB = 2 register
+  // budget), so one block's epilogue streams overlap another block's operand loads
+  constexpr int ONE_STAGE = BigCfg<BCO, BPIX>::STAGE > BigCfg<BCO, BPIX>::EPI ? BigCfg<BCO, BPIX>::STAGE
+                                                                               : BigCfg<BCO, BPIX>::EPI;
+  const int smem = g.Ktot / 64 > 1 ? SMEM : ONE_STAGE;
+  hipLaunchKernelGGL((conv_fwd_big_kernel<T, WCO, FJ, MINB>), dim3(tiles_co * tiles_pix), dim3(512), smem, s,
                      static_cast<const T*>(x), static_cast<const T*>(w), bias, static_cast<T*>(y),
                      static_cast<const T*>(zero), g, tiles_co, part, nparts, static_cast<const T*>(addend), bf);
 }
 
 // variant -> (WCO, FJ): tile BCO x BPIX
 //   0: 256 x 256   1: 128 x 256   2: 64 x 512   3: 256 x 128
+//   4: 128 x 256   5: 256 x 128 at two workgroups per CU (122 VGPRs; for reduction-64 convs --
+//      the 64 x 512 tile does not fit 128 VGPRs without spilling)
 static void big_tile(int variant, int* bco, int* bpix) {
+  if (variant == 4) variant = 1;
+  if (variant == 5) variant = 3;
   switch (variant) {
     case 0: *bco = 256; *bpix = 256; break;
     case 1: *bco = 128; *bpix = 256; break;
@@ -423,10 +438,12 @@ template <typename T>
 void dispatch_big(int variant, const void* x, const void* w, const float* bias, void* y, const void* zero,
                   const GeomB& g, float* part, int nparts, const void* addend, const BnBwdFuse& bf, hipStream_t s) {
   switch (variant) {
-    case 0: launch_big<T, 4, 8>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
-    case 1: launch_big<T, 2, 4>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
-    case 2: launch_big<T, 1, 4>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
-    case 3: launch_big<T, 4, 4>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
+    case 0: launch_big<T, 4, 8, 1>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
+    case 1: launch_big<T, 2, 4, 1>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
+    case 2: launch_big<T, 1, 4, 1>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
+    case 3: launch_big<T, 4, 4, 1>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
+    case 4: launch_big<T, 2, 4, 2>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
+    case 5: launch_big<T, 4, 4, 2>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
   }
 }
 

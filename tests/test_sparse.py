@@ -48,8 +48,11 @@ def test_csr_does_not_densify_for_sparse_ops():
 
 
 def test_row_sparse_ops():
-    a = nd.sparse.row_sparse_array((np.ones((2, 3), np.float32), [4, 1]), shape=(6, 3))
-    np.testing.assert_array_equal(a.indices.asnumpy(), [1, 4])          # sorted on construction
+    u = nd.sparse.row_sparse_array((np.ones((2, 3), np.float32), [4, 1]), shape=(6, 3))
+    np.testing.assert_array_equal(u.indices.asnumpy(), [4, 1])          # kept as given ...
+    with pytest.raises(mx.base.MXNetError):
+        u.check_format()                                                 # ... and reported invalid
+    a = nd.sparse.row_sparse_array((np.ones((2, 3), np.float32), [1, 4]), shape=(6, 3))
     b = nd.sparse.row_sparse_array((np.full((2, 3), 2, np.float32), [1, 5]), shape=(6, 3))
     c = a + b
     assert c.stype == 'row_sparse'

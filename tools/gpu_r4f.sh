@@ -18,3 +18,5 @@ step r4f_ssd_prof.log 300 rocprofv3 --kernel-trace --stats --output-format csv -
 cd $GRAFT_REPO_ROOT
 python tools/prof_summary.py gpurun_out/r4f_ssd_prof 25 > gpurun_out/r4f_ssd_prof_summary.txt 2>&1
 step r4f_bert.log 300 python -u tools/bench_bert.py --batch 32 --steps 20 --warmup 5 --graph
+step r4f_convbig.log 300 $PYT tests/test_hip_kernels.py -k "conv_big or bn_bwd or teedgrad"
+step r4f_bench.log 400 python -u bench.py --steps 30 --warmup 10
