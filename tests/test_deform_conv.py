@@ -27,11 +27,14 @@ def _inputs(case, seed=0):
     return x, off, mask, w
 
 
-def _run(case, x, off, mask, w):
+def _run(case, x, off, mask, w, grad_dtype=None):
     _, _, _, _, _, k, s, p, d, g, dg, _ = case
     leaves = [t.requires_grad_() for t in (x, off, mask, w) if t is not None]
     out = C._deform_conv(x, off, mask, w, None, k, s, p, d, g, dg)
-    gout = torch.linspace(-1, 1, out.numel(), dtype=torch.float32).reshape(out.shape).to(out.device, out.dtype)
+    gout = torch.linspace(-1, 1, out.numel(), dtype=torch.float32).reshape(out.shape)
+    if grad_dtype is not None:
+        gout = gout.to(grad_dtype)          # the output gradient rounded like the device run's
+    gout = gout.to(out.device, out.dtype)
     out.backward(gout)
     return [out.detach().float().cpu()] + [t.grad.detach().float().cpu() for t in leaves]
 
@@ -57,7 +60,7 @@ def test_hip_kernels_match_fp32_reference(case, dtype):
     dev = [t.to('cuda', dtype) if t is not None else None for t in (x, off, mask, w)]
     if dtype != torch.float32:
         # compare against the reference evaluated on the same rounded inputs
-        ref = _run(case, *(t.float().cpu() if t is not None else None for t in dev))
+        ref = _run(case, *(t.float().cpu() if t is not None else None for t in dev), grad_dtype=dtype)
     got = _run(case, *dev)
     tol = 2e-4 if dtype == torch.float32 else 3e-2
     names = ['out', 'dx', 'doffset'] + (['dmask'] if mask is not None else []) + ['dweight']
