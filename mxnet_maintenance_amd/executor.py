@@ -129,7 +129,7 @@ class GraphProgram:
                     raise
                 from .ndarray.register import _placeholder
                 r = _placeholder(attrs, [])
-            except RuntimeError as e:
+            except (RuntimeError, IndexError) as e:
                 if self.failure is not None:
                     from .ndarray.register import _placeholder
                     r = _placeholder(attrs, [])

@@ -218,7 +218,9 @@ class ndarray(NDArray):
             n = self.shape[0]
             if not -n <= key < n:
                 raise IndexError('index %d is out of bounds for axis 0 with size %d' % (key, n))
-        return _np_out(_reg.invoke_fn(lambda t: _index_fn(t, key), [self]))
+        # a basic index is a view only when its result is contiguous (reference: mx.np basic
+        # indexing slices in place along the first axes, and copies otherwise)
+        return _np_out(_reg.invoke_fn(lambda t: _contig(_index_fn(t, key)), [self]))
 
     def __setitem__(self, key, value):
         if isinstance(key, ndarray) and key.dtype == onp.bool_:
@@ -663,7 +665,8 @@ def empty(shape, dtype=None, order='C', ctx=None):
 
 @_export
 def full(shape, fill_value, dtype=None, order='C', ctx=None, out=None):
-    if isinstance(fill_value, NDArray):
+    if isinstance(fill_value, NDArray) or _is_sym(fill_value):
+        # an array fill value (also a graph input in a hybridized block) broadcasts to the shape
         return broadcast_to(fill_value.astype(dtype) if dtype else fill_value, _shape(shape))
     if dtype is None:
         dtype = 'bool' if isinstance(fill_value, builtins.bool) else ('int64' if isinstance(fill_value, int) else 'float32')
@@ -817,11 +820,17 @@ def _mk_unary(name, opname=None):
 
     def f(x, out=None, **kwargs):
         _ufunc_kwargs(kwargs)
+        if (name in _BOOL_UFUNCS and isinstance(out, NDArray) and onp.dtype(out.dtype) != onp.bool_):
+            raise TypeError('%s: the output of a boolean ufunc must be a bool array, got out dtype %s'
+                            % (name, onp.dtype(out.dtype)))
         return _unary(opname, x, out)
     f.__name__ = name
     f.__doc__ = 'Element-wise ``%s`` (NumPy semantics).' % name
     globals()[name] = f
     __all__.append(name)
+
+
+_BOOL_UFUNCS = frozenset(('isnan', 'isinf', 'isfinite', 'isposinf', 'isneginf', 'signbit'))
 
 
 def _mk_binary(name, opname=None):
@@ -995,14 +1004,18 @@ def average(a, axis=None, weights=None, returned=False, out=None):
 
 @_export
 def quantile(a, q, axis=None, out=None, overwrite_input=None, interpolation='linear', keepdims=False):
-    q = q.tolist() if isinstance(q, NDArray) else q
+    if isinstance(q, NDArray) or _is_sym(q):
+        return _call('_npi_quantile_q', _as_nd(a), q, axis=_axis(axis), interpolation=interpolation,
+                     keepdims=keepdims, out=out)
     return _call('_npi_quantile', _as_nd(a), q=q, axis=_axis(axis), interpolation=interpolation, keepdims=keepdims,
                  out=out)
 
 
 @_export
 def percentile(a, q, axis=None, out=None, overwrite_input=None, interpolation='linear', keepdims=False):
-    q = q.tolist() if isinstance(q, NDArray) else q
+    if isinstance(q, NDArray) or _is_sym(q):
+        return _call('_npi_quantile_q', _as_nd(a), q, axis=_axis(axis), interpolation=interpolation,
+                     keepdims=keepdims, percent=True, out=out)
     return _call('_npi_percentile', _as_nd(a), q=q, axis=_axis(axis), interpolation=interpolation,
                  keepdims=keepdims, out=out)
 
@@ -1518,6 +1531,10 @@ def _byte_extent(t):
     base = t.untyped_storage().data_ptr() + t.storage_offset() * t.element_size()
     span = builtins.sum((n - 1) * builtins.abs(st) for n, st in zip(t.shape, t.stride())) * t.element_size()
     return base, base + span + t.element_size()
+
+
+def _contig(t):
+    return t if t.is_contiguous() else t.contiguous()
 
 
 def shares_memory(a, b, max_work=None):

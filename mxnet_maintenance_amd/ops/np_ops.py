@@ -203,7 +203,14 @@ def _sum(a, axis=None, keepdims=False, dtype=None, initial=None):
     if dt is None and (a.dtype == torch.bool):
         dt = torch.int64
     d = _red_dims(a, axis)
-    r = torch.sum(a, dim=d, keepdim=keepdims, dtype=dt) if d else (a.to(dt) if dt else a.clone())
+    if dt is not None and not dt.is_floating_point and a.requires_grad:
+        a = a.detach()                      # an integer result carries no gradient
+    if d and a.dtype in (torch.float16, torch.bfloat16, torch.float32) and (dt is None or dt.is_floating_point):
+        # accumulate one precision up (fp16 -> fp32, fp32 -> fp64: the reference's AccType), then cast
+        acc = torch.float64 if a.dtype == torch.float32 else torch.float32
+        r = torch.sum(a, dim=d, keepdim=keepdims, dtype=acc).to(dt or a.dtype)
+    else:
+        r = torch.sum(a, dim=d, keepdim=keepdims, dtype=dt) if d else (a.to(dt) if dt else a.clone())
     return r + initial if initial is not None else r
 
 
@@ -228,7 +235,12 @@ def _mean(a, axis=None, keepdims=False, dtype=None):
 def _std_var(fn):
     def f(a, axis=None, keepdims=False, dtype=None, ddof=0):
         dt = _td(dtype) or (a.dtype if a.is_floating_point() else _FLOAT)
-        return fn(a.to(dt), dim=_red_dims(a, axis), correction=ddof, keepdim=keepdims)
+        d = _red_dims(a, axis)
+        if not d and a.dim():
+            # no axes: one element per reduction, so sum((x - mean)^2) = 0 over n - ddof = 1 - ddof
+            v = (0 * a.to(dt)) / (1 - ddof) if ddof != 1 else (0 * a.to(dt)) / 0.0
+            return torch.sqrt(v) if fn is torch.std else v
+        return fn(a.to(dt), dim=d, correction=ddof, keepdim=keepdims)
     return f
 
 
@@ -283,6 +295,15 @@ register('_npi_argmin', arg_names=('a',), params={'axis': ('int?', None), 'keepd
 def _cumsum(a, axis=None, dtype=None):
     if axis is None:
         a, axis = a.reshape(-1), 0
+    dt = _td(dtype) or a.dtype
+    if dt in (torch.float16, torch.bfloat16) and 0 < a.shape[axis] <= 4096:
+        # the reference's kernel accumulates in the output type (out[i] = out[i-1] + in[i]); torch
+        # widens half-precision scans internally, which rounds differently
+        x = a.to(dt).movedim(axis, 0)
+        outs = [x[0]]
+        for i in range(1, x.shape[0]):
+            outs.append(outs[-1] + x[i])
+        return (torch.stack(outs) if outs else x.clone()).movedim(0, axis)
     return torch.cumsum(a, dim=axis, dtype=_td(dtype))
 
 
@@ -321,7 +342,7 @@ def _quantile(a, q=0.5, axis=None, interpolation='linear', keepdims=False):
         # torch.quantile takes float/double only: half and integer inputs go through float64
         out_dt = a.dtype if a.is_floating_point() else _FLOAT
         return _quantile(a.double(), q, axis, interpolation, keepdims).to(out_dt)
-    qt = torch.as_tensor(q, dtype=a.dtype, device=a.device)
+    qt = q.to(a.device, a.dtype) if torch.is_tensor(q) else torch.as_tensor(q, dtype=a.dtype, device=a.device)
     x = a
     if axis is None:
         r = torch.quantile(x.reshape(-1), qt, interpolation=interpolation)
@@ -345,6 +366,14 @@ def _quantile(a, q=0.5, axis=None, interpolation='linear', keepdims=False):
 def _percentile(a, q=50.0, axis=None, interpolation='linear', keepdims=False):
     qq = (torch.as_tensor(q, dtype=torch.float64) / 100.0).tolist()
     return _quantile(a, qq, axis, interpolation, keepdims)
+
+
+@register('_npi_quantile_q', arg_names=('a', 'q'), params={'axis': ('axis', None), 'interpolation': ('str', 'linear'),
+                                                          'keepdims': ('bool', False), 'percent': ('bool', False)})
+def _quantile_q(a, q, axis=None, interpolation='linear', keepdims=False, percent=False):
+    """quantile / percentile with the quantiles as an array input (a graph input when hybridized)."""
+    q = q.double() / 100.0 if percent else q.double()
+    return _quantile(a, q, axis, interpolation, keepdims)
 
 
 @register('_npi_median', arg_names=('a',), params={'axis': ('axis', None), 'keepdims': ('bool', False)})
@@ -465,7 +494,13 @@ def _transpose(a, axes=None):
         return a.clone()
     if not axes:
         axes = tuple(reversed(range(a.dim())))
-    return a.permute(*[x % a.dim() for x in axes])
+    if len(axes) != a.dim() or any(not -a.dim() <= x < a.dim() for x in axes):
+        from ..base import MXNetError
+        raise MXNetError('transpose: axes %s do not match an array of %d dimensions' % (tuple(axes), a.dim()))
+    perm = [x % a.dim() for x in axes]
+    if len(set(perm)) != len(perm):
+        raise ValueError('transpose: repeated axis in %s' % (tuple(axes),))
+    return a.permute(*perm)
 
 
 @register('_npi_swapaxes', aliases=('_np_swapaxes',), arg_names=('a',), params={'axis1': ('int', 0), 'axis2': ('int', 0)})
@@ -551,6 +586,15 @@ def _repeat(a, repeats=1, axis=None):
 
 @register('_npi_broadcast_to', aliases=('_np_broadcast_to',), arg_names=('a',), params={'shape': ('shape', ())})
 def _broadcast_to(a, shape=()):
+    shape = list(shape)
+    if any(d == -2 for d in shape):
+        # npx semantics: -2 keeps the input's size of the dimension it aligns with (right-aligned)
+        off = len(shape) - a.dim()
+        for i, d in enumerate(shape):
+            if d == -2:
+                if i - off < 0:
+                    raise ValueError('broadcast_to: -2 at axis %d has no input dimension to copy' % i)
+                shape[i] = a.shape[i - off]
     return a.expand(tuple(shape)).clone()
 
 

@@ -405,6 +405,14 @@ class Symbol:
         if name.startswith('__'):
             raise AttributeError(name)
         from ..ndarray.ndarray import _FLUENT
+        from .. import util as _util
+        if (name in _NP_METHODS and _util.is_np_array() and not vars(self).get('_legacy', False)):
+            # numpy-mode symbols: the method is the mx.np function (numpy axis / keepdims semantics,
+            # e.g. axis=() reduces nothing), not the legacy operator of the same name
+            from .. import numpy as _mnp
+            fn = getattr(_mnp, name, None)
+            if fn is not None:
+                return lambda *a, **k: fn(self, *a, **k)
         if name in _FLUENT and registry.has(_FLUENT[name]):
             opname = _FLUENT[name]
             return lambda *a, **k: _op_func(opname)(self, *a, **k)
@@ -600,6 +608,11 @@ class Symbol:
 # ---------------------------------------------------------------------------
 # graph construction
 # ---------------------------------------------------------------------------
+
+_NP_METHODS = frozenset(('max', 'min', 'sum', 'mean', 'prod', 'std', 'var', 'argmax', 'argmin', 'cumsum',
+                         'clip', 'any', 'all', 'round', 'repeat', 'take', 'dot', 'squeeze', 'swapaxes',
+                         'sort', 'argsort', 'nonzero', 'diagonal', 'tile'))
+
 
 def _create(op_name, inputs, attrs, name=None, attr=None):
     """Create a Symbol applying ``op_name`` to input Symbols (missing args become variables)."""
