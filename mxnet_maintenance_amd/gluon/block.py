@@ -706,13 +706,33 @@ class HybridBlock(Block):
             outs = self._cached_op(feed, ctx.torch_device)
         outs = [NDArray(o) for o in outs]
         if _state.STATE.recording:
-            for o in outs:
+            syms = self._recorded_symbols()
+            for o, sy in zip(outs, syms):
                 o._recorded = True
+                o._symbol = sy
         if _state.STATE.np_array:
             from ..numpy import _np_out
             outs = _np_out(outs)
         ret, _ = _regroup(outs, self._out_format)
         return ret
+
+    def _recorded_symbols(self):
+        """What autograd.get_symbol returns for this block's outputs: the graph's operators inline
+        when there are at most ``inline_limit`` of them (default 2), else one ``_CachedOp`` node
+        holding the graph (reference: CachedOp inlining, imperative/cached_op.cc)."""
+        syms = getattr(self, '_rec_syms', None)
+        if syms is not None and syms[0] is self._cached_graph:
+            return syms[1]
+        out = self._cached_graph[1]
+        ops = sorted({n.op for n in out._topo() if n.op is not None})
+        nops = sum(1 for n in out._topo() if n.op is not None)
+        limit = int(dict(getattr(self, '_flags', ())).get('inline_limit', 2))
+        if nops > limit and ops:
+            from ..symbol import subgraph
+            out = subgraph.partition(out, ops)
+        per = [out._output(i) if len(out.list_outputs()) > 1 else out for i in range(len(out.list_outputs()))]
+        self._rec_syms = (self._cached_graph, per)
+        return per
 
     def _clear_cached_op(self):
         self._cached_graph = ()

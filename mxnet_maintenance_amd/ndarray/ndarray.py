@@ -70,7 +70,7 @@ def _async_upload(src, context):
 class NDArray:
     """An n-dimensional array on a :class:`Context`."""
     __slots__ = ('_data', '_grad', '_grad_req', '_stype', '__weakref__', '_fresh_grad', '_arena', '_host_ctx',
-                 '_exc', '_recorded', '_idt', '_hist', '_engine_var')
+                 '_exc', '_recorded', '_idt', '_hist', '_engine_var', '_symbol')
     __array_priority__ = 1000.0
 
     def __init__(self, data=None, ctx=None, dtype=None, stype='default', writable=True, handle=None):

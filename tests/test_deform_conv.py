@@ -56,6 +56,10 @@ def test_hip_kernels_match_fp32_reference(case, dtype):
     from mxnet_maintenance_amd.ops import kernels
     assert kernels.available(), kernels.load_error()
     x, off, mask, w = _inputs(case)
+    # keep every sampling position's fractional part in [0.25, 0.75): bf16 rounding would otherwise
+    # put some taps exactly on the integer grid, where the bilinear weights' derivative jumps and any
+    # two implementations may take different one-sided offset gradients
+    off = off.floor() + 0.25 + 0.5 * (off - off.floor())
     ref = _run(case, *(t.clone() if t is not None else None for t in (x, off, mask, w)))
     dev = [t.to('cuda', dtype) if t is not None else None for t in (x, off, mask, w)]
     if dtype != torch.float32:
