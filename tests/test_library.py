@@ -72,3 +72,41 @@ def test_load_rejects_bad_paths(tmp_path):
     p.write_text('')
     with pytest.raises(mx.MXNetError):
         mx.library.load(str(p))
+
+
+def test_abi11_extension_library_gemm_ops(tmp_path):
+    """A library exporting the extension ABI v11 entry points (src/ext_examples/gemm_ext_abi11.cc):
+    the stateless ext_gemm and the stateful ext_state_gemm run imperatively and symbolically, with
+    attribute parsing, shape/type inference, workspace allocation and gradients from the library."""
+    src = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'src', 'ext_examples',
+                       'gemm_ext_abi11.cc')
+    so = str(tmp_path / 'libgemm_ext_abi11.so')
+    subprocess.check_call(['g++', '-shared', '-fPIC', '-O2', '-std=c++14', src, '-o', so])
+    mx.library.load(so, verbose=False)
+    assert set(mx.library.loaded_libraries()[so]) == {'ext_gemm', 'ext_state_gemm'}
+    a = np.random.RandomState(0).uniform(-1, 1, (3, 4)).astype(np.float32)
+    b = np.random.RandomState(1).uniform(-1, 1, (4, 5)).astype(np.float32)
+    g = np.random.RandomState(2).uniform(-1, 1, (3, 5)).astype(np.float32)
+    for name in ('ext_gemm', 'ext_state_gemm'):
+        x, y = mx.nd.array(a), mx.nd.array(b)
+        x.attach_grad()
+        y.attach_grad()
+        with mx.autograd.record():
+            out = getattr(mx.nd, name)(x, y)
+        out.backward(mx.nd.array(g))
+        np.testing.assert_allclose(out.asnumpy(), a @ b, rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(x.grad.asnumpy(), g @ b.T, rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(y.grad.asnumpy(), a.T @ g, rtol=1e-5, atol=1e-5)
+    s, t = mx.sym.var('s'), mx.sym.var('t')
+    net = mx.sym.ext_gemm(s, t)
+    assert net.infer_shape(s=(3, 4), t=(4, 5))[1] == [(3, 5)]
+    exe = net.bind(mx.cpu(), args={'s': mx.nd.array(a), 't': mx.nd.array(b)},
+                   args_grad={'s': mx.nd.zeros((3, 4)), 't': mx.nd.zeros((4, 5))})
+    exe.forward(is_train=True)
+    exe.backward([mx.nd.array(g)])
+    np.testing.assert_allclose(exe.outputs[0].asnumpy(), a @ b, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(exe.grad_dict['s'].asnumpy(), g @ b.T, rtol=1e-5, atol=1e-5)
+    with pytest.raises(mx.base.MXNetError, match='float32'):
+        mx.nd.ext_gemm(mx.nd.array(a, dtype='float64'), mx.nd.array(b, dtype='float64'))
+    with pytest.raises(mx.base.MXNetError, match='inner dimensions'):
+        mx.nd.ext_gemm(mx.nd.array(a), mx.nd.array(a))
