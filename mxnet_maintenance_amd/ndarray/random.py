@@ -163,13 +163,28 @@ def multinomial(data, shape=None, get_prob=False, out=None, dtype='int32', **kwa
     p = data._data.float()
     n = int(np.prod(_shape(shape))) if shape else 1
     flat = p.reshape(-1, p.shape[-1])
+    if flat.shape[-1] > 2 ** 24:
+        from ..base import MXNetError
+        raise MXNetError('multinomial: %d categories exceed 2^24 (not exactly representable as float32 indices)'
+                         % flat.shape[-1])
     idx = torch.multinomial(flat, n, replacement=True)
     oshape = tuple(p.shape[:-1]) + (_shape(shape) if shape else ())
     idx = idx.reshape(oshape if oshape else (1,))
     res = NDArray(idx.to(torch_dtype(dtype)))
     if get_prob:
-        lp = torch.log(torch.gather(flat, 1, idx.reshape(flat.shape[0], -1).to(torch.int64)))
-        return res, NDArray(lp.reshape(idx.shape).to(data._data.dtype))
+        # log-probability of each draw; under autograd its gradient flows to ``data``
+        # (d log p_y / d p_y = 1 / p_y, the reference's SampleMultinomialBackward)
+        from .. import _state
+        rec = bool(_state.STATE.recording)
+        with torch.set_grad_enabled(rec):
+            src = data._data.reshape(-1, data._data.shape[-1])
+            lp = torch.log(torch.gather(src.float(), 1, idx.reshape(flat.shape[0], -1).to(torch.int64)))
+            prob = NDArray(lp.reshape(idx.shape).to(data._data.dtype))
+        if rec:
+            from .register import _note_leaves
+            _note_leaves([data])          # grad_req 'write' resets data's gradient buffer first
+            prob._recorded = True
+        return [res, prob]
     return res
 
 
@@ -192,6 +207,23 @@ def bernoulli(prob=None, logit=None, size=None, dtype=None, ctx=None, out=None):
 
 def uniform_like(data, low=0, high=1, **kwargs):
     return NDArray(torch.empty_like(data._data).uniform_(low, high))
+
+
+def _like_op(opname, params):
+    def f(data=None, *args, **kwargs):
+        from .register import invoke_by_name
+        kw = dict(zip(params, args))
+        kw.update(kwargs)
+        return invoke_by_name(opname, [data], kw)
+    f.__name__ = opname[len('_random_'):]
+    return f
+
+
+gamma_like = _like_op('_random_gamma_like', ['alpha', 'beta'])
+exponential_like = _like_op('_random_exponential_like', ['lam'])
+poisson_like = _like_op('_random_poisson_like', ['lam'])
+negative_binomial_like = _like_op('_random_negative_binomial_like', ['k', 'p'])
+generalized_negative_binomial_like = _like_op('_random_generalized_negative_binomial_like', ['mu', 'alpha'])
 
 
 def normal_like(data, loc=0, scale=1, **kwargs):

@@ -27,6 +27,35 @@ generalized_negative_binomial = _dispatch('_random_generalized_negative_binomial
 randint = _dispatch('_random_randint', '_random_randint', ['low', 'high'])
 
 
+def _like(opname, params):
+    def f(data=None, *args, name=None, **kwargs):
+        kw = dict(zip(params, args))
+        kw.update({k: v for k, v in kwargs.items() if k in params})
+        return _op_func(opname)(data, name=name, **kw)
+    f.__name__ = opname[len('_random_'):]
+    return f
+
+
+uniform_like = _like('_random_uniform_like', ['low', 'high'])
+normal_like = _like('_random_normal_like', ['loc', 'scale'])
+gamma_like = _like('_random_gamma_like', ['alpha', 'beta'])
+exponential_like = _like('_random_exponential_like', ['lam'])
+poisson_like = _like('_random_poisson_like', ['lam'])
+negative_binomial_like = _like('_random_negative_binomial_like', ['k', 'p'])
+generalized_negative_binomial_like = _like('_random_generalized_negative_binomial_like', ['mu', 'alpha'])
+
+
+def randn(*shape, loc=0, scale=1, dtype=None, name=None, **kwargs):
+    """Normal samples of the given shape (positional dimensions, like numpy.random.randn)."""
+    if 'shape' in kwargs:
+        shape = kwargs.pop('shape')
+    if isinstance(kwargs.get('data'), Symbol):
+        # sample with the shape of a symbol (the reference forwards ``data`` to the sampler)
+        out = _op_func('_random_normal_like')(kwargs['data'], loc=loc, scale=scale, name=name)
+        return out if dtype is None else _op_func('Cast')(out, dtype=dtype)
+    return normal(loc, scale, shape=tuple(shape) if shape else (), dtype=dtype, name=name)
+
+
 def multinomial(data, shape=None, get_prob=False, dtype='int32', name=None):
     return _op_func('_sample_multinomial')(data, shape=shape or (), get_prob=get_prob, dtype=dtype, name=name)
 
