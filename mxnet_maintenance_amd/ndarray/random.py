@@ -143,20 +143,35 @@ def poisson(lam=1, shape=None, dtype=None, ctx=None, out=None, **kwargs):
     return _out(t.to(torch_dtype(dtype)), out)
 
 
+def _per_element(params, shape, dev):
+    """Parameters as float tensors of shape param.shape + shape (array parameters draw ``shape``
+    samples per element, the reference's _sample_* semantics) plus the output dtype they imply."""
+    arrs = [q for q in params if isinstance(q, NDArray)]
+    s = _shape(shape) if shape else ()
+    if not arrs:
+        return [torch.full(_shape(shape), float(q), device=dev) for q in params], None
+    base = tuple(arrs[0].shape)
+    out = []
+    for q in params:
+        if isinstance(q, NDArray):
+            t = q._data.float().reshape(base + (1,) * len(s)).expand(base + s)
+        else:
+            t = torch.full(base + s, float(q), device=arrs[0]._data.device)
+        out.append(t)
+    return out, arrs[0]._data.dtype
+
+
 def negative_binomial(k=1, p=1, shape=None, dtype=None, ctx=None, out=None, **kwargs):
-    dev = _dev(ctx)
-    s = _shape(shape)
-    g = torch._standard_gamma(torch.full(s, float(k), device=dev)) * ((1 - p) / p)
-    return _out(torch.poisson(g).to(torch_dtype(dtype)), out)
+    (kt, pt), pdt = _per_element([k, p], shape, _dev(ctx))
+    g = torch._standard_gamma(kt) * ((1 - pt) / pt)
+    return _out(torch.poisson(g).to(pdt or torch_dtype(dtype)), out)
 
 
 def generalized_negative_binomial(mu=1, alpha=1, shape=None, dtype=None, ctx=None, out=None, **kwargs):
-    dev = _dev(ctx)
-    s = _shape(shape)
-    if alpha == 0:
-        return _out(torch.poisson(torch.full(s, float(mu), device=dev)).to(torch_dtype(dtype)), out)
-    g = torch._standard_gamma(torch.full(s, 1.0 / alpha, device=dev)) * (mu * alpha)
-    return _out(torch.poisson(g).to(torch_dtype(dtype)), out)
+    (mt, at), pdt = _per_element([mu, alpha], shape, _dev(ctx))
+    safe = torch.where(at > 0, at, torch.ones_like(at))
+    g = torch.where(at > 0, torch._standard_gamma(1.0 / safe) * (mt * safe), mt)
+    return _out(torch.poisson(g).to(pdt or torch_dtype(dtype)), out)
 
 
 def multinomial(data, shape=None, get_prob=False, out=None, dtype='int32', **kwargs):

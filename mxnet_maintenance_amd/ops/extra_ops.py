@@ -428,7 +428,13 @@ def _negbin(k, p):
 
 
 def _gennegbin(mu, alpha):
-    return torch.poisson(torch._standard_gamma(1.0 / alpha) * mu * alpha)
+    """Gamma-Poisson mixture with mean mu and dispersion alpha (alpha = 0: Poisson(mu)); either
+    argument may be a scalar (the *_like samplers) or a per-element tensor."""
+    mu_t = mu if torch.is_tensor(mu) else torch.tensor(float(mu))
+    al_t = alpha if torch.is_tensor(alpha) else torch.full_like(mu_t, float(alpha))
+    safe = torch.where(al_t > 0, al_t, torch.ones_like(al_t))
+    rate = torch.where(al_t > 0, torch._standard_gamma(1.0 / safe) * mu_t * safe, mu_t.expand_as(safe))
+    return torch.poisson(rate)
 
 
 for _name, _args, _draw in [

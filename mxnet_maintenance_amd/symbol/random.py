@@ -7,7 +7,8 @@ def _dispatch(scalar_op, tensor_op, params):
         vals = dict(zip(params, args))
         vals.update({k: v for k, v in kwargs.items() if k in params})
         if any(isinstance(v, Symbol) for v in vals.values()):
-            return _op_func(tensor_op)(*[vals[p] for p in params], shape=shape or (), name=name)
+            extra = {'dtype': dtype} if dtype is not None else {}
+            return _op_func(tensor_op)(*[vals[p] for p in params], shape=shape or (), name=name, **extra)
         kw = {k: v for k, v in vals.items()}
         kw['shape'] = shape or ()
         if dtype is not None:
@@ -18,12 +19,20 @@ def _dispatch(scalar_op, tensor_op, params):
 
 uniform = _dispatch('_random_uniform', '_sample_uniform', ['low', 'high'])
 normal = _dispatch('_random_normal', '_sample_normal', ['loc', 'scale'])
-gamma = _dispatch('_random_gamma', '_random_gamma', ['alpha', 'beta'])
-exponential = _dispatch('_random_exponential', '_random_exponential', ['lam'])
-poisson = _dispatch('_random_poisson', '_random_poisson', ['lam'])
-negative_binomial = _dispatch('_random_negative_binomial', '_random_negative_binomial', ['k', 'p'])
+gamma = _dispatch('_random_gamma', '_sample_gamma', ['alpha', 'beta'])
+_exponential_lam = _dispatch('_random_exponential', '_sample_exponential', ['lam'])
+
+
+def exponential(scale=1, shape=None, dtype=None, name=None, **kwargs):
+    """Exponential samples with mean ``scale`` (rate 1 / scale), as mx.nd.random.exponential."""
+    lam = kwargs.pop('lam', None)
+    if lam is None:
+        lam = (1.0 / scale) if not isinstance(scale, Symbol) else 1.0 / scale
+    return _exponential_lam(lam, shape=shape, dtype=dtype, name=name)
+poisson = _dispatch('_random_poisson', '_sample_poisson', ['lam'])
+negative_binomial = _dispatch('_random_negative_binomial', '_sample_negative_binomial', ['k', 'p'])
 generalized_negative_binomial = _dispatch('_random_generalized_negative_binomial',
-                                          '_random_generalized_negative_binomial', ['mu', 'alpha'])
+                                          '_sample_generalized_negative_binomial', ['mu', 'alpha'])
 randint = _dispatch('_random_randint', '_random_randint', ['low', 'high'])
 
 
