@@ -32,6 +32,11 @@ class MXNetError(RuntimeError):
     """Error raised by the framework (mirrors mxnet.base.MXNetError)."""
 
 
+class MXNetIndexError(MXNetError, IndexError):
+    """An out-of-bounds index inside an operator: an MXNetError that is also an IndexError (the
+    reference maps dmlc's IndexError-typed errors to Python's IndexError)."""
+
+
 class AsyncOpError(MXNetError):
     """Failure inside an operator's *execution* (not its argument / shape checks).  As with the
     reference's threaded engine, the imperative layer does not raise it at the call: the outputs are

@@ -212,6 +212,9 @@ def invoke(op, inputs, attrs, out=None):
         res = _placeholder(attrs, inputs)    # an op fed garbage by a failed input: the input's error wins
     except (RuntimeError, IndexError) as e:
         # operator failures surface as MXNetError (a RuntimeError), as from the reference's C API
+        if isinstance(e, IndexError):
+            from ..base import MXNetIndexError
+            raise MXNetIndexError('Error in operator %s: %s' % (op.name, e)) from e
         raise MXNetError('Error in operator %s: %s' % (op.name, e)) from e
     nvis = op.get_num_visible_outputs(attrs)
     if isinstance(res, (tuple, list)):

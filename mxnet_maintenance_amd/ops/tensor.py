@@ -1125,7 +1125,8 @@ def index_array(data, axes=None):
 @register('_contrib_allclose', aliases=('allclose',), arg_names=('a', 'b'),
           params={'rtol': ('float', 1e-5), 'atol': ('float', 1e-8), 'equal_nan': ('bool', True)})
 def allclose(a, b, rtol=1e-5, atol=1e-8, equal_nan=True):
-    return torch.tensor([float(torch.allclose(a, b, rtol, atol, equal_nan))], device=a.device)
+    # a 0-d result (reference allclose_op-inl.h: TShape(0, -1))
+    return torch.tensor(float(torch.allclose(a, b.to(a.dtype), rtol, atol, equal_nan)), device=a.device)
 
 
 @register('_contrib_div_sqrt_dim', aliases=('div_sqrt_dim',))
