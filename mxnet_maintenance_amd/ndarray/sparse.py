@@ -449,7 +449,9 @@ class RowSparseNDArray(BaseSparseNDArray):
     def __getitem__(self, key):
         if isinstance(key, slice) and key == slice(None):
             return self
-        return NDArray.__getitem__(NDArray(self._densify()), key)
+        # a view of the current dense image (earlier writes through it included); writes into the
+        # view (``out=x[i]``) land in this array, whose rows are re-derived at the next sync
+        return NDArray.__getitem__(NDArray(self._data), key)
 
 
 def _np_of(t):

@@ -808,8 +808,21 @@ class Ftrl(_Stepper):
 
     def update(self, index, weight, grad, state):
         lr, wd, _ = self._begin(index)
-        _oo.ftrl_update(weight._data, grad._data, state[0]._data, state[1]._data, lr=lr, lamda1=self.lamda1,
-                        beta=self.beta, wd=wd, rescale_grad=self.rescale_grad, clip_gradient=self._clip())
+        kw = dict(lr=lr, lamda1=self.lamda1, beta=self.beta, wd=wd, rescale_grad=self.rescale_grad,
+                  clip_gradient=self._clip())
+        if _is_rsp(grad):
+            # a row_sparse gradient updates only its rows (reference: the sparse ftrl_update kernel)
+            w = weight._data
+            rows, gv = _rsp_rows_of(grad, w.device)
+            if rows.numel() == 0:
+                return
+            z, n = state[0]._data, state[1]._data
+            wr, zr, nr = w[rows].clone(), z[rows].clone(), n[rows].clone()
+            _oo.ftrl_update(wr, gv.to(w.dtype).reshape(wr.shape), zr, nr, **kw)
+            with torch.no_grad():
+                w[rows], z[rows], n[rows] = wr, zr, nr
+            return
+        _oo.ftrl_update(weight._data, grad._data, state[0]._data, state[1]._data, **kw)
 
 
 @register
