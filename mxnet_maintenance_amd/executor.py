@@ -150,6 +150,21 @@ class GraphProgram:
         return [vals[s] for s in self.out_slots]
 
 
+# binary / scatter operators whose row_sparse lhs keeps its storage (reference scatter_* and
+# elemwise FInferStorageType: rows come from the lhs, or the union of both row_sparse operands)
+_SPARSE_LHS = frozenset(('_scatter_elemwise_div', '_scatter_plus_scalar', '_scatter_minus_scalar',
+                         '_mul_scalar', '_div_scalar'))
+_SPARSE_BOTH = frozenset(('elemwise_add', 'elemwise_sub', 'elemwise_mul', '_grad_add'))
+
+
+def registry_parse(node):
+    from .ops import registry
+    try:
+        return registry.get(node.op).parse_attrs(node.attrs)
+    except Exception:  # pragma: no cover - unknown attribute formats: infer as dense
+        return {}
+
+
 class Executor:
     """Executor bound to arrays for arguments, gradients and auxiliary states."""
 
@@ -326,6 +341,10 @@ class Executor:
                     b._data.copy_(o.detach())
         else:
             self.outputs = [NDArray(o.detach()) for o in outs]
+        st = self._output_stypes()
+        if st is not None:
+            from .ndarray import sparse
+            self.outputs = [sparse.cast_storage(o, t) if t != 'default' else o for o, t in zip(self.outputs, st)]
         self._failure = getattr(self._prog, 'failure', None)
         self._failure_box = None
         if self._failure is not None:
@@ -334,6 +353,40 @@ class Executor:
             for o in self.outputs:
                 o._exc = box
         return self.outputs
+
+    def _output_stypes(self):
+        """Storage types of the outputs when sparse arguments are bound (reference: FInferStorageType
+        over the graph); None when every argument is dense.  Operators keep a sparse first input's
+        storage where register._kept_stype says so; everything else falls back to dense."""
+        cached = getattr(self, '_stype_cache', False)
+        if cached is not False:
+            return cached
+        from .ndarray.register import _kept_stype
+        args = dict(zip(self._symbol.list_arguments(), self.arg_arrays))
+        if all(getattr(a, 'stype', 'default') == 'default' for a in args.values()):
+            self._stype_cache = None
+            return None
+
+        class _S:
+            __slots__ = ('stype',)
+
+            def __init__(self, st):
+                self.stype = st
+        memo = {}
+        for n in self._symbol._topo():
+            if n.op is None:
+                memo[(id(n), 0)] = getattr(args.get(n.name), 'stype', 'default')
+                continue
+            ins = [memo.get((id(i), j), 'default') for i, j in n.inputs]
+            attrs = registry_parse(n)
+            st = _kept_stype(n.op, [_S(t) for t in ins], attrs) if ins else None
+            if st is None and ins and ins[0] == 'row_sparse':
+                if n.op in _SPARSE_LHS or (n.op in _SPARSE_BOTH and all(t == 'row_sparse' for t in ins)):
+                    st = 'row_sparse'
+
+            memo[(id(n), 0)] = st or 'default'
+        self._stype_cache = [memo.get((id(n), i), 'default') for n, i in self._symbol._outputs]
+        return self._stype_cache
 
     def backward(self, out_grads=None, is_train=True):
         from .ndarray.ndarray import NDArray

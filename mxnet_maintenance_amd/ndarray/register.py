@@ -279,6 +279,13 @@ def _kept_stype(name, inputs, attrs):
     if name == 'clip' and st != 'default':
         lo, hi = attrs.get('a_min', 0), attrs.get('a_max', 0)
         return st if (lo is None or float(lo) <= 0) and (hi is None or float(hi) >= 0) else None
+    if name in ('_contrib_quadratic', 'quadratic') and float(attrs.get('c', 0.0) or 0.0) == 0.0:
+        return st                           # a*x^2 + b*x keeps zeros
+    if st == 'row_sparse' and name == '_square_sum':
+        ax = attrs.get('axis')
+        ax = ax[0] if isinstance(ax, (tuple, list)) and len(ax) == 1 else ax
+        if ax == 1 and bool(attrs.get('keepdims', False)):
+            return 'row_sparse'             # per-row sums of a row_sparse matrix stay row_sparse
     if st == 'csr' and name == 'take' and int(attrs.get('axis', 0)) == 0:
         return 'csr'
     if st == 'csr' and name in ('slice', 'crop', '_slice'):
