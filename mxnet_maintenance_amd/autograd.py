@@ -283,6 +283,9 @@ def get_symbol(x):
     """Return a Symbol for the recorded history of ``x`` (only available for
     arrays produced by a hybridized block; see gluon.block)."""
     sym = getattr(x, '_symbol', None)
+    if isinstance(sym, tuple):
+        block, i = sym                  # an output of a hybridized block (gluon/block.py)
+        return block._recorded_symbols()[i]
     if sym is not None:
         return sym
     if getattr(x, '_hist', None) is None:

@@ -706,10 +706,9 @@ class HybridBlock(Block):
             outs = self._cached_op(feed, ctx.torch_device)
         outs = [NDArray(o) for o in outs]
         if _state.STATE.recording:
-            syms = self._recorded_symbols()
-            for o, sy in zip(outs, syms):
+            for i, o in enumerate(outs):
                 o._recorded = True
-                o._symbol = sy
+                o._symbol = (self, i)       # resolved by autograd.get_symbol only when asked
         if _state.STATE.np_array:
             from ..numpy import _np_out
             outs = _np_out(outs)
