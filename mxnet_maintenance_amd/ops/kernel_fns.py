@@ -359,6 +359,9 @@ _BIG_VARIANTS = {10: (256, 256), 11: (128, 256), 12: (64, 512), 13: (256, 128), 
 # 14 / 15: the 11 / 13 tiles with a 128-VGPR budget, two workgroups per CU -- only for a single
 # K-tile (reduction 64), where one LDS operand stage suffices and the epilogue's HBM streams dominate
 _BIG_SKINNY = (14, 15)
+# offered to the autotuner only with MXAMD_CONV_SKINNY=1: an A/B on the SSD-512 step measured the
+# tree with them 15-20 % slower end to end, so they stay opt-in until that is understood
+_SKINNY_ON = os.environ.get('MXAMD_CONV_SKINNY', '0') == '1'
 # persistent LDS-DMA ring kernel (conv_ring.hip): variant -> (BCO, BPIX); no bias
 _RING_VARIANTS = {20: (128, 128), 21: (256, 128), 22: (128, 256), 23: (64, 256), 24: (256, 256), 25: (64, 128)}
 
@@ -459,7 +462,7 @@ def _fwd_variants(C, K, bias=False, ktot=None):
         v.extend(b for b, (bco, _bpix) in sorted(_RING_VARIANTS.items()) if K % bco == 0)
     if C % 64 == 0:
         v.extend(b for b, (bco, _bpix) in sorted(_BIG_VARIANTS.items())
-                 if K % bco == 0 and (b not in _BIG_SKINNY or ktot == 64))
+                 if K % bco == 0 and (b not in _BIG_SKINNY or (_SKINNY_ON and ktot == 64)))
     if C % 64 == 0 and K % 128 == 0:
         v.append(5)
     if C % 64 == 0:
@@ -1122,7 +1125,7 @@ def _tee_dgrad(gy, x, w, gpass, inplace, bn_src=None):
     if _CONV_HIP and K % 64 == 0 and gy.dtype in (torch.float16, torch.bfloat16) and gy.numel() < 2 ** 31:
         wt = None
         for v, (bco, _bpix) in sorted(_BIG_VARIANTS.items()):
-            if C % bco or (v in _BIG_SKINNY and K != 64):
+            if C % bco or (v in _BIG_SKINNY and not (_SKINNY_ON and K == 64)):
                 continue
             if wt is None:
                 wt = w2.t().contiguous().view(C, 1, 1, K)
