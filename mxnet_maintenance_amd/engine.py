@@ -27,7 +27,7 @@ from contextlib import contextmanager
 
 __all__ = ['bulk', 'set_bulk_size', 'get', 'push', 'push_device', 'stream_wait_var', 'new_var', 'wait_for_var',
            'wait_all', 'native_available', 'Engine', 'debug_access', 'race_violations', 'var_of', 'copy_stream',
-           'host_to_device', 'wait_host_reads']
+           'host_to_device', 'wait_host_reads', 'register_owned_pinned', 'unregister_owned_pinned']
 
 _engine = None
 _lock = threading.Lock()
@@ -178,6 +178,7 @@ def push_device(fn, const_vars=(), mutable_vars=(), stream=None, priority=0, nam
     (default: the caller's current stream) as the current stream and must only *enqueue* work; the
     op completes when issued.  Other streams reading/writing the same variables are ordered after
     it with HIP events, host ops synchronise on it."""
+    _bulking.flush()      # a device op ordered after gathered host ops sees them pushed first
     s, handle, dev = _stream_of(stream)
     if s is None:
         run = fn
@@ -191,6 +192,7 @@ def push_device(fn, const_vars=(), mutable_vars=(), stream=None, priority=0, nam
 
 def stream_wait_var(var, stream=None):
     """Make ``stream`` (default: current) wait on the GPU for the last device write of ``var``."""
+    _bulking.flush()
     s, handle, dev = _stream_of(stream)
     if s is None:
         get().wait_for_var(var)
@@ -226,10 +228,12 @@ def push_write_file(path, data, const_vars=(), mutable_vars=()):
 
 
 def wait_for_var(var):
+    _bulking.flush()
     get().wait_for_var(var)
 
 
 def wait_all():
+    _bulking.flush()
     if _engine is not None:
         _engine.wait_for_all()
 
@@ -339,6 +343,29 @@ _HOST_READS = []
 _HOST_READS_MAX = 256
 
 
+# pinned host ranges whose producer recycles them only after wait_host_reads (e.g. the
+# ImageRecordIter batch ring): H2D copies read them in place.  Any other pinned source (a cpu_pinned
+# NDArray, a DataLoader pin_memory batch) may be overwritten by host code at any time, so its copy
+# reads a private pinned snapshot instead (no write-after-read race on the source).
+_OWNED_PINNED = []
+
+
+def register_owned_pinned(ptr, nbytes):
+    """Declare ``[ptr, ptr + nbytes)`` as pinned memory whose producer calls ``wait_host_reads``
+    before overwriting it."""
+    _OWNED_PINNED.append((int(ptr), int(nbytes)))
+
+
+def unregister_owned_pinned(ptr):
+    _OWNED_PINNED[:] = [(b, n) for (b, n) in _OWNED_PINNED if b != int(ptr)]
+
+
+def _is_owned_pinned(t):
+    p = t.data_ptr()
+    end = p + t.numel() * t.element_size()
+    return any(b <= p and end <= b + n for (b, n) in _OWNED_PINNED)
+
+
 def copy_stream(dev):
     """The dedicated H2D copy stream of device ``dev`` (a torch.device)."""
     import torch
@@ -375,9 +402,12 @@ def host_to_device(src, dev, out=None, var=None, name='h2d'):
     the caller does not own are registered so their producer can ``wait_host_reads``."""
     import torch
     src = src.detach().contiguous()
-    borrowed = src.is_pinned()
+    borrowed = src.is_pinned() and _is_owned_pinned(src)
     if not borrowed:
-        src = src.pin_memory()
+        # private pinned snapshot: later host writes to the source cannot reach the pending DMA
+        snap = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+        snap.copy_(src)
+        src = snap
     cs = copy_stream(dev)
     consumer = torch.cuda.current_stream(dev)
     if out is None:

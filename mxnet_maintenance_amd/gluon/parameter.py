@@ -310,6 +310,11 @@ class Parameter:
         holding every row)."""
         host = cpu()
         reps = self._all_data()
+        tr = self._trainer
+        if self._stype == 'row_sparse' and tr is not None and getattr(tr, '_kvstore', None) is not None:
+            # the kvstore holds the authoritative weight: pull every row first (reference parameter.py:400-403)
+            all_rows = nd.arange(0, self.shape[0], dtype='int64', ctx=reps[0].context)
+            tr._row_sparse_pull(self, reps if len(reps) > 1 else reps[0], all_rows, full_idx=True)
         if len(reps) == 1:
             val = NDArray(reps[0]._data.detach().to('cpu', copy=True))
         else:
@@ -358,21 +363,21 @@ class Parameter:
         if _state.STATE.recording:
             # inside autograd.record() the replica itself (the leaf whose gradient the trainer reads)
             return got
-        for a in (got if isinstance(got, list) else [got]):
-            self._keep_rows(a, row_id)
-        return got
+        # outside record(): a copy holding only the pulled rows, like the reference's pulled row_sparse
+        # array; the replica itself keeps every row (it is what _reduce / save_parameters read)
+        if isinstance(got, list):
+            return [self._masked_rows(a, row_id) for a in got]
+        return self._masked_rows(got, row_id)
 
     @staticmethod
-    def _keep_rows(arr, row_id):
-        """Zero the rows of replica ``arr`` that were not pulled: like the reference's pulled row_sparse
-        copy it then holds only the requested rows (the kvstore keeps the full weight), and it stays the
-        parameter's own array, so gradients computed from it reach the trainer."""
+    def _masked_rows(arr, row_id):
+        """A new array equal to replica ``arr`` on the rows ``row_id`` and zero elsewhere."""
         t = arr._data
         rows = row_id._data.to(device=t.device, dtype=torch.int64).reshape(-1)
-        keep = torch.zeros(t.shape[0], dtype=torch.bool, device=t.device)
-        keep[rows] = True
         with torch.no_grad():
-            t[~keep] = 0
+            out = torch.zeros_like(t)
+            out[rows] = t[rows]
+        return NDArray(out)
 
     def row_sparse_data(self, row_id):
         """The rows ``row_id`` of a row_sparse parameter, on ``row_id``'s context."""

@@ -1,9 +1,11 @@
 """Fused recurrent layers RNN / LSTM / GRU (parity: python/mxnet/gluon/rnn/rnn_layer.py).
 
-Per-layer/direction parameters ``{l,r}{i}_{i2h,h2h,h2r}_{weight,bias}`` are
-concatenated (weights first, then biases — the reference's flat layout) and
-fed to the fused ``RNN`` operator, which runs MIOpen-backed torch RNN kernels
-on the MI355X (or the explicit loop for clipping / variable lengths).
+Each (layer, direction) owns ``{l,r}{layer}_{i2h,h2h[,h2r]}_{weight,bias}``
+parameters.  The forward flattens them into the fused ``RNN`` operator's single
+parameter vector -- every weight (layer-major, direction, group) first, then
+every bias -- which is the layout the reference's cuDNN path uses, so
+``.params`` files interchange.  The operator itself runs the in-tree gfx950
+recurrent kernels (ops/rnn_fns.py) on the GPU.
 """
 import re
 
@@ -14,22 +16,33 @@ from . import rnn_cell
 
 __all__ = ['RNN', 'LSTM', 'GRU']
 
+_GATES = {'rnn_relu': 1, 'rnn_tanh': 1, 'lstm': 4, 'gru': 3}
+_PARAM_RE = re.compile(r'(?P<dir>[lr])(?P<layer>\d+)_(?P<group>i2h|h2h|h2r)_(?P<kind>weight|bias)\Z')
+
 
 class _RNNLayer(HybridBlock):
+    """Shared machinery of the fused layers; subclasses only describe their recurrent state."""
+
     def __init__(self, hidden_size, num_layers, layout, dropout, bidirectional, input_size,
                  i2h_weight_initializer, h2h_weight_initializer, i2h_bias_initializer, h2h_bias_initializer, mode,
                  projection_size, h2r_weight_initializer, lstm_state_clip_min, lstm_state_clip_max,
                  lstm_state_clip_nan, dtype, use_sequence_length=False, **kwargs):
         super().__init__(**kwargs)
-        assert layout in ('TNC', 'NTC'), "Invalid layout %s; must be one of ['TNC' or 'NTC']" % layout
-        self._hidden_size = hidden_size
-        self._projection_size = projection_size if projection_size else None
-        self._num_layers = num_layers
+        if layout not in ('TNC', 'NTC'):
+            raise AssertionError("Invalid layout %s; must be one of ['TNC' or 'NTC']" % layout)
         self._mode = mode
+        self._gates = _GATES[mode]
+        self._hidden_size = hidden_size
+        self._projection_size = projection_size or None
+        self._num_layers = num_layers
         self._layout = layout
         self._dropout = dropout
         self._dir = 2 if bidirectional else 1
         self._input_size = input_size
+        self._inits = {'i2h_weight': i2h_weight_initializer, 'h2h_weight': h2h_weight_initializer,
+                       'i2h_bias': i2h_bias_initializer, 'h2h_bias': h2h_bias_initializer,
+                       'h2r_weight': h2r_weight_initializer}
+        # attribute names kept for code that introspects them (the reference exposes these)
         self._i2h_weight_initializer = i2h_weight_initializer
         self._h2h_weight_initializer = h2h_weight_initializer
         self._i2h_bias_initializer = i2h_bias_initializer
@@ -41,150 +54,161 @@ class _RNNLayer(HybridBlock):
         self._dtype = dtype
         self._use_sequence_length = use_sequence_length
         self.skip_states = None
-        self._gates = {'rnn_relu': 1, 'rnn_tanh': 1, 'lstm': 4, 'gru': 3}[mode]
-        ng, ni, nh = self._gates, input_size, hidden_size
-        npj = self._projection_size
-        for i in range(num_layers):
-            for j in ['l', 'r'][:self._dir]:
-                self._register_param('{}{}_i2h_weight'.format(j, i), (ng * nh, ni), i2h_weight_initializer, dtype)
-                self._register_param('{}{}_h2h_weight'.format(j, i), (ng * nh, npj or nh), h2h_weight_initializer,
-                                     dtype)
-                self._register_param('{}{}_i2h_bias'.format(j, i), (ng * nh,), i2h_bias_initializer, dtype)
-                self._register_param('{}{}_h2h_bias'.format(j, i), (ng * nh,), h2h_bias_initializer, dtype)
-                if npj:
-                    self._register_param('{}{}_h2r_weight'.format(j, i), (npj, nh), h2r_weight_initializer, dtype)
-            ni = (npj or nh) * self._dir
+        for name, shape in self._param_specs():
+            kind = name.split('_', 1)[1]
+            p = self.params.get(name, shape=shape, init=self._inits[kind], allow_deferred_init=True, dtype=dtype)
+            setattr(self, name, p)
 
-    def _register_param(self, name, shape, init, dtype):
-        p = self.params.get(name, shape=shape, init=init, allow_deferred_init=True, dtype=dtype)
-        setattr(self, name, p)
-        return p
+    # ------------------------------------------------------------------ parameter layout
+    def _directions(self):
+        return 'lr'[:self._dir]
+
+    def _param_specs(self):
+        """(name, shape) of every parameter, in registration order."""
+        rows = self._gates * self._hidden_size
+        rec = self._projection_size or self._hidden_size
+        width = self._input_size
+        specs = []
+        for layer in range(self._num_layers):
+            for d in self._directions():
+                tag = '%s%d_' % (d, layer)
+                specs += [(tag + 'i2h_weight', (rows, width)), (tag + 'h2h_weight', (rows, rec)),
+                          (tag + 'i2h_bias', (rows,)), (tag + 'h2h_bias', (rows,))]
+                if self._projection_size:
+                    specs.append((tag + 'h2r_weight', (self._projection_size, self._hidden_size)))
+            width = rec * self._dir
+        return specs
+
+    def _flat_order(self):
+        """Parameter names in the fused operator's flat order: all weights, then all biases."""
+        groups = ('i2h', 'h2h', 'h2r') if self._projection_size else ('i2h', 'h2h')
+        names = []
+        for kind in ('weight', 'bias'):
+            for layer in range(self._num_layers):
+                for d in self._directions():
+                    names += ['%s%d_%s_%s' % (d, layer, g, kind) for g in groups
+                              if not (g == 'h2r' and kind == 'bias')]
+        return names
 
     def __repr__(self):
-        s = '{name}({mapping}, {_layout}'
+        w = self.l0_i2h_weight.shape
+        parts = ['%s -> %s' % (w[1] or None, w[0] // self._gates), self._layout]
         if self._num_layers != 1:
-            s += ', num_layers={_num_layers}'
+            parts.append('num_layers=%d' % self._num_layers)
         if self._dropout != 0:
-            s += ', dropout={_dropout}'
+            parts.append('dropout=%s' % self._dropout)
         if self._dir == 2:
-            s += ', bidirectional'
-        s += ')'
-        shape = self.l0_i2h_weight.shape
-        mapping = '{0} -> {1}'.format(shape[1] if shape[1] else None, shape[0] // self._gates)
-        return s.format(name=self.__class__.__name__, mapping=mapping, **self.__dict__)
+            parts.append('bidirectional')
+        return '%s(%s)' % (type(self).__name__, ', '.join(parts))
 
     def _collect_params_with_prefix(self, prefix=''):
-        # parameter-file names follow the unfused cell layout for compatibility with the reference
-        if prefix:
-            prefix += '.'
-        pattern = re.compile(r'(l|r)(\d+)_(i2h|h2h|h2r)_(weight|bias)\Z')
-
-        def convert_key(m, bidirectional):
-            d, l, g, t = [m.group(i) for i in range(1, 5)]
-            if bidirectional:
-                return '_unfused.{}.{}_cell.{}_{}'.format(l, d, g, t)
-            return '_unfused.{}.{}_{}'.format(l, g, t)
-        bidirectional = any(pattern.match(k).group(1) == 'r' for k in self._reg_params)
-        ret = {prefix + convert_key(pattern.match(key), bidirectional): val for key, val in self._reg_params.items()}
+        # saved names follow the unfused cell stack (`_unfused.<layer>[.<dir>_cell].<group>_<kind>`), the
+        # naming the reference writes, so checkpoints load into either form
+        lead = prefix + '.' if prefix else ''
+        bidir = self._dir == 2
+        out = {}
+        for key, val in self._reg_params.items():
+            m = _PARAM_RE.match(key)
+            cell = '%s.%s_cell' % (m.group('layer'), m.group('dir')) if bidir else m.group('layer')
+            out['%s_unfused.%s.%s_%s' % (lead, cell, m.group('group'), m.group('kind'))] = val
         for name, child in self._children.items():
-            ret.update(child._collect_params_with_prefix(prefix + name))
-        return ret
+            out.update(child._collect_params_with_prefix(lead + name))
+        return out
 
     def state_info(self, batch_size=0):
         raise NotImplementedError
 
+    def _state_spec(self, batch_size, width):
+        return {'shape': (self._num_layers * self._dir, batch_size, width), '__layout__': 'LNC',
+                'dtype': self._dtype}
+
+    # ------------------------------------------------------------------ unfused equivalent
+    def _make_cell(self, prefix, input_size):
+        kw = dict(prefix=prefix, input_size=input_size,
+                  i2h_weight_initializer=self._inits['i2h_weight'], h2h_weight_initializer=self._inits['h2h_weight'],
+                  i2h_bias_initializer=self._inits['i2h_bias'], h2h_bias_initializer=self._inits['h2h_bias'])
+        if self._mode == 'lstm':
+            return rnn_cell.LSTMCell(self._hidden_size, **kw)
+        if self._mode == 'gru':
+            return rnn_cell.GRUCell(self._hidden_size, **kw)
+        return rnn_cell.RNNCell(self._hidden_size, activation=self._mode[len('rnn_'):], **kw)
+
     def _unfuse(self):
-        """Equivalent stack of cells sharing this layer's parameters."""
-        assert not self._projection_size, '_unfuse does not support projection layer yet!'
-        assert not self._lstm_state_clip_min and not self._lstm_state_clip_max, \
-            '_unfuse does not support state clipping yet!'
-        get_cell = {'rnn_relu': lambda **kw: rnn_cell.RNNCell(self._hidden_size, activation='relu', **kw),
-                    'rnn_tanh': lambda **kw: rnn_cell.RNNCell(self._hidden_size, activation='tanh', **kw),
-                    'lstm': lambda **kw: rnn_cell.LSTMCell(self._hidden_size, **kw),
-                    'gru': lambda **kw: rnn_cell.GRUCell(self._hidden_size, **kw)}[self._mode]
+        """A HybridSequentialRNNCell computing the same function with this layer's parameters."""
+        if self._projection_size:
+            raise AssertionError('projection layers have no unfused cell equivalent')
+        if self._lstm_state_clip_min or self._lstm_state_clip_max:
+            raise AssertionError('state clipping has no unfused cell equivalent')
         stack = rnn_cell.HybridSequentialRNNCell(prefix=self.prefix, params=self.params)
         with stack.name_scope():
-            ni = self._input_size
-            for i in range(self._num_layers):
-                kwargs = {'input_size': ni, 'i2h_weight_initializer': self._i2h_weight_initializer,
-                          'h2h_weight_initializer': self._h2h_weight_initializer,
-                          'i2h_bias_initializer': self._i2h_bias_initializer,
-                          'h2h_bias_initializer': self._h2h_bias_initializer}
-                if self._dir == 2:
-                    stack.add(rnn_cell.BidirectionalCell(get_cell(prefix='l%d_' % i, **kwargs),
-                                                         get_cell(prefix='r%d_' % i, **kwargs)))
-                else:
-                    stack.add(get_cell(prefix='l%d_' % i, **kwargs))
-                if self._dropout > 0 and i != self._num_layers - 1:
+            width = self._input_size
+            last = self._num_layers - 1
+            for layer in range(self._num_layers):
+                cells = [self._make_cell('%s%d_' % (d, layer), width) for d in self._directions()]
+                stack.add(rnn_cell.BidirectionalCell(*cells) if len(cells) == 2 else cells[0])
+                if self._dropout > 0 and layer < last:
                     stack.add(rnn_cell.DropoutCell(self._dropout))
-                ni = self._hidden_size * self._dir
+                width = self._hidden_size * self._dir
         return stack
 
+    # ------------------------------------------------------------------ execution
     def cast(self, dtype):
         super().cast(dtype)
         self._dtype = dtype
 
     def begin_state(self, batch_size=0, func=ndarray.zeros, **kwargs):
+        symbolic = 'symbol' in getattr(func, '__module__', '')
         states = []
         for i, info in enumerate(self.state_info(batch_size)):
-            if info is not None:
-                info = dict(info)
-                info.update(kwargs)
-            else:
-                info = dict(kwargs)
-            info.pop('__layout__', None)
-            if 'symbol' in getattr(func, '__module__', ''):
-                info.pop('ctx', None)
-            states.append(func(name='%sh0_%d' % (self.prefix, i), **info))
+            spec = dict(info or {})
+            spec.update(kwargs)
+            spec.pop('__layout__', None)
+            if symbolic:
+                spec.pop('ctx', None)
+            states.append(func(name='%sh0_%d' % (self.prefix, i), **spec))
         return states
 
     def __call__(self, inputs, states=None, sequence_length=None, **kwargs):
         self.skip_states = states is None
         if states is None:
             if isinstance(inputs, NDArray):
-                batch_size = inputs.shape[self._layout.find('N')]
-                states = self.begin_state(batch_size, ctx=inputs.context, dtype=inputs.dtype)
+                n = inputs.shape[self._layout.index('N')]
+                states = self.begin_state(n, ctx=inputs.context, dtype=inputs.dtype)
             else:
                 states = self.begin_state(0, func=symbol.zeros)
         if isinstance(states, (NDArray, symbol.Symbol)):
             states = [states]
-        if self._use_sequence_length:
-            return super().__call__(inputs, states, sequence_length, **kwargs)
-        return super().__call__(inputs, states, **kwargs)
+        extra = (sequence_length,) if self._use_sequence_length else ()
+        return super().__call__(inputs, states, *extra, **kwargs)
 
     def hybrid_forward(self, F, inputs, states, sequence_length=None, **kwargs):
         if F is ndarray:
-            batch_size = inputs.shape[self._layout.find('N')]
-            for state, info in zip(states, self.state_info(batch_size)):
-                if state.shape != info['shape']:
+            n = inputs.shape[self._layout.index('N')]
+            for got, want in zip(states, self.state_info(n)):
+                if got.shape != want['shape']:
                     raise ValueError('Invalid recurrent state shape. Expecting %s, got %s.'
-                                     % (str(info['shape']), str(state.shape)))
+                                     % (str(want['shape']), str(got.shape)))
         out = self._forward_kernel(F, inputs, states, sequence_length, **kwargs)
         return out[0] if self.skip_states else out
 
     def _forward_kernel(self, F, inputs, states, sequence_length, **kwargs):
-        if self._layout == 'NTC':
+        time_major = self._layout == 'TNC'
+        if not time_major:
             inputs = F.swapaxes(inputs, dim1=0, dim2=1)
-        groups = ['i2h', 'h2h', 'h2r'] if self._projection_size else ['i2h', 'h2h']
-        params = [kwargs['{}{}_{}_{}'.format(d, l, g, t)].reshape(-1)
-                  for t in ['weight', 'bias']
-                  for l in range(self._num_layers)
-                  for d in ['l', 'r'][:self._dir]
-                  for g in groups if g != 'h2r' or t != 'bias']
-        params = F._internal._rnn_param_concat(*params, dim=0)
-        rnn_args = list(states) + ([sequence_length] if self._use_sequence_length else [])
-        rnn = F.RNN(inputs, params, *rnn_args, use_sequence_length=self._use_sequence_length,
+        flat = F._internal._rnn_param_concat(*[kwargs[n].reshape(-1) for n in self._flat_order()], dim=0)
+        args = list(states)
+        if self._use_sequence_length:
+            args.append(sequence_length)
+        res = F.RNN(inputs, flat, *args, use_sequence_length=self._use_sequence_length,
                     state_size=self._hidden_size, projection_size=self._projection_size,
                     num_layers=self._num_layers, bidirectional=self._dir == 2, p=self._dropout, state_outputs=True,
                     mode=self._mode, lstm_state_clip_min=self._lstm_state_clip_min,
                     lstm_state_clip_max=self._lstm_state_clip_max, lstm_state_clip_nan=self._lstm_state_clip_nan)
-        if self._mode == 'lstm':
-            outputs, states = rnn[0], [rnn[1], rnn[2]]
-        else:
-            outputs, states = rnn[0], [rnn[1]]
-        if self._layout == 'NTC':
+        nstate = 2 if self._mode == 'lstm' else 1
+        outputs, new_states = res[0], [res[1 + i] for i in range(nstate)]
+        if not time_major:
             outputs = F.swapaxes(outputs, dim1=0, dim2=1)
-        return outputs, states
+        return outputs, new_states
 
 
 class RNN(_RNNLayer):
@@ -198,8 +222,7 @@ class RNN(_RNNLayer):
                          'rnn_' + activation, None, None, None, None, False, dtype, **kwargs)
 
     def state_info(self, batch_size=0):
-        return [{'shape': (self._num_layers * self._dir, batch_size, self._hidden_size), '__layout__': 'LNC',
-                 'dtype': self._dtype}]
+        return [self._state_spec(batch_size, self._hidden_size)]
 
 
 class LSTM(_RNNLayer):
@@ -215,15 +238,8 @@ class LSTM(_RNNLayer):
                          state_clip_nan, dtype, **kwargs)
 
     def state_info(self, batch_size=0):
-        if self._projection_size is None:
-            return [{'shape': (self._num_layers * self._dir, batch_size, self._hidden_size), '__layout__': 'LNC',
-                     'dtype': self._dtype},
-                    {'shape': (self._num_layers * self._dir, batch_size, self._hidden_size), '__layout__': 'LNC',
-                     'dtype': self._dtype}]
-        return [{'shape': (self._num_layers * self._dir, batch_size, self._projection_size), '__layout__': 'LNC',
-                 'dtype': self._dtype},
-                {'shape': (self._num_layers * self._dir, batch_size, self._hidden_size), '__layout__': 'LNC',
-                 'dtype': self._dtype}]
+        h = self._projection_size or self._hidden_size
+        return [self._state_spec(batch_size, h), self._state_spec(batch_size, self._hidden_size)]
 
 
 class GRU(_RNNLayer):
@@ -237,5 +253,4 @@ class GRU(_RNNLayer):
                          'gru', None, None, None, None, False, dtype, **kwargs)
 
     def state_info(self, batch_size=0):
-        return [{'shape': (self._num_layers * self._dir, batch_size, self._hidden_size), '__layout__': 'LNC',
-                 'dtype': self._dtype}]
+        return [self._state_spec(batch_size, self._hidden_size)]

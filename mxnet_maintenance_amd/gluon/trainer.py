@@ -186,6 +186,10 @@ class Trainer:
         if isinstance(kvstore, (_kvs.KVStoreBase,)):
             kv = kvstore
         elif kvstore is None or kvstore is False:
+            if sparse_weight:
+                # reference trainer.py _create_sparse_kvstore: sparse weights live on a kvstore
+                raise TypeError('Cannot create a KVStore with row_sparse weights when kvstore=%s; '
+                                'pass a kvstore type such as "local" or "device".' % (kvstore,))
             kv = None
         else:
             # reference: no kvstore for one device on one machine unless the weights are sparse

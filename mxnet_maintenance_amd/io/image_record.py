@@ -69,6 +69,11 @@ class _PinnedRing:
         self._ptrs = [self._store.alloc(nbytes) for _ in range(count)]
         self._nbytes = nbytes
         self._i = 0
+        if self.pinned:
+            # take() waits for pending H2D reads of a slot before reusing it: copies may read in place
+            from .. import engine     # pylint: disable=import-outside-toplevel
+            for p in self._ptrs:
+                engine.register_owned_pinned(p, nbytes)
 
     def take(self, shape, dtype):
         ptr = self._ptrs[self._i % len(self._ptrs)]
@@ -82,7 +87,9 @@ class _PinnedRing:
 
     def __del__(self):
         try:
+            from .. import engine     # pylint: disable=import-outside-toplevel
             for p in self._ptrs:
+                engine.unregister_owned_pinned(p)
                 self._store.free(p)
             self._store.release_all()
         except Exception:      # pylint: disable=broad-except

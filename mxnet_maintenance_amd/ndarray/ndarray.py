@@ -454,6 +454,10 @@ class NDArray:
             if not t.is_floating_point():
                 raise MXNetError('Inplace operations (+=, -=, x[:]=, etc) are not supported when recording with '
                                  'autograd: the %s target cannot carry the value\'s gradient' % t.dtype)
+            if t._base is not None:
+                # replacing a view's storage would silently detach it from its parent array
+                raise MXNetError('Inplace operations (+=, -=, x[:]=, etc) are not supported when recording with '
+                                 'autograd: the target is a view of another array')
             new = t.detach().clone()
             new[key] = v.to(new.device, new.dtype)
             self._data = new
@@ -478,7 +482,13 @@ class NDArray:
             while v.dim() > key.dim() and v.shape[0] == 1:
                 v = v[0]
             with torch.no_grad():
-                t.view(-1)[key.reshape(-1)] = v.expand(key.shape).reshape(-1)
+                vals = v.expand(key.shape).reshape(-1)
+                if t.is_contiguous():
+                    t.view(-1)[key.reshape(-1)] = vals
+                else:
+                    # strided / transposed target: scatter through the unravelled indices
+                    idx = torch.unravel_index(key.reshape(-1), t.shape)
+                    t[idx] = vals
             return
         if flips:
             # negative-step slices: write the mirrored positive-step slice with the value flipped
