@@ -19,47 +19,36 @@ __all__ = ['RNNParams', 'BaseRNNCell', 'RNNCell', 'LSTMCell', 'GRUCell', 'FusedR
            'BaseConvRNNCell', 'ConvRNNCell', 'ConvLSTMCell', 'ConvGRUCell']
 
 
-def _cells_state_info(cells):
-    return [info for c in cells for info in c.state_info]
+def _time_major_split(length, inputs, layout, merge, in_layout=None):
+    """Bring ``inputs`` into the requested form and return (inputs, time axis of ``layout``).
 
-
-def _cells_begin_state(cells, **kwargs):
-    return [s for c in cells for s in c.begin_state(**kwargs)]
-
-
-def _cells_unpack_weights(cells, args):
-    for c in cells:
-        args = c.unpack_weights(args)
-    return args
-
-
-def _cells_pack_weights(cells, args):
-    for c in cells:
-        args = c.pack_weights(args)
-    return args
-
-
-def _normalize_sequence(length, inputs, layout, merge, in_layout=None):
-    """Inputs as either one merged Symbol (time along ``layout``'s T axis) or a list of ``length``
-    per-step Symbols; returns (inputs, time_axis)."""
+    ``merge`` True: one Symbol with time on the layout's T axis; False: a list of ``length``
+    per-step Symbols; None: leave whichever form was given.  ``in_layout`` names the layout of a
+    merged input when it differs from ``layout``."""
     if inputs is None:
         raise AssertionError('unroll(inputs=None) is not supported; pass the input symbol(s)')
-    axis = layout.find('T')
-    in_axis = in_layout.find('T') if in_layout is not None else axis
-    if isinstance(inputs, symbol.Symbol):
-        if merge is False:
-            if len(inputs.list_outputs()) != 1:
-                raise AssertionError('unroll needs a single-output input symbol or a list of symbols')
-            inputs = list(symbol.split(inputs, axis=in_axis, num_outputs=length, squeeze_axis=1))
-    else:
+    t_axis = layout.find('T')
+    src_axis = t_axis if in_layout is None else in_layout.find('T')
+    merged = isinstance(inputs, symbol.Symbol)
+    if merged and merge is False:
+        if len(inputs.list_outputs()) != 1:
+            raise AssertionError('unroll needs a single-output input symbol or a list of symbols')
+        steps = symbol.split(inputs, axis=src_axis, num_outputs=length, squeeze_axis=1)
+        return list(steps), t_axis
+    if not merged:
         if length is not None and len(inputs) != length:
             raise AssertionError('unroll length %s but %d input steps' % (length, len(inputs)))
-        if merge is True:
-            inputs = symbol.Concat(*[symbol.expand_dims(i, axis=axis) for i in inputs], dim=axis)
-            in_axis = axis
-    if isinstance(inputs, symbol.Symbol) and axis != in_axis:
-        inputs = symbol.swapaxes(inputs, dim0=axis, dim1=in_axis)
-    return inputs, axis
+        if merge is not True:
+            return inputs, t_axis
+        inputs = symbol.Concat(*[symbol.expand_dims(step, axis=t_axis) for step in inputs], dim=t_axis)
+        src_axis = t_axis
+    if src_axis != t_axis:
+        inputs = symbol.swapaxes(inputs, dim0=t_axis, dim1=src_axis)
+    return inputs, t_axis
+
+
+# kept under the reference's private name for code written against it
+_normalize_sequence = _time_major_split
 
 
 class RNNParams:
@@ -71,23 +60,25 @@ class RNNParams:
 
     def get(self, name, **kwargs):
         """The Variable ``<prefix><name>`` (created on first request with ``kwargs``)."""
-        full = self._prefix + name
-        if full not in self._params:
-            self._params[full] = symbol.Variable(full, **kwargs)
-        return self._params[full]
+        key = self._prefix + name
+        var = self._params.get(key)
+        if var is None:
+            var = self._params[key] = symbol.Variable(key, **kwargs)
+        return var
 
 
 class BaseRNNCell:
-    """Abstract cell: subclasses implement ``state_info`` and ``__call__``."""
+    """Abstract cell: subclasses implement ``state_info`` and ``__call__``.
+
+    Subclasses with fused gates list the per-gate name suffixes in ``_GATES`` (their order is the
+    row order of the fused i2h / h2h weights)."""
+
+    _GATES = ()
 
     def __init__(self, prefix='', params=None):
-        if params is None:
-            params = RNNParams(prefix)
-            self._own_params = True
-        else:
-            self._own_params = False
+        self._owns_params = params is None
         self._prefix = prefix
-        self._params = params
+        self._params = RNNParams(prefix) if params is None else params
         self._modified = False
         self.reset()
 
@@ -95,16 +86,16 @@ class BaseRNNCell:
         """Forget the time-step counters (call before building a new graph)."""
         self._init_counter = -1
         self._counter = -1
-        if hasattr(self, '_cells'):
-            for c in self._cells:
-                c.reset()
+        for child in getattr(self, '_cells', ()):
+            child.reset()
 
     def __call__(self, inputs, states):
         raise NotImplementedError
 
     @property
     def params(self):
-        self._own_params = False
+        # once a caller holds the container it may be shared: the cell no longer owns it exclusively
+        self._owns_params = False
         return self._params
 
     @property
@@ -117,74 +108,85 @@ class BaseRNNCell:
 
     @property
     def _gate_names(self):
-        return ()
+        return self._GATES
 
-    def begin_state(self, func=symbol.zeros, **kwargs):
-        """Initial states (zeros by default; batch dimension 0 = inferred at bind time)."""
+    def _check_unmodified(self):
         if self._modified:
             raise AssertionError('after applying a modifier cell (e.g. ZoneoutCell) the base cell '
                                  'cannot be called directly; call the modifier cell instead')
-        states = []
+
+    def begin_state(self, func=symbol.zeros, **kwargs):
+        """Initial states (zeros by default; batch dimension 0 = inferred at bind time)."""
+        self._check_unmodified()
+        out = []
         for info in self.state_info:
             self._init_counter += 1
-            name = '%sbegin_state_%d' % (self._prefix, self._init_counter)
-            kw = dict(kwargs)
-            if info is not None:
-                kw.update(info)
-            states.append(func(name=name, **kw))
-        return states
+            spec = dict(kwargs)
+            spec.update(info or {})
+            out.append(func(name='%sbegin_state_%d' % (self._prefix, self._init_counter), **spec))
+        return out
+
+    def _standard_params(self, i2h_bias_init=None):
+        """The four fused-gate Variables of a single-layer cell."""
+        get = self.params.get
+        self._iW = get('i2h_weight')
+        self._hW = get('h2h_weight')
+        self._iB = get('i2h_bias') if i2h_bias_init is None else get('i2h_bias', init=i2h_bias_init)
+        self._hB = get('h2h_bias')
+
+    def _nc_states(self, count):
+        return [{'shape': (0, self._num_hidden), '__layout__': 'NC'} for _ in range(count)]
 
     # ---------------------------------------------------------------- (un)packing
+    def _gate_key(self, group, gate, kind):
+        return '%s%s%s_%s' % (self._prefix, group, gate, kind)
+
     def unpack_weights(self, args):
         """Split fused gate weights/biases in ``args`` into per-gate entries."""
-        args = dict(args)
-        if not self._gate_names:
-            return args
-        h = self._num_hidden
-        for group in ('i2h', 'h2h'):
-            w = args.pop('%s%s_weight' % (self._prefix, group))
-            b = args.pop('%s%s_bias' % (self._prefix, group))
-            for j, gate in enumerate(self._gate_names):
-                args['%s%s%s_weight' % (self._prefix, group, gate)] = w[j * h:(j + 1) * h].copy()
-                args['%s%s%s_bias' % (self._prefix, group, gate)] = b[j * h:(j + 1) * h].copy()
-        return args
+        out = dict(args)
+        rows = getattr(self, '_num_hidden', 0)
+        for group in ('i2h', 'h2h') if self._gate_names else ():
+            for kind in ('weight', 'bias'):
+                fused = out.pop(self._gate_key(group, '', kind))
+                for j, gate in enumerate(self._gate_names):
+                    out[self._gate_key(group, gate, kind)] = fused[j * rows:(j + 1) * rows].copy()
+        return out
 
     def pack_weights(self, args):
         """Inverse of ``unpack_weights``."""
         from .. import ndarray as nd
-        args = dict(args)
-        if not self._gate_names:
-            return args
-        for group in ('i2h', 'h2h'):
+        out = dict(args)
+        for group in ('i2h', 'h2h') if self._gate_names else ():
             for kind in ('weight', 'bias'):
-                parts = [args.pop('%s%s%s_%s' % (self._prefix, group, gate, kind)) for gate in self._gate_names]
-                args['%s%s_%s' % (self._prefix, group, kind)] = nd.concat(*parts, dim=0)
-        return args
+                pieces = [out.pop(self._gate_key(group, gate, kind)) for gate in self._gate_names]
+                out[self._gate_key(group, '', kind)] = nd.concat(*pieces, dim=0)
+        return out
 
     # ---------------------------------------------------------------- unrolling
     def unroll(self, length, inputs, begin_state=None, layout='NTC', merge_outputs=None):
         """Apply the cell ``length`` times; returns (outputs, states)."""
         self.reset()
-        inputs, _ = _normalize_sequence(length, inputs, layout, False)
-        states = self.begin_state() if begin_state is None else begin_state
-        outputs = []
-        for t in range(length):
-            out, states = self(inputs[t], states)
-            outputs.append(out)
-        outputs, _ = _normalize_sequence(length, outputs, layout, merge_outputs)
-        return outputs, states
+        steps, _ = _time_major_split(length, inputs, layout, False)
+        states = begin_state if begin_state is not None else self.begin_state()
+        outs = []
+        for x in steps:
+            y, states = self(x, states)
+            outs.append(y)
+        outs, _ = _time_major_split(length, outs, layout, merge_outputs)
+        return outs, states
 
     def _get_activation(self, inputs, activation, **kwargs):
-        if isinstance(activation, string_types):
-            return symbol.Activation(inputs, act_type=activation, **kwargs)
-        return activation(inputs, **kwargs)
+        if not isinstance(activation, string_types):
+            return activation(inputs, **kwargs)
+        return symbol.Activation(inputs, act_type=activation, **kwargs)
 
-    def _fc_pair(self, inputs, prev_h, gates, name):
-        """i2h(inputs) and h2h(prev_h) projections for ``gates`` fused gates."""
-        n = gates * self._num_hidden
-        i2h = symbol.FullyConnected(data=inputs, weight=self._iW, bias=self._iB, num_hidden=n, name=name + 'i2h')
-        h2h = symbol.FullyConnected(data=prev_h, weight=self._hW, bias=self._hB, num_hidden=n, name=name + 'h2h')
-        return i2h, h2h
+    def _fc_pair(self, inputs, prev_h, name):
+        """i2h(inputs) and h2h(prev_h) projections for all of the cell's fused gates."""
+        width = len(self._gate_names) * self._num_hidden
+        return (symbol.FullyConnected(data=inputs, weight=self._iW, bias=self._iB, num_hidden=width,
+                                      name=name + 'i2h'),
+                symbol.FullyConnected(data=prev_h, weight=self._hW, bias=self._hB, num_hidden=width,
+                                      name=name + 'h2h'))
 
     def _step_name(self):
         self._counter += 1
@@ -194,284 +196,288 @@ class BaseRNNCell:
 class RNNCell(BaseRNNCell):
     """Elman cell: h' = act(W_i x + b_i + W_h h + b_h)."""
 
+    _GATES = ('',)
+
     def __init__(self, num_hidden, activation='tanh', prefix='rnn_', params=None):
         super().__init__(prefix=prefix, params=params)
         self._num_hidden = num_hidden
         self._activation = activation
-        self._iW = self.params.get('i2h_weight')
-        self._iB = self.params.get('i2h_bias')
-        self._hW = self.params.get('h2h_weight')
-        self._hB = self.params.get('h2h_bias')
+        self._standard_params()
 
     @property
     def state_info(self):
-        return [{'shape': (0, self._num_hidden), '__layout__': 'NC'}]
-
-    @property
-    def _gate_names(self):
-        return ('',)
+        return self._nc_states(1)
 
     def __call__(self, inputs, states):
-        name = self._step_name()
-        i2h, h2h = self._fc_pair(inputs, states[0], 1, name)
-        out = self._get_activation(i2h + h2h, self._activation, name=name + 'out')
-        return out, [out]
+        tag = self._step_name()
+        i2h, h2h = self._fc_pair(inputs, states[0], tag)
+        h = self._get_activation(i2h + h2h, self._activation, name=tag + 'out')
+        return h, [h]
 
 
 class LSTMCell(BaseRNNCell):
     """Long short-term memory cell; ``forget_bias`` initialises the forget-gate bias."""
 
+    _GATES = ('_i', '_f', '_c', '_o')
+
     def __init__(self, num_hidden, prefix='lstm_', params=None, forget_bias=1.0):
         super().__init__(prefix=prefix, params=params)
         self._num_hidden = num_hidden
-        self._iW = self.params.get('i2h_weight')
-        self._hW = self.params.get('h2h_weight')
-        self._iB = self.params.get('i2h_bias', init=init.LSTMBias(forget_bias=forget_bias))
-        self._hB = self.params.get('h2h_bias')
+        self._standard_params(i2h_bias_init=init.LSTMBias(forget_bias=forget_bias))
 
     @property
     def state_info(self):
-        return [{'shape': (0, self._num_hidden), '__layout__': 'NC'},
-                {'shape': (0, self._num_hidden), '__layout__': 'NC'}]
-
-    @property
-    def _gate_names(self):
-        return ('_i', '_f', '_c', '_o')
+        return self._nc_states(2)
 
     def __call__(self, inputs, states):
-        name = self._step_name()
-        i2h, h2h = self._fc_pair(inputs, states[0], 4, name)
-        gates = symbol.SliceChannel(i2h + h2h, num_outputs=4, name=name + 'slice')
-        in_gate = symbol.Activation(gates[0], act_type='sigmoid', name=name + 'i')
-        forget_gate = symbol.Activation(gates[1], act_type='sigmoid', name=name + 'f')
-        in_transform = symbol.Activation(gates[2], act_type='tanh', name=name + 'c')
-        out_gate = symbol.Activation(gates[3], act_type='sigmoid', name=name + 'o')
-        next_c = symbol._internal._plus(forget_gate * states[1], in_gate * in_transform, name=name + 'state')
-        next_h = symbol._internal._mul(out_gate, symbol.Activation(next_c, act_type='tanh'), name=name + 'out')
-        return next_h, [next_h, next_c]
+        tag = self._step_name()
+        i2h, h2h = self._fc_pair(inputs, states[0], tag)
+        pre = symbol.SliceChannel(i2h + h2h, num_outputs=4, name=tag + 'slice')
+        act = [symbol.Activation(pre[k], act_type='tanh' if k == 2 else 'sigmoid', name=tag + 'ifco'[k])
+               for k in range(4)]
+        c = symbol._internal._plus(act[1] * states[1], act[0] * act[2], name=tag + 'state')
+        h = symbol._internal._mul(act[3], symbol.Activation(c, act_type='tanh'), name=tag + 'out')
+        return h, [h, c]
 
 
 class GRUCell(BaseRNNCell):
     """Gated recurrent unit (Cho et al. 2014), cuDNN / fused-op variant."""
 
+    _GATES = ('_r', '_z', '_o')
+
     def __init__(self, num_hidden, prefix='gru_', params=None):
         super().__init__(prefix=prefix, params=params)
         self._num_hidden = num_hidden
-        self._iW = self.params.get('i2h_weight')
-        self._iB = self.params.get('i2h_bias')
-        self._hW = self.params.get('h2h_weight')
-        self._hB = self.params.get('h2h_bias')
+        self._standard_params()
 
     @property
     def state_info(self):
-        return [{'shape': (0, self._num_hidden), '__layout__': 'NC'}]
-
-    @property
-    def _gate_names(self):
-        return ('_r', '_z', '_o')
+        return self._nc_states(1)
 
     def __call__(self, inputs, states):
-        name = self._step_name()
-        prev_h = states[0]
-        i2h, h2h = self._fc_pair(inputs, prev_h, 3, name)
-        i_r, i_z, i_n = symbol.SliceChannel(i2h, num_outputs=3, name=name + 'i2h_slice')
-        h_r, h_z, h_n = symbol.SliceChannel(h2h, num_outputs=3, name=name + 'h2h_slice')
-        reset = symbol.Activation(i_r + h_r, act_type='sigmoid', name=name + 'r_act')
-        update = symbol.Activation(i_z + h_z, act_type='sigmoid', name=name + 'z_act')
-        cand = symbol.Activation(i_n + reset * h_n, act_type='tanh', name=name + 'h_act')
-        next_h = symbol._internal._plus((1. - update) * cand, update * prev_h, name=name + 'out')
-        return next_h, [next_h]
+        tag = self._step_name()
+        h_prev = states[0]
+        i2h, h2h = self._fc_pair(inputs, h_prev, tag)
+        xr, xz, xn = symbol.SliceChannel(i2h, num_outputs=3, name=tag + 'i2h_slice')
+        hr, hz, hn = symbol.SliceChannel(h2h, num_outputs=3, name=tag + 'h2h_slice')
+        r = symbol.Activation(xr + hr, act_type='sigmoid', name=tag + 'r_act')
+        z = symbol.Activation(xz + hz, act_type='sigmoid', name=tag + 'z_act')
+        n = symbol.Activation(xn + r * hn, act_type='tanh', name=tag + 'h_act')
+        h = symbol._internal._plus((1. - z) * n, z * h_prev, name=tag + 'out')
+        return h, [h]
+
+
+_MODE_GATES = {'rnn_relu': RNNCell._GATES, 'rnn_tanh': RNNCell._GATES, 'lstm': LSTMCell._GATES,
+               'gru': GRUCell._GATES}
 
 
 class FusedRNNCell(BaseRNNCell):
     """Multi-layer (bi)directional RNN on the fused ``RNN`` operator (one flat parameter Variable)."""
 
-    _GATES = {'rnn_relu': ('',), 'rnn_tanh': ('',), 'lstm': ('_i', '_f', '_c', '_o'), 'gru': ('_r', '_z', '_o')}
-
     def __init__(self, num_hidden, num_layers=1, mode='lstm', bidirectional=False, dropout=0., get_next_state=False,
                  forget_bias=1.0, prefix=None, params=None):
-        if prefix is None:
-            prefix = '%s_' % mode
-        super().__init__(prefix=prefix, params=params)
+        super().__init__(prefix='%s_' % mode if prefix is None else prefix, params=params)
         self._num_hidden = num_hidden
         self._num_layers = num_layers
         self._mode = mode
         self._bidirectional = bidirectional
         self._dropout = dropout
         self._get_next_state = get_next_state
-        self._directions = ['l', 'r'] if bidirectional else ['l']
-        initializer = init.FusedRNN(None, num_hidden, num_layers, mode, bidirectional, forget_bias)
-        self._parameter = self.params.get('parameters', init=initializer)
+        self._dirs = 'lr' if bidirectional else 'l'
+        self._directions = list(self._dirs)
+        flat_init = init.FusedRNN(None, num_hidden, num_layers, mode, bidirectional, forget_bias)
+        self._parameter = self.params.get('parameters', init=flat_init)
+
+    @property
+    def _GATES(self):      # noqa: N802 -- per-instance: depends on the mode
+        return _MODE_GATES[self._mode]
 
     @property
     def state_info(self):
-        b = len(self._directions)
-        n = 2 if self._mode == 'lstm' else 1
-        return [{'shape': (b * self._num_layers, 0, self._num_hidden), '__layout__': 'LNC'}] * n
-
-    @property
-    def _gate_names(self):
-        return self._GATES[self._mode]
+        shape = (len(self._dirs) * self._num_layers, 0, self._num_hidden)
+        return [{'shape': shape, '__layout__': 'LNC'} for _ in range(2 if self._mode == 'lstm' else 1)]
 
     @property
     def _num_gates(self):
-        return len(self._gate_names)
+        return len(self._GATES)
+
+    def _layout_pieces(self, input_size):
+        """(name, offset, shape) of every per-(layer, direction, gate) piece of the flat vector, and
+        its total length: all weights (i2h then h2h per layer/direction) first, then all biases."""
+        h, nd_ = self._num_hidden, len(self._dirs)
+        pieces, pos = [], 0
+        for kind in ('weight', 'bias'):
+            for layer in range(self._num_layers):
+                width = input_size if layer == 0 else h * nd_
+                for d in self._dirs:
+                    for group, cols in (('i2h', width), ('h2h', h)):
+                        for gate in self._GATES:
+                            shape = (h, cols) if kind == 'weight' else (h,)
+                            name = '%s%s%d_%s%s_%s' % (self._prefix, d, layer, group, gate, kind)
+                            pieces.append((name, pos, shape))
+                            pos += h * (cols if kind == 'weight' else 1)
+        return pieces, pos
 
     def _slice_weights(self, arr, li, lh):
-        """Views of the per-(layer, direction, gate) pieces of the flat parameter array ``arr``
-        (``li``: input size of layer 0, ``lh``: hidden size), keyed by unfused names."""
-        out = {}
-        g = self._num_gates
-        h = self._num_hidden
-        pos = 0
-        for layer in range(self._num_layers):
-            for d in self._directions:
-                width = li if layer == 0 else lh * len(self._directions)
-                for group, cols in (('i2h', width), ('h2h', lh)):
-                    for gate in self._gate_names:
-                        name = '%s%s%d_%s%s_weight' % (self._prefix, d, layer, group, gate)
-                        out[name] = arr[pos:pos + h * cols].reshape((h, cols))
-                        pos += h * cols
-        for layer in range(self._num_layers):
-            for d in self._directions:
-                for group in ('i2h', 'h2h'):
-                    for gate in self._gate_names:
-                        out['%s%s%d_%s%s_bias' % (self._prefix, d, layer, group, gate)] = arr[pos:pos + h]
-                        pos += h
-        if pos != arr.size:
-            raise AssertionError('parameter vector of %d elements, expected %d' % (arr.size, pos))
-        return out
+        """Views of the per-(layer, direction, gate) pieces of ``arr`` keyed by unfused names."""
+        del lh    # the hidden size is the cell's own
+        pieces, total = self._layout_pieces(li)
+        if total != arr.size:
+            raise AssertionError('parameter vector of %d elements, expected %d' % (arr.size, total))
+        return {name: arr[off:off + _prod(shape)].reshape(shape) for name, off, shape in pieces}
 
     def _input_size(self, total):
         """Layer-0 input size implied by a flat parameter count."""
-        g, h, d, L = self._num_gates, self._num_hidden, len(self._directions), self._num_layers
-        rest = (L - 1) * d * g * h * (h * d + h + 2) + d * g * h * (h + 2)
-        return (total - rest) // (d * g * h)
+        g, h, d = self._num_gates, self._num_hidden, len(self._dirs)
+        deeper = (self._num_layers - 1) * d * g * h * (h * d + h + 2)
+        return (total - deeper - d * g * h * (h + 2)) // (d * g * h)
 
     def unpack_weights(self, args):
-        args = dict(args)
-        arr = args.pop(self._parameter.name)
-        li = self._input_size(arr.size)
-        for k, v in self._slice_weights(arr, li, self._num_hidden).items():
-            args[k] = v.copy()
-        return args
+        out = dict(args)
+        flat = out.pop(self._parameter.name)
+        for name, view in self._slice_weights(flat, self._input_size(flat.size), self._num_hidden).items():
+            out[name] = view.copy()
+        return out
 
     def pack_weights(self, args):
         from .. import ndarray as nd
-        args = dict(args)
-        w0 = args['%sl0_i2h%s_weight' % (self._prefix, self._gate_names[0])]
-        li = w0.shape[1]
-        total = self._num_gates * self._num_hidden * len(self._directions) * (
-            li + self._num_hidden + 2) + (self._num_layers - 1) * len(self._directions) * self._num_gates * \
-            self._num_hidden * (self._num_hidden * len(self._directions) + self._num_hidden + 2)
-        arr = nd.zeros((total,), ctx=w0.context, dtype=w0.dtype)
-        for k, v in self._slice_weights(arr, li, self._num_hidden).items():
-            v[:] = args.pop(k).reshape(v.shape)
-        args[self._parameter.name] = arr
-        return args
+        out = dict(args)
+        first = out['%sl0_i2h%s_weight' % (self._prefix, self._GATES[0])]
+        pieces, total = self._layout_pieces(first.shape[1])
+        flat = nd.zeros((total,), ctx=first.context, dtype=first.dtype)
+        for name, off, shape in pieces:
+            flat[off:off + _prod(shape)] = out.pop(name).reshape((-1,))
+        out[self._parameter.name] = flat
+        return out
 
     def __call__(self, inputs, states):
         raise NotImplementedError('FusedRNNCell cannot be stepped; use unroll')
 
     def unroll(self, length, inputs, begin_state=None, layout='NTC', merge_outputs=None):
         self.reset()
-        inputs, axis = _normalize_sequence(length, inputs, layout, True)
-        if axis == 1:
+        seq, t_axis = _time_major_split(length, inputs, layout, True)
+        batch_major = t_axis == 1
+        if batch_major:
             warnings.warn('NTC layout detected: FusedRNNCell runs in TNC, inputs are transposed')
-            inputs = symbol.swapaxes(inputs, dim0=0, dim1=1)
-        states = self.begin_state() if begin_state is None else begin_state
-        kw = {'state_cell': states[1]} if self._mode == 'lstm' else {}
-        rnn = symbol.RNN(data=inputs, parameters=self._parameter, state=states[0], state_size=self._num_hidden,
+            seq = symbol.swapaxes(seq, dim0=0, dim1=1)
+        states = begin_state if begin_state is not None else self.begin_state()
+        extra = {'state_cell': states[1]} if self._mode == 'lstm' else {}
+        res = symbol.RNN(data=seq, parameters=self._parameter, state=states[0], state_size=self._num_hidden,
                          num_layers=self._num_layers, bidirectional=self._bidirectional, p=self._dropout,
-                         state_outputs=self._get_next_state, mode=self._mode, name=self._prefix + 'rnn', **kw)
-        if not self._get_next_state:
-            outputs, states = rnn, []
-        elif self._mode == 'lstm':
-            outputs, states = rnn[0], [rnn[1], rnn[2]]
+                         state_outputs=self._get_next_state, mode=self._mode, name=self._prefix + 'rnn', **extra)
+        if self._get_next_state:
+            outs = res[0]
+            new_states = [res[k] for k in range(1, 3 if self._mode == 'lstm' else 2)]
         else:
-            outputs, states = rnn[0], [rnn[1]]
-        if axis == 1:
-            outputs = symbol.swapaxes(outputs, dim0=0, dim1=1)
-        outputs, _ = _normalize_sequence(length, outputs, layout, merge_outputs)
-        return outputs, states
+            outs, new_states = res, []
+        if batch_major:
+            outs = symbol.swapaxes(outs, dim0=0, dim1=1)
+        outs, _ = _time_major_split(length, outs, layout, merge_outputs)
+        return outs, new_states
 
     def unfuse(self):
         """An equivalent ``SequentialRNNCell`` of unfused cells (weights via unpack_weights)."""
-        make = {'rnn_relu': lambda p: RNNCell(self._num_hidden, activation='relu', prefix=p),
-                'rnn_tanh': lambda p: RNNCell(self._num_hidden, activation='tanh', prefix=p),
-                'lstm': lambda p: LSTMCell(self._num_hidden, prefix=p),
-                'gru': lambda p: GRUCell(self._num_hidden, prefix=p)}[self._mode]
+        def cell(pfx):
+            if self._mode == 'lstm':
+                return LSTMCell(self._num_hidden, prefix=pfx)
+            if self._mode == 'gru':
+                return GRUCell(self._num_hidden, prefix=pfx)
+            return RNNCell(self._num_hidden, activation=self._mode[len('rnn_'):], prefix=pfx)
         stack = SequentialRNNCell()
-        for i in range(self._num_layers):
+        for layer in range(self._num_layers):
+            fwd = cell('%sl%d_' % (self._prefix, layer))
             if self._bidirectional:
-                stack.add(BidirectionalCell(make('%sl%d_' % (self._prefix, i)), make('%sr%d_' % (self._prefix, i)),
-                                            output_prefix='%sbi_l%d_' % (self._prefix, i)))
+                stack.add(BidirectionalCell(fwd, cell('%sr%d_' % (self._prefix, layer)),
+                                            output_prefix='%sbi_l%d_' % (self._prefix, layer)))
             else:
-                stack.add(make('%sl%d_' % (self._prefix, i)))
-            if self._dropout > 0 and i != self._num_layers - 1:
-                stack.add(DropoutCell(self._dropout, prefix='%s_dropout%d_' % (self._prefix, i)))
+                stack.add(fwd)
+            if self._dropout > 0 and layer + 1 < self._num_layers:
+                stack.add(DropoutCell(self._dropout, prefix='%s_dropout%d_' % (self._prefix, layer)))
         return stack
 
 
-class SequentialRNNCell(BaseRNNCell):
+def _prod(shape):
+    n = 1
+    for s in shape:
+        n *= s
+    return n
+
+
+class _Container(BaseRNNCell):
+    """A cell built from child cells (``self._cells``): states, weights and parameters are the
+    concatenation of the children's."""
+
+    def _adopt(self, children, shared):
+        """Merge the children's Variables into this container's (and, when this container was given
+        ``params``, the container's into every child's first)."""
+        for child in children:
+            if shared:
+                if not child._owns_params:
+                    raise AssertionError('with params given to the container, child cells must own theirs')
+                child.params._params.update(self._params._params)
+        for child in children:
+            self._params._params.update(child.params._params)
+
+    @property
+    def state_info(self):
+        return [info for child in self._cells for info in child.state_info]
+
+    def begin_state(self, **kwargs):
+        self._check_unmodified()
+        return [st for child in self._cells for st in child.begin_state(**kwargs)]
+
+    def unpack_weights(self, args):
+        for child in self._cells:
+            args = child.unpack_weights(args)
+        return args
+
+    def pack_weights(self, args):
+        for child in self._cells:
+            args = child.pack_weights(args)
+        return args
+
+    def _per_child(self, states):
+        """``states`` cut into the children's consecutive slices."""
+        cuts, at = [], 0
+        for child in self._cells:
+            n = len(child.state_info)
+            cuts.append(states[at:at + n])
+            at += n
+        return cuts
+
+
+class SequentialRNNCell(_Container):
     """Stack of cells: the output of cell i is the input of cell i+1."""
 
     def __init__(self, params=None):
         super().__init__(prefix='', params=params)
-        self._override_cell_params = params is not None
+        self._shared = params is not None
         self._cells = []
 
     def add(self, cell):
         self._cells.append(cell)
-        if self._override_cell_params:
-            if not cell._own_params:
-                raise AssertionError('with params given to SequentialRNNCell, child cells must own theirs')
-            cell.params._params.update(self.params._params)
-        self.params._params.update(cell.params._params)
-
-    @property
-    def state_info(self):
-        return _cells_state_info(self._cells)
-
-    def begin_state(self, **kwargs):
-        if self._modified:
-            raise AssertionError('modified cell: call the modifier instead')
-        return _cells_begin_state(self._cells, **kwargs)
-
-    def unpack_weights(self, args):
-        return _cells_unpack_weights(self._cells, args)
-
-    def pack_weights(self, args):
-        return _cells_pack_weights(self._cells, args)
-
-    def _split_states(self, states):
-        out, p = [], 0
-        for c in self._cells:
-            n = len(c.state_info)
-            out.append(states[p:p + n])
-            p += n
-        return out
+        self._adopt([cell], self._shared)
 
     def __call__(self, inputs, states):
         self._counter += 1
-        new_states = []
-        for cell, st in zip(self._cells, self._split_states(states)):
-            if isinstance(cell, BidirectionalCell):
+        carried = []
+        for child, st in zip(self._cells, self._per_child(states)):
+            if isinstance(child, BidirectionalCell):
                 raise AssertionError('BidirectionalCell cannot be stepped; unroll the stack instead')
-            inputs, st = cell(inputs, st)
-            new_states.extend(st)
-        return inputs, new_states
+            inputs, st = child(inputs, st)
+            carried += st
+        return inputs, carried
 
     def unroll(self, length, inputs, begin_state=None, layout='NTC', merge_outputs=None):
         self.reset()
-        states = self.begin_state() if begin_state is None else begin_state
-        new_states = []
-        last = len(self._cells) - 1
-        for i, (cell, st) in enumerate(zip(self._cells, self._split_states(states))):
-            inputs, st = cell.unroll(length, inputs=inputs, begin_state=st, layout=layout,
-                                     merge_outputs=None if i < last else merge_outputs)
-            new_states.extend(st)
-        return inputs, new_states
+        states = begin_state if begin_state is not None else self.begin_state()
+        carried = []
+        depth = len(self._cells)
+        for k, (child, st) in enumerate(zip(self._cells, self._per_child(states))):
+            merge = merge_outputs if k == depth - 1 else None
+            inputs, st = child.unroll(length, inputs=inputs, begin_state=st, layout=layout, merge_outputs=merge)
+            carried += st
+        return inputs, carried
 
 
 class DropoutCell(BaseRNNCell):
@@ -488,16 +494,14 @@ class DropoutCell(BaseRNNCell):
         return []
 
     def __call__(self, inputs, states):
-        if self.dropout > 0:
-            inputs = symbol.Dropout(data=inputs, p=self.dropout)
-        return inputs, states
+        return (symbol.Dropout(data=inputs, p=self.dropout) if self.dropout > 0 else inputs), states
 
     def unroll(self, length, inputs, begin_state=None, layout='NTC', merge_outputs=None):
         self.reset()
-        inputs, _ = _normalize_sequence(length, inputs, layout, merge_outputs)
-        if isinstance(inputs, symbol.Symbol):
-            return self(inputs, [])
-        return super().unroll(length, inputs, begin_state=begin_state, layout=layout, merge_outputs=merge_outputs)
+        seq, _ = _time_major_split(length, inputs, layout, merge_outputs)
+        if not isinstance(seq, symbol.Symbol):
+            return super().unroll(length, seq, begin_state=begin_state, layout=layout, merge_outputs=merge_outputs)
+        return self(seq, [])
 
 
 class ModifierCell(BaseRNNCell):
@@ -505,26 +509,29 @@ class ModifierCell(BaseRNNCell):
 
     def __init__(self, base_cell):
         super().__init__()
-        base_cell._modified = True
         self.base_cell = base_cell
+        base_cell._modified = True
 
     @property
     def params(self):
-        self._own_params = False
+        self._owns_params = False
         return self.base_cell.params
 
     @property
     def state_info(self):
         return self.base_cell.state_info
 
-    def begin_state(self, init_sym=symbol.zeros, **kwargs):
-        if self._modified:
-            raise AssertionError('modified cell: call the outer modifier instead')
+    def _run_unwrapped(self, fn, *args, **kwargs):
+        """Call ``fn`` of the base cell with its 'modified' guard lifted."""
         self.base_cell._modified = False
         try:
-            return self.base_cell.begin_state(func=init_sym, **kwargs)
+            return fn(*args, **kwargs)
         finally:
             self.base_cell._modified = True
+
+    def begin_state(self, init_sym=symbol.zeros, **kwargs):
+        self._check_unmodified()
+        return self._run_unwrapped(self.base_cell.begin_state, func=init_sym, **kwargs)
 
     def unpack_weights(self, args):
         return self.base_cell.unpack_weights(args)
@@ -540,10 +547,11 @@ class ZoneoutCell(ModifierCell):
     """Zoneout (Krueger et al. 2016): randomly keep previous outputs / states."""
 
     def __init__(self, base_cell, zoneout_outputs=0., zoneout_states=0.):
-        if isinstance(base_cell, FusedRNNCell):
-            raise AssertionError('FusedRNNCell does not support zoneout; unfuse() it first')
-        if isinstance(base_cell, BidirectionalCell):
-            raise AssertionError('BidirectionalCell does not support zoneout; apply it to the inner cells')
+        for bad, why in ((FusedRNNCell, 'FusedRNNCell does not support zoneout; unfuse() it first'),
+                         (BidirectionalCell, 'BidirectionalCell does not support zoneout; apply it to the inner '
+                                             'cells')):
+            if isinstance(base_cell, bad):
+                raise AssertionError(why)
         super().__init__(base_cell)
         self.zoneout_outputs = zoneout_outputs
         self.zoneout_states = zoneout_states
@@ -553,96 +561,72 @@ class ZoneoutCell(ModifierCell):
         super().reset()
         self.prev_output = None
 
+    @staticmethod
+    def _keep(p, new, old):
+        """Element-wise: ``new`` where a dropout mask of rate ``p`` is set, else ``old``."""
+        return symbol.where(symbol.Dropout(symbol.ones_like(new), p=p), new, old)
+
     def __call__(self, inputs, states):
-        cell = self.base_cell
-        next_output, next_states = cell(inputs, states)
-        mask = lambda p, like: symbol.Dropout(symbol.ones_like(like), p=p)   # noqa: E731
-        prev = self.prev_output if self.prev_output is not None else symbol.zeros_like(next_output)
-        out = symbol.where(mask(self.zoneout_outputs, next_output), next_output, prev) \
-            if self.zoneout_outputs != 0. else next_output
+        y, new_states = self.base_cell(inputs, states)
+        if self.zoneout_outputs != 0.:
+            last = symbol.zeros_like(y) if self.prev_output is None else self.prev_output
+            y = self._keep(self.zoneout_outputs, y, last)
         if self.zoneout_states != 0.:
-            next_states = [symbol.where(mask(self.zoneout_states, n), n, o) for n, o in zip(next_states, states)]
-        self.prev_output = out
-        return out, next_states
+            new_states = [self._keep(self.zoneout_states, n, o) for n, o in zip(new_states, states)]
+        self.prev_output = y
+        return y, new_states
 
 
 class ResidualCell(ModifierCell):
     """Adds the step input to the wrapped cell's output (He et al. 2016 style)."""
 
     def __call__(self, inputs, states):
-        out, states = self.base_cell(inputs, states)
-        return symbol.elemwise_add(out, inputs, name='%s_plus_residual' % out.name), states
+        y, states = self.base_cell(inputs, states)
+        return symbol.elemwise_add(y, inputs, name='%s_plus_residual' % y.name), states
 
     def unroll(self, length, inputs, begin_state=None, layout='NTC', merge_outputs=None):
         self.reset()
-        self.base_cell._modified = False
-        outputs, states = self.base_cell.unroll(length, inputs=inputs, begin_state=begin_state, layout=layout,
-                                                merge_outputs=merge_outputs)
-        self.base_cell._modified = True
-        merge = isinstance(outputs, symbol.Symbol) if merge_outputs is None else merge_outputs
-        inputs, _ = _normalize_sequence(length, inputs, layout, merge)
-        if merge:
-            outputs = symbol.elemwise_add(outputs, inputs)
-        else:
-            outputs = [symbol.elemwise_add(o, i) for o, i in zip(outputs, inputs)]
-        return outputs, states
+        ys, states = self._run_unwrapped(self.base_cell.unroll, length, inputs=inputs, begin_state=begin_state,
+                                         layout=layout, merge_outputs=merge_outputs)
+        merged = isinstance(ys, symbol.Symbol) if merge_outputs is None else merge_outputs
+        xs, _ = _time_major_split(length, inputs, layout, merged)
+        if merged:
+            return symbol.elemwise_add(ys, xs), states
+        return [symbol.elemwise_add(y, x) for y, x in zip(ys, xs)], states
 
 
-class BidirectionalCell(BaseRNNCell):
+class BidirectionalCell(_Container):
     """Runs ``l_cell`` forward and ``r_cell`` backward in time and concatenates their outputs."""
 
     def __init__(self, l_cell, r_cell, params=None, output_prefix='bi_'):
         super().__init__('', params=params)
         self._output_prefix = output_prefix
-        self._override_cell_params = params is not None
-        if self._override_cell_params:
-            if not (l_cell._own_params and r_cell._own_params):
-                raise AssertionError('with params given, the inner cells must own theirs')
-            l_cell.params._params.update(self.params._params)
-            r_cell.params._params.update(self.params._params)
-        self.params._params.update(l_cell.params._params)
-        self.params._params.update(r_cell.params._params)
+        self._adopt([l_cell, r_cell], params is not None)
         self._cells = [l_cell, r_cell]
-
-    def unpack_weights(self, args):
-        return _cells_unpack_weights(self._cells, args)
-
-    def pack_weights(self, args):
-        return _cells_pack_weights(self._cells, args)
 
     def __call__(self, inputs, states):
         raise NotImplementedError('BidirectionalCell cannot be stepped; use unroll')
 
-    @property
-    def state_info(self):
-        return _cells_state_info(self._cells)
-
-    def begin_state(self, **kwargs):
-        if self._modified:
-            raise AssertionError('modified cell: call the modifier instead')
-        return _cells_begin_state(self._cells, **kwargs)
-
     def unroll(self, length, inputs, begin_state=None, layout='NTC', merge_outputs=None):
         self.reset()
-        inputs, axis = _normalize_sequence(length, inputs, layout, False)
-        states = self.begin_state() if begin_state is None else begin_state
-        l_cell, r_cell = self._cells
-        nl = len(l_cell.state_info)
-        l_out, l_states = l_cell.unroll(length, inputs=inputs, begin_state=states[:nl], layout=layout,
-                                        merge_outputs=merge_outputs)
-        r_out, r_states = r_cell.unroll(length, inputs=list(reversed(inputs)), begin_state=states[nl:],
-                                        layout=layout, merge_outputs=merge_outputs)
+        steps, t_axis = _time_major_split(length, inputs, layout, False)
+        states = begin_state if begin_state is not None else self.begin_state()
+        fwd_cell, bwd_cell = self._cells
+        split = len(fwd_cell.state_info)
+        fwd, fwd_states = fwd_cell.unroll(length, inputs=steps, begin_state=states[:split], layout=layout,
+                                          merge_outputs=merge_outputs)
+        bwd, bwd_states = bwd_cell.unroll(length, inputs=steps[::-1], begin_state=states[split:], layout=layout,
+                                          merge_outputs=merge_outputs)
         if merge_outputs is None:
-            merge_outputs = isinstance(l_out, symbol.Symbol) and isinstance(r_out, symbol.Symbol)
-            l_out, _ = _normalize_sequence(None, l_out, layout, merge_outputs)
-            r_out, _ = _normalize_sequence(None, r_out, layout, merge_outputs)
+            merge_outputs = isinstance(fwd, symbol.Symbol) and isinstance(bwd, symbol.Symbol)
+            fwd, _ = _time_major_split(None, fwd, layout, merge_outputs)
+            bwd, _ = _time_major_split(None, bwd, layout, merge_outputs)
         if merge_outputs:
-            r_out = symbol.reverse(r_out, axis=axis)
-            outputs = symbol.Concat(l_out, r_out, dim=2, name='%sout' % self._output_prefix)
+            outs = symbol.Concat(fwd, symbol.reverse(bwd, axis=t_axis), dim=2, name=self._output_prefix + 'out')
         else:
-            outputs = [symbol.Concat(l, r, dim=1, name='%st%d' % (self._output_prefix, i))
-                       for i, (l, r) in enumerate(zip(l_out, reversed(r_out)))]
-        return outputs, l_states + r_states
+            outs = [symbol.Concat(f, b, dim=1, name='%st%d' % (self._output_prefix, t))
+                    for t, (f, b) in enumerate(zip(fwd, bwd[::-1]))]
+        return outs, fwd_states + bwd_states
 
 
 class BaseConvRNNCell(BaseRNNCell):
@@ -667,14 +651,11 @@ class BaseConvRNNCell(BaseRNNCell):
                                   pad=i2h_pad, dilate=i2h_dilate, layout=conv_layout)
         self._state_shape = conv.infer_shape(data=input_shape)[1][0]
         self._state_shape = (0,) + tuple(self._state_shape[1:])
-        self._iW = self.params.get('i2h_weight')
-        self._hW = self.params.get('h2h_weight')
-        self._iB = self.params.get('i2h_bias')
-        self._hB = self.params.get('h2h_bias')
+        self._standard_params()
 
     @property
     def _num_gates(self):
-        return len(self._gate_names)
+        return len(self._GATES)
 
     @property
     def state_info(self):
@@ -703,15 +684,13 @@ class ConvRNNCell(BaseConvRNNCell):
         super().__init__(input_shape, num_hidden, h2h_kernel, h2h_dilate, i2h_kernel, i2h_stride, i2h_pad,
                          i2h_dilate, activation, prefix, params, conv_layout)
 
-    @property
-    def _gate_names(self):
-        return ('',)
+    _GATES = ('',)
 
     def __call__(self, inputs, states):
-        name = self._step_name()
-        i2h, h2h = self._conv_forward(inputs, states, name)
-        out = self._get_activation(i2h + h2h, self._activation, name=name + 'out')
-        return out, [out]
+        tag = self._step_name()
+        i2h, h2h = self._conv_forward(inputs, states, tag)
+        h = self._get_activation(i2h + h2h, self._activation, name=tag + 'out')
+        return h, [h]
 
 
 class ConvLSTMCell(BaseConvRNNCell):
@@ -724,9 +703,7 @@ class ConvLSTMCell(BaseConvRNNCell):
                          i2h_dilate, activation, prefix, params, conv_layout)
         self._iB = self.params.get('i2h_bias', init=init.LSTMBias(forget_bias=forget_bias))
 
-    @property
-    def _gate_names(self):
-        return ('_i', '_f', '_c', '_o')
+    _GATES = ('_i', '_f', '_c', '_o')
 
     def __call__(self, inputs, states):
         name = self._step_name()
@@ -749,9 +726,7 @@ class ConvGRUCell(BaseConvRNNCell):
         super().__init__(input_shape, num_hidden, h2h_kernel, h2h_dilate, i2h_kernel, i2h_stride, i2h_pad,
                          i2h_dilate, activation, prefix, params, conv_layout)
 
-    @property
-    def _gate_names(self):
-        return ('_r', '_z', '_o')
+    _GATES = ('_r', '_z', '_o')
 
     def __call__(self, inputs, states):
         name = self._step_name()
