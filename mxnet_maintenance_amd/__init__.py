@@ -53,6 +53,10 @@ from . import monitor as mon
 from . import profiler
 from . import runtime
 from . import test_utils
+from . import registry
+from . import error
+from . import executor_manager
+from . import notebook
 from . import util
 from . import operator
 from . import image

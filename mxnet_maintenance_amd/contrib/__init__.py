@@ -6,6 +6,7 @@ from . import text  # noqa: F401
 from . import svrg_optimization  # noqa: F401
 from . import autograd  # noqa: F401
 from . import io  # noqa: F401
+from . import tensorboard  # noqa: F401
 from .. import ndarray as _nd
 from .. import symbol as _sym
 ndarray = _nd.contrib
