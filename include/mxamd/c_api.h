@@ -1,0 +1,103 @@
+/*
+ * C API of mxnet_maintenance_amd (libmxamd.so): the subset of the reference's
+ * include/mxnet/c_api.h that language bindings and C/C++ hosts use -- NDArrays,
+ * imperative operator invocation with autograd, Symbols, Executors and KVStores.
+ * Every function returns 0 on success and -1 on failure (message in MXGetLastError()).
+ * Pointers returned by a call stay valid until the next call on the same handle
+ * (or, for functions without a handle argument, the next such call on the same thread).
+ */
+#ifndef MXAMD_C_API_H_
+#define MXAMD_C_API_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* NDArrayHandle;
+typedef void* SymbolHandle;
+typedef void* ExecutorHandle;
+typedef void* KVStoreHandle;
+typedef void* OpHandle;
+typedef OpHandle AtomicSymbolCreator;
+
+const char* MXGetLastError(void);
+int MXGetVersion(int* out);
+
+/* NDArray: dev_type 1 cpu, 2 gpu, 3 cpu_pinned; dtype 0 f32, 1 f64, 2 f16, 3 u8, 4 i32, 5 i8,
+   6 i64, 7 bool, 12 bf16 */
+int MXNDArrayCreateNone(NDArrayHandle* out);
+int MXNDArrayCreate(const uint32_t* shape, uint32_t ndim, int dev_type, int dev_id, int delay_alloc,
+                    NDArrayHandle* out);
+int MXNDArrayCreateEx(const uint32_t* shape, uint32_t ndim, int dev_type, int dev_id, int delay_alloc, int dtype,
+                      NDArrayHandle* out);
+int MXNDArrayFree(NDArrayHandle handle);
+int MXNDArrayGetShape(NDArrayHandle handle, uint32_t* out_dim, const uint32_t** out_pdata);
+int MXNDArrayGetDType(NDArrayHandle handle, int* out_dtype);
+int MXNDArrayGetContext(NDArrayHandle handle, int* out_dev_type, int* out_dev_id);
+int MXNDArraySyncCopyFromCPU(NDArrayHandle handle, const void* data, size_t size);
+int MXNDArraySyncCopyToCPU(NDArrayHandle handle, void* data, size_t size);
+int MXNDArrayWaitToRead(NDArrayHandle handle);
+int MXNDArrayWaitAll(void);
+int MXNDArraySave(const char* fname, uint32_t num_args, NDArrayHandle* args, const char** keys);
+int MXNDArrayLoad(const char* fname, uint32_t* out_size, NDArrayHandle** out_arr, uint32_t* out_name_size,
+                  const char*** out_names);
+int MXNDArrayReshape(NDArrayHandle handle, int ndim, int* dims, NDArrayHandle* out);
+int MXNDArraySlice(NDArrayHandle handle, uint32_t slice_begin, uint32_t slice_end, NDArrayHandle* out);
+int MXNDArrayAt(NDArrayHandle handle, uint32_t idx, NDArrayHandle* out);
+int MXNDArrayGetGrad(NDArrayHandle handle, NDArrayHandle* out);
+
+/* operators and autograd */
+int MXListAllOpNames(uint32_t* out_size, const char*** out_array);
+int NNGetOpHandle(const char* op_name, OpHandle* op_out);
+int MXImperativeInvoke(AtomicSymbolCreator creator, int num_inputs, NDArrayHandle* inputs, int* num_outputs,
+                       NDArrayHandle** outputs, int num_params, const char** param_keys, const char** param_vals);
+int MXAutogradSetIsRecording(int is_recording, int* prev);
+int MXAutogradSetIsTraining(int is_training, int* prev);
+int MXAutogradMarkVariables(uint32_t num_var, NDArrayHandle* var_handles, uint32_t* reqs_array,
+                            NDArrayHandle* grad_handles);
+int MXAutogradBackward(uint32_t num_output, NDArrayHandle* output_handles, NDArrayHandle* ograd_handles,
+                       int retain_graph);
+
+/* symbols */
+int MXSymbolCreateFromJSON(const char* json, SymbolHandle* out);
+int MXSymbolCreateFromFile(const char* fname, SymbolHandle* out);
+int MXSymbolSaveToJSON(SymbolHandle symbol, const char** out_json);
+int MXSymbolFree(SymbolHandle symbol);
+int MXSymbolGetName(SymbolHandle symbol, const char** out, int* success);
+int MXSymbolListArguments(SymbolHandle symbol, uint32_t* out_size, const char*** out_str_array);
+int MXSymbolListOutputs(SymbolHandle symbol, uint32_t* out_size, const char*** out_str_array);
+int MXSymbolListAuxiliaryStates(SymbolHandle symbol, uint32_t* out_size, const char*** out_str_array);
+int MXSymbolCreateVariable(const char* name, SymbolHandle* out);
+int MXSymbolCreateAtomicSymbol(AtomicSymbolCreator creator, uint32_t num_param, const char** keys, const char** vals,
+                               SymbolHandle* out);
+int MXSymbolCompose(SymbolHandle sym, const char* name, uint32_t num_args, const char** keys, SymbolHandle* args);
+int MXSymbolInferShape(SymbolHandle sym, uint32_t num_args, const char** keys, const uint32_t* arg_ind_ptr,
+                       const uint32_t* arg_shape_data, uint32_t* in_shape_size, const uint32_t** in_shape_ndim,
+                       const uint32_t*** in_shape_data, uint32_t* out_shape_size, const uint32_t** out_shape_ndim,
+                       const uint32_t*** out_shape_data, uint32_t* aux_shape_size, const uint32_t** aux_shape_ndim,
+                       const uint32_t*** aux_shape_data, int* complete);
+
+/* executors (grad_req_type: 0 null, 1 write, 2 inplace, 3 add) */
+int MXExecutorBind(SymbolHandle symbol_handle, int dev_type, int dev_id, uint32_t len, NDArrayHandle* in_args,
+                   NDArrayHandle* arg_grad_store, uint32_t* grad_req_type, uint32_t aux_states_len,
+                   NDArrayHandle* aux_states, ExecutorHandle* out);
+int MXExecutorForward(ExecutorHandle handle, int is_train);
+int MXExecutorBackward(ExecutorHandle handle, uint32_t len, NDArrayHandle* head_grads);
+int MXExecutorOutputs(ExecutorHandle handle, uint32_t* out_size, NDArrayHandle** out);
+int MXExecutorFree(ExecutorHandle handle);
+
+/* key-value stores */
+int MXKVStoreCreate(const char* type, KVStoreHandle* out);
+int MXKVStoreInit(KVStoreHandle handle, uint32_t num, const int* keys, NDArrayHandle* vals);
+int MXKVStorePush(KVStoreHandle handle, uint32_t num, const int* keys, NDArrayHandle* vals, int priority);
+int MXKVStorePull(KVStoreHandle handle, uint32_t num, const int* keys, NDArrayHandle* vals, int priority);
+int MXKVStoreFree(KVStoreHandle handle);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif  // MXAMD_C_API_H_

@@ -158,15 +158,24 @@ class GraphStep:
         if self._graph is None:
             if self._calls <= self._warmup:
                 return self._run_eager(inputs)
+            err = None
             try:
                 self._capture(inputs)
             except Exception as e:      # pylint: disable=broad-except
+                err = e
+            # data parallel: the ranks decide TOGETHER -- one rank replaying a graph while another
+            # runs eagerly would pair their collectives differently (hang risk)
+            if not self._all_ranks_ok(err is None):
+                if self._graph is not None:
+                    self._drop_graph()
                 if not self._fallback:
-                    raise
+                    raise err if err is not None else RuntimeError('GraphStep: capture failed on another rank')
                 import warnings
-                warnings.warn('GraphStep: capture failed (%s); running the step eagerly' % e)
+                warnings.warn('GraphStep: capture failed (%s); running the step eagerly on every rank'
+                              % (err if err is not None else 'on another rank'))
                 self._eager_only = True
-                torch.cuda.synchronize()
+                if torch.cuda.is_available():
+                    torch.cuda.synchronize()
                 return self._run_eager(inputs)
         else:
             self._load_inputs(inputs)
@@ -175,6 +184,22 @@ class GraphStep:
         self._rng.add_(1)
         self._graph.replay()
         return self._static_out
+
+    @staticmethod
+    def _all_ranks_ok(ok):
+        """MIN over ranks of a success flag (CPU collective; True with one process)."""
+        from ..parallel import dist
+        if dist.world_size() <= 1:
+            return ok
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(t, op='min')
+        return bool(t.item())
+
+    def _drop_graph(self):
+        if self._trainer is not None:
+            self._trainer._exit_graph_mode()
+        self._graph = None
+        self._static_out = None
 
     def reset(self):
         """Drop the captured graph (e.g. after a shape change); the next call re-captures."""

@@ -102,9 +102,16 @@ def conv(data, weight, bias, stride, pad, dilate, groups, channel_last):
         wl = weight.permute(0, 2, 3, 1).contiguous()
         if _K.conv_ok(xl, wl, stride, pad, dilate, groups):
             return _K.ConvNHWC.apply(xl, wl, bias, tuple(stride), tuple(pad), tuple(dilate)).permute(0, 3, 1, 2)
+    if channel_last and _use_hip(data) and _K.conv_ok(data, weight, stride, pad, dilate, groups):
+        return _K.ConvNHWC.apply(data, weight, bias, tuple(stride), tuple(pad), tuple(dilate))
+    if _use_hip(data):
+        # grouped / dilated / 1-D / 3-D / fp32 / odd channel counts: the general in-tree MFMA kernel
+        # (src/kernels/conv_gen.hip), chosen per shape against MIOpen by measured forward time
+        from . import conv_gen
+        y = conv_gen.conv(data, weight, bias, tuple(stride), tuple(pad), tuple(dilate), groups, channel_last)
+        if y is not None:
+            return y
     if channel_last:
-        if _use_hip(data) and _K.conv_ok(data, weight, stride, pad, dilate, groups):
-            return _K.ConvNHWC.apply(data, weight, bias, tuple(stride), tuple(pad), tuple(dilate))
         x = _nd_to_ncx(data)
         w = _nd_to_ncx(weight)
     else:

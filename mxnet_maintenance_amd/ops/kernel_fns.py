@@ -679,26 +679,57 @@ def _time_candidates(cands, reps=3, key=None, tol=2e-2):
     for _ in range(_TUNE_ROUNDS):
         for name, fn in ok:
             fn()
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            for _ in range(reps):
-                r = fn()
-            e.record()
-            e.synchronize()
-            t = s.elapsed_time(e)
+            t, r = _measure(fn, reps)
             if name not in times or t < times[name]:
                 times[name] = t
                 outs[name] = r
+    # data parallel: every rank must run the same kernels (the slowest rank sets the step time, and
+    # ranks that disagree would differ numerically) -- agree on per-candidate times first
+    names = [n for n, _ in cands]
+    agreed = _agree_times([times.get(n, float('inf')) for n in names])
     best, best_t = None, None
-    for name, _ in ok:
-        t = times[name]
+    for name, t in zip(names, agreed):
+        if t == float('inf'):
+            continue
         if key is not None:
             _TIMES.setdefault(key, {})[name] = t / reps
         if name in _VENDOR:
             t *= 1.0 + _VENDOR_MARGIN     # near-ties (within timing noise) go to the in-tree kernels
         if best_t is None or t < best_t:
             best, best_t = name, t
+    if best is not None and best not in outs:
+        best = None                         # (cannot happen: a finite agreed time was timed here too)
     return best, (outs[best] if best is not None else None)
+
+
+def _measure(fn, reps):
+    """(ms for ``reps`` calls of ``fn``, last result): HIP events on a GPU, wall clock otherwise."""
+    if torch.cuda.is_available():
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            r = fn()
+        e.record()
+        e.synchronize()
+        return s.elapsed_time(e), r
+    import time
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = fn()
+    return (time.perf_counter() - t0) * 1e3, r
+
+
+def _agree_times(vals):
+    """Per-candidate times made identical on every rank: the MAX over ranks (a candidate rejected
+    by the numerics check anywhere is out everywhere).  A CPU all-reduce over the gloo side group,
+    so no GPU stream or RCCL communicator is touched; every rank autotunes the same keys in the same
+    order (one model per rank), which keeps these collectives matched."""
+    from ..parallel import dist
+    if dist.world_size() <= 1 or not vals:
+        return vals
+    t = torch.tensor(vals, dtype=torch.float64)
+    dist.all_reduce(t, op='max')
+    return [float(v) for v in t.tolist()]
 
 
 # ---- deterministic execution (MXNET_ENFORCE_DETERMINISM; reference: the cuDNN algorithm filter of
@@ -747,6 +778,49 @@ def _akey(key):
     return key + ('det',) if _DETERMINISTIC[0] else key
 
 
+# Persisted tuning table (MXAMD_AUTOTUNE_FILE=path, JSON {repr(key): candidate}): read by every rank at
+# first use, so a multi-GPU job whose ranks all load the same file runs identical kernels without
+# timing anything; new choices are appended by rank 0.
+_FILE_ALGO = {}
+_FILE_STATE = {'loaded': False}
+
+
+def _tuning_file():
+    return os.environ.get('MXAMD_AUTOTUNE_FILE', '')
+
+
+def _load_tuning_file():
+    if _FILE_STATE['loaded']:
+        return
+    _FILE_STATE['loaded'] = True
+    path = _tuning_file()
+    if path and os.path.exists(path):
+        import json
+        try:
+            with open(path) as f:
+                _FILE_ALGO.update(json.load(f))
+        except (OSError, ValueError):
+            pass
+
+
+def _save_tuning_file(key, name):
+    path = _tuning_file()
+    if not path or name is None:
+        return
+    from ..parallel import dist
+    if dist.rank() != 0:
+        return
+    import json
+    _FILE_ALGO[repr(key)] = name
+    tmp = path + '.tmp'
+    try:
+        with open(tmp, 'w') as f:
+            json.dump(_FILE_ALGO, f, indent=0, sort_keys=True)
+        os.replace(tmp, path)
+    except OSError:
+        pass
+
+
 def _select(key, cands, default, timing=None):
     """Run the cached / autotuned / default candidate and return its result.
 
@@ -755,11 +829,17 @@ def _select(key, cands, default, timing=None):
     key = _akey(key)
     cands = _det_filter(cands)
     timing = _det_filter(timing)
+    _load_tuning_file()
     name = _ALGO.get(key)
+    if name is None:
+        name = _FILE_ALGO.get(repr(key))
+        if name is not None and name in dict(cands):
+            _ALGO[key] = name
     if name is None:
         if _AUTOTUNE and not torch.cuda.is_current_stream_capturing() and len(cands) > 1:
             name, out = _time_candidates(timing or cands, key=key)
             _ALGO[key] = name
+            _save_tuning_file(key, name)
             return out
         name = default
     table = dict(cands)

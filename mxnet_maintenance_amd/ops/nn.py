@@ -197,6 +197,12 @@ def deconvolution(data, weight, bias=None, kernel=(), stride=(), dilate=(), pad=
             tot = full - target_shape[i]
             pad[i] = (tot + 1) // 2
             adj[i] = tot % 2
+    if data.is_cuda and hip_ops._use_hip(data):
+        # in-tree transposed convolution (the data gradient of a conv, src/kernels/conv_gen.hip)
+        from . import conv_gen
+        y = conv_gen.deconv(data, weight, bias, stride, pad, dilate, adj, num_group, _is_channel_last(layout))
+        if y is not None:
+            return y
     fn = {1: F.conv_transpose1d, 2: F.conv_transpose2d, 3: F.conv_transpose3d}[nsp]
     y = fn(x, w, bias, stride=stride, padding=pad, output_padding=adj, groups=num_group, dilation=dilate)
     return _from_ncx(y, layout)
@@ -1095,6 +1101,12 @@ def unpack_rnn_params(params, mode, num_layers, input_size, state_size, bidirect
     return ws
 
 
+def _kernels_required():
+    """MXAMD_REQUIRE_HIP=1: GPU ops must run on the in-tree kernels (no silent vendor fallback)."""
+    import os
+    return os.environ.get('MXAMD_REQUIRE_HIP', '0') == '1'
+
+
 def _cell_step(mode, x, h, c, wi, wh, bi, bh, wr, clip):
     gi = F.linear(x, wi, bi)
     gh = F.linear(h, wh, bh)
@@ -1196,6 +1208,15 @@ def rnn(data, parameters, state, state_cell=None, sequence_length=None, state_si
                                       and tuple(state_cell.shape) != (num_layers * d, data.shape[1], state_size)):
         # the fused torch kernels do not validate state shapes
         raise MXNetError('RNN: state shape %s does not match %s' % (tuple(state.shape), want))
+    from . import rnn_fns
+    if rnn_fns.available(data) and not projection_size:
+        # in-tree gfx950 recurrent kernels (src/kernels/rnn.hip): fused gate GEMM + cell per step
+        out, h, c = rnn_fns.fused_rnn(data, ws, state, state_cell, mode, num_layers, bidirectional, p, train)
+        if mode == 'lstm':
+            return (out, h, c) if state_outputs else out
+        return (out, h) if state_outputs else out
+    if data.is_cuda and _kernels_required():
+        raise MXNetError('RNN: the in-tree recurrent kernels are not available on this GPU build')
     if mode == 'lstm':
         out, h, c = torch._VF.lstm(data, (state, state_cell), flat, True, num_layers, p, train,
                                    bidirectional, False)

@@ -149,6 +149,13 @@ int create_impl(const char* json, const void* params, int param_size, int dev_ty
 
 }  // namespace
 
+// shared with c_api.cc (same library): the embedded interpreter and the last-error slot
+namespace mxamd_capi {
+bool ensure_python() { return ::ensure_python(); }
+int fail_from_python() { return ::fail_from_python(); }
+int fail(const char* msg) { return ::fail(msg); }
+}  // namespace mxamd_capi
+
 extern "C" {
 
 typedef void* PredictorHandle;

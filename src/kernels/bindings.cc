@@ -145,6 +145,15 @@ void slab_reduce(int out_dtype, float* slab, int splits, int64_t n, void* out, i
 void twobit_quantize(int dtype, const void* g, float* res, void* packed, int64_t n, float thr, hipStream_t s);
 void twobit_dequantize_sum(const void* packed, int64_t row_bytes, int nrows, int64_t n, float thr, float* out,
                            hipStream_t s);
+void conv_gen(int dtype, int mode, const void* src, const void* wsrc, const float* bias, void* dst, const int* geom,
+              int splits, hipStream_t s);
+void rnn_fwd_seq(int dtype, int mode, const float* gx, const void* h0, const float* c0, const void* whh,
+                 const float* bhh, void* out, int ldo, float* cseq, float* save, int Tn, int N, int H, int reverse,
+                 hipStream_t s);
+void rnn_bwd_seq(int dtype, int mode, const void* whhT, const void* dy, int ldy, const float* dhT,
+                 const float* save, const float* cseq, const float* c0, const void* h0, const void* out, int ldo,
+                 void* dgh, void* dgx, float* dc, float* dhd, float* dh0, int Tn, int N, int H, int reverse,
+                 hipStream_t s);
 }  // namespace mxamd
 
 using namespace mxamd;
@@ -220,6 +229,31 @@ PYBIND11_MODULE(_hip_kernels, m) {
     gemm_nt(dt, P<void>(a), P<void>(b), P<float>(bias), P<void>(addend), P<void>(c), out_f32, M, N, K, lda, ldb, ldc,
             act, cfg, splits, P<float>(ws), S(s));
     check_launch("gemm_nt");
+  });
+  // general implicit-GEMM convolution: grouped / dilated / 1-3-D / fp32 / transposed (src/kernels/conv_gen.hip)
+  m.def("conv_gen", [](int dt, int mode, uintptr_t src, uintptr_t wsrc, uintptr_t bias, uintptr_t dst,
+                       std::vector<int> geom, int splits, uintptr_t s) {
+    if (geom.size() != 22) throw std::runtime_error("conv_gen: geometry needs 22 ints");
+    conv_gen(dt, mode, P<const void>(src), P<const void>(wsrc), P<const float>(bias), P<void>(dst), geom.data(),
+             splits, S(s));
+    check_launch("conv_gen");
+  });
+  // fused recurrent layers: one (layer, direction) over a whole sequence (src/kernels/rnn.hip)
+  m.def("rnn_fwd_seq", [](int dt, int mode, uintptr_t gx, uintptr_t h0, uintptr_t c0, uintptr_t whh, uintptr_t bhh,
+                          uintptr_t out, int ldo, uintptr_t cseq, uintptr_t save, int T, int N, int H, int reverse,
+                          uintptr_t s) {
+    rnn_fwd_seq(dt, mode, P<const float>(gx), P<const void>(h0), P<const float>(c0), P<const void>(whh),
+                P<const float>(bhh), P<void>(out), ldo, P<float>(cseq), P<float>(save), T, N, H, reverse, S(s));
+    check_launch("rnn_fwd_seq");
+  });
+  m.def("rnn_bwd_seq", [](int dt, int mode, uintptr_t whhT, uintptr_t dy, int ldy, uintptr_t dhT, uintptr_t save,
+                          uintptr_t cseq, uintptr_t c0, uintptr_t h0, uintptr_t out, int ldo, uintptr_t dgh,
+                          uintptr_t dgx, uintptr_t dc, uintptr_t dhd, uintptr_t dh0, int T, int N, int H, int reverse,
+                          uintptr_t s) {
+    rnn_bwd_seq(dt, mode, P<const void>(whhT), P<const void>(dy), ldy, P<const float>(dhT), P<const float>(save),
+                P<const float>(cseq), P<const float>(c0), P<const void>(h0), P<const void>(out), ldo, P<void>(dgh),
+                P<void>(dgx), P<float>(dc), P<float>(dhd), P<float>(dh0), T, N, H, reverse, S(s));
+    check_launch("rnn_bwd_seq");
   });
   m.def("gemm_nt_tile_n", &gemm_nt_tile_n);
   m.def("gemm_nt_tile_m", &gemm_nt_tile_m);

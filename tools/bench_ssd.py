@@ -54,6 +54,9 @@ def main():
     ap.add_argument('--gpus', type=int, default=1, help='worker processes (one per GPU)')
     ap.add_argument('--deformable', type=int, default=1,
                     help='deformable 3x3 convs in the extra feature layers (the config\'s deformable/im2col conv)')
+    ap.add_argument('--graph', type=int, default=1,
+                    help='capture the whole step (forward, MultiBoxTarget, loss, backward, update) in one HIP graph '
+                         '(gluon.GraphStep; eager fallback if capture fails)')
     args = ap.parse_args()
     launch = _load_launcher()
     if launch.needs_launch(args.gpus):
@@ -85,6 +88,9 @@ def main():
                                                           'multi_precision': args.dtype != 'float32'},
                             kvstore='device')
     step = ssd.SSDTrainStep(net, trainer, (S, S))
+    use_graph = bool(args.graph) and gpu
+    if use_graph:
+        step = gluon.GraphStep(step, trainer, warmup=max(1, args.warmup - 1), fallback=True)
     gen = torch.Generator().manual_seed(11 + rank)
     x = nd.random.uniform(-1, 1, shape=(B, S, S, 3), ctx=ctx).astype(args.dtype)
     labels = nd.array(synthetic_labels(B, 16, args.classes, gen).numpy(), ctx=ctx)
@@ -116,7 +122,8 @@ def main():
             'config': {'model': 'SSD-ResNet50 v1b', 'image_size': S, 'per_gpu_batch': B, 'global_batch': B * n,
                        'classes': args.classes, 'anchors': int(net.anchors((S, S), ctx).shape[1]),
                        'parallelism': 'dp%d' % n, 'final_loss': round(float(L.asscalar()), 4),
-                       'deformable_extras': bool(args.deformable)},
+                       'deformable_extras': bool(args.deformable),
+                       'hip_graph': bool(use_graph and getattr(step, 'captured', False))},
         }), flush=True)
     if n > 1:
         torch.distributed.destroy_process_group()

@@ -105,20 +105,24 @@ def build_hip(jobs):
 
 
 def build_capi(jobs):
-    """``libmxamd_predict.so``: the C predict API (src/capi), a C ABI over an embedded CPython."""
+    """``libmxamd_predict.so`` / ``libmxamd.so``: the C predict API and the general C API (src/capi), a C
+    ABI over the framework in an embedded (or the host's) CPython."""
     import sysconfig
     srcs = sorted(glob.glob(os.path.join(ROOT, 'src', 'capi', '*.cc')))
     if not srcs:
         return None
     os.makedirs(LIB, exist_ok=True)
     out = os.path.join(LIB, 'libmxamd_predict.so')
-    if not _newer(srcs, out):
+    if not _newer(srcs, out) and os.path.exists(os.path.join(LIB, 'libmxamd.so')):
         return out
     inc = sysconfig.get_paths()['include']
     libdir = sysconfig.get_config_var('LIBDIR')
     ver = sysconfig.get_config_var('LDVERSION') or sysconfig.get_python_version()
     _run(['g++', '-O2', '-fPIC', '-shared', '-std=c++17', '-fvisibility=hidden', '-I' + inc] + srcs +
          ['-o', out, '-L' + libdir, '-lpython' + ver, '-ldl', '-Wl,-rpath,' + libdir])
+    # the same library under the general C API's name (include/mxamd/c_api.h)
+    import shutil
+    shutil.copyfile(out, os.path.join(LIB, 'libmxamd.so'))
     return out
 
 
