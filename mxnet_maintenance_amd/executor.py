@@ -84,8 +84,13 @@ class GraphProgram:
         names = op.get_arg_names(attrs) + op.get_aux_names(attrs)
         return [names[j] if j < len(names) else 'input%d' % j for j in range(n)]
 
-    def run(self, feed, monitor=None, monitor_all=False, record=None):
+    def run(self, feed, monitor=None, monitor_all=False, record=None, int_dtypes=None):
         """``feed``: dict var name -> torch tensor.  Returns output tensors.
+
+        ``int_dtypes`` (var name -> integer torch dtype) marks inputs that are integer variables
+        carried in float64 for autograd (NDArray.attach_grad); operators on them, and operators
+        casting a differentiable input to an integer dtype, run the shadow path of the imperative
+        invoke, and ``self.out_idts`` reports the outputs' integer dtypes.
 
         ``monitor(name, tensor)`` is called for every operator output (and,
         with ``monitor_all``, every operator input) — the engine-level monitor
@@ -94,6 +99,9 @@ class GraphProgram:
         vals = [None] * self.nslots
         for name, s in self.name_to_slot.items():
             vals[s] = feed.get(name)
+        islot = {}
+        if int_dtypes:
+            islot = {self.name_to_slot[n]: d for n, d in int_dtypes.items() if n in self.name_to_slot}
         self.failure = None       # first operator execution failure of this run (deferred to sync)
         for fn, ins, attrs, outs, name, opname in self.steps:
             args = [vals[i] for i in ins]
@@ -113,7 +121,10 @@ class GraphProgram:
                         monitor(var, a)
                     monitor('%s_%s' % (name, argn[j]), a)
             try:
-                if _profiler.active_symbolic:
+                if (islot and any(i in islot for i in ins)) or (attrs.get('dtype') is not None and
+                                                                 _int_dtype_attr(attrs) and torch.is_grad_enabled()):
+                    r = self._run_shadow(fn, args, attrs, ins, outs, islot, opname)
+                elif _profiler.active_symbolic:
                     with _profiler.op_span(_profiler.current_scope() + opname, symbolic=True):
                         r = fn(*args, **attrs)
                 else:
@@ -147,7 +158,37 @@ class GraphProgram:
                 for o, on in zip(outs, onames):
                     if vals[o] is not None:
                         monitor('%s_%s' % (name, on), vals[o])
+        self.out_idts = [islot.get(s) for s in self.out_slots] if islot else None
         return [vals[s] for s in self.out_slots]
+
+    @staticmethod
+    def _run_shadow(fn, args, attrs, ins, outs, islot, opname=None):
+        """One operator over integer values carried in float64 (see ``run``): the integer result's
+        values and dtype, the float copy's gradient path."""
+        from .ndarray.register import _merge_shadow, INT_ZERO_GRAD
+        true_args = [a.detach().to(islot[i]) if (i in islot and a is not None) else a for a, i in zip(args, ins)]
+        with torch.no_grad():
+            res_t = fn(*true_args, **attrs)
+        multi = isinstance(res_t, (tuple, list))
+        if not torch.is_grad_enabled() or not any(a is not None and a.requires_grad for a in args) or \
+                opname in INT_ZERO_GRAD:
+            for o in outs:
+                islot.pop(o, None)
+            return res_t
+        kw_f = dict(attrs, dtype='float64') if _int_dtype_attr(attrs) else attrs
+        res_f = fn(*args, **kw_f)
+        pairs = [_merge_shadow(f, t) for f, t in zip(res_f, res_t)] if multi else [_merge_shadow(res_f, res_t)]
+        for o, (_, d) in zip(outs, pairs):
+            if d is not None:
+                islot[o] = d
+            else:
+                islot.pop(o, None)
+        return [p[0] for p in pairs] if multi else pairs[0][0]
+
+
+def _int_dtype_attr(attrs):
+    dt = attrs.get('dtype')
+    return dt is not None and str(dt).replace('torch.', '').startswith(('int', 'uint', 'bool'))
 
 
 # binary / scatter operators whose row_sparse lhs keeps its storage (reference scatter_* and

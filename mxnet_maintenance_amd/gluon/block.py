@@ -529,12 +529,13 @@ class CachedOp:
         self.flags = dict(flags)
         self._graphs = {}
 
-    def __call__(self, feed, ctx_dev):
+    def __call__(self, feed, ctx_dev, int_dtypes=None):
         static = self.flags.get('static_alloc') and self.flags.get('static_shape')
-        if static and not _state.STATE.recording and ctx_dev.type == 'cuda' and \
+        if static and not _state.STATE.recording and ctx_dev.type == 'cuda' and not int_dtypes and \
                 not torch.cuda.is_current_stream_capturing():     # inside a GraphStep capture: just run
+            self.prog.out_idts = None
             return self._replay(feed)
-        return self.prog.run(feed)
+        return self.prog.run(feed, int_dtypes=int_dtypes)
 
     def _replay(self, feed):
         key = tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(feed.items()) if v is not None) + \
@@ -686,8 +687,12 @@ class HybridBlock(Block):
                 p._finish_deferred_init()
             pdata = [(n, p.data(ctx)) for n, p in self._param_map]
         feed = {}
+        idts = None
         for n, a in zip(self._data_names, args_without_none):
             feed[n] = a._data
+            if getattr(a, '_idt', None) is not None:
+                idts = idts or {}
+                idts[n] = a._idt
         rec = _state.STATE.recording
         if rec:
             tl = _state.STATE.tape_leaves
@@ -701,10 +706,15 @@ class HybridBlock(Block):
             feed[n] = d._data
         if torch.is_grad_enabled() != rec:
             with torch.set_grad_enabled(rec):
-                outs = self._cached_op(feed, ctx.torch_device)
+                outs = self._cached_op(feed, ctx.torch_device, idts)
         else:
-            outs = self._cached_op(feed, ctx.torch_device)
+            outs = self._cached_op(feed, ctx.torch_device, idts)
+        out_idts = self._cached_op.prog.out_idts
         outs = [NDArray(o) for o in outs]
+        if out_idts:
+            for o, d in zip(outs, out_idts):
+                if d is not None:
+                    o._idt = d
         if _state.STATE.recording:
             for i, o in enumerate(outs):
                 o._recorded = True

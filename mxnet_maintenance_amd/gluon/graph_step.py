@@ -92,7 +92,7 @@ class GraphStep:
 
     @staticmethod
     def _device(inputs):
-        dev = next((_tensor_of(x).device for x in inputs if _tensor_of(x) is not None), None)
+        dev = next((_tensor_of(x).device for x in inputs if torch.is_tensor(_tensor_of(x))), None)
         if dev is None and torch.cuda.is_available():      # closure-only step: the current device
             dev = torch.device('cuda', torch.cuda.current_device())
         return dev
@@ -113,7 +113,8 @@ class GraphStep:
         dev = self._device(inputs)
         if dev is None or dev.type != 'cuda':
             raise RuntimeError('GraphStep captures HIP work: inputs must live on a GPU context')
-        self._static_in = [NDArray(t.clone()) if isinstance(x, NDArray) else t.clone()
+        # tensors get static device buffers; other arguments (ints, flags) are captured as constants
+        self._static_in = [NDArray(t.clone()) if isinstance(x, NDArray) else (t.clone() if torch.is_tensor(t) else x)
                            for x, t in zip(inputs, tin)]
         self._rng = torch.zeros(1, dtype=torch.int64, device=dev)
         if self._trainer is not None:
@@ -140,6 +141,10 @@ class GraphStep:
             raise ValueError('GraphStep: expected %d inputs, got %d' % (len(self._static_in), len(inputs)))
         for dst, src in zip(self._static_in, inputs):
             d, t = _tensor_of(dst), _tensor_of(src)
+            if not torch.is_tensor(d):
+                if d != t:
+                    raise ValueError('GraphStep: non-tensor argument %r differs from the captured %r' % (t, d))
+                continue
             if d.shape != t.shape or d.dtype != t.dtype:
                 raise ValueError('GraphStep: input %s/%s differs from the captured %s/%s'
                                  % (tuple(t.shape), t.dtype, tuple(d.shape), d.dtype))

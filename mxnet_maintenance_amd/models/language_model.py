@@ -3,7 +3,8 @@
 Parity: example/gluon/word_language_model/model.py + train.py in the
 reference (Embedding -> stacked LSTM/GRU/RNN -> Dense decoder, optional weight
 tying, truncated BPTT with detached hidden state).  The recurrent stack is the
-fused ``RNN`` operator (torch's fused LSTM kernels on the GPU).
+fused ``RNN`` operator, which on the GPU runs the in-tree gfx950 recurrent
+kernels (src/kernels/rnn.hip: per-step MFMA gate GEMM fused with the cell).
 """
 from ..gluon import nn, rnn, HybridBlock
 

@@ -143,8 +143,19 @@ def _placeholder(attrs, inputs):
     return torch.zeros(shape, dtype=td, device=dev)
 
 
-def _shadowed(arrays):
-    return any(x is not None and getattr(x, '_idt', None) is not None for x in arrays)
+def _int_dtype_attr(attrs):
+    dt = attrs.get('dtype')
+    return dt is not None and str(dt).replace('torch.', '').startswith(('int', 'uint', 'bool'))
+
+
+def _shadowed(arrays, attrs=None):
+    """Integer variables among the inputs, or (while recording) a differentiable input cast to an
+    integer result dtype: both run the float shadow path so the gradient survives the integer
+    values (the reference's reductions with an integer dtype still back-propagate)."""
+    if any(x is not None and getattr(x, '_idt', None) is not None for x in arrays):
+        return True
+    return attrs is not None and _state.STATE.recording and _int_dtype_attr(attrs) and \
+        any(x is not None and x._data.requires_grad for x in arrays)
 
 
 def _true_inputs(arrays):
@@ -162,13 +173,21 @@ def _merge_shadow(res_f, res_t):
     return res_f + (res_t.to(res_f.dtype) - res_f).detach(), res_t.dtype
 
 
-def _run_shadow(fn, inputs, kw):
+# operators whose integer instantiation has a zero gradient in the reference (mshadow_op's
+# mod_grad / mod_rgrad are 0 except for floating types)
+INT_ZERO_GRAD = frozenset(('_npi_mod', '_npi_mod_scalar', '_npi_fmod', '_npi_fmod_scalar'))
+
+
+def _run_shadow(fn, inputs, kw, opname=None):
     """Run ``fn`` on arrays some of which are integer variables carried in float64."""
     with torch.no_grad():
         res_t = fn(*_true_inputs(inputs), **kw)
-    if not _state.STATE.recording:
+    if not _state.STATE.recording or opname in INT_ZERO_GRAD:
         return res_t, None
-    res_f = _run(fn, [None if x is None else x._data for x in inputs], kw)
+    kw_f = kw
+    if _int_dtype_attr(kw):
+        kw_f = dict(kw, dtype='float64')     # an integer result dtype keeps the float path differentiable
+    res_f = _run(fn, [None if x is None else x._data for x in inputs], kw_f)
     if isinstance(res_t, (tuple, list)):
         pairs = [_merge_shadow(f, t) for f, t in zip(res_f, res_t)]
         return type(res_t)(p[0] for p in pairs), [p[1] for p in pairs]
@@ -192,8 +211,8 @@ def invoke(op, inputs, attrs, out=None):
         box = engine.rng_failure()
     idts = None
     try:
-        if _shadowed(inputs) and not _amp.active:
-            res, idts = _run_shadow(op.fn, inputs, attrs)
+        if _shadowed(inputs, attrs) and not _amp.active:
+            res, idts = _run_shadow(op.fn, inputs, attrs, op.name)
         elif _profiler.active_imperative:
             with _profiler.op_span(_profiler.current_scope() + op.name):
                 res = _run(op.fn, tin, attrs)

@@ -2,7 +2,8 @@
 src/operator/numpy/linalg/*).  Each function is a registered ``_npi_*`` op
 (torch.linalg underneath: rocSOLVER/hipBLAS on the GPU), differentiable where
 torch.linalg is."""
-from .multiarray import _call, _as_nd
+from .multiarray import _call, _as_nd, _is_sym
+from ..ndarray.ndarray import NDArray
 
 __all__ = ['norm', 'svd', 'cholesky', 'inv', 'det', 'slogdet', 'solve', 'tensorinv', 'tensorsolve', 'pinv',
            'eigvals', 'eig', 'eigvalsh', 'eigh', 'qr', 'lstsq', 'matrix_rank', 'matrix_power', 'multi_dot', 'cond']
@@ -50,7 +51,9 @@ def tensorsolve(a, b, axes=None):
 
 
 def pinv(a, rcond=1e-15, hermitian=False):
-    return _call('_npi_pinv', _as_nd(a), rcond=float(rcond), hermitian=hermitian)
+    if isinstance(rcond, NDArray) or _is_sym(rcond):
+        return _call('_npi_pinv', _as_nd(a), rcond, hermitian=hermitian)
+    return _call('_npi_pinv_scalar_rcond', _as_nd(a), rcond=float(rcond), hermitian=hermitian)
 
 
 def eigvals(a):

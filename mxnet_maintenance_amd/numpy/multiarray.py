@@ -11,6 +11,7 @@ operator, so it works imperatively on ndarrays and builds graph nodes when given
 Symbols (``F.np.*`` inside a hybridized block).
 """
 import builtins
+import functools
 import numbers
 
 import numpy as onp
@@ -27,6 +28,105 @@ from ..ndarray import register as _reg
 from ..ops import registry as _registry
 
 __all__ = []   # filled at the end
+
+
+# ---------------------------------------------------------------------------
+# Host-computed functions inside hybridized graphs.  Functions whose output shape depends on the
+# data (unique, bincount, nonzero-style indices, ...) or that run on the host (window functions,
+# sampling helpers) become ONE graph node of the generic ``_np_host_call`` operator when called
+# with Symbols: the Symbol arguments are the node's inputs, every other argument is stored as a
+# JSON attribute, and the executor calls the same Python function on the NDArrays at run time
+# (the reference runs these as dynamic-shape FComputeEx operators).
+_HOST_FNS = {}
+
+
+def _host_graph(name, nout=1, stack=False):
+    """Decorator: make ``f`` build an ``_np_host_call`` node when any argument is a Symbol (or in
+    forced-symbol mode); ``nout`` is an int or ``f(bound_arguments) -> int``.  With ``stack`` a
+    tuple result whose length depends on input shapes (unravel_index, diag_indices_from) becomes
+    one stacked array in the graph, as the reference's operators return it."""
+    import inspect
+    import json
+
+    def deco(f):
+        sig = inspect.signature(f)
+        _HOST_FNS[name] = (f, stack)
+
+        @functools.wraps(f)
+        def g(*args, **kwargs):
+            if not (_FORCE_SYM[0] or builtins.any(_is_sym(a) for a in args)
+                    or builtins.any(_is_sym(v) for v in kwargs.values())):
+                return f(*args, **kwargs)
+            bound = sig.bind(*args, **kwargs)
+            bound.apply_defaults()
+            inputs, names, consts = [], [], {}
+            for k, v in bound.arguments.items():
+                if _is_sym(v):
+                    inputs.append(v)
+                    names.append(k)
+                elif isinstance(v, (list, tuple)) and v and builtins.all(_is_sym(x) for x in v):
+                    raise MXNetError('%s: lists of symbols are not supported in a graph' % name)
+                else:
+                    consts[k] = _json_value(v)
+            n = nout(bound.arguments) if callable(nout) else nout
+            from ..symbol.symbol import _op_func
+            return _op_func('_npi_host_call')(*inputs, fn=name, names=json.dumps(names), kwargs=json.dumps(consts),
+                                             nout=n, num_args=len(inputs))
+        return g
+    return deco
+
+
+class _FORCE_SYM_OFF:
+    """Run a host function imperatively even while a graph is being traced."""
+
+    def __enter__(self):
+        self._prev, _FORCE_SYM[0] = _FORCE_SYM[0], False
+
+    def __exit__(self, *exc):
+        _FORCE_SYM[0] = self._prev
+
+
+def _json_value(v):
+    if isinstance(v, (onp.dtype, type)) or isinstance(v, torch.dtype):
+        return {'__dtype__': _dtype_name(v)}
+    if isinstance(v, onp.generic):
+        return v.item()
+    if isinstance(v, tuple):
+        return {'__tuple__': [_json_value(x) for x in v]}
+    if isinstance(v, list):
+        return [_json_value(x) for x in v]
+    if isinstance(v, NDArray):
+        return {'__array__': v.asnumpy().tolist(), 'dtype': str(v.dtype)}
+    return v
+
+
+def _from_json_value(v):
+    if isinstance(v, dict):
+        if '__dtype__' in v:
+            return v['__dtype__']
+        if '__tuple__' in v:
+            return tuple(_from_json_value(x) for x in v['__tuple__'])
+        if '__array__' in v:
+            return array(onp.asarray(v['__array__'], dtype=v['dtype']))
+    if isinstance(v, list):
+        return [_from_json_value(x) for x in v]
+    return v
+
+
+def _run_host_call(inputs, fn, inputs_json, kwargs_json):
+    """Executor side of ``_np_host_call``: the registered function on NDArray views of ``inputs``."""
+    import json
+    f, do_stack = _HOST_FNS[fn]
+    kw = {k: _from_json_value(v) for k, v in json.loads(kwargs_json).items()}
+    for k, t in zip(json.loads(inputs_json), inputs):
+        kw[k] = ndarray(t)
+    with _FORCE_SYM_OFF():
+        res = f(**kw)
+    if do_stack:
+        res = stack(res) if len(res) else zeros((0,), dtype='int64')
+    if isinstance(res, (list, tuple)):
+        return tuple(r._data if isinstance(r, NDArray) else torch.as_tensor(r) for r in res)
+    return res._data if isinstance(res, NDArray) else torch.as_tensor(res)
 
 
 def _export(f):
@@ -1157,7 +1257,8 @@ def trace(a, offset=0, axis1=0, axis2=1, out=None):
 def pad(x, pad_width, mode='constant', **kwargs):
     pw = pad_width.tolist() if isinstance(pad_width, NDArray) else pad_width
     return _call('_npi_pad', _as_nd(x), pad_width=pw, mode=mode,
-                 constant_values=float(kwargs.get('constant_values', 0)))
+                 constant_values=float(kwargs.get('constant_values', 0)),
+                 reflect_type=kwargs.get('reflect_type', 'even'))
 
 
 @_export
@@ -1309,6 +1410,7 @@ def diff(a, n=1, axis=-1, prepend=None, append=None):  # pylint: disable=redefin
 
 
 @_export
+@_host_graph('ediff1d')
 def ediff1d(ary, to_end=None, to_begin=None):
     d = diff(ravel(ary))
     parts = ([ravel(_as_nd(to_begin, ary.context))] if to_begin is not None else []) + [d] + \
@@ -1335,13 +1437,14 @@ def insert(arr, obj, values, axis=None):
     o = obj.tolist() if isinstance(obj, NDArray) else obj
     if isinstance(o, slice):
         n = arr.shape[axis] if axis is not None else arr.size
-        o = list(range(n + 1))[o]
+        o = list(range(n))[o]
     if _is_scalar(values):
         return _call('_npi_insert_scalar', arr, obj=o, values=_py(values), axis=axis)
     return _call('_npi_insert_tensor', arr, _as_nd(values, arr.context), obj=o, axis=axis)
 
 
 @_export
+@_host_graph('resize')
 def resize(a, new_shape):
     new_shape = _shape(new_shape)
     n = int(onp.prod(new_shape))
@@ -1407,22 +1510,26 @@ def _host(a):
 
 
 @_export
+@_host_graph('nonzero', stack=True)
 def nonzero(a):
     t = _as_nd(a)._data
     return tuple(ndarray(x) for x in torch.nonzero(t, as_tuple=True))
 
 
 @_export
+@_host_graph('argwhere')
 def argwhere(a):
     return ndarray(torch.nonzero(_as_nd(a)._data))
 
 
 @_export
+@_host_graph('flatnonzero')
 def flatnonzero(a):
     return ndarray(torch.nonzero(_as_nd(a)._data.reshape(-1)).reshape(-1))
 
 
 @_export
+@_host_graph('unique', nout=lambda b: 1 + builtins.sum(builtins.bool(b[k]) for k in ('return_index', 'return_inverse', 'return_counts')))
 def unique(ar, return_index=False, return_inverse=False, return_counts=False, axis=None):
     res = onp.unique(_host(ar), return_index, return_inverse, return_counts, axis)
     ctx = ar.context if isinstance(ar, NDArray) else None
@@ -1432,6 +1539,7 @@ def unique(ar, return_index=False, return_inverse=False, return_counts=False, ax
 
 
 @_export
+@_host_graph('bincount')
 def bincount(x, weights=None, minlength=0):
     t = _as_nd(x)._data
     w = None if weights is None else _as_nd(weights)._data
@@ -1439,6 +1547,7 @@ def bincount(x, weights=None, minlength=0):
 
 
 @_export
+@_host_graph('histogram', nout=2)
 def histogram(a, bins=10, range=None, normed=None, weights=None, density=None):  # pylint: disable=redefined-builtin
     b = _host(bins) if isinstance(bins, NDArray) else bins
     h, e = onp.histogram(_host(a), b, range, density=density,
@@ -1448,6 +1557,7 @@ def histogram(a, bins=10, range=None, normed=None, weights=None, density=None): 
 
 
 @_export
+@_host_graph('unravel_index', stack=True)
 def unravel_index(indices, shape, order='C'):
     r = onp.unravel_index(_host(indices).astype(onp.int64), shape, order)
     return tuple(array(x, dtype=onp.int64) for x in r)
@@ -1460,6 +1570,7 @@ def ravel_multi_index(multi_index, dims, mode='raise', order='C'):
 
 
 @_export
+@_host_graph('diag_indices_from', stack=True)
 def diag_indices_from(arr):
     n = arr.shape[0]
     return tuple(arange(n, dtype='int64', ctx=arr.context) for _ in range(arr.ndim))
@@ -1488,13 +1599,13 @@ def searchsorted(a, v, side='left', sorter=None):
 
 @_export
 def polyval(p, x):
-    r = zeros_like(x) if isinstance(x, NDArray) else 0.0
-    for c in (p if not isinstance(p, NDArray) else [p[i] for i in range(p.shape[0])]):
-        r = r * x + c
-    return r
+    if _is_scalar(x) and not _is_sym(p):
+        return _call('_npi_polyval', _as_nd(p), _as_nd(onp.asarray(x), p.context if isinstance(p, NDArray) else None))
+    return _call('_npi_polyval', _as_nd(p), _as_nd(x))
 
 
 @_export
+@_host_graph('interp')
 def interp(x, xp, fp, left=None, right=None, period=None):
     r = onp.interp(_host(x), _host(xp), _host(fp), left, right, period)
     return array(r, dtype=onp.float32)
@@ -1505,16 +1616,19 @@ def interp(x, xp, fp, left=None, right=None, period=None):
 # ---------------------------------------------------------------------------
 
 @_export
+@_host_graph('hanning')
 def hanning(M, dtype=None, ctx=None):
     return array(onp.hanning(M), dtype=dtype or onp.float32, ctx=ctx)
 
 
 @_export
+@_host_graph('hamming')
 def hamming(M, dtype=None, ctx=None):
     return array(onp.hamming(M), dtype=dtype or onp.float32, ctx=ctx)
 
 
 @_export
+@_host_graph('blackman')
 def blackman(M, dtype=None, ctx=None):
     return array(onp.blackman(M), dtype=dtype or onp.float32, ctx=ctx)
 

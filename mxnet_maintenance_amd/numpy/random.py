@@ -9,7 +9,7 @@ import torch
 
 from ..context import current_context
 from ..ndarray.ndarray import NDArray
-from .multiarray import _call, ndarray, _is_scalar
+from .multiarray import _call, ndarray, _is_scalar, _host_graph
 
 __all__ = ['randint', 'uniform', 'normal', 'lognormal', 'logistic', 'gumbel', 'multinomial', 'multivariate_normal',
            'choice', 'rayleigh', 'rand', 'exponential', 'weibull', 'pareto', 'power', 'shuffle', 'gamma', 'beta',
@@ -167,13 +167,18 @@ def multinomial(n, pvals, size=None):
     return ndarray(counts.reshape(tuple(shp) + (p.numel(),)))
 
 
+@_host_graph('random_multivariate_normal')
 def multivariate_normal(mean, cov, size=None, check_valid=None, tol=None):
+    """Samples of shape ``size + broadcast(mean.shape, cov.shape[:-1])`` in the dtype of ``mean``."""
     dev = mean.context.torch_device if isinstance(mean, NDArray) else torch.device('cpu')
-    m, c = _t(mean, dev).float(), _t(cov, dev).float()
+    mt = _t(mean, dev)
+    m, c = mt.double(), _t(cov, dev).double()
     d = torch.distributions.MultivariateNormal(m, covariance_matrix=c)
-    return ndarray(d.sample(_size(size) or ()))
+    r = d.sample(_size(size) or ())
+    return ndarray(r.to(mt.dtype if mt.is_floating_point() else torch.float32))
 
 
+@_host_graph('random_choice')
 def choice(a, size=None, replace=True, p=None, ctx=None, out=None):
     dev = _dev(ctx)
     if isinstance(a, int):

@@ -8,6 +8,8 @@ hybridized blocks.
 """
 import functools
 
+import torch
+
 from .. import _state
 from ..context import cpu, gpu, num_gpus, current_context, cpu_pinned  # noqa: F401
 from ..util import (set_np, reset_np, is_np_array, is_np_shape, use_np, use_np_array, use_np_shape,  # noqa: F401
@@ -15,6 +17,8 @@ from ..util import (set_np, reset_np, is_np_array, is_np_shape, use_np, use_np_a
 from ..ndarray.ndarray import NDArray, waitall  # noqa: F401
 from ..ndarray import register as _reg
 from ..ops import registry as _registry
+from ..base import torch_dtype as _torch_dtype
+from ..numpy.multiarray import _host_graph
 
 
 def _is_sym(x):
@@ -83,11 +87,14 @@ def reshape(a, newshape, reverse=False, order='C'):
                  reverse=reverse, order=order)
 
 
+@_host_graph('npx_nonzero')
 def nonzero(a):
-    """Indices of non-zero elements as an ``(N, ndim)`` int64 array."""
+    """Indices of non-zero elements as an ``(N, ndim)`` int64 array (a 0-d input counts as 1-d,
+    as in src/operator/numpy/np_nonzero_op.cc)."""
     import torch
     from ..numpy import ndarray
-    return ndarray(torch.nonzero(a._data))
+    t = a._data
+    return ndarray(torch.nonzero(t.reshape(1) if t.dim() == 0 else t))
 
 
 def seed(seed=None, ctx='all', **kwargs):  # pylint: disable=redefined-outer-name
@@ -128,15 +135,31 @@ def _random_ns():
     from ..numpy import ndarray, random as nprand
 
     def bernoulli(prob=None, logit=None, size=None, dtype=None, ctx=None, out=None):
+        """Bernoulli samples from ``prob`` or ``logit`` (exactly one of them; probabilities outside
+        [0, 1] raise ValueError, as src/operator/numpy/random/np_bernoulli_op.h checks)."""
         from ..numpy.multiarray import _call
+        if (prob is None) == (logit is None):
+            raise ValueError('bernoulli: exactly one of prob and logit must be given')
+        shp = None if size is None else ((size,) if isinstance(size, int) else tuple(size))
         if logit is not None:
-            prob = 1.0 / (1.0 + __import__('math').exp(-logit)) if not isinstance(logit, NDArray) else \
-                ndarray(torch.sigmoid(logit._data))
-        if isinstance(prob, NDArray):
-            shp = tuple(size) if size is not None else tuple(prob.shape)
-            return ndarray((torch.rand(shp, device=prob._data.device) < prob._data).float())
-        return _call('_npi_bernoulli', prob=float(prob), size=(size,) if isinstance(size, int) else (size or ()),
-                     ctx=ctx or current_context(), dtype=dtype or 'float32')
+            p = torch.sigmoid(logit._data.double()) if isinstance(logit, NDArray) else \
+                torch.tensor(1.0 / (1.0 + __import__('math').exp(-logit)), dtype=torch.float64)
+        elif isinstance(prob, NDArray):
+            p = prob._data
+            if p.numel() and (bool((p < 0).any()) or bool((p > 1).any())):
+                raise ValueError('bernoulli: prob must lie in [0, 1]')
+        else:
+            if not 0.0 <= float(prob) <= 1.0:
+                raise ValueError('bernoulli: prob must lie in [0, 1]')
+            return _call('_npi_bernoulli', prob=float(prob), size=shp or (), ctx=ctx or current_context(),
+                         dtype=dtype or 'float32')
+        shp = tuple(p.shape) if shp is None else shp
+        r = torch.rand(shp, device=p.device, dtype=torch.float64) < p.double()
+        res = ndarray(r.to(_torch_dtype(dtype or 'float32')))
+        if out is not None:
+            out[...] = res
+            return out
+        return res
 
     def uniform_n(low=0.0, high=1.0, batch_shape=None, dtype=None, ctx=None):
         # output shape = batch_shape + the parameters' broadcast shape (reference: np_random_n ops)

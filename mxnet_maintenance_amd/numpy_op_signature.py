@@ -33,6 +33,13 @@ def _get_builtin_op(op_name):
     op = getattr(module, rest, None)
     if op is None:
         raise ValueError('Cannot find operator {} in module {}'.format(rest, module.__name__))
+    from . import _numpy_op_doc
+    doc = getattr(_numpy_op_doc, op_name, None)
+    if doc is not None and getattr(op, '__signature__', None) is None:
+        try:
+            op.__signature__ = inspect.signature(doc)
+        except (AttributeError, TypeError):
+            pass
     return op
 
 

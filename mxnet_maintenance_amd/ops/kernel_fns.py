@@ -846,9 +846,48 @@ def _select(key, cands, default, timing=None):
     return (table[name] if name in table else cands[0][1])()
 
 
+_NCU = {}
+
+
+def _num_cus(dev):
+    n = _NCU.get(dev)
+    if n is None:
+        n = _NCU[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return n
+
+
+def pw_ok(x, kin, nout):
+    """True when the streaming 1x1 kernel (src/kernels/conv_pw.hip) takes a Cin=kin -> Cout=nout conv of
+    the NHWC activation ``x``."""
+    return (_CONV_HIP and x.is_cuda and x.dtype in (torch.float16, torch.bfloat16) and x.is_contiguous()
+            and x.data_ptr() % 16 == 0 and hasattr(_K.lib(), 'conv_pw_stream')
+            and bool(_K.lib().conv_pw_stream_ok(int(kin), int(nout))))
+
+
+def conv_pw(x, w2, bn_stats=False):
+    """y = x . w2^T for NHWC ``x`` [..., Cin] and ``w2`` [Cout, Cin] on the streaming 1x1 kernel;
+    ``bn_stats``: BatchNorm sum / sum-of-squares partials in ``y._mxamd_bn_part`` (one per workgroup)."""
+    C = x.shape[-1]
+    K = w2.shape[0]
+    M = x.numel() // C
+    w2 = w2.contiguous()
+    y = torch.empty(x.shape[:-1] + (K,), dtype=x.dtype, device=x.device)
+    lib = _K.lib()
+    grid = lib.conv_pw_stream_grid(M, C, K, _num_cus(x.device))
+    part = torch.empty(2 * K * grid, dtype=torch.float32, device=x.device) if bn_stats else None
+    lib.conv_pw_stream(_DT[x.dtype], x.data_ptr(), w2.data_ptr(), y.data_ptr(), _zero_page(x.device).data_ptr(), M, C,
+                       K, _p(part), grid, _stream())
+    if part is not None:
+        y._mxamd_bn_part = (part, grid)
+    return y
+
+
 def _fwd_candidates(x, w, stride, pad, bias):
     c = []
     K, R, S, C = w.shape
+    if (R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0) and bias is None
+            and pw_ok(x, C, K)):
+        c.append(('pw', lambda: conv_pw(x, w.reshape(K, C), bn_stats=bool(_state.STATE.training))))
     if stem_ok(x, w, stride, pad, bias):
         c.append(('stem', lambda: conv_stem_fwd(x, w, pad, bn_stats=bool(_state.STATE.training))))
     if conv_ok_shape(x, w, stride, pad):
@@ -922,6 +961,8 @@ def _dgrad_candidates(dy, x, w, stride, pad):
     K, R, S, C = w.shape
     if R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0):
         c.append(('mm', lambda: torch.mm(dy.reshape(-1, K), w.reshape(K, C)).view(x.shape)))
+        if pw_ok(dy, K, C):
+            c.append(('pw', lambda: conv_pw(dy, w.reshape(K, C).t())))
         c.extend(_gemm_dgrad_1x1(dy, w, x.shape))
     if (tuple(stride) == (1, 1) and C % 64 == 0 and K % 32 == 0 and 2 * pad[0] == R - 1 and 2 * pad[1] == S - 1
             and _CONV_HIP):

@@ -14,6 +14,7 @@ the HIP kernels (ops/hip_ops.py) directly, and the torch reference path views
 it as a channels_last NCHW tensor (zero copies).
 """
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -1209,7 +1210,7 @@ def rnn(data, parameters, state, state_cell=None, sequence_length=None, state_si
         # the fused torch kernels do not validate state shapes
         raise MXNetError('RNN: state shape %s does not match %s' % (tuple(state.shape), want))
     from . import rnn_fns
-    if rnn_fns.available(data) and not projection_size:
+    if rnn_fns.available(data) and not projection_size and os.environ.get('MXAMD_RNN_VENDOR', '0') != '1':
         # in-tree gfx950 recurrent kernels (src/kernels/rnn.hip): fused gate GEMM + cell per step
         out, h, c = rnn_fns.fused_rnn(data, ws, state, state_cell, mode, num_layers, bidirectional, p, train)
         if mode == 'lstm':

@@ -209,6 +209,9 @@ def _sum(a, axis=None, keepdims=False, dtype=None, initial=None):
         # accumulate one precision up (fp16 -> fp32, fp32 -> fp64: the reference's AccType), then cast
         acc = torch.float64 if a.dtype == torch.float32 else torch.float32
         r = torch.sum(a, dim=d, keepdim=keepdims, dtype=acc).to(dt or a.dtype)
+    elif d and dt is not None and dt.is_floating_point and a.is_floating_point() and \
+            torch.finfo(a.dtype).bits > torch.finfo(dt).bits:
+        r = torch.sum(a, dim=d, keepdim=keepdims).to(dt)    # accumulate in the wider input type
     else:
         r = torch.sum(a, dim=d, keepdim=keepdims, dtype=dt) if d else (a.to(dt) if dt else a.clone())
     return r + initial if initial is not None else r
@@ -228,6 +231,15 @@ def _mean(a, axis=None, keepdims=False, dtype=None):
     dt = _td(dtype) or (a.dtype if a.is_floating_point() else _FLOAT)
     d = _red_dims(a, axis)
     acc = dt if dt.is_floating_point else torch.float64     # integer dtype: float mean, then cast
+    if a.is_floating_point() and acc.is_floating_point and torch.finfo(a.dtype).bits > torch.finfo(acc).bits:
+        acc = a.dtype          # narrowing dtype: reduce (and differentiate) in the input precision
+    if not dt.is_floating_point and not a.is_floating_point() and d:
+        # integer input and result: numpy sums in the result type (wrapping) and truncates the quotient
+        n = 1
+        for k in d:
+            n *= a.shape[k]
+        s_ = torch.sum(a.to(dt), dim=d, keepdim=keepdims, dtype=dt)
+        return torch.trunc(s_.to(torch.float64) / max(n, 1)).to(dt)
     r = torch.mean(a.to(acc), dim=d, keepdim=keepdims) if d else a.to(acc).clone()
     return r.to(dt)
 
@@ -643,35 +655,41 @@ def _trace(a, offset=0, axis1=0, axis2=1):
 @register('_npi_pad', arg_names=('a',), params={'pad_width': ('any', ()), 'mode': ('str', 'constant'),
                                                'constant_values': ('float', 0.0), 'reflect_type': ('str', 'even')})
 def _pad(a, pad_width=(), mode='constant', constant_values=0.0, reflect_type='even'):
+    """numpy.pad (src/operator/numpy/np_pad_op-inl.h).  Constant padding is one device op; the
+    index-permuting modes (reflect, symmetric, edge, wrap) gather through a host-computed index
+    map (numpy's own rules applied to element codes); the statistic modes pad axis by axis."""
     pw = onp.broadcast_to(onp.asarray(pad_width, dtype=onp.int64).reshape(-1, 2) if onp.ndim(pad_width) else
                           onp.full((1, 2), pad_width), (a.dim(), 2))
-    flat = []
-    for lo, hi in reversed(pw.tolist()):
-        flat += [lo, hi]
-    tmode = {'constant': 'constant', 'reflect': 'reflect', 'edge': 'replicate', 'wrap': 'circular',
-             'symmetric': None}[mode]
-    if tmode == 'constant':
+    if mode == 'constant':
+        flat = []
+        for lo, hi in reversed(pw.tolist()):
+            flat += [lo, hi]
         return torch.nn.functional.pad(a, flat, value=constant_values)
-    if tmode is None:      # symmetric: reflect including the edge sample
-        x = a
-        for d, (lo, hi) in enumerate(pw.tolist()):
-            parts = []
-            if lo:
-                parts.append(torch.flip(x.narrow(d, 0, lo), (d,)))
-            parts.append(x)
-            if hi:
-                parts.append(torch.flip(x.narrow(d, x.shape[d] - hi, hi), (d,)))
-            x = torch.cat(parts, d)
-        return x
-    x = _fl(a)
-    nspatial = max(1, a.dim() - 2)
-    lead = a.dim() - nspatial
-    xx = x.reshape((1, -1) + tuple(x.shape[lead:])) if lead != 2 else x
-    out = torch.nn.functional.pad(xx, flat[:2 * nspatial], mode=tmode)
-    out = out.reshape(tuple(x.shape[:lead]) + tuple(out.shape[2:])) if lead != 2 else out
-    if any(flat[2 * nspatial:]):
-        raise NotImplementedError('non-constant padding of leading axes')
-    return out.to(a.dtype)
+    if mode in ('reflect', 'symmetric', 'edge', 'wrap'):
+        if reflect_type != 'even' and mode in ('reflect', 'symmetric'):
+            raise NotImplementedError("pad: reflect_type='odd'")
+        return _gather_map(onp.pad(_codes(tuple(a.shape)), pw, mode=mode), a)
+    stat = {'minimum': lambda x, d: x.amin(d, keepdim=True), 'maximum': lambda x, d: x.amax(d, keepdim=True),
+            'mean': lambda x, d: x.mean(d, keepdim=True) if x.is_floating_point() else
+            x.double().mean(d, keepdim=True).round().to(x.dtype)}.get(mode)
+    if stat is None:
+        raise MXNetError('pad: unsupported mode %s' % mode)
+    x = a
+    for d, (lo, hi) in enumerate(pw.tolist()):
+        if not (lo or hi):
+            continue
+        s_ = stat(x, d)
+        shp = list(x.shape)
+        parts = []
+        if lo:
+            shp[d] = lo
+            parts.append(s_.expand(shp))
+        parts.append(x)
+        if hi:
+            shp[d] = hi
+            parts.append(s_.expand(shp))
+        x = torch.cat(parts, d)
+    return x
 
 
 @register('_npi_clip', aliases=('_np_clip',), arg_names=('a',), params={'a_min': ('float?', None), 'a_max': ('float?', None)})
@@ -866,18 +884,35 @@ def _cross(a, b, axisa=-1, axisb=-1, axisc=-1, axis=None):
     return torch.movedim(torch.linalg.cross(a, b), -1, axisc)
 
 
+def _gather_map(idx, arr, values=None):
+    """Gather ``arr`` (codes >= 0) and ``values`` (codes < 0, value element ``-code - 1``) into the
+    layout described by the int64 code array ``idx`` -- differentiable in both sources."""
+    t = torch.as_tensor(onp.ascontiguousarray(idx), dtype=torch.long, device=arr.device)
+    src = arr.reshape(-1)
+    if values is not None:
+        src = torch.cat([src, values.to(arr.dtype).reshape(-1)])
+        t = torch.where(t >= 0, t, arr.numel() - 1 - t)
+    return src[t.reshape(-1)].reshape(t.shape)
+
+
+def _codes(shape):
+    return onp.arange(int(onp.prod(shape, dtype=onp.int64)), dtype=onp.int64).reshape(shape)
+
+
 @register('_npi_delete', arg_names=('arr',), params={'obj': ('any', 0), 'axis': ('int?', None)})
 def _delete(arr, obj=0, axis=None):
-    if axis is None:
-        arr, axis = arr.reshape(-1), 0
-    n = arr.shape[axis]
-    keep = torch.ones(n, dtype=torch.bool)
+    """numpy.delete via an index map computed on the host (src/operator/numpy/np_delete_op-inl.h):
+    out-of-range entries of an index list are ignored, as in the reference."""
+    codes = _codes(tuple(arr.shape))
+    n = codes.size if axis is None else codes.shape[axis]
     if isinstance(obj, slice):
-        keep[obj] = False
+        o = obj
+    elif onp.ndim(obj) == 0:
+        o = int(obj)
     else:
-        idx = torch.as_tensor(obj, dtype=torch.long).reshape(-1)
-        keep[idx % n] = False
-    return torch.index_select(arr, axis, torch.nonzero(keep).reshape(-1).to(arr.device))
+        o = onp.asarray(obj, dtype=onp.int64).reshape(-1)
+        o = o[(o >= 0) & (o < n)]
+    return _gather_map(onp.delete(codes, o, axis=axis), arr)
 
 
 @register('_npi_insert_scalar', arg_names=('arr',), params={'obj': ('any', 0), 'values': ('any', 0.0),
@@ -892,29 +927,13 @@ def _insert_tensor(arr, values, obj=0, axis=None):
 
 
 def _insert_t(arr, values, obj, axis):
-    if axis is None:
-        arr, axis = arr.reshape(-1), 0
-    axis %= max(arr.dim(), 1)
-    n = arr.shape[axis]
-    if isinstance(obj, int):
-        v = values
-        while v.dim() < arr.dim():
-            v = v.unsqueeze(0)
-        v = torch.movedim(v, 0, axis)
-        k = v.shape[axis]
-        pos = onp.full(k, obj + n if obj < 0 else obj)
-    else:
-        pos = onp.arange(n + 1)[obj] if isinstance(obj, slice) else onp.asarray(obj, dtype=onp.int64).reshape(-1)
-        pos = onp.where(pos < 0, pos + n, pos)
-        k = len(pos)
-        v = values
-    tshape = list(arr.shape)
-    tshape[axis] = k
-    v = v.to(arr.dtype).expand(tshape) if v.dim() <= arr.dim() else v
-    mapping = onp.insert(onp.arange(n), pos, onp.arange(n, n + k)) if not isinstance(obj, int) else \
-        onp.insert(onp.arange(n), int(pos[0]), onp.arange(n, n + k))
-    src = torch.cat([arr, v.to(arr.device)], axis)
-    return torch.index_select(src, axis, torch.as_tensor(mapping, dtype=torch.long, device=arr.device))
+    """numpy.insert: the host computes where every output element comes from (numpy's own
+    placement and broadcasting rules on index codes), the device gathers."""
+    o = obj if isinstance(obj, slice) or onp.ndim(obj) == 0 else onp.asarray(obj, dtype=onp.int64)
+    if onp.ndim(o) == 0 and not isinstance(o, slice):
+        o = int(o)
+    vcodes = -1 - _codes(tuple(values.shape))
+    return _gather_map(onp.insert(_codes(tuple(arr.shape)), o, vcodes, axis=axis), arr, values)
 
 
 # ---------------------------------------------------------------------------
@@ -1012,8 +1031,13 @@ _lin('det', lambda A: torch.linalg.det(_fl(A)))
 _lin('slogdet', lambda A: tuple(torch.linalg.slogdet(_fl(A))), 2)
 _lin('solve', lambda A, B: torch.linalg.solve(_fl(A), _fl(B)) if B.dim() != A.dim() - 1 else
      torch.linalg.solve(_fl(A), _fl(B).unsqueeze(-1)).squeeze(-1), args=('A', 'B'))
-_lin('pinv', lambda A, rcond=1e-15, hermitian=False: torch.linalg.pinv(_fl(A), rtol=rcond, hermitian=hermitian),
+_lin('pinv_scalar_rcond', lambda A, rcond=1e-15, hermitian=False: torch.linalg.pinv(_fl(A), rtol=rcond,
+                                                                                     hermitian=hermitian),
      params={'rcond': ('float', 1e-15), 'hermitian': ('bool', False)})
+# rcond as an array broadcast over the batch of matrices (numpy.linalg.pinv)
+_lin('pinv', lambda A, rcond, hermitian=False: torch.linalg.pinv(_fl(A), rtol=rcond.to(_fl(A).dtype),
+                                                                 hermitian=hermitian),
+     params={'hermitian': ('bool', False)}, args=('A', 'rcond'))
 _lin('eigvals', lambda A: torch.linalg.eigvals(_fl(A)).real)
 _lin('eig', lambda A: tuple(t.real for t in torch.linalg.eig(_fl(A))), 2)
 _lin('eigvalsh', lambda A, UPLO='L': torch.linalg.eigvalsh(_fl(A), UPLO=UPLO), params={'UPLO': ('str', 'L')})
@@ -1045,7 +1069,17 @@ def _tensorinv(a, ind=2):
 
 @register('_npi_tensorsolve', arg_names=('a', 'b'), params={'a_axes': ('shape?', None)})
 def _tensorsolve(a, b, a_axes=None):
-    return torch.linalg.tensorsolve(_fl(a), _fl(b), dims=a_axes)
+    """numpy.linalg.tensorsolve's reshaping rules, including 0-d operands and a.ndim == b.ndim."""
+    a, b = _fl(a), _fl(b)
+    an = a.dim()
+    if a_axes is not None:
+        order = [k for k in range(an) if k not in [x % an for x in a_axes]] + [x % an for x in a_axes]
+        a = a.permute(order)
+    tail = tuple(a.shape)[-(an - b.dim()):]
+    n = int(onp.prod(tail, dtype=onp.int64))
+    if n * n != a.numel() or n != b.numel():
+        raise MXNetError('tensorsolve: a of shape %s is not square for b of shape %s' % (tuple(a.shape), tuple(b.shape)))
+    return torch.linalg.solve(a.reshape(n, n), b.reshape(n)).reshape(tail)
 
 
 @register('_npi_multi_dot', arg_names=lambda a: ['data%d' % i for i in range(int(a.get('num_args', 1)))],
@@ -1303,3 +1337,52 @@ def _np_sampler(*arrays, kind='normal', pscal=(), size=None, ctx=None, dtype='fl
     cdt = torch.float32 if dt in (torch.float16, torch.bfloat16) and dev.type == 'cpu' else dt
     ps = [(p.expand(shape) if p.dim() else p).to(cdt) for p in ps]
     return _sampler_draw(kind, ps, shape, dev, cdt).to(dt)
+
+
+
+# ---------------------------------------------------------------------------
+# generic node for host-computed / data-dependent numpy functions in graphs (see
+# numpy/multiarray.py _host_graph): the function is looked up by name at run time
+# ---------------------------------------------------------------------------
+@register('_npi_host_call', arg_names=lambda a: ['data%d' % i for i in range(int(a.get('num_args', 0) or 0))],
+          key_var_num_args='num_args', num_outputs=lambda a: int(a.get('nout', 1) or 1),
+          params={'fn': ('str', ''), 'names': ('str', '[]'), 'kwargs': ('str', '{}'), 'nout': ('int', 1),
+                  'num_args': ('int', 0)})
+def np_host_call(*data, fn='', names='[]', kwargs='{}', nout=1, num_args=0):
+    from ..numpy import multiarray as _ma
+    return _ma._run_host_call(list(data), fn, names, kwargs)
+
+
+@register('_npi_polyval', arg_names=['p', 'x'])
+def npi_polyval(p, x):
+    """Horner evaluation of the coefficient vector ``p`` at ``x`` (src/operator/numpy/np_polynomial_op.cc)."""
+    dt = torch.promote_types(p.dtype, x.dtype)
+    r = torch.zeros_like(x, dtype=dt)
+    for i in range(p.shape[0]):
+        r = r * x + p[i]
+    return r
+
+
+# ---------------------------------------------------------------------------
+# boolean-mask assignment (a[mask] = v with the mask starting at ``start_axis``)
+# src/operator/numpy/np_boolean_mask_assign.cc
+# ---------------------------------------------------------------------------
+def _mask_assign(data, mask, value, start_axis):
+    start_axis %= max(data.dim(), 1)
+    if tuple(data.shape[start_axis:start_axis + mask.dim()]) != tuple(mask.shape):
+        raise MXNetError('boolean_mask_assign: mask of shape %s does not match data %s at axis %d'
+                         % (tuple(mask.shape), tuple(data.shape), start_axis))
+    out = data.clone()
+    out[(slice(None),) * start_axis + (mask.to(torch.bool),)] = value.to(out.dtype)   # broadcasts
+    return out
+
+
+@register('_npi_boolean_mask_assign_scalar', arg_names=('data', 'mask'),
+          params={'value': ('float', 0.0), 'start_axis': ('int', 0)})
+def _bool_assign_scalar(data, mask, value=0.0, start_axis=0):
+    return _mask_assign(data, mask, torch.tensor(value, device=data.device), start_axis)
+
+
+@register('_npi_boolean_mask_assign_tensor', arg_names=('data', 'mask', 'value'), params={'start_axis': ('int', 0)})
+def _bool_assign_tensor(data, mask, value, start_axis=0):
+    return _mask_assign(data, mask, value, start_axis)

@@ -145,6 +145,10 @@ void slab_reduce(int out_dtype, float* slab, int splits, int64_t n, void* out, i
 void twobit_quantize(int dtype, const void* g, float* res, void* packed, int64_t n, float thr, hipStream_t s);
 void twobit_dequantize_sum(const void* packed, int64_t row_bytes, int nrows, int64_t n, float thr, float* out,
                            hipStream_t s);
+int conv_pw_stream_ok(int kin, int nout);
+int conv_pw_stream_grid(int M, int kin, int nout, int ncu);
+void conv_pw_stream(int dtype, const void* x, const void* w, void* y, const void* zero, int M, int kin, int nout,
+                    float* part, int grid, hipStream_t s);
 void conv_gen(int dtype, int mode, const void* src, const void* wsrc, const float* bias, void* dst, const int* geom,
               int splits, hipStream_t s);
 void rnn_fwd_seq(int dtype, int mode, const float* gx, const void* h0, const float* c0, const void* whh,
@@ -229,6 +233,15 @@ PYBIND11_MODULE(_hip_kernels, m) {
     gemm_nt(dt, P<void>(a), P<void>(b), P<float>(bias), P<void>(addend), P<void>(c), out_f32, M, N, K, lda, ldb, ldc,
             act, cfg, splits, P<float>(ws), S(s));
     check_launch("gemm_nt");
+  });
+  // streaming 1x1 convolution for small reductions (src/kernels/conv_pw.hip)
+  m.def("conv_pw_stream_ok", &conv_pw_stream_ok);
+  m.def("conv_pw_stream_grid", &conv_pw_stream_grid);
+  m.def("conv_pw_stream", [](int dt, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t zero, int M, int kin, int nout,
+                             uintptr_t part, int grid, uintptr_t s) {
+    conv_pw_stream(dt, P<const void>(x), P<const void>(w), P<void>(y), P<const void>(zero), M, kin, nout,
+                   P<float>(part), grid, S(s));
+    check_launch("conv_pw_stream");
   });
   // general implicit-GEMM convolution: grouped / dilated / 1-3-D / fp32 / transposed (src/kernels/conv_gen.hip)
   m.def("conv_gen", [](int dt, int mode, uintptr_t src, uintptr_t wsrc, uintptr_t bias, uintptr_t dst,

@@ -1,0 +1,359 @@
+// Streaming pointwise (1x1, stride 1) convolution for small reductions (gfx950).
+//
+// The 1x1 convolutions of a bottleneck with Cin = 64..512 do ~50-200 FLOP per byte they move, far
+// below the MFMA/HBM balance point (~400): they are memory-bound, and the general tiled kernels
+// (conv_big / conv_ring) run them at 1.5-3 TB/s because every workgroup walks load -> MFMA ->
+// epilogue with little overlap and re-reads the weight panel per tile.  This kernel is built for
+// the stream instead:
+//
+//   * persistent: 2 workgroups per CU walk the pixel tiles (XCD-aware order), so one workgroup's
+//     epilogue stores overlap the other's loads and MFMAs;
+//   * the whole weight matrix lives in REGISTERS for the kernel's lifetime -- wave (wc, wp) keeps the
+//     A fragments of its NOUT/WC output channels over the full reduction (<= 64 VGPRs);
+//   * input pixel tiles [BM][KIN] stream through an NST-stage LDS ring by LDS-DMA
+//     (global_load_lds_dwordx4, XOR-swizzled 16-byte chunks, out-of-range pixels from a zero page),
+//     D = NST-1 tiles in flight; the wait is a counted `s_waitcnt vmcnt(N)` with N known at compile
+//     time (every iteration issues the same number of VM ops), never a drain, plus a raw s_barrier;
+//   * epilogue: accumulators -> fp16/bf16 [BM][NOUT] LDS image (row pitch +16 B, conflict-free 8-byte
+//     writes) -> whole 16-byte row chunks -> coalesced global stores of complete pixel rows;
+//   * optional BatchNorm statistics: each thread keeps per-channel sum / sum-of-squares of the
+//     rows it stores over ALL its tiles; at the end one partial per workgroup per channel
+//     ([2][NOUT][grid] channel-major, the layout bn_nhwc.hip's finalize consumes).
+//
+// Requirements (host-checked): NHWC, KIN in {64,128,256,512}, NOUT in {64..1024} with
+// NOUT/WC * KIN <= 8192 (the register budget for the resident weights).
+#include <stdexcept>
+
+#include "common.h"
+
+namespace mxamd {
+
+namespace {
+
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void gbl_void;
+
+template <typename T>
+struct PwM;
+template <>
+struct PwM<__half> {
+  static __device__ __forceinline__ f4_t mma(const u32x4& a, const u32x4& b, f4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8_t, a), __builtin_bit_cast(half8_t, b), c,
+                                                  0, 0, 0);
+  }
+  static __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
+    __half2 lo = __floats2half2_rn(a, b), hi = __floats2half2_rn(c, d);
+    return uint2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
+  }
+};
+template <>
+struct PwM<__hip_bfloat16> {
+  static __device__ __forceinline__ f4_t mma(const u32x4& a, const u32x4& b, f4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                   c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ uint32_t two(float a, float b) {
+    return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, __float2bfloat16(a))) |
+           (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, __float2bfloat16(b))) << 16);
+  }
+  static __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
+    return uint2{two(a, b), two(c, d)};
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int KIN, int NOUT>
+struct PwCfg {
+  // pixels per tile: the input stage at most 16 KB and the epilogue image at most 32 KB
+  static constexpr int BM = (16384 / NOUT) < (8192 / KIN) ? (16384 / NOUT) : (8192 / KIN);
+  static constexpr int WC = NOUT / 16 < 8 ? NOUT / 16 : 8;  // waves along output channels
+  static constexpr int WP = 8 / WC;                        // waves along pixels
+  static constexpr int FC = NOUT / WC / 16;                // channel fragments per wave
+  static constexpr int FP = BM / WP / 16;                  // pixel fragments per wave
+  static constexpr int KS = KIN / 32;                      // MFMA k-steps
+  static constexpr int ROWB = KIN * 2;                     // input row bytes
+  static constexpr int STAGE = BM * ROWB;                  // one input tile
+  static constexpr int LPT = STAGE / (512 * 16);           // LDS-DMA instructions per thread per tile
+  static constexpr int PITCH = NOUT * 2 + 16;              // epilogue image row pitch
+  static constexpr int EPI = BM * PITCH;
+  static constexpr int OCH = NOUT / 8;                     // 16-byte chunks per output row
+  static constexpr int SPT = (BM * OCH + 511) / 512;       // 16-byte stores per thread per tile (uniform)
+  // deepest ring that keeps two workgroups per CU (<= 80 KB each)
+  static constexpr int NST = (4 * STAGE + EPI <= 80 * 1024) ? 4 : ((3 * STAGE + EPI <= 80 * 1024) ? 3 : 2);
+  static constexpr int D = NST - 1;
+  static constexpr int SMEM = NST * STAGE + EPI;
+  static_assert(FC >= 1 && FP >= 1, "at least one fragment pair per wave");
+  static_assert(LPT >= 1 && STAGE % (512 * 16) == 0, "whole LDS-DMA instructions per tile");
+  static_assert((BM * OCH) % 512 == 0 || BM * OCH < 512, "whole store rounds, or a single partial one");
+  static_assert(512 % OCH == 0, "a thread keeps one output chunk");
+  static_assert(D * (LPT + SPT) < 64, "vmcnt range");
+  static_assert(FC * KS * 4 <= 64, "resident weights exceed the register budget");
+  static_assert(ROWB % 128 == 0, "rows of whole 128-byte swizzle groups");
+};
+
+// Wait until at most `n` VM ops are outstanding (n rounded DOWN to an available level: waiting for
+// more than necessary is always safe).
+__device__ __forceinline__ void vm_wait_le(int n) {
+  if (n >= 48) vm_wait<48>();
+  else if (n >= 32) vm_wait<32>();
+  else if (n >= 24) vm_wait<24>();
+  else if (n >= 16) vm_wait<16>();
+  else if (n >= 12) vm_wait<12>();
+  else if (n >= 8) vm_wait<8>();
+  else if (n >= 6) vm_wait<6>();
+  else if (n >= 4) vm_wait<4>();
+  else if (n >= 3) vm_wait<3>();
+  else if (n >= 2) vm_wait<2>();
+  else if (n >= 1) vm_wait<1>();
+  else vm_wait<0>();
+}
+
+template <typename T, int KIN, int NOUT, bool STATS>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) conv_pw_stream_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                                T* __restrict__ y, const T* __restrict__ zero, int M,
+                                                                int ntiles, float* __restrict__ part) {
+  using C = PwCfg<KIN, NOUT>;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wc = wid % C::WC, wp = wid / C::WC;
+  const int grid = gridDim.x;
+  // XCD-aware: workgroups sharing an XCD take consecutive tiles
+  const int xcd = blockIdx.x & 7;
+  const int q8 = grid >> 3, r8 = grid & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+
+  // ---- resident weights: A fragments of this wave's channels, all k-steps
+  u32x4 wa[C::FC][C::KS];
+#pragma unroll
+  for (int f = 0; f < C::FC; ++f)
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) {
+      const int co = wc * C::FC * 16 + f * 16 + (lane & 15);
+      wa[f][s] = *reinterpret_cast<const u32x4*>(w + static_cast<int64_t>(co) * KIN + s * 32 + (lane >> 4) * 8);
+    }
+
+  // the weight loads retire here, before the ring starts: inside the loop the only VM ops are the
+  // ring's LDS-DMAs and the epilogue stores, so the counted waits below stay exact
+  vm_wait<0>();
+#pragma unroll
+  for (int f = 0; f < C::FC; ++f)
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) asm volatile("" ::"v"(wa[f][s]));
+
+  // ---- LDS-DMA issue of input tile `t` into ring stage `st`: instruction i of this thread covers
+  // bytes [(i*8+wid)*1024, +1024) of the stage (linear destination, swizzled source chunk)
+  auto issue = [&](int t, int st) {
+    char* sb = smem + st * C::STAGE;
+#pragma unroll
+    for (int i = 0; i < C::LPT; ++i) {
+      const int byte = ((i * 8 + wid) * 64 + lane) * 16;  // destination byte within the stage (linear)
+      const int row = byte / C::ROWB;
+      const int slot = (byte % C::ROWB) / 16;
+      const int chunk = slot ^ (row & 7);               // source chunk for this slot (XOR swizzle)
+      const int p = t * C::BM + row;
+      const T* src = p < M ? x + static_cast<int64_t>(p) * KIN + chunk * 8 : zero + (chunk & 7) * 8;
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sb + (i * 8 + wid) * 1024), 16, 0, 0);
+    }
+  };
+
+  const int my_tiles = wg < ntiles ? (ntiles - wg + grid - 1) / grid : 0;
+  for (int j = 0; j < C::D && j < my_tiles; ++j) issue(wg + j * grid, j);
+
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    s1[e] = 0.f;
+    s2[e] = 0.f;
+  }
+  const int my_c8 = tid % C::OCH;  // this thread's fixed output chunk (8 channels) in the epilogue
+  char* epi = smem + C::NST * C::STAGE;
+
+  for (int it = 0; it < my_tiles; ++it) {
+    const int t = wg + it * grid;
+    const int st = it % C::NST;
+    // issue tile it+D (into the stage freed by tile it-1, whose reads ended before the last barrier)
+    if (it + C::D < my_tiles) issue(wg + (it + C::D) * grid, (it + C::D) % C::NST);
+    // VM ops younger than tile it's DMA: the tiles issued after it, and the epilogue stores of the
+    // iterations run since it was issued (tile j < D came from the prologue, tile j >= D from
+    // iteration j - D)
+    {
+      const int later = (my_tiles - 1 - it) < C::D ? (my_tiles - 1 - it) : C::D;
+      const int epis = it < C::D ? it : C::D;
+      if (later == C::D && epis == C::D) vm_wait<C::D*(C::LPT + C::SPT)>();
+      else vm_wait_le(later * C::LPT + epis * C::SPT);
+    }
+    lds_barrier();
+
+    // ---- MFMA: C[co][pix] over the tile
+    const char* sb = smem + st * C::STAGE;
+    f4_t acc[C::FC][C::FP];
+#pragma unroll
+    for (int f = 0; f < C::FC; ++f)
+#pragma unroll
+      for (int p = 0; p < C::FP; ++p) acc[f][p] = f4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) {
+      u32x4 bf[C::FP];
+#pragma unroll
+      for (int p = 0; p < C::FP; ++p) {
+        const int row = wp * C::FP * 16 + p * 16 + (lane & 15);
+        const int chunk = s * 4 + (lane >> 4);
+        bf[p] = *reinterpret_cast<const u32x4*>(sb + row * C::ROWB + ((chunk ^ (row & 7)) * 16));
+      }
+#pragma unroll
+      for (int f = 0; f < C::FC; ++f)
+#pragma unroll
+        for (int p = 0; p < C::FP; ++p) acc[f][p] = PwM<T>::mma(wa[f][s], bf[p], acc[f][p]);
+    }
+    // ---- epilogue image: lane holds co = base + 4*(lane>>4) + {0..3} of pixel base + (lane & 15)
+#pragma unroll
+    for (int f = 0; f < C::FC; ++f)
+#pragma unroll
+      for (int p = 0; p < C::FP; ++p) {
+        const int pix = wp * C::FP * 16 + p * 16 + (lane & 15);
+        const int co = wc * C::FC * 16 + f * 16 + (lane >> 4) * 4;
+        const f4_t v = acc[f][p];
+        *reinterpret_cast<uint2*>(epi + pix * C::PITCH + co * 2) = PwM<T>::pack4(v[0], v[1], v[2], v[3]);
+      }
+    lds_barrier();
+    // ---- coalesced row stores (exactly SPT per thread: rows past M go out of range by buffer bounds)
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        y, 0, static_cast<int>(static_cast<uint32_t>(M) * NOUT * sizeof(T)), 0x00020000);
+#pragma unroll
+    for (int k = 0; k < C::SPT; ++k) {
+      // every lane issues the store (uniform VM-op count per wave for the counted waits): chunks past
+      // the tile or rows past M get an out-of-range offset and are dropped by the buffer bounds
+      const int e = tid + k * 512;
+      const bool in_tile = e < C::BM * C::OCH;
+      const int pix = in_tile ? e / C::OCH : 0;
+      const int c8 = e % C::OCH;
+      const int p = t * C::BM + pix;
+      Vec8<T> v;
+      v.raw = *reinterpret_cast<const uint4*>(epi + pix * C::PITCH + c8 * 16);
+      const bool live = in_tile && p < M;
+      const uint32_t off = live ? (static_cast<uint32_t>(p) * NOUT + c8 * 8) * sizeof(T) : 0xFFFFFFF0u;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v.raw), yrs, off, 0, 0);
+      if (STATS && live) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float z = v.get(q);
+          s1[q] += z;
+          s2[q] += z * z;
+        }
+      }
+    }
+    (void)my_c8;
+  }
+  if (STATS) {
+    // every thread's chunk is fixed (tid % OCH): combine the 512/OCH threads of each chunk through
+    // LDS, one partial per workgroup per channel
+    vm_wait<0>();
+    lds_barrier();
+    float* red = reinterpret_cast<float*>(smem);
+    constexpr int ROWS = 512 / C::OCH;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      red[(tid / C::OCH) * NOUT + my_c8 * 8 + q] = s1[q];
+      red[ROWS * NOUT + (tid / C::OCH) * NOUT + my_c8 * 8 + q] = s2[q];
+    }
+    lds_barrier();
+    for (int qq = tid; qq < 2 * NOUT; qq += 512) {
+      const int which = qq / NOUT, ch = qq - which * NOUT;
+      const float* col = red + which * ROWS * NOUT + ch;
+      float a = 0.f;
+      for (int r = 0; r < ROWS; ++r) a += col[r * NOUT];
+      part[static_cast<int64_t>(which) * NOUT * grid + static_cast<int64_t>(ch) * grid + wg] = a;
+    }
+  }
+}
+
+template <typename T, int KIN, int NOUT>
+void launch_pw(const void* x, const void* w, void* y, const void* zero, int M, float* part, int grid, hipStream_t s) {
+  using C = PwCfg<KIN, NOUT>;
+  static_assert(C::SMEM <= 80 * 1024, "two workgroups per CU");
+  static_assert(C::NST >= 2, "ring depth");
+  const int ntiles = (M + C::BM - 1) / C::BM;
+  if (part) {
+    static bool set = false;
+    if (!set) {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pw_stream_kernel<T, KIN, NOUT, true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
+      set = true;
+    }
+    hipLaunchKernelGGL((conv_pw_stream_kernel<T, KIN, NOUT, true>), dim3(grid), dim3(512), C::SMEM, s,
+                       static_cast<const T*>(x), static_cast<const T*>(w), static_cast<T*>(y),
+                       static_cast<const T*>(zero), M, ntiles, part);
+  } else {
+    static bool set = false;
+    if (!set) {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pw_stream_kernel<T, KIN, NOUT, false>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
+      set = true;
+    }
+    hipLaunchKernelGGL((conv_pw_stream_kernel<T, KIN, NOUT, false>), dim3(grid), dim3(512), C::SMEM, s,
+                       static_cast<const T*>(x), static_cast<const T*>(w), static_cast<T*>(y),
+                       static_cast<const T*>(zero), M, ntiles, part);
+  }
+}
+
+// (Cin, Cout) pairs built: the resident weights of (128, 512) and (256, 256) spill at 128 VGPRs
+#define MXAMD_PW_SHAPES(X) \
+  X(64, 64) X(64, 128) X(64, 256) X(128, 128) X(128, 256) X(256, 64) X(256, 128) X(512, 128)
+
+template <typename T>
+bool dispatch_pw(int kin, int nout, const void* x, const void* w, void* y, const void* zero, int M, float* part,
+                 int grid, hipStream_t s) {
+#define MXAMD_PW_CASE(K, N)                                        \
+  if (kin == K && nout == N) {                                     \
+    launch_pw<T, K, N>(x, w, y, zero, M, part, grid, s);           \
+    return true;                                                   \
+  }
+  MXAMD_PW_SHAPES(MXAMD_PW_CASE)
+#undef MXAMD_PW_CASE
+  return false;
+}
+
+}  // namespace
+
+// 1 when conv_pw_stream handles a 1x1 stride-1 NHWC conv with Cin = kin, Cout = nout.
+int conv_pw_stream_ok(int kin, int nout) {
+#define MXAMD_PW_OK(K, N) \
+  if (kin == K && nout == N) return 1;
+  MXAMD_PW_SHAPES(MXAMD_PW_OK)
+#undef MXAMD_PW_OK
+  return 0;
+}
+
+// Workgroups the kernel launches (= BatchNorm partials per channel when statistics are requested).
+int conv_pw_stream_grid(int M, int kin, int nout, int ncu) {
+  const int bm = (16384 / nout) < (8192 / kin) ? (16384 / nout) : (8192 / kin);
+  const int ntiles = (M + bm - 1) / bm;
+  const int g = 2 * ncu;
+  return ntiles < g ? ntiles : g;
+}
+
+void conv_pw_stream(int dtype, const void* x, const void* w, void* y, const void* zero, int M, int kin, int nout,
+                    float* part, int grid, hipStream_t s) {
+  MXAMD_HOST_CHECK(conv_pw_stream_ok(kin, nout), "conv_pw_stream: unsupported (Cin, Cout)");
+  MXAMD_HOST_CHECK(grid >= 1 && (int64_t)M * nout * 2 < (1ll << 31) - 64 && (int64_t)M * kin < (1ll << 31),
+                   "conv_pw_stream: tensor too large for 32-bit offsets");
+  bool ok = false;
+  if (dtype == kF16) ok = dispatch_pw<__half>(kin, nout, x, w, y, zero, M, part, grid, s);
+  else if (dtype == kBF16) ok = dispatch_pw<__hip_bfloat16>(kin, nout, x, w, y, zero, M, part, grid, s);
+  MXAMD_HOST_CHECK(ok, "conv_pw_stream: dtype must be f16 or bf16");
+}
+
+}  // namespace mxamd

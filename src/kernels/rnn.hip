@@ -7,7 +7,8 @@
 // MI355X design (not a cuDNN translation):
 //   * the input projection of every time step is ONE large GEMM done by the caller (in-tree
 //     MFMA GEMM / hipBLASLt), giving gx[t][n][G*H] in fp32 with the biases folded in;
-//   * per time step ONE launch computes, for a 16(batch) x 16(hidden) tile per wave, the
+//   * per time step ONE launch computes, for a 16(batch) x 16(hidden) tile per workgroup (its 4
+//     waves split the reduction and combine through LDS), the
 //     recurrent GEMM h_{t-1} . W_hh^T of EVERY gate of those hidden units on the matrix cores
 //     (v_mfma_f32_16x16x32_{f16,bf16}, or the exact-f32 v_mfma_f32_16x16x4_f32 for fp32
 //     layers) and then the cell's pointwise update in registers -- the gate pre-activations
@@ -95,24 +96,30 @@ struct RFrag<__hip_bfloat16> {
 
 template <>
 struct RFrag<float> {
-  typedef float frag;
-  static constexpr int KSTEP = 4;
-  static __device__ __forceinline__ frag load(const float* row, int k0, int lane, int K, bool ok, bool) {
-    const int k = k0 + (lane >> 4);
-    return (ok && k < K) ? row[k] : 0.f;
-  }
-  static __device__ __forceinline__ f4_t mma(const frag& a, const frag& b, f4_t c) {
+  static __device__ __forceinline__ f4_t mma1(float a, float b, f4_t c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
   }
   static __device__ __forceinline__ float from(float v) { return v; }
   static __device__ __forceinline__ float to(float v) { return v; }
 };
 
-// acc[g] += A[n0.., :K] . Bt[g*gstride + j0.., :K]^T for the wave's 16 x 16 tile
+__device__ __forceinline__ float4 load4f(const float* row, int k, int K, bool ok, bool aligned) {
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (!ok) return v;
+  if (aligned && k + 4 <= K) return *reinterpret_cast<const float4*>(row + k);
+  if (k < K) v.x = row[k];
+  if (k + 1 < K) v.y = row[k + 1];
+  if (k + 2 < K) v.z = row[k + 2];
+  if (k + 3 < K) v.w = row[k + 3];
+  return v;
+}
+
+// acc[g] += A[n0.., kslice] . Bt[g*gstride + j0.., kslice]^T for the 16 x 16 tile, over the k-chunks
+// of this wave (the 4 waves of a workgroup interleave chunks; their partial sums are combined after).
 template <typename T, int G>
 __device__ __forceinline__ void tile_gemm(f4_t (&acc)[G], const T* A, int lda, int nrows, const T* Bt, int ldb,
-                                          int gstride, int ncols, int K, int n0, int j0, int lane, bool aligned) {
-  using F = RFrag<T>;
+                                          int gstride, int ncols, int K, int n0, int j0, int lane, int wave,
+                                          bool aligned) {
   const int r = lane & 15;
   const bool aok = n0 + r < nrows;
   const bool bok = j0 + r < ncols;
@@ -120,10 +127,50 @@ __device__ __forceinline__ void tile_gemm(f4_t (&acc)[G], const T* A, int lda, i
   const T* brow[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) brow[g] = Bt + static_cast<int64_t>(g * gstride + (bok ? j0 + r : 0)) * ldb;
-  for (int k0 = 0; k0 < K; k0 += F::KSTEP) {
-    const typename F::frag a = F::load(arow, k0, lane, K, aok, aligned);
+  if constexpr (sizeof(T) == 4) {
+    // exact-f32 MFMA, 4 k per instruction; each lane loads 4 consecutive k (16 bytes) and the 4
+    // MFMAs of the chunk take element s of every lane: the k order is permuted identically for A
+    // and B, so the sum is unchanged
+    const int kq = (lane >> 4) * 4;
+#pragma unroll 2
+    for (int k0 = wave * 16; k0 < K; k0 += 64) {
+      const float4 a = load4f(reinterpret_cast<const float*>(arow), k0 + kq, K, aok, aligned);
 #pragma unroll
-    for (int g = 0; g < G; ++g) acc[g] = F::mma(a, F::load(brow[g], k0, lane, K, bok, aligned), acc[g]);
+      for (int g = 0; g < G; ++g) {
+        const float4 b = load4f(reinterpret_cast<const float*>(brow[g]), k0 + kq, K, bok, aligned);
+        acc[g] = RFrag<float>::mma1(a.x, b.x, acc[g]);
+        acc[g] = RFrag<float>::mma1(a.y, b.y, acc[g]);
+        acc[g] = RFrag<float>::mma1(a.z, b.z, acc[g]);
+        acc[g] = RFrag<float>::mma1(a.w, b.w, acc[g]);
+      }
+    }
+  } else {
+    using F = RFrag<T>;
+#pragma unroll 2
+    for (int k0 = wave * 32; k0 < K; k0 += 128) {
+      const typename F::frag a = F::load(arow, k0, lane, K, aok, aligned);
+#pragma unroll
+      for (int g = 0; g < G; ++g) acc[g] = F::mma(a, F::load(brow[g], k0, lane, K, bok, aligned), acc[g]);
+    }
+  }
+}
+
+// Combine the 4 waves' partial tiles through LDS: on return, `v[g]` holds element q = wave of the
+// summed accumulators (row (lane>>4)*4 + wave, column lane & 15) -- each wave then finishes one
+// of the four rows a lane holds.
+template <int G>
+__device__ __forceinline__ void reduce4(const f4_t (&acc)[G], float (&v)[G], float* red, int lane, int wave) {
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[((wave * G + g) * 4 + q) * 64 + lane] = acc[g][q];
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) t += red[((w * G + g) * 4 + wave) * 64 + lane];
+    v[g] = t;
   }
 }
 
@@ -140,56 +187,55 @@ __global__ void __launch_bounds__(256) rnn_step_fwd_kernel(const T* __restrict__
   constexpr int G = RnnG<MODE>::G;
   constexpr int SV = RnnG<MODE>::SAVE;
   using F = RFrag<T>;
+  __shared__ float red[4 * G * 4 * 64];
   const int lane = threadIdx.x & 63;
-  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int tn = w / ntj, tj = w - tn * ntj;
+  const int wave = threadIdx.x >> 6;
+  // one workgroup per 16 x 16 tile; its 4 waves split the reduction
+  const int tn = blockIdx.x / ntj, tj = blockIdx.x - tn * ntj;
   const int n0 = tn * 16, j0 = tj * 16;
-  if (n0 >= N) return;  // whole wave (no barriers in this kernel)
   f4_t acc[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) acc[g] = f4_t{0.f, 0.f, 0.f, 0.f};
-  tile_gemm<T, G>(acc, hprev, ldh, N, whh, H, H, H, H, n0, j0, lane, aligned != 0);
+  tile_gemm<T, G>(acc, hprev, ldh, N, whh, H, H, H, H, n0, j0, lane, wave, aligned != 0);
+  float pre[G];
+  reduce4<G>(acc, pre, red, lane, wave);
 
   const int j = j0 + (lane & 15);
-  if (j >= H) return;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int n = n0 + (lane >> 4) * 4 + q;
-    if (n >= N) break;
-    const float* gxr = gx + static_cast<int64_t>(n) * G * H;
-    float* sv = save + static_cast<int64_t>(n) * SV * H;
-    const int64_t nh = static_cast<int64_t>(n) * H + j;
-    float h;
-    if (MODE == kLstm) {
-      const float i = sigm(acc[0][q] + gxr[j]);
-      const float f = sigm(acc[1 % G][q] + gxr[H + j]);
-      const float g = tanhf(acc[2 % G][q] + gxr[2 * H + j]);
-      const float o = sigm(acc[3 % G][q] + gxr[3 * H + j]);
-      const float c = f * cprev[nh] + i * g;
-      h = o * tanhf(c);
-      cout[nh] = c;
-      sv[j] = i;
-      sv[H + j] = f;
-      sv[2 * H + j] = g;
-      sv[3 * H + j] = o;
-    } else if (MODE == kGru) {
-      const float r = sigm(acc[0][q] + gxr[j] + bhh[j]);
-      const float z = sigm(acc[1 % G][q] + gxr[H + j] + bhh[H + j]);
-      const float hn = acc[2 % G][q] + bhh[2 * H + j];
-      const float nn = tanhf(gxr[2 * H + j] + r * hn);
-      const float hp = F::to(hprev[static_cast<int64_t>(n) * ldh + j]);
-      h = (1.f - z) * nn + z * hp;
-      sv[j] = r;
-      sv[H + j] = z;
-      sv[2 * H + j] = nn;
-      sv[3 * H + j] = hn;
-    } else {
-      const float pre = acc[0][q] + gxr[j];
-      h = MODE == kRnnTanh ? tanhf(pre) : fmaxf(pre, 0.f);
-      sv[j] = h;
-    }
-    hout[static_cast<int64_t>(n) * ldo + j] = F::from(h);
+  const int n = n0 + (lane >> 4) * 4 + wave;   // this wave finishes row q = wave of the lane's four
+  if (j >= H || n >= N) return;
+  const float* gxr = gx + static_cast<int64_t>(n) * G * H;
+  float* sv = save + static_cast<int64_t>(n) * SV * H;
+  const int64_t nh = static_cast<int64_t>(n) * H + j;
+  float h;
+  if (MODE == kLstm) {
+    const float i = sigm(pre[0] + gxr[j]);
+    const float f = sigm(pre[1 % G] + gxr[H + j]);
+    const float g = tanhf(pre[2 % G] + gxr[2 * H + j]);
+    const float o = sigm(pre[3 % G] + gxr[3 * H + j]);
+    const float c = f * cprev[nh] + i * g;
+    h = o * tanhf(c);
+    cout[nh] = c;
+    sv[j] = i;
+    sv[H + j] = f;
+    sv[2 * H + j] = g;
+    sv[3 * H + j] = o;
+  } else if (MODE == kGru) {
+    const float r = sigm(pre[0] + gxr[j] + bhh[j]);
+    const float z = sigm(pre[1 % G] + gxr[H + j] + bhh[H + j]);
+    const float hn = pre[2 % G] + bhh[2 * H + j];
+    const float nn = tanhf(gxr[2 * H + j] + r * hn);
+    const float hp = F::to(hprev[static_cast<int64_t>(n) * ldh + j]);
+    h = (1.f - z) * nn + z * hp;
+    sv[j] = r;
+    sv[H + j] = z;
+    sv[2 * H + j] = nn;
+    sv[3 * H + j] = hn;
+  } else {
+    const float p = pre[0] + gxr[j];
+    h = MODE == kRnnTanh ? tanhf(p) : fmaxf(p, 0.f);
+    sv[j] = h;
   }
+  hout[static_cast<int64_t>(n) * ldo + j] = F::from(h);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -204,58 +250,57 @@ __global__ void __launch_bounds__(256) rnn_step_bwd_kernel(
   constexpr int G = RnnG<MODE>::G;
   constexpr int SV = RnnG<MODE>::SAVE;
   using F = RFrag<T>;
+  __shared__ float red[4 * 4 * 64];
   const int lane = threadIdx.x & 63;
-  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int tn = w / ntj, tj = w - tn * ntj;
+  const int wave = threadIdx.x >> 6;
+  const int tn = blockIdx.x / ntj, tj = blockIdx.x - tn * ntj;
   const int n0 = tn * 16, j0 = tj * 16;
-  if (n0 >= N) return;
   f4_t acc[1] = {f4_t{0.f, 0.f, 0.f, 0.f}};
-  if (dgh_next != nullptr) tile_gemm<T, 1>(acc, dgh_next, G * H, N, whhT, G * H, 0, H, G * H, n0, j0, lane, aligned != 0);
+  if (dgh_next != nullptr)
+    tile_gemm<T, 1>(acc, dgh_next, G * H, N, whhT, G * H, 0, H, G * H, n0, j0, lane, wave, aligned != 0);
+  float dsum[1];
+  reduce4<1>(acc, dsum, red, lane, wave);
 
   const int j = j0 + (lane & 15);
-  if (j >= H) return;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int n = n0 + (lane >> 4) * 4 + q;
-    if (n >= N) break;
-    const int64_t nh = static_cast<int64_t>(n) * H + j;
-    float d = acc[0][q];
-    if (dh_last != nullptr) d += dh_last[nh];
-    if (dhd != nullptr) d += dhd[nh];
-    if (dh_out != nullptr) {  // final pass: the gradient of the initial state, no cell derivative
-      dh_out[nh] = d;
-      continue;
-    }
-    if (dy != nullptr) d += F::to(dy[static_cast<int64_t>(n) * ldy + j]);
-    const float* sv = save + static_cast<int64_t>(n) * SV * H;
-    T* gh = dgh + static_cast<int64_t>(n) * G * H;
-    if (MODE == kLstm) {
-      const float i = sv[j], f = sv[H + j], g = sv[2 * H + j], o = sv[3 * H + j];
-      const float tc = tanhf(cur_c[nh]);
-      const float dct = dc[nh] + d * o * (1.f - tc * tc);
-      gh[j] = F::from(dct * g * i * (1.f - i));
-      gh[H + j] = F::from(dct * cprev[nh] * f * (1.f - f));
-      gh[2 * H + j] = F::from(dct * i * (1.f - g * g));
-      gh[3 * H + j] = F::from(d * tc * o * (1.f - o));
-      dc[nh] = dct * f;
-    } else if (MODE == kGru) {
-      const float r = sv[j], z = sv[H + j], nn = sv[2 * H + j], hn = sv[3 * H + j];
-      const float hp = F::to(hprev[static_cast<int64_t>(n) * ldh + j]);
-      const float dn = d * (1.f - z) * (1.f - nn * nn);
-      const float dz = d * (hp - nn) * z * (1.f - z);
-      const float dr = dn * hn * r * (1.f - r);
-      T* gx = dgx + static_cast<int64_t>(n) * G * H;
-      gh[j] = F::from(dr);
-      gh[H + j] = F::from(dz);
-      gh[2 * H + j] = F::from(dn * r);
-      gx[j] = F::from(dr);
-      gx[H + j] = F::from(dz);
-      gx[2 * H + j] = F::from(dn);
-      dhd[nh] = d * z;  // the direct h_{t-1} -> h_t path, added by the previous step's launch
-    } else {
-      const float h = sv[j];
-      gh[j] = F::from(MODE == kRnnTanh ? d * (1.f - h * h) : (h > 0.f ? d : 0.f));
-    }
+  const int n = n0 + (lane >> 4) * 4 + wave;
+  if (j >= H || n >= N) return;
+  const int64_t nh = static_cast<int64_t>(n) * H + j;
+  float d = dsum[0];
+  if (dh_last != nullptr) d += dh_last[nh];
+  if (dhd != nullptr) d += dhd[nh];
+  if (dh_out != nullptr) {  // final pass: the gradient of the initial state, no cell derivative
+    dh_out[nh] = d;
+    return;
+  }
+  if (dy != nullptr) d += F::to(dy[static_cast<int64_t>(n) * ldy + j]);
+  const float* sv = save + static_cast<int64_t>(n) * SV * H;
+  T* gh = dgh + static_cast<int64_t>(n) * G * H;
+  if (MODE == kLstm) {
+    const float i = sv[j], f = sv[H + j], g = sv[2 * H + j], o = sv[3 * H + j];
+    const float tc = tanhf(cur_c[nh]);
+    const float dct = dc[nh] + d * o * (1.f - tc * tc);
+    gh[j] = F::from(dct * g * i * (1.f - i));
+    gh[H + j] = F::from(dct * cprev[nh] * f * (1.f - f));
+    gh[2 * H + j] = F::from(dct * i * (1.f - g * g));
+    gh[3 * H + j] = F::from(d * tc * o * (1.f - o));
+    dc[nh] = dct * f;
+  } else if (MODE == kGru) {
+    const float r = sv[j], z = sv[H + j], nn = sv[2 * H + j], hn = sv[3 * H + j];
+    const float hp = F::to(hprev[static_cast<int64_t>(n) * ldh + j]);
+    const float dn = d * (1.f - z) * (1.f - nn * nn);
+    const float dz = d * (hp - nn) * z * (1.f - z);
+    const float dr = dn * hn * r * (1.f - r);
+    T* gxo = dgx + static_cast<int64_t>(n) * G * H;
+    gh[j] = F::from(dr);
+    gh[H + j] = F::from(dz);
+    gh[2 * H + j] = F::from(dn * r);
+    gxo[j] = F::from(dr);
+    gxo[H + j] = F::from(dz);
+    gxo[2 * H + j] = F::from(dn);
+    dhd[nh] = d * z;  // the direct h_{t-1} -> h_t path, added by the previous step's launch
+  } else {
+    const float h = sv[j];
+    gh[j] = F::from(MODE == kRnnTanh ? d * (1.f - h * h) : (h > 0.f ? d : 0.f));
   }
 }
 
@@ -265,9 +310,9 @@ void fwd_seq(const float* gx, const void* h0, const float* c0, const void* whh, 
   constexpr int G = RnnG<MODE>::G;
   constexpr int SV = RnnG<MODE>::SAVE;
   const int ntj = (H + 15) / 16;
-  const int waves = ((N + 15) / 16) * ntj;
-  const int blocks = (waves + 3) / 4;
-  const int aligned = (H % 8 == 0 && ldo % 8 == 0 && (reinterpret_cast<uintptr_t>(out) % 16) == 0 &&
+  const int blocks = ((N + 15) / 16) * ntj;  // one workgroup (4 waves, split-K) per 16 x 16 tile
+  const int vec = sizeof(T) == 4 ? 4 : 8;
+  const int aligned = (H % vec == 0 && ldo % vec == 0 && (reinterpret_cast<uintptr_t>(out) % 16) == 0 &&
                        (reinterpret_cast<uintptr_t>(h0) % 16) == 0 && (reinterpret_cast<uintptr_t>(whh) % 16) == 0)
                           ? 1
                           : 0;
@@ -293,9 +338,9 @@ void bwd_seq(const void* whhT, const void* dy, int ldy, const float* dhT, const 
   constexpr int G = RnnG<MODE>::G;
   constexpr int SV = RnnG<MODE>::SAVE;
   const int ntj = (H + 15) / 16;
-  const int waves = ((N + 15) / 16) * ntj;
-  const int blocks = (waves + 3) / 4;
-  const int aligned = (H % 8 == 0 && (reinterpret_cast<uintptr_t>(whhT) % 16) == 0 &&
+  const int blocks = ((N + 15) / 16) * ntj;
+  const int vec = sizeof(T) == 4 ? 4 : 8;
+  const int aligned = ((G * H) % vec == 0 && (reinterpret_cast<uintptr_t>(whhT) % 16) == 0 &&
                        (reinterpret_cast<uintptr_t>(dgh) % 16) == 0)
                           ? 1
                           : 0;

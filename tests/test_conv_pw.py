@@ -1,0 +1,32 @@
+"""Streaming 1x1 convolution (src/kernels/conv_pw.hip) vs fp32 PyTorch: outputs and the fused BatchNorm
+statistics partials."""
+import pytest
+import torch
+
+from mxnet_maintenance_amd.ops import kernel_fns as KF
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize('kin,nout,M,dt', [(64, 256, 3136 * 2 + 40, torch.float16), (256, 64, 5000, torch.bfloat16),
+                                           (64, 64, 777, torch.float16), (512, 128, 1568, torch.float16),
+                                           (256, 128, 2049, torch.bfloat16), (128, 128, 100, torch.float16),
+                                           (128, 256, 3000, torch.bfloat16), (64, 128, 1000, torch.float16)])
+def test_conv_pw_matches_fp32(kin, nout, M, dt):
+    dev = torch.device('cuda', 0)
+    assert KF.pw_ok(torch.empty(1, kin, dtype=dt, device=dev), kin, nout)
+    g = torch.Generator().manual_seed(kin + nout)
+    x = (torch.rand(M, kin, generator=g) * 2 - 1).to(dev, dt).view(1, 1, M, kin)
+    w = ((torch.rand(nout, kin, generator=g) * 2 - 1) / kin ** 0.5).to(dev, dt)
+    y = KF.conv_pw(x, w, bn_stats=True)
+    ref = x.float().reshape(M, kin) @ w.float().t()
+    err = float((y.float().reshape(M, nout) - ref).norm() / ref.norm())
+    assert err < 1e-2, err
+    part, nparts = y._mxamd_bn_part
+    p = part.view(2, nout, nparts).sum(-1)
+    yr = y.float().reshape(M, nout)
+    assert float((p[0] - yr.sum(0)).abs().max()) < 1e-2 * float(yr.abs().sum(0).max() + 1)
+    assert float((p[1] - (yr * yr).sum(0)).abs().max()) < 1e-3 * float((yr * yr).sum(0).max() + 1)
+    # no statistics requested: same output
+    y2 = KF.conv_pw(x, w)
+    assert torch.equal(y2, y)

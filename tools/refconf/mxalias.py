@@ -52,6 +52,18 @@ if not any(isinstance(f, _AliasFinder) for f in sys.meta_path):
 # failures measure this framework, not the NumPy version of the image.
 import numpy as _np   # noqa: E402
 for _old, _new in (('NaN', 'nan'), ('Inf', 'inf'), ('Infinity', 'inf'), ('PINF', 'inf'), ('NINF', None),
-                   ('float_', 'float64'), ('complex_', 'complex128'), ('unicode_', 'str_'), ('string_', 'bytes_')):
+                   ('float_', 'float64'), ('round_', 'round'), ('product', 'prod'), ('cumproduct', 'cumprod'),
+                   ('alltrue', 'all'), ('sometrue', 'any'), ('complex_', 'complex128'), ('unicode_', 'str_'), ('string_', 'bytes_')):
     if not hasattr(_np, _old):
         setattr(_np, _old, -_np.inf if _new is None else getattr(_np, _new))
+
+_np_nonzero = _np.nonzero
+
+
+def _nonzero_1x(a):
+    """NumPy 1.x treated a 0-d array as 1-d in nonzero (NumPy 2 raises)."""
+    a = _np.asarray(a)
+    return _np_nonzero(_np.atleast_1d(a)) if a.ndim == 0 else _np_nonzero(a)
+
+
+_np.nonzero = _nonzero_1x
