@@ -195,7 +195,33 @@ def _int_dtype_attr(attrs):
 # elemwise FInferStorageType: rows come from the lhs, or the union of both row_sparse operands)
 _SPARSE_LHS = frozenset(('_scatter_elemwise_div', '_scatter_plus_scalar', '_scatter_minus_scalar',
                          '_mul_scalar', '_div_scalar'))
-_SPARSE_BOTH = frozenset(('elemwise_add', 'elemwise_sub', 'elemwise_mul', '_grad_add'))
+_SPARSE_ADD = frozenset(('elemwise_add', 'elemwise_sub', '_grad_add', '_plus', '_minus', '_add', '_sub'))
+_SPARSE_MUL = frozenset(('elemwise_mul', '_mul'))
+_SPARSE_SAME = frozenset(('_maximum', '_minimum', '_hypot', 'maximum', 'minimum', 'hypot'))
+
+
+def _binary_stype(op, ins):
+    """Output storage of the sparse-aware binary operators (FInferStorageType of
+    src/operator/tensor/elemwise_binary_op_basic.cc and elemwise_scatter_op.cc); None when the
+    operator has no rule here."""
+    if not ins or all(t == 'default' for t in ins):
+        return None
+    if op in _SPARSE_LHS:
+        return ins[0] if ins[0] != 'default' else None
+    if len(ins) != 2:
+        return None
+    lt, rt = ins
+    if op in _SPARSE_ADD or op in _SPARSE_SAME:
+        return lt if lt == rt else 'default'
+    if op in _SPARSE_MUL:
+        if lt == rt:
+            return lt
+        if 'default' in (lt, rt):
+            return rt if lt == 'default' else lt          # dense * sparse keeps the sparse pattern
+        return 'default'
+    if op in ('elemwise_div', '_div'):
+        return 'default'
+    return None
 
 
 def registry_parse(node):
@@ -420,10 +446,9 @@ class Executor:
                 continue
             ins = [memo.get((id(i), j), 'default') for i, j in n.inputs]
             attrs = registry_parse(n)
-            st = _kept_stype(n.op, [_S(t) for t in ins], attrs) if ins else None
-            if st is None and ins and ins[0] == 'row_sparse':
-                if n.op in _SPARSE_LHS or (n.op in _SPARSE_BOTH and all(t == 'row_sparse' for t in ins)):
-                    st = 'row_sparse'
+            st = _binary_stype(n.op, ins)
+            if st is None:
+                st = _kept_stype(n.op, [_S(t) for t in ins], attrs) if ins else None
 
             memo[(id(n), 0)] = st or 'default'
         self._stype_cache = [memo.get((id(n), i), 'default') for n, i in self._symbol._outputs]

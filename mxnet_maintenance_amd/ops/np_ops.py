@@ -144,10 +144,20 @@ def _heaviside(a, b):
     return torch.heaviside(a.to(rt), b.to(rt))
 
 
+def _maxmin(is_max):
+    def f(a, b):
+        from .tensor import _maximum, _minimum
+        if a.dtype != b.dtype:
+            rt = torch.promote_types(a.dtype, b.dtype)
+            a, b = a.to(rt), b.to(rt)
+        return _maximum(a, b) if is_max else _minimum(a, b)
+    return f
+
+
 _BINARY = {
     'add': torch.add, 'subtract': _sub, 'multiply': torch.mul, 'true_divide': torch.true_divide,
     'floor_divide': _floor_divide, 'mod': _mod, 'fmod': torch.fmod, 'power': _power,
-    'maximum': torch.maximum, 'minimum': torch.minimum, 'fmax': torch.fmax, 'fmin': torch.fmin,
+    'maximum': _maxmin(True), 'minimum': _maxmin(False), 'fmax': torch.fmax, 'fmin': torch.fmin,
     'arctan2': _fbin(torch.atan2), 'hypot': _fbin(torch.hypot), 'copysign': _fbin(torch.copysign),
     'ldexp': _ldexp, 'lcm': torch.lcm, 'gcd': torch.gcd, 'bitwise_and': torch.bitwise_and,
     'bitwise_or': torch.bitwise_or, 'bitwise_xor': torch.bitwise_xor, 'logical_and': torch.logical_and,

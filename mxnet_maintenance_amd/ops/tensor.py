@@ -78,14 +78,64 @@ def _relu(x):
     return _Relu.apply(x) if x.requires_grad and x.is_floating_point() else torch.relu(x)
 
 
+def _tgamma(x):
+    """Gamma function with C tgamma's signs and poles: negative between odd/even negative integers,
+    +inf at +0, nan at negative integers."""
+    x = x if x.is_floating_point() else x.to(torch.float32)
+    mag = torch.exp(torch.lgamma(x))
+    neg_odd = (x < 0) & (torch.remainder(torch.ceil(-x), 2) == 1)
+    r = torch.where(neg_odd, -mag, mag)
+    return torch.where((x < 0) & (x == torch.floor(x)), torch.full_like(r, float('nan')), r)
+
+
+class _Gamma(torch.autograd.Function):
+    """d/dx gamma = gamma(x) * psi(x), with psi = +inf at the non-positive integers (the reference's
+    psi, src/operator/mshadow_op.h special_functions::cephes::psi)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        y = _tgamma(x)
+        ctx.save_for_backward(x, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y = ctx.saved_tensors
+        return g * y * _psi_ref(x)
+
+
+def _gamma(x):
+    return _Gamma.apply(x) if x.requires_grad else _tgamma(x)
+
+
+def _psi_ref(x):
+    return torch.where((x <= 0) & (x == torch.floor(x)), torch.full_like(x, float('inf')), torch.digamma(x))
+
+
+class _Gammaln(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        return torch.lgamma(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, = ctx.saved_tensors
+        return g * _psi_ref(x)
+
+
+def _gammaln(x):
+    return _Gammaln.apply(x) if x.requires_grad else torch.lgamma(x)
+
+
 _UNARY = {
     'abs': torch.abs, 'sign': torch.sign, 'round': torch.round,
     'rint': torch.round, 'ceil': torch.ceil, 'floor': torch.floor, 'trunc': torch.trunc,
     'fix': torch.trunc, 'square': torch.square, 'sqrt': torch.sqrt, 'rsqrt': torch.rsqrt,
     'cbrt': _cbrt, 'rcbrt': _rcbrt,
     'exp': torch.exp, 'log': torch.log, 'log10': torch.log10, 'log2': torch.log2,
-    'log1p': torch.log1p, 'expm1': torch.expm1, 'gamma': lambda x: torch.exp(torch.lgamma(x)),
-    'gammaln': torch.lgamma, 'erf': torch.erf, 'erfinv': torch.erfinv,
+    'log1p': torch.log1p, 'expm1': torch.expm1, 'gamma': _gamma,
+    'gammaln': _gammaln, 'erf': torch.erf, 'erfinv': torch.erfinv,
     'sin': torch.sin, 'cos': torch.cos, 'tan': torch.tan, 'arcsin': torch.asin,
     'arccos': torch.acos, 'arctan': torch.atan, 'degrees': torch.rad2deg,
     'radians': torch.deg2rad, 'sinh': torch.sinh, 'cosh': torch.cosh, 'tanh': torch.tanh,
@@ -225,10 +275,49 @@ def _logical(f):
     return g
 
 
+class _MaxMin(torch.autograd.Function):
+    """maximum / minimum with the reference's tie rule: the whole gradient goes to the lhs where
+    lhs >= rhs (maximum) or lhs <= rhs (minimum) -- mshadow_op::ge / le, not torch's even split."""
+
+    @staticmethod
+    def forward(ctx, a, b, is_max):
+        ctx.is_max = is_max
+        ctx.save_for_backward(a, b)
+        return torch.maximum(a, b) if is_max else torch.minimum(a, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        take_a = (a >= b) if ctx.is_max else (a <= b)
+        ga = torch.where(take_a, g, torch.zeros_like(g))
+        gb = g - ga
+        return _sum_to(ga, a.shape).to(a.dtype), _sum_to(gb, b.shape).to(b.dtype), None
+
+
+def _sum_to(g, shape):
+    if tuple(g.shape) == tuple(shape):
+        return g
+    lead = g.dim() - len(shape)
+    dims = list(range(lead)) + [lead + i for i, n in enumerate(shape) if n == 1 and g.shape[lead + i] != 1]
+    return g.sum(dim=dims, keepdim=True).reshape(shape) if dims else g.reshape(shape)
+
+
+def _maximum(a, b):
+    if (a.requires_grad or b.requires_grad) and a.is_floating_point() and b.is_floating_point():
+        return _MaxMin.apply(a, b, True)
+    return torch.maximum(a, b)
+
+
+def _minimum(a, b):
+    if (a.requires_grad or b.requires_grad) and a.is_floating_point() and b.is_floating_point():
+        return _MaxMin.apply(a, b, False)
+    return torch.minimum(a, b)
+
+
 _BINARY = {
     'add': torch.add, 'sub': torch.sub, 'mul': torch.mul,
     'div': lambda a, b: torch.div(a, b) if (a.is_floating_point() if torch.is_tensor(a) else True) else torch.div(a, b, rounding_mode='trunc'),
-    'mod': _mod, 'power': torch.pow, 'maximum': torch.maximum, 'minimum': torch.minimum,
+    'mod': _mod, 'power': torch.pow, 'maximum': _maximum, 'minimum': _minimum,
     'hypot': torch.hypot,
     'equal': _cmp(torch.eq), 'not_equal': _cmp(torch.ne), 'greater': _cmp(torch.gt),
     'greater_equal': _cmp(torch.ge), 'lesser': _cmp(torch.lt), 'lesser_equal': _cmp(torch.le),

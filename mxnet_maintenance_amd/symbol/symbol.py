@@ -559,7 +559,9 @@ class Symbol:
             if shared_buffer is not None and n in shared_buffer and shared_buffer[n].shape == tuple(s):
                 args.append(shared_buffer[n])
             else:
-                a = nd.zeros(s, ctx=place(n), dtype=t or np.float32)
+                st = (stype_dict or {}).get(n, 'default')
+                a = nd.zeros(s, ctx=place(n), dtype=t or np.float32, stype=st) if st != 'default' else \
+                    nd.zeros(s, ctx=place(n), dtype=t or np.float32)
                 if shared_buffer is not None:
                     shared_buffer[n] = a
                 args.append(a)
@@ -569,11 +571,29 @@ class Symbol:
             reqs = dict(zip(arg_names, grad_req))
         else:
             reqs = {n: grad_req.get(n, 'null') for n in arg_names}
-        grads = {n: nd.zeros(s, ctx=place(n), dtype=t or np.float32)
+        rsp_grads = self._row_sparse_grad_args()
+        grads = {n: (nd.zeros(s, ctx=place(n), dtype=t or np.float32, stype='row_sparse') if n in rsp_grads else
+                     nd.zeros(s, ctx=place(n), dtype=t or np.float32))
                  for n, s, t in zip(arg_names, arg_shapes, arg_types) if reqs.get(n, 'null') != 'null'}
         aux = [nd.zeros(s, ctx=ctx, dtype=t or np.float32) for s, t in zip(aux_shapes, aux_types)]
         from . import subgraph
         return Executor(subgraph.env_partition(self), ctx, args, grads, reqs, aux)
+
+    def _row_sparse_grad_args(self):
+        """Arguments whose gradient storage the backward storage-type inference makes row_sparse:
+        the weight of an Embedding with ``sparse_grad`` (src/operator/tensor/indexing_op.cc
+        EmbeddingOpBackwardStorageType) when no other consumer needs a dense gradient."""
+        rsp, dense = set(), set()
+        for n in self._topo():
+            if n.op is None:
+                continue
+            sparse_w = n.op in ('Embedding', '_contrib_SparseEmbedding') and \
+                (n.op == '_contrib_SparseEmbedding' or str(n.attrs.get('sparse_grad', 'False')) in ('True', 'true', '1'))
+            for k, (src, _j) in enumerate(n.inputs):
+                if src.op is not None:
+                    continue
+                (rsp if (sparse_w and k == 1) else dense).add(src.name)
+        return rsp - dense
 
     def eval(self, ctx=None, **kwargs):
         from ..context import current_context
