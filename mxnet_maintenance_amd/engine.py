@@ -366,6 +366,18 @@ def _is_owned_pinned(t):
     return any(b <= p and end <= b + n for (b, n) in _OWNED_PINNED)
 
 
+_COMM_STREAMS = {}
+
+
+def comm_stream(dev):
+    """The communication stream of device ``dev`` (kvstore reduce/broadcast engine ops)."""
+    import torch
+    s = _COMM_STREAMS.get(dev)
+    if s is None:
+        s = _COMM_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
 def copy_stream(dev):
     """The dedicated H2D copy stream of device ``dev`` (a torch.device)."""
     import torch

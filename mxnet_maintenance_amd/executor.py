@@ -10,6 +10,8 @@ same program drives ``Executor`` and Gluon's hybridized ``CachedOp``; with
 static shapes the program can be captured into a HIP graph (see
 gluon/block.py).  Gradients come from the autograd tape of the forward run.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -103,64 +105,125 @@ class GraphProgram:
         if int_dtypes:
             islot = {self.name_to_slot[n]: d for n, d in int_dtypes.items() if n in self.name_to_slot}
         self.failure = None       # first operator execution failure of this run (deferred to sync)
-        for fn, ins, attrs, outs, name, opname in self.steps:
-            args = [vals[i] for i in ins]
-            if _amp.active:
-                args = _amp.cast_inputs(opname, args, attrs)
-            if record is not None:
-                record.append((name, args))
-            if monitor is not None and monitor_all:
-                # reference order: a variable input under its own name, then every input as
-                # <node>_<argument name>
-                argn = self._input_names(opname, attrs, len(args))
-                for j, a in enumerate(args):
-                    if a is None:
-                        continue
-                    var = self._var_of_slot.get(ins[j])
-                    if var is not None:
-                        monitor(var, a)
-                    monitor('%s_%s' % (name, argn[j]), a)
-            try:
-                if (islot and any(i in islot for i in ins)) or (attrs.get('dtype') is not None and
-                                                                 _int_dtype_attr(attrs) and torch.is_grad_enabled()):
-                    r = self._run_shadow(fn, args, attrs, ins, outs, islot, opname)
-                elif _profiler.active_symbolic:
-                    with _profiler.op_span(_profiler.current_scope() + opname, symbolic=True):
+        sched = self._stream_sched(vals) if _GRAPH_STREAMS > 1 else None
+        try:
+            for si, (fn, ins, attrs, outs, name, opname) in enumerate(self.steps):
+                args = [vals[i] for i in ins]
+                if sched is not None:
+                    sched.before(si, args)
+                if _amp.active:
+                    args = _amp.cast_inputs(opname, args, attrs)
+                if record is not None:
+                    record.append((name, args))
+                if monitor is not None and monitor_all:
+                    # reference order: a variable input under its own name, then every input as
+                    # <node>_<argument name>
+                    argn = self._input_names(opname, attrs, len(args))
+                    for j, a in enumerate(args):
+                        if a is None:
+                            continue
+                        var = self._var_of_slot.get(ins[j])
+                        if var is not None:
+                            monitor(var, a)
+                        monitor('%s_%s' % (name, argn[j]), a)
+                try:
+                    if (islot and any(i in islot for i in ins)) or (attrs.get('dtype') is not None and
+                                                                     _int_dtype_attr(attrs) and torch.is_grad_enabled()):
+                        r = self._run_shadow(fn, args, attrs, ins, outs, islot, opname)
+                    elif _profiler.active_symbolic:
+                        with _profiler.op_span(_profiler.current_scope() + opname, symbolic=True):
+                            r = fn(*args, **attrs)
+                    else:
                         r = fn(*args, **attrs)
-                else:
-                    r = fn(*args, **attrs)
-            except AsyncOpError as e:
-                # the graph keeps running on a zero stand-in; the outputs carry the failure
-                from .ndarray.register import _placeholder
-                if self.failure is None:
-                    self.failure = AsyncOpError('Error in operator %s (%s): %s' % (name, opname, e))
-                r = _placeholder(attrs, [])
-            except MXNetError:
-                if self.failure is None:
-                    raise
-                from .ndarray.register import _placeholder
-                r = _placeholder(attrs, [])
-            except (RuntimeError, IndexError) as e:
-                if self.failure is not None:
+                except AsyncOpError as e:
+                    # the graph keeps running on a zero stand-in; the outputs carry the failure
+                    from .ndarray.register import _placeholder
+                    if self.failure is None:
+                        self.failure = AsyncOpError('Error in operator %s (%s): %s' % (name, opname, e))
+                    r = _placeholder(attrs, [])
+                except MXNetError:
+                    if self.failure is None:
+                        raise
                     from .ndarray.register import _placeholder
                     r = _placeholder(attrs, [])
+                except (RuntimeError, IndexError) as e:
+                    if self.failure is not None:
+                        from .ndarray.register import _placeholder
+                        r = _placeholder(attrs, [])
+                    else:
+                        raise MXNetError('Error in operator %s (%s): %s' % (name, opname, e)) from e
+                if sched is not None:
+                    sched.after(si)
+                if len(outs) == 1:
+                    vals[outs[0]] = r[0] if isinstance(r, (tuple, list)) else r
                 else:
-                    raise MXNetError('Error in operator %s (%s): %s' % (name, opname, e)) from e
-            if len(outs) == 1:
-                vals[outs[0]] = r[0] if isinstance(r, (tuple, list)) else r
-            else:
-                for o, t in zip(outs, r):
-                    vals[o] = t
-            if monitor is not None:
-                op = registry.get(opname)
-                onames = op.output_names or (['output'] if len(outs) == 1 else
-                                             ['output%d' % k for k in range(len(outs))])
-                for o, on in zip(outs, onames):
-                    if vals[o] is not None:
-                        monitor('%s_%s' % (name, on), vals[o])
+                    for o, t in zip(outs, r):
+                        vals[o] = t
+                if monitor is not None:
+                    op = registry.get(opname)
+                    onames = op.output_names or (['output'] if len(outs) == 1 else
+                                                 ['output%d' % k for k in range(len(outs))])
+                    for o, on in zip(outs, onames):
+                        if vals[o] is not None:
+                            monitor('%s_%s' % (name, on), vals[o])
+        finally:
+            if sched is not None:
+                torch.cuda.set_stream(sched.main)
         self.out_idts = [islot.get(s) for s in self.out_slots] if islot else None
+        if sched is not None:
+            sched.finish([vals[s] for s in self.out_slots])
         return [vals[s] for s in self.out_slots]
 
+    # ------------------------------------------------------------------ multi-stream schedule
+    def _stream_plan(self, nstreams):
+        """Static assignment of the graph's operators to ``nstreams`` HIP streams (the dependency
+        engine's job for a bound graph, src/executor/graph_executor.cc + threaded_engine): an operator
+        continues the stream of its latest producer while that stream's last operator is that
+        producer; a heavy operator (conv, FC, ...) whose producers' streams have moved on starts a
+        branch on a side stream.  Cross-stream edges become event waits.  Returns (stream index per
+        step, producer steps to wait for per step, steps whose completion is recorded)."""
+        producer = {}
+        for i, st in enumerate(self.steps):
+            for o in st[3]:
+                producer[o] = i
+        n = len(self.steps)
+        stream_of = [0] * n
+        tail = [-1] * nstreams
+        waits = [()] * n
+        need_ev = set()
+        rr = 1
+        for i, (_fn, ins, _attrs, _outs, _name, opname) in enumerate(self.steps):
+            prods = sorted({producer[x] for x in ins if x in producer})
+            # an operator fed only by graph inputs hangs off a virtual producer (-1) on the caller's
+            # stream: the first such operator continues it, later ones can branch
+            cands = prods or [-1]
+            # streams on which a producer is still the last operator; joins prefer the lowest
+            # (the caller's stream keeps the trunk)
+            live = [stream_of[p] if p >= 0 else 0 for p in cands if tail[stream_of[p] if p >= 0 else 0] == p]
+            choice = min(live) if live else None
+            if choice is None:
+                if opname in _BRANCH_OPS and nstreams > 1:
+                    choice = rr
+                    rr = 1 + rr % (nstreams - 1)
+                else:
+                    choice = stream_of[prods[-1]] if prods else 0
+            stream_of[i] = choice
+            tail[choice] = i
+            w = tuple(p for p in prods if stream_of[p] != choice)
+            waits[i] = w
+            need_ev.update(w)
+        return stream_of, waits, need_ev
+
+    def _stream_sched(self, vals):
+        dev = next((v.device for v in vals if isinstance(v, torch.Tensor) and v.is_cuda), None)
+        if dev is None or torch.cuda.is_current_stream_capturing() and not _GRAPH_STREAMS_CAPTURE:
+            return None
+        plan = getattr(self, '_splan', None)
+        if plan is None:
+            plan = self._splan = self._stream_plan(_GRAPH_STREAMS)
+        if max(plan[0], default=0) == 0:
+            return None
+        return _StreamSched(plan, dev)
     @staticmethod
     def _run_shadow(fn, args, attrs, ins, outs, islot, opname=None):
         """One operator over integer values carried in float64 (see ``run``): the integer result's
@@ -184,6 +247,76 @@ class GraphProgram:
             else:
                 islot.pop(o, None)
         return [p[0] for p in pairs] if multi else pairs[0][0]
+
+
+_GRAPH_STREAMS = int(os.environ.get('MXNET_GRAPH_STREAMS', '1') or 1)
+_GRAPH_STREAMS_CAPTURE = os.environ.get('MXNET_GRAPH_STREAMS_CAPTURE', '1') == '1'
+# operators worth a branch of their own on a side stream
+_BRANCH_OPS = frozenset(('Convolution', 'Deconvolution', 'FullyConnected', '_contrib_DeformableConvolution',
+                         '_contrib_ModulatedDeformableConvolution', 'Pooling', 'dot', 'batch_dot', '_npi_matmul',
+                         'RNN', '_FusedOp'))
+_SIDE_STREAMS = {}
+
+
+def _side_streams(dev, n):
+    lst = _SIDE_STREAMS.get(dev)
+    if lst is None or len(lst) < n:
+        lst = _SIDE_STREAMS[dev] = [torch.cuda.Stream(device=dev) for _ in range(n)]
+    return lst
+
+
+class _StreamSched:
+    """Runs one GraphProgram pass on the streams of a static plan (see GraphProgram._stream_plan):
+    side streams fork from the caller's stream at their first operator and join it at the end, so
+    the pass is also capturable into one HIP graph with parallel branches.  Tensors that cross
+    streams are recorded on the consuming stream for the caching allocator."""
+
+    def __init__(self, plan, dev):
+        self.stream_of, self.waits, self.need_ev = plan
+        self.main = torch.cuda.current_stream(dev)
+        self.streams = [self.main] + _side_streams(dev, _GRAPH_STREAMS - 1)
+        self.events = {}
+        self.started = set()
+        self.start_ev = None
+        self.side_steps = set()
+
+    def before(self, i, args):
+        k = self.stream_of[i]
+        s = self.streams[k]
+        if k and k not in self.started:
+            if self.start_ev is None:
+                self.start_ev = torch.cuda.Event()
+                self.start_ev.record(self.main)
+            s.wait_event(self.start_ev)
+            self.started.add(k)
+        for p in self.waits[i]:
+            s.wait_event(self.events[p])
+        if k or self.waits[i]:
+            for a in args:
+                if isinstance(a, torch.Tensor) and a.is_cuda:
+                    a.record_stream(s)
+        if k:
+            self.side_steps.add(i)
+            torch.cuda.set_stream(s)
+
+    def after(self, i):
+        k = self.stream_of[i]
+        if k:
+            torch.cuda.set_stream(self.main)
+        if i in self.need_ev:
+            ev = torch.cuda.Event()
+            ev.record(self.streams[k])
+            self.events[i] = ev
+
+    def finish(self, outs):
+        for k in sorted(self.started):
+            ev = torch.cuda.Event()
+            ev.record(self.streams[k])
+            self.main.wait_event(ev)
+        if self.side_steps:
+            for o in outs:
+                if isinstance(o, torch.Tensor) and o.is_cuda:
+                    o.record_stream(self.main)
 
 
 def _int_dtype_attr(attrs):

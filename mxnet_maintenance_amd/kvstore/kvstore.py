@@ -217,6 +217,43 @@ class KVStore(KVStoreBase):
                 t.copy_(flat[off:off + n].view(t.shape))
                 off += n
 
+    # ------------------------------------------------------------ engine scheduling
+    def _on_engine(self, fn, reads, writes, name):
+        """Run the communication ``fn`` as one dependency-engine device op on the device's comm
+        stream (reference: KVStoreLocal/KVStoreNCCL push their reduce/broadcast through
+        Engine::PushAsync with the arrays' variables).  The op reads the variables of ``reads``,
+        writes those of ``writes`` and this store's own variable (one total order of collectives
+        per process, the same on every rank); it starts after the work already queued on the
+        caller's stream (which produced the gradients), and the caller's stream waits on the GPU
+        for it before anything queued later can touch ``writes``.  Host arrays, and processes
+        without the native engine, run ``fn`` in place."""
+        from .. import engine
+        flat_r = [a for v in reads for a in _as_list(v)]
+        flat_w = [a for v in writes for a in _as_list(v)]
+        dev = next((a._data.device for a in flat_r + flat_w if a._data.is_cuda), None)
+        if dev is None or not engine.native_available() or torch.cuda.is_current_stream_capturing() or \
+                _env_flag('MXAMD_KVSTORE_ENGINE', True) is False:
+            fn()
+            return
+        if getattr(self, '_engine_var', None) is None:
+            self._engine_var = engine.new_var('kvstore')
+        comm = engine.comm_stream(dev)
+        producer = torch.cuda.current_stream(dev)
+        ready = torch.cuda.Event()
+        ready.record(producer)
+        wvars = [engine.var_of(a) for a in flat_w]
+        rvars = [engine.var_of(a) for a in flat_r if all(engine.var_of(a) is not w for w in wvars)]
+        for a in flat_r + flat_w:
+            a._data.record_stream(comm)
+
+        def op():
+            torch.cuda.current_stream().wait_event(ready)
+            with torch.no_grad():
+                fn()
+        engine.push_device(op, rvars, [self._engine_var] + wvars, stream=comm, name=name)
+        for v in wvars:
+            engine.stream_wait_var(v, producer)
+
     # ------------------------------------------------------------------- API
     def _keys(self, key):
         """``key`` as a list, checked against the store's key kind (all int or all str)."""
@@ -276,10 +313,14 @@ class KVStore(KVStoreBase):
             if len(kept) != len(keys):
                 keys = [k for k, _ in kept]
                 outs = [o for _, o in kept]
-        with torch.no_grad():
-            # written through .data: a pull into a parameter is an engine-ordered write in the
-            # reference, not an autograd-visible in-place op on a recorded leaf
-            self._fan_out([self._store[k]._data for k in keys], outs)
+        # written through .data: a pull into a parameter is an engine-ordered write in the
+        # reference, not an autograd-visible in-place op on a recorded leaf
+        stored = [self._store[k] for k in keys]
+
+        def comm():
+            with torch.no_grad():
+                self._fan_out([st._data for st in stored], outs)
+        self._on_engine(comm, stored, outs, 'kvstore_pull')
 
     def pushpull(self, key, value, out=None, priority=0):
         """Sum ``value`` over devices and workers and write the result to ``out``.
@@ -294,10 +335,13 @@ class KVStore(KVStoreBase):
         keys = self._keys(key)
         vals = value if isinstance(key, (list, tuple)) else [value]
         outs = vals if out is None else (out if isinstance(key, (list, tuple)) else [out])
-        with torch.no_grad():
-            sums = self._local_sums(keys, vals)
-            self._allreduce_many(sums, keys)
-            self._fan_out(sums, outs)
+
+        def comm():
+            with torch.no_grad():
+                sums = self._local_sums(keys, vals)
+                self._allreduce_many(sums, keys)
+                self._fan_out(sums, outs)
+        self._on_engine(comm, vals, outs, 'kvstore_pushpull')
 
     def broadcast(self, key, value, out, priority=0):
         self.init(key, value)
@@ -376,6 +420,12 @@ def create(name='local'):
         from .dist_async import KVStoreDistAsync
         return KVStoreDistAsync()
     return KVStore(name)
+
+
+def _env_flag(name, default):
+    import os
+    v = os.environ.get(name)
+    return default if v is None else v not in ('0', 'false', 'False', '')
 
 
 def _rsp_rows(st, idx):

@@ -85,6 +85,16 @@ def _nchw_on_hip(data):
 _NCHW_VIA_NHWC = os.environ.get('MXAMD_NCHW_VIA_NHWC', '1') == '1'
 
 
+def _nhwc_weight(w):
+    """KRSC layout of a KCRS weight for the channels-last kernels: a free view for 1x1 kernels, one
+    permuted copy otherwise (ResNet-50: ~50 MB of the ~25 GB a training step moves).  Not cached: the
+    optimizer kernels and replayed HIP graphs update weights without bumping tensor versions, so a
+    cache could serve stale weights."""
+    if w.shape[2] == 1 and w.shape[3] == 1 and w.is_contiguous():
+        return w.view(w.shape[0], 1, 1, w.shape[1])
+    return w.permute(0, 2, 3, 1).contiguous()
+
+
 def conv(data, weight, bias, stride, pad, dilate, groups, channel_last):
     nsp = data.dim() - 2
     if groups > 1 and nsp == 2 and _use_hip(data):
@@ -99,7 +109,7 @@ def conv(data, weight, bias, stride, pad, dilate, groups, channel_last):
         # NCHW API, channels-last execution: activations stay NHWC in memory between HIP kernels
         # (NCHW-shaped permuted views), so the default layout runs on the same MFMA kernels
         xl = _as_nhwc_view(data)
-        wl = weight.permute(0, 2, 3, 1).contiguous()
+        wl = _nhwc_weight(weight)
         if _K.conv_ok(xl, wl, stride, pad, dilate, groups):
             return _K.ConvNHWC.apply(xl, wl, bias, tuple(stride), tuple(pad), tuple(dilate)).permute(0, 3, 1, 2)
     if channel_last and _use_hip(data) and _K.conv_ok(data, weight, stride, pad, dilate, groups):
@@ -271,7 +281,17 @@ def pool(data, pool_type, kernel, stride, pad, convention, count_include_pad, ch
 # ---------------------------------------------------------------------------
 
 def relu(x):
+    if _use_hip(x) and _K.relu_ok(x):
+        return _K.ReluHip.apply(x)
     return torch.relu(x)
+
+
+def binary(op, a, b):
+    """Broadcast add/sub/mul/div/maximum/minimum of two same-dtype GPU tensors on the in-tree
+    kernel; None when the operands do not qualify (the caller runs the torch op)."""
+    if isinstance(a, torch.Tensor) and isinstance(b, torch.Tensor) and _use_hip(a) and _K.binary_ok(a, b):
+        return _K.BinaryHip.apply(a, b, op)
+    return None
 
 
 def gelu(x):

@@ -272,6 +272,141 @@ def gap_ok(x):
     return x.dtype in _DT and x.is_contiguous() and x.shape[-1] % 8 == 0
 
 
+# ---------------------------------------------------------------------------------- pointwise
+class ReluHip(torch.autograd.Function):
+    """relu / _backward_relu on src/kernels/pointwise.hip (16-byte vector lanes)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        _K.lib().relu_forward(_DT[x.dtype], x.data_ptr(), y.data_ptr(), x.numel(), _stream())
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        y, = ctx.saved_tensors
+        gy = gy.contiguous()
+        dx = torch.empty_like(y)
+        _K.lib().relu_backward(_DT[y.dtype], y.data_ptr(), gy.data_ptr(), dx.data_ptr(), y.numel(), _stream())
+        return dx
+
+
+def relu_ok(x):
+    return x.dtype in _DT and x.is_cuda and x.numel() > 0 and x.data_ptr() % 16 == 0 and x.is_contiguous()
+
+
+_PW_OPS = {'add': 0, 'sub': 1, 'mul': 2, 'div': 3, 'maximum': 4, 'minimum': 5}
+
+
+def _bcast_strides(t, shape):
+    """Element strides of ``t`` broadcast to ``shape`` (0 on broadcast axes)."""
+    lead = len(shape) - t.dim()
+    st = [0] * lead + list(t.stride())
+    sz = [1] * lead + list(t.shape)
+    return [0 if sz[d] == 1 and shape[d] != 1 else st[d] for d in range(len(shape))]
+
+
+def _collapse(shape, sa, sb):
+    """Merge adjacent dimensions that are contiguous for both operands (fewer index divisions)."""
+    dims = [(n, a, b) for n, a, b in zip(shape, sa, sb) if n != 1] or [(1, 0, 0)]
+    out = [list(dims[-1])]
+    for n, a, b in reversed(dims[:-1]):
+        pn, pa, pb = out[0]
+        if a == pa * pn and b == pb * pn:
+            out[0] = [n * pn, pa, pb]
+        else:
+            out.insert(0, [n, a, b])
+    return [d[0] for d in out], [d[1] for d in out], [d[2] for d in out]
+
+
+def _is_row(t, full):
+    """``t`` equals the trailing dimensions of ``full`` (after dropping its leading size-1 axes)."""
+    ts = tuple(t.shape)
+    while ts and ts[0] == 1:
+        ts = ts[1:]
+    return len(ts) <= len(full) and ts == full[len(full) - len(ts):]
+
+
+def binary_hip(op, a, b):
+    """``a op b`` with NumPy broadcasting on src/kernels/pointwise.hip (same dtype operands).  Equal
+    shapes and a row operand repeated along the leading axes run 16-byte vector lanes; any other
+    broadcast runs the strided kernel."""
+    shape = torch.broadcast_shapes(a.shape, b.shape)
+    out = torch.empty(shape, dtype=a.dtype, device=a.device)
+    n = out.numel()
+    if n == 0:
+        return out
+    vec = 4 if a.dtype == torch.float32 else 8
+    aligned = a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
+    mode, row = 3, 0
+    full = tuple(shape)
+    if aligned and a.is_contiguous() and b.is_contiguous():
+        if tuple(a.shape) == full and tuple(b.shape) == full:
+            mode = 0
+        elif tuple(a.shape) == full and _is_row(b, full) and b.numel() % vec == 0:
+            mode, row = 1, b.numel()
+        elif tuple(b.shape) == full and _is_row(a, full) and a.numel() % vec == 0:
+            mode, row = 2, a.numel()
+    if mode == 3:
+        shp, sa, sb = _collapse(list(shape), _bcast_strides(a, shape), _bcast_strides(b, shape))
+        if len(shp) > 6:
+            return {'add': torch.add, 'sub': torch.sub, 'mul': torch.mul, 'div': torch.div,
+                    'maximum': torch.maximum, 'minimum': torch.minimum}[op](a, b)
+    else:
+        shp, sa, sb = [], [], []
+    _K.lib().pointwise_binary(_DT[a.dtype], _PW_OPS[op], a.data_ptr(), b.data_ptr(), out.data_ptr(), n, mode, row,
+                              shp, sa, sb, _stream())
+    return out
+
+
+def _sum_to(g, shape):
+    if tuple(g.shape) == tuple(shape):
+        return g
+    return g.sum_to_size(shape) if len(shape) else g.sum()
+
+
+class BinaryHip(torch.autograd.Function):
+    """Broadcast add/sub/mul/div/maximum/minimum: forward and the element-wise parts of the backward
+    on the in-tree kernel; broadcast axes of the gradients are reduced with sum_to_size."""
+
+    @staticmethod
+    def forward(ctx, a, b, op):
+        ctx.op = op
+        ctx.sa, ctx.sb = tuple(a.shape), tuple(b.shape)
+        if op in ('mul', 'div', 'maximum', 'minimum'):
+            ctx.save_for_backward(a, b)
+        return binary_hip(op, a, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        op = ctx.op
+        g = g.contiguous()
+        if op == 'add':
+            return _sum_to(g, ctx.sa), _sum_to(g, ctx.sb), None
+        if op == 'sub':
+            return _sum_to(g, ctx.sa), _sum_to(-g, ctx.sb), None
+        a, b = ctx.saved_tensors
+        if op == 'mul':
+            return _sum_to(binary_hip('mul', g, b), ctx.sa), _sum_to(binary_hip('mul', g, a), ctx.sb), None
+        if op == 'div':
+            ga = binary_hip('div', g, b)
+            gb = -binary_hip('div', binary_hip('mul', ga, a), b)
+            return _sum_to(ga, ctx.sa), _sum_to(gb, ctx.sb), None
+        take_a = (a >= b) if op == 'maximum' else (a <= b)
+        ga = torch.where(take_a, g, torch.zeros_like(g))
+        return _sum_to(ga, ctx.sa), _sum_to(g - ga, ctx.sb), None
+
+
+def binary_ok(a, b):
+    return (a.is_cuda and b.is_cuda and a.dtype == b.dtype and a.dtype in _DT and a.numel() > 0 and
+            b.numel() > 0 and a.device == b.device)
+
+
+__all__ += ['ReluHip', 'relu_ok', 'BinaryHip', 'binary_ok', 'binary_hip']
+
+
 
 
 def flat_sgd(w, g, mom, w32, lr, wd, momentum, rescale, clip, hp=None):
@@ -864,19 +999,24 @@ def pw_ok(x, kin, nout):
             and bool(_K.lib().conv_pw_stream_ok(int(kin), int(nout))))
 
 
-def conv_pw(x, w2, bn_stats=False):
-    """y = x . w2^T for NHWC ``x`` [..., Cin] and ``w2`` [Cout, Cin] on the streaming 1x1 kernel;
-    ``bn_stats``: BatchNorm sum / sum-of-squares partials in ``y._mxamd_bn_part`` (one per workgroup)."""
+def conv_pw(x, w2, bn_stats=False, addend=None):
+    """y = x . w2^T (+ addend) for NHWC ``x`` [..., Cin] and ``w2`` [Cout, Cin] on the streaming 1x1
+    kernel; ``bn_stats``: BatchNorm sum / sum-of-squares partials in ``y._mxamd_bn_part`` (one per
+    workgroup); ``addend`` (the output's shape and dtype) is added in the epilogue."""
     C = x.shape[-1]
     K = w2.shape[0]
     M = x.numel() // C
     w2 = w2.contiguous()
     y = torch.empty(x.shape[:-1] + (K,), dtype=x.dtype, device=x.device)
+    if addend is not None:
+        addend = addend.contiguous()
+        if tuple(addend.shape) != tuple(y.shape) or addend.dtype != y.dtype or addend.data_ptr() % 16:
+            raise ValueError('conv_pw: addend must match the output (shape, dtype, 16-byte alignment)')
     lib = _K.lib()
     grid = lib.conv_pw_stream_grid(M, C, K, _num_cus(x.device))
     part = torch.empty(2 * K * grid, dtype=torch.float32, device=x.device) if bn_stats else None
     lib.conv_pw_stream(_DT[x.dtype], x.data_ptr(), w2.data_ptr(), y.data_ptr(), _zero_page(x.device).data_ptr(), M, C,
-                       K, _p(part), grid, _stream())
+                       K, _p(part), grid, _stream(), _p(addend))
     if part is not None:
         y._mxamd_bn_part = (part, grid)
     return y
@@ -1260,6 +1400,10 @@ def _tee_dgrad(gy, x, w, gpass, inplace, bn_src=None):
                 # statistics from this dgrad's epilogue
                 fused.append(('hip%d+bn' % v, lambda big=big: big(bn=bn_src)))
     cands.extend(_gemm_dgrad_1x1(gy, w, x.shape, addend=gpass))
+    if pw_ok(gy, K, C) and (gpass is None or (gpass.is_contiguous() and gpass.data_ptr() % 16 == 0)):
+        # streaming 1x1 kernel: small reductions (K <= 512) are memory-bound; the shortcut gradient
+        # is added in its epilogue
+        cands.append(('pw', lambda: conv_pw(gy, w2.t(), addend=gpass)))
     # autotuning runs every candidate: use an out-of-place GEMM there (the in-place one would
     # accumulate into gpass once per timing repetition)
     cands.append(('mm', lambda: mm() if not (gpass is not None and inplace) else

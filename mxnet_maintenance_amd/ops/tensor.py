@@ -75,6 +75,9 @@ class _Relu(torch.autograd.Function):
 
 
 def _relu(x):
+    if x.is_cuda:
+        from . import hip_ops
+        return hip_ops.relu(x)         # src/kernels/pointwise.hip
     return _Relu.apply(x) if x.requires_grad and x.is_floating_point() else torch.relu(x)
 
 
@@ -348,17 +351,31 @@ _BCAST_NAMES = {'add': ['broadcast_add', 'broadcast_plus'], 'sub': ['broadcast_s
                 'logical_xor': ['broadcast_logical_xor']}
 
 
-def _make_binary(f):
-    def op(lhs, rhs):
+_HIP_BINARY = ('add', 'sub', 'mul', 'div', 'maximum', 'minimum')
+
+
+def _make_binary(f, name=None):
+    if name not in _HIP_BINARY:
+        def op(lhs, rhs):
+            return f(lhs, rhs)
+        return op
+
+    def op_hip(lhs, rhs):
+        # GPU operands of one dtype: the in-tree broadcast kernel (src/kernels/pointwise.hip)
+        if lhs.is_cuda:
+            from . import hip_ops
+            r = hip_ops.binary(name, lhs, rhs)
+            if r is not None:
+                return r
         return f(lhs, rhs)
-    return op
+    return op_hip
 
 
 for _k, _f in _BINARY.items():
     names = _ELEMWISE_NAMES[_k]
-    register(names[0], _make_binary(_f), arg_names=('lhs', 'rhs'), aliases=names[1:])
+    register(names[0], _make_binary(_f, _k), arg_names=('lhs', 'rhs'), aliases=names[1:])
     bn = _BCAST_NAMES[_k]
-    register(bn[0], _make_binary(_f), arg_names=('lhs', 'rhs'), aliases=bn[1:])
+    register(bn[0], _make_binary(_f, _k), arg_names=('lhs', 'rhs'), aliases=bn[1:])
 
 
 def _make_scalar(f, reverse=False):

@@ -50,6 +50,10 @@ void softmax_ce_forward(int dtype, int label_is_int, const void* logits, const v
 void softmax_ce_backward(int dtype, int label_is_int, const void* logits, const void* label, const float* lse,
                          const float* gout, void* dlogits, int N, int K, hipStream_t s);
 void gap_nhwc_forward(int dtype, const void* x, void* y, int N, int HW, int C, hipStream_t s);
+void relu_forward(int dtype, const void* x, void* y, int64_t n, hipStream_t s);
+void relu_backward(int dtype, const void* y, const void* dy, void* dx, int64_t n, hipStream_t s);
+void pointwise_binary(int dtype, int op, const void* a, const void* b, void* out, int64_t n, int mode, int64_t row,
+                      int ndim, const int64_t* shape, const int64_t* astride, const int64_t* bstride, hipStream_t s);
 void gap_nhwc_backward(int dtype, const void* dy, void* dx, int N, int HW, int C, hipStream_t s);
 void flat_sgd(int dtype, void* w, const void* g, float* mom, float* w32, int64_t n, float lr, float wd,
               float momentum, float rescale, float clip, const float* hp, hipStream_t s);
@@ -148,7 +152,7 @@ void twobit_dequantize_sum(const void* packed, int64_t row_bytes, int nrows, int
 int conv_pw_stream_ok(int kin, int nout);
 int conv_pw_stream_grid(int M, int kin, int nout, int ncu);
 void conv_pw_stream(int dtype, const void* x, const void* w, void* y, const void* zero, int M, int kin, int nout,
-                    float* part, int grid, hipStream_t s);
+                    float* part, int grid, hipStream_t s, const void* addend);
 void conv_gen(int dtype, int mode, const void* src, const void* wsrc, const float* bias, void* dst, const int* geom,
               int splits, hipStream_t s);
 void rnn_fwd_seq(int dtype, int mode, const float* gx, const void* h0, const float* c0, const void* whh,
@@ -238,9 +242,9 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("conv_pw_stream_ok", &conv_pw_stream_ok);
   m.def("conv_pw_stream_grid", &conv_pw_stream_grid);
   m.def("conv_pw_stream", [](int dt, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t zero, int M, int kin, int nout,
-                             uintptr_t part, int grid, uintptr_t s) {
+                             uintptr_t part, int grid, uintptr_t s, uintptr_t addend) {
     conv_pw_stream(dt, P<const void>(x), P<const void>(w), P<void>(y), P<const void>(zero), M, kin, nout,
-                   P<float>(part), grid, S(s));
+                   P<float>(part), grid, S(s), P<const void>(addend));
     check_launch("conv_pw_stream");
   });
   // general implicit-GEMM convolution: grouped / dilated / 1-3-D / fp32 / transposed (src/kernels/conv_gen.hip)
@@ -362,6 +366,22 @@ PYBIND11_MODULE(_hip_kernels, m) {
     softmax_ce_backward(dt, li, P<void>(logits), P<void>(label), P<float>(lse), P<float>(gout), P<void>(dlogits), N,
                         K, S(s));
     check_launch("softmax_ce_backward");
+  });
+  m.def("relu_forward", [](int dt, uintptr_t x, uintptr_t y, int64_t n, uintptr_t s) {
+    relu_forward(dt, P<void>(x), P<void>(y), n, S(s));
+    check_launch("relu_forward");
+  });
+  m.def("relu_backward", [](int dt, uintptr_t y, uintptr_t dy, uintptr_t dx, int64_t n, uintptr_t s) {
+    relu_backward(dt, P<void>(y), P<void>(dy), P<void>(dx), n, S(s));
+    check_launch("relu_backward");
+  });
+  m.def("pointwise_binary", [](int dt, int op, uintptr_t a, uintptr_t b, uintptr_t out, int64_t n, int mode,
+                               int64_t row, std::vector<int64_t> shape, std::vector<int64_t> sa,
+                               std::vector<int64_t> sb, uintptr_t s) {
+    if (shape.size() != sa.size() || shape.size() != sb.size()) throw std::runtime_error("pointwise_binary: rank");
+    pointwise_binary(dt, op, P<void>(a), P<void>(b), P<void>(out), n, mode, row, static_cast<int>(shape.size()),
+                     shape.data(), sa.data(), sb.data(), S(s));
+    check_launch("pointwise_binary");
   });
   m.def("gap_nhwc_forward", [](int dt, uintptr_t x, uintptr_t y, int N, int HW, int C, uintptr_t s) {
     gap_nhwc_forward(dt, P<void>(x), P<void>(y), N, HW, C, S(s));

@@ -18,7 +18,10 @@
 //     writes) -> whole 16-byte row chunks -> coalesced global stores of complete pixel rows;
 //   * optional BatchNorm statistics: each thread keeps per-channel sum / sum-of-squares of the
 //     rows it stores over ALL its tiles; at the end one partial per workgroup per channel
-//     ([2][NOUT][grid] channel-major, the layout bn_nhwc.hip's finalize consumes).
+//     ([2][NOUT][grid] channel-major, the layout bn_nhwc.hip's finalize consumes);
+//   * optional addend (y = conv + addend: the identity-shortcut gradient of a tee dgrad): the
+//     addend chunks a thread stores for tile i+1 are loaded into registers right after tile i's
+//     stores, so they travel while tile i+1's MFMAs run; the counted waits include them.
 //
 // Requirements (host-checked): NHWC, KIN in {64,128,256,512}, NOUT in {64..1024} with
 // NOUT/WC * KIN <= 8192 (the register budget for the resident weights).
@@ -119,10 +122,10 @@ __device__ __forceinline__ void vm_wait_le(int n) {
   else vm_wait<0>();
 }
 
-template <typename T, int KIN, int NOUT, bool STATS>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) conv_pw_stream_kernel(const T* __restrict__ x, const T* __restrict__ w,
-                                                                T* __restrict__ y, const T* __restrict__ zero, int M,
-                                                                int ntiles, float* __restrict__ part) {
+template <typename T, int KIN, int NOUT, bool STATS, bool ADD>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) conv_pw_stream_kernel(
+    const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y, const T* __restrict__ zero, int M, int ntiles,
+    float* __restrict__ part, const T* __restrict__ addend) {
   using C = PwCfg<KIN, NOUT>;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x;
@@ -172,6 +175,25 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) c
   const int my_tiles = wg < ntiles ? (ntiles - wg + grid - 1) / grid : 0;
   for (int j = 0; j < C::D && j < my_tiles; ++j) issue(wg + j * grid, j);
 
+  // ---- addend chunks of tile `t` (same chunk mapping as the store loop; dead chunks read an
+  // out-of-range offset, so every lane issues exactly SPT loads)
+  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<T*>(ADD ? addend : y), 0, static_cast<int>(static_cast<uint32_t>(M) * NOUT * sizeof(T)), 0x00020000);
+  u32x4 addv[ADD ? C::SPT : 1];
+  auto load_add = [&](int t) {
+#pragma unroll
+    for (int k = 0; k < C::SPT; ++k) {
+      const int e = tid + k * 512;
+      const bool in_tile = e < C::BM * C::OCH;
+      const int pix = in_tile ? e / C::OCH : 0;
+      const int p = t * C::BM + pix;
+      const uint32_t off = (in_tile && p < M) ? (static_cast<uint32_t>(p) * NOUT + (e % C::OCH) * 8) * sizeof(T)
+                                              : 0xFFFFFFF0u;
+      addv[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ars, off, 0, 0));
+    }
+  };
+  if (ADD && my_tiles > 0) load_add(wg);
+
   float s1[8], s2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -189,11 +211,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) c
     // VM ops younger than tile it's DMA: the tiles issued after it, and the epilogue stores of the
     // iterations run since it was issued (tile j < D came from the prologue, tile j >= D from
     // iteration j - D)
+    // (with ADD, also the addend loads of tiles it-D+1 .. it, issued after tile it's DMA)
     {
       const int later = (my_tiles - 1 - it) < C::D ? (my_tiles - 1 - it) : C::D;
       const int epis = it < C::D ? it : C::D;
-      if (later == C::D && epis == C::D) vm_wait<C::D*(C::LPT + C::SPT)>();
-      else vm_wait_le(later * C::LPT + epis * C::SPT);
+      const int adds = ADD ? (it + 1 < C::D ? it + 1 : C::D) : 0;
+      if (later == C::D && epis == C::D) vm_wait<C::D*(C::LPT + (ADD ? 2 : 1) * C::SPT)>();
+      else vm_wait_le(later * C::LPT + (epis + adds) * C::SPT);
     }
     lds_barrier();
 
@@ -229,6 +253,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) c
         *reinterpret_cast<uint2*>(epi + pix * C::PITCH + co * 2) = PwM<T>::pack4(v[0], v[1], v[2], v[3]);
       }
     lds_barrier();
+    // the addend of this tile has landed once at most tile it+D's DMA (issued after it) is pending
+    if (ADD) vm_wait_le(it + C::D < my_tiles ? C::LPT : 0);
     // ---- coalesced row stores (exactly SPT per thread: rows past M go out of range by buffer bounds)
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
         y, 0, static_cast<int>(static_cast<uint32_t>(M) * NOUT * sizeof(T)), 0x00020000);
@@ -243,6 +269,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) c
       const int p = t * C::BM + pix;
       Vec8<T> v;
       v.raw = *reinterpret_cast<const uint4*>(epi + pix * C::PITCH + c8 * 16);
+      if (ADD) {
+        Vec8<T> a;
+        a.raw = __builtin_bit_cast(uint4, addv[k]);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v.set(q, v.get(q) + a.get(q));
+      }
       const bool live = in_tile && p < M;
       const uint32_t off = live ? (static_cast<uint32_t>(p) * NOUT + c8 * 8) * sizeof(T) : 0xFFFFFFF0u;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v.raw), yrs, off, 0, 0);
@@ -256,6 +288,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) c
       }
     }
     (void)my_c8;
+    if (ADD && it + 1 < my_tiles) load_add(t + grid);
   }
   if (STATS) {
     // every thread's chunk is fixed (tid % OCH): combine the 512/OCH threads of each chunk through
@@ -280,32 +313,35 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) c
   }
 }
 
+template <typename T, int KIN, int NOUT, bool STATS, bool ADD>
+void launch_pw_v(const void* x, const void* w, void* y, const void* zero, int M, float* part, const void* addend,
+                 int grid, hipStream_t s) {
+  using C = PwCfg<KIN, NOUT>;
+  static bool set = false;
+  if (!set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
+    set = true;
+  }
+  const int ntiles = (M + C::BM - 1) / C::BM;
+  hipLaunchKernelGGL((conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD>), dim3(grid), dim3(512), C::SMEM, s,
+                     static_cast<const T*>(x), static_cast<const T*>(w), static_cast<T*>(y),
+                     static_cast<const T*>(zero), M, ntiles, part, static_cast<const T*>(addend));
+}
+
 template <typename T, int KIN, int NOUT>
-void launch_pw(const void* x, const void* w, void* y, const void* zero, int M, float* part, int grid, hipStream_t s) {
+void launch_pw(const void* x, const void* w, void* y, const void* zero, int M, float* part, const void* addend,
+               int grid, hipStream_t s) {
   using C = PwCfg<KIN, NOUT>;
   static_assert(C::SMEM <= 80 * 1024, "two workgroups per CU");
   static_assert(C::NST >= 2, "ring depth");
-  const int ntiles = (M + C::BM - 1) / C::BM;
+  static_assert(C::D * (C::LPT + 2 * C::SPT) < 64, "vmcnt range with the addend loads");
   if (part) {
-    static bool set = false;
-    if (!set) {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pw_stream_kernel<T, KIN, NOUT, true>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
-      set = true;
-    }
-    hipLaunchKernelGGL((conv_pw_stream_kernel<T, KIN, NOUT, true>), dim3(grid), dim3(512), C::SMEM, s,
-                       static_cast<const T*>(x), static_cast<const T*>(w), static_cast<T*>(y),
-                       static_cast<const T*>(zero), M, ntiles, part);
+    if (addend) launch_pw_v<T, KIN, NOUT, true, true>(x, w, y, zero, M, part, addend, grid, s);
+    else launch_pw_v<T, KIN, NOUT, true, false>(x, w, y, zero, M, part, addend, grid, s);
   } else {
-    static bool set = false;
-    if (!set) {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pw_stream_kernel<T, KIN, NOUT, false>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
-      set = true;
-    }
-    hipLaunchKernelGGL((conv_pw_stream_kernel<T, KIN, NOUT, false>), dim3(grid), dim3(512), C::SMEM, s,
-                       static_cast<const T*>(x), static_cast<const T*>(w), static_cast<T*>(y),
-                       static_cast<const T*>(zero), M, ntiles, part);
+    if (addend) launch_pw_v<T, KIN, NOUT, false, true>(x, w, y, zero, M, part, addend, grid, s);
+    else launch_pw_v<T, KIN, NOUT, false, false>(x, w, y, zero, M, part, addend, grid, s);
   }
 }
 
@@ -315,10 +351,10 @@ void launch_pw(const void* x, const void* w, void* y, const void* zero, int M, f
 
 template <typename T>
 bool dispatch_pw(int kin, int nout, const void* x, const void* w, void* y, const void* zero, int M, float* part,
-                 int grid, hipStream_t s) {
+                 const void* addend, int grid, hipStream_t s) {
 #define MXAMD_PW_CASE(K, N)                                        \
   if (kin == K && nout == N) {                                     \
-    launch_pw<T, K, N>(x, w, y, zero, M, part, grid, s);           \
+    launch_pw<T, K, N>(x, w, y, zero, M, part, addend, grid, s);   \
     return true;                                                   \
   }
   MXAMD_PW_SHAPES(MXAMD_PW_CASE)
@@ -346,13 +382,13 @@ int conv_pw_stream_grid(int M, int kin, int nout, int ncu) {
 }
 
 void conv_pw_stream(int dtype, const void* x, const void* w, void* y, const void* zero, int M, int kin, int nout,
-                    float* part, int grid, hipStream_t s) {
+                    float* part, int grid, hipStream_t s, const void* addend) {
   MXAMD_HOST_CHECK(conv_pw_stream_ok(kin, nout), "conv_pw_stream: unsupported (Cin, Cout)");
   MXAMD_HOST_CHECK(grid >= 1 && (int64_t)M * nout * 2 < (1ll << 31) - 64 && (int64_t)M * kin < (1ll << 31),
                    "conv_pw_stream: tensor too large for 32-bit offsets");
   bool ok = false;
-  if (dtype == kF16) ok = dispatch_pw<__half>(kin, nout, x, w, y, zero, M, part, grid, s);
-  else if (dtype == kBF16) ok = dispatch_pw<__hip_bfloat16>(kin, nout, x, w, y, zero, M, part, grid, s);
+  if (dtype == kF16) ok = dispatch_pw<__half>(kin, nout, x, w, y, zero, M, part, addend, grid, s);
+  else if (dtype == kBF16) ok = dispatch_pw<__hip_bfloat16>(kin, nout, x, w, y, zero, M, part, addend, grid, s);
   MXAMD_HOST_CHECK(ok, "conv_pw_stream: dtype must be f16 or bf16");
 }
 

@@ -30,3 +30,39 @@ def test_conv_pw_matches_fp32(kin, nout, M, dt):
     # no statistics requested: same output
     y2 = KF.conv_pw(x, w)
     assert torch.equal(y2, y)
+
+
+@pytest.mark.parametrize('kin,nout,M,dt', [(64, 256, 3136 * 3 + 17, torch.float16), (128, 256, 4000, torch.bfloat16),
+                                           (256, 64, 2001, torch.float16), (64, 64, 65, torch.bfloat16),
+                                           (512, 128, 3000, torch.float16)])
+def test_conv_pw_addend_epilogue(kin, nout, M, dt):
+    """y = x . w^T + addend (the identity-shortcut gradient of a tee dgrad) in the epilogue."""
+    dev = torch.device('cuda', 0)
+    g = torch.Generator().manual_seed(3 * kin + nout)
+    x = (torch.rand(M, kin, generator=g) * 2 - 1).to(dev, dt).view(1, 1, M, kin)
+    w = ((torch.rand(nout, kin, generator=g) * 2 - 1) / kin ** 0.5).to(dev, dt)
+    a = (torch.rand(M, nout, generator=g) * 2 - 1).to(dev, dt).view(1, 1, M, nout)
+    y = KF.conv_pw(x, w, addend=a)
+    ref = x.float().reshape(M, kin) @ w.float().t() + a.float().reshape(M, nout)
+    err = float((y.float().reshape(M, nout) - ref).norm() / ref.norm())
+    assert err < 1e-2, err
+    # with statistics as well (they cover the summed output)
+    y2 = KF.conv_pw(x, w, bn_stats=True, addend=a)
+    assert torch.equal(y2, y)
+    part, nparts = y2._mxamd_bn_part
+    yr = y.float().reshape(M, nout)
+    assert float((part.view(2, nout, nparts).sum(-1)[0] - yr.sum(0)).abs().max()) < \
+        1e-2 * float(yr.abs().sum(0).max() + 1)
+
+
+def test_tee_dgrad_pw_candidate_matches_mm():
+    """The tee dgrad's streaming-kernel candidate equals dY . W + dShortcut."""
+    dev = torch.device('cuda', 0)
+    dt = torch.float16
+    N, H, W, C, K = 2, 28, 28, 256, 64
+    gy = (torch.randn(N, H, W, K, device=dev) * 0.1).to(dt)
+    gpass = (torch.randn(N, H, W, C, device=dev) * 0.1).to(dt)
+    w = (torch.randn(K, 1, 1, C, device=dev) / C ** 0.5).to(dt)
+    y = KF.conv_pw(gy, w.reshape(K, C).t(), addend=gpass)
+    ref = gy.float().reshape(-1, K) @ w.float().reshape(K, C) + gpass.float().reshape(-1, C)
+    assert float((y.float().reshape(-1, C) - ref).abs().max()) < 2e-2
