@@ -640,6 +640,20 @@ class HybridBlock(Block):
         self._param_map = [(n, params[n]) for n in input_names if n in param_names]
         self._cached_op = CachedOp(self._fuse_for(out, args), self._flags)
 
+    def _apply_backend(self, feed, ctx):
+        """hybridize(backend=...) / optimize_for: run the backend (an extension library's graph pass
+        or partitioner, or a registered subgraph backend) on the cached graph with the bound arrays,
+        once; arrays a pass adds become extra inputs of the cached graph."""
+        from ..ndarray.ndarray import NDArray
+        sym = self._cached_op.sym
+        aux_names = set(sym.list_auxiliary_states())
+        args = {k: NDArray(v) for k, v in feed.items() if k not in aux_names and v is not None}
+        aux = {k: NDArray(v) for k, v in feed.items() if k in aux_names and v is not None}
+        new = sym.optimize_for(self._backend, args, aux, ctx=ctx, **(self._backend_opts or {}))
+        self._extra_inputs = {k: v for k, v in list(args.items()) + list(aux.items()) if k not in feed}
+        self._cached_op = CachedOp(new, self._flags)
+        self._backend_applied = True
+
     @staticmethod
     def _fuse_for(out, args):
         """Pointwise fusion of the cached graph when it will run on a GPU (reference: the cached op's
@@ -704,6 +718,10 @@ class HybridBlock(Block):
                     tl[id(a)] = a
         for n, d in pdata:
             feed[n] = d._data
+        if self._backend and not getattr(self, '_backend_applied', False):
+            self._apply_backend(feed, ctx)
+        for n, d in getattr(self, '_extra_inputs', {}).items():
+            feed[n] = d._data
         if torch.is_grad_enabled() != rec:
             with torch.set_grad_enabled(rec):
                 outs = self._cached_op(feed, ctx.torch_device, idts)
@@ -746,6 +764,8 @@ class HybridBlock(Block):
     def _clear_cached_op(self):
         self._cached_graph = ()
         self._cached_op = None
+        self._backend_applied = False
+        self._extra_inputs = {}
 
     def register_child(self, block, name=None):
         if not isinstance(block, HybridBlock):
@@ -756,6 +776,7 @@ class HybridBlock(Block):
 
     def hybridize(self, active=True, backend=None, backend_opts=None, clear=True, **kwargs):
         self._backend = backend
+        self._backend_applied = False
         if backend_opts is not None:
             assert isinstance(backend_opts, dict), 'HybridBlock hybridize requires backend_opts to be a dictionary.'
             self._backend_opts = backend_opts

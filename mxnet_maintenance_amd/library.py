@@ -18,8 +18,8 @@ framework (``mx.nd.<name>``, ``mx.sym.<name>``, hybridized blocks), with
 * gradients through autograd: the library's backward receives ``[out grads, inputs, outputs]``
   and writes the input gradients (the lib_api convention).
 
-Partitioner / graph-pass registrations (``_partRegSize`` / ``_passRegSize``) are reported, not
-run: graph partitioning here goes through ``symbol.subgraph`` backends.
+Graph passes, partitioners and subgraph operators the library registers are driven by
+library_graph.py: ``Symbol.optimize_for(<pass or partitioner name>, args, aux, **options)``.
 """
 import ctypes
 import importlib.util
@@ -424,9 +424,13 @@ def _load_lib_api(path, verbose):
     lib = _Lib(path)
     from .ops import registry
     names = []
+    from . import library_graph
     for i in range(lib.dll._opRegSize()):
         op = _LibOp(lib, i)
         if op.is_subgraph_op:
+            # runs the subgraph a library partitioner formed (library_graph.register_subgraph_op)
+            library_graph.register_subgraph_op(op)
+            names.append(op.name)
             continue
         registry.register(op.name, _make_fn(op),
                           arg_names=(lambda op: lambda attrs: ['data%d' % j
@@ -434,12 +438,10 @@ def _load_lib_api(path, verbose):
                           num_outputs=(lambda op: lambda attrs: op.num_inouts(attrs)[1])(op),
                           extra_params=True)
         names.append(op.name)
-    parts = lib.dll._partRegSize() if hasattr(lib.dll, '_partRegSize') else 0
-    passes = lib.dll._passRegSize() if hasattr(lib.dll, '_passRegSize') else 0
+    passes, parts = library_graph.register_library(lib)
     if verbose:
-        print('library %s (extension ABI v%d): registered %s%s' % (
-            os.path.basename(path), lib.version, names,
-            '' if not (parts or passes) else ' (%d partitioners / %d graph passes not run)' % (parts, passes)))
+        print('library %s (extension ABI v%d): registered operators %s, graph passes %s, partitioners %s' % (
+            os.path.basename(path), lib.version, names, passes, parts))
     return lib, names
 
 

@@ -90,7 +90,7 @@ class OpDef:
                 if s is not None and isinstance(s[0], str) and s[0].endswith('?'):
                     out[k] = None       # an optional parameter explicitly set to None
                 continue
-            if k.startswith('__') and k.endswith('__'):
+            if k.startswith('__') and k.endswith('__') and k not in spec:
                 continue
             s = spec.get(k)
             if s is None:

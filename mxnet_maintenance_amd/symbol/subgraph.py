@@ -59,25 +59,20 @@ def _depends_on(node, members, memo):
     return hit
 
 
-def partition(sym, op_names):
-    """Partition ``sym``: every convex group of nodes whose operator is in ``op_names`` becomes one
-    ``_CachedOp`` node.  Returns a new Symbol (``sym`` is unchanged)."""
-    from .symbol import Symbol, _Node, _aux_var_ids
-    wanted = {id(registry.get(n)) for n in op_names if registry.has(n)}
-    if not wanted:
-        return sym
-    order = sym._topo()
-    index = {id(n): i for i, n in enumerate(order)}
-    groups = []          # list of member lists
-    member_sets = []
-    group_of = {}
+def _group_convex(order, selectable, joinable=None):
+    """Greedy convex grouping in topological order: a selectable node joins the group of one of its
+    inputs when ``joinable(input_node, node, group_members)`` allows it and the group stays convex
+    (no path leaves the group and comes back); otherwise it starts a group.  Returns member lists."""
+    groups, member_sets, group_of = [], [], {}
     for n in order:
-        if n.op is None or id(n.opdef()) not in wanted:
+        if n.op is None or not selectable(n):
             continue
         chosen = None
         for a, _ in n.inputs:
             g = group_of.get(id(a))
             if g is None or g == chosen:
+                continue
+            if joinable is not None and not joinable(a, n, groups[g]):
                 continue
             members = member_sets[g]
             memo = {}
@@ -91,9 +86,14 @@ def partition(sym, op_names):
         groups[chosen].append(n)
         member_sets[chosen].add(id(n))
         group_of[id(n)] = chosen
-    if not groups:
-        return sym
-    # entries consumed outside their group (or graph outputs)
+    return groups
+
+
+def describe_groups(sym, order, groups):
+    """Per group: its external input entries (``ext``, in the order a depth-first walk of the original
+    graph reaches them), the entries used outside it (``outs``), the positions of auxiliary inputs
+    among ``ext`` (``aux``) and the subgraph as a JSON-able dict whose inputs are ``data<i>``."""
+    group_of = {id(m): gi for gi, g in enumerate(groups) for m in g}
     used_outside = set()
     for n in order:
         for a, j in n.inputs:
@@ -103,31 +103,12 @@ def partition(sym, op_names):
         if id(n) in group_of:
             used_outside.add((id(n), j))
     aux_of = _aux_positions(order)
-    remap = {}
-    last = {gi: g[-1] for gi, g in enumerate(groups)}
-    built = {}
-
-    def entry(a, j):
-        r = remap.get((id(a), j))
-        return r if r is not None else (remap.get(('node', id(a)), a), j)
-
-    for n in order:
-        gi = group_of.get(id(n))
-        if gi is None:
-            if n.op is None:
-                continue
-            nn = _Node(n.op, n.name, n.attrs, [entry(a, j) for a, j in n.inputs])
-            remap[('node', id(n))] = nn
-            continue
-        if last[gi] is not n:
-            continue
-        members = member_sets[gi]
+    descs = []
+    for gi, g in enumerate(groups):
+        members = {id(m) for m in g}
         ext, ext_idx, aux_idx = [], {}, []
         sub_nodes, local = [], {}
-        outs = [(m, j) for m in groups[gi] for j in range(m.num_outputs()) if (id(m), j) in used_outside]
-        # external entries numbered in the order a depth-first walk of the original graph reaches them
-        # (through the group's outputs, inputs in order), so the partitioned graph lists its variables
-        # in the original order
+        outs = [(m, j) for m in g for j in range(m.num_outputs()) if (id(m), j) in used_outside]
         seen = set()
         for root, _ in outs:
             stack = [(root, 0)]
@@ -150,14 +131,14 @@ def partition(sym, op_names):
         for k, (a, j) in enumerate(ext):
             sub_nodes.append({'op': 'null', 'name': 'data%d' % k, 'inputs': []})
             local[('ext', id(a), j)] = len(sub_nodes) - 1
-        for m in groups[gi]:
+        for m in g:
             ins = []
-            for p, (a, j) in enumerate(m.inputs):
+            for p_, (a, j) in enumerate(m.inputs):
                 if id(a) in members:
                     ins.append([local[id(a)], j, 0])
                     continue
                 k = ext_idx[(id(a), j)]
-                if (id(m), p) in aux_of and k not in aux_idx:
+                if (id(m), p_) in aux_of and k not in aux_idx:
                     aux_idx.append(k)
                 ins.append([local[('ext', id(a), j)], 0, 0])
             attrs = {k: str(v) for k, v in m.attrs.items()}
@@ -165,15 +146,58 @@ def partition(sym, op_names):
             local[id(m)] = len(sub_nodes) - 1
         graph = {'nodes': sub_nodes, 'arg_nodes': [i for i, d in enumerate(sub_nodes) if d['op'] == 'null'],
                  'heads': [[local[id(m)], j, 0] for m, j in outs], 'attrs': {}}
-        node = _Node('_CachedOp', 'sg_%s_%d' % (groups[gi][0].name, gi),
-                     {'num_inputs': str(len(ext)), 'num_outputs': str(len(outs)),
-                      'aux_indices': ','.join(str(i) for i in aux_idx), 'subgraph': json.dumps(graph)},
-                     [entry(a, j) for a, j in ext])
-        for k, (m, j) in enumerate(outs):
+        descs.append({'ext': ext, 'outs': outs, 'aux': aux_idx, 'graph': graph})
+    return descs
+
+
+def rebuild(sym, order, groups, descs, make_node):
+    """The partitioned Symbol: group ``gi`` becomes ``make_node(gi, desc, input_entries)`` (a new
+    node whose outputs are ``desc['outs']`` in order); every other node is copied."""
+    from .symbol import Symbol, _Node
+    group_of = {id(m): gi for gi, g in enumerate(groups) for m in g}
+    last = {gi: g[-1] for gi, g in enumerate(groups)}
+    remap = {}
+
+    def entry(a, j):
+        r = remap.get((id(a), j))
+        return r if r is not None else (remap.get(('node', id(a)), a), j)
+
+    for n in order:
+        gi = group_of.get(id(n))
+        if gi is None:
+            if n.op is None:
+                continue
+            remap[('node', id(n))] = _Node(n.op, n.name, n.attrs, [entry(a, j) for a, j in n.inputs])
+            continue
+        if last[gi] is not n:
+            continue
+        d = descs[gi]
+        node = make_node(gi, d, [entry(a, j) for a, j in d['ext']])
+        for k, (m, j) in enumerate(d['outs']):
             remap[(id(m), j)] = (node, k)
-        built[gi] = node
     new_outs = [entry(n, j) if n.op is not None else (n, j) for n, j in sym._outputs]
     return Symbol(new_outs)
+
+
+def partition(sym, op_names):
+    """Partition ``sym``: every convex group of nodes whose operator is in ``op_names`` becomes one
+    ``_CachedOp`` node.  Returns a new Symbol (``sym`` is unchanged)."""
+    from .symbol import _Node
+    wanted = {id(registry.get(n)) for n in op_names if registry.has(n)}
+    if not wanted:
+        return sym
+    order = sym._topo()
+    groups = _group_convex(order, lambda n: id(n.opdef()) in wanted)
+    if not groups:
+        return sym
+    descs = describe_groups(sym, order, groups)
+
+    def make(gi, d, inputs):
+        return _Node('_CachedOp', 'sg_%s_%d' % (groups[gi][0].name, gi),
+                     {'num_inputs': str(len(d['ext'])), 'num_outputs': str(len(d['outs'])),
+                      'aux_indices': ','.join(str(i) for i in d['aux']), 'subgraph': json.dumps(d['graph'])},
+                     inputs)
+    return rebuild(sym, order, groups, descs, make)
 
 
 def _aux_positions(order):

@@ -615,9 +615,23 @@ class Symbol:
         return '\n'.join(lines)
 
     def optimize_for(self, backend, args=None, aux=None, ctx=None, **kwargs):
-        """Partition for a subgraph backend whose operator names were registered
-        (MXSetSubgraphPropertyOpNames[V2]); the graph is returned unchanged for unknown backends.
-        ``args`` / ``aux`` (shapes/dtypes source) and options such as ``dedup_subgraph`` are accepted."""
+        """Apply the graph pass or partitioner ``backend`` registered by an extension library
+        (library_graph.py: the library sees the graph, ``args`` / ``aux`` and the options in
+        ``kwargs``; arrays a pass allocates are added to ``args`` / ``aux`` when they are dicts), or
+        partition for a subgraph backend whose operator names were registered
+        (MXSetSubgraphPropertyOpNames[V2]); the graph is returned unchanged for unknown backends."""
+        from .. import library_graph
+        opts = {k: v for k, v in kwargs.items() if k not in ('shape_dict', 'type_dict', 'stype_dict', 'skip_infer')}
+        a = args if isinstance(args, dict) else (dict(zip(self.list_arguments(), args)) if args else None)
+        x = aux if isinstance(aux, dict) else (dict(zip(self.list_auxiliary_states(), aux)) if aux else None)
+        res = library_graph.optimize_for(self, backend, a, x, **opts)
+        if res is not None:
+            sym, new_args, new_aux = res
+            if isinstance(args, dict):
+                args.update({k: v for k, v in new_args.items() if k not in args})
+            if isinstance(aux, dict):
+                aux.update({k: v for k, v in new_aux.items() if k not in aux})
+            return sym
         from . import subgraph
         return subgraph.partition_for_backend(self, backend)
 
