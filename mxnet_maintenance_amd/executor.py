@@ -250,7 +250,7 @@ class GraphProgram:
 
 
 _GRAPH_STREAMS = int(os.environ.get('MXNET_GRAPH_STREAMS', '1') or 1)
-_GRAPH_STREAMS_CAPTURE = os.environ.get('MXNET_GRAPH_STREAMS_CAPTURE', '1') == '1'
+_GRAPH_STREAMS_CAPTURE = os.environ.get('MXNET_GRAPH_STREAMS_CAPTURE', '0') == '1'
 # operators worth a branch of their own on a side stream
 _BRANCH_OPS = frozenset(('Convolution', 'Deconvolution', 'FullyConnected', '_contrib_DeformableConvolution',
                          '_contrib_ModulatedDeformableConvolution', 'Pooling', 'dot', 'batch_dot', '_npi_matmul',

@@ -1013,7 +1013,7 @@ def conv_pw(x, w2, bn_stats=False, addend=None):
         if tuple(addend.shape) != tuple(y.shape) or addend.dtype != y.dtype or addend.data_ptr() % 16:
             raise ValueError('conv_pw: addend must match the output (shape, dtype, 16-byte alignment)')
     lib = _K.lib()
-    grid = lib.conv_pw_stream_grid(M, C, K, _num_cus(x.device))
+    grid = lib.conv_pw_stream_grid(M, C, K, _num_cus(x.device), int(addend is not None))
     part = torch.empty(2 * K * grid, dtype=torch.float32, device=x.device) if bn_stats else None
     lib.conv_pw_stream(_DT[x.dtype], x.data_ptr(), w2.data_ptr(), y.data_ptr(), _zero_page(x.device).data_ptr(), M, C,
                        K, _p(part), grid, _stream(), _p(addend))

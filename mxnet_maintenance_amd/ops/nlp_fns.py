@@ -382,6 +382,7 @@ def _fc_wgrad(dy2, x2, w, w_ref):
 
 
 _COLSUM_PART = {}
+_COLSUM_CNT = {}
 
 
 def bias_grad(dy2, b_ref, bdt):
@@ -392,13 +393,24 @@ def bias_grad(dy2, b_ref, bdt):
         return torch.sum(dy2, 0, dtype=torch.float32).to(bdt)
     lib = _K.lib()
     n = lib.colsum_partials(M, N)
-    part = _COLSUM_PART.get(dy2.device)
+    # scratch per (device, stream): concurrent reductions on different streams must not share it
+    skey = (dy2.device, torch.cuda.current_stream(dy2.device).cuda_stream)
+    part = _COLSUM_PART.get(skey)
     if part is None or part.numel() < n:
-        part = _COLSUM_PART[dy2.device] = torch.empty(n, dtype=torch.float32, device=dy2.device)
+        part = _COLSUM_PART[skey] = torch.empty(n, dtype=torch.float32, device=dy2.device)
     tgt = _leaf_grad(b_ref, N, dtype=bdt) if (bdt in _DT and _FC_DIRECT) else None
     out = tgt if tgt is not None else torch.empty(N, dtype=torch.float32, device=dy2.device)
-    lib.colsum_rows(_DT[dy2.dtype], dy2.data_ptr(), _KF._zeros_f32(N, dy2.device).data_ptr(), part.data_ptr(), M, N,
-                    _DT[out.dtype], out.data_ptr(), int(tgt is not None), _stream())
+    if hasattr(lib, 'colsum_rows_fused'):
+        # one launch: the last block of each column strip finalises it (self-resetting counters)
+        cnt = _COLSUM_CNT.get(skey)
+        strips = lib.colsum_strips(N)
+        if cnt is None or cnt.numel() < strips:
+            cnt = _COLSUM_CNT[skey] = torch.zeros(max(strips, 64), dtype=torch.int32, device=dy2.device)
+        lib.colsum_rows_fused(_DT[dy2.dtype], dy2.data_ptr(), part.data_ptr(), cnt.data_ptr(), M, N, _DT[out.dtype],
+                              out.data_ptr(), int(tgt is not None), _stream())
+    else:
+        lib.colsum_rows(_DT[dy2.dtype], dy2.data_ptr(), _KF._zeros_f32(N, dy2.device).data_ptr(), part.data_ptr(),
+                        M, N, _DT[out.dtype], out.data_ptr(), int(tgt is not None), _stream())
     if tgt is not None:
         return None
     return out.to(bdt)

@@ -51,6 +51,9 @@ void softmax_ce_backward(int dtype, int label_is_int, const void* logits, const 
                          const float* gout, void* dlogits, int N, int K, hipStream_t s);
 void gap_nhwc_forward(int dtype, const void* x, void* y, int N, int HW, int C, hipStream_t s);
 void relu_forward(int dtype, const void* x, void* y, int64_t n, hipStream_t s);
+int colsum_strips(int C);
+void colsum_rows_fused(int dtype, const void* x, float* part, unsigned* counters, int64_t R, int C, int out_dtype,
+                       void* out, int accum, hipStream_t s);
 void relu_backward(int dtype, const void* y, const void* dy, void* dx, int64_t n, hipStream_t s);
 void pointwise_binary(int dtype, int op, const void* a, const void* b, void* out, int64_t n, int mode, int64_t row,
                       int ndim, const int64_t* shape, const int64_t* astride, const int64_t* bstride, hipStream_t s);
@@ -150,7 +153,7 @@ void twobit_quantize(int dtype, const void* g, float* res, void* packed, int64_t
 void twobit_dequantize_sum(const void* packed, int64_t row_bytes, int nrows, int64_t n, float thr, float* out,
                            hipStream_t s);
 int conv_pw_stream_ok(int kin, int nout);
-int conv_pw_stream_grid(int M, int kin, int nout, int ncu);
+int conv_pw_stream_grid(int M, int kin, int nout, int ncu, int add);
 void conv_pw_stream(int dtype, const void* x, const void* w, void* y, const void* zero, int M, int kin, int nout,
                     float* part, int grid, hipStream_t s, const void* addend);
 void conv_gen(int dtype, int mode, const void* src, const void* wsrc, const float* bias, void* dst, const int* geom,
@@ -240,7 +243,9 @@ PYBIND11_MODULE(_hip_kernels, m) {
   });
   // streaming 1x1 convolution for small reductions (src/kernels/conv_pw.hip)
   m.def("conv_pw_stream_ok", &conv_pw_stream_ok);
-  m.def("conv_pw_stream_grid", &conv_pw_stream_grid);
+  m.def("conv_pw_stream_grid", [](int M, int kin, int nout, int ncu, int add) {
+    return conv_pw_stream_grid(M, kin, nout, ncu, add);
+  }, pybind11::arg("M"), pybind11::arg("kin"), pybind11::arg("nout"), pybind11::arg("ncu"), pybind11::arg("add") = 0);
   m.def("conv_pw_stream", [](int dt, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t zero, int M, int kin, int nout,
                              uintptr_t part, int grid, uintptr_t s, uintptr_t addend) {
     conv_pw_stream(dt, P<const void>(x), P<const void>(w), P<void>(y), P<const void>(zero), M, kin, nout,
@@ -366,6 +371,12 @@ PYBIND11_MODULE(_hip_kernels, m) {
     softmax_ce_backward(dt, li, P<void>(logits), P<void>(label), P<float>(lse), P<float>(gout), P<void>(dlogits), N,
                         K, S(s));
     check_launch("softmax_ce_backward");
+  });
+  m.def("colsum_strips", &colsum_strips);
+  m.def("colsum_rows_fused", [](int dt, uintptr_t x, uintptr_t part, uintptr_t counters, int64_t R, int C, int odt,
+                                uintptr_t out, int accum, uintptr_t s) {
+    colsum_rows_fused(dt, P<void>(x), P<float>(part), P<unsigned>(counters), R, C, odt, P<void>(out), accum, S(s));
+    check_launch("colsum_rows_fused");
   });
   m.def("relu_forward", [](int dt, uintptr_t x, uintptr_t y, int64_t n, uintptr_t s) {
     relu_forward(dt, P<void>(x), P<void>(y), n, S(s));

@@ -76,32 +76,50 @@ __device__ __forceinline__ void vm_wait() {
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int KIN, int NOUT>
+// pixels per tile: the input stage at most 16 KB and the epilogue image at most 32 KB; with an
+// addend, at most 32 pixels (its LDS stage is as large as the image) but whole 8 KB LDS-DMA rounds
+// for both the input and the addend stage
+constexpr int pw_bm(int kin, int nout, bool add) {
+  const int bm0 = (16384 / nout) < (8192 / kin) ? (16384 / nout) : (8192 / kin);
+  if (!add) return bm0;
+  int bm = bm0 < 32 ? bm0 : 32;
+  if (bm < 4096 / nout) bm = 4096 / nout;
+  if (bm < 4096 / kin) bm = 4096 / kin;
+  return bm;
+}
+
+template <int KIN, int NOUT, int WPC = 2, bool ADD = false>
 struct PwCfg {
-  // pixels per tile: the input stage at most 16 KB and the epilogue image at most 32 KB
-  static constexpr int BM = (16384 / NOUT) < (8192 / KIN) ? (16384 / NOUT) : (8192 / KIN);
+  static constexpr int BM = pw_bm(KIN, NOUT, ADD);
   static constexpr int WC = NOUT / 16 < 8 ? NOUT / 16 : 8;  // waves along output channels
   static constexpr int WP = 8 / WC;                        // waves along pixels
   static constexpr int FC = NOUT / WC / 16;                // channel fragments per wave
   static constexpr int FP = BM / WP / 16;                  // pixel fragments per wave
   static constexpr int KS = KIN / 32;                      // MFMA k-steps
   static constexpr int ROWB = KIN * 2;                     // input row bytes
-  static constexpr int STAGE = BM * ROWB;                  // one input tile
-  static constexpr int LPT = STAGE / (512 * 16);           // LDS-DMA instructions per thread per tile
+  static constexpr int STAGE_IN = BM * ROWB;               // one input tile
+  static constexpr int STAGE_ADD = ADD ? BM * NOUT * 2 : 0;  // its addend rows (linear)
+  static constexpr int STAGE = STAGE_IN + STAGE_ADD;
+  static constexpr int LPT = STAGE_IN / (512 * 16);        // LDS-DMA instructions per thread per tile
+  static constexpr int APT = STAGE_ADD / (512 * 16);       // ... for the addend
   static constexpr int PITCH = NOUT * 2 + 16;              // epilogue image row pitch
   static constexpr int EPI = BM * PITCH;
   static constexpr int OCH = NOUT / 8;                     // 16-byte chunks per output row
   static constexpr int SPT = (BM * OCH + 511) / 512;       // 16-byte stores per thread per tile (uniform)
-  // deepest ring that keeps two workgroups per CU (<= 80 KB each)
-  static constexpr int NST = (4 * STAGE + EPI <= 80 * 1024) ? 4 : ((3 * STAGE + EPI <= 80 * 1024) ? 3 : 2);
+  // deepest ring (<= 4 stages) that keeps WPC workgroups per CU in the 160 KB of LDS
+  static constexpr int LDS = WPC == 1 ? 156 * 1024 : 80 * 1024;
+  static constexpr int NST = (4 * STAGE + EPI <= LDS) ? 4 : ((3 * STAGE + EPI <= LDS) ? 3 : 2);
   static constexpr int D = NST - 1;
   static constexpr int SMEM = NST * STAGE + EPI;
   static_assert(FC >= 1 && FP >= 1, "at least one fragment pair per wave");
-  static_assert(LPT >= 1 && STAGE % (512 * 16) == 0, "whole LDS-DMA instructions per tile");
+  static_assert(LPT >= 1 && STAGE_IN % (512 * 16) == 0, "whole LDS-DMA instructions per tile");
+  static_assert(!ADD || (APT >= 1 && STAGE_ADD % (512 * 16) == 0), "whole LDS-DMA instructions per addend tile");
+  static_assert(!ADD || WPC == 1, "the addend stage needs the LDS of a whole CU");
   static_assert((BM * OCH) % 512 == 0 || BM * OCH < 512, "whole store rounds, or a single partial one");
   static_assert(512 % OCH == 0, "a thread keeps one output chunk");
-  static_assert(D * (LPT + SPT) < 64, "vmcnt range");
-  static_assert(FC * KS * 4 <= 64, "resident weights exceed the register budget");
+  static_assert(D * (LPT + APT + SPT) < 64, "vmcnt range");
+  // resident weights: a quarter of the VGPR budget (128 at 2 workgroups per CU, 256 at 1)
+  static_assert(FC * KS * 4 <= (WPC == 1 ? 128 : 64), "resident weights exceed the register budget");
   static_assert(ROWB % 128 == 0, "rows of whole 128-byte swizzle groups");
 };
 
@@ -122,11 +140,11 @@ __device__ __forceinline__ void vm_wait_le(int n) {
   else vm_wait<0>();
 }
 
-template <typename T, int KIN, int NOUT, bool STATS, bool ADD>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) conv_pw_stream_kernel(
+template <typename T, int KIN, int NOUT, bool STATS, bool ADD, int WPC>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WPC))) conv_pw_stream_kernel(
     const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y, const T* __restrict__ zero, int M, int ntiles,
     float* __restrict__ part, const T* __restrict__ addend) {
-  using C = PwCfg<KIN, NOUT>;
+  using C = PwCfg<KIN, NOUT, WPC, ADD>;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -170,29 +188,20 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) c
       const T* src = p < M ? x + static_cast<int64_t>(p) * KIN + chunk * 8 : zero + (chunk & 7) * 8;
       __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sb + (i * 8 + wid) * 1024), 16, 0, 0);
     }
+    // the tile's addend rows, linear after the input (rows past M read the zero page)
+#pragma unroll
+    for (int i = 0; i < C::APT; ++i) {
+      const int byte = ((i * 8 + wid) * 64 + lane) * 16;
+      const int row = byte / (NOUT * 2);
+      const int p = t * C::BM + row;
+      const T* src = p < M ? addend + static_cast<int64_t>(p) * NOUT + (byte % (NOUT * 2)) / 2 : zero;
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sb + C::STAGE_IN + (i * 8 + wid) * 1024), 16,
+                                       0, 0);
+    }
   };
 
   const int my_tiles = wg < ntiles ? (ntiles - wg + grid - 1) / grid : 0;
   for (int j = 0; j < C::D && j < my_tiles; ++j) issue(wg + j * grid, j);
-
-  // ---- addend chunks of tile `t` (same chunk mapping as the store loop; dead chunks read an
-  // out-of-range offset, so every lane issues exactly SPT loads)
-  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<T*>(ADD ? addend : y), 0, static_cast<int>(static_cast<uint32_t>(M) * NOUT * sizeof(T)), 0x00020000);
-  u32x4 addv[ADD ? C::SPT : 1];
-  auto load_add = [&](int t) {
-#pragma unroll
-    for (int k = 0; k < C::SPT; ++k) {
-      const int e = tid + k * 512;
-      const bool in_tile = e < C::BM * C::OCH;
-      const int pix = in_tile ? e / C::OCH : 0;
-      const int p = t * C::BM + pix;
-      const uint32_t off = (in_tile && p < M) ? (static_cast<uint32_t>(p) * NOUT + (e % C::OCH) * 8) * sizeof(T)
-                                              : 0xFFFFFFF0u;
-      addv[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ars, off, 0, 0));
-    }
-  };
-  if (ADD && my_tiles > 0) load_add(wg);
 
   float s1[8], s2[8];
 #pragma unroll
@@ -206,20 +215,28 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) c
   for (int it = 0; it < my_tiles; ++it) {
     const int t = wg + it * grid;
     const int st = it % C::NST;
-    // issue tile it+D (into the stage freed by tile it-1, whose reads ended before the last barrier)
-    if (it + C::D < my_tiles) issue(wg + (it + C::D) * grid, (it + C::D) % C::NST);
-    // VM ops younger than tile it's DMA: the tiles issued after it, and the epilogue stores of the
-    // iterations run since it was issued (tile j < D came from the prologue, tile j >= D from
-    // iteration j - D)
-    // (with ADD, also the addend loads of tiles it-D+1 .. it, issued after tile it's DMA)
-    {
+    if (!ADD) {
+      // issue tile it+D (into the stage freed by tile it-1, whose reads ended before the last barrier)
+      if (it + C::D < my_tiles) issue(wg + (it + C::D) * grid, (it + C::D) % C::NST);
+      // VM ops younger than tile it's DMA: the tiles issued after it, and the epilogue stores of the
+      // iterations run since it was issued (tile j < D came from the prologue, tile j >= D from
+      // iteration j - D)
       const int later = (my_tiles - 1 - it) < C::D ? (my_tiles - 1 - it) : C::D;
       const int epis = it < C::D ? it : C::D;
-      const int adds = ADD ? (it + 1 < C::D ? it + 1 : C::D) : 0;
-      if (later == C::D && epis == C::D) vm_wait<C::D*(C::LPT + (ADD ? 2 : 1) * C::SPT)>();
-      else vm_wait_le(later * C::LPT + (epis + adds) * C::SPT);
+      if (later == C::D && epis == C::D) vm_wait<C::D*(C::LPT + C::SPT)>();
+      else vm_wait_le(later * C::LPT + epis * C::SPT);
+      lds_barrier();
+    } else {
+      // the store loop reads the addend part of a stage, so tile it+D (into tile it-1's stage) is
+      // issued only after the barrier every thread reaches once its stores of tile it-1 are out:
+      // younger than tile it's DMA are tiles it+1 .. it+D-1 and the stores of the iterations since
+      const int later = (my_tiles - 1 - it) < C::D - 1 ? (my_tiles - 1 - it) : C::D - 1;
+      const int epis = it < C::D ? it : C::D;
+      if (later == C::D - 1 && epis == C::D) vm_wait<(C::D - 1) * (C::LPT + C::APT) + C::D * C::SPT>();
+      else vm_wait_le(later * (C::LPT + C::APT) + epis * C::SPT);
+      lds_barrier();
+      if (it + C::D < my_tiles) issue(wg + (it + C::D) * grid, (it + C::D) % C::NST);
     }
-    lds_barrier();
 
     // ---- MFMA: C[co][pix] over the tile
     const char* sb = smem + st * C::STAGE;
@@ -253,8 +270,6 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) c
         *reinterpret_cast<uint2*>(epi + pix * C::PITCH + co * 2) = PwM<T>::pack4(v[0], v[1], v[2], v[3]);
       }
     lds_barrier();
-    // the addend of this tile has landed once at most tile it+D's DMA (issued after it) is pending
-    if (ADD) vm_wait_le(it + C::D < my_tiles ? C::LPT : 0);
     // ---- coalesced row stores (exactly SPT per thread: rows past M go out of range by buffer bounds)
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
         y, 0, static_cast<int>(static_cast<uint32_t>(M) * NOUT * sizeof(T)), 0x00020000);
@@ -271,7 +286,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) c
       v.raw = *reinterpret_cast<const uint4*>(epi + pix * C::PITCH + c8 * 16);
       if (ADD) {
         Vec8<T> a;
-        a.raw = __builtin_bit_cast(uint4, addv[k]);
+        a.raw = *reinterpret_cast<const uint4*>(sb + C::STAGE_IN + pix * (NOUT * 2) + c8 * 16);
 #pragma unroll
         for (int q = 0; q < 8; ++q) v.set(q, v.get(q) + a.get(q));
       }
@@ -288,7 +303,6 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) c
       }
     }
     (void)my_c8;
-    if (ADD && it + 1 < my_tiles) load_add(t + grid);
   }
   if (STATS) {
     // every thread's chunk is fixed (tid % OCH): combine the 512/OCH threads of each chunk through
@@ -313,48 +327,50 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) c
   }
 }
 
-template <typename T, int KIN, int NOUT, bool STATS, bool ADD>
+template <typename T, int KIN, int NOUT, int WPC, bool STATS, bool ADD>
 void launch_pw_v(const void* x, const void* w, void* y, const void* zero, int M, float* part, const void* addend,
                  int grid, hipStream_t s) {
-  using C = PwCfg<KIN, NOUT>;
+  using C = PwCfg<KIN, NOUT, WPC, ADD>;
   static bool set = false;
   if (!set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD, WPC>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
     set = true;
   }
   const int ntiles = (M + C::BM - 1) / C::BM;
-  hipLaunchKernelGGL((conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD>), dim3(grid), dim3(512), C::SMEM, s,
+  hipLaunchKernelGGL((conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD, WPC>), dim3(grid), dim3(512), C::SMEM, s,
                      static_cast<const T*>(x), static_cast<const T*>(w), static_cast<T*>(y),
                      static_cast<const T*>(zero), M, ntiles, part, static_cast<const T*>(addend));
 }
 
-template <typename T, int KIN, int NOUT>
+template <typename T, int KIN, int NOUT, int WPC>
 void launch_pw(const void* x, const void* w, void* y, const void* zero, int M, float* part, const void* addend,
                int grid, hipStream_t s) {
-  using C = PwCfg<KIN, NOUT>;
-  static_assert(C::SMEM <= 80 * 1024, "two workgroups per CU");
-  static_assert(C::NST >= 2, "ring depth");
-  static_assert(C::D * (C::LPT + 2 * C::SPT) < 64, "vmcnt range with the addend loads");
+  using C = PwCfg<KIN, NOUT, WPC>;
+  using CA = PwCfg<KIN, NOUT, 1, true>;
+  static_assert(C::SMEM <= C::LDS && CA::SMEM <= CA::LDS, "workgroups per CU");
+  static_assert(C::NST >= 2 && CA::NST >= 2, "ring depth");
   if (part) {
-    if (addend) launch_pw_v<T, KIN, NOUT, true, true>(x, w, y, zero, M, part, addend, grid, s);
-    else launch_pw_v<T, KIN, NOUT, true, false>(x, w, y, zero, M, part, addend, grid, s);
+    if (addend) launch_pw_v<T, KIN, NOUT, 1, true, true>(x, w, y, zero, M, part, addend, grid, s);
+    else launch_pw_v<T, KIN, NOUT, WPC, true, false>(x, w, y, zero, M, part, addend, grid, s);
   } else {
-    if (addend) launch_pw_v<T, KIN, NOUT, false, true>(x, w, y, zero, M, part, addend, grid, s);
-    else launch_pw_v<T, KIN, NOUT, false, false>(x, w, y, zero, M, part, addend, grid, s);
+    if (addend) launch_pw_v<T, KIN, NOUT, 1, false, true>(x, w, y, zero, M, part, addend, grid, s);
+    else launch_pw_v<T, KIN, NOUT, WPC, false, false>(x, w, y, zero, M, part, addend, grid, s);
   }
 }
 
-// (Cin, Cout) pairs built: the resident weights of (128, 512) and (256, 256) spill at 128 VGPRs
-#define MXAMD_PW_SHAPES(X) \
-  X(64, 64) X(64, 128) X(64, 256) X(128, 128) X(128, 256) X(256, 64) X(256, 128) X(512, 128)
+// (Cin, Cout, workgroups per CU) built: weight matrices up to 32K elements stay resident at two
+// workgroups per CU (128 VGPRs); up to 128K elements at one workgroup per CU (256 VGPRs)
+#define MXAMD_PW_SHAPES(X)                                                                          \
+  X(64, 64, 2) X(64, 128, 2) X(64, 256, 2) X(128, 128, 2) X(128, 256, 2) X(256, 64, 2) X(256, 128, 2) \
+  X(512, 128, 2) X(128, 512, 1) X(256, 512, 1) X(512, 256, 1)
 
 template <typename T>
 bool dispatch_pw(int kin, int nout, const void* x, const void* w, void* y, const void* zero, int M, float* part,
                  const void* addend, int grid, hipStream_t s) {
-#define MXAMD_PW_CASE(K, N)                                        \
+#define MXAMD_PW_CASE(K, N, W)                                     \
   if (kin == K && nout == N) {                                     \
-    launch_pw<T, K, N>(x, w, y, zero, M, part, addend, grid, s);   \
+    launch_pw<T, K, N, W>(x, w, y, zero, M, part, addend, grid, s); \
     return true;                                                   \
   }
   MXAMD_PW_SHAPES(MXAMD_PW_CASE)
@@ -364,20 +380,21 @@ bool dispatch_pw(int kin, int nout, const void* x, const void* w, void* y, const
 
 }  // namespace
 
-// 1 when conv_pw_stream handles a 1x1 stride-1 NHWC conv with Cin = kin, Cout = nout.
+// Workgroups per CU (> 0) when conv_pw_stream handles a 1x1 stride-1 NHWC conv with Cin = kin,
+// Cout = nout; 0 otherwise.
 int conv_pw_stream_ok(int kin, int nout) {
-#define MXAMD_PW_OK(K, N) \
-  if (kin == K && nout == N) return 1;
+#define MXAMD_PW_OK(K, N, W) \
+  if (kin == K && nout == N) return W;
   MXAMD_PW_SHAPES(MXAMD_PW_OK)
 #undef MXAMD_PW_OK
   return 0;
 }
 
 // Workgroups the kernel launches (= BatchNorm partials per channel when statistics are requested).
-int conv_pw_stream_grid(int M, int kin, int nout, int ncu) {
-  const int bm = (16384 / nout) < (8192 / kin) ? (16384 / nout) : (8192 / kin);
+int conv_pw_stream_grid(int M, int kin, int nout, int ncu, int add) {
+  const int bm = pw_bm(kin, nout, add != 0);
   const int ntiles = (M + bm - 1) / bm;
-  const int g = 2 * ncu;
+  const int g = (add ? 1 : conv_pw_stream_ok(kin, nout)) * ncu;   // workgroups per CU x CUs
   return ntiles < g ? ntiles : g;
 }
 
