@@ -1014,11 +1014,13 @@ def conv_pw(x, w2, bn_stats=False, addend=None):
             raise ValueError('conv_pw: addend must match the output (shape, dtype, 16-byte alignment)')
     lib = _K.lib()
     grid = lib.conv_pw_stream_grid(M, C, K, _num_cus(x.device), int(addend is not None))
-    part = torch.empty(2 * K * grid, dtype=torch.float32, device=x.device) if bn_stats else None
+    # BatchNorm partials: one per tile walker of a Cout slice (grid / slices per channel)
+    nparts = grid // max(1, lib.conv_pw_stream_slices(C, K))
+    part = torch.empty(2 * K * nparts, dtype=torch.float32, device=x.device) if bn_stats else None
     lib.conv_pw_stream(_DT[x.dtype], x.data_ptr(), w2.data_ptr(), y.data_ptr(), _zero_page(x.device).data_ptr(), M, C,
                        K, _p(part), grid, _stream(), _p(addend))
     if part is not None:
-        y._mxamd_bn_part = (part, grid)
+        y._mxamd_bn_part = (part, nparts)
     return y
 
 

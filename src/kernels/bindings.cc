@@ -154,6 +154,7 @@ void twobit_dequantize_sum(const void* packed, int64_t row_bytes, int nrows, int
                            hipStream_t s);
 int conv_pw_stream_ok(int kin, int nout);
 int conv_pw_stream_grid(int M, int kin, int nout, int ncu, int add);
+int conv_pw_stream_slices(int kin, int nout);
 void conv_pw_stream(int dtype, const void* x, const void* w, void* y, const void* zero, int M, int kin, int nout,
                     float* part, int grid, hipStream_t s, const void* addend);
 void conv_gen(int dtype, int mode, const void* src, const void* wsrc, const float* bias, void* dst, const int* geom,
@@ -243,6 +244,7 @@ PYBIND11_MODULE(_hip_kernels, m) {
   });
   // streaming 1x1 convolution for small reductions (src/kernels/conv_pw.hip)
   m.def("conv_pw_stream_ok", &conv_pw_stream_ok);
+  m.def("conv_pw_stream_slices", &conv_pw_stream_slices);
   m.def("conv_pw_stream_grid", [](int M, int kin, int nout, int ncu, int add) {
     return conv_pw_stream_grid(M, kin, nout, ncu, add);
   }, pybind11::arg("M"), pybind11::arg("kin"), pybind11::arg("nout"), pybind11::arg("ncu"), pybind11::arg("add") = 0);

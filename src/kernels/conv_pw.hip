@@ -79,10 +79,13 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // pixels per tile: the input stage at most 16 KB and the epilogue image at most 32 KB; with an
 // addend, at most 32 pixels (its LDS stage is as large as the image) but whole 8 KB LDS-DMA rounds
 // for both the input and the addend stage
+// (nout = the output channels one workgroup computes: a slice of the layer's when it is sliced)
 constexpr int pw_bm(int kin, int nout, bool add) {
-  const int bm0 = (16384 / nout) < (8192 / kin) ? (16384 / nout) : (8192 / kin);
+  const int in_rows = (8192 / kin) > 16 ? (8192 / kin) : 16;    // Cin >= 1024: 16 rows of up to 32 KB
+  const int bm0 = (16384 / nout) < in_rows ? (16384 / nout) : in_rows;
   if (!add) return bm0;
   int bm = bm0 < 32 ? bm0 : 32;
+  if (bm > 8192 / nout) bm = 8192 / nout;                         // addend stage <= 16 KB
   if (bm < 4096 / nout) bm = 4096 / nout;
   if (bm < 4096 / kin) bm = 4096 / kin;
   return bm;
@@ -140,7 +143,9 @@ __device__ __forceinline__ void vm_wait_le(int n) {
   else vm_wait<0>();
 }
 
-template <typename T, int KIN, int NOUT, bool STATS, bool ADD, int WPC>
+// NOUT: output channels per workgroup; S: slices of the layer's NOUT * S output channels (the
+// workgroups of one tile's slices are adjacent in the XCD-aware order, so they share its input in L2)
+template <typename T, int KIN, int NOUT, bool STATS, bool ADD, int WPC, int S>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WPC))) conv_pw_stream_kernel(
     const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y, const T* __restrict__ zero, int M, int ntiles,
     float* __restrict__ part, const T* __restrict__ addend) {
@@ -154,7 +159,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
   // XCD-aware: workgroups sharing an XCD take consecutive tiles
   const int xcd = blockIdx.x & 7;
   const int q8 = grid >> 3, r8 = grid & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  const int wg0 = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  constexpr int NT = NOUT * S;             // the layer's output channels (row stride of y / addend)
+  const int slice = S > 1 ? wg0 % S : 0;
+  const int wg = S > 1 ? wg0 / S : wg0;    // tile walker within the slice
+  const int gs = grid / S;                 // tile walkers per slice (the grid is a multiple of S)
 
   // ---- resident weights: A fragments of this wave's channels, all k-steps
   u32x4 wa[C::FC][C::KS];
@@ -162,7 +171,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
   for (int f = 0; f < C::FC; ++f)
 #pragma unroll
     for (int s = 0; s < C::KS; ++s) {
-      const int co = wc * C::FC * 16 + f * 16 + (lane & 15);
+      const int co = slice * NOUT + wc * C::FC * 16 + f * 16 + (lane & 15);
       wa[f][s] = *reinterpret_cast<const u32x4*>(w + static_cast<int64_t>(co) * KIN + s * 32 + (lane >> 4) * 8);
     }
 
@@ -194,14 +203,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
       const int byte = ((i * 8 + wid) * 64 + lane) * 16;
       const int row = byte / (NOUT * 2);
       const int p = t * C::BM + row;
-      const T* src = p < M ? addend + static_cast<int64_t>(p) * NOUT + (byte % (NOUT * 2)) / 2 : zero;
+      const T* src = p < M ? addend + static_cast<int64_t>(p) * NT + slice * NOUT + (byte % (NOUT * 2)) / 2 : zero;
       __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sb + C::STAGE_IN + (i * 8 + wid) * 1024), 16,
                                        0, 0);
     }
   };
 
-  const int my_tiles = wg < ntiles ? (ntiles - wg + grid - 1) / grid : 0;
-  for (int j = 0; j < C::D && j < my_tiles; ++j) issue(wg + j * grid, j);
+  const int my_tiles = wg < ntiles ? (ntiles - wg + gs - 1) / gs : 0;
+  for (int j = 0; j < C::D && j < my_tiles; ++j) issue(wg + j * gs, j);
 
   float s1[8], s2[8];
 #pragma unroll
@@ -213,11 +222,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
   char* epi = smem + C::NST * C::STAGE;
 
   for (int it = 0; it < my_tiles; ++it) {
-    const int t = wg + it * grid;
+    const int t = wg + it * gs;
     const int st = it % C::NST;
     if (!ADD) {
       // issue tile it+D (into the stage freed by tile it-1, whose reads ended before the last barrier)
-      if (it + C::D < my_tiles) issue(wg + (it + C::D) * grid, (it + C::D) % C::NST);
+      if (it + C::D < my_tiles) issue(wg + (it + C::D) * gs, (it + C::D) % C::NST);
       // VM ops younger than tile it's DMA: the tiles issued after it, and the epilogue stores of the
       // iterations run since it was issued (tile j < D came from the prologue, tile j >= D from
       // iteration j - D)
@@ -235,7 +244,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
       if (later == C::D - 1 && epis == C::D) vm_wait<(C::D - 1) * (C::LPT + C::APT) + C::D * C::SPT>();
       else vm_wait_le(later * (C::LPT + C::APT) + epis * C::SPT);
       lds_barrier();
-      if (it + C::D < my_tiles) issue(wg + (it + C::D) * grid, (it + C::D) % C::NST);
+      if (it + C::D < my_tiles) issue(wg + (it + C::D) * gs, (it + C::D) % C::NST);
     }
 
     // ---- MFMA: C[co][pix] over the tile
@@ -272,7 +281,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
     lds_barrier();
     // ---- coalesced row stores (exactly SPT per thread: rows past M go out of range by buffer bounds)
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
-        y, 0, static_cast<int>(static_cast<uint32_t>(M) * NOUT * sizeof(T)), 0x00020000);
+        y, 0, static_cast<int>(static_cast<uint32_t>(M) * NT * sizeof(T)), 0x00020000);
 #pragma unroll
     for (int k = 0; k < C::SPT; ++k) {
       // every lane issues the store (uniform VM-op count per wave for the counted waits): chunks past
@@ -291,7 +300,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
         for (int q = 0; q < 8; ++q) v.set(q, v.get(q) + a.get(q));
       }
       const bool live = in_tile && p < M;
-      const uint32_t off = live ? (static_cast<uint32_t>(p) * NOUT + c8 * 8) * sizeof(T) : 0xFFFFFFF0u;
+      const uint32_t off = live ? (static_cast<uint32_t>(p) * NT + slice * NOUT + c8 * 8) * sizeof(T) : 0xFFFFFFF0u;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v.raw), yrs, off, 0, 0);
       if (STATS && live) {
 #pragma unroll
@@ -322,28 +331,28 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
       const float* col = red + which * ROWS * NOUT + ch;
       float a = 0.f;
       for (int r = 0; r < ROWS; ++r) a += col[r * NOUT];
-      part[static_cast<int64_t>(which) * NOUT * grid + static_cast<int64_t>(ch) * grid + wg] = a;
+      part[static_cast<int64_t>(which) * NT * gs + static_cast<int64_t>(slice * NOUT + ch) * gs + wg] = a;
     }
   }
 }
 
-template <typename T, int KIN, int NOUT, int WPC, bool STATS, bool ADD>
+template <typename T, int KIN, int NOUT, int WPC, int S, bool STATS, bool ADD>
 void launch_pw_v(const void* x, const void* w, void* y, const void* zero, int M, float* part, const void* addend,
                  int grid, hipStream_t s) {
   using C = PwCfg<KIN, NOUT, WPC, ADD>;
   static bool set = false;
   if (!set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD, WPC>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD, WPC, S>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
     set = true;
   }
   const int ntiles = (M + C::BM - 1) / C::BM;
-  hipLaunchKernelGGL((conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD, WPC>), dim3(grid), dim3(512), C::SMEM, s,
+  hipLaunchKernelGGL((conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD, WPC, S>), dim3(grid), dim3(512), C::SMEM, s,
                      static_cast<const T*>(x), static_cast<const T*>(w), static_cast<T*>(y),
                      static_cast<const T*>(zero), M, ntiles, part, static_cast<const T*>(addend));
 }
 
-template <typename T, int KIN, int NOUT, int WPC>
+template <typename T, int KIN, int NOUT, int WPC, int S>
 void launch_pw(const void* x, const void* w, void* y, const void* zero, int M, float* part, const void* addend,
                int grid, hipStream_t s) {
   using C = PwCfg<KIN, NOUT, WPC>;
@@ -351,27 +360,29 @@ void launch_pw(const void* x, const void* w, void* y, const void* zero, int M, f
   static_assert(C::SMEM <= C::LDS && CA::SMEM <= CA::LDS, "workgroups per CU");
   static_assert(C::NST >= 2 && CA::NST >= 2, "ring depth");
   if (part) {
-    if (addend) launch_pw_v<T, KIN, NOUT, 1, true, true>(x, w, y, zero, M, part, addend, grid, s);
-    else launch_pw_v<T, KIN, NOUT, WPC, true, false>(x, w, y, zero, M, part, addend, grid, s);
+    if (addend) launch_pw_v<T, KIN, NOUT, 1, S, true, true>(x, w, y, zero, M, part, addend, grid, s);
+    else launch_pw_v<T, KIN, NOUT, WPC, S, true, false>(x, w, y, zero, M, part, addend, grid, s);
   } else {
-    if (addend) launch_pw_v<T, KIN, NOUT, 1, false, true>(x, w, y, zero, M, part, addend, grid, s);
-    else launch_pw_v<T, KIN, NOUT, WPC, false, false>(x, w, y, zero, M, part, addend, grid, s);
+    if (addend) launch_pw_v<T, KIN, NOUT, 1, S, false, true>(x, w, y, zero, M, part, addend, grid, s);
+    else launch_pw_v<T, KIN, NOUT, WPC, S, false, false>(x, w, y, zero, M, part, addend, grid, s);
   }
 }
 
-// (Cin, Cout, workgroups per CU) built: weight matrices up to 32K elements stay resident at two
-// workgroups per CU (128 VGPRs); up to 128K elements at one workgroup per CU (256 VGPRs)
-#define MXAMD_PW_SHAPES(X)                                                                          \
-  X(64, 64, 2) X(64, 128, 2) X(64, 256, 2) X(128, 128, 2) X(128, 256, 2) X(256, 64, 2) X(256, 128, 2) \
-  X(512, 128, 2) X(128, 512, 1) X(256, 512, 1) X(512, 256, 1)
+// (Cin, Cout per workgroup, workgroups per CU, slices) built: weight matrices up to 32K elements stay
+// resident at two workgroups per CU (128 VGPRs), up to 128K elements at one workgroup per CU; larger
+// layers are sliced along Cout (Cout = Cout per workgroup x slices)
+#define MXAMD_PW_SHAPES(X)                                                                                  \
+  X(64, 64, 2, 1) X(64, 128, 2, 1) X(64, 256, 2, 1) X(128, 128, 2, 1) X(128, 256, 2, 1) X(256, 64, 2, 1)     \
+  X(256, 128, 2, 1) X(512, 128, 2, 1) X(128, 512, 1, 1) X(256, 512, 1, 1) X(512, 256, 1, 1) X(256, 512, 1, 2) \
+  X(1024, 128, 1, 2) X(512, 256, 1, 8)
 
 template <typename T>
 bool dispatch_pw(int kin, int nout, const void* x, const void* w, void* y, const void* zero, int M, float* part,
                  const void* addend, int grid, hipStream_t s) {
-#define MXAMD_PW_CASE(K, N, W)                                     \
-  if (kin == K && nout == N) {                                     \
-    launch_pw<T, K, N, W>(x, w, y, zero, M, part, addend, grid, s); \
-    return true;                                                   \
+#define MXAMD_PW_CASE(K, N, W, SL)                                        \
+  if (kin == K && nout == N * SL) {                                       \
+    launch_pw<T, K, N, W, SL>(x, w, y, zero, M, part, addend, grid, s);   \
+    return true;                                                          \
   }
   MXAMD_PW_SHAPES(MXAMD_PW_CASE)
 #undef MXAMD_PW_CASE
@@ -383,25 +394,39 @@ bool dispatch_pw(int kin, int nout, const void* x, const void* w, void* y, const
 // Workgroups per CU (> 0) when conv_pw_stream handles a 1x1 stride-1 NHWC conv with Cin = kin,
 // Cout = nout; 0 otherwise.
 int conv_pw_stream_ok(int kin, int nout) {
-#define MXAMD_PW_OK(K, N, W) \
-  if (kin == K && nout == N) return W;
+#define MXAMD_PW_OK(K, N, W, SL) \
+  if (kin == K && nout == N * SL) return W;
   MXAMD_PW_SHAPES(MXAMD_PW_OK)
 #undef MXAMD_PW_OK
   return 0;
 }
 
 // Workgroups the kernel launches (= BatchNorm partials per channel when statistics are requested).
+// Cout slices of a (Cin, Cout) layer (1 when not sliced, 0 when not built).
+int conv_pw_stream_slices(int kin, int nout) {
+#define MXAMD_PW_SL(K, N, W, SL) \
+  if (kin == K && nout == N * SL) return SL;
+  MXAMD_PW_SHAPES(MXAMD_PW_SL)
+#undef MXAMD_PW_SL
+  return 0;
+}
+
 int conv_pw_stream_grid(int M, int kin, int nout, int ncu, int add) {
-  const int bm = pw_bm(kin, nout, add != 0);
+  const int sl = conv_pw_stream_slices(kin, nout);
+  if (sl == 0) return 0;
+  const int bm = pw_bm(kin, nout / sl, add != 0);
   const int ntiles = (M + bm - 1) / bm;
-  const int g = (add ? 1 : conv_pw_stream_ok(kin, nout)) * ncu;   // workgroups per CU x CUs
-  return ntiles < g ? ntiles : g;
+  const int wpc = add ? 1 : conv_pw_stream_ok(kin, nout);
+  int per = (wpc * ncu + sl - 1) / sl;                 // tile walkers per slice
+  if (per > ntiles) per = ntiles;
+  return per * sl;
 }
 
 void conv_pw_stream(int dtype, const void* x, const void* w, void* y, const void* zero, int M, int kin, int nout,
                     float* part, int grid, hipStream_t s, const void* addend) {
   MXAMD_HOST_CHECK(conv_pw_stream_ok(kin, nout), "conv_pw_stream: unsupported (Cin, Cout)");
-  MXAMD_HOST_CHECK(grid >= 1 && (int64_t)M * nout * 2 < (1ll << 31) - 64 && (int64_t)M * kin < (1ll << 31),
+  MXAMD_HOST_CHECK(grid >= 1 && grid % conv_pw_stream_slices(kin, nout) == 0 &&
+                   (int64_t)M * nout * 2 < (1ll << 31) - 64 && (int64_t)M * kin < (1ll << 31),
                    "conv_pw_stream: tensor too large for 32-bit offsets");
   bool ok = false;
   if (dtype == kF16) ok = dispatch_pw<__half>(kin, nout, x, w, y, zero, M, part, addend, grid, s);

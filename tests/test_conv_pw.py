@@ -13,7 +13,8 @@ pytestmark = pytest.mark.gpu
                                            (256, 128, 2049, torch.bfloat16), (128, 128, 100, torch.float16),
                                            (128, 256, 3000, torch.bfloat16), (64, 128, 1000, torch.float16),
                                            (128, 512, 1600, torch.float16), (256, 512, 900, torch.bfloat16),
-                                           (512, 256, 2500, torch.float16)])
+                                           (512, 256, 2500, torch.float16), (256, 1024, 1700, torch.float16),
+                                           (1024, 256, 1000, torch.bfloat16), (512, 2048, 300, torch.float16)])
 def test_conv_pw_matches_fp32(kin, nout, M, dt):
     dev = torch.device('cuda', 0)
     assert KF.pw_ok(torch.empty(1, kin, dtype=dt, device=dev), kin, nout)
@@ -37,7 +38,8 @@ def test_conv_pw_matches_fp32(kin, nout, M, dt):
 @pytest.mark.parametrize('kin,nout,M,dt', [(64, 256, 3136 * 3 + 17, torch.float16), (128, 256, 4000, torch.bfloat16),
                                            (256, 64, 2001, torch.float16), (64, 64, 65, torch.bfloat16),
                                            (512, 128, 3000, torch.float16), (128, 512, 3136 + 5, torch.float16),
-                                           (256, 512, 1000, torch.bfloat16)])
+                                           (256, 512, 1000, torch.bfloat16), (256, 1024, 1568 + 3, torch.float16),
+                                           (512, 2048, 200, torch.bfloat16)])
 def test_conv_pw_addend_epilogue(kin, nout, M, dt):
     """y = x . w^T + addend (the identity-shortcut gradient of a tee dgrad) in the epilogue."""
     dev = torch.device('cuda', 0)
