@@ -93,6 +93,18 @@ def mark_variables(variables, gradients, grad_reqs='write'):
         if r == 'null':
             v._grad_req = None
             continue
+        if not v._data.is_floating_point() or getattr(v, '_idt', None) is not None:
+            # integer variable: carried in float64 with its dtype in _idt (NDArray.attach_grad); the
+            # gradient buffer becomes a float64 buffer reporting the integer dtype as well
+            import torch
+            idt = getattr(v, '_idt', None) or v._data.dtype
+            if not v._data.is_floating_point():
+                v._data = v._data.detach().to(torch.float64)
+                v._idt = idt
+            if not g._data.is_floating_point():
+                gidt = g._data.dtype
+                g._data = g._data.to(torch.float64)
+                g._idt = gidt
         v._set_grad_buffer(g._data, r)
         v._grad = g
 

@@ -495,10 +495,16 @@ class Executor:
         arg_names = self._symbol.list_arguments()
         feed = {}
         leaves = []
+        int_dtypes = None
         for n, a in zip(arg_names, self.arg_arrays):
             t = a._data.detach()
-            if need_grad and self._grad_req[n] != 'null' and (t.is_floating_point() or t.is_complex()):
-                # integer inputs (indices, labels) are not differentiable: their gradient stays zero
+            if need_grad and self._grad_req[n] != 'null':
+                if not (t.is_floating_point() or t.is_complex()):
+                    # an integer argument with a gradient: carried in float64 through the graph's
+                    # integer shadow path (GraphProgram.run), so casts out of it back-propagate
+                    int_dtypes = int_dtypes or {}
+                    int_dtypes[n] = t.dtype
+                    t = t.to(torch.float64)
                 t = t.requires_grad_(True)
                 leaves.append((n, t))
             feed[n] = t
@@ -515,7 +521,7 @@ class Executor:
                     _call_monitor(cb, name, NDArray(t.detach()))
             record = [] if (mon is not None and need_grad) else None
             with torch.set_grad_enabled(need_grad):
-                outs = self._prog.run(feed, mon, self._monitor_all, record)
+                outs = self._prog.run(feed, mon, self._monitor_all, record, int_dtypes=int_dtypes)
             self._mon_record = record
             self._mon_grads = {}
             if record:
@@ -533,14 +539,16 @@ class Executor:
             _state.STATE.training = prev_train
         self._leaves = leaves
         self._out_tensors = outs
-        if len(self.outputs) == len(outs) and all(
-                b.shape == tuple(o.shape) and b._data.dtype == o.dtype for b, o in zip(self.outputs, outs)):
+        idts = getattr(self._prog, 'out_idts', None) or [None] * len(outs)
+        vals = [o.detach().to(d) if d is not None else o.detach() for o, d in zip(outs, idts)]
+        if len(self.outputs) == len(vals) and all(
+                b.shape == tuple(o.shape) and b._data.dtype == o.dtype for b, o in zip(self.outputs, vals)):
             # write into the bind-time output arrays (they may be views shared with a reshaped executor)
             with torch.no_grad():
-                for b, o in zip(self.outputs, outs):
-                    b._data.copy_(o.detach())
+                for b, o in zip(self.outputs, vals):
+                    b._data.copy_(o)
         else:
-            self.outputs = [NDArray(o.detach()) for o in outs]
+            self.outputs = [NDArray(o) for o in vals]
         st = self._output_stypes()
         if st is not None:
             from .ndarray import sparse

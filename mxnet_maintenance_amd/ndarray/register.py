@@ -175,7 +175,8 @@ def _merge_shadow(res_f, res_t):
 
 # operators whose integer instantiation has a zero gradient in the reference (mshadow_op's
 # mod_grad / mod_rgrad are 0 except for floating types)
-INT_ZERO_GRAD = frozenset(('_npi_mod', '_npi_mod_scalar', '_npi_fmod', '_npi_fmod_scalar'))
+INT_ZERO_GRAD = frozenset(('_npi_mod', '_npi_mod_scalar', '_npi_fmod', '_npi_fmod_scalar', '_mod', 'broadcast_mod',
+                           '_mod_scalar', '_rmod_scalar'))
 
 
 def _run_shadow(fn, inputs, kw, opname=None):

@@ -21,6 +21,7 @@ imperatively (with autograd), symbolically (infer_shape via the prop's
 ``infer_shape``) and inside hybridized blocks.
 """
 import collections
+import warnings
 import ctypes  # noqa: F401  (part of the reference module's star-import surface)
 import torch
 
@@ -279,8 +280,35 @@ registry.register('Custom', _custom_fn, arg_names=_custom_args, aux_names=_custo
 # ---------------------------------------------------------------------------
 
 class PythonOp:
+    """Deprecated operator front-end (reference python/mxnet/operator.py:51-152). ``get_symbol``
+    registers a private CustomOpProp that forwards shape inference and forward/backward to this
+    instance, so the op runs through the same Custom-op path as :class:`CustomOp`."""
+
+    _array_kind = 'ndarray'
+    _count = 0
+
     def __init__(self, need_top_grad=True):
+        self.info_ = None
         self.need_top_grad_ = need_top_grad
+        warnings.warn('PythonOp has been deprecated. Please use CustomOp')
+
+    def __call__(self, *args, **kwargs):
+        return self.get_symbol(*args, **kwargs)
+
+    def get_symbol(self, *args, **kwargs):
+        """Symbol applying this operator to ``args`` (call once per stateful instance)."""
+        if self.info_ is None:
+            PythonOp._count += 1
+            self.info_ = '_pythonop_%s_%d' % (type(self).__name__, PythonOp._count)
+            register(self.info_)(_python_op_prop(self))
+        from . import symbol as _sym
+        return _sym.Custom(*args, op_type=self.info_, **kwargs)
+
+    def forward(self, in_data, out_data):
+        out_data[0][:] = in_data[0]
+
+    def backward(self, out_grad, in_data, out_data, in_grad):
+        in_grad[0][:] = 1.0
 
     def list_outputs(self):
         return ['output']
@@ -296,16 +324,68 @@ class PythonOp:
 
 
 class NDArrayOp(PythonOp):
-    def forward(self, in_data, out_data):
-        raise NotImplementedError
+    """PythonOp whose forward/backward receive NDArrays (reference operator.py:255-362)."""
 
-    def backward(self, out_grad, in_data, out_data, in_grad):
-        raise NotImplementedError
+    def __init__(self, need_top_grad=True):
+        super().__init__(need_top_grad)
+        warnings.warn('NDArrayOp has been deprecated. Please use CustomOp')
+
+    def declare_backward_dependency(self, out_grad, in_data, out_data):
+        deps = []
+        if self.need_top_grad():
+            deps.extend(out_grad)
+        deps.extend(in_data)
+        deps.extend(out_data)
+        return deps
 
 
 class NumpyOp(PythonOp):
-    def forward(self, in_data, out_data):
-        raise NotImplementedError
+    """PythonOp whose forward/backward receive numpy arrays, written back after the call
+    (reference operator.py:155-252)."""
 
-    def backward(self, out_grad, in_data, out_data, in_grad):
-        raise NotImplementedError
+    _array_kind = 'numpy'
+
+    def __init__(self, need_top_grad=True):
+        super().__init__(need_top_grad)
+        warnings.warn('NumpyOp has been deprecated. Please use CustomOp')
+
+
+def _python_op_prop(pyop):
+    """CustomOpProp class bound to one PythonOp instance."""
+    as_numpy = pyop._array_kind == 'numpy'
+
+    def _call(fn, groups, written):
+        if not as_numpy:
+            fn(*groups)
+            return
+        host = [[a.asnumpy() for a in g] for g in groups]
+        fn(*host)
+        for gi in written:
+            for dst, src in zip(groups[gi], host[gi]):
+                dst[:] = src
+
+    class _Op(CustomOp):
+        def forward(self, is_train, req, in_data, out_data, aux):
+            _call(pyop.forward, [in_data, out_data], written=(1,))
+
+        def backward(self, req, out_grad, in_data, out_data, in_grad, aux):
+            _call(pyop.backward, [out_grad, in_data, out_data, in_grad], written=(3,))
+
+    class _Prop(CustomOpProp):
+        def __init__(self):
+            super().__init__(need_top_grad=pyop.need_top_grad())
+
+        def list_arguments(self):
+            return pyop.list_arguments()
+
+        def list_outputs(self):
+            return pyop.list_outputs()
+
+        def infer_shape(self, in_shape):
+            ins, outs = pyop.infer_shape(in_shape)[:2]
+            return ins, outs, []
+
+        def create_operator(self, ctx, in_shapes, in_dtypes):
+            return _Op()
+
+    return _Prop

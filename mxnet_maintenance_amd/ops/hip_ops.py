@@ -280,8 +280,12 @@ def pool(data, pool_type, kernel, stride, pad, convention, count_include_pad, ch
 # elementwise / normalisation
 # ---------------------------------------------------------------------------
 
+# MXAMD_HIP_ELEMWISE=0 sends relu and the broadcast binaries back to torch (A/B switch)
+_HIP_ELEMWISE = os.environ.get('MXAMD_HIP_ELEMWISE', '1') == '1'
+
+
 def relu(x):
-    if _use_hip(x) and _K.relu_ok(x):
+    if _HIP_ELEMWISE and _use_hip(x) and _K.relu_ok(x):
         return _K.ReluHip.apply(x)
     return torch.relu(x)
 
@@ -289,7 +293,8 @@ def relu(x):
 def binary(op, a, b):
     """Broadcast add/sub/mul/div/maximum/minimum of two same-dtype GPU tensors on the in-tree
     kernel; None when the operands do not qualify (the caller runs the torch op)."""
-    if isinstance(a, torch.Tensor) and isinstance(b, torch.Tensor) and _use_hip(a) and _K.binary_ok(a, b):
+    if (_HIP_ELEMWISE and isinstance(a, torch.Tensor) and isinstance(b, torch.Tensor) and _use_hip(a)
+            and _K.binary_ok(a, b)):
         return _K.BinaryHip.apply(a, b, op)
     return None
 

@@ -258,7 +258,10 @@ def linalg_makediag(A, offset=0):
 
 @register('_linalg_extracttrian', aliases=('linalg_extracttrian',), params={'offset': ('int', 0), 'lower': ('bool', True)})
 def linalg_extracttrian(A, offset=0, lower=True):
+    # a non-zero offset picks the side itself; ``lower`` only decides at offset 0
+    # (reference src/operator/tensor/la_op.h: trian ops)
     n = A.shape[-1]
+    lower = offset < 0 or (offset == 0 and lower)
     idx = torch.tril_indices(n, n, offset) if lower else torch.triu_indices(n, n, offset)
     return A[..., idx[0], idx[1]]
 
@@ -267,6 +270,7 @@ def linalg_extracttrian(A, offset=0, lower=True):
 def linalg_maketrian(A, offset=0, lower=True):
     m = A.shape[-1]
     n = int((math.sqrt(8 * m + 1) - 1) / 2) + abs(offset)
+    lower = offset < 0 or (offset == 0 and lower)
     out = torch.zeros(A.shape[:-1] + (n, n), dtype=A.dtype, device=A.device)
     idx = torch.tril_indices(n, n, offset) if lower else torch.triu_indices(n, n, offset)
     out[..., idx[0], idx[1]] = A

@@ -887,8 +887,11 @@ def ctc_loss(data, label, *lengths, use_data_lengths=False, use_label_lengths=Fa
     if use_label_lengths:
         ll = lengths[li].to(torch.int64)
     else:
-        ll = pad_mask.sum(1)
-    logp = torch.log_softmax(data.float(), dim=2)
+        ll = pad_mask.to(torch.int64).cumprod(1).sum(1)      # labels end at the first padding value
+    # frames past a sequence's length never reach the loss or its gradient, whatever they hold
+    valid = torch.arange(T, device=data.device)[:, None] < dl.to(data.device)[None, :]
+    x = torch.where(valid[:, :, None], data.float(), torch.zeros((), device=data.device))
+    logp = torch.log_softmax(x, dim=2)
     loss = F.ctc_loss(logp, lab.clamp(min=0), dl.cpu(), ll.cpu(), blank=blank, reduction='none',
                       zero_infinity=True)
     return loss.to(data.dtype), torch.zeros_like(data)

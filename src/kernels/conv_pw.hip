@@ -84,10 +84,12 @@ constexpr int pw_bm(int kin, int nout, bool add) {
   const int in_rows = (8192 / kin) > 16 ? (8192 / kin) : 16;    // Cin >= 1024: 16 rows of up to 32 KB
   const int bm0 = (16384 / nout) < in_rows ? (16384 / nout) : in_rows;
   if (!add) return bm0;
+  // with an addend: at most 32 pixels and a 16 KB addend stage (deep rings), at least one 16-row
+  // fragment per pixel wave (the LDS-DMA rounds of a tile may then be partial: see issue())
+  const int wp = 8 / ((nout / 16) < 8 ? (nout / 16) : 8);
   int bm = bm0 < 32 ? bm0 : 32;
-  if (bm > 8192 / nout) bm = 8192 / nout;                         // addend stage <= 16 KB
-  if (bm < 4096 / nout) bm = 4096 / nout;
-  if (bm < 4096 / kin) bm = 4096 / kin;
+  if (bm > 8192 / nout) bm = 8192 / nout;
+  if (bm < 16 * wp) bm = 16 * wp;
   return bm;
 }
 
@@ -105,26 +107,52 @@ struct PwCfg {
   static constexpr int STAGE = STAGE_IN + STAGE_ADD;
   static constexpr int LPT = STAGE_IN / (512 * 16);        // LDS-DMA instructions per thread per tile
   static constexpr int APT = STAGE_ADD / (512 * 16);       // ... for the addend
+  // with an addend, a tile's 1 KB LDS-DMA instructions go round-robin over the 8 waves (rounds may be
+  // partial): TI input and TA addend instructions
+  static constexpr int TI = STAGE_IN / 1024;
+  static constexpr int TA = STAGE_ADD / 1024;
   static constexpr int PITCH = NOUT * 2 + 16;              // epilogue image row pitch
   static constexpr int EPI = BM * PITCH;
   static constexpr int OCH = NOUT / 8;                     // 16-byte chunks per output row
   static constexpr int SPT = (BM * OCH + 511) / 512;       // 16-byte stores per thread per tile (uniform)
   // deepest ring (<= 4 stages) that keeps WPC workgroups per CU in the 160 KB of LDS
   static constexpr int LDS = WPC == 1 ? 156 * 1024 : 80 * 1024;
-  static constexpr int NST = (4 * STAGE + EPI <= LDS) ? 4 : ((3 * STAGE + EPI <= LDS) ? 3 : 2);
+  static constexpr int NMAX = ADD ? 6 : 4;
+  static constexpr int NST = (NMAX * STAGE + EPI <= LDS) ? NMAX
+                           : ((NMAX - 1) * STAGE + EPI <= LDS) ? NMAX - 1
+                           : ((NMAX - 2) * STAGE + EPI <= LDS) ? NMAX - 2 : 2;
   static constexpr int D = NST - 1;
   static constexpr int SMEM = NST * STAGE + EPI;
   static_assert(FC >= 1 && FP >= 1, "at least one fragment pair per wave");
-  static_assert(LPT >= 1 && STAGE_IN % (512 * 16) == 0, "whole LDS-DMA instructions per tile");
-  static_assert(!ADD || (APT >= 1 && STAGE_ADD % (512 * 16) == 0), "whole LDS-DMA instructions per addend tile");
+  static_assert(ADD || (LPT >= 1 && STAGE_IN % (512 * 16) == 0), "whole LDS-DMA instructions per tile");
+  static_assert(!ADD || (STAGE_IN % 1024 == 0 && STAGE_ADD % 1024 == 0), "whole 1 KB LDS-DMA instructions");
   static_assert(!ADD || WPC == 1, "the addend stage needs the LDS of a whole CU");
   static_assert((BM * OCH) % 512 == 0 || BM * OCH < 512, "whole store rounds, or a single partial one");
   static_assert(512 % OCH == 0, "a thread keeps one output chunk");
-  static_assert(D * (LPT + APT + SPT) < 64, "vmcnt range");
+  static_assert(D * ((TI + 7) / 8 + (TA + 7) / 8 + SPT) < 64, "vmcnt range");
   // resident weights: a quarter of the VGPR budget (128 at 2 workgroups per CU, 256 at 1)
   static_assert(FC * KS * 4 <= (WPC == 1 ? 128 : 64), "resident weights exceed the register budget");
   static_assert(ROWB % 128 == 0, "rows of whole 128-byte swizzle groups");
 };
+
+// Wait until at most `n` VM ops are outstanding, exactly (0 <= n < 40; larger n round down).
+__device__ __forceinline__ void vm_wait_n(int n) {
+  switch (n) {
+#define MXAMD_VMW(K) \
+  case K:            \
+    vm_wait<K>();    \
+    break;
+    MXAMD_VMW(0) MXAMD_VMW(1) MXAMD_VMW(2) MXAMD_VMW(3) MXAMD_VMW(4) MXAMD_VMW(5) MXAMD_VMW(6) MXAMD_VMW(7)
+    MXAMD_VMW(8) MXAMD_VMW(9) MXAMD_VMW(10) MXAMD_VMW(11) MXAMD_VMW(12) MXAMD_VMW(13) MXAMD_VMW(14) MXAMD_VMW(15)
+    MXAMD_VMW(16) MXAMD_VMW(17) MXAMD_VMW(18) MXAMD_VMW(19) MXAMD_VMW(20) MXAMD_VMW(21) MXAMD_VMW(22)
+    MXAMD_VMW(23) MXAMD_VMW(24) MXAMD_VMW(25) MXAMD_VMW(26) MXAMD_VMW(27) MXAMD_VMW(28) MXAMD_VMW(29)
+    MXAMD_VMW(30) MXAMD_VMW(31) MXAMD_VMW(32) MXAMD_VMW(33) MXAMD_VMW(34) MXAMD_VMW(35) MXAMD_VMW(36)
+    MXAMD_VMW(37) MXAMD_VMW(38) MXAMD_VMW(39)
+#undef MXAMD_VMW
+    default:
+      vm_wait<39>();
+  }
+}
 
 // Wait until at most `n` VM ops are outstanding (n rounded DOWN to an available level: waiting for
 // more than necessary is always safe).
@@ -187,27 +215,35 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
   // bytes [(i*8+wid)*1024, +1024) of the stage (linear destination, swizzled source chunk)
   auto issue = [&](int t, int st) {
     char* sb = smem + st * C::STAGE;
+    // input instruction i covers bytes [i*1024, +1024) of the stage (linear destination, swizzled
+    // source chunk); without an addend every wave issues LPT, with one instruction i goes to wave i % 8
+    constexpr int NI = ADD ? (C::TI + 7) / 8 : C::LPT;
 #pragma unroll
-    for (int i = 0; i < C::LPT; ++i) {
-      const int byte = ((i * 8 + wid) * 64 + lane) * 16;  // destination byte within the stage (linear)
+    for (int j = 0; j < NI; ++j) {
+      const int i = j * 8 + wid;
+      if (ADD && i >= C::TI) break;
+      const int byte = (i * 64 + lane) * 16;               // destination byte within the stage (linear)
       const int row = byte / C::ROWB;
       const int slot = (byte % C::ROWB) / 16;
       const int chunk = slot ^ (row & 7);               // source chunk for this slot (XOR swizzle)
       const int p = t * C::BM + row;
       const T* src = p < M ? x + static_cast<int64_t>(p) * KIN + chunk * 8 : zero + (chunk & 7) * 8;
-      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sb + (i * 8 + wid) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sb + i * 1024), 16, 0, 0);
     }
     // the tile's addend rows, linear after the input (rows past M read the zero page)
 #pragma unroll
-    for (int i = 0; i < C::APT; ++i) {
-      const int byte = ((i * 8 + wid) * 64 + lane) * 16;
+    for (int j = 0; j < (C::TA + 7) / 8; ++j) {
+      const int i = j * 8 + wid;
+      if (i >= C::TA) break;
+      const int byte = (i * 64 + lane) * 16;
       const int row = byte / (NOUT * 2);
       const int p = t * C::BM + row;
       const T* src = p < M ? addend + static_cast<int64_t>(p) * NT + slice * NOUT + (byte % (NOUT * 2)) / 2 : zero;
-      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sb + C::STAGE_IN + (i * 8 + wid) * 1024), 16,
-                                       0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sb + C::STAGE_IN + i * 1024), 16, 0, 0);
     }
   };
+  // LDS-DMA instructions this wave issues per tile (uniform over the wave)
+  const int ops_per_tile = ADD ? (C::TI - wid + 7) / 8 + (C::TA - wid + 7) / 8 : C::LPT;
 
   const int my_tiles = wg < ntiles ? (ntiles - wg + gs - 1) / gs : 0;
   for (int j = 0; j < C::D && j < my_tiles; ++j) issue(wg + j * gs, j);
@@ -241,8 +277,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
       // younger than tile it's DMA are tiles it+1 .. it+D-1 and the stores of the iterations since
       const int later = (my_tiles - 1 - it) < C::D - 1 ? (my_tiles - 1 - it) : C::D - 1;
       const int epis = it < C::D ? it : C::D;
-      if (later == C::D - 1 && epis == C::D) vm_wait<(C::D - 1) * (C::LPT + C::APT) + C::D * C::SPT>();
-      else vm_wait_le(later * (C::LPT + C::APT) + epis * C::SPT);
+      vm_wait_n(later * ops_per_tile + epis * C::SPT);
       lds_barrier();
       if (it + C::D < my_tiles) issue(wg + (it + C::D) * gs, (it + C::D) % C::NST);
     }
