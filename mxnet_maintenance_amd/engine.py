@@ -443,3 +443,158 @@ def async_copy_ok(src, dev):
     import torch
     return (dev.type == 'cuda' and src.device.type == 'cpu' and not (src.requires_grad and torch.is_grad_enabled())
             and src.numel() * src.element_size() >= _ASYNC_MIN_BYTES)
+
+
+# ---------------------------------------------------------------- imperative GPU ops on worker streams
+# Reference: ThreadedEnginePerDevice (src/engine/threaded_engine_perdevice.cc) runs GPU operators on
+# MXNET_GPU_WORKER_NTHREADS worker streams per device; an operator waits for the writers of the arrays
+# it reads and for the readers / writer of the arrays it writes, so independent chains overlap.
+# Here, with MXNET_GPU_WORKER_NTHREADS = N > 1, every imperative operator is issued (from the calling
+# thread: no hand-off, so no added latency) on one of N streams of its device -- slot 0 is the caller's
+# current stream, slots 1..N-1 are worker streams:
+#   * a chain stays on the stream that produced its inputs; an operator whose GPU inputs no worker
+#     slot produced (parameters, uploaded data) starts a new chain on the next slot, round-robin;
+#   * an input produced on another slot makes the operator's stream wait for that slot on the GPU
+#     (stream-on-stream wait) and is recorded on it for the caching allocator; an in-place write
+#     (``out=``) also waits for the slots that read the target since its last write;
+#   * host-visible points -- asnumpy / wait_to_read / waitall, copies, setitem, optimizer and kvstore
+#     updates -- first join the worker slots into the caller's stream (join_workers), so every code
+#     path outside operator dispatch sees finished results.
+# The default (1) keeps everything on the caller's stream.
+GPU_WORKERS = max(1, int(os.environ.get('MXNET_GPU_WORKER_NTHREADS', '1') or 1))
+
+
+class _Workers:
+    def __init__(self):
+        self.streams = {}     # device index -> [None, stream 1, ..., stream N-1]
+        self.rr = {}          # device index -> next slot for a new chain
+        self.dirty = {}       # device index -> slots with work not yet joined into the caller's stream
+        self.depth = 0        # > 0 while an operator body runs (nested operators stay on its stream)
+
+    def stream(self, dev, sid):
+        import torch
+        if sid == 0:
+            return torch.cuda.current_stream(dev)
+        lst = self.streams.get(dev)
+        if lst is None or len(lst) < GPU_WORKERS:
+            lst = self.streams[dev] = [None] + [torch.cuda.Stream(device=dev) for _ in range(GPU_WORKERS - 1)]
+        return lst[sid]
+
+
+_workers = _Workers()
+
+
+def set_gpu_workers(n):
+    """Number of streams imperative GPU operators spread over per device (1 = the caller's stream
+    only); returns the previous value.  Joins the current worker streams first."""
+    global GPU_WORKERS
+    join_workers()
+    prev, GPU_WORKERS = GPU_WORKERS, max(1, int(n))
+    return prev
+
+
+def _gpu_device(tensors):
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            return t.device.index
+    return None
+
+
+_epoch = [0]     # bumped at every host-visible point (join_workers)
+
+
+def _slot_of(t):
+    """Worker slot that produced tensor ``t`` (or the base of the view ``t``); None when it was
+    written outside operator dispatch (ordered on the caller's stream)."""
+    sid = getattr(t, '_mx_sid', None)
+    if sid is None and t._base is not None:
+        sid = getattr(t._base, '_mx_sid', None)
+    return sid if sid is not None and sid < GPU_WORKERS else None
+
+
+def op_stream(tensors):
+    """(slot, stream) an imperative operator on the input ``tensors`` runs on, with the waits and
+    allocator records for inputs produced elsewhere issued; (None, None) without a GPU input."""
+    dev = _gpu_device(tensors)
+    if dev is None:
+        return None, None
+    sid = None
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            sid = _slot_of(t)
+            if sid is not None:
+                break
+    if sid is None:
+        sid = _workers.rr.get(dev, 0)
+        _workers.rr[dev] = (sid + 1) % GPU_WORKERS
+    stream = _workers.stream(dev, sid)
+    for t in tensors:
+        if t is None or not t.is_cuda:
+            continue
+        xs = _slot_of(t)
+        if xs is None:
+            # written on the caller's stream: a worker slot orders after it once per epoch
+            if sid != 0:
+                seen = getattr(t, '_mx_seen', None)
+                if seen is None or seen[0] != _epoch[0]:
+                    seen = (_epoch[0], set())
+                    t._mx_seen = seen
+                if sid not in seen[1]:
+                    stream.wait_stream(_workers.stream(dev, 0))
+                    seen[1].add(sid)
+                t.record_stream(stream)
+        elif xs != sid:
+            stream.wait_stream(_workers.stream(dev, xs))
+            t.record_stream(stream)
+        rd = getattr(t, '_mx_readers', None)
+        if rd is None:
+            t._mx_readers = {sid}
+        else:
+            rd.add(sid)
+    return sid, stream
+
+
+def op_written(t, sid, stream):
+    """Before an in-place write of tensor ``t`` on slot ``sid``: wait for its writer and readers."""
+    if t.is_cuda:
+        dev = t.device.index
+        prev = _slot_of(t)
+        for r in set(getattr(t, '_mx_readers', None) or ()) | {prev if prev is not None else 0}:
+            if r != sid and r < GPU_WORKERS:
+                stream.wait_stream(_workers.stream(dev, r))
+    t._mx_readers = None
+    op_done([t], sid)
+
+
+def op_done(tensors, sid):
+    """Mark output ``tensors`` as produced on slot ``sid``."""
+    for t in tensors:
+        if isinstance(t, _torch_tensor()):
+            t._mx_sid = sid
+    if sid:
+        dev = _gpu_device([t for t in tensors if isinstance(t, _torch_tensor())])
+        if dev is not None:
+            _workers.dirty.setdefault(dev, set()).add(sid)
+
+
+def _torch_tensor():
+    import torch
+    return torch.Tensor
+
+
+def join_workers(dev=None):
+    """Make the caller's current stream (of ``dev``, default every device) wait on the GPU for all
+    work issued on the worker slots so far (a host-visible point: starts a new epoch)."""
+    if _workers.depth:
+        return            # inside an operator body: its own stream is already the right one
+    _epoch[0] += 1
+    if not _workers.dirty:
+        return
+    import torch
+    devs = [dev] if dev is not None else list(_workers.dirty)
+    for d in devs:
+        slots = _workers.dirty.pop(d, None)
+        if slots:
+            cur = torch.cuda.current_stream(d)
+            for sid in slots:
+                cur.wait_stream(_workers.stream(d, sid))

@@ -491,6 +491,8 @@ class Executor:
         return self._run(is_train, need_grad)
 
     def _run(self, is_train, need_grad):
+        from . import engine as _eng
+        _eng.join_workers()   # graph programs run on the caller's stream
         from .ndarray.ndarray import NDArray
         arg_names = self._symbol.list_arguments()
         feed = {}

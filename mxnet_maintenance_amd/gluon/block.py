@@ -676,6 +676,8 @@ class HybridBlock(Block):
             raise ValueError(error_msg)
 
     def _call_cached_op(self, *args):
+        from .. import engine as _eng
+        _eng.join_workers()   # graph programs run on the caller's stream
         if self._cached_op is None:
             self._build_cache(*args)
         args, fmt = _flatten(args, 'input')

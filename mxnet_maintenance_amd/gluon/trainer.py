@@ -26,6 +26,7 @@ import warnings
 import numpy as np
 import torch
 
+from .. import engine as _engine
 from .. import optimizer as opt
 from ..base import MXNetError
 from ..context import Context
@@ -362,6 +363,7 @@ class Trainer:
 
     def step(self, batch_size, ignore_stale_grad=False):
         """One optimisation step: reduce gradients, then update with lr * (grad / batch_size)."""
+        _engine.join_workers()   # worker-stream operators (engine.op_stream) done first
         rescale_grad = self._scale / batch_size
         self._check_and_rescale_grad(rescale_grad)
         self._prepare()
@@ -383,6 +385,7 @@ class Trainer:
         return False
 
     def allreduce_grads(self):
+        _engine.join_workers()
         self._prepare()
         assert not (self._kvstore and self._update_on_kvstore), \
             'allreduce_grads() when parameters are updated on kvstore is not supported. Try setting ' \
@@ -417,6 +420,7 @@ class Trainer:
             self._kvstore.pushpull(keys, vals, vals)
 
     def update(self, batch_size, ignore_stale_grad=False):
+        _engine.join_workers()
         self._prepare()
         assert not (self._kvstore and self._update_on_kvstore), \
             'update() when parameters are updated on kvstore is not supported. Try setting `update_on_kvstore` ' \

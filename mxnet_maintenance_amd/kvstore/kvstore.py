@@ -27,6 +27,7 @@ import torch
 
 from .comm import DeviceComm
 
+from .. import engine as _engine_mod
 from ..base import MXNetError, string_types
 from ..ndarray.ndarray import NDArray
 from .. import optimizer as opt
@@ -280,6 +281,7 @@ class KVStore(KVStoreBase):
             self._store[k] = NDArray(t)
 
     def push(self, key, value, priority=0):
+        _engine_mod.join_workers()
         keys = self._keys(key)
         vals = value if isinstance(key, (list, tuple)) else [value]
         merged = []
@@ -303,6 +305,7 @@ class KVStore(KVStoreBase):
         return self._str_keys[k]
 
     def pull(self, key, out=None, priority=0, ignore_sparse=True):
+        _engine_mod.join_workers()
         assert out is not None
         keys = self._keys(key)
         outs = out if isinstance(key, (list, tuple)) else [out]
@@ -328,6 +331,7 @@ class KVStore(KVStoreBase):
         With an optimizer set (update_on_kvstore) this is push + pull; otherwise
         it is an in-place all-reduce (the Gluon Trainer fast path).
         """
+        _engine_mod.join_workers()
         if self._updater is not None:
             self.push(key, value, priority)
             self.pull(key, out if out is not None else value, priority)
@@ -348,6 +352,7 @@ class KVStore(KVStoreBase):
         self.pull(key, out, priority)
 
     def row_sparse_pull(self, key, out=None, priority=0, row_ids=None):
+        _engine_mod.join_workers()
         assert out is not None and row_ids is not None
         keys = self._keys(key)
         outs = out if isinstance(key, (list, tuple)) else [out]

@@ -15,6 +15,7 @@ import numpy as np
 import torch
 
 from .. import _state
+from .. import engine as _engine
 from ..base import (MXNetError, numeric_types, integer_types, torch_dtype, np_dtype,
                     dtype_name)
 from ..context import Context, current_context, context_from_torch
@@ -237,6 +238,7 @@ class NDArray:
             engine.rethrow(box)
 
     def wait_to_read(self):
+        _engine.join_workers()
         var = getattr(self, '_engine_var', None)
         if var is not None:
             # an array written by an engine op (e.g. an async host -> device copy): its variable
@@ -249,6 +251,7 @@ class NDArray:
     wait_to_write = wait_to_read
 
     def asnumpy(self):
+        _engine.join_workers()
         self._rethrow()
         t = self._data.detach()
         idt = getattr(self, '_idt', None)
@@ -291,6 +294,7 @@ class NDArray:
         return NDArray(self._data.detach().clone())
 
     def copyto(self, other):
+        _engine.join_workers()
         if isinstance(other, NDArray):
             if other is self:
                 return other
@@ -316,6 +320,7 @@ class NDArray:
     def as_in_context(self, context):
         if self.context == context:
             return self
+        _engine.join_workers()
         if context.device_typeid == 3:
             t = self._data.detach().cpu()
             if torch.cuda.is_available():
@@ -435,6 +440,7 @@ class NDArray:
         return out
 
     def __setitem__(self, key, value):
+        _engine.join_workers()
         key = _convert_key(key)
         if isinstance(value, NDArray):
             _share_failure(value, self)          # writing a failed result fails the target too
@@ -1086,6 +1092,7 @@ def moveaxis(tensor, source, destination):
 def waitall():
     """Block until all pending device work and engine work has completed; then raise the oldest
     deferred operator failure, if any (every pending failure is cleared)."""
+    _engine.join_workers()
     if torch.cuda.is_available() and torch.cuda.is_initialized():
         torch.cuda.synchronize()
     from .. import engine

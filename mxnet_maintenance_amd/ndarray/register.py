@@ -5,9 +5,12 @@ src/imperative/imperative.cc (Imperative::Invoke / RecordOp).  Instead of
 generating ctypes stubs we bind each registered OpDef to a Python function that
 runs the op's torch-level implementation under the right autograd mode.
 """
+import contextlib
+
 import torch
 
 from .. import _state
+from .. import engine as _engine
 from .. import profiler as _profiler
 from ..ops import amp_dispatch as _amp
 from ..base import MXNetError, AsyncOpError
@@ -15,6 +18,7 @@ from ..ops import registry
 from .ndarray import NDArray
 
 _SKIP_KW = ('name', 'attr', 'out')
+_NULL_CTX = contextlib.nullcontext()
 _NP_CLS = [None]     # mx.np.ndarray, set when mx.numpy is imported
 
 
@@ -211,14 +215,24 @@ def invoke(op, inputs, attrs, out=None):
         from .. import engine
         box = engine.rng_failure()
     idts = None
+    ws_sid = ws_stream = None
+    sctx = _NULL_CTX
+    if _engine.GPU_WORKERS > 1 and not _engine._workers.depth:
+        # MXNET_GPU_WORKER_NTHREADS > 1: the operator's worker stream (engine.op_stream); operators
+        # nested in its body (Custom ops) run on that stream without bookkeeping
+        ws_sid, ws_stream = _engine.op_stream(tin)
+        if ws_stream is not None:
+            sctx = torch.cuda.stream(ws_stream)
+            _engine._workers.depth += 1
     try:
-        if _shadowed(inputs, attrs) and not _amp.active:
-            res, idts = _run_shadow(op.fn, inputs, attrs, op.name)
-        elif _profiler.active_imperative:
-            with _profiler.op_span(_profiler.current_scope() + op.name):
+        with sctx:
+            if _shadowed(inputs, attrs) and not _amp.active:
+                res, idts = _run_shadow(op.fn, inputs, attrs, op.name)
+            elif _profiler.active_imperative:
+                with _profiler.op_span(_profiler.current_scope() + op.name):
+                    res = _run(op.fn, tin, attrs)
+            else:
                 res = _run(op.fn, tin, attrs)
-        else:
-            res = _run(op.fn, tin, attrs)
     except AsyncOpError as e:
         from .. import engine
         if box is None:
@@ -236,11 +250,16 @@ def invoke(op, inputs, attrs, out=None):
             from ..base import MXNetIndexError
             raise MXNetIndexError('Error in operator %s: %s' % (op.name, e)) from e
         raise MXNetError('Error in operator %s: %s' % (op.name, e)) from e
+    finally:
+        if ws_stream is not None:
+            _engine._workers.depth -= 1
     nvis = op.get_num_visible_outputs(attrs)
     if isinstance(res, (tuple, list)):
         outs = [NDArray(r) for r in res[:nvis]]
     else:
         outs = [NDArray(res)]
+    if ws_sid is not None:
+        _engine.op_done([o._data for o in outs], ws_sid)
     st = _kept_stype(op.name, inputs, attrs) if out is None else None
     if st is not None and not _state.STATE.recording:
         from . import sparse
@@ -273,7 +292,9 @@ def invoke(op, inputs, attrs, out=None):
             if _state.STATE.recording and o._data.requires_grad:
                 t._data = o._data
             else:
-                with torch.no_grad():
+                with torch.no_grad(), (torch.cuda.stream(ws_stream) if ws_stream is not None else _NULL_CTX):
+                    if ws_sid is not None:
+                        _engine.op_written(t._data, ws_sid, ws_stream)
                     t._data.copy_(o._data.reshape(t.shape) if o.shape != t.shape and o.size == t.size else o._data)
         return out
     if len(outs) == 1:

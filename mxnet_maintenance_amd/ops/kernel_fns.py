@@ -656,9 +656,24 @@ def conv_wgrad(x, dy, wshape, stride, pad, out=None, accum=False, dma=True, ring
     return out
 
 
+def _taps_t(w, out, src, base, rstride):
+    """out[base[z] + c*rstride[z] + k] = w[k, tap src[z], c] for every slot z, one launch
+    (src/kernels/pointwise.hip weight_taps_t)."""
+    K, R, S, C = w.shape
+    for i in range(0, len(src), 32):
+        _K.lib().weight_taps_t(w.element_size(), w.data_ptr(), out.data_ptr(), K, R * S, C, src[i:i + 32],
+                               base[i:i + 32], rstride[i:i + 32], _stream())
+    return out
+
+
 def _dgrad_weight(w):
     """Weight of the equivalent forward conv computing dX from dY (stride 1): [Cin][R][S][Cout], flipped."""
-    return w.flip(1, 2).permute(3, 1, 2, 0).contiguous()
+    K, R, S, C = w.shape
+    if not (w.is_cuda and w.is_contiguous() and w.element_size() in (2, 4) and _K.available()):
+        return w.flip(1, 2).permute(3, 1, 2, 0).contiguous()
+    T = R * S
+    out = torch.empty((C, R, S, K), dtype=w.dtype, device=w.device)
+    return _taps_t(w, out, [T - 1 - t for t in range(T)], [t * K for t in range(T)], [T * K] * T)
 
 
 def _phase_taps(R, P, s, ph):
@@ -680,8 +695,8 @@ _PHASE_PLANS = {}
 
 def _phase_plan(wshape, stride, pad, device):
     """Per (weight shape, stride, pad): the phases with taps [(ph, pw, R_i, S_i, pad_h, pad_w, w_off)], the
-    phases no tap reaches, and one gather index that builds every phase's weight slice
-    ([C][R_i][S_i][K], concatenated) from W [K][R][S][C] in a single kernel."""
+    phases no tap reaches, and the tap-transpose table ([(tap, out offset, row stride)], total size) that
+    builds every phase's weight slice ([C][R_i][S_i][K], concatenated) from W [K][R][S][C] in one launch."""
     key = (tuple(wshape), tuple(stride), tuple(pad), device)
     plan = _PHASE_PLANS.get(key)
     if plan is not None:
@@ -700,17 +715,14 @@ def _phase_plan(wshape, stride, pad, device):
             dw = [d for d, _ in tw]
             if dh != list(range(dh[0], dh[0] + len(dh))) or dw != list(range(dw[0], dw[0] + len(dw))):
                 raise ValueError('conv_dgrad_strided: non-contiguous phase taps')
-            rr = torch.tensor([r for _, r in th])
-            ss = torch.tensor([c for _, c in tw])
-            kk = torch.arange(K)
-            cc = torch.arange(C)
-            # element (c, i, j, k) of the slice <- W[k, rr[i], ss[j], c]
-            src = (((kk[None, None, None, :] * R + rr[None, :, None, None]) * S + ss[None, None, :, None]) * C
-                   + cc[:, None, None, None])
-            idx.append(src.reshape(-1))
+            # element (c, i, j, k) of the slice <- W[k, rr[i], ss[j], c]: one tap-transpose slot per (i, j)
+            nt = len(th) * len(tw)
+            for i, (_, r) in enumerate(th):
+                for j, (_, c) in enumerate(tw):
+                    idx.append((r * S + c, off + (i * len(tw) + j) * K, nt * K))
             phases.append((ph, pw, len(th), len(tw), -dh[0], -dw[0], off))
-            off += src.numel()
-    plan = (phases, empty, torch.cat(idx).to(device))
+            off += C * nt * K
+    plan = (phases, empty, (idx, off))
     _PHASE_PLANS[key] = plan
     return plan
 
@@ -732,7 +744,9 @@ def conv_dgrad_strided(dy, w, stride, pad, xshape, bco=128):
     dx = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
     if len(empty) > 3:
         raise ValueError('conv_dgrad_strided: at most 3 phases without taps')
-    wsub = w.reshape(-1).index_select(0, gidx)
+    slots, total = gidx
+    wsub = _taps_t(w.contiguous(), torch.empty(total, dtype=w.dtype, device=w.device), [t[0] for t in slots],
+                   [t[1] for t in slots], [t[2] for t in slots])
     cols = list(zip(*phases))
     _K.lib().conv_nhwc_dgrad_phases_glds(_DT[dy.dtype], dy.data_ptr(), wsub.data_ptr(), dx.data_ptr(),
                                          _zero_page(dy.device).data_ptr(), N, dy.shape[1], dy.shape[2], K, C, Ho, Wo,
@@ -999,27 +1013,51 @@ def pw_ok(x, kin, nout):
             and bool(_K.lib().conv_pw_stream_ok(int(kin), int(nout))))
 
 
-def conv_pw(x, w2, bn_stats=False, addend=None):
+def pw_bnb_ok(kin, nout, add, bn_src):
+    """True when the streaming 1x1 kernel has a BatchNorm-backward statistics epilogue for this
+    (Cin, Cout, addend) and the BN's ReLU mask source (2: from z, 3: forward mask bits)."""
+    return (bn_src is not None and int(bn_src[5]) in (2, 3) and hasattr(_K.lib(), 'conv_pw_stream_bnb_ok')
+            and bool(_K.lib().conv_pw_stream_bnb_ok(int(kin), int(nout), int(bool(add)), int(bn_src[5]))))
+
+
+def conv_pw(x, w2, bn_stats=False, addend=None, bn_bwd=None):
     """y = x . w2^T (+ addend) for NHWC ``x`` [..., Cin] and ``w2`` [Cout, Cin] on the streaming 1x1
     kernel; ``bn_stats``: BatchNorm sum / sum-of-squares partials in ``y._mxamd_bn_part`` (one per
-    workgroup); ``addend`` (the output's shape and dtype) is added in the epilogue."""
+    workgroup); ``addend`` (the output's shape and dtype) is added in the epilogue.  ``bn_bwd`` (a
+    BatchNorm's ``_mxamd_bn_src`` record, y being that BN's incoming gradient): its backward statistics
+    (sum dz, sum dz*(z-mean)) from the epilogue, attached as ``y._mxamd_bn_bwd``."""
     C = x.shape[-1]
     K = w2.shape[0]
     M = x.numel() // C
-    w2 = w2.contiguous()
+    # a dgrad's w2 is the transpose of a contiguous [Cin][Cout] weight: the kernel transposes it while
+    # loading its resident fragments (no per-call transposed copy)
+    wt = int(w2.dim() == 2 and w2.stride() == (1, K) and not w2.is_contiguous() and w2.data_ptr() % 16 == 0
+             and K % 8 == 0)
+    if not wt:
+        w2 = w2.contiguous()
     y = torch.empty(x.shape[:-1] + (K,), dtype=x.dtype, device=x.device)
     if addend is not None:
         addend = addend.contiguous()
         if tuple(addend.shape) != tuple(y.shape) or addend.dtype != y.dtype or addend.data_ptr() % 16:
             raise ValueError('conv_pw: addend must match the output (shape, dtype, 16-byte alignment)')
     lib = _K.lib()
-    grid = lib.conv_pw_stream_grid(M, C, K, _num_cus(x.device), int(addend is not None))
+    grid = lib.conv_pw_stream_grid(M, C, K, _num_cus(x.device), int(addend is not None or bn_bwd is not None))
     # BatchNorm partials: one per tile walker of a Cout slice (grid / slices per channel)
     nparts = grid // max(1, lib.conv_pw_stream_slices(C, K))
-    part = torch.empty(2 * K * nparts, dtype=torch.float32, device=x.device) if bn_stats else None
+    part = torch.empty(2 * K * nparts, dtype=torch.float32, device=x.device) if (bn_stats or bn_bwd) else None
+    bkw = {}
+    if bn_bwd is not None:
+        assert not bn_stats, 'conv_pw: forward and backward statistics are exclusive'
+        z, bmean, bscale, bshift, bmask, bmode, _token = bn_bwd
+        assert z.shape == y.shape and z.dtype == y.dtype and z.is_contiguous() and z.data_ptr() % 16 == 0
+        bkw = dict(bn_z=z.data_ptr(), bn_mask=_p(bmask), bn_mean=bmean.data_ptr(), bn_scale=_p(bscale),
+                   bn_shift=_p(bshift), bn_mode=int(bmode))
     lib.conv_pw_stream(_DT[x.dtype], x.data_ptr(), w2.data_ptr(), y.data_ptr(), _zero_page(x.device).data_ptr(), M, C,
-                       K, _p(part), grid, _stream(), _p(addend))
-    if part is not None:
+                       K, _p(part), grid, _stream(), _p(addend), wt, **bkw)
+    if bn_bwd is not None:
+        # pinned to this exact gradient tensor version (see conv_fwd)
+        y._mxamd_bn_bwd = (part, nparts, bn_bwd[6], y._version)
+    elif part is not None:
         y._mxamd_bn_part = (part, nparts)
     return y
 
@@ -1177,6 +1215,9 @@ def _dgrad_bn_candidates(dy, x, w, stride, pad, bn_src):
     cands = _dgrad_candidates(dy, x, w, stride, pad)
     K, R, S, C = w.shape
     fused = []
+    if (R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0) and pw_ok(dy, K, C)
+            and pw_bnb_ok(K, C, False, bn_src)):
+        fused.append(('pw+bn', lambda: conv_pw(dy, w.reshape(K, C).t(), bn_bwd=bn_src)))
     if (_CONV_HIP and tuple(stride) == (1, 1) and 2 * pad[0] == R - 1 and 2 * pad[1] == S - 1
             and K % 64 == 0):
         for v in _fwd_variants(K, C, ktot=R * S * K):
@@ -1406,6 +1447,8 @@ def _tee_dgrad(gy, x, w, gpass, inplace, bn_src=None):
         # streaming 1x1 kernel: small reductions (K <= 512) are memory-bound; the shortcut gradient
         # is added in its epilogue
         cands.append(('pw', lambda: conv_pw(gy, w2.t(), addend=gpass)))
+        if fuse_bn and gpass is not None and pw_bnb_ok(K, C, True, bn_src):
+            fused.append(('pw+bn', lambda: conv_pw(gy, w2.t(), addend=gpass, bn_bwd=bn_src)))
     # autotuning runs every candidate: use an out-of-place GEMM there (the in-place one would
     # accumulate into gpass once per timing repetition)
     cands.append(('mm', lambda: mm() if not (gpass is not None and inplace) else

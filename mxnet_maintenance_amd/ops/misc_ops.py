@@ -173,14 +173,16 @@ def linalg_gemm2(A, B, transpose_a=False, transpose_b=False, alpha=1.0, axis=-2)
     return _rows_back(alpha * torch.matmul(_t(A, transpose_a), _t(B, transpose_b)), axis, nd)
 
 
-@register('_linalg_potrf', aliases=('linalg_potrf',))
-def linalg_potrf(A):
-    return torch.linalg.cholesky(A)
+@register('_linalg_potrf', aliases=('linalg_potrf',), params={'lower': ('bool', True)})
+def linalg_potrf(A, lower=True):
+    """Cholesky factor: lower L with A = L L^T, or (lower=False) upper U with A = U^T U."""
+    return torch.linalg.cholesky(A, upper=not lower)
 
 
-@register('_linalg_potri', aliases=('linalg_potri',))
-def linalg_potri(A):
-    return torch.cholesky_inverse(A)
+@register('_linalg_potri', aliases=('linalg_potri',), params={'lower': ('bool', True)})
+def linalg_potri(A, lower=True):
+    """Inverse of L L^T (or U^T U when lower=False) from its Cholesky factor."""
+    return torch.cholesky_inverse(A, upper=not lower)
 
 
 @register('_linalg_trmm', aliases=('linalg_trmm',), arg_names=('A', 'B'),

@@ -274,6 +274,12 @@ def _fc_fwd_cands(x2, w, b):
     if K % 32 == 0 and N % 64 == 0 and x2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0:
         c.append(('hip', lambda: _KF.conv_fwd(x2.view(M, 1, 1, K), w.view(N, 1, 1, K), (1, 1), (0, 0),
                                               b).view(M, N)))
+        # the conv kernels' large-tile LDS-DMA variants (big 256x256 / 128x256 tiles, persistent ring)
+        # are GEMMs on a [M,1,1,K] view as well
+        for v in _KF._fwd_variants(K, N, b is not None, ktot=K):
+            if v >= 10:
+                c.append(('hip%d' % v, lambda v=v: _KF.conv_fwd(x2.view(M, 1, 1, K), w.view(N, 1, 1, K), (1, 1),
+                                                                (0, 0), b, v).view(M, N)))
     c.extend(_G.candidates(x2, w, bias=b))
     c.append(('mm', lambda: torch.nn.functional.linear(x2, w, None if b is None else b.to(x2.dtype))))
     return c
@@ -286,6 +292,12 @@ def _fc_dgrad_cands(dy2, w):
     if N % 32 == 0 and K % 64 == 0:
         c.append(('hip', lambda: _KF.conv_fwd(dy2.view(M, 1, 1, N), w.t().contiguous().view(K, 1, 1, N), (1, 1),
                                               (0, 0)).view(M, K)))
+        if dy2.data_ptr() % 16 == 0:
+            for v in _KF._fwd_variants(N, K, False, ktot=N):
+                if v >= 10:
+                    c.append(('hip%d' % v, lambda v=v: _KF.conv_fwd(dy2.view(M, 1, 1, N),
+                                                                    w.t().contiguous().view(K, 1, 1, N), (1, 1),
+                                                                    (0, 0), None, v).view(M, K)))
     # dX = dY . W = dY . (W^T)^T: the GEMM kernel on a fresh W^T (a small copy; the weight may
     # change in place between steps through the fused optimizer's raw pointers, so no caching)
     if (N % 64 == 0 and K % 64 == 0 and dy2.is_cuda and dy2.dtype in _G._DT and w.dtype == dy2.dtype
@@ -382,7 +394,6 @@ def _fc_wgrad(dy2, x2, w, w_ref):
 
 
 _COLSUM_PART = {}
-_COLSUM_CNT = {}
 
 
 def bias_grad(dy2, b_ref, bdt):
@@ -400,17 +411,9 @@ def bias_grad(dy2, b_ref, bdt):
         part = _COLSUM_PART[skey] = torch.empty(n, dtype=torch.float32, device=dy2.device)
     tgt = _leaf_grad(b_ref, N, dtype=bdt) if (bdt in _DT and _FC_DIRECT) else None
     out = tgt if tgt is not None else torch.empty(N, dtype=torch.float32, device=dy2.device)
-    if hasattr(lib, 'colsum_rows_fused'):
-        # one launch: the last block of each column strip finalises it (self-resetting counters)
-        cnt = _COLSUM_CNT.get(skey)
-        strips = lib.colsum_strips(N)
-        if cnt is None or cnt.numel() < strips:
-            cnt = _COLSUM_CNT[skey] = torch.zeros(max(strips, 64), dtype=torch.int32, device=dy2.device)
-        lib.colsum_rows_fused(_DT[dy2.dtype], dy2.data_ptr(), part.data_ptr(), cnt.data_ptr(), M, N, _DT[out.dtype],
-                              out.data_ptr(), int(tgt is not None), _stream())
-    else:
-        lib.colsum_rows(_DT[dy2.dtype], dy2.data_ptr(), _KF._zeros_f32(N, dy2.device).data_ptr(), part.data_ptr(),
-                        M, N, _DT[out.dtype], out.data_ptr(), int(tgt is not None), _stream())
+    # two launches (partial rows, then their sum); see bn_nhwc.hip on why not one
+    lib.colsum_rows(_DT[dy2.dtype], dy2.data_ptr(), _KF._zeros_f32(N, dy2.device).data_ptr(), part.data_ptr(),
+                    M, N, _DT[out.dtype], out.data_ptr(), int(tgt is not None), _stream())
     if tgt is not None:
         return None
     return out.to(bdt)

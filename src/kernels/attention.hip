@@ -39,6 +39,7 @@
 #include <stdexcept>
 
 #include "common.h"
+#include "mfma.h"
 
 namespace mxamd {
 
@@ -59,8 +60,7 @@ struct AOp;
 template <>
 struct AOp<__hip_bfloat16> {
   static __device__ __forceinline__ f4 mma(const u4& a, const u4& b, f4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
-                                                   c, 0, 0, 0);
+    return mfma::Op<__hip_bfloat16>::run(a, b, c);
   }
   static __device__ __forceinline__ uint32_t pack2(float a, float b) {
     uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
@@ -75,8 +75,7 @@ struct AOp<__hip_bfloat16> {
 template <>
 struct AOp<__half> {
   static __device__ __forceinline__ f4 mma(const u4& a, const u4& b, f4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8_t, a), __builtin_bit_cast(half8_t, b), c,
-                                                  0, 0, 0);
+    return mfma::Op<__half>::run(a, b, c);
   }
   static __device__ __forceinline__ uint32_t pack2(float a, float b) {
     __half2 h = __floats2half2_rn(a, b);

@@ -51,9 +51,6 @@ void softmax_ce_backward(int dtype, int label_is_int, const void* logits, const 
                          const float* gout, void* dlogits, int N, int K, hipStream_t s);
 void gap_nhwc_forward(int dtype, const void* x, void* y, int N, int HW, int C, hipStream_t s);
 void relu_forward(int dtype, const void* x, void* y, int64_t n, hipStream_t s);
-int colsum_strips(int C);
-void colsum_rows_fused(int dtype, const void* x, float* part, unsigned* counters, int64_t R, int C, int out_dtype,
-                       void* out, int accum, hipStream_t s);
 void relu_backward(int dtype, const void* y, const void* dy, void* dx, int64_t n, hipStream_t s);
 void pointwise_binary(int dtype, int op, const void* a, const void* b, void* out, int64_t n, int mode, int64_t row,
                       int ndim, const int64_t* shape, const int64_t* astride, const int64_t* bstride, hipStream_t s);
@@ -155,8 +152,13 @@ void twobit_dequantize_sum(const void* packed, int64_t row_bytes, int nrows, int
 int conv_pw_stream_ok(int kin, int nout);
 int conv_pw_stream_grid(int M, int kin, int nout, int ncu, int add);
 int conv_pw_stream_slices(int kin, int nout);
+void weight_taps_t(int elem_bytes, const void* w, void* out, int K, int RS, int C, int n, const int* src,
+                   const int64_t* base, const int64_t* rstride, hipStream_t s);
 void conv_pw_stream(int dtype, const void* x, const void* w, void* y, const void* zero, int M, int kin, int nout,
-                    float* part, int grid, hipStream_t s, const void* addend);
+                    float* part, int grid, hipStream_t s, const void* addend, int wt, const void* bn_z,
+                    const uint8_t* bn_mask, const float* bn_mean, const float* bn_scale, const float* bn_shift,
+                    int bn_mode);
+int conv_pw_stream_bnb_ok(int kin, int nout, int add, int mode);
 void conv_gen(int dtype, int mode, const void* src, const void* wsrc, const float* bias, void* dst, const int* geom,
               int splits, hipStream_t s);
 void rnn_fwd_seq(int dtype, int mode, const float* gx, const void* h0, const float* c0, const void* whh,
@@ -243,17 +245,31 @@ PYBIND11_MODULE(_hip_kernels, m) {
     check_launch("gemm_nt");
   });
   // streaming 1x1 convolution for small reductions (src/kernels/conv_pw.hip)
+  m.def("weight_taps_t", [](int eb, uintptr_t w, uintptr_t out, int K, int RS, int C, std::vector<int> src,
+                            std::vector<int64_t> base, std::vector<int64_t> rstride, uintptr_t s) {
+    if (src.size() != base.size() || src.size() != rstride.size()) throw std::runtime_error("weight_taps_t: table sizes");
+    weight_taps_t(eb, P<const void>(w), P<void>(out), K, RS, C, static_cast<int>(src.size()), src.data(), base.data(),
+                  rstride.data(), S(s));
+    check_launch("weight_taps_t");
+  });
   m.def("conv_pw_stream_ok", &conv_pw_stream_ok);
   m.def("conv_pw_stream_slices", &conv_pw_stream_slices);
   m.def("conv_pw_stream_grid", [](int M, int kin, int nout, int ncu, int add) {
     return conv_pw_stream_grid(M, kin, nout, ncu, add);
   }, pybind11::arg("M"), pybind11::arg("kin"), pybind11::arg("nout"), pybind11::arg("ncu"), pybind11::arg("add") = 0);
   m.def("conv_pw_stream", [](int dt, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t zero, int M, int kin, int nout,
-                             uintptr_t part, int grid, uintptr_t s, uintptr_t addend) {
+                             uintptr_t part, int grid, uintptr_t s, uintptr_t addend, int wt, uintptr_t bn_z,
+                             uintptr_t bn_mask, uintptr_t bn_mean, uintptr_t bn_scale, uintptr_t bn_shift, int bn_mode) {
     conv_pw_stream(dt, P<const void>(x), P<const void>(w), P<void>(y), P<const void>(zero), M, kin, nout,
-                   P<float>(part), grid, S(s), P<const void>(addend));
+                   P<float>(part), grid, S(s), P<const void>(addend), wt, P<const void>(bn_z), P<const uint8_t>(bn_mask),
+                   P<const float>(bn_mean), P<const float>(bn_scale), P<const float>(bn_shift), bn_mode);
     check_launch("conv_pw_stream");
-  });
+  }, pybind11::arg("dt"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("zero"),
+     pybind11::arg("M"), pybind11::arg("kin"), pybind11::arg("nout"), pybind11::arg("part"), pybind11::arg("grid"),
+     pybind11::arg("s"), pybind11::arg("addend"), pybind11::arg("wt") = 0, pybind11::arg("bn_z") = 0,
+     pybind11::arg("bn_mask") = 0, pybind11::arg("bn_mean") = 0, pybind11::arg("bn_scale") = 0,
+     pybind11::arg("bn_shift") = 0, pybind11::arg("bn_mode") = 0);
+  m.def("conv_pw_stream_bnb_ok", &conv_pw_stream_bnb_ok);
   // general implicit-GEMM convolution: grouped / dilated / 1-3-D / fp32 / transposed (src/kernels/conv_gen.hip)
   m.def("conv_gen", [](int dt, int mode, uintptr_t src, uintptr_t wsrc, uintptr_t bias, uintptr_t dst,
                        std::vector<int> geom, int splits, uintptr_t s) {
@@ -373,12 +389,6 @@ PYBIND11_MODULE(_hip_kernels, m) {
     softmax_ce_backward(dt, li, P<void>(logits), P<void>(label), P<float>(lse), P<float>(gout), P<void>(dlogits), N,
                         K, S(s));
     check_launch("softmax_ce_backward");
-  });
-  m.def("colsum_strips", &colsum_strips);
-  m.def("colsum_rows_fused", [](int dt, uintptr_t x, uintptr_t part, uintptr_t counters, int64_t R, int C, int odt,
-                                uintptr_t out, int accum, uintptr_t s) {
-    colsum_rows_fused(dt, P<void>(x), P<float>(part), P<unsigned>(counters), R, C, odt, P<void>(out), accum, S(s));
-    check_launch("colsum_rows_fused");
   });
   m.def("relu_forward", [](int dt, uintptr_t x, uintptr_t y, int64_t n, uintptr_t s) {
     relu_forward(dt, P<void>(x), P<void>(y), n, S(s));

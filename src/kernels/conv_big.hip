@@ -27,6 +27,7 @@
 #include <stdexcept>
 
 #include "common.h"
+#include "mfma.h"
 
 namespace mxamd {
 
@@ -40,39 +41,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void gbl_void;
 
 template <typename T>
-struct MfmaB;
-template <>
-struct MfmaB<__half> {
-  static __device__ __forceinline__ f4_t run(const u32x4& a, const u32x4& b, f4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8_t, a), __builtin_bit_cast(half8_t, b), c,
-                                                  0, 0, 0);
-  }
-  static __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
-    __half2 lo = __floats2half2_rn(a, b), hi = __floats2half2_rn(c, d);
-    uint2 r;
-    r.x = *reinterpret_cast<uint32_t*>(&lo);
-    r.y = *reinterpret_cast<uint32_t*>(&hi);
-    return r;
-  }
-};
-template <>
-struct MfmaB<__hip_bfloat16> {
-  static __device__ __forceinline__ f4_t run(const u32x4& a, const u32x4& b, f4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
-                                                   c, 0, 0, 0);
-  }
-  static __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
-    // plain conversions (v_cvt_pk_bf16_f32): round-to-nearest-even, NaN stays NaN
-    __hip_bfloat16 h0 = __float2bfloat16(a), h1 = __float2bfloat16(b), h2 = __float2bfloat16(c),
-                   h3 = __float2bfloat16(d);
-    uint2 r;
-    r.x = static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h0)) |
-          (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h1)) << 16);
-    r.y = static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h2)) |
-          (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h3)) << 16);
-    return r;
-  }
-};
+struct MfmaB : mfma::Op<T> {};   // 16x16x32 MFMA + epilogue packs (mfma.h)
 
 // Optional BatchNorm-backward statistics fused into the epilogue of a dgrad: y here is the gradient
 // dy arriving at a BatchNorm(+ReLU) whose input was z; per (channel, pixel tile) the kernel emits

@@ -21,6 +21,7 @@
 #include <stdexcept>
 
 #include "common.h"
+#include "mfma.h"
 
 namespace mxamd {
 
@@ -58,16 +59,14 @@ struct GFrag16 {
 template <>
 struct GFrag<__half> : GFrag16<__half> {
   static __device__ __forceinline__ f4_t mma(const frag& a, const frag& b, f4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8_t, a), __builtin_bit_cast(half8_t, b), c,
-                                                  0, 0, 0);
+    return mfma::Op<__half>::run(a, b, c);
   }
   static __device__ __forceinline__ __half out(float v) { return __float2half(v); }
 };
 template <>
 struct GFrag<__hip_bfloat16> : GFrag16<__hip_bfloat16> {
   static __device__ __forceinline__ f4_t mma(const frag& a, const frag& b, f4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
-                                                   c, 0, 0, 0);
+    return mfma::Op<__hip_bfloat16>::run(a, b, c);
   }
   static __device__ __forceinline__ __hip_bfloat16 out(float v) { return __float2bfloat16(v); }
 };

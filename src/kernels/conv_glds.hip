@@ -21,6 +21,7 @@
 #include <stdexcept>
 
 #include "common.h"
+#include "mfma.h"
 
 namespace mxamd {
 
@@ -34,40 +35,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void gbl_void;
 
 template <typename T>
-struct Mfma;
-template <>
-struct Mfma<__half> {
-  static __device__ __forceinline__ f4_t run(const u32x4& a, const u32x4& b, f4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8_t, a), __builtin_bit_cast(half8_t, b), c,
-                                                  0, 0, 0);
-  }
-  static __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
-    __half2 lo = __floats2half2_rn(a, b), hi = __floats2half2_rn(c, d);
-    uint2 r;
-    r.x = *reinterpret_cast<uint32_t*>(&lo);
-    r.y = *reinterpret_cast<uint32_t*>(&hi);
-    return r;
-  }
-};
-template <>
-struct Mfma<__hip_bfloat16> {
-  static __device__ __forceinline__ f4_t run(const u32x4& a, const u32x4& b, f4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
-                                                   c, 0, 0, 0);
-  }
-  static __device__ __forceinline__ uint32_t bf2(float a, float b) {
-    uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
-    ua += 0x7fff + ((ua >> 16) & 1);
-    ub += 0x7fff + ((ub >> 16) & 1);
-    return (ua >> 16) | (ub & 0xffff0000u);
-  }
-  static __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
-    uint2 r;
-    r.x = bf2(a, b);
-    r.y = bf2(c, d);
-    return r;
-  }
-};
+struct Mfma : mfma::Op<T> {};   // 16x16x32 MFMA + epilogue packs (mfma.h)
 
 struct GeomG {
   int N, H, W, C, K, R, S;

@@ -19,15 +19,19 @@
 //   * optional BatchNorm statistics: each thread keeps per-channel sum / sum-of-squares of the
 //     rows it stores over ALL its tiles; at the end one partial per workgroup per channel
 //     ([2][NOUT][grid] channel-major, the layout bn_nhwc.hip's finalize consumes);
-//   * optional addend (y = conv + addend: the identity-shortcut gradient of a tee dgrad): the
-//     addend chunks a thread stores for tile i+1 are loaded into registers right after tile i's
-//     stores, so they travel while tile i+1's MFMAs run; the counted waits include them.
+//   * optional addend (y = conv + addend: the identity-shortcut gradient of a tee dgrad), streamed
+//     through its own part of each ring stage by the same LDS-DMA rounds;
+//   * optional BatchNorm-backward statistics (y is the gradient of a BN(+ReLU) output): the BN's input
+//     z (and, for a residual tail, its 1-bit ReLU mask) ride in the stage as well, and each thread
+//     accumulates sum(dz) and sum(dz * (z - mean)), dz = y masked by the ReLU, over the rows it stores
+//     -- the BN's own backward reduction pass over (y, z) is not run.
 //
 // Requirements (host-checked): NHWC, KIN in {64,128,256,512}, NOUT in {64..1024} with
 // NOUT/WC * KIN <= 8192 (the register budget for the resident weights).
 #include <stdexcept>
 
 #include "common.h"
+#include "mfma.h"
 
 namespace mxamd {
 
@@ -41,30 +45,10 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void gbl_void;
 
 template <typename T>
-struct PwM;
-template <>
-struct PwM<__half> {
-  static __device__ __forceinline__ f4_t mma(const u32x4& a, const u32x4& b, f4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8_t, a), __builtin_bit_cast(half8_t, b), c,
-                                                  0, 0, 0);
-  }
-  static __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
-    __half2 lo = __floats2half2_rn(a, b), hi = __floats2half2_rn(c, d);
-    return uint2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
-  }
-};
-template <>
-struct PwM<__hip_bfloat16> {
-  static __device__ __forceinline__ f4_t mma(const u32x4& a, const u32x4& b, f4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
-                                                   c, 0, 0, 0);
-  }
-  static __device__ __forceinline__ uint32_t two(float a, float b) {
-    return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, __float2bfloat16(a))) |
-           (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, __float2bfloat16(b))) << 16);
-  }
-  static __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
-    return uint2{two(a, b), two(c, d)};
+struct PwM : mfma::Op<T> {   // 16x16x32 MFMA + epilogue packs (mfma.h)
+  template <typename V>
+  static __device__ __forceinline__ f4_t mma(const V& a, const V& b, f4_t c) {
+    return mfma::Op<T>::run(a, b, c);
   }
 };
 
@@ -80,7 +64,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // addend, at most 32 pixels (its LDS stage is as large as the image) but whole 8 KB LDS-DMA rounds
 // for both the input and the addend stage
 // (nout = the output channels one workgroup computes: a slice of the layer's when it is sliced)
-constexpr int pw_bm(int kin, int nout, bool add) {
+constexpr int pw_bm(int kin, int nout, bool add) {   // add: any extra stream (addend / BN-backward)
   const int in_rows = (8192 / kin) > 16 ? (8192 / kin) : 16;    // Cin >= 1024: 16 rows of up to 32 KB
   const int bm0 = (16384 / nout) < in_rows ? (16384 / nout) : in_rows;
   if (!add) return bm0;
@@ -93,9 +77,24 @@ constexpr int pw_bm(int kin, int nout, bool add) {
   return bm;
 }
 
-template <int KIN, int NOUT, int WPC = 2, bool ADD = false>
+// BN-backward statistics modes of the epilogue (bn_nhwc.hip's ReLU mask sources)
+constexpr int kPwBnbNone = 0;
+constexpr int kPwBnbPlain = 1;    // no ReLU
+constexpr int kPwBnbFromZ = 2;    // mask = z * scale + shift > 0
+constexpr int kPwBnbMask = 3;     // 1 bit per element written by the forward
+
+struct PwBnb {
+  const void* z;          // the BN's input, [M][NT]
+  const uint8_t* mask;    // kPwBnbMask: [M * NT / 8]
+  const float* mean;
+  const float* scale;     // kPwBnbFromZ
+  const float* shift;
+};
+
+template <int KIN, int NOUT, int WPC = 2, bool ADD = false, int BNB = kPwBnbNone>
 struct PwCfg {
-  static constexpr int BM = pw_bm(KIN, NOUT, ADD);
+  static constexpr bool EXT = ADD || BNB != kPwBnbNone;    // extra streams besides the input
+  static constexpr int BM = pw_bm(KIN, NOUT, EXT);
   static constexpr int WC = NOUT / 16 < 8 ? NOUT / 16 : 8;  // waves along output channels
   static constexpr int WP = 8 / WC;                        // waves along pixels
   static constexpr int FC = NOUT / WC / 16;                // channel fragments per wave
@@ -104,32 +103,39 @@ struct PwCfg {
   static constexpr int ROWB = KIN * 2;                     // input row bytes
   static constexpr int STAGE_IN = BM * ROWB;               // one input tile
   static constexpr int STAGE_ADD = ADD ? BM * NOUT * 2 : 0;  // its addend rows (linear)
-  static constexpr int STAGE = STAGE_IN + STAGE_ADD;
+  static constexpr int STAGE_Z = BNB ? BM * NOUT * 2 : 0;    // the BN input rows (linear)
+  static constexpr int STAGE_M = BNB == kPwBnbMask ? (BM * NOUT / 8 + 1023) / 1024 * 1024 : 0;  // mask bytes
+  static constexpr int STAGE = STAGE_IN + STAGE_ADD + STAGE_Z + STAGE_M;
   static constexpr int LPT = STAGE_IN / (512 * 16);        // LDS-DMA instructions per thread per tile
   static constexpr int APT = STAGE_ADD / (512 * 16);       // ... for the addend
   // with an addend, a tile's 1 KB LDS-DMA instructions go round-robin over the 8 waves (rounds may be
   // partial): TI input and TA addend instructions
   static constexpr int TI = STAGE_IN / 1024;
   static constexpr int TA = STAGE_ADD / 1024;
+  static constexpr int TZ = STAGE_Z / 1024;
+  static constexpr int TM = STAGE_M / 1024;
   static constexpr int PITCH = NOUT * 2 + 16;              // epilogue image row pitch
   static constexpr int EPI = BM * PITCH;
   static constexpr int OCH = NOUT / 8;                     // 16-byte chunks per output row
   static constexpr int SPT = (BM * OCH + 511) / 512;       // 16-byte stores per thread per tile (uniform)
   // deepest ring (<= 4 stages) that keeps WPC workgroups per CU in the 160 KB of LDS
   static constexpr int LDS = WPC == 1 ? 156 * 1024 : 80 * 1024;
-  static constexpr int NMAX = ADD ? 6 : 4;
+  static constexpr int NMAX = EXT ? 6 : 4;
   static constexpr int NST = (NMAX * STAGE + EPI <= LDS) ? NMAX
                            : ((NMAX - 1) * STAGE + EPI <= LDS) ? NMAX - 1
                            : ((NMAX - 2) * STAGE + EPI <= LDS) ? NMAX - 2 : 2;
   static constexpr int D = NST - 1;
   static constexpr int SMEM = NST * STAGE + EPI;
   static_assert(FC >= 1 && FP >= 1, "at least one fragment pair per wave");
-  static_assert(ADD || (LPT >= 1 && STAGE_IN % (512 * 16) == 0), "whole LDS-DMA instructions per tile");
-  static_assert(!ADD || (STAGE_IN % 1024 == 0 && STAGE_ADD % 1024 == 0), "whole 1 KB LDS-DMA instructions");
-  static_assert(!ADD || WPC == 1, "the addend stage needs the LDS of a whole CU");
+  static_assert(EXT || (LPT >= 1 && STAGE_IN % (512 * 16) == 0), "whole LDS-DMA instructions per tile");
+  static_assert(!EXT || (STAGE_IN % 1024 == 0 && STAGE_ADD % 1024 == 0 && STAGE_Z % 1024 == 0),
+                "whole 1 KB LDS-DMA instructions");
+  static_assert(!EXT || WPC == 1, "the extra stages need the LDS of a whole CU");
+  static_assert(BNB != kPwBnbMask || (NOUT / 8) % 16 == 0, "mask rows of whole 16-byte chunks");
   static_assert((BM * OCH) % 512 == 0 || BM * OCH < 512, "whole store rounds, or a single partial one");
   static_assert(512 % OCH == 0, "a thread keeps one output chunk");
-  static_assert(D * ((TI + 7) / 8 + (TA + 7) / 8 + SPT) < 64, "vmcnt range");
+  static_assert(D * ((TI + 7) / 8 + (TA + 7) / 8 + (TZ + 7) / 8 + (TM + 7) / 8 + SPT) < (EXT ? 40 : 64),
+                "vmcnt range (vm_wait_n covers < 40)");
   // resident weights: a quarter of the VGPR budget (128 at 2 workgroups per CU, 256 at 1)
   static_assert(FC * KS * 4 <= (WPC == 1 ? 128 : 64), "resident weights exceed the register budget");
   static_assert(ROWB % 128 == 0, "rows of whole 128-byte swizzle groups");
@@ -173,11 +179,12 @@ __device__ __forceinline__ void vm_wait_le(int n) {
 
 // NOUT: output channels per workgroup; S: slices of the layer's NOUT * S output channels (the
 // workgroups of one tile's slices are adjacent in the XCD-aware order, so they share its input in L2)
-template <typename T, int KIN, int NOUT, bool STATS, bool ADD, int WPC, int S>
+template <typename T, int KIN, int NOUT, bool STATS, bool ADD, int WPC, int S, int BNB>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WPC))) conv_pw_stream_kernel(
     const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y, const T* __restrict__ zero, int M, int ntiles,
-    float* __restrict__ part, const T* __restrict__ addend) {
-  using C = PwCfg<KIN, NOUT, WPC, ADD>;
+    float* __restrict__ part, const T* __restrict__ addend, int wt, PwBnb bnb) {
+  using C = PwCfg<KIN, NOUT, WPC, ADD, BNB>;
+  constexpr bool EXT = C::EXT;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -195,17 +202,50 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
 
   // ---- resident weights: A fragments of this wave's channels, all k-steps
   u32x4 wa[C::FC][C::KS];
+  if (!wt) {
 #pragma unroll
-  for (int f = 0; f < C::FC; ++f)
+    for (int f = 0; f < C::FC; ++f)
 #pragma unroll
-    for (int s = 0; s < C::KS; ++s) {
-      const int co = slice * NOUT + wc * C::FC * 16 + f * 16 + (lane & 15);
-      wa[f][s] = *reinterpret_cast<const u32x4*>(w + static_cast<int64_t>(co) * KIN + s * 32 + (lane >> 4) * 8);
-    }
+      for (int s = 0; s < C::KS; ++s) {
+        const int co = slice * NOUT + wc * C::FC * 16 + f * 16 + (lane & 15);
+        wa[f][s] = *reinterpret_cast<const u32x4*>(w + static_cast<int64_t>(co) * KIN + s * 32 + (lane >> 4) * 8);
+      }
+  } else {
+    // w is [KIN][NT] (a dgrad's untransposed weight): lane loads 8 consecutive channels of one input
+    // row of the fragment's 32 x 16 block (row lane/2, channels (lane&1)*8..+8) ...
+#pragma unroll
+    for (int f = 0; f < C::FC; ++f)
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        const int k = s * 32 + (lane >> 1);
+        const int co = slice * NOUT + wc * C::FC * 16 + f * 16 + (lane & 1) * 8;
+        wa[f][s] = *reinterpret_cast<const u32x4*>(w + static_cast<int64_t>(k) * NT + co);
+      }
+  }
 
   // the weight loads retire here, before the ring starts: inside the loop the only VM ops are the
   // ring's LDS-DMAs and the epilogue stores, so the counted waits below stay exact
   vm_wait<0>();
+  if (wt) {
+    // ... and the block is transposed through this wave's 1280-byte LDS scratch ([16 ch][40 halves],
+    // 16-byte aligned rows): written column-wise, read back as the lane's 8 consecutive k of its channel
+    // (the ring's stages are still free; a wave's LDS ops complete in order)
+    uint16_t* scr = reinterpret_cast<uint16_t*>(smem + wid * 1280);
+#pragma unroll
+    for (int f = 0; f < C::FC; ++f)
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        const uint4 v = __builtin_bit_cast(uint4, wa[f][s]);
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          scr[((lane & 1) * 8 + q) * 40 + (lane >> 1)] = static_cast<uint16_t>(wv[q >> 1] >> ((q & 1) * 16));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        wa[f][s] = *reinterpret_cast<const u32x4*>(scr + (lane & 15) * 40 + (lane >> 4) * 8);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    __syncthreads();
+  }
 #pragma unroll
   for (int f = 0; f < C::FC; ++f)
 #pragma unroll
@@ -217,11 +257,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
     char* sb = smem + st * C::STAGE;
     // input instruction i covers bytes [i*1024, +1024) of the stage (linear destination, swizzled
     // source chunk); without an addend every wave issues LPT, with one instruction i goes to wave i % 8
-    constexpr int NI = ADD ? (C::TI + 7) / 8 : C::LPT;
+    constexpr int NI = EXT ? (C::TI + 7) / 8 : C::LPT;
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int i = j * 8 + wid;
-      if (ADD && i >= C::TI) break;
+      if (EXT && i >= C::TI) break;
       const int byte = (i * 64 + lane) * 16;               // destination byte within the stage (linear)
       const int row = byte / C::ROWB;
       const int slot = (byte % C::ROWB) / 16;
@@ -241,9 +281,40 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
       const T* src = p < M ? addend + static_cast<int64_t>(p) * NT + slice * NOUT + (byte % (NOUT * 2)) / 2 : zero;
       __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sb + C::STAGE_IN + i * 1024), 16, 0, 0);
     }
+    // the BN input rows (same layout as the addend)
+#pragma unroll
+    for (int j = 0; j < (C::TZ + 7) / 8; ++j) {
+      const int i = j * 8 + wid;
+      if (i >= C::TZ) break;
+      const int byte = (i * 64 + lane) * 16;
+      const int row = byte / (NOUT * 2);
+      const int p = t * C::BM + row;
+      const T* src = p < M ? static_cast<const T*>(bnb.z) + static_cast<int64_t>(p) * NT + slice * NOUT +
+                                 (byte % (NOUT * 2)) / 2
+                           : zero;
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sb + C::STAGE_IN + C::STAGE_ADD + i * 1024), 16, 0,
+                                       0);
+    }
+    // the mask bytes of the tile's rows ([BM][NOUT / 8]; the stage's tail past them reads the zero page)
+#pragma unroll
+    for (int j = 0; j < (C::TM + 7) / 8; ++j) {
+      const int i = j * 8 + wid;
+      if (i >= C::TM) break;
+      const int byte = (i * 64 + lane) * 16;
+      const int row = byte / (NOUT / 8);
+      const int p = t * C::BM + row;
+      const void* src = (row < C::BM && p < M)
+                            ? static_cast<const void*>(bnb.mask + (static_cast<int64_t>(p) * NT + slice * NOUT) / 8 +
+                                                       byte % (NOUT / 8))
+                            : static_cast<const void*>(zero);
+      __builtin_amdgcn_global_load_lds((gbl_void*)src,
+                                       (lds_void*)(sb + C::STAGE_IN + C::STAGE_ADD + C::STAGE_Z + i * 1024), 16, 0, 0);
+    }
   };
   // LDS-DMA instructions this wave issues per tile (uniform over the wave)
-  const int ops_per_tile = ADD ? (C::TI - wid + 7) / 8 + (C::TA - wid + 7) / 8 : C::LPT;
+  const int ops_per_tile = EXT ? (C::TI - wid + 7) / 8 + (C::TA - wid + 7) / 8 + (C::TZ - wid + 7) / 8 +
+                                      (C::TM - wid + 7) / 8
+                                : C::LPT;
 
   const int my_tiles = wg < ntiles ? (ntiles - wg + gs - 1) / gs : 0;
   for (int j = 0; j < C::D && j < my_tiles; ++j) issue(wg + j * gs, j);
@@ -256,11 +327,20 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
   }
   const int my_c8 = tid % C::OCH;  // this thread's fixed output chunk (8 channels) in the epilogue
   char* epi = smem + C::NST * C::STAGE;
+  // BN-backward constants of this thread's 8 channels
+  float bmean[8], bsc[8], bsh[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int ch = slice * NOUT + my_c8 * 8 + q;
+    bmean[q] = BNB ? bnb.mean[ch] : 0.f;
+    bsc[q] = BNB == kPwBnbFromZ ? bnb.scale[ch] : 0.f;
+    bsh[q] = BNB == kPwBnbFromZ ? bnb.shift[ch] : 0.f;
+  }
 
   for (int it = 0; it < my_tiles; ++it) {
     const int t = wg + it * gs;
     const int st = it % C::NST;
-    if (!ADD) {
+    if (!EXT) {
       // issue tile it+D (into the stage freed by tile it-1, whose reads ended before the last barrier)
       if (it + C::D < my_tiles) issue(wg + (it + C::D) * gs, (it + C::D) % C::NST);
       // VM ops younger than tile it's DMA: the tiles issued after it, and the epilogue stores of the
@@ -335,6 +415,24 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
         for (int q = 0; q < 8; ++q) v.set(q, v.get(q) + a.get(q));
       }
       const bool live = in_tile && p < M;
+      if (BNB && live) {
+        Vec8<T> zv;
+        zv.raw = *reinterpret_cast<const uint4*>(sb + C::STAGE_IN + C::STAGE_ADD + pix * (NOUT * 2) + c8 * 16);
+        const uint32_t mb =
+            BNB == kPwBnbMask ? static_cast<uint32_t>(*reinterpret_cast<const uint8_t*>(
+                                    sb + C::STAGE_IN + C::STAGE_ADD + C::STAGE_Z + pix * (NOUT / 8) + c8))
+                              : 0xffu;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float zq = zv.get(q);
+          bool keep = true;
+          if (BNB == kPwBnbFromZ) keep = fmaf(zq, bsc[q], bsh[q]) > 0.f;
+          if (BNB == kPwBnbMask) keep = (mb >> q) & 1u;
+          const float dz = keep ? v.get(q) : 0.f;
+          s1[q] += dz;
+          s2[q] += dz * (zq - bmean[q]);
+        }
+      }
       const uint32_t off = live ? (static_cast<uint32_t>(p) * NT + slice * NOUT + c8 * 8) * sizeof(T) : 0xFFFFFFF0u;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v.raw), yrs, off, 0, 0);
       if (STATS && live) {
@@ -348,7 +446,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
     }
     (void)my_c8;
   }
-  if (STATS) {
+  if (STATS || BNB) {
     // every thread's chunk is fixed (tid % OCH): combine the 512/OCH threads of each chunk through
     // LDS, one partial per workgroup per channel
     vm_wait<0>();
@@ -371,35 +469,64 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
   }
 }
 
-template <typename T, int KIN, int NOUT, int WPC, int S, bool STATS, bool ADD>
+template <typename T, int KIN, int NOUT, int WPC, int S, bool STATS, bool ADD, int BNB = kPwBnbNone>
 void launch_pw_v(const void* x, const void* w, void* y, const void* zero, int M, float* part, const void* addend,
-                 int grid, hipStream_t s) {
-  using C = PwCfg<KIN, NOUT, WPC, ADD>;
+                 int grid, hipStream_t s, int wt, const PwBnb& bnb = PwBnb{}) {
+  using C = PwCfg<KIN, NOUT, WPC, ADD, BNB>;
+  static_assert(C::SMEM <= C::LDS && C::NST >= 2, "LDS budget / ring depth");
   static bool set = false;
   if (!set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD, WPC, S>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD, WPC, S, BNB>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
     set = true;
   }
   const int ntiles = (M + C::BM - 1) / C::BM;
-  hipLaunchKernelGGL((conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD, WPC, S>), dim3(grid), dim3(512), C::SMEM, s,
-                     static_cast<const T*>(x), static_cast<const T*>(w), static_cast<T*>(y),
-                     static_cast<const T*>(zero), M, ntiles, part, static_cast<const T*>(addend));
+  hipLaunchKernelGGL((conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD, WPC, S, BNB>), dim3(grid), dim3(512), C::SMEM,
+                     s, static_cast<const T*>(x), static_cast<const T*>(w), static_cast<T*>(y),
+                     static_cast<const T*>(zero), M, ntiles, part, static_cast<const T*>(addend), wt, bnb);
+}
+
+// BN-backward variants built: relu-from-z without an addend (a dgrad feeding BN+ReLU) and the
+// residual tail's mask with an addend (a tee dgrad feeding the previous block's tail)
+template <int KIN, int NOUT>
+constexpr bool pw_bnb_built(bool add, int mode) {
+  return add ? (mode == kPwBnbMask && (NOUT / 8) % 16 == 0) : mode == kPwBnbFromZ;
+}
+
+template <typename T, int KIN, int NOUT, int S>
+bool launch_pw_bnb(const void* x, const void* w, void* y, const void* zero, int M, float* part, const void* addend,
+                   int grid, hipStream_t s, int wt, const PwBnb& bnb, int mode) {
+  if constexpr ((NOUT / 8) % 16 == 0) {
+    if (addend && mode == kPwBnbMask) {
+      launch_pw_v<T, KIN, NOUT, 1, S, false, true, kPwBnbMask>(x, w, y, zero, M, part, addend, grid, s, wt, bnb);
+      return true;
+    }
+  }
+  if (!addend && mode == kPwBnbFromZ) {
+    launch_pw_v<T, KIN, NOUT, 1, S, false, false, kPwBnbFromZ>(x, w, y, zero, M, part, addend, grid, s, wt, bnb);
+    return true;
+  }
+  return false;
 }
 
 template <typename T, int KIN, int NOUT, int WPC, int S>
 void launch_pw(const void* x, const void* w, void* y, const void* zero, int M, float* part, const void* addend,
-               int grid, hipStream_t s) {
+               int grid, hipStream_t s, int wt, const PwBnb* bnb, int mode) {
+  if (bnb) {
+    MXAMD_HOST_CHECK((launch_pw_bnb<T, KIN, NOUT, S>(x, w, y, zero, M, part, addend, grid, s, wt, *bnb, mode)),
+                     "conv_pw_stream: BN-backward variant not built");
+    return;
+  }
   using C = PwCfg<KIN, NOUT, WPC>;
   using CA = PwCfg<KIN, NOUT, 1, true>;
   static_assert(C::SMEM <= C::LDS && CA::SMEM <= CA::LDS, "workgroups per CU");
   static_assert(C::NST >= 2 && CA::NST >= 2, "ring depth");
   if (part) {
-    if (addend) launch_pw_v<T, KIN, NOUT, 1, S, true, true>(x, w, y, zero, M, part, addend, grid, s);
-    else launch_pw_v<T, KIN, NOUT, WPC, S, true, false>(x, w, y, zero, M, part, addend, grid, s);
+    if (addend) launch_pw_v<T, KIN, NOUT, 1, S, true, true>(x, w, y, zero, M, part, addend, grid, s, wt);
+    else launch_pw_v<T, KIN, NOUT, WPC, S, true, false>(x, w, y, zero, M, part, addend, grid, s, wt);
   } else {
-    if (addend) launch_pw_v<T, KIN, NOUT, 1, S, false, true>(x, w, y, zero, M, part, addend, grid, s);
-    else launch_pw_v<T, KIN, NOUT, WPC, S, false, false>(x, w, y, zero, M, part, addend, grid, s);
+    if (addend) launch_pw_v<T, KIN, NOUT, 1, S, false, true>(x, w, y, zero, M, part, addend, grid, s, wt);
+    else launch_pw_v<T, KIN, NOUT, WPC, S, false, false>(x, w, y, zero, M, part, addend, grid, s, wt);
   }
 }
 
@@ -413,10 +540,10 @@ void launch_pw(const void* x, const void* w, void* y, const void* zero, int M, f
 
 template <typename T>
 bool dispatch_pw(int kin, int nout, const void* x, const void* w, void* y, const void* zero, int M, float* part,
-                 const void* addend, int grid, hipStream_t s) {
+                 const void* addend, int grid, hipStream_t s, int wt, const PwBnb* bnb, int mode) {
 #define MXAMD_PW_CASE(K, N, W, SL)                                        \
   if (kin == K && nout == N * SL) {                                       \
-    launch_pw<T, K, N, W, SL>(x, w, y, zero, M, part, addend, grid, s);   \
+    launch_pw<T, K, N, W, SL>(x, w, y, zero, M, part, addend, grid, s, wt, bnb, mode); \
     return true;                                                          \
   }
   MXAMD_PW_SHAPES(MXAMD_PW_CASE)
@@ -446,6 +573,16 @@ int conv_pw_stream_slices(int kin, int nout) {
   return 0;
 }
 
+// Whether a BN-backward statistics epilogue is built for (Cin, Cout, addend, mode).
+int conv_pw_stream_bnb_ok(int kin, int nout, int add, int mode) {
+#define MXAMD_PW_BOK(K, N, W, SL) \
+  if (kin == K && nout == N * SL) return pw_bnb_built<K, N>(add != 0, mode) ? 1 : 0;
+  MXAMD_PW_SHAPES(MXAMD_PW_BOK)
+#undef MXAMD_PW_BOK
+  return 0;
+}
+
+// add: the launch streams an extra tensor (addend and / or BN-backward input): 1 workgroup per CU
 int conv_pw_stream_grid(int M, int kin, int nout, int ncu, int add) {
   const int sl = conv_pw_stream_slices(kin, nout);
   if (sl == 0) return 0;
@@ -458,14 +595,25 @@ int conv_pw_stream_grid(int M, int kin, int nout, int ncu, int add) {
 }
 
 void conv_pw_stream(int dtype, const void* x, const void* w, void* y, const void* zero, int M, int kin, int nout,
-                    float* part, int grid, hipStream_t s, const void* addend) {
+                    float* part, int grid, hipStream_t s, const void* addend, int wt, const void* bn_z,
+                    const uint8_t* bn_mask, const float* bn_mean, const float* bn_scale, const float* bn_shift,
+                    int bn_mode) {
   MXAMD_HOST_CHECK(conv_pw_stream_ok(kin, nout), "conv_pw_stream: unsupported (Cin, Cout)");
   MXAMD_HOST_CHECK(grid >= 1 && grid % conv_pw_stream_slices(kin, nout) == 0 &&
                    (int64_t)M * nout * 2 < (1ll << 31) - 64 && (int64_t)M * kin < (1ll << 31),
                    "conv_pw_stream: tensor too large for 32-bit offsets");
+  PwBnb bnb{bn_z, bn_mask, bn_mean, bn_scale, bn_shift};
+  const PwBnb* pb = nullptr;
+  if (bn_z) {
+    MXAMD_HOST_CHECK(part && bn_mean && conv_pw_stream_bnb_ok(kin, nout, addend != nullptr, bn_mode) &&
+                         (bn_mode != kPwBnbFromZ || (bn_scale && bn_shift)) && (bn_mode != kPwBnbMask || bn_mask),
+                     "conv_pw_stream: BN-backward statistics need partials, mean, a built mode and its mask source");
+    pb = &bnb;
+  }
   bool ok = false;
-  if (dtype == kF16) ok = dispatch_pw<__half>(kin, nout, x, w, y, zero, M, part, addend, grid, s);
-  else if (dtype == kBF16) ok = dispatch_pw<__hip_bfloat16>(kin, nout, x, w, y, zero, M, part, addend, grid, s);
+  if (dtype == kF16) ok = dispatch_pw<__half>(kin, nout, x, w, y, zero, M, part, addend, grid, s, wt, pb, bn_mode);
+  else if (dtype == kBF16)
+    ok = dispatch_pw<__hip_bfloat16>(kin, nout, x, w, y, zero, M, part, addend, grid, s, wt, pb, bn_mode);
   MXAMD_HOST_CHECK(ok, "conv_pw_stream: dtype must be f16 or bf16");
 }
 

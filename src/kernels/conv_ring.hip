@@ -29,6 +29,7 @@
 #include <stdexcept>
 
 #include "common.h"
+#include "mfma.h"
 
 namespace mxamd {
 
@@ -42,31 +43,11 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void gbl_void;
 
+// 16x16x32 MFMA (mfma.h); the epilogue keeps its packed pairs in a native 2-vector
 template <typename T>
-struct MfmaR;
-template <>
-struct MfmaR<__half> {
-  static __device__ __forceinline__ f4_t run(const u32x4& a, const u32x4& b, f4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8_t, a), __builtin_bit_cast(half8_t, b), c,
-                                                  0, 0, 0);
-  }
+struct MfmaR : mfma::Op<T> {
   static __device__ __forceinline__ u32x2 pack4(float a, float b, float c, float d) {
-    __half2 lo = __floats2half2_rn(a, b), hi = __floats2half2_rn(c, d);
-    return u32x2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
-  }
-};
-template <>
-struct MfmaR<__hip_bfloat16> {
-  static __device__ __forceinline__ f4_t run(const u32x4& a, const u32x4& b, f4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
-                                                   c, 0, 0, 0);
-  }
-  static __device__ __forceinline__ uint32_t two(float a, float b) {
-    return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, __float2bfloat16(a))) |
-           (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, __float2bfloat16(b))) << 16);
-  }
-  static __device__ __forceinline__ u32x2 pack4(float a, float b, float c, float d) {
-    return u32x2{two(a, b), two(c, d)};
+    return u32x2{mfma::Op<T>::two(a, b), mfma::Op<T>::two(c, d)};
   }
 };
 

@@ -28,6 +28,7 @@
 #include <stdexcept>
 
 #include "common.h"
+#include "mfma.h"
 
 namespace mxamd {
 
@@ -39,28 +40,7 @@ typedef float f4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 template <typename T>
-struct StemMfma;
-template <>
-struct StemMfma<__half> {
-  static __device__ __forceinline__ f4_t run(const u32x4& a, const u32x4& b, f4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8_t, a), __builtin_bit_cast(half8_t, b), c,
-                                                  0, 0, 0);
-  }
-  static __device__ __forceinline__ uint32_t two(float a, float b) {
-    return __builtin_bit_cast(uint32_t, __floats2half2_rn(a, b));
-  }
-};
-template <>
-struct StemMfma<__hip_bfloat16> {
-  static __device__ __forceinline__ f4_t run(const u32x4& a, const u32x4& b, f4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
-                                                   c, 0, 0, 0);
-  }
-  static __device__ __forceinline__ uint32_t two(float a, float b) {
-    return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, __float2bfloat16(a))) |
-           (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, __float2bfloat16(b))) << 16);
-  }
-};
+struct StemMfma : mfma::Op<T> {};   // 16x16x32 MFMA + epilogue packs (mfma.h)
 
 struct StemGeom {
   int N, H, W, C, K, R, S;

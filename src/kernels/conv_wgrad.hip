@@ -34,6 +34,7 @@
 #include <stdexcept>
 
 #include "common.h"
+#include "mfma.h"
 
 namespace mxamd {
 
@@ -64,21 +65,7 @@ inline FastDiv make_fastdiv(uint32_t d) {
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) { return (__umulhi(n, f.m) + n) >> f.s; }
 
 template <typename T>
-struct Mfma16;
-template <>
-struct Mfma16<__half> {
-  static __device__ __forceinline__ f4_t run(v8s a, v8s b, f4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8_t, a), __builtin_bit_cast(half8_t, b), c,
-                                                  0, 0, 0);
-  }
-};
-template <>
-struct Mfma16<__hip_bfloat16> {
-  static __device__ __forceinline__ f4_t run(v8s a, v8s b, f4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
-                                                   c, 0, 0, 0);
-  }
-};
+struct Mfma16 : mfma::Op<T> {};   // 16x16x32 MFMA (mfma.h)
 
 struct WgradGeom {
   int N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw;

@@ -25,6 +25,7 @@
 #include <stdexcept>
 
 #include "common.h"
+#include "mfma.h"
 
 namespace mxamd {
 
@@ -38,47 +39,7 @@ typedef __attribute__((address_space(3))) void g_lds_void;
 typedef __attribute__((address_space(1))) void g_gbl_void;
 
 template <typename T>
-struct GMfma;
-template <>
-struct GMfma<__half> {
-  static __device__ __forceinline__ g_f4 run(const g_u32x4& a, const g_u32x4& b, g_f4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(g_half8, a), __builtin_bit_cast(g_half8, b), c,
-                                                  0, 0, 0);
-  }
-  static __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
-    __half2 lo = __floats2half2_rn(a, b), hi = __floats2half2_rn(c, d);
-    uint2 r;
-    r.x = *reinterpret_cast<uint32_t*>(&lo);
-    r.y = *reinterpret_cast<uint32_t*>(&hi);
-    return r;
-  }
-  static __device__ __forceinline__ float4 unpack4(uint2 v) {
-    __half2 lo = *reinterpret_cast<__half2*>(&v.x), hi = *reinterpret_cast<__half2*>(&v.y);
-    float2 a = __half22float2(lo), b = __half22float2(hi);
-    return make_float4(a.x, a.y, b.x, b.y);
-  }
-};
-template <>
-struct GMfma<__hip_bfloat16> {
-  static __device__ __forceinline__ g_f4 run(const g_u32x4& a, const g_u32x4& b, g_f4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(g_bf16x8, a), __builtin_bit_cast(g_bf16x8, b),
-                                                   c, 0, 0, 0);
-  }
-  static __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
-    __hip_bfloat16 h0 = __float2bfloat16(a), h1 = __float2bfloat16(b), h2 = __float2bfloat16(c),
-                   h3 = __float2bfloat16(d);
-    uint2 r;
-    r.x = static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h0)) |
-          (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h1)) << 16);
-    r.y = static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h2)) |
-          (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h3)) << 16);
-    return r;
-  }
-  static __device__ __forceinline__ float4 unpack4(uint2 v) {
-    return make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u), __uint_as_float(v.y << 16),
-                       __uint_as_float(v.y & 0xffff0000u));
-  }
-};
+struct GMfma : mfma::Op<T> {};   // 16x16x32 MFMA + epilogue packs (mfma.h)
 
 enum GemmAct : int { kActNone = 0, kActRelu = 1, kActGelu = 2 };
 

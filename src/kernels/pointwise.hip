@@ -204,7 +204,61 @@ void binary_dispatch(int op, const T* a, const T* b, T* out, int64_t n, int mode
   }
 }
 
+
+// ------------------------------------------------------------------------ weight tap transposes
+// out[base[z] + c * rstride[z] + k] = w[k][src[z]][c] for every slot z: the flipped / transposed
+// [Cin][taps][Cout] weight of a data-gradient conv (and the per-phase tap subsets of a strided one) in
+// ONE launch per weight, instead of a flip kernel plus a permute copy (or an int64 index gather).
+constexpr int kTapMax = 32;
+struct TapTable {
+  int src[kTapMax];
+  int64_t base[kTapMax];
+  int64_t rstride[kTapMax];
+};
+
+template <typename E>
+__global__ void __launch_bounds__(256) weight_taps_t_kernel(const E* __restrict__ w, E* __restrict__ out, int K, int RS,
+                                                            int C, TapTable tt) {
+  __shared__ E tile[64][65];
+  const int z = blockIdx.z;
+  const int k0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int src = tt.src[z];
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int kk = i >> 6, cc = i & 63;
+    const int k = k0 + kk, c = c0 + cc;
+    if (k < K && c < C) tile[kk][cc] = w[(static_cast<int64_t>(k) * RS + src) * C + c];
+  }
+  __syncthreads();
+  const int64_t base = tt.base[z], rs = tt.rstride[z];
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int cc = i >> 6, kk = i & 63;
+    const int k = k0 + kk, c = c0 + cc;
+    if (k < K && c < C) out[base + static_cast<int64_t>(c) * rs + k] = tile[kk][cc];
+  }
+}
+
 }  // namespace
+
+void weight_taps_t(int elem_bytes, const void* w, void* out, int K, int RS, int C, int n, const int* src,
+                   const int64_t* base, const int64_t* rstride, hipStream_t s) {
+  MXAMD_HOST_CHECK(n >= 1 && n <= kTapMax, "weight_taps_t: 1..32 tap slots");
+  TapTable tt{};
+  for (int z = 0; z < n; ++z) {
+    MXAMD_HOST_CHECK(src[z] >= 0 && src[z] < RS, "weight_taps_t: tap index out of range");
+    tt.src[z] = src[z];
+    tt.base[z] = base[z];
+    tt.rstride[z] = rstride[z];
+  }
+  const dim3 grid((C + 63) / 64, (K + 63) / 64, n);
+  if (elem_bytes == 2)
+    hipLaunchKernelGGL(weight_taps_t_kernel<uint16_t>, grid, dim3(256), 0, s, static_cast<const uint16_t*>(w),
+                       static_cast<uint16_t*>(out), K, RS, C, tt);
+  else if (elem_bytes == 4)
+    hipLaunchKernelGGL(weight_taps_t_kernel<uint32_t>, grid, dim3(256), 0, s, static_cast<const uint32_t*>(w),
+                       static_cast<uint32_t*>(out), K, RS, C, tt);
+  else
+    throw std::runtime_error("weight_taps_t: 2- or 4-byte elements");
+}
 
 void relu_forward(int dtype, const void* x, void* y, int64_t n, hipStream_t s) {
   const unsigned blocks = pw_blocks(n / 8 + 1);

@@ -21,6 +21,7 @@
 #include <stdexcept>
 
 #include "common.h"
+#include "mfma.h"
 
 namespace mxamd {
 
@@ -72,8 +73,7 @@ struct RFrag<__half> {
     return load8(row, k0 + (lane >> 4) * 8, K, ok, al);
   }
   static __device__ __forceinline__ f4_t mma(const frag& a, const frag& b, f4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8_t, a), __builtin_bit_cast(half8_t, b), c,
-                                                  0, 0, 0);
+    return mfma::Op<__half>::run(a, b, c);
   }
   static __device__ __forceinline__ __half from(float v) { return __float2half(v); }
   static __device__ __forceinline__ float to(__half v) { return __half2float(v); }
@@ -87,8 +87,7 @@ struct RFrag<__hip_bfloat16> {
     return load8(row, k0 + (lane >> 4) * 8, K, ok, al);
   }
   static __device__ __forceinline__ f4_t mma(const frag& a, const frag& b, f4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
-                                                   c, 0, 0, 0);
+    return mfma::Op<__hip_bfloat16>::run(a, b, c);
   }
   static __device__ __forceinline__ __hip_bfloat16 from(float v) { return __float2bfloat16(v); }
   static __device__ __forceinline__ float to(__hip_bfloat16 v) { return __bfloat162float(v); }

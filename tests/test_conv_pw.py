@@ -71,3 +71,85 @@ def test_tee_dgrad_pw_candidate_matches_mm():
     y = KF.conv_pw(gy, w.reshape(K, C).t(), addend=gpass)
     ref = gy.float().reshape(-1, K) @ w.float().reshape(K, C) + gpass.float().reshape(-1, C)
     assert float((y.float().reshape(-1, C) - ref).abs().max()) < 2e-2
+
+
+@pytest.mark.parametrize('kin,nout,M,dt', [(64, 256, 3136 + 40, torch.float16), (256, 64, 2000, torch.bfloat16),
+                                           (64, 64, 777, torch.float16), (512, 128, 1568, torch.float16),
+                                           (128, 512, 1600, torch.float16), (512, 256, 900, torch.bfloat16),
+                                           (256, 1024, 1700, torch.float16), (512, 2048, 300, torch.float16),
+                                           (1024, 256, 500, torch.bfloat16)])
+@pytest.mark.parametrize('add', [False, True])
+def test_conv_pw_transposed_weight_view(kin, nout, M, dt, add):
+    """A dgrad passes w2 as the transpose of a contiguous [Cin][Cout] weight; the kernel transposes it
+    while loading its resident fragments and must equal the run on the materialised transpose."""
+    dev = torch.device('cuda', 0)
+    g = torch.Generator().manual_seed(5 * kin + nout)
+    x = (torch.rand(M, kin, generator=g) * 2 - 1).to(dev, dt).view(1, 1, M, kin)
+    wk = ((torch.rand(kin, nout, generator=g) * 2 - 1) / kin ** 0.5).to(dev, dt)   # [Cin][Cout]
+    a = (torch.rand(M, nout, generator=g) * 2 - 1).to(dev, dt).view(1, 1, M, nout) if add else None
+    y_view = KF.conv_pw(x, wk.t(), addend=a)
+    y_copy = KF.conv_pw(x, wk.t().contiguous(), addend=a)
+    assert torch.equal(y_view, y_copy)
+    ref = x.float().reshape(M, kin) @ wk.float() + (a.float().reshape(M, nout) if add else 0)
+    err = float((y_view.float().reshape(M, nout) - ref).norm() / ref.norm())
+    assert err < 1e-2, err
+
+
+def _bnb_ref(y, z, mean, scale=None, shift=None, mask=None):
+    yf, zf = y.float().reshape(-1, y.shape[-1]), z.float().reshape(-1, z.shape[-1])
+    if mask is not None:
+        bits = ((mask.view(-1, 1).int() >> torch.arange(8, device=y.device)) & 1).reshape(yf.shape)
+        keep = bits.bool()
+    else:
+        keep = zf * scale + shift > 0
+    dz = torch.where(keep, yf, torch.zeros_like(yf))
+    return dz.sum(0), (dz * (zf - mean)).sum(0)
+
+
+@pytest.mark.parametrize('kin,nout,M,dt', [(512, 128, 3000, torch.float16), (256, 64, 2001, torch.bfloat16),
+                                           (512, 256, 1568, torch.float16), (128, 128, 777, torch.float16)])
+def test_conv_pw_bn_backward_stats_from_z(kin, nout, M, dt):
+    """dgrad feeding BN+ReLU: the epilogue's (sum dz, sum dz*(z-mean)) partials, the ReLU mask recomputed
+    from the BN input z and the forward's scale/shift; the output itself is unchanged."""
+    dev = torch.device('cuda', 0)
+    g = torch.Generator().manual_seed(7 * kin + nout)
+    x = (torch.rand(M, kin, generator=g) * 2 - 1).to(dev, dt).view(1, 1, M, kin)
+    wk = ((torch.rand(kin, nout, generator=g) * 2 - 1) / kin ** 0.5).to(dev, dt)
+    z = (torch.rand(M, nout, generator=g) * 2 - 1).to(dev, dt).view(1, 1, M, nout)
+    mean = (torch.rand(nout, generator=g) * 0.2 - 0.1).to(dev)
+    scale = (torch.rand(nout, generator=g) + 0.5).to(dev)
+    shift = (torch.rand(nout, generator=g) - 0.5).to(dev)
+    assert KF.pw_bnb_ok(kin, nout, False, (z, mean, scale, shift, None, 2, None))
+    y = KF.conv_pw(x, wk.t(), bn_bwd=(z, mean, scale, shift, None, 2, 'tok'))
+    assert torch.equal(y, KF.conv_pw(x, wk.t()))
+    part, nparts, tok, ver = y._mxamd_bn_bwd
+    assert tok == 'tok' and ver == y._version
+    s1, s2 = part.view(2, nout, nparts).sum(-1)
+    r1, r2 = _bnb_ref(y, z, mean, scale, shift)
+    torch.testing.assert_close(s1, r1, rtol=1e-3, atol=1e-2 * float(r1.abs().max() + 1))
+    torch.testing.assert_close(s2, r2, rtol=1e-3, atol=1e-2 * float(r2.abs().max() + 1))
+
+
+@pytest.mark.parametrize('kin,nout,M,dt', [(128, 256, 3136 + 5, torch.float16), (128, 512, 1600, torch.bfloat16),
+                                           (256, 512, 1000, torch.float16), (256, 1024, 1568 + 3, torch.float16),
+                                           (512, 2048, 200, torch.bfloat16)])
+def test_conv_pw_tee_bn_backward_stats_mask(kin, nout, M, dt):
+    """Tee dgrad feeding the previous block's residual tail: y = conv + addend, with the tail's backward
+    statistics from its 1-bit forward ReLU mask."""
+    dev = torch.device('cuda', 0)
+    g = torch.Generator().manual_seed(11 * kin + nout)
+    x = (torch.rand(M, kin, generator=g) * 2 - 1).to(dev, dt).view(1, 1, M, kin)
+    wk = ((torch.rand(kin, nout, generator=g) * 2 - 1) / kin ** 0.5).to(dev, dt)
+    a = (torch.rand(M, nout, generator=g) * 2 - 1).to(dev, dt).view(1, 1, M, nout)
+    z = (torch.rand(M, nout, generator=g) * 2 - 1).to(dev, dt).view(1, 1, M, nout)
+    mask = torch.randint(0, 256, (M * nout // 8,), generator=g, dtype=torch.int32).to(torch.uint8).to(dev)
+    mean = (torch.rand(nout, generator=g) * 0.2 - 0.1).to(dev)
+    src = (z, mean, None, None, mask, 3, 'tok')
+    assert KF.pw_bnb_ok(kin, nout, True, src)
+    y = KF.conv_pw(x, wk.t(), addend=a, bn_bwd=src)
+    assert torch.equal(y, KF.conv_pw(x, wk.t(), addend=a))
+    part, nparts, _tok, _ver = y._mxamd_bn_bwd
+    s1, s2 = part.view(2, nout, nparts).sum(-1)
+    r1, r2 = _bnb_ref(y, z, mean, mask=mask)
+    torch.testing.assert_close(s1, r1, rtol=1e-3, atol=1e-2 * float(r1.abs().max() + 1))
+    torch.testing.assert_close(s2, r2, rtol=1e-3, atol=1e-2 * float(r2.abs().max() + 1))

@@ -85,9 +85,8 @@ def test_registered_ops_run_the_kernel():
 
 @pytest.mark.parametrize('M,N,dt', [(4096, 768, torch.bfloat16), (333, 3072, torch.float16), (64, 8, torch.float32),
                                     (20000, 1024, torch.bfloat16)])
-def test_bias_grad_single_launch_colsum(M, N, dt):
-    """Bias gradient column sums in one launch (last block of each strip finalises), repeated so the
-    self-resetting strip counters are exercised."""
+def test_bias_grad_colsum(M, N, dt):
+    """Bias gradient column sums (partial rows + their sum), repeated on the shared scratch."""
     from mxnet_maintenance_amd.ops import nlp_fns
     g = torch.Generator().manual_seed(M + N)
     dy = (torch.rand(M, N, generator=g) * 2 - 1).to('cuda', dt)
@@ -95,3 +94,29 @@ def test_bias_grad_single_launch_colsum(M, N, dt):
     for _ in range(3):
         out = nlp_fns.bias_grad(dy, None, torch.float32)
         torch.testing.assert_close(out.float(), ref, rtol=1e-3, atol=1e-2 * (M ** 0.5) / 10)
+
+
+@pytest.mark.parametrize('shape,dt', [((64, 3, 3, 64), torch.float16), ((256, 3, 3, 128), torch.bfloat16),
+                                      ((96, 5, 3, 40), torch.float32), ((512, 1, 1, 2048), torch.float16)])
+def test_dgrad_weight_tap_transpose(shape, dt):
+    """The flipped [Cin][R][S][Cout] data-gradient weight from the tap-transpose kernel equals torch's
+    flip + permute."""
+    w = torch.randn(shape, device='cuda').to(dt)
+    assert torch.equal(K._dgrad_weight(w), w.flip(1, 2).permute(3, 1, 2, 0).contiguous())
+
+
+@pytest.mark.parametrize('wshape,stride,pad', [((128, 3, 3, 64), (2, 2), (1, 1)), ((256, 1, 1, 128), (2, 2), (0, 0)),
+                                               ((64, 3, 3, 128), (2, 2), (1, 1))])
+def test_phase_weight_slices(wshape, stride, pad):
+    """The per-phase tap slices of a strided dgrad ([C][R_i][S_i][K], concatenated) built in one launch
+    equal the slices gathered on the host."""
+    w = torch.randn(wshape, device='cuda').to(torch.float16)
+    phases, _empty, (slots, total) = K._phase_plan(w.shape, stride, pad, w.device)
+    got = K._taps_t(w, torch.empty(total, dtype=w.dtype, device=w.device), [t[0] for t in slots],
+                    [t[1] for t in slots], [t[2] for t in slots])
+    Kc, R, S, C = wshape
+    for ph, pw, ri, si, _a, _b, off in phases:
+        rr = [r for _, r in K._phase_taps(R, pad[0], stride[0], ph)]
+        ss = [c for _, c in K._phase_taps(S, pad[1], stride[1], pw)]
+        ref = w[:, rr][:, :, ss].permute(3, 1, 2, 0).contiguous().reshape(-1)
+        assert torch.equal(got[off:off + ref.numel()], ref)

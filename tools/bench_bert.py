@@ -129,10 +129,12 @@ def main():
             'config': {'model': args.model, 'per_gpu_batch': B, 'seq_len': S, 'masked_positions': P,
                        'optimizer': args.optimizer, 'parallelism': 'dp%d' % n, 'hip_graph': args.graph,
                        'final_loss': round(float(last.asscalar()), 4)}}), flush=True)
-    if args.trace_loss:
+    if args.trace_loss or os.environ.get('MXAMD_BENCH_VERBOSE', '0') == '1':
         from mxnet_maintenance_amd.ops import kernel_fns
+        times = kernel_fns.conv_algo_times()
         for k, v in sorted(kernel_fns._ALGO.items(), key=str):
-            print('algo', v, k, file=sys.stderr)
+            t = ' '.join('%s=%.3f' % (n, ms) for n, ms in sorted(times.get(k, {}).items(), key=lambda z: z[1]))
+            print('algo', v, k, t, file=sys.stderr)
     if dist.world_size() > 1:
         torch.distributed.destroy_process_group()
 
