@@ -237,6 +237,46 @@ __global__ void __launch_bounds__(256) weight_taps_t_kernel(const E* __restrict_
   }
 }
 
+// 16-byte version (K, C, every base and row stride multiples of 8 halves): two vector loads per lane
+// issued together, an LDS transpose, two vector stores -- the scalar loop above is load-latency bound
+__global__ void __launch_bounds__(256) weight_taps_t_vec_kernel(const uint16_t* __restrict__ w,
+                                                                uint16_t* __restrict__ out, int K, int RS, int C,
+                                                                TapTable tt) {
+  __shared__ __attribute__((aligned(16))) uint16_t tile[64][72];
+  const int z = blockIdx.z;
+  const int k0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int src = tt.src[z];
+  const int tid = threadIdx.x;
+  uint4 r[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int v = tid + i * 256;
+    const int k = k0 + (v >> 3), c = c0 + (v & 7) * 8;
+    r[i] = (k < K && c < C) ? *reinterpret_cast<const uint4*>(w + (static_cast<int64_t>(k) * RS + src) * C + c)
+                            : uint4{0u, 0u, 0u, 0u};
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int v = tid + i * 256;
+    *reinterpret_cast<uint4*>(&tile[v >> 3][(v & 7) * 8]) = r[i];
+  }
+  __syncthreads();
+  const int64_t base = tt.base[z], rs = tt.rstride[z];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int v = tid + i * 256;
+    const int cc = v >> 3, kv = (v & 7) * 8;
+    const int c = c0 + cc, k = k0 + kv;
+    if (c < C && k < K) {
+      uint32_t q[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        q[j] = static_cast<uint32_t>(tile[kv + 2 * j][cc]) | (static_cast<uint32_t>(tile[kv + 2 * j + 1][cc]) << 16);
+      *reinterpret_cast<uint4*>(out + base + static_cast<int64_t>(c) * rs + k) = uint4{q[0], q[1], q[2], q[3]};
+    }
+  }
+}
+
 }  // namespace
 
 void weight_taps_t(int elem_bytes, const void* w, void* out, int K, int RS, int C, int n, const int* src,
@@ -250,7 +290,13 @@ void weight_taps_t(int elem_bytes, const void* w, void* out, int K, int RS, int 
     tt.rstride[z] = rstride[z];
   }
   const dim3 grid((C + 63) / 64, (K + 63) / 64, n);
-  if (elem_bytes == 2)
+  bool vec = elem_bytes == 2 && K % 8 == 0 && C % 8 == 0 && reinterpret_cast<uintptr_t>(w) % 16 == 0 &&
+             reinterpret_cast<uintptr_t>(out) % 16 == 0;
+  for (int z = 0; z < n && vec; ++z) vec = base[z] % 8 == 0 && rstride[z] % 8 == 0;
+  if (vec)
+    hipLaunchKernelGGL(weight_taps_t_vec_kernel, grid, dim3(256), 0, s, static_cast<const uint16_t*>(w),
+                       static_cast<uint16_t*>(out), K, RS, C, tt);
+  else if (elem_bytes == 2)
     hipLaunchKernelGGL(weight_taps_t_kernel<uint16_t>, grid, dim3(256), 0, s, static_cast<const uint16_t*>(w),
                        static_cast<uint16_t*>(out), K, RS, C, tt);
   else if (elem_bytes == 4)

@@ -6,6 +6,12 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 
+def _relnorm(a, b):
+    """Relative error in the 2-norm, ||a - b|| / ||b|| (fp32)."""
+    a, b = a.detach().float().reshape(-1).cpu(), b.detach().float().reshape(-1).cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
 def _lib():
     from mxnet_maintenance_amd.ops import kernels
     assert kernels.available(), 'HIP kernel extension not loaded: %s' % kernels.load_error()
@@ -263,7 +269,7 @@ def test_conv_nhwc_autograd_matches_fp32(cfg):
     dxf, dwf = torch.autograd.grad(yf, (xf, wf), dy.float())
     torch.testing.assert_close(y.float(), yf, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(dx.float(), dxf, rtol=3e-2, atol=3e-2)
-    torch.testing.assert_close(dw.float(), dwf, rtol=5e-2, atol=5e-1)
+    assert _relnorm(dw, dwf) < 1e-2, _relnorm(dw, dwf)     # fp16 products summed over N*H*W pixels
 
 
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16, torch.float32])
@@ -359,7 +365,7 @@ def test_conv_tee_fused_shortcut_grad():
     dx_ref = (gy.float().reshape(-1, Cout) @ wf).view(x.shape) + gp.float()
     torch.testing.assert_close(x.grad.float(), dx_ref, rtol=2e-2, atol=3e-2)
     dw_ref = (gy.float().reshape(-1, Cout).t() @ xf.reshape(-1, Cin)).view(Cout, 1, 1, Cin) + 0.5
-    torch.testing.assert_close(w.grad.float(), dw_ref, rtol=2e-2, atol=2.0)
+    assert _relnorm(w.grad, dw_ref) < 1e-2, _relnorm(w.grad, dw_ref)
 
 
 @pytest.mark.parametrize('cfg', [(256, 256, 1, False), (256, 512, 2, True), (64, 256, 1, True)])
@@ -667,8 +673,8 @@ def test_conv_big_bn_stats_addend(dtype, cfg):
         torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
         part, nparts = y._mxamd_bn_part
         p = part.view(2, Cout, nparts)
-        torch.testing.assert_close(p[0].sum(1), ref.sum((0, 1, 2)), rtol=1e-2, atol=0.5)
-        torch.testing.assert_close(p[1].sum(1), (ref * ref).sum((0, 1, 2)), rtol=1e-2, atol=0.5)
+        assert _relnorm(p[0].sum(1), ref.sum((0, 1, 2))) < 1e-2
+        assert _relnorm(p[1].sum(1), (ref * ref).sum((0, 1, 2))) < 1e-2
         add = torch.randn_like(y)
         y2 = KF.conv_fwd(x, w, (s, s), (pad, pad), None, v, addend=add)
         torch.testing.assert_close(y2.float(), ref + add.float(), rtol=tol, atol=2 * tol)
@@ -709,8 +715,8 @@ def test_conv_ring_bn_stats(dtype, cfg):
         torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol, msg=lambda m: 'variant %d: %s' % (v, m))
         part, nparts = y._mxamd_bn_part
         p = part.view(2, Cout, nparts)
-        torch.testing.assert_close(p[0].sum(1), ref.sum((0, 1, 2)), rtol=1e-2, atol=0.5)
-        torch.testing.assert_close(p[1].sum(1), (ref * ref).sum((0, 1, 2)), rtol=1e-2, atol=0.5)
+        assert _relnorm(p[0].sum(1), ref.sum((0, 1, 2))) < 1e-2
+        assert _relnorm(p[1].sum(1), (ref * ref).sum((0, 1, 2))) < 1e-2
         y2 = KF.conv_fwd(x, w, (s, s), (pad, pad), None, v)
         assert torch.equal(y2, y)
 
@@ -765,7 +771,7 @@ def test_linear_direct_weight_and_bias_grads():
             y = net(x)
         y.backward()
     dy = np.ones((xs.shape[0], 256), np.float32)
-    np.testing.assert_allclose(net.weight.grad().asnumpy().astype(np.float32), dy.T @ xs, rtol=3e-2, atol=0.5)
+    assert _relnorm(torch.from_numpy(net.weight.grad().asnumpy().astype(np.float32)), torch.from_numpy(dy.T @ xs)) < 1e-2
     np.testing.assert_allclose(net.bias.grad().asnumpy().astype(np.float32), dy.sum(0), rtol=2e-2)
     assert w.shape == (256, 128)
 

@@ -97,7 +97,8 @@ def test_bias_grad_colsum(M, N, dt):
 
 
 @pytest.mark.parametrize('shape,dt', [((64, 3, 3, 64), torch.float16), ((256, 3, 3, 128), torch.bfloat16),
-                                      ((96, 5, 3, 40), torch.float32), ((512, 1, 1, 2048), torch.float16)])
+                                      ((96, 5, 3, 40), torch.float32), ((512, 1, 1, 2048), torch.float16),
+                                      ((60, 3, 3, 36), torch.float16), ((130, 3, 3, 72), torch.bfloat16)])
 def test_dgrad_weight_tap_transpose(shape, dt):
     """The flipped [Cin][R][S][Cout] data-gradient weight from the tap-transpose kernel equals torch's
     flip + permute."""
