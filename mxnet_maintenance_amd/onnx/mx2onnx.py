@@ -1,0 +1,654 @@
+"""Symbol (+ parameters) -> ONNX model (opset 13).
+
+Behaviour of the reference exporter (python/mxnet/onnx/mx2onnx/_export_model.py:51 ``export_model``,
+_export_onnx.py ``MXNetGraph.create_onnx_graph_proto``, _op_translations_opset13.py): the symbol's
+JSON graph is walked in topological order, parameter variables become initializers, the other
+variables graph inputs with the given shapes / dtypes, and every operator is translated by a
+registered converter into one or more ONNX nodes.  Attribute strings are parsed from the JSON
+(``"(3, 3)"``, ``"True"``...).  Shapes MXNet leaves to run time that ONNX needs constant (Reshape's
+special codes) come from this framework's shape inference of the node.
+"""
+import json
+
+import numpy as np
+
+from . import _proto as P
+
+_CONVERTERS = {}
+
+
+def register(*names):
+    def deco(fn):
+        for n in names:
+            _CONVERTERS[n] = fn
+        return fn
+    return deco
+
+
+def get_operator_support(opset_version=None):
+    """Operators this exporter translates (``opset_version`` accepted for API parity; opset 13 is
+    written)."""
+    return sorted(_CONVERTERS)
+
+
+# ---------------------------------------------------------------- attribute parsing
+def _tup(v, default=None):
+    if v is None:
+        return default
+    if isinstance(v, (list, tuple)):
+        return tuple(int(x) for x in v)
+    s = str(v).strip().strip('()[]')
+    if not s:
+        return ()
+    return tuple(int(float(x)) for x in s.split(',') if x.strip() not in ('', 'None'))
+
+
+def _ftup(v):
+    s = str(v).strip().strip('()[]')
+    return tuple(float(x) for x in s.split(',') if x.strip())
+
+
+def _bool(v, default=False):
+    if v is None:
+        return default
+    return str(v).strip() in ('True', 'true', '1')
+
+
+def _float(v, default):
+    return default if v is None or str(v) == 'None' else float(v)
+
+
+def _int(v, default):
+    return default if v is None or str(v) == 'None' else int(float(v))
+
+
+# ---------------------------------------------------------------- conversion context
+class _Ctx:
+    def __init__(self, sym, params, opset):
+        self.sym = sym
+        self.params = params
+        self.opset = opset
+        self.nodes = []
+        self.inits = {}
+        self._n = 0
+        self.shapes = {}
+
+    def uid(self, base):
+        self._n += 1
+        return '%s__%d' % (base, self._n)
+
+    def const(self, base, arr):
+        name = self.uid(base)
+        self.inits[name] = np.asarray(arr)
+        return name
+
+    def add(self, op_type, inputs, outputs, **attrs):
+        self.nodes.append(P.make_node(op_type, list(inputs), list(outputs), name=self.uid(outputs[0]), **attrs))
+
+    def param(self, name):
+        return self.inits.get(name)
+
+    def out_shape(self, node_name):
+        """Static shape of ``node_name``'s first output (from this framework's shape inference)."""
+        return self.shapes.get(node_name)
+
+
+def _scalar_const(ctx, base, v, dtype=np.float32):
+    return ctx.const(base, np.asarray(v, dtype=dtype))
+
+
+# ---------------------------------------------------------------- converters
+@register('Convolution')
+def _conv(ctx, name, a, ins, outs):
+    k = _tup(a.get('kernel'))
+    nd = len(k)
+    layout = a.get('layout')
+    if layout not in (None, 'None', 'NCHW', 'NCW', 'NCDHW'):
+        raise NotImplementedError('ONNX export: Convolution layout %s (ONNX Conv is channels-first)' % layout)
+    pad = _tup(a.get('pad'), (0,) * nd) or (0,) * nd
+    ins = ins[:2] if _bool(a.get('no_bias')) else ins
+    ctx.add('Conv', ins, outs, kernel_shape=list(k), strides=list(_tup(a.get('stride'), (1,) * nd) or (1,) * nd),
+            dilations=list(_tup(a.get('dilate'), (1,) * nd) or (1,) * nd), pads=list(pad) + list(pad),
+            group=_int(a.get('num_group'), 1))
+
+
+@register('Deconvolution')
+def _deconv(ctx, name, a, ins, outs):
+    k = _tup(a.get('kernel'))
+    nd = len(k)
+    pad = _tup(a.get('pad'), (0,) * nd) or (0,) * nd
+    ins = ins[:2] if _bool(a.get('no_bias'), True) else ins
+    ctx.add('ConvTranspose', ins, outs, kernel_shape=list(k),
+            strides=list(_tup(a.get('stride'), (1,) * nd) or (1,) * nd),
+            dilations=list(_tup(a.get('dilate'), (1,) * nd) or (1,) * nd), pads=list(pad) + list(pad),
+            output_padding=list(_tup(a.get('adj'), (0,) * nd) or (0,) * nd), group=_int(a.get('num_group'), 1))
+
+
+@register('FullyConnected')
+def _fc(ctx, name, a, ins, outs):
+    no_bias = _bool(a.get('no_bias'))
+    if _bool(a.get('flatten'), True):
+        flat = ctx.uid(name + '_flatten')
+        ctx.add('Flatten', [ins[0]], [flat], axis=1)
+        ctx.add('Gemm', [flat, ins[1]] + ([] if no_bias else [ins[2]]), outs, alpha=1.0, beta=1.0, transA=0, transB=1)
+        return
+    w = ctx.param(ins[1])
+    if w is not None:
+        wt = ctx.const(ins[1] + '_T', np.ascontiguousarray(w.T))
+    else:
+        wt = ctx.uid(ins[1] + '_T')
+        ctx.add('Transpose', [ins[1]], [wt], perm=[1, 0])
+    if no_bias:
+        ctx.add('MatMul', [ins[0], wt], outs)
+    else:
+        mm = ctx.uid(name + '_matmul')
+        ctx.add('MatMul', [ins[0], wt], [mm])
+        ctx.add('Add', [mm, ins[2]], outs)
+
+
+_ACT = {'relu': 'Relu', 'sigmoid': 'Sigmoid', 'tanh': 'Tanh', 'softrelu': 'Softplus', 'softsign': 'Softsign'}
+
+
+@register('Activation')
+def _act(ctx, name, a, ins, outs):
+    t = a.get('act_type')
+    if t not in _ACT:
+        raise NotImplementedError('ONNX export: Activation act_type=%s' % t)
+    ctx.add(_ACT[t], ins[:1], outs)
+
+
+def _gelu(ctx, name, x, outs):
+    d = ctx.uid(name + '_div')
+    ctx.add('Div', [x, _scalar_const(ctx, 'sqrt2', np.sqrt(2.0))], [d])
+    e = ctx.uid(name + '_erf')
+    ctx.add('Erf', [d], [e])
+    p = ctx.uid(name + '_plus1')
+    ctx.add('Add', [e, _scalar_const(ctx, 'one', 1.0)], [p])
+    m = ctx.uid(name + '_mul')
+    ctx.add('Mul', [x, p], [m])
+    ctx.add('Mul', [m, _scalar_const(ctx, 'half', 0.5)], outs)
+
+
+@register('LeakyReLU')
+def _leaky(ctx, name, a, ins, outs):
+    t = a.get('act_type', 'leaky')
+    slope = _float(a.get('slope'), 0.25)
+    if t == 'leaky':
+        ctx.add('LeakyRelu', ins[:1], outs, alpha=slope)
+    elif t == 'elu':
+        ctx.add('Elu', ins[:1], outs, alpha=slope)
+    elif t == 'selu':
+        ctx.add('Selu', ins[:1], outs, alpha=1.6732632423543772, gamma=1.0507009873554805)
+    elif t == 'gelu':
+        _gelu(ctx, name, ins[0], outs)
+    elif t == 'prelu':
+        g = ctx.param(ins[1])
+        if g is None:
+            raise NotImplementedError('ONNX export: prelu with a non-parameter slope')
+        shape = ctx.out_shape(name)
+        nd = len(shape) if shape else 4
+        slope_name = ctx.const(ins[1] + '_bcast', g.reshape((-1,) + (1,) * max(0, nd - 2)))
+        ctx.add('PRelu', [ins[0], slope_name], outs)
+    else:
+        raise NotImplementedError('ONNX export: LeakyReLU act_type=%s' % t)
+
+
+@register('BatchNorm', '_contrib_SyncBatchNorm')
+def _bn(ctx, name, a, ins, outs):
+    gamma = ins[1]
+    if _bool(a.get('fix_gamma'), True):
+        g = ctx.param(ins[1])
+        n = g.shape[0] if g is not None else None
+        if n is None:
+            raise NotImplementedError('ONNX export: fix_gamma BatchNorm needs gamma as a parameter')
+        gamma = ctx.const(ins[1] + '_ones', np.ones(n, dtype=np.float32))
+    ctx.add('BatchNormalization', [ins[0], gamma, ins[2], ins[3], ins[4]], outs[:1],
+            epsilon=_float(a.get('eps'), 1e-3), momentum=_float(a.get('momentum'), 0.9))
+
+
+@register('InstanceNorm')
+def _inorm(ctx, name, a, ins, outs):
+    ctx.add('InstanceNormalization', ins[:3], outs, epsilon=_float(a.get('eps'), 1e-3))
+
+
+@register('LayerNorm')
+def _lnorm(ctx, name, a, ins, outs):
+    axis = _int(a.get('axis'), -1)
+    eps = _float(a.get('eps'), 1e-5)
+    m = ctx.uid(name + '_mean')
+    ctx.add('ReduceMean', [ins[0]], [m], axes=[axis], keepdims=1)
+    d = ctx.uid(name + '_centered')
+    ctx.add('Sub', [ins[0], m], [d])
+    sq = ctx.uid(name + '_sq')
+    ctx.add('Mul', [d, d], [sq])
+    v = ctx.uid(name + '_var')
+    ctx.add('ReduceMean', [sq], [v], axes=[axis], keepdims=1)
+    ve = ctx.uid(name + '_var_eps')
+    ctx.add('Add', [v, _scalar_const(ctx, 'eps', eps)], [ve])
+    sd = ctx.uid(name + '_std')
+    ctx.add('Sqrt', [ve], [sd])
+    nrm = ctx.uid(name + '_norm')
+    ctx.add('Div', [d, sd], [nrm])
+    sc = ctx.uid(name + '_scaled')
+    ctx.add('Mul', [nrm, ins[1]], [sc])
+    ctx.add('Add', [sc, ins[2]], outs[:1])
+
+
+@register('Pooling')
+def _pool(ctx, name, a, ins, outs):
+    ptype = a.get('pool_type', 'max')
+    if _bool(a.get('global_pool')):
+        op = {'max': 'GlobalMaxPool', 'avg': 'GlobalAveragePool'}.get(ptype)
+        if op is None:
+            raise NotImplementedError('ONNX export: global %s pooling' % ptype)
+        ctx.add(op, ins[:1], outs)
+        return
+    k = _tup(a.get('kernel'))
+    nd = len(k)
+    pad = _tup(a.get('pad'), (0,) * nd) or (0,) * nd
+    kw = dict(kernel_shape=list(k), strides=list(_tup(a.get('stride'), (1,) * nd) or (1,) * nd),
+              pads=list(pad) + list(pad), ceil_mode=int(a.get('pooling_convention', 'valid') == 'full'))
+    if ptype == 'max':
+        ctx.add('MaxPool', ins[:1], outs, **kw)
+    elif ptype == 'avg':
+        ctx.add('AveragePool', ins[:1], outs, count_include_pad=int(_bool(a.get('count_include_pad'), True)), **kw)
+    elif ptype == 'lp':
+        ctx.add('LpPool', ins[:1], outs, p=_int(a.get('p_value'), 2), **{k_: v for k_, v in kw.items()
+                                                                         if k_ != 'ceil_mode'})
+    else:
+        raise NotImplementedError('ONNX export: pool_type %s' % ptype)
+
+
+_BINARY = {'elemwise_add': 'Add', '_plus': 'Add', '_Plus': 'Add', 'broadcast_add': 'Add', '_add': 'Add',
+           'broadcast_plus': 'Add', 'elemwise_sub': 'Sub', '_minus': 'Sub', '_Minus': 'Sub', 'broadcast_sub': 'Sub',
+           '_sub': 'Sub', 'broadcast_minus': 'Sub', 'elemwise_mul': 'Mul', '_mul': 'Mul', '_Mul': 'Mul',
+           'broadcast_mul': 'Mul', 'elemwise_div': 'Div', '_div': 'Div', '_Div': 'Div', 'broadcast_div': 'Div',
+           '_maximum': 'Max', 'broadcast_maximum': 'Max', '_minimum': 'Min', 'broadcast_minimum': 'Min',
+           '_power': 'Pow', 'broadcast_power': 'Pow', '_equal': 'Equal', 'broadcast_equal': 'Equal',
+           '_greater': 'Greater', 'broadcast_greater': 'Greater', '_lesser': 'Less', 'broadcast_lesser': 'Less'}
+
+
+def _binary(op):
+    def conv(ctx, name, a, ins, outs):
+        ctx.add(op, ins[:2], outs)
+    return conv
+
+
+for _k, _v in _BINARY.items():
+    register(_k)(_binary(_v))
+
+_SCALAR = {'_plus_scalar': ('Add', False), '_PlusScalar': ('Add', False), '_minus_scalar': ('Sub', False),
+           '_MinusScalar': ('Sub', False), '_rminus_scalar': ('Sub', True), '_RMinusScalar': ('Sub', True),
+           '_mul_scalar': ('Mul', False), '_MulScalar': ('Mul', False), '_div_scalar': ('Div', False),
+           '_DivScalar': ('Div', False), '_rdiv_scalar': ('Div', True), '_RDivScalar': ('Div', True),
+           '_power_scalar': ('Pow', False), '_PowerScalar': ('Pow', False), '_rpower_scalar': ('Pow', True),
+           '_maximum_scalar': ('Max', False), '_minimum_scalar': ('Min', False)}
+
+
+def _scalar_op(op, rev):
+    def conv(ctx, name, a, ins, outs):
+        c = _scalar_const(ctx, name + '_scalar', _float(a.get('scalar'), 0.0))
+        ctx.add(op, [c, ins[0]] if rev else [ins[0], c], outs)
+    return conv
+
+
+for _k, (_op, _rev) in _SCALAR.items():
+    register(_k)(_scalar_op(_op, _rev))
+
+_UNARY = {'relu': 'Relu', 'sigmoid': 'Sigmoid', 'tanh': 'Tanh', 'exp': 'Exp', 'log': 'Log', 'sqrt': 'Sqrt',
+          'abs': 'Abs', 'negative': 'Neg', 'floor': 'Floor', 'ceil': 'Ceil', 'sin': 'Sin', 'cos': 'Cos',
+          'tan': 'Tan', 'arcsin': 'Asin', 'arccos': 'Acos', 'arctan': 'Atan', 'erf': 'Erf', 'reciprocal': 'Reciprocal',
+          'softsign': 'Softsign', 'sign': 'Sign', 'round': 'Round', 'logical_not': 'Not',
+          '_copy': 'Identity', 'identity': 'Identity', 'BlockGrad': 'Identity', 'stop_gradient': 'Identity',
+          'Dropout': 'Identity', 'make_loss': 'Identity', 'MakeLoss': 'Identity'}
+
+
+def _unary(op):
+    def conv(ctx, name, a, ins, outs):
+        ctx.add(op, ins[:1], outs[:1])
+    return conv
+
+
+for _k, _v in _UNARY.items():
+    register(_k)(_unary(_v))
+
+
+@register('square')
+def _square(ctx, name, a, ins, outs):
+    ctx.add('Mul', [ins[0], ins[0]], outs)
+
+
+@register('rsqrt')
+def _rsqrt(ctx, name, a, ins, outs):
+    s = ctx.uid(name + '_sqrt')
+    ctx.add('Sqrt', ins[:1], [s])
+    ctx.add('Reciprocal', [s], outs)
+
+
+@register('softmax', 'SoftmaxActivation', 'SoftmaxOutput', 'Softmax')
+def _softmax(ctx, name, a, ins, outs):
+    if 'axis' in a:
+        axis = _int(a.get('axis'), -1)
+    else:
+        axis = 1 if (a.get('mode') == 'channel' or _bool(a.get('multi_output'))) else -1
+    if _float(a.get('temperature'), 1.0) != 1.0:
+        t = ctx.uid(name + '_tempered')
+        ctx.add('Div', [ins[0], _scalar_const(ctx, 'temperature', _float(a.get('temperature'), 1.0))], [t])
+        ctx.add('Softmax', [t], outs[:1], axis=axis)
+    else:
+        ctx.add('Softmax', ins[:1], outs[:1], axis=axis)
+
+
+@register('log_softmax')
+def _log_softmax(ctx, name, a, ins, outs):
+    ctx.add('LogSoftmax', ins[:1], outs, axis=_int(a.get('axis'), -1))
+
+
+@register('Flatten', 'flatten')
+def _flatten(ctx, name, a, ins, outs):
+    ctx.add('Flatten', ins[:1], outs, axis=1)
+
+
+@register('Reshape', 'reshape')
+def _reshape(ctx, name, a, ins, outs):
+    shape = ctx.out_shape(name)
+    if shape is None:
+        shape = _tup(a.get('shape'))
+        if any(s < -1 for s in shape):
+            raise NotImplementedError('ONNX export: Reshape %s needs known input shapes' % (shape,))
+    ctx.add('Reshape', [ins[0], ctx.const(name + '_shape', np.asarray(shape, dtype=np.int64))], outs)
+
+
+@register('Concat', 'concat')
+def _concat(ctx, name, a, ins, outs):
+    ctx.add('Concat', ins, outs, axis=_int(a.get('dim'), 1))
+
+
+@register('transpose')
+def _transpose(ctx, name, a, ins, outs):
+    axes = _tup(a.get('axes'), ())
+    ctx.add('Transpose', ins[:1], outs, perm=list(axes) if axes else None)
+
+
+@register('expand_dims')
+def _expand(ctx, name, a, ins, outs):
+    ctx.add('Unsqueeze', [ins[0], ctx.const(name + '_axes', np.asarray([_int(a.get('axis'), 0)], np.int64))], outs)
+
+
+@register('squeeze')
+def _squeeze(ctx, name, a, ins, outs):
+    ax = _tup(a.get('axis'), ())
+    extra = [ctx.const(name + '_axes', np.asarray(ax, np.int64))] if ax else []
+    ctx.add('Squeeze', [ins[0]] + extra, outs)
+
+
+@register('clip')
+def _clip(ctx, name, a, ins, outs):
+    ctx.add('Clip', [ins[0], _scalar_const(ctx, name + '_min', _float(a.get('a_min'), -np.inf)),
+                     _scalar_const(ctx, name + '_max', _float(a.get('a_max'), np.inf))], outs)
+
+
+def _reduce(op):
+    def conv(ctx, name, a, ins, outs):
+        ax = _tup(a.get('axis'), ())
+        keep = int(_bool(a.get('keepdims')))
+        if _bool(a.get('exclude')):
+            raise NotImplementedError('ONNX export: %s with exclude=True' % op)
+        if op == 'ReduceSum':        # opset 13: axes is an input
+            extra = [ctx.const(name + '_axes', np.asarray(ax, np.int64))] if ax else []
+            ctx.add(op, [ins[0]] + extra, outs, keepdims=keep)
+        else:
+            ctx.add(op, ins[:1], outs, keepdims=keep, axes=list(ax) if ax else None)
+    return conv
+
+
+for _k, _v in {'mean': 'ReduceMean', 'sum': 'ReduceSum', 'max': 'ReduceMax', 'min': 'ReduceMin',
+               'prod': 'ReduceProd'}.items():
+    register(_k)(_reduce(_v))
+
+
+@register('dot', 'batch_dot', '_linalg_gemm2', 'linalg_gemm2')
+def _dot(ctx, name, a, ins, outs):
+    x, y = ins[0], ins[1]
+    perm2 = None
+    sh = ctx.out_shape(name)
+    nd = len(sh) if sh else 2
+    if nd >= 2:
+        perm2 = list(range(nd - 2)) + [nd - 1, nd - 2]
+    if _bool(a.get('transpose_a')):
+        t = ctx.uid(name + '_aT')
+        ctx.add('Transpose', [x], [t], perm=perm2)
+        x = t
+    if _bool(a.get('transpose_b')):
+        t = ctx.uid(name + '_bT')
+        ctx.add('Transpose', [y], [t], perm=perm2)
+        y = t
+    alpha = _float(a.get('alpha'), 1.0)
+    if alpha != 1.0:
+        mm = ctx.uid(name + '_mm')
+        ctx.add('MatMul', [x, y], [mm])
+        ctx.add('Mul', [mm, _scalar_const(ctx, 'alpha', alpha)], outs)
+    else:
+        ctx.add('MatMul', [x, y], outs)
+
+
+@register('Embedding')
+def _embedding(ctx, name, a, ins, outs):
+    idx = ctx.uid(name + '_idx')
+    ctx.add('Cast', [ins[0]], [idx], to=7)
+    ctx.add('Gather', [ins[1], idx], outs, axis=0)
+
+
+@register('take')
+def _take(ctx, name, a, ins, outs):
+    idx = ctx.uid(name + '_idx')
+    ctx.add('Cast', [ins[1]], [idx], to=7)
+    ctx.add('Gather', [ins[0], idx], outs, axis=_int(a.get('axis'), 0))
+
+
+@register('Cast', 'cast')
+def _cast(ctx, name, a, ins, outs):
+    ctx.add('Cast', ins[:1], outs, to=P.dtype_to_onnx(np.dtype(a.get('dtype', 'float32'))))
+
+
+@register('slice_axis')
+def _slice_axis(ctx, name, a, ins, outs):
+    end = a.get('end')
+    end = np.iinfo(np.int64).max if end in (None, 'None') else int(end)
+    ctx.add('Slice', [ins[0], ctx.const(name + '_starts', np.asarray([int(a.get('begin'))], np.int64)),
+                      ctx.const(name + '_ends', np.asarray([end], np.int64)),
+                      ctx.const(name + '_axes', np.asarray([int(a.get('axis'))], np.int64))], outs)
+
+
+@register('slice')
+def _slice(ctx, name, a, ins, outs):
+    b = [0 if x.strip() in ('None', '') else int(x) for x in str(a.get('begin')).strip('()[]').split(',')
+         if x.strip() != '']
+    e = [np.iinfo(np.int64).max if x.strip() in ('None', '') else int(x)
+         for x in str(a.get('end')).strip('()[]').split(',') if x.strip() != '']
+    st = a.get('step')
+    s = [1 if x.strip() in ('None', '') else int(x) for x in str(st).strip('()[]').split(',') if x.strip() != ''] \
+        if st not in (None, 'None', '()', '[]') else [1] * len(b)
+    ctx.add('Slice', [ins[0], ctx.const(name + '_starts', np.asarray(b, np.int64)),
+                      ctx.const(name + '_ends', np.asarray(e, np.int64)),
+                      ctx.const(name + '_axes', np.arange(len(b), dtype=np.int64)),
+                      ctx.const(name + '_steps', np.asarray(s, np.int64))], outs)
+
+
+@register('Pad', 'pad')
+def _pad(ctx, name, a, ins, outs):
+    pw = _tup(a.get('pad_width'))
+    pads = list(pw[0::2]) + list(pw[1::2])
+    mode = a.get('mode', 'constant')
+    ctx.add('Pad', [ins[0], ctx.const(name + '_pads', np.asarray(pads, np.int64)),
+                    _scalar_const(ctx, name + '_value', _float(a.get('constant_value'), 0.0))], outs,
+            mode={'constant': 'constant', 'edge': 'edge', 'reflect': 'reflect'}[mode])
+
+
+@register('UpSampling')
+def _upsample(ctx, name, a, ins, outs):
+    if a.get('sample_type', 'nearest') != 'nearest':
+        raise NotImplementedError('ONNX export: bilinear UpSampling')
+    sc = _float(a.get('scale'), 1.0)
+    ctx.add('Resize', [ins[0], ctx.const(name + '_roi', np.zeros(0, np.float32)),
+                       ctx.const(name + '_scales', np.asarray([1, 1, sc, sc], np.float32))], outs, mode='nearest')
+
+
+@register('SliceChannel', 'split')
+def _split(ctx, name, a, ins, outs):
+    axis = _int(a.get('axis'), 1)
+    n = _int(a.get('num_outputs'), 1)
+    if _bool(a.get('squeeze_axis')):
+        parts = [ctx.uid(o + '_unsq') for o in outs[:n]]
+        ctx.add('Split', [ins[0]], parts, axis=axis)
+        ax = ctx.const(name + '_axes', np.asarray([axis], np.int64))
+        for p_, o in zip(parts, outs[:n]):
+            ctx.add('Squeeze', [p_, ax], [o])
+    else:
+        ctx.add('Split', [ins[0]], outs[:n], axis=axis)
+
+
+@register('broadcast_to')
+def _bcast_to(ctx, name, a, ins, outs):
+    shape = ctx.out_shape(name) or _tup(a.get('shape'))
+    ctx.add('Expand', [ins[0], ctx.const(name + '_shape', np.asarray(shape, np.int64))], outs)
+
+
+@register('tile')
+def _tile(ctx, name, a, ins, outs):
+    ctx.add('Tile', [ins[0], ctx.const(name + '_reps', np.asarray(_tup(a.get('reps')), np.int64))], outs)
+
+
+@register('where')
+def _where(ctx, name, a, ins, outs):
+    c = ctx.uid(name + '_cond')
+    ctx.add('Cast', [ins[0]], [c], to=9)
+    ctx.add('Where', [c, ins[1], ins[2]], outs)
+
+
+def _arg(op):
+    def conv(ctx, name, a, ins, outs):
+        i = ctx.uid(name + '_i64')
+        ctx.add(op, ins[:1], [i], axis=_int(a.get('axis'), 0), keepdims=int(_bool(a.get('keepdims'))))
+        ctx.add('Cast', [i], outs, to=1)      # MXNet returns the indices as float32
+    return conv
+
+
+register('argmax')(_arg('ArgMax'))
+register('argmin')(_arg('ArgMin'))
+
+
+@register('add_n', 'ElementWiseSum')
+def _add_n(ctx, name, a, ins, outs):
+    ctx.add('Sum', ins, outs)
+
+
+# ---------------------------------------------------------------- driver
+def _infer_node_shapes(sym, in_shapes):
+    """name -> first-output shape of every operator node (this framework's shape inference)."""
+    out = {}
+    try:
+        internals = sym.get_internals()
+        names = internals.list_outputs()
+        _, shapes, _ = internals.infer_shape(**in_shapes)
+        for n, s in zip(names, shapes or []):
+            if s is None:
+                continue
+            base = n[:-len('_output')] if n.endswith('_output') else n
+            out.setdefault(base, tuple(int(d) for d in s))
+            if n.endswith('_output0'):
+                out.setdefault(n[:-len('_output0')], tuple(int(d) for d in s))
+    except Exception:     # pylint: disable=broad-except
+        pass
+    return out
+
+
+def create_model(sym, params, in_shapes, in_types, opset_version=13, producer='mxnet_maintenance_amd'):
+    """ModelProto for ``sym`` with ``params`` (name -> NDArray / numpy, args and aux)."""
+    from ..ndarray.ndarray import NDArray
+    pvals = {}
+    for k, v in params.items():
+        k = k.split(':', 1)[1] if k.startswith(('arg:', 'aux:')) else k
+        pvals[k] = v.asnumpy() if isinstance(v, NDArray) else np.asarray(v)
+    graph = json.loads(sym.tojson())
+    nodes = graph['nodes']
+    data_names = [n['name'] for n in nodes if n['op'] == 'null' and n['name'] not in pvals]
+    if len(in_shapes) != len(data_names):
+        raise ValueError('export_model: %d input shapes for data inputs %s' % (len(in_shapes), data_names))
+    shape_map = dict(zip(data_names, [tuple(s) for s in in_shapes]))
+    ctx = _Ctx(sym, pvals, opset_version)
+    ctx.shapes = _infer_node_shapes(sym, shape_map)
+    heads = graph['heads']
+    nout_of = {}
+    for h in heads:
+        nout_of[h[0]] = max(nout_of.get(h[0], 1), h[1] + 1)
+
+    def tname(nid, idx):
+        nm = nodes[nid]['name']
+        return nm if idx == 0 else '%s_output%d' % (nm, idx)
+
+    g = P.GraphProto(name=producer + '_graph')
+    for nid, n in enumerate(nodes):
+        if n['op'] == 'null':
+            if n['name'] in pvals:
+                ctx.inits[n['name']] = pvals[n['name']]
+            continue
+        conv = _CONVERTERS.get(n['op'])
+        if conv is None:
+            raise NotImplementedError('ONNX export: no converter for operator %s (node %s)' % (n['op'], n['name']))
+        attrs = n.get('attrs', n.get('param', {})) or {}
+        ins = [tname(i[0], i[1]) for i in n['inputs']]
+        nout = max([nout_of.get(nid, 1)] + [_int(attrs.get('num_outputs'), 1) if n['op'] in ('SliceChannel', 'split')
+                                             else 1])
+        outs = [tname(nid, j) for j in range(nout)]
+        conv(ctx, n['name'], attrs, ins, outs)
+    g.node.extend(ctx.nodes)
+    for k, v in ctx.inits.items():
+        g.initializer.append(P.make_tensor(k, v))
+    for nm, t in zip(data_names, in_types):
+        g.input.append(P.make_value_info(nm, P.dtype_to_onnx(np.dtype(t)), shape_map[nm]))
+    _, out_shapes, _ = sym.infer_shape(**shape_map)
+    for (nid, idx, _v), shp in zip(heads, out_shapes or [None] * len(heads)):
+        g.output.append(P.make_value_info(tname(nid, idx), 1, shp or ()))
+    m = P.ModelProto(ir_version=P.IR_VERSION, producer_name=producer, producer_version='1.0', model_version=1)
+    m.opset_import.add(domain='', version=opset_version)
+    m.graph.CopyFrom(g)
+    return m
+
+
+def export_model(sym, params, in_shapes=None, in_types=np.float32, onnx_file_path='model.onnx', verbose=False,
+                 dynamic=False, dynamic_input_shapes=None, run_shape_inference=False, input_type=None,
+                 input_shape=None, large_model=False):
+    """Export ``sym`` (Symbol or JSON path) with ``params`` (dict, [arg, aux] or .params path) to an
+    ONNX file; returns the path (reference python/mxnet/onnx/mx2onnx/_export_model.py:51)."""
+    from .. import symbol as _symbol
+    from .. import ndarray as _nd
+    if input_type is not None:
+        in_types = input_type
+    if input_shape is not None:
+        in_shapes = input_shape
+    if isinstance(sym, str):
+        sym = _symbol.load(sym)
+    if isinstance(params, str):
+        params = _nd.load(params)
+    if isinstance(params, (list, tuple)):
+        merged = {}
+        for p in params:
+            merged.update(p)
+        params = merged
+    if not isinstance(in_types, (list, tuple)):
+        in_types = [in_types] * len(in_shapes)
+    if dynamic:
+        dyn = dynamic_input_shapes or [[None] * len(s) for s in in_shapes]
+    model = create_model(sym, params, in_shapes, in_types)
+    if dynamic:
+        for vi, ds in zip(model.graph.input, dyn):
+            for d, v in zip(vi.type.tensor_type.shape.dim, ds):
+                if v is None:
+                    d.ClearField('dim_value')
+                    d.dim_param = 'dyn'
+    with open(onnx_file_path, 'wb') as f:
+        f.write(model.SerializeToString())
+    if verbose:
+        print('exported %d ONNX nodes to %s' % (len(model.graph.node), onnx_file_path))
+    return onnx_file_path
