@@ -582,11 +582,27 @@ def _torch_tensor():
     return torch.Tensor
 
 
+_JOIN_HOOKS = []
+
+
+def add_join_hook(fn):
+    """``fn()`` runs at every host-visible point (join_workers): other side streams' joins."""
+    if fn not in _JOIN_HOOKS:
+        _JOIN_HOOKS.append(fn)
+
+
+def run_join_hooks():
+    for fn in _JOIN_HOOKS:
+        fn()
+
+
 def join_workers(dev=None):
     """Make the caller's current stream (of ``dev``, default every device) wait on the GPU for all
     work issued on the worker slots so far (a host-visible point: starts a new epoch)."""
     if _workers.depth:
         return            # inside an operator body: its own stream is already the right one
+    for fn in _JOIN_HOOKS:
+        fn()
     _epoch[0] += 1
     if not _workers.dirty:
         return

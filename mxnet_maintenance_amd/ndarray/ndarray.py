@@ -710,6 +710,7 @@ class NDArray:
         if _state.STATE.recording and (self._data.requires_grad or r._data.requires_grad) and not self._data.is_leaf:
             self._data = r._data
         else:
+            _engine.join_workers()
             with torch.no_grad():
                 self._data.copy_(r._data)
 
@@ -830,6 +831,7 @@ def _inplace(self, other, torch_fn, bop, sop):
         self._data = r._data
         return self
     o = other._data if isinstance(other, NDArray) else other
+    _engine.join_workers()       # a direct write on the caller's stream (worker streams done first)
     with torch.no_grad():
         if torch.is_tensor(o) and o.shape != self._data.shape:
             torch_fn(self._data, o.expand_as(self._data) if o.dim() <= self._data.dim() else o)

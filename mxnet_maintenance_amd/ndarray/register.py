@@ -206,6 +206,8 @@ def invoke(op, inputs, attrs, out=None):
     Failures of the operator's execution (AsyncOpError) and failed inputs do not raise here: the
     outputs carry the failure to the next synchronisation point (engine.rethrow / rethrow_all)."""
     tin = [None if x is None else x._data for x in inputs]
+    if _engine._JOIN_HOOKS and not _engine._workers.depth:
+        _engine.run_join_hooks()      # e.g. weight gradients still running on a side stream
     _note_leaves(inputs)
     if _amp.active:
         tin = _amp.cast_inputs(op.name, tin, attrs)

@@ -1335,6 +1335,51 @@ def _wgrad(dy, x, w, w_ref, stride, pad):
     return dw
 
 
+# ---------------------------------------------------------------- weight gradients on a side stream
+# The backward of a conv layer is dgrad (feeds the previous BatchNorm's memory-bound backward) and wgrad
+# (compute-bound, needed only by the optimizer).  With MXAMD_WGRAD_STREAM=1 the wgrad is issued on a
+# per-device side stream forked from the caller's stream, so it runs under the following BatchNorm /
+# dgrad kernels instead of in series with them.  Its operands stay referenced until the join, which
+# happens at every host-visible point (engine.join_workers: Trainer / KVStore / asnumpy / dispatch),
+# before a gradient bucket's all-reduce, and inside a captured HIP graph before the optimizer.
+_WGRAD_SIDE = [os.environ.get('MXAMD_WGRAD_STREAM', '0') == '1']
+_SIDE_STREAMS = {}
+_SIDE_KEEP = []
+_SIDE_DIRTY = set()
+
+
+def join_side_streams():
+    """Make each device's current stream wait for the side-stream weight gradients issued so far."""
+    if not _SIDE_DIRTY:
+        return
+    for dev in list(_SIDE_DIRTY):
+        torch.cuda.current_stream(dev).wait_stream(_SIDE_STREAMS[dev])
+    _SIDE_DIRTY.clear()
+    del _SIDE_KEEP[:]
+
+
+def _wgrad_maybe_side(dy, x, w, w_ref, stride, pad):
+    if not (_WGRAD_SIDE[0] and dy.is_cuda):
+        return _wgrad(dy, x, w, w_ref, stride, pad)
+    dev = dy.device.index
+    side = _SIDE_STREAMS.get(dev)
+    if side is None:
+        side = _SIDE_STREAMS[dev] = torch.cuda.Stream(device=dev)
+        from .. import engine
+        engine.add_join_hook(join_side_streams)
+    main = torch.cuda.current_stream(dev)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        dw = _wgrad(dy, x, w, w_ref, stride, pad)
+    _SIDE_KEEP.append((dy, x))
+    _SIDE_DIRTY.add(dev)
+    if dw is not None:
+        # returned to autograd, which consumes it on the caller's stream
+        main.wait_stream(side)
+        dw.record_stream(main)
+    return dw
+
+
 class ConvNHWC(torch.autograd.Function):
     """2-D NHWC convolution with per-shape algorithm selection (HIP MFMA kernel / hipBLASLt / MIOpen)."""
 
@@ -1356,6 +1401,9 @@ class ConvNHWC(torch.autograd.Function):
         dy = dy.contiguous()
         stride, pad = ctx.stride, ctx.pad
         dx = dw = db = None
+        if ctx.needs_input_grad[1] and _WGRAD_SIDE[0]:
+            # first, so that it overlaps the dgrad and what follows it
+            dw = _wgrad_maybe_side(dy, x, w, ctx.w_ref, stride, pad)
         if ctx.needs_input_grad[0]:
             key = ('dgrad', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), x.dtype)
             if _bn_bwd_fusable(ctx.bn_src, x.shape):
@@ -1363,7 +1411,7 @@ class ConvNHWC(torch.autograd.Function):
                 dx = _select(key + ('bnbwd',), cands, _dgrad_default(w, stride), timing=timing)
             else:
                 dx = _select(key, _dgrad_candidates(dy, x, w, stride, pad), _dgrad_default(w, stride))
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and not _WGRAD_SIDE[0]:
             dw = _wgrad(dy, x, w, ctx.w_ref, stride, pad)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum(dim=(0, 1, 2))
@@ -1400,9 +1448,11 @@ class ConvTeeNHWC(torch.autograd.Function):
         if gy is None:
             return gpass, None, None
         gy = gy.contiguous()
+        if ctx.needs_input_grad[1] and _WGRAD_SIDE[0]:
+            dw = _wgrad_maybe_side(gy, x, w, ctx.w_ref, (1, 1), (0, 0))
         if ctx.needs_input_grad[0]:
             dx = _tee_dgrad(gy, x, w, gpass, ctx.inplace_grad, ctx.bn_src)
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and not _WGRAD_SIDE[0]:
             dw = _wgrad(gy, x, w, ctx.w_ref, (1, 1), (0, 0))
         return dx, dw, None
 

@@ -114,6 +114,8 @@ class GradBuckets:
         def hook(_t):
             b.ready += 1
             if b.ready == b.count and b.handle is None:
+                from .. import engine
+                engine.join_workers()     # gradients written on side streams are complete first
                 b.handle = dist.all_reduce(b.flat, async_op=True)
         return hook
 

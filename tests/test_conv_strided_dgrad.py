@@ -86,9 +86,14 @@ def test_strided_dgrad_kernel_matches_fp32(case, dtype, bco):
 def test_phase_plan_gather_builds_tap_slices():
     K, R, S, C = 64, 3, 3, 32
     w = torch.randn(K, R, S, C)
-    phases, empty, gidx = KF._phase_plan(w.shape, (2, 2), (1, 1), w.device)
+    phases, empty, (slots, total) = KF._phase_plan(w.shape, (2, 2), (1, 1), w.device)
     assert not empty and len(phases) == 4
-    flat = w.reshape(-1).index_select(0, gidx)
+    # the tap-transpose table (what weight_taps_t executes): out[base + c*rstride + k] = w[k, tap, c]
+    flat = torch.zeros(total)
+    wt = w.reshape(K, R * S, C)
+    for tap, base, rs in slots:
+        idx = base + torch.arange(C)[:, None] * rs + torch.arange(K)[None, :]
+        flat[idx.reshape(-1)] = wt[:, tap, :].t().reshape(-1)
     wp = w.permute(3, 1, 2, 0)
     for ph, pw, r, s, _, _, off in phases:
         rr = [t for _, t in KF._phase_taps(R, 1, 2, ph)]

@@ -76,3 +76,38 @@ def test_autograd_through_worker_streams(workers):
     y1.backward()
     engine.set_gpu_workers(2)
     onp.testing.assert_allclose(g, w.grad.asnumpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_side_stream_weight_gradients_match():
+    """MXAMD_WGRAD_STREAM: conv weight gradients issued on a side stream equal the in-order ones, and
+    the trainer step joins the stream before it reads them."""
+    if not torch.cuda.is_available():
+        pytest.skip('needs a GPU')
+    from mxnet_maintenance_amd.ops import kernel_fns as KF
+    from mxnet_maintenance_amd.gluon import nn
+    ctx = mx.gpu(0)
+    x = mx.nd.array(onp.random.RandomState(0).randn(8, 14, 14, 64), ctx=ctx, dtype='float16')
+    results = []
+    prev = KF._WGRAD_SIDE[0]
+    for side in (False, True):
+        KF._WGRAD_SIDE[0] = side
+        mx.random.seed(3)
+        net = nn.HybridSequential()
+        with net.name_scope():
+            net.add(nn.Conv2D(64, 3, padding=1, layout='NHWC', in_channels=64, use_bias=False),
+                    nn.BatchNorm(axis=3, in_channels=64), nn.Activation('relu'),
+                    nn.Conv2D(64, 1, layout='NHWC', in_channels=64, use_bias=False))
+        net.initialize(mx.init.Xavier(), ctx=ctx)
+        net.cast('float16')
+        trainer = mx.gluon.Trainer(net.collect_params(), 'sgd', {'learning_rate': 0.1, 'multi_precision': True})
+        with mx.autograd.record():
+            loss = (net(x).astype('float32') ** 2).mean()
+        loss.backward()
+        grads = [p.grad().asnumpy().astype('float32') for p in net.collect_params().values() if p.grad_req != 'null']
+        trainer.step(8)
+        w = [p.data().asnumpy().astype('float32') for p in net.collect_params().values()]
+        results.append((grads, w))
+        assert not KF._SIDE_DIRTY
+    KF._WGRAD_SIDE[0] = prev
+    for a, b in zip(results[0][0] + results[0][1], results[1][0] + results[1][1]):
+        onp.testing.assert_allclose(a, b, rtol=1e-3, atol=1e-4)
