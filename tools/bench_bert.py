@@ -45,6 +45,10 @@ def main():
     ap.add_argument('--gpus', type=int, default=1, help='worker processes (one per GPU)')
     ap.add_argument('--graph', action='store_true', help='capture the whole step in a HIP graph (GraphStep)')
     ap.add_argument('--trace-loss', action='store_true', help='print every step\'s loss (debugging; syncs)')
+    ap.add_argument('--gemm-table', default=os.path.join(os.path.dirname(os.path.abspath(__file__)), 'tunableop',
+                                                          'bert_base_b32_s128_bf16_gfx950.csv'),
+                    help='hipBLASLt/rocBLAS solution table (PyTorch TunableOp CSV) for the library GEMMs; '
+                         '"none" keeps the library heuristics, "tune" measures a new one')
     args = ap.parse_args()
     launch = _load_launcher()
     if launch.needs_launch(args.gpus):
@@ -55,6 +59,21 @@ def main():
         # debugging: torch.empty returns NaN-filled memory, exposing reads of unwritten buffers
         torch.use_deterministic_algorithms(True, warn_only=True)
         torch.utils.deterministic.fill_uninitialized_memory = True
+    if args.gemm_table != 'none' and torch.cuda.is_available():
+        # per-shape library GEMM solutions measured on gfx950 (tools/tunableop/; +2-3 % here): the table
+        # is read, not re-tuned, unless --gemm-table tune; shapes it lacks keep the default heuristics
+        import torch.cuda.tunable as tunable
+        tunable.enable(True)
+        if args.gemm_table == 'tune':
+            tunable.tuning_enable(True)
+        elif os.path.exists(args.gemm_table) and (args.batch, args.seq) == (32, 128):
+            import tempfile
+            tunable.tuning_enable(False)
+            # results the run writes at exit go to a scratch file, never over the committed table
+            tunable.set_filename(os.path.join(tempfile.gettempdir(), 'mxamd_tunableop_%d.csv' % os.getpid()))
+            tunable.read_file(args.gemm_table)
+        else:
+            tunable.enable(False)
     import mxnet_maintenance_amd as mx
     from mxnet_maintenance_amd import gluon, autograd, nd
     from mxnet_maintenance_amd.models import bert as bert_mod
