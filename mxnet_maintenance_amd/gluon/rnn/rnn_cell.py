@@ -26,7 +26,11 @@ tensor_types = (Symbol, NDArray)
 
 
 def _listify(x):
-    return list(x) if isinstance(x, (list, tuple)) else [x]
+    if isinstance(x, (list, tuple)):
+        return list(x)
+    if isinstance(x, Symbol) and len(x.list_outputs()) > 1:
+        return [x[i] for i in range(len(x.list_outputs()))]     # e.g. a split into per-step outputs
+    return [x]
 
 
 def _namespace(x):
@@ -99,6 +103,17 @@ def _format_sequence(length, inputs, layout, merge, in_layout=None):
 def _zero_states(cell, F, begin_state, steps, batch):
     if begin_state is not None:
         return begin_state
+    if F is not ndarray and isinstance(steps, (list, tuple)) and steps:
+        # traced graph: zeros sized by the first step's batch (N, ...) on every call, not zeros with an
+        # unknown batch dim that a cached graph would fix at its first input shape
+        x0 = steps[0]
+        z = F.zeros_like(F.slice_axis(x0, axis=1, begin=0, end=1))
+        out = []
+        for info in cell.state_info(0):
+            shp = tuple(info['shape'])
+            zz = F.reshape(z, shape=(-1,) + (1,) * (len(shp) - 1))
+            out.append(F.broadcast_to(zz, shape=(0,) + shp[1:]))
+        return out
     kwargs = {'func': F.zeros, 'batch_size': batch}
     if F is ndarray:
         kwargs['ctx'] = steps[0].context if isinstance(steps, (list, tuple)) else steps.context

@@ -118,6 +118,16 @@ class _RNNLayer(HybridBlock):
     def state_info(self, batch_size=0):
         raise NotImplementedError
 
+    def _symbol_begin_state(self, inputs):
+        """Zero initial states of a traced graph, sized by the batch of ``inputs`` on every call:
+        a (1, N, 1) zero slice of the input broadcast to (layers * directions, N, width) -- unlike
+        zeros with an unknown batch dim, it stays right when a cached graph sees another batch size."""
+        t_axis, c_axis = self._layout.index('T'), self._layout.index('C')
+        z = symbol.slice_axis(symbol.slice_axis(inputs, axis=t_axis, begin=0, end=1), axis=c_axis, begin=0, end=1)
+        z = symbol.reshape(symbol.zeros_like(z), shape=(1, -1, 1))
+        return [symbol.broadcast_to(z, shape=(info['shape'][0], 0, info['shape'][2]))
+                for info in self.state_info(0)]
+
     def _state_spec(self, batch_size, width):
         return {'shape': (self._num_layers * self._dir, batch_size, width), '__layout__': 'LNC',
                 'dtype': self._dtype}
@@ -175,7 +185,7 @@ class _RNNLayer(HybridBlock):
                 n = inputs.shape[self._layout.index('N')]
                 states = self.begin_state(n, ctx=inputs.context, dtype=inputs.dtype)
             else:
-                states = self.begin_state(0, func=symbol.zeros)
+                states = self._symbol_begin_state(inputs)
         if isinstance(states, (NDArray, symbol.Symbol)):
             states = [states]
         extra = (sequence_length,) if self._use_sequence_length else ()

@@ -1007,6 +1007,17 @@ def _unify_shapes(order, seeds):
                     total = math.prod(dst)
                     if known and total % known == 0:
                         changed |= merge(keys[0], tuple(d if d > 0 else total // known for d in src))
+                elif src is not None and dst is None:
+                    # partial input: the output dims that do not move with the unknown ones are known
+                    # (e.g. reshape(-1) of an RNN weight with unknown input size gives (-1,), so the
+                    # parameter concatenation downstream can solve for it backwards)
+                    try:
+                        a_ = _run_meta(n.opdef(), n.parsed(), [_subst([src], _PROBES[0])[0]], [torch.float32])[0][0]
+                        b_ = _run_meta(n.opdef(), n.parsed(), [_subst([src], _PROBES[1])[0]], [torch.float32])[0][0]
+                        if len(a_) == len(b_):
+                            changed |= merge(out, tuple(x if x == y else -1 for x, y in zip(a_, b_)))
+                    except Exception:   # pylint: disable=broad-except
+                        pass
             elif n.op not in _PROBE_SKIP:
                 changed |= _probe_node(n, keys, part, merge, memo)
         if not changed:
@@ -1072,13 +1083,14 @@ def _probe_node(n, keys, part, merge, memo):
     memo[id(n)] = sig
     changed = False
     # parameters (weights, biases) from partially known data: probe the data dims
-    if ins and ins[0] is not None and any(s is None for s in ins[1:]):
+    if ins and ins[0] is not None and any(s is None or any(v <= 0 for v in s) for s in ins[1:]):
         def filled(v):
             return [None if x is None else _subst([x], v)[0] for x in ins]
         a = _probe_params(n, filled(_PROBES[0]))
         b = _probe_params(n, filled(_PROBES[1]))
         for idx in a:
-            if idx < len(keys) and ins[idx] is None and idx in b and len(a[idx]) == len(b[idx]):
+            if (idx < len(keys) and idx > 0 and (ins[idx] is None or any(v <= 0 for v in ins[idx])) and idx in b
+                    and len(a[idx]) == len(b[idx])):
                 changed |= merge(keys[idx], tuple(x if x == y else -1 for x, y in zip(a[idx], b[idx])))
         ins = [part.get(k) for k in keys]
     if not ins or any(s is None for s in ins):
