@@ -387,6 +387,7 @@ class NDArray:
             self._grad._idt = idt
             if self.__class__ is not NDArray:
                 self._grad.__class__ = self.__class__
+            t.grad = self._grad._data       # autograd accumulates straight into the buffer
             self._grad_req = grad_req
             return
         t.requires_grad_(True)
@@ -434,6 +435,11 @@ class NDArray:
         if r.dim() == 0 and not _state.STATE.np_shape:
             r = r.reshape(1)
         out = NDArray(r)
+        idt = getattr(self, '_idt', None)
+        if idt is not None:
+            out._idt = idt                  # an integer variable's float64 carrier: the result is integer too
+        if _state.STATE.recording and self._grad_req is not None:
+            _state.STATE.tape_leaves[id(self)] = self
         box = getattr(self, '_exc', None)
         if box is not None:
             out._exc = box

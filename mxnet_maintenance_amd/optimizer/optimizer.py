@@ -388,7 +388,10 @@ def _lazy_adam_rows(w, g, mean, var, lr, beta1, beta2, eps, wd, rescale, clip):
     if idx.numel() == 0:
         return
     rows = w.index_select(0, idx).float()
-    step = _prep_grad(gr, rows, wd, rescale, clip)
+    # Adam's order (AdamDnsRspDnsKernel): weight decay joins the gradient before the clip
+    step = gr * rescale + wd * rows if wd else gr * rescale
+    if clip is not None and clip >= 0:
+        step = step.clamp(-clip, clip)
     m = mean.index_select(0, idx).float().mul_(beta1).add_(step, alpha=1 - beta1)
     v = var.index_select(0, idx).float().mul_(beta2).addcmul_(step, step, value=1 - beta2)
     mean.index_copy_(0, idx, m.to(mean.dtype))
