@@ -155,6 +155,14 @@ class BatchNormNHWC(torch.autograd.Function):
             y._mxamd_bn_src = (x, mean, scale if relu_mode == 2 else None, shift if relu_mode == 2 else None,
                                mask if relu_mode == 3 else None, relu_mode, ctx.bn_token)
         ctx.refs = (gamma, beta)
+        # residual tail fed by a projection shortcut's BatchNorm (no ReLU): the tail's backward apply
+        # also reduces that BN's backward statistics (its incoming gradient is the tail's dz)
+        ctx.add_src = None
+        if relu_mode == 3 and training and _BN_BWD_FUSE[0]:
+            src = getattr(addend, '_mxamd_bn_src', None)
+            if (src is not None and src[5] == 0 and tuple(src[0].shape) == tuple(x.shape)
+                    and src[0].dtype == x.dtype and src[0].is_contiguous()):
+                ctx.add_src = src
         # invstd_out: the third output is the batch 1/sqrt(var + eps) the kernel already wrote (the
         # reference's training-mode extra output) instead of the variance
         third = invstd if (invstd_out and training) else var
@@ -198,11 +206,20 @@ class BatchNormNHWC(torch.autograd.Function):
             dg_ptr, db_ptr, accum = out[0].data_ptr(), out[1].data_ptr(), 0
         ymask = y if relu_mode == 3 else None
         y = y if relu_mode == 1 else None
+        ds = ctx.add_src if dz is not None else None
+        dkw = {}
+        if ds is not None:
+            ds_nblk = lib.bn_partials_rows(R, C)
+            ds_part = torch.empty(2 * ds_nblk * C, dtype=torch.float32, device=dev)
+            dkw = dict(ds_z=ds[0].data_ptr(), ds_mean=ds[1].data_ptr(), ds_part=ds_part.data_ptr())
         lib.bn_nhwc_backward(_DT[x.dtype], x.data_ptr(), gy.data_ptr(), _p(y), _p(ymask), dx.data_ptr(), _p(dz),
                              g.data_ptr(),
                              mean.data_ptr(), invstd.data_ptr(), _p(fscale), _p(fshift), part.data_ptr(), dg_ptr,
                              db_ptr, out[2].data_ptr(), R, C, relu_mode, 0, int(training), accum, _stream(),
-                             ext_nblk)
+                             ext_nblk, **dkw)
+        if ds is not None:
+            # consumed by the shortcut BN's backward (token + version checked there)
+            dz._mxamd_bn_bwd = (ds_part, ds_nblk, ds[6], dz._version)
         if direct:
             # returning None: torch still runs the leaves' AccumulateGrad node with an undefined
             # gradient, which fires their post-accumulate hooks (bucketed all-reduce readiness)
@@ -510,9 +527,9 @@ def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=Non
     row-contiguous epilogue, 20..25 = persistent LDS-DMA ring kernel (see _RING_VARIANTS; no bias).
     ``bn_stats`` (big / ring kernels): also emit per-channel BatchNorm
     sum / sum-of-squares partials of y, attached to y as ``y._mxamd_bn_part``; ``addend`` (big kernel
-    only, same shape/dtype as y): y = conv + addend.  ``bn_bwd`` (big kernel only; a BatchNorm's
-    ``_mxamd_bn_src`` record): y is that BN's incoming gradient -- also emit its backward statistics
-    (sum dz, sum dz*(z-mean)), attached to y as ``y._mxamd_bn_bwd``."""
+    only, same shape/dtype as y): y = conv + addend.  ``bn_bwd`` (big kernel, or glds 5 / 6 when
+    glds_bnb_ok; a BatchNorm's ``_mxamd_bn_src`` record): y is that BN's incoming gradient -- also emit
+    its backward statistics (sum dz, sum dz*(z-mean)), attached to y as ``y._mxamd_bn_bwd``."""
     N, H, W, C = x.shape
     K, R, S, _ = w.shape
     Ho = (H + 2 * pad[0] - R) // stride[0] + 1
@@ -566,13 +583,37 @@ def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=Non
             y._mxamd_bn_part = (part, nparts)
         return y
     if variant in (5, 6):
-        _K.lib().conv_nhwc_fwd_glds(_DT[x.dtype], x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(),
-                                    _zero_page(x.device).data_ptr(), N, H, W, C, K, R, S, stride[0], stride[1],
-                                    pad[0], pad[1], 128 if variant == 5 else 64, _stream())
+        lib = _K.lib()
+        bco = 128 if variant == 5 else 64
+        bkw = _glds_bnb(bn_bwd, y, lib.conv_glds_bwd_nparts(N * Ho * Wo, bco))
+        part = bkw.pop('_part', None)
+        lib.conv_nhwc_fwd_glds(_DT[x.dtype], x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(),
+                               _zero_page(x.device).data_ptr(), N, H, W, C, K, R, S, stride[0], stride[1],
+                               pad[0], pad[1], bco, _stream(), **bkw)
+        if part is not None:
+            y._mxamd_bn_bwd = (part, bkw['bn_nparts'], bn_bwd[6], y._version)
         return y
     _K.lib().conv_nhwc_fwd(_DT[x.dtype], x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), N, H, W, C, K, R, S,
                            stride[0], stride[1], pad[0], pad[1], int(variant), _stream())
     return y
+
+
+def glds_bnb_ok(bn_src):
+    """The LDS-DMA (glds / phase) kernels emit BN-backward statistics for a BN without ReLU or with
+    the ReLU mask recomputed from z (modes 0 / 2), not from a stored mask bitmap."""
+    return bn_src is not None and int(bn_src[5]) in (0, 2) and hasattr(_K.lib(), 'conv_glds_bwd_nparts')
+
+
+def _glds_bnb(bn_bwd, y, nparts):
+    """Launch keywords of the glds / phase kernels' BN-backward statistics epilogue (and '_part', the
+    partials buffer, which the caller attaches to y)."""
+    if bn_bwd is None:
+        return {}
+    z, bmean, bscale, bshift, _bmask, bmode, _token = bn_bwd
+    assert int(bmode) in (0, 2) and z.shape == y.shape and z.dtype == y.dtype and z.is_contiguous()
+    part = torch.empty(2 * y.shape[-1] * nparts, dtype=torch.float32, device=y.device)
+    return dict(bn_z=z.data_ptr(), bn_mean=bmean.data_ptr(), bn_scale=_p(bscale), bn_shift=_p(bshift),
+                bn_part=part.data_ptr(), bn_nparts=nparts, _part=part)
 
 
 _ZERO = {}
@@ -727,12 +768,14 @@ def _phase_plan(wshape, stride, pad, device):
     return plan
 
 
-def conv_dgrad_strided(dy, w, stride, pad, xshape, bco=128):
+def conv_dgrad_strided(dy, w, stride, pad, xshape, bco=128, bn_bwd=None):
     """Data gradient of a stride-s conv as s*s sub-pixel phases in one launch (src/kernels/conv_glds.hip
     conv_nhwc_dgrad_phases_glds): phase (ph, pw) of dX -- rows s*a + ph, columns s*b + pw -- is a
     stride-1 conv of dY with the taps of W that reach it, written in place; the first phase's
-    epilogue also clears the phases no tap reaches (1x1 stride 2: 3 of 4).  No zero-stuffed dY and no scatter pass (cf. the reference's cuDNN backward-data,
-    src/operator/nn/cudnn/cudnn_convolution-inl.h)."""
+    epilogue also clears the phases no tap reaches (1x1 stride 2: 3 of 4).  No zero-stuffed dY and no
+    scatter pass (cf. the reference's cuDNN backward-data, src/operator/nn/cudnn/cudnn_convolution-inl.h).
+    ``bn_bwd`` (glds_bnb_ok): dX is the gradient of that BatchNorm's output -- the epilogue also emits
+    its backward statistics, attached as ``dx._mxamd_bn_bwd``."""
     K, R, S, C = w.shape
     N, H, W, _ = xshape
     st = stride[0]
@@ -748,11 +791,16 @@ def conv_dgrad_strided(dy, w, stride, pad, xshape, bco=128):
     wsub = _taps_t(w.contiguous(), torch.empty(total, dtype=w.dtype, device=w.device), [t[0] for t in slots],
                    [t[1] for t in slots], [t[2] for t in slots])
     cols = list(zip(*phases))
-    _K.lib().conv_nhwc_dgrad_phases_glds(_DT[dy.dtype], dy.data_ptr(), wsub.data_ptr(), dx.data_ptr(),
-                                         _zero_page(dy.device).data_ptr(), N, dy.shape[1], dy.shape[2], K, C, Ho, Wo,
-                                         st, list(cols[0]), list(cols[1]), list(cols[2]), list(cols[3]),
-                                         list(cols[4]), list(cols[5]), list(cols[6]), [e[0] for e in empty],
-                                         [e[1] for e in empty], bco, _stream())
+    lib = _K.lib()
+    bkw = _glds_bnb(bn_bwd, dx, len(phases) * lib.conv_glds_bwd_nparts(N * Ho * Wo, bco)) if bn_bwd else {}
+    part = bkw.pop('_part', None)
+    lib.conv_nhwc_dgrad_phases_glds(_DT[dy.dtype], dy.data_ptr(), wsub.data_ptr(), dx.data_ptr(),
+                                    _zero_page(dy.device).data_ptr(), N, dy.shape[1], dy.shape[2], K, C, Ho, Wo,
+                                    st, list(cols[0]), list(cols[1]), list(cols[2]), list(cols[3]),
+                                    list(cols[4]), list(cols[5]), list(cols[6]), [e[0] for e in empty],
+                                    [e[1] for e in empty], bco, _stream(), **bkw)
+    if part is not None:
+        dx._mxamd_bn_bwd = (part, bkw['bn_nparts'], bn_bwd[6], dx._version)
     return dx
 
 
@@ -1208,8 +1256,9 @@ def _charge_bn_bwd(cands, z):
 
 
 def _dgrad_bn_candidates(dy, x, w, stride, pad, bn_src):
-    """Stride-1 dgrad candidates when a BatchNorm produced x: the plain candidates plus big-tile
-    variants whose epilogue also emits that BatchNorm's backward statistics ('hipN+bn').  Returns
+    """Dgrad candidates when a BatchNorm produced x: the plain candidates plus the kernels whose
+    epilogue also emits that BatchNorm's backward statistics ('pw+bn', 'hipN+bn' for the big-tile and
+    LDS-DMA stride-1 kernels, 'phaseN+bn' for the strided phase kernel).  Returns
     (candidates, timing closures): autotuning weighs the fused epilogue's extra cost against the
     reduction pass it saves."""
     cands = _dgrad_candidates(dy, x, w, stride, pad)
@@ -1221,10 +1270,15 @@ def _dgrad_bn_candidates(dy, x, w, stride, pad, bn_src):
     if (_CONV_HIP and tuple(stride) == (1, 1) and 2 * pad[0] == R - 1 and 2 * pad[1] == S - 1
             and K % 64 == 0):
         for v in _fwd_variants(K, C, ktot=R * S * K):
-            if v in _BIG_VARIANTS:
+            if v in _BIG_VARIANTS or (v in (5, 6) and glds_bnb_ok(bn_src)):
                 fused.append(('hip%d+bn' % v, lambda v=v: conv_fwd(dy, _dgrad_weight(w), (1, 1),
                                                                    (R - 1 - pad[0], S - 1 - pad[1]), None, v,
                                                                    bn_bwd=bn_src)))
+    if glds_bnb_ok(bn_src):
+        for bco in (128, 64):
+            if conv_dgrad_strided_ok(dy, w, stride, pad, x.shape, bco):
+                fused.append(('phase%d+bn' % bco, lambda bco=bco: conv_dgrad_strided(dy, w, stride, pad, x.shape, bco,
+                                                                                     bn_bwd=bn_src)))
     return cands + fused, _charge_bn_bwd(cands, bn_src[0]) + fused
 
 

@@ -25,7 +25,7 @@ void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, c
                       void* dz,
                       const float* gamma, const float* mean, const float* invstd, const float* fscale,
                       const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R, int C,
-                      int relu_mode, int fix_gamma, int training, int accum, hipStream_t s, int ext_nblk);
+                      int relu_mode, int fix_gamma, int training, int accum, hipStream_t s, int ext_nblk, const void* ds_z, const float* ds_mean, float* ds_part);
 int bn_partials_rows(int64_t R, int C);
 void gemm_nt(int dtype, const void* a, const void* b, const float* bias, const void* addend, void* c, int out_f32,
              int M, int N, int K, int lda, int ldb, int ldc, int act, int cfg, int splits, float* ws, hipStream_t s);
@@ -68,12 +68,15 @@ void conv_nhwc_fwd_big(int dtype, const void* x, const void* w, const float* bia
 int conv_nhwc_fwd_big_bwd_nparts(int N, int H, int W, int R, int S, int sh, int sw, int ph, int pw, int variant);
 void conv_nhwc_fwd_glds(int dtype, const void* x, const void* w, const float* bias, void* y, const void* zero, int N,
                         int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int bco,
-                        hipStream_t s);
+                        hipStream_t s, const void* bn_z, const float* bn_mean, const float* bn_scale,
+                        const float* bn_shift, float* bn_part, int bn_nparts);
+int conv_glds_bwd_nparts(int M, int bco);
 void conv_nhwc_dgrad_phases_glds(int dtype, const void* dy, const void* w, void* dx, const void* zero, int N, int Hi,
                                  int Wi, int Cin, int Cout, int Ho, int Wo, int stride, int nph, const int* ph,
                                  const int* pw, const int* R, const int* S, const int* pad_h, const int* pad_w,
                                  const int64_t* w_off, int nzero, const int* zph, const int* zpw, int bco,
-                                 hipStream_t s);
+                                 hipStream_t s, const void* bn_z, const float* bn_mean, const float* bn_scale,
+                                 const float* bn_shift, float* bn_part, int bn_nparts);
 int conv_nhwc_fwd_ring_nparts(int N, int H, int W, int R, int S, int sh, int sw, int ph, int pw, int variant);
 void conv_nhwc_fwd_ring(int dtype, const void* x, const void* w, void* y, const void* zero, int N, int H, int W, int C,
                         int K, int R, int S, int sh, int sw, int ph, int pw, int variant, float* part, int nparts,
@@ -370,15 +373,18 @@ PYBIND11_MODULE(_hip_kernels, m) {
                                uintptr_t dz,
                                uintptr_t g, uintptr_t mean, uintptr_t inv, uintptr_t fscale, uintptr_t fshift,
                                uintptr_t part, uintptr_t dgamma, uintptr_t dbeta, uintptr_t coef, int64_t R, int C,
-                               int relu_mode, int fix_gamma, int training, int accum, uintptr_t s, int ext_nblk) {
+                               int relu_mode, int fix_gamma, int training, int accum, uintptr_t s, int ext_nblk,
+                               uintptr_t ds_z, uintptr_t ds_mean, uintptr_t ds_part) {
     bn_nhwc_backward(dt, P<void>(x), P<void>(dy), P<void>(y), P<uint8_t>(mask), P<void>(dx), P<void>(dz), P<float>(g), P<float>(mean),
                      P<float>(inv), P<float>(fscale), P<float>(fshift), P<float>(part), P<float>(dgamma),
-                     P<float>(dbeta), P<float>(coef), R, C, relu_mode, fix_gamma, training, accum, S(s), ext_nblk);
+                     P<float>(dbeta), P<float>(coef), R, C, relu_mode, fix_gamma, training, accum, S(s), ext_nblk,
+                     P<const void>(ds_z), P<const float>(ds_mean), P<float>(ds_part));
     check_launch("bn_nhwc_backward");
   }, py::arg("dt"), py::arg("x"), py::arg("dy"), py::arg("y"), py::arg("mask"), py::arg("dx"), py::arg("dz"),
      py::arg("g"), py::arg("mean"), py::arg("inv"), py::arg("fscale"), py::arg("fshift"), py::arg("part"),
      py::arg("dgamma"), py::arg("dbeta"), py::arg("coef"), py::arg("R"), py::arg("C"), py::arg("relu_mode"),
-     py::arg("fix_gamma"), py::arg("training"), py::arg("accum"), py::arg("stream"), py::arg("ext_nblk") = 0);
+     py::arg("fix_gamma"), py::arg("training"), py::arg("accum"), py::arg("stream"), py::arg("ext_nblk") = 0,
+     py::arg("ds_z") = 0, py::arg("ds_mean") = 0, py::arg("ds_part") = 0);
   m.def("softmax_ce_forward", [](int dt, int li, uintptr_t logits, uintptr_t label, uintptr_t loss, uintptr_t lse,
                                  int N, int K, uintptr_t s) {
     softmax_ce_forward(dt, li, P<void>(logits), P<void>(label), P<float>(loss), P<float>(lse), N, K, S(s));
@@ -436,17 +442,26 @@ PYBIND11_MODULE(_hip_kernels, m) {
   });
   m.def("conv_nhwc_fwd_glds", [](int dt, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, uintptr_t zero, int N,
                                  int H, int W, int C, int K, int R, int Sf, int sh, int sw, int ph, int pw, int bco,
-                                 uintptr_t s) {
+                                 uintptr_t s, uintptr_t bn_z, uintptr_t bn_mean, uintptr_t bn_scale,
+                                 uintptr_t bn_shift, uintptr_t bn_part, int bn_nparts) {
     conv_nhwc_fwd_glds(dt, P<void>(x), P<void>(w), P<float>(bias), P<void>(y), P<void>(zero), N, H, W, C, K, R, Sf,
-                       sh, sw, ph, pw, bco, S(s));
+                       sh, sw, ph, pw, bco, S(s), P<void>(bn_z), P<float>(bn_mean), P<float>(bn_scale),
+                       P<float>(bn_shift), P<float>(bn_part), bn_nparts);
     check_launch("conv_nhwc_fwd_glds");
-  });
+  }, py::arg("dtype"), py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("zero"), py::arg("N"),
+     py::arg("H"), py::arg("W"), py::arg("C"), py::arg("K"), py::arg("R"), py::arg("S"), py::arg("sh"),
+     py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("bco"), py::arg("stream"), py::arg("bn_z") = 0,
+     py::arg("bn_mean") = 0, py::arg("bn_scale") = 0, py::arg("bn_shift") = 0, py::arg("bn_part") = 0,
+     py::arg("bn_nparts") = 0);
+  // BN-backward partials per channel of a glds launch over M output pixels (per phase for the phase kernel)
+  m.def("conv_glds_bwd_nparts", &conv_glds_bwd_nparts);
   // the sub-pixel phases of a strided data gradient, one launch, written in place into dX
   m.def("conv_nhwc_dgrad_phases_glds",
         [](int dt, uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t zero, int N, int Hi, int Wi, int Cin, int Cout,
            int Ho, int Wo, int stride, std::vector<int> ph, std::vector<int> pw, std::vector<int> R,
            std::vector<int> Sf, std::vector<int> pad_h, std::vector<int> pad_w, std::vector<int64_t> w_off,
-           std::vector<int> zph, std::vector<int> zpw, int bco, uintptr_t s) {
+           std::vector<int> zph, std::vector<int> zpw, int bco, uintptr_t s, uintptr_t bn_z, uintptr_t bn_mean,
+           uintptr_t bn_scale, uintptr_t bn_shift, uintptr_t bn_part, int bn_nparts) {
           const size_t n = ph.size();
           if (pw.size() != n || R.size() != n || Sf.size() != n || pad_h.size() != n || pad_w.size() != n ||
               w_off.size() != n || zph.size() != zpw.size())
@@ -454,9 +469,16 @@ PYBIND11_MODULE(_hip_kernels, m) {
           conv_nhwc_dgrad_phases_glds(dt, P<void>(dy), P<void>(w), P<void>(dx), P<void>(zero), N, Hi, Wi, Cin, Cout,
                                       Ho, Wo, stride, (int)n, ph.data(), pw.data(), R.data(), Sf.data(),
                                       pad_h.data(), pad_w.data(), w_off.data(), (int)zph.size(), zph.data(),
-                                      zpw.data(), bco, S(s));
+                                      zpw.data(), bco, S(s), P<void>(bn_z), P<float>(bn_mean), P<float>(bn_scale),
+                                      P<float>(bn_shift), P<float>(bn_part), bn_nparts);
           check_launch("conv_nhwc_dgrad_phases_glds");
-        });
+        },
+        py::arg("dtype"), py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("zero"), py::arg("N"), py::arg("Hi"),
+        py::arg("Wi"), py::arg("Cin"), py::arg("Cout"), py::arg("Ho"), py::arg("Wo"), py::arg("stride"),
+        py::arg("ph"), py::arg("pw"), py::arg("R"), py::arg("S"), py::arg("pad_h"), py::arg("pad_w"),
+        py::arg("w_off"), py::arg("zph"), py::arg("zpw"), py::arg("bco"), py::arg("stream"), py::arg("bn_z") = 0,
+        py::arg("bn_mean") = 0, py::arg("bn_scale") = 0, py::arg("bn_shift") = 0, py::arg("bn_part") = 0,
+        py::arg("bn_nparts") = 0);
   // 512-thread big-tile kernel: variant 0..3 = 256x256, 128x256, 64x512, 256x128 (co x pix), 4 / 5 =
   // 128x256 / 256x128 at two workgroups per CU;
   // part (optional): channel-major [2][K][nparts] BatchNorm sum / sum-of-squares partials of y

@@ -22,6 +22,7 @@
 // is covered by C/8 lanes so loads are fully coalesced for any C % 8 == 0.
 // Reductions: per-thread fp32 registers -> LDS tree -> per-block partials ->
 // one block per channel combines the (channel-major) partials in fp64.
+#include <cstdlib>
 #include <stdexcept>
 
 #include <algorithm>
@@ -335,9 +336,110 @@ __global__ void __launch_bounds__(kBnThreads) bn_bwd_apply_kernel(
   }
 }
 
+// Residual-tail backward apply (mask from the forward's bits) that also reduces the statistics of
+// the BatchNorm that produced the tail's addend (a projection shortcut's BN, no ReLU): its incoming
+// gradient is exactly dz, so sum(dz) and sum(dz * (z_ds - mean_ds)) are accumulated here while dz is
+// in registers -- the shortcut BN's own reduction pass (a re-read of dz and z_ds) is not run.
+// Geometry of bn_reduce_kernel (fixed 8-channel group per thread, rows strided by rpi).
+template <typename T>
+__global__ void __launch_bounds__(kBnThreads) bn_tail_bwd_ds_kernel(
+    const T* __restrict__ x, const T* __restrict__ dy, const uint8_t* __restrict__ mask,
+    const float* __restrict__ A, const float* __restrict__ B, const float* __restrict__ Cc, T* __restrict__ dx,
+    T* __restrict__ dz_out, const T* __restrict__ zds, const float* __restrict__ mean_ds, float* __restrict__ part1,
+    float* __restrict__ part2, int64_t R, int C, int tpr, int rpi, int64_t rows_per_block) {
+  const int tid = threadIdx.x;
+  const int lane_c = tid % tpr;
+  const int lane_r = tid / tpr;
+  const int cbase = blockIdx.y * tpr * 8 + lane_c * 8;
+  float s1[8], s2[8], ka[8], kb[8], kc[8], km[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    s1[i] = 0.f;
+    s2[i] = 0.f;
+    ka[i] = A[cbase + i];
+    kb[i] = B[cbase + i];
+    kc[i] = Cc[cbase + i];
+    km[i] = mean_ds[cbase + i];
+  }
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  int64_t r1 = r0 + rows_per_block;
+  if (r1 > R) r1 = R;
+  const bool spare = lane_r >= rpi;
+  if (spare) r1 = r0;
+  constexpr int UNR = 2;
+  auto body = [&](const Vec8<T>& vx, const Vec8<T>& vdy, const Vec8<T>& vz, uint32_t mb, int64_t off) {
+    Vec8<T> out, dz;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float d = ((mb >> i) & 1u) ? vdy.get(i) : 0.f;
+      dz.set(i, d);
+      out.set(i, ka[i] * d + kb[i] * vx.get(i) + kc[i]);
+      s1[i] += d;
+      s2[i] += d * (vz.get(i) - km[i]);
+    }
+    out.store(dx + off);
+    dz.store(dz_out + off);
+  };
+  int64_t r = r0 + lane_r;
+  for (; r + (UNR - 1) * rpi < r1; r += UNR * rpi) {
+    Vec8<T> vx[UNR], vdy[UNR], vz[UNR];
+    uint32_t vm[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int64_t off = (r + u * rpi) * C + cbase;
+      vx[u].load(x + off);
+      vdy[u].load(dy + off);
+      vz[u].load(zds + off);
+      vm[u] = mask[off >> 3];
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) body(vx[u], vdy[u], vz[u], vm[u], (r + u * rpi) * C + cbase);
+  }
+  for (; r < r1; r += rpi) {
+    const int64_t off = r * C + cbase;
+    Vec8<T> vx, vdy, vz;
+    vx.load(x + off);
+    vdy.load(dy + off);
+    vz.load(zds + off);
+    body(vx, vdy, vz, mask[off >> 3], off);
+  }
+  __shared__ float sh1[kBnThreads * 8];
+  __shared__ float sh2[kBnThreads * 8];
+  const int cb = tpr * 8;
+  if (!spare) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sh1[lane_r * cb + lane_c * 8 + i] = s1[i];
+      sh2[lane_r * cb + lane_c * 8 + i] = s2[i];
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < cb; c += kBnThreads) {
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < rpi; ++rr) {
+      a += sh1[rr * cb + c];
+      b += sh2[rr * cb + c];
+    }
+    const int64_t o = static_cast<int64_t>(blockIdx.y * cb + c) * gridDim.x + blockIdx.x;
+    part1[o] = a;
+    part2[o] = b;
+  }
+}
+
 // ---------------------------------------------------------------- launchers
 
-static inline int64_t bn_rows_per_block(int64_t R, int C, const BnGeom& g, int* nblk, int total_blocks = 512) {
+// workgroups of the reduction-geometry kernels (bn_reduce, bn_tail_bwd_ds): MXAMD_BN_BLOCKS, default 512
+static int bn_total_blocks() {
+  static const int v = [] {
+    const char* e = std::getenv("MXAMD_BN_BLOCKS");
+    const int n = e ? std::atoi(e) : 0;
+    return n >= 64 && n <= 16384 ? n : 512;
+  }();
+  return v;
+}
+
+static inline int64_t bn_rows_per_block(int64_t R, int C, const BnGeom& g, int* nblk,
+                                        int total_blocks = bn_total_blocks()) {
   const int cblocks = C / g.cb;
   int64_t target = total_blocks / cblocks;   // default ~2 blocks per CU; partial rows stay few
   if (target < 8) target = 8;
@@ -411,7 +513,7 @@ static void bn_backward_impl(const void* x, const void* dy, const void* y, const
                              const float* gamma, const float* mean, const float* invstd, const float* fscale,
                              const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R,
                              int C, int relu_mode, int fix_gamma, int training, int accum, hipStream_t s,
-                             int ext_nblk) {
+                             int ext_nblk, const void* ds_z, const float* ds_mean, float* ds_part) {
   BnGeom g = bn_geom(C);
   int nblk;
   int64_t rpb = bn_rows_per_block(R, C, g, &nblk);
@@ -446,6 +548,17 @@ static void bn_backward_impl(const void* x, const void* dy, const void* y, const
   if (blocks > 256 * 16) blocks = 256 * 16;
   T* dxa = static_cast<T*>(dx);
   T* dza = static_cast<T*>(dz);
+  if (ds_z) {
+    // residual tail whose addend came from a shortcut BatchNorm: its backward statistics ride along
+    MXAMD_HOST_CHECK(relu_mode == kReluFromMask && dz && ds_mean && ds_part,
+                     "bn_nhwc_backward: shortcut statistics need the tail's mask mode, dz and the BN's mean");
+    int dnblk;
+    const int64_t drpb = bn_rows_per_block(R, C, g, &dnblk);
+    hipLaunchKernelGGL((bn_tail_bwd_ds_kernel<T>), dim3(dnblk, C / g.cb), dim3(kBnThreads), 0, s, xa, dya, mask, A, B,
+                       Cc, dxa, dza, static_cast<const T*>(ds_z), ds_mean, ds_part,
+                       ds_part + static_cast<int64_t>(dnblk) * C, R, C, g.tpr, g.rpi, drpb);
+    return;
+  }
 #define BWD(RL, WD)                                                                                      \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RL, WD>), dim3(blocks), dim3(kBnThreads), 0, s, xa, dya, ya, mask, A, B, \
                      Cc, fscale, fshift, dxa, dza, nvec, C)
@@ -619,19 +732,21 @@ void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, c
                       void* dz,
                       const float* gamma, const float* mean, const float* invstd, const float* fscale,
                       const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R, int C,
-                      int relu_mode, int fix_gamma, int training, int accum, hipStream_t s, int ext_nblk) {
+                      int relu_mode, int fix_gamma, int training, int accum, hipStream_t s, int ext_nblk,
+                      const void* ds_z, const float* ds_mean, float* ds_part) {
   switch (dtype) {
     case kF16:
       bn_backward_impl<__half>(x, dy, y, mask, dx, dz, gamma, mean, invstd, fscale, fshift, part, dgamma, dbeta, coef, R,
-                               C, relu_mode, fix_gamma, training, accum, s, ext_nblk);
+                               C, relu_mode, fix_gamma, training, accum, s, ext_nblk, ds_z, ds_mean, ds_part);
       break;
     case kBF16:
       bn_backward_impl<__hip_bfloat16>(x, dy, y, mask, dx, dz, gamma, mean, invstd, fscale, fshift, part, dgamma, dbeta,
-                                       coef, R, C, relu_mode, fix_gamma, training, accum, s, ext_nblk);
+                                       coef, R, C, relu_mode, fix_gamma, training, accum, s, ext_nblk, ds_z, ds_mean,
+                                       ds_part);
       break;
     default:
       bn_backward_impl<float>(x, dy, y, mask, dx, dz, gamma, mean, invstd, fscale, fshift, part, dgamma, dbeta, coef, R,
-                              C, relu_mode, fix_gamma, training, accum, s, ext_nblk);
+                              C, relu_mode, fix_gamma, training, accum, s, ext_nblk, ds_z, ds_mean, ds_part);
   }
 }
 

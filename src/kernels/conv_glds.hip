@@ -51,6 +51,25 @@ struct GeomG {
   int64_t zob[3];
 };
 
+// optional BatchNorm-backward statistics of the output (y is the gradient of a BN(+ReLU) output whose
+// input is z; ReLU mask recomputed as z*scale + shift > 0, none when scale/shift are null): per-channel (sum dz, sum dz*(z - mean))
+// partials, channel-major [2][K][nparts], one per (pixel tile, pixel wave) -- the BN's own reduction
+// pass over (y, z) is then skipped
+struct BnbG {
+  const void* z;
+  const float* mean;
+  const float* scale;
+  const float* shift;
+  float* part;
+  int nparts;
+};
+
+__device__ __forceinline__ float sum16(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
   __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)lds_base, 16, 0, 0);
 }
@@ -58,13 +77,15 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
 template <typename T, int BCO>
 __device__ __forceinline__ void glds_body(const T* __restrict__ x, const T* __restrict__ w,
                                           const float* __restrict__ bias, T* __restrict__ y,
-                                          const T* __restrict__ zero, const GeomG& g, int tiles_co);
+                                          const T* __restrict__ zero, const GeomG& g, int tiles_co,
+                                          const BnbG& bn, int part_base);
 
 template <typename T, int BCO>
 __global__ void __launch_bounds__(256) conv_fwd_glds_kernel(const T* __restrict__ x, const T* __restrict__ w,
                                                             const float* __restrict__ bias, T* __restrict__ y,
-                                                            const T* __restrict__ zero, GeomG g, int tiles_co) {
-  glds_body<T, BCO>(x, w, bias, y, zero, g, tiles_co);
+                                                            const T* __restrict__ zero, GeomG g, int tiles_co,
+                                                            BnbG bn) {
+  glds_body<T, BCO>(x, w, bias, y, zero, g, tiles_co, bn, 0);
 }
 
 // All sub-pixel phases of a strided data gradient in one launch: blockIdx.y picks the phase (its
@@ -78,15 +99,17 @@ struct PhaseSet {
 template <typename T, int BCO>
 __global__ void __launch_bounds__(256) conv_phase_glds_kernel(const T* __restrict__ dy, const T* __restrict__ w,
                                                               T* __restrict__ dx, const T* __restrict__ zero,
-                                                              PhaseSet ps, int tiles_co) {
+                                                              PhaseSet ps, int tiles_co, BnbG bn) {
   const int ph = blockIdx.y;
-  glds_body<T, BCO>(dy, w + ps.w_off[ph], nullptr, dx, zero, ps.g[ph], tiles_co);
+  // each phase's (pixel tile, wave) partials get their own slots
+  glds_body<T, BCO>(dy, w + ps.w_off[ph], nullptr, dx, zero, ps.g[ph], tiles_co, bn, ph * bn.nparts / gridDim.y);
 }
 
 template <typename T, int BCO>
 __device__ __forceinline__ void glds_body(const T* __restrict__ x, const T* __restrict__ w,
                                           const float* __restrict__ bias, T* __restrict__ y,
-                                          const T* __restrict__ zero, const GeomG& g, int tiles_co) {
+                                          const T* __restrict__ zero, const GeomG& g, int tiles_co,
+                                          const BnbG& bn, int part_base) {
   constexpr int WAVES_CO = BCO / 64;
   constexpr int WAVES_PIX = 4 / WAVES_CO;
   constexpr int BPIX = WAVES_PIX * 64;
@@ -200,6 +223,8 @@ __device__ __forceinline__ void glds_body(const T* __restrict__ x, const T* __re
 
   // ---- epilogue: lane holds co = base + 4*(lane>>4) + {0..3} for pixel base + (lane&15)
   const int co_l = (lane >> 4) * 4;
+  const bool bnb = bn.part != nullptr;
+  const T* zb = static_cast<const T*>(bn.z);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int co = co0 + wco * 64 + i * 16 + co_l;
@@ -210,6 +235,17 @@ __device__ __forceinline__ void glds_body(const T* __restrict__ x, const T* __re
       b2 = bias[co + 2];
       b3 = bias[co + 3];
     }
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+    float bm[4], bsc[4], bsh[4];
+    if (bnb) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        bm[t] = bn.mean[co + t];
+        // no scale/shift: a BN without ReLU -- 0*z + 1 > 0 keeps every element
+        bsc[t] = bn.scale ? bn.scale[co + t] : 0.f;
+        bsh[t] = bn.shift ? bn.shift[co + t] : 1.f;
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int p = pix0 + wpix * 64 + j * 16 + frag_r;
@@ -219,6 +255,34 @@ __device__ __forceinline__ void glds_body(const T* __restrict__ x, const T* __re
         const int64_t off = q * g.og + (p - q * g.Wo) * g.oc + g.ob;
         *reinterpret_cast<uint2*>(y + off + co) = v;
         for (int z = 0; z < g.nz; ++z) *reinterpret_cast<uint2*>(y + off - g.ob + g.zob[z] + co) = uint2{0u, 0u};
+        if (bnb) {
+          // statistics of the stored (rounded) gradient, as the BN's own pass would read it
+          const float4 dv = Mfma<T>::unpack4(v);
+          const float4 zv = Mfma<T>::unpack4(*reinterpret_cast<const uint2*>(zb + off + co));
+          const float d4[4] = {dv.x, dv.y, dv.z, dv.w}, z4[4] = {zv.x, zv.y, zv.z, zv.w};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const float dz = fmaf(z4[t], bsc[t], bsh[t]) > 0.f ? d4[t] : 0.f;
+            s1[t] += dz;
+            s2[t] += dz * (z4[t] - bm[t]);
+          }
+        }
+      }
+    }
+    if (bnb) {
+      // the 16 lanes of a channel group hold different pixels: sum them, one partial per wave
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s1[t] = sum16(s1[t]);
+        s2[t] = sum16(s2[t]);
+      }
+      if (frag_r == 0) {
+        const int pid = part_base + tpix * WAVES_PIX + wpix;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          bn.part[static_cast<int64_t>(co + t) * bn.nparts + pid] = s1[t];
+          bn.part[(static_cast<int64_t>(g.K) + co + t) * bn.nparts + pid] = s2[t];
+        }
       }
     }
   }
@@ -226,21 +290,29 @@ __device__ __forceinline__ void glds_body(const T* __restrict__ x, const T* __re
 
 template <typename T, int BCO>
 void launch_glds(const void* x, const void* w, const float* bias, void* y, const void* zero, const GeomG& g,
-                 hipStream_t s) {
+                 hipStream_t s, const BnbG& bn) {
   constexpr int BPIX = (4 / (BCO / 64)) * 64;
   const int tiles_co = g.K / BCO;
   const int tiles_pix = (g.M + BPIX - 1) / BPIX;
   hipLaunchKernelGGL((conv_fwd_glds_kernel<T, BCO>), dim3(tiles_co * tiles_pix), dim3(256), 0, s,
                      static_cast<const T*>(x), static_cast<const T*>(w), bias, static_cast<T*>(y),
-                     static_cast<const T*>(zero), g, tiles_co);
+                     static_cast<const T*>(zero), g, tiles_co, bn);
 }
 
 }  // namespace
 
 // bco: 128 (128x128 tile) or 64 (64 co x 256 pix).  zero: >= 128 bytes of zeros (device).
+// BN-backward partials per channel of a glds launch over M output pixels (pixel tiles x pixel waves).
+int conv_glds_bwd_nparts(int M, int bco) {
+  const int bpix = bco == 128 ? 128 : 256;
+  const int waves_pix = bco == 128 ? 2 : 4;
+  return ((M + bpix - 1) / bpix) * waves_pix;
+}
+
 void conv_nhwc_fwd_glds(int dtype, const void* x, const void* w, const float* bias, void* y, const void* zero, int N,
                         int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int bco,
-                        hipStream_t s) {
+                        hipStream_t s, const void* bn_z, const float* bn_mean, const float* bn_scale,
+                        const float* bn_shift, float* bn_part, int bn_nparts) {
   GeomG g;
   g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S;
   g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw;
@@ -257,12 +329,15 @@ void conv_nhwc_fwd_glds(int dtype, const void* x, const void* w, const float* bi
   MXAMD_HOST_CHECK((int64_t)N * H * W * C < (1ll << 31) && (int64_t)g.M * K < (1ll << 31) &&
                        (int64_t)K * g.Ktot < (1ll << 31),
                    "conv_nhwc_fwd_glds: tensor too large for 32-bit indexing");
+  const BnbG bn{bn_z, bn_mean, bn_scale, bn_shift, bn_part, bn_nparts};
+  MXAMD_HOST_CHECK(!bn_part || (bn_z && bn_mean && !bn_scale == !bn_shift && bn_nparts == conv_glds_bwd_nparts(g.M, bco)),
+                   "conv_nhwc_fwd_glds: BN-backward statistics need z, mean, scale, shift and nparts");
   if (dtype == kF16) {
-    if (bco == 128) launch_glds<__half, 128>(x, w, bias, y, zero, g, s);
-    else launch_glds<__half, 64>(x, w, bias, y, zero, g, s);
+    if (bco == 128) launch_glds<__half, 128>(x, w, bias, y, zero, g, s, bn);
+    else launch_glds<__half, 64>(x, w, bias, y, zero, g, s, bn);
   } else if (dtype == kBF16) {
-    if (bco == 128) launch_glds<__hip_bfloat16, 128>(x, w, bias, y, zero, g, s);
-    else launch_glds<__hip_bfloat16, 64>(x, w, bias, y, zero, g, s);
+    if (bco == 128) launch_glds<__hip_bfloat16, 128>(x, w, bias, y, zero, g, s, bn);
+    else launch_glds<__hip_bfloat16, 64>(x, w, bias, y, zero, g, s, bn);
   } else {
     throw std::runtime_error("conv_nhwc_fwd_glds: dtype must be f16 or bf16");
   }
@@ -276,7 +351,8 @@ void conv_nhwc_dgrad_phases_glds(int dtype, const void* dy, const void* w, void*
                                  int Wi, int Cin, int Cout, int Ho, int Wo, int stride, int nph, const int* ph,
                                  const int* pw, const int* R, const int* S, const int* pad_h, const int* pad_w,
                                  const int64_t* w_off, int nzero, const int* zph, const int* zpw, int bco,
-                                 hipStream_t s) {
+                                 hipStream_t s, const void* bn_z, const float* bn_mean, const float* bn_scale,
+                                 const float* bn_shift, float* bn_part, int bn_nparts) {
   MXAMD_HOST_CHECK(nph >= 1 && nph <= kMaxPhases, "conv_nhwc_dgrad_phases_glds: 1..4 phases");
   MXAMD_HOST_CHECK(nzero >= 0 && nzero <= 3, "conv_nhwc_dgrad_phases_glds: at most 3 zero phases");
   MXAMD_HOST_CHECK(Cin % 64 == 0 && Cout % bco == 0 && (bco == 64 || bco == 128) && stride >= 1 && Ho > 0 &&
@@ -311,9 +387,15 @@ void conv_nhwc_dgrad_phases_glds(int dtype, const void* dy, const void* w, void*
   const int tiles_co = Cout / bco;
   const int tiles_pix = (N * Ho * Wo + bpix - 1) / bpix;
   dim3 grid(tiles_co * tiles_pix, nph);
+  // partials: every phase gets conv_glds_bwd_nparts(N*Ho*Wo) slots (nparts = nph * that)
+  const BnbG bn{bn_z, bn_mean, bn_scale, bn_shift, bn_part, bn_nparts};
+  // (phases no tap reaches hold zero gradient: they add nothing to the statistics)
+  MXAMD_HOST_CHECK(!bn_part || (bn_z && bn_mean && !bn_scale == !bn_shift &&
+                                bn_nparts == nph * conv_glds_bwd_nparts(N * Ho * Wo, bco)),
+                   "conv_nhwc_dgrad_phases_glds: BN-backward statistics need z, mean, scale, shift and nparts");
 #define MXAMD_PHASES(T, B)                                                                                  \
   hipLaunchKernelGGL((conv_phase_glds_kernel<T, B>), grid, dim3(256), 0, s, static_cast<const T*>(dy),     \
-                     static_cast<const T*>(w), static_cast<T*>(dx), static_cast<const T*>(zero), ps, tiles_co)
+                     static_cast<const T*>(w), static_cast<T*>(dx), static_cast<const T*>(zero), ps, tiles_co, bn)
   if (dtype == kF16) {
     if (bco == 128) MXAMD_PHASES(__half, 128);
     else MXAMD_PHASES(__half, 64);

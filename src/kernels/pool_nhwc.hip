@@ -19,18 +19,21 @@ struct PoolGeom {
   int count_include_pad;
 };
 
-template <typename T, bool MAX>
+// I: the index type -- uint32_t whenever every element offset fits (the pixel / channel decomposition
+// of each vector index is 3 divisions; 64-bit ones are software routines that made the ResNet-50
+// stem pooling backward instruction-bound at ~2 TB/s)
+template <typename T, bool MAX, typename I>
 __global__ void __launch_bounds__(256) pool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
-                                                       uint8_t* __restrict__ arg, PoolGeom g, int64_t nvec) {
-  const int cv = g.C / 8;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec;
-       v += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+                                                       uint8_t* __restrict__ arg, PoolGeom g, I nvec) {
+  const I cv = static_cast<I>(g.C / 8);
+  for (I v = static_cast<I>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec;
+       v += static_cast<I>(gridDim.x) * blockDim.x) {
     const int c8 = static_cast<int>(v % cv) * 8;
-    int64_t p = v / cv;
-    const int wo = static_cast<int>(p % g.Wo);
-    p /= g.Wo;
-    const int ho = static_cast<int>(p % g.Ho);
-    const int n = static_cast<int>(p / g.Ho);
+    I p = v / cv;
+    const int wo = static_cast<int>(p % static_cast<I>(g.Wo));
+    p /= static_cast<I>(g.Wo);
+    const int ho = static_cast<int>(p % static_cast<I>(g.Ho));
+    const int n = static_cast<int>(p / static_cast<I>(g.Ho));
     const int h0 = ho * g.sh - g.ph, w0 = wo * g.sw - g.pw;
     float acc[8];
     uint8_t am[8];
@@ -47,7 +50,7 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(const T* __restrict__ x, 
         const int w = w0 + b;
         if ((unsigned)w >= (unsigned)g.W) continue;
         Vec8<T> vx;
-        vx.load(x + ((static_cast<int64_t>(n) * g.H + h) * g.W + w) * g.C + c8);
+        vx.load(x + ((static_cast<I>(n) * g.H + h) * g.W + w) * g.C + c8);
         ++cnt;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -70,7 +73,7 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(const T* __restrict__ x, 
       uint2 packed;
       packed.x = am[0] | (am[1] << 8) | (am[2] << 16) | (static_cast<uint32_t>(am[3]) << 24);
       packed.y = am[4] | (am[5] << 8) | (am[6] << 16) | (static_cast<uint32_t>(am[7]) << 24);
-      *reinterpret_cast<uint2*>(arg + v * 8) = packed;
+      *reinterpret_cast<uint2*>(arg + static_cast<int64_t>(v) * 8) = packed;
     } else {
       int den = cnt;
       if (g.count_include_pad) {
@@ -81,22 +84,22 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(const T* __restrict__ x, 
 #pragma unroll
       for (int i = 0; i < 8; ++i) out.set(i, acc[i] * inv);
     }
-    out.store(y + v * 8);
+    out.store(y + static_cast<int64_t>(v) * 8);
   }
 }
 
-template <typename T, bool MAX>
+template <typename T, bool MAX, typename I>
 __global__ void __launch_bounds__(256) pool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ arg,
-                                                       T* __restrict__ dx, PoolGeom g, int64_t nvec) {
-  const int cv = g.C / 8;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec;
-       v += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+                                                       T* __restrict__ dx, PoolGeom g, I nvec) {
+  const I cv = static_cast<I>(g.C / 8);
+  for (I v = static_cast<I>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec;
+       v += static_cast<I>(gridDim.x) * blockDim.x) {
     const int c8 = static_cast<int>(v % cv) * 8;
-    int64_t p = v / cv;
-    const int w = static_cast<int>(p % g.W);
-    p /= g.W;
-    const int h = static_cast<int>(p % g.H);
-    const int n = static_cast<int>(p / g.H);
+    I p = v / cv;
+    const int w = static_cast<int>(p % static_cast<I>(g.W));
+    p /= static_cast<I>(g.W);
+    const int h = static_cast<int>(p % static_cast<I>(g.H));
+    const int n = static_cast<int>(p / static_cast<I>(g.H));
     // output windows covering (h, w): ho*sh - ph <= h <= ho*sh - ph + kh - 1
     const int hp = h + g.ph, wp = w + g.pw;
     const int ho_lo = hp - g.kh + 1 > 0 ? (hp - g.kh + g.sh) / g.sh : 0;
@@ -108,7 +111,7 @@ __global__ void __launch_bounds__(256) pool_bwd_kernel(const T* __restrict__ dy,
     for (int i = 0; i < 8; ++i) acc[i] = 0.f;
     for (int ho = ho_lo; ho <= ho_hi; ++ho) {
       for (int wo = wo_lo; wo <= wo_hi; ++wo) {
-        const int64_t o = ((static_cast<int64_t>(n) * g.Ho + ho) * g.Wo + wo) * g.C + c8;
+        const I o = ((static_cast<I>(n) * g.Ho + ho) * g.Wo + wo) * g.C + c8;
         Vec8<T> vd;
         vd.load(dy + o);
         if (MAX) {
@@ -140,8 +143,16 @@ __global__ void __launch_bounds__(256) pool_bwd_kernel(const T* __restrict__ dy,
     Vec8<T> out;
 #pragma unroll
     for (int i = 0; i < 8; ++i) out.set(i, acc[i]);
-    out.store(dx + v * 8);
+    out.store(dx + static_cast<int64_t>(v) * 8);
   }
+}
+
+// every element offset of x and y (and the loop index plus one grid stride) fits in 32 bits
+static inline bool fits32(const PoolGeom& g) {
+  const int64_t big = static_cast<int64_t>(g.N) * g.C * (g.H * static_cast<int64_t>(g.W) > g.Ho * static_cast<int64_t>(g.Wo)
+                                                            ? g.H * static_cast<int64_t>(g.W)
+                                                            : g.Ho * static_cast<int64_t>(g.Wo));
+  return big + 256LL * 32 * 256 * 8 < (1LL << 32);
 }
 
 static inline int grid_for(int64_t nvec) {
@@ -152,23 +163,31 @@ static inline int grid_for(int64_t nvec) {
 template <typename T>
 static void pool_fwd_t(int is_max, const void* x, void* y, uint8_t* arg, const PoolGeom& g, hipStream_t s) {
   const int64_t nvec = static_cast<int64_t>(g.N) * g.Ho * g.Wo * (g.C / 8);
-  if (is_max)
-    hipLaunchKernelGGL((pool_fwd_kernel<T, true>), dim3(grid_for(nvec)), dim3(256), 0, s,
-                       static_cast<const T*>(x), static_cast<T*>(y), arg, g, nvec);
-  else
-    hipLaunchKernelGGL((pool_fwd_kernel<T, false>), dim3(grid_for(nvec)), dim3(256), 0, s,
-                       static_cast<const T*>(x), static_cast<T*>(y), arg, g, nvec);
+  const bool small = fits32(g);
+#define MXAMD_POOL_FWD(MX, I)                                                                               \
+  hipLaunchKernelGGL((pool_fwd_kernel<T, MX, I>), dim3(grid_for(nvec)), dim3(256), 0, s,                     \
+                     static_cast<const T*>(x), static_cast<T*>(y), arg, g, static_cast<I>(nvec))
+  if (is_max) {
+    if (small) MXAMD_POOL_FWD(true, uint32_t); else MXAMD_POOL_FWD(true, int64_t);
+  } else {
+    if (small) MXAMD_POOL_FWD(false, uint32_t); else MXAMD_POOL_FWD(false, int64_t);
+  }
+#undef MXAMD_POOL_FWD
 }
 
 template <typename T>
 static void pool_bwd_t(int is_max, const void* dy, const uint8_t* arg, void* dx, const PoolGeom& g, hipStream_t s) {
   const int64_t nvec = static_cast<int64_t>(g.N) * g.H * g.W * (g.C / 8);
-  if (is_max)
-    hipLaunchKernelGGL((pool_bwd_kernel<T, true>), dim3(grid_for(nvec)), dim3(256), 0, s,
-                       static_cast<const T*>(dy), arg, static_cast<T*>(dx), g, nvec);
-  else
-    hipLaunchKernelGGL((pool_bwd_kernel<T, false>), dim3(grid_for(nvec)), dim3(256), 0, s,
-                       static_cast<const T*>(dy), arg, static_cast<T*>(dx), g, nvec);
+  const bool small = fits32(g);
+#define MXAMD_POOL_BWD(MX, I)                                                                               \
+  hipLaunchKernelGGL((pool_bwd_kernel<T, MX, I>), dim3(grid_for(nvec)), dim3(256), 0, s,                     \
+                     static_cast<const T*>(dy), arg, static_cast<T*>(dx), g, static_cast<I>(nvec))
+  if (is_max) {
+    if (small) MXAMD_POOL_BWD(true, uint32_t); else MXAMD_POOL_BWD(true, int64_t);
+  } else {
+    if (small) MXAMD_POOL_BWD(false, uint32_t); else MXAMD_POOL_BWD(false, int64_t);
+  }
+#undef MXAMD_POOL_BWD
 }
 
 static PoolGeom make_geom(int N, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw,
