@@ -74,6 +74,7 @@ def _leaf_grad(t, numel=None, dtype=torch.float32):
 
 _RELU_FROM_X = [True]    # BN+ReLU backward recomputes the mask from x (debug switch)
 _BN_BWD_FUSE = [os.environ.get('MXAMD_BN_BWD_FUSE', '1') != '0']   # BN-backward stats in dgrad epilogues
+_BN_TAIL_DS = [os.environ.get('MXAMD_BN_TAIL_DS', '1') != '0']     # shortcut-BN stats in the tail backward
 _ZEROS = {}
 
 
@@ -158,7 +159,7 @@ class BatchNormNHWC(torch.autograd.Function):
         # residual tail fed by a projection shortcut's BatchNorm (no ReLU): the tail's backward apply
         # also reduces that BN's backward statistics (its incoming gradient is the tail's dz)
         ctx.add_src = None
-        if relu_mode == 3 and training and _BN_BWD_FUSE[0]:
+        if relu_mode == 3 and training and _BN_BWD_FUSE[0] and _BN_TAIL_DS[0]:
             src = getattr(addend, '_mxamd_bn_src', None)
             if (src is not None and src[5] == 0 and tuple(src[0].shape) == tuple(x.shape)
                     and src[0].dtype == x.dtype and src[0].is_contiguous()):
@@ -209,7 +210,7 @@ class BatchNormNHWC(torch.autograd.Function):
         ds = ctx.add_src if dz is not None else None
         dkw = {}
         if ds is not None:
-            ds_nblk = lib.bn_partials_rows(R, C)
+            ds_nblk = lib.bn_tail_ds_rows(R, C)
             ds_part = torch.empty(2 * ds_nblk * C, dtype=torch.float32, device=dev)
             dkw = dict(ds_z=ds[0].data_ptr(), ds_mean=ds[1].data_ptr(), ds_part=ds_part.data_ptr())
         lib.bn_nhwc_backward(_DT[x.dtype], x.data_ptr(), gy.data_ptr(), _p(y), _p(ymask), dx.data_ptr(), _p(dz),

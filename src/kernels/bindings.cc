@@ -27,6 +27,7 @@ void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, c
                       const float* fshift, float* part, float* dgamma, float* dbeta, float* coef, int64_t R, int C,
                       int relu_mode, int fix_gamma, int training, int accum, hipStream_t s, int ext_nblk, const void* ds_z, const float* ds_mean, float* ds_part);
 int bn_partials_rows(int64_t R, int C);
+int bn_tail_ds_rows(int64_t R, int C);
 void gemm_nt(int dtype, const void* a, const void* b, const float* bias, const void* addend, void* c, int out_f32,
              int M, int N, int K, int lda, int ldb, int ldc, int act, int cfg, int splits, float* ws, hipStream_t s);
 int gemm_nt_tile_n(int cfg);
@@ -192,6 +193,7 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.attr("arch") = "gfx950";
 
   m.def("bn_partials_rows", &bn_partials_rows);
+  m.def("bn_tail_ds_rows", &bn_tail_ds_rows);
   m.def("bn_nhwc_stats", [](int dt, uintptr_t x, uintptr_t center, uintptr_t part, int64_t R, int C, uintptr_t s) {
     int nblk = bn_nhwc_stats(dt, P<const void>(x), P<const float>(center), P<float>(part), R, C, S(s), 512);
     check_launch("bn_nhwc_stats");
