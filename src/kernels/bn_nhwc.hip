@@ -248,6 +248,19 @@ __global__ void __launch_bounds__(kFinThreads) bn_finalize_kernel(
   }
 }
 
+__device__ __forceinline__ void load8f(const float* __restrict__ p, float* o) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+
+// The apply kernels stream 8-element vectors with a grid-stride loop.  When the stride (blocks x 256
+// threads x 8 elements, a multiple of 2048) is a multiple of C -- every C dividing 2048, i.e. all of
+// ResNet's -- each thread keeps one channel group for its whole life: its per-channel coefficients are
+// loaded once into registers instead of per vector (they were 2-5 extra 32-byte cache loads per 16-byte
+// tensor load, L1 traffic that held these kernels near 5 TB/s), and two vectors per iteration are in
+// flight.  Other C fall back to per-vector coefficient loads.
+
 // y = x * scale + shift (+ addend) (relu)
 // MASK: also write the ReLU mask, one byte per 8-element vector (bit i = y[8v+i] > 0)
 template <typename T, bool ADD, bool RELU, bool MASK>
@@ -260,18 +273,9 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_kernel(
   // the channel by a fixed step (< C), so no per-iteration 64-bit modulo.
   int c = static_cast<int>((v * 8) % C);
   const int cstep = static_cast<int>((stride * 8) % C);
-  for (; v < nvec; v += stride, c = (c + cstep >= C) ? c + cstep - C : c + cstep) {
-    const int64_t off = v * 8;
-    Vec8<T> vx, out;
-    vx.load(x + off);
-    const float4 s0 = *reinterpret_cast<const float4*>(scale + c);
-    const float4 s1 = *reinterpret_cast<const float4*>(scale + c + 4);
-    const float4 h0 = *reinterpret_cast<const float4*>(shift + c);
-    const float4 h1 = *reinterpret_cast<const float4*>(shift + c + 4);
-    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-    Vec8<T> va;
-    if (ADD) va.load(addend + off);
+  float sc[8], sh[8];
+  auto compute = [&](const Vec8<T>& vx, const Vec8<T>& va, int64_t vv) {
+    Vec8<T> out;
     uint32_t bits = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -281,8 +285,38 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_kernel(
       if (RELU) r = r > 0.f ? r : 0.f;
       out.set(i, r);
     }
-    out.store(y + off);
-    if (MASK) mask[v] = static_cast<uint8_t>(bits);
+    out.store(y + vv * 8);
+    if (MASK) mask[vv] = static_cast<uint8_t>(bits);
+  };
+  if (cstep == 0) {
+    load8f(scale + c, sc);
+    load8f(shift + c, sh);
+    for (; v + stride < nvec; v += 2 * stride) {
+      Vec8<T> vx0, vx1, va0, va1;
+      vx0.load(x + v * 8);
+      vx1.load(x + (v + stride) * 8);
+      if (ADD) {
+        va0.load(addend + v * 8);
+        va1.load(addend + (v + stride) * 8);
+      }
+      compute(vx0, va0, v);
+      compute(vx1, va1, v + stride);
+    }
+    if (v < nvec) {
+      Vec8<T> vx, va;
+      vx.load(x + v * 8);
+      if (ADD) va.load(addend + v * 8);
+      compute(vx, va, v);
+    }
+    return;
+  }
+  for (; v < nvec; v += stride, c = (c + cstep >= C) ? c + cstep - C : c + cstep) {
+    Vec8<T> vx, va;
+    vx.load(x + v * 8);
+    if (ADD) va.load(addend + v * 8);
+    load8f(scale + c, sc);
+    load8f(shift + c, sh);
+    compute(vx, va, v);
   }
 }
 
@@ -297,42 +331,61 @@ __global__ void __launch_bounds__(kBnThreads) bn_bwd_apply_kernel(
   int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   int c = static_cast<int>((v * 8) % C);
   const int cstep = static_cast<int>((stride * 8) % C);
-  for (; v < nvec; v += stride, c = (c + cstep >= C) ? c + cstep - C : c + cstep) {
-    const int64_t off = v * 8;
-    Vec8<T> vx, vdy, vy, out, dz;
-    vx.load(x + off);
-    vdy.load(dy + off);
-    if (RELU == kReluFromY) vy.load(y + off);
-    const uint32_t mb = RELU == kReluFromMask ? mask[v] : 0u;
-    float fs[8], fh[8];
+  float fs[8], fh[8], ka[8], kb[8], kc[8];
+  auto coef = [&](int cc) {
     if (RELU == kReluFromX) {
-      const float4 s0 = *reinterpret_cast<const float4*>(fscale + c);
-      const float4 s1 = *reinterpret_cast<const float4*>(fscale + c + 4);
-      const float4 h0 = *reinterpret_cast<const float4*>(fshift + c);
-      const float4 h1 = *reinterpret_cast<const float4*>(fshift + c + 4);
-      fs[0] = s0.x; fs[1] = s0.y; fs[2] = s0.z; fs[3] = s0.w; fs[4] = s1.x; fs[5] = s1.y; fs[6] = s1.z; fs[7] = s1.w;
-      fh[0] = h0.x; fh[1] = h0.y; fh[2] = h0.z; fh[3] = h0.w; fh[4] = h1.x; fh[5] = h1.y; fh[6] = h1.z; fh[7] = h1.w;
+      load8f(fscale + cc, fs);
+      load8f(fshift + cc, fh);
     }
-    const float4 a0 = *reinterpret_cast<const float4*>(A + c);
-    const float4 a1 = *reinterpret_cast<const float4*>(A + c + 4);
-    const float4 b0 = *reinterpret_cast<const float4*>(B + c);
-    const float4 b1 = *reinterpret_cast<const float4*>(B + c + 4);
-    const float4 c0 = *reinterpret_cast<const float4*>(Cc + c);
-    const float4 c1 = *reinterpret_cast<const float4*>(Cc + c + 4);
-    const float ka[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    const float kb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-    const float kc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    load8f(A + cc, ka);
+    load8f(B + cc, kb);
+    load8f(Cc + cc, kc);
+  };
+  struct In {
+    Vec8<T> x, dy, y;
+    uint32_t mb;
+  };
+  auto load = [&](In& in, int64_t vv) {
+    in.x.load(x + vv * 8);
+    in.dy.load(dy + vv * 8);
+    if (RELU == kReluFromY) in.y.load(y + vv * 8);
+    in.mb = RELU == kReluFromMask ? mask[vv] : 0u;
+  };
+  auto compute = [&](const In& in, int64_t vv) {
+    Vec8<T> out, dz;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      float d = vdy.get(i);
-      if (RELU == kReluFromY) d = vy.get(i) > 0.f ? d : 0.f;
-      if (RELU == kReluFromX) d = fmaf(vx.get(i), fs[i], fh[i]) > 0.f ? d : 0.f;
-      if (RELU == kReluFromMask) d = ((mb >> i) & 1u) ? d : 0.f;
+      float d = in.dy.get(i);
+      if (RELU == kReluFromY) d = in.y.get(i) > 0.f ? d : 0.f;
+      if (RELU == kReluFromX) d = fmaf(in.x.get(i), fs[i], fh[i]) > 0.f ? d : 0.f;
+      if (RELU == kReluFromMask) d = ((in.mb >> i) & 1u) ? d : 0.f;
       if (WRITE_DZ) dz.set(i, d);
-      out.set(i, ka[i] * d + kb[i] * vx.get(i) + kc[i]);
+      out.set(i, ka[i] * d + kb[i] * in.x.get(i) + kc[i]);
     }
-    out.store(dx + off);
-    if (WRITE_DZ) dz.store(dz_out + off);
+    out.store(dx + vv * 8);
+    if (WRITE_DZ) dz.store(dz_out + vv * 8);
+  };
+  if (cstep == 0) {
+    coef(c);
+    for (; v + stride < nvec; v += 2 * stride) {
+      In i0, i1;
+      load(i0, v);
+      load(i1, v + stride);
+      compute(i0, v);
+      compute(i1, v + stride);
+    }
+    if (v < nvec) {
+      In i0;
+      load(i0, v);
+      compute(i0, v);
+    }
+    return;
+  }
+  for (; v < nvec; v += stride, c = (c + cstep >= C) ? c + cstep - C : c + cstep) {
+    In i0;
+    load(i0, v);
+    coef(c);
+    compute(i0, v);
   }
 }
 
