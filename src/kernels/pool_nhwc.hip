@@ -19,21 +19,56 @@ struct PoolGeom {
   int count_include_pad;
 };
 
+// n / d by multiply-high for n < 2^31 (the uint32_t kernels): the three index divisions per vector are
+// otherwise ~30-instruction integer routines each, and the stem pooling backward was instruction-bound
+struct PDiv {
+  uint32_t m, s;
+};
+
+static inline PDiv make_pdiv(uint32_t d) {
+  PDiv f;
+  f.s = 0;
+  while ((1u << f.s) < d) ++f.s;
+  f.m = static_cast<uint32_t>((((uint64_t)1 << 32) * (((uint64_t)1 << f.s) - d)) / d + 1);
+  return f;
+}
+
+struct PoolDivs {
+  PDiv cv, w, h;   // C/8, the pixel row length and the column height of the indexed grid
+};
+
+template <typename I>
+__device__ __forceinline__ void pool_split(I v, I cv, int W, int H, const PoolDivs& dv, int& c8, int& w, int& h,
+                                           int& n) {
+  if constexpr (sizeof(I) == 4) {
+    const uint32_t p = (__umulhi(v, dv.cv.m) + v) >> dv.cv.s;
+    c8 = static_cast<int>(v - p * cv) * 8;
+    const uint32_t q = (__umulhi(p, dv.w.m) + p) >> dv.w.s;
+    w = static_cast<int>(p - q * static_cast<uint32_t>(W));
+    const uint32_t r = (__umulhi(q, dv.h.m) + q) >> dv.h.s;
+    h = static_cast<int>(q - r * static_cast<uint32_t>(H));
+    n = static_cast<int>(r);
+  } else {
+    c8 = static_cast<int>(v % cv) * 8;
+    I p = v / cv;
+    w = static_cast<int>(p % static_cast<I>(W));
+    p /= static_cast<I>(W);
+    h = static_cast<int>(p % static_cast<I>(H));
+    n = static_cast<int>(p / static_cast<I>(H));
+  }
+}
+
 // I: the index type -- uint32_t whenever every element offset fits (the pixel / channel decomposition
 // of each vector index is 3 divisions; 64-bit ones are software routines that made the ResNet-50
 // stem pooling backward instruction-bound at ~2 TB/s)
 template <typename T, bool MAX, typename I>
 __global__ void __launch_bounds__(256) pool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
-                                                       uint8_t* __restrict__ arg, PoolGeom g, I nvec) {
+                                                       uint8_t* __restrict__ arg, PoolGeom g, I nvec, PoolDivs dv) {
   const I cv = static_cast<I>(g.C / 8);
   for (I v = static_cast<I>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec;
        v += static_cast<I>(gridDim.x) * blockDim.x) {
-    const int c8 = static_cast<int>(v % cv) * 8;
-    I p = v / cv;
-    const int wo = static_cast<int>(p % static_cast<I>(g.Wo));
-    p /= static_cast<I>(g.Wo);
-    const int ho = static_cast<int>(p % static_cast<I>(g.Ho));
-    const int n = static_cast<int>(p / static_cast<I>(g.Ho));
+    int c8, wo, ho, n;
+    pool_split<I>(v, cv, g.Wo, g.Ho, dv, c8, wo, ho, n);
     const int h0 = ho * g.sh - g.ph, w0 = wo * g.sw - g.pw;
     float acc[8];
     uint8_t am[8];
@@ -90,16 +125,12 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(const T* __restrict__ x, 
 
 template <typename T, bool MAX, typename I>
 __global__ void __launch_bounds__(256) pool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ arg,
-                                                       T* __restrict__ dx, PoolGeom g, I nvec) {
+                                                       T* __restrict__ dx, PoolGeom g, I nvec, PoolDivs dv) {
   const I cv = static_cast<I>(g.C / 8);
   for (I v = static_cast<I>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec;
        v += static_cast<I>(gridDim.x) * blockDim.x) {
-    const int c8 = static_cast<int>(v % cv) * 8;
-    I p = v / cv;
-    const int w = static_cast<int>(p % static_cast<I>(g.W));
-    p /= static_cast<I>(g.W);
-    const int h = static_cast<int>(p % static_cast<I>(g.H));
-    const int n = static_cast<int>(p / static_cast<I>(g.H));
+    int c8, w, h, n;
+    pool_split<I>(v, cv, g.W, g.H, dv, c8, w, h, n);
     // output windows covering (h, w): ho*sh - ph <= h <= ho*sh - ph + kh - 1
     const int hp = h + g.ph, wp = w + g.pw;
     const int ho_lo = hp - g.kh + 1 > 0 ? (hp - g.kh + g.sh) / g.sh : 0;
@@ -147,12 +178,58 @@ __global__ void __launch_bounds__(256) pool_bwd_kernel(const T* __restrict__ dy,
   }
 }
 
+// max backward when at most 2 x 2 windows cover an input pixel (kernel <= 2 * stride per axis: the
+// ResNet stem's 3x3 / stride 2): the four candidate windows' dy and argmax words are loaded together,
+// predicated, instead of in a variable-trip loop of dependent loads
+template <typename T, typename I>
+__global__ void __launch_bounds__(256) pool_bwd_max2_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                                            T* __restrict__ dx, PoolGeom g, I nvec, PoolDivs dv) {
+  const I cv = static_cast<I>(g.C / 8);
+  for (I v = static_cast<I>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec;
+       v += static_cast<I>(gridDim.x) * blockDim.x) {
+    int c8, w, h, n;
+    pool_split<I>(v, cv, g.W, g.H, dv, c8, w, h, n);
+    const int ho_hi = min((h + g.ph) / g.sh, g.Ho - 1);
+    const int wo_hi = min((w + g.pw) / g.sw, g.Wo - 1);
+    Vec8<T> vd[4];
+    uint2 pk[4];
+    int idx[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int ho = ho_hi - (t >> 1), wo = wo_hi - (t & 1);
+      const int dh = h - (ho * g.sh - g.ph), dw = w - (wo * g.sw - g.pw);
+      const bool ok = ho >= 0 && wo >= 0 && dh >= 0 && dh < g.kh && dw >= 0 && dw < g.kw;
+      idx[t] = ok ? dh * g.kw + dw : -1;
+      const I o = ok ? ((static_cast<I>(n) * g.Ho + ho) * g.Wo + wo) * g.C + c8 : static_cast<I>(0);
+      vd[t].load(dy + o);
+      pk[t] = *reinterpret_cast<const uint2*>(arg + o);
+    }
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t word = i < 4 ? pk[t].x : pk[t].y;
+        const int a = (word >> ((i & 3) * 8)) & 0xff;
+        if (a == idx[t]) acc[i] += vd[t].get(i);
+      }
+    }
+    Vec8<T> out;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out.set(i, acc[i]);
+    out.store(dx + static_cast<int64_t>(v) * 8);
+  }
+}
+
 // every element offset of x and y (and the loop index plus one grid stride) fits in 32 bits
 static inline bool fits32(const PoolGeom& g) {
   const int64_t big = static_cast<int64_t>(g.N) * g.C * (g.H * static_cast<int64_t>(g.W) > g.Ho * static_cast<int64_t>(g.Wo)
                                                             ? g.H * static_cast<int64_t>(g.W)
                                                             : g.Ho * static_cast<int64_t>(g.Wo));
-  return big + 256LL * 32 * 256 * 8 < (1LL << 32);
+  // (and every vector index plus one grid stride stays below 2^31 for the multiply-high division)
+  return big + 256LL * 32 * 256 * 8 < (1LL << 31);
 }
 
 static inline int grid_for(int64_t nvec) {
@@ -166,7 +243,8 @@ static void pool_fwd_t(int is_max, const void* x, void* y, uint8_t* arg, const P
   const bool small = fits32(g);
 #define MXAMD_POOL_FWD(MX, I)                                                                               \
   hipLaunchKernelGGL((pool_fwd_kernel<T, MX, I>), dim3(grid_for(nvec)), dim3(256), 0, s,                     \
-                     static_cast<const T*>(x), static_cast<T*>(y), arg, g, static_cast<I>(nvec))
+                     static_cast<const T*>(x), static_cast<T*>(y), arg, g, static_cast<I>(nvec),                   \
+                     PoolDivs{make_pdiv(g.C / 8), make_pdiv(g.Wo), make_pdiv(g.Ho)})
   if (is_max) {
     if (small) MXAMD_POOL_FWD(true, uint32_t); else MXAMD_POOL_FWD(true, int64_t);
   } else {
@@ -181,8 +259,14 @@ static void pool_bwd_t(int is_max, const void* dy, const uint8_t* arg, void* dx,
   const bool small = fits32(g);
 #define MXAMD_POOL_BWD(MX, I)                                                                               \
   hipLaunchKernelGGL((pool_bwd_kernel<T, MX, I>), dim3(grid_for(nvec)), dim3(256), 0, s,                     \
-                     static_cast<const T*>(dy), arg, static_cast<T*>(dx), g, static_cast<I>(nvec))
-  if (is_max) {
+                     static_cast<const T*>(dy), arg, static_cast<T*>(dx), g, static_cast<I>(nvec),                 \
+                     PoolDivs{make_pdiv(g.C / 8), make_pdiv(g.W), make_pdiv(g.H)})
+  const bool two = (g.kh + g.sh - 1) / g.sh <= 2 && (g.kw + g.sw - 1) / g.sw <= 2;
+  if (is_max && two && small) {
+    hipLaunchKernelGGL((pool_bwd_max2_kernel<T, uint32_t>), dim3(grid_for(nvec)), dim3(256), 0, s,
+                       static_cast<const T*>(dy), arg, static_cast<T*>(dx), g, static_cast<uint32_t>(nvec),
+                       PoolDivs{make_pdiv(g.C / 8), make_pdiv(g.W), make_pdiv(g.H)});
+  } else if (is_max) {
     if (small) MXAMD_POOL_BWD(true, uint32_t); else MXAMD_POOL_BWD(true, int64_t);
   } else {
     if (small) MXAMD_POOL_BWD(false, uint32_t); else MXAMD_POOL_BWD(false, int64_t);

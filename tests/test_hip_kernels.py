@@ -297,6 +297,23 @@ def test_pool_nhwc_matches_torch(dtype, cfg):
     torch.testing.assert_close(dx.float(), dxf.permute(0, 2, 3, 1), rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize('shape', [(4, 112, 112, 64), (3, 57, 45, 40)])
+def test_pool_nhwc_stem_sized_max(shape):
+    """The stem pooling geometry (and an odd one) through the multiply-high index split, fwd + bwd."""
+    from mxnet_maintenance_amd.ops import kernel_fns as KF
+    _lib()
+    torch.manual_seed(3)
+    x = torch.randn(*shape, device='cuda').half().requires_grad_()
+    y = KF.PoolNHWC.apply(x, 'max', (3, 3), (2, 2), (1, 1), False, True)
+    xf = x.detach().float().permute(0, 3, 1, 2).contiguous().requires_grad_()
+    yf = F.max_pool2d(xf, 3, 2, 1).permute(0, 2, 3, 1)
+    torch.testing.assert_close(y.float(), yf, rtol=0, atol=0)
+    dy = torch.randn_like(y)
+    dx, = torch.autograd.grad(y, x, dy)
+    dxf, = torch.autograd.grad(yf, xf, dy.float())
+    assert _relnorm(dx, dxf.permute(0, 2, 3, 1)) < 1e-3
+
+
 @pytest.mark.parametrize('mode', ['relu', 'add_relu', 'plain'])
 def test_bn_nhwc_direct_grad_accumulate(mode):
     """Inside mx.autograd.backward the BN kernel adds dgamma/dbeta straight into the leaves' fp32 .grad."""
