@@ -178,6 +178,59 @@ __global__ void __launch_bounds__(256) pool_bwd_kernel(const T* __restrict__ dy,
   }
 }
 
+// max forward over a 3x3 window (the ResNet stem): the nine taps are loaded together, predicated (an
+// out-of-image tap reads offset 0 and is ignored), instead of in a loop with early continues
+template <typename T, typename I>
+__global__ void __launch_bounds__(256) pool_fwd_max3_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                            uint8_t* __restrict__ arg, PoolGeom g, I nvec,
+                                                            PoolDivs dv) {
+  const I cv = static_cast<I>(g.C / 8);
+  for (I v = static_cast<I>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec;
+       v += static_cast<I>(gridDim.x) * blockDim.x) {
+    int c8, wo, ho, n;
+    pool_split<I>(v, cv, g.Wo, g.Ho, dv, c8, wo, ho, n);
+    const int h0 = ho * g.sh - g.ph, w0 = wo * g.sw - g.pw;
+    Vec8<T> vx[9];
+    bool ok[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int h = h0 + t / 3, w = w0 + t % 3;
+      ok[t] = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+      const I o = ok[t] ? ((static_cast<I>(n) * g.H + h) * g.W + w) * g.C + c8 : static_cast<I>(0);
+      vx[t].load(x + o);
+    }
+    float acc[8];
+    uint32_t am[8];
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      acc[i] = -INFINITY;
+      am[i] = 0;
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (!ok[t]) continue;
+      any = true;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float f = vx[t].get(i);
+        if (f > acc[i]) {
+          acc[i] = f;
+          am[i] = t;
+        }
+      }
+    }
+    Vec8<T> out;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out.set(i, any ? acc[i] : 0.f);
+    uint2 packed;
+    packed.x = am[0] | (am[1] << 8) | (am[2] << 16) | (am[3] << 24);
+    packed.y = am[4] | (am[5] << 8) | (am[6] << 16) | (am[7] << 24);
+    *reinterpret_cast<uint2*>(arg + static_cast<int64_t>(v) * 8) = packed;
+    out.store(y + static_cast<int64_t>(v) * 8);
+  }
+}
+
 // max backward when at most 2 x 2 windows cover an input pixel (kernel <= 2 * stride per axis: the
 // ResNet stem's 3x3 / stride 2): the four candidate windows' dy and argmax words are loaded together,
 // predicated, instead of in a variable-trip loop of dependent loads
@@ -245,7 +298,11 @@ static void pool_fwd_t(int is_max, const void* x, void* y, uint8_t* arg, const P
   hipLaunchKernelGGL((pool_fwd_kernel<T, MX, I>), dim3(grid_for(nvec)), dim3(256), 0, s,                     \
                      static_cast<const T*>(x), static_cast<T*>(y), arg, g, static_cast<I>(nvec),                   \
                      PoolDivs{make_pdiv(g.C / 8), make_pdiv(g.Wo), make_pdiv(g.Ho)})
-  if (is_max) {
+  if (is_max && small && g.kh == 3 && g.kw == 3) {
+    hipLaunchKernelGGL((pool_fwd_max3_kernel<T, uint32_t>), dim3(grid_for(nvec)), dim3(256), 0, s,
+                       static_cast<const T*>(x), static_cast<T*>(y), arg, g, static_cast<uint32_t>(nvec),
+                       PoolDivs{make_pdiv(g.C / 8), make_pdiv(g.Wo), make_pdiv(g.Ho)});
+  } else if (is_max) {
     if (small) MXAMD_POOL_FWD(true, uint32_t); else MXAMD_POOL_FWD(true, int64_t);
   } else {
     if (small) MXAMD_POOL_FWD(false, uint32_t); else MXAMD_POOL_FWD(false, int64_t);
