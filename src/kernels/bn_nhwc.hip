@@ -313,7 +313,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_kernel(
       if (RELU) r = r > 0.f ? r : 0.f;
       out.set(i, r);
     }
-    vstore(out, y + vv * 8, nt);
+    vstore(out, y + vv * 8, nt == 2 ? 2 : 0);
     if (MASK) mask[vv] = static_cast<uint8_t>(bits);
   };
   if (cstep == 0) {
@@ -390,8 +390,8 @@ __global__ void __launch_bounds__(kBnThreads) bn_bwd_apply_kernel(
       if (WRITE_DZ) dz.set(i, d);
       out.set(i, ka[i] * d + kb[i] * in.x.get(i) + kc[i]);
     }
-    vstore(out, dx + vv * 8, nt);
-    if (WRITE_DZ) vstore(dz, dz_out + vv * 8, nt);
+    vstore(out, dx + vv * 8, nt == 2 ? 2 : 0);
+    if (WRITE_DZ) vstore(dz, dz_out + vv * 8, nt >= 2 ? 2 : 0);
   };
   if (cstep == 0) {
     coef(c);
@@ -459,7 +459,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_tail_bwd_ds_kernel(
       s2[i] += d * (vz.get(i) - km[i]);
     }
     out.store(dx + off);
-    dz.store(dz_out + off);
+    vstore(dz, dz_out + off, nt >= 2 ? 2 : 0);
   };
   int64_t r = r0 + lane_r;
   for (; r + (UNR - 1) * rpi < r1; r += UNR * rpi) {
@@ -509,7 +509,8 @@ __global__ void __launch_bounds__(kBnThreads) bn_tail_bwd_ds_kernel(
 
 // ---------------------------------------------------------------- launchers
 
-// non-temporal policy of the apply kernels (MXAMD_BN_NT: 0 off, 1 loads (default), 2 loads + stores).
+// non-temporal policy of the apply kernels (MXAMD_BN_NT: 0 off, 1 loads (default), 2 loads + stores,
+// 3 loads + the residual tail's dz store -- dz is read only after the whole block's backward).
 // Their inputs are dead once applied in the step's order, so keeping them out of the caches leaves
 // the Infinity Cache to the convolutions: ResNet-50 b256 11,308 -> 11,658 img/s (nt 1) / 11,582 (nt 2)
 // in one same-box A/B (profiles/r5v_*)
