@@ -43,14 +43,18 @@ class LayerNorm(torch.autograd.Function):
         lib = _K.lib()
         D = x.shape[-1]
         M = x.numel() // D
-        g = _f32(gamma)
-        b = _f32(beta)
+        # gamma/beta in the activation dtype are read as they are (no conversion kernels per call)
+        pt = int(gamma.dtype == x.dtype and beta.dtype == x.dtype and gamma.is_contiguous() and beta.is_contiguous()
+                 and gamma.data_ptr() % 16 == 0 and beta.data_ptr() % 16 == 0)
+        g = gamma if pt else _f32(gamma)
+        b = beta if pt else _f32(beta)
         y = torch.empty_like(x)
         stats = torch.empty(2, M, dtype=torch.float32, device=x.device)
         mean, rstd = stats[0], stats[1]
         lib.layernorm_forward(_DT[x.dtype], x.data_ptr(), g.data_ptr(), b.data_ptr(), y.data_ptr(), mean.data_ptr(),
-                              rstd.data_ptr(), M, D, float(eps), _stream())
+                              rstd.data_ptr(), M, D, float(eps), _stream(), pt=pt)
         ctx.save_for_backward(x, g, mean, rstd)
+        ctx.pt = pt
         ctx.refs = (gamma, beta)
         shp = tuple(x.shape[:-1]) + (1,)
         if want_stats:
@@ -88,7 +92,7 @@ class LayerNorm(torch.autograd.Function):
             dg, db, accum, gdt = out[0], out[1], 0, _DT[torch.float32]
         lib.layernorm_backward(_DT[x.dtype], x.data_ptr(), gy.data_ptr(), g.data_ptr(), mean.data_ptr(),
                                rstd.data_ptr(), dx.data_ptr(), part.data_ptr(), dg.data_ptr(), db.data_ptr(), gdt,
-                               accum, M, D, _stream())
+                               accum, M, D, _stream(), pt=ctx.pt)
         if accum:
             return dx, None, None, None, None
         return (dx, dg.view(gamma.shape).to(gamma.dtype) if need_g else None,

@@ -99,9 +99,9 @@ int64_t conv_stem_wgrad_workspace(int N, int H, int W, int R, int S, int ph, int
 void conv_stem_wgrad(int dtype, const void* x, const void* dy, float* slab, int out_dtype, void* out, int accum, int N,
                      int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, hipStream_t s);
 int layernorm_bwd_partials(int M);
-void layernorm_forward(int dtype, const void* x, const float* gamma, const float* beta, void* y, float* mean,
+void layernorm_forward(int dtype, const void* x, const void* gamma, const void* beta, int pt, void* y, float* mean,
                        float* rstd, int M, int D, float eps, hipStream_t s);
-void layernorm_backward(int dtype, const void* x, const void* dy, const float* gamma, const float* mean,
+void layernorm_backward(int dtype, const void* x, const void* dy, const void* gamma, int pt, const float* mean,
                         const float* rstd, void* dx, float* part, void* dgamma, void* dbeta, int gdtype, int accum,
                         int M, int D, hipStream_t s);
 void gelu_forward(int dtype, const void* x, void* y, int64_t n, hipStream_t s);
@@ -548,19 +548,23 @@ PYBIND11_MODULE(_hip_kernels, m) {
     check_launch("conv_nhwc_wgrad");
   });
   m.def("layernorm_bwd_partials", &layernorm_bwd_partials);
+  // pt: gamma / beta in the activation dtype (else fp32)
   m.def("layernorm_forward", [](int dt, uintptr_t x, uintptr_t g, uintptr_t b, uintptr_t y, uintptr_t mean,
-                                uintptr_t rstd, int M, int D, float eps, uintptr_t s) {
-    layernorm_forward(dt, P<void>(x), P<float>(g), P<float>(b), P<void>(y), P<float>(mean), P<float>(rstd), M, D, eps,
-                      S(s));
+                                uintptr_t rstd, int M, int D, float eps, uintptr_t s, int pt) {
+    layernorm_forward(dt, P<void>(x), P<void>(g), P<void>(b), pt, P<void>(y), P<float>(mean), P<float>(rstd), M, D,
+                      eps, S(s));
     check_launch("layernorm_forward");
-  });
+  }, py::arg("dtype"), py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("y"), py::arg("mean"),
+     py::arg("rstd"), py::arg("M"), py::arg("D"), py::arg("eps"), py::arg("stream"), py::arg("pt") = 0);
   m.def("layernorm_backward", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t g, uintptr_t mean, uintptr_t rstd,
                                  uintptr_t dx, uintptr_t part, uintptr_t dg, uintptr_t db, int gdt, int accum, int M,
-                                 int D, uintptr_t s) {
-    layernorm_backward(dt, P<void>(x), P<void>(dy), P<float>(g), P<float>(mean), P<float>(rstd), P<void>(dx),
+                                 int D, uintptr_t s, int pt) {
+    layernorm_backward(dt, P<void>(x), P<void>(dy), P<void>(g), pt, P<float>(mean), P<float>(rstd), P<void>(dx),
                        P<float>(part), P<void>(dg), P<void>(db), gdt, accum, M, D, S(s));
     check_launch("layernorm_backward");
-  });
+  }, py::arg("dtype"), py::arg("x"), py::arg("dy"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
+     py::arg("dx"), py::arg("part"), py::arg("dgamma"), py::arg("dbeta"), py::arg("gdtype"), py::arg("accum"),
+     py::arg("M"), py::arg("D"), py::arg("stream"), py::arg("pt") = 0);
   m.def("gelu_forward", [](int dt, uintptr_t x, uintptr_t y, int64_t n, uintptr_t s) {
     gelu_forward(dt, P<void>(x), P<void>(y), n, S(s));
     check_launch("gelu_forward");

@@ -47,11 +47,25 @@ __device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
+// a per-column parameter vector: fp32, or (pt != 0) in the activation dtype T -- bf16/fp16 gamma/beta
+// are read as they are instead of through a conversion kernel per call
+template <typename T>
+__device__ __forceinline__ void ld8p(const void* p, int i8, int pt, float (&v)[8]) {
+  if (pt) {
+    Vec8<T> t;
+    t.load(static_cast<const T*>(p) + i8);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = t.get(i);
+  } else {
+    ld8f(static_cast<const float*>(p) + i8, v);
+  }
+}
+
 // ------------------------------------------------------------------ LayerNorm
 // x, y: [M, D] (D % 8 == 0, D <= 512*VPL); gamma/beta fp32 [D]; mean/rstd fp32 [M]
 template <typename T, int VPL>
-__global__ void __launch_bounds__(256) layernorm_fwd_kernel(const T* __restrict__ x, const float* __restrict__ gamma,
-                                                            const float* __restrict__ beta, T* __restrict__ y,
+__global__ void __launch_bounds__(256) layernorm_fwd_kernel(const T* __restrict__ x, const void* __restrict__ gamma,
+                                                            const void* __restrict__ beta, int pt, T* __restrict__ y,
                                                             float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                             int M, int D, float eps) {
   const int lane = threadIdx.x & 63;
@@ -96,8 +110,8 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const T* __restrict_
     const int c = lane + j * 64;
     if (c < nv) {
       float g[8], b[8], o[8];
-      ld8f(gamma + c * 8, g);
-      ld8f(beta + c * 8, b);
+      ld8p<T>(gamma, c * 8, pt, g);
+      ld8p<T>(beta, c * 8, pt, b);
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = (v[j][i] - mean) * rstd * g[i] + b[i];
       st8(yr + c * 8, o);
@@ -108,7 +122,7 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const T* __restrict_
 // dx = rstd * (dy*g - mean(dy*g) - xhat * mean(dy*g*xhat)); per-block partial dgamma/dbeta
 template <typename T, int VPL>
 __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy,
-                                                            const float* __restrict__ gamma,
+                                                            const void* __restrict__ gamma, int pt,
                                                             const float* __restrict__ mean_in,
                                                             const float* __restrict__ rstd_in, T* __restrict__ dx,
                                                             float* __restrict__ part, int M, int D) {
@@ -133,7 +147,7 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const T* __restrict_
         float xv[8], dv[8], g[8];
         ld8(xr + c * 8, xv);
         ld8(dyr + c * 8, dv);
-        ld8f(gamma + c * 8, g);
+        ld8p<T>(gamma, c * 8, pt, g);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           xh[j][i] = (xv[i] - mean) * rstd;
@@ -428,18 +442,19 @@ int layernorm_bwd_partials(int M) {
   return nb > 512 ? 512 : nb;
 }
 
-void layernorm_forward(int dtype, const void* x, const float* gamma, const float* beta, void* y, float* mean,
+// pt: gamma / beta are in the activation dtype (else fp32)
+void layernorm_forward(int dtype, const void* x, const void* gamma, const void* beta, int pt, void* y, float* mean,
                        float* rstd, int M, int D, float eps, hipStream_t s) {
   MXAMD_HOST_CHECK(D % 8 == 0, "layernorm: D must be a multiple of 8");
   const int vpl = pick_vpl(D);
   dim3 grid((M + 3) / 4);
   MXAMD_DTYPE_SWITCH(dtype, MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((layernorm_fwd_kernel<T, VPL>), grid, dim3(256),
-                                                                     0, s, static_cast<const T*>(x), gamma, beta,
+                                                                     0, s, static_cast<const T*>(x), gamma, beta, pt,
                                                                      static_cast<T*>(y), mean, rstd, M, D, eps)))
 }
 
 // part: fp32 workspace of layernorm_bwd_partials(M) * 2 * D; dgamma/dbeta fp32 [D] (written or accumulated)
-void layernorm_backward(int dtype, const void* x, const void* dy, const float* gamma, const float* mean,
+void layernorm_backward(int dtype, const void* x, const void* dy, const void* gamma, int pt, const float* mean,
                         const float* rstd, void* dx, float* part, void* dgamma, void* dbeta, int gdtype, int accum,
                         int M, int D, hipStream_t s) {
   MXAMD_HOST_CHECK(D % 8 == 0, "layernorm: D must be a multiple of 8");
@@ -447,7 +462,7 @@ void layernorm_backward(int dtype, const void* x, const void* dy, const float* g
   const int nb = layernorm_bwd_partials(M);
   MXAMD_DTYPE_SWITCH(dtype, MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((layernorm_bwd_kernel<T, VPL>), dim3(nb),
                                                                      dim3(256), 0, s, static_cast<const T*>(x),
-                                                                     static_cast<const T*>(dy), gamma, mean, rstd,
+                                                                     static_cast<const T*>(dy), gamma, pt, mean, rstd,
                                                                      static_cast<T*>(dx), part, M, D)))
   // dgamma / dbeta straight into the parameters' gradient buffers in their own dtype (fp32 / bf16 / fp16)
   MXAMD_DTYPE_SWITCH(gdtype, hipLaunchKernelGGL((column_sum_kernel<T>), dim3((2 * D + 7) / 8), dim3(256), 0, s,

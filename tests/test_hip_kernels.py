@@ -434,28 +434,31 @@ def test_bottleneck_fused_tee_matches_fp32_reference(cfg):
 # ---------------------------------------------------------------- transformer-path kernels
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16, torch.float32])
 @pytest.mark.parametrize('shape', [(64, 768), (3, 37, 1024), (8, 4096), (5, 24)])
-def test_layernorm_fwd_bwd(dtype, shape):
+@pytest.mark.parametrize('pdt', ['f32', 'same'])
+def test_layernorm_fwd_bwd(dtype, shape, pdt):
+    """pdt 'same': gamma/beta in the activation dtype, read by the kernels directly (pt=1)."""
     K = _lib()
     torch.manual_seed(3)
     D = shape[-1]
     x = torch.randn(*shape, device='cuda').to(dtype).requires_grad_()
-    g = (torch.rand(D, device='cuda') + 0.5).requires_grad_()
-    b = torch.randn(D, device='cuda').requires_grad_()
+    gdt = torch.float32 if pdt == 'f32' else dtype
+    g = (torch.rand(D, device='cuda') + 0.5).to(gdt).requires_grad_()
+    b = torch.randn(D, device='cuda').to(gdt).requires_grad_()
     assert K.ln_ok(x)
     y, mean, std = K.LayerNorm.apply(x, g, b, 1e-5)
     dy = torch.randn_like(y)
     dx, dg, db = torch.autograd.grad(y, (x, g, b), dy)
     xf = x.detach().float().requires_grad_()
-    gf = g.detach().clone().requires_grad_()
-    bf = b.detach().clone().requires_grad_()
+    gf = g.detach().float().clone().requires_grad_()
+    bf = b.detach().float().clone().requires_grad_()
     yf = F.layer_norm(xf, (D,), gf, bf, 1e-5)
     dxf, dgf, dbf = torch.autograd.grad(yf, (xf, gf, bf), dy.float())
     tol = {torch.float16: 2e-2, torch.bfloat16: 8e-2, torch.float32: 1e-4}[dtype]
     torch.testing.assert_close(y.float(), yf, rtol=tol, atol=tol)
     torch.testing.assert_close(mean.float().squeeze(-1), xf.mean(-1), rtol=tol, atol=tol)
     torch.testing.assert_close(dx.float(), dxf, rtol=tol, atol=tol * 4)
-    torch.testing.assert_close(dg, dgf, rtol=tol, atol=tol * max(1.0, x.numel() / D / 8))
-    torch.testing.assert_close(db, dbf, rtol=tol, atol=tol * max(1.0, x.numel() / D / 8))
+    torch.testing.assert_close(dg.float(), dgf, rtol=tol, atol=tol * max(1.0, x.numel() / D / 8))
+    torch.testing.assert_close(db.float(), dbf, rtol=tol, atol=tol * max(1.0, x.numel() / D / 8))
 
 
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16, torch.float32])
