@@ -74,6 +74,8 @@ from . import numpy_dispatch_protocol
 from . import numpy_extension as npx
 from . import rtc
 from . import numpy_op_signature
+from . import log
+from . import libinfo
 from .util import is_np_array, is_np_shape, set_np, reset_np, use_np, np_shape, np_array, set_np_shape, use_np_shape, use_np_array
 
 # A process launched as a dist_async server (DMLC_ROLE=server / scheduler) serves and exits at import,

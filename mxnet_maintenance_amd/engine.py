@@ -23,6 +23,7 @@ validates the version / exclusive access of its variables when it starts, and
 """
 import os
 import threading
+import weakref
 from contextlib import contextmanager
 
 __all__ = ['bulk', 'set_bulk_size', 'get', 'push', 'push_device', 'stream_wait_var', 'new_var', 'wait_for_var',
@@ -72,6 +73,9 @@ class _PyEngine:
         self.push(fn, const_vars, mutable_vars, priority, name)
 
     def stream_wait_var(self, v, stream, device):
+        pass
+
+    def clear_exception(self, v):
         pass
 
     debug = False
@@ -198,6 +202,11 @@ def stream_wait_var(var, stream=None):
         get().wait_for_var(var)
         return
     get().stream_wait_var(var, handle, dev)
+
+
+def clear_exception(var):
+    """Drop a pending failure of ``var`` (one already reported through another variable)."""
+    get().clear_exception(var)
 
 
 def debug_access(var, write=False):
@@ -469,6 +478,11 @@ class _Workers:
         self.streams = {}     # device index -> [None, stream 1, ..., stream N-1]
         self.rr = {}          # device index -> next slot for a new chain
         self.dirty = {}       # device index -> slots with work not yet joined into the caller's stream
+        # device index -> weak references to outputs produced on worker slots since the last join: the
+        # caching allocator ties their blocks to the worker stream, so the join records them on the
+        # caller's stream too (else a block freed while the caller's stream still reads it could be
+        # handed to the next worker-stream allocation)
+        self.produced = {}
         self.depth = 0        # > 0 while an operator body runs (nested operators stay on its stream)
 
     def stream(self, dev, sid):
@@ -572,9 +586,14 @@ def op_done(tensors, sid):
         if isinstance(t, _torch_tensor()):
             t._mx_sid = sid
     if sid:
-        dev = _gpu_device([t for t in tensors if isinstance(t, _torch_tensor())])
+        ts = [t for t in tensors if isinstance(t, _torch_tensor())]
+        dev = _gpu_device(ts)
         if dev is not None:
             _workers.dirty.setdefault(dev, set()).add(sid)
+            lst = _workers.produced.setdefault(dev, [])
+            for t in ts:
+                if t.is_cuda:
+                    lst.append(weakref.ref(t))
 
 
 def _torch_tensor():
@@ -610,7 +629,12 @@ def join_workers(dev=None):
     devs = [dev] if dev is not None else list(_workers.dirty)
     for d in devs:
         slots = _workers.dirty.pop(d, None)
+        produced = _workers.produced.pop(d, ())
         if slots:
             cur = torch.cuda.current_stream(d)
             for sid in slots:
                 cur.wait_stream(_workers.stream(d, sid))
+            for ref in produced:
+                t = ref()
+                if t is not None:
+                    t.record_stream(cur)

@@ -232,7 +232,10 @@ class KVStore(KVStoreBase):
         flat_r = [a for v in reads for a in _as_list(v)]
         flat_w = [a for v in writes for a in _as_list(v)]
         dev = next((a._data.device for a in flat_r + flat_w if a._data.is_cuda), None)
-        if dev is None or not engine.native_available() or torch.cuda.is_current_stream_capturing() or \
+        # one comm stream orders one device's work: arrays spread over several GPUs of this process
+        # (each with its own caller streams) run in place instead
+        multi = len({a._data.device for a in flat_r + flat_w if a._data.is_cuda}) > 1
+        if dev is None or multi or not engine.native_available() or torch.cuda.is_current_stream_capturing() or \
                 _env_flag('MXAMD_KVSTORE_ENGINE', True) is False:
             fn()
             return
@@ -252,8 +255,16 @@ class KVStore(KVStoreBase):
             with torch.no_grad():
                 fn()
         engine.push_device(op, rvars, [self._engine_var] + wvars, stream=comm, name=name)
-        for v in wvars:
-            engine.stream_wait_var(v, producer)
+        try:
+            for v in wvars:
+                engine.stream_wait_var(v, producer)
+        except Exception:
+            # the failure is reported here, once: clear it from the store's ordering variable and
+            # from the other outputs, so the next collective on this store runs again
+            engine.clear_exception(self._engine_var)
+            for v in wvars:
+                engine.clear_exception(v)
+            raise
 
     # ------------------------------------------------------------------- API
     def _keys(self, key):

@@ -9,6 +9,8 @@ from . import multiarray
 from .multiarray import *  # noqa: F401,F403
 from .multiarray import ndarray, _np_out
 from . import linalg, random
+from . import io
+from .io import genfromtxt  # noqa: F401
 from . import _internal
 from . import fallback as _fallback
 from . import fallback

@@ -195,6 +195,12 @@ def _leaky(ctx, name, a, ins, outs):
 
 @register('BatchNorm', '_contrib_SyncBatchNorm')
 def _bn(ctx, name, a, ins, outs):
+    axis = _int(a.get('axis'), 1)
+    if axis != 1:
+        # ONNX BatchNormalization normalises over axis 1; a negative axis is resolved by the input rank
+        shape = ctx.out_shape(name)
+        if not (shape and axis < 0 and axis + len(shape) == 1):
+            raise NotImplementedError('ONNX export: BatchNorm axis=%d (ONNX BatchNormalization uses axis 1)' % axis)
     gamma = ins[1]
     if _bool(a.get('fix_gamma'), True):
         g = ctx.param(ins[1])
@@ -236,6 +242,9 @@ def _lnorm(ctx, name, a, ins, outs):
 
 @register('Pooling')
 def _pool(ctx, name, a, ins, outs):
+    layout = a.get('layout')
+    if layout not in (None, 'None', 'NCHW', 'NCW', 'NCDHW'):
+        raise NotImplementedError('ONNX export: Pooling layout %s (ONNX pooling is channels-first)' % layout)
     ptype = a.get('pool_type', 'max')
     if _bool(a.get('global_pool')):
         op = {'max': 'GlobalMaxPool', 'avg': 'GlobalAveragePool'}.get(ptype)

@@ -508,7 +508,11 @@ def conv_stem_wgrad(x, dy, wshape, pad, out=None, accum=False):
 
 
 # 512-thread big-tile LDS-DMA kernel (conv_big.hip): variant -> (BCO, BPIX)
-_BIG_VARIANTS = {10: (256, 256), 11: (128, 256), 12: (64, 512), 13: (256, 128), 14: (128, 256), 15: (256, 128)}
+_BIG_VARIANTS = {10: (256, 256), 11: (128, 256), 12: (64, 512), 13: (256, 128), 14: (128, 256), 15: (256, 128),
+                 # the 10..13 tiles on v_mfma_f32_32x32x16 (conv_big.hip MF = 32)
+                 16: (256, 256), 17: (128, 256), 18: (64, 512), 19: (256, 128),
+                 # 224 / 448-pixel tiles (FJ = 7): fill 7/8 of the CUs on the 14x14 / 28x28 layers
+                 26: (256, 224), 27: (128, 448)}
 # 14 / 15: the 11 / 13 tiles with a 128-VGPR budget, two workgroups per CU -- only for a single
 # K-tile (reduction 64), where one LDS operand stage suffices and the epilogue's HBM streams dominate
 _BIG_SKINNY = (14, 15)
@@ -1605,7 +1609,8 @@ def _pool_out(n, k, s, p, full):
 
 
 def pool_ok(x, kernel, stride, pad):
-    return (x.dim() == 4 and x.dtype in _DT and x.is_contiguous() and x.shape[3] % 8 == 0
+    return (x.dim() == 4 and x.dtype in _DT and x.is_contiguous() and x.shape[3] % 8 == 0 and x.numel() > 0
+            and min(x.shape[1] + 2 * pad[0] - kernel[0], x.shape[2] + 2 * pad[1] - kernel[1]) >= 0
             and len(kernel) == 2 and kernel[0] * kernel[1] <= 256 and x.data_ptr() % 16 == 0
             and all(p < k for p, k in zip(pad, kernel)))
 

@@ -10,10 +10,12 @@ The int32 products are computed exactly (integer values are exactly
 representable in fp32 GEMM accumulations up to 2**24 per partial sum; the
 reduction is done in fp64 for larger K), so results match an integer GEMM.
 """
+import numpy as np
 import torch
 import torch.nn.functional as F
 
 from .registry import register
+from ..base import MXNetError
 
 INT8_MAX = 127.0
 UINT8_MAX = 255.0
@@ -518,3 +520,70 @@ def intgemm_fully_connected(data, weight, *rest, num_hidden=1, no_bias=False, fl
             out = out + bias.double()
         out = out.float()
     return out.reshape(*lead, weight.shape[0])
+
+
+def _smooth_or_none(p, eps=0.0001):
+    """Move ``eps`` of mass onto every zero bin, taken evenly off the non-zero bins; None when the
+    distribution is all zeros or the correction would exceed a whole unit."""
+    zeros = p == 0
+    nz = p.size - int(zeros.sum())
+    if nz == 0:
+        return None
+    eps1 = eps * float(zeros.sum()) / float(nz)
+    if eps1 >= 1.0:
+        return None
+    return p + np.where(zeros, eps, -eps1)
+
+
+def calibrate_entropy_host(hist, edges, num_quantized_bins=255):
+    """(threshold, divergence): the symmetric clipping threshold whose int8 re-quantisation Q of the
+    clipped histogram P has the smallest KL(P || Q) -- every candidate width from num_quantized_bins/2
+    to half the histogram, as the reference's calibrate.cc:CalibrateComputeCPU evaluates it (the sliced
+    counts are integral there, the clipped outliers are folded into the end bins of P)."""
+    hist = np.asarray(hist, dtype=np.float32).reshape(-1)
+    edges = np.asarray(edges, dtype=np.float32).reshape(-1)
+    nb = hist.size
+    if edges.size != nb + 1:
+        raise MXNetError('_contrib_calibrate_entropy: hist_edges must have len(hist) + 1 entries')
+    zero = nb // 2
+    half_q = num_quantized_bins // 2
+    cum = np.concatenate([[0.0], np.cumsum(hist, dtype=np.float64)])
+    best_div, best_th = np.float32(np.finfo(np.float32).max), None
+    for i in range(half_q, zero + 1):
+        lo, hi = zero - i, zero + i + 1
+        sliced = np.floor(hist[lo:hi]).astype(np.float64)          # the reference's size_t counts
+        p = hist[lo:hi].astype(np.float64).copy()
+        p[0] = cum[lo + 1]                                         # bins 0..lo folded into the first
+        p[-1] = cum[nb] - cum[hi]                                  # bins hi.. folded into the last
+        merged = sliced.size // num_quantized_bins
+        qb = np.array([sliced[j * merged:(j + 1) * merged].sum() for j in range(num_quantized_bins)])
+        qb[-1] += sliced[num_quantized_bins * merged:].sum()
+        q = np.zeros(sliced.size)
+        for j in range(num_quantized_bins):
+            s0 = j * merged
+            s1 = sliced.size if j == num_quantized_bins - 1 else (j + 1) * merged
+            norm = int(np.count_nonzero(sliced[s0:s1]))
+            if norm:
+                seg = p[s0:s1] != 0
+                q[s0:s1][seg] = qb[j] / norm
+        ps, qs = _smooth_or_none(p), _smooth_or_none(q)
+        if qs is None or ps is None:
+            div = np.float32(np.inf)
+        else:
+            ps = ps / ps.sum()
+            qs = qs / qs.sum()
+            div = np.float32(np.sum(ps * np.log(ps / qs)))
+        if best_th is None or div < best_div:
+            best_div, best_th = div, edges[hi]
+    return float(best_th), float(best_div)
+
+
+@register('_contrib_calibrate_entropy', arg_names=('hist', 'hist_edges'), num_outputs=2,
+          params={'num_quantized_bins': ('int', 255)})
+def calibrate_entropy(hist, hist_edges, num_quantized_bins=255):
+    """Calibrated threshold and its KL divergence for a histogram (reference:
+    src/operator/quantization/calibrate.cc:193); a host computation over the small histogram."""
+    th, div = calibrate_entropy_host(hist.detach().float().cpu().numpy(), hist_edges.detach().float().cpu().numpy(),
+                                     int(num_quantized_bins))
+    dev = hist.device
+    return (torch.tensor([th], dtype=torch.float32, device=dev), torch.tensor([div], dtype=torch.float32, device=dev))

@@ -509,28 +509,15 @@ __global__ void __launch_bounds__(kBnThreads) bn_tail_bwd_ds_kernel(
 
 // ---------------------------------------------------------------- launchers
 
-// non-temporal policy of the apply kernels (MXAMD_BN_NT: 0 off, 1 loads (default), 2 loads + stores,
-// 3 loads + the residual tail's dz store -- dz is read only after the whole block's backward).
-// Their inputs are dead once applied in the step's order, so keeping them out of the caches leaves
-// the Infinity Cache to the convolutions: ResNet-50 b256 11,308 -> 11,658 img/s (nt 1) / 11,582 (nt 2)
-// in one same-box A/B (profiles/r5v_*)
-static int bn_nt() {
-  static const int v = [] {
-    const char* e = std::getenv("MXAMD_BN_NT");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v;
-}
+// non-temporal policy of the apply kernels: their inputs are dead once applied in the step's order, so
+// non-temporal loads keep them out of the Infinity Cache and leave it to the convolutions (ResNet-50 b256
+// 11,308 -> 11,658 img/s in one same-box A/B, profiles/r5v_*); non-temporal stores as well measured
+// as noise (profiles/r5aa_*), so the stores stay cached
+static int bn_nt() { return 1; }
 
-// workgroups of the reduction-geometry kernels (bn_reduce, bn_tail_bwd_ds): MXAMD_BN_BLOCKS, default 512
-static int bn_total_blocks() {
-  static const int v = [] {
-    const char* e = std::getenv("MXAMD_BN_BLOCKS");
-    const int n = e ? std::atoi(e) : 0;
-    return n >= 64 && n <= 16384 ? n : 512;
-  }();
-  return v;
-}
+// workgroups of the reduction-geometry kernels (bn_reduce, bn_tail_bwd_ds): ~2 per CU (512 / 1024
+// measured within noise, profiles/r5s_*)
+static int bn_total_blocks() { return 512; }
 
 static inline int64_t bn_rows_per_block(int64_t R, int C, const BnGeom& g, int* nblk,
                                         int total_blocks = bn_total_blocks(), int min_rows = 0) {
@@ -548,14 +535,7 @@ static inline int64_t bn_rows_per_block(int64_t R, int C, const BnGeom& g, int* 
 // the residual-tail kernel with the shortcut statistics streams 4 tensors in and 2 out: it wants a
 // larger grid than the 2-input reductions (measured: 1.06 -> 0.76 ms/step for 4 calls at 512 -> 1024);
 // at least 64 rows per block keeps the partials small for wide layers (C = 2048: 1 block column)
-static int bn_tail_blocks() {
-  static const int v = [] {
-    const char* e = std::getenv("MXAMD_BN_TAIL_BLOCKS");
-    const int n = e ? std::atoi(e) : 0;
-    return n >= 64 && n <= 16384 ? n : 1024;
-  }();
-  return v;
-}
+static int bn_tail_blocks() { return 1024; }
 
 int bn_tail_ds_rows(int64_t R, int C) {
   BnGeom g = bn_geom(C);

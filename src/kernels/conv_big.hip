@@ -25,6 +25,7 @@
 //
 // Requirements (host-checked): Cin % 64 == 0, Cout % BCO == 0, dilation 1.
 #include <stdexcept>
+#include <type_traits>
 
 #include "common.h"
 #include "mfma.h"
@@ -92,7 +93,10 @@ struct BigCfg {
 // MINB = workgroups per CU the register budget is sized for: MINB 2 caps a wave at 128 VGPRs
 // (4 waves per SIMD) and halves the epilogue's register ring -- the variant for single-K-tile
 // (reduction 64) convs, whose time is the epilogue's HBM traffic, not MFMA.
-template <typename T, int WCO, int FJ, int MINB>
+// MF = MFMA shape: 16 -> v_mfma_f32_16x16x32 (4 x FJ accumulators of 16x16 per wave), 32 ->
+// v_mfma_f32_32x32x16 (2 x FJ/2 accumulators of 32x32; the LDS image then uses the (row >> 1) & 7
+// chunk swizzle, which keeps both the 32-row and the 16-row fragment reads conflict-free).
+template <typename T, int WCO, int FJ, int MINB, int MF>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * MINB))) conv_fwd_big_kernel(const T* __restrict__ x, const T* __restrict__ w,
                                                            const float* __restrict__ bias, T* __restrict__ y,
                                                            const T* __restrict__ zero, GeomB g, int tiles_co,
@@ -106,7 +110,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * MI
   constexpr int STAGE = BigCfg<BCO, BPIX>::STAGE;
   constexpr int PITCH = BigCfg<BCO, BPIX>::PITCH;
   constexpr int A_INS = BCO / 64;  // wave-instructions (8 rows each) per wave for A
-  constexpr int B_INS = BPIX / 64;
+  // 8 waves x 8 rows per LDS-DMA round; a 224-pixel tile (FJ = 7) takes a half round at the end
+  constexpr int B_INS = (BPIX + 63) / 64;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
 
   const int tid = threadIdx.x;
@@ -124,8 +129,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * MI
   const int co0 = tco * BCO;
   const int pix0 = tpix * BPIX;
 
+  static_assert(MF == 16 || (MF == 32 && FJ % 2 == 0), "conv_big: MFMA shape");
   const int lrow = lane >> 3;
-  const int gch = (lane & 7) ^ lrow;
+  // this lane's LDS slot (row (i*8 + wid)*8 + lrow, chunk position lane & 7) holds source chunk
+  // (lane & 7) ^ swizzle(row); the swizzle is the same for every i (rows 64 apart)
+  const int gch = (lane & 7) ^ (MF == 32 ? (((wid & 1) << 2) | (lrow >> 1)) : lrow);
 
   int a_off[A_INS];
 #pragma unroll
@@ -163,6 +171,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * MI
     const int doff = (r * g.W + s) * g.C + c0;
 #pragma unroll
     for (int i = 0; i < B_INS; ++i) {
+      if (BPIX % 64 != 0 && (i * 8 + wid) * 8 >= BPIX) continue;   // wave-uniform: past the tile
       const int hi = b_hi[i] + r, wi = b_wi[i] + s;
       const bool ok = (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
       const T* src = ok ? x + b_base[i] + doff : zsrc;
@@ -170,19 +179,23 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * MI
     }
   };
 
-  f4_t acc[4][FJ];
+  constexpr int NI = MF == 32 ? 2 : 4;        // co fragments per wave (64 channels)
+  constexpr int NJ = MF == 32 ? FJ / 2 : FJ;   // pixel fragments per wave
+  typedef typename std::conditional<MF == 32, mfma::f16x, f4_t>::type acc_t;
+  acc_t acc[NI][NJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
-    for (int j = 0; j < FJ; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = acc_t{};
 
   const int wco = wid % WCO;
   const int wpix = wid / WCO;
   const int frag_r = lane & 15;
   const int fchunk = lane >> 4;
-  const int a_row0 = (wco * 64 + frag_r) * 128;
-  const int b_row0 = A_BYTES + (wpix * FJ * 16 + frag_r) * 128;
-  const int sw = frag_r & 7;
+  const int a_row0 = (wco * 64 + (MF == 32 ? (lane & 31) : frag_r)) * 128;
+  const int b_row0 = A_BYTES + (wpix * FJ * 16 + (MF == 32 ? (lane & 31) : frag_r)) * 128;
+  // fragment rows differ from a_row0 / b_row0 by multiples of 16, so the swizzle is per lane
+  const int sw = MF == 32 ? ((lane & 31) >> 1) & 7 : frag_r & 7;
 
   issue(0, 0);
   __syncthreads();
@@ -190,62 +203,123 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * MI
     const int stage = kt & 1;
     if (kt + 1 < KT) issue(kt + 1, stage ^ 1);
     const char* sb = smem + stage * STAGE;
+    if constexpr (MF == 32) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int ch = ((kk * 4 + fchunk) ^ sw) * 16;
-      u32x4 af[4], bf[FJ];
+      for (int kk = 0; kk < 4; ++kk) {
+        const int ch = ((kk * 2 + (lane >> 5)) ^ sw) * 16;
+        u32x4 af[NI], bf[NJ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u32x4*>(sb + a_row0 + i * 16 * 128 + ch);
+        for (int i = 0; i < NI; ++i) af[i] = *reinterpret_cast<const u32x4*>(sb + a_row0 + i * 32 * 128 + ch);
 #pragma unroll
-      for (int j = 0; j < FJ; ++j) bf[j] = *reinterpret_cast<const u32x4*>(sb + b_row0 + j * 16 * 128 + ch);
+        for (int j = 0; j < NJ; ++j) bf[j] = *reinterpret_cast<const u32x4*>(sb + b_row0 + j * 32 * 128 + ch);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < FJ; ++j) acc[i][j] = MfmaB<T>::run(af[i], bf[j], acc[i][j]);
+          for (int j = 0; j < NJ; ++j) acc[i][j] = MfmaB<T>::run32(af[i], bf[j], acc[i][j]);
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ch = ((kk * 4 + fchunk) ^ sw) * 16;
+        u32x4 af[NI], bf[NJ];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) af[i] = *reinterpret_cast<const u32x4*>(sb + a_row0 + i * 16 * 128 + ch);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bf[j] = *reinterpret_cast<const u32x4*>(sb + b_row0 + j * 16 * 128 + ch);
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = MfmaB<T>::run(af[i], bf[j], acc[i][j]);
+      }
     }
     __syncthreads();
   }
 
-  // ---- epilogue. Lane holds co = wco*64 + i*16 + 4*(lane>>4) + {0..3} for pixel wpix*FJ*16 + j*16 + (lane&15)
-  const int co_l = (lane >> 4) * 4;
+  // ---- epilogue, stage 1: accumulators (+bias) -> LDS [pix][co] image (+ per-wave BN partials).
+  // Every lane owns groups of 4 consecutive channels of one pixel; emit(cl, pl, v) takes one group.
   const int pw0 = wpix * FJ * 16;
+  auto bias4 = [&](int cl, float* b) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int cl = wco * 64 + i * 16 + co_l;  // channel within the block tile
-    float b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
-    if (bias) {
-      b0 = bias[co0 + cl];
-      b1 = bias[co0 + cl + 1];
-      b2 = bias[co0 + cl + 2];
-      b3 = bias[co0 + cl + 3];
+    for (int t = 0; t < 4; ++t) b[t] = bias ? bias[co0 + cl + t] : 0.f;
+  };
+  auto write_part = [&](int cl, const float* s, const float* q) {
+    const int pid = tpix * WPIX + wpix;
+    const int64_t c = co0 + cl;
+    float* p1 = part;
+    float* p2 = part + static_cast<int64_t>(g.K) * nparts;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      p1[(c + t) * nparts + pid] = s[t];
+      p2[(c + t) * nparts + pid] = q[t];
     }
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, q0 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;
+  };
+  if constexpr (MF == 32) {
+    // lane holds channels wco*64 + i*32 + 8*gq + 4*(lane>>5) + {0..3} (regs 4gq..4gq+3) of pixel
+    // pw0 + j*32 + (lane & 31)
 #pragma unroll
-    for (int j = 0; j < FJ; ++j) {
-      const int pl = pw0 + j * 16 + frag_r;
-      const float v0 = acc[i][j][0] + b0, v1 = acc[i][j][1] + b1, v2 = acc[i][j][2] + b2, v3 = acc[i][j][3] + b3;
-      *reinterpret_cast<uint2*>(smem + pl * PITCH + cl * 2) = MfmaB<T>::pack4(v0, v1, v2, v3);
-      if (part != nullptr && pix0 + pl < g.M) {
-        s0 += v0; s1 += v1; s2 += v2; s3 += v3;
-        q0 += v0 * v0; q1 += v1 * v1; q2 += v2 * v2; q3 += v3 * v3;
+    for (int i = 0; i < NI; ++i) {
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int cl = wco * 64 + i * 32 + gq * 8 + (lane >> 5) * 4;
+        float b[4], s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
+        bias4(cl, b);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int pl = pw0 + j * 32 + (lane & 31);
+          float v[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[t] = acc[i][j][gq * 4 + t] + b[t];
+          *reinterpret_cast<uint2*>(smem + pl * PITCH + cl * 2) = MfmaB<T>::pack4(v[0], v[1], v[2], v[3]);
+          if (part != nullptr && pix0 + pl < g.M) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              s4[t] += v[t];
+              q4[t] += v[t] * v[t];
+            }
+          }
+        }
+        if (part != nullptr) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            s4[t] = row16_sum(s4[t]);
+            s4[t] += __shfl_xor(s4[t], 16, 64);
+            q4[t] = row16_sum(q4[t]);
+            q4[t] += __shfl_xor(q4[t], 16, 64);
+          }
+          if ((lane & 31) == 0) write_part(cl, s4, q4);
+        }
       }
     }
-    if (part != nullptr) {
-      s0 = row16_sum(s0); s1 = row16_sum(s1); s2 = row16_sum(s2); s3 = row16_sum(s3);
-      q0 = row16_sum(q0); q1 = row16_sum(q1); q2 = row16_sum(q2); q3 = row16_sum(q3);
-      if (frag_r == 0) {
-        const int pid = tpix * WPIX + wpix;
-        const int64_t c = co0 + cl;
-        float* p1 = part;
-        float* p2 = part + static_cast<int64_t>(g.K) * nparts;
-        p1[(c + 0) * nparts + pid] = s0;
-        p1[(c + 1) * nparts + pid] = s1;
-        p1[(c + 2) * nparts + pid] = s2;
-        p1[(c + 3) * nparts + pid] = s3;
-        p2[(c + 0) * nparts + pid] = q0;
-        p2[(c + 1) * nparts + pid] = q1;
-        p2[(c + 2) * nparts + pid] = q2;
-        p2[(c + 3) * nparts + pid] = q3;
+  } else {
+    // lane holds co = wco*64 + i*16 + 4*(lane>>4) + {0..3} for pixel pw0 + j*16 + (lane&15)
+    const int co_l = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int cl = wco * 64 + i * 16 + co_l;  // channel within the block tile
+      float b[4], s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
+      bias4(cl, b);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int pl = pw0 + j * 16 + frag_r;
+        float v[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = acc[i][j][t] + b[t];
+        *reinterpret_cast<uint2*>(smem + pl * PITCH + cl * 2) = MfmaB<T>::pack4(v[0], v[1], v[2], v[3]);
+        if (part != nullptr && pix0 + pl < g.M) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            s4[t] += v[t];
+            q4[t] += v[t] * v[t];
+          }
+        }
+      }
+      if (part != nullptr) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          s4[t] = row16_sum(s4[t]);
+          q4[t] = row16_sum(q4[t]);
+        }
+        if (frag_r == 0) write_part(cl, s4, q4);
       }
     }
   }
@@ -360,7 +434,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * MI
   }
 }
 
-template <typename T, int WCO, int FJ, int MINB>
+template <typename T, int WCO, int FJ, int MINB, int MF = 16>
 void launch_big(const void* x, const void* w, const float* bias, void* y, const void* zero, const GeomB& g,
                 float* part, int nparts, const void* addend, const BnBwdFuse& bf, hipStream_t s) {
   constexpr int BCO = WCO * 64;
@@ -369,7 +443,7 @@ void launch_big(const void* x, const void* w, const float* bias, void* y, const 
   static_assert(SMEM <= 160 * 1024, "conv_big: LDS budget");
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_fwd_big_kernel<T, WCO, FJ, MINB>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_fwd_big_kernel<T, WCO, FJ, MINB, MF>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     attr_set = true;
   }
@@ -382,7 +456,7 @@ void launch_big(const void* x, const void* w, const float* bias, void* y, const 
   constexpr int ONE_STAGE = BigCfg<BCO, BPIX>::STAGE > BigCfg<BCO, BPIX>::EPI ? BigCfg<BCO, BPIX>::STAGE
                                                                                : BigCfg<BCO, BPIX>::EPI;
   const int smem = g.Ktot / 64 > 1 ? SMEM : ONE_STAGE;
-  hipLaunchKernelGGL((conv_fwd_big_kernel<T, WCO, FJ, MINB>), dim3(tiles_co * tiles_pix), dim3(512), smem, s,
+  hipLaunchKernelGGL((conv_fwd_big_kernel<T, WCO, FJ, MINB, MF>), dim3(tiles_co * tiles_pix), dim3(512), smem, s,
                      static_cast<const T*>(x), static_cast<const T*>(w), bias, static_cast<T*>(y),
                      static_cast<const T*>(zero), g, tiles_co, part, nparts, static_cast<const T*>(addend), bf);
 }
@@ -391,9 +465,15 @@ void launch_big(const void* x, const void* w, const float* bias, void* y, const 
 //   0: 256 x 256   1: 128 x 256   2: 64 x 512   3: 256 x 128
 //   4: 128 x 256   5: 256 x 128 at two workgroups per CU (122 VGPRs; for reduction-64 convs --
 //      the 64 x 512 tile does not fit 128 VGPRs without spilling)
+//   6..9: the 0..3 tiles on v_mfma_f32_32x32x16
+//   16: 256 x 224   17: 128 x 448 (FJ = 7): M = N*H*W of ResNet's 14x14 / 28x28 layers is 196 * 2^k, so
+//       256-pixel tiles leave a quarter of the CUs idle in the last round; 224-pixel tiles fill 7/8
 static void big_tile(int variant, int* bco, int* bpix) {
+  if (variant == 16) { *bco = 256; *bpix = 224; return; }
+  if (variant == 17) { *bco = 128; *bpix = 448; return; }
   if (variant == 4) variant = 1;
   if (variant == 5) variant = 3;
+  if (variant >= 6 && variant <= 9) variant -= 6;
   switch (variant) {
     case 0: *bco = 256; *bpix = 256; break;
     case 1: *bco = 128; *bpix = 256; break;
@@ -413,6 +493,13 @@ void dispatch_big(int variant, const void* x, const void* w, const float* bias, 
     case 3: launch_big<T, 4, 4, 1>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
     case 4: launch_big<T, 2, 4, 2>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
     case 5: launch_big<T, 4, 4, 2>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
+    case 6: launch_big<T, 4, 8, 1, 32>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
+    case 7: launch_big<T, 2, 4, 1, 32>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
+    case 8: launch_big<T, 1, 4, 1, 32>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
+    case 9: launch_big<T, 4, 4, 1, 32>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
+    case 16: launch_big<T, 4, 7, 1>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
+    case 17: launch_big<T, 2, 7, 1>(x, w, bias, y, zero, g, part, nparts, addend, bf, s); break;
+    default: throw std::runtime_error("conv_nhwc_fwd_big: unknown variant");
   }
 }
 

@@ -234,10 +234,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const T* __res
   }
 }
 
-// cache policy of the LDS-DMA operand loads (x and dY are dead after the weight gradient; 2 = NT)
-#ifndef MXAMD_WGRAD_AUX
-#define MXAMD_WGRAD_AUX 0
-#endif
+// the LDS-DMA operand loads use the default cache policy (a non-temporal policy on x / dY measured as
+// noise on the ResNet-50 step, profiles/r5x_*)
 
 // LDS-DMA variant: the same sub-tile images filled with global_load_lds_dwordx4
 // (one wave-instruction = 8 rows x 128 B of a sub-tile, lane L -> row L>>3,
@@ -330,7 +328,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_glds_kernel(const T* 
         src = x + ((int64_t)(nimg * g.H + hi) * g.W + wi) * g.C + d_col[i];
       }
       __builtin_amdgcn_global_load_lds((gbl_void_t*)(ok ? src : zsrc), (lds_void_t*)(sbase + d_lds[i]), 16, 0,
-                                       MXAMD_WGRAD_AUX);
+                                       0);
     }
   };
 
@@ -500,7 +498,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_ring_kernel(const T* 
         src = x + ((int64_t)(nimg * g.H + hi) * g.W + wi) * g.C + d_col[i];
       }
       __builtin_amdgcn_global_load_lds((gbl_void_t*)(ok ? src : zsrc), (lds_void_t*)(sbase + d_lds[i]), 16, 0,
-                                       MXAMD_WGRAD_AUX);
+                                       0);
     }
     ++i_kt;
     i_stage = (i_stage + 1 == NST) ? 0 : i_stage + 1;

@@ -23,25 +23,12 @@ namespace mxamd {
 
 namespace {
 
-// MXAMD_OPT_NT (build-time, default 0): non-temporal optimizer-state traffic -- every element is touched
-// once per step, so the streams could stay out of the Infinity Cache.  Measured against it: BERT b32
-// 465k -> 459k (1: loads) / 430k tok/s (2: loads + stores), profiles/r5ac_optimizer_nt_ab.txt
-#ifndef MXAMD_OPT_NT
-#define MXAMD_OPT_NT 0
-#endif
-typedef unsigned int opt_u32x4 __attribute__((ext_vector_type(4)));
-
+// Plain (cached) loads and stores for the optimizer state: a non-temporal policy was measured slower
+// on BERT b32 (465k -> 459k tok/s with nt loads, 430k with nt loads + stores; profiles/r5ac_*).
 template <typename T>
 __device__ __forceinline__ void ldv(const T* p, float (&v)[8]) {
   Vec8<T> t;
-  if constexpr (MXAMD_OPT_NT != 0) {
-    opt_u32x4* d = reinterpret_cast<opt_u32x4*>(&t);
-#pragma unroll
-    for (int k = 0; k < static_cast<int>(sizeof(Vec8<T>) / 16); ++k)
-      d[k] = __builtin_nontemporal_load(reinterpret_cast<const opt_u32x4*>(p) + k);
-  } else {
-    t.load(p);
-  }
+  t.load(p);
 #pragma unroll
   for (int i = 0; i < 8; ++i) v[i] = t.get(i);
 }
@@ -50,14 +37,7 @@ __device__ __forceinline__ void stv(T* p, const float (&v)[8]) {
   Vec8<T> t;
 #pragma unroll
   for (int i = 0; i < 8; ++i) t.set(i, v[i]);
-  if constexpr (MXAMD_OPT_NT > 1) {
-    const opt_u32x4* d = reinterpret_cast<const opt_u32x4*>(&t);
-#pragma unroll
-    for (int k = 0; k < static_cast<int>(sizeof(Vec8<T>) / 16); ++k)
-      __builtin_nontemporal_store(d[k], reinterpret_cast<opt_u32x4*>(p) + k);
-  } else {
-    t.store(p);
-  }
+  t.store(p);
 }
 
 constexpr int kAdam = 0;   // g += wd*w ; w -= lr * m / (sqrt(v) + eps)

@@ -10,6 +10,7 @@
 //   max backward: gather form — each input element sums dy of the (few)
 //                 windows that cover it and chose it; no atomics, no memset.
 //   avg         : forward averages, backward gathers dy / count.
+#include <stdexcept>
 #include "common.h"
 
 namespace mxamd {
@@ -26,6 +27,8 @@ struct PDiv {
 };
 
 static inline PDiv make_pdiv(uint32_t d) {
+  // divisors are positive extents below 2^31 (host-checked by the launchers and pool_ok)
+  if (d == 0 || d > (1u << 31)) throw std::runtime_error("pool_nhwc: divisor out of range");
   PDiv f;
   f.s = 0;
   while ((1u << f.s) < d) ++f.s;

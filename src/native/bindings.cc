@@ -106,6 +106,7 @@ PYBIND11_MODULE(_native, m) {
                Rethrow(std::current_exception());
              }
            })
+      .def("clear_exception", &Engine::ClearException, py::arg("var"))
       .def_property_readonly("debug", &Engine::debug)
       .def_property_readonly("violations", &Engine::violations)
       .def_property_readonly("last_violation", &Engine::last_violation)

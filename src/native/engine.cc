@@ -433,8 +433,13 @@ void Engine::StreamWaitVar(const VarHandle& v, uintptr_t stream, int device) {
     std::lock_guard<std::mutex> lk(v->mu);
     ev = v->write_ev;
     exc = v->exc;
+    v->exc = nullptr;   // reported here, like WaitForVar: later ops on v run again
   }
-  if (exc) std::rethrow_exception(exc);
+  if (exc) {
+    std::lock_guard<std::mutex> lk(excmu_);
+    if (global_exc_ == exc) global_exc_ = nullptr;
+    std::rethrow_exception(exc);
+  }
   if (!ev || (ev->stream == stream && ev->device == device)) return;
   HipRt& rt = HipRt::Get();
   int prev = -1;
@@ -443,6 +448,19 @@ void Engine::StreamWaitVar(const VarHandle& v, uintptr_t stream, int device) {
   const int rc = rt.stream_wait_event(reinterpret_cast<void*>(stream), ev->ev, 0);
   if (device >= 0 && device != prev) rt.set_device(prev);
   HipCheck(rc, "hipStreamWaitEvent");
+}
+
+void Engine::ClearException(const VarHandle& v) {
+  std::exception_ptr exc;
+  {
+    std::lock_guard<std::mutex> lk(v->mu);
+    exc = v->exc;
+    v->exc = nullptr;
+  }
+  if (exc) {
+    std::lock_guard<std::mutex> lk(excmu_);
+    if (global_exc_ == exc) global_exc_ = nullptr;
+  }
 }
 
 void Engine::WaitForAll() {

@@ -102,7 +102,11 @@ class Engine {
   void WaitForVar(const VarHandle& v);
   // Make `stream` wait (on the GPU) for the device write of `v`: blocks the caller only until the ops
   // pushed on `v` so far have been *issued*, never on GPU execution.
+  // A pending exception of `v` is rethrown here once and cleared (WaitForVar semantics).
   void StreamWaitVar(const VarHandle& v, uintptr_t stream, int device);
+  // Drop a pending exception of `v` that was reported elsewhere (e.g. a shared ordering variable
+  // whose failing op's error already reached the caller through an output variable).
+  void ClearException(const VarHandle& v);
   // Debug mode: declare a direct (non-engine) access; a conflicting active engine access is a race.
   void DebugAccess(const VarHandle& v, bool write);
   bool debug() const { return debug_; }

@@ -31,3 +31,24 @@ def test_pushpull_on_comm_stream_matches_sum():
     assert torch.device('cuda', 0) in engine._COMM_STREAMS
     kv.pull(3, out=out)
     mx.nd.waitall()
+
+
+def test_failed_pushpull_does_not_poison_the_store():
+    """A pushpull whose engine op fails (shape mismatch) raises once; the store's ordering variable
+    and the outputs' variables are cleared, so the next valid pushpull on the same store runs."""
+    if not torch.cuda.is_available():
+        pytest.skip('needs a GPU')
+    if not engine.native_available():
+        pytest.skip('native engine not built')
+    from mxnet_maintenance_amd.base import MXNetError
+    ctx = mx.gpu(0)
+    kv = mx.kv.create('device')
+    kv.init(5, mx.nd.zeros((8, 4), ctx=ctx))
+    good = mx.nd.ones((8, 4), ctx=ctx)
+    out = mx.nd.zeros((8, 4), ctx=ctx)
+    with pytest.raises((MXNetError, RuntimeError, ValueError)):
+        kv.pushpull(5, [good, mx.nd.ones((3, 3), ctx=ctx)], out=out)
+        out.wait_to_read()
+    kv.pushpull(5, [good, good * 2], out=out)
+    onp.testing.assert_allclose(out.asnumpy(), onp.full((8, 4), 3.0))
+    mx.nd.waitall()

@@ -23,14 +23,17 @@ def _worker(rank, world, port, q, which):
         dist.init()
         if which == 'autotune':
             from mxnet_maintenance_amd.ops import kernel_fns as KF
-            # rank 0 measures A fast, rank 1 measures B fast: without agreement they would diverge
-            delay = {0: {'candA': 0.001, 'candB': 0.005}, 1: {'candA': 0.010, 'candB': 0.004}}[rank]
+            # rank 0 measures A fast, rank 1 measures B fast: without agreement they would diverge.
+            # The per-rank times are injected (no sleeps), so host load cannot change the outcome.
+            delay = {0: {'candA': 1.0, 'candB': 5.0}, 1: {'candA': 10.0, 'candB': 4.0}}[rank]
+
+            def fake_measure(fn, reps):
+                r = fn()
+                return delay[r] * reps, r
+            KF._measure = fake_measure
 
             def mk(name):
-                def f():
-                    time.sleep(delay[name])
-                    return name
-                return f
+                return lambda: name
             best, out = KF._time_candidates([('candA', mk('candA')), ('candB', mk('candB'))], reps=1,
                                             key=('test', rank))
             q.put((rank, best, out))

@@ -111,3 +111,24 @@ def test_side_stream_weight_gradients_match():
     KF._WGRAD_SIDE[0] = prev
     for a, b in zip(results[0][0] + results[0][1], results[1][0] + results[1][1]):
         onp.testing.assert_allclose(a, b, rtol=1e-3, atol=1e-4)
+
+
+def test_worker_output_read_after_join_survives_reuse(workers):
+    """An output produced on a worker slot, read on the caller's stream after the join (a D2D
+    copyto) and then freed, is recorded on the caller's stream: the next worker-slot allocation does
+    not get its block while the copy may still read it."""
+    ctx = mx.gpu(0)
+    rs = onp.random.RandomState(3)
+    w = mx.nd.array(rs.randn(512, 512) * 0.04, ctx=ctx)
+    xs = [mx.nd.array(rs.randn(256, 512) * 0.1, ctx=ctx) for _ in range(2)]
+    refs = [onp.tanh(x.asnumpy() @ w.asnumpy()) for x in xs]
+    dsts = []
+    for x in xs * 3:
+        a = mx.nd.tanh(mx.nd.dot(x, w))
+        d = mx.nd.zeros(a.shape, ctx=ctx)
+        a.copyto(d)
+        del a                                  # freed while the copy may still be queued
+        _ = mx.nd.tanh(mx.nd.dot(x * 2, w))    # new worker-slot allocation right after
+        dsts.append(d)
+    for i, d in enumerate(dsts):
+        onp.testing.assert_allclose(d.asnumpy(), refs[i % 2], rtol=1e-4, atol=1e-5)

@@ -41,7 +41,7 @@ def family(v):
     if v in KF._RING_VARIANTS:
         return 'ring'
     if v in KF._BIG_VARIANTS:
-        return 'big'
+        return 'big32' if 16 <= v <= 19 else ('big224' if v in (26, 27) else 'big')
     return 'glds' if v in (5, 6) else 'reg'
 
 
@@ -53,7 +53,7 @@ def main():
     a = ap.parse_args()
     N = a.batch
     dt = torch.float16
-    fams = ('ring', 'big', 'glds', 'vendor')
+    fams = ('ring', 'big', 'big32', 'big224', 'glds', 'vendor')
     tot = {f: 0.0 for f in fams}
     best_tot = 0.0
     for (H, Cin, Cout, k, s, cnt) in LAYERS:
