@@ -22,6 +22,11 @@ typedef void* ExecutorHandle;
 typedef void* KVStoreHandle;
 typedef void* OpHandle;
 typedef OpHandle AtomicSymbolCreator;
+typedef void* CachedOpHandle;
+typedef void* ProfileHandle;
+typedef void* DataIterCreator;
+typedef void* DataIterHandle;
+typedef void* RecordIOHandle;
 
 const char* MXGetLastError(void);
 int MXGetVersion(int* out);
@@ -95,6 +100,112 @@ int MXKVStoreInit(KVStoreHandle handle, uint32_t num, const int* keys, NDArrayHa
 int MXKVStorePush(KVStoreHandle handle, uint32_t num, const int* keys, NDArrayHandle* vals, int priority);
 int MXKVStorePull(KVStoreHandle handle, uint32_t num, const int* keys, NDArrayHandle* vals, int priority);
 int MXKVStoreFree(KVStoreHandle handle);
+
+/* ---- NDArray extras (storage types: 0 default, 1 row_sparse, 2 csr) */
+int MXNDArrayGetData(NDArrayHandle handle, void** out_pdata);
+int MXNDArrayGetStorageType(NDArrayHandle handle, int* out_storage_type);
+int MXNDArrayDetach(NDArrayHandle handle, NDArrayHandle* out);
+int MXNDArraySetGradState(NDArrayHandle handle, int state);
+int MXNDArrayGetGradState(NDArrayHandle handle, int* out);
+int MXNDArraySaveRawBytes(NDArrayHandle handle, size_t* out_size, const char** out_buf);
+int MXNDArrayLoadFromRawBytes(const void* buf, size_t size, NDArrayHandle* out);
+int MXNDArraySyncCopyFromNDArray(NDArrayHandle handle_dst, const NDArrayHandle handle_src, const int i);
+int MXNDArrayWaitToWrite(NDArrayHandle handle);
+
+/* ---- autograd extras */
+#ifndef __cplusplus
+#include <stdbool.h>
+#endif
+int MXAutogradIsRecording(bool* curr);
+int MXAutogradIsTraining(bool* curr);
+int MXAutogradBackwardEx(uint32_t num_output, NDArrayHandle* output_handles, NDArrayHandle* ograd_handles,
+                         uint32_t num_variables, NDArrayHandle* var_handles, int retain_graph, int create_graph,
+                         int is_train, NDArrayHandle** grad_handles, int** grad_stypes);
+
+/* ---- CachedOp: a Symbol run imperatively (inputs in list_inputs order), recorded by autograd */
+int MXCreateCachedOp(SymbolHandle handle, CachedOpHandle* out);
+int MXCreateCachedOpEx(SymbolHandle handle, int num_flags, const char** keys, const char** vals,
+                       CachedOpHandle* out);
+int MXInvokeCachedOp(CachedOpHandle handle, int num_inputs, NDArrayHandle* inputs, int* num_outputs,
+                     NDArrayHandle** outputs);
+int MXInvokeCachedOpEx(CachedOpHandle handle, int num_inputs, NDArrayHandle* inputs, int* num_outputs,
+                       NDArrayHandle** outputs, const int** out_stypes);
+int MXFreeCachedOp(CachedOpHandle handle);
+
+/* ---- profiler */
+int MXSetProfilerConfig(int num_params, const char* const* keys, const char* const* vals);
+int MXSetProfilerState(int state);
+int MXDumpProfile(int finished);
+int MXAggregateProfileStatsPrint(const char** out_str, int reset);
+int MXProfilePause(int paused);
+int MXProfileCreateDomain(const char* domain, ProfileHandle* out);
+int MXProfileCreateTask(ProfileHandle domain, const char* task_name, ProfileHandle* out);
+int MXProfileDurationStart(ProfileHandle duration_handle);
+int MXProfileDurationStop(ProfileHandle duration_handle);
+int MXProfileSetMarker(ProfileHandle domain, const char* instant_marker_name, const char* scope);
+int MXProfileDestroyHandle(ProfileHandle frame_handle);
+
+/* ---- data iterators (CSVIter, LibSVMIter, MNISTIter, ImageRecordIter, ...) */
+int MXListDataIters(uint32_t* out_size, DataIterCreator** out_array);
+int MXDataIterGetIterInfo(DataIterCreator creator, const char** name, const char** description, uint32_t* num_args,
+                          const char*** arg_names, const char*** arg_type_infos, const char*** arg_descriptions);
+int MXDataIterCreateIter(DataIterCreator handle, uint32_t num_param, const char** keys, const char** vals,
+                         DataIterHandle* out);
+int MXDataIterFree(DataIterHandle handle);
+int MXDataIterNext(DataIterHandle handle, int* out);
+int MXDataIterBeforeFirst(DataIterHandle handle);
+int MXDataIterGetData(DataIterHandle handle, NDArrayHandle* out);
+int MXDataIterGetLabel(DataIterHandle handle, NDArrayHandle* out);
+int MXDataIterGetIndex(DataIterHandle handle, uint64_t** out_index, uint64_t* out_size);
+int MXDataIterGetPadNum(DataIterHandle handle, int* pad);
+
+/* ---- RecordIO (a record read at end of file returns buf = NULL, size = 0) */
+int MXRecordIOWriterCreate(const char* uri, RecordIOHandle* out);
+int MXRecordIOWriterFree(RecordIOHandle handle);
+int MXRecordIOWriterWriteRecord(RecordIOHandle handle, const char* buf, size_t size);
+int MXRecordIOWriterTell(RecordIOHandle handle, size_t* pos);
+int MXRecordIOReaderCreate(const char* uri, RecordIOHandle* out);
+int MXRecordIOReaderFree(RecordIOHandle handle);
+int MXRecordIOReaderReadRecord(RecordIOHandle handle, char const** buf, size_t* size);
+int MXRecordIOReaderSeek(RecordIOHandle handle, size_t pos);
+int MXRecordIOReaderTell(RecordIOHandle handle, size_t* pos);
+
+/* ---- KVStore extras */
+int MXKVStoreInitEx(KVStoreHandle handle, uint32_t num, const char** keys, NDArrayHandle* vals);
+int MXKVStorePushEx(KVStoreHandle handle, uint32_t num, const char** keys, NDArrayHandle* vals, int priority);
+int MXKVStorePullEx(KVStoreHandle handle, uint32_t num, const char** keys, NDArrayHandle* vals, int priority);
+int MXKVStorePushPull(KVStoreHandle handle, uint32_t vnum, const int* vkeys, uint32_t onum, const int* okeys,
+                      NDArrayHandle* vals, NDArrayHandle* outs, int priority);
+int MXKVStorePushPullEx(KVStoreHandle handle, uint32_t vnum, const char** vkeys, uint32_t onum, const char** okeys,
+                        NDArrayHandle* vals, NDArrayHandle* outs, int priority);
+int MXKVStoreGetType(KVStoreHandle handle, const char** type);
+int MXKVStoreGetRank(KVStoreHandle handle, int* ret);
+int MXKVStoreGetGroupSize(KVStoreHandle handle, int* ret);
+int MXKVStoreBarrier(KVStoreHandle handle);
+
+/* ---- runtime */
+int MXRandomSeed(int seed);
+int MXRandomSeedContext(int seed, int dev_type, int dev_id);
+int MXNotifyShutdown(void);
+int MXSetNumOMPThreads(int thread_num);
+int MXGetGPUCount(int* out);
+int MXGetGPUMemoryInformation64(int dev, uint64_t* free_mem, uint64_t* total_mem);
+int MXEngineSetBulkSize(int bulk_size, int* prev_bulk_size);
+int MXSetIsNumpyShape(int is_np_shape, int* prev);
+int MXIsNumpyShape(int* curr);
+
+/* ---- Symbol / Executor extras */
+int MXSymbolCopy(SymbolHandle symbol, SymbolHandle* out);
+int MXSymbolPrint(SymbolHandle symbol, const char** out_str);
+int MXSymbolGetAttr(SymbolHandle symbol, const char* key, const char** out, int* success);
+int MXSymbolSetAttr(SymbolHandle symbol, const char* key, const char* value);
+int MXSymbolGetInternals(SymbolHandle symbol, SymbolHandle* out);
+int MXSymbolGetChildren(SymbolHandle symbol, SymbolHandle* out);
+int MXSymbolGetOutput(SymbolHandle symbol, uint32_t index, SymbolHandle* out);
+int MXSymbolGetNumOutputs(SymbolHandle symbol, uint32_t* output_count);
+int MXSymbolCreateGroup(uint32_t num_symbols, SymbolHandle* symbols, SymbolHandle* out);
+int MXSymbolSaveToFile(SymbolHandle symbol, const char* fname);
+int MXExecutorPrint(ExecutorHandle handle, const char** out_str);
 
 #ifdef __cplusplus
 }
