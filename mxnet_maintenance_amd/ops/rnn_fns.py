@@ -9,7 +9,9 @@ direction) the work is split the MI355X way:
   every gate of a 16x16 (batch x hidden) tile on the matrix cores and the cell update in
   registers; fp32 layers use the exact-f32 MFMA;
 * backward (``rnn_bwd_seq``) produces the gate gradients step by step with the same fused
-  structure, then the weight / input gradients are three large GEMMs over all steps.
+  structure, then the weight / input gradients are three large GEMMs over all steps: dX on the
+  in-tree GEMM (gemm.hip), dW_ih / dW_hh on the in-tree TN weight-gradient kernel (conv_wgrad.hip),
+  hipBLASLt only for widths that do not tile (I, H not multiples of 64) or fp32 layers.
 
 Each (layer, direction) is one ``torch.autograd.Function``; layers chain through autograd
 (inter-layer dropout in between), directions are concatenated along the feature axis.
@@ -41,6 +43,56 @@ def _proj(x2, w, bias):
             return G.gemm_nt(x2, w, bias=bias, out_f32=True, cfg=cfgs[0])
     return torch.addmm(bias.float(), x2.float(), w.float().t()) if x2.dtype != torch.float32 else \
         torch.addmm(bias, x2, w.t())
+
+
+# which path each backward GEMM took (tests assert the in-tree one): 'gemm' = gemm.hip (dX),
+# 'wgrad' = conv_wgrad.hip's TN reduction (dW), 'vendor' = torch.mm (hipBLASLt) / fp32
+DISPATCH = {'gemm': 0, 'wgrad': 0, 'vendor': 0}
+
+
+def _require_hip():
+    import os
+    return os.environ.get('MXAMD_REQUIRE_HIP', '0') == '1'
+
+
+def _vendor(what):
+    if _require_hip():
+        from ..base import MXNetError
+        raise MXNetError('RNN backward: %s does not tile for the in-tree GEMM kernels (MXAMD_REQUIRE_HIP=1)' % what)
+    DISPATCH['vendor'] += 1
+
+
+def _input_grad(g, w):
+    """dX = g . w for g [M, G*H] and the layer weight w [G*H, I]: the in-tree NT GEMM on w^T (one
+    small transposed copy per call), tile chosen by the autotuner among the gemm.hip configs."""
+    from . import gemm as G
+    from . import kernel_fns as KF
+    wt = w.t().contiguous()
+    if g.dtype in G._DT and g.is_contiguous() and G.gemm_ok(g, wt):
+        cands = G.candidates(g, wt)
+        if cands:
+            DISPATCH['gemm'] += 1
+            key = ('rnn_dx', tuple(g.shape), tuple(wt.shape), g.dtype)
+            return KF._select(key, cands, cands[0][0])
+    _vendor('dX %s x %s' % (tuple(g.shape), tuple(w.shape)))
+    return torch.mm(g, w)
+
+
+def _weight_grad(g, x, wdtype):
+    """dW = g^T . x for g [M, G*H], x [M, C]: a reduction over the M = T*N rows, i.e. the weight
+    gradient of a 1x1 convolution -- the in-tree TN kernel of conv_wgrad.hip (fp32 slabs + a
+    deterministic reduce)."""
+    from . import kernel_fns as KF
+    M, GH = g.shape
+    C = x.shape[1]
+    x4 = x.contiguous().view(1, 1, M, C)
+    if g.dtype == x.dtype and KF.conv_wgrad_ok(x4, torch.empty((GH, 1, 1, C), device='meta')):
+        DISPATCH['wgrad'] += 1
+        out = torch.empty((GH, 1, 1, C), dtype=wdtype, device=g.device)
+        KF.conv_wgrad(x4, g.contiguous().view(1, 1, M, GH), (GH, 1, 1, C), (1, 1), (0, 0), out=out)
+        return out.view(GH, C)
+    _vendor('dW %s x %s' % (tuple(g.shape), tuple(x.shape)))
+    return torch.mm(g.t(), x)
 
 
 class _LayerDir(torch.autograd.Function):
@@ -110,9 +162,9 @@ class _LayerDir(torch.autograd.Function):
         gH = dgh.reshape(T * N, G * H)
         # h_{t-1} of every step in forward order
         hprev = torch.cat([out[1:], h0[None]], 0) if reverse else torch.cat([h0[None], out[:-1]], 0)
-        dx = torch.mm(gX, w_ih).view(T, N, I) if ctx.needs_input_grad[0] else None
-        dw_ih = torch.mm(gX.t(), x.reshape(T * N, I)) if ctx.needs_input_grad[3] else None
-        dw_hh = torch.mm(gH.t(), hprev.reshape(T * N, H)) if ctx.needs_input_grad[4] else None
+        dx = _input_grad(gX, w_ih).view(T, N, I) if ctx.needs_input_grad[0] else None
+        dw_ih = _weight_grad(gX, x.reshape(T * N, I), w_ih.dtype) if ctx.needs_input_grad[3] else None
+        dw_hh = _weight_grad(gH, hprev.reshape(T * N, H), w_hh.dtype) if ctx.needs_input_grad[4] else None
         db_ih = gX.sum(0, dtype=torch.float32) if ctx.needs_input_grad[5] else None
         db_hh = gH.sum(0, dtype=torch.float32) if ctx.needs_input_grad[6] else None
         dc0 = dc.to(ctx.c0_dtype) if (dc is not None and ctx.has_c0) else None

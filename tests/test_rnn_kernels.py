@@ -71,20 +71,29 @@ def test_fused_rnn_matches_fp32_reference(mode, dt, H):
 
 
 def test_rnn_op_runs_in_tree_kernels():
-    """The registered RNN operator takes the in-tree path on the GPU (a Gluon LSTM layer step)."""
+    """The registered RNN operator takes the in-tree path on the GPU (a Gluon LSTM layer step): the
+    recurrent kernels forward and backward, dX on gemm.hip and dW on conv_wgrad.hip -- counted per
+    dispatch, with MXAMD_REQUIRE_HIP=1 turning any vendor fallback into an error."""
     import os
     import mxnet_maintenance_amd as mx
     from mxnet_maintenance_amd import gluon, autograd, nd
+    from mxnet_maintenance_amd.ops import rnn_fns
     os.environ['MXAMD_REQUIRE_HIP'] = '1'
     try:
         layer = gluon.rnn.LSTM(64, num_layers=2, bidirectional=True)
         layer.initialize(ctx=mx.gpu(0))
-        x = nd.random.uniform(shape=(12, 8, 32), ctx=mx.gpu(0))
+        layer.cast('float16')
+        x = nd.random.uniform(shape=(12, 8, 64), ctx=mx.gpu(0)).astype('float16')
         x.attach_grad()
+        before = dict(rnn_fns.DISPATCH)
         with autograd.record():
             y = layer(x)
         y.backward()
         assert y.shape == (12, 8, 128)
         assert float(x.grad.abs().sum().asscalar()) > 0
+        # 2 layers x 2 directions: one dX GEMM and two dW reductions each
+        assert rnn_fns.DISPATCH['gemm'] - before['gemm'] == 4
+        assert rnn_fns.DISPATCH['wgrad'] - before['wgrad'] == 8
+        assert rnn_fns.DISPATCH['vendor'] == before['vendor']
     finally:
         os.environ.pop('MXAMD_REQUIRE_HIP', None)
