@@ -460,15 +460,12 @@ def async_copy_ok(src, dev):
 # it reads and for the readers / writer of the arrays it writes, so independent chains overlap.
 # Here, with MXNET_GPU_WORKER_NTHREADS = N > 1, every imperative operator is issued (from the calling
 # thread: no hand-off, so no added latency) on one of N streams of its device -- slot 0 is the caller's
-# current stream, slots 1..N-1 are worker streams:
-#   * a chain stays on the stream that produced its inputs; an operator whose GPU inputs no worker
-#     slot produced (parameters, uploaded data) starts a new chain on the next slot, round-robin;
-#   * an input produced on another slot makes the operator's stream wait for that slot on the GPU
-#     (stream-on-stream wait) and is recorded on it for the caching allocator; an in-place write
-#     (``out=``) also waits for the slots that read the target since its last write;
-#   * host-visible points -- asnumpy / wait_to_read / waitall, copies, setitem, optimizer and kvstore
-#     updates -- first join the worker slots into the caller's stream (join_workers), so every code
-#     path outside operator dispatch sees finished results.
+# current stream, slots 1..N-1 are worker streams.  The dependency state is kept by the native
+# engine's Dispatcher (src/native/engine.{h,cc}) on the engine variables of the arrays (one variable
+# per storage, shared by views): a chain stays on the stream that produced its inputs, cross-slot
+# inputs and in-place targets are waited for on the GPU with lazily recorded HIP events, and
+# host-visible points -- asnumpy / wait_to_read / waitall, copies, setitem, optimizer and kvstore
+# updates -- join the worker slots into the caller's stream (join_workers).
 # The default (1) keeps everything on the caller's stream.
 GPU_WORKERS = max(1, int(os.environ.get('MXNET_GPU_WORKER_NTHREADS', '1') or 1))
 
@@ -476,22 +473,34 @@ GPU_WORKERS = max(1, int(os.environ.get('MXNET_GPU_WORKER_NTHREADS', '1') or 1))
 class _Workers:
     def __init__(self):
         self.streams = {}     # device index -> [None, stream 1, ..., stream N-1]
-        self.rr = {}          # device index -> next slot for a new chain
-        self.dirty = {}       # device index -> slots with work not yet joined into the caller's stream
+        self.depth = 0        # > 0 while an operator body runs (nested operators stay on its stream)
+        self.pending = []     # (device, slot, read vars) of the operators being issued (a stack)
+        self.dirty = {}       # device index -> True when a worker slot has work since the last join
         # device index -> weak references to outputs produced on worker slots since the last join: the
         # caching allocator ties their blocks to the worker stream, so the join records them on the
         # caller's stream too (else a block freed while the caller's stream still reads it could be
         # handed to the next worker-stream allocation)
         self.produced = {}
-        self.depth = 0        # > 0 while an operator body runs (nested operators stay on its stream)
+        self.disp = None
+
+    def dispatcher(self):
+        if self.disp is None:
+            nat = _load_native()
+            if nat is None:
+                raise RuntimeError('worker-stream dispatch needs the native engine (tools/build_native.py)')
+            self.disp = nat.Dispatcher(False)
+        return self.disp
 
     def stream(self, dev, sid):
         import torch
         if sid == 0:
             return torch.cuda.current_stream(dev)
         lst = self.streams.get(dev)
-        if lst is None or len(lst) < GPU_WORKERS:
-            lst = self.streams[dev] = [None] + [torch.cuda.Stream(device=dev) for _ in range(GPU_WORKERS - 1)]
+        if lst is None or len(lst) != GPU_WORKERS:
+            old = lst or [None]
+            lst = self.streams[dev] = [None] + [old[i] if i < len(old) else torch.cuda.Stream(device=dev)
+                                                for i in range(1, GPU_WORKERS)]
+            self.dispatcher().set_streams(dev, [int(x.cuda_stream) for x in lst[1:]])
         return lst[sid]
 
 
@@ -504,6 +513,8 @@ def set_gpu_workers(n):
     global GPU_WORKERS
     join_workers()
     prev, GPU_WORKERS = GPU_WORKERS, max(1, int(n))
+    if GPU_WORKERS > 1 and _load_native() is None:
+        GPU_WORKERS = 1           # the dependency state lives in the native engine
     return prev
 
 
@@ -514,86 +525,68 @@ def _gpu_device(tensors):
     return None
 
 
-_epoch = [0]     # bumped at every host-visible point (join_workers)
+def _dvar(t):
+    """The engine variable of tensor ``t``'s storage (views share their base's)."""
+    base = t._base if t._base is not None else t
+    v = getattr(base, '_mx_var', None)
+    if v is None:
+        v = base._mx_var = get().new_var('')
+    return v
 
 
-def _slot_of(t):
-    """Worker slot that produced tensor ``t`` (or the base of the view ``t``); None when it was
-    written outside operator dispatch (ordered on the caller's stream)."""
-    sid = getattr(t, '_mx_sid', None)
-    if sid is None and t._base is not None:
-        sid = getattr(t._base, '_mx_sid', None)
-    return sid if sid is not None and sid < GPU_WORKERS else None
+def slot_of(t):
+    """Worker slot that last wrote tensor (or NDArray) ``t`` through dispatch; None when it was
+    written outside operator dispatch (on the caller's stream)."""
+    t = getattr(t, '_data', t)
+    base = t._base if t._base is not None else t
+    v = getattr(base, '_mx_var', None)
+    if v is None or _load_native() is None:
+        return None
+    s = _load_native().Dispatcher.slot_of(v)
+    return s if s >= 0 else None
 
 
 def op_stream(tensors):
-    """(slot, stream) an imperative operator on the input ``tensors`` runs on, with the waits and
-    allocator records for inputs produced elsewhere issued; (None, None) without a GPU input."""
+    """(slot, stream) an imperative operator on the input ``tensors`` runs on, with the GPU waits for
+    inputs produced on other slots issued by the native dispatcher; (None, None) without a GPU input."""
     dev = _gpu_device(tensors)
     if dev is None:
         return None, None
-    sid = None
-    for t in tensors:
-        if t is not None and t.is_cuda:
-            sid = _slot_of(t)
-            if sid is not None:
-                break
-    if sid is None:
-        sid = _workers.rr.get(dev, 0)
-        _workers.rr[dev] = (sid + 1) % GPU_WORKERS
+    _workers.stream(dev, 1)                 # worker streams exist and are known to the dispatcher
+    import torch
+    cur = torch.cuda.current_stream(dev)
+    reads = [_dvar(t) for t in tensors if t is not None and t.is_cuda]
+    sid = _workers.dispatcher().begin(dev, int(cur.cuda_stream), reads)
     stream = _workers.stream(dev, sid)
-    for t in tensors:
-        if t is None or not t.is_cuda:
-            continue
-        xs = _slot_of(t)
-        if xs is None:
-            # written on the caller's stream: a worker slot orders after it once per epoch
-            if sid != 0:
-                seen = getattr(t, '_mx_seen', None)
-                if seen is None or seen[0] != _epoch[0]:
-                    seen = (_epoch[0], set())
-                    t._mx_seen = seen
-                if sid not in seen[1]:
-                    stream.wait_stream(_workers.stream(dev, 0))
-                    seen[1].add(sid)
-                t.record_stream(stream)
-        elif xs != sid:
-            stream.wait_stream(_workers.stream(dev, xs))
-            t.record_stream(stream)
-        rd = getattr(t, '_mx_readers', None)
-        if rd is None:
-            t._mx_readers = {sid}
-        else:
-            rd.add(sid)
+    if sid:
+        for t in tensors:
+            if t is not None and t.is_cuda:
+                t.record_stream(stream)     # the caching allocator keeps inputs alive for this stream
+    _workers.pending.append((dev, sid, reads))
     return sid, stream
 
 
 def op_written(t, sid, stream):
     """Before an in-place write of tensor ``t`` on slot ``sid``: wait for its writer and readers."""
     if t.is_cuda:
+        import torch
         dev = t.device.index
-        prev = _slot_of(t)
-        for r in set(getattr(t, '_mx_readers', None) or ()) | {prev if prev is not None else 0}:
-            if r != sid and r < GPU_WORKERS:
-                stream.wait_stream(_workers.stream(dev, r))
-    t._mx_readers = None
-    op_done([t], sid)
+        _workers.dispatcher().write(dev, int(torch.cuda.current_stream(dev).cuda_stream), sid, _dvar(t))
+        _workers.dispatcher().end(dev, sid, [], [_dvar(t)])
 
 
 def op_done(tensors, sid):
-    """Mark output ``tensors`` as produced on slot ``sid``."""
-    for t in tensors:
-        if isinstance(t, _torch_tensor()):
-            t._mx_sid = sid
-    if sid:
-        ts = [t for t in tensors if isinstance(t, _torch_tensor())]
-        dev = _gpu_device(ts)
-        if dev is not None:
-            _workers.dirty.setdefault(dev, set()).add(sid)
-            lst = _workers.produced.setdefault(dev, [])
-            for t in ts:
-                if t.is_cuda:
-                    lst.append(weakref.ref(t))
+    """Mark output ``tensors`` as produced on slot ``sid`` (closes the operator op_stream opened)."""
+    if not _workers.pending:
+        return
+    dev, slot, reads = _workers.pending.pop()
+    ts = [t for t in tensors if isinstance(t, _torch_tensor()) and t.is_cuda]
+    _workers.dispatcher().end(dev, slot, reads, [_dvar(t) for t in ts])
+    if slot:
+        _workers.dirty[dev] = True
+        lst = _workers.produced.setdefault(dev, [])
+        for t in ts:
+            lst.append(weakref.ref(t))
 
 
 def _torch_tensor():
@@ -622,19 +615,17 @@ def join_workers(dev=None):
         return            # inside an operator body: its own stream is already the right one
     for fn in _JOIN_HOOKS:
         fn()
-    _epoch[0] += 1
     if not _workers.dirty:
         return
     import torch
     devs = [dev] if dev is not None else list(_workers.dirty)
     for d in devs:
-        slots = _workers.dirty.pop(d, None)
+        if not _workers.dirty.pop(d, False):
+            continue
         produced = _workers.produced.pop(d, ())
-        if slots:
-            cur = torch.cuda.current_stream(d)
-            for sid in slots:
-                cur.wait_stream(_workers.stream(d, sid))
-            for ref in produced:
-                t = ref()
-                if t is not None:
-                    t.record_stream(cur)
+        cur = torch.cuda.current_stream(d)
+        _workers.dispatcher().join(d, int(cur.cuda_stream))
+        for ref in produced:
+            t = ref()
+            if t is not None:
+                t.record_stream(cur)

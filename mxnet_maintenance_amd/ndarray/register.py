@@ -7,6 +7,8 @@ runs the op's torch-level implementation under the right autograd mode.
 """
 import contextlib
 
+import sys
+
 import torch
 
 from .. import _state
@@ -255,6 +257,8 @@ def invoke(op, inputs, attrs, out=None):
     finally:
         if ws_stream is not None:
             _engine._workers.depth -= 1
+            if sys.exc_info()[0] is not None:
+                _engine._workers.pending.pop()      # the operator raised: no op_done will close it
     nvis = op.get_num_visible_outputs(attrs)
     if isinstance(res, (tuple, list)):
         outs = [NDArray(r) for r in res[:nvis]]

@@ -48,6 +48,17 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("version", [](const Var& v) { return v.version; })
       .def_property_readonly("name", [](const Var& v) { return v.name; });
 
+  py::class_<Dispatcher>(m, "Dispatcher")
+      .def(py::init<bool>(), py::arg("trace") = false)
+      .def("set_streams", &Dispatcher::SetStreams, py::arg("device"), py::arg("workers"))
+      .def("begin", &Dispatcher::Begin, py::arg("device"), py::arg("cur"), py::arg("reads"))
+      .def("write", &Dispatcher::Write, py::arg("device"), py::arg("cur"), py::arg("slot"), py::arg("target"))
+      .def("end", &Dispatcher::End, py::arg("device"), py::arg("slot"), py::arg("reads"), py::arg("writes"))
+      .def("join", &Dispatcher::Join, py::arg("device"), py::arg("cur"))
+      .def_static("slot_of", &Dispatcher::SlotOf)
+      .def("take_trace", &Dispatcher::TakeTrace)
+      .def_property_readonly("waits", &Dispatcher::waits);
+
   py::class_<Engine>(m, "Engine")
       .def(py::init<int, bool, bool>(), py::arg("num_workers") = 4, py::arg("naive") = false,
            py::arg("debug") = false)

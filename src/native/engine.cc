@@ -492,4 +492,164 @@ void Engine::WaitForAll() {
   if (exc) std::rethrow_exception(exc);
 }
 
+// ------------------------------------------------------------------ imperative dispatch (engine.h)
+Dispatcher::~Dispatcher() {
+  if (trace_) return;
+  for (auto& d : devs_)
+    for (auto& sl : d.slots)
+      if (sl.ev) HipRt::Get().event_destroy(sl.ev);
+}
+
+Dispatcher::Dev& Dispatcher::D(int device) {
+  if (device < 0) throw std::runtime_error("dispatcher: bad device");
+  if (static_cast<int>(devs_.size()) <= device) devs_.resize(device + 1);
+  Dev& d = devs_[device];
+  if (d.slots.empty()) d.slots.resize(1);
+  return d;
+}
+
+void Dispatcher::SetStreams(int device, const std::vector<uintptr_t>& workers) {
+  std::lock_guard<std::mutex> lk(mu_);
+  Dev& d = D(device);
+  if (workers.size() + 1 > 32) throw std::runtime_error("dispatcher: at most 32 slots per device");
+  d.slots.resize(workers.size() + 1);
+  for (size_t i = 0; i < workers.size(); ++i) d.slots[i + 1].stream = workers[i];
+  if (d.rr >= static_cast<int>(d.slots.size())) d.rr = 0;
+}
+
+// make slot `waiter` wait for slot `on`'s operators up to `seq` (seq 0: everything issued so far)
+void Dispatcher::WaitFor(int device, Dev& d, int waiter, uintptr_t cur, int on, uint64_t seq) {
+  if (waiter == on) return;
+  Slot& src = d.slots[on];
+  const uint64_t need = seq ? seq : src.seq;
+  ++waits_;
+  if (trace_) {
+    log_.emplace_back(device, waiter, on);
+    return;
+  }
+  HipRt& rt = HipRt::Get();
+  if (!src.has_ev || src.rec_seq < need || on == 0) {
+    // slot 0 is the caller's stream: outside writes are not counted, so its event is always fresh
+    if (!src.ev) HipCheck(rt.event_create(&src.ev, 0x2 /* hipEventDisableTiming */), "hipEventCreateWithFlags");
+    HipCheck(rt.event_record(src.ev, reinterpret_cast<void*>(StreamOf(d, on, cur))), "hipEventRecord");
+    src.has_ev = true;
+    src.rec_seq = src.seq;
+  }
+  HipCheck(rt.stream_wait_event(reinterpret_cast<void*>(StreamOf(d, waiter, cur)), src.ev, 0),
+           "hipStreamWaitEvent");
+}
+
+int Dispatcher::Begin(int device, uintptr_t cur, const std::vector<VarHandle>& reads) {
+  std::lock_guard<std::mutex> lk(mu_);
+  Dev& d = D(device);
+  const int ns = static_cast<int>(d.slots.size());
+  int slot = -1;
+  for (const auto& v : reads) {
+    std::lock_guard<std::mutex> vl(v->mu);
+    if (v->d_wslot >= 0 && v->d_wslot < ns) {
+      slot = v->d_wslot;
+      break;
+    }
+  }
+  if (slot < 0) {
+    slot = d.rr;
+    d.rr = (d.rr + 1) % ns;
+  }
+  // one wait per source slot: the newest op it must cover (0 = everything issued so far)
+  std::vector<int64_t> need(ns, -1);
+  auto want = [&](int on, uint64_t q) {
+    if (on == slot) return;
+    if (need[on] < 0 || q == 0 || (need[on] != 0 && static_cast<int64_t>(q) > need[on])) need[on] = static_cast<int64_t>(q);
+  };
+  for (const auto& v : reads) {
+    std::lock_guard<std::mutex> vl(v->mu);
+    if (v->d_wslot >= 0 && v->d_wslot < ns) {
+      want(v->d_wslot, v->d_wseq);
+      continue;
+    }
+    // written on the caller's stream: a worker slot orders after it once per epoch
+    if (slot == 0) continue;
+    if (v->d_ext_epoch != epoch_) {
+      v->d_ext_epoch = epoch_;
+      v->d_ext_mask = 0;
+    }
+    if (v->d_ext_mask & (1u << slot)) continue;
+    v->d_ext_mask |= 1u << slot;
+    want(0, 0);
+  }
+  for (int on = 0; on < ns; ++on)
+    if (need[on] >= 0) WaitFor(device, d, slot, cur, on, static_cast<uint64_t>(need[on]));
+  return slot;
+}
+
+void Dispatcher::Write(int device, uintptr_t cur, int slot, const VarHandle& v) {
+  std::lock_guard<std::mutex> lk(mu_);
+  Dev& d = D(device);
+  const int ns = static_cast<int>(d.slots.size());
+  std::vector<int64_t> need(ns, -1);
+  auto want = [&](int on, uint64_t q) {
+    if (on == slot) return;
+    if (need[on] < 0 || q == 0 || (need[on] != 0 && static_cast<int64_t>(q) > need[on])) need[on] = static_cast<int64_t>(q);
+  };
+  {
+    std::lock_guard<std::mutex> vl(v->mu);
+    if (v->d_wslot >= 0 && v->d_wslot < ns) want(v->d_wslot, v->d_wseq);
+    else want(0, 0);
+    for (const auto& r : v->d_readers)
+      if (r.first < ns) want(r.first, r.second);
+  }
+  for (int on = 0; on < ns; ++on)
+    if (need[on] >= 0) WaitFor(device, d, slot, cur, on, static_cast<uint64_t>(need[on]));
+}
+
+void Dispatcher::End(int device, int slot, const std::vector<VarHandle>& reads, const std::vector<VarHandle>& writes) {
+  std::lock_guard<std::mutex> lk(mu_);
+  Dev& d = D(device);
+  const uint64_t seq = ++d.slots[slot].seq;
+  if (slot) d.dirty |= 1u << slot;
+  for (const auto& v : reads) {
+    std::lock_guard<std::mutex> vl(v->mu);
+    bool found = false;
+    for (auto& r : v->d_readers)
+      if (r.first == slot) {
+        r.second = seq;
+        found = true;
+      }
+    if (!found) v->d_readers.emplace_back(slot, seq);
+  }
+  for (const auto& v : writes) {
+    std::lock_guard<std::mutex> vl(v->mu);
+    v->d_wslot = slot;
+    v->d_wseq = seq;
+    v->d_readers.clear();
+  }
+}
+
+std::vector<int> Dispatcher::Join(int device, uintptr_t cur) {
+  std::lock_guard<std::mutex> lk(mu_);
+  ++epoch_;
+  std::vector<int> joined;
+  if (device < 0 || device >= static_cast<int>(devs_.size())) return joined;
+  Dev& d = devs_[device];
+  for (int s = 1; s < static_cast<int>(d.slots.size()); ++s) {
+    if (!(d.dirty & (1u << s))) continue;
+    WaitFor(device, d, 0, cur, s, 0);
+    joined.push_back(s);
+  }
+  d.dirty = 0;
+  return joined;
+}
+
+int Dispatcher::SlotOf(const VarHandle& v) {
+  std::lock_guard<std::mutex> vl(v->mu);
+  return v->d_wslot;
+}
+
+std::vector<std::tuple<int, int, int>> Dispatcher::TakeTrace() {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<std::tuple<int, int, int>> out;
+  out.swap(log_);
+  return out;
+}
+
 }  // namespace mxamd

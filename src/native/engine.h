@@ -36,6 +36,7 @@
 #include <queue>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 namespace mxamd {
@@ -65,6 +66,15 @@ struct Var {
   // debug-mode bookkeeping
   uint64_t pushed_writes = 0;
   int active_readers = 0, active_writers = 0;
+  // imperative dispatch on worker streams (Dispatcher): the slot / op sequence number of the last
+  // dispatched writer (slot -1: written outside dispatch, i.e. on the caller's stream), the
+  // (slot, seq) readers since that write, and the slots that already ordered themselves after the
+  // caller's stream for an outside write in the current dispatch epoch
+  int d_wslot = -1;
+  uint64_t d_wseq = 0;
+  std::vector<std::pair<int, uint64_t>> d_readers;
+  uint64_t d_ext_epoch = 0;
+  uint32_t d_ext_mask = 0;
 };
 
 using VarHandle = std::shared_ptr<Var>;
@@ -85,6 +95,61 @@ struct Opr {
   int device = -1;
   // debug mode: expected version of each const / mutable var when the op starts
   std::vector<uint64_t> expect_const, expect_mut;
+};
+
+// Imperative operators on N streams per device (the ThreadedEnginePerDevice GPU workers of
+// src/engine/threaded_engine_perdevice.cc, with the issue done inline by the calling thread: the
+// operators are host-cheap kernel launches, so handing them to worker threads would only add
+// latency).  Slot 0 is the caller's current stream, slots 1..N-1 are worker streams.  The dependency
+// state lives on the engine variables of the arrays (Var::d_*):
+//   * an operator runs on the slot that last wrote its first dispatched input (a chain stays on its
+//     stream), else on the next slot round-robin;
+//   * it waits on the GPU for writers of its inputs on other slots, and an in-place write also for
+//     the other slots' readers of the target since its last write;
+//   * inputs written outside dispatch (on the caller's stream) order a worker slot after the
+//     caller's stream once per epoch;
+//   * join() (every host-visible point) makes the caller's stream wait for all slots with work and
+//     starts a new epoch.
+// Cross-stream edges are HIP events recorded lazily: one event per slot is recorded only when a
+// waiter needs it and no recorded event already covers the op it waits for.  With trace = true no
+// HIP call is made and every wait edge is logged instead (CPU tests of the protocol).
+class Dispatcher {
+ public:
+  explicit Dispatcher(bool trace) : trace_(trace) {}
+  ~Dispatcher();
+  void SetStreams(int device, const std::vector<uintptr_t>& workers);
+  int Begin(int device, uintptr_t cur, const std::vector<VarHandle>& reads);
+  void Write(int device, uintptr_t cur, int slot, const VarHandle& target);
+  void End(int device, int slot, const std::vector<VarHandle>& reads, const std::vector<VarHandle>& writes);
+  // returns the slots joined
+  std::vector<int> Join(int device, uintptr_t cur);
+  static int SlotOf(const VarHandle& v);
+  std::vector<std::tuple<int, int, int>> TakeTrace();
+  uint64_t waits() const { return waits_; }
+
+ private:
+  struct Slot {
+    uintptr_t stream = 0;
+    uint64_t seq = 0;       // operators issued on this slot
+    uint64_t rec_seq = 0;   // ops covered by the last recorded event
+    void* ev = nullptr;
+    bool has_ev = false;
+  };
+  struct Dev {
+    std::vector<Slot> slots;   // [0] = the caller's stream (handle passed per call)
+    uint32_t dirty = 0;
+    int rr = 0;
+  };
+  Dev& D(int device);
+  void WaitFor(int device, Dev& d, int waiter, uintptr_t cur, int on, uint64_t seq);
+  uintptr_t StreamOf(Dev& d, int slot, uintptr_t cur) { return slot == 0 ? cur : d.slots[slot].stream; }
+
+  bool trace_;
+  std::mutex mu_;
+  std::vector<Dev> devs_;
+  uint64_t epoch_ = 1;
+  uint64_t waits_ = 0;
+  std::vector<std::tuple<int, int, int>> log_;
 };
 
 class Engine {

@@ -36,7 +36,7 @@ def _chains(ctx, n=12):
 def test_independent_chains_take_different_streams(workers):
     ctx = mx.gpu(0)
     a, b, _w = _chains(ctx)
-    assert {getattr(a._data, '_mx_sid', None), getattr(b._data, '_mx_sid', None)} == {0, 1}
+    assert {engine.slot_of(a), engine.slot_of(b)} == {0, 1}
     c = a + b                       # joins the chains: waits for the other stream on the GPU
     got = (a.asnumpy(), b.asnumpy(), c.asnumpy())
     engine.set_gpu_workers(1)
