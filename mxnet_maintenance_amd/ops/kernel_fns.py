@@ -603,6 +603,42 @@ def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=Non
     return y
 
 
+def halo_ok(x, w, stride, pad):
+    """True when the halo-tile 3x3 kernel (src/kernels/conv_halo.hip: C = K = 64, stride 1, pad 1)
+    takes this NHWC conv."""
+    K, R, S, C = w.shape
+    return (_CONV_HIP and x.is_cuda and x.dtype in (torch.float16, torch.bfloat16) and x.dim() == 4
+            and x.is_contiguous() and w.is_contiguous() and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+            and hasattr(_K.lib(), 'conv3x3_halo')
+            and bool(_K.lib().conv3x3_halo_ok(C, K, R, S, stride[0], stride[1], pad[0], pad[1], x.shape[2])))
+
+
+def conv_halo(x, w, bn_stats=False, bn_bwd=None):
+    """y = conv3x3(x, w) (stride 1, pad 1, C = K = 64) on the halo-tile kernel.  ``bn_stats``: BatchNorm
+    sum / sum-of-squares partials attached as ``y._mxamd_bn_part`` (one per workgroup); ``bn_bwd`` (a
+    BatchNorm's ``_mxamd_bn_src`` record with mode 0 / 2, y being that BN's incoming gradient): its
+    backward statistics attached as ``y._mxamd_bn_bwd``."""
+    N, H, W, C = x.shape
+    K = w.shape[0]
+    lib = _K.lib()
+    y = torch.empty((N, H, W, K), dtype=x.dtype, device=x.device)
+    nparts = lib.conv3x3_halo_nparts(N, H)
+    part = torch.empty(2 * K * nparts, dtype=torch.float32, device=x.device) if (bn_stats or bn_bwd) else None
+    kw = {}
+    if bn_bwd is not None:
+        z, bmean, bscale, bshift, _bmask, bmode, _token = bn_bwd
+        assert int(bmode) in (0, 2) and z.shape == y.shape and z.dtype == y.dtype and z.is_contiguous()
+        kw = dict(bn_z=z.data_ptr(), bn_mean=bmean.data_ptr(), bn_scale=_p(bscale), bn_shift=_p(bshift),
+                  bn_mode=int(bmode), bn_part=part.data_ptr())
+    lib.conv3x3_halo(_DT[x.dtype], x.data_ptr(), w.data_ptr(), y.data_ptr(), _zero_page(x.device).data_ptr(), N, H,
+                     W, C, K, _p(part) if bn_bwd is None else 0, nparts if bn_bwd is None else 0, s=_stream(), **kw)
+    if bn_bwd is not None:
+        y._mxamd_bn_bwd = (part, nparts, bn_bwd[6], y._version)
+    elif part is not None:
+        y._mxamd_bn_part = (part, nparts)
+    return y
+
+
 def glds_bnb_ok(bn_src):
     """The LDS-DMA (glds / phase) kernels emit BN-backward statistics for a BN without ReLU or with
     the ReLU mask recomputed from z (modes 0 / 2), not from a stored mask bitmap."""
@@ -1123,6 +1159,8 @@ def _fwd_candidates(x, w, stride, pad, bias):
         c.append(('pw', lambda: conv_pw(x, w.reshape(K, C), bn_stats=bool(_state.STATE.training))))
     if stem_ok(x, w, stride, pad, bias):
         c.append(('stem', lambda: conv_stem_fwd(x, w, pad, bn_stats=bool(_state.STATE.training))))
+    if bias is None and halo_ok(x, w, stride, pad):
+        c.append(('halo', lambda: conv_halo(x, w, bn_stats=bool(_state.STATE.training))))
     if conv_ok_shape(x, w, stride, pad):
         c.append(('hip', lambda: conv_fwd(x, w, stride, pad, bias)))
         stats = bool(_state.STATE.training)
@@ -1206,6 +1244,8 @@ def _dgrad_candidates(dy, x, w, stride, pad):
     for bco in (128, 64):
         if conv_dgrad_strided_ok(dy, w, stride, pad, x.shape, bco):
             c.append(('phase%d' % bco, lambda bco=bco: conv_dgrad_strided(dy, w, stride, pad, x.shape, bco)))
+    if halo_ok(dy, w, stride, pad) and tuple(dy.shape) == tuple(x.shape[:3]) + (K,):
+        c.append(('halo', lambda: conv_halo(dy, _dgrad_weight(w))))
     c.append(('miopen', lambda: _conv_bwd_torch(dy, x, w, stride, pad, (True, False))[0]))
     return c
 
@@ -1279,6 +1319,8 @@ def _dgrad_bn_candidates(dy, x, w, stride, pad, bn_src):
                 fused.append(('hip%d+bn' % v, lambda v=v: conv_fwd(dy, _dgrad_weight(w), (1, 1),
                                                                    (R - 1 - pad[0], S - 1 - pad[1]), None, v,
                                                                    bn_bwd=bn_src)))
+    if glds_bnb_ok(bn_src) and halo_ok(dy, w, stride, pad) and tuple(dy.shape) == tuple(x.shape[:3]) + (K,):
+        fused.append(('halo+bn', lambda: conv_halo(dy, _dgrad_weight(w), bn_bwd=bn_src)))
     if glds_bnb_ok(bn_src):
         for bco in (128, 64):
             if conv_dgrad_strided_ok(dy, w, stride, pad, x.shape, bco):

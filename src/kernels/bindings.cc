@@ -82,6 +82,11 @@ int conv_nhwc_fwd_ring_nparts(int N, int H, int W, int R, int S, int sh, int sw,
 void conv_nhwc_fwd_ring(int dtype, const void* x, const void* w, void* y, const void* zero, int N, int H, int W, int C,
                         int K, int R, int S, int sh, int sw, int ph, int pw, int variant, float* part, int nparts,
                         hipStream_t s);
+bool conv3x3_halo_ok(int C, int K, int R, int S, int sh, int sw, int ph, int pw, int W);
+int conv3x3_halo_nparts(int N, int H);
+void conv3x3_halo(int dtype, const void* x, const void* w, void* y, const void* zero, int N, int H, int W, int C, int K,
+                  float* part, int nparts, const void* bn_z, const float* bn_mean, const float* bn_scale,
+                  const float* bn_shift, int bn_mode, float* bn_part, hipStream_t s);
 int conv_nhwc_wgrad_ring_ok(int C, int K, int R, int S, int variant);
 int64_t conv_nhwc_wgrad_ring_workspace(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
                                        int variant);
@@ -528,6 +533,20 @@ PYBIND11_MODULE(_hip_kernels, m) {
                        variant, P<float>(part), nparts, S(s));
     check_launch("conv_nhwc_fwd_ring");
   });
+  // 3x3 stride-1 C = K = 64 halo-tile conv (conv_halo.hip): resident weights, one patch per 4 rows
+  m.def("conv3x3_halo_ok", &conv3x3_halo_ok);
+  m.def("conv3x3_halo_nparts", &conv3x3_halo_nparts);
+  m.def("conv3x3_halo", [](int dt, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t zero, int N, int H, int W, int C,
+                           int K, uintptr_t part, int nparts, uintptr_t bn_z, uintptr_t bn_mean, uintptr_t bn_scale,
+                           uintptr_t bn_shift, int bn_mode, uintptr_t bn_part, uintptr_t s) {
+    conv3x3_halo(dt, P<void>(x), P<void>(w), P<void>(y), P<void>(zero), N, H, W, C, K, P<float>(part), nparts,
+                 P<void>(bn_z), P<float>(bn_mean), P<float>(bn_scale), P<float>(bn_shift), bn_mode, P<float>(bn_part),
+                 S(s));
+    check_launch("conv3x3_halo");
+  }, py::arg("dt"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("zero"), py::arg("N"), py::arg("H"),
+     py::arg("W"), py::arg("C"), py::arg("K"), py::arg("part"), py::arg("nparts"), py::arg("bn_z") = 0,
+     py::arg("bn_mean") = 0, py::arg("bn_scale") = 0, py::arg("bn_shift") = 0, py::arg("bn_mode") = 0,
+     py::arg("bn_part") = 0, py::arg("s") = 0);
   m.def("conv_nhwc_wgrad_workspace", &conv_nhwc_wgrad_workspace);
   // weight gradient on the LDS-DMA ring (variants 1..5, see conv_wgrad.hip)
   m.def("conv_nhwc_wgrad_ring_ok", &conv_nhwc_wgrad_ring_ok);

@@ -38,6 +38,8 @@ def timeit(fn, iters=8):
 
 
 def family(v):
+    if v == 'halo':
+        return 'halo'
     if v in KF._RING_VARIANTS:
         return 'ring'
     if v in KF._BIG_VARIANTS:
@@ -53,7 +55,7 @@ def main():
     a = ap.parse_args()
     N = a.batch
     dt = torch.float16
-    fams = ('ring', 'big', 'big32', 'big224', 'glds', 'vendor')
+    fams = ('ring', 'big', 'big32', 'big224', 'glds', 'halo', 'vendor')
     tot = {f: 0.0 for f in fams}
     best_tot = 0.0
     for (H, Cin, Cout, k, s, cnt) in LAYERS:
@@ -69,6 +71,8 @@ def main():
             cands = {}
             for v in KF._fwd_variants(Cin, Cout):
                 cands[v] = (lambda v=v: KF.conv_fwd(x, w, (s, s), (pad, pad), None, v, bn_stats=a.stats))
+            if KF.halo_ok(x, w, (s, s), (pad, pad)):
+                cands['halo'] = (lambda: KF.conv_halo(x, w, bn_stats=a.stats))
             xc, wc = x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2)
             cands['vendor'] = lambda: F.conv2d(xc, wc, None, s, pad)
             ref = cands['vendor']().permute(0, 2, 3, 1).float()
