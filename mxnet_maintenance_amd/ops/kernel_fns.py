@@ -523,7 +523,24 @@ _SKINNY_ON = os.environ.get('MXAMD_CONV_SKINNY', '0') == '1'
 _RING_VARIANTS = {20: (128, 128), 21: (256, 128), 22: (128, 256), 23: (64, 256), 24: (256, 256), 25: (64, 128)}
 
 
-def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=None, bn_bwd=None):
+def conv_up2_ok(dy, w, stride, pad, xshape):
+    """The 1x1 stride-2 data gradient as one big-tile GEMM pass writing the 2x-upsampled, zero-filled
+    dX (conv_big.hip GeomB::up)."""
+    K, R, S, C = w.shape
+    return (_CONV_HIP and R == 1 and S == 1 and tuple(stride) == (2, 2) and tuple(pad) == (0, 0)
+            and dy.dtype in (torch.float16, torch.bfloat16) and dy.is_cuda and dy.dim() == 4 and K % 64 == 0
+            and xshape[1] == 2 * dy.shape[1] and xshape[2] == 2 * dy.shape[2] and xshape[3] == C)
+
+
+def conv_dgrad_up2(dy, w, variant, bn_bwd=None):
+    """dX of a 1x1 stride-2 conv: dY . W on the big-tile kernel, each result pixel stored at (2h, 2w) of
+    dX and its three 2x2 siblings zeroed by the same epilogue."""
+    K, _, _, C = w.shape
+    wt = w.reshape(K, C).t().contiguous().view(C, 1, 1, K)
+    return conv_fwd(dy.contiguous(), wt, (1, 1), (0, 0), None, variant, bn_bwd=bn_bwd, up=2)
+
+
+def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=None, bn_bwd=None, up=0):
     """y[N,Ho,Wo,K] = conv(x[N,H,W,C], w[K,R,S,C]) on the MFMA implicit-GEMM kernel.
 
     ``variant``: 0 = heuristic tile, 1..4 = (BCO, BK) in (128,64) (128,32) (64,64) (64,32),
@@ -539,7 +556,8 @@ def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=Non
     K, R, S, _ = w.shape
     Ho = (H + 2 * pad[0] - R) // stride[0] + 1
     Wo = (W + 2 * pad[1] - S) // stride[1] + 1
-    y = torch.empty((N, Ho, Wo, K), dtype=x.dtype, device=x.device)
+    assert up in (0, 2) and (up == 0 or (variant in _BIG_VARIANTS and addend is None and not bn_stats))
+    y = torch.empty((N, Ho * max(up, 1), Wo * max(up, 1), K), dtype=x.dtype, device=x.device)
     if N * Ho * Wo * K >= 2 ** 31:
         raise ValueError('conv_fwd: output too large for 32-bit indexing')
     b = _f32(bias) if bias is not None else None
@@ -577,7 +595,7 @@ def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=Non
                        bn_mask=_p(bmask), bn_mode=int(bmode), bn_part=bpart.data_ptr(), bn_nparts=bnp)
         lib.conv_nhwc_fwd_big(_DT[x.dtype], x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(),
                               _zero_page(x.device).data_ptr(), N, H, W, C, K, R, S, stride[0], stride[1],
-                              pad[0], pad[1], v, _p(part), nparts, _p(addend), _stream(), **bkw)
+                              pad[0], pad[1], v, _p(part), nparts, _p(addend), _stream(), up=int(up), **bkw)
         if bkw:
             # the version pins the statistics to exactly this gradient: when y has several consumers,
             # autograd may accumulate the others' gradients into this tensor in place (bumping its
@@ -881,7 +899,15 @@ def _rel_err(a, b):
 
 
 _VENDOR = ('mm', 'miopen')
-_VENDOR_MARGIN = float(os.environ.get('MXAMD_VENDOR_MARGIN', '0.05'))
+# library candidates under other names: the split-K weight gradients are hipBLASLt batched GEMMs
+_VENDOR_PREFIX = ('splitk', 'blaslt')
+# near-ties go to the in-tree kernels: a library candidate must be this much faster to be picked
+# (8 %: on ResNet-50 b256 that moves five weight gradients in-tree for ~0.03 ms/step)
+_VENDOR_MARGIN = float(os.environ.get('MXAMD_VENDOR_MARGIN', '0.08'))
+
+
+def _is_vendor(name):
+    return name in _VENDOR or name.startswith(_VENDOR_PREFIX)
 _TUNE_ROUNDS = int(os.environ.get('MXAMD_TUNE_ROUNDS', '2'))
 
 
@@ -931,7 +957,7 @@ def _time_candidates(cands, reps=3, key=None, tol=2e-2):
             continue
         if key is not None:
             _TIMES.setdefault(key, {})[name] = t / reps
-        if name in _VENDOR:
+        if _is_vendor(name):
             t *= 1.0 + _VENDOR_MARGIN     # near-ties (within timing noise) go to the in-tree kernels
         if best_t is None or t < best_t:
             best, best_t = name, t
@@ -1246,6 +1272,10 @@ def _dgrad_candidates(dy, x, w, stride, pad):
             c.append(('phase%d' % bco, lambda bco=bco: conv_dgrad_strided(dy, w, stride, pad, x.shape, bco)))
     if halo_ok(dy, w, stride, pad) and tuple(dy.shape) == tuple(x.shape[:3]) + (K,):
         c.append(('halo', lambda: conv_halo(dy, _dgrad_weight(w))))
+    if conv_up2_ok(dy, w, stride, pad, x.shape):
+        for v, (bco, _bpix) in sorted(_BIG_VARIANTS.items()):
+            if C % bco == 0 and v not in _BIG_SKINNY:
+                c.append(('up%d' % v, lambda v=v: conv_dgrad_up2(dy, w, v)))
     c.append(('miopen', lambda: _conv_bwd_torch(dy, x, w, stride, pad, (True, False))[0]))
     return c
 
@@ -1319,6 +1349,10 @@ def _dgrad_bn_candidates(dy, x, w, stride, pad, bn_src):
                 fused.append(('hip%d+bn' % v, lambda v=v: conv_fwd(dy, _dgrad_weight(w), (1, 1),
                                                                    (R - 1 - pad[0], S - 1 - pad[1]), None, v,
                                                                    bn_bwd=bn_src)))
+    if conv_up2_ok(dy, w, stride, pad, x.shape):
+        for v, (bco, _bpix) in sorted(_BIG_VARIANTS.items()):
+            if C % bco == 0 and v not in _BIG_SKINNY:
+                fused.append(('up%d+bn' % v, lambda v=v: conv_dgrad_up2(dy, w, v, bn_bwd=bn_src)))
     if glds_bnb_ok(bn_src) and halo_ok(dy, w, stride, pad) and tuple(dy.shape) == tuple(x.shape[:3]) + (K,):
         fused.append(('halo+bn', lambda: conv_halo(dy, _dgrad_weight(w), bn_bwd=bn_src)))
     if glds_bnb_ok(bn_src):

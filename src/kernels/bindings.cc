@@ -65,7 +65,7 @@ void conv_nhwc_fwd_big(int dtype, const void* x, const void* w, const float* bia
                        int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int variant,
                        float* part, int nparts, const void* addend, hipStream_t s, const void* bn_z,
                        const float* bn_mean, const float* bn_scale, const float* bn_shift, const uint8_t* bn_mask,
-                       int bn_mode, float* bn_part, int bn_nparts);
+                       int bn_mode, float* bn_part, int bn_nparts, int up);
 int conv_nhwc_fwd_big_bwd_nparts(int N, int H, int W, int R, int S, int sh, int sw, int ph, int pw, int variant);
 void conv_nhwc_fwd_glds(int dtype, const void* x, const void* w, const float* bias, void* y, const void* zero, int N,
                         int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int bco,
@@ -512,17 +512,17 @@ PYBIND11_MODULE(_hip_kernels, m) {
                                 int H, int W, int C, int K, int R, int Sf, int sh, int sw, int ph, int pw, int variant,
                                 uintptr_t part, int nparts, uintptr_t addend, uintptr_t s, uintptr_t bz,
                                 uintptr_t bmean, uintptr_t bscale, uintptr_t bshift, uintptr_t bmask, int bmode,
-                                uintptr_t bpart, int bnparts) {
+                                uintptr_t bpart, int bnparts, int up) {
     conv_nhwc_fwd_big(dt, P<void>(x), P<void>(w), P<float>(bias), P<void>(y), P<void>(zero), N, H, W, C, K, R, Sf, sh,
                       sw, ph, pw, variant, P<float>(part), nparts, P<void>(addend), S(s), P<void>(bz), P<float>(bmean),
-                      P<float>(bscale), P<float>(bshift), P<uint8_t>(bmask), bmode, P<float>(bpart), bnparts);
+                      P<float>(bscale), P<float>(bshift), P<uint8_t>(bmask), bmode, P<float>(bpart), bnparts, up);
     check_launch("conv_nhwc_fwd_big");
   }, py::arg("dt"), py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("zero"), py::arg("N"),
      py::arg("H"), py::arg("W"), py::arg("C"), py::arg("K"), py::arg("R"), py::arg("S"), py::arg("sh"),
      py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("variant"), py::arg("part"), py::arg("nparts"),
      py::arg("addend"), py::arg("stream"), py::arg("bn_z") = 0, py::arg("bn_mean") = 0, py::arg("bn_scale") = 0,
      py::arg("bn_shift") = 0, py::arg("bn_mask") = 0, py::arg("bn_mode") = 0, py::arg("bn_part") = 0,
-     py::arg("bn_nparts") = 0);
+     py::arg("bn_nparts") = 0, py::arg("up") = 0);
   // persistent LDS-DMA ring kernel (conv_ring.hip): variant 0..5 = 128x128x4, 256x128x3, 128x256x3, 64x256x4,
   // 256x256x2, 64x128x4 (co x pix x stages); part as above
   m.def("conv_nhwc_fwd_ring_nparts", &conv_nhwc_fwd_ring_nparts);

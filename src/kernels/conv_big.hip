@@ -66,6 +66,10 @@ struct GeomB {
   int sh, sw, ph, pw;
   int M;     // N*Ho*Wo
   int Ktot;  // R*S*C
+  // up = 2: y is the 2x-upsampled, zero-filled image [N][2Ho][2Wo][K]: output pixel (n, ho, wo) lands at
+  // (n, 2ho, 2wo) and the epilogue writes zeros to its three other 2x2 siblings -- the data gradient of a
+  // 1x1 stride-2 convolution in one pass over dX (no memset, no scatter)
+  int up;
 };
 
 __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
@@ -353,12 +357,20 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * MI
   constexpr int D = ITERS < DMAX ? ITERS : DMAX;
   const T* zsrc_b = static_cast<const T*>(bf.z);
   uint4 ad_ring[D], z_ring[D];
+  auto out_pix = [&](int p) -> int64_t {
+    if (g.up != 2) return p;
+    const int n = p / (g.Ho * g.Wo);
+    const int rem = p - n * g.Ho * g.Wo;
+    const int ho = rem / g.Wo;
+    const int wo = rem - ho * g.Wo;
+    return ((int64_t)n * 2 * g.Ho + 2 * ho) * (2 * g.Wo) + 2 * wo;
+  };
   auto row_off = [&](int it, int64_t* off) -> bool {
     const int e = tid + it * 512;
     const int pl = e / CPR;
     const int c8 = e - pl * CPR;
     const int p = pix0 + pl;
-    *off = (int64_t)p * g.K + co0 + c8 * 8;
+    *off = out_pix(p < g.M ? p : 0) * g.K + co0 + c8 * 8;
     return p < g.M;
   };
 #pragma unroll
@@ -394,6 +406,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * MI
         for (int t = 0; t < 8; ++t) v.set(t, v.get(t) + a.get(t));
       }
       v.store(y + off);
+      if (g.up == 2) {
+        // the three zero siblings of this pixel in its 2x2 block of the upsampled image
+        const uint4 z4 = {0u, 0u, 0u, 0u};
+        const int64_t rowp = (int64_t)2 * g.Wo * g.K;
+        *reinterpret_cast<uint4*>(y + off + g.K) = z4;
+        *reinterpret_cast<uint4*>(y + off + rowp) = z4;
+        *reinterpret_cast<uint4*>(y + off + rowp + g.K) = z4;
+      }
       if (bnb) {
         Vec8<T> zv;
         zv.raw = z_cur;
@@ -528,7 +548,7 @@ void conv_nhwc_fwd_big(int dtype, const void* x, const void* w, const float* bia
                        int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int variant,
                        float* part, int nparts, const void* addend, hipStream_t s, const void* bn_z,
                        const float* bn_mean, const float* bn_scale, const float* bn_shift, const uint8_t* bn_mask,
-                       int bn_mode, float* bn_part, int bn_nparts) {
+                       int bn_mode, float* bn_part, int bn_nparts, int up) {
   GeomB g;
   g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S;
   g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw;
@@ -536,9 +556,12 @@ void conv_nhwc_fwd_big(int dtype, const void* x, const void* w, const float* bia
   g.Wo = (W + 2 * pw - S) / sw + 1;
   g.M = N * g.Ho * g.Wo;
   g.Ktot = R * S * C;
+  g.up = up;
   int bco, bpix;
   big_tile(variant, &bco, &bpix);
   MXAMD_HOST_CHECK(C % 64 == 0 && K % bco == 0, "conv_nhwc_fwd_big: need Cin % 64 == 0 and Cout % BCO == 0");
+  MXAMD_HOST_CHECK(up == 0 || (up == 2 && addend == nullptr && (int64_t)g.M * 4 * K < (1ll << 31)),
+                   "conv_nhwc_fwd_big: the 2x upsampled output takes no addend and must fit 32-bit indexing");
   MXAMD_HOST_CHECK((int64_t)N * H * W * C < (1ll << 31) && (int64_t)g.M * K < (1ll << 31) &&
                        (int64_t)K * g.Ktot < (1ll << 31),
                    "conv_nhwc_fwd_big: tensor too large for 32-bit indexing");

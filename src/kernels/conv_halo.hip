@@ -95,6 +95,7 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(const T* __restrict__
   char* const wbuf = smem;
   char* const pbuf0 = smem + kWBytes;
   char* const zrow = pbuf0 + 2 * patch_bytes;      // 128 B of zeros: halo columns, columns >= W
+  float* const bnc = reinterpret_cast<float*>(zrow + 128);   // BN-backward: mean / scale / shift [3][64]
 
   const int grid = gridDim.x;
   const int g0 = blockIdx.x;
@@ -123,6 +124,11 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(const T* __restrict__
   if (my_tiles == 0) return;
   // ---- prologue: zero row, resident weights (576 rows: 72 DMA groups, 9 per wave), first patch
   if (tid < 8) *reinterpret_cast<hu32x4*>(zrow + tid * 16) = hu32x4{0u, 0u, 0u, 0u};
+  if (STATS == 2 && tid < 64) {
+    bnc[tid] = bb.mean[tid];
+    bnc[64 + tid] = bb.mode == 2 ? bb.scale[tid] : 0.f;
+    bnc[128 + tid] = bb.mode == 2 ? bb.shift[tid] : 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
     const int gi = i * 8 + wid;
@@ -161,25 +167,32 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(const T* __restrict__
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int t = 0; t < 4; ++t) s1[i][t] = s2[i][t] = 0.f;
-  float bmean[4][4], bsc[4][4], bsh[4][4];
-  if (STATS == 2) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int c = i * 16 + fc * 4 + t;
-        bmean[i][t] = bb.mean[c];
-        bsc[i][t] = bb.mode == 2 ? bb.scale[c] : 0.f;
-        bsh[i][t] = bb.mode == 2 ? bb.shift[c] : 0.f;
-      }
-  }
-  // VM ops per wave of one epilogue: 8 stores (+ 8 z loads for the BN-backward statistics)
-  constexpr int EPI_OPS = STATS == 2 ? 16 : 8;
+  // VM ops per wave issued after the next patch's DMA: the 8 epilogue stores (the BN-backward z
+  // rows of a tile are loaded BEFORE that DMA, under the tile's MFMAs)
+  constexpr int EPI_OPS = 8;
 
   for (int it = 0; it < my_tiles; ++it) {
     const int t = g0 + it * grid;
     const int b = it & 1;
     const bool more = it + 1 < my_tiles;
+    const int n = t / g.tiles_per_img;
+    const int h0 = (t - n * g.tiles_per_img) * kTH;
+    hu32x2 zv[2][4];
+    if (STATS == 2) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int q = wid * 32 + j * 16 + fr;
+        const int hr = q >> 6, wc = q & 63;
+        const int h = h0 + hr;
+        const bool ok = wc < W && h < g.H;
+        const uint32_t pix = static_cast<uint32_t>((n * g.H + h) * W + wc);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t off = ok ? (pix * 64u + static_cast<uint32_t>(i * 16 + fc * 4)) * sizeof(T) : kOOB;
+          zv[j][i] = __builtin_amdgcn_raw_buffer_load_b64(zrs, off, 0, 0);
+        }
+      }
+    }
     if (more) issue_patch(t + grid, b ^ 1);
     const char* pb = pbuf0 + b * patch_bytes;
 
@@ -223,8 +236,6 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(const T* __restrict__
     }
 
     // ---- epilogue: 8 buffer stores per lane (out-of-range pixels dropped), statistics in registers
-    const int n = t / g.tiles_per_img;
-    const int h0 = (t - n * g.tiles_per_img) * kTH;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int q = wid * 32 + j * 16 + fr;
@@ -232,14 +243,6 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(const T* __restrict__
       const int h = h0 + hr;
       const bool ok = wc < W && h < g.H;
       const uint32_t pix = static_cast<uint32_t>((n * g.H + h) * W + wc);
-      hu32x2 zv[4];
-      if (STATS == 2) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t off = ok ? (pix * 64u + static_cast<uint32_t>(i * 16 + fc * 4)) * sizeof(T) : kOOB;
-          zv[i] = __builtin_amdgcn_raw_buffer_load_b64(zrs, off, 0, 0);
-        }
-      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t off = ok ? (pix * 64u + static_cast<uint32_t>(i * 16 + fc * 4)) * sizeof(T) : kOOB;
@@ -256,15 +259,16 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(const T* __restrict__
         if (STATS == 2 && ok) {
           // the statistics use the rounded gradient, as the BatchNorm backward reads it
           const float4 dv = mfma::Op<T>::unpack4(pk);
-          const float4 zf = mfma::Op<T>::unpack4(uint2{zv[i][0], zv[i][1]});
+          const float4 zf = mfma::Op<T>::unpack4(uint2{zv[j][i][0], zv[j][i][1]});
           const float dvs[4] = {dv.x, dv.y, dv.z, dv.w};
           const float zfs[4] = {zf.x, zf.y, zf.z, zf.w};
+          const int c0 = i * 16 + fc * 4;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const bool keep = bb.mode == 2 ? fmaf(zfs[e], bsc[i][e], bsh[i][e]) > 0.f : true;
+            const bool keep = bb.mode == 2 ? fmaf(zfs[e], bnc[64 + c0 + e], bnc[128 + c0 + e]) > 0.f : true;
             const float dz = keep ? dvs[e] : 0.f;
             s1[i][e] += dz;
-            s2[i][e] += dz * (zfs[e] - bmean[i][e]);
+            s2[i][e] += dz * (zfs[e] - bnc[c0 + e]);
           }
         }
       }
@@ -306,7 +310,7 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(const T* __restrict__
   }
 }
 
-int halo_smem_bytes(int W) { return kWBytes + 2 * (((kTH + 2) * W + 7) / 8 * 1024) + 128; }
+int halo_smem_bytes(int W) { return kWBytes + 2 * (((kTH + 2) * W + 7) / 8 * 1024) + 128 + 3 * 64 * 4; }
 
 template <typename T, int STATS>
 void launch_halo(const void* x, const void* w, void* y, const void* zero, const HaloGeom& g, int grid, float* part,
