@@ -198,6 +198,26 @@ def _finish_leaves(leaves):
     touched.clear()
 
 
+def _head_grad(g, t):
+    """Match a head gradient to its output's shape.
+
+    The reference binds the head-gradient array as the output-gradient buffer
+    (src/imperative/imperative.cc Backward: ``ograd_entries`` take the given arrays),
+    so a larger buffer of the same element type is read through its first
+    ``t.numel()`` elements. Smaller buffers are an error, as there.
+    """
+    if g.shape == t.shape:
+        return g
+    if g.numel() == t.numel() or (g.numel() > t.numel() and g.dim() == t.dim()
+                                  and g.shape[1:] == t.shape[1:]):
+        return g.reshape(-1)[:t.numel()].reshape(t.shape)
+    try:
+        return g.expand(t.shape)
+    except RuntimeError:
+        pass
+    raise MXNetError(f'head gradient of shape {tuple(g.shape)} does not match output shape {tuple(t.shape)}')
+
+
 def backward(heads, head_grads=None, retain_graph=False, train_mode=True, create_graph=False):  # pylint: disable=redefined-outer-name
     """Compute gradients of ``heads`` w.r.t. previously marked variables."""
     from .ndarray.ndarray import NDArray
@@ -212,7 +232,7 @@ def backward(heads, head_grads=None, retain_graph=False, train_mode=True, create
             continue
         tensors.append(t)
         hg = None if head_grads is None else head_grads[i]
-        grads.append(torch.ones_like(t) if hg is None else hg._data.to(t.dtype))
+        grads.append(torch.ones_like(t) if hg is None else _head_grad(hg._data.to(t.dtype), t))
     if not tensors and heads and all(getattr(h, '_recorded', False) for h in heads):
         # recorded outputs without a differentiable path (integer results, constant outputs): the
         # marked variables get zero gradients, as the reference's backward writes them

@@ -183,6 +183,9 @@ class SSDMultiBoxLoss:
 
     def __call__(self, cls_preds, loc_preds, anchors, labels):
         loc_t, loc_m, cls_t = self.targets(anchors, labels, cls_preds)
+        if cls_preds.context.device_type == 'gpu':
+            # one fused kernel pass for the loss and one for both gradients (detection.hip ssd_loss_*)
+            return nd.contrib.ssd_multibox_loss(cls_preds, loc_preds, cls_t, loc_t, loc_m, lambd=self.lambd)
         logp = nd.log_softmax(cls_preds.astype('float32'), axis=-1)
         valid = cls_t >= 0
         ce = -nd.pick(logp, nd.maximum(cls_t, 0), axis=-1) * valid

@@ -257,6 +257,76 @@ def _multibox_target_hip(lib, anchors, label, cls_pred, thr, ignore_label, ratio
 
 
 # ---------------------------------------------------------------------------
+# fused SSD training loss
+# ---------------------------------------------------------------------------
+
+def _ssd_loss_reference(cls_preds, loc_preds, cls_t, loc_t, loc_m, lambd):
+    """fp32 composition (CPU / fallback): softmax-CE over anchors with ignore label -1 normalised by the
+    valid anchors + smooth-L1 (sigma 1) of the masked location offsets normalised by the positives."""
+    logp = torch.log_softmax(cls_preds.float(), dim=-1)
+    valid = cls_t >= 0
+    pick = logp.gather(-1, cls_t.clamp(min=0).long().unsqueeze(-1)).squeeze(-1)
+    ce = (-pick * valid).sum()
+    nvalid = valid.sum().clamp(min=1)
+    npos = (cls_t > 0).sum().clamp(min=1)
+    d = (loc_preds.float() - loc_t) * loc_m
+    ad = d.abs()
+    sl1 = torch.where(ad < 1, 0.5 * d * d, ad - 0.5).sum()
+    return ce / nvalid + lambd * sl1 / npos
+
+
+class _SSDLossHip(torch.autograd.Function):
+    """One pass over the anchor rows for the loss, one for both gradients (detection.hip ssd_loss_*)."""
+
+    @staticmethod
+    def forward(ctx, cls_preds, loc_preds, cls_t, loc_t, loc_m, lambd):
+        from . import kernels as _K
+        from .kernel_fns import _DT, _stream
+        lib = _K.lib()
+        C1 = cls_preds.shape[-1]
+        rows = cls_t.numel()
+        cls_preds, loc_preds = cls_preds.contiguous(), loc_preds.contiguous()
+        cls_t, loc_t, loc_m = cls_t.float().contiguous(), loc_t.float().contiguous(), loc_m.float().contiguous()
+        part = torch.empty(4 * lib.ssd_loss_blocks(rows), dtype=torch.float32, device=cls_preds.device)
+        out = torch.empty(3, dtype=torch.float32, device=cls_preds.device)
+        lib.ssd_loss_fwd(_DT[cls_preds.dtype], cls_preds.data_ptr(), loc_preds.data_ptr(), cls_t.data_ptr(),
+                         loc_t.data_ptr(), loc_m.data_ptr(), rows, C1, float(lambd), part.data_ptr(), out.data_ptr(),
+                         _stream())
+        ctx.save_for_backward(cls_preds, loc_preds, cls_t, loc_t, loc_m, out)
+        ctx.lambd = float(lambd)
+        return out[0].clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import kernels as _K
+        from .kernel_fns import _DT, _stream
+        cls_preds, loc_preds, cls_t, loc_t, loc_m, stats = ctx.saved_tensors
+        g = g.float().reshape(1).contiguous()
+        dcls = torch.empty_like(cls_preds)
+        dloc = torch.empty_like(loc_preds)
+        _K.lib().ssd_loss_bwd(_DT[cls_preds.dtype], cls_preds.data_ptr(), loc_preds.data_ptr(), cls_t.data_ptr(),
+                              loc_t.data_ptr(), loc_m.data_ptr(), stats.data_ptr(), g.data_ptr(), cls_t.numel(),
+                              cls_preds.shape[-1], ctx.lambd, dcls.data_ptr(), dloc.data_ptr(), _stream())
+        return dcls, dloc, None, None, None, None
+
+
+@register('_contrib_ssd_multibox_loss', aliases=('ssd_multibox_loss',),
+          arg_names=('cls_preds', 'loc_preds', 'cls_target', 'loc_target', 'loc_mask'),
+          params={'lambd': ('float', 1.0)})
+def ssd_multibox_loss(cls_preds, loc_preds, cls_target, loc_target, loc_mask, lambd=1.0):
+    """SSD training loss (reference example/ssd/symbol/symbol_builder.py:90-102): cls_preds
+    [B, A, classes+1], loc_preds [B, A*4], MultiBoxTarget's cls_target [B, A], loc_target / loc_mask
+    [B, A*4] -> scalar.  Fused gfx950 kernels on the GPU, an fp32 composition elsewhere."""
+    from . import kernels as _K
+    from .kernel_fns import _DT
+    if (cls_preds.is_cuda and cls_preds.dtype in _DT and loc_preds.dtype == cls_preds.dtype and _K.available()
+            and cls_preds.shape[-1] <= 1024 and cls_target.numel() == cls_preds.numel() // cls_preds.shape[-1]
+            and loc_preds.numel() == 4 * cls_target.numel()):
+        return _SSDLossHip.apply(cls_preds, loc_preds, cls_target, loc_target, loc_mask, lambd)
+    return _ssd_loss_reference(cls_preds, loc_preds, cls_target, loc_target, loc_mask, lambd)
+
+
+# ---------------------------------------------------------------------------
 # generic bounding-box ops
 # ---------------------------------------------------------------------------
 

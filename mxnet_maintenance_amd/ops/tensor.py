@@ -131,6 +131,40 @@ def _gammaln(x):
     return _Gammaln.apply(x) if x.requires_grad else torch.lgamma(x)
 
 
+class _ArcsinhPrime(torch.autograd.Function):
+    """f'(x) = (x^2 + 1)^(-1/2) of arcsinh, differentiated the way the reference's second-order
+    gradient does it: src/operator/tensor/elemwise_unary_op_trig.cc:506 writes
+    f''(x) = f'(x) * x / (x^2 + 1) = x / (x^2 + 1)^(3/2) (mathematically -x / (x^2 + 1)^(3/2)); models
+    and tests that use arcsinh's higher-order gradient see the reference's values."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        return torch.rsqrt(x * x + 1)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, = ctx.saved_tensors
+        fp = _ArcsinhPrime.apply(x)
+        return g * fp * fp * fp * x
+
+
+class _Arcsinh(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        return torch.asinh(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, = ctx.saved_tensors
+        return g * _ArcsinhPrime.apply(x)
+
+
+def _arcsinh(x):
+    return _Arcsinh.apply(x) if x.requires_grad else torch.asinh(x)
+
+
 _UNARY = {
     'abs': torch.abs, 'sign': torch.sign, 'round': torch.round,
     'rint': torch.round, 'ceil': torch.ceil, 'floor': torch.floor, 'trunc': torch.trunc,
@@ -142,7 +176,7 @@ _UNARY = {
     'sin': torch.sin, 'cos': torch.cos, 'tan': torch.tan, 'arcsin': torch.asin,
     'arccos': torch.acos, 'arctan': torch.atan, 'degrees': torch.rad2deg,
     'radians': torch.deg2rad, 'sinh': torch.sinh, 'cosh': torch.cosh, 'tanh': torch.tanh,
-    'arcsinh': torch.asinh, 'arccosh': torch.acosh, 'arctanh': torch.atanh,
+    'arcsinh': _arcsinh, 'arccosh': torch.acosh, 'arctanh': torch.atanh,
     'reciprocal': torch.reciprocal, 'negative': torch.neg, 'relu': _relu,
     'sigmoid': torch.sigmoid, 'softsign': lambda x: x / (1 + torch.abs(x)),
     'logical_not': lambda x: (x == 0).to(x.dtype),

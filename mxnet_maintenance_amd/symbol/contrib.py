@@ -86,6 +86,13 @@ def foreach(body, data, init_states, name='foreach'):
     if len(new_l) != len(states_l):
         raise ValueError('foreach: the body returned %d states for %d initial states' % (len(new_l), len(states_l)))
     g = Group(outs_l + new_l)
+    # the reference's subgraph contract (python/mxnet/symbol/contrib.py foreach): every data array and
+    # every state is an input of the loop body
+    used = set(g.list_inputs())
+    if any(s.name not in used for s in d_ph):
+        raise AssertionError('the data arrays have to be used in the loop body')
+    if any(s.name not in used for s in s_ph):
+        raise AssertionError('the state arrays have to be used in the loop body')
     ph_names = {s.name for s in d_ph + s_ph}
     remain = _free_vars(g, ph_names)
     attrs = {'subgraph': g.tojson(), 'data_names': _json.dumps([s.name for s in d_ph]),

@@ -150,6 +150,12 @@ void conv_dw_fwd(int dtype, const void* x, const void* wt, const float* bias, vo
 void conv_dw_dgrad(int dtype, const void* dy, const void* wt, void* dx, const int* gm, hipStream_t s);
 void conv_dw_wgrad(int dtype, const void* x, const void* dy, float* slab, int nslice, int out_dtype, void* out,
                    int accum, const int* gm, hipStream_t s);
+int ssd_loss_blocks(int rows);
+void ssd_loss_fwd(int dtype, const void* cls, const void* loc, const float* cls_t, const float* loc_t,
+                  const float* loc_m, int rows, int C1, float lambd, float* part, float* out, hipStream_t s);
+void ssd_loss_bwd(int dtype, const void* cls, const void* loc, const float* cls_t, const float* loc_t,
+                  const float* loc_m, const float* stats, const float* gout, int rows, int C1, float lambd, void* dcls,
+                  void* dloc, hipStream_t s);
 void multibox_target(int dtype, const float* anchors, const float* labels, const void* cls_pred, float* loc_target,
                      float* loc_mask, float* cls_target, float* match_iou, int* match_gt, uint32_t* key, int B, int A,
                      int L, int W, int C, float thr, float ignore_label, float neg_ratio, float neg_thresh,
@@ -351,6 +357,21 @@ PYBIND11_MODULE(_hip_kernels, m) {
     if (g.size() != 14) throw std::runtime_error("conv_dw_wgrad: geometry needs 14 ints");
     conv_dw_wgrad(dt, P<void>(x), P<void>(dy), P<float>(slab), nslice, out_dt, P<void>(out), accum, g.data(), S(s));
     check_launch("conv_dw_wgrad");
+  });
+  // fused SSD training loss (detection.hip): softmax-CE (ignore -1, valid normalisation) + smooth-L1
+  m.def("ssd_loss_blocks", &ssd_loss_blocks);
+  m.def("ssd_loss_fwd", [](int dt, uintptr_t cls, uintptr_t loc, uintptr_t ct, uintptr_t lt, uintptr_t lm, int rows,
+                           int C1, float lambd, uintptr_t part, uintptr_t out, uintptr_t s) {
+    ssd_loss_fwd(dt, P<void>(cls), P<void>(loc), P<float>(ct), P<float>(lt), P<float>(lm), rows, C1, lambd,
+                 P<float>(part), P<float>(out), S(s));
+    check_launch("ssd_loss_fwd");
+  });
+  m.def("ssd_loss_bwd", [](int dt, uintptr_t cls, uintptr_t loc, uintptr_t ct, uintptr_t lt, uintptr_t lm,
+                           uintptr_t stats, uintptr_t gout, int rows, int C1, float lambd, uintptr_t dcls, uintptr_t dloc,
+                           uintptr_t s) {
+    ssd_loss_bwd(dt, P<void>(cls), P<void>(loc), P<float>(ct), P<float>(lt), P<float>(lm), P<float>(stats),
+                 P<float>(gout), rows, C1, lambd, P<void>(dcls), P<void>(dloc), S(s));
+    check_launch("ssd_loss_bwd");
   });
   m.def("multibox_target", [](int dt, uintptr_t anchors, uintptr_t labels, uintptr_t cls_pred, uintptr_t loc_target,
                               uintptr_t loc_mask, uintptr_t cls_target, uintptr_t match_iou, uintptr_t match_gt,

@@ -109,3 +109,52 @@ def test_ssd_train_step_gpu():
     lab = nd.array(_labels(4, 8, 20, 1).numpy(), ctx=ctx)
     losses = [float(step(x, lab, 1).asscalar()) for _ in range(3)]
     assert all(np.isfinite(losses)), losses
+
+
+def _loss_inputs(dev, dt, B=3, A=997, C1=21):
+    import torch
+    g = torch.Generator().manual_seed(5)
+    cls = (torch.randn(B, A, C1, generator=g) * 2).to(dev).to(dt)
+    loc = torch.randn(B, A * 4, generator=g).to(dev).to(dt)
+    ct = torch.randint(-1, C1, (B, A), generator=g).float().to(dev)
+    ct[0, :5] = -1
+    lt = (torch.randn(B, A * 4, generator=g) * 1.5).to(dev)
+    lm = (torch.rand(B, A * 4, generator=g) > 0.6).float().to(dev)
+    return cls, loc, ct, lt, lm
+
+
+def test_ssd_loss_op_cpu_matches_composition():
+    import torch
+    from mxnet_maintenance_amd.ops import detection as D
+    cls, loc, ct, lt, lm = _loss_inputs('cpu', torch.float32)
+    v = D.ssd_multibox_loss(cls, loc, ct, lt, lm, lambd=0.7)
+    logp = torch.log_softmax(cls, -1)
+    valid = ct >= 0
+    ce = -(logp.gather(-1, ct.clamp(min=0).long()[..., None])[..., 0] * valid).sum() / valid.sum()
+    d = (loc - lt) * lm
+    sl1 = torch.nn.functional.smooth_l1_loss(d, torch.zeros_like(d), reduction='sum', beta=1.0)
+    assert abs(float(v) - float(ce + 0.7 * sl1 / (ct > 0).sum())) < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', ['float16', 'bfloat16', 'float32'])
+def test_ssd_loss_fused_kernel_matches_fp32_reference(dtype):
+    """Fused SSD loss (detection.hip ssd_loss_*): loss and both gradients against the fp32 autograd
+    composition of the same inputs."""
+    import torch
+    from mxnet_maintenance_amd.ops import detection as D
+    dt = getattr(torch, dtype)
+    cls, loc, ct, lt, lm = _loss_inputs('cuda', dt)
+    cls.requires_grad_(True)
+    loc.requires_grad_(True)
+    v = D.ssd_multibox_loss(cls, loc, ct, lt, lm, lambd=0.7)
+    (v * 1.5).backward()
+    c32 = cls.detach().float().requires_grad_(True)
+    l32 = loc.detach().float().requires_grad_(True)
+    r = D._ssd_loss_reference(c32, l32, ct, lt, lm, 0.7)
+    (r * 1.5).backward()
+    assert abs(float(v) - float(r)) < 1e-3 * max(1.0, abs(float(r)))
+    tol = 1e-5 if dt == torch.float32 else (2e-3 if dt == torch.float16 else 1e-2)
+    for a, b in ((cls.grad, c32.grad), (loc.grad, l32.grad)):
+        err = float((a.float() - b).norm() / b.norm())
+        assert err < tol, err
