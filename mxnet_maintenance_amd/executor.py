@@ -571,7 +571,7 @@ class Executor:
         cached = getattr(self, '_stype_cache', False)
         if cached is not False:
             return cached
-        from .ndarray.register import _kept_stype
+        from .ndarray.register import _kept_stype, _check_storage
         args = dict(zip(self._symbol.list_arguments(), self.arg_arrays))
         if all(getattr(a, 'stype', 'default') == 'default' for a in args.values()):
             self._stype_cache = None
@@ -589,6 +589,7 @@ class Executor:
                 continue
             ins = [memo.get((id(i), j), 'default') for i, j in n.inputs]
             attrs = registry_parse(n)
+            _check_storage(n.op, ins, attrs)
             st = _binary_stype(n.op, ins)
             if st is None:
                 st = _kept_stype(n.op, [_S(t) for t in ins], attrs) if ins else None

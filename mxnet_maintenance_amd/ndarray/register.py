@@ -213,6 +213,8 @@ def invoke(op, inputs, attrs, out=None):
     _note_leaves(inputs)
     if _amp.active:
         tin = _amp.cast_inputs(op.name, tin, attrs)
+    if op.name in _BN_OPS:
+        _check_storage(op.name, [getattr(x, 'stype', 'default') for x in inputs], attrs)
     box = _failed_input(inputs)
     sampler = _is_sampler(op.name)
     if sampler and box is None:
@@ -314,6 +316,18 @@ _ZERO_PRESERVING = frozenset((
     'abs', 'sign', 'round', 'rint', 'ceil', 'floor', 'trunc', 'fix', 'square', 'sqrt', 'sin', 'tan',
     'arcsin', 'arctan', 'sinh', 'tanh', 'arcsinh', 'arctanh', 'expm1', 'log1p', 'relu', 'negative',
     'degrees', 'radians', '_copy', 'identity', 'cbrt', 'Cast', 'cast', 'stop_gradient', 'BlockGrad'))
+
+
+_BN_OPS = ('BatchNorm', 'BatchNorm_v1', 'CuDNNBatchNorm', '_contrib_BatchNormWithReLU', 'BatchNormWithReLU')
+
+
+def _check_storage(name, stypes, attrs):
+    """Storage combinations an operator rejects at storage inference (reference:
+    src/operator/nn/batch_norm.cc:528, BatchNormStorageType: ``fix_gamma`` with sparse inputs)."""
+    if name in _BN_OPS and any(s != 'default' for s in stypes):
+        fg = attrs.get('fix_gamma', True)
+        if fg if isinstance(fg, bool) else str(fg) in ('True', 'true', '1'):
+            raise MXNetError('fix_gamma=True is not supported for sparse ndarrays. Tracked at #11647')
 
 
 def _kept_stype(name, inputs, attrs):

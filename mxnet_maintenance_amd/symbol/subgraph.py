@@ -262,6 +262,28 @@ def _prog(subgraph):
     return p
 
 
+def user_attrs(attrs):
+    """Attributes of a ``_CachedOp`` built by hand from any symbol's JSON (reference
+    tests/python/unittest/test_subgraph.py:27: ``mx.sym._internal._CachedOp(*args, subgraph=js)``):
+    the positional inputs follow the subgraph's ``list_inputs()``; its variables are renamed
+    ``data<i>`` in that order and the auxiliary positions recorded, as a partitioned group's are."""
+    from .symbol import load_json
+    g = json.loads(attrs['subgraph'])
+    sym = load_json(attrs['subgraph'])
+    inputs = sym.list_inputs()
+    aux = set(sym.list_auxiliary_states())
+    idx = {n: i for i, n in enumerate(inputs)}
+    for nd in g['nodes']:
+        if nd['op'] == 'null' and nd['name'] in idx:
+            nd['name'] = 'data%d' % idx[nd['name']]
+    out = dict(attrs)
+    out['num_inputs'] = len(inputs)
+    out['num_outputs'] = len(sym.list_outputs())
+    out['aux_indices'] = ','.join(str(i) for i, n in enumerate(inputs) if n in aux)
+    out['subgraph'] = json.dumps(g)
+    return out
+
+
 def _cached_args(a):
     n = int(a.get('num_inputs', 0))
     aux = {int(x) for x in str(a.get('aux_indices', '') or '').split(',') if x != ''}

@@ -651,6 +651,9 @@ _NP_METHODS = frozenset(('max', 'min', 'sum', 'mean', 'prod', 'std', 'var', 'arg
 def _create(op_name, inputs, attrs, name=None, attr=None):
     """Create a Symbol applying ``op_name`` to input Symbols (missing args become variables)."""
     op = registry.get(op_name)
+    if op.name == '_CachedOp' and attrs.get('subgraph') and 'num_inputs' not in attrs:
+        from .subgraph import user_attrs
+        attrs = user_attrs(attrs)
     # the default node name follows the name the operator was called by (an alias such as flip
     # names its node flip0, as the reference's generated functions do)
     hint = (op_name if op_name.lower().lstrip('_') else op.name).lower()

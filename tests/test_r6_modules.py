@@ -78,3 +78,21 @@ def test_calibrate_entropy_op():
     h2[990:1011] = 100.0
     th2, _ = mx.nd.contrib.calibrate_entropy(mx.nd.array(h2), mx.nd.array(e.astype(np.float32)))
     assert float(th2.asnumpy()[0]) < 1.5
+
+
+def test_user_cached_op_subgraph_matches_graph():
+    """A ``_CachedOp`` built from any symbol's JSON runs that symbol on its positional inputs."""
+    a, b = mx.sym.Variable('a'), mx.sym.Variable('b')
+    c = a * b + a
+    y = mx.sym._internal._CachedOp(mx.sym.Variable('a'), mx.sym.Variable('b'), subgraph=c.tojson()) * 2
+    av, bv = mx.nd.array(np.random.rand(3, 4)), mx.nd.array(np.random.rand(3, 4))
+    out = y.bind(mx.cpu(), {'a': av, 'b': bv}).forward()[0].asnumpy()
+    np.testing.assert_allclose(out, 2 * (av.asnumpy() * bv.asnumpy() + av.asnumpy()), rtol=1e-6)
+
+
+def test_batchnorm_fix_gamma_rejects_sparse():
+    x = mx.nd.array(np.random.rand(2, 3)).tostype('row_sparse')
+    g, bt = mx.nd.ones((3,)), mx.nd.zeros((3,))
+    with pytest.raises(mx.base.MXNetError):
+        mx.nd.BatchNorm(x, g, bt, mx.nd.zeros((3,)), mx.nd.ones((3,)), fix_gamma=True)
+    mx.nd.BatchNorm(x, g, bt, mx.nd.zeros((3,)), mx.nd.ones((3,)), fix_gamma=False)
