@@ -3,9 +3,15 @@
 Parity: src/operator/contrib/deformable_convolution*, modulated_deformable_convolution*,
 sync_batch_norm*.  On the GPU deformable convolution runs the in-tree gfx950 kernels of
 src/kernels/deform_conv.hip: a deformable im2col (bilinear sampling at the offset taps, mask
-applied) feeding one batched grouped GEMM, and for the backward col2im (data gradient, fp32
-atomics) + col2im_coord (offset / mask gradients, register reductions) around the transposed
-GEMMs.  On the CPU the same math is one ``grid_sample`` per kernel tap (bilinear, zero outside)
+applied) writing one K-contiguous column row per output pixel, contracted on the matrix cores by
+the in-tree GEMMs (reference: deformable_convolution-inl.h:150-159 -- im2col + linalg_gemm per
+group):
+  forward      out[N*L, O]   = cols[N*L, C*K] . W[O, C*K]^T (+ bias)  gemm.hip NT, bias in the epilogue
+  weight grad  dW[O, C*K]    = dout^T . cols                          conv_wgrad.hip TN (fp32 slabs)
+  column grad  dcols[N*L,C*K] = dout . W  (fp32 out)                  gemm.hip NT on W^T
+the output stays NHWC in memory (an NCHW view), and the backward runs col2im (data gradient, fp32
+atomics) + col2im_coord (offset / mask gradients, register reductions) on the fp32 column
+gradient.  fp32 operands keep the plane layout contracted by torch.matmul.  On the CPU the same math is one ``grid_sample`` per kernel tap (bilinear, zero outside)
 followed by the grouped GEMM, differentiated by autograd.
 """
 import torch
@@ -98,6 +104,168 @@ class _DeformConvHip(torch.autograd.Function):
         return gx32.to(x.dtype), goff, gmask, gw.reshape(weight.shape).to(weight.dtype), None, None
 
 
+DISPATCH = {'gemm': 0, 'plane': 0}
+
+
+def _pick(key, cands, fallback):
+    """Autotuned in-tree GEMM candidate for ``key``; ``fallback`` (torch) when none tiles the shape."""
+    from .kernel_fns import _select
+    if not cands:
+        from .rnn_fns import _require_hip
+        if _require_hip():
+            from ..base import MXNetError
+            raise MXNetError('deformable convolution: %r does not tile for the in-tree GEMM kernels' % (key,))
+        return fallback()
+    return _select(key, cands, cands[0][0])
+
+
+def _pixel_rows(t):
+    """[N, F, Ho, Wo] (NCHW-shaped) -> ([N, Ho, Wo, F] view with unit feature stride, row stride):
+    free for channels-last memory, including a channel slice of a wider buffer (the output-channel
+    padded offset conv), one copy otherwise."""
+    v = t.permute(0, 2, 3, 1)
+    N, Ho, Wo, F = v.shape
+    ld = v.stride(2)
+    if not (v.stride(3) == 1 and ld >= F and v.stride(1) == Wo * ld and v.stride(0) == Ho * Wo * ld
+            and v.data_ptr() % 16 == 0):
+        v = v.contiguous()
+        ld = F
+    return v, ld
+
+
+def _nhwc_ok(x, weight, dg, kernel):
+    C = x.shape[1]
+    return (C // dg) % 64 == 0 and kernel[0] * kernel[1] <= 16
+
+
+class _DeformConvRows(torch.autograd.Function):
+    """Deformable conv (f16/bf16) with row columns [N*L, C*K] on the in-tree MFMA GEMMs.  Channels-last
+    (``nhwc``): image, offsets, mask and all their gradients in [N, H, W, C] memory, the sampling and the
+    fused backward (data + offset + mask gradients in one pass) one wave per output pixel."""
+
+    @staticmethod
+    def forward(ctx, x, offset, mask, weight, bias, geom, num_group):
+        from . import kernels as _K
+        from . import gemm as G
+        from .kernel_fns import _DT, _stream
+        lib = _K.lib()
+        N, C, H, W = x.shape
+        O = weight.shape[0]
+        Ho, Wo = geom[4], geom[5]
+        K = geom[6] * geom[7]
+        L = Ho * Wo
+        nhwc = _nhwc_ok(x, weight, geom[14], (geom[6], geom[7]))
+        cols = torch.empty((N * L, C * K), dtype=x.dtype, device=x.device)
+        if nhwc:
+            x = x.permute(0, 2, 3, 1).contiguous()                  # free for channels-last activations
+            offset, ld_off = _pixel_rows(offset)
+            mask, ld_msk = _pixel_rows(mask) if mask is not None else (None, 0)
+            lib.deform_im2col_nhwc(_DT[x.dtype], x.data_ptr(), offset.data_ptr(),
+                                   0 if mask is None else mask.data_ptr(), cols.data_ptr(), list(geom), ld_off,
+                                   ld_msk, _stream())
+            ctx.ld = (ld_off, ld_msk)
+        else:
+            x, offset = x.contiguous(), offset.contiguous()
+            mask = mask.contiguous() if mask is not None else None
+            lib.deform_im2col(_DT[x.dtype], x.data_ptr(), offset.data_ptr(), 0 if mask is None else mask.data_ptr(),
+                              cols.data_ptr(), list(geom) + [1], _stream())
+        ctx.nhwc = nhwc
+        g = num_group
+        cg, og = (C // g) * K, O // g
+        wmat = weight.reshape(O, cg).contiguous()
+        b32 = None if bias is None else bias.float().contiguous()
+        out = torch.empty((N * L, O), dtype=x.dtype, device=x.device)
+        for gi in range(g):
+            a = cols[:, gi * cg:(gi + 1) * cg]
+            b = wmat[gi * og:(gi + 1) * og]
+            bb = None if b32 is None else b32[gi * og:(gi + 1) * og]
+            o = out[:, gi * og:(gi + 1) * og]
+            cands = [(n, (lambda c=c: G.gemm_nt(a, b, bias=bb, out=o, cfg=c)))
+                     for n, c in ((n, G.parse_name(n)) for n, _ in G.candidates(a, b))
+                     if g == 1 or c[1] == 1]
+            _pick(('deform_fwd', tuple(a.shape), tuple(b.shape), x.dtype, bb is not None), cands,
+                  lambda: o.copy_(torch.addmm(bb.to(x.dtype), a, b.t()) if bb is not None else a @ b.t()))
+        DISPATCH['gemm'] += 1
+        ctx.save_for_backward(x, offset, mask, wmat, cols)
+        ctx.geom, ctx.g, ctx.has_bias = geom, g, bias is not None
+        ctx.bdtype = None if bias is None else bias.dtype
+        ctx.wdtype = weight.dtype
+        return out.view(N, Ho, Wo, O).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, gout):
+        from . import kernels as _K
+        from . import gemm as G
+        from . import kernel_fns as KF
+        from .kernel_fns import _DT, _stream
+        lib = _K.lib()
+        x, offset, mask, wmat, cols = ctx.saved_tensors
+        geom, g = ctx.geom, ctx.g
+        N, C = geom[0], geom[1]
+        O = wmat.shape[0]
+        L = geom[4] * geom[5]
+        K = geom[6] * geom[7]
+        M = N * L
+        cg, og = (C // g) * K, O // g
+        go = gout.permute(0, 2, 3, 1).reshape(M, O).contiguous()
+        gw = torch.empty((O, cg), dtype=ctx.wdtype, device=x.device)
+        gcols = torch.empty((M, C * K), dtype=torch.float32, device=x.device)
+        for gi in range(g):
+            dy = go[:, gi * og:(gi + 1) * og]
+            xc = cols[:, gi * cg:(gi + 1) * cg]
+            # weight gradient: a 1x1-conv weight gradient over the M output pixels (TN, fp32 slabs);
+            # a group's column / gradient slices are made contiguous for it
+            xcc, dyc = (xc, dy) if g == 1 else (xc.contiguous(), dy.contiguous())
+            if KF.conv_wgrad_ok(xcc.view(1, 1, M, cg), torch.empty((og, 1, 1, cg), device='meta')):
+                KF.conv_wgrad(xcc.view(1, 1, M, cg), dyc.view(1, 1, M, og), (og, 1, 1, cg), (1, 1), (0, 0),
+                              out=gw[gi * og:(gi + 1) * og].view(og, 1, 1, cg))
+            else:
+                _pick(('deform_dw', tuple(dy.shape), tuple(xc.shape), x.dtype), [],
+                      lambda: gw[gi * og:(gi + 1) * og].copy_(dy.t() @ xc))
+            # column gradient in fp32 (the offset gradient is a difference of products)
+            wt = wmat[gi * og:(gi + 1) * og].t().contiguous()
+            o = gcols[:, gi * cg:(gi + 1) * cg]
+            cands = [(n, (lambda c=c: G.gemm_nt(dy, wt, out=o, out_f32=True, cfg=c)))
+                     for n, c in ((n, G.parse_name(n)) for n, _ in G.candidates(dy, wt, out_f32=True))
+                     if g == 1 or c[1] == 1]
+            _pick(('deform_dcols', tuple(dy.shape), tuple(wt.shape), x.dtype), cands,
+                  lambda: o.copy_(dy.float() @ wt.float().t()))
+        mptr = 0 if mask is None else mask.data_ptr()
+        if ctx.nhwc:
+            # x [N, H, W, C], offsets / mask pixel rows: one fused pass, gradients channels-last
+            gx32 = torch.zeros(x.shape, dtype=torch.float32, device=x.device)
+            dg = geom[14]
+            goff = torch.empty((N, geom[4], geom[5], 2 * K * dg), dtype=offset.dtype, device=x.device)
+            gmask = (torch.empty((N, geom[4], geom[5], K * dg), dtype=mask.dtype, device=x.device)
+                     if mask is not None else None)
+            lib.deform_bwd_nhwc(_DT[x.dtype], x.data_ptr(), offset.data_ptr(), mptr, gcols.data_ptr(),
+                                gx32.data_ptr(), goff.data_ptr(), 0 if gmask is None else gmask.data_ptr(),
+                                list(geom), ctx.ld[0], ctx.ld[1], _stream())
+            gx = gx32.to(x.dtype).permute(0, 3, 1, 2)
+            goff = goff.permute(0, 3, 1, 2)
+            gmask = gmask.permute(0, 3, 1, 2) if gmask is not None else None
+        else:
+            gx32 = torch.zeros(x.shape, dtype=torch.float32, device=x.device)
+            g16 = list(geom) + [1]
+            lib.deform_col2im(_DT[x.dtype], offset.data_ptr(), mptr, gcols.data_ptr(), gx32.data_ptr(), g16,
+                              _stream())
+            goff = torch.empty_like(offset)
+            gmask = torch.empty_like(mask) if mask is not None else None
+            lib.deform_col2im_coord(_DT[x.dtype], x.data_ptr(), offset.data_ptr(), mptr, gcols.data_ptr(),
+                                    goff.data_ptr(), 0 if gmask is None else gmask.data_ptr(), g16, _stream())
+            gx = gx32.to(x.dtype)
+        gb = go.float().sum(0).to(ctx.bdtype) if ctx.has_bias else None
+        return (gx, goff, gmask, gw.view(O, C // g, geom[6], geom[7]), gb, None, None)
+
+
+def _rows_ok(x, weight, num_group, kernel):
+    from . import gemm as G
+    C, O = x.shape[1], weight.shape[0]
+    K = kernel[0] * kernel[1]
+    cg, og = (C // num_group) * K, O // num_group
+    return (x.dtype in G._DT and cg % 64 == 0 and og % 64 == 0 and 64 * min(16, max(1, 512 // K)) * K * 2 <= 65536)
+
+
 def _deform_hip_ok(x, offset, mask, weight):
     from . import kernels as _K
     from .kernel_fns import _DT
@@ -116,6 +284,9 @@ def _deform_conv(x, offset, mask, weight, bias, kernel, stride, pad, dilate, num
         Ho, Wo = offset.shape[2], offset.shape[3]
         geom = (N, C, H, W, Ho, Wo, kernel[0], kernel[1], stride[0], stride[1], pad[0], pad[1], dilate[0],
                 dilate[1], dg)
+        if _rows_ok(x, weight, num_group, kernel):
+            return _DeformConvRows.apply(x, offset, mask, weight, bias, geom, num_group)
+        DISPATCH['plane'] += 1
         out = _DeformConvHip.apply(x, offset, mask, weight, geom, num_group)
         return out if bias is None else out + bias.view(1, -1, 1, 1).to(out.dtype)
     cols = _deform_columns(x, offset, mask, kernel, stride, pad, dilate, dg)

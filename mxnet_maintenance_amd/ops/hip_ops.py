@@ -111,8 +111,12 @@ def conv(data, weight, bias, stride, pad, dilate, groups, channel_last):
         xl = _as_nhwc_view(data)
         wl = _nhwc_weight(weight)
         if _K.conv_ok(xl, wl, stride, pad, dilate, groups):
+            if _K.kpad_ok(xl, wl):
+                return _K.conv_kpad(xl, wl, bias, stride, pad, dilate).permute(0, 3, 1, 2)
             return _K.ConvNHWC.apply(xl, wl, bias, tuple(stride), tuple(pad), tuple(dilate)).permute(0, 3, 1, 2)
     if channel_last and _use_hip(data) and _K.conv_ok(data, weight, stride, pad, dilate, groups):
+        if _K.kpad_ok(data, weight):
+            return _K.conv_kpad(data, weight, bias, stride, pad, dilate)
         return _K.ConvNHWC.apply(data, weight, bias, tuple(stride), tuple(pad), tuple(dilate))
     if _use_hip(data):
         # grouped / dilated / 1-D / 3-D / fp32 / odd channel counts: the general in-tree MFMA kernel

@@ -1663,13 +1663,33 @@ def conv_algo_times():
     return {k: dict(v) for k, v in _TIMES.items()}
 
 
+_KPAD = _os.environ.get('MXAMD_CONV_KPAD', '1') == '1'
+
+
+def kpad_ok(x, w):
+    """Output channels that do not tile the MFMA kernels (detection heads: anchors x (classes + 1),
+    deformable offsets: 2 x taps) with input channels that do."""
+    return _KPAD and w.shape[0] % 64 != 0 and w.shape[3] % 64 == 0 and w.shape[0] >= 8
+
+
+def conv_kpad(x, w, bias, stride, pad, dilate):
+    """NHWC conv with the output channels zero-padded to a multiple of 64, so the forward, data and
+    weight gradients run on the in-tree MFMA kernels instead of MIOpen; the result is the first
+    ``K`` channels (a strided view), the padding's gradients are dropped by autograd."""
+    K = w.shape[0]
+    Kp = (K + 63) // 64 * 64
+    wp = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, 0, 0, Kp - K))
+    bp = None if bias is None else torch.nn.functional.pad(bias, (0, Kp - K))
+    return ConvNHWC.apply(x, wp, bp, tuple(stride), tuple(pad), tuple(dilate))[..., :K]
+
+
 def conv_ok(x, w, stride, pad, dilate, groups):
     # any 2-D fp16/bf16 NHWC conv goes through ConvNHWC's algorithm selection
     return (len(stride) == 2 and x.dim() == 4 and groups == 1 and tuple(dilate) == (1, 1) and x.is_contiguous()
             and w.is_contiguous() and x.dtype in (torch.float16, torch.bfloat16) and w.dtype == x.dtype)
 
 
-__all__ += ['ConvNHWC', 'ConvTeeNHWC', 'conv_fwd', 'conv_ok_shape', 'conv_wgrad', 'conv_wgrad_ok', 'stem_ok',
+__all__ += ['ConvNHWC', 'ConvTeeNHWC', 'conv_kpad', 'kpad_ok', 'conv_fwd', 'conv_ok_shape', 'conv_wgrad', 'conv_wgrad_ok', 'stem_ok',
             'conv_stem_fwd', 'conv_stem_wgrad']
 
 

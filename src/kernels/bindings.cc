@@ -139,13 +139,17 @@ void pool_nhwc_backward(int dtype, int is_max, const void* dy, const uint8_t* ar
                         hipStream_t s);
 void deform_im2col(int dtype, const void* x, const void* off, const void* msk, void* cols, int N, int C, int H, int W,
                    int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int dg,
-                   hipStream_t s);
+                   int rows, hipStream_t s);
 void deform_col2im(int dtype, const void* off, const void* msk, const void* gcols, float* gx, int N, int C, int H,
                    int W, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int dg,
-                   hipStream_t s);
+                   int rows, hipStream_t s);
 void deform_col2im_coord(int dtype, const void* x, const void* off, const void* msk, const void* gcols, void* goff,
                          void* gmsk, int N, int C, int H, int W, int Ho, int Wo, int kh, int kw, int sh, int sw,
-                         int ph, int pw, int dh, int dw, int dg, hipStream_t s);
+                         int ph, int pw, int dh, int dw, int dg, int rows, hipStream_t s);
+void deform_im2col_nhwc(int dtype, const void* x, const void* off, const void* msk, void* cols, const int* g,
+                        int ld_off, int ld_msk, hipStream_t s);
+void deform_bwd_nhwc(int dtype, const void* x, const void* off, const void* msk, const void* gcols, float* gx,
+                     void* goff, void* gmsk, const int* g, int ld_off, int ld_msk, hipStream_t s);
 void conv_dw_fwd(int dtype, const void* x, const void* wt, const float* bias, void* y, const int* gm, hipStream_t s);
 void conv_dw_dgrad(int dtype, const void* dy, const void* wt, void* dx, const int* gm, hipStream_t s);
 void conv_dw_wgrad(int dtype, const void* x, const void* dy, float* slab, int nslice, int out_dtype, void* out,
@@ -317,28 +321,47 @@ PYBIND11_MODULE(_hip_kernels, m) {
     slab_reduce(odt, P<float>(slab), splits, n, P<void>(out), accum, S(s));
     check_launch("slab_reduce");
   });
-  // deformable convolution (NCHW): geometry g = [N, C, H, W, Ho, Wo, kh, kw, sh, sw, ph, pw, dh, dw, dg]
+  // deformable convolution (NCHW): geometry g = [N, C, H, W, Ho, Wo, kh, kw, sh, sw, ph, pw, dh, dw, dg(, rows)]
+  // rows = 1: columns [N*Ho*Wo][C*kh*kw] (the MFMA GEMM operand layout), else [N][C*kh*kw][Ho*Wo]
   m.def("deform_im2col", [](int dt, uintptr_t x, uintptr_t off, uintptr_t msk, uintptr_t cols, std::vector<int> g,
                             uintptr_t s) {
-    if (g.size() != 15) throw std::runtime_error("deform_im2col: geometry needs 15 ints");
+    if (g.size() != 15 && g.size() != 16) throw std::runtime_error("deform_im2col: geometry needs 15 or 16 ints");
+    const int rows = g.size() == 16 ? g[15] : 0;
     deform_im2col(dt, P<void>(x), P<void>(off), P<void>(msk), P<void>(cols), g[0], g[1], g[2], g[3], g[4], g[5], g[6],
-                  g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14], S(s));
+                  g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14], rows, S(s));
     check_launch("deform_im2col");
   });
   m.def("deform_col2im", [](int dt, uintptr_t off, uintptr_t msk, uintptr_t gcols, uintptr_t gx, std::vector<int> g,
                             uintptr_t s) {
-    if (g.size() != 15) throw std::runtime_error("deform_col2im: geometry needs 15 ints");
+    if (g.size() != 15 && g.size() != 16) throw std::runtime_error("deform_col2im: geometry needs 15 or 16 ints");
+    const int rows = g.size() == 16 ? g[15] : 0;
     deform_col2im(dt, P<void>(off), P<void>(msk), P<void>(gcols), P<float>(gx), g[0], g[1], g[2], g[3], g[4], g[5],
-                  g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14], S(s));
+                  g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14], rows, S(s));
     check_launch("deform_col2im");
   });
   m.def("deform_col2im_coord", [](int dt, uintptr_t x, uintptr_t off, uintptr_t msk, uintptr_t gcols, uintptr_t goff,
                                   uintptr_t gmsk, std::vector<int> g, uintptr_t s) {
-    if (g.size() != 15) throw std::runtime_error("deform_col2im_coord: geometry needs 15 ints");
+    if (g.size() != 15 && g.size() != 16) throw std::runtime_error("deform_col2im_coord: geometry needs 15 or 16 ints");
+    const int rows = g.size() == 16 ? g[15] : 0;
     deform_col2im_coord(dt, P<void>(x), P<void>(off), P<void>(msk), P<void>(gcols), P<void>(goff), P<void>(gmsk),
                         g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14],
-                        S(s));
+                        rows, S(s));
     check_launch("deform_col2im_coord");
+  });
+  // channels-last deformable conv (same 15-int geometry; x / offsets / mask / gradients NHWC, offsets and
+  // mask rows ld_off / ld_msk elements apart)
+  m.def("deform_im2col_nhwc", [](int dt, uintptr_t x, uintptr_t off, uintptr_t msk, uintptr_t cols, std::vector<int> g,
+                                 int ld_off, int ld_msk, uintptr_t s) {
+    if (g.size() != 15) throw std::runtime_error("deform_im2col_nhwc: geometry needs 15 ints");
+    deform_im2col_nhwc(dt, P<void>(x), P<void>(off), P<void>(msk), P<void>(cols), g.data(), ld_off, ld_msk, S(s));
+    check_launch("deform_im2col_nhwc");
+  });
+  m.def("deform_bwd_nhwc", [](int dt, uintptr_t x, uintptr_t off, uintptr_t msk, uintptr_t gcols, uintptr_t gx,
+                              uintptr_t goff, uintptr_t gmsk, std::vector<int> g, int ld_off, int ld_msk, uintptr_t s) {
+    if (g.size() != 15) throw std::runtime_error("deform_bwd_nhwc: geometry needs 15 ints");
+    deform_bwd_nhwc(dt, P<void>(x), P<void>(off), P<void>(msk), P<void>(gcols), P<float>(gx), P<void>(goff),
+                    P<void>(gmsk), g.data(), ld_off, ld_msk, S(s));
+    check_launch("deform_bwd_nhwc");
   });
   // depthwise NHWC conv; geometry g = [N, H, W, C, Ho, Wo, R, S, sh, sw, ph, pw, dh, dw]; wt = [R*S][C]
   m.def("conv_dw_fwd", [](int dt, uintptr_t x, uintptr_t wt, uintptr_t bias, uintptr_t y, std::vector<int> g,

@@ -71,3 +71,62 @@ def test_hip_kernels_match_fp32_reference(case, dtype):
     for name, a, b in zip(names, got, ref):
         err = (a - b).norm() / b.norm().clamp_min(1e-12)
         assert err < tol, (name, float(err))
+
+
+ROW_CASES = [
+    # shapes whose column width C/g*K and output channels O/g tile the in-tree MFMA GEMMs
+    (2, 64, 9, 11, 64, (3, 3), (1, 1), (1, 1), (1, 1), 1, 1, False),
+    (2, 128, 10, 10, 128, (3, 3), (2, 2), (1, 1), (1, 1), 2, 2, True),
+    (4, 256, 8, 8, 256, (3, 3), (2, 2), (1, 1), (1, 1), 1, 1, False),     # an SSD-512 extra layer
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', ROW_CASES)
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+def test_row_columns_on_intree_gemms_match_fp32_reference(case, dtype):
+    """f16/bf16 deformable conv on the row-column layout: im2col rows -> gemm.hip (forward, fp32
+    column gradient), conv_wgrad.hip (weight gradient) -- no torch GEMM (MXAMD_REQUIRE_HIP)."""
+    import os
+    from mxnet_maintenance_amd.ops import kernels
+    assert kernels.available(), kernels.load_error()
+    x, off, mask, w = _inputs(case)
+    off = off.floor() + 0.25 + 0.5 * (off - off.floor())
+    dev = [t.to('cuda', dtype) if t is not None else None for t in (x, off, mask, w)]
+    ref = _run(case, *(t.float().cpu() if t is not None else None for t in dev), grad_dtype=dtype)
+    before = C.DISPATCH['gemm']
+    os.environ['MXAMD_REQUIRE_HIP'] = '1'
+    try:
+        got = _run(case, *dev)
+    finally:
+        os.environ.pop('MXAMD_REQUIRE_HIP', None)
+    assert C.DISPATCH['gemm'] == before + 1
+    names = ['out', 'dx', 'doffset'] + (['dmask'] if mask is not None else []) + ['dweight']
+    for name, a, b in zip(names, got, ref):
+        err = (a - b).norm() / b.norm().clamp_min(1e-12)
+        assert err < 3e-2, (name, float(err))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('modulated', [False, True])
+def test_channels_last_inputs_and_strided_offsets(modulated):
+    """The channels-last path takes NHWC-memory activations and offsets that are a channel slice of a
+    wider buffer (the padded offset conv's output) without copies; gradients match the fp32 reference."""
+    from mxnet_maintenance_amd.ops import kernels
+    assert kernels.available(), kernels.load_error()
+    case = (2, 128, 10, 10, 128, (3, 3), (1, 1), (1, 1), (1, 1), 1, 1, modulated)
+    x, off, mask, w = _inputs(case)
+    off = off.floor() + 0.25 + 0.5 * (off - off.floor())
+    dt = torch.float16
+    xd = x.to('cuda', dt).permute(0, 2, 3, 1).contiguous().permute(0, 3, 1, 2)     # NHWC memory
+    wide = torch.zeros(off.shape[0], off.shape[2], off.shape[3], 64, dtype=dt, device='cuda')
+    wide[..., :off.shape[1]] = off.to('cuda', dt).permute(0, 2, 3, 1)
+    offd = wide[..., :off.shape[1]].permute(0, 3, 1, 2)                             # strided channel slice
+    maskd = mask.to('cuda', dt) if mask is not None else None
+    dev = [xd, offd, maskd, w.to('cuda', dt)]
+    ref = _run(case, *(t.float().cpu() if t is not None else None for t in dev), grad_dtype=dt)
+    got = _run(case, *[t.detach() if t is not None else None for t in dev])
+    names = ['out', 'dx', 'doffset'] + (['dmask'] if mask is not None else []) + ['dweight']
+    for name, a, b in zip(names, got, ref):
+        err = (a - b).norm() / b.norm().clamp_min(1e-12)
+        assert err < 3e-2, (name, float(err))

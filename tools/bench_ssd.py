@@ -125,6 +125,13 @@ def main():
                        'deformable_extras': bool(args.deformable),
                        'hip_graph': bool(use_graph and getattr(step, 'captured', False))},
         }), flush=True)
+    if os.environ.get('MXAMD_BENCH_VERBOSE', '0') == '1' and rank == 0:
+        # per-shape autotune winners and candidate times (conv, GEMM, deformable GEMM keys)
+        from mxnet_maintenance_amd.ops import kernel_fns
+        times = kernel_fns.conv_algo_times()
+        for k, v in sorted(kernel_fns.conv_algos().items(), key=str):
+            t = ' '.join('%s=%.3f' % (nm, ms) for nm, ms in sorted(times.get(k, {}).items(), key=lambda z: z[1]))
+            print('conv-algo', v, k, t, file=sys.stderr)
     if n > 1:
         torch.distributed.destroy_process_group()
 
