@@ -118,6 +118,14 @@ def conv(data, weight, bias, stride, pad, dilate, groups, channel_last):
         if _K.kpad_ok(data, weight):
             return _K.conv_kpad(data, weight, bias, stride, pad, dilate)
         return _K.ConvNHWC.apply(data, weight, bias, tuple(stride), tuple(pad), tuple(dilate))
+    if nsp == 2 and groups == 1 and _use_hip(data) and tuple(dilate) != (1, 1):
+        # dilated (atrous) 2-D convs: the big-tile / weight-gradient MFMA kernels with dilated taps
+        xl = data if channel_last else (_as_nhwc_view(data) if _nchw_on_hip(data) else None)
+        if xl is not None:
+            wl = weight if channel_last else _nhwc_weight(weight)
+            if _K.dil_ok(xl, wl, dilate):
+                y = _K.ConvDilNHWC.apply(xl, wl, bias, tuple(stride), tuple(pad), tuple(dilate))
+                return y if channel_last else y.permute(0, 3, 1, 2)
     if _use_hip(data):
         # grouped / dilated / 1-D / 3-D / fp32 / odd channel counts: the general in-tree MFMA kernel
         # (src/kernels/conv_gen.hip), chosen per shape against MIOpen by measured forward time

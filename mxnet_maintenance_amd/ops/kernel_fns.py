@@ -540,7 +540,7 @@ def conv_dgrad_up2(dy, w, variant, bn_bwd=None):
     return conv_fwd(dy.contiguous(), wt, (1, 1), (0, 0), None, variant, bn_bwd=bn_bwd, up=2)
 
 
-def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=None, bn_bwd=None, up=0):
+def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=None, bn_bwd=None, up=0, dil=(1, 1)):
     """y[N,Ho,Wo,K] = conv(x[N,H,W,C], w[K,R,S,C]) on the MFMA implicit-GEMM kernel.
 
     ``variant``: 0 = heuristic tile, 1..4 = (BCO, BK) in (128,64) (128,32) (64,64) (64,32),
@@ -551,11 +551,15 @@ def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=Non
     sum / sum-of-squares partials of y, attached to y as ``y._mxamd_bn_part``; ``addend`` (big kernel
     only, same shape/dtype as y): y = conv + addend.  ``bn_bwd`` (big kernel, or glds 5 / 6 when
     glds_bnb_ok; a BatchNorm's ``_mxamd_bn_src`` record): y is that BN's incoming gradient -- also emit
-    its backward statistics (sum dz, sum dz*(z-mean)), attached to y as ``y._mxamd_bn_bwd``."""
+    its backward statistics (sum dz, sum dz*(z-mean)), attached to y as ``y._mxamd_bn_bwd``.
+    ``dil`` (big kernel only, no fused epilogues): dilated taps."""
     N, H, W, C = x.shape
     K, R, S, _ = w.shape
-    Ho = (H + 2 * pad[0] - R) // stride[0] + 1
-    Wo = (W + 2 * pad[1] - S) // stride[1] + 1
+    dil = tuple(dil)
+    Ho = (H + 2 * pad[0] - dil[0] * (R - 1) - 1) // stride[0] + 1
+    Wo = (W + 2 * pad[1] - dil[1] * (S - 1) - 1) // stride[1] + 1
+    assert dil == (1, 1) or (variant in _BIG_VARIANTS and not bn_stats and bn_bwd is None and up == 0), \
+        'conv_fwd: dilation runs on the big-tile kernel without fused epilogues'
     assert up in (0, 2) and (up == 0 or (variant in _BIG_VARIANTS and addend is None and not bn_stats))
     y = torch.empty((N, Ho * max(up, 1), Wo * max(up, 1), K), dtype=x.dtype, device=x.device)
     if N * Ho * Wo * K >= 2 ** 31:
@@ -595,7 +599,8 @@ def conv_fwd(x, w, stride, pad, bias=None, variant=0, bn_stats=False, addend=Non
                        bn_mask=_p(bmask), bn_mode=int(bmode), bn_part=bpart.data_ptr(), bn_nparts=bnp)
         lib.conv_nhwc_fwd_big(_DT[x.dtype], x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(),
                               _zero_page(x.device).data_ptr(), N, H, W, C, K, R, S, stride[0], stride[1],
-                              pad[0], pad[1], v, _p(part), nparts, _p(addend), _stream(), up=int(up), **bkw)
+                              pad[0], pad[1], v, _p(part), nparts, _p(addend), _stream(), up=int(up), dh=dil[0],
+                              dw=dil[1], **bkw)
         if bkw:
             # the version pins the statistics to exactly this gradient: when y has several consumers,
             # autograd may accumulate the others' gradients into this tensor in place (bumping its
@@ -719,7 +724,7 @@ def conv_wgrad_ok(x, w):
             and x.numel() < 2 ** 31 and x.data_ptr() % 16 == 0)
 
 
-def conv_wgrad(x, dy, wshape, stride, pad, out=None, accum=False, dma=True, ring=0):
+def conv_wgrad(x, dy, wshape, stride, pad, out=None, accum=False, dma=True, ring=0, dil=(1, 1)):
     """dW[K,R,S,C] of an NHWC conv on MFMA (split-pixel fp32 slabs + reduce).
 
     ``out`` (optional, contiguous, f16/bf16/f32) receives the result; with
@@ -731,15 +736,17 @@ def conv_wgrad(x, dy, wshape, stride, pad, out=None, accum=False, dma=True, ring
     K, R, S, _ = wshape
     dy = dy.contiguous()
     assert dy.dtype == x.dtype and dy.shape[0] == N and dy.shape[3] == K
-    Ho = (H + 2 * pad[0] - R) // stride[0] + 1
-    Wo = (W + 2 * pad[1] - S) // stride[1] + 1
+    dh, dw = dil
+    Ho = (H + 2 * pad[0] - dh * (R - 1) - 1) // stride[0] + 1
+    Wo = (W + 2 * pad[1] - dw * (S - 1) - 1) // stride[1] + 1
     assert tuple(dy.shape[1:3]) == (Ho, Wo), 'conv_wgrad: dy shape does not match the conv geometry'
     assert dy.numel() < 2 ** 31 and dy.data_ptr() % 16 == 0
     lib = _K.lib()
     if ring:
-        ws = lib.conv_nhwc_wgrad_ring_workspace(N, H, W, C, K, R, S, stride[0], stride[1], pad[0], pad[1], ring)
+        ws = lib.conv_nhwc_wgrad_ring_workspace(N, H, W, C, K, R, S, stride[0], stride[1], pad[0], pad[1], ring,
+                                                dh=dh, dw=dw)
     else:
-        ws = lib.conv_nhwc_wgrad_workspace(N, H, W, C, K, R, S, stride[0], stride[1], pad[0], pad[1])
+        ws = lib.conv_nhwc_wgrad_workspace(N, H, W, C, K, R, S, stride[0], stride[1], pad[0], pad[1], dh=dh, dw=dw)
     slab = torch.empty(ws, dtype=torch.float32, device=x.device)
     if out is None:
         out = torch.empty((K, R, S, C), dtype=x.dtype, device=x.device)
@@ -748,11 +755,11 @@ def conv_wgrad(x, dy, wshape, stride, pad, out=None, accum=False, dma=True, ring
     if ring:
         lib.conv_nhwc_wgrad_ring(_DT[x.dtype], x.data_ptr(), dy.data_ptr(), slab.data_ptr(), _DT[out.dtype],
                                  out.data_ptr(), int(bool(accum)), N, H, W, C, K, R, S, stride[0], stride[1], pad[0],
-                                 pad[1], _zero_page(x.device).data_ptr(), int(ring), _stream())
+                                 pad[1], _zero_page(x.device).data_ptr(), int(ring), _stream(), dh=dh, dw=dw)
         return out
     lib.conv_nhwc_wgrad(_DT[x.dtype], x.data_ptr(), dy.data_ptr(), slab.data_ptr(), _DT[out.dtype], out.data_ptr(),
                         int(bool(accum)), N, H, W, C, K, R, S, stride[0], stride[1], pad[0], pad[1],
-                        _zero_page(x.device).data_ptr() if dma else 0, _stream())
+                        _zero_page(x.device).data_ptr() if dma else 0, _stream(), dh=dh, dw=dw)
     return out
 
 
@@ -1663,6 +1670,82 @@ def conv_algo_times():
     return {k: dict(v) for k, v in _TIMES.items()}
 
 
+def _conv_bwd_dil_torch(dy, x, w, stride, pad, dil, mask):
+    """MIOpen (through aten) gradients of a dilated NHWC conv: (dx, dw) per ``mask``."""
+    r = torch.ops.aten.convolution_backward(dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2),
+                                            None, tuple(stride), tuple(pad), tuple(dil), False, (0, 0), 1,
+                                            (mask[0], mask[1], False))
+    return (r[0].permute(0, 2, 3, 1).contiguous() if mask[0] else None,
+            r[1].permute(0, 2, 3, 1).contiguous() if mask[1] else None)
+
+
+def dil_ok(x, w, dilate):
+    """Dilated NHWC convs (DeepLab atrous layers) on the big-tile forward / data-gradient kernels and
+    the MFMA weight-gradient kernels."""
+    K, R, S, C = w.shape
+    return (_CONV_HIP and tuple(dilate) != (1, 1) and C % 64 == 0 and K % 64 == 0 and x.is_contiguous()
+            and x.dtype in (torch.float16, torch.bfloat16) and x.numel() < 2 ** 31)
+
+
+class ConvDilNHWC(torch.autograd.Function):
+    """Dilated 2-D NHWC convolution: forward on conv_big.hip with dilated taps; data gradient (stride 1)
+    = the same kernel over dY with the flipped weight, dilation d and padding d*(R-1) - p; weight
+    gradient on conv_wgrad.hip with dilated taps; each pass timed against MIOpen per shape (reference:
+    the dilate parameter of src/operator/nn/convolution-inl.h)."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, stride, pad, dilate):
+        K, R, S, C = w.shape
+        key = ('fwd-dil', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), tuple(dilate), x.dtype,
+               bias is not None)
+        cands = [('hip%d' % v, lambda v=v: conv_fwd(x, w, stride, pad, bias, v, dil=dilate))
+                 for v, (bco, _bpix) in sorted(_BIG_VARIANTS.items()) if K % bco == 0 and v not in _BIG_SKINNY]
+
+        def miopen():
+            y = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), bias, tuple(stride),
+                                           tuple(pad), tuple(dilate))
+            return y.permute(0, 2, 3, 1).contiguous()
+        cands.append(('miopen', miopen))
+        y = _select(key, cands, cands[0][0])
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (tuple(stride), tuple(pad), tuple(dilate))
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, pad, dil = ctx.cfg
+        dy = dy.contiguous()
+        K, R, S, C = w.shape
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            key = ('dgrad-dil', tuple(x.shape), tuple(w.shape), stride, pad, dil, x.dtype)
+            cands = []
+            pp = (dil[0] * (R - 1) - pad[0], dil[1] * (S - 1) - pad[1])
+            if stride == (1, 1) and pp[0] >= 0 and pp[1] >= 0:
+                cands = [('hip%d' % v, lambda v=v: conv_fwd(dy, _dgrad_weight(w), (1, 1), pp, None, v, dil=dil))
+                         for v, (bco, _bpix) in sorted(_BIG_VARIANTS.items())
+                         if C % bco == 0 and v not in _BIG_SKINNY]
+            cands.append(('miopen', lambda: _conv_bwd_dil_torch(dy, x, w, stride, pad, dil, (True, False))[0]))
+            dx = _select(key, cands, cands[0][0])
+        if ctx.needs_input_grad[1]:
+            key = ('wgrad-dil', tuple(x.shape), tuple(w.shape), stride, pad, dil, x.dtype)
+            cands = []
+            if conv_wgrad_ok(x, w):
+                cands.append(('hip', lambda: conv_wgrad(x, dy, w.shape, stride, pad, dil=dil)))
+                lib = _K.lib()
+                for v in range(1, 10):
+                    if lib.conv_nhwc_wgrad_ring_ok(C, K, R, S, v):
+                        cands.append(('ring%d' % v, lambda v=v: conv_wgrad(x, dy, w.shape, stride, pad, ring=v,
+                                                                          dil=dil)))
+            cands.append(('miopen', lambda: _conv_bwd_dil_torch(dy, x, w, stride, pad, dil, (False, True))[1]))
+            dw = _select(key, cands, cands[0][0]).to(w.dtype)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy.float().sum(dim=(0, 1, 2))
+        return dx, dw, db, None, None, None
+
+
 _KPAD = _os.environ.get('MXAMD_CONV_KPAD', '1') == '1'
 
 
@@ -1689,7 +1772,7 @@ def conv_ok(x, w, stride, pad, dilate, groups):
             and w.is_contiguous() and x.dtype in (torch.float16, torch.bfloat16) and w.dtype == x.dtype)
 
 
-__all__ += ['ConvNHWC', 'ConvTeeNHWC', 'conv_kpad', 'kpad_ok', 'conv_fwd', 'conv_ok_shape', 'conv_wgrad', 'conv_wgrad_ok', 'stem_ok',
+__all__ += ['ConvNHWC', 'ConvTeeNHWC', 'ConvDilNHWC', 'dil_ok', 'conv_kpad', 'kpad_ok', 'conv_fwd', 'conv_ok_shape', 'conv_wgrad', 'conv_wgrad_ok', 'stem_ok',
             'conv_stem_fwd', 'conv_stem_wgrad']
 
 

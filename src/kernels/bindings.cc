@@ -65,7 +65,7 @@ void conv_nhwc_fwd_big(int dtype, const void* x, const void* w, const float* bia
                        int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int variant,
                        float* part, int nparts, const void* addend, hipStream_t s, const void* bn_z,
                        const float* bn_mean, const float* bn_scale, const float* bn_shift, const uint8_t* bn_mask,
-                       int bn_mode, float* bn_part, int bn_nparts, int up);
+                       int bn_mode, float* bn_part, int bn_nparts, int up, int dh, int dw);
 int conv_nhwc_fwd_big_bwd_nparts(int N, int H, int W, int R, int S, int sh, int sw, int ph, int pw, int variant);
 void conv_nhwc_fwd_glds(int dtype, const void* x, const void* w, const float* bias, void* y, const void* zero, int N,
                         int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int bco,
@@ -89,14 +89,15 @@ void conv3x3_halo(int dtype, const void* x, const void* w, void* y, const void* 
                   const float* bn_shift, int bn_mode, float* bn_part, hipStream_t s);
 int conv_nhwc_wgrad_ring_ok(int C, int K, int R, int S, int variant);
 int64_t conv_nhwc_wgrad_ring_workspace(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
-                                       int variant);
+                                       int variant, int dh, int dw);
 void conv_nhwc_wgrad_ring(int dtype, const void* x, const void* dy, float* slab, int out_dtype, void* out, int accum,
                           int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
-                          const void* zero, int variant, hipStream_t s);
-int64_t conv_nhwc_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw);
+                          const void* zero, int variant, hipStream_t s, int dh, int dw);
+int64_t conv_nhwc_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
+                                  int dh, int dw);
 void conv_nhwc_wgrad(int dtype, const void* x, const void* dy, float* slab, int out_dtype, void* out, int accum, int N,
                      int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, const void* zero,
-                     hipStream_t s);
+                     hipStream_t s, int dh, int dw);
 int conv_stem_grid(int N, int H, int W, int R, int S, int ph, int pw);
 void conv_stem_fwd(int dtype, const void* x, const void* w, void* y, int N, int H, int W, int C, int K, int R, int S,
                    int sh, int sw, int ph, int pw, float* part, int nparts, hipStream_t s);
@@ -556,17 +557,18 @@ PYBIND11_MODULE(_hip_kernels, m) {
                                 int H, int W, int C, int K, int R, int Sf, int sh, int sw, int ph, int pw, int variant,
                                 uintptr_t part, int nparts, uintptr_t addend, uintptr_t s, uintptr_t bz,
                                 uintptr_t bmean, uintptr_t bscale, uintptr_t bshift, uintptr_t bmask, int bmode,
-                                uintptr_t bpart, int bnparts, int up) {
+                                uintptr_t bpart, int bnparts, int up, int dh, int dw) {
     conv_nhwc_fwd_big(dt, P<void>(x), P<void>(w), P<float>(bias), P<void>(y), P<void>(zero), N, H, W, C, K, R, Sf, sh,
                       sw, ph, pw, variant, P<float>(part), nparts, P<void>(addend), S(s), P<void>(bz), P<float>(bmean),
-                      P<float>(bscale), P<float>(bshift), P<uint8_t>(bmask), bmode, P<float>(bpart), bnparts, up);
+                      P<float>(bscale), P<float>(bshift), P<uint8_t>(bmask), bmode, P<float>(bpart), bnparts, up, dh,
+                      dw);
     check_launch("conv_nhwc_fwd_big");
   }, py::arg("dt"), py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("zero"), py::arg("N"),
      py::arg("H"), py::arg("W"), py::arg("C"), py::arg("K"), py::arg("R"), py::arg("S"), py::arg("sh"),
      py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("variant"), py::arg("part"), py::arg("nparts"),
      py::arg("addend"), py::arg("stream"), py::arg("bn_z") = 0, py::arg("bn_mean") = 0, py::arg("bn_scale") = 0,
      py::arg("bn_shift") = 0, py::arg("bn_mask") = 0, py::arg("bn_mode") = 0, py::arg("bn_part") = 0,
-     py::arg("bn_nparts") = 0, py::arg("up") = 0);
+     py::arg("bn_nparts") = 0, py::arg("up") = 0, py::arg("dh") = 1, py::arg("dw") = 1);
   // persistent LDS-DMA ring kernel (conv_ring.hip): variant 0..5 = 128x128x4, 256x128x3, 128x256x3, 64x256x4,
   // 256x256x2, 64x128x4 (co x pix x stages); part as above
   m.def("conv_nhwc_fwd_ring_nparts", &conv_nhwc_fwd_ring_nparts);
@@ -591,25 +593,35 @@ PYBIND11_MODULE(_hip_kernels, m) {
      py::arg("W"), py::arg("C"), py::arg("K"), py::arg("part"), py::arg("nparts"), py::arg("bn_z") = 0,
      py::arg("bn_mean") = 0, py::arg("bn_scale") = 0, py::arg("bn_shift") = 0, py::arg("bn_mode") = 0,
      py::arg("bn_part") = 0, py::arg("s") = 0);
-  m.def("conv_nhwc_wgrad_workspace", &conv_nhwc_wgrad_workspace);
+  m.def("conv_nhwc_wgrad_workspace", &conv_nhwc_wgrad_workspace, py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"),
+        py::arg("K"), py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
+        py::arg("dh") = 1, py::arg("dw") = 1);
   // weight gradient on the LDS-DMA ring (variants 1..5, see conv_wgrad.hip)
   m.def("conv_nhwc_wgrad_ring_ok", &conv_nhwc_wgrad_ring_ok);
-  m.def("conv_nhwc_wgrad_ring_workspace", &conv_nhwc_wgrad_ring_workspace);
+  m.def("conv_nhwc_wgrad_ring_workspace", &conv_nhwc_wgrad_ring_workspace, py::arg("N"), py::arg("H"), py::arg("W"),
+        py::arg("C"), py::arg("K"), py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
+        py::arg("pw"), py::arg("variant"), py::arg("dh") = 1, py::arg("dw") = 1);
   m.def("conv_nhwc_wgrad_ring", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t slab, int odt, uintptr_t out,
                                    int accum, int N, int H, int W, int C, int K, int R, int Sf, int sh, int sw, int ph,
-                                   int pw, uintptr_t zero, int variant, uintptr_t s) {
+                                   int pw, uintptr_t zero, int variant, uintptr_t s, int dh, int dw) {
     conv_nhwc_wgrad_ring(dt, P<void>(x), P<void>(dy), P<float>(slab), odt, P<void>(out), accum, N, H, W, C, K, R, Sf,
-                         sh, sw, ph, pw, P<void>(zero), variant, S(s));
+                         sh, sw, ph, pw, P<void>(zero), variant, S(s), dh, dw);
     check_launch("conv_nhwc_wgrad_ring");
-  });
+  }, py::arg("dt"), py::arg("x"), py::arg("dy"), py::arg("slab"), py::arg("odt"), py::arg("out"), py::arg("accum"),
+     py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("K"), py::arg("R"), py::arg("S"), py::arg("sh"),
+     py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("zero"), py::arg("variant"), py::arg("stream"),
+     py::arg("dh") = 1, py::arg("dw") = 1);
   // zero: 0 -> register-staged kernel, else a >=128-byte zero page -> LDS-DMA kernel
   m.def("conv_nhwc_wgrad", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t slab, int odt, uintptr_t out, int accum,
                               int N, int H, int W, int C, int K, int R, int Sf, int sh, int sw, int ph, int pw,
-                              uintptr_t zero, uintptr_t s) {
+                              uintptr_t zero, uintptr_t s, int dh, int dw) {
     conv_nhwc_wgrad(dt, P<void>(x), P<void>(dy), P<float>(slab), odt, P<void>(out), accum, N, H, W, C, K, R, Sf, sh,
-                    sw, ph, pw, P<void>(zero), S(s));
+                    sw, ph, pw, P<void>(zero), S(s), dh, dw);
     check_launch("conv_nhwc_wgrad");
-  });
+  }, py::arg("dt"), py::arg("x"), py::arg("dy"), py::arg("slab"), py::arg("odt"), py::arg("out"), py::arg("accum"),
+     py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("K"), py::arg("R"), py::arg("S"), py::arg("sh"),
+     py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("zero"), py::arg("stream"), py::arg("dh") = 1,
+     py::arg("dw") = 1);
   m.def("layernorm_bwd_partials", &layernorm_bwd_partials);
   // pt: gamma / beta in the activation dtype (else fp32)
   m.def("layernorm_forward", [](int dt, uintptr_t x, uintptr_t g, uintptr_t b, uintptr_t y, uintptr_t mean,

@@ -70,6 +70,7 @@ struct GeomB {
   // (n, 2ho, 2wo) and the epilogue writes zeros to its three other 2x2 siblings -- the data gradient of a
   // 1x1 stride-2 convolution in one pass over dX (no memset, no scatter)
   int up;
+  int dh, dw;  // dilation: tap (r, s) reads input row ho*sh - ph + r*dh, column wo*sw - pw + s*dw
 };
 
 __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
@@ -172,11 +173,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * MI
     char* sbase = smem + stage * STAGE;
 #pragma unroll
     for (int i = 0; i < A_INS; ++i) glds16(w + a_off[i] + k0, sbase + (i * 8 + wid) * 1024);
-    const int doff = (r * g.W + s) * g.C + c0;
+    const int doff = (r * g.dh * g.W + s * g.dw) * g.C + c0;
 #pragma unroll
     for (int i = 0; i < B_INS; ++i) {
       if (BPIX % 64 != 0 && (i * 8 + wid) * 8 >= BPIX) continue;   // wave-uniform: past the tile
-      const int hi = b_hi[i] + r, wi = b_wi[i] + s;
+      const int hi = b_hi[i] + r * g.dh, wi = b_wi[i] + s * g.dw;
       const bool ok = (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
       const T* src = ok ? x + b_base[i] + doff : zsrc;
       glds16(src, sbase + A_BYTES + (i * 8 + wid) * 1024);
@@ -548,12 +549,17 @@ void conv_nhwc_fwd_big(int dtype, const void* x, const void* w, const float* bia
                        int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int variant,
                        float* part, int nparts, const void* addend, hipStream_t s, const void* bn_z,
                        const float* bn_mean, const float* bn_scale, const float* bn_shift, const uint8_t* bn_mask,
-                       int bn_mode, float* bn_part, int bn_nparts, int up) {
+                       int bn_mode, float* bn_part, int bn_nparts, int up, int dh, int dw) {
   GeomB g;
   g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S;
   g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw;
-  g.Ho = (H + 2 * ph - R) / sh + 1;
-  g.Wo = (W + 2 * pw - S) / sw + 1;
+  g.dh = dh; g.dw = dw;
+  MXAMD_HOST_CHECK(dh >= 1 && dw >= 1, "conv_nhwc_fwd_big: dilation must be >= 1");
+  MXAMD_HOST_CHECK((dh == 1 && dw == 1) || (part == nullptr && bn_part == nullptr && up == 0),
+                   "conv_nhwc_fwd_big: dilated convolutions take no fused BN epilogue / upsampled output");
+  g.Ho = (H + 2 * ph - dh * (R - 1) - 1) / sh + 1;
+  g.Wo = (W + 2 * pw - dw * (S - 1) - 1) / sw + 1;
+  MXAMD_HOST_CHECK(g.Ho > 0 && g.Wo > 0, "conv_nhwc_fwd_big: empty output");
   g.M = N * g.Ho * g.Wo;
   g.Ktot = R * S * C;
   g.up = up;

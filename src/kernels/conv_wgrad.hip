@@ -69,6 +69,7 @@ struct Mfma16 : mfma::Op<T> {};   // 16x16x32 MFMA (mfma.h)
 
 struct WgradGeom {
   int N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw;
+  int dh, dw;   // dilation: tap (r, s) reads input row ho*sh - ph + r*dh, column wo*sw - pw + s*dw
   int P;        // N*Ho*Wo output pixels (reduction length)
   int RSC;      // R*S*C (GEMM rows)
   int tiles_m;  // RSC / (16*FM*WM)
@@ -141,8 +142,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(const T* __res
       const int n = m0 + sub * 64 + ch * 8;  // rsc column
       const int rs = n / g.C;
       s_col[i] = n - rs * g.C;
-      s_r[i] = rs / g.S;
-      s_s[i] = rs - s_r[i] * g.S;
+      s_r[i] = (rs / g.S) * g.dh;
+      s_s[i] = (rs - (rs / g.S) * g.S) * g.dw;
     } else {
       s_col[i] = n0 + (sub - XSUB) * 64 + ch * 8;
       s_r[i] = s_s[i] = 0;
@@ -296,8 +297,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_glds_kernel(const T* 
       const int n = m0 + sub * 64;           // first rsc column of the sub-tile (one (r, s): C % 64 == 0)
       const int rs = n / g.C;
       d_col[i] = n - rs * g.C + gch * 8;
-      d_r[i] = rs / g.S;
-      d_s[i] = rs - d_r[i] * g.S;
+      d_r[i] = (rs / g.S) * g.dh;
+      d_s[i] = (rs - (rs / g.S) * g.S) * g.dw;
     } else {
       d_col[i] = n0 + (sub - WM) * 64 + gch * 8;
       d_r[i] = d_s[i] = 0;
@@ -465,8 +466,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_ring_kernel(const T* 
       const int n = m0 + sub * 64;
       const int rs = n / g.C;
       d_col[i] = n - rs * g.C + gch * 8;
-      d_r[i] = rs / g.S;
-      d_s[i] = rs - d_r[i] * g.S;
+      d_r[i] = (rs / g.S) * g.dh;
+      d_s[i] = (rs - (rs / g.S) * g.S) * g.dw;
     } else {
       d_col[i] = n0 + (sub - XSUB) * 64 + gch * 8;
       d_r[i] = d_s[i] = 0;
@@ -656,9 +657,10 @@ struct WgradPlan {
   int wm, wn, fm, splits, plen;
 };
 
-WgradPlan plan_wgrad(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw) {
+WgradPlan plan_wgrad(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int dh = 1,
+                     int dw = 1) {
   WgradPlan pl;
-  const int Ho = (H + 2 * ph - R) / sh + 1, Wo = (W + 2 * pw - S) / sw + 1;
+  const int Ho = (H + 2 * ph - dh * (R - 1) - 1) / sh + 1, Wo = (W + 2 * pw - dw * (S - 1) - 1) / sw + 1;
   const int RSC = R * S * C;
   const int64_t P = (int64_t)N * Ho * Wo;
   pl.fm = 4;
@@ -738,9 +740,9 @@ static bool ring_wgrad_cfg(int variant, RingW* c) {
 }
 
 static WgradPlan plan_wgrad_ring(const RingW& c, int N, int H, int W, int C, int K, int R, int S, int sh, int sw,
-                                 int ph, int pw) {
+                                 int ph, int pw, int dh = 1, int dw = 1) {
   WgradPlan pl;
-  const int Ho = (H + 2 * ph - R) / sh + 1, Wo = (W + 2 * pw - S) / sw + 1;
+  const int Ho = (H + 2 * ph - dh * (R - 1) - 1) / sh + 1, Wo = (W + 2 * pw - dw * (S - 1) - 1) / sw + 1;
   const int RSC = R * S * C;
   const int64_t P = (int64_t)N * Ho * Wo;
   pl.fm = 4;
@@ -804,36 +806,38 @@ int conv_nhwc_wgrad_ring_ok(int C, int K, int R, int S, int variant) {
 }
 
 int64_t conv_nhwc_wgrad_ring_workspace(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
-                                       int variant) {
+                                       int variant, int dh, int dw) {
   RingW c;
   MXAMD_HOST_CHECK(ring_wgrad_cfg(variant, &c), "conv_nhwc_wgrad_ring: unknown variant");
-  WgradPlan pl = plan_wgrad_ring(c, N, H, W, C, K, R, S, sh, sw, ph, pw);
+  WgradPlan pl = plan_wgrad_ring(c, N, H, W, C, K, R, S, sh, sw, ph, pw, dh, dw);
   return (int64_t)pl.splits * K * R * S * C;
 }
 
 void conv_nhwc_wgrad_ring(int dtype, const void* x, const void* dy, float* slab, int out_dtype, void* out, int accum,
                           int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
-                          const void* zero, int variant, hipStream_t s) {
+                          const void* zero, int variant, hipStream_t s, int dh, int dw) {
   RingW c;
   MXAMD_HOST_CHECK(ring_wgrad_cfg(variant, &c) && conv_nhwc_wgrad_ring_ok(C, K, R, S, variant) && zero != nullptr,
                    "conv_nhwc_wgrad_ring: variant does not tile this weight");
+  MXAMD_HOST_CHECK(dh >= 1 && dw >= 1, "conv_nhwc_wgrad_ring: dilation must be >= 1");
   WgradGeom g;
   g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S;
   g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw;
-  g.Ho = (H + 2 * ph - R) / sh + 1;
-  g.Wo = (W + 2 * pw - S) / sw + 1;
+  g.dh = dh; g.dw = dw;
+  g.Ho = (H + 2 * ph - dh * (R - 1) - 1) / sh + 1;
+  g.Wo = (W + 2 * pw - dw * (S - 1) - 1) / sw + 1;
   const int64_t P = (int64_t)N * g.Ho * g.Wo;
   MXAMD_HOST_CHECK(P < (1ll << 31) && (int64_t)N * H * W * C < (1ll << 31) && P * K < (1ll << 31),
                    "conv_nhwc_wgrad_ring: tensor too large for 32-bit indexing");
   g.P = (int)P;
   g.RSC = R * S * C;
-  WgradPlan pl = plan_wgrad_ring(c, N, H, W, C, K, R, S, sh, sw, ph, pw);
+  WgradPlan pl = plan_wgrad_ring(c, N, H, W, C, K, R, S, sh, sw, ph, pw, dh, dw);
   g.tiles_m = g.RSC / (16 * c.fm * c.wm);
   g.tiles = g.tiles_m * (K / (64 * c.wn));
   g.plen = pl.plen;
   g.fWo = make_fastdiv(g.Wo);
   g.fHoWo = make_fastdiv(g.Ho * g.Wo);
-  const bool ident = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
+  const bool ident = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && dh == 1 && dw == 1;
   if (dtype == kF16) dispatch_wgrad_ring<__half>(variant, x, dy, slab, g, pl.splits, ident, zero, s);
   else if (dtype == kBF16) dispatch_wgrad_ring<__hip_bfloat16>(variant, x, dy, slab, g, pl.splits, ident, zero, s);
   else throw std::runtime_error("conv_nhwc_wgrad_ring: dtype must be f16 or bf16");
@@ -844,8 +848,9 @@ void conv_nhwc_wgrad_ring(int dtype, const void* x, const void* dy, float* slab,
 }
 
 // Number of fp32 slab elements conv_nhwc_wgrad needs (splits * K * R*S*C).
-int64_t conv_nhwc_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw) {
-  WgradPlan pl = plan_wgrad(N, H, W, C, K, R, S, sh, sw, ph, pw);
+int64_t conv_nhwc_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
+                                  int dh, int dw) {
+  WgradPlan pl = plan_wgrad(N, H, W, C, K, R, S, sh, sw, ph, pw, dh, dw);
   return (int64_t)pl.splits * K * R * S * C;
 }
 
@@ -854,25 +859,27 @@ int64_t conv_nhwc_wgrad_workspace(int N, int H, int W, int C, int K, int R, int 
 // zero: optional >= 128-byte zero page; when given, the LDS-DMA kernel variant runs.
 void conv_nhwc_wgrad(int dtype, const void* x, const void* dy, float* slab, int out_dtype, void* out, int accum, int N,
                      int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, const void* zero,
-                     hipStream_t s) {
+                     hipStream_t s, int dh, int dw) {
   MXAMD_HOST_CHECK(C % 64 == 0 && K % 64 == 0, "conv_nhwc_wgrad: need Cin % 64 == 0 and Cout % 64 == 0");
+  MXAMD_HOST_CHECK(dh >= 1 && dw >= 1, "conv_nhwc_wgrad: dilation must be >= 1");
   WgradGeom g;
   g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S;
   g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw;
-  g.Ho = (H + 2 * ph - R) / sh + 1;
-  g.Wo = (W + 2 * pw - S) / sw + 1;
+  g.dh = dh; g.dw = dw;
+  g.Ho = (H + 2 * ph - dh * (R - 1) - 1) / sh + 1;
+  g.Wo = (W + 2 * pw - dw * (S - 1) - 1) / sw + 1;
   const int64_t P = (int64_t)N * g.Ho * g.Wo;
   MXAMD_HOST_CHECK(P < (1ll << 31) && (int64_t)N * H * W * C < (1ll << 31) && P * K < (1ll << 31),
                    "conv_nhwc_wgrad: tensor too large for 32-bit indexing");
   g.P = (int)P;
   g.RSC = R * S * C;
-  WgradPlan pl = plan_wgrad(N, H, W, C, K, R, S, sh, sw, ph, pw);
+  WgradPlan pl = plan_wgrad(N, H, W, C, K, R, S, sh, sw, ph, pw, dh, dw);
   g.tiles_m = g.RSC / (16 * pl.fm * pl.wm);
   g.tiles = g.tiles_m * (K / (64 * pl.wn));
   g.plen = pl.plen;
   g.fWo = make_fastdiv(g.Wo);
   g.fHoWo = make_fastdiv(g.Ho * g.Wo);
-  const bool ident = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
+  const bool ident = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && dh == 1 && dw == 1;
   if (dtype == kF16) dispatch_wgrad<__half>(x, dy, slab, g, pl, ident, zero, s);
   else if (dtype == kBF16) dispatch_wgrad<__hip_bfloat16>(x, dy, slab, g, pl, ident, zero, s);
   else throw std::runtime_error("conv_nhwc_wgrad: dtype must be f16 or bf16");

@@ -13,3 +13,5 @@ timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 python tools/trace_window.py gpurun_out/r6o_prof --steps 4 --top 60 > gpurun_out/r6o_window.txt 2>&1; head -12 gpurun_out/r6o_window.txt | cut -c1-160
 grep -i deform gpurun_out/r6o_window.txt | cut -c1-140
 rm -rf gpurun_out/r6o_prof
+timeout -k 10 300 python -u tools/bench_conv_gen.py > gpurun_out/r6o_conv_gen.txt 2>&1 || { echo CONVGEN FAILED; tail -20 gpurun_out/r6o_conv_gen.txt; exit 1; }
+cat gpurun_out/r6o_conv_gen.txt
