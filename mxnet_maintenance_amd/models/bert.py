@@ -25,6 +25,18 @@ BERT_CONFIGS = {
 }
 
 
+class _ResidualLayerNorm(nn.LayerNorm):
+    """LayerNorm(residual + Dropout(data)): the sub-layer tail as the fused add_dropout_layernorm
+    operator (same parameters as the LayerNorm it replaces)."""
+
+    def __init__(self, dropout=0.0, **kwargs):
+        super().__init__(**kwargs)
+        self._p = dropout
+
+    def hybrid_forward(self, F, data, residual, gamma, beta):
+        return F.contrib.add_dropout_layernorm(data, residual, gamma, beta, p=self._p, eps=self._epsilon)
+
+
 class BERTEncoderCell(HybridBlock):
     """Post-LN transformer layer: x + Attn(x) -> LN -> x + FFN(x) -> LN on (S, B, C) inputs."""
 
@@ -40,11 +52,10 @@ class BERTEncoderCell(HybridBlock):
             # one (C -> 3C) projection whose output is interleaved per head as [q k v]
             self.attn_qkv = nn.Dense(3 * units, flatten=False, in_units=units, prefix='attn_qkv_')
             self.attn_proj = nn.Dense(units, flatten=False, in_units=units, prefix='attn_proj_')
-            self.ln1 = nn.LayerNorm(epsilon=layer_norm_eps, in_channels=units, prefix='ln1_')
+            self.ln1 = _ResidualLayerNorm(dropout=dropout, epsilon=layer_norm_eps, in_channels=units, prefix='ln1_')
             self.ffn_1 = nn.Dense(hidden_size, flatten=False, in_units=units, activation=None, prefix='ffn1_')
             self.ffn_2 = nn.Dense(units, flatten=False, in_units=hidden_size, prefix='ffn2_')
-            self.ln2 = nn.LayerNorm(epsilon=layer_norm_eps, in_channels=units, prefix='ln2_')
-            self.drop = nn.Dropout(dropout) if dropout else None
+            self.ln2 = _ResidualLayerNorm(dropout=dropout, epsilon=layer_norm_eps, in_channels=units, prefix='ln2_')
 
     def hybrid_forward(self, F, x, mask=None):
         qkv = self.attn_qkv(x)
@@ -63,14 +74,9 @@ class BERTEncoderCell(HybridBlock):
             if self._dropout:
                 att = F.Dropout(att, p=self._dropout)
             ctx = F.contrib.interleaved_matmul_selfatt_valatt(qkv, att, heads=self._heads)
-        h = self.attn_proj(ctx)
-        if self.drop is not None:
-            h = self.drop(h)
-        x = self.ln1(x + h)
+        x = self.ln1(self.attn_proj(ctx), x)             # LN(x + dropout(h)), one fused kernel
         f = self.ffn_2(F.LeakyReLU(self.ffn_1(x), act_type='gelu'))
-        if self.drop is not None:
-            f = self.drop(f)
-        return self.ln2(x + f)
+        return self.ln2(f, x)
 
 
 class BERTEncoder(HybridBlock):

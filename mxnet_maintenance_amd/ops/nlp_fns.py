@@ -12,7 +12,7 @@ from . import kernels as _K
 from .. import _state
 from .kernel_fns import _DT, _stream, _p, _f32, _leaf_grad
 
-__all__ = ['LayerNorm', 'GELU', 'Softmax', 'Dropout', 'ln_ok', 'ew_ok', 'softmax_ok',
+__all__ = ['LayerNorm', 'AddDropoutLN', 'GELU', 'Softmax', 'Dropout', 'ln_ok', 'ew_ok', 'softmax_ok',
            'flat_adam', 'lamb_update', 'seg_sumsq', 'all_finite', 'ChunkTable']
 
 
@@ -96,6 +96,66 @@ class LayerNorm(torch.autograd.Function):
         if accum:
             return dx, None, None, None, None
         return (dx, dg.view(gamma.shape).to(gamma.dtype) if need_g else None,
+                db.view(beta.shape).to(beta.dtype) if need_b else None, None, None)
+
+
+class AddDropoutLN(torch.autograd.Function):
+    """y = LayerNorm(x + dropout_p(h)) over the last axis in one kernel (the post-LN transformer
+    sub-layer tail); backward: the residual gradient, the dropout-masked branch gradient and
+    dgamma / dbeta in one kernel."""
+
+    @staticmethod
+    def forward(ctx, x, h, gamma, beta, eps, p):
+        lib = _K.lib()
+        D = x.shape[-1]
+        M = x.numel() // D
+        pt = int(gamma.dtype == x.dtype and beta.dtype == x.dtype and gamma.is_contiguous() and beta.is_contiguous()
+                 and gamma.data_ptr() % 16 == 0 and beta.data_ptr() % 16 == 0)
+        g = gamma if pt else _f32(gamma)
+        b = beta if pt else _f32(beta)
+        y = torch.empty_like(x)
+        sm = torch.empty_like(x)
+        stats = torch.empty(2, M, dtype=torch.float32, device=x.device)
+        mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device) if p > 0 else None
+        ctr = _state.GRAPH_RNG[0]
+        base = ctr.data_ptr() if (p > 0 and ctr is not None and torch.cuda.is_current_stream_capturing()) else 0
+        lib.add_dropout_ln_forward(_DT[x.dtype], x.data_ptr(), h.data_ptr(), g.data_ptr(), b.data_ptr(), pt,
+                                   y.data_ptr(), sm.data_ptr(), _p(mask), stats[0].data_ptr(), stats[1].data_ptr(),
+                                   M, D, float(eps), float(p), _seed() if p > 0 else 0, base, _stream())
+        ctx.save_for_backward(sm, g, stats, mask)
+        ctx.cfg = (pt, float(p))
+        ctx.refs = (gamma, beta)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = _K.lib()
+        sm, g, stats, mask = ctx.saved_tensors
+        pt, p = ctx.cfg
+        gamma, beta = ctx.refs
+        gy = gy.contiguous()
+        D = sm.shape[-1]
+        M = sm.numel() // D
+        ds = torch.empty_like(sm)
+        dh = torch.empty_like(sm)
+        nb = lib.layernorm_bwd_partials(M)
+        part = torch.empty(nb * 2 * D, dtype=torch.float32, device=sm.device)
+        need_g, need_b = ctx.needs_input_grad[2], ctx.needs_input_grad[3]
+        same = gamma.dtype == beta.dtype and gamma.dtype in _DT
+        tg = _leaf_grad(gamma, D, dtype=gamma.dtype) if (need_g and same) else None
+        tb = _leaf_grad(beta, D, dtype=beta.dtype) if (need_b and same) else None
+        if tg is not None and tb is not None:
+            dg, db, accum, gdt = tg, tb, 1, _DT[gamma.dtype]
+        else:
+            out = torch.empty(2, D, dtype=torch.float32, device=sm.device)
+            dg, db, accum, gdt = out[0], out[1], 0, _DT[torch.float32]
+        lib.add_dropout_ln_backward(_DT[sm.dtype], sm.data_ptr(), gy.data_ptr(), g.data_ptr(), pt,
+                                    stats[0].data_ptr(), stats[1].data_ptr(), _p(mask), p, ds.data_ptr(),
+                                    dh.data_ptr(), part.data_ptr(), dg.data_ptr(), db.data_ptr(), gdt, accum, M, D,
+                                    _stream())
+        if accum:
+            return ds, dh, None, None, None, None
+        return (ds, dh, dg.view(gamma.shape).to(gamma.dtype) if need_g else None,
                 db.view(beta.shape).to(beta.dtype) if need_b else None, None, None)
 
 

@@ -678,6 +678,25 @@ def layer_norm(data, gamma, beta, axis=-1, eps=1e-5, output_mean_var=False):
     return y.to(data.dtype), mean.to(data.dtype), std.to(data.dtype)
 
 
+def _adln_infer(s):
+    shape = s[0] if s[0] is not None else s[1]
+    if shape is None:
+        return {}
+    return {0: tuple(shape), 1: tuple(shape), 2: (shape[-1],), 3: (shape[-1],)}
+
+
+@register('_contrib_add_dropout_layernorm', aliases=('add_dropout_layernorm',),
+          arg_names=('data', 'residual', 'gamma', 'beta'),
+          infer_params=lambda s, a: _adln_infer(s),
+          params={'p': ('float', 0.0), 'eps': ('float', 1e-5)})
+def add_dropout_layernorm(data, residual, gamma, beta, p=0.0, eps=1e-5):
+    """LayerNorm(residual + Dropout(data, p)) over the last axis -- the post-LN transformer sub-layer
+    tail as one fused operator (the reference composes Dropout, elemwise_add and LayerNorm:
+    src/operator/nn/dropout-inl.h, layer_norm-inl.h); dropout is active in training mode only."""
+    active = _state.STATE.training and p > 0
+    return hip_ops.add_dropout_layer_norm(residual, data, gamma, beta, eps, p if active else 0.0)
+
+
 @register('GroupNorm', arg_names=('data', 'gamma', 'beta'), num_outputs=3, num_visible_outputs=_ln_nvis,
           infer_params=lambda s, a: {1: (a.get('num_groups', 1),), 2: (a.get('num_groups', 1),)},
           params={'num_groups': ('int', 1), 'eps': ('float', 1e-5), 'output_mean_var': ('bool', False)})

@@ -110,6 +110,12 @@ void layernorm_forward(int dtype, const void* x, const void* gamma, const void* 
 void layernorm_backward(int dtype, const void* x, const void* dy, const void* gamma, int pt, const float* mean,
                         const float* rstd, void* dx, float* part, void* dgamma, void* dbeta, int gdtype, int accum,
                         int M, int D, hipStream_t s);
+void add_dropout_ln_forward(int dtype, const void* x, const void* h, const void* gamma, const void* beta, int pt,
+                            void* y, void* s_out, uint8_t* mask, float* mean, float* rstd, int M, int D, float eps,
+                            float p, uint64_t seed, const uint64_t* seed_base, hipStream_t s);
+void add_dropout_ln_backward(int dtype, const void* s_in, const void* dy, const void* gamma, int pt, const float* mean,
+                             const float* rstd, const uint8_t* mask, float p, void* ds, void* dh, float* part,
+                             void* dgamma, void* dbeta, int gdtype, int accum, int M, int D, hipStream_t s);
 void gelu_forward(int dtype, const void* x, void* y, int64_t n, hipStream_t s);
 void gelu_backward(int dtype, const void* x, const void* dy, void* dx, int64_t n, hipStream_t s);
 void softmax_forward(int dtype, int log, const void* x, void* y, int M, int L, float scale, hipStream_t s);
@@ -640,6 +646,24 @@ PYBIND11_MODULE(_hip_kernels, m) {
   }, py::arg("dtype"), py::arg("x"), py::arg("dy"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
      py::arg("dx"), py::arg("part"), py::arg("dgamma"), py::arg("dbeta"), py::arg("gdtype"), py::arg("accum"),
      py::arg("M"), py::arg("D"), py::arg("stream"), py::arg("pt") = 0);
+  // y = LayerNorm(x + dropout(h)) and its backward (ds, dh = dropout'(ds), dgamma / dbeta)
+  m.def("add_dropout_ln_forward", [](int dt, uintptr_t x, uintptr_t h, uintptr_t g, uintptr_t b, int pt, uintptr_t y,
+                                     uintptr_t sum, uintptr_t mask, uintptr_t mean, uintptr_t rstd, int M, int D,
+                                     float eps, float p, uint64_t seed, uintptr_t seed_base, uintptr_t s) {
+    add_dropout_ln_forward(dt, P<void>(x), P<void>(h), P<void>(g), P<void>(b), pt, P<void>(y), P<void>(sum),
+                           P<uint8_t>(mask), P<float>(mean), P<float>(rstd), M, D, eps, p, seed,
+                           P<uint64_t>(seed_base), S(s));
+    check_launch("add_dropout_ln_forward");
+  });
+  m.def("add_dropout_ln_backward", [](int dt, uintptr_t sum, uintptr_t dy, uintptr_t g, int pt, uintptr_t mean,
+                                      uintptr_t rstd, uintptr_t mask, float p, uintptr_t ds, uintptr_t dh,
+                                      uintptr_t part, uintptr_t dg, uintptr_t db, int gdt, int accum, int M, int D,
+                                      uintptr_t s) {
+    add_dropout_ln_backward(dt, P<void>(sum), P<void>(dy), P<void>(g), pt, P<float>(mean), P<float>(rstd),
+                            P<uint8_t>(mask), p, P<void>(ds), P<void>(dh), P<float>(part), P<void>(dg), P<void>(db),
+                            gdt, accum, M, D, S(s));
+    check_launch("add_dropout_ln_backward");
+  });
   m.def("gelu_forward", [](int dt, uintptr_t x, uintptr_t y, int64_t n, uintptr_t s) {
     gelu_forward(dt, P<void>(x), P<void>(y), n, S(s));
     check_launch("gelu_forward");

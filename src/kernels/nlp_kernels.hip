@@ -403,6 +403,182 @@ __global__ void __launch_bounds__(256) dropout_bwd_kernel(const T* __restrict__ 
   }
 }
 
+
+// ------------------------------------------------------------------ residual + dropout + LayerNorm
+// The post-LN transformer sub-layer tail  y = LayerNorm(x + dropout(h)):  one wave per row draws the
+// dropout keep bits (the same Philox counters as dropout_fwd_kernel: one draw per 8-element vector),
+// forms s = x + keep*h/(1-p) (kept, rounded to T, for the backward), normalises it and writes y -- the
+// separate dropout, add and LayerNorm passes (and their launches) collapse into one read of x and h.
+template <typename T, int VPL, bool DROP>
+__global__ void __launch_bounds__(256) add_dropout_ln_fwd_kernel(
+    const T* __restrict__ x, const T* __restrict__ h, const void* __restrict__ gamma, const void* __restrict__ beta,
+    int pt, T* __restrict__ y, T* __restrict__ s_out, uint8_t* __restrict__ mask, float* __restrict__ mean_out,
+    float* __restrict__ rstd_out, int M, int D, float eps, float p, uint64_t seed,
+    const uint64_t* __restrict__ seed_base) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nv = D >> 3;
+  if (DROP && seed_base != nullptr) seed += seed_base[0] * 0x9E3779B97F4A7C15ull;
+  const uint32_t thresh = (uint32_t)fminf(p * 4294967296.f, 4294967295.f);
+  const float sc = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  const T* xr = x + (int64_t)row * D;
+  const T* hr = h + (int64_t)row * D;
+  T* sr = s_out + (int64_t)row * D;
+  float v[VPL][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + j * 64;
+    if (c < nv) {
+      float xv[8], hv[8];
+      ld8(xr + c * 8, xv);
+      ld8(hr + c * 8, hv);
+      if (DROP) {
+        const int64_t vec = (int64_t)row * nv + c;
+        const uint4 r0 = Philox::run(make_uint4((uint32_t)vec, (uint32_t)(vec >> 32), 0u, 0u), key);
+        const uint4 r1 = Philox::run(make_uint4((uint32_t)vec, (uint32_t)(vec >> 32), 1u, 0u), key);
+        const uint32_t u[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+        uint32_t bits = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const bool keep = u[i] >= thresh;
+          bits |= (keep ? 1u : 0u) << i;
+          hv[i] = keep ? hv[i] * sc : 0.f;
+        }
+        mask[vec] = (uint8_t)bits;
+      }
+      Vec8<T> t;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t.set(i, xv[i] + hv[i]);
+      t.store(sr + c * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        v[j][i] = t.get(i);          // the rounded sum: what the backward re-reads
+        sum += v[j][i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[j][i] = 0.f;
+    }
+  }
+  const float mean = wave_sum(sum) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    if (lane + j * 64 < nv) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = v[j][i] - mean;
+        q += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / D + eps);
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+  T* yr = y + (int64_t)row * D;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + j * 64;
+    if (c < nv) {
+      float g[8], b[8], o[8];
+      ld8p<T>(gamma, c * 8, pt, g);
+      ld8p<T>(beta, c * 8, pt, b);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (v[j][i] - mean) * rstd * g[i] + b[i];
+      st8(yr + c * 8, o);
+    }
+  }
+}
+
+// its backward: ds = LayerNorm'(s) dy (the residual branch's gradient) and dh = keep * ds / (1-p) in one
+// pass, with the dgamma / dbeta column partials of layernorm_bwd_kernel
+template <typename T, int VPL, bool DROP>
+__global__ void __launch_bounds__(256) add_dropout_ln_bwd_kernel(
+    const T* __restrict__ x, const T* __restrict__ dy, const void* __restrict__ gamma, int pt,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const uint8_t* __restrict__ mask, float p,
+    T* __restrict__ dx, T* __restrict__ dh, float* __restrict__ part, int M, int D) {
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int nv = D >> 3;
+  const float sc = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  float pg[VPL][8], pb[VPL][8];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pg[j][i] = pb[j][i] = 0.f;
+  for (int row = blockIdx.x * 4 + w; row < M; row += gridDim.x * 4) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    const T* xr = x + (int64_t)row * D;
+    const T* dyr = dy + (int64_t)row * D;
+    float xh[VPL][8], gd[VPL][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + j * 64;
+      if (c < nv) {
+        float xv[8], dv[8], g[8];
+        ld8(xr + c * 8, xv);
+        ld8(dyr + c * 8, dv);
+        ld8p<T>(gamma, c * 8, pt, g);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          xh[j][i] = (xv[i] - mean) * rstd;
+          gd[j][i] = dv[i] * g[i];
+          s1 += gd[j][i];
+          s2 += gd[j][i] * xh[j][i];
+          pg[j][i] += dv[i] * xh[j][i];
+          pb[j][i] += dv[i];
+        }
+      }
+    }
+    const float m1 = wave_sum(s1) / D, m2 = wave_sum(s2) / D;
+    T* dxr = dx + (int64_t)row * D;
+    T* dhr = dh + (int64_t)row * D;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + j * 64;
+      if (c < nv) {
+        float o[8], oh[8];
+        const uint32_t bits = DROP ? mask[(int64_t)row * nv + c] : 0xffu;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          o[i] = rstd * (gd[j][i] - m1 - xh[j][i] * m2);
+          oh[i] = DROP ? (((bits >> i) & 1u) ? o[i] * sc : 0.f) : o[i];
+        }
+        st8(dxr + c * 8, o);
+        st8(dhr + c * 8, oh);
+      }
+    }
+  }
+  __shared__ float sh[2][4][512];
+  float* pgo = part + (int64_t)blockIdx.x * 2 * D;
+  for (int base = 0; base < D; base += 512) {
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + j * 64;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int col = c * 8 + i - base;
+        if (c < nv && col >= 0 && col < 512) {
+          sh[0][w][col] = pg[j][i];
+          sh[1][w][col] = pb[j][i];
+        }
+      }
+    }
+    __syncthreads();
+    for (int col = threadIdx.x; col < 512 && base + col < D; col += 256) {
+      pgo[base + col] = sh[0][0][col] + sh[0][1][col] + sh[0][2][col] + sh[0][3][col];
+      pgo[D + base + col] = sh[1][0][col] + sh[1][1][col] + sh[1][2][col] + sh[1][3][col];
+    }
+    __syncthreads();
+  }
+}
+
 inline int ew_blocks(int64_t nvec) {
   int64_t b = (nvec + 255) / 256;
   return (int)(b > 256 * 16 ? 256 * 16 : (b < 1 ? 1 : b));
@@ -465,6 +641,71 @@ void layernorm_backward(int dtype, const void* x, const void* dy, const void* ga
                                                                      static_cast<const T*>(dy), gamma, pt, mean, rstd,
                                                                      static_cast<T*>(dx), part, M, D)))
   // dgamma / dbeta straight into the parameters' gradient buffers in their own dtype (fp32 / bf16 / fp16)
+  MXAMD_DTYPE_SWITCH(gdtype, hipLaunchKernelGGL((column_sum_kernel<T>), dim3((2 * D + 7) / 8), dim3(256), 0, s,
+                                                part, nb, 2 * D, static_cast<T*>(dgamma), static_cast<T*>(dbeta), D,
+                                                accum))
+}
+
+
+// y = LayerNorm(x + dropout_p(h)); s = x + dropout_p(h) (T), mask (1 bit per element, p > 0 only)
+void add_dropout_ln_forward(int dtype, const void* x, const void* h, const void* gamma, const void* beta, int pt,
+                            void* y, void* s_out, uint8_t* mask, float* mean, float* rstd, int M, int D, float eps,
+                            float p, uint64_t seed, const uint64_t* seed_base, hipStream_t s) {
+  MXAMD_HOST_CHECK(D % 8 == 0 && (dtype == kF16 || dtype == kBF16), "add_dropout_ln: D % 8 == 0, f16/bf16");
+  MXAMD_HOST_CHECK(p == 0.f || mask != nullptr, "add_dropout_ln: dropout needs a mask buffer");
+  const int vpl = pick_vpl(D);
+  dim3 grid((M + 3) / 4);
+  if (dtype == kF16) {
+    typedef __half T;
+    if (p > 0.f)
+      MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((add_dropout_ln_fwd_kernel<T, VPL, true>), grid, dim3(256), 0, s,
+                                               (const T*)x, (const T*)h, gamma, beta, pt, (T*)y, (T*)s_out, mask, mean,
+                                               rstd, M, D, eps, p, seed, seed_base))
+    else
+      MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((add_dropout_ln_fwd_kernel<T, VPL, false>), grid, dim3(256), 0, s,
+                                               (const T*)x, (const T*)h, gamma, beta, pt, (T*)y, (T*)s_out, mask, mean,
+                                               rstd, M, D, eps, p, seed, seed_base))
+  } else {
+    typedef __hip_bfloat16 T;
+    if (p > 0.f)
+      MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((add_dropout_ln_fwd_kernel<T, VPL, true>), grid, dim3(256), 0, s,
+                                               (const T*)x, (const T*)h, gamma, beta, pt, (T*)y, (T*)s_out, mask, mean,
+                                               rstd, M, D, eps, p, seed, seed_base))
+    else
+      MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((add_dropout_ln_fwd_kernel<T, VPL, false>), grid, dim3(256), 0, s,
+                                               (const T*)x, (const T*)h, gamma, beta, pt, (T*)y, (T*)s_out, mask, mean,
+                                               rstd, M, D, eps, p, seed, seed_base))
+  }
+}
+
+// ds (residual gradient) and dh (= dropout'(ds)) of add_dropout_ln_forward; dgamma / dbeta as layernorm_backward
+void add_dropout_ln_backward(int dtype, const void* s_in, const void* dy, const void* gamma, int pt, const float* mean,
+                             const float* rstd, const uint8_t* mask, float p, void* ds, void* dh, float* part,
+                             void* dgamma, void* dbeta, int gdtype, int accum, int M, int D, hipStream_t s) {
+  MXAMD_HOST_CHECK(D % 8 == 0 && (dtype == kF16 || dtype == kBF16), "add_dropout_ln: D % 8 == 0, f16/bf16");
+  const int vpl = pick_vpl(D);
+  const int nb = layernorm_bwd_partials(M);
+  if (dtype == kF16) {
+    typedef __half T;
+    if (p > 0.f)
+      MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((add_dropout_ln_bwd_kernel<T, VPL, true>), dim3(nb), dim3(256), 0, s,
+                                               (const T*)s_in, (const T*)dy, gamma, pt, mean, rstd, mask, p, (T*)ds,
+                                               (T*)dh, part, M, D))
+    else
+      MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((add_dropout_ln_bwd_kernel<T, VPL, false>), dim3(nb), dim3(256), 0, s,
+                                               (const T*)s_in, (const T*)dy, gamma, pt, mean, rstd, mask, p, (T*)ds,
+                                               (T*)dh, part, M, D))
+  } else {
+    typedef __hip_bfloat16 T;
+    if (p > 0.f)
+      MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((add_dropout_ln_bwd_kernel<T, VPL, true>), dim3(nb), dim3(256), 0, s,
+                                               (const T*)s_in, (const T*)dy, gamma, pt, mean, rstd, mask, p, (T*)ds,
+                                               (T*)dh, part, M, D))
+    else
+      MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((add_dropout_ln_bwd_kernel<T, VPL, false>), dim3(nb), dim3(256), 0, s,
+                                               (const T*)s_in, (const T*)dy, gamma, pt, mean, rstd, mask, p, (T*)ds,
+                                               (T*)dh, part, M, D))
+  }
   MXAMD_DTYPE_SWITCH(gdtype, hipLaunchKernelGGL((column_sum_kernel<T>), dim3((2 * D + 7) / 8), dim3(256), 0, s,
                                                 part, nb, 2 * D, static_cast<T*>(dgamma), static_cast<T*>(dbeta), D,
                                                 accum))
