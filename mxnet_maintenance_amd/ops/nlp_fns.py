@@ -397,6 +397,12 @@ def _fc_wgrad_cands(dy2, x2, w):
     if K % 64 == 0 and N % 64 == 0 and x2.data_ptr() % 16 == 0:
         c.append(('hip', lambda: _KF.conv_wgrad(x2.view(M, 1, 1, K), dy2.view(M, 1, 1, N), (N, 1, 1, K), (1, 1),
                                                 (0, 0)).view(N, K)))
+        # the persistent LDS-DMA ring weight-gradient kernels (conv_wgrad.hip), TN on a [M,1,1,*] view
+        lib = _K.lib()
+        for v in range(1, 10):
+            if lib.conv_nhwc_wgrad_ring_ok(K, N, 1, 1, v):
+                c.append(('ring%d' % v, lambda v=v: _KF.conv_wgrad(x2.view(M, 1, 1, K), dy2.view(M, 1, 1, N),
+                                                                   (N, 1, 1, K), (1, 1), (0, 0), ring=v).view(N, K)))
     c.append(('mm', lambda: torch.mm(dy2.t(), x2)))
     return c
 
@@ -446,9 +452,9 @@ def _fc_wgrad(dy2, x2, w, w_ref):
     tgt = _leaf_grad(w_ref, dtype=w.dtype) if (algo is not None and _FC_DIRECT) else None
     if tgt is not None:
         N, K = w.shape
-        if algo == 'hip':
+        if algo == 'hip' or algo.startswith('ring'):
             _KF.conv_wgrad(x2.view(-1, 1, 1, K), dy2.view(-1, 1, 1, N), (N, 1, 1, K), (1, 1), (0, 0),
-                           out=tgt.view(N, 1, 1, K), accum=True)
+                           out=tgt.view(N, 1, 1, K), accum=True, ring=int(algo[4:]) if algo != 'hip' else 0)
         elif algo.startswith('sk'):
             _splitk_wgrad(dy2, x2, int(algo[2:]), tgt.view(N, K), True)
         else:
