@@ -34,7 +34,10 @@ class _ResidualLayerNorm(nn.LayerNorm):
         self._p = dropout
 
     def hybrid_forward(self, F, data, residual, gamma, beta):
-        return F.contrib.add_dropout_layernorm(data, residual, gamma, beta, p=self._p, eps=self._epsilon)
+        # data = sub-layer(residual) starts with a Dense on residual: its data gradient absorbs the
+        # residual gradient (no separate accumulation)
+        return F.contrib.add_dropout_layernorm(data, residual, gamma, beta, p=self._p, eps=self._epsilon,
+                                               fuse_residual_grad=True)
 
 
 class BERTEncoderCell(HybridBlock):

@@ -329,11 +329,12 @@ def layer_norm(data, gamma, beta, eps, want_stats=True):
     return y.to(data.dtype), mean.to(data.dtype), std.to(data.dtype)
 
 
-def add_dropout_layer_norm(x, h, gamma, beta, eps, p):
+def add_dropout_layer_norm(x, h, gamma, beta, eps, p, handoff=False):
     """LayerNorm(x + dropout_p(h)) over the last axis: one HIP kernel each way on the GPU."""
-    if (_use_hip(x) and _K.ln_ok(x) and h.shape == x.shape and h.dtype == x.dtype and h.is_contiguous()
+    if (_use_hip(x) and x.dtype in (torch.float16, torch.bfloat16) and _K.ln_ok(x) and h.shape == x.shape
+            and h.dtype == x.dtype and h.is_contiguous()
             and h.data_ptr() % 16 == 0 and 0.0 <= p < 1.0):
-        return _K.AddDropoutLN.apply(x, h, gamma, beta, eps, p)
+        return _K.AddDropoutLN.apply(x, h, gamma, beta, eps, p, bool(handoff))
     if p > 0:
         h = h * (torch.rand_like(h, dtype=torch.float32) >= p).to(h.dtype) / (1 - p)
     return layer_norm(x + h, gamma, beta, eps, False)[0]

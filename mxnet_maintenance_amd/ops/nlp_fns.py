@@ -99,16 +99,25 @@ class LayerNorm(torch.autograd.Function):
                 db.view(beta.shape).to(beta.dtype) if need_b else None, None, None)
 
 
+# residual-gradient handoff to the Dense data gradient and bias gradients from the fused LayerNorm
+# backward's partials (MXAMD_RESIDUAL_HANDOFF=0: autograd accumulation and separate column sums, for A/B)
+_HANDOFF = __import__('os').environ.get('MXAMD_RESIDUAL_HANDOFF', '1') == '1'
+
+
 class AddDropoutLN(torch.autograd.Function):
     """y = LayerNorm(x + dropout_p(h)) over the last axis in one kernel (the post-LN transformer
     sub-layer tail); backward: the residual gradient, the dropout-masked branch gradient and
     dgamma / dbeta in one kernel."""
 
     @staticmethod
-    def forward(ctx, x, h, gamma, beta, eps, p):
+    def forward(ctx, x, h, gamma, beta, eps, p, handoff=False):
         lib = _K.lib()
         D = x.shape[-1]
         M = x.numel() // D
+        # handoff: x also feeds a FullyConnected (Linear below) whose backward runs after this one (a
+        # transformer sub-layer: x -> Dense -> ... -> h); the residual gradient is then added by that
+        # layer's data-gradient GEMM (addend) instead of by a separate autograd accumulation
+        ctx.res_src = x if (handoff and _HANDOFF and getattr(x, '_mxamd_fc_input', False)) else None
         pt = int(gamma.dtype == x.dtype and beta.dtype == x.dtype and gamma.is_contiguous() and beta.is_contiguous()
                  and gamma.data_ptr() % 16 == 0 and beta.data_ptr() % 16 == 0)
         g = gamma if pt else _f32(gamma)
@@ -149,14 +158,23 @@ class AddDropoutLN(torch.autograd.Function):
         else:
             out = torch.empty(2, D, dtype=torch.float32, device=sm.device)
             dg, db, accum, gdt = out[0], out[1], 0, _DT[torch.float32]
+        # column sums of dh (partials per block): the bias gradient of the Linear that produced h
+        hpart = torch.empty(nb * D, dtype=torch.float32, device=sm.device)
         lib.add_dropout_ln_backward(_DT[sm.dtype], sm.data_ptr(), gy.data_ptr(), g.data_ptr(), pt,
                                     stats[0].data_ptr(), stats[1].data_ptr(), _p(mask), p, ds.data_ptr(),
-                                    dh.data_ptr(), part.data_ptr(), dg.data_ptr(), db.data_ptr(), gdt, accum, M, D,
-                                    _stream())
+                                    dh.data_ptr(), part.data_ptr(), hpart.data_ptr(), dg.data_ptr(), db.data_ptr(),
+                                    gdt, accum, M, D, _stream())
+        if _HANDOFF:
+            dh._mxamd_bias_part = (hpart, nb, dh._version)
+        dx = ds
+        if ctx.res_src is not None and ctx.needs_input_grad[0]:
+            ctx.res_src._mxamd_res_grad = ds
+            dx = None
+        ctx.res_src = None
         if accum:
-            return ds, dh, None, None, None, None
-        return (ds, dh, dg.view(gamma.shape).to(gamma.dtype) if need_g else None,
-                db.view(beta.shape).to(beta.dtype) if need_b else None, None, None)
+            return dx, dh, None, None, None, None, None
+        return (dx, dh, dg.view(gamma.shape).to(gamma.dtype) if need_g else None,
+                db.view(beta.shape).to(beta.dtype) if need_b else None, None, None, None)
 
 
 class GELU(torch.autograd.Function):
@@ -349,10 +367,28 @@ def _fc_fwd_cands(x2, w, b):
     return c
 
 
-def _fc_dgrad_cands(dy2, w):
+def _fc_dgrad_cands(dy2, w, addend=None):
+    """dX = dY . W (+ addend: a residual gradient folded into the GEMM epilogue / beta = 1)."""
     M, N = dy2.shape
     K = w.shape[1]
     c = []
+    if addend is not None:
+        if N % 32 == 0 and K % 64 == 0 and dy2.data_ptr() % 16 == 0:
+            for v in _KF._fwd_variants(N, K, False, ktot=N):
+                if v in _KF._BIG_VARIANTS and v not in _KF._BIG_SKINNY:
+                    c.append(('hip%d' % v, lambda v=v: _KF.conv_fwd(dy2.view(M, 1, 1, N),
+                                                                    w.t().contiguous().view(K, 1, 1, N), (1, 1),
+                                                                    (0, 0), None, v,
+                                                                    addend=addend.view(M, 1, 1, K)).view(M, K)))
+        if (N % 64 == 0 and K % 64 == 0 and dy2.is_cuda and dy2.dtype in _G._DT and w.dtype == dy2.dtype
+                and dy2.is_contiguous() and dy2.data_ptr() % 16 == 0 and _K.available()):
+            for cfg in _G.configs(M, K, N, _G.AUTOTUNE_TILES):
+                c.append(('gemm%ds%d' % cfg, lambda cfg=cfg: _G.gemm_nt(dy2, w.t().contiguous(), addend=addend,
+                                                                         cfg=cfg)))
+        # the library GEMM plus one add: torch.addmm would first copy the addend into its output and
+        # then run a beta = 1 GEMM, slower than both (measured in the BERT step)
+        c.append(('mm', lambda: torch.mm(dy2, w).add_(addend)))
+        return c
     if N % 32 == 0 and K % 64 == 0:
         c.append(('hip', lambda: _KF.conv_fwd(dy2.view(M, 1, 1, N), w.t().contiguous().view(K, 1, 1, N), (1, 1),
                                               (0, 0)).view(M, K)))
@@ -421,6 +457,9 @@ class Linear(torch.autograd.Function):
         ctx.bdt = b.dtype if b is not None else None
         ctx.xshape = x.shape
         ctx.refs = (w, b)
+        # a residual gradient may be handed to this layer's data gradient (AddDropoutLN handoff)
+        x._mxamd_fc_input = True
+        ctx.x_src = x
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -430,13 +469,28 @@ class Linear(torch.autograd.Function):
         N = w.shape[0]
         dy2 = dy.reshape(-1, N).contiguous()
         dx = dw = db = None
+        res = getattr(ctx.x_src, '_mxamd_res_grad', None)
+        if res is not None:
+            del ctx.x_src._mxamd_res_grad
+        ctx.x_src = None
         if ctx.needs_input_grad[0]:
-            key = ('fc_dgrad', tuple(dy2.shape), tuple(w.shape), dy.dtype)
-            dx = _KF._select(key, _fc_dgrad_cands(dy2, w.contiguous()), 'mm').view(ctx.xshape)
+            if res is not None:
+                add = res.reshape(-1, w.shape[1]).contiguous()
+                key = ('fc_dgrad_add', tuple(dy2.shape), tuple(w.shape), dy.dtype)
+                dx = _KF._select(key, _fc_dgrad_cands(dy2, w.contiguous(), add), 'mm').view(ctx.xshape)
+            else:
+                key = ('fc_dgrad', tuple(dy2.shape), tuple(w.shape), dy.dtype)
+                dx = _KF._select(key, _fc_dgrad_cands(dy2, w.contiguous()), 'mm').view(ctx.xshape)
+        elif res is not None:
+            dx = res
         if ctx.needs_input_grad[1]:
             dw = _fc_wgrad(dy2, x2, w, w_ref)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = bias_grad(dy2, b_ref, ctx.bdt)
+            bp = getattr(dy, '_mxamd_bias_part', None)
+            if bp is not None and bp[2] == dy._version and dy.shape[-1] == N:
+                db = _bias_from_partials(bp[0], bp[1], N, b_ref, ctx.bdt, dy.device)
+            else:
+                db = bias_grad(dy2, b_ref, ctx.bdt)
         return dx, dw, db
 
 
@@ -487,6 +541,16 @@ def bias_grad(dy2, b_ref, bdt):
     if tgt is not None:
         return None
     return out.to(bdt)
+
+
+def _bias_from_partials(part, nb, N, b_ref, bdt, dev):
+    """db from column partials an earlier kernel already reduced (add_dropout_ln backward): one small
+    column-sum launch, accumulated straight into the bias's .grad buffer when possible."""
+    tgt = _leaf_grad(b_ref, N, dtype=bdt) if (bdt in _DT and _FC_DIRECT) else None
+    out = tgt if tgt is not None else torch.empty(N, dtype=torch.float32, device=dev)
+    _K.lib().column_sum_partials(_DT[out.dtype], part.data_ptr(), nb, N, out.data_ptr(), int(tgt is not None),
+                                 _stream())
+    return None if tgt is not None else out.to(bdt)
 
 
 _IDX_T = {torch.float32: 0, torch.int64: 1, torch.int32: 2}

@@ -688,13 +688,16 @@ def _adln_infer(s):
 @register('_contrib_add_dropout_layernorm', aliases=('add_dropout_layernorm',),
           arg_names=('data', 'residual', 'gamma', 'beta'),
           infer_params=lambda s, a: _adln_infer(s),
-          params={'p': ('float', 0.0), 'eps': ('float', 1e-5)})
-def add_dropout_layernorm(data, residual, gamma, beta, p=0.0, eps=1e-5):
+          params={'p': ('float', 0.0), 'eps': ('float', 1e-5), 'fuse_residual_grad': ('bool', False)})
+def add_dropout_layernorm(data, residual, gamma, beta, p=0.0, eps=1e-5, fuse_residual_grad=False):
     """LayerNorm(residual + Dropout(data, p)) over the last axis -- the post-LN transformer sub-layer
     tail as one fused operator (the reference composes Dropout, elemwise_add and LayerNorm:
-    src/operator/nn/dropout-inl.h, layer_norm-inl.h); dropout is active in training mode only."""
+    src/operator/nn/dropout-inl.h, layer_norm-inl.h); dropout is active in training mode only.
+    ``fuse_residual_grad``: ``data`` is computed from ``residual`` through a FullyConnected (a
+    transformer sub-layer), so that layer's data-gradient GEMM adds the residual gradient (GPU)."""
     active = _state.STATE.training and p > 0
-    return hip_ops.add_dropout_layer_norm(residual, data, gamma, beta, eps, p if active else 0.0)
+    return hip_ops.add_dropout_layer_norm(residual, data, gamma, beta, eps, p if active else 0.0,
+                                          fuse_residual_grad)
 
 
 @register('GroupNorm', arg_names=('data', 'gamma', 'beta'), num_outputs=3, num_visible_outputs=_ln_nvis,

@@ -115,7 +115,9 @@ void add_dropout_ln_forward(int dtype, const void* x, const void* h, const void*
                             float p, uint64_t seed, const uint64_t* seed_base, hipStream_t s);
 void add_dropout_ln_backward(int dtype, const void* s_in, const void* dy, const void* gamma, int pt, const float* mean,
                              const float* rstd, const uint8_t* mask, float p, void* ds, void* dh, float* part,
-                             void* dgamma, void* dbeta, int gdtype, int accum, int M, int D, hipStream_t s);
+                             float* hpart, void* dgamma, void* dbeta, int gdtype, int accum, int M, int D,
+                             hipStream_t s);
+void column_sum_partials(int gdtype, const float* part, int nb, int ncol, void* out, int accum, hipStream_t s);
 void gelu_forward(int dtype, const void* x, void* y, int64_t n, hipStream_t s);
 void gelu_backward(int dtype, const void* x, const void* dy, void* dx, int64_t n, hipStream_t s);
 void softmax_forward(int dtype, int log, const void* x, void* y, int M, int L, float scale, hipStream_t s);
@@ -657,12 +659,16 @@ PYBIND11_MODULE(_hip_kernels, m) {
   });
   m.def("add_dropout_ln_backward", [](int dt, uintptr_t sum, uintptr_t dy, uintptr_t g, int pt, uintptr_t mean,
                                       uintptr_t rstd, uintptr_t mask, float p, uintptr_t ds, uintptr_t dh,
-                                      uintptr_t part, uintptr_t dg, uintptr_t db, int gdt, int accum, int M, int D,
-                                      uintptr_t s) {
+                                      uintptr_t part, uintptr_t hpart, uintptr_t dg, uintptr_t db, int gdt, int accum,
+                                      int M, int D, uintptr_t s) {
     add_dropout_ln_backward(dt, P<void>(sum), P<void>(dy), P<void>(g), pt, P<float>(mean), P<float>(rstd),
-                            P<uint8_t>(mask), p, P<void>(ds), P<void>(dh), P<float>(part), P<void>(dg), P<void>(db),
-                            gdt, accum, M, D, S(s));
+                            P<uint8_t>(mask), p, P<void>(ds), P<void>(dh), P<float>(part), P<float>(hpart),
+                            P<void>(dg), P<void>(db), gdt, accum, M, D, S(s));
     check_launch("add_dropout_ln_backward");
+  });
+  m.def("column_sum_partials", [](int gdt, uintptr_t part, int nb, int ncol, uintptr_t out, int accum, uintptr_t s) {
+    column_sum_partials(gdt, P<float>(part), nb, ncol, P<void>(out), accum, S(s));
+    check_launch("column_sum_partials");
   });
   m.def("gelu_forward", [](int dt, uintptr_t x, uintptr_t y, int64_t n, uintptr_t s) {
     gelu_forward(dt, P<void>(x), P<void>(y), n, S(s));

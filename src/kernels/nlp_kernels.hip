@@ -501,16 +501,18 @@ template <typename T, int VPL, bool DROP>
 __global__ void __launch_bounds__(256) add_dropout_ln_bwd_kernel(
     const T* __restrict__ x, const T* __restrict__ dy, const void* __restrict__ gamma, int pt,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const uint8_t* __restrict__ mask, float p,
-    T* __restrict__ dx, T* __restrict__ dh, float* __restrict__ part, int M, int D) {
+    T* __restrict__ dx, T* __restrict__ dh, float* __restrict__ part, float* __restrict__ hpart, int M, int D) {
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int nv = D >> 3;
   const float sc = p < 1.f ? 1.f / (1.f - p) : 0.f;
-  float pg[VPL][8], pb[VPL][8];
+  // pg / pb: dgamma / dbeta column partials; ph (hpart != null): column sums of dh -- the bias gradient
+  // of the layer that produced h, so that layer's backward needs no reduction pass of its own
+  float pg[VPL][8], pb[VPL][8], ph[VPL][8];
 #pragma unroll
   for (int j = 0; j < VPL; ++j)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) pg[j][i] = pb[j][i] = 0.f;
+    for (int i = 0; i < 8; ++i) pg[j][i] = pb[j][i] = ph[j][i] = 0.f;
   for (int row = blockIdx.x * 4 + w; row < M; row += gridDim.x * 4) {
     const float mean = mean_in[row], rstd = rstd_in[row];
     const T* xr = x + (int64_t)row * D;
@@ -551,12 +553,19 @@ __global__ void __launch_bounds__(256) add_dropout_ln_bwd_kernel(
           oh[i] = DROP ? (((bits >> i) & 1u) ? o[i] * sc : 0.f) : o[i];
         }
         st8(dxr + c * 8, o);
-        st8(dhr + c * 8, oh);
+        // the sums use the stored (rounded) dh, as a separate reduction over dh would
+        Vec8<T> th;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) th.set(i, oh[i]);
+        th.store(dhr + c * 8);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) ph[j][i] += th.get(i);
       }
     }
   }
-  __shared__ float sh[2][4][512];
+  __shared__ float sh[3][4][512];
   float* pgo = part + (int64_t)blockIdx.x * 2 * D;
+  float* pho = hpart != nullptr ? hpart + (int64_t)blockIdx.x * D : nullptr;
   for (int base = 0; base < D; base += 512) {
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
@@ -567,6 +576,7 @@ __global__ void __launch_bounds__(256) add_dropout_ln_bwd_kernel(
         if (c < nv && col >= 0 && col < 512) {
           sh[0][w][col] = pg[j][i];
           sh[1][w][col] = pb[j][i];
+          sh[2][w][col] = ph[j][i];
         }
       }
     }
@@ -574,6 +584,7 @@ __global__ void __launch_bounds__(256) add_dropout_ln_bwd_kernel(
     for (int col = threadIdx.x; col < 512 && base + col < D; col += 256) {
       pgo[base + col] = sh[0][0][col] + sh[0][1][col] + sh[0][2][col] + sh[0][3][col];
       pgo[D + base + col] = sh[1][0][col] + sh[1][1][col] + sh[1][2][col] + sh[1][3][col];
+      if (pho != nullptr) pho[base + col] = sh[2][0][col] + sh[2][1][col] + sh[2][2][col] + sh[2][3][col];
     }
     __syncthreads();
   }
@@ -681,7 +692,8 @@ void add_dropout_ln_forward(int dtype, const void* x, const void* h, const void*
 // ds (residual gradient) and dh (= dropout'(ds)) of add_dropout_ln_forward; dgamma / dbeta as layernorm_backward
 void add_dropout_ln_backward(int dtype, const void* s_in, const void* dy, const void* gamma, int pt, const float* mean,
                              const float* rstd, const uint8_t* mask, float p, void* ds, void* dh, float* part,
-                             void* dgamma, void* dbeta, int gdtype, int accum, int M, int D, hipStream_t s) {
+                             float* hpart, void* dgamma, void* dbeta, int gdtype, int accum, int M, int D,
+                             hipStream_t s) {
   MXAMD_HOST_CHECK(D % 8 == 0 && (dtype == kF16 || dtype == kBF16), "add_dropout_ln: D % 8 == 0, f16/bf16");
   const int vpl = pick_vpl(D);
   const int nb = layernorm_bwd_partials(M);
@@ -690,25 +702,31 @@ void add_dropout_ln_backward(int dtype, const void* s_in, const void* dy, const 
     if (p > 0.f)
       MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((add_dropout_ln_bwd_kernel<T, VPL, true>), dim3(nb), dim3(256), 0, s,
                                                (const T*)s_in, (const T*)dy, gamma, pt, mean, rstd, mask, p, (T*)ds,
-                                               (T*)dh, part, M, D))
+                                               (T*)dh, part, hpart, M, D))
     else
       MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((add_dropout_ln_bwd_kernel<T, VPL, false>), dim3(nb), dim3(256), 0, s,
                                                (const T*)s_in, (const T*)dy, gamma, pt, mean, rstd, mask, p, (T*)ds,
-                                               (T*)dh, part, M, D))
+                                               (T*)dh, part, hpart, M, D))
   } else {
     typedef __hip_bfloat16 T;
     if (p > 0.f)
       MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((add_dropout_ln_bwd_kernel<T, VPL, true>), dim3(nb), dim3(256), 0, s,
                                                (const T*)s_in, (const T*)dy, gamma, pt, mean, rstd, mask, p, (T*)ds,
-                                               (T*)dh, part, M, D))
+                                               (T*)dh, part, hpart, M, D))
     else
       MXAMD_VPL_SWITCH(vpl, hipLaunchKernelGGL((add_dropout_ln_bwd_kernel<T, VPL, false>), dim3(nb), dim3(256), 0, s,
                                                (const T*)s_in, (const T*)dy, gamma, pt, mean, rstd, mask, p, (T*)ds,
-                                               (T*)dh, part, M, D))
+                                               (T*)dh, part, hpart, M, D))
   }
   MXAMD_DTYPE_SWITCH(gdtype, hipLaunchKernelGGL((column_sum_kernel<T>), dim3((2 * D + 7) / 8), dim3(256), 0, s,
                                                 part, nb, 2 * D, static_cast<T*>(dgamma), static_cast<T*>(dbeta), D,
                                                 accum))
+}
+
+// out[c] (+)= sum_b part[b][c], c < ncol: the column partials an earlier kernel left (add_dropout_ln's dh sums)
+void column_sum_partials(int gdtype, const float* part, int nb, int ncol, void* out, int accum, hipStream_t s) {
+  MXAMD_DTYPE_SWITCH(gdtype, hipLaunchKernelGGL((column_sum_kernel<T>), dim3((ncol + 7) / 8), dim3(256), 0, s, part,
+                                                nb, ncol, static_cast<T*>(out), static_cast<T*>(out), ncol, accum))
 }
 
 void gelu_forward(int dtype, const void* x, void* y, int64_t n, hipStream_t s) {

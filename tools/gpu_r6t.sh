@@ -4,7 +4,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gemm.py > gpurun_out/r6t_tests.log 2>&1 || { echo TESTS FAILED; tail -30 gpurun_out/r6t_tests.log; exit 1; }
+timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gemm.py tests/test_add_dropout_ln.py tests/test_models.py > gpurun_out/r6t_tests.log 2>&1 || { echo TESTS FAILED; tail -30 gpurun_out/r6t_tests.log; exit 1; }
 tail -1 gpurun_out/r6t_tests.log
 MXAMD_BENCH_VERBOSE=1 timeout -k 10 400 python -u tools/bench_bert.py --graph --gemm-table none --steps 20 --warmup 5 > gpurun_out/r6t_bert.log 2>&1 || { echo BERT FAILED; tail -20 gpurun_out/r6t_bert.log; exit 1; }
 grep -v "algo" gpurun_out/r6t_bert.log | tail -1 | cut -c1-200
