@@ -110,7 +110,9 @@ __device__ __forceinline__ float sum16(float v) {
   return v;
 }
 
-constexpr int kWPitch = 8 * 32 * 2 + 16;   // LDS weight image [64 ch][8 rows][32 taps] row pitch (bytes)
+constexpr int kWPitch = 8 * 32 * 2 + 32;   // LDS weight image [64 ch][8 rows][32 taps] row pitch (bytes):
+                                           // 136 dwords, so the 16 lanes of a ds_read_b128 group start on
+                                           // distinct 4-bank slots (132 collided: 4(fr + fg))
 
 template <typename T>
 __global__ void __launch_bounds__(256) conv_stem_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w,
