@@ -115,13 +115,17 @@ constexpr int kWPitch = 8 * 32 * 2 + 32;   // LDS weight image [64 ch][8 rows][3
                                            // distinct 4-bank slots (132 collided: 4(fr + fg))
 
 template <typename T>
-__global__ void __launch_bounds__(256) conv_stem_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w,
+__global__ void __launch_bounds__(256, 3) conv_stem_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w,
                                                             T* __restrict__ y, StemGeom g,
                                                             float* __restrict__ part, int nparts) {
-  __shared__ __attribute__((aligned(16))) char smem[kPatchBytes + kPix * kOutPitch + 64 * kWPitch];
+  // the output image reuses the patch's LDS (a barrier separates the last patch read from the first
+  // image write): 53 KB per workgroup, three workgroups per CU -- the kernel waits on its input gathers
+  // for most of its cycles, and a third workgroup hides more of that latency
+  constexpr int kStage = kPatchBytes > kPix * kOutPitch ? kPatchBytes : kPix * kOutPitch;
+  __shared__ __attribute__((aligned(16))) char smem[kStage + 64 * kWPitch];
   char* patch = smem;
-  char* outimg = smem + kPatchBytes;
-  char* wimg = outimg + kPix * kOutPitch;
+  char* outimg = smem;
+  char* wimg = smem + kStage;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = tid >> 6;
@@ -176,6 +180,7 @@ __global__ void __launch_bounds__(256) conv_stem_fwd_kernel(const T* __restrict_
     }
 
     // epilogue: lane holds channels 16i + 4fg + q of pixel (row 2wv + jf, column fr)
+    __syncthreads();                     // every wave's patch reads done: the image overwrites the patch
     int n, oh0, ow0;
     tile_origin(g, tile, &n, &oh0, &ow0);
 #pragma unroll
@@ -386,9 +391,16 @@ void stem_check(int C, int K, int R, int S, int sh, int sw) {
 
 }  // namespace
 
+// forward: three resident workgroups per CU (53 KB of LDS each), persistent
 int conv_stem_grid(int N, int H, int W, int R, int S, int ph, int pw) {
   const StemGeom g = stem_geom(N, H, W, 1, 64, R, S, ph, pw);
-  return g.ntiles < 512 ? g.ntiles : 512;     // ~2 resident workgroups per CU (VGPR-bound), persistent
+  return g.ntiles < 768 ? g.ntiles : 768;
+}
+
+// weight gradient: ~2 resident workgroups per CU (VGPR-bound), one fp32 slab each
+static int stem_wgrad_grid(int N, int H, int W, int R, int S, int ph, int pw) {
+  const StemGeom g = stem_geom(N, H, W, 1, 64, R, S, ph, pw);
+  return g.ntiles < 512 ? g.ntiles : 512;
 }
 
 void conv_stem_fwd(int dtype, const void* x, const void* w, void* y, int N, int H, int W, int C, int K, int R, int S,
@@ -411,14 +423,14 @@ void conv_stem_fwd(int dtype, const void* x, const void* w, void* y, int N, int 
 }
 
 int64_t conv_stem_wgrad_workspace(int N, int H, int W, int R, int S, int ph, int pw) {
-  return static_cast<int64_t>(conv_stem_grid(N, H, W, R, S, ph, pw)) * 64 * 256;
+  return static_cast<int64_t>(stem_wgrad_grid(N, H, W, R, S, ph, pw)) * 64 * 256;
 }
 
 void conv_stem_wgrad(int dtype, const void* x, const void* dy, float* slab, int out_dtype, void* out, int accum, int N,
                      int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, hipStream_t s) {
   stem_check(C, K, R, S, sh, sw);
   const StemGeom g = stem_geom(N, H, W, C, K, R, S, ph, pw);
-  const int grid = conv_stem_grid(N, H, W, R, S, ph, pw);
+  const int grid = stem_wgrad_grid(N, H, W, R, S, ph, pw);
   if (g.ntiles == 0) return;
   if (dtype == kF16)
     hipLaunchKernelGGL(conv_stem_wgrad_kernel<__half>, dim3(grid), dim3(256), 0, s, static_cast<const __half*>(x),
