@@ -289,7 +289,9 @@ __global__ void __launch_bounds__(256) conv_stem_wgrad_kernel(const T* __restric
 
     const uint16_t* dyh = reinterpret_cast<const uint16_t*>(dyimg);
     const uint16_t* ph = reinterpret_cast<const uint16_t*>(patch);
-    // 4 K-steps of 32 pixels; lane's 8 pixels: p = 32 ks + 8 fg + j
+    // 4 K-steps of 32 pixels; lane's 8 pixels: p = 32 ks + 4 j + fg (any pixel order inside a K-step
+    // works as long as both operands use it; this one puts the four lane groups of a 16-bit LDS read on
+    // neighbouring pixels -- distinct banks -- where 8 fg + j put them 8 pixels = 0 mod 32 banks apart)
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       u32x4 af[4];
@@ -298,7 +300,7 @@ __global__ void __launch_bounds__(256) conv_stem_wgrad_kernel(const T* __restric
         uint16_t e[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int p = 32 * ks + 8 * fg + j;
+          const int p = 32 * ks + 4 * j + fg;
           e[j] = dyh[(p * kDyPitch) / 2 + 16 * i + fr];
         }
         af[i] = u32x4{static_cast<uint32_t>(e[0]) | (static_cast<uint32_t>(e[1]) << 16),
@@ -316,7 +318,7 @@ __global__ void __launch_bounds__(256) conv_stem_wgrad_kernel(const T* __restric
           uint16_t e[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const int p = 32 * ks + 8 * fg + j;
+            const int p = 32 * ks + 4 * j + fg;
             const int ohl = p / kTW, owl = p % kTW;
             e[j] = ph[((2 * ohl + r) * kPW + 2 * owl + s) * 4 + c];
           }
