@@ -240,7 +240,7 @@ constexpr int kTapFrags = 16;
 constexpr int kDyPitch = 64 * 2 + 16;
 
 template <typename T>
-__global__ void __launch_bounds__(256) conv_stem_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+__global__ void __launch_bounds__(256, 3) conv_stem_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                                               float* __restrict__ slab, StemGeom g) {
   __shared__ __attribute__((aligned(16))) char smem[kPatchBytes + kPix * kDyPitch];
   char* patch = smem;
@@ -399,10 +399,10 @@ int conv_stem_grid(int N, int H, int W, int R, int S, int ph, int pw) {
   return g.ntiles < 768 ? g.ntiles : 768;
 }
 
-// weight gradient: ~2 resident workgroups per CU (VGPR-bound), one fp32 slab each
+// weight gradient: three resident workgroups per CU (148 registers, 25 KB LDS), one fp32 slab each
 static int stem_wgrad_grid(int N, int H, int W, int R, int S, int ph, int pw) {
   const StemGeom g = stem_geom(N, H, W, 1, 64, R, S, ph, pw);
-  return g.ntiles < 512 ? g.ntiles : 512;
+  return g.ntiles < 768 ? g.ntiles : 768;
 }
 
 void conv_stem_fwd(int dtype, const void* x, const void* w, void* y, int N, int H, int W, int C, int K, int R, int S,
