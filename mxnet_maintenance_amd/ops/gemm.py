@@ -16,7 +16,8 @@ _DT = {torch.float16: 1, torch.bfloat16: 2}
 ACT = {None: 0, 'none': 0, 'relu': 1, 'gelu': 2}
 # tile config -> (BN output columns, BM output rows) of one workgroup (gemm.hip dispatch_gemm)
 TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (256, 128), 4: (128, 256), 5: (256, 256), 6: (64, 64),
-         7: (128, 128), 8: (256, 128), 9: (128, 64), 10: (64, 64), 11: (128, 256)}   # 7..11: 3-4 LDS stages
+         7: (128, 128), 8: (256, 128), 9: (128, 64), 10: (64, 64), 11: (128, 256),   # 7..11: 3-4 LDS stages
+         12: (128, 64), 13: (64, 128)}   # 3 stages at two workgroups per CU
 _WS = {}
 
 
@@ -47,7 +48,7 @@ def gemm_ok(a, b):
 
 
 # the tile configs worth timing per shape (the 3-4 stage rings measured no faster on MI355X)
-AUTOTUNE_TILES = (0, 1, 2, 3, 6)
+AUTOTUNE_TILES = (0, 1, 2, 3, 6, 12)
 
 
 def configs(M, N, K, tiles=None):

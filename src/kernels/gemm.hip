@@ -298,8 +298,10 @@ void launch_gemm(GemmArgs g, hipStream_t s) {
 // config -> (BN x BM) tile, LDS stages:
 //   0: 128x128 4w 2st   1: 128x64 4w 2st   2: 64x128 4w 2st   3: 256x128 8w 2st   4: 128x256 8w 2st
 //   5: 256x256 8w 2st   6: 64x64 2w 2st    7: 128x128 4w 3st  8: 256x128 8w 3st   9: 128x64 4w 4st
-//  10: 64x64 2w 4st    11: 128x256 8w 3st
-constexpr int kGemmCfgs = 12;
+//  10: 64x64 2w 4st    11: 128x256 8w 3st  12: 128x64 4w 3st  13: 64x128 4w 3st
+// (12 / 13: three 24 KB stages = 72 KB, so two workgroups still share a CU -- the 2-stage tiles wait on
+// their single look-ahead stage for ~55 % of their wave cycles, the 4-stage ones keep one workgroup per CU)
+constexpr int kGemmCfgs = 14;
 template <typename T>
 void dispatch_gemm(int cfg, const GemmArgs& g, hipStream_t s) {
   switch (cfg) {
@@ -315,6 +317,8 @@ void dispatch_gemm(int cfg, const GemmArgs& g, hipStream_t s) {
     case 9: launch_gemm<T, 2, 2, 2, 4>(g, s); break;
     case 10: launch_gemm<T, 1, 2, 2, 4>(g, s); break;
     case 11: launch_gemm<T, 2, 4, 4, 3>(g, s); break;
+    case 12: launch_gemm<T, 2, 2, 2, 3>(g, s); break;
+    case 13: launch_gemm<T, 1, 4, 2, 3>(g, s); break;
     default: throw std::runtime_error("gemm_nt: unknown tile config");
   }
 }
@@ -322,13 +326,13 @@ void dispatch_gemm(int cfg, const GemmArgs& g, hipStream_t s) {
 }  // namespace
 
 int gemm_nt_tile_n(int cfg) {
-  static const int bn[kGemmCfgs] = {128, 128, 64, 256, 128, 256, 64, 128, 256, 128, 64, 128};
+  static const int bn[kGemmCfgs] = {128, 128, 64, 256, 128, 256, 64, 128, 256, 128, 64, 128, 128, 64};
   MXAMD_HOST_CHECK(cfg >= 0 && cfg < kGemmCfgs, "gemm_nt: unknown tile config");
   return bn[cfg];
 }
 
 int gemm_nt_tile_m(int cfg) {
-  static const int bm[kGemmCfgs] = {128, 64, 128, 128, 256, 256, 64, 128, 128, 64, 64, 256};
+  static const int bm[kGemmCfgs] = {128, 64, 128, 128, 256, 256, 64, 128, 128, 64, 64, 256, 64, 128};
   MXAMD_HOST_CHECK(cfg >= 0 && cfg < kGemmCfgs, "gemm_nt: unknown tile config");
   return bm[cfg];
 }
