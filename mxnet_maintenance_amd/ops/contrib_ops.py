@@ -189,6 +189,7 @@ class _DeformConvRows(torch.autograd.Function):
         ctx.save_for_backward(x, offset, mask, wmat, cols)
         ctx.geom, ctx.g, ctx.has_bias = geom, g, bias is not None
         ctx.bdtype = None if bias is None else bias.dtype
+        ctx.b_ref = bias
         ctx.wdtype = weight.dtype
         return out.view(N, Ho, Wo, O).permute(0, 3, 1, 2)
 
@@ -254,7 +255,10 @@ class _DeformConvRows(torch.autograd.Function):
             lib.deform_col2im_coord(_DT[x.dtype], x.data_ptr(), offset.data_ptr(), mptr, gcols.data_ptr(),
                                     goff.data_ptr(), 0 if gmask is None else gmask.data_ptr(), g16, _stream())
             gx = gx32.to(x.dtype)
-        gb = go.float().sum(0).to(ctx.bdtype) if ctx.has_bias else None
+        gb = None
+        if ctx.has_bias:
+            from .nlp_fns import bias_grad
+            gb = bias_grad(go, ctx.b_ref, ctx.bdtype)
         return (gx, goff, gmask, gw.view(O, C // g, geom[6], geom[7]), gb, None, None)
 
 

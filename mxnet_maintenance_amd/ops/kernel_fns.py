@@ -1535,6 +1535,7 @@ class ConvNHWC(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.pad = stride, pad
         ctx.has_bias = bias is not None
+        ctx.b_ref = bias
         ctx.w_ref = w
         ctx.bn_src = getattr(x, '_mxamd_bn_src', None)
         return y
@@ -1558,8 +1559,15 @@ class ConvNHWC(torch.autograd.Function):
         if ctx.needs_input_grad[1] and not _WGRAD_SIDE[0]:
             dw = _wgrad(dy, x, w, ctx.w_ref, stride, pad)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = dy.float().sum(dim=(0, 1, 2))
+            db = _conv_bias_grad(dy, ctx.b_ref)
         return dx, dw, db, None, None, None
+
+
+def _conv_bias_grad(dy, b_ref):
+    """Bias gradient of an NHWC conv: column sums of dY [N*H*W, K] on the HIP reduce kernels, straight into
+    the bias's .grad buffer when it is a leaf (None returned then) -- no fp32 copy of dY."""
+    from .nlp_fns import bias_grad
+    return bias_grad(dy.reshape(-1, dy.shape[-1]), b_ref, b_ref.dtype)
 
 
 class ConvTeeNHWC(torch.autograd.Function):
@@ -1712,6 +1720,7 @@ class ConvDilNHWC(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.cfg = (tuple(stride), tuple(pad), tuple(dilate))
         ctx.has_bias = bias is not None
+        ctx.b_ref = bias
         return y
 
     @staticmethod
@@ -1744,7 +1753,7 @@ class ConvDilNHWC(torch.autograd.Function):
             cands.append(('miopen', lambda: _conv_bwd_dil_torch(dy, x, w, stride, pad, dil, (False, True))[1]))
             dw = _select(key, cands, cands[0][0]).to(w.dtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = dy.float().sum(dim=(0, 1, 2))
+            db = _conv_bias_grad(dy, ctx.b_ref)
         return dx, dw, db, None, None, None
 
 
