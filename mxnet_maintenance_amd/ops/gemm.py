@@ -17,7 +17,10 @@ ACT = {None: 0, 'none': 0, 'relu': 1, 'gelu': 2}
 # tile config -> (BN output columns, BM output rows) of one workgroup (gemm.hip dispatch_gemm)
 TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (256, 128), 4: (128, 256), 5: (256, 256), 6: (64, 64),
          7: (128, 128), 8: (256, 128), 9: (128, 64), 10: (64, 64), 11: (128, 256),   # 7..11: 3-4 LDS stages
-         12: (128, 64), 13: (64, 128)}   # 3 stages at two workgroups per CU
+         12: (128, 64), 13: (64, 128),   # 3 stages at two workgroups per CU
+         # whole-wave grids on transformer shapes (M = 4096: N = 768 -> 256 tiles of 192x64, N = 3072 ->
+         # 256 of 192x256 / 384x128, 512 of 192x128 at two workgroups per CU)
+         14: (192, 64), 15: (192, 128), 16: (192, 256), 17: (384, 128)}
 _WS = {}
 
 
@@ -48,7 +51,7 @@ def gemm_ok(a, b):
 
 
 # the tile configs worth timing per shape (the 3-4 stage rings measured no faster on MI355X)
-AUTOTUNE_TILES = (0, 1, 2, 3, 6, 12)
+AUTOTUNE_TILES = (0, 1, 2, 3, 6, 12, 14, 15, 16, 17)
 
 
 def configs(M, N, K, tiles=None):
@@ -83,14 +86,17 @@ def gemm_nt(a, b, bias=None, act=None, addend=None, out=None, out_f32=False, cfg
     if addend is not None:
         assert addend.dtype == odt and tuple(addend.shape) == (M, N) and addend.stride(1) == 1
         assert addend.stride(0) == out.stride(0)
-    b32 = None
+    b32, lowp = None, 0
     if bias is not None:
-        b32 = bias if (bias.dtype == torch.float32 and bias.is_contiguous()) else bias.float().contiguous()
+        if bias.dtype == a.dtype and bias.is_contiguous() and bias.data_ptr() % 8 == 0:
+            b32, lowp = bias, 1          # read in the operand dtype by the epilogue: no fp32 copy per call
+        else:
+            b32 = bias if (bias.dtype == torch.float32 and bias.is_contiguous()) else bias.float().contiguous()
     ws = _workspace(splits * M * N, a.device) if splits > 1 else None
     _K.lib().gemm_nt(_DT[a.dtype], a.data_ptr(), b.data_ptr(), 0 if b32 is None else b32.data_ptr(),
                      0 if addend is None else addend.data_ptr(), out.data_ptr(), int(bool(out_f32)), M, N, K,
                      a.stride(0), b.stride(0), out.stride(0), ACT[act], int(tile), int(splits),
-                     0 if ws is None else ws.data_ptr(), _stream())
+                     0 if ws is None else ws.data_ptr(), _stream(), bias_lowp=lowp)
     return out
 
 

@@ -192,7 +192,19 @@ class GELU(torch.autograd.Function):
         x, = ctx.saved_tensors
         gy = gy.contiguous()
         dx = torch.empty_like(x)
-        _K.lib().gelu_backward(_DT[x.dtype], x.data_ptr(), gy.data_ptr(), dx.data_ptr(), x.numel(), _stream())
+        lib = _K.lib()
+        N = x.shape[-1] if x.dim() else 1
+        if x.dim() >= 2 and N % 8 == 0 and x.is_contiguous() and hasattr(lib, 'gelu_backward_colpart'):
+            # the producing Dense's bias gradient rides along as column partials (consumed by
+            # Linear.backward through dx._mxamd_bias_part, like the add_dropout_layernorm tail's)
+            M = x.numel() // N
+            nb = lib.gelu_colpart_blocks(M, N)
+            part = torch.empty(nb, N, dtype=torch.float32, device=x.device)
+            lib.gelu_backward_colpart(_DT[x.dtype], x.data_ptr(), gy.data_ptr(), dx.data_ptr(), part.data_ptr(), M, N,
+                                      _stream())
+            dx._mxamd_bias_part = (part, nb, dx._version)
+            return dx
+        lib.gelu_backward(_DT[x.dtype], x.data_ptr(), gy.data_ptr(), dx.data_ptr(), x.numel(), _stream())
         return dx
 
 
@@ -367,6 +379,17 @@ def _fc_fwd_cands(x2, w, b):
     return c
 
 
+def _wt(w):
+    """W^T ([in][out]) for the K-contiguous data-gradient GEMMs: the in-tree LDS-tiled transpose
+    (pointwise.hip weight_taps_t, the conv data-gradient weight path with one tap) -- torch's strided
+    transpose copy of a 768 x 3072 bf16 weight took ~15 us, enough to hand every BERT data gradient to
+    hipBLASLt although the GEMM itself is faster in-tree (tools/bench_gemm.py)."""
+    N, K = w.shape
+    if w.is_contiguous() and N % 8 == 0 and K % 8 == 0:
+        return _KF._dgrad_weight(w.view(N, 1, 1, K)).view(K, N)
+    return w.t().contiguous()
+
+
 def _fc_dgrad_cands(dy2, w, addend=None):
     """dX = dY . W (+ addend: a residual gradient folded into the GEMM epilogue / beta = 1)."""
     M, N = dy2.shape
@@ -377,33 +400,33 @@ def _fc_dgrad_cands(dy2, w, addend=None):
             for v in _KF._fwd_variants(N, K, False, ktot=N):
                 if v in _KF._BIG_VARIANTS and v not in _KF._BIG_SKINNY:
                     c.append(('hip%d' % v, lambda v=v: _KF.conv_fwd(dy2.view(M, 1, 1, N),
-                                                                    w.t().contiguous().view(K, 1, 1, N), (1, 1),
+                                                                    _wt(w).view(K, 1, 1, N), (1, 1),
                                                                     (0, 0), None, v,
                                                                     addend=addend.view(M, 1, 1, K)).view(M, K)))
         if (N % 64 == 0 and K % 64 == 0 and dy2.is_cuda and dy2.dtype in _G._DT and w.dtype == dy2.dtype
                 and dy2.is_contiguous() and dy2.data_ptr() % 16 == 0 and _K.available()):
             for cfg in _G.configs(M, K, N, _G.AUTOTUNE_TILES):
-                c.append(('gemm%ds%d' % cfg, lambda cfg=cfg: _G.gemm_nt(dy2, w.t().contiguous(), addend=addend,
+                c.append(('gemm%ds%d' % cfg, lambda cfg=cfg: _G.gemm_nt(dy2, _wt(w), addend=addend,
                                                                          cfg=cfg)))
         # the library GEMM plus one add: torch.addmm would first copy the addend into its output and
         # then run a beta = 1 GEMM, slower than both (measured in the BERT step)
         c.append(('mm', lambda: torch.mm(dy2, w).add_(addend)))
         return c
     if N % 32 == 0 and K % 64 == 0:
-        c.append(('hip', lambda: _KF.conv_fwd(dy2.view(M, 1, 1, N), w.t().contiguous().view(K, 1, 1, N), (1, 1),
+        c.append(('hip', lambda: _KF.conv_fwd(dy2.view(M, 1, 1, N), _wt(w).view(K, 1, 1, N), (1, 1),
                                               (0, 0)).view(M, K)))
         if dy2.data_ptr() % 16 == 0:
             for v in _KF._fwd_variants(N, K, False, ktot=N):
                 if v >= 10:
                     c.append(('hip%d' % v, lambda v=v: _KF.conv_fwd(dy2.view(M, 1, 1, N),
-                                                                    w.t().contiguous().view(K, 1, 1, N), (1, 1),
+                                                                    _wt(w).view(K, 1, 1, N), (1, 1),
                                                                     (0, 0), None, v).view(M, K)))
     # dX = dY . W = dY . (W^T)^T: the GEMM kernel on a fresh W^T (a small copy; the weight may
     # change in place between steps through the fused optimizer's raw pointers, so no caching)
     if (N % 64 == 0 and K % 64 == 0 and dy2.is_cuda and dy2.dtype in _G._DT and w.dtype == dy2.dtype
             and dy2.is_contiguous() and dy2.data_ptr() % 16 == 0 and _K.available()):
         for cfg in _G.configs(M, K, N, _G.AUTOTUNE_TILES):
-            c.append(('gemm%ds%d' % cfg, lambda cfg=cfg: _G.gemm_nt(dy2, w.t().contiguous(), cfg=cfg)))
+            c.append(('gemm%ds%d' % cfg, lambda cfg=cfg: _G.gemm_nt(dy2, _wt(w), cfg=cfg)))
     c.append(('mm', lambda: torch.mm(dy2, w)))
     return c
 

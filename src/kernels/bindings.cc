@@ -28,8 +28,9 @@ void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, c
                       int relu_mode, int fix_gamma, int training, int accum, hipStream_t s, int ext_nblk, const void* ds_z, const float* ds_mean, float* ds_part);
 int bn_partials_rows(int64_t R, int C);
 int bn_tail_ds_rows(int64_t R, int C);
-void gemm_nt(int dtype, const void* a, const void* b, const float* bias, const void* addend, void* c, int out_f32,
-             int M, int N, int K, int lda, int ldb, int ldc, int act, int cfg, int splits, float* ws, hipStream_t s);
+void gemm_nt(int dtype, const void* a, const void* b, const void* bias, const void* addend, void* c, int out_f32,
+             int M, int N, int K, int lda, int ldb, int ldc, int act, int cfg, int splits, float* ws, hipStream_t s,
+             int bias_lowp);
 int gemm_nt_tile_n(int cfg);
 int gemm_nt_tile_m(int cfg);
 void int8_gemm(const int8_t* A, const int8_t* B, int32_t* C, int M, int N, int K, hipStream_t s);
@@ -120,6 +121,9 @@ void add_dropout_ln_backward(int dtype, const void* s_in, const void* dy, const 
 void column_sum_partials(int gdtype, const float* part, int nb, int ncol, void* out, int accum, hipStream_t s);
 void gelu_forward(int dtype, const void* x, void* y, int64_t n, hipStream_t s);
 void gelu_backward(int dtype, const void* x, const void* dy, void* dx, int64_t n, hipStream_t s);
+void gelu_backward_colpart(int dtype, const void* x, const void* dy, void* dx, float* part, int M, int N,
+                           hipStream_t s);
+int gelu_colpart_blocks(int M, int N);
 void softmax_forward(int dtype, int log, const void* x, void* y, int M, int L, float scale, hipStream_t s);
 void softmax_backward(int dtype, int log, const void* y, const void* dy, void* dx, int M, int L, float scale,
                       hipStream_t s);
@@ -266,13 +270,16 @@ PYBIND11_MODULE(_hip_kernels, m) {
     twobit_dequantize_sum(P<void>(packed), row_bytes, nrows, n, thr, P<float>(out), S(s));
     check_launch("twobit_dequantize_sum");
   });
+  // bias_lowp: the bias is in the operand dtype (read as such in the epilogue), else fp32
   m.def("gemm_nt", [](int dt, uintptr_t a, uintptr_t b, uintptr_t bias, uintptr_t addend, uintptr_t c, int out_f32,
                       int M, int N, int K, int lda, int ldb, int ldc, int act, int cfg, int splits, uintptr_t ws,
-                      uintptr_t s) {
-    gemm_nt(dt, P<void>(a), P<void>(b), P<float>(bias), P<void>(addend), P<void>(c), out_f32, M, N, K, lda, ldb, ldc,
-            act, cfg, splits, P<float>(ws), S(s));
+                      uintptr_t s, int bias_lowp) {
+    gemm_nt(dt, P<void>(a), P<void>(b), P<void>(bias), P<void>(addend), P<void>(c), out_f32, M, N, K, lda, ldb, ldc,
+            act, cfg, splits, P<float>(ws), S(s), bias_lowp);
     check_launch("gemm_nt");
-  });
+  }, py::arg("dt"), py::arg("a"), py::arg("b"), py::arg("bias"), py::arg("addend"), py::arg("c"), py::arg("out_f32"),
+     py::arg("M"), py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("act"),
+     py::arg("cfg"), py::arg("splits"), py::arg("ws"), py::arg("s"), py::arg("bias_lowp") = 0);
   // streaming 1x1 convolution for small reductions (src/kernels/conv_pw.hip)
   m.def("weight_taps_t", [](int eb, uintptr_t w, uintptr_t out, int K, int RS, int C, std::vector<int> src,
                             std::vector<int64_t> base, std::vector<int64_t> rstride, uintptr_t s) {
@@ -673,6 +680,12 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("gelu_forward", [](int dt, uintptr_t x, uintptr_t y, int64_t n, uintptr_t s) {
     gelu_forward(dt, P<void>(x), P<void>(y), n, S(s));
     check_launch("gelu_forward");
+  });
+  m.def("gelu_colpart_blocks", &gelu_colpart_blocks);
+  m.def("gelu_backward_colpart", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t dx, uintptr_t part, int M, int N,
+                                    uintptr_t s) {
+    gelu_backward_colpart(dt, P<void>(x), P<void>(dy), P<void>(dx), P<float>(part), M, N, S(s));
+    check_launch("gelu_backward_colpart");
   });
   m.def("gelu_backward", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t dx, int64_t n, uintptr_t s) {
     gelu_backward(dt, P<void>(x), P<void>(dy), P<void>(dx), n, S(s));

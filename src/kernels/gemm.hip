@@ -15,7 +15,8 @@
 //     ds_read_b128 fragment reads are conflict-free; a 2-4 stage LDS ring where the wait before a
 //     K-step is a counted `s_waitcnt vmcnt` + raw barrier, so the DMAs of the next steps stay in
 //     flight across it (a K = 768 GEMM has only 12 steps: latency, not bandwidth, bounds it);
-//   * tiles from 64x128 (256 threads, 48 KiB LDS: three workgroups per CU) to 256x256 (512 threads);
+//   * tiles from 64x128 (256 threads, 48 KiB LDS: three workgroups per CU) to 256x256 (512 threads),
+//     and 192 / 384-column tiles whose grids fill the 256 CUs in whole waves on transformer shapes;
 //     small GEMMs (BERT: 4096 tokens x 768) also split K across workgroups: fp32 partial slabs,
 //     summed with the same epilogue by gemm_splitk_reduce -- deterministic, no atomics;
 //   * XCD-aware bijective block remap: consecutive tiles of one A row-panel land on one XCD's L2.
@@ -81,20 +82,27 @@ __device__ __forceinline__ void g_lds_barrier() { asm volatile("s_waitcnt lgkmcn
 struct GemmArgs {
   const void* a;       // [M][lda] (K-contiguous rows)
   const void* b;       // [N][ldb]
-  const float* bias;   // [N] or null
+  const void* bias;    // [N] (fp32, or the operand dtype when bias_lowp) or null
   const void* addend;  // [M][ldc] (output dtype) or null
   void* c;             // [M][ldc]
   float* ws;           // split-K partial slabs [splits][M][N] (fp32) or null
   int M, N, K, lda, ldb, ldc;
-  int act, out_f32, splits, tiles_n, tiles_m;
+  int act, out_f32, splits, tiles_n, tiles_m, bias_lowp;
 };
 
-// WN waves along n (64 columns each), WM waves along m (FJ*16 rows each), NST LDS stages
-template <typename T, int WN, int WM, int FJ, int NST>
+// bias[n .. n+3] as fp32 (the bias may be kept in the operand dtype: no per-call fp32 copy)
+template <typename T>
+__device__ __forceinline__ float4 gemm_bias4(const GemmArgs& g, int n) {
+  if (g.bias_lowp) return GMfma<T>::unpack4(*reinterpret_cast<const uint2*>(static_cast<const T*>(g.bias) + n));
+  return *reinterpret_cast<const float4*>(static_cast<const float*>(g.bias) + n);
+}
+
+// WN waves along n (FI*16 columns each), WM waves along m (FJ*16 rows each), NST LDS stages
+template <typename T, int WN, int WM, int FJ, int NST, int FI = 4>
 __global__ void __launch_bounds__(64 * WN * WM) gemm_nt_kernel(GemmArgs g) {
   constexpr int WAVES = WN * WM;
   constexpr int NT = 64 * WAVES;
-  constexpr int BN = WN * 64;
+  constexpr int BN = WN * FI * 16;
   constexpr int BM = WM * FJ * 16;
   constexpr int B_BYTES = BN * 128;
   constexpr int STAGE = (BN + BM) * 128;
@@ -149,9 +157,9 @@ __global__ void __launch_bounds__(64 * WN * WM) gemm_nt_kernel(GemmArgs g) {
     for (int i = 0; i < A_INS; ++i) g_glds16(a_src[i] + k0, sb + B_BYTES + (i * WAVES + wid) * 1024);
   };
 
-  g_f4 acc[4][FJ];
+  g_f4 acc[FI][FJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FI; ++i)
 #pragma unroll
     for (int j = 0; j < FJ; ++j) acc[i][j] = g_f4{0.f, 0.f, 0.f, 0.f};
 
@@ -159,7 +167,7 @@ __global__ void __launch_bounds__(64 * WN * WM) gemm_nt_kernel(GemmArgs g) {
   const int wm = wid / WN;
   const int frag_r = lane & 15;
   const int fchunk = lane >> 4;
-  const int b_row0 = (wn * 64 + frag_r) * 128;
+  const int b_row0 = (wn * FI * 16 + frag_r) * 128;
   const int a_row0 = B_BYTES + (wm * FJ * 16 + frag_r) * 128;
   const int sw = frag_r & 7;
 
@@ -179,24 +187,24 @@ __global__ void __launch_bounds__(64 * WN * WM) gemm_nt_kernel(GemmArgs g) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int ch = ((kk * 4 + fchunk) ^ sw) * 16;
-      g_u32x4 bf[4], af[FJ];
+      g_u32x4 bf[FI], af[FJ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) bf[i] = *reinterpret_cast<const g_u32x4*>(sb + b_row0 + i * 16 * 128 + ch);
+      for (int i = 0; i < FI; ++i) bf[i] = *reinterpret_cast<const g_u32x4*>(sb + b_row0 + i * 16 * 128 + ch);
 #pragma unroll
       for (int j = 0; j < FJ; ++j) af[j] = *reinterpret_cast<const g_u32x4*>(sb + a_row0 + j * 16 * 128 + ch);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FI; ++i)
 #pragma unroll
         for (int j = 0; j < FJ; ++j) acc[i][j] = GMfma<T>::run(bf[i], af[j], acc[i][j]);
     }
     stage = stage + 1 == NST ? 0 : stage + 1;
   }
 
-  // ---- epilogue: lane holds columns n0 + wn*64 + i*16 + 4*(lane>>4) + {0..3} of row m0 + wm*FJ*16 + j*16 + (lane&15)
+  // ---- epilogue: lane holds columns n0 + wn*FI*16 + i*16 + 4*(lane>>4) + {0..3} of row m0 + wm*FJ*16 + j*16 + (lane&15)
   const int cq = (lane >> 4) * 4;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int n = n0 + wn * 64 + i * 16 + cq;
+  for (int i = 0; i < FI; ++i) {
+    const int n = n0 + wn * FI * 16 + i * 16 + cq;
     if (g.splits > 1) {
       float* ws = g.ws + static_cast<int64_t>(split) * g.M * g.N;
 #pragma unroll
@@ -209,7 +217,7 @@ __global__ void __launch_bounds__(64 * WN * WM) gemm_nt_kernel(GemmArgs g) {
       continue;
     }
     float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (g.bias) bb = *reinterpret_cast<const float4*>(g.bias + n);
+    if (g.bias) bb = gemm_bias4<T>(g, n);
 #pragma unroll
     for (int j = 0; j < FJ; ++j) {
       const int m = m0 + wm * FJ * 16 + j * 16 + frag_r;
@@ -250,7 +258,7 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce_kernel(GemmArgs g) {
       s.x += p.x; s.y += p.y; s.z += p.z; s.w += p.w;
     }
     if (g.bias) {
-      const float4 bb = *reinterpret_cast<const float4*>(g.bias + n);
+      const float4 bb = gemm_bias4<T>(g, n);
       s.x += bb.x; s.y += bb.y; s.z += bb.z; s.w += bb.w;
     }
     s.x = gemm_act(s.x, g.act); s.y = gemm_act(s.y, g.act); s.z = gemm_act(s.z, g.act); s.w = gemm_act(s.w, g.act);
@@ -271,22 +279,22 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce_kernel(GemmArgs g) {
   }
 }
 
-template <typename T, int WN, int WM, int FJ, int NST>
+template <typename T, int WN, int WM, int FJ, int NST, int FI = 4>
 void launch_gemm(GemmArgs g, hipStream_t s) {
-  constexpr int BN = WN * 64;
+  constexpr int BN = WN * FI * 16;
   constexpr int BM = WM * FJ * 16;
   constexpr int SMEM = NST * (BN + BM) * 128;
   static_assert(SMEM <= 160 * 1024, "gemm: LDS budget");
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<T, WN, WM, FJ, NST>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<T, WN, WM, FJ, NST, FI>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     attr_set = true;
   }
   g.tiles_n = g.N / BN;
   g.tiles_m = (g.M + BM - 1) / BM;
   const int blocks = g.tiles_n * g.tiles_m * g.splits;
-  hipLaunchKernelGGL((gemm_nt_kernel<T, WN, WM, FJ, NST>), dim3(blocks), dim3(64 * WN * WM), SMEM, s, g);
+  hipLaunchKernelGGL((gemm_nt_kernel<T, WN, WM, FJ, NST, FI>), dim3(blocks), dim3(64 * WN * WM), SMEM, s, g);
   if (g.splits > 1) {
     const int64_t n4 = static_cast<int64_t>(g.M) * g.N / 4;
     int rb = static_cast<int>((n4 + 255) / 256);
@@ -301,7 +309,13 @@ void launch_gemm(GemmArgs g, hipStream_t s) {
 //  10: 64x64 2w 4st    11: 128x256 8w 3st  12: 128x64 4w 3st  13: 64x128 4w 3st
 // (12 / 13: three 24 KB stages = 72 KB, so two workgroups still share a CU -- the 2-stage tiles wait on
 // their single look-ahead stage for ~55 % of their wave cycles, the 4-stage ones keep one workgroup per CU)
-constexpr int kGemmCfgs = 14;
+//  14: 192x64 4w 3st (48 columns per wave)   15: 192x128 4w 2st (96 columns per wave, 2 WG/CU)
+//  16: 192x256 8w 2st   17: 384x128 8w 2st
+// (14-17: 192 / 384-column tiles whose grids are whole multiples of the 256 CUs on the transformer
+// shapes -- M = 4096 tokens: N = 768 -> 64 x 4 tiles of 192x64, N = 3072 -> 16 x 16 of 192x256 or
+// 32 x 8 of 384x128, 512 of 192x128 at two per CU -- where the power-of-two tiles leave a quarter of
+// the chip idle in the last wave)
+constexpr int kGemmCfgs = 18;
 template <typename T>
 void dispatch_gemm(int cfg, const GemmArgs& g, hipStream_t s) {
   switch (cfg) {
@@ -319,6 +333,10 @@ void dispatch_gemm(int cfg, const GemmArgs& g, hipStream_t s) {
     case 11: launch_gemm<T, 2, 4, 4, 3>(g, s); break;
     case 12: launch_gemm<T, 2, 2, 2, 3>(g, s); break;
     case 13: launch_gemm<T, 1, 4, 2, 3>(g, s); break;
+    case 14: launch_gemm<T, 4, 1, 4, 3, 3>(g, s); break;
+    case 15: launch_gemm<T, 2, 2, 4, 2, 6>(g, s); break;
+    case 16: launch_gemm<T, 2, 4, 4, 2, 6>(g, s); break;
+    case 17: launch_gemm<T, 4, 2, 4, 2, 6>(g, s); break;
     default: throw std::runtime_error("gemm_nt: unknown tile config");
   }
 }
@@ -326,19 +344,22 @@ void dispatch_gemm(int cfg, const GemmArgs& g, hipStream_t s) {
 }  // namespace
 
 int gemm_nt_tile_n(int cfg) {
-  static const int bn[kGemmCfgs] = {128, 128, 64, 256, 128, 256, 64, 128, 256, 128, 64, 128, 128, 64};
+  static const int bn[kGemmCfgs] = {128, 128, 64, 256, 128, 256, 64, 128, 256, 128, 64, 128, 128, 64,
+                                     192, 192, 192, 384};
   MXAMD_HOST_CHECK(cfg >= 0 && cfg < kGemmCfgs, "gemm_nt: unknown tile config");
   return bn[cfg];
 }
 
 int gemm_nt_tile_m(int cfg) {
-  static const int bm[kGemmCfgs] = {128, 64, 128, 128, 256, 256, 64, 128, 128, 64, 64, 256, 64, 128};
+  static const int bm[kGemmCfgs] = {128, 64, 128, 128, 256, 256, 64, 128, 128, 64, 64, 256, 64, 128,
+                                     64, 128, 256, 128};
   MXAMD_HOST_CHECK(cfg >= 0 && cfg < kGemmCfgs, "gemm_nt: unknown tile config");
   return bm[cfg];
 }
 
-void gemm_nt(int dtype, const void* a, const void* b, const float* bias, const void* addend, void* c, int out_f32,
-             int M, int N, int K, int lda, int ldb, int ldc, int act, int cfg, int splits, float* ws, hipStream_t s) {
+void gemm_nt(int dtype, const void* a, const void* b, const void* bias, const void* addend, void* c, int out_f32,
+             int M, int N, int K, int lda, int ldb, int ldc, int act, int cfg, int splits, float* ws, hipStream_t s,
+             int bias_lowp) {
   const int bn = gemm_nt_tile_n(cfg);
   MXAMD_HOST_CHECK(M > 0 && K % 64 == 0 && N % bn == 0, "gemm_nt: need K % 64 == 0 and N % tile_n == 0");
   MXAMD_HOST_CHECK(lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0 && lda >= K && ldb >= K && ldc >= N,
@@ -348,7 +369,9 @@ void gemm_nt(int dtype, const void* a, const void* b, const float* bias, const v
   MXAMD_HOST_CHECK(act >= 0 && act <= 2, "gemm_nt: act must be 0 (none), 1 (relu) or 2 (gelu)");
   MXAMD_HOST_CHECK(static_cast<int64_t>(M) * lda < (1ll << 40) && static_cast<int64_t>(N) * ldb < (1ll << 40),
                    "gemm_nt: operand too large");
-  GemmArgs g{a, b, bias, addend, c, ws, M, N, K, lda, ldb, ldc, act, out_f32, splits, 0, 0};
+  MXAMD_HOST_CHECK(bias == nullptr || reinterpret_cast<uintptr_t>(bias) % (bias_lowp ? 8 : 16) == 0,
+                   "gemm_nt: bias must be 8-byte (16-bit dtype) / 16-byte (fp32) aligned");
+  GemmArgs g{a, b, bias, addend, c, ws, M, N, K, lda, ldb, ldc, act, out_f32, splits, 0, 0, bias_lowp ? 1 : 0};
   if (dtype == kF16) dispatch_gemm<__half>(cfg, g, s);
   else if (dtype == kBF16) dispatch_gemm<__hip_bfloat16>(cfg, g, s);
   else throw std::runtime_error("gemm_nt: dtype must be f16 or bf16");

@@ -254,6 +254,70 @@ __global__ void __launch_bounds__(256) gelu_kernel(const T* __restrict__ x, cons
   }
 }
 
+// GELU backward over [M][N] rows that also leaves the column sums of dx -- the bias gradient of the Dense
+// layer that produced x (BERT's FFN-1) -- as per-block partials part[blockIdx.x][N] (column_sum_partials
+// finishes them): the bias-gradient pass re-reading dx is not run. Thread (ct, rl) owns the 8-column groups
+// ct, ct + nt, ... and every RL-th row of the block (rows rl, rl + RL, ...), two rows of loads in flight;
+// the RL row-lanes combine through LDS ([RL][N] fp32) before the block's partial row is written.
+template <typename T>
+__global__ void __launch_bounds__(1024) gelu_bwd_colpart_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                                T* __restrict__ dx, float* __restrict__ part, int M,
+                                                                int N, int rpb, int nt, int RL) {
+  extern __shared__ float gsh[];
+  const int G = N / 8;
+  const int ct = threadIdx.x % nt, rl = threadIdx.x / nt;
+  const int r0 = blockIdx.x * rpb;
+  const int r1 = r0 + rpb < M ? r0 + rpb : M;
+  for (int g = ct; g < G; g += nt) {
+    float s[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = 0.f;
+    int r = r0 + rl;
+    for (; r + RL < r1; r += 2 * RL) {
+      float xv[2][8], d[2][8];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int64_t off = (int64_t)(r + u * RL) * N + g * 8;
+        ld8(x + off, xv[u]);
+        ld8(dy + off, d[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          o[i] = d[u][i] * gelu_grad_f(xv[u][i]);
+          s[i] += o[i];
+        }
+        st8(dx + (int64_t)(r + u * RL) * N + g * 8, o);
+      }
+    }
+    if (r < r1) {
+      const int64_t off = (int64_t)r * N + g * 8;
+      float xv[8], d[8], o[8];
+      ld8(x + off, xv);
+      ld8(dy + off, d);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        o[i] = d[i] * gelu_grad_f(xv[i]);
+        s[i] += o[i];
+      }
+      st8(dx + off, o);
+    }
+    float* po = RL > 1 ? gsh + rl * N + g * 8 : part + (int64_t)blockIdx.x * N + g * 8;
+    *reinterpret_cast<float4*>(po) = make_float4(s[0], s[1], s[2], s[3]);
+    *reinterpret_cast<float4*>(po + 4) = make_float4(s[4], s[5], s[6], s[7]);
+  }
+  if (RL > 1) {
+    __syncthreads();
+    for (int c = threadIdx.x; c < N; c += blockDim.x) {
+      float a = 0.f;
+      for (int q = 0; q < RL; ++q) a += gsh[q * N + c];
+      part[(int64_t)blockIdx.x * N + c] = a;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ softmax (last axis)
 // y = softmax(x * scale) (LOG: log_softmax); one wave per row, row in registers
 template <typename T, int VPL, bool LOG>
@@ -733,6 +797,42 @@ void gelu_forward(int dtype, const void* x, void* y, int64_t n, hipStream_t s) {
   MXAMD_HOST_CHECK(n % 8 == 0, "gelu: numel must be a multiple of 8");
   MXAMD_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((gelu_kernel<T, false>), dim3(ew_blocks(n / 8)), dim3(256), 0, s,
                                                static_cast<const T*>(x), nullptr, static_cast<T*>(y), n / 8))
+}
+
+// row blocks of gelu_backward_colpart for an [M][N] problem (= the partial rows it writes)
+int gelu_colpart_blocks(int M, int N) {
+  const int nb = M < 256 ? M : 256;
+  return nb > 0 ? nb : 1;
+}
+
+void gelu_backward_colpart(int dtype, const void* x, const void* dy, void* dx, float* part, int M, int N,
+                           hipStream_t s) {
+  MXAMD_HOST_CHECK(M > 0 && N % 8 == 0 && (dtype == kF16 || dtype == kBF16), "gelu_backward_colpart: N % 8, f16/bf16");
+  const int nb = gelu_colpart_blocks(M, N);
+  const int rpb = (M + nb - 1) / nb;
+  const int G = N / 8;
+  // column threads: every 8-column group once, or a divisor of the group count near 256 (N = 3072: 384
+  // groups -> 192 threads x 2) so no thread walks one group more than the others; row-lanes up to 768
+  // threads per block (~12 waves per CU over the 256 blocks) while their [RL][N] LDS image fits 48 KB
+  int nt = G;
+  if (G > 256) {
+    nt = 256;
+    for (int c : {256, 192, 128}) {
+      if (G % c == 0) {
+        nt = c;
+        break;
+      }
+    }
+  }
+  int RL = 768 / nt;
+  if (RL > 8) RL = 8;
+  if (RL > rpb) RL = rpb;
+  if (RL > 12288 / N) RL = 12288 / N;
+  if (RL < 1) RL = 1;
+  const size_t lds = RL > 1 ? static_cast<size_t>(RL) * N * sizeof(float) : 0;
+  MXAMD_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((gelu_bwd_colpart_kernel<T>), dim3(nb), dim3(nt * RL), lds, s,
+                                               static_cast<const T*>(x), static_cast<const T*>(dy),
+                                               static_cast<T*>(dx), part, M, N, rpb, nt, RL))
 }
 
 void gelu_backward(int dtype, const void* x, const void* dy, void* dx, int64_t n, hipStream_t s) {

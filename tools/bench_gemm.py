@@ -41,6 +41,7 @@ def main():
         dy = torch.randn(M, N, device='cuda', dtype=dt)
         fl = 2.0 * M * N * K
         ref_f = torch.nn.functional.linear(x.float(), w.float())
+        ref_d = dy.float() @ w.float()
         cands = {'fwd': [('mm', lambda: torch.nn.functional.linear(x, w))],
                  'dgrad': [('mm', lambda: torch.mm(dy, w))],
                  'wgrad': [('mm', lambda: torch.mm(dy.t(), x))]}
@@ -60,6 +61,7 @@ def main():
             from mxnet_maintenance_amd.ops import gemm as G
             for cfg in G.configs(M, N, K):
                 cands['fwd'].append(('gemm%s' % (cfg,), lambda cfg=cfg: G.gemm_nt(x, w, cfg=cfg)))
+            for cfg in G.configs(M, K, N):      # dX = dy . W: K output columns, reduction over N
                 cands['dgrad'].append(('gemm%s' % (cfg,), lambda cfg=cfg: G.gemm_nt(dy, wt, cfg=cfg)))
         for kind, cl in cands.items():
             res = []
@@ -68,6 +70,8 @@ def main():
                     out = fn()
                     if kind == 'fwd':
                         err = float((out.float() - ref_f).abs().max() / ref_f.abs().max())
+                    elif kind == 'dgrad':
+                        err = float((out.float() - ref_d).abs().max() / ref_d.abs().max())
                     else:
                         err = 0.0
                     t = timeit(fn, a.iters)
@@ -83,8 +87,11 @@ def main():
             print('%-5s M%d N%d K%d | mm %.1f us %.0f TF/s | best %s %.1f us %.0f TF/s (err %.1e)'
                   % (kind, M, N, K, mm[0] * 1e3, fl / mm[0] / 1e9, best[1], best[0] * 1e3, fl / best[0] / 1e9,
                      best[2]), flush=True)
-            for t, name, err in res[:6]:
+            for t, name, err in res[:8]:
                 print('      %-24s %.1f us %.0f TF/s err %.1e' % (name, t * 1e3, fl / t / 1e9, err))
+            bad = [(name, err) for t, name, err in res if err > 2e-2]
+            if bad:
+                print('      WRONG RESULTS: %s' % bad, flush=True)
     for kind, (m, b) in tot.items():
         print('total %-5s mm %.1f us, best %.1f us' % (kind, m * 1e3, b * 1e3))
 
