@@ -224,7 +224,7 @@ class _DeformConvRows(torch.autograd.Function):
                 _pick(('deform_dw', tuple(dy.shape), tuple(xc.shape), x.dtype), [],
                       lambda: gw[gi * og:(gi + 1) * og].copy_(dy.t() @ xc))
             # column gradient in fp32 (the offset gradient is a difference of products)
-            wt = wmat[gi * og:(gi + 1) * og].t().contiguous()
+            wt = KF.transpose2d(wmat[gi * og:(gi + 1) * og])
             o = gcols[:, gi * cg:(gi + 1) * cg]
             cands = [(n, (lambda c=c: G.gemm_nt(dy, wt, out=o, out_f32=True, cfg=c)))
                      for n, c in ((n, G.parse_name(n)) for n, _ in G.candidates(dy, wt, out_f32=True))

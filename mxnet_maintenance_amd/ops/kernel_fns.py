@@ -535,8 +535,7 @@ def conv_up2_ok(dy, w, stride, pad, xshape):
 def conv_dgrad_up2(dy, w, variant, bn_bwd=None):
     """dX of a 1x1 stride-2 conv: dY . W on the big-tile kernel, each result pixel stored at (2h, 2w) of
     dX and its three 2x2 siblings zeroed by the same epilogue."""
-    K, _, _, C = w.shape
-    wt = w.reshape(K, C).t().contiguous().view(C, 1, 1, K)
+    wt = _dgrad_weight(w.contiguous())          # [C][1][1][K]: the 1x1 weight transposed
     return conv_fwd(dy.contiguous(), wt, (1, 1), (0, 0), None, variant, bn_bwd=bn_bwd, up=2)
 
 
@@ -781,6 +780,15 @@ def _dgrad_weight(w):
     T = R * S
     out = torch.empty((C, R, S, K), dtype=w.dtype, device=w.device)
     return _taps_t(w, out, [T - 1 - t for t in range(T)], [t * K for t in range(T)], [T * K] * T)
+
+
+def transpose2d(w):
+    """w^T of a 2-D [R][C] tensor, contiguous: the LDS-tiled tap-transpose kernel (pointwise.hip) for
+    16-bit / fp32 CUDA tensors, else torch's strided copy (several us per weight-sized call on gfx950)."""
+    R, C = w.shape
+    if w.is_cuda and w.is_contiguous() and w.element_size() in (2, 4) and R % 8 == 0 and C % 8 == 0:
+        return _dgrad_weight(w.view(R, 1, 1, C)).view(C, R)
+    return w.t().contiguous()
 
 
 def _phase_taps(R, P, s, ph):
@@ -1307,7 +1315,7 @@ def _gemm_dgrad_1x1(dy, w, xshape, addend=None):
     for cfg in G.configs(d2.shape[0], C, K, G.AUTOTUNE_TILES):
         def run(cfg=cfg):
             add = addend.contiguous().view(-1, C) if addend is not None else None
-            return G.gemm_nt(d2, w.reshape(K, C).t().contiguous(), addend=add, cfg=cfg).view(xshape)
+            return G.gemm_nt(d2, transpose2d(w.reshape(K, C)), addend=add, cfg=cfg).view(xshape)
         out.append(('gemm%ds%d' % cfg, run))
     return out
 
@@ -1634,7 +1642,9 @@ def _tee_dgrad(gy, x, w, gpass, inplace, bn_src=None):
             if C % bco or (v in _BIG_SKINNY and not (_SKINNY_ON and K == 64)):
                 continue
             if wt is None:
-                wt = w2.t().contiguous().view(C, 1, 1, K)
+                # W^T [C][1][1][K] on the LDS-tiled tap-transpose kernel (torch's strided transpose copy
+                # cost ~6 us per call here)
+                wt = _dgrad_weight(w.contiguous())
 
             def big(v=v, wt=wt, bn=None):
                 add = gpass.contiguous() if gpass is not None else None

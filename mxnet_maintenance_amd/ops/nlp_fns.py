@@ -380,14 +380,11 @@ def _fc_fwd_cands(x2, w, b):
 
 
 def _wt(w):
-    """W^T ([in][out]) for the K-contiguous data-gradient GEMMs: the in-tree LDS-tiled transpose
-    (pointwise.hip weight_taps_t, the conv data-gradient weight path with one tap) -- torch's strided
-    transpose copy of a 768 x 3072 bf16 weight took ~15 us, enough to hand every BERT data gradient to
-    hipBLASLt although the GEMM itself is faster in-tree (tools/bench_gemm.py)."""
-    N, K = w.shape
-    if w.is_contiguous() and N % 8 == 0 and K % 8 == 0:
-        return _KF._dgrad_weight(w.view(N, 1, 1, K)).view(K, N)
-    return w.t().contiguous()
+    """W^T ([in][out]) for the K-contiguous data-gradient GEMMs on the in-tree LDS-tiled transpose
+    (kernel_fns.transpose2d): torch's strided transpose copy of a 768 x 3072 bf16 weight took ~15 us,
+    enough to hand every BERT data gradient to hipBLASLt although the GEMM itself is faster in-tree
+    (tools/bench_gemm.py)."""
+    return _KF.transpose2d(w)
 
 
 def _fc_dgrad_cands(dy2, w, addend=None):

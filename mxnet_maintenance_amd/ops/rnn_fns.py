@@ -67,7 +67,7 @@ def _input_grad(g, w):
     small transposed copy per call), tile chosen by the autotuner among the gemm.hip configs."""
     from . import gemm as G
     from . import kernel_fns as KF
-    wt = w.t().contiguous()
+    wt = KF.transpose2d(w)
     if g.dtype in G._DT and g.is_contiguous() and G.gemm_ok(g, wt):
         cands = G.candidates(g, wt)
         if cands:
@@ -143,7 +143,8 @@ class _LayerDir(torch.autograd.Function):
         dev = x.device
         dy = dy.contiguous().to(dt) if dy is not None else None
         dhT32 = dhT.float().contiguous() if dhT is not None else torch.zeros((N, H), dtype=torch.float32, device=dev)
-        whhT = w_hh.t().contiguous()
+        from . import kernel_fns as _KF2
+        whhT = _KF2.transpose2d(w_hh)
         dgh = torch.empty((T, N, G * H), dtype=dt, device=dev)
         gru = mode == 'gru'
         dgx = torch.empty_like(dgh) if gru else None
