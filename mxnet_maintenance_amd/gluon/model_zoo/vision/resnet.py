@@ -37,6 +37,27 @@ def _bn(layout, relu=False, fuse=False, **kw):
     return nn.BatchNorm(axis=_bn_axis(layout), **kw)
 
 
+class _StemBNReLUPool(nn.BatchNormReLU):
+    """The stem's BatchNorm + ReLU + 3x3/2 max pooling as one operator (``fuse=True``, NHWC): the pooling
+    kernel normalises each window tap itself, so the 112x112 normalised activation is never written or
+    re-read (ops/nn.py ``_contrib_BatchNormReLUMaxPool``). Same parameters as BatchNormReLU."""
+
+    def hybrid_forward(self, F, x, gamma, beta, running_mean, running_var):
+        return F.contrib.BatchNormReLUMaxPool(x, gamma, beta, running_mean, running_var, name='fwd',
+                                              kernel=(3, 3), stride=(2, 2), pad=(1, 1), **self._kwargs)
+
+
+def _stem_tail(features, layout, fuse):
+    """BatchNorm + ReLU + max pooling after the 7x7 stem convolution."""
+    if fuse and layout == 'NHWC':
+        features.add(_StemBNReLUPool(axis=_bn_axis(layout)))
+        return
+    features.add(_bn(layout, True, fuse))
+    if not fuse:
+        features.add(nn.Activation('relu'))
+    features.add(nn.MaxPool2D(3, 2, 1, layout=layout))
+
+
 class _ResidualTail(_BatchNorm):
     """relu(BN(x) + shortcut) of a residual block: one fused HIP kernel when ``fuse``; otherwise this
     block is the plain BN and the owning residual block adds and activates (``_finish``), so the
@@ -210,10 +231,8 @@ class ResNetV1(_ResNetBase):
             if thumbnail:
                 self.features.add(_conv(channels[0], 3, 1, 1, 0, layout))
             else:
-                self.features.add(_conv(channels[0], 7, 2, 3, 0, layout), _bn(layout, True, fuse))
-                if not fuse:
-                    self.features.add(nn.Activation('relu'))
-                self.features.add(nn.MaxPool2D(3, 2, 1, layout=layout))
+                self.features.add(_conv(channels[0], 7, 2, 3, 0, layout))
+                _stem_tail(self.features, layout, fuse)
             for i, n in enumerate(layers):
                 self.features.add(self._stage(block, n, channels[i + 1], 1 if i == 0 else 2, i + 1,
                                               channels[i], layout, fuse))
@@ -237,10 +256,8 @@ class ResNetV2(_ResNetBase):
             if thumbnail:
                 self.features.add(_conv(channels[0], 3, 1, 1, 0, layout))
             else:
-                self.features.add(_conv(channels[0], 7, 2, 3, 0, layout), _bn(layout, True, fuse))
-                if not fuse:
-                    self.features.add(nn.Activation('relu'))
-                self.features.add(nn.MaxPool2D(3, 2, 1, layout=layout))
+                self.features.add(_conv(channels[0], 7, 2, 3, 0, layout))
+                _stem_tail(self.features, layout, fuse)
             in_channels = channels[0]
             for i, n in enumerate(layers):
                 self.features.add(self._stage(block, n, channels[i + 1], 1 if i == 0 else 2, i + 1,

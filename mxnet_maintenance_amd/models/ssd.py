@@ -69,9 +69,11 @@ class SSD(HybridBlock):
         self._anchor_cache = {}
         with self.name_scope():
             backbone = vision.get_model(base, layout=layout, fuse=fuse)
-            # stage-3 output (stride 16) and stage-4 output (stride 32)
-            self.stage3 = backbone.features[:6]
-            self.stage4 = backbone.features[6]
+            # stage-3 output (stride 16) and stage-4 output (stride 32): the features end with
+            # ... stage3, stage4, global pooling (the stem's layer count depends on ``fuse``)
+            nf_ = len(backbone.features)
+            self.stage3 = backbone.features[:nf_ - 2]
+            self.stage4 = backbone.features[nf_ - 2]
             self.extras = nn.HybridSequential(prefix='extras_')
             with self.extras.name_scope():
                 for k, (nf, s, p) in enumerate(zip(num_filters, strides, pads)):

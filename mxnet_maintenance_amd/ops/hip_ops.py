@@ -154,6 +154,21 @@ def conv_tee(data, weight, inplace_grad=False):
 # BatchNorm
 # ---------------------------------------------------------------------------
 
+def batch_norm_relu_maxpool(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_gamma, training,
+                            axis, kernel, stride, pad, invstd_out=False):
+    """max_pool(relu(BatchNorm(data))) -- the ResNet stem after its 7x7 conv. On channel-last HIP tensors
+    one statistics pass and one pooling pass that applies the BatchNorm + ReLU to each window tap
+    (kernel_fns.bnrelu_pool_ok); otherwise BatchNorm+ReLU followed by the pooling operator."""
+    nd = data.dim()
+    if (nd == 4 and axis % nd == 3 and _use_hip(data) and _K.bnrelu_pool_ok(data, kernel, stride, pad)):
+        g = torch.ones_like(gamma) if fix_gamma else gamma
+        return _K.BatchNormNHWC.apply(data, g, beta, None, eps, training, True, moving_mean, moving_var, momentum,
+                                      invstd_out, (tuple(kernel), tuple(stride), tuple(pad)))
+    out, m, v = batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_gamma, training, axis,
+                           'relu', invstd_out=invstd_out)
+    return pool(out, 'max', tuple(kernel), tuple(stride), tuple(pad), 'valid', True, axis % nd == nd - 1), m, v
+
+
 def batch_norm(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_gamma, training,
                axis, act_type, addend=None, invstd_out=False):
     """BatchNorm with MXNet semantics; returns (out, mean, var) -- (out, mean, 1/sqrt(var + eps)) in

@@ -75,6 +75,7 @@ def _leaf_grad(t, numel=None, dtype=torch.float32):
 _RELU_FROM_X = [True]    # BN+ReLU backward recomputes the mask from x (debug switch)
 _BN_BWD_FUSE = [os.environ.get('MXAMD_BN_BWD_FUSE', '1') != '0']   # BN-backward stats in dgrad epilogues
 _BN_TAIL_DS = [os.environ.get('MXAMD_BN_TAIL_DS', '1') != '0']     # shortcut-BN stats in the tail backward
+_BN_POOL_BWD = [True]    # stem BN+ReLU+pool backward as two gather passes (tests flip it for the A/B)
 _ZEROS = {}
 
 
@@ -91,7 +92,10 @@ class BatchNormNHWC(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, addend, eps, training, relu, moving_mean, moving_var, momentum=None,
-                invstd_out=False):
+                invstd_out=False, pool=None):
+        # pool = ((kh, kw), (sh, sw), (ph, pw)): 3x3 max pooling of the BN + ReLU output in one pass
+        # (pool_nhwc.hip's BatchNorm prologue; bnrelu_pool_ok) -- the normalised activation is never
+        # materialised and the backward routes the pooled gradient first
         lib = _K.lib()
         C = x.shape[-1]
         R = x.numel() // C
@@ -99,7 +103,8 @@ class BatchNormNHWC(torch.autograd.Function):
         g = _f32(gamma)
         b = _f32(beta)
         mm = _f32(moving_mean)
-        y = torch.empty_like(x)
+        assert pool is None or (relu and addend is None)
+        y = torch.empty_like(x) if pool is None else None
         if addend is not None:
             assert addend.shape == x.shape and addend.dtype == x.dtype
             addend = addend.contiguous()
@@ -131,7 +136,7 @@ class BatchNormNHWC(torch.autograd.Function):
         # never re-reads y (two full-tensor reads fewer per call)
         mask = (torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev)
                 if (addend is not None and relu and _RELU_FROM_X[0]) else None)
-        lib.bn_nhwc_forward(_DT[x.dtype], x.data_ptr(), _p(addend), y.data_ptr(), _p(mask), g.data_ptr(),
+        lib.bn_nhwc_forward(_DT[x.dtype], x.data_ptr(), _p(addend), _p(y), _p(mask), g.data_ptr(),
                             b.data_ptr(),
                             center.data_ptr(), _p(part), mean.data_ptr(), invstd.data_ptr(), var.data_ptr(),
                             scale.data_ptr(), shift.data_ptr(), R, C, float(eps), int(bool(training)),
@@ -141,14 +146,27 @@ class BatchNormNHWC(torch.autograd.Function):
             with torch.no_grad():
                 moving_mean.mul_(momentum).add_(mean.to(moving_mean.dtype), alpha=1 - momentum)
                 moving_var.mul_(momentum).add_(var.to(moving_var.dtype), alpha=1 - momentum)
+        ctx.pool = None
+        if pool is not None:
+            (kh, kw), (sh, sw), (ph, pw) = pool
+            N, H, W = x.shape[:3]
+            Ho, Wo = _pool_out(H, kh, sh, ph, False), _pool_out(W, kw, sw, pw, False)
+            y = torch.empty((N, Ho, Wo, C), dtype=x.dtype, device=dev)
+            arg = torch.empty((N, Ho, Wo, C), dtype=torch.uint8, device=dev)
+            ctx.pool = (N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, 1)
+            lib.pool_nhwc_forward_bnrelu(_DT[x.dtype], x.data_ptr(), y.data_ptr(), arg.data_ptr(), *ctx.pool,
+                                         _stream(), scale.data_ptr(), shift.data_ptr())
+            mask = arg        # saved in the mask slot: relu_mode 2 recomputes the ReLU mask from x
         # ReLU mask in backward: recomputed from x*scale+shift for BN+ReLU (y not kept),
         # read from y only for the residual tail (its mask also depends on the addend)
         relu_mode = 0 if not relu else (1 if not _RELU_FROM_X[0] else (3 if addend is not None else 2))
+        if pool is not None:
+            relu_mode = 2
         ctx.save_for_backward(x, y if relu_mode == 1 else mask, g, mean, invstd,
                               scale if relu_mode == 2 else None, shift if relu_mode == 2 else None)
         ctx.cfg = (relu_mode, bool(training), addend is not None, gamma.dtype, beta.dtype)
         ctx.bn_token = None
-        if training and relu_mode in (0, 2, 3) and _BN_BWD_FUSE[0]:
+        if training and relu_mode in (0, 2, 3) and _BN_BWD_FUSE[0] and pool is None:
             # a consumer convolution's dgrad (big-tile kernel) may emit this BN's backward statistics
             # from its epilogue: it needs z (= x here), mean, the ReLU mask source, and a token that
             # identifies this BN call (checked in backward)
@@ -179,11 +197,21 @@ class BatchNormNHWC(torch.autograd.Function):
         relu_mode, training, has_add, gdt, bdt = ctx.cfg
         gamma_ref, beta_ref = ctx.refs
         if gy is None:
-            return (None,) * 11
+            return (None,) * 12
         gy = gy.contiguous()
         C = x.shape[-1]
         R = x.numel() // C
         dev = x.device
+        fused_pool = False
+        if ctx.pool is not None:
+            fused_pool = (x.dtype in (torch.float16, torch.bfloat16) and 256 % (C // 8) == 0
+                          and hasattr(lib, 'bn_pool_backward') and _BN_POOL_BWD[0])
+            if not fused_pool:
+                # the pooled gradient routed back to the BN output's shape first (argmax gather)
+                gyd = torch.empty_like(x)
+                lib.pool_nhwc_backward(_DT[x.dtype], 1, gy.data_ptr(), y.data_ptr(), gyd.data_ptr(), *ctx.pool,
+                                       _stream())
+                gy, y = gyd, None
         dx = torch.empty_like(x)
         dz = torch.empty_like(x) if has_add else None
         ext = getattr(gy, '_mxamd_bn_bwd', None)
@@ -205,6 +233,19 @@ class BatchNormNHWC(torch.autograd.Function):
             dg_ptr, db_ptr, accum = dg_buf.data_ptr(), tb.data_ptr(), 1
         else:
             dg_ptr, db_ptr, accum = out[0].data_ptr(), out[1].data_ptr(), 0
+        if fused_pool:
+            # statistics and dx straight from the pooled gradient (two gather passes, pool_nhwc.hip): the
+            # routed full-resolution gradient is never materialised
+            N_, H_, W_, C_, Ho_, Wo_, kh, kw, sh, sw, ph, pw, _ = ctx.pool
+            ppart = torch.empty(2 * lib.bn_pool_bwd_blocks() * C, dtype=torch.float32, device=dev)
+            lib.bn_pool_backward(_DT[x.dtype], x.data_ptr(), gy.data_ptr(), y.data_ptr(), dx.data_ptr(), g.data_ptr(),
+                                 mean.data_ptr(), invstd.data_ptr(), fscale.data_ptr(), fshift.data_ptr(),
+                                 ppart.data_ptr(), dg_ptr, db_ptr, out[2].data_ptr(), N_, H_, W_, C_, Ho_, Wo_, kh, kw,
+                                 sh, sw, ph, pw, 0, int(training), accum, _stream())
+            if direct:
+                return dx, None, None, None, None, None, None, None, None, None, None, None
+            return (dx, out[0].to(gdt) if need_g else None, out[1].to(bdt) if need_b else None,
+                    None, None, None, None, None, None, None, None, None)
         ymask = y if relu_mode == 3 else None
         y = y if relu_mode == 1 else None
         ds = ctx.add_src if dz is not None else None
@@ -229,7 +270,14 @@ class BatchNormNHWC(torch.autograd.Function):
         else:
             dgamma = out[0].to(gdt) if need_g else None
             dbeta = out[1].to(bdt) if need_b else None
-        return dx, dgamma, dbeta, dz, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dz, None, None, None, None, None, None, None, None
+
+
+def bnrelu_pool_ok(x, kernel, stride, pad):
+    """BatchNorm + ReLU + max pooling in one pass (BatchNormNHWC pool=): 3x3 windows, NHWC f16/bf16/f32
+    with C % 8 == 0 and 32-bit element offsets (pool_nhwc.hip pool_fwd_max3_kernel<AFF>)."""
+    return (bn_ok(x) and tuple(kernel) == (3, 3) and pool_ok(x, kernel, stride, pad)
+            and x.numel() + 256 * 32 * 256 * 8 < 2 ** 31 and hasattr(_K.lib(), 'pool_nhwc_forward_bnrelu'))
 
 
 class SoftmaxCE(torch.autograd.Function):

@@ -49,6 +49,6 @@ def lib():
 # Operator wrappers and their shape/dtype predicates (which calls the kernels support; anything
 # else takes the torch path, itself MIOpen / hipBLASLt on ROCm) live next to the kernels they drive.
 from .kernel_fns import *  # noqa: E402,F401,F403
-from .kernel_fns import bn_ok, ce_ok, gap_ok, conv_ok, conv_tee_ok, pool_ok  # noqa: E402,F401
+from .kernel_fns import bn_ok, ce_ok, gap_ok, conv_ok, conv_tee_ok, pool_ok, bnrelu_pool_ok  # noqa: E402,F401
 from .nlp_fns import *  # noqa: E402,F401,F403
 from .nlp_fns import ln_ok, ew_ok, gemm_ok, embedding_ok  # noqa: E402,F401

@@ -194,7 +194,8 @@ class GELU(torch.autograd.Function):
         dx = torch.empty_like(x)
         lib = _K.lib()
         N = x.shape[-1] if x.dim() else 1
-        if x.dim() >= 2 and N % 8 == 0 and x.is_contiguous() and hasattr(lib, 'gelu_backward_colpart'):
+        if (x.dim() >= 2 and N % 8 == 0 and x.dtype in (torch.float16, torch.bfloat16) and x.is_contiguous()
+                and hasattr(lib, "gelu_backward_colpart")):
             # the producing Dense's bias gradient rides along as column partials (consumed by
             # Linear.backward through dx._mxamd_bias_part, like the add_dropout_layernorm tail's)
             M = x.numel() // N

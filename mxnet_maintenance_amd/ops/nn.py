@@ -256,6 +256,25 @@ def batch_norm_relu(data, gamma, beta, moving_mean, moving_var, eps=1e-3, moment
                               training, axis, 'relu', invstd_out=True)
 
 
+_BNPOOL_PARAMS = dict(_BN_PARAMS, kernel=('shape', (3, 3)), stride=('shape', (2, 2)), pad=('shape', (1, 1)))
+
+
+@register('_contrib_BatchNormReLUMaxPool', aliases=('BatchNormReLUMaxPool',),
+          arg_names=('data', 'gamma', 'beta'), aux_names=('moving_mean', 'moving_var'),
+          num_outputs=3, num_visible_outputs=_bn_nvis, infer_params=_bn_infer, params=_BNPOOL_PARAMS)
+def batch_norm_relu_maxpool(data, gamma, beta, moving_mean, moving_var, eps=1e-3, momentum=0.9, fix_gamma=True,
+                            use_global_stats=False, output_mean_var=False, axis=1, cudnn_off=False, act_type=None,
+                            min_calib_range=None, max_calib_range=None, kernel=(3, 3), stride=(2, 2), pad=(1, 1)):
+    """``Pooling(relu(BatchNorm(data)), pool_type='max')`` (valid convention): the ResNet stem's BatchNorm,
+    ReLU and 3x3/2 max pooling as one operator -- the pooling kernel applies the normalisation to each
+    window tap, so the normalised full-resolution activation is never written (pool_nhwc.hip). Outputs
+    and moving-statistics updates are BatchNorm's; the first output is pooled."""
+    training = _state.STATE.training and not use_global_stats
+    return hip_ops.batch_norm_relu_maxpool(data, gamma, beta, moving_mean, moving_var, eps, momentum, fix_gamma,
+                                           training, axis, _tup(kernel, 2, 1), _tup(stride, 2, 1), _tup(pad, 2, 0),
+                                           invstd_out=True)
+
+
 @register('_contrib_BatchNormAddReLU', aliases=('BatchNormAddReLU',),
           arg_names=('data', 'addend', 'gamma', 'beta'), aux_names=('moving_mean', 'moving_var'),
           num_outputs=3, num_visible_outputs=_bn_nvis,

@@ -146,7 +146,14 @@ void lamb_update(int dtype, void* w, const void* g, float* mean, float* var, flo
 void seg_sumsq(int dtype, const void* x, const void* chunks, int nchunks, float* out, int nseg, hipStream_t s);
 void all_finite(int dtype, const void* x, int64_t n, float scale, int* flag, int init, hipStream_t s);
 void pool_nhwc_forward(int dtype, int is_max, const void* x, void* y, uint8_t* arg, int N, int H, int W, int C,
-                       int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip, hipStream_t s);
+                       int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip, hipStream_t s,
+                       const float* scale, const float* shift);
+int bn_pool_bwd_blocks();
+void bn_pool_backward(int dtype, const void* x, const void* dy, const uint8_t* arg, void* dx, const float* gamma,
+                      const float* mean, const float* invstd, const float* fscale, const float* fshift, float* part,
+                      float* dgamma, float* dbeta, float* coef, int N, int H, int W, int C, int Ho, int Wo, int kh,
+                      int kw, int sh, int sw, int ph, int pw, int fix_gamma, int training, int accum,
+                      hipStream_t s);
 void pool_nhwc_backward(int dtype, int is_max, const void* dy, const uint8_t* arg, void* dx, int N, int H, int W,
                         int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip,
                         hipStream_t s);
@@ -775,8 +782,29 @@ PYBIND11_MODULE(_hip_kernels, m) {
                                 int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip,
                                 uintptr_t s) {
     pool_nhwc_forward(dt, is_max, P<void>(x), P<void>(y), P<uint8_t>(arg), N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw,
-                      cip, S(s));
+                      cip, S(s), nullptr, nullptr);
     check_launch("pool_nhwc_forward");
+  });
+  // backward of max_pool(relu(BatchNorm(x))): statistics gather, finalize, dx gather (pool_nhwc.hip)
+  m.def("bn_pool_bwd_blocks", &bn_pool_bwd_blocks);
+  m.def("bn_pool_backward", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t arg, uintptr_t dx, uintptr_t gamma,
+                               uintptr_t mean, uintptr_t invstd, uintptr_t fscale, uintptr_t fshift, uintptr_t part,
+                               uintptr_t dgamma, uintptr_t dbeta, uintptr_t coef, int N, int H, int W, int C, int Ho,
+                               int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int fix_gamma, int training,
+                               int accum, uintptr_t s) {
+    bn_pool_backward(dt, P<void>(x), P<void>(dy), P<uint8_t>(arg), P<void>(dx), P<float>(gamma), P<float>(mean),
+                     P<float>(invstd), P<float>(fscale), P<float>(fshift), P<float>(part), P<float>(dgamma),
+                     P<float>(dbeta), P<float>(coef), N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, fix_gamma, training,
+                     accum, S(s));
+    check_launch("bn_pool_backward");
+  });
+  // 3x3 max pooling of relu(x * scale + shift): the stem's BatchNorm + ReLU folded into the pooling
+  m.def("pool_nhwc_forward_bnrelu", [](int dt, uintptr_t x, uintptr_t y, uintptr_t arg, int N, int H, int W, int C,
+                                       int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip,
+                                       uintptr_t s, uintptr_t scale, uintptr_t shift) {
+    pool_nhwc_forward(dt, 1, P<void>(x), P<void>(y), P<uint8_t>(arg), N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, cip,
+                      S(s), P<float>(scale), P<float>(shift));
+    check_launch("pool_nhwc_forward_bnrelu");
   });
   m.def("pool_nhwc_backward", [](int dt, int is_max, uintptr_t dy, uintptr_t arg, uintptr_t dx, int N, int H, int W,
                                  int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip,

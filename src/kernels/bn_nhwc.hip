@@ -580,6 +580,9 @@ static void bn_forward_impl(const void* x, const void* addend, void* y, uint8_t*
                        beta, nullptr, eps, mean, invstd, var, scale, shift, nullptr, fix_gamma, 1, momentum, mm_upd,
                        mv_upd, 0);
   }
+  // y == nullptr: statistics (and scale / shift) only -- the consumer applies them (the stem's BN + ReLU
+  // folded into the max pooling, pool_nhwc.hip)
+  if (y == nullptr) return;
   const int64_t nvec = R * C / 8;
   int blocks = static_cast<int>((nvec + kBnThreads - 1) / kBnThreads);
   if (blocks > 256 * 16) blocks = 256 * 16;
@@ -820,6 +823,17 @@ void bn_nhwc_forward(int dtype, const void* x, const void* addend, void* y, uint
       bn_forward_impl<float>(x, addend, y, mask, gamma, beta, center, part, mean, invstd, var, scale, shift, R, C, eps,
                              training, relu, fix_gamma, momentum, mm_upd, mv_upd, ext_nblk, s);
   }
+}
+
+// Backward finalize from channel-major partials part[2][C][nblk] of sum(dz), sum(dz * (x - mean)) produced by
+// another kernel (the stem's fused pooling backward, pool_nhwc.hip): dgamma / dbeta (accumulated when
+// accum) and the dx coefficients coef[3][C].
+void bn_finalize_backward(const float* part, int nblk, int C, int64_t R, const float* mean, const float* gamma,
+                          const float* invstd, float* dgamma, float* dbeta, float* coef, int fix_gamma, int training,
+                          int accum, hipStream_t s) {
+  hipLaunchKernelGGL((bn_finalize_kernel<1>), dim3(C), dim3(kFinThreads), 0, s, part,
+                     part + static_cast<int64_t>(nblk) * C, nblk, C, R, mean, gamma, nullptr, invstd, 0.f, dgamma,
+                     dbeta, coef, coef + C, coef + 2 * C, nullptr, fix_gamma, training, 0.f, nullptr, nullptr, accum);
 }
 
 void bn_nhwc_backward(int dtype, const void* x, const void* dy, const void* y, const uint8_t* mask, void* dx,

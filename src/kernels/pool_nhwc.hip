@@ -182,11 +182,15 @@ __global__ void __launch_bounds__(256) pool_bwd_kernel(const T* __restrict__ dy,
 }
 
 // max forward over a 3x3 window (the ResNet stem): the nine taps are loaded together, predicated (an
-// out-of-image tap reads offset 0 and is ignored), instead of in a loop with early continues
-template <typename T, typename I>
+// out-of-image tap reads offset 0 and is ignored), instead of in a loop with early continues.
+// AFF: the window's input is relu(x * scale[c] + shift[c]) -- the BatchNorm + ReLU in front of the stem
+// pooling applied to each tap on the fly (max and ReLU commute, out-of-image taps stay excluded), so the
+// normalised activation is never written or re-read; the argmax indexes the largest affine value.
+template <typename T, typename I, bool AFF>
 __global__ void __launch_bounds__(256) pool_fwd_max3_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                             uint8_t* __restrict__ arg, PoolGeom g, I nvec,
-                                                            PoolDivs dv) {
+                                                            PoolDivs dv, const float* __restrict__ scale,
+                                                            const float* __restrict__ shift) {
   const I cv = static_cast<I>(g.C / 8);
   for (I v = static_cast<I>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec;
        v += static_cast<I>(gridDim.x) * blockDim.x) {
@@ -202,6 +206,15 @@ __global__ void __launch_bounds__(256) pool_fwd_max3_kernel(const T* __restrict_
       const I o = ok[t] ? ((static_cast<I>(n) * g.H + h) * g.W + w) * g.C + c8 : static_cast<I>(0);
       vx[t].load(x + o);
     }
+    float sc[8], sf[8];
+    if (AFF) {
+      const float4 a0 = *reinterpret_cast<const float4*>(scale + c8);
+      const float4 a1 = *reinterpret_cast<const float4*>(scale + c8 + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(shift + c8);
+      const float4 b1 = *reinterpret_cast<const float4*>(shift + c8 + 4);
+      sc[0] = a0.x; sc[1] = a0.y; sc[2] = a0.z; sc[3] = a0.w; sc[4] = a1.x; sc[5] = a1.y; sc[6] = a1.z; sc[7] = a1.w;
+      sf[0] = b0.x; sf[1] = b0.y; sf[2] = b0.z; sf[3] = b0.w; sf[4] = b1.x; sf[5] = b1.y; sf[6] = b1.z; sf[7] = b1.w;
+    }
     float acc[8];
     uint32_t am[8];
     bool any = false;
@@ -216,7 +229,7 @@ __global__ void __launch_bounds__(256) pool_fwd_max3_kernel(const T* __restrict_
       any = true;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const float f = vx[t].get(i);
+        const float f = AFF ? fmaf(vx[t].get(i), sc[i], sf[i]) : vx[t].get(i);
         if (f > acc[i]) {
           acc[i] = f;
           am[i] = t;
@@ -225,7 +238,7 @@ __global__ void __launch_bounds__(256) pool_fwd_max3_kernel(const T* __restrict_
     }
     Vec8<T> out;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) out.set(i, any ? acc[i] : 0.f);
+    for (int i = 0; i < 8; ++i) out.set(i, any ? (AFF ? fmaxf(acc[i], 0.f) : acc[i]) : 0.f);
     uint2 packed;
     packed.x = am[0] | (am[1] << 8) | (am[2] << 16) | (am[3] << 24);
     packed.y = am[4] | (am[5] << 8) | (am[6] << 16) | (am[7] << 24);
@@ -279,6 +292,107 @@ __global__ void __launch_bounds__(256) pool_bwd_max2_kernel(const T* __restrict_
   }
 }
 
+// ---- BatchNorm + ReLU + max pooling backward (the stem; forward: pool_fwd_max3_kernel<AFF>)
+// Gather form per input vector (8 channels of one pixel, as pool_bwd_max2_kernel): the pooled gradient
+// routed to it through the <= 2 x 2 covering windows whose argmax chose it, masked by the ReLU recomputed
+// from x (dz = routed * [x * scale + shift > 0]).
+//   STATS: per-channel sum(dz), sum(dz * (x - mean)) -> channel-major partials [2][C][gridDim.x]; every
+//          thread keeps one channel group (blockDim 256 and the grid stride are multiples of C / 8)
+//   else : dx = A * dz + B * x + Cc (the BatchNorm backward, coefficients from bn_finalize_backward)
+// The dense routed gradient is never written: one gather pass for the statistics and one for dx replace
+// the pooling backward's dense write plus the BatchNorm backward's reduction and apply passes.
+template <typename T, bool STATS>
+__global__ void __launch_bounds__(256) bnpool_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                         const uint8_t* __restrict__ arg, const float* __restrict__ k0,
+                                                         const float* __restrict__ k1, const float* __restrict__ k2,
+                                                         const float* __restrict__ k3, const float* __restrict__ k4,
+                                                         T* __restrict__ dx, float* __restrict__ part, PoolGeom g,
+                                                         uint32_t nvec, PoolDivs dv) {
+  // STATS: k0 = mean, k1 = fscale, k2 = fshift;  apply: k0 = A, k1 = B, k2 = Cc, k3 = fscale, k4 = fshift
+  const uint32_t cv = static_cast<uint32_t>(g.C / 8);
+  // C / 8 divides 256 (host-checked), so the grid stride is a multiple of it: a thread's channel group is
+  // fixed and its per-channel constants are loaded once
+  const int c8f = static_cast<int>((blockIdx.x * 256u + threadIdx.x) % cv) * 8;
+  auto ld8c = [&](const float* p, float* o) {
+    const float4 u = *reinterpret_cast<const float4*>(p + c8f);
+    const float4 w = *reinterpret_cast<const float4*>(p + c8f + 4);
+    o[0] = u.x; o[1] = u.y; o[2] = u.z; o[3] = u.w; o[4] = w.x; o[5] = w.y; o[6] = w.z; o[7] = w.w;
+  };
+  float a[8], b[8], c[8], fs[8], fh[8];
+  ld8c(k0, a);
+  ld8c(STATS ? k1 : k3, fs);
+  ld8c(STATS ? k2 : k4, fh);
+  if (!STATS) {
+    ld8c(k1, b);
+    ld8c(k2, c);
+  }
+  float s1[8], s2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    s1[i] = 0.f;
+    s2[i] = 0.f;
+  }
+  for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < nvec; v += gridDim.x * 256u) {
+    int c8, w, h, n;
+    pool_split<uint32_t>(v, cv, g.W, g.H, dv, c8, w, h, n);
+    const int ho_hi = min((h + g.ph) / g.sh, g.Ho - 1);
+    const int wo_hi = min((w + g.pw) / g.sw, g.Wo - 1);
+    Vec8<T> vd[4];
+    uint2 pk[4];
+    int idx[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int ho = ho_hi - (t >> 1), wo = wo_hi - (t & 1);
+      const int dh = h - (ho * g.sh - g.ph), dw = w - (wo * g.sw - g.pw);
+      const bool ok = ho >= 0 && wo >= 0 && dh >= 0 && dh < g.kh && dw >= 0 && dw < g.kw;
+      idx[t] = ok ? dh * g.kw + dw : -1;
+      const uint32_t o = ok ? ((static_cast<uint32_t>(n) * g.Ho + ho) * g.Wo + wo) * g.C + c8 : 0u;
+      vd[t].load(dy + o);
+      pk[t] = *reinterpret_cast<const uint2*>(arg + o);
+    }
+    Vec8<T> vx;
+    vx.load(x + static_cast<uint32_t>(v) * 8);
+    Vec8<T> out;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float acc = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t word = i < 4 ? pk[t].x : pk[t].y;
+        if (static_cast<int>((word >> ((i & 3) * 8)) & 0xff) == idx[t]) acc += vd[t].get(i);
+      }
+      const float xi = vx.get(i);
+      const float dz = fmaf(xi, fs[i], fh[i]) > 0.f ? acc : 0.f;
+      if (STATS) {
+        s1[i] += dz;
+        s2[i] += dz * (xi - a[i]);
+      } else {
+        out.set(i, a[i] * dz + b[i] * xi + c[i]);
+      }
+    }
+    if (!STATS) out.store(dx + static_cast<uint32_t>(v) * 8);
+  }
+  if (STATS) {
+    // threads tid, tid + cv, ... share a channel group: combine them through LDS, one partial per block
+    __shared__ float red[2][256 * 8];
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[0][tid * 8 + i] = s1[i];
+      red[1][tid * 8 + i] = s2[i];
+    }
+    __syncthreads();
+    const int rows = 256 / static_cast<int>(cv);
+    for (int q = tid; q < 2 * g.C; q += 256) {
+      const int which = q / g.C, ch = q - which * g.C;
+      const int grp = ch / 8, e = ch % 8;
+      float sum = 0.f;
+      for (int r = 0; r < rows; ++r) sum += red[which][(r * cv + grp) * 8 + e];
+      part[(static_cast<int64_t>(which) * g.C + ch) * gridDim.x + blockIdx.x] = sum;
+    }
+  }
+}
+
 // every element offset of x and y (and the loop index plus one grid stride) fits in 32 bits
 static inline bool fits32(const PoolGeom& g) {
   const int64_t big = static_cast<int64_t>(g.N) * g.C * (g.H * static_cast<int64_t>(g.W) > g.Ho * static_cast<int64_t>(g.Wo)
@@ -294,17 +408,28 @@ static inline int grid_for(int64_t nvec) {
 }
 
 template <typename T>
-static void pool_fwd_t(int is_max, const void* x, void* y, uint8_t* arg, const PoolGeom& g, hipStream_t s) {
+static void pool_fwd_t(int is_max, const void* x, void* y, uint8_t* arg, const PoolGeom& g, hipStream_t s,
+                       const float* scale, const float* shift) {
   const int64_t nvec = static_cast<int64_t>(g.N) * g.Ho * g.Wo * (g.C / 8);
   const bool small = fits32(g);
+  if (scale) {
+    MXAMD_HOST_CHECK(is_max && small && g.kh == 3 && g.kw == 3 && shift != nullptr &&
+                         reinterpret_cast<uintptr_t>(scale) % 16 == 0 && reinterpret_cast<uintptr_t>(shift) % 16 == 0,
+                     "pool_nhwc: the BatchNorm+ReLU prologue is built for 3x3 max pooling (32-bit offsets, "
+                     "16-byte aligned fp32 scale / shift)");
+    hipLaunchKernelGGL((pool_fwd_max3_kernel<T, uint32_t, true>), dim3(grid_for(nvec)), dim3(256), 0, s,
+                       static_cast<const T*>(x), static_cast<T*>(y), arg, g, static_cast<uint32_t>(nvec),
+                       PoolDivs{make_pdiv(g.C / 8), make_pdiv(g.Wo), make_pdiv(g.Ho)}, scale, shift);
+    return;
+  }
 #define MXAMD_POOL_FWD(MX, I)                                                                               \
   hipLaunchKernelGGL((pool_fwd_kernel<T, MX, I>), dim3(grid_for(nvec)), dim3(256), 0, s,                     \
                      static_cast<const T*>(x), static_cast<T*>(y), arg, g, static_cast<I>(nvec),                   \
                      PoolDivs{make_pdiv(g.C / 8), make_pdiv(g.Wo), make_pdiv(g.Ho)})
   if (is_max && small && g.kh == 3 && g.kw == 3) {
-    hipLaunchKernelGGL((pool_fwd_max3_kernel<T, uint32_t>), dim3(grid_for(nvec)), dim3(256), 0, s,
+    hipLaunchKernelGGL((pool_fwd_max3_kernel<T, uint32_t, false>), dim3(grid_for(nvec)), dim3(256), 0, s,
                        static_cast<const T*>(x), static_cast<T*>(y), arg, g, static_cast<uint32_t>(nvec),
-                       PoolDivs{make_pdiv(g.C / 8), make_pdiv(g.Wo), make_pdiv(g.Ho)});
+                       PoolDivs{make_pdiv(g.C / 8), make_pdiv(g.Wo), make_pdiv(g.Ho)}, nullptr, nullptr);
   } else if (is_max) {
     if (small) MXAMD_POOL_FWD(true, uint32_t); else MXAMD_POOL_FWD(true, int64_t);
   } else {
@@ -342,12 +467,55 @@ static PoolGeom make_geom(int N, int H, int W, int C, int Ho, int Wo, int kh, in
   return g;
 }
 
+// scale / shift (optional, fp32 [C]): pool relu(x * scale + shift) instead of x (3x3 max pooling only)
 void pool_nhwc_forward(int dtype, int is_max, const void* x, void* y, uint8_t* arg, int N, int H, int W, int C,
-                       int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip, hipStream_t s) {
+                       int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int cip, hipStream_t s,
+                       const float* scale, const float* shift) {
   PoolGeom g = make_geom(N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, cip);
-  if (dtype == kF16) pool_fwd_t<__half>(is_max, x, y, arg, g, s);
-  else if (dtype == kBF16) pool_fwd_t<__hip_bfloat16>(is_max, x, y, arg, g, s);
-  else pool_fwd_t<float>(is_max, x, y, arg, g, s);
+  if (dtype == kF16) pool_fwd_t<__half>(is_max, x, y, arg, g, s, scale, shift);
+  else if (dtype == kBF16) pool_fwd_t<__hip_bfloat16>(is_max, x, y, arg, g, s, scale, shift);
+  else pool_fwd_t<float>(is_max, x, y, arg, g, s, scale, shift);
+}
+
+void bn_finalize_backward(const float* part, int nblk, int C, int64_t R, const float* mean, const float* gamma,
+                          const float* invstd, float* dgamma, float* dbeta, float* coef, int fix_gamma, int training,
+                          int accum, hipStream_t s);
+
+// Partial rows (= blocks) of the statistics pass of bn_pool_backward: 8 blocks per CU to keep enough gathers
+// in flight, still few partials per channel for the finalize.
+int bn_pool_bwd_blocks() { return 2048; }
+
+// Backward of max_pool(relu(BatchNorm(x))) (3x3 windows, stride >= 2): statistics gather pass -> finalize
+// (dgamma / dbeta into dgamma / dbeta, accumulated when accum; coefficients into coef[3][C]) -> dx gather pass.
+// part: 2 * bn_pool_bwd_blocks() * C floats of scratch.
+void bn_pool_backward(int dtype, const void* x, const void* dy, const uint8_t* arg, void* dx, const float* gamma,
+                      const float* mean, const float* invstd, const float* fscale, const float* fshift, float* part,
+                      float* dgamma, float* dbeta, float* coef, int N, int H, int W, int C, int Ho, int Wo, int kh,
+                      int kw, int sh, int sw, int ph, int pw, int fix_gamma, int training, int accum,
+                      hipStream_t s) {
+  PoolGeom g = make_geom(N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, 1);
+  const int cv = C / 8;
+  MXAMD_HOST_CHECK(256 % cv == 0 && fits32(g) && (kh + sh - 1) / sh <= 2 && (kw + sw - 1) / sw <= 2,
+                   "bn_pool_backward: C / 8 must divide 256, 32-bit offsets, windows covering <= 2 x 2");
+  MXAMD_HOST_CHECK(dtype == kF16 || dtype == kBF16, "bn_pool_backward: f16 / bf16");
+  const uint32_t nvec = static_cast<uint32_t>(static_cast<int64_t>(N) * H * W * cv);
+  const PoolDivs dv{make_pdiv(cv), make_pdiv(W), make_pdiv(H)};
+  const int nb = bn_pool_bwd_blocks();
+  const int64_t R = static_cast<int64_t>(N) * H * W;
+#define MXAMD_BNPOOL(TT)                                                                                           \
+  hipLaunchKernelGGL((bnpool_bwd_kernel<TT, true>), dim3(nb), dim3(256), 0, s, static_cast<const TT*>(x),         \
+                     static_cast<const TT*>(dy), arg, mean, fscale, fshift, nullptr, nullptr, nullptr, part, g, nvec, \
+                     dv);                                                                                          \
+  bn_finalize_backward(part, nb, C, R, mean, gamma, invstd, dgamma, dbeta, coef, fix_gamma, training, accum, s);   \
+  hipLaunchKernelGGL((bnpool_bwd_kernel<TT, false>), dim3(grid_for(nvec)), dim3(256), 0, s,                       \
+                     static_cast<const TT*>(x), static_cast<const TT*>(dy), arg, coef, coef + C, coef + 2 * C,      \
+                     fscale, fshift, static_cast<TT*>(dx), nullptr, g, nvec, dv)
+  if (dtype == kF16) {
+    MXAMD_BNPOOL(__half);
+  } else {
+    MXAMD_BNPOOL(__hip_bfloat16);
+  }
+#undef MXAMD_BNPOOL
 }
 
 void pool_nhwc_backward(int dtype, int is_max, const void* dy, const uint8_t* arg, void* dx, int N, int H, int W,
