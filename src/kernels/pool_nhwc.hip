@@ -393,6 +393,114 @@ __global__ void __launch_bounds__(256) bnpool_bwd_kernel(const T* __restrict__ x
   }
 }
 
+// The same for the stem's exact geometry (3x3 windows, stride 2, pad 1): a thread takes the 2 x 2 input
+// pixels (2a + {0,1}, 2b + {0,1}) of one channel group, which are covered by exactly the four windows
+// (a + {0,1}, b + {0,1}) -- pixel (2a, 2b) by (a, b) only, (2a + 1, 2b + 1) by all four -- so the pooled
+// gradient and argmax words are gathered once per 4 pixels instead of 4 candidates per pixel.
+template <typename T, bool STATS>
+__global__ void __launch_bounds__(256) bnpool_bwd_s2_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                            const uint8_t* __restrict__ arg,
+                                                            const float* __restrict__ k0, const float* __restrict__ k1,
+                                                            const float* __restrict__ k2, const float* __restrict__ k3,
+                                                            const float* __restrict__ k4, T* __restrict__ dx,
+                                                            float* __restrict__ part, PoolGeom g, int Hb, int Wb,
+                                                            uint32_t nvec, PoolDivs dv) {
+  const uint32_t cv = static_cast<uint32_t>(g.C / 8);
+  const int c8f = static_cast<int>((blockIdx.x * 256u + threadIdx.x) % cv) * 8;
+  auto ld8c = [&](const float* p, float* o) {
+    const float4 u = *reinterpret_cast<const float4*>(p + c8f);
+    const float4 w = *reinterpret_cast<const float4*>(p + c8f + 4);
+    o[0] = u.x; o[1] = u.y; o[2] = u.z; o[3] = u.w; o[4] = w.x; o[5] = w.y; o[6] = w.z; o[7] = w.w;
+  };
+  float ka[8], kb[8], kc[8], fs[8], fh[8];
+  ld8c(k0, ka);
+  ld8c(STATS ? k1 : k3, fs);
+  ld8c(STATS ? k2 : k4, fh);
+  if (!STATS) {
+    ld8c(k1, kb);
+    ld8c(k2, kc);
+  }
+  float s1[8], s2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    s1[i] = 0.f;
+    s2[i] = 0.f;
+  }
+  for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < nvec; v += gridDim.x * 256u) {
+    int c8, bb, aa, n;
+    pool_split<uint32_t>(v, cv, Wb, Hb, dv, c8, bb, aa, n);
+    // the four covering windows (a + ta, b + tb)
+    Vec8<T> vd[4];
+    uint2 pk[4];
+    bool wok[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int ho = aa + (t >> 1), wo = bb + (t & 1);
+      wok[t] = ho < g.Ho && wo < g.Wo;
+      const uint32_t o = wok[t] ? ((static_cast<uint32_t>(n) * g.Ho + ho) * g.Wo + wo) * g.C + c8 : 0u;
+      vd[t].load(dy + o);
+      pk[t] = *reinterpret_cast<const uint2*>(arg + o);
+    }
+    // the four input pixels
+    Vec8<T> vx[4];
+    bool pok[4];
+    uint32_t po[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int h = 2 * aa + (q >> 1), w = 2 * bb + (q & 1);
+      pok[q] = h < g.H && w < g.W;
+      po[q] = pok[q] ? ((static_cast<uint32_t>(n) * g.H + h) * g.W + w) * g.C + c8 : 0u;
+      vx[q].load(x + po[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int dh = q >> 1, dw = q & 1;
+      Vec8<T> out;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float acc = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int ta = t >> 1, tb = t & 1;
+          // tap of pixel q inside window t: row dh - 2 ta + 1, column dw - 2 tb + 1 (pixel (2a, .) is not in
+          // window row a + 1: dh = 0, ta = 1 gives row -1)
+          if (dh - 2 * ta + 1 < 0 || dw - 2 * tb + 1 < 0) continue;
+          const int tap = (dh - 2 * ta + 1) * 3 + (dw - 2 * tb + 1);
+          const uint32_t word = i < 4 ? pk[t].x : pk[t].y;
+          if (wok[t] && static_cast<int>((word >> ((i & 3) * 8)) & 0xff) == tap) acc += vd[t].get(i);
+        }
+        const float xi = vx[q].get(i);
+        const float dz = (pok[q] && fmaf(xi, fs[i], fh[i]) > 0.f) ? acc : 0.f;
+        if (STATS) {
+          s1[i] += dz;
+          s2[i] += dz * (xi - ka[i]);
+        } else {
+          out.set(i, ka[i] * dz + kb[i] * xi + kc[i]);
+        }
+      }
+      if (!STATS && pok[q]) out.store(dx + po[q]);
+    }
+  }
+  if (STATS) {
+    __shared__ float red[2][256 * 8];
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[0][tid * 8 + i] = s1[i];
+      red[1][tid * 8 + i] = s2[i];
+    }
+    __syncthreads();
+    const int rows = 256 / static_cast<int>(cv);
+    for (int q = tid; q < 2 * g.C; q += 256) {
+      const int which = q / g.C, ch = q - which * g.C;
+      const int grp = ch / 8, e = ch % 8;
+      float sum = 0.f;
+      for (int r = 0; r < rows; ++r) sum += red[which][(r * cv + grp) * 8 + e];
+      part[(static_cast<int64_t>(which) * g.C + ch) * gridDim.x + blockIdx.x] = sum;
+    }
+  }
+}
+
 // every element offset of x and y (and the loop index plus one grid stride) fits in 32 bits
 static inline bool fits32(const PoolGeom& g) {
   const int64_t big = static_cast<int64_t>(g.N) * g.C * (g.H * static_cast<int64_t>(g.W) > g.Ho * static_cast<int64_t>(g.Wo)
@@ -502,6 +610,28 @@ void bn_pool_backward(int dtype, const void* x, const void* dy, const uint8_t* a
   const PoolDivs dv{make_pdiv(cv), make_pdiv(W), make_pdiv(H)};
   const int nb = bn_pool_bwd_blocks();
   const int64_t R = static_cast<int64_t>(N) * H * W;
+  if (kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1) {
+    // 2 x 2 input pixels per thread, the four covering windows gathered once
+    const int Hb = (H + 1) / 2, Wb = (W + 1) / 2;
+    MXAMD_HOST_CHECK(Ho == (H - 1) / 2 + 1 && Wo == (W - 1) / 2 + 1, "bn_pool_backward: stride-2 output extent");
+    const uint32_t nv4 = static_cast<uint32_t>(static_cast<int64_t>(N) * Hb * Wb * cv);
+    const PoolDivs dv4{make_pdiv(cv), make_pdiv(Wb), make_pdiv(Hb)};
+#define MXAMD_BNPOOL4(TT)                                                                                          \
+    hipLaunchKernelGGL((bnpool_bwd_s2_kernel<TT, true>), dim3(nb), dim3(256), 0, s, static_cast<const TT*>(x),    \
+                       static_cast<const TT*>(dy), arg, mean, fscale, fshift, nullptr, nullptr, nullptr, part, g, Hb, \
+                       Wb, nv4, dv4);                                                                              \
+    bn_finalize_backward(part, nb, C, R, mean, gamma, invstd, dgamma, dbeta, coef, fix_gamma, training, accum, s); \
+    hipLaunchKernelGGL((bnpool_bwd_s2_kernel<TT, false>), dim3(grid_for(nv4)), dim3(256), 0, s,                  \
+                       static_cast<const TT*>(x), static_cast<const TT*>(dy), arg, coef, coef + C, coef + 2 * C,    \
+                       fscale, fshift, static_cast<TT*>(dx), nullptr, g, Hb, Wb, nv4, dv4)
+    if (dtype == kF16) {
+      MXAMD_BNPOOL4(__half);
+    } else {
+      MXAMD_BNPOOL4(__hip_bfloat16);
+    }
+#undef MXAMD_BNPOOL4
+    return;
+  }
 #define MXAMD_BNPOOL(TT)                                                                                           \
   hipLaunchKernelGGL((bnpool_bwd_kernel<TT, true>), dim3(nb), dim3(256), 0, s, static_cast<const TT*>(x),         \
                      static_cast<const TT*>(dy), arg, mean, fscale, fshift, nullptr, nullptr, nullptr, part, g, nvec, \
