@@ -165,6 +165,8 @@ class BatchNormNHWC(torch.autograd.Function):
         ctx.save_for_backward(x, y if relu_mode == 1 else mask, g, mean, invstd,
                               scale if relu_mode == 2 else None, shift if relu_mode == 2 else None)
         ctx.cfg = (relu_mode, bool(training), addend is not None, gamma.dtype, beta.dtype)
+        # the addend is a tee conv's passthrough: the shortcut gradient may be handed over lazily
+        ctx.tee_key = getattr(addend, '_mxamd_tee_key', None) if (addend is not None and relu_mode == 3) else None
         ctx.bn_token = None
         if training and relu_mode in (0, 2, 3) and _BN_BWD_FUSE[0] and pool is None:
             # a consumer convolution's dgrad (big-tile kernel) may emit this BN's backward statistics
@@ -249,6 +251,12 @@ class BatchNormNHWC(torch.autograd.Function):
         ymask = y if relu_mode == 3 else None
         y = y if relu_mode == 1 else None
         ds = ctx.add_src if dz is not None else None
+        # identity shortcut into a tee data gradient that takes a masked addend: d_addend = gy * mask is
+        # not written here; gy goes back with the mask attached (ConvTeeNHWC._tee_dgrad multiplies it in)
+        lazy = (dz is not None and ds is None and ymask is not None and ctx.tee_key is not None
+                and lazy_shortcut_ok(ctx.tee_key))
+        if lazy:
+            dz = None
         dkw = {}
         if ds is not None:
             ds_nblk = lib.bn_tail_ds_rows(R, C)
@@ -262,6 +270,9 @@ class BatchNormNHWC(torch.autograd.Function):
         if ds is not None:
             # consumed by the shortcut BN's backward (token + version checked there)
             dz._mxamd_bn_bwd = (ds_part, ds_nblk, ds[6], dz._version)
+        if lazy:
+            gy._mxamd_lazy_mask = (ymask, gy._version)
+            dz = gy
         if direct:
             # returning None: torch still runs the leaves' AccumulateGrad node with an undefined
             # gradient, which fires their post-accumulate hooks (bucketed all-reduce readiness)
@@ -1200,7 +1211,7 @@ def pw_bnb_ok(kin, nout, add, bn_src):
             and bool(_K.lib().conv_pw_stream_bnb_ok(int(kin), int(nout), int(bool(add)), int(bn_src[5]))))
 
 
-def conv_pw(x, w2, bn_stats=False, addend=None, bn_bwd=None):
+def conv_pw(x, w2, bn_stats=False, addend=None, bn_bwd=None, addend_mask=None):
     """y = x . w2^T (+ addend) for NHWC ``x`` [..., Cin] and ``w2`` [Cout, Cin] on the streaming 1x1
     kernel; ``bn_stats``: BatchNorm sum / sum-of-squares partials in ``y._mxamd_bn_part`` (one per
     workgroup); ``addend`` (the output's shape and dtype) is added in the epilogue.  ``bn_bwd`` (a
@@ -1232,6 +1243,11 @@ def conv_pw(x, w2, bn_stats=False, addend=None, bn_bwd=None):
         assert z.shape == y.shape and z.dtype == y.dtype and z.is_contiguous() and z.data_ptr() % 16 == 0
         bkw = dict(bn_z=z.data_ptr(), bn_mask=_p(bmask), bn_mean=bmean.data_ptr(), bn_scale=_p(bscale),
                    bn_shift=_p(bshift), bn_mode=int(bmode))
+    if addend_mask is not None:
+        # addend = dy * ReLU bits of a residual tail (its d_addend never materialised: _tee_dgrad)
+        assert bn_bwd is not None and addend is not None and addend_mask.dtype == torch.uint8
+        assert addend_mask.numel() * 8 == addend.numel() and addend_mask.is_contiguous()
+        bkw['addend_mask'] = addend_mask.data_ptr()
     lib.conv_pw_stream(_DT[x.dtype], x.data_ptr(), w2.data_ptr(), y.data_ptr(), _zero_page(x.device).data_ptr(), M, C,
                        K, _p(part), grid, _stream(), _p(addend), wt, **bkw)
     if bn_bwd is not None:
@@ -1646,7 +1662,11 @@ class ConvTeeNHWC(torch.autograd.Function):
         ctx.w_ref = w
         ctx.inplace_grad = inplace_grad
         ctx.bn_src = getattr(x, '_mxamd_bn_src', None)
-        return y, x.view_as(x)
+        xp = x.view_as(x)
+        # the passthrough feeds the block's residual tail: its gradient (the tail's dy * ReLU mask) may
+        # arrive unmaterialised when this data gradient runs the masked-addend streaming kernel
+        xp._mxamd_tee_key = _tee_key(x, w, ctx.bn_src)
+        return y, xp
 
     @staticmethod
     def backward(ctx, gy, gpass):
@@ -1665,12 +1685,51 @@ class ConvTeeNHWC(torch.autograd.Function):
         return dx, dw, None
 
 
+def _tee_key(x, w, bn_src):
+    return ('teedgrad', tuple(x.shape), tuple(w.shape), x.dtype) + (('bnbwd',) if _bn_bwd_fusable(bn_src, x.shape)
+                                                                     else ())
+
+
+_LAZY_DZ = [os.environ.get('MXAMD_LAZY_SHORTCUT_GRAD', '1') != '0']
+_LAZY_USED = [0]    # tee data gradients that consumed a lazy shortcut gradient (tests)
+
+
+def lazy_shortcut_ok(tee_key):
+    """Whether a residual tail may hand its shortcut gradient dz = dy * mask to the tee data gradient
+    unmaterialised: only once that data gradient is known to run the masked-addend streaming kernel."""
+    return _LAZY_DZ[0] and tee_key is not None and _ALGO.get(_akey(tee_key)) == 'pw+bn'
+
+
+def _unpack_lazy_dz(gpass):
+    """(dy, mask) of a lazy shortcut gradient (see BatchNormNHWC.backward), or None."""
+    lz = getattr(gpass, '_mxamd_lazy_mask', None) if gpass is not None else None
+    if lz is None or lz[1] != gpass._version:
+        return None
+    return lz[0]
+
+
+def _materialize_dz(gpass, mask):
+    """dy * mask bits (the fallback when the chosen data gradient cannot take the masked addend)."""
+    bits = (mask.view(-1, 1) >> torch.arange(8, device=mask.device, dtype=torch.uint8)) & 1
+    return gpass * bits.view(gpass.shape).to(gpass.dtype)
+
+
 def _tee_dgrad(gy, x, w, gpass, inplace, bn_src=None):
     """dX = dY . W (+ dShortcut) of a 1x1 stride-1 conv: the in-tree big-tile MFMA kernel with the
-    shortcut gradient read in its epilogue (beta = 1), or hipBLASLt addmm -- autotuned per shape."""
+    shortcut gradient read in its epilogue (beta = 1), or hipBLASLt addmm -- autotuned per shape.
+    A lazy dShortcut (the residual tail's dy with its ReLU mask, never multiplied out) goes to the
+    streaming kernel's masked-addend stage."""
     K, C = w.shape[0], w.shape[3]
     g2 = gy.reshape(-1, K)
     w2 = w.reshape(K, C)
+    amask = _unpack_lazy_dz(gpass)
+    if amask is not None:
+        key = _tee_key(x, w, bn_src)
+        if (_ALGO.get(_akey(key)) == 'pw+bn' and _bn_bwd_fusable(bn_src, x.shape) and pw_ok(gy, K, C)
+                and pw_bnb_ok(K, C, True, bn_src) and gpass.is_contiguous() and gpass.data_ptr() % 16 == 0):
+            _LAZY_USED[0] += 1
+            return conv_pw(gy, w2.t(), addend=gpass, bn_bwd=bn_src, addend_mask=amask)
+        gpass, inplace = _materialize_dz(gpass, amask), True
 
     def mm():
         if gpass is not None and inplace and gpass.is_contiguous():

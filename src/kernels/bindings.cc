@@ -196,7 +196,7 @@ void weight_taps_t(int elem_bytes, const void* w, void* out, int K, int RS, int 
 void conv_pw_stream(int dtype, const void* x, const void* w, void* y, const void* zero, int M, int kin, int nout,
                     float* part, int grid, hipStream_t s, const void* addend, int wt, const void* bn_z,
                     const uint8_t* bn_mask, const float* bn_mean, const float* bn_scale, const float* bn_shift,
-                    int bn_mode);
+                    int bn_mode, const uint8_t* addend_mask);
 int conv_pw_stream_bnb_ok(int kin, int nout, int add, int mode);
 void conv_gen(int dtype, int mode, const void* src, const void* wsrc, const float* bias, void* dst, const int* geom,
               int splits, hipStream_t s);
@@ -302,16 +302,18 @@ PYBIND11_MODULE(_hip_kernels, m) {
   }, pybind11::arg("M"), pybind11::arg("kin"), pybind11::arg("nout"), pybind11::arg("ncu"), pybind11::arg("add") = 0);
   m.def("conv_pw_stream", [](int dt, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t zero, int M, int kin, int nout,
                              uintptr_t part, int grid, uintptr_t s, uintptr_t addend, int wt, uintptr_t bn_z,
-                             uintptr_t bn_mask, uintptr_t bn_mean, uintptr_t bn_scale, uintptr_t bn_shift, int bn_mode) {
+                             uintptr_t bn_mask, uintptr_t bn_mean, uintptr_t bn_scale, uintptr_t bn_shift, int bn_mode,
+                             uintptr_t addend_mask) {
     conv_pw_stream(dt, P<const void>(x), P<const void>(w), P<void>(y), P<const void>(zero), M, kin, nout,
                    P<float>(part), grid, S(s), P<const void>(addend), wt, P<const void>(bn_z), P<const uint8_t>(bn_mask),
-                   P<const float>(bn_mean), P<const float>(bn_scale), P<const float>(bn_shift), bn_mode);
+                   P<const float>(bn_mean), P<const float>(bn_scale), P<const float>(bn_shift), bn_mode,
+                   P<const uint8_t>(addend_mask));
     check_launch("conv_pw_stream");
   }, pybind11::arg("dt"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("zero"),
      pybind11::arg("M"), pybind11::arg("kin"), pybind11::arg("nout"), pybind11::arg("part"), pybind11::arg("grid"),
      pybind11::arg("s"), pybind11::arg("addend"), pybind11::arg("wt") = 0, pybind11::arg("bn_z") = 0,
      pybind11::arg("bn_mask") = 0, pybind11::arg("bn_mean") = 0, pybind11::arg("bn_scale") = 0,
-     pybind11::arg("bn_shift") = 0, pybind11::arg("bn_mode") = 0);
+     pybind11::arg("bn_shift") = 0, pybind11::arg("bn_mode") = 0, pybind11::arg("addend_mask") = 0);
   m.def("conv_pw_stream_bnb_ok", &conv_pw_stream_bnb_ok);
   // general implicit-GEMM convolution: grouped / dilated / 1-3-D / fp32 / transposed (src/kernels/conv_gen.hip)
   m.def("conv_gen", [](int dt, int mode, uintptr_t src, uintptr_t wsrc, uintptr_t bias, uintptr_t dst,

@@ -89,9 +89,11 @@ struct PwBnb {
   const float* mean;
   const float* scale;     // kPwBnbFromZ
   const float* shift;
+  const uint8_t* amask;   // AMK: the addend is masked by these bits ([M * NT / 8]): addend = dy * mask of a
+                          // residual tail's ReLU, its d_addend never materialised (kernel_fns._tee_dgrad)
 };
 
-template <int KIN, int NOUT, int WPC = 2, bool ADD = false, int BNB = kPwBnbNone>
+template <int KIN, int NOUT, int WPC = 2, bool ADD = false, int BNB = kPwBnbNone, bool AMK = false>
 struct PwCfg {
   static constexpr bool EXT = ADD || BNB != kPwBnbNone;    // extra streams besides the input
   static constexpr int BM = pw_bm(KIN, NOUT, EXT);
@@ -105,7 +107,8 @@ struct PwCfg {
   static constexpr int STAGE_ADD = ADD ? BM * NOUT * 2 : 0;  // its addend rows (linear)
   static constexpr int STAGE_Z = BNB ? BM * NOUT * 2 : 0;    // the BN input rows (linear)
   static constexpr int STAGE_M = BNB == kPwBnbMask ? (BM * NOUT / 8 + 1023) / 1024 * 1024 : 0;  // mask bytes
-  static constexpr int STAGE = STAGE_IN + STAGE_ADD + STAGE_Z + STAGE_M;
+  static constexpr int STAGE_AM = AMK ? (BM * NOUT / 8 + 1023) / 1024 * 1024 : 0;   // addend mask bytes
+  static constexpr int STAGE = STAGE_IN + STAGE_ADD + STAGE_Z + STAGE_M + STAGE_AM;
   static constexpr int LPT = STAGE_IN / (512 * 16);        // LDS-DMA instructions per thread per tile
   static constexpr int APT = STAGE_ADD / (512 * 16);       // ... for the addend
   // with an addend, a tile's 1 KB LDS-DMA instructions go round-robin over the 8 waves (rounds may be
@@ -114,6 +117,7 @@ struct PwCfg {
   static constexpr int TA = STAGE_ADD / 1024;
   static constexpr int TZ = STAGE_Z / 1024;
   static constexpr int TM = STAGE_M / 1024;
+  static constexpr int TAM = STAGE_AM / 1024;
   static constexpr int PITCH = NOUT * 2 + 16;              // epilogue image row pitch
   static constexpr int EPI = BM * PITCH;
   static constexpr int OCH = NOUT / 8;                     // 16-byte chunks per output row
@@ -134,8 +138,10 @@ struct PwCfg {
   static_assert(BNB != kPwBnbMask || (NOUT / 8) % 16 == 0, "mask rows of whole 16-byte chunks");
   static_assert((BM * OCH) % 512 == 0 || BM * OCH < 512, "whole store rounds, or a single partial one");
   static_assert(512 % OCH == 0, "a thread keeps one output chunk");
-  static_assert(D * ((TI + 7) / 8 + (TA + 7) / 8 + (TZ + 7) / 8 + (TM + 7) / 8 + SPT) < (EXT ? 40 : 64),
+  static_assert(D * ((TI + 7) / 8 + (TA + 7) / 8 + (TZ + 7) / 8 + (TM + 7) / 8 + (TAM + 7) / 8 + SPT) <
+                    (EXT ? 40 : 64),
                 "vmcnt range (vm_wait_n covers < 40)");
+  static_assert(!AMK || (ADD && (NOUT / 8) % 16 == 0), "the addend mask rides with an addend, whole 16-byte rows");
   // resident weights: a quarter of the VGPR budget (128 at 2 workgroups per CU, 256 at 1)
   static_assert(FC * KS * 4 <= (WPC == 1 ? 128 : 64), "resident weights exceed the register budget");
   static_assert(ROWB % 128 == 0, "rows of whole 128-byte swizzle groups");
@@ -179,11 +185,11 @@ __device__ __forceinline__ void vm_wait_le(int n) {
 
 // NOUT: output channels per workgroup; S: slices of the layer's NOUT * S output channels (the
 // workgroups of one tile's slices are adjacent in the XCD-aware order, so they share its input in L2)
-template <typename T, int KIN, int NOUT, bool STATS, bool ADD, int WPC, int S, int BNB>
+template <typename T, int KIN, int NOUT, bool STATS, bool ADD, int WPC, int S, int BNB, bool AMK = false>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WPC))) conv_pw_stream_kernel(
     const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y, const T* __restrict__ zero, int M, int ntiles,
     float* __restrict__ part, const T* __restrict__ addend, int wt, PwBnb bnb) {
-  using C = PwCfg<KIN, NOUT, WPC, ADD, BNB>;
+  using C = PwCfg<KIN, NOUT, WPC, ADD, BNB, AMK>;
   constexpr bool EXT = C::EXT;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x;
@@ -310,10 +316,25 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
       __builtin_amdgcn_global_load_lds((gbl_void*)src,
                                        (lds_void*)(sb + C::STAGE_IN + C::STAGE_ADD + C::STAGE_Z + i * 1024), 16, 0, 0);
     }
+    // the addend's mask bytes (same layout as the BN mask)
+#pragma unroll
+    for (int j = 0; j < (C::TAM + 7) / 8; ++j) {
+      const int i = j * 8 + wid;
+      if (i >= C::TAM) break;
+      const int byte = (i * 64 + lane) * 16;
+      const int row = byte / (NOUT / 8);
+      const int p = t * C::BM + row;
+      const void* src = (row < C::BM && p < M)
+                            ? static_cast<const void*>(bnb.amask + (static_cast<int64_t>(p) * NT + slice * NOUT) / 8 +
+                                                       byte % (NOUT / 8))
+                            : static_cast<const void*>(zero);
+      __builtin_amdgcn_global_load_lds(
+          (gbl_void*)src, (lds_void*)(sb + C::STAGE_IN + C::STAGE_ADD + C::STAGE_Z + C::STAGE_M + i * 1024), 16, 0, 0);
+    }
   };
   // LDS-DMA instructions this wave issues per tile (uniform over the wave)
   const int ops_per_tile = EXT ? (C::TI - wid + 7) / 8 + (C::TA - wid + 7) / 8 + (C::TZ - wid + 7) / 8 +
-                                      (C::TM - wid + 7) / 8
+                                      (C::TM - wid + 7) / 8 + (C::TAM - wid + 7) / 8
                                 : C::LPT;
 
   const int my_tiles = wg < ntiles ? (ntiles - wg + gs - 1) / gs : 0;
@@ -411,8 +432,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
       if (ADD) {
         Vec8<T> a;
         a.raw = *reinterpret_cast<const uint4*>(sb + C::STAGE_IN + pix * (NOUT * 2) + c8 * 16);
+        const uint32_t amb =
+            AMK ? static_cast<uint32_t>(*reinterpret_cast<const uint8_t*>(
+                      sb + C::STAGE_IN + C::STAGE_ADD + C::STAGE_Z + C::STAGE_M + pix * (NOUT / 8) + c8))
+                : 0xffu;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v.set(q, v.get(q) + a.get(q));
+        for (int q = 0; q < 8; ++q) v.set(q, v.get(q) + (((amb >> q) & 1u) ? a.get(q) : 0.f));
       }
       const bool live = in_tile && p < M;
       if (BNB && live) {
@@ -469,19 +494,20 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
   }
 }
 
-template <typename T, int KIN, int NOUT, int WPC, int S, bool STATS, bool ADD, int BNB = kPwBnbNone>
+template <typename T, int KIN, int NOUT, int WPC, int S, bool STATS, bool ADD, int BNB = kPwBnbNone, bool AMK = false>
 void launch_pw_v(const void* x, const void* w, void* y, const void* zero, int M, float* part, const void* addend,
                  int grid, hipStream_t s, int wt, const PwBnb& bnb = PwBnb{}) {
-  using C = PwCfg<KIN, NOUT, WPC, ADD, BNB>;
+  using C = PwCfg<KIN, NOUT, WPC, ADD, BNB, AMK>;
   static_assert(C::SMEM <= C::LDS && C::NST >= 2, "LDS budget / ring depth");
   static bool set = false;
   if (!set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD, WPC, S, BNB>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
+    hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD, WPC, S, BNB, AMK>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
     set = true;
   }
   const int ntiles = (M + C::BM - 1) / C::BM;
-  hipLaunchKernelGGL((conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD, WPC, S, BNB>), dim3(grid), dim3(512), C::SMEM,
+  hipLaunchKernelGGL((conv_pw_stream_kernel<T, KIN, NOUT, STATS, ADD, WPC, S, BNB, AMK>), dim3(grid), dim3(512), C::SMEM,
                      s, static_cast<const T*>(x), static_cast<const T*>(w), static_cast<T*>(y),
                      static_cast<const T*>(zero), M, ntiles, part, static_cast<const T*>(addend), wt, bnb);
 }
@@ -498,7 +524,11 @@ bool launch_pw_bnb(const void* x, const void* w, void* y, const void* zero, int 
                    int grid, hipStream_t s, int wt, const PwBnb& bnb, int mode) {
   if constexpr ((NOUT / 8) % 16 == 0) {
     if (addend && mode == kPwBnbMask) {
-      launch_pw_v<T, KIN, NOUT, 1, S, false, true, kPwBnbMask>(x, w, y, zero, M, part, addend, grid, s, wt, bnb);
+      if (bnb.amask)
+        launch_pw_v<T, KIN, NOUT, 1, S, false, true, kPwBnbMask, true>(x, w, y, zero, M, part, addend, grid, s, wt,
+                                                                        bnb);
+      else
+        launch_pw_v<T, KIN, NOUT, 1, S, false, true, kPwBnbMask>(x, w, y, zero, M, part, addend, grid, s, wt, bnb);
       return true;
     }
   }
@@ -594,15 +624,18 @@ int conv_pw_stream_grid(int M, int kin, int nout, int ncu, int add) {
   return per * sl;
 }
 
+// addend_mask (optional, BN-mask mode with an addend only): the addend is dy * these ReLU bits
 void conv_pw_stream(int dtype, const void* x, const void* w, void* y, const void* zero, int M, int kin, int nout,
                     float* part, int grid, hipStream_t s, const void* addend, int wt, const void* bn_z,
                     const uint8_t* bn_mask, const float* bn_mean, const float* bn_scale, const float* bn_shift,
-                    int bn_mode) {
+                    int bn_mode, const uint8_t* addend_mask) {
   MXAMD_HOST_CHECK(conv_pw_stream_ok(kin, nout), "conv_pw_stream: unsupported (Cin, Cout)");
   MXAMD_HOST_CHECK(grid >= 1 && grid % conv_pw_stream_slices(kin, nout) == 0 &&
                    (int64_t)M * nout * 2 < (1ll << 31) - 64 && (int64_t)M * kin < (1ll << 31),
                    "conv_pw_stream: tensor too large for 32-bit offsets");
-  PwBnb bnb{bn_z, bn_mask, bn_mean, bn_scale, bn_shift};
+  PwBnb bnb{bn_z, bn_mask, bn_mean, bn_scale, bn_shift, addend_mask};
+  MXAMD_HOST_CHECK(addend_mask == nullptr || (addend && bn_z && bn_mode == kPwBnbMask),
+                   "conv_pw_stream: the addend mask is built for the tee data gradient with the tail's BN statistics");
   const PwBnb* pb = nullptr;
   if (bn_z) {
     MXAMD_HOST_CHECK(part && bn_mean && conv_pw_stream_bnb_ok(kin, nout, addend != nullptr, bn_mode) &&

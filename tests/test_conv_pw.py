@@ -1,5 +1,6 @@
 """Streaming 1x1 convolution (src/kernels/conv_pw.hip) vs fp32 PyTorch: outputs and the fused BatchNorm
 statistics partials."""
+import numpy as np
 import pytest
 import torch
 
@@ -153,3 +154,69 @@ def test_conv_pw_tee_bn_backward_stats_mask(kin, nout, M, dt):
     r1, r2 = _bnb_ref(y, z, mean, mask=mask)
     torch.testing.assert_close(s1, r1, rtol=1e-3, atol=1e-2 * float(r1.abs().max() + 1))
     torch.testing.assert_close(s2, r2, rtol=1e-3, atol=1e-2 * float(r2.abs().max() + 1))
+
+
+@pytest.mark.parametrize('kin,nout,M,dt', [(128, 256, 3136 + 5, torch.float16), (256, 1024, 1568 + 3, torch.float16),
+                                           (512, 2048, 200, torch.bfloat16)])
+def test_conv_pw_tee_masked_addend(kin, nout, M, dt):
+    """The tee dgrad's addend as dy * (a residual tail's ReLU bits), the product never materialised: output and
+    the BN-backward statistics equal the materialised-addend launch bit for bit."""
+    dev = torch.device('cuda', 0)
+    g = torch.Generator().manual_seed(7 * kin + nout)
+    x = (torch.rand(M, kin, generator=g) * 2 - 1).to(dev, dt).view(1, 1, M, kin)
+    wk = ((torch.rand(kin, nout, generator=g) * 2 - 1) / kin ** 0.5).to(dev, dt)
+    dy = (torch.rand(M, nout, generator=g) * 2 - 1).to(dev, dt).view(1, 1, M, nout)
+    amask = torch.randint(0, 256, (M * nout // 8,), generator=g, dtype=torch.int32).to(torch.uint8).to(dev)
+    z = (torch.rand(M, nout, generator=g) * 2 - 1).to(dev, dt).view(1, 1, M, nout)
+    mask = torch.randint(0, 256, (M * nout // 8,), generator=g, dtype=torch.int32).to(torch.uint8).to(dev)
+    mean = (torch.rand(nout, generator=g) * 0.2 - 0.1).to(dev)
+    src = (z, mean, None, None, mask, 3, 'tok')
+    dz = KF._materialize_dz(dy, amask)
+    ref = KF.conv_pw(x, wk.t(), addend=dz, bn_bwd=src)
+    y = KF.conv_pw(x, wk.t(), addend=dy, bn_bwd=src, addend_mask=amask)
+    assert torch.equal(y, ref)
+    assert torch.equal(y._mxamd_bn_bwd[0], ref._mxamd_bn_bwd[0])
+
+
+def test_resnet_lazy_shortcut_gradient_matches_materialised():
+    """ResNet-50 (fused NHWC): with the tee data gradients on the masked-addend streaming kernel, the
+    residual tails hand their shortcut gradient over unmaterialised; every parameter gradient equals
+    the materialised run's."""
+    import mxnet_maintenance_amd as mx
+    from mxnet_maintenance_amd import autograd, gluon, nd
+    ctx = mx.gpu(0)
+    mx.random.seed(3)
+    net = gluon.model_zoo.vision.get_model('resnet50_v1b', layout='NHWC', fuse=True, classes=10)
+    net.initialize(mx.init.Xavier(), ctx=ctx)
+    net.cast('float16')
+    net.hybridize(static_alloc=True, static_shape=True)
+    x = nd.random.uniform(-1, 1, shape=(8, 64, 64, 3), ctx=ctx).astype('float16')
+    y = nd.array([1, 2, 3, 4, 5, 6, 7, 8], ctx=ctx)
+    loss_fn = gluon.loss.SoftmaxCrossEntropyLoss()
+    params = [p for p in net.collect_params().values() if p.grad_req != 'null']
+
+    def grads():
+        with autograd.record():
+            loss = loss_fn(net(x), y)
+        loss.backward()
+        return [p.grad(ctx).astype('float32').asnumpy().copy() for p in params]
+    grads()                                   # autotune every shape
+    forced = 0
+    for k in list(KF._ALGO):
+        if (k[0] == 'teedgrad' and 'bnbwd' in k
+                and KF.pw_ok(torch.empty(1, 1, 8, k[2][0], dtype=k[3], device='cuda'), k[2][0], k[2][3])
+                and KF._K.lib().conv_pw_stream_bnb_ok(k[2][0], k[2][3], 1, 3)):
+            KF._ALGO[k] = 'pw+bn'
+            forced += 1
+    assert forced > 0
+    KF._LAZY_DZ[0] = False
+    ref = grads()
+    ref2 = grads()
+    KF._LAZY_DZ[0] = True
+    used = KF._LAZY_USED[0]
+    got = grads()
+    assert KF._LAZY_USED[0] > used
+    for a, b, c in zip(got, ref, ref2):
+        scale = float(np.abs(b).max()) + 1e-6
+        noise = float(np.abs(c - b).max()) / scale       # run-to-run spread of the materialised path
+        assert float(np.abs(a - b).max()) / scale <= max(2 * noise, 2e-3)
