@@ -87,6 +87,16 @@ def _zeros_f32(n, dev):
     return z
 
 
+class _BnToken:
+    """Identifies one BatchNorm call for the statistics / gradient hand-offs between fused kernels.
+    ``lazy``: (dy, mask, version) when a residual tail handed this (shortcut) BatchNorm its incoming
+    gradient as dy with the tail's ReLU mask still to apply."""
+    __slots__ = ('lazy',)
+
+    def __init__(self):
+        self.lazy = None
+
+
 class BatchNormNHWC(torch.autograd.Function):
     """BatchNorm over the last (channel) axis with optional fused residual add + ReLU."""
 
@@ -172,7 +182,7 @@ class BatchNormNHWC(torch.autograd.Function):
             # a consumer convolution's dgrad (big-tile kernel) may emit this BN's backward statistics
             # from its epilogue: it needs z (= x here), mean, the ReLU mask source, and a token that
             # identifies this BN call (checked in backward)
-            ctx.bn_token = object()
+            ctx.bn_token = _BnToken()
             y._mxamd_bn_src = (x, mean, scale if relu_mode == 2 else None, shift if relu_mode == 2 else None,
                                mask if relu_mode == 3 else None, relu_mode, ctx.bn_token)
         ctx.refs = (gamma, beta)
@@ -214,6 +224,17 @@ class BatchNormNHWC(torch.autograd.Function):
                 lib.pool_nhwc_backward(_DT[x.dtype], 1, gy.data_ptr(), y.data_ptr(), gyd.data_ptr(), *ctx.pool,
                                        _stream())
                 gy, y = gyd, None
+        # a residual tail handed this (shortcut) BatchNorm its gradient lazily: gy is the tail's dy and the
+        # tail's ReLU mask is applied in this backward's passes (unless autograd summed other gradients in)
+        lazy_mask = None
+        tok = ctx.bn_token
+        if tok is not None and tok.lazy is not None:
+            dy_l, mask_l, ver_l = tok.lazy
+            tok.lazy = None
+            if gy is dy_l and gy._version == ver_l and relu_mode == 0 and not has_add and ctx.pool is None:
+                lazy_mask = mask_l
+            else:
+                gy = (gy - dy_l + _materialize_dz(dy_l, mask_l)).contiguous()
         dx = torch.empty_like(x)
         dz = torch.empty_like(x) if has_add else None
         ext = getattr(gy, '_mxamd_bn_bwd', None)
@@ -255,8 +276,14 @@ class BatchNormNHWC(torch.autograd.Function):
         # not written here; gy goes back with the mask attached (ConvTeeNHWC._tee_dgrad multiplies it in)
         lazy = (dz is not None and ds is None and ymask is not None and ctx.tee_key is not None
                 and lazy_shortcut_ok(ctx.tee_key))
-        if lazy:
+        # projection shortcut: its BatchNorm takes dy + this mask directly (relu-from-mask apply)
+        lazy_ds = (dz is not None and ds is not None and ymask is not None and _LAZY_DZ[0]
+                   and isinstance(ds[6], _BnToken))
+        if lazy or lazy_ds:
             dz = None
+        kmode = relu_mode
+        if lazy_mask is not None:
+            kmode, ymask = 3, lazy_mask
         dkw = {}
         if ds is not None:
             ds_nblk = lib.bn_tail_ds_rows(R, C)
@@ -265,11 +292,16 @@ class BatchNormNHWC(torch.autograd.Function):
         lib.bn_nhwc_backward(_DT[x.dtype], x.data_ptr(), gy.data_ptr(), _p(y), _p(ymask), dx.data_ptr(), _p(dz),
                              g.data_ptr(),
                              mean.data_ptr(), invstd.data_ptr(), _p(fscale), _p(fshift), part.data_ptr(), dg_ptr,
-                             db_ptr, out[2].data_ptr(), R, C, relu_mode, 0, int(training), accum, _stream(),
+                             db_ptr, out[2].data_ptr(), R, C, kmode, 0, int(training), accum, _stream(),
                              ext_nblk, **dkw)
         if ds is not None:
             # consumed by the shortcut BN's backward (token + version checked there)
-            dz._mxamd_bn_bwd = (ds_part, ds_nblk, ds[6], dz._version)
+            if lazy_ds:
+                gy._mxamd_bn_bwd = (ds_part, ds_nblk, ds[6], gy._version)
+                ds[6].lazy = (gy, ymask, gy._version)
+                dz = gy
+            else:
+                dz._mxamd_bn_bwd = (ds_part, ds_nblk, ds[6], dz._version)
         if lazy:
             gy._mxamd_lazy_mask = (ymask, gy._version)
             dz = gy

@@ -448,7 +448,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_tail_bwd_ds_kernel(
       s2[i] += d * (vz.get(i) - km[i]);
     }
     out.store(dx + off);
-    vstore(dz, dz_out + off, nt >= 2 ? 2 : 0);
+    if (dz_out != nullptr) vstore(dz, dz_out + off, nt >= 2 ? 2 : 0);   // null: the shortcut gradient stays lazy
   };
   int64_t r = r0 + lane_r;
   for (; r + (UNR - 1) * rpi < r1; r += UNR * rpi) {
@@ -636,8 +636,8 @@ static void bn_backward_impl(const void* x, const void* dy, const void* y, const
   T* dza = static_cast<T*>(dz);
   if (ds_z) {
     // residual tail whose addend came from a shortcut BatchNorm: its backward statistics ride along
-    MXAMD_HOST_CHECK(relu_mode == kReluFromMask && dz && ds_mean && ds_part,
-                     "bn_nhwc_backward: shortcut statistics need the tail's mask mode, dz and the BN's mean");
+    MXAMD_HOST_CHECK(relu_mode == kReluFromMask && ds_mean && ds_part,
+                     "bn_nhwc_backward: shortcut statistics need the tail's mask mode and the BN's mean");
     int dnblk;
     const int64_t drpb = bn_rows_per_block(R, C, g, &dnblk, bn_tail_blocks(), 64);
     hipLaunchKernelGGL((bn_tail_bwd_ds_kernel<T>), dim3(dnblk, C / g.cb), dim3(kBnThreads), 0, s, xa, dya, mask, A, B,

@@ -220,3 +220,44 @@ def test_resnet_lazy_shortcut_gradient_matches_materialised():
         scale = float(np.abs(b).max()) + 1e-6
         noise = float(np.abs(c - b).max()) / scale       # run-to-run spread of the materialised path
         assert float(np.abs(a - b).max()) / scale <= max(2 * noise, 2e-3)
+
+
+@pytest.mark.parametrize('second_consumer', [False, True])
+def test_projection_shortcut_lazy_gradient(second_consumer):
+    """relu(BN1(x) + BN2(s)) with BN2 the projection shortcut: the tail hands BN2 its dy and ReLU mask
+    instead of d_addend; with a second consumer of BN2's output autograd sums the gradients and BN2
+    corrects the sum. Gradients equal the materialised path's."""
+    from mxnet_maintenance_amd.ops import hip_ops as H
+    dev = torch.device('cuda', 0)
+    torch.manual_seed(5)
+    N, Hh, W, C = 4, 14, 14, 256
+    x0 = torch.randn(N, Hh, W, C, device=dev).half()
+    s0 = torch.randn(N, Hh, W, C, device=dev).half()
+    wl = torch.randn(N, Hh, W, C, device=dev)
+    w2 = torch.randn(N, Hh, W, C, device=dev)
+
+    def run(lazy):
+        KF._LAZY_DZ[0] = lazy
+        x = x0.clone().requires_grad_()
+        s = s0.clone().requires_grad_()
+        g1 = (torch.rand(C, device=dev) + 0.5).requires_grad_()
+        b1 = torch.zeros(C, device=dev).requires_grad_()
+        g2 = (torch.rand(C, device=dev) + 0.5).requires_grad_()
+        b2 = torch.zeros(C, device=dev).requires_grad_()
+        torch.manual_seed(9)
+        g1.data.uniform_(0.5, 1.5)
+        g2.data.uniform_(0.5, 1.5)
+        rm1, rv1, rm2, rv2 = (torch.zeros(C, device=dev), torch.ones(C, device=dev),
+                              torch.zeros(C, device=dev), torch.ones(C, device=dev))
+        sc = H.batch_norm(s, g2, b2, rm2, rv2, 1e-5, 0.9, False, True, 3, None)[0]
+        out = H.batch_norm(x, g1, b1, rm1, rv1, 1e-5, 0.9, False, True, 3, 'relu', addend=sc)[0]
+        loss = (out.float() * wl).sum()
+        if second_consumer:
+            loss = loss + (sc.float() * w2).sum()
+        loss.backward()
+        KF._LAZY_DZ[0] = True
+        return [t.grad.float() for t in (x, s, g1, b1, g2, b2)]
+    ref = run(False)
+    got = run(True)
+    for a, b in zip(got, ref):
+        torch.testing.assert_close(a, b, rtol=2e-3, atol=2e-3 * float(b.abs().max() + 1e-6))
