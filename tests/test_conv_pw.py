@@ -216,10 +216,13 @@ def test_resnet_lazy_shortcut_gradient_matches_materialised():
     used = KF._LAZY_USED[0]
     got = grads()
     assert KF._LAZY_USED[0] > used
+    # fp16 forward kernels picked by the autotuner (split-K reductions) are not bitwise reproducible, so
+    # compare in relative norm against the materialised path's own run-to-run spread; a wrong shortcut
+    # gradient (e.g. the mask not applied) is off by tens of percent
     for a, b, c in zip(got, ref, ref2):
-        scale = float(np.abs(b).max()) + 1e-6
-        noise = float(np.abs(c - b).max()) / scale       # run-to-run spread of the materialised path
-        assert float(np.abs(a - b).max()) / scale <= max(2 * noise, 2e-3)
+        nb = float(np.linalg.norm(b)) + 1e-6
+        noise = float(np.linalg.norm(c - b)) / nb
+        assert float(np.linalg.norm(a - b)) / nb <= max(3 * noise, 1e-2)
 
 
 @pytest.mark.parametrize('second_consumer', [False, True])
