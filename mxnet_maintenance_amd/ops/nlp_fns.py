@@ -555,23 +555,24 @@ def bias_grad(dy2, b_ref, bdt):
     if part is None or part.numel() < n:
         part = _COLSUM_PART[skey] = torch.empty(n, dtype=torch.float32, device=dy2.device)
     tgt = _leaf_grad(b_ref, N, dtype=bdt) if (bdt in _DT and _FC_DIRECT) else None
-    out = tgt if tgt is not None else torch.empty(N, dtype=torch.float32, device=dy2.device)
+    # not accumulated in place: written in the bias dtype by the same kernel (fp32 sums), no conversion launch
+    out = tgt if tgt is not None else torch.empty(N, dtype=bdt if bdt in _DT else torch.float32, device=dy2.device)
     # two launches (partial rows, then their sum); see bn_nhwc.hip on why not one
     lib.colsum_rows(_DT[dy2.dtype], dy2.data_ptr(), _KF._zeros_f32(N, dy2.device).data_ptr(), part.data_ptr(),
                     M, N, _DT[out.dtype], out.data_ptr(), int(tgt is not None), _stream())
     if tgt is not None:
         return None
-    return out.to(bdt)
+    return out if out.dtype == bdt else out.to(bdt)
 
 
 def _bias_from_partials(part, nb, N, b_ref, bdt, dev):
     """db from column partials an earlier kernel already reduced (add_dropout_ln backward): one small
     column-sum launch, accumulated straight into the bias's .grad buffer when possible."""
     tgt = _leaf_grad(b_ref, N, dtype=bdt) if (bdt in _DT and _FC_DIRECT) else None
-    out = tgt if tgt is not None else torch.empty(N, dtype=torch.float32, device=dev)
+    out = tgt if tgt is not None else torch.empty(N, dtype=bdt if bdt in _DT else torch.float32, device=dev)
     _K.lib().column_sum_partials(_DT[out.dtype], part.data_ptr(), nb, N, out.data_ptr(), int(tgt is not None),
                                  _stream())
-    return None if tgt is not None else out.to(bdt)
+    return None if tgt is not None else (out if out.dtype == bdt else out.to(bdt))
 
 
 _IDX_T = {torch.float32: 0, torch.int64: 1, torch.int32: 2}
