@@ -432,12 +432,22 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
       if (ADD) {
         Vec8<T> a;
         a.raw = *reinterpret_cast<const uint4*>(sb + C::STAGE_IN + pix * (NOUT * 2) + c8 * 16);
-        const uint32_t amb =
-            AMK ? static_cast<uint32_t>(*reinterpret_cast<const uint8_t*>(
-                      sb + C::STAGE_IN + C::STAGE_ADD + C::STAGE_Z + C::STAGE_M + pix * (NOUT / 8) + c8))
-                : 0xffu;
+        if (AMK) {
+          // mask the addend's 16-bit elements with a bitwise AND (a cleared element is +0): bit 2j / 2j+1 of
+          // the byte selects the low / high half of dword j
+          const uint32_t amb = static_cast<uint32_t>(*reinterpret_cast<const uint8_t*>(
+              sb + C::STAGE_IN + C::STAGE_ADD + C::STAGE_Z + C::STAGE_M + pix * (NOUT / 8) + c8));
+          auto m2 = [&](int j) -> uint32_t {
+            const uint32_t b = (amb >> (2 * j)) & 3u;
+            return (b & 1u) * 0xFFFFu | (b >> 1) * 0xFFFF0000u;
+          };
+          a.raw.x &= m2(0);
+          a.raw.y &= m2(1);
+          a.raw.z &= m2(2);
+          a.raw.w &= m2(3);
+        }
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v.set(q, v.get(q) + (((amb >> q) & 1u) ? a.get(q) : 0.f));
+        for (int q = 0; q < 8; ++q) v.set(q, v.get(q) + a.get(q));
       }
       const bool live = in_tile && p < M;
       if (BNB && live) {
