@@ -60,6 +60,13 @@ __device__ __forceinline__ void vm_wait() {
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// One mask byte from LDS through its aligned dword: the 64 lanes of a store round read 64 consecutive
+// bytes, i.e. 16 dwords with 4 lanes each (a broadcast), where byte-wide reads counted as bank conflicts
+__device__ __forceinline__ uint32_t lds_byte(const char* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  return (*reinterpret_cast<const uint32_t*>(a & ~static_cast<uintptr_t>(3)) >> ((a & 3u) * 8)) & 0xffu;
+}
+
 // pixels per tile: the input stage at most 16 KB and the epilogue image at most 32 KB; with an
 // addend, at most 32 pixels (its LDS stage is as large as the image) but whole 8 KB LDS-DMA rounds
 // for both the input and the addend stage
@@ -435,8 +442,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
         if (AMK) {
           // mask the addend's 16-bit elements with a bitwise AND (a cleared element is +0): bit 2j / 2j+1 of
           // the byte selects the low / high half of dword j
-          const uint32_t amb = static_cast<uint32_t>(*reinterpret_cast<const uint8_t*>(
-              sb + C::STAGE_IN + C::STAGE_ADD + C::STAGE_Z + C::STAGE_M + pix * (NOUT / 8) + c8));
+          const uint32_t amb = lds_byte(sb + C::STAGE_IN + C::STAGE_ADD + C::STAGE_Z + C::STAGE_M + pix * (NOUT / 8) + c8);
           auto m2 = [&](int j) -> uint32_t {
             const uint32_t b = (amb >> (2 * j)) & 3u;
             return (b & 1u) * 0xFFFFu | (b >> 1) * 0xFFFF0000u;
@@ -454,8 +460,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2 * WP
         Vec8<T> zv;
         zv.raw = *reinterpret_cast<const uint4*>(sb + C::STAGE_IN + C::STAGE_ADD + pix * (NOUT * 2) + c8 * 16);
         const uint32_t mb =
-            BNB == kPwBnbMask ? static_cast<uint32_t>(*reinterpret_cast<const uint8_t*>(
-                                    sb + C::STAGE_IN + C::STAGE_ADD + C::STAGE_Z + pix * (NOUT / 8) + c8))
+            BNB == kPwBnbMask ? lds_byte(sb + C::STAGE_IN + C::STAGE_ADD + C::STAGE_Z + pix * (NOUT / 8) + c8)
                               : 0xffu;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
