@@ -101,3 +101,14 @@ def test_fc_layer_uses_gemm_candidates():
     ref = xf @ w.t() + b
     assert _rel(y._data, ref) < 2e-2
     assert _rel(x.grad._data, torch.ones_like(ref) @ w) < 2e-2
+
+
+@pytest.mark.parametrize('shape,dt', [((768, 3072), torch.bfloat16), ((30528, 768), torch.float16),
+                                      ((64, 256), torch.float16), ((40, 24), torch.float32), ((33, 16), torch.float16)])
+def test_transpose2d_matches_torch(shape, dt):
+    """kernel_fns.transpose2d (the LDS-tiled tap-transpose kernel for every weight transpose of the data
+    gradients) equals w.t().contiguous(), including its torch fallback for rows that are not 8-multiples."""
+    from mxnet_maintenance_amd.ops import kernel_fns as KF
+    w = torch.randn(*shape, device='cuda').to(dt)
+    t = KF.transpose2d(w)
+    assert t.is_contiguous() and torch.equal(t, w.t().contiguous())
